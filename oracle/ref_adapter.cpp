@@ -1,0 +1,80 @@
+// C adapter over the REFERENCE's own solver sources, compiled from
+// /root/reference by oracle/Makefile into oracle/_ref/libxfemm_ref.so.
+//
+// TEST INFRASTRUCTURE ONLY (oracle pinning and the bench's cpu_baseline leg).
+// Nothing of the reference is copied: this file only calls
+//   CBigLinProb            cfemm/libfemm/spars.h:38-83   (spars.cpp)
+//   CMSolverMaterialProp   cfemm/libfemm/CMaterialProp.h:193 (CMaterialProp.cpp)
+// through an extern "C" surface matching ora_linprob_ops (static2d_oracle.h).
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "CMaterialProp.h"
+#include "spars.h"
+
+extern "C" {
+
+void *ref_lp_create(int n, int bw, double precision)
+{
+    CBigLinProb *L = new CBigLinProb();
+    L->Precision = precision;
+    L->Create(n, bw);
+    return L;
+}
+
+void ref_lp_destroy(void *L) { delete static_cast<CBigLinProb *>(L); }
+void ref_lp_addto(void *L, double v, int p, int q) { static_cast<CBigLinProb *>(L)->AddTo(v, p, q); }
+double *ref_lp_b(void *L) { return static_cast<CBigLinProb *>(L)->b; }
+double *ref_lp_V(void *L) { return static_cast<CBigLinProb *>(L)->V; }
+void ref_lp_setvalue(void *L, int i, double x) { static_cast<CBigLinProb *>(L)->SetValue(i, x); }
+void ref_lp_periodicity(void *L, int i, int j) { static_cast<CBigLinProb *>(L)->Periodicity(i, j); }
+void ref_lp_antiperiodicity(void *L, int i, int j) { static_cast<CBigLinProb *>(L)->AntiPeriodicity(i, j); }
+void ref_lp_wipe(void *L) { static_cast<CBigLinProb *>(L)->Wipe(); }
+double ref_lp_get(void *L, int p, int q) { return static_cast<CBigLinProb *>(L)->Get(p, q); }
+void ref_lp_multA(void *L, double *X, double *Y) { static_cast<CBigLinProb *>(L)->MultA(X, Y); }
+
+int ref_lp_pcgsolve(void *L, int flag, long long *iters)
+{
+    if (iters) *iters = -1;  // the reference does not report its iteration count
+    return static_cast<CBigLinProb *>(L)->PCGSolve(flag) ? 1 : 0;
+}
+
+// Parse one <BeginBlock> ... <EndBlock> text with the reference parser, run
+// GetSlopes(omega=0) and return the processed curve (B, H.re, slope.re) and mu_x.
+// Returns BHpoints, or -1 on a parse problem.  Arrays must hold `cap` values.
+int ref_block_slopes(const char *block_text, double *B, double *H, double *slope,
+                     int cap, double *mu_x)
+{
+    std::istringstream in(block_text);
+    std::ostringstream err;
+    femm::CMSolverMaterialProp prop = femm::CMSolverMaterialProp::fromStream(in, err);
+    if (prop.BHpoints > 0) prop.GetSlopes(0.0);
+    int n = prop.BHpoints;
+    if (n > cap) return -1;
+    for (int i = 0; i < n; i++) {
+        B[i] = prop.Bdata[i];
+        H[i] = prop.Hdata[i].re;
+        slope[i] = prop.slope[i].re;
+    }
+    *mu_x = prop.mu_x;
+    return n;
+}
+
+// GetBHProps(B) of the processed block, for a batch of flux densities.
+int ref_block_bhprops(const char *block_text, const double *Bq, int nq, double *v, double *dv)
+{
+    std::istringstream in(block_text);
+    std::ostringstream err;
+    femm::CMSolverMaterialProp prop = femm::CMSolverMaterialProp::fromStream(in, err);
+    if (prop.BHpoints > 0) prop.GetSlopes(0.0);
+    for (int i = 0; i < nq; i++) {
+        double vv = 0, dd = 0;
+        prop.GetBHProps(Bq[i], vv, dd);
+        v[i] = vv;
+        dv[i] = dd;
+    }
+    return prop.BHpoints;
+}
+
+}  // extern "C"
