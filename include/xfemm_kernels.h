@@ -1,0 +1,152 @@
+/* xfemm_kernels.h -- C-ABI of the MI355X (gfx950) fsolver hot path.
+ *
+ * Thin boundary between the C++ host side (FSolver, include/xfemm_fsolver.h)
+ * and the hand-written HIP kernels: plain pointers and sizes, no C++ or torch
+ * types.  One xfk_problem holds one static-2D magnetostatic problem resident
+ * in HBM; xfk_static2d() runs the whole reference Static2D on the GPU:
+ * element assembly into CSR, point/segment/(anti)periodic boundary conditions,
+ * the preconditioned conjugate-gradient solve and the nonlinear B-H Newton loop.
+ *
+ * Reference interfaces replaced (temudschin/xfemm @ 2025-02-04):
+ *   xfk_static2d          FSolver::Static2D(CBigLinProb&)   cfemm/fsolver/static2d.cpp:53
+ *                         (called from FSolver::runSolver   cfemm/fsolver/fsolver.cpp:1266)
+ *   xfk_pcg_solve         CBigLinProb::PCGSolve(int flag)   cfemm/libfemm/spars.cpp:238
+ *   xfk_csr_*             CBigLinProb::MultA / Dot          cfemm/libfemm/spars.cpp:167,187
+ *   xfk_problem_create    the state FSolver::LoadMesh + LoadProblemFile leave behind
+ *                         (meshnode, meshele, the prop lists)      cfemm/fsolver/fsolver.cpp:202,350
+ *
+ * All functions return XFK_OK (0) or a negative error code; xfk_last_error()
+ * gives the message of the last failure on the calling thread.  There is no
+ * CPU fallback: without a usable gfx950 device every call fails.
+ */
+#ifndef XFEMM_KERNELS_H
+#define XFEMM_KERNELS_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    XFK_OK = 0,
+    XFK_ERR_ARG = -1,
+    XFK_ERR_HIP = -2,
+    XFK_ERR_SINGULAR = -3,      /* zero diagonal: "singular flag tripped" (spars.cpp:245) */
+    XFK_ERR_NOCONV = -4,        /* iteration cap reached */
+    XFK_ERR_UNSUPPORTED = -5
+};
+
+/* CMSolverMaterialProp after GetSlopes(0) (CMaterialProp.h:193). */
+typedef struct {
+    double mu_x, mu_y;          /* relative permeability */
+    double H_c;                 /* coercivity, A/m */
+    double J_re;                /* applied current density, MA/m^2 */
+    double Cduct;               /* conductivity, MS/m */
+    double LamFill;
+    int LamType;
+    int BHpoints;               /* 0 = linear */
+    const double *B;            /* BHpoints: processed B-H curve (T) */
+    const double *H;            /* BHpoints: A/m (real parts) */
+    const double *slope;        /* BHpoints: dH/dB at the knots */
+} xfk_block_desc;
+
+/* CMBlockLabel (CBlockLabel.h:153) after FSolver::GetFillFactor. */
+typedef struct {
+    int block;                  /* index into blocks */
+    int in_circuit;             /* -1 = none */
+    double mag_dir;             /* magnetisation direction, degrees */
+    int is_wound;
+} xfk_label_desc;
+
+/* CMBoundaryProp (CBoundaryProp.h). */
+typedef struct {
+    int format;                 /* BdryFormat: 0 prescribed A, 2 mixed, 4 periodic, 5 antiperiodic */
+    double A0, A1, A2, phi;
+    double c0, c1;
+} xfk_line_desc;
+
+/* CMPointProp (CPointProp.h). */
+typedef struct {
+    double A_re, A_im, J_re, J_im;
+} xfk_point_desc;
+
+/* CMCircuit (CCircuit.h) after FSolver::LoadProblemFile's serial expansion. */
+typedef struct {
+    int type;                   /* 0 parallel/voltage, 1 not expected here */
+    double amps_re;
+    double dvolts_re;
+} xfk_circuit_desc;
+
+typedef struct {
+    int n_nodes;
+    const double *x, *y;        /* node coordinates, cm */
+    const int *marker;          /* point-prop index or -1 (may be NULL) */
+    int n_elems;
+    const int *p;               /* 3 per element */
+    const int *e;               /* 3 per element: boundary-prop index or -1 (may be NULL) */
+    const int *lbl;             /* block label of each element */
+    int n_blocks;  const xfk_block_desc *blocks;
+    int n_labels;  const xfk_label_desc *labels;
+    int n_lines;   const xfk_line_desc *lines;
+    int n_points;  const xfk_point_desc *points;
+    int n_circs;   const xfk_circuit_desc *circs;
+    int n_pbc;     const int *pbc;      /* 3 per pair: node, node, type (0 periodic, 1 anti) */
+    double precision;           /* [Precision] */
+    int length_units;           /* femm::LengthUnit */
+    int coords;                 /* 0 cartesian, 1 polar */
+    double relax;               /* FSolver::Relax, 1.0 */
+} xfk_problem_desc;
+
+typedef struct {
+    int newton_iters;           /* linear solves performed */
+    long long cg_iters;         /* total PCG iterations */
+    double last_res;            /* last nonlinear residual */
+    double final_er;            /* last PCG preconditioned residual ratio */
+    long long nnz;              /* CSR nonzeros (full symmetric storage) */
+    int ncolors;                /* element colours of the assembly scatter */
+    double ms_symbolic;         /* device time, ms */
+    double ms_assemble;
+    double ms_solve;
+} xfk_result;
+
+typedef struct xfk_problem xfk_problem;
+
+const char *xfk_last_error(void);
+int xfk_device_count(void);
+
+/* Upload a problem; nothing is computed yet.  Host arrays may be freed after. */
+int xfk_problem_create(const xfk_problem_desc *desc, int device, xfk_problem **out);
+void xfk_problem_destroy(xfk_problem *prob);
+
+enum { XFK_REBUILD_SYMBOLIC = 1 };
+
+/* FSolver::Static2D on the device.  flags: XFK_REBUILD_SYMBOLIC rebuilds the
+ * CSR pattern, colouring and boundary maps (they are cached otherwise). */
+int xfk_static2d(xfk_problem *prob, int flags, xfk_result *res);
+
+/* A at every node (V * c, the value fsolver writes to .ans), host copy. */
+int xfk_get_solution(xfk_problem *prob, double *A_host);
+
+/* Circuit results after xfk_static2d: case (0/1), J, dV per circuit. */
+int xfk_get_circuits(xfk_problem *prob, int *ccase, double *J, double *dV);
+
+/* Device views for the bench / tests (stream-ordered on the problem's stream). */
+int xfk_get_csr(xfk_problem *prob, int *rowptr, int *col, double *val, double *b);
+long long xfk_get_nnz(xfk_problem *prob);
+int xfk_get_stream(xfk_problem *prob, void **hip_stream);
+
+/* Stand-alone PCG on a host-supplied full symmetric CSR (testing the solver
+ * alone, CBigLinProb::PCGSolve semantics with the device preconditioner).
+ * V is the initial guess (used when flag != 0) and receives the solution. */
+int xfk_pcg_solve_csr(int n, const int *rowptr, const int *col, const double *val,
+                      const double *b, double *V, int flag, double precision,
+                      int device, long long *iters, double *er);
+
+/* Timing probe of the CG kernels (profiles / roofline): run `iters` PCG
+ * iterations on the assembled system without a convergence stop; returns the
+ * mean device time (ms) of the SpMV kernel and of one whole iteration. */
+int xfk_pcg_time(xfk_problem *prob, int iters, double *ms_spmv, double *ms_iter);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

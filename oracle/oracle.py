@@ -242,3 +242,28 @@ def solve(pr: femfile.FemProblem, mesh: femfile.Mesh, linprob: str = "oracle"):
         raise RuntimeError("oracle Static2D failed")
     circ_out = [(circs[k].Case, circs[k].J, circs[k].dV) for k in range(len(pr.circuits))]
     return A, {"newton_iters": st.newton_iters, "cg_iters": st.cg_iters, "last_res": st.last_res}, circ_out
+
+
+def system(pr: femfile.FemProblem, mesh: femfile.Mesh):
+    """Iter-0 assembled system after all boundary conditions (restated
+    Static2D + CBigLinProb): returns (scipy.sparse.csr_matrix full symmetric, b)."""
+    import scipy.sparse as sp
+    L = lib()
+    L.ora_static2d_system.argtypes = [C.POINTER(OraProblem), iptr, iptr, dptr, C.c_longlong, dptr,
+                                      C.POINTER(C.c_longlong)]
+    P, keep, _ = make_problem(pr, mesh)
+    n = len(mesh.x)
+    cap = 16 * n + 1024
+    rows = np.zeros(cap, np.int32)
+    cols = np.zeros(cap, np.int32)
+    vals = np.zeros(cap)
+    b = np.zeros(n)
+    nnz = C.c_longlong()
+    L.ora_static2d_system(C.byref(P), rows.ctypes.data_as(iptr), cols.ctypes.data_as(iptr),
+                          vals.ctypes.data_as(dptr), cap, b.ctypes.data_as(dptr), C.byref(nnz))
+    k = nnz.value
+    if k > cap:
+        raise RuntimeError("export capacity too small")
+    U = sp.coo_matrix((vals[:k], (rows[:k], cols[:k])), shape=(n, n)).tocsr()
+    D = sp.diags(U.diagonal())
+    return (U + U.T - D).tocsr(), b

@@ -327,23 +327,9 @@ void ora_get_bh_props(const ora_block *m, double B, double *v, double *dv)
 /* FSolver::Static2D (static2d.cpp:53-1033)                                 */
 /* ------------------------------------------------------------------------ */
 
-int ora_static2d(ora_problem *pr, const ora_linprob_ops *ops, double *A_out, ora_stats *stats)
+static void ora_circuits(ora_problem *pr)
 {
-    if (!ops) ops = &k_builtin;
-    const double c = ORA_PI * 4.e-05;
-    const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
-    const int NN = pr->n_nodes, NE = pr->n_elems;
-    double res = 0, lastres = 0, Relax = pr->relax;
-    int Iter = 0, LinearFlag = 1;
-    long long cg_total = 0;
-
-    void *L = ops->create(NN, pr->bandwidth, pr->precision);
-    double *V_old = (double *)calloc(NN, sizeof(double));
-    double *mu1 = (double *)malloc(sizeof(double) * NE);
-    double *mu2 = (double *)malloc(sizeof(double) * NE);
-    double *v12 = (double *)calloc(NE, sizeof(double));
-    for (int i = 0; i < NE; i++) { mu1[i] = -1.; mu2[i] = -1.; }
-
+    const int NE = pr->n_elems;
     /* circuits (static2d.cpp:84-167) */
     if (pr->n_circs > 0) {
         double *CI1 = (double *)calloc(pr->n_circs, sizeof(double));
@@ -386,8 +372,16 @@ int ora_static2d(ora_problem *pr, const ora_linprob_ops *ops, double *A_out, ora
         free(CI1); free(CI2); free(CI3);
     }
 
-    do {
-        if (Iter > 0) ops->wipe(L);
+}
+
+/* one Newton iteration's assembly + boundary conditions (static2d.cpp:186-940) */
+static void ora_assemble(ora_problem *pr, const ora_linprob_ops *ops, void *L, int Iter,
+                         double *mu1, double *mu2, double *v12, int *LinearFlag_io)
+{
+    const double c = ORA_PI * 4.e-05;
+    const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
+    const int NN = pr->n_nodes, NE = pr->n_elems;
+    int LinearFlag = *LinearFlag_io;
         double *b = ops->b(L);
         double *Vv = ops->V(L);
 
@@ -616,6 +610,31 @@ int ora_static2d(ora_problem *pr, const ora_linprob_ops *ops, double *A_out, ora
             if (pr->pbc[3 * k + 2] == 1) ops->antiperiodicity(L, pr->pbc[3 * k], pr->pbc[3 * k + 1]);
         }
 
+    *LinearFlag_io = LinearFlag;
+}
+
+int ora_static2d(ora_problem *pr, const ora_linprob_ops *ops, double *A_out, ora_stats *stats)
+{
+    if (!ops) ops = &k_builtin;
+    const double c = ORA_PI * 4.e-05;
+    const int NN = pr->n_nodes, NE = pr->n_elems;
+    double res = 0, lastres = 0, Relax = pr->relax;
+    int Iter = 0, LinearFlag = 1;
+    long long cg_total = 0;
+
+    void *L = ops->create(NN, pr->bandwidth, pr->precision);
+    double *V_old = (double *)calloc(NN, sizeof(double));
+    double *mu1 = (double *)malloc(sizeof(double) * NE);
+    double *mu2 = (double *)malloc(sizeof(double) * NE);
+    double *v12 = (double *)calloc(NE, sizeof(double));
+    for (int i = 0; i < NE; i++) { mu1[i] = -1.; mu2[i] = -1.; }
+
+    ora_circuits(pr);
+
+    do {
+        if (Iter > 0) ops->wipe(L);
+        ora_assemble(pr, ops, L, Iter, mu1, mu2, v12, &LinearFlag);
+        double *Vv;
         Vv = ops->V(L);
         for (int j = 0; j < NN; j++) V_old[j] = Vv[j];
         long long it = 0;
@@ -654,5 +673,24 @@ int ora_static2d(ora_problem *pr, const ora_linprob_ops *ops, double *A_out, ora
     }
     ops->destroy(L);
     free(V_old); free(mu1); free(mu2); free(v12);
+    return 1;
+}
+
+int ora_static2d_system(ora_problem *pr, int *rows, int *cols, double *vals, long long cap,
+                        double *b_out, long long *nnz_out)
+{
+    const int NN = pr->n_nodes, NE = pr->n_elems;
+    int LinearFlag = 1;
+    void *L = ora_lp_create(NN, pr->bandwidth, pr->precision);
+    double *mu1 = (double *)malloc(sizeof(double) * NE);
+    double *mu2 = (double *)malloc(sizeof(double) * NE);
+    double *v12 = (double *)calloc(NE, sizeof(double));
+    /* circuits are computed by ora_static2d; do the same prologue here */
+    ora_circuits(pr);
+    ora_assemble(pr, &k_builtin, L, 0, mu1, mu2, v12, &LinearFlag);
+    *nnz_out = ora_lp_export_upper(L, rows, cols, vals, cap);
+    for (int i = 0; i < NN; i++) b_out[i] = ((ora_lp *)L)->b[i];
+    ora_lp_destroy(L);
+    free(mu1); free(mu2); free(v12);
     return 1;
 }

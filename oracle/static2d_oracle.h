@@ -111,6 +111,11 @@ const ora_linprob_ops *ora_builtin_linprob(void);
 int ora_static2d(ora_problem *pr, const ora_linprob_ops *ops, double *A_out,
                  ora_stats *stats);
 
+/* Iter-0 system after assembly and all boundary conditions, exported as the
+ * upper-triangular COO of the restated CBigLinProb plus b. */
+int ora_static2d_system(ora_problem *pr, int *rows, int *cols, double *vals, long long cap,
+                        double *b_out, long long *nnz_out);
+
 /* CMSolverMaterialProp::GetBHProps(B, v, dv) on the real axis. */
 void ora_get_bh_props(const ora_block *m, double B, double *v, double *dv);
 

@@ -1,0 +1,71 @@
+"""Shared test helpers: feed identical inputs to the oracle and to the HIP path."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from oracle import femfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def kernel_kwargs(pr: femfile.FemProblem, mesh: femfile.Mesh) -> dict:
+    """Oracle-parsed problem -> keyword arguments of kernels.Static2DProblem."""
+    blocks = []
+    for m in pr.blocks:
+        b = dict(mu_x=m.mu_x, mu_y=m.mu_y, H_c=m.H_c, J_re=m.J_re, Cduct=m.Cduct, LamFill=m.LamFill,
+                 LamType=m.LamType)
+        if m.BHpoints:
+            b.update(B=np.array(m.Bdata), H=np.array(m.Hdata), slope=np.array(m.slope))
+        blocks.append(b)
+    labels = [dict(block=max(lb.BlockType, 0), in_circuit=lb.InCircuit, mag_dir=lb.MagDir,
+                   is_wound=int(lb.bIsWound)) for lb in pr.labels]
+    lines = [dict(format=b.BdryFormat, A0=b.A0, A1=b.A1, A2=b.A2, phi=b.phi, c0=b.c0, c1=b.c1) for b in pr.bdrys]
+    points = [dict(A_re=q.A_re, A_im=q.A_im, J_re=q.J_re, J_im=q.J_im) for q in pr.points]
+    circuits = [dict(type=c.CircType, amps_re=c.Amps_re, dvolts_re=c.dVolts_re) for c in pr.circuits]
+    return dict(x=mesh.x, y=mesh.y, p=mesh.p, lbl=mesh.lbl, marker=mesh.marker, e=mesh.e,
+                pbc=mesh.pbc if len(mesh.pbc) else None, blocks=blocks, labels=labels, lines=lines,
+                points=points, circuits=circuits, precision=pr.Precision, length_units=pr.LengthUnits,
+                coords=pr.Coords, relax=pr.Relax)
+
+
+def synth_to_oracle(kw: dict):
+    """xfemm_amd.synth problem -> (FemProblem, Mesh) for the oracle (slopes via
+    the oracle's GetSlopes restatement), and kernel kwargs with those slopes."""
+    from xfemm_amd import synth
+    pr = femfile.FemProblem()
+    pr.Precision = kw["precision"]
+    pr.LengthUnits = kw["length_units"]
+    pr.Relax = 1.0
+    for b in kw["blocks"]:
+        m = femfile.BlockProp(mu_x=b.get("mu_x", 1.0), mu_y=b.get("mu_y", 1.0), H_c=b.get("H_c", 0.0),
+                              J_re=b.get("J_re", 0.0), Cduct=b.get("Cduct", 0.0),
+                              LamFill=b.get("LamFill", 1.0), LamType=b.get("LamType", 0))
+        if b.get("bh") == "M19":
+            B, H = synth.m19_curve()
+            m.BHpoints, m.Bdata, m.Hdata = len(B), list(B), list(H)
+            femfile.get_slopes(m)
+        pr.blocks.append(m)
+    for lb in kw["labels"]:
+        pr.labels.append(femfile.BlockLabel(BlockType=lb["block"], InCircuit=lb.get("in_circuit", -1),
+                                            MagDir=lb.get("mag_dir", 0.0)))
+    for ln in kw["lines"]:
+        pr.bdrys.append(femfile.BdryProp(BdryFormat=ln.get("format", 0), A0=ln.get("A0", 0.0),
+                                         c0=ln.get("c0", 0.0), c1=ln.get("c1", 0.0)))
+    femfile.get_fill_factor(pr)
+    nn = len(kw["x"])
+    mesh = femfile.Mesh(x=np.asarray(kw["x"], float), y=np.asarray(kw["y"], float),
+                        marker=-np.ones(nn, np.int32), p=np.asarray(kw["p"], np.int32),
+                        e=np.asarray(kw["e"], np.int32), lbl=np.asarray(kw["lbl"], np.int32),
+                        blk=np.array([kw["labels"][l]["block"] for l in kw["lbl"]], np.int32),
+                        pbc=np.zeros((0, 3), np.int32))
+    return pr, mesh, kernel_kwargs(pr, mesh)
+
+
+def rel_err(a, b):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    scale = max(np.abs(b).max(), 1e-300)
+    return float(np.abs(a - b).max() / scale)

@@ -1,0 +1,985 @@
+// Host driver + C-ABI of the MI355X fsolver hot path (include/xfemm_kernels.h).
+//
+// xfk_static2d() is FSolver::Static2D (cfemm/fsolver/static2d.cpp:53-1033) on
+// the GPU.  Host work per problem is limited to O(boundary) preparation done
+// once at creation: circuit totals (static2d.cpp:84-167, element order, so the
+// circuit J/dV are bit-identical to the reference), the first/last Dirichlet
+// value of every fixed node in the reference's SetValue call order
+// (static2d.cpp:827-926), and the composition of the sequential
+// Periodicity/AntiPeriodicity calls (spars.cpp:366-474) into one linear
+// averaging map over CSR slots.  Everything else runs on the device.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <set>
+#include <unordered_map>
+
+#include "xfk_kernels.h"
+
+namespace xfk {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+
+#define XFK_REQUIRE(cond, code, msg)  \
+    do {                              \
+        if (!(cond)) {                \
+            ::xfk::set_error(msg);    \
+            return code;              \
+        }                             \
+    } while (0)
+
+using Terms = std::vector<std::pair<long long, double>>;
+
+static inline long long ukey(int r, int c)
+{
+    if (c < r) std::swap(r, c);
+    return ((long long)r << 32) | (unsigned)c;
+}
+
+static Terms lin2(double a, const Terms &x, double b, const Terms &y)
+{
+    std::map<long long, double> m;
+    for (auto &t : x) m[t.first] += a * t.second;
+    for (auto &t : y) m[t.first] += b * t.second;
+    Terms out;
+    for (auto &kv : m)
+        if (kv.second != 0.0) out.push_back(kv);
+    return out;
+}
+
+// Symbolic composition of CBigLinProb::Periodicity / AntiPeriodicity
+// (spars.cpp:366-474) applied in pbclist order (static2d.cpp:929-940).  Each
+// touched matrix entry / RHS entry becomes a linear combination of the
+// post-Dirichlet values; sets of rows k are structural supersets of the
+// reference's value-based scan, which is exact because averaging zeros gives
+// zero.
+static int build_pbc_map(xfk_problem *P)
+{
+    const int npbc = (int)P->hpbc.size() / 3;
+    if (npbc == 0) return XFK_OK;
+    std::unordered_map<int, std::set<int>> N0;  // original neighbours of pbc nodes
+    for (int k = 0; k < npbc; ++k) {
+        N0[P->hpbc[3 * k]];
+        N0[P->hpbc[3 * k + 1]];
+    }
+    for (int e = 0; e < P->NE; ++e)
+        for (int j = 0; j < 3; ++j) {
+            auto it = N0.find(P->hp[3 * e + j]);
+            if (it == N0.end()) continue;
+            for (int m = 0; m < 3; ++m)
+                if (m != j) it->second.insert(P->hp[3 * e + m]);
+        }
+    std::unordered_map<int, std::set<int>> Ncur = N0;
+    std::unordered_map<long long, Terms> E;
+    std::unordered_map<int, Terms> Eb;
+    std::set<long long> fill;
+    auto is_orig = [&](int r, int c) -> bool {
+        if (r == c) return true;
+        auto it = N0.find(r);
+        if (it != N0.end()) return it->second.count(c) > 0;
+        it = N0.find(c);
+        if (it != N0.end()) return it->second.count(r) > 0;
+        return false;
+    };
+    auto get = [&](int r, int c) -> Terms {
+        long long k = ukey(r, c);
+        auto it = E.find(k);
+        if (it != E.end()) return it->second;
+        if (is_orig(r, c)) return Terms{{k, 1.0}};
+        return Terms{};
+    };
+    auto getb = [&](int i) -> Terms {
+        auto it = Eb.find(i);
+        if (it != Eb.end()) return it->second;
+        return Terms{{(long long)i, 1.0}};
+    };
+    for (int q = 0; q < npbc; ++q) {
+        int i = P->hpbc[3 * q], j = P->hpbc[3 * q + 1], t = P->hpbc[3 * q + 2];
+        if (t != 0 && t != 1) continue;  // static2d.cpp:932-939 only handles 0 and 1
+        if (i < 0 || j < 0 || i >= P->N || j >= P->N) {
+            set_error("pbc node index out of range");
+            return XFK_ERR_ARG;
+        }
+        if (j < i) std::swap(i, j);
+        const double sg = (t == 0) ? 1.0 : -1.0;
+        std::set<int> K;
+        for (int k : Ncur[i]) K.insert(k);
+        for (int k : Ncur[j]) K.insert(k);
+        K.erase(i);
+        K.erase(j);
+        for (int k : K) {
+            Terms v1 = get(k, i), v2 = get(k, j);
+            Terms c = lin2(0.5, v1, 0.5 * sg, v2);
+            E[ukey(k, i)] = c;
+            E[ukey(k, j)] = (sg > 0) ? c : lin2(-1.0, c, 0.0, Terms{});
+            for (int m : {i, j})
+                if (!is_orig(k, m)) fill.insert(ukey(k, m));
+            Ncur[i].insert(k);
+            Ncur[j].insert(k);
+            auto itk = Ncur.find(k);
+            if (itk != Ncur.end()) {
+                itk->second.insert(i);
+                itk->second.insert(j);
+            }
+        }
+        Terms d = lin2(0.5, get(i, i), 0.5, get(j, j));
+        E[ukey(i, i)] = d;
+        E[ukey(j, j)] = d;
+        Terms bi = getb(i), bj = getb(j);
+        Terms c = lin2(0.5, bi, 0.5 * sg, bj);
+        Eb[i] = c;
+        Eb[j] = (sg > 0) ? c : lin2(-1.0, c, 0.0, Terms{});
+    }
+    P->pbc_fill.assign(fill.begin(), fill.end());
+    P->pbc_entry_key.clear();
+    P->pbc_entry_terms.clear();
+    std::vector<long long> keys;
+    for (auto &kv : E) keys.push_back(kv.first);
+    std::sort(keys.begin(), keys.end());
+    for (long long k : keys) {
+        P->pbc_entry_key.push_back(k);
+        P->pbc_entry_terms.push_back(E[k]);
+    }
+    P->pbc_b_key.clear();
+    P->pbc_b_terms.clear();
+    std::vector<int> bk;
+    for (auto &kv : Eb) bk.push_back(kv.first);
+    std::sort(bk.begin(), bk.end());
+    for (int k : bk) {
+        P->pbc_b_key.push_back(k);
+        std::vector<std::pair<int, double>> tt;
+        for (auto &t : Eb[k]) tt.push_back({(int)t.first, t.second});
+        P->pbc_b_terms.push_back(tt);
+    }
+    return XFK_OK;
+}
+
+template <class T>
+static hipError_t upload(DBuf<T> &d, const T *h, size_t n, hipStream_t s)
+{
+    hipError_t e = d.alloc(n ? n : 1);
+    if (e != hipSuccess || n == 0) return e;
+    return hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, s);
+}
+
+// device -> host read-back ordered on the problem's (non-blocking) stream
+static hipError_t d2h(void *dst, const void *src, size_t bytes, hipStream_t s)
+{
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(s);
+}
+
+static hipError_t exclusive_scan(hipStream_t s, const int *in, int *out, int n)
+{
+    // out has n+1 entries; out[n] = total
+    void *tmp = nullptr;
+    size_t bytes = 0;
+    hipError_t e = hipcub::DeviceScan::InclusiveSum(tmp, bytes, in, out + 1, n, s);
+    if (e != hipSuccess) return e;
+    e = hipMalloc(&tmp, bytes ? bytes : 1);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(out, 0, sizeof(int), s);
+    if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(tmp, bytes, in, out + 1, n, s);
+    hipError_t e2 = hipStreamSynchronize(s);
+    (void)hipFree(tmp);
+    return e != hipSuccess ? e : e2;
+}
+
+static int build_symbolic(xfk_problem *P)
+{
+    hipStream_t s = P->stream;
+    const int N = P->N, NE = P->NE;
+    // node -> incident elements
+    DBuf<int> deg, cursor;
+    XFK_CHECK(deg.alloc(N));
+    XFK_CHECK(cursor.alloc(N));
+    XFK_CHECK(P->n2e_ptr.alloc(N + 1));
+    XFK_CHECK(P->n2e.alloc(3 * (size_t)NE));
+    XFK_CHECK(hipMemsetAsync(deg.p, 0, sizeof(int) * N, s));
+    XFK_CHECK(hipMemsetAsync(cursor.p, 0, sizeof(int) * N, s));
+    launch_count_incidence(s, NE, P->p_raw.p, deg.p);
+    XFK_CHECK(exclusive_scan(s, deg.p, P->n2e_ptr.p, N));
+    launch_fill_n2e(s, NE, P->p_raw.p, P->n2e_ptr.p, cursor.p, P->n2e.p);
+    launch_sort_segments(s, N, P->n2e_ptr.p, P->n2e.p);
+
+    // periodic fill-in entries, CSR by row
+    DBuf<int> fill_ptr, fill_col;
+    const int *fp = nullptr, *fc = nullptr;
+    if (!P->pbc_fill.empty()) {
+        std::vector<std::vector<int>> rows(N);
+        for (long long k : P->pbc_fill) {
+            int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
+            rows[r].push_back(c);
+            rows[c].push_back(r);
+        }
+        std::vector<int> hptr(N + 1, 0), hcol;
+        for (int r = 0; r < N; ++r) {
+            std::sort(rows[r].begin(), rows[r].end());
+            hptr[r + 1] = hptr[r] + (int)rows[r].size();
+            hcol.insert(hcol.end(), rows[r].begin(), rows[r].end());
+        }
+        XFK_CHECK(upload(fill_ptr, hptr.data(), hptr.size(), s));
+        XFK_CHECK(upload(fill_col, hcol.data(), hcol.size(), s));
+        XFK_CHECK(hipStreamSynchronize(s));
+        fp = fill_ptr.p;
+        fc = fill_col.p;
+    }
+
+    // CSR pattern
+    DBuf<int> rowcnt;
+    XFK_CHECK(rowcnt.alloc(N));
+    XFK_CHECK(P->rowptr.alloc(N + 1));
+    launch_row_count(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, rowcnt.p);
+    XFK_CHECK(exclusive_scan(s, rowcnt.p, P->rowptr.p, N));
+    int nnz = 0;
+    XFK_CHECK(d2h(&nnz, P->rowptr.p + N, sizeof(int), s));
+    P->nnz = nnz;
+    XFK_CHECK(P->col.alloc(nnz));
+    XFK_CHECK(P->val.alloc(nnz));
+    XFK_CHECK(P->diag.alloc(N));
+    launch_row_fill(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, P->rowptr.p, P->col.p, P->diag.p);
+
+    // Jones-Plassmann colouring of elements (shared node = conflict)
+    XFK_CHECK(P->color.alloc(NE));
+    XFK_CHECK(hipMemsetAsync(P->color.p, 0xff, sizeof(int) * NE, s));
+    DBuf<int> cnt;
+    XFK_CHECK(cnt.alloc(1));
+    XFK_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int), s));
+    int colored = 0, rounds = 0;
+    while (colored < NE) {
+        launch_color_round(s, NE, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, P->color.p, cnt.p);
+        XFK_CHECK(hipMemcpyAsync(&colored, cnt.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        XFK_CHECK(hipStreamSynchronize(s));
+        XFK_REQUIRE(++rounds < 10000, XFK_ERR_UNSUPPORTED, "element colouring did not terminate");
+    }
+    const int maxc = 128;
+    DBuf<int> hist;
+    XFK_CHECK(hist.alloc(maxc + 1));
+    XFK_CHECK(hipMemsetAsync(hist.p, 0, sizeof(int) * (maxc + 1), s));
+    launch_color_hist(s, NE, P->color.p, hist.p, maxc);
+    std::vector<int> hh(maxc + 1);
+    XFK_CHECK(d2h(hh.data(), hist.p, sizeof(int) * (maxc + 1), s));
+    XFK_REQUIRE(hh[maxc] == 0, XFK_ERR_UNSUPPORTED, "more than 128 element colours needed");
+    int nc = 0;
+    for (int c = 0; c < maxc; ++c)
+        if (hh[c]) nc = c + 1;
+    P->ncolors = nc;
+    P->color_off.assign(nc + 1, 0);
+    for (int c = 0; c < nc; ++c) P->color_off[c + 1] = P->color_off[c] + hh[c];
+
+    // stable sort of elements by colour -> perm (colour order -> raw element)
+    {
+        DBuf<int> keys_out, iota;
+        XFK_CHECK(keys_out.alloc(NE));
+        XFK_CHECK(iota.alloc(NE));
+        XFK_CHECK(P->perm.alloc(NE));
+        launch_iota(s, NE, iota.p);
+        void *tmp = nullptr;
+        size_t bytes = 0;
+        XFK_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, P->color.p, keys_out.p, iota.p, P->perm.p, NE,
+                                                     0, 8, s));
+        XFK_CHECK(hipMalloc(&tmp, bytes ? bytes : 1));
+        hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, bytes, P->color.p, keys_out.p, iota.p, P->perm.p,
+                                                          NE, 0, 8, s);
+        hipError_t e2 = hipStreamSynchronize(s);
+        (void)hipFree(tmp);
+        XFK_CHECK(e);
+        XFK_CHECK(e2);
+    }
+    XFK_CHECK(P->erec.alloc(NE));
+    XFK_CHECK(P->ebits.alloc(NE));
+    XFK_CHECK(P->slot.alloc(9 * (size_t)NE));
+    launch_build_erec(s, NE, P->perm.p, P->p_raw.p, P->lbl_raw.p, P->ebits_raw.p, P->erec.p, P->ebits.p);
+    XFK_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int), s));
+    launch_build_slots(s, NE, P->erec.p, P->rowptr.p, P->col.p, P->slot.p, cnt.p);
+    int bad = 0;
+    XFK_CHECK(d2h(&bad, cnt.p, sizeof(int), s));
+    XFK_REQUIRE(bad == 0, XFK_ERR_HIP, "internal: element slot missing from the CSR pattern");
+    XFK_CHECK(P->mu1.alloc(NE));
+    XFK_CHECK(P->mu2.alloc(NE));
+
+    // rows adjacent to fixed nodes
+    {
+        DBuf<int> flag;
+        XFK_CHECK(flag.alloc(N));
+        launch_mark_fix_adj(s, N, P->rowptr.p, P->col.p, P->fixed.p, flag.p);
+        XFK_CHECK(P->fix_cols_row.alloc(N));
+        XFK_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int), s));
+        launch_compact_flags(s, N, flag.p, cnt.p, P->fix_cols_row.p);
+        XFK_CHECK(d2h(&P->nfix_cols, cnt.p, sizeof(int), s));
+    }
+
+    // periodic averaging maps -> CSR slots
+    P->pm_n = 0;
+    P->pb_n = 0;
+    if (!P->pbc_entry_key.empty()) {
+        std::vector<int> rc_dst, dst_owner, src_rc, ptr{0};
+        std::vector<double> w;
+        for (size_t m = 0; m < P->pbc_entry_key.size(); ++m) {
+            long long k = P->pbc_entry_key[m];
+            int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
+            const Terms &tt = P->pbc_entry_terms[m];
+            // one gather entry per destination slot (both triangles)
+            int ndst = (r == c) ? 1 : 2;
+            for (int d = 0; d < ndst; ++d) {
+                rc_dst.push_back(d == 0 ? r : c);
+                rc_dst.push_back(d == 0 ? c : r);
+                for (auto &t : tt) {
+                    src_rc.push_back((int)(t.first >> 32));
+                    src_rc.push_back((int)(t.first & 0xffffffff));
+                    w.push_back(t.second);
+                }
+                ptr.push_back((int)w.size());
+            }
+        }
+        int nd = (int)rc_dst.size() / 2, ns = (int)w.size();
+        DBuf<int> d_rc, s_rc;
+        XFK_CHECK(upload(d_rc, rc_dst.data(), rc_dst.size(), s));
+        XFK_CHECK(upload(s_rc, src_rc.data(), src_rc.size(), s));
+        XFK_CHECK(P->pm_dst.alloc(nd));
+        XFK_CHECK(P->pm_src.alloc(ns ? ns : 1));
+        launch_lookup_slots(s, nd, d_rc.p, P->rowptr.p, P->col.p, P->pm_dst.p);
+        launch_lookup_slots(s, ns, s_rc.p, P->rowptr.p, P->col.p, P->pm_src.p);
+        XFK_CHECK(upload(P->pm_ptr, ptr.data(), ptr.size(), s));
+        XFK_CHECK(upload(P->pm_w, w.data(), w.size(), s));
+        XFK_CHECK(P->pm_tmp.alloc(nd));
+        XFK_CHECK(hipStreamSynchronize(s));
+        // every slot must exist
+        std::vector<int> chk(nd), chk2(ns);
+        XFK_CHECK(d2h(chk.data(), P->pm_dst.p, sizeof(int) * nd, s));
+        if (ns) XFK_CHECK(d2h(chk2.data(), P->pm_src.p, sizeof(int) * ns, s));
+        for (int v : chk) XFK_REQUIRE(v >= 0, XFK_ERR_HIP, "internal: periodic map slot missing");
+        for (int v : chk2) XFK_REQUIRE(v >= 0, XFK_ERR_HIP, "internal: periodic map source slot missing");
+        P->pm_n = nd;
+
+        std::vector<int> bd, bsrc, bptr{0};
+        std::vector<double> bw;
+        for (size_t m = 0; m < P->pbc_b_key.size(); ++m) {
+            bd.push_back(P->pbc_b_key[m]);
+            for (auto &t : P->pbc_b_terms[m]) {
+                bsrc.push_back(t.first);
+                bw.push_back(t.second);
+            }
+            bptr.push_back((int)bw.size());
+        }
+        XFK_CHECK(upload(P->pb_dst, bd.data(), bd.size(), s));
+        XFK_CHECK(upload(P->pb_src, bsrc.data(), bsrc.size(), s));
+        XFK_CHECK(upload(P->pb_ptr, bptr.data(), bptr.size(), s));
+        XFK_CHECK(upload(P->pb_w, bw.data(), bw.size(), s));
+        XFK_CHECK(P->pb_tmp.alloc(bd.size()));
+        XFK_CHECK(hipStreamSynchronize(s));
+        P->pb_n = (int)bd.size();
+    }
+
+    // vectors and reduction scratch
+    for (DBuf<double> *v : {&P->b, &P->V, &P->Vold, &P->R, &P->P, &P->U, &P->dinv}) XFK_CHECK(v->alloc(N));
+    XFK_CHECK(P->partials.alloc(2 * kRedGrid));
+    XFK_CHECK(P->counters.alloc(8));
+    XFK_CHECK(hipMemsetAsync(P->counters.p, 0, sizeof(unsigned) * 8, s));
+    XFK_CHECK(P->pcg.alloc(1));
+    XFK_CHECK(P->nws.alloc(1));
+    XFK_CHECK(hipStreamSynchronize(s));
+    P->symbolic_ready = true;
+    return XFK_OK;
+}
+
+// numeric assembly + boundary conditions for Newton iteration `iter`
+static int assemble(xfk_problem *P, int iter)
+{
+    hipStream_t s = P->stream;
+    XFK_CHECK(hipMemsetAsync(P->val.p, 0, sizeof(double) * P->nnz, s));
+    XFK_CHECK(hipMemsetAsync(P->b.p, 0, sizeof(double) * P->N, s));
+    AssembleArgs A;
+    A.erec = P->erec.p;
+    A.ebits = P->ebits.p;
+    A.slot = P->slot.p;
+    A.x = P->x.p;
+    A.y = P->y.p;
+    A.labels = P->labels.p;
+    A.blocks = P->blocks.p;
+    A.lines = P->lines.p;
+    A.circs = P->circs.p;
+    A.bhB = P->bhB.p;
+    A.bhH = P->bhH.p;
+    A.bhS = P->bhS.p;
+    A.mu1 = P->mu1.p;
+    A.mu2 = P->mu2.p;
+    A.V = P->V.p;
+    A.val = P->val.p;
+    A.b = P->b.p;
+    A.iter = iter;
+    for (int c = 0; c < P->ncolors; ++c) launch_assemble_color(s, P->color_off[c], P->color_off[c + 1], A);
+    launch_point_currents(s, P->npt, P->pt_nodes.p, P->pt_J.p, P->b.p);
+    launch_dirichlet(s, P->nfix_rows, P->fix_rows.p, P->nfix_cols, P->fix_cols_row.p, P->rowptr.p, P->col.p,
+                     P->diag.p, P->fixed.p, P->fix_first.p, P->fix_last.p, P->val.p, P->b.p);
+    launch_map(s, P->pm_n, P->pm_dst.p, P->pm_ptr.p, P->pm_src.p, P->pm_w.p, P->val.p, P->pm_tmp.p);
+    launch_map(s, P->pb_n, P->pb_dst.p, P->pb_ptr.p, P->pb_src.p, P->pb_w.p, P->b.p, P->pb_tmp.p);
+    XFK_CHECK(hipGetLastError());
+    return XFK_OK;
+}
+
+// CBigLinProb::PCGSolve(flag) on the assembled system (Jacobi-preconditioned)
+static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
+{
+    hipStream_t s = P->stream;
+    const int N = P->N;
+    PcgScalars init{};
+    init.tol = P->precision;
+    XFK_CHECK(hipMemcpyAsync(P->pcg.p, &init, sizeof(PcgScalars), hipMemcpyHostToDevice, s));
+    launch_diag_inv(s, N, P->diag.p, P->val.p, P->dinv.p, P->pcg.p);
+    XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(PcgScalars), hipMemcpyDeviceToHost, s));
+    XFK_CHECK(hipStreamSynchronize(s));
+    if (P->pcg_host->singular) {
+        set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
+        return XFK_ERR_SINGULAR;
+    }
+    launch_pcg_init(s, N, flag, P->rowptr.p, P->col.p, P->val.p, P->b.p, P->V.p, P->R.p, P->P.p, P->dinv.p,
+                    P->partials.p, P->counters.p, P->pcg.p);
+    long long launched = 0;
+    int batch = 16;
+    for (;;) {
+        for (int k = 0; k < batch; ++k) {
+            launch_pcg_spmv(s, N, P->rowptr.p, P->col.p, P->val.p, P->P.p, P->U.p, P->partials.p,
+                            P->counters.p + 1, P->pcg.p);
+            launch_pcg_update(s, N, P->V.p, P->R.p, P->P.p, P->U.p, P->dinv.p, P->partials.p, P->counters.p + 2,
+                              P->pcg.p);
+            launch_pcg_dir(s, N, P->R.p, P->dinv.p, P->P.p, P->pcg.p);
+        }
+        launched += batch;
+        XFK_CHECK(hipGetLastError());
+        XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(PcgScalars), hipMemcpyDeviceToHost, s));
+        XFK_CHECK(hipStreamSynchronize(s));
+        const PcgScalars &S = *P->pcg_host;
+        if (S.done) break;
+        if (launched >= max_iters) {
+            set_error("PCG did not converge within the iteration cap");
+            return XFK_ERR_NOCONV;
+        }
+        // size the next batch from the observed convergence rate
+        double rate = (S.iters > 0 && S.er > 0 && S.er < 1) ? std::log(S.er) / (double)S.iters : 0.0;
+        long long rem = rate < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / rate) : 2 * batch;
+        rem = std::max<long long>(8, std::min<long long>(rem + 2, 512));
+        batch = (int)rem;
+    }
+    return XFK_OK;
+}
+
+}  // namespace xfk
+
+using namespace xfk;
+
+extern "C" {
+
+const char *xfk_last_error(void) { return g_err.c_str(); }
+
+int xfk_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void xfk_problem_destroy(xfk_problem *P)
+{
+    if (!P) return;
+    (void)hipSetDevice(P->device);
+    if (P->stream) (void)hipStreamSynchronize(P->stream);
+    P->x.free(); P->y.free(); P->p_raw.free(); P->lbl_raw.free(); P->ebits_raw.free();
+    P->blocks.free(); P->labels.free(); P->lines.free(); P->circs.free();
+    P->bhB.free(); P->bhH.free(); P->bhS.free();
+    P->n2e_ptr.free(); P->n2e.free(); P->rowptr.free(); P->col.free(); P->diag.free();
+    P->color.free(); P->perm.free(); P->erec.free(); P->ebits.free(); P->slot.free();
+    P->mu1.free(); P->mu2.free();
+    P->pt_nodes.free(); P->pt_J.free(); P->fixed.free(); P->fix_first.free(); P->fix_last.free();
+    P->fix_rows.free(); P->fix_cols.free(); P->fix_cols_node.free(); P->fix_cols_row.free();
+    P->pm_dst.free(); P->pm_ptr.free(); P->pm_src.free(); P->pm_w.free(); P->pm_tmp.free();
+    P->pb_dst.free(); P->pb_ptr.free(); P->pb_src.free(); P->pb_w.free(); P->pb_tmp.free();
+    P->val.free(); P->b.free(); P->V.free(); P->Vold.free(); P->R.free(); P->P.free(); P->U.free();
+    P->dinv.free(); P->partials.free(); P->counters.free(); P->pcg.free(); P->nws.free();
+    if (P->pcg_host) (void)hipHostFree(P->pcg_host);
+    if (P->nws_host) (void)hipHostFree(P->nws_host);
+    if (P->stream) (void)hipStreamDestroy(P->stream);
+    delete P;
+}
+
+int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
+{
+    XFK_REQUIRE(d && out, XFK_ERR_ARG, "null argument");
+    *out = nullptr;
+    XFK_REQUIRE(d->n_nodes > 0 && d->n_elems > 0, XFK_ERR_ARG, "empty mesh");
+    XFK_REQUIRE(d->x && d->y && d->p && d->lbl, XFK_ERR_ARG, "missing mesh arrays");
+    XFK_REQUIRE(d->n_blocks > 0 && d->blocks && d->n_labels > 0 && d->labels, XFK_ERR_ARG,
+                "missing block or label tables");
+    XFK_REQUIRE(d->n_lines == 0 || d->lines, XFK_ERR_ARG, "missing boundary table");
+    XFK_REQUIRE(d->n_points == 0 || d->points, XFK_ERR_ARG, "missing point table");
+    XFK_REQUIRE(d->n_circs == 0 || d->circs, XFK_ERR_ARG, "missing circuit table");
+    XFK_REQUIRE(d->n_pbc == 0 || d->pbc, XFK_ERR_ARG, "missing pbc table");
+    XFK_REQUIRE(d->n_lines < 1023, XFK_ERR_UNSUPPORTED, "at most 1022 boundary properties");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        set_error("no HIP device available (the fsolver hot path has no CPU fallback)");
+        return XFK_ERR_HIP;
+    }
+    XFK_REQUIRE(device >= 0 && device < ndev, XFK_ERR_ARG, "device index out of range");
+
+    const int N = d->n_nodes, NE = d->n_elems;
+    for (long long i = 0; i < 3LL * NE; ++i)
+        XFK_REQUIRE(d->p[i] >= 0 && d->p[i] < N, XFK_ERR_ARG, "element node index out of range");
+    for (int i = 0; i < NE; ++i)
+        XFK_REQUIRE(d->lbl[i] >= 0 && d->lbl[i] < d->n_labels, XFK_ERR_ARG, "element label out of range");
+    for (int k = 0; k < d->n_labels; ++k) {
+        XFK_REQUIRE(d->labels[k].block >= 0 && d->labels[k].block < d->n_blocks, XFK_ERR_ARG,
+                    "label block index out of range");
+        XFK_REQUIRE(d->labels[k].in_circuit < d->n_circs, XFK_ERR_ARG, "label circuit index out of range");
+    }
+    for (int k = 0; k < d->n_blocks; ++k) {
+        const xfk_block_desc &b = d->blocks[k];
+        XFK_REQUIRE(b.BHpoints == 0 || (b.BHpoints >= 2 && b.B && b.H && b.slope), XFK_ERR_ARG,
+                    "B-H curve needs >= 2 points with slopes");
+    }
+    if (d->marker)
+        for (int i = 0; i < N; ++i)
+            XFK_REQUIRE(d->marker[i] < d->n_points, XFK_ERR_ARG, "node point-property index out of range");
+    if (d->e)
+        for (long long i = 0; i < 3LL * NE; ++i)
+            XFK_REQUIRE(d->e[i] < d->n_lines, XFK_ERR_ARG, "edge boundary-property index out of range");
+
+    xfk_problem *P = new xfk_problem();
+    P->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking) != hipSuccess) {
+        set_error("cannot initialise the HIP device/stream");
+        delete P;
+        return XFK_ERR_HIP;
+    }
+    auto fail = [&](int code) {
+        xfk_problem_destroy(P);
+        return code;
+    };
+    P->N = N;
+    P->NE = NE;
+    P->precision = d->precision;
+    P->relax = d->relax;
+    P->length_units = d->length_units;
+    P->coords = d->coords;
+    P->hx.assign(d->x, d->x + N);
+    P->hy.assign(d->y, d->y + N);
+    P->hp.assign(d->p, d->p + 3LL * NE);
+    P->hlbl.assign(d->lbl, d->lbl + NE);
+    P->hmarker.assign(N, -1);
+    if (d->marker) P->hmarker.assign(d->marker, d->marker + N);
+    P->he.assign(3LL * NE, -1);
+    if (d->e) P->he.assign(d->e, d->e + 3LL * NE);
+    if (d->n_pbc) P->hpbc.assign(d->pbc, d->pbc + 3LL * d->n_pbc);
+    P->hlines.assign(d->lines, d->lines + d->n_lines);
+    P->hpoints.assign(d->points, d->points + d->n_points);
+    const double c = kC;
+    const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
+    XFK_REQUIRE(d->length_units >= 0 && d->length_units < 6, fail(XFK_ERR_ARG), "bad length units");
+
+    // tables
+    std::vector<DevBlock> blk(d->n_blocks);
+    std::vector<double> hB, hH, hS;
+    for (int k = 0; k < d->n_blocks; ++k) {
+        const xfk_block_desc &b = d->blocks[k];
+        DevBlock &o = blk[k];
+        o.mu_x = b.mu_x; o.mu_y = b.mu_y; o.H_c = b.H_c; o.J_re = b.J_re; o.Cduct = b.Cduct;
+        o.LamFill = b.LamFill; o.LamType = b.LamType; o.BHpoints = b.BHpoints;
+        o.bh_off = (int)hB.size();
+        o.pad = 0;
+        for (int i = 0; i < b.BHpoints; ++i) {
+            hB.push_back(b.B[i]);
+            hH.push_back(b.H[i]);
+            hS.push_back(b.slope[i]);
+        }
+    }
+    if (hB.empty()) { hB.push_back(0); hH.push_back(0); hS.push_back(0); }
+    std::vector<DevLabel> lab(d->n_labels);
+    for (int k = 0; k < d->n_labels; ++k) {
+        const xfk_label_desc &l = d->labels[k];
+        double t = l.mag_dir;
+        lab[k].cos_m = cos(t * kPI / 180.);
+        lab[k].sin_m = sin(t * kPI / 180.);
+        lab[k].blk = l.block;
+        lab[k].in_circuit = l.in_circuit;
+        lab[k].is_wound = l.is_wound;
+        lab[k].pad = 0;
+    }
+    std::vector<DevLine> lin(std::max(1, d->n_lines));
+    for (int k = 0; k < d->n_lines; ++k) {
+        lin[k].c0 = d->lines[k].c0;
+        lin[k].c1 = d->lines[k].c1;
+        lin[k].format = d->lines[k].format;
+        lin[k].pad = 0;
+    }
+    // which elements are nonlinear -> LinearFlag (static2d.cpp:633-639)
+    for (int i = 0; i < NE && !P->any_nonlinear; ++i)
+        if (blk[lab[d->lbl[i]].blk].BHpoints != 0) P->any_nonlinear = true;
+
+    // circuits, element order (static2d.cpp:84-167)
+    std::vector<DevCirc> circ(std::max(1, d->n_circs));
+    if (d->n_circs > 0) {
+        std::vector<double> I1(d->n_circs, 0.0), I2(d->n_circs, 0.0), I3(d->n_circs, 0.0);
+        for (int i = 0; i < NE; ++i) {
+            const DevLabel &L = lab[d->lbl[i]];
+            if (L.in_circuit == -1) continue;
+            const int *n = d->p + 3LL * i;
+            double p0 = d->y[n[1]] - d->y[n[2]], p1 = d->y[n[2]] - d->y[n[0]];
+            double q0 = d->x[n[2]] - d->x[n[1]], q1 = d->x[n[0]] - d->x[n[2]];
+            double a = (p0 * q1 - p1 * q0) / 2.;
+            double Cduct = blk[L.blk].Cduct;
+            if (L.is_wound) Cduct = 0;
+            I1[L.in_circuit] += a;
+            I2[L.in_circuit] += a * Cduct;
+            I3[L.in_circuit] += blk[L.blk].J_re * a * 100.;
+        }
+        for (int k = 0; k < d->n_circs; ++k) {
+            DevCirc &C = circ[k];
+            C.amps_re = d->circs[k].amps_re;
+            C.dvolts_re = d->circs[k].dvolts_re;
+            C.type = d->circs[k].type;
+            C.J = 0; C.dV = 0; C.ccase = 0;
+            if (C.type == 0) {
+                if (I2[k] == 0) {
+                    C.ccase = 1;
+                    C.J = (I1[k] == 0.) ? 0. : 0.01 * (C.amps_re - I3[k]) / I1[k];
+                } else {
+                    C.ccase = 0;
+                    C.dV = -0.01 * (C.amps_re - I3[k]) / I2[k];
+                }
+            } else {
+                C.ccase = 0;
+                C.dV = C.dvolts_re;
+            }
+        }
+    }
+
+    // edges -> packed 3 x 10-bit boundary-property indices
+    std::vector<int> ebits(NE, 0);
+    for (int i = 0; i < NE; ++i)
+        for (int j = 0; j < 3; ++j) {
+            int ej = P->he[3LL * i + j];
+            if (ej >= 0) ebits[i] |= (ej + 1) << (10 * j);
+        }
+
+    // point currents and Dirichlet values in the reference's SetValue order
+    std::vector<int> pt_nodes;
+    std::vector<double> pt_J;
+    std::vector<unsigned char> fixed(N, 0);
+    std::vector<double> first(N, 0.0), last(N, 0.0);
+    auto set_value = [&](int i, double x) {
+        if (!fixed[i]) first[i] = x;
+        fixed[i] = 1;
+        last[i] = x;
+    };
+    for (int i = 0; i < N; ++i) {
+        int m = P->hmarker[i];
+        if (m >= 0 && d->points[m].J_re != 0.0) {
+            pt_nodes.push_back(i);
+            pt_J.push_back(0.01 * d->points[m].J_re);
+        }
+    }
+    for (int i = 0; i < N; ++i) {
+        int m = P->hmarker[i];
+        if (m >= 0 && d->points[m].J_re == 0 && d->points[m].J_im == 0) set_value(i, d->points[m].A_re / c);
+    }
+    for (int i = 0; i < NE; ++i)
+        for (int j = 0; j < 3; ++j) {
+            int k = (j + 1) % 3;
+            int sgi = P->he[3LL * i + j];
+            if (sgi < 0 || d->lines[sgi].format != 0) continue;
+            const xfk_line_desc &ln = d->lines[sgi];
+            int nodes2[2] = {d->p[3LL * i + j], d->p[3LL * i + k]};
+            for (int m = 0; m < 2; ++m) {
+                double x = d->x[nodes2[m]], y = d->y[nodes2[m]], a;
+                if (d->coords == 0) {
+                    x /= units[d->length_units];
+                    y /= units[d->length_units];
+                    a = ln.A0 + x * ln.A1 + y * ln.A2;
+                } else {
+                    double r = sqrt(x * x + y * y), t;
+                    if ((x == 0) && (y == 0)) t = 0;
+                    else t = atan2(y, x) / kDEG;
+                    r /= units[d->length_units];
+                    a = ln.A0 + r * ln.A1 + t * ln.A2;
+                }
+                a *= cos(ln.phi * kDEG);
+                set_value(nodes2[m], a / c);
+            }
+        }
+    std::vector<int> fix_rows;
+    for (int i = 0; i < N; ++i)
+        if (fixed[i]) fix_rows.push_back(i);
+    P->npt = (int)pt_nodes.size();
+    P->nfix_rows = (int)fix_rows.size();
+
+    int rc = build_pbc_map(P);
+    if (rc != XFK_OK) return fail(rc);
+
+    hipStream_t s = P->stream;
+    hipError_t e = hipSuccess;
+#define UP(buf, ptr, n) if (e == hipSuccess) e = upload(buf, ptr, n, s)
+    UP(P->x, d->x, (size_t)N);
+    UP(P->y, d->y, (size_t)N);
+    UP(P->p_raw, d->p, 3 * (size_t)NE);
+    UP(P->lbl_raw, d->lbl, (size_t)NE);
+    UP(P->ebits_raw, ebits.data(), (size_t)NE);
+    UP(P->blocks, blk.data(), blk.size());
+    UP(P->labels, lab.data(), lab.size());
+    UP(P->lines, lin.data(), lin.size());
+    UP(P->circs, circ.data(), circ.size());
+    UP(P->bhB, hB.data(), hB.size());
+    UP(P->bhH, hH.data(), hH.size());
+    UP(P->bhS, hS.data(), hS.size());
+    UP(P->pt_nodes, pt_nodes.data(), pt_nodes.size());
+    UP(P->pt_J, pt_J.data(), pt_J.size());
+    UP(P->fixed, fixed.data(), fixed.size());
+    UP(P->fix_first, first.data(), first.size());
+    UP(P->fix_last, last.data(), last.size());
+    UP(P->fix_rows, fix_rows.data(), fix_rows.size());
+#undef UP
+    if (e == hipSuccess) e = hipHostMalloc((void **)&P->pcg_host, sizeof(PcgScalars));
+    if (e == hipSuccess) e = hipHostMalloc((void **)&P->nws_host, sizeof(NewtonScalars));
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        set_error(std::string("upload failed: ") + hipGetErrorString(e));
+        return fail(XFK_ERR_HIP);
+    }
+    P->nblocks = d->n_blocks;
+    P->nlabels = d->n_labels;
+    P->nlines = d->n_lines;
+    P->ncircs = d->n_circs;
+    *out = P;
+    return XFK_OK;
+}
+
+int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
+{
+    XFK_REQUIRE(P, XFK_ERR_ARG, "null problem");
+    XFK_CHECK(hipSetDevice(P->device));
+    hipStream_t s = P->stream;
+    hipEvent_t e0, e1, e2;
+    XFK_CHECK(hipEventCreate(&e0));
+    XFK_CHECK(hipEventCreate(&e1));
+    XFK_CHECK(hipEventCreate(&e2));
+    xfk_result R{};
+    int rc = XFK_OK;
+    float ms = 0;
+    XFK_CHECK(hipEventRecord(e0, s));
+    if (!P->symbolic_ready || (flags & XFK_REBUILD_SYMBOLIC)) {
+        P->symbolic_ready = false;
+        rc = build_symbolic(P);
+        if (rc != XFK_OK) return rc;
+    }
+    XFK_CHECK(hipEventRecord(e1, s));
+    XFK_CHECK(hipEventSynchronize(e1));
+    XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    R.ms_symbolic = ms;
+
+    const int N = P->N;
+    XFK_CHECK(hipMemsetAsync(P->V.p, 0, sizeof(double) * N, s));   // CBigLinProb::Create: V = 0
+    double Relax = P->relax, resn = 0, lastres = 0;
+    int Iter = 0;
+    bool LinearFlag = !P->any_nonlinear;
+    const long long cap = std::max<long long>(100000, 20LL * N);
+    for (;;) {
+        XFK_CHECK(hipEventRecord(e0, s));
+        rc = assemble(P, Iter);
+        if (rc != XFK_OK) return rc;
+        XFK_CHECK(hipMemcpyAsync(P->Vold.p, P->V.p, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
+        XFK_CHECK(hipEventRecord(e1, s));
+        rc = pcg_solve(P, Iter, cap);
+        if (rc != XFK_OK) return rc;
+        XFK_CHECK(hipEventRecord(e2, s));
+        XFK_CHECK(hipEventSynchronize(e2));
+        XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        R.ms_assemble += ms;
+        XFK_CHECK(hipEventElapsedTime(&ms, e1, e2));
+        R.ms_solve += ms;
+        R.cg_iters += P->pcg_host->iters;
+        R.final_er = P->pcg_host->er;
+
+        if (!LinearFlag) {
+            launch_newton_res(s, N, P->V.p, P->Vold.p, P->partials.p, P->counters.p + 3, P->nws.p);
+            XFK_CHECK(hipMemcpyAsync(P->nws_host, P->nws.p, sizeof(NewtonScalars), hipMemcpyDeviceToHost, s));
+            XFK_CHECK(hipStreamSynchronize(s));
+            const double x = P->nws_host->dx2, y = P->nws_host->v2;
+            if (y == 0) LinearFlag = true;
+            else {
+                lastres = resn;
+                resn = sqrt(x / y);
+            }
+            if (Iter > 5) {
+                if ((resn > lastres) && (Relax > 0.125)) Relax /= 2.;
+                else Relax += 0.1 * (1. - Relax);
+                launch_relax(s, N, Relax, P->V.p, P->Vold.p);
+            }
+        }
+        if ((resn < 100. * P->precision) && (Iter > 0)) LinearFlag = true;
+        Iter++;
+        if (LinearFlag) break;
+        if (Iter > 10000) {
+            set_error("nonlinear iteration did not converge");
+            return XFK_ERR_NOCONV;
+        }
+    }
+    XFK_CHECK(hipStreamSynchronize(s));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(e2);
+    R.newton_iters = Iter;
+    R.last_res = resn;
+    R.nnz = P->nnz;
+    R.ncolors = P->ncolors;
+    P->last = R;
+    if (res) *res = R;
+    return XFK_OK;
+}
+
+int xfk_get_solution(xfk_problem *P, double *A)
+{
+    XFK_REQUIRE(P && A, XFK_ERR_ARG, "null argument");
+    XFK_REQUIRE(P->symbolic_ready, XFK_ERR_ARG, "no solution yet");
+    XFK_CHECK(hipSetDevice(P->device));
+    XFK_CHECK(hipMemcpyAsync(A, P->V.p, sizeof(double) * P->N, hipMemcpyDeviceToHost, P->stream));
+    XFK_CHECK(hipStreamSynchronize(P->stream));
+    for (int i = 0; i < P->N; ++i) A[i] = A[i] * kC;   // L.b[i] = L.V[i]*c (static2d.cpp:1018-1021)
+    return XFK_OK;
+}
+
+int xfk_get_circuits(xfk_problem *P, int *ccase, double *J, double *dV)
+{
+    XFK_REQUIRE(P, XFK_ERR_ARG, "null problem");
+    if (P->ncircs == 0) return XFK_OK;
+    std::vector<DevCirc> h(P->ncircs);
+    XFK_CHECK(d2h(h.data(), P->circs.p, sizeof(DevCirc) * P->ncircs, P->stream));
+    for (int k = 0; k < P->ncircs; ++k) {
+        if (ccase) ccase[k] = h[k].ccase;
+        if (J) J[k] = h[k].J;
+        if (dV) dV[k] = h[k].dV;
+    }
+    return XFK_OK;
+}
+
+long long xfk_get_nnz(xfk_problem *P) { return P ? P->nnz : -1; }
+
+int xfk_get_csr(xfk_problem *P, int *rowptr, int *col, double *val, double *b)
+{
+    XFK_REQUIRE(P && P->symbolic_ready, XFK_ERR_ARG, "no assembled system");
+    XFK_CHECK(hipSetDevice(P->device));
+    XFK_CHECK(hipStreamSynchronize(P->stream));
+    if (rowptr) XFK_CHECK(d2h(rowptr, P->rowptr.p, sizeof(int) * (P->N + 1), P->stream));
+    if (col) XFK_CHECK(d2h(col, P->col.p, sizeof(int) * P->nnz, P->stream));
+    if (val) XFK_CHECK(d2h(val, P->val.p, sizeof(double) * P->nnz, P->stream));
+    if (b) XFK_CHECK(d2h(b, P->b.p, sizeof(double) * P->N, P->stream));
+    return XFK_OK;
+}
+
+int xfk_get_stream(xfk_problem *P, void **st)
+{
+    XFK_REQUIRE(P && st, XFK_ERR_ARG, "null argument");
+    *st = (void *)P->stream;
+    return XFK_OK;
+}
+
+int xfk_pcg_solve_csr(int n, const int *rowptr, const int *col, const double *val, const double *b, double *V,
+                      int flag, double precision, int device, long long *iters, double *er)
+{
+    XFK_REQUIRE(n > 0 && rowptr && col && val && b && V, XFK_ERR_ARG, "null argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        set_error("no HIP device available (the fsolver hot path has no CPU fallback)");
+        return XFK_ERR_HIP;
+    }
+    XFK_CHECK(hipSetDevice(device));
+    xfk_problem *P = new xfk_problem();
+    P->device = device;
+    P->N = n;
+    P->nnz = rowptr[n];
+    P->precision = precision;
+    int rc = XFK_OK;
+    hipError_t e = hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking);
+    // diagonal positions
+    std::vector<int> diag(n, -1);
+    for (int i = 0; i < n; ++i)
+        for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
+            if (col[k] == i) diag[i] = k;
+    for (int i = 0; i < n && rc == XFK_OK; ++i)
+        if (diag[i] < 0) {
+            set_error("row without a diagonal entry");
+            rc = XFK_ERR_SINGULAR;
+        }
+    hipStream_t s = P->stream;
+    if (e == hipSuccess) e = upload(P->rowptr, rowptr, (size_t)n + 1, s);
+    if (e == hipSuccess) e = upload(P->col, col, (size_t)P->nnz, s);
+    if (e == hipSuccess) e = upload(P->val, val, (size_t)P->nnz, s);
+    if (e == hipSuccess) e = upload(P->b, b, (size_t)n, s);
+    if (e == hipSuccess) e = upload(P->V, V, (size_t)n, s);
+    if (e == hipSuccess) e = upload(P->diag, diag.data(), (size_t)n, s);
+    for (DBuf<double> *v : {&P->R, &P->P, &P->U, &P->dinv})
+        if (e == hipSuccess) e = v->alloc(n);
+    if (e == hipSuccess) e = P->partials.alloc(2 * kRedGrid);
+    if (e == hipSuccess) e = P->counters.alloc(8);
+    if (e == hipSuccess) e = hipMemsetAsync(P->counters.p, 0, sizeof(unsigned) * 8, s);
+    if (e == hipSuccess) e = P->pcg.alloc(1);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&P->pcg_host, sizeof(PcgScalars));
+    if (e != hipSuccess) {
+        set_error(std::string("pcg setup failed: ") + hipGetErrorString(e));
+        rc = XFK_ERR_HIP;
+    }
+    if (rc == XFK_OK) rc = pcg_solve(P, flag, std::max<long long>(100000, 20LL * n));
+    if (rc == XFK_OK || rc == XFK_ERR_NOCONV) {
+        if (d2h(V, P->V.p, sizeof(double) * n, P->stream) != hipSuccess) rc = XFK_ERR_HIP;
+        if (iters) *iters = P->pcg_host->iters;
+        if (er) *er = P->pcg_host->er;
+    }
+    xfk_problem_destroy(P);
+    return rc;
+}
+
+int xfk_pcg_time(xfk_problem *P, int iters, double *ms_spmv, double *ms_iter)
+{
+    XFK_REQUIRE(P && P->symbolic_ready && iters > 0, XFK_ERR_ARG, "no assembled system");
+    XFK_CHECK(hipSetDevice(P->device));
+    hipStream_t s = P->stream;
+    const int N = P->N;
+    PcgScalars init{};
+    init.tol = 0.0;   // never converges: fixed iteration count
+    XFK_CHECK(hipMemcpyAsync(P->pcg.p, &init, sizeof(PcgScalars), hipMemcpyHostToDevice, s));
+    launch_diag_inv(s, N, P->diag.p, P->val.p, P->dinv.p, P->pcg.p);
+    launch_pcg_init(s, N, 1, P->rowptr.p, P->col.p, P->val.p, P->b.p, P->V.p, P->R.p, P->P.p, P->dinv.p,
+                    P->partials.p, P->counters.p, P->pcg.p);
+    std::vector<hipEvent_t> ev(2 * iters + 2);
+    for (auto &x : ev) XFK_CHECK(hipEventCreate(&x));
+    XFK_CHECK(hipEventRecord(ev[2 * iters], s));
+    for (int k = 0; k < iters; ++k) {
+        XFK_CHECK(hipEventRecord(ev[2 * k], s));
+        launch_pcg_spmv(s, N, P->rowptr.p, P->col.p, P->val.p, P->P.p, P->U.p, P->partials.p, P->counters.p + 1,
+                        P->pcg.p);
+        XFK_CHECK(hipEventRecord(ev[2 * k + 1], s));
+        launch_pcg_update(s, N, P->V.p, P->R.p, P->P.p, P->U.p, P->dinv.p, P->partials.p, P->counters.p + 2,
+                          P->pcg.p);
+        launch_pcg_dir(s, N, P->R.p, P->dinv.p, P->P.p, P->pcg.p);
+    }
+    XFK_CHECK(hipEventRecord(ev[2 * iters + 1], s));
+    XFK_CHECK(hipEventSynchronize(ev[2 * iters + 1]));
+    double sum = 0;
+    for (int k = 0; k < iters; ++k) {
+        float m = 0;
+        XFK_CHECK(hipEventElapsedTime(&m, ev[2 * k], ev[2 * k + 1]));
+        sum += m;
+    }
+    float tot = 0;
+    XFK_CHECK(hipEventElapsedTime(&tot, ev[2 * iters], ev[2 * iters + 1]));
+    for (auto &x : ev) (void)hipEventDestroy(x);
+    if (ms_spmv) *ms_spmv = sum / iters;
+    if (ms_iter) *ms_iter = tot / iters;
+    return XFK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,923 @@
+// HIP kernels of the fsolver static-2D hot path for MI355X (gfx950, CDNA4).
+//
+// Reference behaviour (temudschin/xfemm): FSolver::Static2D
+// (cfemm/fsolver/static2d.cpp:53-1033) and CBigLinProb (cfemm/libfemm/spars.cpp).
+// Design notes are in DESIGN.md; the host driver is xfk_api.hip.
+//
+// Conventions: 256-thread workgroups (4 waves of 64), f64 arithmetic (the
+// reference is double), grid-wide reductions are deterministic two-level sums
+// (wave shuffle -> LDS -> per-block partial -> last-arriving block sums the
+// partials in block order).  The last-block hand-off follows the
+// sc1-store / relaxed-ticket / sc1-load form of cdna_hip_programming.md
+// Guideline 16 (no L2 write-back fences on the hot path).
+#include "xfk_kernels.h"
+
+namespace xfk {
+
+// --------------------------------------------------------------------------
+// reduction helpers
+// --------------------------------------------------------------------------
+
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Sum over the workgroup; result valid in thread 0.  `lds` holds >= 4 doubles.
+__device__ __forceinline__ double block_sum(double v, double *lds)
+{
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) lds[wid] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) {
+        const int nw = (blockDim.x + 63) >> 6;
+        for (int w = 0; w < nw; ++w) r += lds[w];
+    }
+    return r;
+}
+
+// Publish NV per-block partial sums and decide whether this block arrived
+// last.  Returns true in every thread of the last block, which may then read
+// all partials with sc1 loads (ticket form, Guideline 16 table row 1).
+template <int NV>
+__device__ __forceinline__ bool publish_partials(const double (&v)[NV], double *partials,
+                                                 unsigned *counter, int *lds_flag)
+{
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+            __hip_atomic_store(&partials[k * gridDim.x + blockIdx.x], v[k], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *lds_flag = (t == gridDim.x - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    return *lds_flag != 0;
+}
+
+// In the last block: sum partials k of all blocks in block order (result in thread 0).
+__device__ __forceinline__ double gather_partials(const double *partials, int k, double *lds)
+{
+    double s = 0.0;
+    const int G = gridDim.x;
+    // fixed per-thread strided order -> deterministic
+    for (int i = threadIdx.x; i < G; i += blockDim.x)
+        s += __hip_atomic_load(&partials[k * G + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return block_sum(s, lds);
+}
+
+__device__ __forceinline__ void reset_counter(unsigned *counter)
+{
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// --------------------------------------------------------------------------
+// symbolic phase: node->element lists, CSR pattern, colouring, slot maps
+// --------------------------------------------------------------------------
+
+__global__ void k_count_incidence(int NE, const int *__restrict__ p, int *__restrict__ deg)
+{
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= NE) return;
+    atomicAdd(&deg[p[3 * e + 0]], 1);
+    atomicAdd(&deg[p[3 * e + 1]], 1);
+    atomicAdd(&deg[p[3 * e + 2]], 1);
+}
+
+__global__ void k_fill_n2e(int NE, const int *__restrict__ p, const int *__restrict__ ptr,
+                           int *__restrict__ cursor, int *__restrict__ n2e)
+{
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= NE) return;
+    for (int j = 0; j < 3; ++j) {
+        int v = p[3 * e + j];
+        int pos = atomicAdd(&cursor[v], 1);
+        n2e[ptr[v] + pos] = e;
+    }
+}
+
+// Deterministic order of each node's element list (insertion sort, lists are short).
+__global__ void k_sort_segments(int N, const int *__restrict__ ptr, int *__restrict__ a)
+{
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= N) return;
+    int s = ptr[v], e = ptr[v + 1];
+    for (int i = s + 1; i < e; ++i) {
+        int key = a[i];
+        int j = i - 1;
+        while (j >= s && a[j] > key) {
+            a[j + 1] = a[j];
+            --j;
+        }
+        a[j + 1] = key;
+    }
+}
+
+// Candidate column t of row v: vertices of incident elements, then fill-ins, then v.
+struct RowCands {
+    const int *p, *n2e_ptr, *n2e, *fill_ptr, *fill_col;
+    __device__ __forceinline__ int count(int v) const
+    {
+        int ne = n2e_ptr[v + 1] - n2e_ptr[v];
+        int nf = fill_ptr ? (fill_ptr[v + 1] - fill_ptr[v]) : 0;
+        return 3 * ne + nf + 1;
+    }
+    __device__ __forceinline__ int get(int v, int t) const
+    {
+        int ne = n2e_ptr[v + 1] - n2e_ptr[v];
+        if (t < 3 * ne) return p[3 * n2e[n2e_ptr[v] + t / 3] + (t % 3)];
+        t -= 3 * ne;
+        int nf = fill_ptr ? (fill_ptr[v + 1] - fill_ptr[v]) : 0;
+        if (t < nf) return fill_col[fill_ptr[v] + t];
+        return v;
+    }
+};
+
+__global__ void k_row_count(int N, RowCands rc, int *__restrict__ rowcnt)
+{
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= N) return;
+    int m = rc.count(v), u = 0;
+    for (int t = 0; t < m; ++t) {
+        int c = rc.get(v, t);
+        bool seen = false;
+        for (int s = 0; s < t && !seen; ++s) seen = (rc.get(v, s) == c);
+        u += seen ? 0 : 1;
+    }
+    rowcnt[v] = u;
+}
+
+__global__ void k_row_fill(int N, RowCands rc, const int *__restrict__ rowptr, int *__restrict__ col,
+                           int *__restrict__ diag)
+{
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= N) return;
+    int base = rowptr[v], len = 0;
+    int m = rc.count(v);
+    for (int t = 0; t < m; ++t) {
+        int c = rc.get(v, t);
+        // insertion into the sorted row, skipping duplicates
+        int j = len - 1;
+        bool dup = false;
+        for (int s = 0; s < len; ++s)
+            if (col[base + s] == c) { dup = true; break; }
+        if (dup) continue;
+        while (j >= 0 && col[base + j] > c) {
+            col[base + j + 1] = col[base + j];
+            --j;
+        }
+        col[base + j + 1] = c;
+        ++len;
+    }
+    for (int s = 0; s < len; ++s)
+        if (col[base + s] == v) diag[v] = base + s;
+}
+
+__device__ __forceinline__ unsigned hash_u32(unsigned x)
+{
+    x ^= x >> 16; x *= 0x7feb352dU;
+    x ^= x >> 15; x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+// One Jones-Plassmann round: an uncoloured element whose (hash, index)
+// priority beats every uncoloured element sharing a node with it takes the
+// smallest colour unused by its coloured neighbours.
+__global__ void k_color_round(int NE, const int *__restrict__ p, const int *__restrict__ n2e_ptr,
+                              const int *__restrict__ n2e, int *__restrict__ color,
+                              int *__restrict__ ncolored)
+{
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= NE) return;
+    if (color[e] >= 0) return;
+    const unsigned he = hash_u32((unsigned)e);
+    unsigned long long used0 = 0, used1 = 0;
+    for (int j = 0; j < 3; ++j) {
+        int v = p[3 * e + j];
+        for (int t = n2e_ptr[v]; t < n2e_ptr[v + 1]; ++t) {
+            int f = n2e[t];
+            if (f == e) continue;
+            int cf = __hip_atomic_load(&color[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cf < 0) {
+                unsigned hf = hash_u32((unsigned)f);
+                if (hf > he || (hf == he && f > e)) return;
+            } else if (cf < 64) {
+                used0 |= 1ull << cf;
+            } else if (cf < 128) {
+                used1 |= 1ull << (cf - 64);
+            }
+        }
+    }
+    int c;
+    if (~used0) c = __ffsll((long long)~used0) - 1;
+    else if (~used1) c = 64 + __ffsll((long long)~used1) - 1;
+    else c = 1000;  // > 128 colours: flagged by the host
+    __hip_atomic_store(&color[e], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    atomicAdd(ncolored, 1);
+}
+
+__global__ void k_color_hist(int NE, const int *__restrict__ color, int *__restrict__ hist, int maxc)
+{
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= NE) return;
+    int c = color[e];
+    atomicAdd(&hist[c < maxc ? c : maxc], 1);
+}
+
+__global__ void k_iota(int n, int *__restrict__ a)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = i;
+}
+
+__global__ void k_build_erec(int NE, const int *__restrict__ perm, const int *__restrict__ p,
+                             const int *__restrict__ lbl, const int *__restrict__ ebits_raw,
+                             int4 *__restrict__ erec, int *__restrict__ ebits)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= NE) return;
+    int e = perm[i];
+    erec[i] = make_int4(p[3 * e], p[3 * e + 1], p[3 * e + 2], lbl[e]);
+    ebits[i] = ebits_raw[e];
+}
+
+__device__ __forceinline__ int find_slot(const int *__restrict__ rowptr, const int *__restrict__ col,
+                                         int r, int c)
+{
+    int lo = rowptr[r], hi = rowptr[r + 1] - 1;
+    while (lo <= hi) {
+        int mid = (lo + hi) >> 1;
+        int v = col[mid];
+        if (v == c) return mid;
+        if (v < c) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    return -1;
+}
+
+__global__ void k_build_slots(int NE, const int4 *__restrict__ erec, const int *__restrict__ rowptr,
+                              const int *__restrict__ col, int *__restrict__ slot, int *__restrict__ bad)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= NE) return;
+    int4 r = erec[i];
+    int n[3] = {r.x, r.y, r.z};
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            int s = find_slot(rowptr, col, n[j], n[k]);
+            if (s < 0) atomicAdd(bad, 1);
+            slot[9 * i + 3 * j + k] = s;
+        }
+}
+
+// (row, col) pairs -> CSR slots (periodic-map preparation)
+__global__ void k_lookup_slots(int n, const int *__restrict__ rc, const int *__restrict__ rowptr,
+                               const int *__restrict__ col, int *__restrict__ out)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = find_slot(rowptr, col, rc[2 * i], rc[2 * i + 1]);
+}
+
+// rows that hold a fixed (Dirichlet) column but are not fixed themselves
+__global__ void k_mark_fix_adj(int N, const int *__restrict__ rowptr, const int *__restrict__ col,
+                               const unsigned char *__restrict__ fixed, int *__restrict__ flag)
+{
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    int f = 0;
+    if (!fixed[r])
+        for (int k = rowptr[r]; k < rowptr[r + 1]; ++k) f |= fixed[col[k]];
+    flag[r] = f;
+}
+
+__global__ void k_compact_flags(int N, const int *__restrict__ flag, int *__restrict__ cursor,
+                                int *__restrict__ out)
+{
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N || !flag[r]) return;
+    out[atomicAdd(cursor, 1)] = r;
+}
+
+// --------------------------------------------------------------------------
+// numeric assembly (static2d.cpp:352-816), one launch per colour
+// --------------------------------------------------------------------------
+
+// CMSolverMaterialProp::GetBHProps (CMaterialProp.cpp:997-1057), real axis.
+__device__ void get_bh_props(const DevBlock &m, const double *__restrict__ Bt, const double *__restrict__ Ht,
+                             const double *__restrict__ St, double B, double &v, double &dv)
+{
+    const double b = fabs(B);
+    const int n = m.BHpoints;
+    const double *Bd = Bt + m.bh_off, *Hd = Ht + m.bh_off, *sl = St + m.bh_off;
+    if (b == 0) { v = sl[0]; dv = 0; return; }
+    if (b > Bd[n - 1]) {
+        double h = (Hd[n - 1] + sl[n - 1] * (b - Bd[n - 1]));
+        double dh = sl[n - 1];
+        v = h / b;
+        dv = 0.5 * (dh / (b * b) - h / (b * b * b));
+        return;
+    }
+    for (int i = 0; i < n - 1; ++i)
+        if ((b >= Bd[i]) && (b <= Bd[i + 1])) {
+            double l = (Bd[i + 1] - Bd[i]);
+            double z = (b - Bd[i]) / l;
+            double z2 = z * z;
+            double h = (1. - 3. * z2 + 2. * z2 * z) * Hd[i] + z * (1. - 2. * z + z2) * l * sl[i] +
+                       z2 * (3. - 2. * z) * Hd[i + 1] + z2 * (z - 1.) * l * sl[i + 1];
+            double dh = 6. * z * (z - 1.) * Hd[i] / l + (1. - 4. * z + 3. * z * z) * sl[i] +
+                        6. * z * (1. - z) * Hd[i + 1] / l + z * (3. * z - 2.) * sl[i + 1];
+            v = h / b;
+            dv = 0.5 * (dh / (b * b) - h / (b * b * b));
+            return;
+        }
+}
+
+// AssembleArgs: see xfk_kernels.h
+
+__global__ void __launch_bounds__(kBlock) k_assemble_color(int begin, int end, AssembleArgs A)
+{
+    // LDS-staged element -> CSR slot maps: the tile's 9-int records are one
+    // contiguous span, loaded coalesced and read back per element.
+    __shared__ int s_slot[kBlock * 9 + kBlock / 8];
+    const int tile0 = begin + blockIdx.x * kBlock;
+    const int ntile = min(kBlock, end - tile0);
+    if (ntile <= 0) return;
+    for (int k = threadIdx.x; k < ntile * 9; k += kBlock) {
+        int e = k / 9;
+        s_slot[k + (e >> 3)] = A.slot[(size_t)tile0 * 9 + k];   // pad one int per 8 records
+    }
+    __syncthreads();
+    const int li = threadIdx.x;
+    if (li >= ntile) return;
+    const int i = tile0 + li;
+    const int4 r = A.erec[i];
+    const int n[3] = {r.x, r.y, r.z};
+    const DevLabel lab = A.labels[r.w];
+    const DevBlock bp = A.blocks[lab.blk];
+    const double X[3] = {A.x[n[0]], A.x[n[1]], A.x[n[2]]};
+    const double Y[3] = {A.y[n[0]], A.y[n[1]], A.y[n[2]]};
+
+    double p[3], q[3];
+    p[0] = Y[1] - Y[2]; p[1] = Y[2] - Y[0]; p[2] = Y[0] - Y[1];
+    q[0] = X[2] - X[1]; q[1] = X[0] - X[2]; q[2] = X[1] - X[0];
+    const double a = (p[0] * q[1] - p[1] * q[0]) / 2.;
+    const double K = (-1. / (4. * a));
+    double Mx[3][3], My[3][3], Me[3][3], Mn[3][3], be[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            Mx[j][k] = K * p[j] * p[k];
+            My[j][k] = K * q[j] * q[k];
+            Me[j][k] = 0.;
+            Mn[j][k] = 0.;
+        }
+        be[j] = 0.;
+    }
+
+    // mixed boundary conditions on the element's edges (static2d.cpp:459-480)
+    const int eb = A.ebits[i];
+    if (eb) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            int ej = ((eb >> (10 * j)) & 1023) - 1;
+            if (ej < 0) continue;
+            const DevLine ln = A.lines[ej];
+            if (ln.format != 2) continue;
+            int k = (j + 1) % 3;
+            double lj = sqrt(pow(X[k] - X[j], 2.) + pow(Y[k] - Y[j], 2.));
+            double Kb = -0.0001 * kC * ln.c0 * lj / 6.;
+            Me[j][j] += Kb * 2.;
+            Me[k][k] += Kb * 2.;
+            Me[j][k] += Kb;
+            Me[k][j] += Kb;
+            Kb = (ln.c1 * lj / 2.) * 0.0001;
+            be[j] += Kb;
+            be[k] += Kb;
+        }
+    }
+
+    // source current density (static2d.cpp:482-507)
+    double t = 0;
+    if (lab.in_circuit >= 0) {
+        const DevCirc C = A.circs[lab.in_circuit];
+        if (C.ccase == 1) t = C.J;
+        if (C.ccase == 0) t = -C.dV * bp.Cduct;
+    }
+    const double Ks = -(bp.J_re + t) * a / 3.;
+    be[0] += Ks; be[1] += Ks; be[2] += Ks;
+
+    // magnetisation (static2d.cpp:584-598)
+    if (bp.H_c != 0.0) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            int k = (j + 1) % 3;
+            double Km = 0.0001 * bp.H_c * (lab.cos_m * (X[k] - X[j]) + lab.sin_m * (Y[k] - Y[j])) / 2.;
+            be[j] += Km;
+            be[k] += Km;
+        }
+    }
+
+    // permeability (static2d.cpp:600-797)
+    double m1, m2;
+    const double Vn[3] = {A.V[n[0]], A.V[n[1]], A.V[n[2]]};
+    if (A.iter == 0) {
+        const double f = bp.LamFill;
+        if (bp.LamType == 0) { m1 = bp.mu_x * f + (1. - f); m2 = bp.mu_y * f + (1. - f); }
+        else if (bp.LamType == 1) { m1 = bp.mu_x * f + (1. - f); m2 = bp.mu_x / (f + bp.mu_x * (1. - f)); }
+        else if (bp.LamType == 2) { m2 = bp.mu_y * f + (1. - f); m1 = bp.mu_y / (f + bp.mu_y * (1. - f)); }
+        else { m1 = 1; m2 = 1; }
+        A.mu1[i] = m1;
+        A.mu2[i] = m2;
+    } else {
+        m1 = A.mu1[i];
+        m2 = A.mu2[i];
+        if (bp.BHpoints > 0 && bp.LamType <= 2 && (bp.LamType != 0 || m1 == m2)) {
+            const double f = bp.LamFill;
+            double B1 = 0., B2 = 0.;
+            if (bp.LamType == 0) {
+                for (int j = 0; j < 3; ++j) { B1 += Vn[j] * q[j]; B2 += Vn[j] * p[j]; }
+            } else if (bp.LamType == 1) {
+                for (int j = 0; j < 3; ++j) { B1 += Vn[j] * q[j]; B2 += Vn[j] * p[j] / f; }
+            } else {
+                for (int j = 0; j < 3; ++j) { B1 += (Vn[j] * q[j]) / f; B2 += Vn[j] * p[j]; }
+            }
+            const double B = kC * sqrt(B1 * B1 + B2 * B2) / (0.02 * a);
+            double mu = 0, dv = 0;
+            get_bh_props(bp, A.bhB, A.bhH, A.bhS, B, mu, dv);
+            mu = 1. / (kMUO * mu);
+            double v[3], u[3];
+            if (bp.LamType == 0) {
+                m1 = mu; m2 = mu;
+                for (int j = 0; j < 3; ++j) {
+                    v[j] = 0;
+                    for (int w = 0; w < 3; ++w) v[j] += (Mx[j][w] + My[j][w]) * Vn[w];
+                }
+                const double Kn = -200. * kC * kC * kC * dv / a;
+                for (int j = 0; j < 3; ++j)
+                    for (int w = 0; w < 3; ++w) Mn[j][w] = Kn * v[j] * v[w];
+            } else {
+                if (bp.LamType == 1) { m1 = mu * f; m2 = mu / (f + mu * (1. - f)); }
+                else { m2 = mu * f; m1 = mu / (f + mu * (1. - f)); }
+                for (int j = 0; j < 3; ++j) {
+                    v[j] = 0; u[j] = 0;
+                    for (int w = 0; w < 3; ++w) {
+                        if (bp.LamType == 1) {
+                            v[j] += (My[j][w] / f + Mx[j][w]) * Vn[w];
+                            u[j] += (My[j][w] / f + f * Mx[j][w]) * Vn[w];
+                        } else {
+                            v[j] += (Mx[j][w] / f + My[j][w]) * Vn[w];
+                            u[j] += (Mx[j][w] / f + f * My[j][w]) * Vn[w];
+                        }
+                    }
+                }
+                const double Kn = -100. * kC * kC * kC * dv / (a);
+                for (int j = 0; j < 3; ++j)
+                    for (int w = 0; w < 3; ++w) Mn[j][w] = Kn * (v[j] * u[w] + v[w] * u[j]);
+            }
+            A.mu1[i] = m1;
+            A.mu2[i] = m2;
+        }
+    }
+
+    // element matrix, v12 == 0 outside incremental problems (static2d.cpp:799-805)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            Me[j][k] += (Mx[j][k] / m2 + My[j][k] / m1 + Mn[j][k]);
+            be[j] += Mn[j][k] * Vn[k];
+        }
+
+    // colour-exclusive scatter: no other element of this launch touches n[*]
+    const int *sl = &s_slot[li * 9 + (li >> 3)];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double m = (k >= j) ? Me[j][k] : Me[k][j];   // upper value, exact symmetry
+            A.val[sl[3 * j + k]] -= m;
+        }
+        A.b[n[j]] -= be[j];
+    }
+}
+
+// point currents (static2d.cpp:818-825)
+__global__ void k_point_currents(int n, const int *__restrict__ nodes, const double *__restrict__ J,
+                                 double *__restrict__ b)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) b[nodes[i]] += J[i];
+}
+
+// CBigLinProb::SetValue (spars.cpp:318-346) for every fixed node: its row
+// keeps only the diagonal, b = diag * value (last value set wins)
+__global__ void k_dirichlet_rows(int n, const int *__restrict__ rows, const int *__restrict__ rowptr,
+                                 const int *__restrict__ diag, double *__restrict__ val,
+                                 double *__restrict__ b, const double *__restrict__ fix_last)
+{
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    int r = rows[t];
+    int d = diag[r];
+    for (int k = rowptr[r]; k < rowptr[r + 1]; ++k)
+        if (k != d) val[k] = 0.0;
+    b[r] = val[d] * fix_last[r];
+}
+
+// the column half of SetValue: b[k] -= A(k,i)*x_i, A(k,i) = 0 (first value set)
+__global__ void k_dirichlet_cols(int n, const int *__restrict__ rows, const int *__restrict__ rowptr,
+                                 const int *__restrict__ col, const unsigned char *__restrict__ fixed,
+                                 const double *__restrict__ fix_first, double *__restrict__ val,
+                                 double *__restrict__ b)
+{
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    int r = rows[t];
+    double br = b[r];
+    for (int k = rowptr[r]; k < rowptr[r + 1]; ++k) {
+        int c = col[k];
+        if (fixed[c]) {
+            double z = val[k];
+            if (z != 0) {
+                br = br - (z * fix_first[c]);
+                val[k] = 0.0;
+            }
+        }
+    }
+    b[r] = br;
+}
+
+// (anti)periodic averaging map (CBigLinProb::Periodicity / AntiPeriodicity,
+// spars.cpp:366-474, composed on the host): dst <- sum w * src, two phases
+__global__ void k_map_gather(int n, const int *__restrict__ ptr, const int *__restrict__ src,
+                             const double *__restrict__ w, const double *__restrict__ data,
+                             double *__restrict__ tmp)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s = 0.0;
+    for (int k = ptr[i]; k < ptr[i + 1]; ++k) s += w[k] * data[src[k]];
+    tmp[i] = s;
+}
+
+__global__ void k_map_scatter(int n, const int *__restrict__ dst, const double *__restrict__ tmp,
+                              double *__restrict__ data)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) data[dst[i]] = tmp[i];
+}
+
+// Jacobi preconditioner + the reference's singularity check (spars.cpp:245)
+__global__ void k_diag_inv(int N, const int *__restrict__ diag, const double *__restrict__ val,
+                           double *__restrict__ dinv, PcgScalars *__restrict__ S)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    double d = val[diag[i]];
+    if (d == 0.0) {
+        S->singular = 1;
+        dinv[i] = 0.0;
+    } else {
+        dinv[i] = 1.0 / d;
+    }
+}
+
+// --------------------------------------------------------------------------
+// PCG (CBigLinProb::PCGSolve, spars.cpp:238-316) with the Jacobi
+// preconditioner M = diag(A).  Three launches per iteration, each ending in a
+// deterministic grid reduction whose last block updates the scalars.
+// --------------------------------------------------------------------------
+
+constexpr int kTileRows = kBlock;        // rows per LDS row tile
+constexpr int kTileCap = 2048;           // products staged per pass (16 KiB of f64)
+
+// y = A x for the rows of one tile, CSR-stream: the tile's nonzeros are read
+// coalesced (val, col), multiplied by the gathered x and staged in LDS; each
+// thread then reduces its own row from LDS.
+__device__ __forceinline__ double tile_spmv_row(int r0, int N, const int *__restrict__ rowptr,
+                                                const int *__restrict__ col,
+                                                const double *__restrict__ val,
+                                                const double *__restrict__ x, double *lds)
+{
+    const int r = r0 + threadIdx.x;
+    const int rend = min(r0 + kTileRows, N);
+    const int s = rowptr[r0], e = rowptr[rend];
+    const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
+    double acc = 0.0;
+    for (int c0 = s; c0 < e; c0 += kTileCap) {
+        const int c1 = min(e, c0 + kTileCap);
+        for (int k = c0 + threadIdx.x; k < c1; k += kBlock) lds[k - c0] = val[k] * x[col[k]];
+        __syncthreads();
+        const int a = max(my_s, c0), z = min(my_e, c1);
+        for (int k = a; k < z; ++k) acc += lds[k - c0];
+        __syncthreads();
+    }
+    return acc;
+}
+
+// R = b - A V (V = 0 when flag == 0), P = M^-1 R; partials z.r and (M^-1 b).b
+__global__ void __launch_bounds__(kBlock) k_pcg_init(int N, int flag, const int *__restrict__ rowptr,
+                                                     const int *__restrict__ col, const double *__restrict__ val,
+                                                     const double *__restrict__ b, double *__restrict__ V,
+                                                     double *__restrict__ R, double *__restrict__ P,
+                                                     const double *__restrict__ dinv, double *partials,
+                                                     unsigned *counter, PcgScalars *S)
+{
+    __shared__ double lds[kTileCap];
+    __shared__ double red[8];
+    __shared__ int last;
+    double zr = 0.0, zb = 0.0;
+    const int ntiles = (N + kTileRows - 1) / kTileRows;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int r0 = tile * kTileRows;
+        double ax = 0.0;
+        if (flag) ax = tile_spmv_row(r0, N, rowptr, col, val, V, lds);
+        const int r = r0 + threadIdx.x;
+        if (r < N) {
+            const double br = b[r], di = dinv[r];
+            const double rr = br - ax;
+            const double z = rr * di;
+            if (!flag) V[r] = 0.0;
+            R[r] = rr;
+            P[r] = z;
+            zr += z * rr;
+            zb += (br * di) * br;
+        }
+    }
+    double v[2];
+    v[0] = block_sum(zr, red);
+    v[1] = block_sum(zb, red);
+    if (publish_partials<2>(v, partials, counter, &last)) {
+        double a0 = gather_partials(partials, 0, red);
+        double a1 = gather_partials(partials, 1, red);
+        if (threadIdx.x == 0) {
+            S->res = a0;
+            S->res_o = a1;
+            S->iters = 0;
+            S->er = (a1 == 0.0) ? 0.0 : sqrt(a0 / a1);
+            S->done = (a1 == 0.0) ? 1 : 0;
+            reset_counter(counter);
+        }
+    }
+}
+
+// U = A P; partial P.U; last block: del = res / pAp
+__global__ void __launch_bounds__(kBlock) k_pcg_spmv(int N, const int *__restrict__ rowptr,
+                                                     const int *__restrict__ col, const double *__restrict__ val,
+                                                     const double *__restrict__ P, double *__restrict__ U,
+                                                     double *partials, unsigned *counter, PcgScalars *S)
+{
+    if (S->done) return;
+    __shared__ double lds[kTileCap];
+    __shared__ double red[8];
+    __shared__ int last;
+    double pu = 0.0;
+    const int ntiles = (N + kTileRows - 1) / kTileRows;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int r0 = tile * kTileRows;
+        double u = tile_spmv_row(r0, N, rowptr, col, val, P, lds);
+        const int r = r0 + threadIdx.x;
+        if (r < N) {
+            U[r] = u;
+            pu += P[r] * u;
+        }
+    }
+    double v[1];
+    v[0] = block_sum(pu, red);
+    if (publish_partials<1>(v, partials, counter, &last)) {
+        double s = gather_partials(partials, 0, red);
+        if (threadIdx.x == 0) {
+            S->del = S->res / s;
+            reset_counter(counter);
+        }
+    }
+}
+
+// V += del P; R -= del U; partial (M^-1 R).R; last block: rho, res, er, done
+__global__ void __launch_bounds__(kBlock) k_pcg_update(int N, double *__restrict__ V, double *__restrict__ R,
+                                                       const double *__restrict__ P, const double *__restrict__ U,
+                                                       const double *__restrict__ dinv, double *partials,
+                                                       unsigned *counter, PcgScalars *S)
+{
+    if (S->done) return;
+    __shared__ double red[8];
+    __shared__ int last;
+    const double del = S->del;
+    double zr = 0.0;
+    for (int r = blockIdx.x * kBlock + threadIdx.x; r < N; r += gridDim.x * kBlock) {
+        double v = V[r], rr = R[r];
+        v += (del * P[r]);
+        rr -= (del * U[r]);
+        V[r] = v;
+        R[r] = rr;
+        zr += (rr * dinv[r]) * rr;
+    }
+    double v[1];
+    v[0] = block_sum(zr, red);
+    if (publish_partials<1>(v, partials, counter, &last)) {
+        double s = gather_partials(partials, 0, red);
+        if (threadIdx.x == 0) {
+            S->rho = s / S->res;
+            S->res = s;
+            S->er = sqrt(s / S->res_o);
+            S->iters += 1;
+            if (S->er <= S->tol) S->done = 1;
+            reset_counter(counter);
+        }
+    }
+}
+
+// P = M^-1 R + rho P
+__global__ void __launch_bounds__(kBlock) k_pcg_dir(int N, const double *__restrict__ R,
+                                                    const double *__restrict__ dinv, double *__restrict__ P,
+                                                    const PcgScalars *S)
+{
+    if (S->done) return;
+    const double rho = S->rho;
+    for (int r = blockIdx.x * kBlock + threadIdx.x; r < N; r += gridDim.x * kBlock)
+        P[r] = R[r] * dinv[r] + (rho * P[r]);
+}
+
+// nonlinear residual sums (static2d.cpp:953-970)
+__global__ void __launch_bounds__(kBlock) k_newton_res(int N, const double *__restrict__ V,
+                                                       const double *__restrict__ Vold, double *partials,
+                                                       unsigned *counter, NewtonScalars *S)
+{
+    __shared__ double red[8];
+    __shared__ int last;
+    double dx = 0.0, vv = 0.0;
+    for (int r = blockIdx.x * kBlock + threadIdx.x; r < N; r += gridDim.x * kBlock) {
+        double v = V[r], d = v - Vold[r];
+        dx += d * d;
+        vv += v * v;
+    }
+    double v[2];
+    v[0] = block_sum(dx, red);
+    v[1] = block_sum(vv, red);
+    if (publish_partials<2>(v, partials, counter, &last)) {
+        double a0 = gather_partials(partials, 0, red);
+        double a1 = gather_partials(partials, 1, red);
+        if (threadIdx.x == 0) {
+            S->dx2 = a0;
+            S->v2 = a1;
+            reset_counter(counter);
+        }
+    }
+}
+
+__global__ void k_relax(int N, double relax, double *__restrict__ V, const double *__restrict__ Vold)
+{
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < N; r += gridDim.x * blockDim.x)
+        V[r] = relax * V[r] + (1.0 - relax) * Vold[r];
+}
+
+__global__ void k_scale(int N, double s, const double *__restrict__ V, double *__restrict__ out)
+{
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < N) out[r] = V[r] * s;
+}
+
+// --------------------------------------------------------------------------
+// launch wrappers (host side)
+// --------------------------------------------------------------------------
+
+static inline int nblk(long long n) { return (int)((n + kBlock - 1) / kBlock); }
+
+int grid_reduce(int N)
+{
+    int t = (N + kTileRows - 1) / kTileRows;
+    return t < kRedGrid ? (t > 0 ? t : 1) : kRedGrid;
+}
+
+void launch_count_incidence(hipStream_t s, int NE, const int *p, int *deg)
+{
+    if (NE) k_count_incidence<<<nblk(NE), kBlock, 0, s>>>(NE, p, deg);
+}
+void launch_fill_n2e(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e)
+{
+    if (NE) k_fill_n2e<<<nblk(NE), kBlock, 0, s>>>(NE, p, ptr, cursor, n2e);
+}
+void launch_sort_segments(hipStream_t s, int N, const int *ptr, int *a)
+{
+    if (N) k_sort_segments<<<nblk(N), kBlock, 0, s>>>(N, ptr, a);
+}
+void launch_row_count(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e,
+                      const int *fill_ptr, const int *fill_col, int *rowcnt)
+{
+    RowCands rc{p, n2e_ptr, n2e, fill_ptr, fill_col};
+    if (N) k_row_count<<<nblk(N), kBlock, 0, s>>>(N, rc, rowcnt);
+}
+void launch_row_fill(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e,
+                     const int *fill_ptr, const int *fill_col, const int *rowptr, int *col, int *diag)
+{
+    RowCands rc{p, n2e_ptr, n2e, fill_ptr, fill_col};
+    if (N) k_row_fill<<<nblk(N), kBlock, 0, s>>>(N, rc, rowptr, col, diag);
+}
+void launch_color_round(hipStream_t s, int NE, const int *p, const int *n2e_ptr, const int *n2e, int *color,
+                        int *ncolored)
+{
+    if (NE) k_color_round<<<nblk(NE), kBlock, 0, s>>>(NE, p, n2e_ptr, n2e, color, ncolored);
+}
+void launch_color_hist(hipStream_t s, int NE, const int *color, int *hist, int maxc)
+{
+    if (NE) k_color_hist<<<nblk(NE), kBlock, 0, s>>>(NE, color, hist, maxc);
+}
+void launch_iota(hipStream_t s, int n, int *a)
+{
+    if (n) k_iota<<<nblk(n), kBlock, 0, s>>>(n, a);
+}
+void launch_build_erec(hipStream_t s, int NE, const int *perm, const int *p, const int *lbl, const int *ebits_raw,
+                       int4 *erec, int *ebits)
+{
+    if (NE) k_build_erec<<<nblk(NE), kBlock, 0, s>>>(NE, perm, p, lbl, ebits_raw, erec, ebits);
+}
+void launch_build_slots(hipStream_t s, int NE, const int4 *erec, const int *rowptr, const int *col, int *slot,
+                        int *bad)
+{
+    if (NE) k_build_slots<<<nblk(NE), kBlock, 0, s>>>(NE, erec, rowptr, col, slot, bad);
+}
+void launch_lookup_slots(hipStream_t s, int n, const int *rc, const int *rowptr, const int *col, int *out)
+{
+    if (n) k_lookup_slots<<<nblk(n), kBlock, 0, s>>>(n, rc, rowptr, col, out);
+}
+void launch_mark_fix_adj(hipStream_t s, int N, const int *rowptr, const int *col, const unsigned char *fixed,
+                         int *flag)
+{
+    if (N) k_mark_fix_adj<<<nblk(N), kBlock, 0, s>>>(N, rowptr, col, fixed, flag);
+}
+void launch_compact_flags(hipStream_t s, int N, const int *flag, int *cursor, int *out)
+{
+    if (N) k_compact_flags<<<nblk(N), kBlock, 0, s>>>(N, flag, cursor, out);
+}
+void launch_assemble_color(hipStream_t s, int begin, int end, const AssembleArgs &A)
+{
+    if (end > begin) k_assemble_color<<<nblk(end - begin), kBlock, 0, s>>>(begin, end, A);
+}
+void launch_point_currents(hipStream_t s, int n, const int *nodes, const double *J, double *b)
+{
+    if (n) k_point_currents<<<nblk(n), kBlock, 0, s>>>(n, nodes, J, b);
+}
+void launch_dirichlet(hipStream_t s, int nrows, const int *rows, int nadj, const int *adj, const int *rowptr,
+                      const int *col, const int *diag, const unsigned char *fixed, const double *fix_first,
+                      const double *fix_last, double *val, double *b)
+{
+    if (nadj) k_dirichlet_cols<<<nblk(nadj), kBlock, 0, s>>>(nadj, adj, rowptr, col, fixed, fix_first, val, b);
+    if (nrows) k_dirichlet_rows<<<nblk(nrows), kBlock, 0, s>>>(nrows, rows, rowptr, diag, val, b, fix_last);
+}
+void launch_map(hipStream_t s, int n, const int *dst, const int *ptr, const int *src, const double *w,
+                double *data, double *tmp)
+{
+    if (!n) return;
+    k_map_gather<<<nblk(n), kBlock, 0, s>>>(n, ptr, src, w, data, tmp);
+    k_map_scatter<<<nblk(n), kBlock, 0, s>>>(n, dst, tmp, data);
+}
+void launch_diag_inv(hipStream_t s, int N, const int *diag, const double *val, double *dinv, PcgScalars *S)
+{
+    if (N) k_diag_inv<<<nblk(N), kBlock, 0, s>>>(N, diag, val, dinv, S);
+}
+void launch_pcg_init(hipStream_t s, int N, int flag, const int *rowptr, const int *col, const double *val,
+                     const double *b, double *V, double *R, double *P, const double *dinv, double *partials,
+                     unsigned *counter, PcgScalars *S)
+{
+    k_pcg_init<<<grid_reduce(N), kBlock, 0, s>>>(N, flag, rowptr, col, val, b, V, R, P, dinv, partials, counter, S);
+}
+void launch_pcg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *P,
+                     double *U, double *partials, unsigned *counter, PcgScalars *S)
+{
+    k_pcg_spmv<<<grid_reduce(N), kBlock, 0, s>>>(N, rowptr, col, val, P, U, partials, counter, S);
+}
+void launch_pcg_update(hipStream_t s, int N, double *V, double *R, const double *P, const double *U,
+                       const double *dinv, double *partials, unsigned *counter, PcgScalars *S)
+{
+    k_pcg_update<<<grid_reduce(N), kBlock, 0, s>>>(N, V, R, P, U, dinv, partials, counter, S);
+}
+void launch_pcg_dir(hipStream_t s, int N, const double *R, const double *dinv, double *P, const PcgScalars *S)
+{
+    k_pcg_dir<<<grid_reduce(N), kBlock, 0, s>>>(N, R, dinv, P, S);
+}
+void launch_newton_res(hipStream_t s, int N, const double *V, const double *Vold, double *partials,
+                       unsigned *counter, NewtonScalars *S)
+{
+    k_newton_res<<<grid_reduce(N), kBlock, 0, s>>>(N, V, Vold, partials, counter, S);
+}
+void launch_relax(hipStream_t s, int N, double relax, double *V, const double *Vold)
+{
+    k_relax<<<grid_reduce(N), kBlock, 0, s>>>(N, relax, V, Vold);
+}
+void launch_scale(hipStream_t s, int N, double sc, const double *V, double *out)
+{
+    if (N) k_scale<<<nblk(N), kBlock, 0, s>>>(N, sc, V, out);
+}
+
+}  // namespace xfk

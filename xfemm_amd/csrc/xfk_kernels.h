@@ -1,0 +1,66 @@
+// Launch wrappers of the device kernels (xfk_device.hip), used by xfk_api.hip.
+#pragma once
+
+#include "xfk_internal.h"
+
+namespace xfk {
+
+struct AssembleArgs {
+    const int4 *erec;
+    const int *ebits;
+    const int *slot;
+    const double *x, *y;
+    const DevLabel *labels;
+    const DevBlock *blocks;
+    const DevLine *lines;
+    const DevCirc *circs;
+    const double *bhB, *bhH, *bhS;
+    double *mu1, *mu2;
+    const double *V;
+    double *val, *b;
+    int iter;
+};
+
+int grid_reduce(int N);
+
+void launch_count_incidence(hipStream_t s, int NE, const int *p, int *deg);
+void launch_fill_n2e(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e);
+void launch_sort_segments(hipStream_t s, int N, const int *ptr, int *a);
+void launch_row_count(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e,
+                      const int *fill_ptr, const int *fill_col, int *rowcnt);
+void launch_row_fill(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e,
+                     const int *fill_ptr, const int *fill_col, const int *rowptr, int *col, int *diag);
+void launch_color_round(hipStream_t s, int NE, const int *p, const int *n2e_ptr, const int *n2e, int *color,
+                        int *ncolored);
+void launch_color_hist(hipStream_t s, int NE, const int *color, int *hist, int maxc);
+void launch_iota(hipStream_t s, int n, int *a);
+void launch_build_erec(hipStream_t s, int NE, const int *perm, const int *p, const int *lbl, const int *ebits_raw,
+                       int4 *erec, int *ebits);
+void launch_build_slots(hipStream_t s, int NE, const int4 *erec, const int *rowptr, const int *col, int *slot,
+                        int *bad);
+void launch_lookup_slots(hipStream_t s, int n, const int *rc, const int *rowptr, const int *col, int *out);
+void launch_mark_fix_adj(hipStream_t s, int N, const int *rowptr, const int *col, const unsigned char *fixed,
+                         int *flag);
+void launch_compact_flags(hipStream_t s, int N, const int *flag, int *cursor, int *out);
+void launch_assemble_color(hipStream_t s, int begin, int end, const AssembleArgs &A);
+void launch_point_currents(hipStream_t s, int n, const int *nodes, const double *J, double *b);
+void launch_dirichlet(hipStream_t s, int nrows, const int *rows, int nadj, const int *adj, const int *rowptr,
+                      const int *col, const int *diag, const unsigned char *fixed, const double *fix_first,
+                      const double *fix_last, double *val, double *b);
+void launch_map(hipStream_t s, int n, const int *dst, const int *ptr, const int *src, const double *w,
+                double *data, double *tmp);
+void launch_diag_inv(hipStream_t s, int N, const int *diag, const double *val, double *dinv, PcgScalars *S);
+void launch_pcg_init(hipStream_t s, int N, int flag, const int *rowptr, const int *col, const double *val,
+                     const double *b, double *V, double *R, double *P, const double *dinv, double *partials,
+                     unsigned *counter, PcgScalars *S);
+void launch_pcg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *P,
+                     double *U, double *partials, unsigned *counter, PcgScalars *S);
+void launch_pcg_update(hipStream_t s, int N, double *V, double *R, const double *P, const double *U,
+                       const double *dinv, double *partials, unsigned *counter, PcgScalars *S);
+void launch_pcg_dir(hipStream_t s, int N, const double *R, const double *dinv, double *P, const PcgScalars *S);
+void launch_newton_res(hipStream_t s, int N, const double *V, const double *Vold, double *partials,
+                       unsigned *counter, NewtonScalars *S);
+void launch_relax(hipStream_t s, int N, double relax, double *V, const double *Vold);
+void launch_scale(hipStream_t s, int N, double sc, const double *V, double *out);
+
+}  // namespace xfk

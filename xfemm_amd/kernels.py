@@ -1,0 +1,264 @@
+"""ctypes binding of the C-ABI in include/xfemm_kernels.h (lib/libxfemm_kernels.so).
+
+This is the Python view of the MI355X hot path used by tests and bench.py.
+There is no CPU fallback: if the HIP library is missing, or no gfx950 device
+is present, every solve raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(HERE, "lib")
+KERNELS_SO = os.path.join(LIB_DIR, "libxfemm_kernels.so")
+
+dptr = C.POINTER(C.c_double)
+iptr = C.POINTER(C.c_int)
+
+XFK_OK = 0
+XFK_REBUILD_SYMBOLIC = 1
+
+# every symbol include/xfemm_kernels.h declares
+EXPORTED = (
+    "xfk_last_error", "xfk_device_count", "xfk_problem_create", "xfk_problem_destroy",
+    "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz",
+    "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_time",
+)
+
+
+class BlockDesc(C.Structure):
+    _fields_ = [("mu_x", C.c_double), ("mu_y", C.c_double), ("H_c", C.c_double),
+                ("J_re", C.c_double), ("Cduct", C.c_double), ("LamFill", C.c_double),
+                ("LamType", C.c_int), ("BHpoints", C.c_int),
+                ("B", dptr), ("H", dptr), ("slope", dptr)]
+
+
+class LabelDesc(C.Structure):
+    _fields_ = [("block", C.c_int), ("in_circuit", C.c_int), ("mag_dir", C.c_double),
+                ("is_wound", C.c_int)]
+
+
+class LineDesc(C.Structure):
+    _fields_ = [("format", C.c_int), ("A0", C.c_double), ("A1", C.c_double), ("A2", C.c_double),
+                ("phi", C.c_double), ("c0", C.c_double), ("c1", C.c_double)]
+
+
+class PointDesc(C.Structure):
+    _fields_ = [("A_re", C.c_double), ("A_im", C.c_double), ("J_re", C.c_double),
+                ("J_im", C.c_double)]
+
+
+class CircuitDesc(C.Structure):
+    _fields_ = [("type", C.c_int), ("amps_re", C.c_double), ("dvolts_re", C.c_double)]
+
+
+class ProblemDesc(C.Structure):
+    _fields_ = [("n_nodes", C.c_int), ("x", dptr), ("y", dptr), ("marker", iptr),
+                ("n_elems", C.c_int), ("p", iptr), ("e", iptr), ("lbl", iptr),
+                ("n_blocks", C.c_int), ("blocks", C.POINTER(BlockDesc)),
+                ("n_labels", C.c_int), ("labels", C.POINTER(LabelDesc)),
+                ("n_lines", C.c_int), ("lines", C.POINTER(LineDesc)),
+                ("n_points", C.c_int), ("points", C.POINTER(PointDesc)),
+                ("n_circs", C.c_int), ("circs", C.POINTER(CircuitDesc)),
+                ("n_pbc", C.c_int), ("pbc", iptr),
+                ("precision", C.c_double), ("length_units", C.c_int), ("coords", C.c_int),
+                ("relax", C.c_double)]
+
+
+class Result(C.Structure):
+    _fields_ = [("newton_iters", C.c_int), ("cg_iters", C.c_longlong), ("last_res", C.c_double),
+                ("final_er", C.c_double), ("nnz", C.c_longlong), ("ncolors", C.c_int),
+                ("ms_symbolic", C.c_double), ("ms_assemble", C.c_double), ("ms_solve", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+class XfkError(RuntimeError):
+    pass
+
+
+def load_library(path: str = KERNELS_SO):
+    """Load lib/libxfemm_kernels.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise XfkError("HIP library %s not built (run __graft_entry__.build() / make -C xfemm_amd)" % path)
+    L = C.CDLL(path)
+    L.xfk_last_error.restype = C.c_char_p
+    L.xfk_device_count.restype = C.c_int
+    L.xfk_problem_create.argtypes = [C.POINTER(ProblemDesc), C.c_int, C.POINTER(C.c_void_p)]
+    L.xfk_problem_destroy.argtypes = [C.c_void_p]
+    L.xfk_static2d.argtypes = [C.c_void_p, C.c_int, C.POINTER(Result)]
+    L.xfk_get_solution.argtypes = [C.c_void_p, dptr]
+    L.xfk_get_circuits.argtypes = [C.c_void_p, iptr, dptr, dptr]
+    L.xfk_get_csr.argtypes = [C.c_void_p, iptr, iptr, dptr, dptr]
+    L.xfk_get_nnz.argtypes = [C.c_void_p]
+    L.xfk_get_nnz.restype = C.c_longlong
+    L.xfk_get_stream.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+    L.xfk_pcg_solve_csr.argtypes = [C.c_int, iptr, iptr, dptr, dptr, dptr, C.c_int, C.c_double, C.c_int,
+                                    C.POINTER(C.c_longlong), dptr]
+    L.xfk_pcg_time.argtypes = [C.c_void_p, C.c_int, dptr, dptr]
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc != XFK_OK:
+        raise XfkError("xfk error %d: %s" % (rc, _lib.xfk_last_error().decode()))
+
+
+def device_count() -> int:
+    return load_library().xfk_device_count()
+
+
+class _Keep(list):
+    def d(self, a):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        self.append(a)
+        return a.ctypes.data_as(dptr)
+
+    def i(self, a):
+        a = np.ascontiguousarray(a, dtype=np.int32)
+        self.append(a)
+        return a.ctypes.data_as(iptr)
+
+
+class Static2DProblem:
+    """One device-resident static 2-D magnetostatic problem (FSolver::Static2D).
+
+    Arrays follow the reference's in-memory state after FSolver::LoadMesh and
+    LoadProblemFile (cm coordinates, 0-based indices, -1 for "none")."""
+
+    def __init__(self, *, x, y, p, lbl, blocks: Sequence[dict], labels: Sequence[dict],
+                 lines: Sequence[dict] = (), points: Sequence[dict] = (), circuits: Sequence[dict] = (),
+                 marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0,
+                 device=0):
+        L = load_library()
+        keep = _Keep()
+        nb = max(1, len(blocks))
+        bl = (BlockDesc * nb)()
+        for k, b in enumerate(blocks):
+            o = bl[k]
+            o.mu_x, o.mu_y = b.get("mu_x", 1.0), b.get("mu_y", 1.0)
+            o.H_c, o.J_re, o.Cduct = b.get("H_c", 0.0), b.get("J_re", 0.0), b.get("Cduct", 0.0)
+            o.LamFill, o.LamType = b.get("LamFill", 1.0), b.get("LamType", 0)
+            n = len(b.get("B", ()))
+            o.BHpoints = n
+            if n:
+                o.B, o.H, o.slope = keep.d(b["B"]), keep.d(b["H"]), keep.d(b["slope"])
+        lb = (LabelDesc * max(1, len(labels)))()
+        for k, l in enumerate(labels):
+            lb[k].block, lb[k].in_circuit = l["block"], l.get("in_circuit", -1)
+            lb[k].mag_dir, lb[k].is_wound = l.get("mag_dir", 0.0), int(l.get("is_wound", 0))
+        ln = (LineDesc * max(1, len(lines)))()
+        for k, l in enumerate(lines):
+            o = ln[k]
+            o.format = l.get("format", 0)
+            o.A0, o.A1, o.A2, o.phi = l.get("A0", 0.0), l.get("A1", 0.0), l.get("A2", 0.0), l.get("phi", 0.0)
+            o.c0, o.c1 = l.get("c0", 0.0), l.get("c1", 0.0)
+        pt = (PointDesc * max(1, len(points)))()
+        for k, q in enumerate(points):
+            pt[k].A_re, pt[k].A_im = q.get("A_re", 0.0), q.get("A_im", 0.0)
+            pt[k].J_re, pt[k].J_im = q.get("J_re", 0.0), q.get("J_im", 0.0)
+        ci = (CircuitDesc * max(1, len(circuits)))()
+        for k, q in enumerate(circuits):
+            ci[k].type, ci[k].amps_re, ci[k].dvolts_re = q.get("type", 0), q.get("amps_re", 0.0), q.get("dvolts_re", 0.0)
+        D = ProblemDesc()
+        x = np.asarray(x, dtype=np.float64)
+        self.n_nodes = D.n_nodes = len(x)
+        D.x, D.y = keep.d(x), keep.d(y)
+        D.marker = keep.i(marker) if marker is not None else None
+        p = np.asarray(p, dtype=np.int32).reshape(-1)
+        self.n_elems = D.n_elems = len(p) // 3
+        D.p = keep.i(p)
+        D.e = keep.i(np.asarray(e, dtype=np.int32).reshape(-1)) if e is not None else None
+        D.lbl = keep.i(lbl)
+        D.n_blocks, D.blocks = len(blocks), bl
+        D.n_labels, D.labels = len(labels), lb
+        D.n_lines, D.lines = len(lines), ln
+        D.n_points, D.points = len(points), pt
+        D.n_circs, D.circs = len(circuits), ci
+        if pbc is not None and len(pbc):
+            pb = np.asarray(pbc, dtype=np.int32).reshape(-1)
+            D.n_pbc, D.pbc = len(pb) // 3, keep.i(pb)
+        else:
+            D.n_pbc, D.pbc = 0, None
+        D.precision, D.length_units, D.coords, D.relax = precision, length_units, coords, relax
+        self.n_circs = len(circuits)
+        h = C.c_void_p()
+        _check(L.xfk_problem_create(C.byref(D), device, C.byref(h)))
+        self._h = h
+        self.result: Optional[Result] = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().xfk_problem_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, rebuild_symbolic: bool = False) -> dict:
+        r = Result()
+        _check(_lib.xfk_static2d(self._h, XFK_REBUILD_SYMBOLIC if rebuild_symbolic else 0, C.byref(r)))
+        self.result = r
+        return r.as_dict()
+
+    def solution(self) -> np.ndarray:
+        A = np.zeros(self.n_nodes)
+        _check(_lib.xfk_get_solution(self._h, A.ctypes.data_as(dptr)))
+        return A
+
+    def circuits(self):
+        n = self.n_circs
+        cc = np.zeros(max(1, n), np.int32)
+        J = np.zeros(max(1, n))
+        dV = np.zeros(max(1, n))
+        _check(_lib.xfk_get_circuits(self._h, cc.ctypes.data_as(iptr), J.ctypes.data_as(dptr),
+                                     dV.ctypes.data_as(dptr)))
+        return cc[:n], J[:n], dV[:n]
+
+    def csr(self):
+        nnz = _lib.xfk_get_nnz(self._h)
+        rp = np.zeros(self.n_nodes + 1, np.int32)
+        col = np.zeros(nnz, np.int32)
+        val = np.zeros(nnz)
+        b = np.zeros(self.n_nodes)
+        _check(_lib.xfk_get_csr(self._h, rp.ctypes.data_as(iptr), col.ctypes.data_as(iptr),
+                                val.ctypes.data_as(dptr), b.ctypes.data_as(dptr)))
+        return rp, col, val, b
+
+    def pcg_time(self, iters: int = 50):
+        ms_spmv = C.c_double()
+        ms_iter = C.c_double()
+        _check(_lib.xfk_pcg_time(self._h, iters, C.byref(ms_spmv), C.byref(ms_iter)))
+        return ms_spmv.value, ms_iter.value
+
+
+def pcg_solve_csr(rowptr, col, val, b, V0=None, flag=0, precision=1e-8, device=0):
+    """Stand-alone device PCG on a full symmetric CSR (CBigLinProb::PCGSolve semantics)."""
+    L = load_library()
+    n = len(rowptr) - 1
+    rp = np.ascontiguousarray(rowptr, np.int32)
+    cl = np.ascontiguousarray(col, np.int32)
+    vl = np.ascontiguousarray(val, np.float64)
+    bb = np.ascontiguousarray(b, np.float64)
+    V = np.zeros(n) if V0 is None else np.array(V0, dtype=np.float64)
+    it = C.c_longlong()
+    er = C.c_double()
+    _check(L.xfk_pcg_solve_csr(n, rp.ctypes.data_as(iptr), cl.ctypes.data_as(iptr), vl.ctypes.data_as(dptr),
+                               bb.ctypes.data_as(dptr), V.ctypes.data_as(dptr), flag, precision, device,
+                               C.byref(it), C.byref(er)))
+    return V, it.value, er.value

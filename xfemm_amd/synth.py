@@ -1,0 +1,175 @@
+"""Synthetic magnetostatic problems on refined square-domain meshes.
+
+The bench workloads of BASELINE.json ("Synthetic 2M-tri square-domain
+magnetostatic", linear mu and M-19 nonlinear B-H) need meshes far larger than
+the reference's test problems; fmesher (Triangle) is outside this project's
+scope, so this module generates structured triangulations directly in the
+in-memory form FSolver::LoadMesh produces (cfemm/fsolver/fsolver.cpp:350-718):
+node coordinates in cm, 0-based element nodes, block-label index per element,
+boundary-property index per element edge, plus the .fem-level property tables.
+
+Geometry (unit square of side L cm, n x n cells, each split into 2 triangles
+with alternating diagonals):
+  * air everywhere, Dirichlet A = 0 ("A=0" boundary, BdryFormat 0) on the outer edge
+  * a steel C-core (linear mu_r or the M-19 B-H curve, LamFill 0.98, LamType 0)
+  * two coil sides with +J / -J (MA/m^2)
+  * a NdFeB magnet block (H_c = 979 kA/m, magnetised along +y)
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def m19_curve():
+    """M-19 steel B-H points (FEMM material library, mfemm/matlib.dat:1168-1221)."""
+    path = os.path.join(_HERE, "data", "M19_Steel.bh")
+    data = np.loadtxt(path)
+    return data[:, 0].copy(), data[:, 1].copy()
+
+
+def square_mesh(n: int, L: float = 10.0, order: str = "rows"):
+    """Nodes (n+1)^2 on [0,L]^2 (cm), 2 n^2 triangles (counter-clockwise)."""
+    m = n + 1
+    xs = np.linspace(0.0, L, m)
+    X, Y = np.meshgrid(xs, xs, indexing="xy")     # row j = y index
+    x = X.reshape(-1).copy()
+    y = Y.reshape(-1).copy()
+    j, i = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    i = i.reshape(-1)
+    j = j.reshape(-1)
+    n00 = j * m + i
+    n10 = n00 + 1
+    n01 = n00 + m
+    n11 = n01 + 1
+    alt = ((i + j) & 1) == 0
+    # two triangles per cell, both counter-clockwise
+    t1 = np.where(alt[:, None], np.stack([n00, n10, n11], 1), np.stack([n00, n10, n01], 1))
+    t2 = np.where(alt[:, None], np.stack([n00, n11, n01], 1), np.stack([n10, n11, n01], 1))
+    p = np.empty((2 * n * n, 3), dtype=np.int32)
+    p[0::2] = t1
+    p[1::2] = t2
+    return x, y, p
+
+
+def _boundary_edges(p, x, y, L, tol):
+    """e[el, j] = 0 for edges (p[j], p[j+1]) on the outer boundary, else -1."""
+    on = (np.abs(x) < tol) | (np.abs(x - L) < tol) | (np.abs(y) < tol) | (np.abs(y - L) < tol)
+    e = -np.ones(p.shape, dtype=np.int32)
+    for j in range(3):
+        a, b = p[:, j], p[:, (j + 1) % 3]
+        same_x = (np.abs(x[a] - x[b]) < tol) & ((np.abs(x[a]) < tol) | (np.abs(x[a] - L) < tol))
+        same_y = (np.abs(y[a] - y[b]) < tol) & ((np.abs(y[a]) < tol) | (np.abs(y[a] - L) < tol))
+        e[(on[a] & on[b]) & (same_x | same_y), j] = 0
+    return e
+
+
+def magnetostatic(n: int, nonlinear: bool = False, L: float = 10.0, J: float = 2.0,
+                  mu_steel: float = 1000.0, precision: float = 1e-8, with_magnet: bool = True):
+    """Keyword arguments for kernels.Static2DProblem (and the oracle) of an
+    n x n-cell square problem: 2 n^2 triangles, (n+1)^2 nodes."""
+    x, y, p = square_mesh(n, L)
+    cx = (x[p[:, 0]] + x[p[:, 1]] + x[p[:, 2]]) / 3.0
+    cy = (y[p[:, 0]] + y[p[:, 1]] + y[p[:, 2]]) / 3.0
+    u, v = cx / L, cy / L
+    lbl = np.zeros(len(p), dtype=np.int32)                       # 0: air
+    core = (u > 0.25) & (u < 0.75) & (v > 0.25) & (v < 0.75)
+    window = (u > 0.35) & (u < 0.65) & (v > 0.35) & (v < 0.65)
+    gap = (u > 0.70) & (v > 0.45) & (v < 0.55)
+    steel = core & ~window & ~gap
+    lbl[steel] = 1                                               # 1: steel
+    coil_a = (u > 0.37) & (u < 0.45) & (v > 0.38) & (v < 0.62)
+    coil_b = (u > 0.55) & (u < 0.63) & (v > 0.38) & (v < 0.62)
+    lbl[coil_a] = 2                                              # 2: coil +J
+    lbl[coil_b] = 3                                              # 3: coil -J
+    if with_magnet:
+        mag = (u > 0.08) & (u < 0.16) & (v > 0.40) & (v < 0.60)
+        lbl[mag] = 4                                             # 4: magnet
+    blocks = [
+        dict(mu_x=1.0, mu_y=1.0),                                # air
+        dict(mu_x=mu_steel, mu_y=mu_steel, LamFill=1.0),         # steel (linear)
+        dict(mu_x=1.0, mu_y=1.0, J_re=J),                        # coil +
+        dict(mu_x=1.0, mu_y=1.0, J_re=-J),                       # coil -
+        dict(mu_x=1.049, mu_y=1.049, H_c=979000.0, Cduct=0.667), # NdFeB 40 MGOe
+    ]
+    if nonlinear:
+        blocks[1] = dict(mu_x=1.0, mu_y=1.0, LamFill=0.98, LamType=0, bh="M19")
+    labels = [dict(block=0), dict(block=1), dict(block=2), dict(block=3), dict(block=4, mag_dir=90.0)]
+    tol = 1e-9 * L
+    e = _boundary_edges(p, x, y, L, tol)
+    lines = [dict(format=0)]
+    return dict(x=x, y=y, p=p, lbl=lbl, e=e, marker=None, pbc=None, blocks=blocks, labels=labels,
+                lines=lines, points=[], circuits=[], precision=precision, length_units=2, coords=0, relax=1.0)
+
+
+def fem_text(blocks, lines, precision=1e-8, units="centimeters") -> str:
+    """A .fem header carrying the property tables (no geometry: meshes are given)."""
+    out = ["[Format]      =  4.0", "[Frequency]   =  0", "[Precision]   =  %.17g" % precision,
+           "[MinAngle]    =  30", "[Depth]       =  1", "[LengthUnits] =  %s" % units,
+           "[ProblemType] =  planar", "[Coordinates] =  cartesian", "[ACSolver]    =  0",
+           '[PrevSoln]    = ""', "[PrevType]    =  0", '[Comment]     =  "synthetic"',
+           "[PointProps]   = 0", "[BdryProps]   = %d" % len(lines)]
+    for k, ln in enumerate(lines):
+        out += ["  <BeginBdry>", '    <BdryName> = "b%d"' % k, "    <BdryType> = %d" % ln.get("format", 0),
+                "    <A_0> = %.17g" % ln.get("A0", 0.0), "    <A_1> = 0", "    <A_2> = 0", "    <Phi> = 0",
+                "    <c0> = %.17g" % ln.get("c0", 0.0), "    <c0i> = 0", "    <c1> = %.17g" % ln.get("c1", 0.0),
+                "    <c1i> = 0", "    <Mu_ssd> = 0", "    <Sigma_ssd> = 0", "  <EndBdry>"]
+    out.append("[BlockProps]  = %d" % len(blocks))
+    for k, b in enumerate(blocks):
+        out += ["  <BeginBlock>", '    <BlockName> = "m%d"' % k, "    <Mu_x> = %.17g" % b.get("mu_x", 1.0),
+                "    <Mu_y> = %.17g" % b.get("mu_y", 1.0), "    <H_c> = %.17g" % b.get("H_c", 0.0),
+                "    <H_cAngle> = 0", "    <J_re> = %.17g" % b.get("J_re", 0.0), "    <J_im> = 0",
+                "    <Sigma> = %.17g" % b.get("Cduct", 0.0), "    <d_lam> = 0", "    <Phi_h> = 0",
+                "    <Phi_hx> = 0", "    <Phi_hy> = 0", "    <LamType> = %d" % b.get("LamType", 0),
+                "    <LamFill> = %.17g" % b.get("LamFill", 1.0), "    <NStrands> = 0", "    <WireD> = 0"]
+        if b.get("bh") == "M19":
+            B, H = m19_curve()
+            out.append("    <BHPoints> = %d" % len(B))
+            out += ["      %.17g\t%.17g" % (bb, hh) for bb, hh in zip(B, H)]
+        else:
+            out.append("    <BHPoints> = 0")
+        out.append("  <EndBlock>")
+    out.append("[CircuitProps]  = 0")
+    return "\n".join(out) + "\n"
+
+
+def write_problem(base: str, kw: dict, label_xy: Optional[np.ndarray] = None) -> None:
+    """Write <base>.fem/.node/.ele/.edge/.pbc in the fmesher layout so the same
+    synthetic problem runs through the file-based FSolver path."""
+    x, y, p, lbl, e = kw["x"], kw["y"], kw["p"], kw["lbl"], kw["e"]
+    conv = 1.0   # centimeters
+    text = fem_text(kw["blocks"], kw["lines"], kw["precision"])
+    labels = kw["labels"]
+    text += "[NumPoints] = 0\n[NumSegments] = 0\n[NumArcSegments] = 0\n[NumHoles] = 0\n"
+    text += "[NumBlockLabels] = %d\n" % len(labels)
+    for k, lb in enumerate(labels):
+        text += "0\t0\t%d\t-1\t%d\t%.17g\t0\t1\t0\n" % (lb["block"] + 1, lb.get("in_circuit", -1) + 1,
+                                                        lb.get("mag_dir", 0.0))
+    with open(base + ".fem", "w") as fh:
+        fh.write(text)
+    with open(base + ".node", "w") as fh:
+        fh.write("%d\t2\t0\t1\n" % len(x))
+        for i in range(len(x)):
+            fh.write("%d\t%.17g\t%.17g\t0\n" % (i, x[i] / conv, y[i] / conv))
+    with open(base + ".ele", "w") as fh:
+        fh.write("%d\t3\t1\n" % len(p))
+        for i in range(len(p)):
+            fh.write("%d\t%d\t%d\t%d\t%d\n" % (i, p[i, 0], p[i, 1], p[i, 2], lbl[i] + 1))
+    edges = {}
+    for i in range(len(p)):
+        for j in range(3):
+            a, b = int(p[i, j]), int(p[i, (j + 1) % 3])
+            k = (min(a, b), max(a, b))
+            mk = -(int(e[i, j]) + 2) if e[i, j] >= 0 else 0
+            if k not in edges or mk != 0:
+                edges[k] = mk
+    with open(base + ".edge", "w") as fh:
+        fh.write("%d\t1\n" % len(edges))
+        for n, (k, mk) in enumerate(sorted(edges.items())):
+            fh.write("%d\t%d\t%d\t%d\n" % (n, k[0], k[1], mk))
+    with open(base + ".pbc", "w") as fh:
+        fh.write("0\n0\n")
