@@ -1,0 +1,71 @@
+/* xfemm_fsolver.h -- C-ABI of the file-based magnetics solver (FSolver) whose
+ * static-2D hot path runs on MI355X (include/xfemm_kernels.h).
+ *
+ * This is the surface the reference's own foreign-function binding drives:
+ * mfemm/mexfsolver.cpp (the MATLAB/Octave MEX gateway) creates an FSolver,
+ * sets PathName and the WarnMessage/PrintMessage hooks, calls
+ * LoadProblemFile() and runSolver(verbose), and returns 1/2 on failure.
+ * Each entry point below replaces one step of that sequence:
+ *
+ *   xfemm_fsolver_create / _destroy     std::make_shared<FSolver>()        mexfsolver.cpp:31
+ *   xfemm_fsolver_set_message_handlers  SolveObj->WarnMessage/PrintMessage mexfsolver.cpp:100-111
+ *   xfemm_fsolver_set_pathname          SolveObj->PathName                 mexfsolver.cpp:115
+ *   xfemm_fsolver_load_problem_file     FSolver::LoadProblemFile()         fsolver/fsolver.cpp:202
+ *   xfemm_fsolver_run_solver            FSolver::runSolver(verbose)        fsolver/fsolver.cpp:1213
+ *   xfemm_fsolver_set_delete_mesh_files FSolver::LoadMesh(deleteFiles)     fsolver/fsolver.cpp:350
+ *
+ * Boolean results follow the reference: 1 = success (true), 0 = failure.
+ * Output: <PathName>.ans in the reference's WriteStatic2D layout
+ * (fsolver/static2d.cpp:1038-1195).
+ */
+#ifndef XFEMM_FSOLVER_H
+#define XFEMM_FSOLVER_H
+
+#include "xfemm_kernels.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct xfemm_fsolver xfemm_fsolver;
+typedef int (*xfemm_message_fn)(const char *fmt, ...);
+
+xfemm_fsolver *xfemm_fsolver_create(void);
+void xfemm_fsolver_destroy(xfemm_fsolver *s);
+void xfemm_fsolver_set_message_handlers(xfemm_fsolver *s, xfemm_message_fn warn, xfemm_message_fn print);
+int xfemm_fsolver_set_pathname(xfemm_fsolver *s, const char *path_without_extension);
+int xfemm_fsolver_set_device(xfemm_fsolver *s, int device);
+int xfemm_fsolver_set_delete_mesh_files(xfemm_fsolver *s, int delete_files);
+int xfemm_fsolver_load_problem_file(xfemm_fsolver *s);
+int xfemm_fsolver_run_solver(xfemm_fsolver *s, int verbose);
+
+/* Host-only steps of runSolver, for callers that drive them one by one:
+ * FSolver::LoadMesh (fsolver.cpp:350) and FSolver::Cuthill (cuthill.cpp:88). */
+int xfemm_fsolver_load_mesh(xfemm_fsolver *s);
+int xfemm_fsolver_cuthill(xfemm_fsolver *s);
+int xfemm_fsolver_get_nodes(xfemm_fsolver *s, double *x_cm, double *y_cm, int *marker);
+int xfemm_fsolver_get_element_edges(xfemm_fsolver *s, int *e);
+int xfemm_fsolver_get_pbcs(xfemm_fsolver *s, int *pbc3);
+int xfemm_fsolver_num_pbcs(xfemm_fsolver *s);
+int xfemm_fsolver_bandwidth(xfemm_fsolver *s);
+/* processed B-H curve of block k after LoadProblemFile (GetSlopes); returns BHpoints */
+int xfemm_fsolver_get_block_bh(xfemm_fsolver *s, int k, double *B, double *H, double *slope, double *mu_x);
+
+/* state after run_solver (renumbered order, as written to the .ans) */
+int xfemm_fsolver_num_nodes(xfemm_fsolver *s);
+int xfemm_fsolver_num_elements(xfemm_fsolver *s);
+int xfemm_fsolver_get_solution(xfemm_fsolver *s, double *x, double *y, double *A);
+int xfemm_fsolver_get_elements(xfemm_fsolver *s, int *p, int *lbl);
+int xfemm_fsolver_get_stats(xfemm_fsolver *s, xfk_result *out);
+const char *xfemm_fsolver_last_error(xfemm_fsolver *s);
+
+/* CMMaterialProp::GetSlopes(0) (libfemm/CMaterialProp.cpp:127): processes a
+ * B-H curve in place (B, H: n points) and writes the knot slopes; returns the
+ * initial relative permeability in *mu_x.  1 on success. */
+int xfemm_bh_get_slopes(int n, double *B, double *H, double *slope, int lam_type, double lam_fill,
+                        double *mu_x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -106,6 +106,8 @@ typedef struct {
     double ms_symbolic;         /* device time, ms */
     double ms_assemble;
     double ms_solve;
+    double spmv_ms_avg;         /* XFK_TIME_SPMV: mean HIP-event time of one SpMV launch */
+    int spmv_samples;           /* launches sampled (every 16th PCG iteration) */
 } xfk_result;
 
 typedef struct xfk_problem xfk_problem;
@@ -117,10 +119,12 @@ int xfk_device_count(void);
 int xfk_problem_create(const xfk_problem_desc *desc, int device, xfk_problem **out);
 void xfk_problem_destroy(xfk_problem *prob);
 
-enum { XFK_REBUILD_SYMBOLIC = 1 };
+enum { XFK_REBUILD_SYMBOLIC = 1, XFK_TIME_SPMV = 2 };
 
 /* FSolver::Static2D on the device.  flags: XFK_REBUILD_SYMBOLIC rebuilds the
- * CSR pattern, colouring and boundary maps (they are cached otherwise). */
+ * CSR pattern, colouring and boundary maps (they are cached otherwise);
+ * XFK_TIME_SPMV brackets every 16th SpMV launch with HIP events on the
+ * solver stream and reports the mean launch duration. */
 int xfk_static2d(xfk_problem *prob, int flags, xfk_result *res);
 
 /* A at every node (V * c, the value fsolver writes to .ans), host copy. */

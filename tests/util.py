@@ -53,14 +53,21 @@ def synth_to_oracle(kw: dict):
                                             MagDir=lb.get("mag_dir", 0.0)))
     for ln in kw["lines"]:
         pr.bdrys.append(femfile.BdryProp(BdryFormat=ln.get("format", 0), A0=ln.get("A0", 0.0),
+                                         A1=ln.get("A1", 0.0), A2=ln.get("A2", 0.0), phi=ln.get("phi", 0.0),
                                          c0=ln.get("c0", 0.0), c1=ln.get("c1", 0.0)))
+    for q in kw.get("points", []):
+        pr.points.append(femfile.PointProp(A_re=q.get("A_re", 0.0), A_im=q.get("A_im", 0.0),
+                                           J_re=q.get("J_re", 0.0), J_im=q.get("J_im", 0.0)))
     femfile.get_fill_factor(pr)
     nn = len(kw["x"])
+    marker = kw.get("marker")
+    pbc = kw.get("pbc")
     mesh = femfile.Mesh(x=np.asarray(kw["x"], float), y=np.asarray(kw["y"], float),
-                        marker=-np.ones(nn, np.int32), p=np.asarray(kw["p"], np.int32),
+                        marker=-np.ones(nn, np.int32) if marker is None else np.asarray(marker, np.int32),
+                        p=np.asarray(kw["p"], np.int32),
                         e=np.asarray(kw["e"], np.int32), lbl=np.asarray(kw["lbl"], np.int32),
                         blk=np.array([kw["labels"][l]["block"] for l in kw["lbl"]], np.int32),
-                        pbc=np.zeros((0, 3), np.int32))
+                        pbc=np.zeros((0, 3), np.int32) if pbc is None else np.asarray(pbc, np.int32))
     return pr, mesh, kernel_kwargs(pr, mesh)
 
 

@@ -1,0 +1,533 @@
+// FSolver host logic over the MI355X kernels (see fsolver.h).
+#include "fsolver.h"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <utility>
+
+namespace xfemm {
+
+int PrintWarningMsg(const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    int r = vfprintf(stderr, fmt, ap);
+    va_end(ap);
+    return r;
+}
+
+FSolver::FSolver() : WarnMessage(&PrintWarningMsg), PrintMessage(&PrintWarningMsg) {}
+
+void FSolver::warn(const std::string &msg)
+{
+    lastError = msg;
+    WarnMessage("%s", msg.c_str());
+}
+
+std::string FSolver::getErrorString(LoadMeshErr err)
+{
+    switch (err) {
+    case NOERROR: return std::string();
+    case BADEDGEFILE: return "problem loading mesh:\nCould not open .edge file.\n";
+    case BADELEMENTFILE: return "problem loading mesh:\nCould not open .ele file.\n";
+    case BADFEMFILE: return "problem loading mesh:\nCould not open .fem file.\n";
+    case BADNODEFILE: return "problem loading mesh:\nCould not open .node file.\n";
+    case BADPBCFILE: return "problem loading mesh:\nCould not open .pbc file.\n";
+    case MISSINGMATPROPS: return "problem loading mesh:\nMaterial properties have not been defined for all regions.\n";
+    case ELMLABELTOOBIG:
+        return "problem loading mesh:\nElemnet label number was greater than the number of labels in the problem.\n";
+    case UNSUPPORTEDMESH: return "problem loading mesh:\nair-gap elements are not supported by this solver build.\n";
+    }
+    return std::string();
+}
+
+bool FSolver::LoadProblemFile()
+{
+    Relax = 1.;
+    std::string err;
+    FemmProblemData &base = *this;
+    if (!ParseFemFile(PathName + ".fem", base, err)) {
+        warn(err);
+        return false;
+    }
+    if (!previousSolutionFile.empty()) {
+        warn("previous-solution (incremental/frozen permeability) problems are not supported by this solver build\n");
+        return false;
+    }
+    for (auto &prop : blockproplist)
+        if (prop.BHpoints > 0) {
+            if (!prop.GetSlopes()) {
+                warn("bad B-H curve in material " + prop.BlockName + "\n");
+                return false;
+            }
+            prop.MuMax = 0;
+        }
+    const int NumBlockLabels = (int)labellist.size();
+    for (auto &lb : labellist)
+        if (lb.InCircuit >= (int)circproplist.size()) {
+            warn("block label refers to an undefined circuit\n");
+            return false;
+        }
+    int NumCircProps = (int)circproplist.size();
+    if (NumCircProps == 0) return true;
+    // serial circuits -> one parallel circuit per block label (fsolver.cpp:280-317)
+    for (auto &c : circproplist) c.OrigCirc = -1;
+    NumCircPropsOrig = NumCircProps;
+    for (int k = 0; k < NumBlockLabels; k++)
+        if (labellist[k].InCircuit >= 0) {
+            int ic = labellist[k].InCircuit;
+            if (circproplist[ic].CircType == 1) {
+                CMCircuit ncirc = circproplist[ic];
+                ncirc.OrigCirc = ic;
+                ncirc.Amps_im *= labellist[k].Turns;
+                ncirc.Amps_re *= labellist[k].Turns;
+                circproplist.push_back(ncirc);
+                labellist[k].InCircuit = NumCircProps;
+                NumCircProps++;
+            }
+        }
+    for (auto &c : circproplist)
+        if (c.CircType == 1) c.CircType = 0;
+    return true;
+}
+
+LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
+{
+    char s[1024];
+    std::string infile = PathName + ".node";
+    FILE *fp = fopen(infile.c_str(), "rt");
+    if (!fp) return BADNODEFILE;
+    int k = 0, j = 0;
+    if (!fgets(s, 1024, fp) || sscanf(s, "%i", &k) != 1) {
+        fclose(fp);
+        return BADNODEFILE;
+    }
+    NumNodes = k;
+    meshnode.assign(k, CNode());
+    const double conv = 100 * kLengthConvMeters[LengthUnits];
+    for (int i = 0; i < k; i++) {
+        CNode node;
+        if (fscanf(fp, "%i %lf %lf %i", &j, &node.x, &node.y, &j) != 4) {
+            fclose(fp);
+            return BADNODEFILE;
+        }
+        node.BoundaryMarker = (j > 1) ? j - 2 : -1;
+        node.x *= conv;   // lengths in cm (fsolver.cpp:386-388)
+        node.y *= conv;
+        meshnode[i] = node;
+    }
+    fclose(fp);
+
+    infile = PathName + ".pbc";
+    fp = fopen(infile.c_str(), "rt");
+    if (!fp) return BADPBCFILE;
+    NumPBCs = 0;
+    if (fgets(s, 1024, fp)) sscanf(s, "%i", &NumPBCs);
+    pbclist.clear();
+    for (int i = 0; i < NumPBCs; i++) {
+        CCommonPoint pbc;
+        if (!fgets(s, 1024, fp) || sscanf(s, "%i %i %i %i", &j, &pbc.x, &pbc.y, &pbc.t) != 4) {
+            fclose(fp);
+            return BADPBCFILE;
+        }
+        pbclist.push_back(pbc);
+    }
+    NumAirGapElems = 0;
+    if (fgets(s, 1024, fp)) sscanf(s, "%i", &NumAirGapElems);
+    fclose(fp);
+    if (NumAirGapElems != 0) return UNSUPPORTEDMESH;
+
+    infile = PathName + ".ele";
+    fp = fopen(infile.c_str(), "rt");
+    if (!fp) return BADELEMENTFILE;
+    if (!fgets(s, 1024, fp) || sscanf(s, "%i", &k) != 1) {
+        fclose(fp);
+        return BADELEMENTFILE;
+    }
+    NumEls = k;
+    meshele.assign(k, CMElement());
+    int defaultLabel = -1;
+    for (int i = 0; i < (int)labellist.size(); i++)
+        if (labellist[i].IsDefault) defaultLabel = i;
+    auto remove_files = [&]() {
+        for (const char *ext : {".ele", ".node", ".pbc", ".poly", ".edge"}) remove((PathName + ext).c_str());
+    };
+    for (int i = 0; i < k; i++) {
+        CMElement elm;
+        if (fscanf(fp, "%i %i %i %i %i", &j, &elm.p[0], &elm.p[1], &elm.p[2], &elm.lbl) != 5) {
+            fclose(fp);
+            return BADELEMENTFILE;
+        }
+        elm.lbl--;
+        if (elm.lbl < 0) elm.lbl = defaultLabel;
+        if (elm.lbl < 0) {
+            char buf[256];
+            snprintf(buf, sizeof buf, "The element number %i had label %i\n", i, elm.lbl);
+            warn(std::string("Material properties have not been defined for all regions.\n") + buf);
+            fclose(fp);
+            if (deleteFiles) remove_files();
+            return MISSINGMATPROPS;
+        }
+        if (elm.lbl >= (int)labellist.size()) {
+            fclose(fp);
+            if (deleteFiles) remove_files();
+            return ELMLABELTOOBIG;
+        }
+        for (int q = 0; q < 3; q++)
+            if (elm.p[q] < 0 || elm.p[q] >= NumNodes) {
+                fclose(fp);
+                return BADELEMENTFILE;
+            }
+        elm.blk = labellist[elm.lbl].BlockType;
+        meshele[i] = elm;
+    }
+    fclose(fp);
+
+    // node -> element membership (fsolver.cpp:628-657)
+    std::vector<std::vector<int>> mbr(NumNodes);
+    for (int i = 0; i < NumEls; i++)
+        for (int q = 0; q < 3; q++) mbr[meshele[i].p[q]].push_back(i);
+
+    infile = PathName + ".edge";
+    fp = fopen(infile.c_str(), "rt");
+    if (!fp) return BADEDGEFILE;
+    int nedge = 0, flag = 0;
+    if (fscanf(fp, "%i", &nedge) != 1 || fscanf(fp, "%i", &flag) != 1) {
+        fclose(fp);
+        return BADEDGEFILE;
+    }
+    edges_.clear();
+    edges_.reserve(nedge);
+    for (int i = 0; i < nedge; i++) {
+        int n0, n1;
+        if (fscanf(fp, "%i %i %i %i", &j, &n0, &n1, &j) != 4) {
+            fclose(fp);
+            return BADEDGEFILE;
+        }
+        if (n0 < 0 || n1 < 0 || n0 >= NumNodes || n1 >= NumNodes) {
+            fclose(fp);
+            return BADEDGEFILE;
+        }
+        edges_.push_back({n0, n1, j});
+        if (j < 0) {
+            int bc = -(j + 2);
+            for (int el : mbr[n0]) {
+                CMElement &e = meshele[el];
+                if ((e.p[0] == n0 && e.p[1] == n1) || (e.p[0] == n1 && e.p[1] == n0)) e.e[0] = bc;
+                if ((e.p[1] == n0 && e.p[2] == n1) || (e.p[1] == n1 && e.p[2] == n0)) e.e[1] = bc;
+                if ((e.p[2] == n0 && e.p[0] == n1) || (e.p[2] == n1 && e.p[0] == n0)) e.e[2] = bc;
+            }
+        }
+    }
+    fclose(fp);
+    if (deleteFiles)
+        for (const char *ext : {".ele", ".node", ".pbc", ".poly"}) remove((PathName + ext).c_str());
+    return NOERROR;
+}
+
+int FSolver::SortElements()
+{
+    // comb sort on p0+p1+p2 (cuthill.cpp:39-86); not stable, restated exactly
+    std::vector<long long> Score(NumEls);
+    for (int k = 0; k < NumEls; k++) Score[k] = (long long)meshele[k].p[0] + meshele[k].p[1] + meshele[k].p[2];
+    int gap = NumEls, i = 0;
+    do {
+        if (gap > 1) {
+            gap = (gap * 10) / 13;
+            if ((gap == 10) || (gap == 9)) gap = 11;
+        }
+        i = 0;
+        for (int j = 0; (j + gap) < NumEls; j++) {
+            if (Score[j] > Score[j + gap]) {
+                int k = j + gap;
+                std::swap(Score[k], Score[j]);
+                std::swap(meshele[k], meshele[j]);
+                i = 1;
+            }
+        }
+    } while ((gap > 1) && (i > 0));
+    return true;
+}
+
+int FSolver::Cuthill(bool deleteFiles)
+{
+    // reverse-less Cuthill-McKee of cuthill.cpp:88-390, on the .edge connectivity
+    const int n_lines = (int)edges_.size();
+    std::vector<int> numcon(NumNodes, 0), newnum(NumNodes, -1), nxtnum(NumNodes, -1);
+    for (auto &e : edges_) {
+        numcon[e[0]]++;
+        numcon[e[1]]++;
+    }
+    std::vector<std::vector<int>> ocon(NumNodes);
+    for (int i = 0; i < NumNodes; i++) ocon[i].reserve(numcon[i]);
+    for (auto &e : edges_) {
+        ocon[e[0]].push_back(e[1]);
+        ocon[e[1]].push_back(e[0]);
+    }
+    if (deleteFiles) remove((PathName + ".edge").c_str());
+    // bubble sort by increasing connectivity
+    for (int n0 = 0; n0 < NumNodes; n0++) {
+        std::vector<int> &l = ocon[n0];
+        const int m = (int)l.size();
+        for (int a = 1; a < m; a++)
+            for (int j = 1; j < m; j++)
+                if (numcon[l[j]] < numcon[l[j - 1]]) std::swap(l[j], l[j - 1]);
+    }
+    long long j = numcon[0];
+    int n0 = 0;
+    for (long long i = 1; i < NumNodes; i++) {
+        if (numcon[i] < j) {
+            j = numcon[i];
+            n0 = (int)i;
+        }
+        if (j == 2) i = n_lines;
+    }
+    newnum[n0] = 0;
+    int n = 1;
+    nxtnum[0] = n0;
+    if (NumNodes > 1) {
+        do {
+            for (int c : ocon[n0])
+                if (newnum[c] < 0) {
+                    newnum[c] = n;
+                    nxtnum[n] = c;
+                    n++;
+                }
+            const int nextpos = newnum[n0] + 1;
+            if (nextpos >= NumNodes || nxtnum[nextpos] < 0) {
+                if (n >= NumNodes) break;
+                for (int i = 0; i < NumNodes; i++)
+                    if (newnum[i] < 0) {
+                        j = numcon[i];
+                        n0 = i;
+                        break;
+                    }
+                for (int i = 0; i < NumNodes; i++) {
+                    if ((newnum[i] < 0) && (numcon[i] < j)) {
+                        j = numcon[i];
+                        n0 = i;
+                    }
+                    if (j == 2) break;
+                }
+                newnum[n0] = n;
+                nxtnum[n] = n0;
+                n++;
+            } else {
+                n0 = nxtnum[nextpos];
+            }
+        } while (n < NumNodes);
+    }
+    for (auto &p : pbclist) {
+        p.x = newnum[p.x];
+        p.y = newnum[p.y];
+    }
+    int newwide = 0;
+    for (int a = 0; a < NumNodes; a++)
+        for (int c : ocon[a]) newwide = std::max(newwide, std::abs(newnum[a] - newnum[c]));
+    BandWidth = newwide + 1;
+    for (auto &e : meshele)
+        for (int q = 0; q < 3; q++) e.p[q] = newnum[e.p[q]];
+    // SortNodes (fsolver.cpp:1341-1353): node i moves to slot newnum[i]
+    std::vector<CNode> sorted(NumNodes);
+    for (int i = 0; i < NumNodes; i++) sorted[newnum[i]] = meshnode[i];
+    meshnode.swap(sorted);
+    SortElements();
+    return true;
+}
+
+void FSolver::GetFillFactor(int lbl)
+{
+    // static problems: only bIsWound matters (fsolver.cpp:1096-1105)
+    CMBlockLabel &bl = labellist[lbl];
+    const int lt = (bl.BlockType >= 0) ? blockproplist[bl.BlockType].LamType : 0;
+    bl.bIsWound = (std::abs(bl.Turns) > 1) || (lt > 2);
+}
+
+int FSolver::Static2D()
+{
+    for (int i = 0; i < (int)labellist.size(); i++) GetFillFactor(i);
+    for (auto &lb : labellist)
+        if (!lb.MagDirFctn.empty()) {
+            warn("Lua magnetisation-direction functions are not supported by this solver build\n");
+            return false;
+        }
+    // property tables -> C-ABI descriptors
+    std::vector<xfk_block_desc> blk(blockproplist.size());
+    for (size_t k = 0; k < blockproplist.size(); k++) {
+        const CMSolverMaterialProp &m = blockproplist[k];
+        xfk_block_desc &d = blk[k];
+        d.mu_x = m.mu_x; d.mu_y = m.mu_y; d.H_c = m.H_c; d.J_re = m.J_re; d.Cduct = m.Cduct;
+        d.LamFill = m.LamFill; d.LamType = m.LamType; d.BHpoints = m.BHpoints;
+        d.B = m.Bdata.empty() ? nullptr : m.Bdata.data();
+        d.H = m.Hdata.empty() ? nullptr : m.Hdata.data();
+        d.slope = m.slope.empty() ? nullptr : m.slope.data();
+    }
+    if (blk.empty()) {
+        warn("no block properties defined\n");
+        return false;
+    }
+    std::vector<xfk_label_desc> lab(labellist.size());
+    for (size_t k = 0; k < labellist.size(); k++) {
+        lab[k].block = labellist[k].BlockType >= 0 ? labellist[k].BlockType : 0;
+        lab[k].in_circuit = labellist[k].InCircuit;
+        lab[k].mag_dir = labellist[k].MagDir;
+        lab[k].is_wound = labellist[k].bIsWound ? 1 : 0;
+    }
+    std::vector<xfk_line_desc> lin(lineproplist.size());
+    for (size_t k = 0; k < lineproplist.size(); k++) {
+        const CMBoundaryProp &b = lineproplist[k];
+        lin[k] = xfk_line_desc{b.BdryFormat, b.A0, b.A1, b.A2, b.phi, b.c0_re, b.c1_re};
+    }
+    std::vector<xfk_point_desc> pts(nodeproplist.size());
+    for (size_t k = 0; k < nodeproplist.size(); k++)
+        pts[k] = xfk_point_desc{nodeproplist[k].A_re, nodeproplist[k].A_im, nodeproplist[k].J_re, nodeproplist[k].J_im};
+    std::vector<xfk_circuit_desc> cir(circproplist.size());
+    for (size_t k = 0; k < circproplist.size(); k++)
+        cir[k] = xfk_circuit_desc{circproplist[k].CircType, circproplist[k].Amps_re, circproplist[k].dVolts_re};
+    std::vector<double> x(NumNodes), y(NumNodes);
+    std::vector<int> marker(NumNodes), p(3LL * NumEls), e(3LL * NumEls), lbl(NumEls), pbc(3LL * NumPBCs);
+    for (int i = 0; i < NumNodes; i++) {
+        x[i] = meshnode[i].x;
+        y[i] = meshnode[i].y;
+        marker[i] = meshnode[i].BoundaryMarker;
+        if (marker[i] >= (int)nodeproplist.size()) marker[i] = -1;
+    }
+    for (int i = 0; i < NumEls; i++) {
+        if (labellist[meshele[i].lbl].BlockType < 0) {
+            warn("an element lies in a region without material (hole label)\n");
+            return false;
+        }
+        for (int q = 0; q < 3; q++) {
+            p[3LL * i + q] = meshele[i].p[q];
+            int eq = meshele[i].e[q];
+            e[3LL * i + q] = (eq >= 0 && eq < (int)lineproplist.size()) ? eq : -1;
+        }
+        lbl[i] = meshele[i].lbl;
+    }
+    for (int k = 0; k < NumPBCs; k++) {
+        pbc[3 * k] = pbclist[k].x;
+        pbc[3 * k + 1] = pbclist[k].y;
+        pbc[3 * k + 2] = pbclist[k].t;
+    }
+    xfk_problem_desc d{};
+    d.n_nodes = NumNodes; d.x = x.data(); d.y = y.data(); d.marker = marker.data();
+    d.n_elems = NumEls; d.p = p.data(); d.e = e.data(); d.lbl = lbl.data();
+    d.n_blocks = (int)blk.size(); d.blocks = blk.data();
+    d.n_labels = (int)lab.size(); d.labels = lab.data();
+    d.n_lines = (int)lin.size(); d.lines = lin.empty() ? nullptr : lin.data();
+    d.n_points = (int)pts.size(); d.points = pts.empty() ? nullptr : pts.data();
+    d.n_circs = (int)cir.size(); d.circs = cir.empty() ? nullptr : cir.data();
+    d.n_pbc = NumPBCs; d.pbc = NumPBCs ? pbc.data() : nullptr;
+    d.precision = Precision;
+    d.length_units = (int)LengthUnits;
+    d.coords = (int)Coords;
+    d.relax = Relax;
+
+    xfk_problem *prob = nullptr;
+    int rc = xfk_problem_create(&d, device, &prob);
+    if (rc == XFK_OK) rc = xfk_static2d(prob, 0, &stats);
+    if (rc == XFK_OK) {
+        A.assign(NumNodes, 0.0);
+        rc = xfk_get_solution(prob, A.data());
+    }
+    if (rc == XFK_OK && !circproplist.empty()) {
+        std::vector<int> cc(circproplist.size());
+        std::vector<double> J(circproplist.size()), dV(circproplist.size());
+        rc = xfk_get_circuits(prob, cc.data(), J.data(), dV.data());
+        for (size_t k = 0; rc == XFK_OK && k < circproplist.size(); k++) {
+            circproplist[k].Case = cc[k];
+            circproplist[k].J = J[k];
+            circproplist[k].dV = dV[k];
+        }
+    }
+    if (rc != XFK_OK) warn(std::string("GPU solver error: ") + xfk_last_error() + "\n");
+    if (prob) xfk_problem_destroy(prob);
+    return rc == XFK_OK;
+}
+
+int FSolver::WriteStatic2D()
+{
+    const double unitconv[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
+    std::string fin = PathName + ".fem", fout = PathName + ".ans";
+    FILE *fz = fopen(fin.c_str(), "rt");
+    if (!fz) {
+        warn("Couldn't open " + fin + "\n");
+        return false;
+    }
+    FILE *fp = fopen(fout.c_str(), "wt");
+    if (!fp) {
+        fclose(fz);
+        warn("Couldn't write to " + fout + "\n");
+        return false;
+    }
+    char c[1024];
+    while (fgets(c, 1024, fz) != nullptr) fputs(c, fp);
+    fclose(fz);
+    fprintf(fp, "[Solution]\n");
+    const double cf = unitconv[LengthUnits];
+    fprintf(fp, "%i\n", NumNodes);
+    for (int i = 0; i < NumNodes; i++)
+        fprintf(fp, "%.17g\t%.17g\t%.17g\t%i\n", meshnode[i].x / cf, meshnode[i].y / cf, A[i],
+                meshnode[i].BoundaryMarker);
+    fprintf(fp, "%i\n", NumEls);
+    for (int i = 0; i < NumEls; i++)
+        fprintf(fp, "%i\t%i\t%i\t%i\n", meshele[i].p[0], meshele[i].p[1], meshele[i].p[2], meshele[i].lbl);
+    fprintf(fp, "%i\n", (int)labellist.size());
+    for (size_t k = 0; k < labellist.size(); k++) {
+        int i = labellist[k].InCircuit;
+        if (i < 0) fprintf(fp, "1\t0\n");
+        else {
+            if (circproplist[i].Case == 0) fprintf(fp, "0\t%.17g\n", circproplist[i].dV);
+            if (circproplist[i].Case == 1) fprintf(fp, "1\t%.17g\n", circproplist[i].J);
+        }
+    }
+    fprintf(fp, "%i\n", NumPBCs);
+    for (int k = 0; k < NumPBCs; k++) fprintf(fp, "%i\t%i\t%i\n", pbclist[k].x, pbclist[k].y, pbclist[k].t);
+    fprintf(fp, "%i\n", NumAirGapElems);
+    fclose(fp);
+    return true;
+}
+
+bool FSolver::runSolver(bool verbose)
+{
+    LoadMeshErr err = LoadMesh(deleteMeshFiles);
+    if (err != NOERROR) {
+        warn(getErrorString(err));
+        return false;
+    }
+    if (previousSolutionFile.empty()) {
+        if (verbose) PrintMessage("renumbering nodes using Cuthill-McKee method\n");
+        if (!Cuthill(deleteMeshFiles)) {
+            warn("problem renumbering node points\n");
+            return false;
+        }
+    }
+    if (verbose) {
+        PrintMessage("solving...\n");
+        PrintMessage("Problem Statistics:\n%i nodes\n%i elements\nPrecision: %f\n", NumNodes, NumEls, Precision);
+    }
+    if (Frequency != 0) {
+        warn("harmonic (Frequency != 0) problems are not supported by this solver build\n");
+        return false;
+    }
+    if (ProblemTypeV != PLANAR) {
+        warn("axisymmetric problems are not supported by this solver build\n");
+        return false;
+    }
+    if (!Static2D()) {
+        warn("Couldn't solve the problem\n");
+        return false;
+    }
+    if (verbose) PrintMessage("Static 2-D problem solved\n");
+    if (!WriteStatic2D()) {
+        warn("couldn't write results to disk\n");
+        return false;
+    }
+    if (verbose) PrintMessage("results written to disk\n");
+    return true;
+}
+
+}  // namespace xfemm

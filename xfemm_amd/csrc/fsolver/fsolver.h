@@ -1,0 +1,66 @@
+// FSolver: the magnetics solver object of the reference (cfemm/fsolver/fsolver.h),
+// re-hosted over the MI355X kernels (include/xfemm_kernels.h).
+//
+// Same public surface and behaviour for the static planar path:
+//   PathName, LoadProblemFile(), LoadMesh(), Cuthill(), runSolver(verbose),
+//   Static2D(), WriteStatic2D(), WarnMessage / PrintMessage hooks,
+//   meshnode / meshele / *proplist / pbclist state.
+// The linear system never exists on the host: Static2D() uploads the mesh
+// and property tables and runs assembly + PCG + Newton on the GPU.
+#pragma once
+
+#include <array>
+#include <string>
+#include <vector>
+
+#include "../../../include/xfemm_kernels.h"
+#include "femm_problem.h"
+
+namespace xfemm {
+
+enum LoadMeshErr { NOERROR, BADFEMFILE, BADNODEFILE, BADPBCFILE, BADELEMENTFILE, BADEDGEFILE, MISSINGMATPROPS,
+                   ELMLABELTOOBIG, UNSUPPORTEDMESH };
+
+int PrintWarningMsg(const char *fmt, ...);
+
+class FSolver : public FemmProblemData {
+public:
+    FSolver();
+    ~FSolver() = default;
+
+    // General problem attributes (fsolver.h / feasolver.h)
+    std::string PathName;
+    double Relax = 0.0;
+    int NumNodes = 0, NumEls = 0, BandWidth = 0, NumPBCs = 0, NumAirGapElems = 0, NumCircPropsOrig = 0;
+    std::vector<CNode> meshnode;
+    std::vector<CMElement> meshele;
+    std::vector<CCommonPoint> pbclist;
+
+    int (*WarnMessage)(const char *, ...);
+    int (*PrintMessage)(const char *, ...);
+
+    // GPU selection and file handling
+    int device = 0;
+    bool deleteMeshFiles = true;
+
+    bool LoadProblemFile();                              // fsolver.cpp:202-348
+    LoadMeshErr LoadMesh(bool deleteFiles = true);       // fsolver.cpp:350-718
+    int Cuthill(bool deleteFiles = true);                // cuthill.cpp:88-390
+    int SortElements();                                  // cuthill.cpp:39-86
+    bool runSolver(bool verbose = false);                // fsolver.cpp:1213-1338
+    int Static2D();                                      // static2d.cpp:53-1033 (on the GPU)
+    int WriteStatic2D();                                 // static2d.cpp:1038-1195
+    void GetFillFactor(int lbl);                         // fsolver.cpp:1083-1105 (static)
+    static std::string getErrorString(LoadMeshErr err);
+
+    // result of the last Static2D: A (= V*c) per node, in meshnode order
+    std::vector<double> A;
+    xfk_result stats{};
+    std::string lastError;
+
+private:
+    std::vector<std::array<int, 3>> edges_;   // .edge content: n0, n1, marker
+    void warn(const std::string &msg);
+};
+
+}  // namespace xfemm

@@ -445,8 +445,15 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
     int batch = 16;
     for (;;) {
         for (int k = 0; k < batch; ++k) {
+            const bool stamp = P->time_spmv && ((launched + k) % 16 == 0) &&
+                               P->spmv_used + 2 <= (int)P->spmv_ev.size();
+            if (stamp) XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used], s));
             launch_pcg_spmv(s, N, P->rowptr.p, P->col.p, P->val.p, P->P.p, P->U.p, P->partials.p,
                             P->counters.p + 1, P->pcg.p);
+            if (stamp) {
+                XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used + 1], s));
+                P->spmv_used += 2;
+            }
             launch_pcg_update(s, N, P->V.p, P->R.p, P->P.p, P->U.p, P->dinv.p, P->partials.p, P->counters.p + 2,
                               P->pcg.p);
             launch_pcg_dir(s, N, P->R.p, P->dinv.p, P->P.p, P->pcg.p);
@@ -490,6 +497,7 @@ void xfk_problem_destroy(xfk_problem *P)
     if (!P) return;
     (void)hipSetDevice(P->device);
     if (P->stream) (void)hipStreamSynchronize(P->stream);
+    for (auto &ev : P->spmv_ev) (void)hipEventDestroy(ev);
     P->x.free(); P->y.free(); P->p_raw.free(); P->lbl_raw.free(); P->ebits_raw.free();
     P->blocks.free(); P->labels.free(); P->lines.free(); P->circs.free();
     P->bhB.free(); P->bhH.free(); P->bhS.free();
@@ -770,6 +778,12 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     xfk_result R{};
     int rc = XFK_OK;
     float ms = 0;
+    P->time_spmv = (flags & XFK_TIME_SPMV) != 0;
+    P->spmv_used = 0;
+    if (P->time_spmv && P->spmv_ev.empty()) {
+        P->spmv_ev.resize(2 * 512);
+        for (auto &ev : P->spmv_ev) XFK_CHECK(hipEventCreate(&ev));
+    }
     XFK_CHECK(hipEventRecord(e0, s));
     if (!P->symbolic_ready || (flags & XFK_REBUILD_SYMBOLIC)) {
         P->symbolic_ready = false;
@@ -832,6 +846,16 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipEventDestroy(e2);
+    if (P->time_spmv && P->spmv_used > 0) {
+        double sum = 0;
+        for (int k = 0; k < P->spmv_used; k += 2) {
+            float m = 0;
+            XFK_CHECK(hipEventElapsedTime(&m, P->spmv_ev[k], P->spmv_ev[k + 1]));
+            sum += m;
+        }
+        R.spmv_samples = P->spmv_used / 2;
+        R.spmv_ms_avg = sum / R.spmv_samples;
+    }
     R.newton_iters = Iter;
     R.last_res = resn;
     R.nnz = P->nnz;

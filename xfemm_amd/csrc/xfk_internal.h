@@ -197,6 +197,11 @@ struct xfk_problem {
     xfk::PcgScalars *pcg_host = nullptr;  // pinned mirror
     xfk::NewtonScalars *nws_host = nullptr;
 
+    // live SpMV launch timing (XFK_TIME_SPMV)
+    bool time_spmv = false;
+    std::vector<hipEvent_t> spmv_ev;   // pairs
+    int spmv_used = 0;
+
     // last-solve statistics
     xfk_result last{};
 };

@@ -21,6 +21,7 @@ iptr = C.POINTER(C.c_int)
 
 XFK_OK = 0
 XFK_REBUILD_SYMBOLIC = 1
+XFK_TIME_SPMV = 2
 
 # every symbol include/xfemm_kernels.h declares
 EXPORTED = (
@@ -72,7 +73,8 @@ class ProblemDesc(C.Structure):
 class Result(C.Structure):
     _fields_ = [("newton_iters", C.c_int), ("cg_iters", C.c_longlong), ("last_res", C.c_double),
                 ("final_er", C.c_double), ("nnz", C.c_longlong), ("ncolors", C.c_int),
-                ("ms_symbolic", C.c_double), ("ms_assemble", C.c_double), ("ms_solve", C.c_double)]
+                ("ms_symbolic", C.c_double), ("ms_assemble", C.c_double), ("ms_solve", C.c_double),
+                ("spmv_ms_avg", C.c_double), ("spmv_samples", C.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -210,9 +212,10 @@ class Static2DProblem:
         except Exception:
             pass
 
-    def solve(self, rebuild_symbolic: bool = False) -> dict:
+    def solve(self, rebuild_symbolic: bool = False, time_spmv: bool = False) -> dict:
         r = Result()
-        _check(_lib.xfk_static2d(self._h, XFK_REBUILD_SYMBOLIC if rebuild_symbolic else 0, C.byref(r)))
+        flags = (XFK_REBUILD_SYMBOLIC if rebuild_symbolic else 0) | (XFK_TIME_SPMV if time_spmv else 0)
+        _check(_lib.xfk_static2d(self._h, flags, C.byref(r)))
         self.result = r
         return r.as_dict()
 

@@ -99,6 +99,12 @@ def magnetostatic(n: int, nonlinear: bool = False, L: float = 10.0, J: float = 2
     if nonlinear:
         blocks[1] = dict(mu_x=1.0, mu_y=1.0, LamFill=0.98, LamType=0, bh="M19")
     labels = [dict(block=0), dict(block=1), dict(block=2), dict(block=3), dict(block=4, mag_dir=90.0)]
+    for b in blocks:
+        if b.get("bh") == "M19":
+            from .fsolver import bh_get_slopes
+            Bc, Hc, Sc, mu = bh_get_slopes(*m19_curve(), lam_type=b.get("LamType", 0),
+                                           lam_fill=b.get("LamFill", 1.0))
+            b.update(B=Bc, H=Hc, slope=Sc, mu_x=mu, mu_y=mu)
     tol = 1e-9 * L
     e = _boundary_edges(p, x, y, L, tol)
     lines = [dict(format=0)]
@@ -173,3 +179,60 @@ def write_problem(base: str, kw: dict, label_xy: Optional[np.ndarray] = None) ->
             fh.write("%d\t%d\t%d\t%d\n" % (n, k[0], k[1], mk))
     with open(base + ".pbc", "w") as fh:
         fh.write("0\n0\n")
+
+
+def bc_showcase(n: int, anti: bool = False, nonlinear: bool = False, L: float = 10.0):
+    """Every static boundary-condition path of Static2D on one square mesh:
+    left side prescribed A = (A0 + A1*y)*cos(phi) (BdryFormat 0, static2d.cpp:840-926),
+    right side mixed c0/c1 (BdryFormat 2, static2d.cpp:459-480), bottom/top
+    periodic or antiperiodic node pairs including the corner nodes
+    (static2d.cpp:929-940), a point current and a prescribed point value
+    (static2d.cpp:818-838)."""
+    kw = magnetostatic(n, nonlinear=nonlinear, L=L)
+    x, y, p = kw["x"], kw["y"], kw["p"]
+    tol = 1e-9 * L
+    m = n + 1
+    e = -np.ones(p.shape, dtype=np.int32)
+    for j in range(3):
+        a, b = p[:, j], p[:, (j + 1) % 3]
+        left = (np.abs(x[a]) < tol) & (np.abs(x[b]) < tol)
+        right = (np.abs(x[a] - L) < tol) & (np.abs(x[b] - L) < tol)
+        bot = (np.abs(y[a]) < tol) & (np.abs(y[b]) < tol)
+        top = (np.abs(y[a] - L) < tol) & (np.abs(y[b] - L) < tol)
+        e[left, j] = 0
+        e[right, j] = 1
+        e[bot | top, j] = 2
+    kw["e"] = e
+    kw["lines"] = [dict(format=0, A0=1e-3, A1=2e-4, A2=0.0, phi=30.0),
+                   dict(format=2, c0=3.0, c1=0.5),
+                   dict(format=5 if anti else 4)]
+    bottom = np.arange(m)                 # row 0
+    top = (m - 1) * m + np.arange(m)      # row n
+    kw["pbc"] = np.stack([bottom, top, np.full(m, 1 if anti else 0)], 1).astype(np.int32)
+    marker = -np.ones(len(x), dtype=np.int32)
+    marker[(m // 2) * m + m // 3] = 0     # point current
+    marker[(m // 3) * m + (2 * m) // 3] = 1   # fixed A
+    kw["marker"] = marker
+    kw["points"] = [dict(J_re=5.0), dict(A_re=2e-3)]
+    return kw
+
+
+def bc_chain(n: int, L: float = 10.0):
+    """Doubly periodic square: left/right and bottom/top node pairs, so the
+    four corner nodes each sit in two pairs and the reference's sequential
+    CBigLinProb::Periodicity calls (spars.cpp:421-474) chain.  A prescribed
+    point value pins the otherwise floating potential."""
+    kw = magnetostatic(n, L=L)
+    x, y, p = kw["x"], kw["y"], kw["p"]
+    m = n + 1
+    kw["e"] = -np.ones(p.shape, dtype=np.int32)
+    kw["lines"] = [dict(format=4)]
+    rows = np.arange(m)
+    lr = np.stack([rows * m, rows * m + (m - 1), np.zeros(m, int)], 1)
+    bt = np.stack([np.arange(m), (m - 1) * m + np.arange(m), np.zeros(m, int)], 1)
+    kw["pbc"] = np.concatenate([lr, bt]).astype(np.int32)
+    marker = -np.ones(len(x), dtype=np.int32)
+    marker[(m // 2) * m + m // 2] = 0
+    kw["marker"] = marker
+    kw["points"] = [dict(A_re=0.0)]
+    return kw
