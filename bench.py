@@ -38,9 +38,10 @@ def _hip_sync():
 
 
 def spmv_bytes(n_rows, nnz):
-    """Algorithmic HBM bytes of one CSR SpMV launch (k_pcg_spmv):
-    val 8 B + col 4 B per nonzero, rowptr 4 B per row (+1), x read once 8 B
-    per row, y write 8 B per row (the fused p.Ap dot re-reads x from cache)."""
+    """Algorithmic HBM bytes of one CSR SpMV launch of the PCG (k_cg_spmv,
+    xfemm_amd/csrc/xfk_pcg.hip): val 8 B + col 4 B per nonzero, rowptr 4 B per
+    row (+1), u read once 8 B per row, w written 8 B per row (the fused u.w
+    partial re-reads u from cache)."""
     return 12 * nnz + 4 * (n_rows + 1) + 16 * n_rows
 
 
@@ -126,7 +127,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # roofline of the dominant kernel (CSR SpMV of the PCG), measured live
+    # roofline of the dominant kernel (the CSR SpMV of the PCG), measured live
     spmv_ms = sum(r["spmv_ms_avg"] * r["spmv_samples"] for r in results) / max(
         1, sum(r["spmv_samples"] for r in results))
     nnz = results[-1]["nnz"]
@@ -157,7 +158,7 @@ def main():
             "nnz": nnz,
             "pcg_iters": results[-1]["cg_iters"],
             "newton_iters": results[-1]["newton_iters"],
-            "preconditioner": "jacobi",
+            "preconditioner": "jacobi", "pcg": "Chronopoulos-Gear, 2 launches/iteration",
             "ms_symbolic": results[-1]["ms_symbolic"],
             "ms_assemble": results[-1]["ms_assemble"],
             "ms_solve": results[-1]["ms_solve"],
@@ -165,7 +166,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_pcg_spmv",
+            "kernel": "k_cg_spmv (CSR SpMV of the PCG, LDS row tiles, fused u.w partial)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -191,6 +191,8 @@ static hipError_t exclusive_scan(hipStream_t s, const int *in, int *out, int n)
     return e != hipSuccess ? e : e2;
 }
 
+static int alloc_cg(xfk_problem *P);
+
 static int build_symbolic(xfk_problem *P)
 {
     hipStream_t s = P->stream;
@@ -378,12 +380,14 @@ static int build_symbolic(xfk_problem *P)
     }
 
     // vectors and reduction scratch
-    for (DBuf<double> *v : {&P->b, &P->V, &P->Vold, &P->R, &P->P, &P->U, &P->dinv}) XFK_CHECK(v->alloc(N));
+    for (DBuf<double> *v : {&P->b, &P->V, &P->Vold, &P->P, &P->dinv}) XFK_CHECK(v->alloc(N));
     XFK_CHECK(P->partials.alloc(2 * kRedGrid));
     XFK_CHECK(P->counters.alloc(8));
     XFK_CHECK(hipMemsetAsync(P->counters.p, 0, sizeof(unsigned) * 8, s));
     XFK_CHECK(P->pcg.alloc(1));
     XFK_CHECK(P->nws.alloc(1));
+    int rc2 = alloc_cg(P);
+    if (rc2 != XFK_OK) return rc2;
     XFK_CHECK(hipStreamSynchronize(s));
     P->symbolic_ready = true;
     return XFK_OK;
@@ -424,47 +428,99 @@ static int assemble(xfk_problem *P, int iter)
     return XFK_OK;
 }
 
-// CBigLinProb::PCGSolve(flag) on the assembled system (Jacobi-preconditioned)
-static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
+// CBigLinProb::PCGSolve(flag) on the assembled system (Jacobi-preconditioned,
+// two launches per iteration: xfk_pcg.hip)
+static int alloc_cg(xfk_problem *P)
+{
+    const int N = P->N, G = std::max(cg_grid(N), cg_axpy_grid(N));
+    XFK_CHECK(P->R2.alloc((size_t)N));      // r
+    XFK_CHECK(P->W2.alloc((size_t)N));      // w = A u
+    XFK_CHECK(P->Z2.alloc(2 * (size_t)N));  // z (first half), u = M^-1 r (second half)
+    XFK_CHECK(P->part_cg.alloc(3 * (size_t)G));   // gamma[2] + delta
+    XFK_CHECK(P->part_reso.alloc((size_t)G));
+    return XFK_OK;
+}
+
+static CgAxpyArgs cg_args(xfk_problem *P, long long it)
+{
+    const int N = P->N, G = std::max(cg_grid(N), cg_axpy_grid(N));
+    CgAxpyArgs A;
+    A.W = P->W2.p;
+    A.dinv = P->dinv.p;
+    A.Z = P->Z2.p;
+    A.U = P->Z2.p + N;
+    A.P = P->P.p;
+    A.V = P->V.p;
+    A.R = P->R2.p;
+    A.gam_in = P->part_cg.p + (size_t)(it & 1) * G;
+    A.gam_out = P->part_cg.p + (size_t)((it + 1) & 1) * G;
+    A.del_in = P->part_cg.p + 2 * (size_t)G;
+    A.reso = P->part_reso.p;
+    A.Ggam = (it == 0) ? cg_grid(N) : cg_axpy_grid(N);
+    A.Gdel = cg_grid(N);
+    A.S = P->pcg.p;
+    A.it = it;
+    A.N = N;
+    return A;
+}
+
+static int pcg_start(xfk_problem *P, int flag)
 {
     hipStream_t s = P->stream;
     const int N = P->N;
-    PcgScalars init{};
+    CgState init{};
     init.tol = P->precision;
-    XFK_CHECK(hipMemcpyAsync(P->pcg.p, &init, sizeof(PcgScalars), hipMemcpyHostToDevice, s));
+    XFK_CHECK(hipMemcpyAsync(P->pcg.p, &init, sizeof(CgState), hipMemcpyHostToDevice, s));
     launch_diag_inv(s, N, P->diag.p, P->val.p, P->dinv.p, P->pcg.p);
-    XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(PcgScalars), hipMemcpyDeviceToHost, s));
+    XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(CgState), hipMemcpyDeviceToHost, s));
     XFK_CHECK(hipStreamSynchronize(s));
     if (P->pcg_host->singular) {
         set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
         return XFK_ERR_SINGULAR;
     }
-    launch_pcg_init(s, N, flag, P->rowptr.p, P->col.p, P->val.p, P->b.p, P->V.p, P->R.p, P->P.p, P->dinv.p,
-                    P->partials.p, P->counters.p, P->pcg.p);
-    long long launched = 0;
+    const CgAxpyArgs A0 = cg_args(P, 0);
+    launch_cg_init(s, N, flag, P->rowptr.p, P->col.p, P->val.p, P->b.p, P->V.p, A0.R, A0.U, A0.Z, A0.P, P->W2.p,
+                   P->dinv.p, P->part_reso.p, (double *)A0.gam_in, (double *)A0.del_in);
+    return XFK_OK;
+}
+
+// one PCG iteration: the streaming update then the SpMV (optionally bracketed
+// by HIP events for the live roofline)
+static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
+{
+    hipStream_t s = P->stream;
+    const CgAxpyArgs A = cg_args(P, it);
+    launch_cg_axpy(s, A);
+    if (stamp) XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used], s));
+    launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, (double *)A.del_in, P->pcg.p);
+    if (stamp) {
+        XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used + 1], s));
+        P->spmv_used += 2;
+    }
+    return XFK_OK;
+}
+
+static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
+{
+    hipStream_t s = P->stream;
+    int rc = alloc_cg(P);
+    if (rc != XFK_OK) return rc;
+    rc = pcg_start(P, flag);
+    if (rc != XFK_OK) return rc;
+    long long it = 0;
     int batch = 16;
     for (;;) {
-        for (int k = 0; k < batch; ++k) {
-            const bool stamp = P->time_spmv && ((launched + k) % 16 == 0) &&
-                               P->spmv_used + 2 <= (int)P->spmv_ev.size();
-            if (stamp) XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used], s));
-            launch_pcg_spmv(s, N, P->rowptr.p, P->col.p, P->val.p, P->P.p, P->U.p, P->partials.p,
-                            P->counters.p + 1, P->pcg.p);
-            if (stamp) {
-                XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used + 1], s));
-                P->spmv_used += 2;
-            }
-            launch_pcg_update(s, N, P->V.p, P->R.p, P->P.p, P->U.p, P->dinv.p, P->partials.p, P->counters.p + 2,
-                              P->pcg.p);
-            launch_pcg_dir(s, N, P->R.p, P->dinv.p, P->P.p, P->pcg.p);
+        for (int k = 0; k < batch; ++k, ++it) {
+            const bool stamp = P->time_spmv && (it % 16 == 0) && P->spmv_used + 2 <= (int)P->spmv_ev.size();
+            rc = pcg_iteration(P, it, stamp);
+            if (rc != XFK_OK) return rc;
         }
-        launched += batch;
         XFK_CHECK(hipGetLastError());
-        XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(PcgScalars), hipMemcpyDeviceToHost, s));
+        XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(CgState), hipMemcpyDeviceToHost, s));
         XFK_CHECK(hipStreamSynchronize(s));
-        const PcgScalars &S = *P->pcg_host;
+        const CgState &S = *P->pcg_host;
         if (S.done) break;
-        if (launched >= max_iters) {
+        if (it >= max_iters) {
             set_error("PCG did not converge within the iteration cap");
             return XFK_ERR_NOCONV;
         }
@@ -508,7 +564,8 @@ void xfk_problem_destroy(xfk_problem *P)
     P->fix_rows.free(); P->fix_cols.free(); P->fix_cols_node.free(); P->fix_cols_row.free();
     P->pm_dst.free(); P->pm_ptr.free(); P->pm_src.free(); P->pm_w.free(); P->pm_tmp.free();
     P->pb_dst.free(); P->pb_ptr.free(); P->pb_src.free(); P->pb_w.free(); P->pb_tmp.free();
-    P->val.free(); P->b.free(); P->V.free(); P->Vold.free(); P->R.free(); P->P.free(); P->U.free();
+    P->val.free(); P->b.free(); P->V.free(); P->Vold.free(); P->P.free();
+    P->R2.free(); P->W2.free(); P->Z2.free(); P->part_cg.free(); P->part_reso.free();
     P->dinv.free(); P->partials.free(); P->counters.free(); P->pcg.free(); P->nws.free();
     if (P->pcg_host) (void)hipHostFree(P->pcg_host);
     if (P->nws_host) (void)hipHostFree(P->nws_host);
@@ -751,7 +808,7 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
     UP(P->fix_last, last.data(), last.size());
     UP(P->fix_rows, fix_rows.data(), fix_rows.size());
 #undef UP
-    if (e == hipSuccess) e = hipHostMalloc((void **)&P->pcg_host, sizeof(PcgScalars));
+    if (e == hipSuccess) e = hipHostMalloc((void **)&P->pcg_host, sizeof(CgState));
     if (e == hipSuccess) e = hipHostMalloc((void **)&P->nws_host, sizeof(NewtonScalars));
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {
@@ -945,13 +1002,13 @@ int xfk_pcg_solve_csr(int n, const int *rowptr, const int *col, const double *va
     if (e == hipSuccess) e = upload(P->b, b, (size_t)n, s);
     if (e == hipSuccess) e = upload(P->V, V, (size_t)n, s);
     if (e == hipSuccess) e = upload(P->diag, diag.data(), (size_t)n, s);
-    for (DBuf<double> *v : {&P->R, &P->P, &P->U, &P->dinv})
+    for (DBuf<double> *v : {&P->P, &P->dinv})
         if (e == hipSuccess) e = v->alloc(n);
     if (e == hipSuccess) e = P->partials.alloc(2 * kRedGrid);
     if (e == hipSuccess) e = P->counters.alloc(8);
     if (e == hipSuccess) e = hipMemsetAsync(P->counters.p, 0, sizeof(unsigned) * 8, s);
     if (e == hipSuccess) e = P->pcg.alloc(1);
-    if (e == hipSuccess) e = hipHostMalloc((void **)&P->pcg_host, sizeof(PcgScalars));
+    if (e == hipSuccess) e = hipHostMalloc((void **)&P->pcg_host, sizeof(CgState));
     if (e != hipSuccess) {
         set_error(std::string("pcg setup failed: ") + hipGetErrorString(e));
         rc = XFK_ERR_HIP;
@@ -971,38 +1028,40 @@ int xfk_pcg_time(xfk_problem *P, int iters, double *ms_spmv, double *ms_iter)
     XFK_REQUIRE(P && P->symbolic_ready && iters > 0, XFK_ERR_ARG, "no assembled system");
     XFK_CHECK(hipSetDevice(P->device));
     hipStream_t s = P->stream;
-    const int N = P->N;
-    PcgScalars init{};
-    init.tol = 0.0;   // never converges: fixed iteration count
-    XFK_CHECK(hipMemcpyAsync(P->pcg.p, &init, sizeof(PcgScalars), hipMemcpyHostToDevice, s));
-    launch_diag_inv(s, N, P->diag.p, P->val.p, P->dinv.p, P->pcg.p);
-    launch_pcg_init(s, N, 1, P->rowptr.p, P->col.p, P->val.p, P->b.p, P->V.p, P->R.p, P->P.p, P->dinv.p,
-                    P->partials.p, P->counters.p, P->pcg.p);
-    std::vector<hipEvent_t> ev(2 * iters + 2);
-    for (auto &x : ev) XFK_CHECK(hipEventCreate(&x));
-    XFK_CHECK(hipEventRecord(ev[2 * iters], s));
-    for (int k = 0; k < iters; ++k) {
-        XFK_CHECK(hipEventRecord(ev[2 * k], s));
-        launch_pcg_spmv(s, N, P->rowptr.p, P->col.p, P->val.p, P->P.p, P->U.p, P->partials.p, P->counters.p + 1,
-                        P->pcg.p);
-        XFK_CHECK(hipEventRecord(ev[2 * k + 1], s));
-        launch_pcg_update(s, N, P->V.p, P->R.p, P->P.p, P->U.p, P->dinv.p, P->partials.p, P->counters.p + 2,
-                          P->pcg.p);
-        launch_pcg_dir(s, N, P->R.p, P->dinv.p, P->P.p, P->pcg.p);
+    const double tol = P->precision;
+    P->precision = 0.0;   // never converges: fixed iteration count
+    int rc = pcg_start(P, 1);
+    P->precision = tol;
+    if (rc != XFK_OK) return rc;
+    if ((int)P->spmv_ev.size() < 2 * iters) {
+        for (auto &ev : P->spmv_ev) (void)hipEventDestroy(ev);
+        P->spmv_ev.resize(2 * iters);
+        for (auto &ev : P->spmv_ev) XFK_CHECK(hipEventCreate(&ev));
     }
-    XFK_CHECK(hipEventRecord(ev[2 * iters + 1], s));
-    XFK_CHECK(hipEventSynchronize(ev[2 * iters + 1]));
-    double sum = 0;
+    hipEvent_t t0, t1;
+    XFK_CHECK(hipEventCreate(&t0));
+    XFK_CHECK(hipEventCreate(&t1));
+    P->spmv_used = 0;
+    XFK_CHECK(hipEventRecord(t0, s));
     for (int k = 0; k < iters; ++k) {
+        rc = pcg_iteration(P, k, true);
+        if (rc != XFK_OK) return rc;
+    }
+    XFK_CHECK(hipEventRecord(t1, s));
+    XFK_CHECK(hipEventSynchronize(t1));
+    double sum = 0;
+    for (int k = 0; k < P->spmv_used; k += 2) {
         float m = 0;
-        XFK_CHECK(hipEventElapsedTime(&m, ev[2 * k], ev[2 * k + 1]));
+        XFK_CHECK(hipEventElapsedTime(&m, P->spmv_ev[k], P->spmv_ev[k + 1]));
         sum += m;
     }
     float tot = 0;
-    XFK_CHECK(hipEventElapsedTime(&tot, ev[2 * iters], ev[2 * iters + 1]));
-    for (auto &x : ev) (void)hipEventDestroy(x);
-    if (ms_spmv) *ms_spmv = sum / iters;
+    XFK_CHECK(hipEventElapsedTime(&tot, t0, t1));
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    if (ms_spmv) *ms_spmv = sum / (P->spmv_used / 2);
     if (ms_iter) *ms_iter = tot / iters;
+    P->spmv_used = 0;
     return XFK_OK;
 }
 

@@ -580,7 +580,7 @@ __global__ void k_map_scatter(int n, const int *__restrict__ dst, const double *
 
 // Jacobi preconditioner + the reference's singularity check (spars.cpp:245)
 __global__ void k_diag_inv(int N, const int *__restrict__ diag, const double *__restrict__ val,
-                           double *__restrict__ dinv, PcgScalars *__restrict__ S)
+                           double *__restrict__ dinv, CgState *__restrict__ S)
 {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
@@ -591,162 +591,6 @@ __global__ void k_diag_inv(int N, const int *__restrict__ diag, const double *__
     } else {
         dinv[i] = 1.0 / d;
     }
-}
-
-// --------------------------------------------------------------------------
-// PCG (CBigLinProb::PCGSolve, spars.cpp:238-316) with the Jacobi
-// preconditioner M = diag(A).  Three launches per iteration, each ending in a
-// deterministic grid reduction whose last block updates the scalars.
-// --------------------------------------------------------------------------
-
-constexpr int kTileRows = kBlock;        // rows per LDS row tile
-constexpr int kTileCap = 2048;           // products staged per pass (16 KiB of f64)
-
-// y = A x for the rows of one tile, CSR-stream: the tile's nonzeros are read
-// coalesced (val, col), multiplied by the gathered x and staged in LDS; each
-// thread then reduces its own row from LDS.
-__device__ __forceinline__ double tile_spmv_row(int r0, int N, const int *__restrict__ rowptr,
-                                                const int *__restrict__ col,
-                                                const double *__restrict__ val,
-                                                const double *__restrict__ x, double *lds)
-{
-    const int r = r0 + threadIdx.x;
-    const int rend = min(r0 + kTileRows, N);
-    const int s = rowptr[r0], e = rowptr[rend];
-    const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
-    double acc = 0.0;
-    for (int c0 = s; c0 < e; c0 += kTileCap) {
-        const int c1 = min(e, c0 + kTileCap);
-        for (int k = c0 + threadIdx.x; k < c1; k += kBlock) lds[k - c0] = val[k] * x[col[k]];
-        __syncthreads();
-        const int a = max(my_s, c0), z = min(my_e, c1);
-        for (int k = a; k < z; ++k) acc += lds[k - c0];
-        __syncthreads();
-    }
-    return acc;
-}
-
-// R = b - A V (V = 0 when flag == 0), P = M^-1 R; partials z.r and (M^-1 b).b
-__global__ void __launch_bounds__(kBlock) k_pcg_init(int N, int flag, const int *__restrict__ rowptr,
-                                                     const int *__restrict__ col, const double *__restrict__ val,
-                                                     const double *__restrict__ b, double *__restrict__ V,
-                                                     double *__restrict__ R, double *__restrict__ P,
-                                                     const double *__restrict__ dinv, double *partials,
-                                                     unsigned *counter, PcgScalars *S)
-{
-    __shared__ double lds[kTileCap];
-    __shared__ double red[8];
-    __shared__ int last;
-    double zr = 0.0, zb = 0.0;
-    const int ntiles = (N + kTileRows - 1) / kTileRows;
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int r0 = tile * kTileRows;
-        double ax = 0.0;
-        if (flag) ax = tile_spmv_row(r0, N, rowptr, col, val, V, lds);
-        const int r = r0 + threadIdx.x;
-        if (r < N) {
-            const double br = b[r], di = dinv[r];
-            const double rr = br - ax;
-            const double z = rr * di;
-            if (!flag) V[r] = 0.0;
-            R[r] = rr;
-            P[r] = z;
-            zr += z * rr;
-            zb += (br * di) * br;
-        }
-    }
-    double v[2];
-    v[0] = block_sum(zr, red);
-    v[1] = block_sum(zb, red);
-    if (publish_partials<2>(v, partials, counter, &last)) {
-        double a0 = gather_partials(partials, 0, red);
-        double a1 = gather_partials(partials, 1, red);
-        if (threadIdx.x == 0) {
-            S->res = a0;
-            S->res_o = a1;
-            S->iters = 0;
-            S->er = (a1 == 0.0) ? 0.0 : sqrt(a0 / a1);
-            S->done = (a1 == 0.0) ? 1 : 0;
-            reset_counter(counter);
-        }
-    }
-}
-
-// U = A P; partial P.U; last block: del = res / pAp
-__global__ void __launch_bounds__(kBlock) k_pcg_spmv(int N, const int *__restrict__ rowptr,
-                                                     const int *__restrict__ col, const double *__restrict__ val,
-                                                     const double *__restrict__ P, double *__restrict__ U,
-                                                     double *partials, unsigned *counter, PcgScalars *S)
-{
-    if (S->done) return;
-    __shared__ double lds[kTileCap];
-    __shared__ double red[8];
-    __shared__ int last;
-    double pu = 0.0;
-    const int ntiles = (N + kTileRows - 1) / kTileRows;
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int r0 = tile * kTileRows;
-        double u = tile_spmv_row(r0, N, rowptr, col, val, P, lds);
-        const int r = r0 + threadIdx.x;
-        if (r < N) {
-            U[r] = u;
-            pu += P[r] * u;
-        }
-    }
-    double v[1];
-    v[0] = block_sum(pu, red);
-    if (publish_partials<1>(v, partials, counter, &last)) {
-        double s = gather_partials(partials, 0, red);
-        if (threadIdx.x == 0) {
-            S->del = S->res / s;
-            reset_counter(counter);
-        }
-    }
-}
-
-// V += del P; R -= del U; partial (M^-1 R).R; last block: rho, res, er, done
-__global__ void __launch_bounds__(kBlock) k_pcg_update(int N, double *__restrict__ V, double *__restrict__ R,
-                                                       const double *__restrict__ P, const double *__restrict__ U,
-                                                       const double *__restrict__ dinv, double *partials,
-                                                       unsigned *counter, PcgScalars *S)
-{
-    if (S->done) return;
-    __shared__ double red[8];
-    __shared__ int last;
-    const double del = S->del;
-    double zr = 0.0;
-    for (int r = blockIdx.x * kBlock + threadIdx.x; r < N; r += gridDim.x * kBlock) {
-        double v = V[r], rr = R[r];
-        v += (del * P[r]);
-        rr -= (del * U[r]);
-        V[r] = v;
-        R[r] = rr;
-        zr += (rr * dinv[r]) * rr;
-    }
-    double v[1];
-    v[0] = block_sum(zr, red);
-    if (publish_partials<1>(v, partials, counter, &last)) {
-        double s = gather_partials(partials, 0, red);
-        if (threadIdx.x == 0) {
-            S->rho = s / S->res;
-            S->res = s;
-            S->er = sqrt(s / S->res_o);
-            S->iters += 1;
-            if (S->er <= S->tol) S->done = 1;
-            reset_counter(counter);
-        }
-    }
-}
-
-// P = M^-1 R + rho P
-__global__ void __launch_bounds__(kBlock) k_pcg_dir(int N, const double *__restrict__ R,
-                                                    const double *__restrict__ dinv, double *__restrict__ P,
-                                                    const PcgScalars *S)
-{
-    if (S->done) return;
-    const double rho = S->rho;
-    for (int r = blockIdx.x * kBlock + threadIdx.x; r < N; r += gridDim.x * kBlock)
-        P[r] = R[r] * dinv[r] + (rho * P[r]);
 }
 
 // nonlinear residual sums (static2d.cpp:953-970)
@@ -796,7 +640,7 @@ static inline int nblk(long long n) { return (int)((n + kBlock - 1) / kBlock); }
 
 int grid_reduce(int N)
 {
-    int t = (N + kTileRows - 1) / kTileRows;
+    int t = (N + kBlock - 1) / kBlock;
     return t < kRedGrid ? (t > 0 ? t : 1) : kRedGrid;
 }
 
@@ -882,29 +726,9 @@ void launch_map(hipStream_t s, int n, const int *dst, const int *ptr, const int 
     k_map_gather<<<nblk(n), kBlock, 0, s>>>(n, ptr, src, w, data, tmp);
     k_map_scatter<<<nblk(n), kBlock, 0, s>>>(n, dst, tmp, data);
 }
-void launch_diag_inv(hipStream_t s, int N, const int *diag, const double *val, double *dinv, PcgScalars *S)
+void launch_diag_inv(hipStream_t s, int N, const int *diag, const double *val, double *dinv, CgState *S)
 {
     if (N) k_diag_inv<<<nblk(N), kBlock, 0, s>>>(N, diag, val, dinv, S);
-}
-void launch_pcg_init(hipStream_t s, int N, int flag, const int *rowptr, const int *col, const double *val,
-                     const double *b, double *V, double *R, double *P, const double *dinv, double *partials,
-                     unsigned *counter, PcgScalars *S)
-{
-    k_pcg_init<<<grid_reduce(N), kBlock, 0, s>>>(N, flag, rowptr, col, val, b, V, R, P, dinv, partials, counter, S);
-}
-void launch_pcg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *P,
-                     double *U, double *partials, unsigned *counter, PcgScalars *S)
-{
-    k_pcg_spmv<<<grid_reduce(N), kBlock, 0, s>>>(N, rowptr, col, val, P, U, partials, counter, S);
-}
-void launch_pcg_update(hipStream_t s, int N, double *V, double *R, const double *P, const double *U,
-                       const double *dinv, double *partials, unsigned *counter, PcgScalars *S)
-{
-    k_pcg_update<<<grid_reduce(N), kBlock, 0, s>>>(N, V, R, P, U, dinv, partials, counter, S);
-}
-void launch_pcg_dir(hipStream_t s, int N, const double *R, const double *dinv, double *P, const PcgScalars *S)
-{
-    k_pcg_dir<<<grid_reduce(N), kBlock, 0, s>>>(N, R, dinv, P, S);
 }
 void launch_newton_res(hipStream_t s, int N, const double *V, const double *Vold, double *partials,
                        unsigned *counter, NewtonScalars *S)

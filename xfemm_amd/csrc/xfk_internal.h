@@ -82,6 +82,20 @@ struct PcgScalars {
     long long iters;
 };
 
+// State of the fused PCG (xfk_pcg.hip), device resident.  gam/alp are
+// rings indexed by iteration parity: launch i writes slot i&1 and reads
+// slot (i-1)&1, which the previous launch wrote.
+struct CgState {
+    double res_o;     // (M^-1 b).b
+    double gam[2];    // gamma_i = r_i . M^-1 r_i
+    double alp[2];    // alpha_i
+    double er;        // sqrt(gamma_i / res_o)
+    double tol;
+    int done;
+    int singular;
+    long long iters;
+};
+
 struct NewtonScalars {
     double dx2;       // sum (V - Vold)^2
     double v2;        // sum V^2
@@ -189,12 +203,15 @@ struct xfk_problem {
     std::vector<int> pbc_b_key;
 
     // numeric
-    xfk::DBuf<double> val, b, V, Vold, R, P, U, dinv;
-    xfk::DBuf<double> partials;       // kRedGrid * 2
+    xfk::DBuf<double> val, b, V, Vold, P, dinv;
+    xfk::DBuf<double> R2, W2, Z2;     // double-buffered PCG vectors (2N each)
+    xfk::DBuf<double> part_cg;        // 2 parities x 2 values x G
+    xfk::DBuf<double> part_reso;      // 2 x G
+    xfk::DBuf<double> partials;       // kRedGrid * 2 (Newton residual)
     xfk::DBuf<unsigned> counters;     // ticket counters
-    xfk::DBuf<xfk::PcgScalars> pcg;
+    xfk::DBuf<xfk::CgState> pcg;
     xfk::DBuf<xfk::NewtonScalars> nws;
-    xfk::PcgScalars *pcg_host = nullptr;  // pinned mirror
+    xfk::CgState *pcg_host = nullptr;  // pinned mirror
     xfk::NewtonScalars *nws_host = nullptr;
 
     // live SpMV launch timing (XFK_TIME_SPMV)

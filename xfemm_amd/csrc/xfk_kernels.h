@@ -23,6 +23,28 @@ struct AssembleArgs {
 
 int grid_reduce(int N);
 
+struct CgAxpyArgs {
+    const double *W, *dinv;
+    double *Z, *P, *V, *R, *U;
+    const double *gam_in;            // gamma_i partials (Ggam), previous k_cg_axpy / init
+    const double *del_in;            // delta_i partials (Gdel), previous k_cg_spmv
+    const double *reso;              // (M^-1 b).b partials (Gdel), read at it == 0
+    double *gam_out;                 // gamma_i+1 partials
+    int Ggam, Gdel;
+    CgState *S;
+    long long it;
+    int N;
+};
+
+int cg_grid(int N);
+int cg_axpy_grid(int N);
+void launch_cg_init(hipStream_t s, int N, int flag, const int *rowptr, const int *col, const double *val,
+                    const double *b, double *V, double *R, double *U, double *Z, double *P, double *W,
+                    const double *dinv, double *part_reso, double *part_gam0, double *part_del);
+void launch_cg_axpy(hipStream_t s, const CgAxpyArgs &A);
+void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *U,
+                    double *W, double *part_del, const CgState *S);
+
 void launch_count_incidence(hipStream_t s, int NE, const int *p, int *deg);
 void launch_fill_n2e(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e);
 void launch_sort_segments(hipStream_t s, int N, const int *ptr, int *a);
@@ -49,15 +71,7 @@ void launch_dirichlet(hipStream_t s, int nrows, const int *rows, int nadj, const
                       const double *fix_last, double *val, double *b);
 void launch_map(hipStream_t s, int n, const int *dst, const int *ptr, const int *src, const double *w,
                 double *data, double *tmp);
-void launch_diag_inv(hipStream_t s, int N, const int *diag, const double *val, double *dinv, PcgScalars *S);
-void launch_pcg_init(hipStream_t s, int N, int flag, const int *rowptr, const int *col, const double *val,
-                     const double *b, double *V, double *R, double *P, const double *dinv, double *partials,
-                     unsigned *counter, PcgScalars *S);
-void launch_pcg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *P,
-                     double *U, double *partials, unsigned *counter, PcgScalars *S);
-void launch_pcg_update(hipStream_t s, int N, double *V, double *R, const double *P, const double *U,
-                       const double *dinv, double *partials, unsigned *counter, PcgScalars *S);
-void launch_pcg_dir(hipStream_t s, int N, const double *R, const double *dinv, double *P, const PcgScalars *S);
+void launch_diag_inv(hipStream_t s, int N, const int *diag, const double *val, double *dinv, CgState *S);
 void launch_newton_res(hipStream_t s, int N, const double *V, const double *Vold, double *partials,
                        unsigned *counter, NewtonScalars *S);
 void launch_relax(hipStream_t s, int N, double relax, double *V, const double *Vold);

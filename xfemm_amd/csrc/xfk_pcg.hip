@@ -1,0 +1,282 @@
+// Preconditioned conjugate gradient of the fsolver hot path, one fused launch
+// per iteration.
+//
+// Reference: CBigLinProb::PCGSolve (cfemm/libfemm/spars.cpp:238-316) -- same
+// PCG, same stopping test sqrt(z.r / z0.b) <= Precision, same initial guess
+// semantics (flag), Jacobi preconditioner M = diag(A) instead of the
+// reference's sequential SSOR sweep.
+//
+// Formulation: the Chronopoulos-Gear arrangement of PCG, in which both inner
+// products of an iteration (gamma = r.u, delta = w.u with u = M^-1 r, w = A u)
+// come from ONE reduction phase.  With z = A p and q = M^-1 z kept as
+// recurrences, iteration i is
+//     beta  = gamma_i / gamma_{i-1},   alpha = gamma_i / (delta_i - beta gamma_i / alpha_{i-1})
+//     z_i   = w_i + beta z_{i-1}        p_i   = u_i + beta p_{i-1}
+//     x    += alpha p_i                 r_i+1 = r_i - alpha z_i
+//     w_i+1 = A u_i+1,  u_i+1 = M^-1 r_i+1,   partials of gamma_i+1, delta_i+1
+// so a whole iteration is one launch: every workgroup first reduces the
+// previous launch's per-block partials itself (identical order in every
+// block -> bit-identical alpha/beta everywhere, no atomics, no fan-in tail),
+// then updates its own rows and runs its LDS row tile of the SpMV, gathering
+// u_i+1 at the neighbour columns on the fly from the previous iterate.
+#include "xfk_kernels.h"
+
+namespace xfk {
+
+constexpr int kCgBlock = 1024;            // 16 waves; one row tile per workgroup
+constexpr int kCgCap = 8 * kCgBlock;      // products staged per LDS pass (64 KiB)
+
+__device__ __forceinline__ double cg_wave_sum(double v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// two simultaneous workgroup sums, results broadcast to every thread
+__device__ __forceinline__ void cg_block_sum2(double &a, double &b, double *red)
+{
+    a = cg_wave_sum(a);
+    b = cg_wave_sum(b);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) {
+        red[2 * wid] = a;
+        red[2 * wid + 1] = b;
+    }
+    __syncthreads();
+    double sa = 0.0, sb = 0.0;
+    const int nw = blockDim.x >> 6;
+    for (int w = 0; w < nw; ++w) {
+        sa += red[2 * w];
+        sb += red[2 * w + 1];
+    }
+    a = sa;
+    b = sb;
+}
+
+// deterministic sum of G partials (pairs) of the previous launch, in every block
+__device__ __forceinline__ void cg_reduce_partials(const double *__restrict__ part, int G, double &a, double &b,
+                                                   double *red)
+{
+    double sa = 0.0, sb = 0.0;
+    for (int i = threadIdx.x; i < G; i += blockDim.x) {
+        sa += part[i];
+        sb += part[G + i];
+    }
+    cg_block_sum2(sa, sb, red);
+    a = sa;
+    b = sb;
+}
+
+// y = sum_k val[k] * X(col[k]) for the rows of one tile; CSR-stream through LDS
+template <class XF>
+__device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restrict__ rowptr,
+                                               const int *__restrict__ col, const double *__restrict__ val,
+                                               XF X, double *lds)
+{
+    const int r = r0 + threadIdx.x;
+    const int rend = min(r0 + kCgBlock, N);
+    const int s = rowptr[r0], e = rowptr[rend];
+    const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
+    double acc = 0.0;
+    for (int c0 = s; c0 < e; c0 += kCgCap) {
+        const int c1 = min(e, c0 + kCgCap);
+        int cidx[8];
+        double v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int k = c0 + threadIdx.x + m * kCgBlock;
+            cidx[m] = (k < c1) ? col[k] : -1;
+            v[m] = (k < c1) ? val[k] : 0.0;
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int k = c0 + threadIdx.x + m * kCgBlock;
+            if (cidx[m] >= 0) lds[k - c0] = v[m] * X(cidx[m]);
+        }
+        __syncthreads();
+        const int a = max(my_s, c0), z = min(my_e, c1);
+        for (int k = a; k < z; ++k) acc += lds[k - c0];
+        __syncthreads();
+    }
+    return acc;
+}
+
+// Launch structure per iteration i (two launches, one reduction phase):
+//   k_cg_axpy(i): reduce the gamma_i (own previous launch) and delta_i (SpMV)
+//                 partials -> alpha, beta, convergence test; stream the own
+//                 rows: z, p, x, r updated in place, u = M^-1 r written;
+//                 partials gamma_i+1 = r.u.      88 B/row, vectorised 2 rows/lane
+//   k_cg_spmv(i): w = A u (CSR-stream, LDS row tiles), partials delta_i+1 = u.w
+constexpr int kAxBlock = 256;
+constexpr int kAxGrid = 1024;             // fixed grid of the streaming kernel
+
+// r0 = b - A x0 (x0 = 0 when flag == 0), u0 = M^-1 r0, z_{-1} = p_{-1} = 0;
+// partials of (M^-1 b).b and gamma_0 = r0.u0
+__global__ void __launch_bounds__(kCgBlock) k_cg_init_r(int N, int flag, const int *__restrict__ rowptr,
+                                                        const int *__restrict__ col, const double *__restrict__ val,
+                                                        const double *__restrict__ b, double *__restrict__ V,
+                                                        double *__restrict__ R, double *__restrict__ U,
+                                                        double *__restrict__ Z, double *__restrict__ P,
+                                                        const double *__restrict__ dinv, double *__restrict__ part_reso,
+                                                        double *__restrict__ part_gam0)
+{
+    __shared__ __attribute__((aligned(16))) double lds[kCgCap];
+    __shared__ double red[2 * (kCgBlock / 64)];
+    const int r0 = blockIdx.x * kCgBlock;
+    double ax = 0.0;
+    if (flag) ax = cg_tile_spmv(r0, N, rowptr, col, val, [&](int j) { return V[j]; }, lds);
+    const int r = r0 + threadIdx.x;
+    double ro = 0.0, g = 0.0;
+    if (r < N) {
+        const double br = b[r], di = dinv[r];
+        const double rr = br - ax;
+        const double u = di * rr;
+        R[r] = rr;
+        U[r] = u;
+        Z[r] = 0.0;
+        P[r] = 0.0;
+        if (!flag) V[r] = 0.0;
+        ro = (br * di) * br;
+        g = rr * u;
+    }
+    cg_block_sum2(ro, g, red);
+    if (threadIdx.x == 0) {
+        part_reso[blockIdx.x] = ro;
+        part_gam0[blockIdx.x] = g;
+    }
+}
+
+// w = A u; partials delta = u.w
+__global__ void __launch_bounds__(kCgBlock) k_cg_spmv(int N, const int *__restrict__ rowptr,
+                                                      const int *__restrict__ col, const double *__restrict__ val,
+                                                      const double *__restrict__ U, double *__restrict__ W,
+                                                      double *__restrict__ part_del, const CgState *S)
+{
+    if (S && S->done) return;
+    __shared__ __attribute__((aligned(16))) double lds[kCgCap];
+    __shared__ double red[2 * (kCgBlock / 64)];
+    const int r0 = blockIdx.x * kCgBlock;
+    const double w = cg_tile_spmv(r0, N, rowptr, col, val, [&](int j) { return U[j]; }, lds);
+    const int r = r0 + threadIdx.x;
+    double d = 0.0, zero = 0.0;
+    if (r < N) {
+        W[r] = w;
+        d = w * U[r];
+    }
+    cg_block_sum2(d, zero, red);
+    if (threadIdx.x == 0) part_del[blockIdx.x] = d;
+}
+
+// one pair of deterministic sums over two partial arrays of different lengths
+__device__ __forceinline__ void cg_reduce2(const double *__restrict__ pa, int Ga, const double *__restrict__ pb,
+                                           int Gb, double &a, double &b, double *red)
+{
+    double sa = 0.0, sb = 0.0;
+    for (int i = threadIdx.x; i < Ga; i += blockDim.x) sa += pa[i];
+    for (int i = threadIdx.x; i < Gb; i += blockDim.x) sb += pb[i];
+    cg_block_sum2(sa, sb, red);
+    a = sa;
+    b = sb;
+}
+
+// CgAxpyArgs: xfk_kernels.h
+__global__ void __launch_bounds__(kAxBlock) k_cg_axpy(CgAxpyArgs A)
+{
+    __shared__ double red[2 * (kAxBlock / 64)];
+    CgState *S = A.S;
+    if (S->done) return;
+    double gam, del;
+    cg_reduce2(A.gam_in, A.Ggam, A.del_in, A.Gdel, gam, del, red);
+    double res_o;
+    if (A.it == 0) {
+        double unused;
+        cg_reduce2(A.reso, A.Gdel, A.reso, 0, res_o, unused, red);
+    } else {
+        res_o = S->res_o;
+    }
+    double beta = 0.0, alpha;
+    if (A.it == 0) {
+        alpha = gam / del;
+    } else {
+        const double gp = S->gam[(A.it - 1) & 1], ap = S->alp[(A.it - 1) & 1];
+        beta = gam / gp;
+        alpha = gam / (del - beta * gam / ap);
+    }
+    const double er = (res_o == 0.0) ? 0.0 : sqrt(gam / res_o);
+    const bool stop = (res_o == 0.0) || (A.it >= 1 && er <= S->tol);   // spars.cpp:259, 313
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (A.it == 0) S->res_o = res_o;
+        S->er = er;
+        S->iters = A.it;
+        if (stop) S->done = 1;
+        S->gam[A.it & 1] = gam;
+        S->alp[A.it & 1] = alpha;
+    }
+    if (stop) return;
+    const int N = A.N;
+    double g = 0.0;
+    const int npair = N >> 1;
+    const double2 *W2 = reinterpret_cast<const double2 *>(A.W);
+    double2 *Z2 = reinterpret_cast<double2 *>(A.Z);
+    double2 *P2 = reinterpret_cast<double2 *>(A.P);
+    double2 *V2 = reinterpret_cast<double2 *>(A.V);
+    double2 *R2 = reinterpret_cast<double2 *>(A.R);
+    double2 *U2 = reinterpret_cast<double2 *>(A.U);
+    const double2 *D2 = reinterpret_cast<const double2 *>(A.dinv);
+    for (int k = blockIdx.x * kAxBlock + threadIdx.x; k < npair; k += gridDim.x * kAxBlock) {
+        const double2 w = W2[k], zo = Z2[k], po = P2[k], x = V2[k], ri = R2[k], di = D2[k];
+        double2 z, p, rn, u;
+        z.x = w.x + beta * zo.x;          z.y = w.y + beta * zo.y;
+        p.x = di.x * ri.x + beta * po.x;  p.y = di.y * ri.y + beta * po.y;
+        rn.x = ri.x - alpha * z.x;        rn.y = ri.y - alpha * z.y;
+        u.x = di.x * rn.x;                u.y = di.y * rn.y;
+        double2 xn;
+        xn.x = x.x + alpha * p.x;         xn.y = x.y + alpha * p.y;
+        Z2[k] = z; P2[k] = p; V2[k] = xn; R2[k] = rn; U2[k] = u;
+        g += rn.x * u.x + rn.y * u.y;
+    }
+    if ((N & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        const int r = N - 1;
+        const double z = A.W[r] + beta * A.Z[r];
+        const double p = A.dinv[r] * A.R[r] + beta * A.P[r];
+        const double rn = A.R[r] - alpha * z;
+        const double u = A.dinv[r] * rn;
+        A.V[r] = A.V[r] + alpha * p;
+        A.Z[r] = z; A.P[r] = p; A.R[r] = rn; A.U[r] = u;
+        g += rn * u;
+    }
+    double zero = 0.0;
+    cg_block_sum2(g, zero, red);
+    if (threadIdx.x == 0) A.gam_out[blockIdx.x] = g;
+}
+
+int cg_grid(int N) { return (N + kCgBlock - 1) / kCgBlock; }
+int cg_axpy_grid(int N)
+{
+    int g = (N / 2 + kAxBlock - 1) / kAxBlock;
+    return g < 1 ? 1 : (g < kAxGrid ? g : kAxGrid);
+}
+
+void launch_cg_init(hipStream_t s, int N, int flag, const int *rowptr, const int *col, const double *val,
+                    const double *b, double *V, double *R, double *U, double *Z, double *P, double *W,
+                    const double *dinv, double *part_reso, double *part_gam0, double *part_del)
+{
+    const int G = cg_grid(N);
+    k_cg_init_r<<<G, kCgBlock, 0, s>>>(N, flag, rowptr, col, val, b, V, R, U, Z, P, dinv, part_reso, part_gam0);
+    k_cg_spmv<<<G, kCgBlock, 0, s>>>(N, rowptr, col, val, U, W, part_del, nullptr);
+}
+
+void launch_cg_axpy(hipStream_t s, const CgAxpyArgs &A)
+{
+    k_cg_axpy<<<cg_axpy_grid(A.N), kAxBlock, 0, s>>>(A);
+}
+
+void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *U,
+                    double *W, double *part_del, const CgState *S)
+{
+    k_cg_spmv<<<cg_grid(N), kCgBlock, 0, s>>>(N, rowptr, col, val, U, W, part_del, S);
+}
+
+}  // namespace xfk
