@@ -108,6 +108,7 @@ typedef struct {
     double ms_solve;
     double spmv_ms_avg;         /* XFK_TIME_SPMV: mean HIP-event time of one SpMV launch */
     int spmv_samples;           /* launches sampled (every 16th PCG iteration) */
+    int color_rounds;           /* Jones-Plassmann rounds of the element colouring */
 } xfk_result;
 
 typedef struct xfk_problem xfk_problem;

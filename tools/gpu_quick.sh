@@ -1,4 +1,5 @@
+# GPU tests + parity/timing probe; stops at the first failing step.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?" >> gpurun_out/pytest_gpu.log
-timeout -k 10 300 python tools/gpu_probe.py > gpurun_out/probe.log 2>&1; echo "probe rc=$?" >> gpurun_out/probe.log
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 && \
+timeout -k 10 300 python tools/gpu_probe.py > gpurun_out/probe.log 2>&1

@@ -175,20 +175,25 @@ static hipError_t d2h(void *dst, const void *src, size_t bytes, hipStream_t s)
     return hipStreamSynchronize(s);
 }
 
-static hipError_t exclusive_scan(hipStream_t s, const int *in, int *out, int n)
+// hipcub temporary storage, kept on the problem (no hipMalloc/hipFree per call)
+static hipError_t cub_scratch(xfk_problem *P, size_t bytes, void **out)
+{
+    hipError_t e = P->cub_tmp.alloc(bytes ? bytes : 1);
+    *out = P->cub_tmp.p;
+    return e;
+}
+
+static hipError_t exclusive_scan(xfk_problem *P, const int *in, int *out, int n)
 {
     // out has n+1 entries; out[n] = total
+    hipStream_t s = P->stream;
     void *tmp = nullptr;
     size_t bytes = 0;
     hipError_t e = hipcub::DeviceScan::InclusiveSum(tmp, bytes, in, out + 1, n, s);
-    if (e != hipSuccess) return e;
-    e = hipMalloc(&tmp, bytes ? bytes : 1);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(out, 0, sizeof(int), s);
+    if (e == hipSuccess) e = cub_scratch(P, bytes, &tmp);
+    if (e == hipSuccess) e = hipMemsetAsync(out, 0, sizeof(int), s);
     if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(tmp, bytes, in, out + 1, n, s);
-    hipError_t e2 = hipStreamSynchronize(s);
-    (void)hipFree(tmp);
-    return e != hipSuccess ? e : e2;
+    return e;
 }
 
 static int alloc_cg(xfk_problem *P);
@@ -206,7 +211,7 @@ static int build_symbolic(xfk_problem *P)
     XFK_CHECK(hipMemsetAsync(deg.p, 0, sizeof(int) * N, s));
     XFK_CHECK(hipMemsetAsync(cursor.p, 0, sizeof(int) * N, s));
     launch_count_incidence(s, NE, P->p_raw.p, deg.p);
-    XFK_CHECK(exclusive_scan(s, deg.p, P->n2e_ptr.p, N));
+    XFK_CHECK(exclusive_scan(P, deg.p, P->n2e_ptr.p, N));
     launch_fill_n2e(s, NE, P->p_raw.p, P->n2e_ptr.p, cursor.p, P->n2e.p);
     launch_sort_segments(s, N, P->n2e_ptr.p, P->n2e.p);
 
@@ -238,7 +243,7 @@ static int build_symbolic(xfk_problem *P)
     XFK_CHECK(rowcnt.alloc(N));
     XFK_CHECK(P->rowptr.alloc(N + 1));
     launch_row_count(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, rowcnt.p);
-    XFK_CHECK(exclusive_scan(s, rowcnt.p, P->rowptr.p, N));
+    XFK_CHECK(exclusive_scan(P, rowcnt.p, P->rowptr.p, N));
     int nnz = 0;
     XFK_CHECK(d2h(&nnz, P->rowptr.p + N, sizeof(int), s));
     P->nnz = nnz;
@@ -247,19 +252,29 @@ static int build_symbolic(xfk_problem *P)
     XFK_CHECK(P->diag.alloc(N));
     launch_row_fill(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, P->rowptr.p, P->col.p, P->diag.p);
 
-    // Jones-Plassmann colouring of elements (shared node = conflict)
+    // Jones-Plassmann colouring of elements (shared node = conflict) over a
+    // shrinking worklist; the host reads the pending count every kSyncRounds.
     XFK_CHECK(P->color.alloc(NE));
     XFK_CHECK(hipMemsetAsync(P->color.p, 0xff, sizeof(int) * NE, s));
-    DBuf<int> cnt;
+    constexpr int kMaxRounds = 4096, kSyncRounds = 6;
+    DBuf<int> wl0, wl1, wlcnt, cnt;
+    XFK_CHECK(wl0.alloc(NE));
+    XFK_CHECK(wl1.alloc(NE));
+    XFK_CHECK(wlcnt.alloc(kMaxRounds));
     XFK_CHECK(cnt.alloc(1));
-    XFK_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int), s));
-    int colored = 0, rounds = 0;
-    while (colored < NE) {
-        launch_color_round(s, NE, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, P->color.p, cnt.p);
-        XFK_CHECK(hipMemcpyAsync(&colored, cnt.p, sizeof(int), hipMemcpyDeviceToHost, s));
-        XFK_CHECK(hipStreamSynchronize(s));
-        XFK_REQUIRE(++rounds < 10000, XFK_ERR_UNSUPPORTED, "element colouring did not terminate");
+    XFK_CHECK(hipMemsetAsync(wlcnt.p, 0, sizeof(int) * kMaxRounds, s));
+    int pending = NE, round = 0;
+    while (pending > 0) {
+        XFK_REQUIRE(round + kSyncRounds <= kMaxRounds, XFK_ERR_UNSUPPORTED, "element colouring did not terminate");
+        for (int k = 0; k < kSyncRounds; ++k, ++round) {
+            const int *in = round == 0 ? nullptr : ((round - 1) & 1 ? wl1.p : wl0.p);
+            int *out = (round & 1) ? wl1.p : wl0.p;
+            launch_color_round(s, round, pending, in, round == 0 ? nullptr : wlcnt.p + round - 1, NE, out,
+                               wlcnt.p + round, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, P->color.p);
+        }
+        XFK_CHECK(d2h(&pending, wlcnt.p + round - 1, sizeof(int), s));
     }
+    P->color_rounds = round;
     const int maxc = 128;
     DBuf<int> hist;
     XFK_CHECK(hist.alloc(maxc + 1));
@@ -286,13 +301,10 @@ static int build_symbolic(xfk_problem *P)
         size_t bytes = 0;
         XFK_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, P->color.p, keys_out.p, iota.p, P->perm.p, NE,
                                                      0, 8, s));
-        XFK_CHECK(hipMalloc(&tmp, bytes ? bytes : 1));
-        hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, bytes, P->color.p, keys_out.p, iota.p, P->perm.p,
-                                                          NE, 0, 8, s);
-        hipError_t e2 = hipStreamSynchronize(s);
-        (void)hipFree(tmp);
-        XFK_CHECK(e);
-        XFK_CHECK(e2);
+        XFK_CHECK(cub_scratch(P, bytes, &tmp));
+        XFK_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, P->color.p, keys_out.p, iota.p, P->perm.p, NE,
+                                                     0, 8, s));
+        XFK_CHECK(hipStreamSynchronize(s));   // keys_out / iota leave scope
     }
     XFK_CHECK(P->erec.alloc(NE));
     XFK_CHECK(P->ebits.alloc(NE));
@@ -917,6 +929,7 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     R.last_res = resn;
     R.nnz = P->nnz;
     R.ncolors = P->ncolors;
+    R.color_rounds = P->color_rounds;
     P->last = R;
     if (res) *res = R;
     return XFK_OK;

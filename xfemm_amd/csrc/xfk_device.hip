@@ -187,48 +187,80 @@ __device__ __forceinline__ unsigned hash_u32(unsigned x)
     return x;
 }
 
-// One Jones-Plassmann round: an uncoloured element whose (hash, index)
-// priority beats every uncoloured element sharing a node with it takes the
-// smallest colour unused by its coloured neighbours.
-__global__ void k_color_round(int NE, const int *__restrict__ p, const int *__restrict__ n2e_ptr,
-                              const int *__restrict__ n2e, int *__restrict__ color,
-                              int *__restrict__ ncolored)
+// One Jones-Plassmann round over a worklist of uncoloured elements.  An
+// element whose (hash, index) priority beats every still-pending element
+// sharing a node with it takes the smallest colour unused by its coloured
+// neighbours; the others are appended to the next round's worklist (one
+// atomic per wave).  Colour words carry the round that wrote them,
+// (round << 8) | colour, and a neighbour coloured in the *current* round
+// counts as pending: every decision depends only on the state at the start
+// of the round, so the colouring is deterministic whatever the wave timing.
+__global__ void __launch_bounds__(kBlock) k_color_round(int round, const int *__restrict__ wl_in,
+                                                        const int *__restrict__ n_in_p, int n_in_static,
+                                                        int *__restrict__ wl_out, int *__restrict__ n_out,
+                                                        const int *__restrict__ p, const int *__restrict__ n2e_ptr,
+                                                        const int *__restrict__ n2e, int *__restrict__ color)
 {
-    int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= NE) return;
-    if (color[e] >= 0) return;
-    const unsigned he = hash_u32((unsigned)e);
-    unsigned long long used0 = 0, used1 = 0;
-    for (int j = 0; j < 3; ++j) {
-        int v = p[3 * e + j];
-        for (int t = n2e_ptr[v]; t < n2e_ptr[v + 1]; ++t) {
-            int f = n2e[t];
-            if (f == e) continue;
-            int cf = __hip_atomic_load(&color[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cf < 0) {
-                unsigned hf = hash_u32((unsigned)f);
-                if (hf > he || (hf == he && f > e)) return;
-            } else if (cf < 64) {
-                used0 |= 1ull << cf;
-            } else if (cf < 128) {
-                used1 |= 1ull << (cf - 64);
+    const int n_in = n_in_p ? *n_in_p : n_in_static;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool lose = false;
+    int e = -1;
+    if (i < n_in) {
+        e = wl_in ? wl_in[i] : i;
+        const unsigned he = hash_u32((unsigned)e);
+        unsigned long long used0 = 0, used1 = 0;
+        for (int j = 0; j < 3 && !lose; ++j) {
+            const int v = p[3 * e + j];
+            const int t1 = n2e_ptr[v + 1];
+            for (int t = n2e_ptr[v]; t < t1; ++t) {
+                const int f = n2e[t];
+                if (f == e) continue;
+                const int cf = __hip_atomic_load(&color[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (cf < 0 || (cf >> 8) == round) {
+                    const unsigned hf = hash_u32((unsigned)f);
+                    if (hf > he || (hf == he && f > e)) { lose = true; break; }
+                } else {
+                    const int c = cf & 255;
+                    if (c < 64) used0 |= 1ull << c;
+                    else if (c < 128) used1 |= 1ull << (c - 64);
+                }
             }
         }
+        if (!lose) {
+            int c;
+            if (~used0) c = __ffsll((long long)~used0) - 1;
+            else if (~used1) c = 64 + __ffsll((long long)~used1) - 1;
+            else c = 255;  // > 128 colours: flagged by the host
+            __hip_atomic_store(&color[e], (round << 8) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-    int c;
-    if (~used0) c = __ffsll((long long)~used0) - 1;
-    else if (~used1) c = 64 + __ffsll((long long)~used1) - 1;
-    else c = 1000;  // > 128 colours: flagged by the host
-    __hip_atomic_store(&color[e], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    atomicAdd(ncolored, 1);
+    const unsigned long long m = __ballot(lose);
+    if (m) {
+        const int lane = threadIdx.x & 63;
+        const int leader = __ffsll((long long)m) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(n_out, (int)__popcll(m));
+        base = __shfl(base, leader, 64);
+        if (lose) wl_out[base + (int)__popcll(m & ((1ull << lane) - 1ull))] = e;
+    }
 }
 
-__global__ void k_color_hist(int NE, const int *__restrict__ color, int *__restrict__ hist, int maxc)
+// Strip the round tags and count elements per colour (LDS-private histogram,
+// one global atomic per bin per block).
+__global__ void __launch_bounds__(kBlock) k_color_hist(int NE, int *__restrict__ color, int *__restrict__ hist,
+                                                       int maxc)
 {
-    int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= NE) return;
-    int c = color[e];
-    atomicAdd(&hist[c < maxc ? c : maxc], 1);
+    __shared__ int h[256];
+    for (int k = threadIdx.x; k < 256; k += kBlock) h[k] = 0;
+    __syncthreads();
+    for (int e = blockIdx.x * kBlock + threadIdx.x; e < NE; e += gridDim.x * kBlock) {
+        const int c = color[e] & 255;
+        color[e] = c;
+        atomicAdd(&h[c < maxc ? c : maxc], 1);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k <= maxc; k += kBlock)
+        if (h[k]) atomicAdd(&hist[k], h[k]);
 }
 
 __global__ void k_iota(int n, int *__restrict__ a)
@@ -668,14 +700,16 @@ void launch_row_fill(hipStream_t s, int N, const int *p, const int *n2e_ptr, con
     RowCands rc{p, n2e_ptr, n2e, fill_ptr, fill_col};
     if (N) k_row_fill<<<nblk(N), kBlock, 0, s>>>(N, rc, rowptr, col, diag);
 }
-void launch_color_round(hipStream_t s, int NE, const int *p, const int *n2e_ptr, const int *n2e, int *color,
-                        int *ncolored)
+void launch_color_round(hipStream_t s, int round, int grid_n, const int *wl_in, const int *n_in_p, int n_in_static,
+                        int *wl_out, int *n_out, const int *p, const int *n2e_ptr, const int *n2e, int *color)
 {
-    if (NE) k_color_round<<<nblk(NE), kBlock, 0, s>>>(NE, p, n2e_ptr, n2e, color, ncolored);
+    if (grid_n > 0)
+        k_color_round<<<nblk(grid_n), kBlock, 0, s>>>(round, wl_in, n_in_p, n_in_static, wl_out, n_out, p, n2e_ptr,
+                                                      n2e, color);
 }
-void launch_color_hist(hipStream_t s, int NE, const int *color, int *hist, int maxc)
+void launch_color_hist(hipStream_t s, int NE, int *color, int *hist, int maxc)
 {
-    if (NE) k_color_hist<<<nblk(NE), kBlock, 0, s>>>(NE, color, hist, maxc);
+    if (NE) k_color_hist<<<std::min(nblk(NE), 2048), kBlock, 0, s>>>(NE, color, hist, maxc);
 }
 void launch_iota(hipStream_t s, int n, int *a)
 {

@@ -170,6 +170,8 @@ struct xfk_problem {
     xfk::DBuf<int> n2e_ptr, n2e;     // node -> incident elements (sorted)
     xfk::DBuf<int> rowptr, col, diag;
     xfk::DBuf<int> color;            // per raw element
+    int color_rounds = 0;            // Jones-Plassmann rounds of the last symbolic build
+    xfk::DBuf<char> cub_tmp;         // hipcub temporary storage
     xfk::DBuf<int> perm;             // colour order -> raw element
     xfk::DBuf<int4> erec;            // colour order
     xfk::DBuf<int> ebits;            // colour order

@@ -52,9 +52,9 @@ void launch_row_count(hipStream_t s, int N, const int *p, const int *n2e_ptr, co
                       const int *fill_ptr, const int *fill_col, int *rowcnt);
 void launch_row_fill(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e,
                      const int *fill_ptr, const int *fill_col, const int *rowptr, int *col, int *diag);
-void launch_color_round(hipStream_t s, int NE, const int *p, const int *n2e_ptr, const int *n2e, int *color,
-                        int *ncolored);
-void launch_color_hist(hipStream_t s, int NE, const int *color, int *hist, int maxc);
+void launch_color_round(hipStream_t s, int round, int grid_n, const int *wl_in, const int *n_in_p, int n_in_static,
+                        int *wl_out, int *n_out, const int *p, const int *n2e_ptr, const int *n2e, int *color);
+void launch_color_hist(hipStream_t s, int NE, int *color, int *hist, int maxc);
 void launch_iota(hipStream_t s, int n, int *a);
 void launch_build_erec(hipStream_t s, int NE, const int *perm, const int *p, const int *lbl, const int *ebits_raw,
                        int4 *erec, int *ebits);

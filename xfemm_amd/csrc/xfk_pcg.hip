@@ -1,5 +1,5 @@
-// Preconditioned conjugate gradient of the fsolver hot path, one fused launch
-// per iteration.
+// Preconditioned conjugate gradient of the fsolver hot path, two launches per
+// iteration.
 //
 // Reference: CBigLinProb::PCGSolve (cfemm/libfemm/spars.cpp:238-316) -- same
 // PCG, same stopping test sqrt(z.r / z0.b) <= Precision, same initial guess
@@ -8,17 +8,17 @@
 //
 // Formulation: the Chronopoulos-Gear arrangement of PCG, in which both inner
 // products of an iteration (gamma = r.u, delta = w.u with u = M^-1 r, w = A u)
-// come from ONE reduction phase.  With z = A p and q = M^-1 z kept as
-// recurrences, iteration i is
+// come from ONE reduction phase.  With z = A p kept as a recurrence,
+// iteration i is
 //     beta  = gamma_i / gamma_{i-1},   alpha = gamma_i / (delta_i - beta gamma_i / alpha_{i-1})
 //     z_i   = w_i + beta z_{i-1}        p_i   = u_i + beta p_{i-1}
 //     x    += alpha p_i                 r_i+1 = r_i - alpha z_i
-//     w_i+1 = A u_i+1,  u_i+1 = M^-1 r_i+1,   partials of gamma_i+1, delta_i+1
-// so a whole iteration is one launch: every workgroup first reduces the
-// previous launch's per-block partials itself (identical order in every
-// block -> bit-identical alpha/beta everywhere, no atomics, no fan-in tail),
-// then updates its own rows and runs its LDS row tile of the SpMV, gathering
-// u_i+1 at the neighbour columns on the fly from the previous iterate.
+//     u_i+1 = M^-1 r_i+1,  w_i+1 = A u_i+1,  partials of gamma_i+1, delta_i+1
+// The launch boundary between the streaming update (k_cg_axpy) and the SpMV
+// (k_cg_spmv) is the only grid-wide synchronisation.  Every workgroup of
+// k_cg_axpy first reduces the previous launches' per-block partials itself
+// (identical order in every block -> bit-identical alpha/beta everywhere, no
+// atomics, no fan-in tail).
 #include "xfk_kernels.h"
 
 namespace xfk {

@@ -74,7 +74,8 @@ class Result(C.Structure):
     _fields_ = [("newton_iters", C.c_int), ("cg_iters", C.c_longlong), ("last_res", C.c_double),
                 ("final_er", C.c_double), ("nnz", C.c_longlong), ("ncolors", C.c_int),
                 ("ms_symbolic", C.c_double), ("ms_assemble", C.c_double), ("ms_solve", C.c_double),
-                ("spmv_ms_avg", C.c_double), ("spmv_samples", C.c_int)]
+                ("spmv_ms_avg", C.c_double), ("spmv_samples", C.c_int),
+                ("color_rounds", C.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
