@@ -16,6 +16,7 @@
 #include <cstring>
 #include <map>
 #include <set>
+#include <type_traits>
 #include <unordered_map>
 
 #include "xfk_kernels.h"
@@ -198,25 +199,66 @@ static hipError_t exclusive_scan(xfk_problem *P, const int *in, int *out, int n)
 
 static int alloc_cg(xfk_problem *P);
 
+// Temporaries of the symbolic phase, carved from one persistent device buffer
+// (P->sym_tmp) so that a rebuild performs no hipMalloc/hipFree.
+struct SymTmp {
+    static constexpr int kMaxRounds = 4096;
+    static constexpr int kMaxColors = 128;
+    // zero-initialised block (one memset)
+    int *deg, *cursor, *cnt, *hist;
+    // uninitialised
+    int *rowcnt, *keys_out, *iota, *flag, *iperm, *rowtmp;
+    unsigned char *active;
+    unsigned long long *maxkey, *used;
+    size_t zero_bytes = 0, bytes = 0;
+
+    void carve(char *base, int N, int NE, int nfill)
+    {
+        size_t off = 0;
+        auto take = [&](auto *&ptr, size_t n) {
+            using T = std::remove_reference_t<decltype(*ptr)>;
+            off = (off + 255) & ~size_t(255);
+            ptr = base ? reinterpret_cast<T *>(base + off) : nullptr;
+            off += (n ? n : 1) * sizeof(T);
+        };
+        take(deg, N);
+        take(cursor, N);
+        take(cnt, 4);
+        take(hist, kMaxColors + 1);
+        zero_bytes = off;
+        take(rowcnt, N);
+        take(active, N);
+        take(keys_out, NE);
+        take(iota, NE);
+        take(flag, N);
+        take(maxkey, N);
+        take(used, 2 * (size_t)N);
+        take(iperm, NE);
+        take(rowtmp, (size_t)row_tmp_size(N, NE, nfill));
+        bytes = off;
+    }
+};
+
 static int build_symbolic(xfk_problem *P)
 {
     hipStream_t s = P->stream;
     const int N = P->N, NE = P->NE;
+    SymTmp T;
+    const int nfill = 2 * (int)P->pbc_fill.size();
+    T.carve(nullptr, N, NE, nfill);
+    XFK_CHECK(P->sym_tmp.alloc(T.bytes));
+    T.carve(P->sym_tmp.p, N, NE, nfill);
+    XFK_CHECK(hipMemsetAsync(P->sym_tmp.p, 0, T.zero_bytes, s));
+
     // node -> incident elements
-    DBuf<int> deg, cursor;
-    XFK_CHECK(deg.alloc(N));
-    XFK_CHECK(cursor.alloc(N));
     XFK_CHECK(P->n2e_ptr.alloc(N + 1));
     XFK_CHECK(P->n2e.alloc(3 * (size_t)NE));
-    XFK_CHECK(hipMemsetAsync(deg.p, 0, sizeof(int) * N, s));
-    XFK_CHECK(hipMemsetAsync(cursor.p, 0, sizeof(int) * N, s));
-    launch_count_incidence(s, NE, P->p_raw.p, deg.p);
-    XFK_CHECK(exclusive_scan(P, deg.p, P->n2e_ptr.p, N));
-    launch_fill_n2e(s, NE, P->p_raw.p, P->n2e_ptr.p, cursor.p, P->n2e.p);
+    launch_count_incidence(s, NE, P->p_raw.p, T.deg);
+    XFK_CHECK(exclusive_scan(P, T.deg, P->n2e_ptr.p, N));
+    launch_fill_n2e(s, NE, P->p_raw.p, P->n2e_ptr.p, T.cursor, P->n2e.p);
     launch_sort_segments(s, N, P->n2e_ptr.p, P->n2e.p);
 
     // periodic fill-in entries, CSR by row
-    DBuf<int> fill_ptr, fill_col;
     const int *fp = nullptr, *fc = nullptr;
     if (!P->pbc_fill.empty()) {
         std::vector<std::vector<int>> rows(N);
@@ -231,57 +273,47 @@ static int build_symbolic(xfk_problem *P)
             hptr[r + 1] = hptr[r] + (int)rows[r].size();
             hcol.insert(hcol.end(), rows[r].begin(), rows[r].end());
         }
-        XFK_CHECK(upload(fill_ptr, hptr.data(), hptr.size(), s));
-        XFK_CHECK(upload(fill_col, hcol.data(), hcol.size(), s));
+        XFK_CHECK(upload(P->fill_ptr, hptr.data(), hptr.size(), s));
+        XFK_CHECK(upload(P->fill_col, hcol.data(), hcol.size(), s));
         XFK_CHECK(hipStreamSynchronize(s));
-        fp = fill_ptr.p;
-        fc = fill_col.p;
+        fp = P->fill_ptr.p;
+        fc = P->fill_col.p;
     }
 
     // CSR pattern
-    DBuf<int> rowcnt;
-    XFK_CHECK(rowcnt.alloc(N));
     XFK_CHECK(P->rowptr.alloc(N + 1));
-    launch_row_count(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, rowcnt.p);
-    XFK_CHECK(exclusive_scan(P, rowcnt.p, P->rowptr.p, N));
+    launch_row_build(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, T.rowtmp, T.rowcnt);
+    XFK_CHECK(exclusive_scan(P, T.rowcnt, P->rowptr.p, N));
     int nnz = 0;
     XFK_CHECK(d2h(&nnz, P->rowptr.p + N, sizeof(int), s));
     P->nnz = nnz;
     XFK_CHECK(P->col.alloc(nnz));
     XFK_CHECK(P->val.alloc(nnz));
     XFK_CHECK(P->diag.alloc(N));
-    launch_row_fill(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, P->rowptr.p, P->col.p, P->diag.p);
+    launch_row_copy(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, T.rowtmp, P->rowptr.p, P->col.p, P->diag.p);
 
-    // Jones-Plassmann colouring of elements (shared node = conflict) over a
-    // shrinking worklist; the host reads the pending count every kSyncRounds.
+    // Jones-Plassmann colouring of elements (shared node = conflict) over
+    // full-array sweeps (kernels in xfk_device.hip); the host checks for
+    // completion every kSyncRounds rounds.
     XFK_CHECK(P->color.alloc(NE));
     XFK_CHECK(hipMemsetAsync(P->color.p, 0xff, sizeof(int) * NE, s));
-    constexpr int kMaxRounds = 4096, kSyncRounds = 6;
-    DBuf<int> wl0, wl1, wlcnt, cnt;
-    XFK_CHECK(wl0.alloc(NE));
-    XFK_CHECK(wl1.alloc(NE));
-    XFK_CHECK(wlcnt.alloc(kMaxRounds));
-    XFK_CHECK(cnt.alloc(1));
-    XFK_CHECK(hipMemsetAsync(wlcnt.p, 0, sizeof(int) * kMaxRounds, s));
-    int pending = NE, round = 0;
-    while (pending > 0) {
-        XFK_REQUIRE(round + kSyncRounds <= kMaxRounds, XFK_ERR_UNSUPPORTED, "element colouring did not terminate");
-        for (int k = 0; k < kSyncRounds; ++k, ++round) {
-            const int *in = round == 0 ? nullptr : ((round - 1) & 1 ? wl1.p : wl0.p);
-            int *out = (round & 1) ? wl1.p : wl0.p;
-            launch_color_round(s, round, pending, in, round == 0 ? nullptr : wlcnt.p + round - 1, NE, out,
-                               wlcnt.p + round, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, P->color.p);
-        }
-        XFK_CHECK(d2h(&pending, wlcnt.p + round - 1, sizeof(int), s));
+    constexpr int kSyncRounds = 6;
+    XFK_CHECK(hipMemsetAsync(T.active, 1, (size_t)N, s));
+    int round = 0, last = 0;
+    for (;;) {
+        XFK_REQUIRE(round < SymTmp::kMaxRounds, XFK_ERR_UNSUPPORTED, "element colouring did not terminate");
+        for (int k = 0; k < kSyncRounds; ++k, ++round)
+            launch_jp_round(s, N, NE, round, T.active, T.cnt + 2, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, P->color.p,
+                            T.maxkey, T.used);
+        XFK_CHECK(d2h(&last, T.cnt + 2, sizeof(int), s));
+        if (last < round) break;       // the last round launched left nothing pending
     }
+    round = last + 1;                  // rounds that coloured something
     P->color_rounds = round;
-    const int maxc = 128;
-    DBuf<int> hist;
-    XFK_CHECK(hist.alloc(maxc + 1));
-    XFK_CHECK(hipMemsetAsync(hist.p, 0, sizeof(int) * (maxc + 1), s));
-    launch_color_hist(s, NE, P->color.p, hist.p, maxc);
+    const int maxc = SymTmp::kMaxColors;
+    launch_color_hist(s, NE, P->color.p, T.hist, maxc);
     std::vector<int> hh(maxc + 1);
-    XFK_CHECK(d2h(hh.data(), hist.p, sizeof(int) * (maxc + 1), s));
+    XFK_CHECK(d2h(hh.data(), T.hist, sizeof(int) * (maxc + 1), s));
     XFK_REQUIRE(hh[maxc] == 0, XFK_ERR_UNSUPPORTED, "more than 128 element colours needed");
     int nc = 0;
     for (int c = 0; c < maxc; ++c)
@@ -291,43 +323,33 @@ static int build_symbolic(xfk_problem *P)
     for (int c = 0; c < nc; ++c) P->color_off[c + 1] = P->color_off[c] + hh[c];
 
     // stable sort of elements by colour -> perm (colour order -> raw element)
+    XFK_CHECK(P->perm.alloc(NE));
+    launch_iota(s, NE, T.iota);
     {
-        DBuf<int> keys_out, iota;
-        XFK_CHECK(keys_out.alloc(NE));
-        XFK_CHECK(iota.alloc(NE));
-        XFK_CHECK(P->perm.alloc(NE));
-        launch_iota(s, NE, iota.p);
         void *tmp = nullptr;
         size_t bytes = 0;
-        XFK_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, P->color.p, keys_out.p, iota.p, P->perm.p, NE,
-                                                     0, 8, s));
+        XFK_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, P->color.p, T.keys_out, T.iota, P->perm.p, NE, 0,
+                                                     8, s));
         XFK_CHECK(cub_scratch(P, bytes, &tmp));
-        XFK_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, P->color.p, keys_out.p, iota.p, P->perm.p, NE,
-                                                     0, 8, s));
-        XFK_CHECK(hipStreamSynchronize(s));   // keys_out / iota leave scope
+        XFK_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, P->color.p, T.keys_out, T.iota, P->perm.p, NE, 0,
+                                                     8, s));
     }
     XFK_CHECK(P->erec.alloc(NE));
     XFK_CHECK(P->ebits.alloc(NE));
     XFK_CHECK(P->slot.alloc(9 * (size_t)NE));
-    launch_build_erec(s, NE, P->perm.p, P->p_raw.p, P->lbl_raw.p, P->ebits_raw.p, P->erec.p, P->ebits.p);
-    XFK_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int), s));
-    launch_build_slots(s, NE, P->erec.p, P->rowptr.p, P->col.p, P->slot.p, cnt.p);
-    int bad = 0;
-    XFK_CHECK(d2h(&bad, cnt.p, sizeof(int), s));
-    XFK_REQUIRE(bad == 0, XFK_ERR_HIP, "internal: element slot missing from the CSR pattern");
-    XFK_CHECK(P->mu1.alloc(NE));
-    XFK_CHECK(P->mu2.alloc(NE));
+    launch_build_erec(s, NE, P->perm.p, P->p_raw.p, P->lbl_raw.p, P->ebits_raw.p, P->erec.p, P->ebits.p, T.iperm);
+    launch_build_slots(s, NE, P->p_raw.p, T.iperm, P->rowptr.p, P->col.p, P->slot.p, T.cnt);
 
     // rows adjacent to fixed nodes
-    {
-        DBuf<int> flag;
-        XFK_CHECK(flag.alloc(N));
-        launch_mark_fix_adj(s, N, P->rowptr.p, P->col.p, P->fixed.p, flag.p);
-        XFK_CHECK(P->fix_cols_row.alloc(N));
-        XFK_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int), s));
-        launch_compact_flags(s, N, flag.p, cnt.p, P->fix_cols_row.p);
-        XFK_CHECK(d2h(&P->nfix_cols, cnt.p, sizeof(int), s));
-    }
+    launch_mark_fix_adj(s, N, P->rowptr.p, P->col.p, P->fixed.p, T.flag);
+    XFK_CHECK(P->fix_cols_row.alloc(N));
+    launch_compact_flags(s, N, T.flag, T.cnt + 1, P->fix_cols_row.p);
+    int hc[2];
+    XFK_CHECK(d2h(hc, T.cnt, sizeof(int) * 2, s));
+    XFK_REQUIRE(hc[0] == 0, XFK_ERR_HIP, "internal: element slot missing from the CSR pattern");
+    P->nfix_cols = hc[1];
+    XFK_CHECK(P->mu1.alloc(NE));
+    XFK_CHECK(P->mu2.alloc(NE));
 
     // periodic averaging maps -> CSR slots
     P->pm_n = 0;

@@ -119,7 +119,14 @@ __global__ void k_sort_segments(int N, const int *__restrict__ ptr, int *__restr
     }
 }
 
-// Candidate column t of row v: vertices of incident elements, then fill-ins, then v.
+// CSR row v = sorted unique {vertices of the elements incident to v} u
+// {periodic fill-in columns of v} u {v}.  One thread per row gathers its
+// candidates into LDS (or, for rows with more than kRowLds candidates, into
+// its own region of `tmp`), sorts and de-duplicates them there, and leaves the
+// row at tmp[cand_base(v)]; k_row_copy moves it to its CSR place after the
+// row-length scan.
+constexpr int kRowLds = 32;
+
 struct RowCands {
     const int *p, *n2e_ptr, *n2e, *fill_ptr, *fill_col;
     __device__ __forceinline__ int count(int v) const
@@ -128,55 +135,62 @@ struct RowCands {
         int nf = fill_ptr ? (fill_ptr[v + 1] - fill_ptr[v]) : 0;
         return 3 * ne + nf + 1;
     }
-    __device__ __forceinline__ int get(int v, int t) const
+    __device__ __forceinline__ long long base(int v) const
     {
-        int ne = n2e_ptr[v + 1] - n2e_ptr[v];
-        if (t < 3 * ne) return p[3 * n2e[n2e_ptr[v] + t / 3] + (t % 3)];
-        t -= 3 * ne;
-        int nf = fill_ptr ? (fill_ptr[v + 1] - fill_ptr[v]) : 0;
-        if (t < nf) return fill_col[fill_ptr[v] + t];
-        return v;
+        return 3LL * n2e_ptr[v] + (fill_ptr ? fill_ptr[v] : 0) + v;
     }
 };
 
-__global__ void k_row_count(int N, RowCands rc, int *__restrict__ rowcnt)
+__global__ void __launch_bounds__(kBlock) k_row_build(int N, RowCands rc, int *__restrict__ tmp,
+                                                      int *__restrict__ rowcnt)
 {
-    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ int s_c[kBlock * (kRowLds + 1)];
+    const int v = blockIdx.x * kBlock + threadIdx.x;
     if (v >= N) return;
-    int m = rc.count(v), u = 0;
-    for (int t = 0; t < m; ++t) {
-        int c = rc.get(v, t);
-        bool seen = false;
-        for (int s = 0; s < t && !seen; ++s) seen = (rc.get(v, s) == c);
-        u += seen ? 0 : 1;
+    const int m = rc.count(v);
+    int *out = tmp + rc.base(v);
+    int *c = (m <= kRowLds) ? &s_c[threadIdx.x * (kRowLds + 1)] : out;
+    int k = 0;
+    const int t1 = rc.n2e_ptr[v + 1];
+    for (int t = rc.n2e_ptr[v]; t < t1; ++t) {
+        const int f = rc.n2e[t];
+        c[k++] = rc.p[3 * f];
+        c[k++] = rc.p[3 * f + 1];
+        c[k++] = rc.p[3 * f + 2];
     }
+    if (rc.fill_ptr)
+        for (int t = rc.fill_ptr[v]; t < rc.fill_ptr[v + 1]; ++t) c[k++] = rc.fill_col[t];
+    c[k++] = v;
+    // insertion sort, then unique
+    for (int i = 1; i < m; ++i) {
+        const int key = c[i];
+        int j = i - 1;
+        while (j >= 0 && c[j] > key) {
+            c[j + 1] = c[j];
+            --j;
+        }
+        c[j + 1] = key;
+    }
+    int u = 0;
+    for (int i = 0; i < m; ++i)
+        if (u == 0 || c[i] != c[u - 1]) c[u++] = c[i];
+    if (c != out)
+        for (int i = 0; i < u; ++i) out[i] = c[i];
     rowcnt[v] = u;
 }
 
-__global__ void k_row_fill(int N, RowCands rc, const int *__restrict__ rowptr, int *__restrict__ col,
-                           int *__restrict__ diag)
+__global__ void k_row_copy(int N, RowCands rc, const int *__restrict__ tmp, const int *__restrict__ rowptr,
+                           int *__restrict__ col, int *__restrict__ diag)
 {
-    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= N) return;
-    int base = rowptr[v], len = 0;
-    int m = rc.count(v);
-    for (int t = 0; t < m; ++t) {
-        int c = rc.get(v, t);
-        // insertion into the sorted row, skipping duplicates
-        int j = len - 1;
-        bool dup = false;
-        for (int s = 0; s < len; ++s)
-            if (col[base + s] == c) { dup = true; break; }
-        if (dup) continue;
-        while (j >= 0 && col[base + j] > c) {
-            col[base + j + 1] = col[base + j];
-            --j;
-        }
-        col[base + j + 1] = c;
-        ++len;
+    const int *src = tmp + rc.base(v);
+    const int r0 = rowptr[v], len = rowptr[v + 1] - r0;
+    for (int i = 0; i < len; ++i) {
+        const int c = src[i];
+        col[r0 + i] = c;
+        if (c == v) diag[v] = r0 + i;
     }
-    for (int s = 0; s < len; ++s)
-        if (col[base + s] == v) diag[v] = base + s;
 }
 
 __device__ __forceinline__ unsigned hash_u32(unsigned x)
@@ -187,75 +201,94 @@ __device__ __forceinline__ unsigned hash_u32(unsigned x)
     return x;
 }
 
-// One Jones-Plassmann round over a worklist of uncoloured elements.  An
-// element whose (hash, index) priority beats every still-pending element
-// sharing a node with it takes the smallest colour unused by its coloured
-// neighbours; the others are appended to the next round's worklist (one
-// atomic per wave).  Colour words carry the round that wrote them,
-// (round << 8) | colour, and a neighbour coloured in the *current* round
-// counts as pending: every decision depends only on the state at the start
-// of the round, so the colouring is deterministic whatever the wave timing.
-__global__ void __launch_bounds__(kBlock) k_color_round(int round, const int *__restrict__ wl_in,
-                                                        const int *__restrict__ n_in_p, int n_in_static,
-                                                        int *__restrict__ wl_out, int *__restrict__ n_out,
-                                                        const int *__restrict__ p, const int *__restrict__ n2e_ptr,
-                                                        const int *__restrict__ n2e, int *__restrict__ color)
+// Jones-Plassmann colouring of the element conflict graph (two elements
+// conflict when they share a node), expressed through the nodes.  Round r:
+//   k_jp_nodes: for every node that still has a pending incident element,
+//               the largest priority key among those elements and the mask
+//               of colours its coloured incident elements hold;
+//   k_jp_elems: a pending element whose key is the largest at all three of its
+//               nodes (a local maximum: the winners of one round share no
+//               node) takes the smallest colour absent from the three masks.
+// Both passes read only the state left by the previous launch, so the
+// colouring is deterministic.  They sweep the full arrays in mesh order with
+// an early exit for finished items (an inactive node costs one byte read):
+// compacted worklists needed atomics and scrambled the spatial order, both of
+// which cost more than the sweep.  A workgroup with a pending element left
+// after round r stores r + 1 into *pending_round (plain store, one per
+// workgroup); the host stops when a round leaves it unchanged.
+__device__ __forceinline__ unsigned long long jp_key(int e)
 {
-    const int n_in = n_in_p ? *n_in_p : n_in_static;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool lose = false;
-    int e = -1;
-    if (i < n_in) {
-        e = wl_in ? wl_in[i] : i;
-        const unsigned he = hash_u32((unsigned)e);
-        unsigned long long used0 = 0, used1 = 0;
-        for (int j = 0; j < 3 && !lose; ++j) {
-            const int v = p[3 * e + j];
-            const int t1 = n2e_ptr[v + 1];
-            for (int t = n2e_ptr[v]; t < t1; ++t) {
-                const int f = n2e[t];
-                if (f == e) continue;
-                const int cf = __hip_atomic_load(&color[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (cf < 0 || (cf >> 8) == round) {
-                    const unsigned hf = hash_u32((unsigned)f);
-                    if (hf > he || (hf == he && f > e)) { lose = true; break; }
-                } else {
-                    const int c = cf & 255;
-                    if (c < 64) used0 |= 1ull << c;
-                    else if (c < 128) used1 |= 1ull << (c - 64);
-                }
-            }
-        }
-        if (!lose) {
-            int c;
-            if (~used0) c = __ffsll((long long)~used0) - 1;
-            else if (~used1) c = 64 + __ffsll((long long)~used1) - 1;
-            else c = 255;  // > 128 colours: flagged by the host
-            __hip_atomic_store(&color[e], (round << 8) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ((unsigned long long)hash_u32((unsigned)e) << 32) | (unsigned)e;
+}
+
+__global__ void __launch_bounds__(kBlock) k_jp_nodes(int N, unsigned char *__restrict__ active,
+                                                     const int *__restrict__ n2e_ptr, const int *__restrict__ n2e,
+                                                     const int *__restrict__ color,
+                                                     unsigned long long *__restrict__ maxkey,
+                                                     unsigned long long *__restrict__ used)
+{
+    const int v = blockIdx.x * kBlock + threadIdx.x;
+    if (v >= N || !active[v]) return;
+    unsigned long long mk = 0, u0 = 0, u1 = 0;
+    bool pending = false;
+    const int t1 = n2e_ptr[v + 1];
+    for (int t = n2e_ptr[v]; t < t1; ++t) {
+        const int f = n2e[t];
+        const int c = color[f];
+        if (c < 0) {
+            const unsigned long long k = jp_key(f);
+            mk = k > mk ? k : mk;
+            pending = true;
+        } else if (c < 64) {
+            u0 |= 1ull << c;
+        } else if (c < 128) {
+            u1 |= 1ull << (c - 64);
         }
     }
-    const unsigned long long m = __ballot(lose);
-    if (m) {
-        const int lane = threadIdx.x & 63;
-        const int leader = __ffsll((long long)m) - 1;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(n_out, (int)__popcll(m));
-        base = __shfl(base, leader, 64);
-        if (lose) wl_out[base + (int)__popcll(m & ((1ull << lane) - 1ull))] = e;
+    if (pending) {
+        maxkey[v] = mk;
+        used[2 * v] = u0;
+        used[2 * v + 1] = u1;
+    } else {
+        active[v] = 0;
     }
 }
 
-// Strip the round tags and count elements per colour (LDS-private histogram,
-// one global atomic per bin per block).
-__global__ void __launch_bounds__(kBlock) k_color_hist(int NE, int *__restrict__ color, int *__restrict__ hist,
+__global__ void __launch_bounds__(kBlock) k_jp_elems(int NE, int round, int *__restrict__ pending_round,
+                                                     const int *__restrict__ p,
+                                                     const unsigned long long *__restrict__ maxkey,
+                                                     const unsigned long long *__restrict__ used,
+                                                     int *__restrict__ color)
+{
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    bool lose = false;
+    if (e < NE && color[e] < 0) {
+        const unsigned long long k = jp_key(e);
+        const int v0 = p[3 * e], v1 = p[3 * e + 1], v2 = p[3 * e + 2];
+        lose = (maxkey[v0] != k) || (maxkey[v1] != k) || (maxkey[v2] != k);
+        if (!lose) {
+            const unsigned long long u0 = used[2 * v0] | used[2 * v1] | used[2 * v2];
+            const unsigned long long u1 = used[2 * v0 + 1] | used[2 * v1 + 1] | used[2 * v2 + 1];
+            int c;
+            if (~u0) c = __ffsll((long long)~u0) - 1;
+            else if (~u1) c = 64 + __ffsll((long long)~u1) - 1;
+            else c = 255;  // > 128 colours: flagged by the host
+            color[e] = c;
+        }
+    }
+    if (__syncthreads_or(lose) && threadIdx.x == 0) *pending_round = round + 1;
+}
+
+// Count elements per colour (LDS-private histogram, one global atomic per bin
+// per block).
+__global__ void __launch_bounds__(kBlock) k_color_hist(int NE, const int *__restrict__ color, int *__restrict__ hist,
                                                        int maxc)
 {
     __shared__ int h[256];
     for (int k = threadIdx.x; k < 256; k += kBlock) h[k] = 0;
     __syncthreads();
     for (int e = blockIdx.x * kBlock + threadIdx.x; e < NE; e += gridDim.x * kBlock) {
-        const int c = color[e] & 255;
-        color[e] = c;
+        const int c = color[e];
         atomicAdd(&h[c < maxc ? c : maxc], 1);
     }
     __syncthreads();
@@ -271,11 +304,12 @@ __global__ void k_iota(int n, int *__restrict__ a)
 
 __global__ void k_build_erec(int NE, const int *__restrict__ perm, const int *__restrict__ p,
                              const int *__restrict__ lbl, const int *__restrict__ ebits_raw,
-                             int4 *__restrict__ erec, int *__restrict__ ebits)
+                             int4 *__restrict__ erec, int *__restrict__ ebits, int *__restrict__ iperm)
 {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= NE) return;
     int e = perm[i];
+    iperm[e] = i;
     erec[i] = make_int4(p[3 * e], p[3 * e + 1], p[3 * e + 2], lbl[e]);
     ebits[i] = ebits_raw[e];
 }
@@ -294,21 +328,36 @@ __device__ __forceinline__ int find_slot(const int *__restrict__ rowptr, const i
     return -1;
 }
 
-__global__ void k_build_slots(int NE, const int4 *__restrict__ erec, const int *__restrict__ rowptr,
-                              const int *__restrict__ col, int *__restrict__ slot, int *__restrict__ bad)
+// slot[9 i + 3 j + k] = CSR position of (n_j, n_k) of the element at colour
+// position i.  Threads walk the elements in their raw (mesh, spatially
+// coherent) order so that the row gathers hit in cache, one linear scan per
+// row (independent loads; rows are short), and scatter the 9 slots to the
+// element's colour position.
+__global__ void k_build_slots(int NE, const int *__restrict__ p, const int *__restrict__ iperm,
+                              const int *__restrict__ rowptr, const int *__restrict__ col, int *__restrict__ slot,
+                              int *__restrict__ bad)
 {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= NE) return;
-    int4 r = erec[i];
-    int n[3] = {r.x, r.y, r.z};
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= NE) return;
+    const int n[3] = {p[3 * e], p[3 * e + 1], p[3 * e + 2]};
+    int *dst = slot + 9LL * iperm[e];
+    int missing = 0;
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < 3; ++j) {
+        int s[3] = {-1, -1, -1};
+        const int k1 = rowptr[n[j] + 1];
+        for (int k = rowptr[n[j]]; k < k1; ++k) {
+            const int c = col[k];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            int s = find_slot(rowptr, col, n[j], n[k]);
-            if (s < 0) atomicAdd(bad, 1);
-            slot[9 * i + 3 * j + k] = s;
+            for (int q = 0; q < 3; ++q) s[q] = (c == n[q]) ? k : s[q];
         }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            missing |= (s[q] < 0);
+            dst[3 * j + q] = s[q];
+        }
+    }
+    if (missing) atomicAdd(bad, 1);
 }
 
 // (row, col) pairs -> CSR slots (periodic-map preparation)
@@ -688,26 +737,27 @@ void launch_sort_segments(hipStream_t s, int N, const int *ptr, int *a)
 {
     if (N) k_sort_segments<<<nblk(N), kBlock, 0, s>>>(N, ptr, a);
 }
-void launch_row_count(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e,
-                      const int *fill_ptr, const int *fill_col, int *rowcnt)
+long long row_tmp_size(int N, int NE, int nfill) { return 9LL * NE + nfill + N; }
+void launch_row_build(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e, const int *fill_ptr,
+                      const int *fill_col, int *tmp, int *rowcnt)
 {
     RowCands rc{p, n2e_ptr, n2e, fill_ptr, fill_col};
-    if (N) k_row_count<<<nblk(N), kBlock, 0, s>>>(N, rc, rowcnt);
+    if (N) k_row_build<<<nblk(N), kBlock, 0, s>>>(N, rc, tmp, rowcnt);
 }
-void launch_row_fill(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e,
-                     const int *fill_ptr, const int *fill_col, const int *rowptr, int *col, int *diag)
+void launch_row_copy(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e, const int *fill_ptr,
+                     const int *fill_col, const int *tmp, const int *rowptr, int *col, int *diag)
 {
     RowCands rc{p, n2e_ptr, n2e, fill_ptr, fill_col};
-    if (N) k_row_fill<<<nblk(N), kBlock, 0, s>>>(N, rc, rowptr, col, diag);
+    if (N) k_row_copy<<<nblk(N), kBlock, 0, s>>>(N, rc, tmp, rowptr, col, diag);
 }
-void launch_color_round(hipStream_t s, int round, int grid_n, const int *wl_in, const int *n_in_p, int n_in_static,
-                        int *wl_out, int *n_out, const int *p, const int *n2e_ptr, const int *n2e, int *color)
+void launch_jp_round(hipStream_t s, int N, int NE, int round, unsigned char *active, int *pending_round,
+                     const int *p, const int *n2e_ptr, const int *n2e, int *color, unsigned long long *maxkey,
+                     unsigned long long *used)
 {
-    if (grid_n > 0)
-        k_color_round<<<nblk(grid_n), kBlock, 0, s>>>(round, wl_in, n_in_p, n_in_static, wl_out, n_out, p, n2e_ptr,
-                                                      n2e, color);
+    if (N) k_jp_nodes<<<nblk(N), kBlock, 0, s>>>(N, active, n2e_ptr, n2e, color, maxkey, used);
+    if (NE) k_jp_elems<<<nblk(NE), kBlock, 0, s>>>(NE, round, pending_round, p, maxkey, used, color);
 }
-void launch_color_hist(hipStream_t s, int NE, int *color, int *hist, int maxc)
+void launch_color_hist(hipStream_t s, int NE, const int *color, int *hist, int maxc)
 {
     if (NE) k_color_hist<<<std::min(nblk(NE), 2048), kBlock, 0, s>>>(NE, color, hist, maxc);
 }
@@ -716,14 +766,14 @@ void launch_iota(hipStream_t s, int n, int *a)
     if (n) k_iota<<<nblk(n), kBlock, 0, s>>>(n, a);
 }
 void launch_build_erec(hipStream_t s, int NE, const int *perm, const int *p, const int *lbl, const int *ebits_raw,
-                       int4 *erec, int *ebits)
+                       int4 *erec, int *ebits, int *iperm)
 {
-    if (NE) k_build_erec<<<nblk(NE), kBlock, 0, s>>>(NE, perm, p, lbl, ebits_raw, erec, ebits);
+    if (NE) k_build_erec<<<nblk(NE), kBlock, 0, s>>>(NE, perm, p, lbl, ebits_raw, erec, ebits, iperm);
 }
-void launch_build_slots(hipStream_t s, int NE, const int4 *erec, const int *rowptr, const int *col, int *slot,
-                        int *bad)
+void launch_build_slots(hipStream_t s, int NE, const int *p, const int *iperm, const int *rowptr, const int *col,
+                        int *slot, int *bad)
 {
-    if (NE) k_build_slots<<<nblk(NE), kBlock, 0, s>>>(NE, erec, rowptr, col, slot, bad);
+    if (NE) k_build_slots<<<nblk(NE), kBlock, 0, s>>>(NE, p, iperm, rowptr, col, slot, bad);
 }
 void launch_lookup_slots(hipStream_t s, int n, const int *rc, const int *rowptr, const int *col, int *out)
 {

@@ -172,6 +172,8 @@ struct xfk_problem {
     xfk::DBuf<int> color;            // per raw element
     int color_rounds = 0;            // Jones-Plassmann rounds of the last symbolic build
     xfk::DBuf<char> cub_tmp;         // hipcub temporary storage
+    xfk::DBuf<char> sym_tmp;         // symbolic-phase temporaries (SymTmp in xfk_api.hip)
+    xfk::DBuf<int> fill_ptr, fill_col;   // periodic fill-in entries by row
     xfk::DBuf<int> perm;             // colour order -> raw element
     xfk::DBuf<int4> erec;            // colour order
     xfk::DBuf<int> ebits;            // colour order

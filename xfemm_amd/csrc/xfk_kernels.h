@@ -48,18 +48,21 @@ void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, con
 void launch_count_incidence(hipStream_t s, int NE, const int *p, int *deg);
 void launch_fill_n2e(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e);
 void launch_sort_segments(hipStream_t s, int N, const int *ptr, int *a);
-void launch_row_count(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e,
-                      const int *fill_ptr, const int *fill_col, int *rowcnt);
-void launch_row_fill(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e,
-                     const int *fill_ptr, const int *fill_col, const int *rowptr, int *col, int *diag);
-void launch_color_round(hipStream_t s, int round, int grid_n, const int *wl_in, const int *n_in_p, int n_in_static,
-                        int *wl_out, int *n_out, const int *p, const int *n2e_ptr, const int *n2e, int *color);
-void launch_color_hist(hipStream_t s, int NE, int *color, int *hist, int maxc);
+long long row_tmp_size(int N, int NE, int nfill);   // ints of the row-build scratch
+void launch_row_build(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e, const int *fill_ptr,
+                      const int *fill_col, int *tmp, int *rowcnt);
+void launch_row_copy(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e, const int *fill_ptr,
+                     const int *fill_col, const int *tmp, const int *rowptr, int *col, int *diag);
+// one Jones-Plassmann round (node pass + element pass) over the full arrays
+void launch_jp_round(hipStream_t s, int N, int NE, int round, unsigned char *active, int *pending_round,
+                     const int *p, const int *n2e_ptr, const int *n2e, int *color, unsigned long long *maxkey,
+                     unsigned long long *used);
+void launch_color_hist(hipStream_t s, int NE, const int *color, int *hist, int maxc);
 void launch_iota(hipStream_t s, int n, int *a);
 void launch_build_erec(hipStream_t s, int NE, const int *perm, const int *p, const int *lbl, const int *ebits_raw,
-                       int4 *erec, int *ebits);
-void launch_build_slots(hipStream_t s, int NE, const int4 *erec, const int *rowptr, const int *col, int *slot,
-                        int *bad);
+                       int4 *erec, int *ebits, int *iperm);
+void launch_build_slots(hipStream_t s, int NE, const int *p, const int *iperm, const int *rowptr, const int *col,
+                        int *slot, int *bad);
 void launch_lookup_slots(hipStream_t s, int n, const int *rc, const int *rowptr, const int *col, int *out);
 void launch_mark_fix_adj(hipStream_t s, int N, const int *rowptr, const int *col, const unsigned char *fixed,
                          int *flag);
