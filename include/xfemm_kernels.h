@@ -134,6 +134,56 @@ int xfk_get_solution(xfk_problem *prob, double *A_host);
 /* Circuit results after xfk_static2d: case (0/1), J, dV per circuit. */
 int xfk_get_circuits(xfk_problem *prob, int *ccase, double *J, double *dV);
 
+/* ---------------------------------------------------------------------------
+ * Sharded solve (one large mesh across ranks, configs[4]).
+ *
+ * Rows (nodes, in the caller's -- normally Cuthill-McKee -- numbering) are
+ * split into contiguous blocks, one per rank; each rank assembles the
+ * elements touching its rows (ghost elements replicated, no communication),
+ * exchanges the halo of the PCG vector before every SpMV, and all-reduces the
+ * PCG's per-block dot-product partials once per iteration.  Boundary
+ * conditions and circuits are evaluated on the GLOBAL mesh, so every rank
+ * passes the same global description.  Periodic boundaries are not supported
+ * in the sharded solve (XFK_ERR_UNSUPPORTED).
+ *
+ * xfk_static2d and xfk_get_solution are collective over the communicator
+ * (every rank calls them); xfk_get_solution returns the global solution on
+ * every rank.
+ * ------------------------------------------------------------------------- */
+typedef struct xfk_comm xfk_comm;
+
+/* RCCL, one process per GPU: rank 0 creates the 128-byte unique id, the caller
+ * distributes it (e.g. torch.distributed broadcast), every rank then calls
+ * xfk_comm_create_rccl (collective). */
+int xfk_comm_unique_id(void *out, int bytes);
+int xfk_comm_create_rccl(const void *unique_id, int bytes, int rank, int nranks, int device, xfk_comm **out);
+/* In-process group of nranks communicators (one host thread per rank, any
+ * devices, including several ranks on one device): the test transport. */
+int xfk_comm_create_local(int nranks, xfk_comm **out_array);
+void xfk_comm_destroy(xfk_comm *comm);
+int xfk_comm_rank(const xfk_comm *comm);
+int xfk_comm_size(const xfk_comm *comm);
+
+typedef struct {
+    int rank, nranks;
+    int n_global;               /* global nodes */
+    int row0, n_own;            /* owned rows [row0, row0 + n_own) */
+    int n_halo;                 /* halo nodes (local ids n_own .. n_own + n_halo - 1) */
+    int n_elems;                /* local (owned + ghost) elements */
+    int n_send, n_recv;         /* halo ranges */
+} xfk_dist_info;
+
+/* Host-only partition plan (no device needed).  Call once with null arrays to
+ * get the sizes in *info, then with l2g[n_own + n_halo], elems[n_elems],
+ * recv[4 * n_recv] and send[4 * n_send] ({peer, local offset, length, first
+ * global row} per range). */
+int xfk_partition_plan(int n_nodes, int n_elems, const int *p, int rank, int nranks, xfk_dist_info *info,
+                       int *l2g, int *elems, int *recv, int *send);
+
+/* This rank's part of the global problem `desc` on `device`. */
+int xfk_problem_create_dist(const xfk_problem_desc *desc, int device, xfk_comm *comm, xfk_problem **out);
+int xfk_dist_get_info(const xfk_problem *prob, xfk_dist_info *info);
+
 /* Device views for the bench / tests (stream-ordered on the problem's stream). */
 int xfk_get_csr(xfk_problem *prob, int *rowptr, int *col, double *val, double *b);
 long long xfk_get_nnz(xfk_problem *prob);

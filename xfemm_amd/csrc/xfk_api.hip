@@ -19,20 +19,14 @@
 #include <type_traits>
 #include <unordered_map>
 
+#include "xfk_comm.h"
 #include "xfk_kernels.h"
+#include "xfk_partition.h"
 
 namespace xfk {
 
 static thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
-
-#define XFK_REQUIRE(cond, code, msg)  \
-    do {                              \
-        if (!(cond)) {                \
-            ::xfk::set_error(msg);    \
-            return code;              \
-        }                             \
-    } while (0)
 
 using Terms = std::vector<std::pair<long long, double>>;
 
@@ -242,21 +236,21 @@ struct SymTmp {
 static int build_symbolic(xfk_problem *P)
 {
     hipStream_t s = P->stream;
-    const int N = P->N, NE = P->NE;
+    const int N = P->N, NL = P->NL, NE = P->NE;   // owned rows, local nodes, local elements
     SymTmp T;
     const int nfill = 2 * (int)P->pbc_fill.size();
-    T.carve(nullptr, N, NE, nfill);
+    T.carve(nullptr, NL, NE, nfill);
     XFK_CHECK(P->sym_tmp.alloc(T.bytes));
-    T.carve(P->sym_tmp.p, N, NE, nfill);
+    T.carve(P->sym_tmp.p, NL, NE, nfill);
     XFK_CHECK(hipMemsetAsync(P->sym_tmp.p, 0, T.zero_bytes, s));
 
     // node -> incident elements
-    XFK_CHECK(P->n2e_ptr.alloc(N + 1));
+    XFK_CHECK(P->n2e_ptr.alloc(NL + 1));
     XFK_CHECK(P->n2e.alloc(3 * (size_t)NE));
     launch_count_incidence(s, NE, P->p_raw.p, T.deg);
-    XFK_CHECK(exclusive_scan(P, T.deg, P->n2e_ptr.p, N));
+    XFK_CHECK(exclusive_scan(P, T.deg, P->n2e_ptr.p, NL));
     launch_fill_n2e(s, NE, P->p_raw.p, P->n2e_ptr.p, T.cursor, P->n2e.p);
-    launch_sort_segments(s, N, P->n2e_ptr.p, P->n2e.p);
+    launch_sort_segments(s, NL, P->n2e_ptr.p, P->n2e.p);
 
     // periodic fill-in entries, CSR by row
     const int *fp = nullptr, *fc = nullptr;
@@ -298,12 +292,12 @@ static int build_symbolic(xfk_problem *P)
     XFK_CHECK(P->color.alloc(NE));
     XFK_CHECK(hipMemsetAsync(P->color.p, 0xff, sizeof(int) * NE, s));
     constexpr int kSyncRounds = 6;
-    XFK_CHECK(hipMemsetAsync(T.active, 1, (size_t)N, s));
+    XFK_CHECK(hipMemsetAsync(T.active, 1, (size_t)NL, s));
     int round = 0, last = 0;
     for (;;) {
         XFK_REQUIRE(round < SymTmp::kMaxRounds, XFK_ERR_UNSUPPORTED, "element colouring did not terminate");
         for (int k = 0; k < kSyncRounds; ++k, ++round)
-            launch_jp_round(s, N, NE, round, T.active, T.cnt + 2, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, P->color.p,
+            launch_jp_round(s, NL, NE, round, T.active, T.cnt + 2, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, P->color.p,
                             T.maxkey, T.used);
         XFK_CHECK(d2h(&last, T.cnt + 2, sizeof(int), s));
         if (last < round) break;       // the last round launched left nothing pending
@@ -338,7 +332,7 @@ static int build_symbolic(xfk_problem *P)
     XFK_CHECK(P->ebits.alloc(NE));
     XFK_CHECK(P->slot.alloc(9 * (size_t)NE));
     launch_build_erec(s, NE, P->perm.p, P->p_raw.p, P->lbl_raw.p, P->ebits_raw.p, P->erec.p, P->ebits.p, T.iperm);
-    launch_build_slots(s, NE, P->p_raw.p, T.iperm, P->rowptr.p, P->col.p, P->slot.p, T.cnt);
+    launch_build_slots(s, NE, N, P->p_raw.p, T.iperm, P->rowptr.p, P->col.p, P->slot.p, T.cnt);
 
     // rows adjacent to fixed nodes
     launch_mark_fix_adj(s, N, P->rowptr.p, P->col.p, P->fixed.p, T.flag);
@@ -414,7 +408,8 @@ static int build_symbolic(xfk_problem *P)
     }
 
     // vectors and reduction scratch
-    for (DBuf<double> *v : {&P->b, &P->V, &P->Vold, &P->P, &P->dinv}) XFK_CHECK(v->alloc(N));
+    for (DBuf<double> *v : {&P->b, &P->P, &P->dinv}) XFK_CHECK(v->alloc(N));
+    for (DBuf<double> *v : {&P->V, &P->Vold}) XFK_CHECK(v->alloc(NL));
     XFK_CHECK(P->partials.alloc(2 * kRedGrid));
     XFK_CHECK(P->counters.alloc(8));
     XFK_CHECK(hipMemsetAsync(P->counters.p, 0, sizeof(unsigned) * 8, s));
@@ -463,21 +458,37 @@ static int assemble(xfk_problem *P, int iter)
 }
 
 // CBigLinProb::PCGSolve(flag) on the assembled system (Jacobi-preconditioned,
-// two launches per iteration: xfk_pcg.hip)
+// two launches per iteration: xfk_pcg.hip).  Sharded: the halo of u is
+// exchanged before every SpMV and the per-block partials are all-reduced
+// (elementwise, so every rank then sums identical arrays in the same order and
+// takes bit-identical alpha, beta and stopping decisions).
 static int alloc_cg(xfk_problem *P)
 {
-    const int N = P->N, G = std::max(cg_grid(N), cg_axpy_grid(N));
-    XFK_CHECK(P->R2.alloc((size_t)N));      // r
-    XFK_CHECK(P->W2.alloc((size_t)N));      // w = A u
-    XFK_CHECK(P->Z2.alloc(2 * (size_t)N));  // z (first half), u = M^-1 r (second half)
-    XFK_CHECK(P->part_cg.alloc(3 * (size_t)G));   // gamma[2] + delta
-    XFK_CHECK(P->part_reso.alloc((size_t)G));
+    const int N = P->N, NL = P->NL;
+    int G = std::max(cg_grid(N), cg_axpy_grid(N));
+    if (P->comm)
+        for (int q = 0; q < P->nranks; ++q) {
+            const int nq = (int)(row_begin(P->N_global, q + 1, P->nranks) - row_begin(P->N_global, q, P->nranks));
+            G = std::max(G, std::max(cg_grid(nq), cg_axpy_grid(nq)));
+        }
+    P->Gpart = G;
+    XFK_CHECK(P->R2.alloc((size_t)N));            // r
+    XFK_CHECK(P->W2.alloc((size_t)N));            // w = A u
+    XFK_CHECK(P->Z2.alloc((size_t)N + NL));       // z (N), then u = M^-1 r (NL, halo last)
+    XFK_CHECK(P->part_loc.alloc(4 * (size_t)G));
+    if (P->comm) {
+        XFK_CHECK(P->part_glob_buf.alloc(4 * (size_t)G));
+        P->part_glob = P->part_glob_buf.p;
+    } else {
+        P->part_glob = P->part_loc.p;
+    }
     return XFK_OK;
 }
 
 static CgAxpyArgs cg_args(xfk_problem *P, long long it)
 {
-    const int N = P->N, G = std::max(cg_grid(N), cg_axpy_grid(N));
+    const int N = P->N;
+    const size_t G = (size_t)P->Gpart;
     CgAxpyArgs A;
     A.W = P->W2.p;
     A.dinv = P->dinv.p;
@@ -486,16 +497,43 @@ static CgAxpyArgs cg_args(xfk_problem *P, long long it)
     A.P = P->P.p;
     A.V = P->V.p;
     A.R = P->R2.p;
-    A.gam_in = P->part_cg.p + (size_t)(it & 1) * G;
-    A.gam_out = P->part_cg.p + (size_t)((it + 1) & 1) * G;
-    A.del_in = P->part_cg.p + 2 * (size_t)G;
-    A.reso = P->part_reso.p;
-    A.Ggam = (it == 0) ? cg_grid(N) : cg_axpy_grid(N);
-    A.Gdel = cg_grid(N);
+    A.gam_in = P->part_glob + (size_t)(it & 1) * G;
+    A.gam_out = P->part_loc.p + (size_t)((it + 1) & 1) * G;
+    A.del_in = P->part_glob + 2 * G;
+    A.reso = P->part_glob + 3 * G;
+    if (P->comm) {
+        A.Ggam = A.Gdel = (int)G;     // zero beyond this rank's grids
+    } else {
+        A.Ggam = (it == 0) ? cg_grid(N) : cg_axpy_grid(N);
+        A.Gdel = cg_grid(N);
+    }
     A.S = P->pcg.p;
     A.it = it;
     A.N = N;
     return A;
+}
+
+// sum of a host scalar over the ranks (setup-time decisions that must agree)
+static int allreduce_host(xfk_problem *P, double &v)
+{
+    if (!P->comm) return XFK_OK;
+    hipStream_t s = P->stream;
+    XFK_CHECK(P->nws_glob.alloc(4));
+    XFK_CHECK(hipMemcpyAsync(P->nws_glob.p, &v, sizeof(double), hipMemcpyHostToDevice, s));
+    int rc = P->comm->allreduce_sum(P->nws_glob.p, P->nws_glob.p + 2, 1, s);
+    if (rc != XFK_OK) return rc;
+    return d2h(&v, P->nws_glob.p + 2, sizeof(double), s) == hipSuccess ? XFK_OK : XFK_ERR_HIP;
+}
+
+static int exchange(xfk_problem *P, double *vec)
+{
+    return P->comm ? P->comm->exchange(P->halo, vec, P->stream) : XFK_OK;
+}
+
+static int allreduce_partials(xfk_problem *P, int narrays)
+{
+    if (!P->comm) return XFK_OK;
+    return P->comm->allreduce_sum(P->part_loc.p, P->part_glob, (size_t)narrays * P->Gpart, P->stream);
 }
 
 static int pcg_start(xfk_problem *P, int flag)
@@ -505,17 +543,25 @@ static int pcg_start(xfk_problem *P, int flag)
     CgState init{};
     init.tol = P->precision;
     XFK_CHECK(hipMemcpyAsync(P->pcg.p, &init, sizeof(CgState), hipMemcpyHostToDevice, s));
+    if (P->comm) XFK_CHECK(hipMemsetAsync(P->part_loc.p, 0, sizeof(double) * 4 * P->Gpart, s));
     launch_diag_inv(s, N, P->diag.p, P->val.p, P->dinv.p, P->pcg.p);
     XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(CgState), hipMemcpyDeviceToHost, s));
     XFK_CHECK(hipStreamSynchronize(s));
-    if (P->pcg_host->singular) {
+    double singular = P->pcg_host->singular ? 1.0 : 0.0;
+    int rc = allreduce_host(P, singular);
+    if (rc != XFK_OK) return rc;
+    if (singular != 0.0) {
         set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
         return XFK_ERR_SINGULAR;
     }
     const CgAxpyArgs A0 = cg_args(P, 0);
-    launch_cg_init(s, N, flag, P->rowptr.p, P->col.p, P->val.p, P->b.p, P->V.p, A0.R, A0.U, A0.Z, A0.P, P->W2.p,
-                   P->dinv.p, P->part_reso.p, (double *)A0.gam_in, (double *)A0.del_in);
-    return XFK_OK;
+    const size_t G = (size_t)P->Gpart;
+    if (flag && (rc = exchange(P, P->V.p)) != XFK_OK) return rc;
+    launch_cg_init_r(s, N, flag, P->rowptr.p, P->col.p, P->val.p, P->b.p, P->V.p, A0.R, A0.U, A0.Z, A0.P, P->dinv.p,
+                     P->part_loc.p + 3 * G, P->part_loc.p);
+    if ((rc = exchange(P, A0.U)) != XFK_OK) return rc;
+    launch_cg_spmv(s, N, P->rowptr.p, P->col.p, P->val.p, A0.U, P->W2.p, P->part_loc.p + 2 * G, nullptr);
+    return allreduce_partials(P, 4);
 }
 
 // one PCG iteration: the streaming update then the SpMV (optionally bracketed
@@ -525,13 +571,16 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
     hipStream_t s = P->stream;
     const CgAxpyArgs A = cg_args(P, it);
     launch_cg_axpy(s, A);
+    int rc = exchange(P, A.U);
+    if (rc != XFK_OK) return rc;
     if (stamp) XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used], s));
-    launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, (double *)A.del_in, P->pcg.p);
+    launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * (size_t)P->Gpart,
+                   P->pcg.p);
     if (stamp) {
         XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used + 1], s));
         P->spmv_used += 2;
     }
-    return XFK_OK;
+    return allreduce_partials(P, 3);
 }
 
 static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
@@ -588,29 +637,21 @@ void xfk_problem_destroy(xfk_problem *P)
     (void)hipSetDevice(P->device);
     if (P->stream) (void)hipStreamSynchronize(P->stream);
     for (auto &ev : P->spmv_ev) (void)hipEventDestroy(ev);
-    P->x.free(); P->y.free(); P->p_raw.free(); P->lbl_raw.free(); P->ebits_raw.free();
-    P->blocks.free(); P->labels.free(); P->lines.free(); P->circs.free();
-    P->bhB.free(); P->bhH.free(); P->bhS.free();
-    P->n2e_ptr.free(); P->n2e.free(); P->rowptr.free(); P->col.free(); P->diag.free();
-    P->color.free(); P->perm.free(); P->erec.free(); P->ebits.free(); P->slot.free();
-    P->mu1.free(); P->mu2.free();
-    P->pt_nodes.free(); P->pt_J.free(); P->fixed.free(); P->fix_first.free(); P->fix_last.free();
-    P->fix_rows.free(); P->fix_cols.free(); P->fix_cols_node.free(); P->fix_cols_row.free();
-    P->pm_dst.free(); P->pm_ptr.free(); P->pm_src.free(); P->pm_w.free(); P->pm_tmp.free();
-    P->pb_dst.free(); P->pb_ptr.free(); P->pb_src.free(); P->pb_w.free(); P->pb_tmp.free();
-    P->val.free(); P->b.free(); P->V.free(); P->Vold.free(); P->P.free();
-    P->R2.free(); P->W2.free(); P->Z2.free(); P->part_cg.free(); P->part_reso.free();
-    P->dinv.free(); P->partials.free(); P->counters.free(); P->pcg.free(); P->nws.free();
     if (P->pcg_host) (void)hipHostFree(P->pcg_host);
     if (P->nws_host) (void)hipHostFree(P->nws_host);
-    if (P->stream) (void)hipStreamDestroy(P->stream);
-    delete P;
+    hipStream_t s = P->stream;
+    delete P;   // device buffers free themselves (DBuf), on this device
+    if (s) (void)hipStreamDestroy(s);
 }
 
-int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
+}  // extern "C"
+
+// ----------------------------------------------------------------------------
+// problem creation: validation, global preparation, local (per-rank) build
+// ----------------------------------------------------------------------------
+
+static int validate_desc(const xfk_problem_desc *d)
 {
-    XFK_REQUIRE(d && out, XFK_ERR_ARG, "null argument");
-    *out = nullptr;
     XFK_REQUIRE(d->n_nodes > 0 && d->n_elems > 0, XFK_ERR_ARG, "empty mesh");
     XFK_REQUIRE(d->x && d->y && d->p && d->lbl, XFK_ERR_ARG, "missing mesh arrays");
     XFK_REQUIRE(d->n_blocks > 0 && d->blocks && d->n_labels > 0 && d->labels, XFK_ERR_ARG,
@@ -620,13 +661,7 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
     XFK_REQUIRE(d->n_circs == 0 || d->circs, XFK_ERR_ARG, "missing circuit table");
     XFK_REQUIRE(d->n_pbc == 0 || d->pbc, XFK_ERR_ARG, "missing pbc table");
     XFK_REQUIRE(d->n_lines < 1023, XFK_ERR_UNSUPPORTED, "at most 1022 boundary properties");
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
-        set_error("no HIP device available (the fsolver hot path has no CPU fallback)");
-        return XFK_ERR_HIP;
-    }
-    XFK_REQUIRE(device >= 0 && device < ndev, XFK_ERR_ARG, "device index out of range");
-
+    XFK_REQUIRE(d->length_units >= 0 && d->length_units < 6, XFK_ERR_ARG, "bad length units");
     const int N = d->n_nodes, NE = d->n_elems;
     for (long long i = 0; i < 3LL * NE; ++i)
         XFK_REQUIRE(d->p[i] >= 0 && d->p[i] < N, XFK_ERR_ARG, "element node index out of range");
@@ -648,97 +683,100 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
     if (d->e)
         for (long long i = 0; i < 3LL * NE; ++i)
             XFK_REQUIRE(d->e[i] < d->n_lines, XFK_ERR_ARG, "edge boundary-property index out of range");
+    return XFK_OK;
+}
 
-    xfk_problem *P = new xfk_problem();
-    P->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking) != hipSuccess) {
-        set_error("cannot initialise the HIP device/stream");
-        delete P;
+static int check_device(int device)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        set_error("no HIP device available (the fsolver hot path has no CPU fallback)");
         return XFK_ERR_HIP;
     }
-    auto fail = [&](int code) {
-        xfk_problem_destroy(P);
-        return code;
-    };
-    P->N = N;
-    P->NE = NE;
-    P->precision = d->precision;
-    P->relax = d->relax;
-    P->length_units = d->length_units;
-    P->coords = d->coords;
-    P->hx.assign(d->x, d->x + N);
-    P->hy.assign(d->y, d->y + N);
-    P->hp.assign(d->p, d->p + 3LL * NE);
-    P->hlbl.assign(d->lbl, d->lbl + NE);
-    P->hmarker.assign(N, -1);
-    if (d->marker) P->hmarker.assign(d->marker, d->marker + N);
-    P->he.assign(3LL * NE, -1);
-    if (d->e) P->he.assign(d->e, d->e + 3LL * NE);
-    if (d->n_pbc) P->hpbc.assign(d->pbc, d->pbc + 3LL * d->n_pbc);
-    P->hlines.assign(d->lines, d->lines + d->n_lines);
-    P->hpoints.assign(d->points, d->points + d->n_points);
+    XFK_REQUIRE(device >= 0 && device < ndev, XFK_ERR_ARG, "device index out of range");
+    return XFK_OK;
+}
+
+// Everything Static2D derives from the GLOBAL problem before the mesh is split
+// (so a sharded solve sees the same boundary values, point currents and
+// circuit currents as the single-device one).
+struct GlobalPrep {
+    std::vector<DevBlock> blk;
+    std::vector<double> hB, hH, hS;
+    std::vector<DevLabel> lab;
+    std::vector<DevLine> lin;
+    std::vector<DevCirc> circ;
+    std::vector<int> ebits;              // per element: 3 x 10-bit boundary-prop index + 1
+    std::vector<int> pt_nodes;           // nodes with a point current, ascending
+    std::vector<double> pt_J;            // 0.01 * J of each
+    std::vector<unsigned char> fixed;    // per node: Dirichlet value set
+    std::vector<double> first, last;     // first / last value set (CBigLinProb::SetValue order)
+    bool any_nonlinear = false;
+};
+
+static void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
+{
+    const int N = d->n_nodes, NE = d->n_elems;
     const double c = kC;
     const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
-    XFK_REQUIRE(d->length_units >= 0 && d->length_units < 6, fail(XFK_ERR_ARG), "bad length units");
 
     // tables
-    std::vector<DevBlock> blk(d->n_blocks);
-    std::vector<double> hB, hH, hS;
+    G.blk.resize(d->n_blocks);
     for (int k = 0; k < d->n_blocks; ++k) {
         const xfk_block_desc &b = d->blocks[k];
-        DevBlock &o = blk[k];
+        DevBlock &o = G.blk[k];
         o.mu_x = b.mu_x; o.mu_y = b.mu_y; o.H_c = b.H_c; o.J_re = b.J_re; o.Cduct = b.Cduct;
         o.LamFill = b.LamFill; o.LamType = b.LamType; o.BHpoints = b.BHpoints;
-        o.bh_off = (int)hB.size();
+        o.bh_off = (int)G.hB.size();
         o.pad = 0;
         for (int i = 0; i < b.BHpoints; ++i) {
-            hB.push_back(b.B[i]);
-            hH.push_back(b.H[i]);
-            hS.push_back(b.slope[i]);
+            G.hB.push_back(b.B[i]);
+            G.hH.push_back(b.H[i]);
+            G.hS.push_back(b.slope[i]);
         }
     }
-    if (hB.empty()) { hB.push_back(0); hH.push_back(0); hS.push_back(0); }
-    std::vector<DevLabel> lab(d->n_labels);
+    if (G.hB.empty()) { G.hB.push_back(0); G.hH.push_back(0); G.hS.push_back(0); }
+    G.lab.resize(d->n_labels);
     for (int k = 0; k < d->n_labels; ++k) {
         const xfk_label_desc &l = d->labels[k];
         double t = l.mag_dir;
-        lab[k].cos_m = cos(t * kPI / 180.);
-        lab[k].sin_m = sin(t * kPI / 180.);
-        lab[k].blk = l.block;
-        lab[k].in_circuit = l.in_circuit;
-        lab[k].is_wound = l.is_wound;
-        lab[k].pad = 0;
+        G.lab[k].cos_m = cos(t * kPI / 180.);
+        G.lab[k].sin_m = sin(t * kPI / 180.);
+        G.lab[k].blk = l.block;
+        G.lab[k].in_circuit = l.in_circuit;
+        G.lab[k].is_wound = l.is_wound;
+        G.lab[k].pad = 0;
     }
-    std::vector<DevLine> lin(std::max(1, d->n_lines));
+    G.lin.assign(std::max(1, d->n_lines), DevLine{});
     for (int k = 0; k < d->n_lines; ++k) {
-        lin[k].c0 = d->lines[k].c0;
-        lin[k].c1 = d->lines[k].c1;
-        lin[k].format = d->lines[k].format;
-        lin[k].pad = 0;
+        G.lin[k].c0 = d->lines[k].c0;
+        G.lin[k].c1 = d->lines[k].c1;
+        G.lin[k].format = d->lines[k].format;
+        G.lin[k].pad = 0;
     }
     // which elements are nonlinear -> LinearFlag (static2d.cpp:633-639)
-    for (int i = 0; i < NE && !P->any_nonlinear; ++i)
-        if (blk[lab[d->lbl[i]].blk].BHpoints != 0) P->any_nonlinear = true;
+    for (int i = 0; i < NE && !G.any_nonlinear; ++i)
+        if (G.blk[G.lab[d->lbl[i]].blk].BHpoints != 0) G.any_nonlinear = true;
 
     // circuits, element order (static2d.cpp:84-167)
-    std::vector<DevCirc> circ(std::max(1, d->n_circs));
+    G.circ.assign(std::max(1, d->n_circs), DevCirc{});
     if (d->n_circs > 0) {
         std::vector<double> I1(d->n_circs, 0.0), I2(d->n_circs, 0.0), I3(d->n_circs, 0.0);
         for (int i = 0; i < NE; ++i) {
-            const DevLabel &L = lab[d->lbl[i]];
+            const DevLabel &L = G.lab[d->lbl[i]];
             if (L.in_circuit == -1) continue;
             const int *n = d->p + 3LL * i;
             double p0 = d->y[n[1]] - d->y[n[2]], p1 = d->y[n[2]] - d->y[n[0]];
             double q0 = d->x[n[2]] - d->x[n[1]], q1 = d->x[n[0]] - d->x[n[2]];
             double a = (p0 * q1 - p1 * q0) / 2.;
-            double Cduct = blk[L.blk].Cduct;
+            double Cduct = G.blk[L.blk].Cduct;
             if (L.is_wound) Cduct = 0;
             I1[L.in_circuit] += a;
             I2[L.in_circuit] += a * Cduct;
-            I3[L.in_circuit] += blk[L.blk].J_re * a * 100.;
+            I3[L.in_circuit] += G.blk[L.blk].J_re * a * 100.;
         }
         for (int k = 0; k < d->n_circs; ++k) {
-            DevCirc &C = circ[k];
+            DevCirc &C = G.circ[k];
             C.amps_re = d->circs[k].amps_re;
             C.dvolts_re = d->circs[k].dvolts_re;
             C.type = d->circs[k].type;
@@ -759,38 +797,39 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
     }
 
     // edges -> packed 3 x 10-bit boundary-property indices
-    std::vector<int> ebits(NE, 0);
+    auto edge = [&](long long k) { return d->e ? d->e[k] : -1; };
+    G.ebits.assign(NE, 0);
     for (int i = 0; i < NE; ++i)
         for (int j = 0; j < 3; ++j) {
-            int ej = P->he[3LL * i + j];
-            if (ej >= 0) ebits[i] |= (ej + 1) << (10 * j);
+            int ej = edge(3LL * i + j);
+            if (ej >= 0) G.ebits[i] |= (ej + 1) << (10 * j);
         }
 
     // point currents and Dirichlet values in the reference's SetValue order
-    std::vector<int> pt_nodes;
-    std::vector<double> pt_J;
-    std::vector<unsigned char> fixed(N, 0);
-    std::vector<double> first(N, 0.0), last(N, 0.0);
+    G.fixed.assign(N, 0);
+    G.first.assign(N, 0.0);
+    G.last.assign(N, 0.0);
     auto set_value = [&](int i, double x) {
-        if (!fixed[i]) first[i] = x;
-        fixed[i] = 1;
-        last[i] = x;
+        if (!G.fixed[i]) G.first[i] = x;
+        G.fixed[i] = 1;
+        G.last[i] = x;
     };
+    auto marker = [&](int i) { return d->marker ? d->marker[i] : -1; };
     for (int i = 0; i < N; ++i) {
-        int m = P->hmarker[i];
+        int m = marker(i);
         if (m >= 0 && d->points[m].J_re != 0.0) {
-            pt_nodes.push_back(i);
-            pt_J.push_back(0.01 * d->points[m].J_re);
+            G.pt_nodes.push_back(i);
+            G.pt_J.push_back(0.01 * d->points[m].J_re);
         }
     }
     for (int i = 0; i < N; ++i) {
-        int m = P->hmarker[i];
+        int m = marker(i);
         if (m >= 0 && d->points[m].J_re == 0 && d->points[m].J_im == 0) set_value(i, d->points[m].A_re / c);
     }
     for (int i = 0; i < NE; ++i)
         for (int j = 0; j < 3; ++j) {
             int k = (j + 1) % 3;
-            int sgi = P->he[3LL * i + j];
+            int sgi = edge(3LL * i + j);
             if (sgi < 0 || d->lines[sgi].format != 0) continue;
             const xfk_line_desc &ln = d->lines[sgi];
             int nodes2[2] = {d->p[3LL * i + j], d->p[3LL * i + k]};
@@ -811,9 +850,100 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
                 set_value(nodes2[m], a / c);
             }
         }
-    std::vector<int> fix_rows;
-    for (int i = 0; i < N; ++i)
-        if (fixed[i]) fix_rows.push_back(i);
+}
+
+// Build the device problem of one rank (plan == nullptr: the whole mesh).
+static int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *plan, int device,
+                       xfk_comm *comm, xfk_problem **out)
+{
+    xfk_problem *P = new xfk_problem();
+    P->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking) != hipSuccess) {
+        set_error("cannot initialise the HIP device/stream");
+        delete P;
+        return XFK_ERR_HIP;
+    }
+    auto fail = [&](int code) {
+        xfk_problem_destroy(P);
+        return code;
+    };
+    const int Ng = d->n_nodes, NEg = d->n_elems;
+    const int N = plan ? plan->n_own : Ng;                  // owned rows
+    const int NL = plan ? plan->n_own + plan->n_halo : Ng;  // local nodes
+    const int NE = plan ? (int)plan->elems.size() : NEg;
+    auto gnode = [&](int l) { return plan ? plan->l2g[l] : l; };
+    auto gelem = [&](int l) { return plan ? plan->elems[l] : l; };
+    P->N = N;
+    P->NL = NL;
+    P->NE = NE;
+    P->N_global = Ng;
+    P->precision = d->precision;
+    P->relax = d->relax;
+    P->length_units = d->length_units;
+    P->coords = d->coords;
+    P->any_nonlinear = G.any_nonlinear;
+    if (plan) {
+        P->comm = comm;
+        P->rank = plan->rank;
+        P->nranks = plan->nranks;
+        P->row0 = plan->row0;
+        P->halo = plan->halo;
+        P->l2g = plan->l2g;
+    }
+
+    // local mesh
+    std::vector<double> x(NL), y(NL);
+    std::vector<int> g2l_tmp;
+    for (int l = 0; l < NL; ++l) {
+        x[l] = d->x[gnode(l)];
+        y[l] = d->y[gnode(l)];
+    }
+    std::vector<int> pl(3LL * NE), lbl(NE), ebits(NE);
+    if (plan) {
+        // global -> local for the nodes of local elements: owned, or inside a receive range
+        auto g2l = [&](int g) {
+            if (g >= plan->row0 && g < plan->row0 + plan->n_own) return g - plan->row0;
+            for (const HaloRange &r : plan->halo.recv)
+                if (g >= r.g0 && g < r.g0 + r.len) return r.off + (g - r.g0);
+            return -1;
+        };
+        for (int l = 0; l < NE; ++l) {
+            const int e = gelem(l);
+            for (int j = 0; j < 3; ++j) {
+                const int v = g2l(d->p[3LL * e + j]);
+                XFK_REQUIRE(v >= 0, fail(XFK_ERR_ARG), "internal: element node outside the local halo");
+                pl[3LL * l + j] = v;
+            }
+        }
+    } else {
+        pl.assign(d->p, d->p + 3LL * NE);
+    }
+    for (int l = 0; l < NE; ++l) {
+        lbl[l] = d->lbl[gelem(l)];
+        ebits[l] = G.ebits[gelem(l)];
+    }
+    P->hp = pl;
+    if (!plan && d->n_pbc) P->hpbc.assign(d->pbc, d->pbc + 3LL * d->n_pbc);
+
+    // boundary data of the local nodes (global values), owned rows only for rows
+    std::vector<unsigned char> fixed(NL);
+    std::vector<double> first(NL), last(NL);
+    for (int l = 0; l < NL; ++l) {
+        fixed[l] = G.fixed[gnode(l)];
+        first[l] = G.first[gnode(l)];
+        last[l] = G.last[gnode(l)];
+    }
+    std::vector<int> pt_nodes, fix_rows;
+    std::vector<double> pt_J;
+    for (size_t k = 0; k < G.pt_nodes.size(); ++k) {
+        const int g = G.pt_nodes[k];
+        const int l = plan ? g - plan->row0 : g;
+        if (l < 0 || l >= N) continue;
+        pt_nodes.push_back(l);
+        pt_J.push_back(G.pt_J[k]);
+    }
+    for (int l = 0; l < N; ++l)
+        if (fixed[l]) fix_rows.push_back(l);
     P->npt = (int)pt_nodes.size();
     P->nfix_rows = (int)fix_rows.size();
 
@@ -823,18 +953,18 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
     hipStream_t s = P->stream;
     hipError_t e = hipSuccess;
 #define UP(buf, ptr, n) if (e == hipSuccess) e = upload(buf, ptr, n, s)
-    UP(P->x, d->x, (size_t)N);
-    UP(P->y, d->y, (size_t)N);
-    UP(P->p_raw, d->p, 3 * (size_t)NE);
-    UP(P->lbl_raw, d->lbl, (size_t)NE);
+    UP(P->x, x.data(), (size_t)NL);
+    UP(P->y, y.data(), (size_t)NL);
+    UP(P->p_raw, pl.data(), 3 * (size_t)NE);
+    UP(P->lbl_raw, lbl.data(), (size_t)NE);
     UP(P->ebits_raw, ebits.data(), (size_t)NE);
-    UP(P->blocks, blk.data(), blk.size());
-    UP(P->labels, lab.data(), lab.size());
-    UP(P->lines, lin.data(), lin.size());
-    UP(P->circs, circ.data(), circ.size());
-    UP(P->bhB, hB.data(), hB.size());
-    UP(P->bhH, hH.data(), hH.size());
-    UP(P->bhS, hS.data(), hS.size());
+    UP(P->blocks, G.blk.data(), G.blk.size());
+    UP(P->labels, G.lab.data(), G.lab.size());
+    UP(P->lines, G.lin.data(), G.lin.size());
+    UP(P->circs, G.circ.data(), G.circ.size());
+    UP(P->bhB, G.hB.data(), G.hB.size());
+    UP(P->bhH, G.hH.data(), G.hH.size());
+    UP(P->bhS, G.hS.data(), G.hS.size());
     UP(P->pt_nodes, pt_nodes.data(), pt_nodes.size());
     UP(P->pt_J, pt_J.data(), pt_J.size());
     UP(P->fixed, fixed.data(), fixed.size());
@@ -854,6 +984,82 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
     P->nlines = d->n_lines;
     P->ncircs = d->n_circs;
     *out = P;
+    return XFK_OK;
+}
+
+extern "C" {
+
+int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
+{
+    XFK_REQUIRE(d && out, XFK_ERR_ARG, "null argument");
+    *out = nullptr;
+    int rc = validate_desc(d);
+    if (rc == XFK_OK) rc = check_device(device);
+    if (rc != XFK_OK) return rc;
+    GlobalPrep G;
+    prepare_global(d, G);
+    return build_local(d, G, nullptr, device, nullptr, out);
+}
+
+int xfk_partition_plan(int n_nodes, int n_elems, const int *p, int rank, int nranks, xfk_dist_info *info,
+                       int *l2g, int *elems, int *recv, int *send)
+{
+    XFK_REQUIRE(p && info && n_nodes > 0 && n_elems > 0, XFK_ERR_ARG, "null argument");
+    PartPlan plan;
+    XFK_REQUIRE(plan_partition(n_nodes, n_elems, p, rank, nranks, plan), XFK_ERR_ARG,
+                "bad partition: rank / size out of range or fewer nodes than ranks");
+    info->rank = rank;
+    info->nranks = nranks;
+    info->n_global = n_nodes;
+    info->row0 = plan.row0;
+    info->n_own = plan.n_own;
+    info->n_halo = plan.n_halo;
+    info->n_elems = (int)plan.elems.size();
+    info->n_send = (int)plan.halo.send.size();
+    info->n_recv = (int)plan.halo.recv.size();
+    if (l2g) std::copy(plan.l2g.begin(), plan.l2g.end(), l2g);
+    if (elems) std::copy(plan.elems.begin(), plan.elems.end(), elems);
+    auto put = [](const std::vector<HaloRange> &v, int *o) {
+        for (size_t k = 0; k < v.size(); ++k) {
+            o[4 * k] = v[k].peer;
+            o[4 * k + 1] = v[k].off;
+            o[4 * k + 2] = v[k].len;
+            o[4 * k + 3] = v[k].g0;
+        }
+    };
+    if (recv) put(plan.halo.recv, recv);
+    if (send) put(plan.halo.send, send);
+    return XFK_OK;
+}
+
+int xfk_problem_create_dist(const xfk_problem_desc *d, int device, xfk_comm *comm, xfk_problem **out)
+{
+    XFK_REQUIRE(d && out && comm, XFK_ERR_ARG, "null argument");
+    *out = nullptr;
+    int rc = validate_desc(d);
+    if (rc == XFK_OK) rc = check_device(device);
+    if (rc != XFK_OK) return rc;
+    XFK_REQUIRE(d->n_pbc == 0, XFK_ERR_UNSUPPORTED, "periodic boundaries are not supported in the sharded solve");
+    PartPlan plan;
+    XFK_REQUIRE(plan_partition(d->n_nodes, d->n_elems, d->p, comm->rank, comm->size, plan), XFK_ERR_ARG,
+                "bad partition: fewer nodes than ranks");
+    GlobalPrep G;
+    prepare_global(d, G);
+    return build_local(d, G, &plan, device, comm, out);
+}
+
+int xfk_dist_get_info(const xfk_problem *P, xfk_dist_info *info)
+{
+    XFK_REQUIRE(P && info, XFK_ERR_ARG, "null argument");
+    info->rank = P->rank;
+    info->nranks = P->nranks;
+    info->n_global = P->N_global;
+    info->row0 = P->row0;
+    info->n_own = P->N;
+    info->n_halo = P->NL - P->N;
+    info->n_elems = P->NE;
+    info->n_send = (int)P->halo.send.size();
+    info->n_recv = (int)P->halo.recv.size();
     return XFK_OK;
 }
 
@@ -887,13 +1093,14 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     R.ms_symbolic = ms;
 
     const int N = P->N;
-    XFK_CHECK(hipMemsetAsync(P->V.p, 0, sizeof(double) * N, s));   // CBigLinProb::Create: V = 0
+    XFK_CHECK(hipMemsetAsync(P->V.p, 0, sizeof(double) * P->NL, s));   // CBigLinProb::Create: V = 0
     double Relax = P->relax, resn = 0, lastres = 0;
     int Iter = 0;
     bool LinearFlag = !P->any_nonlinear;
     const long long cap = std::max<long long>(100000, 20LL * N);
     for (;;) {
         XFK_CHECK(hipEventRecord(e0, s));
+        if (Iter > 0 && (rc = exchange(P, P->V.p)) != XFK_OK) return rc;   // halo of V for the element B
         rc = assemble(P, Iter);
         if (rc != XFK_OK) return rc;
         XFK_CHECK(hipMemcpyAsync(P->Vold.p, P->V.p, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
@@ -911,7 +1118,14 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
 
         if (!LinearFlag) {
             launch_newton_res(s, N, P->V.p, P->Vold.p, P->partials.p, P->counters.p + 3, P->nws.p);
-            XFK_CHECK(hipMemcpyAsync(P->nws_host, P->nws.p, sizeof(NewtonScalars), hipMemcpyDeviceToHost, s));
+            const double *nws_src = reinterpret_cast<const double *>(P->nws.p);
+            if (P->comm) {
+                XFK_CHECK(P->nws_glob.alloc(4));
+                rc = P->comm->allreduce_sum(nws_src, P->nws_glob.p, 2, s);
+                if (rc != XFK_OK) return rc;
+                nws_src = P->nws_glob.p;
+            }
+            XFK_CHECK(hipMemcpyAsync(P->nws_host, nws_src, sizeof(NewtonScalars), hipMemcpyDeviceToHost, s));
             XFK_CHECK(hipStreamSynchronize(s));
             const double x = P->nws_host->dx2, y = P->nws_host->v2;
             if (y == 0) LinearFlag = true;
@@ -962,9 +1176,29 @@ int xfk_get_solution(xfk_problem *P, double *A)
     XFK_REQUIRE(P && A, XFK_ERR_ARG, "null argument");
     XFK_REQUIRE(P->symbolic_ready, XFK_ERR_ARG, "no solution yet");
     XFK_CHECK(hipSetDevice(P->device));
-    XFK_CHECK(hipMemcpyAsync(A, P->V.p, sizeof(double) * P->N, hipMemcpyDeviceToHost, P->stream));
-    XFK_CHECK(hipStreamSynchronize(P->stream));
-    for (int i = 0; i < P->N; ++i) A[i] = A[i] * kC;   // L.b[i] = L.V[i]*c (static2d.cpp:1018-1021)
+    hipStream_t s = P->stream;
+    if (!P->comm) {
+        XFK_CHECK(d2h(A, P->V.p, sizeof(double) * P->N, s));
+        for (int i = 0; i < P->N; ++i) A[i] = A[i] * kC;   // L.b[i] = L.V[i]*c (static2d.cpp:1018-1021)
+        return XFK_OK;
+    }
+    // sharded: all-gather the owned rows (padded to the largest block)
+    const int R = P->nranks;
+    size_t maxn = 0;
+    for (int q = 0; q < R; ++q)
+        maxn = std::max<size_t>(maxn, row_begin(P->N_global, q + 1, R) - row_begin(P->N_global, q, R));
+    XFK_CHECK(P->gather_buf.alloc(maxn * (1 + R)));
+    double *send = P->gather_buf.p, *recv = P->gather_buf.p + maxn;
+    XFK_CHECK(hipMemsetAsync(send, 0, sizeof(double) * maxn, s));
+    XFK_CHECK(hipMemcpyAsync(send, P->V.p, sizeof(double) * P->N, hipMemcpyDeviceToDevice, s));
+    int rc = P->comm->allgather(send, recv, maxn, s);
+    if (rc != XFK_OK) return rc;
+    std::vector<double> h(maxn * R);
+    XFK_CHECK(d2h(h.data(), recv, sizeof(double) * h.size(), s));
+    for (int q = 0; q < R; ++q) {
+        const long long r0 = row_begin(P->N_global, q, R), r1 = row_begin(P->N_global, q + 1, R);
+        for (long long i = r0; i < r1; ++i) A[i] = h[(size_t)q * maxn + (i - r0)] * kC;
+    }
     return XFK_OK;
 }
 
@@ -1016,6 +1250,7 @@ int xfk_pcg_solve_csr(int n, const int *rowptr, const int *col, const double *va
     xfk_problem *P = new xfk_problem();
     P->device = device;
     P->N = n;
+    P->NL = n;
     P->nnz = rowptr[n];
     P->precision = precision;
     int rc = XFK_OK;

@@ -329,11 +329,11 @@ __device__ __forceinline__ int find_slot(const int *__restrict__ rowptr, const i
 }
 
 // slot[9 i + 3 j + k] = CSR position of (n_j, n_k) of the element at colour
-// position i.  Threads walk the elements in their raw (mesh, spatially
+// position i (-1 for the rows of halo nodes, which a sharded rank does not own).  Threads walk the elements in their raw (mesh, spatially
 // coherent) order so that the row gathers hit in cache, one linear scan per
 // row (independent loads; rows are short), and scatter the 9 slots to the
 // element's colour position.
-__global__ void k_build_slots(int NE, const int *__restrict__ p, const int *__restrict__ iperm,
+__global__ void k_build_slots(int NE, int nrows, const int *__restrict__ p, const int *__restrict__ iperm,
                               const int *__restrict__ rowptr, const int *__restrict__ col, int *__restrict__ slot,
                               int *__restrict__ bad)
 {
@@ -345,6 +345,11 @@ __global__ void k_build_slots(int NE, const int *__restrict__ p, const int *__re
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         int s[3] = {-1, -1, -1};
+        if (n[j] >= nrows) {          // halo row of a sharded problem: not assembled here
+#pragma unroll
+            for (int q = 0; q < 3; ++q) dst[3 * j + q] = -1;
+            continue;
+        }
         const int k1 = rowptr[n[j] + 1];
         for (int k = rowptr[n[j]]; k < k1; ++k) {
             const int c = col[k];
@@ -580,10 +585,12 @@ __global__ void __launch_bounds__(kBlock) k_assemble_color(int begin, int end, A
             be[j] += Mn[j][k] * Vn[k];
         }
 
-    // colour-exclusive scatter: no other element of this launch touches n[*]
+    // colour-exclusive scatter: no other element of this launch touches n[*];
+    // rows of halo nodes (slot -1) belong to another rank
     const int *sl = &s_slot[li * 9 + (li >> 3)];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
+        if (sl[3 * j] < 0) continue;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const double m = (k >= j) ? Me[j][k] : Me[k][j];   // upper value, exact symmetry
@@ -770,10 +777,10 @@ void launch_build_erec(hipStream_t s, int NE, const int *perm, const int *p, con
 {
     if (NE) k_build_erec<<<nblk(NE), kBlock, 0, s>>>(NE, perm, p, lbl, ebits_raw, erec, ebits, iperm);
 }
-void launch_build_slots(hipStream_t s, int NE, const int *p, const int *iperm, const int *rowptr, const int *col,
-                        int *slot, int *bad)
+void launch_build_slots(hipStream_t s, int NE, int nrows, const int *p, const int *iperm, const int *rowptr,
+                        const int *col, int *slot, int *bad)
 {
-    if (NE) k_build_slots<<<nblk(NE), kBlock, 0, s>>>(NE, p, iperm, rowptr, col, slot, bad);
+    if (NE) k_build_slots<<<nblk(NE), kBlock, 0, s>>>(NE, nrows, p, iperm, rowptr, col, slot, bad);
 }
 void launch_lookup_slots(hipStream_t s, int n, const int *rc, const int *rowptr, const int *col, int *out)
 {

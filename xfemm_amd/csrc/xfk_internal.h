@@ -23,6 +23,9 @@
 #include <vector>
 
 #include "../../include/xfemm_kernels.h"
+#include "xfk_partition.h"
+
+struct xfk_comm;
 
 namespace xfk {
 
@@ -40,6 +43,14 @@ constexpr double kC = kPI * 4.e-05;  // static2d.cpp:66
             ::xfk::set_error(std::string(#call) + ": " + hipGetErrorString(_e)); \
             return XFK_ERR_HIP;                                                  \
         }                                                                        \
+    } while (0)
+
+#define XFK_REQUIRE(cond, code, msg)  \
+    do {                              \
+        if (!(cond)) {                \
+            ::xfk::set_error(msg);    \
+            return code;              \
+        }                             \
     } while (0)
 
 void set_error(const std::string &msg);
@@ -134,19 +145,23 @@ struct xfk_problem {
     int device = 0;
     hipStream_t stream = nullptr;
 
-    // sizes
-    int N = 0, NE = 0;
+    // sizes: N owned rows (= all nodes unless sharded), NL local nodes
+    // (owned rows first, then the halo), NE local elements
+    int N = 0, NL = 0, NE = 0;
     long long nnz = 0;
     int ncolors = 0;
     std::vector<int> color_off;      // ncolors + 1 (host)
 
-    // host copies kept for host-side setup (BC maps)
-    std::vector<double> hx, hy;
-    std::vector<int> hp, he, hlbl, hmarker, hpbc;
-    std::vector<xfk_line_desc> hlines;
-    std::vector<xfk_point_desc> hpoints;
-    std::vector<xfk_block_desc> hblocks;
-    std::vector<xfk_label_desc> hlabels;
+    // sharded solve (xfk_problem_create_dist); comm == nullptr otherwise
+    xfk_comm *comm = nullptr;
+    int rank = 0, nranks = 1;
+    int N_global = 0, row0 = 0;
+    std::vector<int> l2g;            // local node -> global node
+    xfk::HaloPlan halo;              // slices of the node vectors exchanged with peers
+    int Gpart = 0;                   // length of each per-block partial array (agreed by all ranks)
+
+    // host copies kept for host-side setup (periodic maps)
+    std::vector<int> hp, hpbc;
     int length_units = 0, coords = 0;
     double precision = 1e-8, relax = 1.0;
     bool any_nonlinear = false;
@@ -206,11 +221,18 @@ struct xfk_problem {
     std::vector<std::vector<std::pair<int, double>>> pbc_b_terms;
     std::vector<int> pbc_b_key;
 
-    // numeric
+    // numeric: V (the PCG iterate x) and U (= M^-1 r) span the NL local
+    // nodes, their halo slices filled by exchanges; the rest span N rows
     xfk::DBuf<double> val, b, V, Vold, P, dinv;
-    xfk::DBuf<double> R2, W2, Z2;     // double-buffered PCG vectors (2N each)
-    xfk::DBuf<double> part_cg;        // 2 parities x 2 values x G
-    xfk::DBuf<double> part_reso;      // 2 x G
+    xfk::DBuf<double> R2, W2, Z2;     // r; w = A u; z (N) followed by u (NL)
+    // per-block partials of the PCG inner products, 4 arrays of Gpart:
+    // gamma (2 parities), delta, (M^-1 b).b.  part_loc is written by the
+    // kernels; part_glob is what they read: the sum over ranks when sharded
+    // (all-reduce), the same memory as part_loc otherwise
+    xfk::DBuf<double> part_loc, part_glob_buf;
+    double *part_glob = nullptr;
+    xfk::DBuf<double> nws_glob;       // all-reduced Newton sums (sharded)
+    xfk::DBuf<double> gather_buf;     // solution all-gather (sharded)
     xfk::DBuf<double> partials;       // kRedGrid * 2 (Newton residual)
     xfk::DBuf<unsigned> counters;     // ticket counters
     xfk::DBuf<xfk::CgState> pcg;

@@ -38,9 +38,11 @@ struct CgAxpyArgs {
 
 int cg_grid(int N);
 int cg_axpy_grid(int N);
-void launch_cg_init(hipStream_t s, int N, int flag, const int *rowptr, const int *col, const double *val,
-                    const double *b, double *V, double *R, double *U, double *Z, double *P, double *W,
-                    const double *dinv, double *part_reso, double *part_gam0, double *part_del);
+// r0 = b - A x0 (x0 = V when flag, else 0), u0 = M^-1 r0, z = p = 0; partials of
+// (M^-1 b).b and gamma_0 (w0 = A u0 follows with launch_cg_spmv, S = nullptr)
+void launch_cg_init_r(hipStream_t s, int N, int flag, const int *rowptr, const int *col, const double *val,
+                      const double *b, double *V, double *R, double *U, double *Z, double *P, const double *dinv,
+                      double *part_reso, double *part_gam0);
 void launch_cg_axpy(hipStream_t s, const CgAxpyArgs &A);
 void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *U,
                     double *W, double *part_del, const CgState *S);
@@ -61,8 +63,8 @@ void launch_color_hist(hipStream_t s, int NE, const int *color, int *hist, int m
 void launch_iota(hipStream_t s, int n, int *a);
 void launch_build_erec(hipStream_t s, int NE, const int *perm, const int *p, const int *lbl, const int *ebits_raw,
                        int4 *erec, int *ebits, int *iperm);
-void launch_build_slots(hipStream_t s, int NE, const int *p, const int *iperm, const int *rowptr, const int *col,
-                        int *slot, int *bad);
+void launch_build_slots(hipStream_t s, int NE, int nrows, const int *p, const int *iperm, const int *rowptr,
+                        const int *col, int *slot, int *bad);
 void launch_lookup_slots(hipStream_t s, int n, const int *rc, const int *rowptr, const int *col, int *out);
 void launch_mark_fix_adj(hipStream_t s, int N, const int *rowptr, const int *col, const unsigned char *fixed,
                          int *flag);

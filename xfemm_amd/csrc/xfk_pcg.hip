@@ -259,13 +259,12 @@ int cg_axpy_grid(int N)
     return g < 1 ? 1 : (g < kAxGrid ? g : kAxGrid);
 }
 
-void launch_cg_init(hipStream_t s, int N, int flag, const int *rowptr, const int *col, const double *val,
-                    const double *b, double *V, double *R, double *U, double *Z, double *P, double *W,
-                    const double *dinv, double *part_reso, double *part_gam0, double *part_del)
+void launch_cg_init_r(hipStream_t s, int N, int flag, const int *rowptr, const int *col, const double *val,
+                      const double *b, double *V, double *R, double *U, double *Z, double *P, const double *dinv,
+                      double *part_reso, double *part_gam0)
 {
-    const int G = cg_grid(N);
-    k_cg_init_r<<<G, kCgBlock, 0, s>>>(N, flag, rowptr, col, val, b, V, R, U, Z, P, dinv, part_reso, part_gam0);
-    k_cg_spmv<<<G, kCgBlock, 0, s>>>(N, rowptr, col, val, U, W, part_del, nullptr);
+    k_cg_init_r<<<cg_grid(N), kCgBlock, 0, s>>>(N, flag, rowptr, col, val, b, V, R, U, Z, P, dinv, part_reso,
+                                                part_gam0);
 }
 
 void launch_cg_axpy(hipStream_t s, const CgAxpyArgs &A)

@@ -28,6 +28,8 @@ EXPORTED = (
     "xfk_last_error", "xfk_device_count", "xfk_problem_create", "xfk_problem_destroy",
     "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz",
     "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_time",
+    "xfk_comm_unique_id", "xfk_comm_create_rccl", "xfk_comm_create_local", "xfk_comm_destroy",
+    "xfk_comm_rank", "xfk_comm_size", "xfk_partition_plan", "xfk_problem_create_dist", "xfk_dist_get_info",
 )
 
 
@@ -81,6 +83,15 @@ class Result(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class DistInfo(C.Structure):
+    _fields_ = [("rank", C.c_int), ("nranks", C.c_int), ("n_global", C.c_int), ("row0", C.c_int),
+                ("n_own", C.c_int), ("n_halo", C.c_int), ("n_elems", C.c_int), ("n_send", C.c_int),
+                ("n_recv", C.c_int)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 _lib = None
 
 
@@ -110,6 +121,17 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_pcg_solve_csr.argtypes = [C.c_int, iptr, iptr, dptr, dptr, dptr, C.c_int, C.c_double, C.c_int,
                                     C.POINTER(C.c_longlong), dptr]
     L.xfk_pcg_time.argtypes = [C.c_void_p, C.c_int, dptr, dptr]
+    vp = C.c_void_p
+    L.xfk_comm_unique_id.argtypes = [C.c_char_p, C.c_int]
+    L.xfk_comm_create_rccl.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
+    L.xfk_comm_create_local.argtypes = [C.c_int, C.POINTER(vp)]
+    L.xfk_comm_destroy.argtypes = [vp]
+    L.xfk_comm_rank.argtypes = [vp]
+    L.xfk_comm_size.argtypes = [vp]
+    L.xfk_partition_plan.argtypes = [C.c_int, C.c_int, iptr, C.c_int, C.c_int, C.POINTER(DistInfo),
+                                     iptr, iptr, iptr, iptr]
+    L.xfk_problem_create_dist.argtypes = [C.POINTER(ProblemDesc), C.c_int, vp, C.POINTER(vp)]
+    L.xfk_dist_get_info.argtypes = [vp, C.POINTER(DistInfo)]
     _lib = L
     return L
 
@@ -144,7 +166,9 @@ class Static2DProblem:
     def __init__(self, *, x, y, p, lbl, blocks: Sequence[dict], labels: Sequence[dict],
                  lines: Sequence[dict] = (), points: Sequence[dict] = (), circuits: Sequence[dict] = (),
                  marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0,
-                 device=0):
+                 device=0, comm: Optional["Comm"] = None):
+        """comm: shard the mesh by row blocks over this communicator (every rank
+        passes the same global problem; solve() and solution() are collective)."""
         L = load_library()
         keep = _Keep()
         nb = max(1, len(blocks))
@@ -198,9 +222,19 @@ class Static2DProblem:
         D.precision, D.length_units, D.coords, D.relax = precision, length_units, coords, relax
         self.n_circs = len(circuits)
         h = C.c_void_p()
-        _check(L.xfk_problem_create(C.byref(D), device, C.byref(h)))
+        self.comm = comm
+        if comm is None:
+            _check(L.xfk_problem_create(C.byref(D), device, C.byref(h)))
+        else:
+            _check(L.xfk_problem_create_dist(C.byref(D), device, comm._h, C.byref(h)))
         self._h = h
+        self.n_rows = self.dist_info()["n_own"] if comm is not None else self.n_nodes
         self.result: Optional[Result] = None
+
+    def dist_info(self) -> dict:
+        info = DistInfo()
+        _check(_lib.xfk_dist_get_info(self._h, C.byref(info)))
+        return info.as_dict()
 
     def close(self):
         if getattr(self, "_h", None):
@@ -235,11 +269,12 @@ class Static2DProblem:
         return cc[:n], J[:n], dV[:n]
 
     def csr(self):
+        """This rank's rows (all rows unless sharded; sharded columns are local ids)."""
         nnz = _lib.xfk_get_nnz(self._h)
-        rp = np.zeros(self.n_nodes + 1, np.int32)
+        rp = np.zeros(self.n_rows + 1, np.int32)
         col = np.zeros(nnz, np.int32)
         val = np.zeros(nnz)
-        b = np.zeros(self.n_nodes)
+        b = np.zeros(self.n_rows)
         _check(_lib.xfk_get_csr(self._h, rp.ctypes.data_as(iptr), col.ctypes.data_as(iptr),
                                 val.ctypes.data_as(dptr), b.ctypes.data_as(dptr)))
         return rp, col, val, b
@@ -266,3 +301,65 @@ def pcg_solve_csr(rowptr, col, val, b, V0=None, flag=0, precision=1e-8, device=0
                                bb.ctypes.data_as(dptr), V.ctypes.data_as(dptr), flag, precision, device,
                                C.byref(it), C.byref(er)))
     return V, it.value, er.value
+
+
+class Comm:
+    """Communicator of the sharded solve (xfk_comm): RCCL, one process per GPU,
+    or an in-process group of ranks driven by one host thread each."""
+
+    def __init__(self, handle):
+        self._h = handle
+        L = load_library()
+        self.rank = L.xfk_comm_rank(handle)
+        self.size = L.xfk_comm_size(handle)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        _check(load_library().xfk_comm_unique_id(buf, 128))
+        return buf.raw
+
+    @classmethod
+    def rccl(cls, unique_id: bytes, rank: int, size: int, device: int) -> "Comm":
+        h = C.c_void_p()
+        _check(load_library().xfk_comm_create_rccl(unique_id, len(unique_id), rank, size, device, C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def local_group(cls, size: int) -> list:
+        hs = (C.c_void_p * size)()
+        _check(load_library().xfk_comm_create_local(size, hs))
+        return [cls(C.c_void_p(hs[q])) for q in range(size)]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().xfk_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def partition_plan(n_nodes: int, p, rank: int, nranks: int) -> dict:
+    """Host-only row-block partition plan of xfk_problem_create_dist (no device)."""
+    L = load_library()
+    p = np.ascontiguousarray(np.asarray(p, dtype=np.int32).reshape(-1))
+    ne = len(p) // 3
+    info = DistInfo()
+    pp = p.ctypes.data_as(iptr)
+    _check(L.xfk_partition_plan(n_nodes, ne, pp, rank, nranks, C.byref(info), None, None, None, None))
+    l2g = np.zeros(info.n_own + info.n_halo, np.int32)
+    elems = np.zeros(max(1, info.n_elems), np.int32)
+    recv = np.zeros(4 * max(1, info.n_recv), np.int32)
+    send = np.zeros(4 * max(1, info.n_send), np.int32)
+    _check(L.xfk_partition_plan(n_nodes, ne, pp, rank, nranks, C.byref(info), l2g.ctypes.data_as(iptr),
+                                elems.ctypes.data_as(iptr), recv.ctypes.data_as(iptr), send.ctypes.data_as(iptr)))
+    d = info.as_dict()
+    d["l2g"] = l2g
+    d["elems"] = elems[:info.n_elems]
+    d["recv"] = recv[:4 * info.n_recv].reshape(-1, 4)   # peer, local offset, length, first global row
+    d["send"] = send[:4 * info.n_send].reshape(-1, 4)
+    return d
