@@ -10,10 +10,17 @@ N = 1 workload: BASELINE configs[2], synthetic 2M-triangle square-domain
 magnetostatic problem with linear mu (1000 x 1000 cells -> 2,000,000
 triangles, 1,002,001 nodes), synthetic data.
 
-N > 1 (one process per GPU, torchrun): every rank solves its own instance of
-the same problem (an independent-problem sweep, e.g. rotor positions): no
-data-path collective, "scaling": "weak".  The host barrier / max-over-ranks
-uses torch.distributed (gloo) on scalars only.
+N > 1 (one process per GPU, torchrun), default --mode sharded: BASELINE
+configs[4], ONE synthetic 20M-triangle mesh (3162 x 3162 cells, 10.0M DoF)
+split in row blocks over the N ranks (xfk_problem_create_dist): each rank
+assembles its rows, the PCG exchanges halo slices (RCCL send/recv) before
+every SpMV and all-reduces its inner-product partials once per iteration
+(RCCL all-reduce over xGMI).  "scaling": "strong" (the mesh is fixed).  After
+the timed region rank 0 solves the same mesh alone on its GPU, so the line
+carries the measured same-mesh speedup.  --mode replicas instead solves one
+independent 2M-tri problem per GPU (parameter sweep; no collective, "weak").
+The host barrier / max-over-ranks and the RCCL unique-id broadcast use
+torch.distributed (gloo) on scalars only.
 
 Output: one JSON line (rank 0) with roofline (SpMV kernel, HIP-event timing
 inside the timed region) and cpu_baseline (reference spars.cpp via oracle/_ref,
@@ -45,6 +52,20 @@ def spmv_bytes(n_rows, nnz):
     return 12 * nnz + 4 * (n_rows + 1) + 16 * n_rows
 
 
+class stdout_to_stderr:
+    """fd-level redirect: native code printing to stdout (the reference's
+    PCGSolve printf, RCCL's init banner) must not mix into the JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def cpu_baseline(n_cells, nonlinear):
     """Reference CPU solver on a bounded sample of the same workload family:
     the reference's own CBigLinProb (spars.cpp: linked-list matrix, SSOR-PCG,
@@ -57,17 +78,10 @@ def cpu_baseline(n_cells, nonlinear):
     kind = "reference" if oracle.ref_available() else "port"
     kw = synth.magnetostatic(n_cells, nonlinear=nonlinear)
     pr, mesh, _ = synth_to_oracle(kw)
-    # the reference's PCGSolve printf()s to stdout: keep stdout for the JSON line
-    sys.stdout.flush()
-    saved = os.dup(1)
-    os.dup2(2, 1)
-    try:
+    with stdout_to_stderr():
         t0 = time.perf_counter()
         _, st, _ = oracle.solve(pr, mesh, "reference" if kind == "reference" else "oracle")
         dt = time.perf_counter() - t0
-    finally:
-        os.dup2(saved, 1)
-        os.close(saved)
     dof = len(mesh.x)
     return {
         "value": dof / dt,
@@ -92,6 +106,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per SpMV launch from a PMC pass (profiles/), if measured")
+    ap.add_argument("--mode", choices=["sharded", "replicas"], default="sharded",
+                    help="N > 1: shard one configs[4] mesh (default) or solve one problem per GPU")
+    ap.add_argument("--shard-cells", type=int, default=3162,
+                    help="cells per side of the sharded mesh (3162 -> 20M triangles, configs[4])")
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="run the RCCL sharded path even at N = 1 (plumbing check)")
+    ap.add_argument("--no-same-mesh-1gpu", action="store_true",
+                    help="skip rank 0's single-GPU solve of the sharded mesh")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -101,11 +123,27 @@ def main():
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         dist.init_process_group("gloo")
+    sharded = (world > 1 and args.mode == "sharded") or args.force_sharded
 
     from xfemm_amd import kernels, synth
-    kw = synth.magnetostatic(args.cells, nonlinear=args.nonlinear)
-    P = kernels.Static2DProblem(device=local, **kw)
-    n_dof = P.n_nodes
+    comm = None
+    if sharded:
+        cells = args.shard_cells if world > 1 else args.cells
+        kw = synth.magnetostatic(cells, nonlinear=args.nonlinear)
+        uid = kernels.Comm.unique_id() if rank == 0 else None
+        if dist is not None:
+            box = [uid]
+            dist.broadcast_object_list(box, src=0)
+            uid = box[0]
+        with stdout_to_stderr():
+            comm = kernels.Comm.rccl(uid, rank, world, local)
+        P = kernels.Static2DProblem(device=local, comm=comm, **kw)
+        n_dof = P.n_nodes                       # global DoF of the sharded mesh
+    else:
+        cells = args.cells
+        kw = synth.magnetostatic(cells, nonlinear=args.nonlinear)
+        P = kernels.Static2DProblem(device=local, **kw)
+        n_dof = P.n_nodes
 
     def barrier():
         _hip_sync()
@@ -131,10 +169,28 @@ def main():
     spmv_ms = sum(r["spmv_ms_avg"] * r["spmv_samples"] for r in results) / max(
         1, sum(r["spmv_samples"] for r in results))
     nnz = results[-1]["nnz"]
-    algo = spmv_bytes(n_dof, nnz)
+    rows = P.n_rows
+    algo = spmv_bytes(rows, nnz)
     achieved = algo / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
     ms_step = 1e3 * elapsed / args.steps
-    value = world * n_dof * args.steps / elapsed
+    value = (1 if sharded else world) * n_dof * args.steps / elapsed
+    pcg_iters = results[-1]["cg_iters"]
+
+    same_mesh = None
+    if sharded and world > 1 and not args.no_same_mesh_1gpu:
+        # strong-scaling reference: rank 0 alone on the same mesh (after the timed region)
+        P.close()
+        if rank == 0:
+            Q = kernels.Static2DProblem(device=local, **kw)
+            Q.solve(rebuild_symbolic=True)
+            t1 = time.perf_counter()
+            r1 = Q.solve(rebuild_symbolic=True)
+            _hip_sync()
+            dt1 = time.perf_counter() - t1
+            Q.close()
+            same_mesh = {"one_gpu_dof_s": n_dof / dt1, "one_gpu_ms_per_step": 1e3 * dt1,
+                         "one_gpu_pcg_iters": r1["cg_iters"], "speedup": value / (n_dof / dt1)}
+        dist.barrier()
     out = {
         "metric": "solved DoF/s (assembly+CG to tol) on 2M-tri magnetostatic",
         "value": value,
@@ -144,25 +200,29 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if sharded else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
         "config": {
             "workload": "configs[%d]: synthetic %d-tri square-domain magnetostatic, %s, tol %g%s" % (
-                3 if args.nonlinear else 2, 2 * args.cells ** 2,
+                4 if sharded else (3 if args.nonlinear else 2), 2 * cells ** 2,
                 "nonlinear M-19 B-H (Newton)" if args.nonlinear else "linear mu",
-                kw["precision"], ", one independent problem per GPU" if world > 1 else ""),
-            "triangles": 2 * args.cells ** 2,
-            "dof_per_gpu": n_dof,
+                kw["precision"], (", row-block sharded over %d GPU(s), RCCL halo + all-reduce" % world)
+                if sharded else (", one independent problem per GPU" if world > 1 else "")),
+            "triangles": 2 * cells ** 2,
+            "dof_total": n_dof * (1 if sharded else world),
+            "dof_per_gpu": rows,
             "nnz": nnz,
-            "pcg_iters": results[-1]["cg_iters"],
+            "pcg_iters": pcg_iters,
+            "ms_per_pcg_iteration": results[-1]["ms_solve"] / max(1, pcg_iters),
             "newton_iters": results[-1]["newton_iters"],
             "preconditioner": "jacobi", "pcg": "Chronopoulos-Gear, 2 launches/iteration",
             "ms_symbolic": results[-1]["ms_symbolic"],
             "ms_assemble": results[-1]["ms_assemble"],
             "ms_solve": results[-1]["ms_solve"],
-            "parallelism": "independent problem per GPU (%d)" % world if world > 1 else "single GPU",
+            "parallelism": ("row-block shards x%d (RCCL)" % world) if sharded else (
+                "independent problem per GPU (%d)" % world if world > 1 else "single GPU"),
         },
         "roofline": {
             "bound": "hbm",
@@ -177,10 +237,15 @@ def main():
             "launches_sampled": sum(r["spmv_samples"] for r in results),
         },
     }
+    if same_mesh is not None:
+        out["config"]["same_mesh_1gpu"] = same_mesh
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_cells, args.nonlinear)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    P.close()
+    if comm is not None:
+        comm.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -139,3 +139,17 @@ def test_sharded_rejects_periodic_boundaries():
         kernels.Static2DProblem(**kw, comm=comms[0])
     for c in comms:
         c.close()
+
+
+def test_rccl_single_rank_is_bit_identical():
+    """The production transport (RCCL) with one rank: init, all-reduce, all-gather."""
+    kw = synth.magnetostatic(40)
+    r1, A1, _ = single(kw)
+    comm = kernels.Comm.rccl(kernels.Comm.unique_id(), 0, 1, 0)
+    P = kernels.Static2DProblem(**kw, comm=comm)
+    r = P.solve()
+    A = P.solution()
+    P.close()
+    comm.close()
+    assert r["cg_iters"] == r1["cg_iters"]
+    assert np.array_equal(A, A1)
