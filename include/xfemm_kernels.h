@@ -109,6 +109,10 @@ typedef struct {
     double spmv_ms_avg;         /* XFK_TIME_SPMV: mean HIP-event time of one SpMV launch */
     int spmv_samples;           /* launches sampled (every 16th PCG iteration) */
     int color_rounds;           /* Jones-Plassmann rounds of the element colouring */
+    int precond;                /* preconditioner of the last solve (XFK_PRECOND_*) */
+    int amg_levels;             /* AMG: levels of the last hierarchy */
+    double amg_op_complexity;   /* AMG: sum of level nonzeros / fine nonzeros */
+    double ms_amg_setup;        /* AMG: device time of the hierarchy setups, ms (inside ms_solve) */
 } xfk_result;
 
 typedef struct xfk_problem xfk_problem;
@@ -121,6 +125,23 @@ int xfk_problem_create(const xfk_problem_desc *desc, int device, xfk_problem **o
 void xfk_problem_destroy(xfk_problem *prob);
 
 enum { XFK_REBUILD_SYMBOLIC = 1, XFK_TIME_SPMV = 2 };
+
+/* Solver options.  The reference preconditions its PCG with a sequential
+ * SSOR sweep (spars.cpp:186-236, CBigLinProb::MultPC); the device offers
+ *   XFK_PRECOND_AMG    smoothed-aggregation AMG V-cycle (default; rebuilt for
+ *                      every matrix the Newton loop assembles; sharded solves
+ *                      use it as a rank-local block preconditioner)
+ *   XFK_PRECOND_JACOBI diag(A)
+ * Both keep the reference's stopping test sqrt(z.r / z0.b) <= Precision.
+ * A hierarchy whose SpGEMM rows overflow the LDS tables falls back to Jacobi
+ * for that solve (xfk_result.precond tells which one ran). */
+enum { XFK_PRECOND_JACOBI = 0, XFK_PRECOND_AMG = 1 };
+enum {
+    XFK_OPT_PRECOND = 1,        /* XFK_PRECOND_* */
+    XFK_OPT_AMG_SWEEPS = 2,     /* Jacobi sweeps before and after the coarse correction (1..8, default 2) */
+    XFK_OPT_AMG_THETA = 3       /* strength threshold (0..1, default 0.08) */
+};
+int xfk_set_option(xfk_problem *prob, int option, double value);
 
 /* FSolver::Static2D on the device.  flags: XFK_REBUILD_SYMBOLIC rebuilds the
  * CSR pattern, colouring and boundary maps (they are cached otherwise);
@@ -195,6 +216,10 @@ int xfk_get_stream(xfk_problem *prob, void **hip_stream);
 int xfk_pcg_solve_csr(int n, const int *rowptr, const int *col, const double *val,
                       const double *b, double *V, int flag, double precision,
                       int device, long long *iters, double *er);
+/* The same with a chosen preconditioner (XFK_PRECOND_*). */
+int xfk_pcg_solve_csr_pc(int n, const int *rowptr, const int *col, const double *val,
+                         const double *b, double *V, int flag, double precision,
+                         int device, int precond, long long *iters, double *er);
 
 /* Timing probe of the CG kernels (profiles / roofline): run `iters` PCG
  * iterations on the assembled system without a convergence stop; returns the

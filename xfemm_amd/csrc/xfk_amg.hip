@@ -1,0 +1,979 @@
+// Smoothed-aggregation AMG preconditioner for the fsolver PCG on MI355X
+// (gfx950).  Design and parameters: xfk_amg.h.  Replaces the reference's SSOR
+// preconditioner (cfemm/libfemm/spars.cpp:186-236, CBigLinProb::MultPC) on the
+// device; the PCG itself (and its stopping test, spars.cpp:259/313) is
+// unchanged.
+//
+// Every setup kernel is deterministic: decisions read only the previous
+// launch's state, floating-point sums run in a fixed order (the SpGEMM
+// accumulates each output entry in product-enumeration order), and atomics
+// are used only where the result does not depend on their order (set
+// membership, counts, max of non-negative values, positions that are sorted
+// afterwards).
+#include <hipcub/hipcub.hpp>
+
+#include <climits>
+#include <cmath>
+
+#include "xfk_amg.h"
+#include "xfk_spmv.h"
+
+namespace xfk {
+
+namespace {
+
+// --------------------------------------------------------------------------
+// small helpers
+// --------------------------------------------------------------------------
+
+constexpr int kB = 256;
+inline int nb(long long n) { return (int)((n + kB - 1) / kB); }
+
+constexpr unsigned long long kStIn = 2ull, kStUnd = 1ull;   // OUT = 0
+
+__device__ __forceinline__ unsigned mix32(unsigned x)
+{
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+// MIS key: (state:2 | hash(i):30 | i:32); max over a neighbourhood picks an
+// IN node first, then the undecided node with the largest (hash, index)
+__device__ __forceinline__ unsigned long long mis_key(unsigned long long st, int i)
+{
+    return (st << 62) | ((unsigned long long)(mix32((unsigned)i) & 0x3FFFFFFFu) << 32) | (unsigned)i;
+}
+__device__ __forceinline__ int key_idx(unsigned long long k) { return (int)(unsigned)(k & 0xFFFFFFFFull); }
+__device__ __forceinline__ unsigned long long key_st(unsigned long long k) { return k >> 62; }
+__device__ __forceinline__ unsigned long long key_low(unsigned long long k) { return k & ((1ull << 62) - 1); }
+
+__device__ __forceinline__ double rho_of(const unsigned long long *p)
+{
+    return __longlong_as_double((long long)*p);
+}
+
+// max of non-negative doubles over the wave, one atomic per wave (bit patterns
+// of non-negative doubles order like the values)
+__device__ __forceinline__ void wave_atomic_max(unsigned long long *dst, double v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    if ((threadIdx.x & 63) == 0 && v > 0.0) atomicMax(dst, (unsigned long long)__double_as_longlong(v));
+}
+
+// --------------------------------------------------------------------------
+// setup: diagonal, strength, Gershgorin bounds
+// --------------------------------------------------------------------------
+
+__global__ void k_amg_diag(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+                           const double *__restrict__ val, double *__restrict__ absd, double *__restrict__ dinv)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double d = 0.0;
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
+        if (col[k] == i) {
+            d = val[k];
+            break;
+        }
+    absd[i] = fabs(d);
+    dinv[i] = (d != 0.0) ? 1.0 / d : 0.0;
+}
+
+// strong flags per nonzero, strong degree per row, lumped filtered diagonal,
+// Gershgorin bounds of D^-1 A (rho[0]) and D_F^-1 A_F (rho[1])
+__global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double theta, const int *__restrict__ rowptr,
+                                                     const int *__restrict__ col, const double *__restrict__ val,
+                                                     const double *__restrict__ absd,
+                                                     unsigned char *__restrict__ sflag, int *__restrict__ sdeg,
+                                                     double *__restrict__ dfinv, unsigned long long *rho)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    double rA = 0.0, rF = 0.0;
+    if (i < n) {
+        const double ai = absd[i];
+        double aii = 0.0, lump = 0.0, sumS = 0.0, sumA = 0.0;
+        int deg = 0;
+        for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+            const int j = col[k];
+            const double a = val[k];
+            unsigned char f = 0;
+            if (j == i) {
+                aii = a;
+            } else if (j < ncl) {
+                sumA += fabs(a);
+                if (a != 0.0 && fabs(a) > theta * sqrt(ai * absd[j])) {
+                    f = 1;
+                    ++deg;
+                    sumS += fabs(a);
+                } else {
+                    lump += a;
+                }
+            }
+            sflag[k] = f;
+        }
+        const double dF = aii + lump;
+        dfinv[i] = (dF != 0.0) ? 1.0 / dF : 0.0;
+        sdeg[i] = deg;
+        if (aii != 0.0) rA = (fabs(aii) + sumA) / fabs(aii);
+        if (dF != 0.0) rF = (fabs(dF) + sumS) / fabs(dF);
+    }
+    wave_atomic_max(&rho[0], rA);
+    wave_atomic_max(&rho[1], rF);
+}
+
+// --------------------------------------------------------------------------
+// setup: MIS-2 aggregation
+// --------------------------------------------------------------------------
+
+__global__ void k_mis_init(int n, const int *__restrict__ sdeg, unsigned long long *__restrict__ key)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) key[i] = mis_key(sdeg[i] > 0 ? kStUnd : 0ull, i);
+}
+
+__global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+                          const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ in,
+                          unsigned long long *__restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    unsigned long long m = in[i];
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
+        if (sflag[k]) m = max(m, in[col[k]]);
+    out[i] = m;
+}
+
+// second max sweep fused with the state update: an undecided node whose
+// distance-2 maximum is itself joins the set; one that sees a set member
+// within distance 2 leaves
+__global__ void k_mis_update(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+                             const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ t1,
+                             unsigned long long *__restrict__ key, int *__restrict__ undecided)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long k = key[i];
+    if (key_st(k) != kStUnd) return;
+    unsigned long long m = t1[i];
+    for (int q = rowptr[i]; q < rowptr[i + 1]; ++q)
+        if (sflag[q]) m = max(m, t1[col[q]]);
+    if (key_idx(m) == i) key[i] = (kStIn << 62) | key_low(k);
+    else if (key_st(m) == kStIn) key[i] = key_low(k);
+    else *undecided = 1;   // benign race: every writer stores 1
+}
+
+__global__ void k_agg_roots(int n, const unsigned long long *__restrict__ key, int *__restrict__ flag)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = key_st(key[i]) == kStIn;
+}
+
+// distance 1: roots keep their aggregate, neighbours of roots join the root
+// with the largest key
+__global__ void k_agg_join1(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+                            const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ key,
+                            const int *__restrict__ rootid, int *__restrict__ agg1)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (key_st(key[i]) == kStIn) {
+        agg1[i] = rootid[i];
+        return;
+    }
+    int bj = -1;
+    unsigned long long best = 0;
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        if (!sflag[k]) continue;
+        const int j = col[k];
+        const unsigned long long kj = key[j];
+        if (key_st(kj) == kStIn && (bj < 0 || key_low(kj) > best)) {
+            best = key_low(kj);
+            bj = j;
+        }
+    }
+    agg1[i] = (bj >= 0) ? rootid[bj] : -1;
+}
+
+// distance 2: the rest join the aggregate of their largest-key neighbour
+// that joined at distance 1
+__global__ void k_agg_join2(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+                            const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ key,
+                            const int *__restrict__ agg1, int *__restrict__ agg)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int a = agg1[i];
+    if (a >= 0) {
+        agg[i] = a;
+        return;
+    }
+    int bj = -1;
+    unsigned long long best = 0;
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        if (!sflag[k]) continue;
+        const int j = col[k];
+        if (agg1[j] < 0) continue;
+        const unsigned long long kl = key_low(key[j]);
+        if (bj < 0 || kl > best) {
+            best = kl;
+            bj = j;
+        }
+    }
+    agg[i] = (bj >= 0) ? agg1[bj] : -1;   // -1: isolated (or unreachable) -> no coarse dof
+}
+
+// --------------------------------------------------------------------------
+// setup: smoothed prolongator P = (I - omega D_F^-1 A_F) P_tent
+// --------------------------------------------------------------------------
+
+// entry k of row i of (I - omega D_F^-1 A_F) restricted to aggregated columns
+struct PEnt {
+    const int *col;
+    const double *val;
+    const unsigned char *sflag;
+    const int *agg;
+    __device__ __forceinline__ bool get(int i, int k, double omega, double dfi, int &J, double &v) const
+    {
+        const int j = col[k];
+        if (j == i) {
+            J = agg[i];
+            v = 1.0 - omega;
+        } else if (sflag[k]) {
+            J = agg[j];
+            v = -omega * dfi * val[k];
+        } else {
+            return false;
+        }
+        return J >= 0;
+    }
+};
+
+__global__ void k_p_count(int n, const int *__restrict__ rowptr, PEnt E, int *__restrict__ cnt)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int s = rowptr[i], e = rowptr[i + 1];
+    int c = 0;
+    for (int k = s; k < e; ++k) {
+        int J;
+        double v;
+        if (!E.get(i, k, 0.0, 0.0, J, v)) continue;
+        bool dup = false;
+        for (int q = s; q < k && !dup; ++q) {
+            int J2;
+            double v2;
+            if (E.get(i, q, 0.0, 0.0, J2, v2) && J2 == J) dup = true;
+        }
+        c += !dup;
+    }
+    cnt[i] = c;
+}
+
+__global__ void k_p_fill(int n, const int *__restrict__ rowptr, PEnt E, const double *__restrict__ dfinv,
+                         const unsigned long long *rho, const int *__restrict__ prow, int *__restrict__ pcol,
+                         double *__restrict__ pval)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double rF = rho_of(rho + 1);
+    const double omega = rF > 0.0 ? (4.0 / 3.0) / rF : 0.0;
+    const double dfi = dfinv[i];
+    const int s = rowptr[i], e = rowptr[i + 1];
+    const int base = prow[i];
+    for (int k = s; k < e; ++k) {
+        int J;
+        double v;
+        if (!E.get(i, k, omega, dfi, J, v)) continue;
+        bool dup = false;
+        int rank = 0;
+        for (int q = s; q < e; ++q) {
+            int J2;
+            double v2;
+            if (!E.get(i, q, omega, dfi, J2, v2)) continue;
+            if (J2 == J && q < k) dup = true;
+            // distinct columns smaller than J, each counted at its first occurrence
+            if (J2 < J) {
+                bool first = true;
+                for (int t = s; t < q && first; ++t) {
+                    int J3;
+                    double v3;
+                    if (E.get(i, t, omega, dfi, J3, v3) && J3 == J2) first = false;
+                }
+                rank += first;
+            }
+        }
+        if (dup) continue;
+        double sum = 0.0;   // entries of the same aggregate, row order
+        for (int q = k; q < e; ++q) {
+            int J2;
+            double v2;
+            if (E.get(i, q, omega, dfi, J2, v2) && J2 == J) sum += v2;
+        }
+        pcol[base + rank] = J;
+        pval[base + rank] = sum;
+    }
+}
+
+// --------------------------------------------------------------------------
+// setup: R = P^T
+// --------------------------------------------------------------------------
+
+__global__ void k_rt_count(int n, const int *__restrict__ prow, const int *__restrict__ pcol, int *__restrict__ rcnt)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (int k = prow[i]; k < prow[i + 1]; ++k) atomicAdd(&rcnt[pcol[k]], 1);
+}
+
+__global__ void k_rt_fill(int n, const int *__restrict__ prow, const int *__restrict__ pcol,
+                          const int *__restrict__ rrow, int *__restrict__ cursor, int *__restrict__ rcol)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (int k = prow[i]; k < prow[i + 1]; ++k) {
+        const int J = pcol[k];
+        rcol[rrow[J] + atomicAdd(&cursor[J], 1)] = i;
+    }
+}
+
+// sort each R row (atomic fill order is arbitrary), then look the values up in P
+__global__ void k_rt_sort_vals(int nc, const int *__restrict__ rrow, int *__restrict__ rcol,
+                               const int *__restrict__ prow, const int *__restrict__ pcol,
+                               const double *__restrict__ pval, double *__restrict__ rval)
+{
+    const int J = blockIdx.x * blockDim.x + threadIdx.x;
+    if (J >= nc) return;
+    const int s = rrow[J], e = rrow[J + 1];
+    for (int a = s + 1; a < e; ++a) {
+        const int key = rcol[a];
+        int b = a - 1;
+        while (b >= s && rcol[b] > key) {
+            rcol[b + 1] = rcol[b];
+            --b;
+        }
+        rcol[b + 1] = key;
+    }
+    for (int a = s; a < e; ++a) {
+        const int i = rcol[a];
+        int lo = prow[i], hi = prow[i + 1] - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (pcol[mid] < J) lo = mid + 1;
+            else hi = mid;
+        }
+        rval[a] = pval[lo];
+    }
+}
+
+// --------------------------------------------------------------------------
+// setup: row-merge SpGEMM C = X Y, one wavefront per row
+// --------------------------------------------------------------------------
+//
+// Products of row r are enumerated in a fixed order (X entries in row order,
+// each Y row in column order), 64 at a time: a wave prefix sum of the Y-row
+// lengths of up to 64 X entries maps lane products to (X entry, Y position).
+// Pass COUNT inserts the output columns into an LDS hash set and returns the
+// row length; pass FILL inserts them again, ranks them (sorted columns) and
+// accumulates each product into its column in enumeration order: within a
+// group of 64 products, the first lane of each column sums the group's
+// products of that column in lane order, then adds the group sum to the LDS
+// accumulator -- the same operation order on every run.
+
+constexpr int kSgHash = 1024;      // hash slots per row (power of two)
+constexpr int kSgMax = 512;        // distinct output columns per row
+
+struct SgMat {
+    const int *rowptr, *col;
+    const double *val;
+};
+
+template <bool FILL>
+__global__ void __launch_bounds__(64) k_spgemm(int nrows, SgMat X, int xcol_lim, SgMat Y, int *__restrict__ cnt_out,
+                                               const int *__restrict__ crow, int *__restrict__ ccol,
+                                               double *__restrict__ cval, int *overflow)
+{
+    __shared__ int hk[kSgHash];
+    __shared__ int hr[FILL ? kSgHash : 1];
+    __shared__ int lst[FILL ? kSgMax : 1], lslot[FILL ? kSgMax : 1];
+    __shared__ double acc[FILL ? kSgMax : 1];
+    __shared__ int c_off[64], c_ys[64];
+    __shared__ double c_xv[64];
+    __shared__ int s_rank[64];
+    __shared__ double s_val[64];
+    __shared__ int s_cnt, s_ovf, s_m;
+
+    const int row = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (row >= nrows) return;
+    for (int t = lane; t < kSgHash; t += 64) hk[t] = -1;
+    if (lane == 0) {
+        s_cnt = 0;
+        s_ovf = 0;
+        s_m = 0;
+    }
+    __syncthreads();
+    const int xs = X.rowptr[row], xe = X.rowptr[row + 1];
+
+    auto insert = [&](int key) -> int {
+        unsigned h = ((unsigned)key * 2654435761u) >> (32 - 10);
+        for (int probe = 0; probe < kSgHash; ++probe) {
+            const int old = atomicCAS(&hk[h], -1, key);
+            if (old == -1) {
+                atomicAdd(&s_cnt, 1);
+                return (int)h;
+            }
+            if (old == key) return (int)h;
+            h = (h + 1) & (kSgHash - 1);
+        }
+        s_ovf = 1;
+        return -1;
+    };
+    auto lookup = [&](int key) -> int {
+        unsigned h = ((unsigned)key * 2654435761u) >> (32 - 10);
+        for (int probe = 0; probe < kSgHash; ++probe) {
+            const int k = hk[h];
+            if (k == key) return (int)h;
+            if (k == -1) return -1;
+            h = (h + 1) & (kSgHash - 1);
+        }
+        return -1;
+    };
+    // stage up to 64 X entries of [e0, xe); returns the group's product count
+    auto stage = [&](int e0) -> int {
+        const int e = e0 + lane;
+        int len = 0, ys = 0;
+        double xv = 0.0;
+        if (e < xe) {
+            const int k = X.col[e];
+            if (k < xcol_lim) {
+                ys = Y.rowptr[k];
+                len = Y.rowptr[k + 1] - ys;
+                xv = X.val ? X.val[e] : 0.0;
+            }
+        }
+        int incl = len;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += t;
+        }
+        const int total = __shfl(incl, 63, 64);
+        c_off[lane] = incl - len;
+        c_ys[lane] = ys;
+        c_xv[lane] = xv;
+        __syncthreads();
+        return total;
+    };
+    // product p of the staged group -> (column, value)
+    auto product = [&](int p, int &key, double &v) {
+        int lo = 0, hi = 63;   // largest entry with c_off <= p
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (c_off[mid] <= p) lo = mid;
+            else hi = mid - 1;
+        }
+        const int q = c_ys[lo] + (p - c_off[lo]);
+        key = Y.col[q];
+        if (FILL) v = c_xv[lo] * Y.val[q];
+    };
+
+    // pass 1: the set of output columns
+    for (int e0 = xs; e0 < xe; e0 += 64) {
+        const int total = stage(e0);
+        for (int p = lane; p < total; p += 64) {
+            int key;
+            double v;
+            product(p, key, v);
+            insert(key);
+        }
+        __syncthreads();
+    }
+    if (!FILL) {
+        if (lane == 0) {
+            cnt_out[row] = s_cnt;
+            if (s_ovf || s_cnt > kSgMax) atomicOr(overflow, 1);
+        }
+        return;
+    }
+    // rank the columns (sorted order) and map hash slot -> rank
+    for (int t = lane; t < kSgHash; t += 64)
+        if (hk[t] != -1) {
+            const int m = atomicAdd(&s_m, 1);
+            if (m < kSgMax) {
+                lst[m] = hk[t];
+                lslot[m] = t;
+            }
+        }
+    __syncthreads();
+    const int cnt = min(s_m, kSgMax);
+    const int cb = crow[row];
+    for (int m = lane; m < cnt; m += 64) {
+        const int key = lst[m];
+        int rank = 0;
+        for (int q = 0; q < cnt; ++q) rank += lst[q] < key;
+        hr[lslot[m]] = rank;
+        ccol[cb + rank] = key;
+        acc[rank] = 0.0;
+    }
+    __syncthreads();
+    // pass 2: values in enumeration order
+    for (int e0 = xs; e0 < xe; e0 += 64) {
+        const int total = stage(e0);
+        for (int p0 = 0; p0 < total; p0 += 64) {
+            const int p = p0 + lane;
+            int rank = -1;
+            double v = 0.0;
+            if (p < total) {
+                int key;
+                product(p, key, v);
+                const int h = lookup(key);
+                rank = (h >= 0) ? hr[h] : -1;
+            }
+            s_rank[lane] = rank;
+            s_val[lane] = v;
+            __syncthreads();
+            if (rank >= 0) {
+                const int m_end = min(64, total - p0);
+                bool leader = true;
+                double sum = 0.0;
+                for (int m = 0; m < m_end; ++m)
+                    if (s_rank[m] == rank) {
+                        if (m < lane) leader = false;
+                        sum += s_val[m];
+                    }
+                if (leader) acc[rank] += sum;
+            }
+            __syncthreads();
+        }
+    }
+    for (int m = lane; m < cnt; m += 64) cval[cb + m] = acc[m];
+}
+
+// --------------------------------------------------------------------------
+// setup: coarsest level, dense inverse
+// --------------------------------------------------------------------------
+
+__global__ void k_dense_scatter(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+                                const double *__restrict__ val, double *__restrict__ M)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (int j = 0; j < n; ++j) M[(size_t)i * n + j] = 0.0;
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
+        if (col[k] < n) M[(size_t)i * n + col[k]] += val[k];
+}
+
+// In-place Gauss-Jordan inversion without pivoting (the level operators are
+// symmetric positive semi-definite).  A pivot that vanishes relative to the
+// largest diagonal entry marks a null direction: its row and column are
+// zeroed, so the result is a generalised inverse on the range.
+__global__ void __launch_bounds__(1024) k_gauss_jordan(int n, double *__restrict__ M)
+{
+    __shared__ double rowk[kAmgDenseMax], colk[kAmgDenseMax];
+    __shared__ double s_maxd, s_piv;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        double m = 0.0;
+        for (int i = 0; i < n; ++i) m = fmax(m, fabs(M[(size_t)i * n + i]));
+        s_maxd = m;
+    }
+    __syncthreads();
+    for (int k = 0; k < n; ++k) {
+        if (tid == 0) s_piv = M[(size_t)k * n + k];
+        __syncthreads();
+        const double piv = s_piv;
+        if (!(fabs(piv) > 1e-13 * s_maxd)) {
+            for (int j = tid; j < n; j += blockDim.x) {
+                M[(size_t)k * n + j] = 0.0;
+                M[(size_t)j * n + k] = 0.0;
+            }
+            __syncthreads();
+            continue;
+        }
+        const double ip = 1.0 / piv;
+        for (int j = tid; j < n; j += blockDim.x) {
+            rowk[j] = (j == k ? 1.0 : M[(size_t)k * n + j]) * ip;
+            colk[j] = M[(size_t)j * n + k];
+        }
+        __syncthreads();
+        for (int idx = tid; idx < n * n; idx += blockDim.x) {
+            const int i = idx / n, j = idx - i * n;
+            if (i == k) M[idx] = rowk[j];
+            else M[idx] = (j == k ? 0.0 : M[idx]) - colk[i] * rowk[j];
+        }
+        __syncthreads();
+    }
+}
+
+// --------------------------------------------------------------------------
+// V-cycle kernels
+// --------------------------------------------------------------------------
+
+enum SmoothMode {
+    kSweepFromZero = 0,   // x1 = w D^-1 b implicit, out = x1 + w D^-1 (b - A x1)
+    kSweep = 1,           // out = x + w D^-1 (b - A x)
+    kResid = 2,           // r = b - A x
+    kResidFromZero = 3    // x1 = w D^-1 b (written to out), r = b - A x1
+};
+
+template <int MODE>
+__global__ void __launch_bounds__(kCgBlock) k_amg_smooth(int n, int ncl, const int *__restrict__ rowptr,
+                                                         const int *__restrict__ col, const double *__restrict__ val,
+                                                         const double *__restrict__ dinv,
+                                                         const unsigned long long *rho, const double *__restrict__ b,
+                                                         const double *__restrict__ x, double *__restrict__ out,
+                                                         double *__restrict__ rout, const int *done)
+{
+    if (done && *done) return;
+    __shared__ __attribute__((aligned(16))) double lds[kCgCap];
+    const double ra = rho_of(rho);
+    const double w = ra > 0.0 ? 1.0 / ra : 0.0;
+    const int r0 = blockIdx.x * kCgBlock;
+    constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
+    double ax;
+    if constexpr (implicit)
+        ax = cg_tile_spmv(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; }, lds);
+    else
+        ax = cg_tile_spmv(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; }, lds);
+    const int i = r0 + threadIdx.x;
+    if (i >= n) return;
+    const double bi = b[i], di = dinv[i];
+    const double xi = implicit ? w * di * bi : x[i];
+    const double res = bi - ax;
+    if constexpr (MODE == kSweepFromZero || MODE == kSweep) out[i] = xi + w * di * res;
+    if constexpr (MODE == kResid || MODE == kResidFromZero) rout[i] = res;
+    if constexpr (MODE == kResidFromZero) out[i] = xi;
+}
+
+__global__ void k_amg_restrict(int nc, const int *__restrict__ rrow, const int *__restrict__ rcol,
+                               const double *__restrict__ rval, const double *__restrict__ r, double *__restrict__ bc,
+                               const int *done)
+{
+    if (done && *done) return;
+    const int I = blockIdx.x * blockDim.x + threadIdx.x;
+    if (I >= nc) return;
+    double s = 0.0;
+    for (int k = rrow[I]; k < rrow[I + 1]; ++k) s += rval[k] * r[rcol[k]];
+    bc[I] = s;
+}
+
+__global__ void k_amg_prolong(int n, const int *__restrict__ prow, const int *__restrict__ pcol,
+                              const double *__restrict__ pval, const double *__restrict__ xc, double *__restrict__ x,
+                              const int *done)
+{
+    if (done && *done) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s = 0.0;
+    for (int k = prow[i]; k < prow[i + 1]; ++k) s += pval[k] * xc[pcol[k]];
+    x[i] += s;
+}
+
+// x = M b, one wavefront per row of the dense coarsest inverse
+__global__ void __launch_bounds__(256) k_dense_mv(int n, const double *__restrict__ M, const double *__restrict__ b,
+                                                  double *__restrict__ x, const int *done)
+{
+    if (done && *done) return;
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (i >= n) return;
+    double s = 0.0;
+    for (int j = lane; j < n; j += 64) s += M[(size_t)i * n + j] * b[j];
+    s = cg_wave_sum(s);
+    if (lane == 0) x[i] = s;
+}
+
+}  // namespace
+
+// --------------------------------------------------------------------------
+// host side
+// --------------------------------------------------------------------------
+
+Amg::~Amg()
+{
+    if (host_int) (void)hipHostFree(host_int);
+}
+
+#define AMG_CHECK(call)                                                          \
+    do {                                                                         \
+        hipError_t _e = (call);                                                  \
+        if (_e != hipSuccess) {                                                  \
+            ::xfk::set_error(std::string(#call) + ": " + hipGetErrorString(_e)); \
+            return XFK_ERR_HIP;                                                  \
+        }                                                                        \
+    } while (0)
+
+namespace {
+
+// out[0..n] = exclusive scan of in[0..n-1], out[n] = total; returns total
+int scan_total(Amg &A, hipStream_t s, const int *in, int *out, int n, long long &total)
+{
+    size_t bytes = 0;
+    AMG_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out + 1, n, s));
+    AMG_CHECK(A.cub_tmp.alloc(bytes ? bytes : 1));
+    AMG_CHECK(hipMemsetAsync(out, 0, sizeof(int), s));
+    if (n > 0) AMG_CHECK(hipcub::DeviceScan::InclusiveSum(A.cub_tmp.p, bytes, in, out + 1, n, s));
+    AMG_CHECK(hipMemcpyAsync(A.host_int, out + n, sizeof(int), hipMemcpyDeviceToHost, s));
+    AMG_CHECK(hipStreamSynchronize(s));
+    total = A.host_int[0];
+    return XFK_OK;
+}
+
+int read_flag(Amg &A, hipStream_t s, int idx, int &v)
+{
+    AMG_CHECK(hipMemcpyAsync(A.host_int + 1, A.dev_int.p + idx, sizeof(int), hipMemcpyDeviceToHost, s));
+    AMG_CHECK(hipStreamSynchronize(s));
+    v = A.host_int[1];
+    return XFK_OK;
+}
+
+}  // namespace
+
+int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *col0, const double *val0,
+               long long nnz0)
+{
+    if (!host_int) AMG_CHECK(hipHostMalloc((void **)&host_int, 4 * sizeof(int)));
+    AMG_CHECK(dev_int.alloc(4));
+    AMG_CHECK(rho.alloc(2 * kAmgMaxLevels));
+    AMG_CHECK(hipMemsetAsync(rho.p, 0, sizeof(unsigned long long) * 2 * kAmgMaxLevels, s));
+    if (L.empty()) L.emplace_back(new AmgLevel());
+    {
+        AmgLevel &F = *L[0];
+        F.n = n0;
+        F.nnz = nnz0;
+        F.ncol_lim = ncl0;
+        F.rowptr = rowptr0;
+        F.col = col0;
+        F.val = val0;
+    }
+    stats = AmgStats();
+    dense_coarse = false;
+    int l = 0;
+    for (;; ++l) {
+        AmgLevel &A = *L[l];
+        const int n = A.n;
+        stats.n[l] = n;
+        stats.nnz[l] = A.nnz;
+        AMG_CHECK(A.dinv.alloc(n));
+        AMG_CHECK(absd.alloc(n));
+        AMG_CHECK(dfinv.alloc(n));
+        AMG_CHECK(cnt.alloc((size_t)n + 1));
+        k_amg_diag<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
+        if (n <= kAmgDenseMax) {
+            dense_coarse = true;
+            break;
+        }
+        AMG_CHECK(sflag.alloc((size_t)A.nnz));
+        k_amg_strength<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
+                                            dfinv.p, rho.p + 2 * l);
+        if (l == kAmgMaxLevels - 1) break;   // smoother-only coarsest level
+        // MIS-2
+        AMG_CHECK(key.alloc(n));
+        AMG_CHECK(t1.alloc(n));
+        k_mis_init<<<nb(n), kB, 0, s>>>(n, cnt.p, key.p);
+        int rounds = 0;
+        for (;;) {
+            for (int b = 0; b < 4; ++b, ++rounds) {
+                AMG_CHECK(hipMemsetAsync(dev_int.p, 0, sizeof(int), s));
+                k_mis_max<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p);
+                k_mis_update<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, dev_int.p);
+            }
+            int und = 0;
+            int rc = read_flag(*this, s, 0, und);
+            if (rc != XFK_OK) return rc;
+            if (!und) break;
+            if (rounds > 4096) {
+                set_error("AMG: MIS-2 aggregation did not terminate");
+                return XFK_ERR_NOCONV;
+            }
+        }
+        stats.mis_rounds[l] = rounds;
+        AMG_CHECK(flag.alloc((size_t)n + 1));
+        AMG_CHECK(cursor.alloc((size_t)n + 1));
+        k_agg_roots<<<nb(n), kB, 0, s>>>(n, key.p, flag.p);
+        long long nc = 0;
+        int rc = scan_total(*this, s, flag.p, cursor.p, n, nc);   // cursor = root ids
+        if (rc != XFK_OK) return rc;
+        if (nc == 0 || nc > (long long)(0.9 * n)) break;   // no useful coarsening: smoother-only coarsest
+        AMG_CHECK(agg1.alloc(n));
+        AMG_CHECK(agg.alloc(n));
+        k_agg_join1<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, cursor.p, agg1.p);
+        k_agg_join2<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, agg1.p, agg.p);
+        // P
+        PEnt E{A.col, A.val, sflag.p, agg.p};
+        k_p_count<<<nb(n), kB, 0, s>>>(n, A.rowptr, E, cnt.p);
+        AMG_CHECK(A.prow.alloc((size_t)n + 1));
+        long long pnnz = 0;
+        if ((rc = scan_total(*this, s, cnt.p, A.prow.p, n, pnnz)) != XFK_OK) return rc;
+        A.nc = (int)nc;
+        A.pnnz = pnnz;
+        AMG_CHECK(A.pcol.alloc((size_t)std::max(1LL, pnnz)));
+        AMG_CHECK(A.pval.alloc((size_t)std::max(1LL, pnnz)));
+        k_p_fill<<<nb(n), kB, 0, s>>>(n, A.rowptr, E, dfinv.p, rho.p + 2 * l, A.prow.p, A.pcol.p, A.pval.p);
+        // R = P^T
+        AMG_CHECK(cnt.alloc((size_t)std::max<long long>(n, nc) + 1));
+        AMG_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * (nc + 1), s));
+        k_rt_count<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, cnt.p);
+        AMG_CHECK(A.rrow.alloc((size_t)nc + 1));
+        long long rnnz = 0;
+        if ((rc = scan_total(*this, s, cnt.p, A.rrow.p, (int)nc, rnnz)) != XFK_OK) return rc;
+        AMG_CHECK(A.rcol.alloc((size_t)std::max(1LL, rnnz)));
+        AMG_CHECK(A.rval.alloc((size_t)std::max(1LL, rnnz)));
+        AMG_CHECK(hipMemsetAsync(cursor.p, 0, sizeof(int) * (nc + 1), s));
+        k_rt_fill<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, A.rrow.p, cursor.p, A.rcol.p);
+        k_rt_sort_vals<<<nb(nc), kB, 0, s>>>((int)nc, A.rrow.p, A.rcol.p, A.prow.p, A.pcol.p, A.pval.p, A.rval.p);
+        // AP = A P
+        AMG_CHECK(hipMemsetAsync(dev_int.p + 2, 0, sizeof(int), s));
+        SgMat SA{A.rowptr, A.col, A.val}, SP{A.prow.p, A.pcol.p, A.pval.p};
+        k_spgemm<false><<<n, 64, 0, s>>>(n, SA, A.ncol_lim, SP, cnt.p, nullptr, nullptr, nullptr, dev_int.p + 2);
+        AMG_CHECK(ap_row.alloc((size_t)n + 1));
+        long long apnnz = 0;
+        if ((rc = scan_total(*this, s, cnt.p, ap_row.p, n, apnnz)) != XFK_OK) return rc;
+        int ovf = 0;
+        if ((rc = read_flag(*this, s, 2, ovf)) != XFK_OK) return rc;
+        if (ovf) {
+            set_error("AMG: a row of A*P exceeds the SpGEMM LDS capacity");
+            return XFK_ERR_UNSUPPORTED;
+        }
+        AMG_CHECK(ap_col.alloc((size_t)std::max(1LL, apnnz)));
+        AMG_CHECK(ap_val.alloc((size_t)std::max(1LL, apnnz)));
+        k_spgemm<true><<<n, 64, 0, s>>>(n, SA, A.ncol_lim, SP, nullptr, ap_row.p, ap_col.p, ap_val.p, dev_int.p + 2);
+        // A_c = R (A P)
+        if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
+        AmgLevel &C = *L[l + 1];
+        SgMat SR{A.rrow.p, A.rcol.p, A.rval.p}, SAP{ap_row.p, ap_col.p, ap_val.p};
+        k_spgemm<false><<<(int)nc, 64, 0, s>>>((int)nc, SR, INT_MAX, SAP, cnt.p, nullptr, nullptr, nullptr,
+                                               dev_int.p + 2);
+        AMG_CHECK(C.rowptr_o.alloc((size_t)nc + 1));
+        long long cnnz = 0;
+        if ((rc = scan_total(*this, s, cnt.p, C.rowptr_o.p, (int)nc, cnnz)) != XFK_OK) return rc;
+        if ((rc = read_flag(*this, s, 2, ovf)) != XFK_OK) return rc;
+        if (ovf) {
+            set_error("AMG: a row of the Galerkin product exceeds the SpGEMM LDS capacity");
+            return XFK_ERR_UNSUPPORTED;
+        }
+        AMG_CHECK(C.col_o.alloc((size_t)std::max(1LL, cnnz)));
+        AMG_CHECK(C.val_o.alloc((size_t)std::max(1LL, cnnz)));
+        k_spgemm<true><<<(int)nc, 64, 0, s>>>((int)nc, SR, INT_MAX, SAP, nullptr, C.rowptr_o.p, C.col_o.p, C.val_o.p,
+                                              dev_int.p + 2);
+        C.n = (int)nc;
+        C.nnz = cnnz;
+        C.ncol_lim = (int)nc;
+        C.rowptr = C.rowptr_o.p;
+        C.col = C.col_o.p;
+        C.val = C.val_o.p;
+    }
+    nlev = l + 1;
+    stats.levels = nlev;
+    double tot = 0;
+    for (int k = 0; k < nlev; ++k) tot += (double)stats.nnz[k];
+    stats.op_complexity = nnz0 > 0 ? tot / (double)nnz0 : 0.0;
+    // vectors
+    for (int k = 0; k < nlev; ++k) {
+        AmgLevel &A = *L[k];
+        AMG_CHECK(A.xa.alloc((size_t)A.n));
+        AMG_CHECK(A.xb.alloc((size_t)A.n));
+        AMG_CHECK(A.r.alloc((size_t)A.n));
+        if (k > 0) AMG_CHECK(A.b.alloc((size_t)A.n));
+    }
+    if (dense_coarse) {
+        AmgLevel &C = *L[nlev - 1];
+        AMG_CHECK(cinv.alloc((size_t)C.n * C.n));
+        k_dense_scatter<<<nb(C.n), kB, 0, s>>>(C.n, C.rowptr, C.col, C.val, cinv.p);
+        k_gauss_jordan<<<1, 1024, 0, s>>>(C.n, cinv.p);
+    }
+    AMG_CHECK(hipGetLastError());
+    AMG_CHECK(hipStreamSynchronize(s));
+    return XFK_OK;
+}
+
+namespace {
+
+void launch_smooth(hipStream_t s, int mode, const AmgLevel &A, const unsigned long long *rho, const double *b,
+                   const double *x, double *out, double *rout, const int *done)
+{
+    const int g = (A.n + kCgBlock - 1) / kCgBlock;
+    switch (mode) {
+    case kSweepFromZero:
+        k_amg_smooth<kSweepFromZero><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho,
+                                                            b, x, out, rout, done);
+        break;
+    case kSweep:
+        k_amg_smooth<kSweep><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
+                                                    out, rout, done);
+        break;
+    case kResid:
+        k_amg_smooth<kResid><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
+                                                    out, rout, done);
+        break;
+    default:
+        k_amg_smooth<kResidFromZero><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho,
+                                                            b, x, out, rout, done);
+        break;
+    }
+}
+
+}  // namespace
+
+// Symmetric V-cycle; returns the buffer holding the level's result.  Level 0
+// writes its result to `out0`.
+static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, double *out0, const int *done)
+{
+    AmgLevel &A = *M.L[l];
+    const unsigned long long *rho = M.rho.p + 2 * l;
+    const int nu = M.sweeps;
+    auto other = [&](double *c) { return c == A.xa.p ? A.xb.p : A.xa.p; };
+    if (l == M.nlev - 1) {
+        double *dst = (l == 0) ? out0 : A.xa.p;
+        if (M.dense_coarse) {
+            k_dense_mv<<<(A.n * 64 + 255) / 256, 256, 0, s>>>(A.n, M.cinv.p, b, dst, done);
+            return dst;
+        }
+        // smoother-only coarsest level: 2 nu sweeps from zero
+        double *cur = A.xa.p;
+        launch_smooth(s, kSweepFromZero, A, rho, b, nullptr, cur, nullptr, done);
+        for (int k = 2; k < 2 * nu; ++k) {
+            double *nx = (k == 2 * nu - 1 && l == 0) ? out0 : other(cur);
+            launch_smooth(s, kSweep, A, rho, b, cur, nx, nullptr, done);
+            cur = nx;
+        }
+        if (l == 0 && cur != out0)
+            (void)hipMemcpyAsync(out0, cur, sizeof(double) * A.n, hipMemcpyDeviceToDevice, s);
+        return cur;
+    }
+    // pre-smoothing (nu sweeps from zero) and residual
+    double *cur = A.xa.p;
+    if (nu == 1) {
+        launch_smooth(s, kResidFromZero, A, rho, b, nullptr, cur, A.r.p, done);
+    } else {
+        launch_smooth(s, kSweepFromZero, A, rho, b, nullptr, cur, nullptr, done);
+        for (int k = 2; k < nu; ++k) {
+            double *nx = other(cur);
+            launch_smooth(s, kSweep, A, rho, b, cur, nx, nullptr, done);
+            cur = nx;
+        }
+        launch_smooth(s, kResid, A, rho, b, cur, nullptr, A.r.p, done);
+    }
+    AmgLevel &C = *M.L[l + 1];
+    k_amg_restrict<<<nb(A.nc), kB, 0, s>>>(A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, done);
+    const double *xc = vcycle_level(M, s, l + 1, C.b.p, nullptr, done);
+    k_amg_prolong<<<nb(A.n), kB, 0, s>>>(A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, done);
+    for (int k = 0; k < nu; ++k) {
+        double *nx = (k == nu - 1 && l == 0) ? out0 : other(cur);
+        launch_smooth(s, kSweep, A, rho, b, cur, nx, nullptr, done);
+        cur = nx;
+    }
+    return cur;
+}
+
+void Amg::vcycle(hipStream_t s, const double *r, double *u, const int *done)
+{
+    vcycle_level(*this, s, 0, r, u, done);
+}
+
+}  // namespace xfk

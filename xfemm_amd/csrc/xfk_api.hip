@@ -10,6 +10,8 @@
 // averaging map over CSR slots.  Everything else runs on the device.
 #include <hipcub/hipcub.hpp>
 
+#include "xfk_amg.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -501,10 +503,11 @@ static CgAxpyArgs cg_args(xfk_problem *P, long long it)
     A.gam_out = P->part_loc.p + (size_t)((it + 1) & 1) * G;
     A.del_in = P->part_glob + 2 * G;
     A.reso = P->part_glob + 3 * G;
+    A.amg = P->pc_used == XFK_PRECOND_AMG;
     if (P->comm) {
         A.Ggam = A.Gdel = (int)G;     // zero beyond this rank's grids
     } else {
-        A.Ggam = (it == 0) ? cg_grid(N) : cg_axpy_grid(N);
+        A.Ggam = (it == 0 || A.amg) ? cg_grid(N) : cg_axpy_grid(N);
         A.Gdel = cg_grid(N);
     }
     A.S = P->pcg.p;
@@ -536,6 +539,40 @@ static int allreduce_partials(xfk_problem *P, int narrays)
     return P->comm->allreduce_sum(P->part_loc.p, P->part_glob, (size_t)narrays * P->Gpart, P->stream);
 }
 
+// AMG hierarchy of the assembled matrix (owned block when sharded); falls
+// back to Jacobi for this solve when the hierarchy cannot be built
+static int amg_setup(xfk_problem *P)
+{
+    P->pc_used = XFK_PRECOND_JACOBI;
+    if (P->precond != XFK_PRECOND_AMG) return XFK_OK;
+    hipStream_t s = P->stream;
+    if (!P->amg) P->amg = new Amg();
+    P->amg->theta = P->amg_theta;
+    P->amg->sweeps = P->amg_sweeps;
+    hipEvent_t e0, e1;
+    XFK_CHECK(hipEventCreate(&e0));
+    XFK_CHECK(hipEventCreate(&e1));
+    XFK_CHECK(hipEventRecord(e0, s));
+    int rc = P->amg->setup(s, P->N, P->N, P->rowptr.p, P->col.p, P->val.p, P->nnz);
+    XFK_CHECK(hipEventRecord(e1, s));
+    XFK_CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    P->last.ms_amg_setup += ms;
+    double ok = (rc == XFK_OK) ? 0.0 : 1.0;   // every rank must take the same preconditioner
+    if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
+    int rc2 = allreduce_host(P, ok);
+    if (rc2 != XFK_OK) return rc2;
+    if (ok == 0.0) {
+        P->pc_used = XFK_PRECOND_AMG;
+        P->last.amg_levels = P->amg->stats.levels;
+        P->last.amg_op_complexity = P->amg->stats.op_complexity;
+    }
+    return XFK_OK;
+}
+
 static int pcg_start(xfk_problem *P, int flag)
 {
     hipStream_t s = P->stream;
@@ -554,11 +591,26 @@ static int pcg_start(xfk_problem *P, int flag)
         set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
         return XFK_ERR_SINGULAR;
     }
+    if ((rc = amg_setup(P)) != XFK_OK) return rc;
     const CgAxpyArgs A0 = cg_args(P, 0);
     const size_t G = (size_t)P->Gpart;
     if (flag && (rc = exchange(P, P->V.p)) != XFK_OK) return rc;
     launch_cg_init_r(s, N, flag, P->rowptr.p, P->col.p, P->val.p, P->b.p, P->V.p, A0.R, A0.U, A0.Z, A0.P, P->dinv.p,
                      P->part_loc.p + 3 * G, P->part_loc.p);
+    if (P->pc_used == XFK_PRECOND_AMG) {
+        // u0 = M^-1 r0; res_o = (M^-1 b).b (one more V-cycle when x0 != 0)
+        P->amg->vcycle(s, A0.R, A0.U, nullptr);
+        if (flag) {
+            P->amg->vcycle(s, P->b.p, P->W2.p, nullptr);
+            launch_cg_dot(s, N, P->b.p, P->W2.p, P->part_loc.p + 3 * G);
+        } else {
+            launch_cg_dot(s, N, P->b.p, A0.U, P->part_loc.p + 3 * G);
+        }
+        if ((rc = exchange(P, A0.U)) != XFK_OK) return rc;
+        launch_cg_spmv(s, N, P->rowptr.p, P->col.p, P->val.p, A0.U, P->W2.p, P->part_loc.p + 2 * G, nullptr, A0.R,
+                       P->part_loc.p);
+        return allreduce_partials(P, 4);
+    }
     if ((rc = exchange(P, A0.U)) != XFK_OK) return rc;
     launch_cg_spmv(s, N, P->rowptr.p, P->col.p, P->val.p, A0.U, P->W2.p, P->part_loc.p + 2 * G, nullptr);
     return allreduce_partials(P, 4);
@@ -570,12 +622,17 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
 {
     hipStream_t s = P->stream;
     const CgAxpyArgs A = cg_args(P, it);
+    const size_t G = (size_t)P->Gpart;
     launch_cg_axpy(s, A);
+    if (A.amg) P->amg->vcycle(s, A.R, A.U, &P->pcg.p->done);
     int rc = exchange(P, A.U);
     if (rc != XFK_OK) return rc;
     if (stamp) XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used], s));
-    launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * (size_t)P->Gpart,
-                   P->pcg.p);
+    if (A.amg)
+        launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G, P->pcg.p, A.R,
+                       P->part_loc.p + (size_t)((it + 1) & 1) * G);
+    else
+        launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G, P->pcg.p);
     if (stamp) {
         XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used + 1], s));
         P->spmv_used += 2;
@@ -591,7 +648,7 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
     rc = pcg_start(P, flag);
     if (rc != XFK_OK) return rc;
     long long it = 0;
-    int batch = 16;
+    int batch = P->pc_used == XFK_PRECOND_AMG ? 8 : 16;
     for (;;) {
         for (int k = 0; k < batch; ++k, ++it) {
             const bool stamp = P->time_spmv && (it % 16 == 0) && P->spmv_used + 2 <= (int)P->spmv_ev.size();
@@ -640,6 +697,7 @@ void xfk_problem_destroy(xfk_problem *P)
     if (P->pcg_host) (void)hipHostFree(P->pcg_host);
     if (P->nws_host) (void)hipHostFree(P->nws_host);
     hipStream_t s = P->stream;
+    delete P->amg;
     delete P;   // device buffers free themselves (DBuf), on this device
     if (s) (void)hipStreamDestroy(s);
 }
@@ -1081,6 +1139,9 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
         P->spmv_ev.resize(2 * 512);
         for (auto &ev : P->spmv_ev) XFK_CHECK(hipEventCreate(&ev));
     }
+    P->last.ms_amg_setup = 0;
+    P->last.amg_levels = 0;
+    P->last.amg_op_complexity = 0;
     XFK_CHECK(hipEventRecord(e0, s));
     if (!P->symbolic_ready || (flags & XFK_REBUILD_SYMBOLIC)) {
         P->symbolic_ready = false;
@@ -1166,6 +1227,10 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     R.nnz = P->nnz;
     R.ncolors = P->ncolors;
     R.color_rounds = P->color_rounds;
+    R.precond = P->pc_used;
+    R.amg_levels = P->last.amg_levels;
+    R.amg_op_complexity = P->last.amg_op_complexity;
+    R.ms_amg_setup = P->last.ms_amg_setup;
     P->last = R;
     if (res) *res = R;
     return XFK_OK;
@@ -1240,6 +1305,35 @@ int xfk_get_stream(xfk_problem *P, void **st)
 int xfk_pcg_solve_csr(int n, const int *rowptr, const int *col, const double *val, const double *b, double *V,
                       int flag, double precision, int device, long long *iters, double *er)
 {
+    return xfk_pcg_solve_csr_pc(n, rowptr, col, val, b, V, flag, precision, device, XFK_PRECOND_JACOBI, iters, er);
+}
+
+int xfk_set_option(xfk_problem *P, int option, double value)
+{
+    XFK_REQUIRE(P, XFK_ERR_ARG, "null problem");
+    switch (option) {
+    case XFK_OPT_PRECOND:
+        XFK_REQUIRE(value == XFK_PRECOND_JACOBI || value == XFK_PRECOND_AMG, XFK_ERR_ARG, "unknown preconditioner");
+        P->precond = (int)value;
+        return XFK_OK;
+    case XFK_OPT_AMG_SWEEPS:
+        XFK_REQUIRE(value >= 1 && value <= 8 && value == (int)value, XFK_ERR_ARG, "AMG sweeps must be 1..8");
+        P->amg_sweeps = (int)value;
+        return XFK_OK;
+    case XFK_OPT_AMG_THETA:
+        XFK_REQUIRE(value >= 0.0 && value < 1.0, XFK_ERR_ARG, "AMG strength threshold must be in [0, 1)");
+        P->amg_theta = value;
+        return XFK_OK;
+    default:
+        set_error("unknown option");
+        return XFK_ERR_ARG;
+    }
+}
+
+int xfk_pcg_solve_csr_pc(int n, const int *rowptr, const int *col, const double *val, const double *b, double *V,
+                         int flag, double precision, int device, int precond, long long *iters, double *er)
+{
+    XFK_REQUIRE(precond == XFK_PRECOND_JACOBI || precond == XFK_PRECOND_AMG, XFK_ERR_ARG, "unknown preconditioner");
     XFK_REQUIRE(n > 0 && rowptr && col && val && b && V, XFK_ERR_ARG, "null argument");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
@@ -1253,6 +1347,7 @@ int xfk_pcg_solve_csr(int n, const int *rowptr, const int *col, const double *va
     P->NL = n;
     P->nnz = rowptr[n];
     P->precision = precision;
+    P->precond = precond;
     int rc = XFK_OK;
     hipError_t e = hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking);
     // diagonal positions

@@ -29,6 +29,8 @@ struct xfk_comm;
 
 namespace xfk {
 
+struct Amg;
+
 constexpr int kBlock = 256;          // 4 waves of 64
 constexpr int kRedGrid = 1024;       // fixed grid of the reduction kernels (4 WG/CU)
 constexpr double kPI = 3.141592653589793238462643383;
@@ -239,6 +241,13 @@ struct xfk_problem {
     xfk::DBuf<xfk::NewtonScalars> nws;
     xfk::CgState *pcg_host = nullptr;  // pinned mirror
     xfk::NewtonScalars *nws_host = nullptr;
+
+    // preconditioner (xfk_set_option): XFK_PRECOND_AMG (default) or XFK_PRECOND_JACOBI
+    int precond = XFK_PRECOND_AMG;
+    int amg_sweeps = 2;
+    double amg_theta = 0.08;
+    xfk::Amg *amg = nullptr;         // hierarchy of the current matrix (xfk_amg.hip)
+    int pc_used = XFK_PRECOND_JACOBI;  // preconditioner of the running solve
 
     // live SpMV launch timing (XFK_TIME_SPMV)
     bool time_spmv = false;

@@ -34,6 +34,7 @@ struct CgAxpyArgs {
     CgState *S;
     long long it;
     int N;
+    int amg;                         // u = M^-1 r comes from the AMG V-cycle (U), gamma from the SpMV
 };
 
 int cg_grid(int N);
@@ -44,8 +45,11 @@ void launch_cg_init_r(hipStream_t s, int N, int flag, const int *rowptr, const i
                       const double *b, double *V, double *R, double *U, double *Z, double *P, const double *dinv,
                       double *part_reso, double *part_gam0);
 void launch_cg_axpy(hipStream_t s, const CgAxpyArgs &A);
+// w = A u, partials of u.w (and of r.u into part_gam when R != nullptr)
 void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *U,
-                    double *W, double *part_del, const CgState *S);
+                    double *W, double *part_del, const CgState *S, const double *R = nullptr,
+                    double *part_gam = nullptr);
+void launch_cg_dot(hipStream_t s, int N, const double *a, const double *b, double *part);
 
 void launch_count_incidence(hipStream_t s, int NE, const int *p, int *deg);
 void launch_fill_n2e(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e);

@@ -20,88 +20,9 @@
 // (identical order in every block -> bit-identical alpha/beta everywhere, no
 // atomics, no fan-in tail).
 #include "xfk_kernels.h"
+#include "xfk_spmv.h"
 
 namespace xfk {
-
-constexpr int kCgBlock = 1024;            // 16 waves; one row tile per workgroup
-constexpr int kCgCap = 8 * kCgBlock;      // products staged per LDS pass (64 KiB)
-
-__device__ __forceinline__ double cg_wave_sum(double v)
-{
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
-// two simultaneous workgroup sums, results broadcast to every thread
-__device__ __forceinline__ void cg_block_sum2(double &a, double &b, double *red)
-{
-    a = cg_wave_sum(a);
-    b = cg_wave_sum(b);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    __syncthreads();
-    if (lane == 0) {
-        red[2 * wid] = a;
-        red[2 * wid + 1] = b;
-    }
-    __syncthreads();
-    double sa = 0.0, sb = 0.0;
-    const int nw = blockDim.x >> 6;
-    for (int w = 0; w < nw; ++w) {
-        sa += red[2 * w];
-        sb += red[2 * w + 1];
-    }
-    a = sa;
-    b = sb;
-}
-
-// deterministic sum of G partials (pairs) of the previous launch, in every block
-__device__ __forceinline__ void cg_reduce_partials(const double *__restrict__ part, int G, double &a, double &b,
-                                                   double *red)
-{
-    double sa = 0.0, sb = 0.0;
-    for (int i = threadIdx.x; i < G; i += blockDim.x) {
-        sa += part[i];
-        sb += part[G + i];
-    }
-    cg_block_sum2(sa, sb, red);
-    a = sa;
-    b = sb;
-}
-
-// y = sum_k val[k] * X(col[k]) for the rows of one tile; CSR-stream through LDS
-template <class XF>
-__device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restrict__ rowptr,
-                                               const int *__restrict__ col, const double *__restrict__ val,
-                                               XF X, double *lds)
-{
-    const int r = r0 + threadIdx.x;
-    const int rend = min(r0 + kCgBlock, N);
-    const int s = rowptr[r0], e = rowptr[rend];
-    const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
-    double acc = 0.0;
-    for (int c0 = s; c0 < e; c0 += kCgCap) {
-        const int c1 = min(e, c0 + kCgCap);
-        int cidx[8];
-        double v[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const int k = c0 + threadIdx.x + m * kCgBlock;
-            cidx[m] = (k < c1) ? col[k] : -1;
-            v[m] = (k < c1) ? val[k] : 0.0;
-        }
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const int k = c0 + threadIdx.x + m * kCgBlock;
-            if (cidx[m] >= 0) lds[k - c0] = v[m] * X(cidx[m]);
-        }
-        __syncthreads();
-        const int a = max(my_s, c0), z = min(my_e, c1);
-        for (int k = a; k < z; ++k) acc += lds[k - c0];
-        __syncthreads();
-    }
-    return acc;
-}
 
 // Launch structure per iteration i (two launches, one reduction phase):
 //   k_cg_axpy(i): reduce the gamma_i (own previous launch) and delta_i (SpMV)
@@ -148,11 +69,13 @@ __global__ void __launch_bounds__(kCgBlock) k_cg_init_r(int N, int flag, const i
     }
 }
 
-// w = A u; partials delta = u.w
+// w = A u; partials delta = u.w and, when the preconditioner is applied
+// outside the update kernel (AMG: R != nullptr), gamma = r.u as well
 __global__ void __launch_bounds__(kCgBlock) k_cg_spmv(int N, const int *__restrict__ rowptr,
                                                       const int *__restrict__ col, const double *__restrict__ val,
                                                       const double *__restrict__ U, double *__restrict__ W,
-                                                      double *__restrict__ part_del, const CgState *S)
+                                                      double *__restrict__ part_del, const CgState *S,
+                                                      const double *__restrict__ R, double *__restrict__ part_gam)
 {
     if (S && S->done) return;
     __shared__ __attribute__((aligned(16))) double lds[kCgCap];
@@ -160,13 +83,18 @@ __global__ void __launch_bounds__(kCgBlock) k_cg_spmv(int N, const int *__restri
     const int r0 = blockIdx.x * kCgBlock;
     const double w = cg_tile_spmv(r0, N, rowptr, col, val, [&](int j) { return U[j]; }, lds);
     const int r = r0 + threadIdx.x;
-    double d = 0.0, zero = 0.0;
+    double d = 0.0, g = 0.0;
     if (r < N) {
         W[r] = w;
-        d = w * U[r];
+        const double u = U[r];
+        d = w * u;
+        if (R) g = R[r] * u;
     }
-    cg_block_sum2(d, zero, red);
-    if (threadIdx.x == 0) part_del[blockIdx.x] = d;
+    cg_block_sum2(d, g, red);
+    if (threadIdx.x == 0) {
+        part_del[blockIdx.x] = d;
+        if (R) part_gam[blockIdx.x] = g;
+    }
 }
 
 // one pair of deterministic sums over two partial arrays of different lengths
@@ -216,6 +144,33 @@ __global__ void __launch_bounds__(kAxBlock) k_cg_axpy(CgAxpyArgs A)
     }
     if (stop) return;
     const int N = A.N;
+    if (A.amg) {
+        // u_i is the V-cycle output already in U; r.u partials come from the SpMV
+        const double2 *U2c = reinterpret_cast<const double2 *>(A.U);
+        double2 *Z2 = reinterpret_cast<double2 *>(A.Z);
+        double2 *P2 = reinterpret_cast<double2 *>(A.P);
+        double2 *V2 = reinterpret_cast<double2 *>(A.V);
+        double2 *R2 = reinterpret_cast<double2 *>(A.R);
+        const double2 *W2 = reinterpret_cast<const double2 *>(A.W);
+        for (int k = blockIdx.x * kAxBlock + threadIdx.x; k < (N >> 1); k += gridDim.x * kAxBlock) {
+            const double2 w = W2[k], zo = Z2[k], po = P2[k], x = V2[k], ri = R2[k], u = U2c[k];
+            double2 z, p, rn, xn;
+            z.x = w.x + beta * zo.x;          z.y = w.y + beta * zo.y;
+            p.x = u.x + beta * po.x;          p.y = u.y + beta * po.y;
+            rn.x = ri.x - alpha * z.x;        rn.y = ri.y - alpha * z.y;
+            xn.x = x.x + alpha * p.x;         xn.y = x.y + alpha * p.y;
+            Z2[k] = z; P2[k] = p; V2[k] = xn; R2[k] = rn;
+        }
+        if ((N & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            const int r = N - 1;
+            const double z = A.W[r] + beta * A.Z[r];
+            const double p = A.U[r] + beta * A.P[r];
+            A.V[r] = A.V[r] + alpha * p;
+            A.R[r] = A.R[r] - alpha * z;
+            A.Z[r] = z; A.P[r] = p;
+        }
+        return;
+    }
     double g = 0.0;
     const int npair = N >> 1;
     const double2 *W2 = reinterpret_cast<const double2 *>(A.W);
@@ -273,9 +228,25 @@ void launch_cg_axpy(hipStream_t s, const CgAxpyArgs &A)
 }
 
 void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *U,
-                    double *W, double *part_del, const CgState *S)
+                    double *W, double *part_del, const CgState *S, const double *R, double *part_gam)
 {
-    k_cg_spmv<<<cg_grid(N), kCgBlock, 0, s>>>(N, rowptr, col, val, U, W, part_del, S);
+    k_cg_spmv<<<cg_grid(N), kCgBlock, 0, s>>>(N, rowptr, col, val, U, W, part_del, S, R, part_gam);
+}
+
+// partials of a.b over the cg_grid(N) layout (the AMG start: (M^-1 b).b)
+__global__ void __launch_bounds__(kCgBlock) k_cg_dot(int N, const double *__restrict__ a, const double *__restrict__ b,
+                                                     double *__restrict__ part)
+{
+    __shared__ double red[2 * (kCgBlock / 64)];
+    const int r = blockIdx.x * kCgBlock + threadIdx.x;
+    double d = (r < N) ? a[r] * b[r] : 0.0, zero = 0.0;
+    cg_block_sum2(d, zero, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = d;
+}
+
+void launch_cg_dot(hipStream_t s, int N, const double *a, const double *b, double *part)
+{
+    k_cg_dot<<<cg_grid(N), kCgBlock, 0, s>>>(N, a, b, part);
 }
 
 }  // namespace xfk

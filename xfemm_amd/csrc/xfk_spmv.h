@@ -1,0 +1,89 @@
+// Device helpers shared by the PCG (xfk_pcg.hip) and the AMG V-cycle
+// (xfk_amg.hip): wavefront/workgroup sums and the CSR-stream tile SpMV.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace xfk {
+
+constexpr int kCgBlock = 1024;            // 16 waves; one row tile per workgroup
+constexpr int kCgCap = 8 * kCgBlock;      // products staged per LDS pass (64 KiB)
+
+__device__ __forceinline__ double cg_wave_sum(double v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// two simultaneous workgroup sums, results broadcast to every thread
+__device__ __forceinline__ void cg_block_sum2(double &a, double &b, double *red)
+{
+    a = cg_wave_sum(a);
+    b = cg_wave_sum(b);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) {
+        red[2 * wid] = a;
+        red[2 * wid + 1] = b;
+    }
+    __syncthreads();
+    double sa = 0.0, sb = 0.0;
+    const int nw = blockDim.x >> 6;
+    for (int w = 0; w < nw; ++w) {
+        sa += red[2 * w];
+        sb += red[2 * w + 1];
+    }
+    a = sa;
+    b = sb;
+}
+
+// deterministic sum of G partials (pairs) of the previous launch, in every block
+__device__ __forceinline__ void cg_reduce_partials(const double *__restrict__ part, int G, double &a, double &b,
+                                                   double *red)
+{
+    double sa = 0.0, sb = 0.0;
+    for (int i = threadIdx.x; i < G; i += blockDim.x) {
+        sa += part[i];
+        sb += part[G + i];
+    }
+    cg_block_sum2(sa, sb, red);
+    a = sa;
+    b = sb;
+}
+
+// y = sum_k val[k] * X(col[k]) for the rows of one tile; CSR-stream through LDS
+template <class XF>
+__device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restrict__ rowptr,
+                                               const int *__restrict__ col, const double *__restrict__ val,
+                                               XF X, double *lds)
+{
+    const int r = r0 + threadIdx.x;
+    const int rend = min(r0 + kCgBlock, N);
+    const int s = rowptr[r0], e = rowptr[rend];
+    const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
+    double acc = 0.0;
+    for (int c0 = s; c0 < e; c0 += kCgCap) {
+        const int c1 = min(e, c0 + kCgCap);
+        int cidx[8];
+        double v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int k = c0 + threadIdx.x + m * kCgBlock;
+            cidx[m] = (k < c1) ? col[k] : -1;
+            v[m] = (k < c1) ? val[k] : 0.0;
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int k = c0 + threadIdx.x + m * kCgBlock;
+            if (cidx[m] >= 0) lds[k - c0] = v[m] * X(cidx[m]);
+        }
+        __syncthreads();
+        const int a = max(my_s, c0), z = min(my_e, c1);
+        for (int k = a; k < z; ++k) acc += lds[k - c0];
+        __syncthreads();
+    }
+    return acc;
+}
+
+}  // namespace xfk

@@ -22,12 +22,18 @@ iptr = C.POINTER(C.c_int)
 XFK_OK = 0
 XFK_REBUILD_SYMBOLIC = 1
 XFK_TIME_SPMV = 2
+XFK_PRECOND_JACOBI = 0
+XFK_PRECOND_AMG = 1
+PRECONDS = {"jacobi": XFK_PRECOND_JACOBI, "amg": XFK_PRECOND_AMG}
+XFK_OPT_PRECOND = 1
+XFK_OPT_AMG_SWEEPS = 2
+XFK_OPT_AMG_THETA = 3
 
 # every symbol include/xfemm_kernels.h declares
 EXPORTED = (
     "xfk_last_error", "xfk_device_count", "xfk_problem_create", "xfk_problem_destroy",
     "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz",
-    "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_time",
+    "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_solve_csr_pc", "xfk_pcg_time", "xfk_set_option",
     "xfk_comm_unique_id", "xfk_comm_create_rccl", "xfk_comm_create_local", "xfk_comm_destroy",
     "xfk_comm_rank", "xfk_comm_size", "xfk_partition_plan", "xfk_problem_create_dist", "xfk_dist_get_info",
 )
@@ -77,7 +83,8 @@ class Result(C.Structure):
                 ("final_er", C.c_double), ("nnz", C.c_longlong), ("ncolors", C.c_int),
                 ("ms_symbolic", C.c_double), ("ms_assemble", C.c_double), ("ms_solve", C.c_double),
                 ("spmv_ms_avg", C.c_double), ("spmv_samples", C.c_int),
-                ("color_rounds", C.c_int)]
+                ("color_rounds", C.c_int), ("precond", C.c_int), ("amg_levels", C.c_int),
+                ("amg_op_complexity", C.c_double), ("ms_amg_setup", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -120,7 +127,10 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_get_stream.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
     L.xfk_pcg_solve_csr.argtypes = [C.c_int, iptr, iptr, dptr, dptr, dptr, C.c_int, C.c_double, C.c_int,
                                     C.POINTER(C.c_longlong), dptr]
+    L.xfk_pcg_solve_csr_pc.argtypes = [C.c_int, iptr, iptr, dptr, dptr, dptr, C.c_int, C.c_double, C.c_int,
+                                       C.c_int, C.POINTER(C.c_longlong), dptr]
     L.xfk_pcg_time.argtypes = [C.c_void_p, C.c_int, dptr, dptr]
+    L.xfk_set_option.argtypes = [C.c_void_p, C.c_int, C.c_double]
     vp = C.c_void_p
     L.xfk_comm_unique_id.argtypes = [C.c_char_p, C.c_int]
     L.xfk_comm_create_rccl.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
@@ -166,9 +176,11 @@ class Static2DProblem:
     def __init__(self, *, x, y, p, lbl, blocks: Sequence[dict], labels: Sequence[dict],
                  lines: Sequence[dict] = (), points: Sequence[dict] = (), circuits: Sequence[dict] = (),
                  marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0,
-                 device=0, comm: Optional["Comm"] = None):
+                 device=0, comm: Optional["Comm"] = None, precond: str = "amg", amg_sweeps: Optional[int] = None,
+                 amg_theta: Optional[float] = None):
         """comm: shard the mesh by row blocks over this communicator (every rank
-        passes the same global problem; solve() and solution() are collective)."""
+        passes the same global problem; solve() and solution() are collective).
+        precond: "amg" (smoothed-aggregation V-cycle, default) or "jacobi"."""
         L = load_library()
         keep = _Keep()
         nb = max(1, len(blocks))
@@ -228,8 +240,16 @@ class Static2DProblem:
         else:
             _check(L.xfk_problem_create_dist(C.byref(D), device, comm._h, C.byref(h)))
         self._h = h
+        self.set_option(XFK_OPT_PRECOND, PRECONDS[precond])
+        if amg_sweeps is not None:
+            self.set_option(XFK_OPT_AMG_SWEEPS, amg_sweeps)
+        if amg_theta is not None:
+            self.set_option(XFK_OPT_AMG_THETA, amg_theta)
         self.n_rows = self.dist_info()["n_own"] if comm is not None else self.n_nodes
         self.result: Optional[Result] = None
+
+    def set_option(self, option: int, value: float):
+        _check(_lib.xfk_set_option(self._h, option, float(value)))
 
     def dist_info(self) -> dict:
         info = DistInfo()
@@ -286,7 +306,7 @@ class Static2DProblem:
         return ms_spmv.value, ms_iter.value
 
 
-def pcg_solve_csr(rowptr, col, val, b, V0=None, flag=0, precision=1e-8, device=0):
+def pcg_solve_csr(rowptr, col, val, b, V0=None, flag=0, precision=1e-8, device=0, precond="jacobi"):
     """Stand-alone device PCG on a full symmetric CSR (CBigLinProb::PCGSolve semantics)."""
     L = load_library()
     n = len(rowptr) - 1
@@ -297,9 +317,9 @@ def pcg_solve_csr(rowptr, col, val, b, V0=None, flag=0, precision=1e-8, device=0
     V = np.zeros(n) if V0 is None else np.array(V0, dtype=np.float64)
     it = C.c_longlong()
     er = C.c_double()
-    _check(L.xfk_pcg_solve_csr(n, rp.ctypes.data_as(iptr), cl.ctypes.data_as(iptr), vl.ctypes.data_as(dptr),
-                               bb.ctypes.data_as(dptr), V.ctypes.data_as(dptr), flag, precision, device,
-                               C.byref(it), C.byref(er)))
+    _check(L.xfk_pcg_solve_csr_pc(n, rp.ctypes.data_as(iptr), cl.ctypes.data_as(iptr), vl.ctypes.data_as(dptr),
+                                  bb.ctypes.data_as(dptr), V.ctypes.data_as(dptr), flag, precision, device,
+                                  PRECONDS[precond], C.byref(it), C.byref(er)))
     return V, it.value, er.value
 
 
