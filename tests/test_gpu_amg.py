@@ -1,0 +1,136 @@
+"""The AMG-preconditioned PCG (xfemm_amd/csrc/xfk_amg.hip) against the oracle.
+
+The reference preconditions CBigLinProb::PCGSolve with SSOR
+(cfemm/libfemm/spars.cpp:186-236); the device's default is a smoothed-
+aggregation AMG V-cycle, with the same stopping test.  Tolerances as in
+test_gpu_static2d.py: A within 1e-6 (linear) / 1e-5 (nonlinear) of max |A|.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import scipy.sparse.linalg as sla
+
+from oracle import oracle
+from util import rel_err, synth_to_oracle
+from xfemm_amd import kernels, synth
+
+pytestmark = pytest.mark.gpu
+
+TOL_LINEAR = 1e-6
+TOL_NONLINEAR = 1e-5
+
+
+def _solve(kw, **opt):
+    P = kernels.Static2DProblem(**kw, **opt)
+    r = P.solve()
+    A = P.solution()
+    P.close()
+    return A, r
+
+
+@pytest.mark.parametrize("cells,nonlinear", [(60, False), (40, True)])
+def test_amg_matches_oracle(cells, nonlinear):
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(cells, nonlinear=nonlinear))
+    A, r = _solve(kw, precond="amg")
+    Ao, st, _ = oracle.solve(pr, mesh)
+    assert r["precond"] == kernels.XFK_PRECOND_AMG and r["amg_levels"] >= 2
+    assert rel_err(A, Ao) <= (TOL_NONLINEAR if nonlinear else TOL_LINEAR)
+
+
+@pytest.mark.parametrize("anti", [False, True])
+def test_amg_periodic_boundaries(anti):
+    pr, mesh, kw = synth_to_oracle(synth.bc_showcase(30, anti=anti, nonlinear=True))
+    A, r = _solve(kw, precond="amg")
+    Ao, _, _ = oracle.solve(pr, mesh)
+    assert r["precond"] == kernels.XFK_PRECOND_AMG
+    assert rel_err(A, Ao) <= TOL_NONLINEAR
+
+
+def test_amg_iterations_nearly_mesh_independent():
+    its = []
+    for cells in (100, 400):
+        kw = synth.magnetostatic(cells)
+        A_amg, r_amg = _solve(kw, precond="amg")
+        A_jac, r_jac = _solve(kw, precond="jacobi")
+        assert rel_err(A_amg, A_jac) <= TOL_LINEAR
+        assert r_amg["cg_iters"] * 10 < r_jac["cg_iters"]
+        its.append(r_amg["cg_iters"])
+    assert its[1] <= 2 * its[0] and its[1] <= 60, its
+
+
+@pytest.mark.parametrize("sweeps", [1, 3])
+def test_amg_sweep_counts(sweeps):
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(50))
+    A, r = _solve(kw, precond="amg", amg_sweeps=sweeps)
+    Ao, _, _ = oracle.solve(pr, mesh)
+    assert rel_err(A, Ao) <= TOL_LINEAR
+
+
+def test_amg_is_deterministic():
+    kw = synth.magnetostatic(200)
+    P = kernels.Static2DProblem(**kw, precond="amg")
+    P.solve()
+    A1 = P.solution()
+    P.solve(rebuild_symbolic=True)
+    A2 = P.solution()
+    P.close()
+    A3, _ = _solve(kw, precond="amg")
+    assert np.array_equal(A1, A2) and np.array_equal(A1, A3)
+
+
+def _laplace_random(n, seed):
+    """5-point operator with random positive conductances and a Dirichlet-like
+    diagonal shift on the first row of nodes (SPD)."""
+    rng = np.random.default_rng(seed)
+    N = n * n
+    idx = np.arange(N).reshape(n, n)
+    rows, cols, vals = [], [], []
+    diag = np.zeros(N)
+    for a, b in [(idx[:, :-1], idx[:, 1:]), (idx[:-1, :], idx[1:, :])]:
+        a = a.ravel()
+        b = b.ravel()
+        c = np.exp(rng.uniform(-3, 3, len(a)))
+        rows += [a, b]
+        cols += [b, a]
+        vals += [-c, -c]
+        np.add.at(diag, a, c)
+        np.add.at(diag, b, c)
+    diag[idx[0]] += 1.0
+    rows.append(np.arange(N))
+    cols.append(np.arange(N))
+    vals.append(diag)
+    M = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(N, N))
+    M.sort_indices()
+    return M
+
+
+@pytest.mark.parametrize("n", [8, 150])
+def test_standalone_amg_pcg(n):
+    M = _laplace_random(n, 3)
+    b = np.random.default_rng(1).standard_normal(M.shape[0])
+    V, it, er = kernels.pcg_solve_csr(M.indptr, M.indices, M.data, b, precision=1e-12, precond="amg")
+    Vd = sla.spsolve(M.tocsc(), b)
+    assert er <= 1e-12
+    assert rel_err(V, Vd) <= 1e-8
+    if n == 8:   # 64 rows: the whole matrix is the dense coarsest level -> exact in one step
+        assert it <= 2
+
+
+def test_amg_without_couplings_uses_smoother_only():
+    N = 1000
+    rp = np.arange(N + 1, dtype=np.int32)
+    col = np.arange(N, dtype=np.int32)
+    val = np.linspace(1.0, 5.0, N)
+    b = np.ones(N)
+    V, it, er = kernels.pcg_solve_csr(rp, col, val, b, precision=1e-12, precond="amg")
+    assert np.allclose(V, 1.0 / val, rtol=1e-10)
+
+
+def test_precond_option_validation():
+    kw = synth.magnetostatic(10)
+    P = kernels.Static2DProblem(**kw)
+    with pytest.raises(kernels.XfkError):
+        P.set_option(kernels.XFK_OPT_PRECOND, 7)
+    with pytest.raises(kernels.XfkError):
+        P.set_option(kernels.XFK_OPT_AMG_SWEEPS, 0)
+    P.close()

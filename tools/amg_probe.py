@@ -12,11 +12,13 @@ from xfemm_amd import kernels, synth  # noqa: E402
 
 cells = [int(a) for a in sys.argv[1:] if not a.startswith("-")] or [100, 1000]
 nonlin = "--nonlinear" in sys.argv
+sweeps = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--sweeps=")] or [2]
 for n in cells:
     kw = synth.magnetostatic(n, nonlinear=nonlin)
     sols = {}
-    for pc in ["jacobi", "amg"]:
-        P = kernels.Static2DProblem(device=0, precond=pc, **kw)
+    for pc in ["jacobi"] + ["amg%d" % k for k in sweeps]:
+        opt = dict(precond="jacobi") if pc == "jacobi" else dict(precond="amg", amg_sweeps=int(pc[3:]))
+        P = kernels.Static2DProblem(device=0, **opt, **kw)
         r = P.solve()
         t0 = time.perf_counter()
         reps = 3
@@ -29,5 +31,6 @@ for n in cells:
               % (n, pc, dt * 1e3, r["newton_iters"], r["cg_iters"], r["ms_symbolic"], r["ms_assemble"],
                  r["ms_solve"], r["ms_amg_setup"], r["amg_levels"], r["amg_op_complexity"]), flush=True)
         P.close()
-    d = np.abs(sols["amg"] - sols["jacobi"]).max() / np.abs(sols["jacobi"]).max()
-    print("   max|A_amg - A_jac|/max|A| = %.3e" % d, flush=True)
+    for k in sols:
+        d = np.abs(sols[k] - sols["jacobi"]).max() / np.abs(sols["jacobi"]).max()
+        print("   %s: max|A - A_jac|/max|A| = %.3e" % (k, d), flush=True)

@@ -35,7 +35,7 @@
 
 namespace xfk {
 
-constexpr int kAmgDenseMax = 256;     // coarsest level solved by its dense inverse
+constexpr int kAmgDenseMax = 128;     // coarsest level solved by its dense inverse (LDS Gauss-Jordan)
 constexpr int kAmgMaxLevels = 16;
 
 struct AmgLevel {

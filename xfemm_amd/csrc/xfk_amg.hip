@@ -84,7 +84,8 @@ __global__ void k_amg_diag(int n, const int *__restrict__ rowptr, const int *__r
     dinv[i] = (d != 0.0) ? 1.0 / d : 0.0;
 }
 
-// strong flags per nonzero, strong degree per row, lumped filtered diagonal,
+// strong flags per nonzero (1 strong off-diagonal, 2 diagonal, 0 weak or
+// outside the block), strong degree per row, lumped filtered diagonal,
 // Gershgorin bounds of D^-1 A (rho[0]) and D_F^-1 A_F (rho[1])
 __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double theta, const int *__restrict__ rowptr,
                                                      const int *__restrict__ col, const double *__restrict__ val,
@@ -104,6 +105,7 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
             unsigned char f = 0;
             if (j == i) {
                 aii = a;
+                f = 2;   // the diagonal: not a neighbour, but kept by the prolongator smoothing
             } else if (j < ncl) {
                 sumA += fabs(a);
                 if (a != 0.0 && fabs(a) > theta * sqrt(ai * absd[j])) {
@@ -138,14 +140,15 @@ __global__ void k_mis_init(int n, const int *__restrict__ sdeg, unsigned long lo
 
 __global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
                           const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ in,
-                          unsigned long long *__restrict__ out)
+                          unsigned long long *__restrict__ out, int *undecided)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     unsigned long long m = in[i];
     for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
-        if (sflag[k]) m = max(m, in[col[k]]);
+        if (sflag[k] == 1) m = max(m, in[col[k]]);
     out[i] = m;
+    if (i == 0) *undecided = 0;   // k_mis_update of this round runs after this launch
 }
 
 // second max sweep fused with the state update: an undecided node whose
@@ -161,7 +164,7 @@ __global__ void k_mis_update(int n, const int *__restrict__ rowptr, const int *_
     if (key_st(k) != kStUnd) return;
     unsigned long long m = t1[i];
     for (int q = rowptr[i]; q < rowptr[i + 1]; ++q)
-        if (sflag[q]) m = max(m, t1[col[q]]);
+        if (sflag[q] == 1) m = max(m, t1[col[q]]);
     if (key_idx(m) == i) key[i] = (kStIn << 62) | key_low(k);
     else if (key_st(m) == kStIn) key[i] = key_low(k);
     else *undecided = 1;   // benign race: every writer stores 1
@@ -188,7 +191,7 @@ __global__ void k_agg_join1(int n, const int *__restrict__ rowptr, const int *__
     int bj = -1;
     unsigned long long best = 0;
     for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
-        if (!sflag[k]) continue;
+        if (sflag[k] != 1) continue;
         const int j = col[k];
         const unsigned long long kj = key[j];
         if (key_st(kj) == kStIn && (bj < 0 || key_low(kj) > best)) {
@@ -215,7 +218,7 @@ __global__ void k_agg_join2(int n, const int *__restrict__ rowptr, const int *__
     int bj = -1;
     unsigned long long best = 0;
     for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
-        if (!sflag[k]) continue;
+        if (sflag[k] != 1) continue;
         const int j = col[k];
         if (agg1[j] < 0) continue;
         const unsigned long long kl = key_low(key[j]);
@@ -225,98 +228,6 @@ __global__ void k_agg_join2(int n, const int *__restrict__ rowptr, const int *__
         }
     }
     agg[i] = (bj >= 0) ? agg1[bj] : -1;   // -1: isolated (or unreachable) -> no coarse dof
-}
-
-// --------------------------------------------------------------------------
-// setup: smoothed prolongator P = (I - omega D_F^-1 A_F) P_tent
-// --------------------------------------------------------------------------
-
-// entry k of row i of (I - omega D_F^-1 A_F) restricted to aggregated columns
-struct PEnt {
-    const int *col;
-    const double *val;
-    const unsigned char *sflag;
-    const int *agg;
-    __device__ __forceinline__ bool get(int i, int k, double omega, double dfi, int &J, double &v) const
-    {
-        const int j = col[k];
-        if (j == i) {
-            J = agg[i];
-            v = 1.0 - omega;
-        } else if (sflag[k]) {
-            J = agg[j];
-            v = -omega * dfi * val[k];
-        } else {
-            return false;
-        }
-        return J >= 0;
-    }
-};
-
-__global__ void k_p_count(int n, const int *__restrict__ rowptr, PEnt E, int *__restrict__ cnt)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int s = rowptr[i], e = rowptr[i + 1];
-    int c = 0;
-    for (int k = s; k < e; ++k) {
-        int J;
-        double v;
-        if (!E.get(i, k, 0.0, 0.0, J, v)) continue;
-        bool dup = false;
-        for (int q = s; q < k && !dup; ++q) {
-            int J2;
-            double v2;
-            if (E.get(i, q, 0.0, 0.0, J2, v2) && J2 == J) dup = true;
-        }
-        c += !dup;
-    }
-    cnt[i] = c;
-}
-
-__global__ void k_p_fill(int n, const int *__restrict__ rowptr, PEnt E, const double *__restrict__ dfinv,
-                         const unsigned long long *rho, const int *__restrict__ prow, int *__restrict__ pcol,
-                         double *__restrict__ pval)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const double rF = rho_of(rho + 1);
-    const double omega = rF > 0.0 ? (4.0 / 3.0) / rF : 0.0;
-    const double dfi = dfinv[i];
-    const int s = rowptr[i], e = rowptr[i + 1];
-    const int base = prow[i];
-    for (int k = s; k < e; ++k) {
-        int J;
-        double v;
-        if (!E.get(i, k, omega, dfi, J, v)) continue;
-        bool dup = false;
-        int rank = 0;
-        for (int q = s; q < e; ++q) {
-            int J2;
-            double v2;
-            if (!E.get(i, q, omega, dfi, J2, v2)) continue;
-            if (J2 == J && q < k) dup = true;
-            // distinct columns smaller than J, each counted at its first occurrence
-            if (J2 < J) {
-                bool first = true;
-                for (int t = s; t < q && first; ++t) {
-                    int J3;
-                    double v3;
-                    if (E.get(i, t, omega, dfi, J3, v3) && J3 == J2) first = false;
-                }
-                rank += first;
-            }
-        }
-        if (dup) continue;
-        double sum = 0.0;   // entries of the same aggregate, row order
-        for (int q = k; q < e; ++q) {
-            int J2;
-            double v2;
-            if (E.get(i, q, omega, dfi, J2, v2) && J2 == J) sum += v2;
-        }
-        pcol[base + rank] = J;
-        pval[base + rank] = sum;
-    }
 }
 
 // --------------------------------------------------------------------------
@@ -341,24 +252,45 @@ __global__ void k_rt_fill(int n, const int *__restrict__ prow, const int *__rest
     }
 }
 
-// sort each R row (atomic fill order is arbitrary), then look the values up in P
-__global__ void k_rt_sort_vals(int nc, const int *__restrict__ rrow, int *__restrict__ rcol,
-                               const int *__restrict__ prow, const int *__restrict__ pcol,
-                               const double *__restrict__ pval, double *__restrict__ rval)
+// sort each R row (the atomic fill order is arbitrary), then look the values
+// up in P.  One wavefront per row: rows of <= 64 entries are sorted by a
+// register bitonic network, longer ones by lane 0 (insertion sort).
+__global__ void __launch_bounds__(256) k_rt_sort_vals(int nc, const int *__restrict__ rrow, int *__restrict__ rcol,
+                                                      const int *__restrict__ prow, const int *__restrict__ pcol,
+                                                      const double *__restrict__ pval, double *__restrict__ rval)
 {
-    const int J = blockIdx.x * blockDim.x + threadIdx.x;
+    const int J = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
     if (J >= nc) return;
-    const int s = rrow[J], e = rrow[J + 1];
-    for (int a = s + 1; a < e; ++a) {
-        const int key = rcol[a];
-        int b = a - 1;
-        while (b >= s && rcol[b] > key) {
-            rcol[b + 1] = rcol[b];
-            --b;
+    const int s = rrow[J], e = rrow[J + 1], len = e - s;
+    if (len <= 64) {
+        int v = (lane < len) ? rcol[s + lane] : INT_MAX;
+#pragma unroll
+        for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const int o = __shfl_xor(v, j, 64);
+                const bool up = ((lane & k) == 0);
+                const bool lower = ((lane & j) == 0);
+                v = (lower == up) ? min(v, o) : max(v, o);
+            }
         }
-        rcol[b + 1] = key;
+        if (lane < len) rcol[s + lane] = v;
+    } else if (lane == 0) {
+        for (int a = s + 1; a < e; ++a) {
+            const int key = rcol[a];
+            int b = a - 1;
+            while (b >= s && rcol[b] > key) {
+                rcol[b + 1] = rcol[b];
+                --b;
+            }
+            rcol[b + 1] = key;
+        }
     }
-    for (int a = s; a < e; ++a) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int a = s + lane; a < e; a += 64) {
         const int i = rcol[a];
         int lo = prow[i], hi = prow[i + 1] - 1;
         while (lo < hi) {
@@ -383,27 +315,47 @@ __global__ void k_rt_sort_vals(int nc, const int *__restrict__ rrow, int *__rest
 // group of 64 products, the first lane of each column sums the group's
 // products of that column in lane order, then adds the group sum to the LDS
 // accumulator -- the same operation order on every run.
+//
+// PMODE builds the smoothed prolongator P = S P_tent directly: X is the level
+// matrix masked to its strong entries and diagonal, with values
+// S = I - omega D_F^-1 A_F, and Y = P_tent is given by the aggregate map
+// (row k = {agg[k] : 1}, empty when k is not aggregated).
 
-constexpr int kSgHash = 1024;      // hash slots per row (power of two)
-constexpr int kSgMax = 512;        // distinct output columns per row
+constexpr int kSgMax = 512;        // distinct output columns per row (COUNT pass hash: 2 kSgMax slots)
 
-struct SgMat {
+constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v >> 1); }
+
+struct SgX {
     const int *rowptr, *col;
     const double *val;
+    int col_lim;                   // X columns >= col_lim are skipped (sharded halo)
+    const unsigned char *mask;     // PMODE: sflag (1 strong, 2 diagonal)
+    const double *dfinv;           // PMODE
+    const unsigned long long *rhoF;   // PMODE
+};
+struct SgY {
+    const int *rowptr, *col;
+    const double *val;
+    const int *agg;                // PMODE: P_tent
 };
 
-template <bool FILL>
-__global__ void __launch_bounds__(64) k_spgemm(int nrows, SgMat X, int xcol_lim, SgMat Y, int *__restrict__ cnt_out,
+// CAP: distinct columns a row may have (FILL is launched with the smallest
+// CAP that covers the longest row the COUNT pass found, so typical levels run
+// with a few KiB of LDS per wave and full occupancy); hash slots = 2 CAP.
+template <bool FILL, bool PMODE, int CAP>
+__global__ void __launch_bounds__(64) k_spgemm(int nrows, SgX X, SgY Y, int *__restrict__ cnt_out,
                                                const int *__restrict__ crow, int *__restrict__ ccol,
                                                double *__restrict__ cval, int *overflow)
 {
+    constexpr int kSgHash = 2 * CAP;
+    constexpr int kHashShift = 32 - ilog2(kSgHash);
     __shared__ int hk[kSgHash];
     __shared__ int hr[FILL ? kSgHash : 1];
-    __shared__ int lst[FILL ? kSgMax : 1], lslot[FILL ? kSgMax : 1];
-    __shared__ double acc[FILL ? kSgMax : 1];
+    __shared__ int lst[FILL ? CAP : 1], lslot[FILL ? CAP : 1];
+    __shared__ double acc[FILL ? CAP : 1];
     __shared__ int c_off[64], c_ys[64];
     __shared__ double c_xv[64];
-    __shared__ int s_rank[64];
+    __shared__ __attribute__((aligned(16))) int s_rank[64];
     __shared__ double s_val[64];
     __shared__ int s_cnt, s_ovf, s_m;
 
@@ -418,23 +370,28 @@ __global__ void __launch_bounds__(64) k_spgemm(int nrows, SgMat X, int xcol_lim,
     }
     __syncthreads();
     const int xs = X.rowptr[row], xe = X.rowptr[row + 1];
+    double omega = 0.0, dfi = 0.0;
+    if (PMODE) {
+        const double rF = rho_of(X.rhoF);
+        omega = rF > 0.0 ? (4.0 / 3.0) / rF : 0.0;
+        dfi = X.dfinv[row];
+    }
 
-    auto insert = [&](int key) -> int {
-        unsigned h = ((unsigned)key * 2654435761u) >> (32 - 10);
+    auto insert = [&](int key) {
+        unsigned h = ((unsigned)key * 2654435761u) >> kHashShift;
         for (int probe = 0; probe < kSgHash; ++probe) {
             const int old = atomicCAS(&hk[h], -1, key);
             if (old == -1) {
                 atomicAdd(&s_cnt, 1);
-                return (int)h;
+                return;
             }
-            if (old == key) return (int)h;
+            if (old == key) return;
             h = (h + 1) & (kSgHash - 1);
         }
         s_ovf = 1;
-        return -1;
     };
     auto lookup = [&](int key) -> int {
-        unsigned h = ((unsigned)key * 2654435761u) >> (32 - 10);
+        unsigned h = ((unsigned)key * 2654435761u) >> kHashShift;
         for (int probe = 0; probe < kSgHash; ++probe) {
             const int k = hk[h];
             if (k == key) return (int)h;
@@ -450,10 +407,19 @@ __global__ void __launch_bounds__(64) k_spgemm(int nrows, SgMat X, int xcol_lim,
         double xv = 0.0;
         if (e < xe) {
             const int k = X.col[e];
-            if (k < xcol_lim) {
-                ys = Y.rowptr[k];
-                len = Y.rowptr[k + 1] - ys;
-                xv = X.val ? X.val[e] : 0.0;
+            if (k < X.col_lim) {
+                if (PMODE) {
+                    const unsigned char f = X.mask[e];
+                    if (f != 0 && Y.agg[k] >= 0) {
+                        ys = k;
+                        len = 1;
+                        xv = (f == 2) ? 1.0 - omega : -omega * dfi * X.val[e];
+                    }
+                } else {
+                    ys = Y.rowptr[k];
+                    len = Y.rowptr[k + 1] - ys;
+                    xv = X.val[e];
+                }
             }
         }
         int incl = len;
@@ -471,15 +437,20 @@ __global__ void __launch_bounds__(64) k_spgemm(int nrows, SgMat X, int xcol_lim,
     };
     // product p of the staged group -> (column, value)
     auto product = [&](int p, int &key, double &v) {
-        int lo = 0, hi = 63;   // largest entry with c_off <= p
+        int lo = 0, hi = 63;   // largest staged entry with c_off <= p
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             if (c_off[mid] <= p) lo = mid;
             else hi = mid - 1;
         }
-        const int q = c_ys[lo] + (p - c_off[lo]);
-        key = Y.col[q];
-        if (FILL) v = c_xv[lo] * Y.val[q];
+        if (PMODE) {
+            key = Y.agg[c_ys[lo]];
+            v = c_xv[lo];
+        } else {
+            const int q = c_ys[lo] + (p - c_off[lo]);
+            key = Y.col[q];
+            if (FILL) v = c_xv[lo] * Y.val[q];
+        }
     };
 
     // pass 1: the set of output columns
@@ -496,7 +467,7 @@ __global__ void __launch_bounds__(64) k_spgemm(int nrows, SgMat X, int xcol_lim,
     if (!FILL) {
         if (lane == 0) {
             cnt_out[row] = s_cnt;
-            if (s_ovf || s_cnt > kSgMax) atomicOr(overflow, 1);
+            if (s_ovf || s_cnt > CAP) atomicOr(overflow, 1);
         }
         return;
     }
@@ -504,13 +475,13 @@ __global__ void __launch_bounds__(64) k_spgemm(int nrows, SgMat X, int xcol_lim,
     for (int t = lane; t < kSgHash; t += 64)
         if (hk[t] != -1) {
             const int m = atomicAdd(&s_m, 1);
-            if (m < kSgMax) {
+            if (m < CAP) {
                 lst[m] = hk[t];
                 lslot[m] = t;
             }
         }
     __syncthreads();
-    const int cnt = min(s_m, kSgMax);
+    const int cnt = min(s_m, CAP);
     const int cb = crow[row];
     for (int m = lane; m < cnt; m += 64) {
         const int key = lst[m];
@@ -522,6 +493,7 @@ __global__ void __launch_bounds__(64) k_spgemm(int nrows, SgMat X, int xcol_lim,
     }
     __syncthreads();
     // pass 2: values in enumeration order
+    const int4 *r4 = reinterpret_cast<const int4 *>(s_rank);
     for (int e0 = xs; e0 < xe; e0 += 64) {
         const int total = stage(e0);
         for (int p0 = 0; p0 < total; p0 += 64) {
@@ -538,14 +510,17 @@ __global__ void __launch_bounds__(64) k_spgemm(int nrows, SgMat X, int xcol_lim,
             s_val[lane] = v;
             __syncthreads();
             if (rank >= 0) {
-                const int m_end = min(64, total - p0);
                 bool leader = true;
                 double sum = 0.0;
-                for (int m = 0; m < m_end; ++m)
-                    if (s_rank[m] == rank) {
-                        if (m < lane) leader = false;
-                        sum += s_val[m];
-                    }
+#pragma unroll
+                for (int m4 = 0; m4 < 16; ++m4) {
+                    const int4 q = r4[m4];
+                    const int m = 4 * m4;
+                    if (q.x == rank) { leader &= (m < lane) ? false : true; sum += s_val[m]; }
+                    if (q.y == rank) { leader &= (m + 1 < lane) ? false : true; sum += s_val[m + 1]; }
+                    if (q.z == rank) { leader &= (m + 2 < lane) ? false : true; sum += s_val[m + 2]; }
+                    if (q.w == rank) { leader &= (m + 3 < lane) ? false : true; sum += s_val[m + 3]; }
+                }
                 if (leader) acc[rank] += sum;
             }
             __syncthreads();
@@ -568,46 +543,50 @@ __global__ void k_dense_scatter(int n, const int *__restrict__ rowptr, const int
         if (col[k] < n) M[(size_t)i * n + col[k]] += val[k];
 }
 
-// In-place Gauss-Jordan inversion without pivoting (the level operators are
-// symmetric positive semi-definite).  A pivot that vanishes relative to the
-// largest diagonal entry marks a null direction: its row and column are
-// zeroed, so the result is a generalised inverse on the range.
-__global__ void __launch_bounds__(1024) k_gauss_jordan(int n, double *__restrict__ M)
+// In-place Gauss-Jordan inversion in LDS without pivoting (the level
+// operators are symmetric positive semi-definite).  A pivot that vanishes
+// relative to the largest diagonal entry marks a null direction: its row and
+// column are zeroed, so the result is a generalised inverse on the range.
+__global__ void __launch_bounds__(1024) k_gauss_jordan(int n, double *__restrict__ Mg)
 {
+    __shared__ double M[kAmgDenseMax * kAmgDenseMax];
     __shared__ double rowk[kAmgDenseMax], colk[kAmgDenseMax];
-    __shared__ double s_maxd, s_piv;
+    __shared__ double s_maxd;
     const int tid = threadIdx.x;
+    const int nn = n * n;
+    for (int idx = tid; idx < nn; idx += blockDim.x) M[idx] = Mg[idx];
+    __syncthreads();
     if (tid == 0) {
         double m = 0.0;
-        for (int i = 0; i < n; ++i) m = fmax(m, fabs(M[(size_t)i * n + i]));
+        for (int i = 0; i < n; ++i) m = fmax(m, fabs(M[i * n + i]));
         s_maxd = m;
     }
     __syncthreads();
     for (int k = 0; k < n; ++k) {
-        if (tid == 0) s_piv = M[(size_t)k * n + k];
-        __syncthreads();
-        const double piv = s_piv;
+        const double piv = M[k * n + k];
         if (!(fabs(piv) > 1e-13 * s_maxd)) {
+            __syncthreads();
             for (int j = tid; j < n; j += blockDim.x) {
-                M[(size_t)k * n + j] = 0.0;
-                M[(size_t)j * n + k] = 0.0;
+                M[k * n + j] = 0.0;
+                M[j * n + k] = 0.0;
             }
             __syncthreads();
             continue;
         }
         const double ip = 1.0 / piv;
         for (int j = tid; j < n; j += blockDim.x) {
-            rowk[j] = (j == k ? 1.0 : M[(size_t)k * n + j]) * ip;
-            colk[j] = M[(size_t)j * n + k];
+            rowk[j] = (j == k ? 1.0 : M[k * n + j]) * ip;
+            colk[j] = M[j * n + k];
         }
         __syncthreads();
-        for (int idx = tid; idx < n * n; idx += blockDim.x) {
+        for (int idx = tid; idx < nn; idx += blockDim.x) {
             const int i = idx / n, j = idx - i * n;
             if (i == k) M[idx] = rowk[j];
             else M[idx] = (j == k ? 0.0 : M[idx]) - colk[i] * rowk[j];
         }
         __syncthreads();
     }
+    for (int idx = tid; idx < nn; idx += blockDim.x) Mg[idx] = M[idx];
 }
 
 // --------------------------------------------------------------------------
@@ -621,6 +600,21 @@ enum SmoothMode {
     kResidFromZero = 3    // x1 = w D^-1 b (written to out), r = b - A x1
 };
 
+template <int MODE>
+__device__ __forceinline__ void smooth_finish(int i, double ax, double w, const double *__restrict__ dinv,
+                                              const double *__restrict__ b, const double *__restrict__ x,
+                                              double *__restrict__ out, double *__restrict__ rout)
+{
+    constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
+    const double bi = b[i], di = dinv[i];
+    const double xi = implicit ? w * di * bi : x[i];
+    const double res = bi - ax;
+    if constexpr (MODE == kSweepFromZero || MODE == kSweep) out[i] = xi + w * di * res;
+    if constexpr (MODE == kResid || MODE == kResidFromZero) rout[i] = res;
+    if constexpr (MODE == kResidFromZero) out[i] = xi;
+}
+
+// level 0: CSR-stream tile SpMV (the PCG's kernel shape)
 template <int MODE>
 __global__ void __launch_bounds__(kCgBlock) k_amg_smooth(int n, int ncl, const int *__restrict__ rowptr,
                                                          const int *__restrict__ col, const double *__restrict__ val,
@@ -641,37 +635,55 @@ __global__ void __launch_bounds__(kCgBlock) k_amg_smooth(int n, int ncl, const i
     else
         ax = cg_tile_spmv(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; }, lds);
     const int i = r0 + threadIdx.x;
-    if (i >= n) return;
-    const double bi = b[i], di = dinv[i];
-    const double xi = implicit ? w * di * bi : x[i];
-    const double res = bi - ax;
-    if constexpr (MODE == kSweepFromZero || MODE == kSweep) out[i] = xi + w * di * res;
-    if constexpr (MODE == kResid || MODE == kResidFromZero) rout[i] = res;
-    if constexpr (MODE == kResidFromZero) out[i] = xi;
+    if (i < n) smooth_finish<MODE>(i, ax, w, dinv, b, x, out, rout);
 }
 
-__global__ void k_amg_restrict(int nc, const int *__restrict__ rrow, const int *__restrict__ rcol,
-                               const double *__restrict__ rval, const double *__restrict__ r, double *__restrict__ bc,
-                               const int *done)
+// G lanes per row, strided over the row, butterfly sum inside the group
+template <int G, class XF>
+__device__ __forceinline__ double group_row_dot(int i, int n, const int *__restrict__ rowptr,
+                                                const int *__restrict__ col, const double *__restrict__ val, XF X)
 {
-    if (done && *done) return;
-    const int I = blockIdx.x * blockDim.x + threadIdx.x;
-    if (I >= nc) return;
+    const int g = threadIdx.x & (G - 1);
     double s = 0.0;
-    for (int k = rrow[I]; k < rrow[I + 1]; ++k) s += rval[k] * r[rcol[k]];
-    bc[I] = s;
+    if (i < n)
+        for (int k = rowptr[i] + g; k < rowptr[i + 1]; k += G) s += val[k] * X(col[k]);
+#pragma unroll
+    for (int off = G >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    return s;
 }
 
-__global__ void k_amg_prolong(int n, const int *__restrict__ prow, const int *__restrict__ pcol,
-                              const double *__restrict__ pval, const double *__restrict__ xc, double *__restrict__ x,
-                              const int *done)
+// coarse levels: G lanes per row
+template <int MODE, int G>
+__global__ void __launch_bounds__(256) k_amg_smooth_g(int n, int ncl, const int *__restrict__ rowptr,
+                                                      const int *__restrict__ col, const double *__restrict__ val,
+                                                      const double *__restrict__ dinv, const unsigned long long *rho,
+                                                      const double *__restrict__ b, const double *__restrict__ x,
+                                                      double *__restrict__ out, double *__restrict__ rout,
+                                                      const int *done)
 {
     if (done && *done) return;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    double s = 0.0;
-    for (int k = prow[i]; k < prow[i + 1]; ++k) s += pval[k] * xc[pcol[k]];
-    x[i] += s;
+    const double ra = rho_of(rho);
+    const double w = ra > 0.0 ? 1.0 / ra : 0.0;
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+    constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
+    double ax;
+    if constexpr (implicit)
+        ax = group_row_dot<G>(i, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; });
+    else
+        ax = group_row_dot<G>(i, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; });
+    if (i < n && (threadIdx.x & (G - 1)) == 0) smooth_finish<MODE>(i, ax, w, dinv, b, x, out, rout);
+}
+
+// y = M x (ACC: y += M x), G lanes per row (restriction R r, prolongation x += P xc)
+template <int G, bool ACC>
+__global__ void __launch_bounds__(256) k_csr_mv_g(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                  const double *__restrict__ val, const double *__restrict__ x,
+                                                  double *__restrict__ y, const int *done)
+{
+    if (done && *done) return;
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const double s = group_row_dot<G>(i, n, rowptr, col, val, [&](int j) { return x[j]; });
+    if (i < n && (threadIdx.x & (G - 1)) == 0) y[i] = ACC ? y[i] + s : s;
 }
 
 // x = M b, one wavefront per row of the dense coarsest inverse
@@ -732,6 +744,63 @@ int read_flag(Amg &A, hipStream_t s, int idx, int &v)
     return XFK_OK;
 }
 
+// C = X Y (rowptr/col/val allocated here); XFK_ERR_UNSUPPORTED on LDS overflow
+template <bool PMODE>
+int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<int> &crow, DBuf<int> &ccol,
+           DBuf<double> &cval, long long &cnnz)
+{
+    AMG_CHECK(M.cnt.alloc((size_t)nrows + 1));
+    AMG_CHECK(hipMemsetAsync(M.dev_int.p + 2, 0, 2 * sizeof(int), s));
+    if (nrows > 0)
+        k_spgemm<false, PMODE, kSgMax><<<nrows, 64, 0, s>>>(nrows, X, Y, M.cnt.p, nullptr, nullptr, nullptr,
+                                                            M.dev_int.p + 2);
+    AMG_CHECK(crow.alloc((size_t)nrows + 1));
+    if (nrows > 0) {   // longest row -> LDS capacity of the FILL pass
+        size_t bytes = 0;
+        AMG_CHECK(hipcub::DeviceReduce::Max(nullptr, bytes, M.cnt.p, M.dev_int.p + 3, nrows, s));
+        AMG_CHECK(M.cub_tmp.alloc(bytes ? bytes : 1));
+        AMG_CHECK(hipcub::DeviceReduce::Max(M.cub_tmp.p, bytes, M.cnt.p, M.dev_int.p + 3, nrows, s));
+    }
+    AMG_CHECK(hipMemcpyAsync(M.host_int + 2, M.dev_int.p + 2, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    int rc = scan_total(M, s, M.cnt.p, crow.p, nrows, cnnz);   // synchronises
+    if (rc != XFK_OK) return rc;
+    const int ovf = M.host_int[2], maxrow = M.host_int[3];
+    if (ovf) {
+        set_error("AMG: a SpGEMM row exceeds the LDS hash capacity");
+        return XFK_ERR_UNSUPPORTED;
+    }
+    AMG_CHECK(ccol.alloc((size_t)std::max(1LL, cnnz)));
+    AMG_CHECK(cval.alloc((size_t)std::max(1LL, cnnz)));
+    if (nrows > 0) {
+        int *of = M.dev_int.p + 2;
+        if (maxrow <= 32)
+            k_spgemm<true, PMODE, 32><<<nrows, 64, 0, s>>>(nrows, X, Y, nullptr, crow.p, ccol.p, cval.p, of);
+        else if (maxrow <= 128)
+            k_spgemm<true, PMODE, 128><<<nrows, 64, 0, s>>>(nrows, X, Y, nullptr, crow.p, ccol.p, cval.p, of);
+        else
+            k_spgemm<true, PMODE, kSgMax><<<nrows, 64, 0, s>>>(nrows, X, Y, nullptr, crow.p, ccol.p, cval.p, of);
+    }
+    return XFK_OK;
+}
+
+// lanes per row for a CSR with this many nonzeros per row on average
+int lanes_for(double per_row)
+{
+    return per_row <= 6.0 ? 4 : (per_row <= 20.0 ? 8 : 16);
+}
+
+void launch_mv(hipStream_t s, int n, const int *rowptr, const int *col, const double *val, const double *x, double *y,
+               bool acc, int G, const int *done)
+{
+    if (n <= 0) return;
+    const int g = (int)(((long long)n * G + 255) / 256);
+#define XFK_MV(GG)                                                                                        \
+    if (acc) k_csr_mv_g<GG, true><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);                    \
+    else k_csr_mv_g<GG, false><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+    if (G == 4) { XFK_MV(4) } else if (G == 8) { XFK_MV(8) } else { XFK_MV(16) }
+#undef XFK_MV
+}
+
 }  // namespace
 
 int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *col0, const double *val0,
@@ -759,6 +828,7 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
         const int n = A.n;
         stats.n[l] = n;
         stats.nnz[l] = A.nnz;
+        A.nc = 0;
         AMG_CHECK(A.dinv.alloc(n));
         AMG_CHECK(absd.alloc(n));
         AMG_CHECK(dfinv.alloc(n));
@@ -777,10 +847,9 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
         AMG_CHECK(t1.alloc(n));
         k_mis_init<<<nb(n), kB, 0, s>>>(n, cnt.p, key.p);
         int rounds = 0;
-        for (;;) {
-            for (int b = 0; b < 4; ++b, ++rounds) {
-                AMG_CHECK(hipMemsetAsync(dev_int.p, 0, sizeof(int), s));
-                k_mis_max<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p);
+        for (int batch = 6;; batch = 2) {
+            for (int b = 0; b < batch; ++b, ++rounds) {
+                k_mis_max<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, dev_int.p);
                 k_mis_update<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, dev_int.p);
             }
             int und = 0;
@@ -804,17 +873,11 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
         AMG_CHECK(agg.alloc(n));
         k_agg_join1<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, cursor.p, agg1.p);
         k_agg_join2<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, agg1.p, agg.p);
-        // P
-        PEnt E{A.col, A.val, sflag.p, agg.p};
-        k_p_count<<<nb(n), kB, 0, s>>>(n, A.rowptr, E, cnt.p);
-        AMG_CHECK(A.prow.alloc((size_t)n + 1));
-        long long pnnz = 0;
-        if ((rc = scan_total(*this, s, cnt.p, A.prow.p, n, pnnz)) != XFK_OK) return rc;
+        // P = (I - omega D_F^-1 A_F) P_tent
+        SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, rho.p + 2 * l + 1};
+        SgY YT{nullptr, nullptr, nullptr, agg.p};
+        if ((rc = spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz)) != XFK_OK) return rc;
         A.nc = (int)nc;
-        A.pnnz = pnnz;
-        AMG_CHECK(A.pcol.alloc((size_t)std::max(1LL, pnnz)));
-        AMG_CHECK(A.pval.alloc((size_t)std::max(1LL, pnnz)));
-        k_p_fill<<<nb(n), kB, 0, s>>>(n, A.rowptr, E, dfinv.p, rho.p + 2 * l, A.prow.p, A.pcol.p, A.pval.p);
         // R = P^T
         AMG_CHECK(cnt.alloc((size_t)std::max<long long>(n, nc) + 1));
         AMG_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * (nc + 1), s));
@@ -826,41 +889,19 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
         AMG_CHECK(A.rval.alloc((size_t)std::max(1LL, rnnz)));
         AMG_CHECK(hipMemsetAsync(cursor.p, 0, sizeof(int) * (nc + 1), s));
         k_rt_fill<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, A.rrow.p, cursor.p, A.rcol.p);
-        k_rt_sort_vals<<<nb(nc), kB, 0, s>>>((int)nc, A.rrow.p, A.rcol.p, A.prow.p, A.pcol.p, A.pval.p, A.rval.p);
-        // AP = A P
-        AMG_CHECK(hipMemsetAsync(dev_int.p + 2, 0, sizeof(int), s));
-        SgMat SA{A.rowptr, A.col, A.val}, SP{A.prow.p, A.pcol.p, A.pval.p};
-        k_spgemm<false><<<n, 64, 0, s>>>(n, SA, A.ncol_lim, SP, cnt.p, nullptr, nullptr, nullptr, dev_int.p + 2);
-        AMG_CHECK(ap_row.alloc((size_t)n + 1));
+        k_rt_sort_vals<<<(int)((nc * 64 + 255) / 256), 256, 0, s>>>((int)nc, A.rrow.p, A.rcol.p, A.prow.p, A.pcol.p,
+                                                                   A.pval.p, A.rval.p);
+        // AP = A P, then A_c = R (A P)
+        SgX XA{A.rowptr, A.col, A.val, A.ncol_lim, nullptr, nullptr, nullptr};
+        SgY YP{A.prow.p, A.pcol.p, A.pval.p, nullptr};
         long long apnnz = 0;
-        if ((rc = scan_total(*this, s, cnt.p, ap_row.p, n, apnnz)) != XFK_OK) return rc;
-        int ovf = 0;
-        if ((rc = read_flag(*this, s, 2, ovf)) != XFK_OK) return rc;
-        if (ovf) {
-            set_error("AMG: a row of A*P exceeds the SpGEMM LDS capacity");
-            return XFK_ERR_UNSUPPORTED;
-        }
-        AMG_CHECK(ap_col.alloc((size_t)std::max(1LL, apnnz)));
-        AMG_CHECK(ap_val.alloc((size_t)std::max(1LL, apnnz)));
-        k_spgemm<true><<<n, 64, 0, s>>>(n, SA, A.ncol_lim, SP, nullptr, ap_row.p, ap_col.p, ap_val.p, dev_int.p + 2);
-        // A_c = R (A P)
+        if ((rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, apnnz)) != XFK_OK) return rc;
         if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
         AmgLevel &C = *L[l + 1];
-        SgMat SR{A.rrow.p, A.rcol.p, A.rval.p}, SAP{ap_row.p, ap_col.p, ap_val.p};
-        k_spgemm<false><<<(int)nc, 64, 0, s>>>((int)nc, SR, INT_MAX, SAP, cnt.p, nullptr, nullptr, nullptr,
-                                               dev_int.p + 2);
-        AMG_CHECK(C.rowptr_o.alloc((size_t)nc + 1));
+        SgX XR{A.rrow.p, A.rcol.p, A.rval.p, INT_MAX, nullptr, nullptr, nullptr};
+        SgY YAP{ap_row.p, ap_col.p, ap_val.p, nullptr};
         long long cnnz = 0;
-        if ((rc = scan_total(*this, s, cnt.p, C.rowptr_o.p, (int)nc, cnnz)) != XFK_OK) return rc;
-        if ((rc = read_flag(*this, s, 2, ovf)) != XFK_OK) return rc;
-        if (ovf) {
-            set_error("AMG: a row of the Galerkin product exceeds the SpGEMM LDS capacity");
-            return XFK_ERR_UNSUPPORTED;
-        }
-        AMG_CHECK(C.col_o.alloc((size_t)std::max(1LL, cnnz)));
-        AMG_CHECK(C.val_o.alloc((size_t)std::max(1LL, cnnz)));
-        k_spgemm<true><<<(int)nc, 64, 0, s>>>((int)nc, SR, INT_MAX, SAP, nullptr, C.rowptr_o.p, C.col_o.p, C.val_o.p,
-                                              dev_int.p + 2);
+        if ((rc = spgemm<false>(*this, s, (int)nc, XR, YAP, C.rowptr_o, C.col_o, C.val_o, cnnz)) != XFK_OK) return rc;
         C.n = (int)nc;
         C.nnz = cnnz;
         C.ncol_lim = (int)nc;
@@ -873,7 +914,6 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
     double tot = 0;
     for (int k = 0; k < nlev; ++k) tot += (double)stats.nnz[k];
     stats.op_complexity = nnz0 > 0 ? tot / (double)nnz0 : 0.0;
-    // vectors
     for (int k = 0; k < nlev; ++k) {
         AmgLevel &A = *L[k];
         AMG_CHECK(A.xa.alloc((size_t)A.n));
@@ -894,27 +934,37 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
 
 namespace {
 
-void launch_smooth(hipStream_t s, int mode, const AmgLevel &A, const unsigned long long *rho, const double *b,
+template <int MODE>
+void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
+                     const double *x, double *out, double *rout, const int *done)
+{
+    if (l == 0) {
+        const int g = (A.n + kCgBlock - 1) / kCgBlock;
+        k_amg_smooth<MODE><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
+                                                  rout, done);
+        return;
+    }
+    const int G = lanes_for(A.n > 0 ? (double)A.nnz / A.n : 1.0);
+    const int g = (int)(((long long)A.n * G + 255) / 256);
+    if (G == 4)
+        k_amg_smooth_g<MODE, 4><<<g, 256, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
+                                                 rout, done);
+    else if (G == 8)
+        k_amg_smooth_g<MODE, 8><<<g, 256, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
+                                                 rout, done);
+    else
+        k_amg_smooth_g<MODE, 16><<<g, 256, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
+                                                  out, rout, done);
+}
+
+void launch_smooth(hipStream_t s, int mode, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
                    const double *x, double *out, double *rout, const int *done)
 {
-    const int g = (A.n + kCgBlock - 1) / kCgBlock;
     switch (mode) {
-    case kSweepFromZero:
-        k_amg_smooth<kSweepFromZero><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho,
-                                                            b, x, out, rout, done);
-        break;
-    case kSweep:
-        k_amg_smooth<kSweep><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
-                                                    out, rout, done);
-        break;
-    case kResid:
-        k_amg_smooth<kResid><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
-                                                    out, rout, done);
-        break;
-    default:
-        k_amg_smooth<kResidFromZero><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho,
-                                                            b, x, out, rout, done);
-        break;
+    case kSweepFromZero: launch_smooth_t<kSweepFromZero>(s, l, A, rho, b, x, out, rout, done); break;
+    case kSweep: launch_smooth_t<kSweep>(s, l, A, rho, b, x, out, rout, done); break;
+    case kResid: launch_smooth_t<kResid>(s, l, A, rho, b, x, out, rout, done); break;
+    default: launch_smooth_t<kResidFromZero>(s, l, A, rho, b, x, out, rout, done); break;
     }
 }
 
@@ -936,10 +986,10 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
         }
         // smoother-only coarsest level: 2 nu sweeps from zero
         double *cur = A.xa.p;
-        launch_smooth(s, kSweepFromZero, A, rho, b, nullptr, cur, nullptr, done);
+        launch_smooth(s, kSweepFromZero, l, A, rho, b, nullptr, cur, nullptr, done);
         for (int k = 2; k < 2 * nu; ++k) {
             double *nx = (k == 2 * nu - 1 && l == 0) ? out0 : other(cur);
-            launch_smooth(s, kSweep, A, rho, b, cur, nx, nullptr, done);
+            launch_smooth(s, kSweep, l, A, rho, b, cur, nx, nullptr, done);
             cur = nx;
         }
         if (l == 0 && cur != out0)
@@ -949,23 +999,24 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     // pre-smoothing (nu sweeps from zero) and residual
     double *cur = A.xa.p;
     if (nu == 1) {
-        launch_smooth(s, kResidFromZero, A, rho, b, nullptr, cur, A.r.p, done);
+        launch_smooth(s, kResidFromZero, l, A, rho, b, nullptr, cur, A.r.p, done);
     } else {
-        launch_smooth(s, kSweepFromZero, A, rho, b, nullptr, cur, nullptr, done);
+        launch_smooth(s, kSweepFromZero, l, A, rho, b, nullptr, cur, nullptr, done);
         for (int k = 2; k < nu; ++k) {
             double *nx = other(cur);
-            launch_smooth(s, kSweep, A, rho, b, cur, nx, nullptr, done);
+            launch_smooth(s, kSweep, l, A, rho, b, cur, nx, nullptr, done);
             cur = nx;
         }
-        launch_smooth(s, kResid, A, rho, b, cur, nullptr, A.r.p, done);
+        launch_smooth(s, kResid, l, A, rho, b, cur, nullptr, A.r.p, done);
     }
     AmgLevel &C = *M.L[l + 1];
-    k_amg_restrict<<<nb(A.nc), kB, 0, s>>>(A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, done);
+    const long long rnnz = A.pnnz;
+    launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false, lanes_for((double)rnnz / A.nc), done);
     const double *xc = vcycle_level(M, s, l + 1, C.b.p, nullptr, done);
-    k_amg_prolong<<<nb(A.n), kB, 0, s>>>(A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, done);
+    launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)rnnz / A.n), done);
     for (int k = 0; k < nu; ++k) {
         double *nx = (k == nu - 1 && l == 0) ? out0 : other(cur);
-        launch_smooth(s, kSweep, A, rho, b, cur, nx, nullptr, done);
+        launch_smooth(s, kSweep, l, A, rho, b, cur, nx, nullptr, done);
         cur = nx;
     }
     return cur;
