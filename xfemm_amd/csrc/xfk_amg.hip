@@ -529,6 +529,214 @@ __global__ void __launch_bounds__(64) k_spgemm(int nrows, SgX X, SgY Y, int *__r
     for (int m = lane; m < cnt; m += 64) cval[cb + m] = acc[m];
 }
 
+// Products per row (upper bound of the output row length), for the choice
+// between the sub-wave and the wave-per-row SpGEMM.
+template <bool PMODE>
+__global__ void k_spgemm_nprod(int nrows, SgX X, SgY Y, int *__restrict__ nprod)
+{
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= nrows) return;
+    int c = 0;
+    for (int e = X.rowptr[row]; e < X.rowptr[row + 1]; ++e) {
+        const int k = X.col[e];
+        if (k >= X.col_lim) continue;
+        if (PMODE) c += (X.mask[e] != 0 && Y.agg[k] >= 0);
+        else c += Y.rowptr[k + 1] - Y.rowptr[k];
+    }
+    nprod[row] = c;
+}
+
+// Sub-wave SpGEMM for rows of at most 64 products (the fine levels: A P,
+// the prolongator): G lanes per row, 64 / G rows per wavefront, the same
+// enumeration / hash / ordered accumulation as k_spgemm within each group.
+// Groups of one wavefront advance independently; their LDS regions are
+// private, and LDS traffic inside a wavefront is ordered, so no workgroup
+// barriers are needed (wave_barrier keeps the compiler from reordering).
+constexpr int kSwCap = 64;
+constexpr int kSwHash = 2 * kSwCap;
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool FILL, bool PMODE, int G>
+__global__ void __launch_bounds__(64) k_spgemm_sw(int nrows, SgX X, SgY Y, int *__restrict__ cnt_out,
+                                                  const int *__restrict__ crow, int *__restrict__ ccol,
+                                                  double *__restrict__ cval)
+{
+    constexpr int W = 64 / G;
+    constexpr int kShift = 32 - ilog2(kSwHash);
+    __shared__ int hk_all[W][kSwHash];
+    __shared__ int hr_all[FILL ? W : 1][kSwHash];
+    __shared__ int lst_all[FILL ? W : 1][kSwCap];
+    __shared__ int lslot_all[FILL ? W : 1][kSwCap];
+    __shared__ double acc_all[FILL ? W : 1][kSwCap];
+    __shared__ int c_off_all[W][G], c_ys_all[W][G];
+    __shared__ double c_xv_all[W][G];
+    __shared__ int s_rank_all[W][G];
+    __shared__ double s_val_all[W][G];
+    __shared__ int s_cnt_all[W], s_m_all[W];
+
+    const int g = threadIdx.x / G, l = threadIdx.x % G;
+    const int row = blockIdx.x * W + g;
+    const bool active = row < nrows;
+    int *hk = hk_all[g];
+    int *hr = hr_all[FILL ? g : 0];
+    int *lst = lst_all[FILL ? g : 0];
+    int *lslot = lslot_all[FILL ? g : 0];
+    double *acc = acc_all[FILL ? g : 0];
+    int *c_off = c_off_all[g], *c_ys = c_ys_all[g];
+    double *c_xv = c_xv_all[g];
+    int *s_rank = s_rank_all[g];
+    double *s_val = s_val_all[g];
+    for (int t = l; t < kSwHash; t += G) hk[t] = -1;
+    if (l == 0) {
+        s_cnt_all[g] = 0;
+        s_m_all[g] = 0;
+    }
+    wave_lds_sync();
+    if (!active) return;
+    const int xs = X.rowptr[row], xe = X.rowptr[row + 1];
+    double omega = 0.0, dfi = 0.0;
+    if (PMODE) {
+        const double rF = rho_of(X.rhoF);
+        omega = rF > 0.0 ? (4.0 / 3.0) / rF : 0.0;
+        dfi = X.dfinv[row];
+    }
+    auto insert = [&](int key) {
+        unsigned h = ((unsigned)key * 2654435761u) >> kShift;
+        for (;;) {   // at most 64 keys in 128 slots: a free slot always exists
+            const int old = atomicCAS(&hk[h], -1, key);
+            if (old == -1) {
+                atomicAdd(&s_cnt_all[g], 1);
+                return;
+            }
+            if (old == key) return;
+            h = (h + 1) & (kSwHash - 1);
+        }
+    };
+    auto lookup = [&](int key) -> int {
+        unsigned h = ((unsigned)key * 2654435761u) >> kShift;
+        while (hk[h] != key) h = (h + 1) & (kSwHash - 1);
+        return (int)h;
+    };
+    // stage G X entries of [e0, xe) (group-wide prefix sum of their Y-row lengths)
+    auto stage = [&](int e0) -> int {
+        const int e = e0 + l;
+        int len = 0, ys = 0;
+        double xv = 0.0;
+        if (e < xe) {
+            const int k = X.col[e];
+            if (k < X.col_lim) {
+                if (PMODE) {
+                    const unsigned char f = X.mask[e];
+                    if (f != 0 && Y.agg[k] >= 0) {
+                        ys = k;
+                        len = 1;
+                        xv = (f == 2) ? 1.0 - omega : -omega * dfi * X.val[e];
+                    }
+                } else {
+                    ys = Y.rowptr[k];
+                    len = Y.rowptr[k + 1] - ys;
+                    xv = X.val[e];
+                }
+            }
+        }
+        int incl = len;
+#pragma unroll
+        for (int off = 1; off < G; off <<= 1) {
+            const int t = __shfl_up(incl, off, G);
+            if (l >= off) incl += t;
+        }
+        const int total = __shfl(incl, G - 1, G);
+        c_off[l] = incl - len;
+        c_ys[l] = ys;
+        c_xv[l] = xv;
+        wave_lds_sync();
+        return total;
+    };
+    auto product = [&](int p, int &key, double &v) {
+        int lo = 0, hi = G - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (c_off[mid] <= p) lo = mid;
+            else hi = mid - 1;
+        }
+        if (PMODE) {
+            key = Y.agg[c_ys[lo]];
+            v = c_xv[lo];
+        } else {
+            const int q = c_ys[lo] + (p - c_off[lo]);
+            key = Y.col[q];
+            if (FILL) v = c_xv[lo] * Y.val[q];
+        }
+    };
+    for (int e0 = xs; e0 < xe; e0 += G) {
+        const int total = stage(e0);
+        for (int p = l; p < total; p += G) {
+            int key;
+            double v;
+            product(p, key, v);
+            insert(key);
+        }
+        wave_lds_sync();
+    }
+    if (!FILL) {
+        if (l == 0) cnt_out[row] = s_cnt_all[g];
+        return;
+    }
+    for (int t = l; t < kSwHash; t += G)
+        if (hk[t] != -1) {
+            const int m = atomicAdd(&s_m_all[g], 1);
+            lst[m] = hk[t];
+            lslot[m] = t;
+        }
+    wave_lds_sync();
+    const int cnt = s_m_all[g];
+    const int cb = crow[row];
+    for (int m = l; m < cnt; m += G) {
+        const int key = lst[m];
+        int rank = 0;
+        for (int q = 0; q < cnt; ++q) rank += lst[q] < key;
+        hr[lslot[m]] = rank;
+        ccol[cb + rank] = key;
+        acc[rank] = 0.0;
+    }
+    wave_lds_sync();
+    for (int e0 = xs; e0 < xe; e0 += G) {
+        const int total = stage(e0);
+        for (int p0 = 0; p0 < total; p0 += G) {
+            const int p = p0 + l;
+            int rank = -1;
+            double v = 0.0;
+            if (p < total) {
+                int key;
+                product(p, key, v);
+                rank = hr[lookup(key)];
+            }
+            s_rank[l] = rank;
+            s_val[l] = v;
+            wave_lds_sync();
+            if (rank >= 0) {
+                bool leader = true;
+                double sum = 0.0;
+#pragma unroll
+                for (int m = 0; m < G; ++m)
+                    if (s_rank[m] == rank) {
+                        leader &= !(m < l);
+                        sum += s_val[m];
+                    }
+                if (leader) acc[rank] += sum;
+            }
+            wave_lds_sync();
+        }
+    }
+    for (int m = l; m < cnt; m += G) cval[cb + m] = acc[m];
+}
+
 // --------------------------------------------------------------------------
 // setup: coarsest level, dense inverse
 // --------------------------------------------------------------------------
@@ -749,13 +957,31 @@ template <bool PMODE>
 int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<int> &crow, DBuf<int> &ccol,
            DBuf<double> &cval, long long &cnnz)
 {
+    constexpr int G = 8;
     AMG_CHECK(M.cnt.alloc((size_t)nrows + 1));
-    AMG_CHECK(hipMemsetAsync(M.dev_int.p + 2, 0, 2 * sizeof(int), s));
-    if (nrows > 0)
-        k_spgemm<false, PMODE, kSgMax><<<nrows, 64, 0, s>>>(nrows, X, Y, M.cnt.p, nullptr, nullptr, nullptr,
-                                                            M.dev_int.p + 2);
     AMG_CHECK(crow.alloc((size_t)nrows + 1));
-    if (nrows > 0) {   // longest row -> LDS capacity of the FILL pass
+    // longest product list -> sub-wave (<= 64 products per row) or wave-per-row kernels
+    int maxprod = 0;
+    if (nrows > 0) {
+        k_spgemm_nprod<PMODE><<<nb(nrows), kB, 0, s>>>(nrows, X, Y, M.cnt.p);
+        size_t bytes = 0;
+        AMG_CHECK(hipcub::DeviceReduce::Max(nullptr, bytes, M.cnt.p, M.dev_int.p + 3, nrows, s));
+        AMG_CHECK(M.cub_tmp.alloc(bytes ? bytes : 1));
+        AMG_CHECK(hipcub::DeviceReduce::Max(M.cub_tmp.p, bytes, M.cnt.p, M.dev_int.p + 3, nrows, s));
+        int rc = read_flag(M, s, 3, maxprod);
+        if (rc != XFK_OK) return rc;
+    }
+    const bool sub = maxprod <= kSwCap;
+    const int gsw = (nrows + 64 / G - 1) / (64 / G);
+    AMG_CHECK(hipMemsetAsync(M.dev_int.p + 2, 0, 2 * sizeof(int), s));
+    if (nrows > 0) {
+        if (sub)
+            k_spgemm_sw<false, PMODE, G><<<gsw, 64, 0, s>>>(nrows, X, Y, M.cnt.p, nullptr, nullptr, nullptr);
+        else
+            k_spgemm<false, PMODE, kSgMax><<<nrows, 64, 0, s>>>(nrows, X, Y, M.cnt.p, nullptr, nullptr, nullptr,
+                                                                M.dev_int.p + 2);
+    }
+    if (nrows > 0 && !sub) {   // longest row -> LDS capacity of the FILL pass
         size_t bytes = 0;
         AMG_CHECK(hipcub::DeviceReduce::Max(nullptr, bytes, M.cnt.p, M.dev_int.p + 3, nrows, s));
         AMG_CHECK(M.cub_tmp.alloc(bytes ? bytes : 1));
@@ -764,7 +990,7 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     AMG_CHECK(hipMemcpyAsync(M.host_int + 2, M.dev_int.p + 2, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     int rc = scan_total(M, s, M.cnt.p, crow.p, nrows, cnnz);   // synchronises
     if (rc != XFK_OK) return rc;
-    const int ovf = M.host_int[2], maxrow = M.host_int[3];
+    const int ovf = sub ? 0 : M.host_int[2], maxrow = sub ? maxprod : M.host_int[3];
     if (ovf) {
         set_error("AMG: a SpGEMM row exceeds the LDS hash capacity");
         return XFK_ERR_UNSUPPORTED;
@@ -773,7 +999,9 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     AMG_CHECK(cval.alloc((size_t)std::max(1LL, cnnz)));
     if (nrows > 0) {
         int *of = M.dev_int.p + 2;
-        if (maxrow <= 32)
+        if (sub)
+            k_spgemm_sw<true, PMODE, G><<<gsw, 64, 0, s>>>(nrows, X, Y, nullptr, crow.p, ccol.p, cval.p);
+        else if (maxrow <= 32)
             k_spgemm<true, PMODE, 32><<<nrows, 64, 0, s>>>(nrows, X, Y, nullptr, crow.p, ccol.p, cval.p, of);
         else if (maxrow <= 128)
             k_spgemm<true, PMODE, 128><<<nrows, 64, 0, s>>>(nrows, X, Y, nullptr, crow.p, ccol.p, cval.p, of);
