@@ -44,12 +44,13 @@ def _hip_sync():
     lib.hipDeviceSynchronize()
 
 
-def spmv_bytes(n_rows, nnz):
+def spmv_bytes(n_rows, nnz, amg=False):
     """Algorithmic HBM bytes of one CSR SpMV launch of the PCG (k_cg_spmv,
     xfemm_amd/csrc/xfk_pcg.hip): val 8 B + col 4 B per nonzero, rowptr 4 B per
     row (+1), u read once 8 B per row, w written 8 B per row (the fused u.w
-    partial re-reads u from cache)."""
-    return 12 * nnz + 4 * (n_rows + 1) + 16 * n_rows
+    partial re-reads u from cache); with the AMG preconditioner the launch
+    also reads r (8 B per row) for the fused r.u partial."""
+    return 12 * nnz + 4 * (n_rows + 1) + (24 if amg else 16) * n_rows
 
 
 class stdout_to_stderr:
@@ -83,16 +84,33 @@ def cpu_baseline(n_cells, nonlinear):
         _, st, _ = oracle.solve(pr, mesh, "reference" if kind == "reference" else "oracle")
         dt = time.perf_counter() - t0
     dof = len(mesh.x)
+    iters = (", %d PCG iters" % st["cg_iters"]) if st["cg_iters"] >= 0 else ""
     return {
         "value": dof / dt,
         "unit": "DoF/s",
         "cores": 1,
         "kind": kind,
-        "sample": "%dx%d-cell square (%d tri, %d DoF)%s: full Static2D (assembly + SSOR-PCG to 1e-8, %d PCG iters) "
+        "sample": "%dx%d-cell square (%d tri, %d DoF)%s: full Static2D (assembly + SSOR-PCG to 1e-8%s) "
                   "in %.1f s; smaller than the GPU workload, so fewer iterations per DoF (favours the CPU)"
-                  % (n_cells, n_cells, 2 * n_cells * n_cells, dof, " M-19" if nonlinear else "",
-                     st["cg_iters"] if st["cg_iters"] >= 0 else -1, dt),
+                  % (n_cells, n_cells, 2 * n_cells * n_cells, dof, " M-19" if nonlinear else "", iters, dt),
     }
+
+
+def pmc_traffic(kernel="k_cg_spmv"):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*_pmc_summary.json, written by tools/profile.sh from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench, gfx950-corrected)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), key=os.path.getmtime)
+    for path in reversed(paths):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if kernel in d:
+            return d[kernel]["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def main():
@@ -102,7 +120,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cells", type=int, default=1000, help="cells per side (2*cells^2 triangles)")
     ap.add_argument("--nonlinear", action="store_true", help="M-19 B-H steel (configs[3])")
-    ap.add_argument("--cpu-cells", type=int, default=500)
+    ap.add_argument("--cpu-cells", type=int, default=700)
+    ap.add_argument("--precond", choices=["amg", "jacobi"], default="amg",
+                    help="device preconditioner of the PCG (the reference uses SSOR)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per SpMV launch from a PMC pass (profiles/), if measured")
@@ -137,12 +157,12 @@ def main():
             uid = box[0]
         with stdout_to_stderr():
             comm = kernels.Comm.rccl(uid, rank, world, local)
-        P = kernels.Static2DProblem(device=local, comm=comm, **kw)
+        P = kernels.Static2DProblem(device=local, comm=comm, precond=args.precond, **kw)
         n_dof = P.n_nodes                       # global DoF of the sharded mesh
     else:
         cells = args.cells
         kw = synth.magnetostatic(cells, nonlinear=args.nonlinear)
-        P = kernels.Static2DProblem(device=local, **kw)
+        P = kernels.Static2DProblem(device=local, precond=args.precond, **kw)
         n_dof = P.n_nodes
 
     def barrier():
@@ -170,9 +190,11 @@ def main():
         1, sum(r["spmv_samples"] for r in results))
     nnz = results[-1]["nnz"]
     rows = P.n_rows
-    algo = spmv_bytes(rows, nnz)
+    amg = results[-1]["precond"] == kernels.XFK_PRECOND_AMG
+    algo = spmv_bytes(rows, nnz, amg)
     achieved = algo / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
     ms_step = 1e3 * elapsed / args.steps
+    traffic, traffic_src = (args.traffic, "--traffic") if args.traffic is not None else pmc_traffic()
     value = (1 if sharded else world) * n_dof * args.steps / elapsed
     pcg_iters = results[-1]["cg_iters"]
 
@@ -181,7 +203,7 @@ def main():
         # strong-scaling reference: rank 0 alone on the same mesh (after the timed region)
         P.close()
         if rank == 0:
-            Q = kernels.Static2DProblem(device=local, **kw)
+            Q = kernels.Static2DProblem(device=local, precond=args.precond, **kw)
             Q.solve(rebuild_symbolic=True)
             t1 = time.perf_counter()
             r1 = Q.solve(rebuild_symbolic=True)
@@ -217,7 +239,11 @@ def main():
             "pcg_iters": pcg_iters,
             "ms_per_pcg_iteration": results[-1]["ms_solve"] / max(1, pcg_iters),
             "newton_iters": results[-1]["newton_iters"],
-            "preconditioner": "jacobi", "pcg": "Chronopoulos-Gear, 2 launches/iteration",
+            "preconditioner": ("smoothed-aggregation AMG V(%d,%d), %d levels, operator complexity %.2f"
+                               % (2, 2, results[-1]["amg_levels"], results[-1]["amg_op_complexity"])) if amg
+                              else "jacobi",
+            "pcg": "Chronopoulos-Gear" + (" + AMG V-cycle" if amg else ", 2 launches/iteration"),
+            "ms_amg_setup": results[-1]["ms_amg_setup"],
             "ms_symbolic": results[-1]["ms_symbolic"],
             "ms_assemble": results[-1]["ms_assemble"],
             "ms_solve": results[-1]["ms_solve"],
@@ -226,12 +252,13 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_cg_spmv (CSR SpMV of the PCG, LDS row tiles, fused u.w partial)",
+            "kernel": "k_cg_spmv (CSR SpMV of the PCG, LDS row tiles, fused u.w and r.u partials)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": args.traffic,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": algo,
             "launch_us": spmv_ms * 1e3,
             "launches_sampled": sum(r["spmv_samples"] for r in results),
