@@ -96,10 +96,12 @@ def cpu_baseline(n_cells, nonlinear):
     }
 
 
-def pmc_traffic(kernel="k_cg_spmv"):
+def pmc_traffic(algo_bytes, kernel="k_cg_spmv"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*_pmc_summary.json, written by tools/profile.sh from separate
-    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench, gfx950-corrected)."""
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench, gfx950-corrected).
+    Only a summary of the same workload counts: its traffic must lie within
+    [0.8, 2] x this launch's algorithmic bytes."""
     import glob
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), key=os.path.getmtime)
     for path in reversed(paths):
@@ -108,7 +110,7 @@ def pmc_traffic(kernel="k_cg_spmv"):
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if kernel in d:
+        if kernel in d and 0.8 * algo_bytes <= d[kernel]["traffic_bytes"] <= 2.0 * algo_bytes:
             return d[kernel]["traffic_bytes"], os.path.relpath(path, ROOT)
     return None, None
 
@@ -194,7 +196,7 @@ def main():
     algo = spmv_bytes(rows, nnz, amg)
     achieved = algo / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
     ms_step = 1e3 * elapsed / args.steps
-    traffic, traffic_src = (args.traffic, "--traffic") if args.traffic is not None else pmc_traffic()
+    traffic, traffic_src = (args.traffic, "--traffic") if args.traffic is not None else pmc_traffic(algo)
     value = (1 if sharded else world) * n_dof * args.steps / elapsed
     pcg_iters = results[-1]["cg_iters"]
 

@@ -1,0 +1,24 @@
+"""In-process sharded solve (N ranks on one GPU) vs single device: iterations, agreement."""
+import os, sys, threading, time
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, R)
+import numpy as np
+from xfemm_amd import kernels, synth
+cells = int(sys.argv[1]) if len(sys.argv) > 1 else 400
+kw = synth.magnetostatic(cells)
+P = kernels.Static2DProblem(**kw); r1 = P.solve(); A1 = P.solution(); P.close()
+print("single: iters %d levels %d" % (r1["cg_iters"], r1["amg_levels"]), flush=True)
+for n in [2, 4, 8]:
+    comms = kernels.Comm.local_group(n)
+    probs = [kernels.Static2DProblem(**kw, comm=comms[q]) for q in range(n)]
+    out = [None] * n
+    def work(q):
+        out[q] = (probs[q].solve(), probs[q].solution())
+    t0 = time.time()
+    th = [threading.Thread(target=work, args=(q,)) for q in range(n)]
+    [t.start() for t in th]; [t.join() for t in th]
+    dt = time.time() - t0
+    r, A = out[0]
+    print("ranks %d: iters %d precond %d levels %d err vs single %.2e (%.2f s)" % (
+        n, r["cg_iters"], r["precond"], r["amg_levels"], np.abs(A - A1).max() / np.abs(A1).max(), dt), flush=True)
+    [p.close() for p in probs]; [c.close() for c in comms]
