@@ -606,12 +606,14 @@ def prepare_problem(pr: FemProblem) -> FemProblem:
 
 
 def get_fill_factor(pr: FemProblem) -> None:
-    """FSolver::GetFillFactor (fsolver.cpp:1083-1105), Frequency == 0 branch."""
+    """FSolver::GetFillFactor (fsolver.cpp:1083-1105): bIsWound, and
+    ProximityMu = 1 unless an AC problem has wound (LamType > 2) regions, whose
+    proximity-effect permeability is not restated by this oracle."""
     for lb in pr.labels:
         bt = pr.blocks[lb.BlockType].LamType if lb.BlockType >= 0 else 0
         lb.bIsWound = (abs(lb.Turns) > 1) or (bt > 2)
-    if pr.Frequency != 0:
-        raise NotImplementedError("harmonic problems are not restated by this oracle")
+        if pr.Frequency != 0 and bt > 2:
+            raise NotImplementedError("AC proximity-effect regions (LamType > 2) are not restated by this oracle")
 
 
 # --------------------------------------------------------------------------

@@ -1,0 +1,746 @@
+/* CPU oracle for the fsolver harmonic-2D path -- TEST INFRASTRUCTURE ONLY.
+ * See harmonic2d_oracle.h for scope and the reference lines each part follows.
+ *
+ * Every complex operation restates femmcomplex.cpp's formula (products as
+ * (ac - bd, ad + bc), quotients through the scaled reciprocal) and every loop
+ * keeps the reference's order, so that the restated CBigComplexLinProb gives
+ * results bit-identical with the reference's cspars.cpp.
+ */
+#include "harmonic2d_oracle.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORA_PI 3.141592653589793238462643383
+#define ORA_DEG 0.01745329251994329576923690768
+
+/* ------------------------------------------------------------------------ */
+/* CComplex restatement (femmcomplex.cpp)                                   */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+    double re, im;
+} cx;
+
+static cx C(double re, double im) { cx z = {re, im}; return z; }
+static cx cadd(cx x, cx y) { return C(x.re + y.re, x.im + y.im); }
+static cx csub(cx x, cx y) { return C(x.re - y.re, x.im - y.im); }
+static cx cneg(cx y) { return C(-y.re, -y.im); }
+static cx cmul(cx x, cx y) { return C(x.re * y.re - x.im * y.im, x.re * y.im + x.im * y.re); }   /* :355 */
+static cx cmuld(cx x, double z) { return C(x.re * z, x.im * z); }                                /* :323 */
+static cx dmulc(double x, cx y) { return C(x * y.re, x * y.im); }                                /* :350 */
+static cx cdivd(cx x, double z) { return C(x.re / z, x.im / z); }                                /* :388 */
+static cx cconj(cx x) { return C(x.re, -x.im); }
+static cx crecip(cx z)
+{   /* the scaled reciprocal of every CComplex quotient (:362-380) */
+    double c;
+    cx y;
+    if (fabs(z.re) > fabs(z.im)) {
+        c = z.im / z.re;
+        y.re = 1. / (z.re * (1. + c * c));
+        y.im = (-c) * y.re;
+    } else {
+        c = z.re / z.im;
+        y.im = (-1.) / (z.im * (1. + c * c));
+        y.re = (-c) * y.im;
+    }
+    return y;
+}
+static cx cdiv(cx x, cx z) { return cmul(x, crecip(z)); }                                        /* :456 */
+static cx ddivc(double x, cx z) { cx y = crecip(z); y.re *= x; y.im *= x; return y; }            /* :433 */
+static cx dplusc(double x, cx y) { return C(x + y.re, y.im); }                                 /* :244 */
+static cx cplusd(cx x, double z) { return C(x.re + z, x.im); }                                 /* :218 */
+static int cnz(cx z) { return (z.re != 0) || (z.im != 0); }
+static cx cx_exp(cx x)
+{   /* :622-634 */
+    const double e = exp(x.re);
+    return C(cos(x.im) * e, sin(x.im) * e);
+}
+static cx cx_tanh(cx x)
+{   /* :675-687 */
+    if (x.re > 0) {
+        cx e = cx_exp(dmulc(-2.0, x));
+        return cdiv(C(1 - e.re, -e.im), C(1 + e.re, e.im));
+    }
+    cx e = cx_exp(dmulc(2.0, x));
+    return cdiv(C(e.re - 1, e.im), C(e.re + 1, e.im));
+}
+
+static const cx I = {0.0, 1.0};
+
+/* ------------------------------------------------------------------------ */
+/* CBigComplexLinProb restatement (cspars.cpp)                              */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+    int len, cap;
+    int *c;
+    cx *x;
+} crow;
+
+typedef struct {
+    int n, bdw, nodes;
+    double precision, lambda;
+    crow *M;
+    cx *b, *V, *P, *R, *U, *Z;
+} clp;
+
+static void crow_reserve(crow *r, int cap)
+{
+    if (cap <= r->cap) return;
+    int nc = r->cap ? r->cap * 2 : 8;
+    while (nc < cap) nc *= 2;
+    r->c = (int *)realloc(r->c, sizeof(int) * nc);
+    r->x = (cx *)realloc(r->x, sizeof(cx) * nc);
+    r->cap = nc;
+}
+
+static void *clp_create(int n, int bw, int nodes, double precision)
+{   /* cspars.cpp:40-45, 119-145 */
+    clp *L = (clp *)calloc(1, sizeof(clp));
+    L->n = n;
+    L->bdw = bw;
+    L->nodes = nodes;
+    L->precision = precision;
+    L->lambda = 1.5;
+    L->M = (crow *)calloc(n, sizeof(crow));
+    L->b = (cx *)calloc(n, sizeof(cx));
+    L->V = (cx *)calloc(n, sizeof(cx));
+    L->P = (cx *)calloc(n, sizeof(cx));
+    L->R = (cx *)calloc(n, sizeof(cx));
+    L->U = (cx *)calloc(n, sizeof(cx));
+    L->Z = (cx *)calloc(n, sizeof(cx));
+    for (int i = 0; i < n; i++) {
+        crow_reserve(&L->M[i], 8);
+        L->M[i].len = 1;
+        L->M[i].c[0] = i;
+        L->M[i].x[0] = C(0, 0);
+    }
+    return L;
+}
+
+static void clp_destroy(void *lp)
+{
+    clp *L = (clp *)lp;
+    if (!L) return;
+    for (int i = 0; i < L->n; i++) {
+        free(L->M[i].c);
+        free(L->M[i].x);
+    }
+    free(L->M);
+    free(L->b); free(L->V); free(L->P); free(L->R); free(L->U); free(L->Z);
+    free(L);
+}
+
+static void lp_put(clp *L, cx v, int p, int q)
+{   /* cspars.cpp:147-233 (k = 0) */
+    if (q < p) { int t = p; p = q; q = t; }
+    crow *r = &L->M[p];
+    int k = 0;
+    while (k < r->len && r->c[k] < q) k++;
+    if (k < r->len && r->c[k] == q) { r->x[k] = v; return; }
+    crow_reserve(r, r->len + 1);
+    memmove(r->c + k + 1, r->c + k, sizeof(int) * (r->len - k));
+    memmove(r->x + k + 1, r->x + k, sizeof(cx) * (r->len - k));
+    r->c[k] = q;
+    r->x[k] = v;
+    r->len++;
+}
+
+static cx lp_get(clp *L, int p, int q)
+{   /* cspars.cpp:235-283 (k = 0) */
+    if (q < p) { int t = p; p = q; q = t; }
+    const crow *r = &L->M[p];
+    for (int k = 0; k < r->len; k++) {
+        if (r->c[k] == q) return r->x[k];
+        if (r->c[k] > q) break;
+    }
+    return C(0, 0);
+}
+
+static void clp_addto(void *lp, double vr, double vi, int p, int q)
+{   /* cspars.cpp:285-288 */
+    clp *L = (clp *)lp;
+    lp_put(L, cadd(lp_get(L, p, q), C(vr, vi)), p, q);
+}
+
+static void clp_get(void *lp, int p, int q, double *vr, double *vi)
+{
+    cx z = lp_get((clp *)lp, p, q);
+    *vr = z.re;
+    *vi = z.im;
+}
+
+static void clp_put(void *lp, double vr, double vi, int p, int q) { lp_put((clp *)lp, C(vr, vi), p, q); }
+static double *clp_b(void *lp) { return (double *)((clp *)lp)->b; }
+static double *clp_V(void *lp) { return (double *)((clp *)lp)->V; }
+
+static void clp_setvalue(void *lp, int i, double xr, double xi)
+{   /* cspars.cpp:482-537 (bNewton false) */
+    clp *L = (clp *)lp;
+    cx x = C(xr, xi);
+    int fst, lst;
+    if (L->bdw == 0) {
+        fst = 0;
+        lst = L->n;
+    } else {
+        fst = i - L->bdw;
+        if (fst < 0) fst = 0;
+        lst = i + L->bdw;
+        if (lst > L->nodes) lst = L->nodes;
+    }
+    for (int k = fst; k < L->n; k++) {
+        if (k == lst) k = L->nodes;
+        if (k >= L->n) break;
+        cx z = lp_get(L, k, i);
+        if (cnz(z)) {
+            L->b[k] = csub(L->b[k], cmul(z, x));
+            if (i != k) lp_put(L, C(0, 0), k, i);
+        }
+    }
+    L->b[i] = cmul(lp_get(L, i, i), x);
+}
+
+static void clp_pair(clp *L, int i, int j, int anti)
+{   /* cspars.cpp:592-675 (AntiPeriodicity), 677-758 (Periodicity), bNewton false */
+    int fst, lst;
+    if (j < i) { int t = j; j = i; i = t; }
+    if (L->bdw == 0) {
+        fst = 0;
+        lst = L->n;
+    } else {
+        fst = i - L->bdw;
+        if (fst < 0) fst = 0;
+        lst = j + L->bdw;
+        if (lst > L->nodes - 1) lst = L->nodes - 1;
+    }
+    for (int k = fst; k < L->n; k++) {
+        if ((k != i) && (k != j)) {
+            cx v1 = lp_get(L, k, i), v2 = lp_get(L, k, j);
+            if (cnz(v1) || cnz(v2)) {
+                if (anti) {
+                    cx c = cdivd(csub(v1, v2), 2.);
+                    lp_put(L, c, k, i);
+                    lp_put(L, cneg(c), k, j);
+                } else {
+                    cx c = cdivd(cadd(v1, v2), 2.);
+                    lp_put(L, c, k, i);
+                    lp_put(L, c, k, j);
+                }
+            }
+        }
+        if ((k == i + L->bdw) && (k < j - L->bdw) && (L->bdw != 0)) k = j - L->bdw;
+        else if (k == lst) k = L->nodes;
+    }
+    cx c = anti ? dmulc(0.5, cadd(lp_get(L, i, i), lp_get(L, j, j)))
+                : cdivd(cadd(lp_get(L, i, i), lp_get(L, j, j)), 2.);
+    lp_put(L, c, i, i);
+    lp_put(L, c, j, j);
+    if (anti) {
+        c = dmulc(0.5, csub(L->b[i], L->b[j]));
+        L->b[i] = c;
+        L->b[j] = cneg(c);
+    } else {
+        c = dmulc(0.5, cadd(L->b[i], L->b[j]));
+        L->b[i] = c;
+        L->b[j] = c;
+    }
+}
+
+static void clp_periodicity(void *lp, int i, int j) { clp_pair((clp *)lp, i, j, 0); }
+static void clp_antiperiodicity(void *lp, int i, int j) { clp_pair((clp *)lp, i, j, 1); }
+
+static void lp_multA(clp *L, const cx *X, cx *Y)
+{   /* cspars.cpp:290-360 (k = 0: complex symmetric) */
+    for (int i = 0; i < L->n; i++) Y[i] = C(0, 0);
+    for (int i = 0; i < L->n; i++) {
+        const crow *r = &L->M[i];
+        Y[i] = cadd(Y[i], cmul(r->x[0], X[i]));
+        for (int k = 1; k < r->len; k++) {
+            int c = r->c[k];
+            Y[i] = cadd(Y[i], cmul(r->x[k], X[c]));
+            Y[c] = cadd(Y[c], cmul(r->x[k], X[i]));
+        }
+    }
+}
+
+static cx lp_dot(const cx *x, const cx *y, int n)
+{   /* cspars.cpp:417-426 */
+    cx z = C(0, 0);
+    for (int i = 0; i < n; i++) z = cadd(z, cmul(x[i], y[i]));
+    return z;
+}
+
+static cx lp_conjdot(const cx *x, const cx *y, int n)
+{   /* cspars.cpp:428-437 */
+    cx z = C(0, 0);
+    for (int i = 0; i < n; i++) z = cadd(z, cmul(cconj(x[i]), y[i]));
+    return z;
+}
+
+static double lp_nrm(const cx *x, int n) { return sqrt(lp_conjdot(x, x, n).re); }   /* cspars.cpp:30 */
+
+static void lp_multpc(clp *L, const cx *X, cx *Y)
+{   /* cspars.cpp:439-480: SSOR */
+    int n = L->n;
+    double lam = L->lambda;
+    cx c = C(lam * (2. - lam), 0);
+    for (int i = 0; i < n; i++) Y[i] = cmul(X[i], c);
+    for (int i = 0; i < n; i++) {
+        const crow *r = &L->M[i];
+        Y[i] = cdiv(Y[i], r->x[0]);
+        for (int k = 1; k < r->len; k++)
+            Y[r->c[k]] = csub(Y[r->c[k]], cmuld(cmul(r->x[k], Y[i]), lam));
+    }
+    for (int i = 0; i < n; i++) Y[i] = cmul(Y[i], L->M[i].x[0]);
+    for (int i = n - 1; i >= 0; i--) {
+        const crow *r = &L->M[i];
+        for (int k = 1; k < r->len; k++) Y[i] = csub(Y[i], cmuld(cmul(r->x[k], Y[r->c[k]]), lam));
+        Y[i] = cdiv(Y[i], r->x[0]);
+    }
+}
+
+static void lp_multappa(clp *L, const cx *X, cx *Y)
+{   /* cspars.cpp:406-415 */
+    lp_multA(L, X, L->Z);
+    lp_multpc(L, L->Z, Y);
+    for (int i = 0; i < L->n; i++) Y[i].im = -Y[i].im;
+    lp_multpc(L, Y, L->Z);
+    lp_multA(L, L->Z, Y);
+    for (int i = 0; i < L->n; i++) Y[i].im = -Y[i].im;
+}
+
+static int lp_pcgsqstart(clp *L)
+{   /* cspars.cpp:764-820 */
+    int n = L->n;
+    for (int i = 0; i < n; i++)
+        if ((L->M[i].x[0].re == 0) && (L->M[i].x[0].im == 0)) {
+            fprintf(stderr, "singular flag tripped.");
+            return 0;
+        }
+    lp_multpc(L, L->b, L->Z);
+    for (int i = 0; i < n; i++) L->Z[i].im = -L->Z[i].im;
+    lp_multpc(L, L->Z, L->P);
+    lp_multA(L, L->P, L->Z);
+    for (int i = 0; i < n; i++) L->P[i] = cconj(L->Z[i]);
+    for (int i = 0; i < n; i++) L->V[i] = C(0, 0);
+    lp_multappa(L, L->V, L->R);
+    for (int i = 0; i < n; i++) L->R[i] = csub(L->P[i], L->R[i]);
+    for (int i = 0; i < n; i++) L->P[i] = L->R[i];
+    cx res = lp_conjdot(L->R, L->R, n);
+    for (int k = 0; k < 3; k++) {
+        lp_multappa(L, L->P, L->U);
+        cx pAp = lp_conjdot(L->P, L->U, n);
+        cx del = cdiv(res, pAp);
+        for (int i = 0; i < n; i++) L->V[i] = cadd(L->V[i], cmul(del, L->P[i]));
+        for (int i = 0; i < n; i++) L->R[i] = csub(L->R[i], cmul(del, L->U[i]));
+        cx res_new = lp_conjdot(L->R, L->R, n);
+        cx rho = cdiv(res_new, res);
+        res = res_new;
+        for (int i = 0; i < n; i++) L->P[i] = cadd(L->R[i], cmul(rho, L->P[i]));
+    }
+    return 1;
+}
+
+static long long g_iters;
+
+static int lp_pbcgsolve(clp *L, int flag)
+{   /* cspars.cpp:822-895 */
+    int n = L->n;
+    if (flag == 0)
+        for (int i = 0; i < n; i++) L->V[i] = C(0, 0);
+    lp_multA(L, L->V, L->R);
+    for (int i = 0; i < n; i++) L->R[i] = csub(L->b[i], L->R[i]);
+    double normb = lp_nrm(L->b, n);
+    double er;
+    lp_multpc(L, L->R, L->Z);
+    for (int i = 0; i < n; i++) L->P[i] = L->Z[i];
+    cx res = lp_dot(L->Z, L->R, n);
+    g_iters = 0;
+    do {
+        lp_multA(L, L->P, L->U);
+        cx pAp = lp_dot(L->P, L->U, n);
+        cx del = cdiv(res, pAp);
+        for (int i = 0; i < n; i++) L->V[i] = cadd(L->V[i], cmul(del, L->P[i]));
+        for (int i = 0; i < n; i++) L->R[i] = csub(L->R[i], cmul(del, L->U[i]));
+        lp_multpc(L, L->R, L->Z);
+        cx res_new = lp_dot(L->Z, L->R, n);
+        cx rho = cdiv(res_new, res);
+        res = res_new;
+        for (int i = 0; i < n; i++) L->P[i] = cadd(L->Z[i], cmul(rho, L->P[i]));
+        er = lp_nrm(L->R, n) / normb;
+        g_iters++;
+    } while (er > L->precision);
+    return 1;
+}
+
+static int clp_solve(void *lp, int flag)
+{   /* cspars.cpp:1062-1081 (bNewton false) */
+    clp *L = (clp *)lp;
+    if (flag == 0)
+        if (lp_pcgsqstart(L) == 0) return 0;
+    return lp_pbcgsolve(L, 2);
+}
+
+static const orh_linprob_ops g_builtin = {clp_create, clp_destroy, clp_addto, clp_get, clp_put,
+                                          clp_b, clp_V, clp_setvalue, clp_periodicity,
+                                          clp_antiperiodicity, clp_solve};
+
+const orh_linprob_ops *orh_builtin_linprob(void) { return &g_builtin; }
+
+/* ------------------------------------------------------------------------ */
+/* FSolver::Harmonic2D (harmonic2d.cpp), linear problems                    */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+    cx mu0, mu1;
+} effmu;
+
+/* effective permeability of each block (harmonic2d.cpp:190-235) */
+static void effective_mu(const orh_problem *pr, double w, effmu *Mu)
+{
+    const cx deg45 = C(1, 1);
+    for (int k = 0; k < pr->n_blocks; k++) {
+        const orh_block *b = &pr->blocks[k];
+        if (b->LamType == 0) {
+            Mu[k].mu0 = dmulc(b->mu_x, cx_exp(cmuld(cmuld(cneg(I), b->Theta_hx), ORA_DEG)));
+            Mu[k].mu1 = dmulc(b->mu_y, cx_exp(cmuld(cmuld(cneg(I), b->Theta_hy), ORA_DEG)));
+            if (b->Lam_d != 0) {
+                if (b->Cduct != 0) {
+                    cx halflag = cx_exp(cdivd(cmuld(cmuld(cneg(I), b->Theta_hx), ORA_DEG), 2.));
+                    double ds = sqrt(2. / (0.4 * ORA_PI * w * b->Cduct * b->mu_x));
+                    cx K = cdivd(cmuld(cmuld(cmul(halflag, deg45), b->Lam_d), 0.001), 2. * ds);
+                    Mu[k].mu0 = cplusd(cmuld(cdiv(cmul(Mu[k].mu0, cx_tanh(K)), K), b->LamFill), 1. - b->LamFill);
+                    halflag = cx_exp(cdivd(cmuld(cmuld(cneg(I), b->Theta_hy), ORA_DEG), 2.));
+                    ds = sqrt(2. / (0.4 * ORA_PI * w * b->Cduct * b->mu_y));
+                    K = cdivd(cmuld(cmuld(cmul(halflag, deg45), b->Lam_d), 0.001), 2. * ds);
+                    Mu[k].mu1 = cplusd(cmuld(cdiv(cmul(Mu[k].mu1, cx_tanh(K)), K), b->LamFill), 1. - b->LamFill);
+                } else {
+                    Mu[k].mu0 = cplusd(cmuld(Mu[k].mu0, b->LamFill), 1. - b->LamFill);
+                    Mu[k].mu1 = cplusd(cmuld(Mu[k].mu1, b->LamFill), 1. - b->LamFill);
+                }
+            }
+        } else {
+            Mu[k].mu0 = C(1, 0);
+            Mu[k].mu1 = C(1, 0);
+        }
+    }
+}
+
+/* circuit cases (harmonic2d.cpp:86-170) */
+static void circuits(orh_problem *pr)
+{
+    int nc = pr->n_circs;
+    if (nc <= 0) return;
+    cx *I1 = (cx *)calloc(nc, sizeof(cx)), *I2 = (cx *)calloc(nc, sizeof(cx)), *I3 = (cx *)calloc(nc, sizeof(cx));
+    for (int i = 0; i < pr->n_elems; i++) {
+        if (pr->lbl[i] < 0) continue;
+        const orh_label *lb = &pr->labels[pr->lbl[i]];
+        if (lb->InCircuit == -1) continue;
+        const int *n = pr->p + 3 * i;
+        double p0 = pr->y[n[1]] - pr->y[n[2]], p1 = pr->y[n[2]] - pr->y[n[0]];
+        double q0 = pr->x[n[2]] - pr->x[n[1]], q1 = pr->x[n[0]] - pr->x[n[2]];
+        double a = (p0 * q1 - p1 * q0) / 2.;
+        const orh_block *b = &pr->blocks[pr->blk[i]];
+        double Cduct = b->Cduct;
+        if (lb->bIsWound) Cduct = 0;
+        int k = lb->InCircuit;
+        I1[k] = cplusd(I1[k], a);
+        I2[k] = cplusd(I2[k], a * Cduct);
+        I3[k] = cadd(I3[k], cmuld(cmuld(dplusc(b->J_re, cmuld(I, b->J_im)), a), 100.));
+    }
+    for (int k = 0; k < nc; k++) {
+        orh_circ *c = &pr->circs[k];
+        c->J_re = c->J_im = c->dV_re = c->dV_im = 0;
+        if (c->CircType == 0) {
+            if (!cnz(I2[k])) {
+                c->Case = 1;
+                if (!cnz(I1[k])) {
+                    c->J_re = c->J_im = 0;
+                } else {
+                    cx amps = dplusc(c->Amps_re, cmuld(I, c->Amps_im));
+                    cx J = cdiv(dmulc(0.01, csub(amps, I3[k])), I1[k]);
+                    c->J_re = J.re;
+                    c->J_im = J.im;
+                }
+            } else {
+                c->Case = 2;
+            }
+        } else {
+            c->Case = 0;
+            cx dV = dplusc(c->dVolts_re, cmuld(I, c->dVolts_im));
+            c->dV_re = dV.re;
+            c->dV_im = dV.im;
+        }
+    }
+    free(I1); free(I2); free(I3);
+}
+
+static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L, const effmu *Mu, double w)
+{
+    const double c = ORA_PI * 4.e-05;
+    const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
+    const cx deg45 = C(1, 1);
+    const int NN = pr->n_nodes;
+    cx *bL = (cx *)ops->b(L);
+    cx *VL = (cx *)ops->V(L);
+    for (int i = 0; i < pr->n_elems; i++) {
+        cx Me[3][3], be[3], Mx[3][3], My[3][3], Mxy[3][3], Mn[3][3];
+        double p[3], q[3], l[3];
+        int n[3];
+        for (int j = 0; j < 3; j++) {
+            for (int k = 0; k < 3; k++) Me[j][k] = Mx[j][k] = My[j][k] = Mxy[j][k] = Mn[j][k] = C(0, 0);
+            be[j] = C(0, 0);
+        }
+        for (int k = 0; k < 3; k++) n[k] = pr->p[3 * i + k];
+        p[0] = pr->y[n[1]] - pr->y[n[2]];
+        p[1] = pr->y[n[2]] - pr->y[n[0]];
+        p[2] = pr->y[n[0]] - pr->y[n[1]];
+        q[0] = pr->x[n[2]] - pr->x[n[1]];
+        q[1] = pr->x[n[0]] - pr->x[n[2]];
+        q[2] = pr->x[n[1]] - pr->x[n[0]];
+        for (int j = 0, k = 1; j < 3; k++, j++) {
+            if (k == 3) k = 0;
+            l[j] = sqrt(pow(pr->x[n[k]] - pr->x[n[j]], 2.) + pow(pr->y[n[k]] - pr->y[n[j]], 2.));
+        }
+        double a = (p[0] * q[1] - p[1] * q[0]) / 2.;
+        const orh_block *blk = &pr->blocks[pr->blk[i]];
+        const orh_label *lab = &pr->labels[pr->lbl[i]];
+        cx K = C(-1. / (4. * a), 0);
+        for (int j = 0; j < 3; j++)
+            for (int k = j; k < 3; k++) {
+                cx t = cmuld(cmuld(K, p[j]), p[k]);
+                Mx[j][k] = cadd(Mx[j][k], t);
+                if (j != k) Mx[k][j] = cadd(Mx[k][j], t);
+            }
+        for (int j = 0; j < 3; j++)
+            for (int k = j; k < 3; k++) {
+                cx t = cmuld(cmuld(K, q[j]), q[k]);
+                My[j][k] = cadd(My[j][k], t);
+                if (j != k) My[k][j] = cadd(My[k][j], t);
+            }
+        for (int j = 0; j < 3; j++)
+            for (int k = j; k < 3; k++) {
+                cx t = cmuld(K, p[j] * q[k] + p[k] * q[j]);
+                Mxy[j][k] = cadd(Mxy[j][k], t);
+                if (j != k) Mxy[k][j] = cadd(Mxy[k][j], t);
+            }
+        /* eddy currents (:387-402) */
+        K = cmuld(cmuld(cmuld(cmuld(cneg(I), a), w), blk->Cduct), c);
+        K = cdivd(K, 12.);
+        if ((blk->LamType == 0) && (blk->Lam_d > 0)) K = C(0, 0);
+        if (lab->bIsWound) K = C(0, 0);
+        for (int j = 0; j < 3; j++)
+            for (int k = j; k < 3; k++) {
+                Me[j][k] = cadd(Me[j][k], K);
+                Me[k][j] = cadd(Me[k][j], K);
+            }
+        /* derivative boundary conditions (:404-438) */
+        for (int j = 0; j < 3; j++) {
+            int ej = pr->e ? pr->e[3 * i + j] : -1;
+            if (ej < 0) continue;
+            const orh_line *ln = &pr->lines[ej];
+            int k = j + 1;
+            if (k == 3) k = 0;
+            if (ln->BdryFormat == 2) {
+                K = cdivd(cmuld(dmulc(-0.0001 * c, C(ln->c0_re, ln->c0_im)), l[j]), 6.);
+                Me[j][j] = cadd(Me[j][j], dmulc(2.0, K));
+                Me[k][k] = cadd(Me[k][k], dmulc(2.0, K));
+                Me[j][k] = cadd(Me[j][k], K);
+                Me[k][j] = cadd(Me[k][j], K);
+                K = cmuld(cdivd(cmuld(C(ln->c1_re, ln->c1_im), l[j]), 2.), 0.0001);
+                be[j] = cadd(be[j], K);
+                be[k] = cadd(be[k], K);
+            }
+            if (ln->BdryFormat == 1) {
+                double ds = sqrt(2. / (0.4 * ORA_PI * w * ln->Sig * ln->Mu));
+                K = cdivd(deg45, -ds * ln->Mu * 100.);
+                K = cmuld(K, l[j] / 6.);
+                Me[j][j] = cadd(Me[j][j], dmulc(2.0, K));
+                Me[k][k] = cadd(Me[k][k], dmulc(2.0, K));
+                Me[j][k] = cadd(Me[j][k], K);
+                Me[k][j] = cadd(Me[k][j], K);
+            }
+        }
+        /* sources (:441-460) */
+        for (int j = 0; j < 3; j++) {
+            cx Jv = C(0, 0);
+            if (lab->InCircuit >= 0) {
+                const orh_circ *cc = &pr->circs[lab->InCircuit];
+                if (cc->Case == 1) Jv = C(cc->J_re, cc->J_im);
+                if (cc->Case == 0) Jv = cmuld(cneg(C(cc->dV_re, cc->dV_im)), blk->Cduct);
+            }
+            K = cdivd(cmuld(cneg(cadd(dplusc(blk->J_re, cmuld(I, blk->J_im)), Jv)), a), 3.);
+            be[j] = cadd(be[j], K);
+            if (lab->InCircuit >= 0 && pr->circs[lab->InCircuit].Case == 2) {
+                int row = NN + lab->InCircuit;
+                bL[row] = cadd(bL[row], K);
+            }
+        }
+        /* Case 2 circuit couplings (:463-472) */
+        if (lab->InCircuit >= 0 && pr->circs[lab->InCircuit].Case == 2) {
+            int cr = NN + lab->InCircuit;
+            cx Kc = cmuld(cmuld(cmuld(cmuld(cneg(I), a), w), blk->Cduct), c);
+            for (int j = 0; j < 3; j++) {
+                double gr, gi;
+                ops->get(L, n[j], cr, &gr, &gi);
+                cx v = cadd(C(gr, gi), cdivd(Kc, 3.));
+                ops->put(L, v.re, v.im, n[j], cr);
+            }
+            double gr, gi;
+            ops->get(L, cr, cr, &gr, &gi);
+            cx v = cadd(C(gr, gi), Kc);
+            ops->put(L, v.re, v.im, cr, cr);
+        }
+        /* element permeability (Iter == 0, linear: :481-486) and the global matrices (:600-630) */
+        cx mu1 = Mu[pr->blk[i]].mu0, mu2 = Mu[pr->blk[i]].mu1, v12 = C(0, 0);
+        for (int j = 0; j < 3; j++)
+            for (int k = 0; k < 3; k++) {
+                Me[j][k] = cadd(Me[j][k], cadd(cadd(cdiv(Mx[j][k], mu2), cdiv(My[j][k], mu1)), cmul(Mxy[j][k], v12)));
+                be[j] = cadd(be[j], cmul(Mn[j][k], VL[n[k]]));
+            }
+        for (int j = 0; j < 3; j++) {
+            for (int k = j; k < 3; k++) ops->addto(L, Me[j][k].re, Me[j][k].im, n[j], n[k]);
+            bL[n[j]] = cadd(bL[n[j]], be[j]);
+        }
+    }
+    /* point currents (:634-641) */
+    for (int i = 0; i < NN; i++) {
+        int m = pr->marker ? pr->marker[i] : -1;
+        if (m >= 0) {
+            cx K = dmulc(0.01, dplusc(pr->points[m].J_re, cmuld(I, pr->points[m].J_im)));
+            bL[i] = cadd(bL[i], cneg(K));
+        }
+    }
+    /* Case 2 total current constraints (:644-650) */
+    for (int i = 0; i < pr->n_circs; i++)
+        if (pr->circs[i].Case == 2)
+            bL[NN + i] = cadd(bL[NN + i], dmulc(0.01, dplusc(pr->circs[i].Amps_re, cmuld(I, pr->circs[i].Amps_im))));
+    /* fixed points (:653-661) */
+    for (int i = 0; i < NN; i++) {
+        int m = pr->marker ? pr->marker[i] : -1;
+        if (m >= 0 && pr->points[m].J_re == 0 && pr->points[m].J_im == 0) {
+            cx K = cdivd(dplusc(pr->points[m].A_re, cmuld(I, pr->points[m].A_im)), c);
+            ops->setvalue(L, i, K.re, K.im);
+        }
+    }
+    /* fixed segments (:664-730) */
+    for (int i = 0; i < pr->n_elems; i++)
+        for (int j = 0; j < 3; j++) {
+            int k = j + 1;
+            if (k == 3) k = 0;
+            int s = pr->e ? pr->e[3 * i + j] : -1;
+            if (s < 0 || pr->lines[s].BdryFormat != 0) continue;
+            const orh_line *ln = &pr->lines[s];
+            int nodes2[2] = {pr->p[3 * i + j], pr->p[3 * i + k]};
+            for (int m = 0; m < 2; m++) {
+                double x = pr->x[nodes2[m]], y = pr->y[nodes2[m]], av;
+                if (pr->coords == 0) {
+                    x /= units[pr->length_units];
+                    y /= units[pr->length_units];
+                    av = ln->A0 + x * ln->A1 + y * ln->A2;
+                } else {
+                    double r = sqrt(x * x + y * y), t;
+                    if ((x == 0) && (y == 0)) t = 0;
+                    else t = atan2(y, x) / ORA_DEG;
+                    r /= units[pr->length_units];
+                    av = ln->A0 + r * ln->A1 + t * ln->A2;
+                }
+                cx K = dmulc(av / c, cx_exp(cmuld(cmuld(I, ln->phi), ORA_DEG)));
+                ops->setvalue(L, nodes2[m], K.re, K.im);
+            }
+        }
+    /* circuits with a priori current / voltage: keep their rows regular (:734-736) */
+    for (int j = 0; j < pr->n_circs; j++)
+        if (pr->circs[j].Case < 2) {
+            double gr, gi;
+            ops->get(L, 0, 0, &gr, &gi);
+            ops->put(L, gr, gi, NN + j, NN + j);
+        }
+    for (int k = 0; k < pr->n_pbc; k++) {
+        if (pr->pbc[3 * k + 2] == 0) ops->periodicity(L, pr->pbc[3 * k], pr->pbc[3 * k + 1]);
+        if (pr->pbc[3 * k + 2] == 1) ops->antiperiodicity(L, pr->pbc[3 * k], pr->pbc[3 * k + 1]);
+    }
+    return 1;
+}
+
+static int check_linear(const orh_problem *pr)
+{
+    for (int k = 0; k < pr->n_blocks; k++) {
+        if (pr->blocks[k].BHpoints != 0) return 0;
+        if (pr->blocks[k].LamType == 1 || pr->blocks[k].LamType == 2 || pr->blocks[k].LamType > 2) return 0;
+    }
+    return 1;
+}
+
+int orh_harmonic2d(orh_problem *pr, const orh_linprob_ops *ops, double *A_out, ora_stats *stats)
+{
+    if (!ops) ops = orh_builtin_linprob();
+    if (!check_linear(pr)) return 0;
+    const double c = ORA_PI * 4.e-05;
+    const double w = pr->frequency * 2. * ORA_PI;
+    const int NN = pr->n_nodes, n = NN + pr->n_circs;
+    effmu *Mu = (effmu *)calloc(pr->n_blocks > 0 ? pr->n_blocks : 1, sizeof(effmu));
+    circuits(pr);
+    effective_mu(pr, w, Mu);
+    void *L = ops->create(n, pr->bandwidth, NN, pr->precision);
+    assemble_and_bc(pr, ops, L, Mu, w);
+    g_iters = -1;
+    int ok = ops->solve(L, 0);
+    if (ok) {
+        const cx *V = (const cx *)ops->V(L);
+        for (int i = 0; i < NN; i++) {
+            A_out[2 * i] = V[i].re * c;
+            A_out[2 * i + 1] = V[i].im * c;
+        }
+        for (int i = 0; i < pr->n_circs; i++)
+            if (pr->circs[i].Case == 2) {   /* L.b[NumNodes+i] = I*c*w*V (:784) and .ans writes it as dV */
+                cx dv = cmul(cmuld(cmuld(I, c), w), V[NN + i]);
+                pr->circs[i].dV_re = dv.re;
+                pr->circs[i].dV_im = dv.im;
+            }
+    }
+    if (stats) {
+        stats->newton_iters = 1;
+        stats->cg_iters = (ops == orh_builtin_linprob()) ? g_iters : -1;
+        stats->last_res = 0;
+    }
+    ops->destroy(L);
+    free(Mu);
+    return ok;
+}
+
+int orh_harmonic2d_system(orh_problem *pr, int *rows, int *cols, double *vals, long long cap, double *b_out,
+                          long long *nnz_out)
+{
+    if (!check_linear(pr)) return 0;
+    const double w = pr->frequency * 2. * ORA_PI;
+    const int NN = pr->n_nodes, n = NN + pr->n_circs;
+    effmu *Mu = (effmu *)calloc(pr->n_blocks > 0 ? pr->n_blocks : 1, sizeof(effmu));
+    circuits(pr);
+    effective_mu(pr, w, Mu);
+    clp *L = (clp *)clp_create(n, pr->bandwidth, NN, pr->precision);
+    assemble_and_bc(pr, orh_builtin_linprob(), L, Mu, w);
+    long long k = 0;
+    for (int i = 0; i < NN; i++) {
+        const crow *r = &L->M[i];
+        for (int t = 0; t < r->len; t++) {
+            if (r->c[t] >= NN) continue;
+            if (k < cap) {
+                rows[k] = i;
+                cols[k] = r->c[t];
+                vals[2 * k] = r->x[t].re;
+                vals[2 * k + 1] = r->x[t].im;
+            }
+            k++;
+        }
+        b_out[2 * i] = L->b[i].re;
+        b_out[2 * i + 1] = L->b[i].im;
+    }
+    *nnz_out = k;
+    clp_destroy(L);
+    free(Mu);
+    return 1;
+}

@@ -5,12 +5,16 @@
 // Nothing of the reference is copied: this file only calls
 //   CBigLinProb            cfemm/libfemm/spars.h:38-83   (spars.cpp)
 //   CMSolverMaterialProp   cfemm/libfemm/CMaterialProp.h:193 (CMaterialProp.cpp)
-// through an extern "C" surface matching ora_linprob_ops (static2d_oracle.h).
+//   CBigComplexLinProb     cfemm/libfemm/cspars.h (cspars.cpp)
+// through extern "C" surfaces matching ora_linprob_ops (static2d_oracle.h) and
+// orh_linprob_ops (harmonic2d_oracle.h).
 #include <sstream>
 #include <string>
 #include <vector>
 
 #include "CMaterialProp.h"
+#include "femmcomplex.h"
+#include "cspars.h"
 #include "spars.h"
 
 extern "C" {
@@ -76,5 +80,32 @@ int ref_block_bhprops(const char *block_text, const double *Bq, int nq, double *
     }
     return prop.BHpoints;
 }
+
+// ---- CBigComplexLinProb (harmonic path) ----
+static CBigComplexLinProb *CL(void *L) { return static_cast<CBigComplexLinProb *>(L); }
+
+void *ref_clp_create(int n, int bw, int nodes, double precision)
+{
+    CBigComplexLinProb *L = new CBigComplexLinProb();
+    L->Precision = precision;
+    L->Create(n, bw, nodes);
+    return L;
+}
+
+void ref_clp_destroy(void *L) { delete CL(L); }
+void ref_clp_addto(void *L, double vr, double vi, int p, int q) { CL(L)->AddTo(CComplex(vr, vi), p, q); }
+void ref_clp_get(void *L, int p, int q, double *vr, double *vi)
+{
+    CComplex z = CL(L)->Get(p, q);
+    *vr = z.re;
+    *vi = z.im;
+}
+void ref_clp_put(void *L, double vr, double vi, int p, int q) { CL(L)->Put(CComplex(vr, vi), p, q); }
+double *ref_clp_b(void *L) { return reinterpret_cast<double *>(CL(L)->b); }
+double *ref_clp_V(void *L) { return reinterpret_cast<double *>(CL(L)->V); }
+void ref_clp_setvalue(void *L, int i, double xr, double xi) { CL(L)->SetValue(i, CComplex(xr, xi)); }
+void ref_clp_periodicity(void *L, int i, int j) { CL(L)->Periodicity(i, j); }
+void ref_clp_antiperiodicity(void *L, int i, int j) { CL(L)->AntiPeriodicity(i, j); }
+int ref_clp_solve(void *L, int flag) { return CL(L)->PBCGSolveMod(flag, false) ? 1 : 0; }
 
 }  // extern "C"

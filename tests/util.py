@@ -16,19 +16,21 @@ def kernel_kwargs(pr: femfile.FemProblem, mesh: femfile.Mesh) -> dict:
     blocks = []
     for m in pr.blocks:
         b = dict(mu_x=m.mu_x, mu_y=m.mu_y, H_c=m.H_c, J_re=m.J_re, Cduct=m.Cduct, LamFill=m.LamFill,
-                 LamType=m.LamType)
+                 LamType=m.LamType, J_im=m.J_im, Theta_hx=m.Theta_hx, Theta_hy=m.Theta_hy, Lam_d=m.Lam_d)
         if m.BHpoints:
             b.update(B=np.array(m.Bdata), H=np.array(m.Hdata), slope=np.array(m.slope))
         blocks.append(b)
     labels = [dict(block=max(lb.BlockType, 0), in_circuit=lb.InCircuit, mag_dir=lb.MagDir,
                    is_wound=int(lb.bIsWound)) for lb in pr.labels]
-    lines = [dict(format=b.BdryFormat, A0=b.A0, A1=b.A1, A2=b.A2, phi=b.phi, c0=b.c0, c1=b.c1) for b in pr.bdrys]
+    lines = [dict(format=b.BdryFormat, A0=b.A0, A1=b.A1, A2=b.A2, phi=b.phi, c0=b.c0, c1=b.c1, c0_im=b.c0i,
+                  c1_im=b.c1i, Mu=b.Mu, Sig=b.Sig) for b in pr.bdrys]
     points = [dict(A_re=q.A_re, A_im=q.A_im, J_re=q.J_re, J_im=q.J_im) for q in pr.points]
-    circuits = [dict(type=c.CircType, amps_re=c.Amps_re, dvolts_re=c.dVolts_re) for c in pr.circuits]
+    circuits = [dict(type=c.CircType, amps_re=c.Amps_re, dvolts_re=c.dVolts_re, amps_im=c.Amps_im,
+                     dvolts_im=c.dVolts_im) for c in pr.circuits]
     return dict(x=mesh.x, y=mesh.y, p=mesh.p, lbl=mesh.lbl, marker=mesh.marker, e=mesh.e,
                 pbc=mesh.pbc if len(mesh.pbc) else None, blocks=blocks, labels=labels, lines=lines,
                 points=points, circuits=circuits, precision=pr.Precision, length_units=pr.LengthUnits,
-                coords=pr.Coords, relax=pr.Relax)
+                coords=pr.Coords, relax=pr.Relax, frequency=pr.Frequency)
 
 
 def synth_to_oracle(kw: dict):
@@ -39,10 +41,13 @@ def synth_to_oracle(kw: dict):
     pr.Precision = kw["precision"]
     pr.LengthUnits = kw["length_units"]
     pr.Relax = 1.0
+    pr.Frequency = kw.get("frequency", 0.0)
     for b in kw["blocks"]:
         m = femfile.BlockProp(mu_x=b.get("mu_x", 1.0), mu_y=b.get("mu_y", 1.0), H_c=b.get("H_c", 0.0),
                               J_re=b.get("J_re", 0.0), Cduct=b.get("Cduct", 0.0),
-                              LamFill=b.get("LamFill", 1.0), LamType=b.get("LamType", 0))
+                              LamFill=b.get("LamFill", 1.0), LamType=b.get("LamType", 0),
+                              J_im=b.get("J_im", 0.0), Theta_hx=b.get("Theta_hx", 0.0),
+                              Theta_hy=b.get("Theta_hy", 0.0), Lam_d=b.get("Lam_d", 0.0))
         if b.get("bh") == "M19":
             B, H = synth.m19_curve()
             m.BHpoints, m.Bdata, m.Hdata = len(B), list(B), list(H)
@@ -50,11 +55,16 @@ def synth_to_oracle(kw: dict):
         pr.blocks.append(m)
     for lb in kw["labels"]:
         pr.labels.append(femfile.BlockLabel(BlockType=lb["block"], InCircuit=lb.get("in_circuit", -1),
-                                            MagDir=lb.get("mag_dir", 0.0)))
+                                            MagDir=lb.get("mag_dir", 0.0), Turns=2 if lb.get("is_wound", 0) else 1))
     for ln in kw["lines"]:
         pr.bdrys.append(femfile.BdryProp(BdryFormat=ln.get("format", 0), A0=ln.get("A0", 0.0),
                                          A1=ln.get("A1", 0.0), A2=ln.get("A2", 0.0), phi=ln.get("phi", 0.0),
-                                         c0=ln.get("c0", 0.0), c1=ln.get("c1", 0.0)))
+                                         c0=ln.get("c0", 0.0), c1=ln.get("c1", 0.0), c0i=ln.get("c0_im", 0.0),
+                                         c1i=ln.get("c1_im", 0.0), Mu=ln.get("Mu", 0.0), Sig=ln.get("Sig", 0.0)))
+    for c in kw.get("circuits", []):
+        pr.circuits.append(femfile.Circuit(CircType=c.get("type", 0), Amps_re=c.get("amps_re", 0.0),
+                                           Amps_im=c.get("amps_im", 0.0), dVolts_re=c.get("dvolts_re", 0.0),
+                                           dVolts_im=c.get("dvolts_im", 0.0)))
     for q in kw.get("points", []):
         pr.points.append(femfile.PointProp(A_re=q.get("A_re", 0.0), A_im=q.get("A_im", 0.0),
                                            J_re=q.get("J_re", 0.0), J_im=q.get("J_im", 0.0)))

@@ -236,3 +236,68 @@ def bc_chain(n: int, L: float = 10.0):
     kw["marker"] = marker
     kw["points"] = [dict(A_re=0.0)]
     return kw
+
+
+def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float = 1e-8, periodic: bool = False,
+             circuits: bool = True):
+    """Keyword arguments of a linear time-harmonic planar problem
+    (FSolver::Harmonic2D, cfemm/fsolver/harmonic2d.cpp) on the magnetostatic
+    square: laminated lossy steel (lamination thickness with conductivity,
+    hysteresis lag), an anisotropic block, a conducting aluminium plate
+    (eddy currents), coils with complex current densities, a prescribed-A
+    side with phase, a mixed side with complex c0/c1, a small-skin-depth side,
+    a complex point current and point value; optionally bottom/top periodic
+    pairs and circuits (a wound coil with specified current -> Case 1, the
+    plate driven by a specified voltage gradient -> Case 0)."""
+    kw = magnetostatic(n, L=L, precision=precision)
+    x, y, p = kw["x"], kw["y"], kw["p"]
+    tol = 1e-9 * L
+    m = n + 1
+    e = -np.ones(p.shape, dtype=np.int32)
+    for j in range(3):
+        a, b = p[:, j], p[:, (j + 1) % 3]
+        left = (np.abs(x[a]) < tol) & (np.abs(x[b]) < tol)
+        right = (np.abs(x[a] - L) < tol) & (np.abs(x[b] - L) < tol)
+        bot = (np.abs(y[a]) < tol) & (np.abs(y[b]) < tol)
+        top = (np.abs(y[a] - L) < tol) & (np.abs(y[b] - L) < tol)
+        e[left, j] = 0
+        e[right, j] = 1
+        e[bot, j] = 3 if periodic else 0
+        e[top, j] = 3 if periodic else 2
+    kw["e"] = e
+    kw["frequency"] = frequency
+    kw["lines"] = [dict(format=0, A0=1e-3, A1=2e-4, A2=0.0, phi=30.0),
+                   dict(format=2, c0=3.0, c0_im=1.0, c1=0.5, c1_im=-0.2),
+                   dict(format=1, Mu=1.0, Sig=5.8),
+                   dict(format=4)]
+    kw["blocks"] = [
+        dict(mu_x=1.0, mu_y=1.0),                                                    # air
+        dict(mu_x=800.0, mu_y=800.0, Lam_d=0.35, LamFill=0.96, Cduct=2.0,             # laminated lossy steel
+             Theta_hx=12.0, Theta_hy=12.0),
+        dict(mu_x=1.0, mu_y=1.0, J_re=2.0, J_im=0.5),                                # coil +
+        dict(mu_x=1.0, mu_y=1.0, J_re=-2.0, J_im=-0.5),                              # coil -
+        dict(mu_x=1.0, mu_y=1.0, Cduct=35.0),                                        # aluminium plate
+        dict(mu_x=50.0, mu_y=5.0, Lam_d=0.5, LamFill=0.9),                           # anisotropic, no conduction
+    ]
+    lbl = kw["lbl"]
+    cx = (x[p[:, 0]] + x[p[:, 1]] + x[p[:, 2]]) / (3.0 * L)
+    cy = (y[p[:, 0]] + y[p[:, 1]] + y[p[:, 2]]) / (3.0 * L)
+    lbl = lbl.copy()
+    lbl[(lbl == 0) & (cx > 0.8) & (cx < 0.95) & (cy > 0.1) & (cy < 0.3)] = 5
+    kw["lbl"] = lbl
+    labels = [dict(block=0), dict(block=1), dict(block=2), dict(block=3), dict(block=4), dict(block=5)]
+    if circuits:
+        labels[2] = dict(block=2, in_circuit=0, is_wound=1)
+        labels[4] = dict(block=4, in_circuit=1)
+        kw["circuits"] = [dict(type=0, amps_re=3.0, amps_im=1.0), dict(type=1, dvolts_re=0.02, dvolts_im=-0.01)]
+    kw["labels"] = labels
+    marker = -np.ones(len(x), dtype=np.int32)
+    marker[(m // 2) * m + m // 3] = 0
+    marker[(m // 3) * m + (2 * m) // 3] = 1
+    kw["marker"] = marker
+    kw["points"] = [dict(J_re=5.0, J_im=2.0), dict(A_re=2e-3, A_im=1e-3)]
+    if periodic:
+        bottom = np.arange(m)
+        top = (m - 1) * m + np.arange(m)
+        kw["pbc"] = np.stack([bottom, top, np.zeros(m)], 1).astype(np.int32)
+    return kw
