@@ -205,6 +205,52 @@ int xfk_partition_plan(int n_nodes, int n_elems, const int *p, int rank, int nra
 int xfk_problem_create_dist(const xfk_problem_desc *desc, int device, xfk_comm *comm, xfk_problem **out);
 int xfk_dist_get_info(const xfk_problem *prob, xfk_dist_info *info);
 
+/* ---------------------------------------------------------------------------
+ * Time-harmonic planar problems: FSolver::Harmonic2D
+ * (cfemm/fsolver/harmonic2d.cpp:36-790) with CBigComplexLinProb::PBCGSolveMod
+ * (cspars.cpp:822-895, 1062-1081) as the solver.
+ *
+ * The base descriptor carries the real parts; these arrays (same lengths as
+ * desc->blocks / lines / circs) carry what the AC formulation adds.  Linear
+ * problems: BHpoints must be 0 and LamType 0 (the reference itself rejects
+ * LamType 1/2 in AC analyses; wound regions with proximity effects, LamType
+ * > 2, and Case-2 circuits -- specified current in a conducting region,
+ * which adds unknowns -- return XFK_ERR_UNSUPPORTED).  Single device.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+    double J_im;                /* imaginary part of the source current density, MA/m^2 */
+    double Theta_hx, Theta_hy;  /* hysteresis lag, degrees */
+    double Lam_d;               /* lamination thickness, mm */
+} xfk_block_ac_desc;
+
+typedef struct {
+    double c0_im, c1_im;        /* mixed BC, imaginary parts */
+    double Mu, Sig;             /* small-skin-depth BC (BdryFormat 1): relative mu, MS/m */
+} xfk_line_ac_desc;
+
+typedef struct {
+    double amps_im, dvolts_im;
+} xfk_circuit_ac_desc;
+
+typedef struct {
+    double frequency;           /* Hz, > 0 */
+    const xfk_block_ac_desc *blocks;
+    const xfk_line_ac_desc *lines;      /* may be NULL when n_lines == 0 */
+    const xfk_circuit_ac_desc *circs;   /* may be NULL when n_circs == 0 */
+} xfk_harmonic_desc;
+
+int xfk_problem_create_harmonic(const xfk_problem_desc *desc, const xfk_harmonic_desc *ac, int device,
+                                xfk_problem **out);
+/* FSolver::Harmonic2D on the device (complex-symmetric COCG, the reference's
+ * stopping test |r| / |b| <= Precision).  flags as for xfk_static2d. */
+int xfk_harmonic2d(xfk_problem *prob, int flags, xfk_result *res);
+/* A = V * c at every node, interleaved (re, im). */
+int xfk_get_solution_complex(xfk_problem *prob, double *A_host);
+/* Circuit results: case, J and dV interleaved (re, im) per circuit. */
+int xfk_get_circuits_complex(xfk_problem *prob, int *ccase, double *J, double *dV);
+/* Assembled complex system after all boundary conditions (val, b interleaved). */
+int xfk_get_csr_complex(xfk_problem *prob, int *rowptr, int *col, double *val, double *b);
+
 /* Device views for the bench / tests (stream-ordered on the problem's stream). */
 int xfk_get_csr(xfk_problem *prob, int *rowptr, int *col, double *val, double *b);
 long long xfk_get_nnz(xfk_problem *prob);

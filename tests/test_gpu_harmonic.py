@@ -1,0 +1,108 @@
+"""Time-harmonic planar path (xfemm_amd/csrc/xfk_harmonic.hip) against the
+harmonic oracle (oracle/harmonic2d_oracle.c, itself bit-identical to the
+reference's cspars.cpp -- tests/test_oracle_harmonic.py).
+
+Tolerances (f64 / complex f64):
+  * assembled complex system after all boundary conditions vs the oracle:
+    max |diff| <= 1e-12 * max |A|  (element scatter order only)
+  * A at every node: max |dA| <= max(1e-6, 2 x the reference's own error) *
+    max |A|, the reference's own error being its distance from the exact
+    solution of the assembled system (both stop at |r| / |b| <= Precision,
+    the reference preconditioning COCG with SSOR, the device with Jacobi)
+  * the device solution solves its own system: |b - A V| / |b| <= 2 Precision
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import scipy.sparse.linalg as sla
+
+from oracle import harmonic as oh
+from util import C_ANS, rel_err, synth_to_oracle
+from xfemm_amd import kernels, synth
+
+pytestmark = pytest.mark.gpu
+
+TOL_SYSTEM = 1e-12
+TOL_A = 1e-6
+
+
+def _problem(kw):
+    pr, mesh, kk = synth_to_oracle(kw)
+    return pr, mesh, kk
+
+
+@pytest.mark.parametrize("periodic", [False, True])
+def test_harmonic_system_matches_oracle(periodic):
+    pr, mesh, kk = _problem(synth.harmonic(20, periodic=periodic))
+    P = kernels.Harmonic2DProblem(**kk)
+    P.solve()
+    rp, col, val, b = P.csr()
+    n = len(rp) - 1
+    G = sp.csr_matrix((val, col, rp), shape=(n, n))
+    O, bo = oh.system(pr, mesh)
+    scale = abs(O).max()
+    assert abs(G - O).max() <= TOL_SYSTEM * scale
+    assert np.abs(b - bo).max() <= TOL_SYSTEM * max(np.abs(bo).max(), 1e-300)
+    P.close()
+
+
+@pytest.mark.parametrize("cells,periodic", [(20, False), (24, True), (60, False)])
+def test_harmonic_solution_matches_oracle(cells, periodic):
+    pr, mesh, kk = _problem(synth.harmonic(cells, periodic=periodic))
+    P = kernels.Harmonic2DProblem(**kk)
+    r = P.solve()
+    A = P.solution()
+    Ao, st, circ_o = oh.solve(pr, mesh)
+    rp, col, val, b = P.csr()
+    n = len(rp) - 1
+    G = sp.csr_matrix((val, col, rp), shape=(n, n))
+    exact = sla.spsolve(G.tocsc(), b) * C_ANS
+    tol = max(TOL_A, 2.0 * rel_err(Ao, exact))
+    assert rel_err(A, Ao) <= tol
+    V = A / C_ANS
+    assert np.linalg.norm(b - G @ V) / np.linalg.norm(b) <= 2 * kk["precision"]
+    cc, J, dV = P.circuits()
+    for k, (case, Jo, dVo) in enumerate(circ_o):
+        assert cc[k] == case
+        assert abs(J[k] - Jo) <= 1e-12 * max(1.0, abs(Jo)) and abs(dV[k] - dVo) <= 1e-12 * max(1.0, abs(dVo))
+    assert r["cg_iters"] > 0
+    P.close()
+
+
+def test_harmonic_without_circuits_and_high_frequency():
+    kw = synth.harmonic(30, frequency=2000.0, circuits=False)
+    pr, mesh, kk = _problem(kw)
+    P = kernels.Harmonic2DProblem(**kk)
+    P.solve()
+    A = P.solution()
+    Ao, _, _ = oh.solve(pr, mesh)
+    rp, col, val, b = P.csr()
+    G = sp.csr_matrix((val, col, rp), shape=(len(rp) - 1,) * 2)
+    exact = sla.spsolve(G.tocsc(), b) * C_ANS
+    assert rel_err(A, Ao) <= max(TOL_A, 2.0 * rel_err(Ao, exact))
+    P.close()
+
+
+def test_harmonic_unsupported_cases_are_reported():
+    kw = synth.harmonic(10)
+    kw["circuits"][1] = dict(type=0, amps_re=1.0)       # specified current in a conductor: Case 2
+    with pytest.raises(kernels.XfkError, match="Case 2"):
+        kernels.Harmonic2DProblem(**kw)
+    kw = synth.harmonic(10)
+    kw["blocks"][1] = dict(kw["blocks"][1], LamType=1)
+    with pytest.raises(kernels.XfkError, match="On-edge lamination"):
+        kernels.Harmonic2DProblem(**kw)
+    kw = synth.magnetostatic(10)
+    with pytest.raises(kernels.XfkError):
+        kernels.Harmonic2DProblem(**dict(kw, frequency=0.0))
+
+
+def test_harmonic_repeatable():
+    kw = synth.harmonic(40)
+    P = kernels.Harmonic2DProblem(**kw)
+    P.solve()
+    A1 = P.solution()
+    P.solve(rebuild_symbolic=True)
+    A2 = P.solution()
+    P.close()
+    assert np.array_equal(A1, A2)

@@ -156,16 +156,9 @@ static int build_pbc_map(xfk_problem *P)
     return XFK_OK;
 }
 
-template <class T>
-static hipError_t upload(DBuf<T> &d, const T *h, size_t n, hipStream_t s)
-{
-    hipError_t e = d.alloc(n ? n : 1);
-    if (e != hipSuccess || n == 0) return e;
-    return hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, s);
-}
 
 // device -> host read-back ordered on the problem's (non-blocking) stream
-static hipError_t d2h(void *dst, const void *src, size_t bytes, hipStream_t s)
+hipError_t d2h(void *dst, const void *src, size_t bytes, hipStream_t s)
 {
     hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
     if (e != hipSuccess) return e;
@@ -235,7 +228,7 @@ struct SymTmp {
     }
 };
 
-static int build_symbolic(xfk_problem *P)
+int build_symbolic(xfk_problem *P)
 {
     hipStream_t s = P->stream;
     const int N = P->N, NL = P->NL, NE = P->NE;   // owned rows, local nodes, local elements
@@ -696,6 +689,7 @@ void xfk_problem_destroy(xfk_problem *P)
     for (auto &ev : P->spmv_ev) (void)hipEventDestroy(ev);
     if (P->pcg_host) (void)hipHostFree(P->pcg_host);
     if (P->nws_host) (void)hipHostFree(P->nws_host);
+    if (P->hc_host) (void)hipHostFree(P->hc_host);
     hipStream_t s = P->stream;
     delete P->amg;
     delete P;   // device buffers free themselves (DBuf), on this device
@@ -704,11 +698,13 @@ void xfk_problem_destroy(xfk_problem *P)
 
 }  // extern "C"
 
+namespace xfk {
+
 // ----------------------------------------------------------------------------
 // problem creation: validation, global preparation, local (per-rank) build
 // ----------------------------------------------------------------------------
 
-static int validate_desc(const xfk_problem_desc *d)
+int validate_desc(const xfk_problem_desc *d)
 {
     XFK_REQUIRE(d->n_nodes > 0 && d->n_elems > 0, XFK_ERR_ARG, "empty mesh");
     XFK_REQUIRE(d->x && d->y && d->p && d->lbl, XFK_ERR_ARG, "missing mesh arrays");
@@ -744,7 +740,7 @@ static int validate_desc(const xfk_problem_desc *d)
     return XFK_OK;
 }
 
-static int check_device(int device)
+int check_device(int device)
 {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
@@ -755,24 +751,7 @@ static int check_device(int device)
     return XFK_OK;
 }
 
-// Everything Static2D derives from the GLOBAL problem before the mesh is split
-// (so a sharded solve sees the same boundary values, point currents and
-// circuit currents as the single-device one).
-struct GlobalPrep {
-    std::vector<DevBlock> blk;
-    std::vector<double> hB, hH, hS;
-    std::vector<DevLabel> lab;
-    std::vector<DevLine> lin;
-    std::vector<DevCirc> circ;
-    std::vector<int> ebits;              // per element: 3 x 10-bit boundary-prop index + 1
-    std::vector<int> pt_nodes;           // nodes with a point current, ascending
-    std::vector<double> pt_J;            // 0.01 * J of each
-    std::vector<unsigned char> fixed;    // per node: Dirichlet value set
-    std::vector<double> first, last;     // first / last value set (CBigLinProb::SetValue order)
-    bool any_nonlinear = false;
-};
-
-static void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
+void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
 {
     const int N = d->n_nodes, NE = d->n_elems;
     const double c = kC;
@@ -911,7 +890,7 @@ static void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
 }
 
 // Build the device problem of one rank (plan == nullptr: the whole mesh).
-static int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *plan, int device,
+int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *plan, int device,
                        xfk_comm *comm, xfk_problem **out)
 {
     xfk_problem *P = new xfk_problem();
@@ -1045,6 +1024,8 @@ static int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const Par
     return XFK_OK;
 }
 
+}  // namespace xfk
+
 extern "C" {
 
 int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
@@ -1124,6 +1105,7 @@ int xfk_dist_get_info(const xfk_problem *P, xfk_dist_info *info)
 int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
 {
     XFK_REQUIRE(P, XFK_ERR_ARG, "null problem");
+    XFK_REQUIRE(!P->harmonic, XFK_ERR_ARG, "harmonic problem: use xfk_harmonic2d");
     XFK_CHECK(hipSetDevice(P->device));
     hipStream_t s = P->stream;
     hipEvent_t e0, e1, e2;

@@ -1,0 +1,896 @@
+// Time-harmonic planar problems on MI355X (gfx950): FSolver::Harmonic2D
+// (cfemm/fsolver/harmonic2d.cpp:36-790) with the complex-symmetric solve of
+// CBigComplexLinProb (cfemm/libfemm/cspars.cpp).
+//
+// Shares the static path's symbolic phase (CSR pattern, element colouring,
+// CSR slots, Dirichlet row/column lists, the composed periodic averaging map)
+// and stores the complex matrix as two value arrays over that pattern
+// (val = real parts, val_im), so the real-weighted periodic map applies to
+// each part unchanged.  Complex arithmetic follows femmcomplex.cpp's formulas
+// (products (ac - bd, ad + bc), quotients through the scaled reciprocal).
+//
+// Solver: the reference's PBCGSolve is COCG -- preconditioned CG with the
+// UNCONJUGATED bilinear form x.y, for complex-symmetric A -- stopping at
+// |r| / |b| <= Precision (cspars.cpp:822-895).  Here it runs in the
+// Chronopoulos-Gear arrangement of xfk_pcg.hip (two launches per iteration,
+// every inner product from one reduction phase) with a complex Jacobi
+// preconditioner in place of the sequential SSOR sweep; the three CGNE
+// start-up iterations of PCGSQStart (cspars.cpp:764-820) are not needed by it
+// and are omitted (the answer is the solution to the same tolerance).
+#include <cmath>
+#include <complex>
+
+#include "xfk_kernels.h"
+#include "xfk_spmv.h"
+
+namespace xfk {
+
+namespace {
+
+// ---- complex helpers (femmcomplex.cpp) ----
+__host__ __device__ __forceinline__ double2 cx(double re, double im) { return make_double2(re, im); }
+__host__ __device__ __forceinline__ double2 cadd(double2 a, double2 b) { return cx(a.x + b.x, a.y + b.y); }
+__host__ __device__ __forceinline__ double2 csub(double2 a, double2 b) { return cx(a.x - b.x, a.y - b.y); }
+__host__ __device__ __forceinline__ double2 cmul(double2 a, double2 b)
+{
+    return cx(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__host__ __device__ __forceinline__ double2 cscale(double2 a, double s) { return cx(a.x * s, a.y * s); }
+__host__ __device__ __forceinline__ double2 crecip(double2 z)
+{
+    double c;
+    double2 y;
+    if (fabs(z.x) > fabs(z.y)) {
+        c = z.y / z.x;
+        y.x = 1. / (z.x * (1. + c * c));
+        y.y = (-c) * y.x;
+    } else {
+        c = z.x / z.y;
+        y.y = (-1.) / (z.y * (1. + c * c));
+        y.x = (-c) * y.y;
+    }
+    return y;
+}
+__host__ __device__ __forceinline__ double2 cdiv(double2 a, double2 b) { return cmul(a, crecip(b)); }
+__host__ __device__ __forceinline__ double2 cexp_(double2 x)
+{
+    const double e = exp(x.x);
+    return cx(cos(x.y) * e, sin(x.y) * e);
+}
+__host__ __device__ __forceinline__ double2 ctanh_(double2 x)
+{
+    if (x.x > 0) {
+        double2 e = cexp_(cscale(x, -2.0));
+        return cdiv(cx(1 - e.x, -e.y), cx(1 + e.x, e.y));
+    }
+    double2 e = cexp_(cscale(x, 2.0));
+    return cdiv(cx(e.x - 1, e.y), cx(e.x + 1, e.y));
+}
+
+struct HarmArgs {
+    const int4 *erec;
+    const int *ebits;
+    const int *slot;
+    const double *x, *y;
+    const DevLabel *labels;
+    const DevBlockAC *blocks;
+    const DevLineAC *lines;
+    const DevCircAC *circs;
+    double *val, *val_im, *b, *b_im;
+    double w;
+};
+
+// One colour of the element loop (harmonic2d.cpp:352-630, linear: Iter == 0,
+// Mn == 0, v12 == 0): element matrices, eddy-current and boundary terms,
+// sources, colour-exclusive scatter into the complex CSR.
+__global__ void __launch_bounds__(kBlock) k_hassemble_color(int begin, int end, HarmArgs A)
+{
+    __shared__ int s_slot[kBlock * 9 + kBlock / 8];
+    const int tile0 = begin + blockIdx.x * kBlock;
+    const int ntile = min(kBlock, end - tile0);
+    if (ntile <= 0) return;
+    for (int k = threadIdx.x; k < ntile * 9; k += kBlock) {
+        int e = k / 9;
+        s_slot[k + (e >> 3)] = A.slot[(size_t)tile0 * 9 + k];
+    }
+    __syncthreads();
+    const int li = threadIdx.x;
+    if (li >= ntile) return;
+    const int i = tile0 + li;
+    const int4 r = A.erec[i];
+    const int n[3] = {r.x, r.y, r.z};
+    const DevLabel lab = A.labels[r.w];
+    const DevBlockAC bp = A.blocks[lab.blk];
+    const double X[3] = {A.x[n[0]], A.x[n[1]], A.x[n[2]]};
+    const double Y[3] = {A.y[n[0]], A.y[n[1]], A.y[n[2]]};
+    double p[3], q[3];
+    p[0] = Y[1] - Y[2]; p[1] = Y[2] - Y[0]; p[2] = Y[0] - Y[1];
+    q[0] = X[2] - X[1]; q[1] = X[0] - X[2]; q[2] = X[1] - X[0];
+    const double a = (p[0] * q[1] - p[1] * q[0]) / 2.;
+    const double K = (-1. / (4. * a));
+    double2 Me[3][3], be[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) Me[j][k] = cx(0, 0);
+        be[j] = cx(0, 0);
+    }
+    // eddy currents (harmonic2d.cpp:387-410)
+    if (bp.eddy && !lab.is_wound && bp.Cduct != 0.0) {
+        const double2 Ke = cx(-0.0 * a * A.w * bp.Cduct * kC / 12., -a * A.w * bp.Cduct * kC / 12.);
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int k = j; k < 3; ++k) {
+                Me[j][k] = cadd(Me[j][k], Ke);
+                Me[k][j] = cadd(Me[k][j], Ke);
+            }
+    }
+    // derivative boundary conditions (harmonic2d.cpp:412-438)
+    const int eb = A.ebits[i];
+    if (eb) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            int ej = ((eb >> (10 * j)) & 1023) - 1;
+            if (ej < 0) continue;
+            const DevLineAC ln = A.lines[ej];
+            if (ln.format != 1 && ln.format != 2) continue;
+            int k = (j + 1) % 3;
+            double lj = sqrt(pow(X[k] - X[j], 2.) + pow(Y[k] - Y[j], 2.));
+            double2 Kb;
+            if (ln.format == 2) {
+                Kb = cscale(cscale(ln.c0, -0.0001 * kC), lj);
+                Kb = cx(Kb.x / 6., Kb.y / 6.);
+                const double2 Kc = cx(ln.c1.x * lj / 2. * 0.0001, ln.c1.y * lj / 2. * 0.0001);
+                be[j] = cadd(be[j], Kc);
+                be[k] = cadd(be[k], Kc);
+            } else {
+                Kb = cscale(ln.zs, lj / 6.);
+            }
+            Me[j][j] = cadd(Me[j][j], cscale(Kb, 2.));
+            Me[k][k] = cadd(Me[k][k], cscale(Kb, 2.));
+            Me[j][k] = cadd(Me[j][k], Kb);
+            Me[k][j] = cadd(Me[k][j], Kb);
+        }
+    }
+    // source current density (harmonic2d.cpp:441-460)
+    double2 Jv = cx(0, 0);
+    if (lab.in_circuit >= 0) {
+        const DevCircAC C = A.circs[lab.in_circuit];
+        if (C.ccase == 1) Jv = C.J;
+        if (C.ccase == 0) Jv = cscale(C.dV, -bp.Cduct);
+    }
+    const double2 Jt = cadd(bp.J, Jv);
+    const double2 Ks = cx((-Jt.x * a) / 3., (-Jt.y * a) / 3.);
+    be[0] = cadd(be[0], Ks);
+    be[1] = cadd(be[1], Ks);
+    be[2] = cadd(be[2], Ks);
+    // Mx / mu2 + My / mu1 (harmonic2d.cpp:600-612)
+    const double2 r1 = crecip(bp.mu1), r2 = crecip(bp.mu2);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double mx = K * p[j] * p[k], my = K * q[j] * q[k];
+            Me[j][k] = cadd(Me[j][k], cadd(cscale(r2, mx), cscale(r1, my)));
+        }
+    const int *sl = &s_slot[li * 9 + (li >> 3)];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        if (sl[3 * j] < 0) continue;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double2 m = (k >= j) ? Me[j][k] : Me[k][j];
+            A.val[sl[3 * j + k]] += m.x;
+            A.val_im[sl[3 * j + k]] += m.y;
+        }
+        A.b[n[j]] += be[j].x;
+        A.b_im[n[j]] += be[j].y;
+    }
+}
+
+__global__ void k_hpoint(int n, const int *__restrict__ nodes, const double *__restrict__ J, double *__restrict__ b,
+                         double *__restrict__ b_im)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    b[nodes[i]] += J[2 * i];
+    b_im[nodes[i]] += J[2 * i + 1];
+}
+
+// CBigComplexLinProb::SetValue (cspars.cpp:482-537), column half: b[k] -= A(k,i) x_i
+// (first value set), A(k,i) = 0
+__global__ void k_hdir_cols(int n, const int *__restrict__ rows, const int *__restrict__ rowptr,
+                            const int *__restrict__ col, const unsigned char *__restrict__ fixed,
+                            const double *__restrict__ first, double *__restrict__ val, double *__restrict__ val_im,
+                            double *__restrict__ b, double *__restrict__ b_im)
+{
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    int r = rows[t];
+    double2 br = cx(b[r], b_im[r]);
+    for (int k = rowptr[r]; k < rowptr[r + 1]; ++k) {
+        int c = col[k];
+        if (!fixed[c]) continue;
+        const double2 z = cx(val[k], val_im[k]);
+        if (z.x != 0 || z.y != 0) {
+            br = csub(br, cmul(z, cx(first[2 * c], first[2 * c + 1])));
+            val[k] = 0.0;
+            val_im[k] = 0.0;
+        }
+    }
+    b[r] = br.x;
+    b_im[r] = br.y;
+}
+
+// row half: the fixed row keeps its diagonal, b = A_ii x_i (last value set)
+__global__ void k_hdir_rows(int n, const int *__restrict__ rows, const int *__restrict__ rowptr,
+                            const int *__restrict__ diag, double *__restrict__ val, double *__restrict__ val_im,
+                            double *__restrict__ b, double *__restrict__ b_im, const double *__restrict__ last)
+{
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    int r = rows[t];
+    int d = diag[r];
+    for (int k = rowptr[r]; k < rowptr[r + 1]; ++k)
+        if (k != d) {
+            val[k] = 0.0;
+            val_im[k] = 0.0;
+        }
+    const double2 v = cmul(cx(val[d], val_im[d]), cx(last[2 * r], last[2 * r + 1]));
+    b[r] = v.x;
+    b_im[r] = v.y;
+}
+
+// complex Jacobi preconditioner + the reference's singularity check (cspars.cpp:772-777)
+__global__ void k_hdiag_inv(int N, const int *__restrict__ diag, const double *__restrict__ val,
+                            const double *__restrict__ val_im, double2 *__restrict__ dinv, CcgState *S)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const double2 d = cx(val[diag[i]], val_im[diag[i]]);
+    if (d.x == 0.0 && d.y == 0.0) {
+        S->singular = 1;
+        dinv[i] = cx(0, 0);
+    } else {
+        dinv[i] = crecip(d);
+    }
+}
+
+// ---- COCG kernels ----
+constexpr int kHcCap = 4 * kCgBlock;   // complex products staged per LDS pass (64 KiB)
+constexpr int kHcAxBlock = 256;
+constexpr int kHcAxGrid = 1024;
+constexpr int kHcParts = 9;            // gam0 re/im, gam1 re/im, del re/im, rr0, rr1, bb
+
+// w = A u over the rows of one tile (CSR-stream through LDS, complex)
+__device__ __forceinline__ double2 hc_tile_spmv(int r0, int N, const int *__restrict__ rowptr,
+                                                const int *__restrict__ col, const double *__restrict__ val,
+                                                const double *__restrict__ val_im, const double2 *__restrict__ X,
+                                                double2 *lds)
+{
+    const int r = r0 + threadIdx.x;
+    const int rend = min(r0 + kCgBlock, N);
+    const int s = rowptr[r0], e = rowptr[rend];
+    const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
+    double2 acc = cx(0, 0);
+    for (int c0 = s; c0 < e; c0 += kHcCap) {
+        const int c1 = min(e, c0 + kHcCap);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int k = c0 + threadIdx.x + m * kCgBlock;
+            if (k < c1) lds[k - c0] = cmul(cx(val[k], val_im[k]), X[col[k]]);
+        }
+        __syncthreads();
+        const int a = max(my_s, c0), z = min(my_e, c1);
+        for (int k = a; k < z; ++k) acc = cadd(acc, lds[k - c0]);
+        __syncthreads();
+    }
+    return acc;
+}
+
+// sums of NV values over the workgroup, broadcast
+template <int NV>
+__device__ __forceinline__ void hc_block_sum(double (&v)[NV], double *red)
+{
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] = cg_wave_sum(v[q]);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < NV; ++q) red[NV * wid + q] = v[q];
+    __syncthreads();
+    const int nw = blockDim.x >> 6;
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+        double t = 0.0;
+        for (int w = 0; w < nw; ++w) t += red[NV * w + q];
+        v[q] = t;
+    }
+}
+
+struct HcArgs {
+    int N;
+    const int *rowptr, *col;
+    const double *val, *val_im;
+    double2 *x, *r, *u, *w, *z, *p;
+    const double2 *dinv;
+    double *part;     // kHcParts arrays of G
+    int G;
+    CcgState *S;
+};
+
+// r = b - A x0 (x0 = 0), u = M^-1 r, z = p = 0; partials gamma_0, |r0|^2, |b|^2
+__global__ void __launch_bounds__(kCgBlock) k_hc_init(HcArgs A, const double *__restrict__ b,
+                                                      const double *__restrict__ b_im)
+{
+    __shared__ double red[3 * (kCgBlock / 64) + 3];
+    const int i = blockIdx.x * kCgBlock + threadIdx.x;
+    double v[4] = {0, 0, 0, 0};
+    if (i < A.N) {
+        const double2 rr = cx(b[i], b_im[i]);
+        const double2 u = cmul(A.dinv[i], rr);
+        A.x[i] = cx(0, 0);
+        A.r[i] = rr;
+        A.u[i] = u;
+        A.z[i] = cx(0, 0);
+        A.p[i] = cx(0, 0);
+        const double2 g = cmul(rr, u);
+        v[0] = g.x;
+        v[1] = g.y;
+        v[2] = rr.x * rr.x + rr.y * rr.y;
+    }
+    double s3[3] = {v[0], v[1], v[2]};
+    hc_block_sum<3>(s3, red);
+    if (threadIdx.x == 0) {
+        A.part[0 * A.G + blockIdx.x] = s3[0];
+        A.part[1 * A.G + blockIdx.x] = s3[1];
+        A.part[6 * A.G + blockIdx.x] = s3[2];
+        A.part[8 * A.G + blockIdx.x] = s3[2];   // |b|^2 = |r0|^2 (x0 = 0)
+    }
+}
+
+// w = A u; partials delta = u.w (unconjugated)
+__global__ void __launch_bounds__(kCgBlock) k_hc_spmv(HcArgs A)
+{
+    if (A.S->done) return;
+    __shared__ __attribute__((aligned(16))) double2 lds[kHcCap];
+    __shared__ double red[2 * (kCgBlock / 64)];
+    const int r0 = blockIdx.x * kCgBlock;
+    const double2 w = hc_tile_spmv(r0, A.N, A.rowptr, A.col, A.val, A.val_im, A.u, lds);
+    const int i = r0 + threadIdx.x;
+    double s2[2] = {0, 0};
+    if (i < A.N) {
+        A.w[i] = w;
+        const double2 d = cmul(A.u[i], w);
+        s2[0] = d.x;
+        s2[1] = d.y;
+    }
+    hc_block_sum<2>(s2, red);
+    if (threadIdx.x == 0) {
+        A.part[4 * A.G + blockIdx.x] = s2[0];
+        A.part[5 * A.G + blockIdx.x] = s2[1];
+    }
+}
+
+// iteration `it`: reduce gamma_it, delta_it, |r_it|^2 (and |b|^2) -> alpha,
+// beta, the reference's stop test |r| / |b| <= Precision; then
+// z = w + beta z, p = u + beta p, x += alpha p, r -= alpha z, u = M^-1 r,
+// partials gamma_it+1, |r_it+1|^2
+__global__ void __launch_bounds__(kHcAxBlock) k_hc_axpy(HcArgs A, long long it, int Ggam)
+{
+    __shared__ double red[5 * (kHcAxBlock / 64)];
+    CcgState *S = A.S;
+    if (S->done) return;
+    const int par = (int)(it & 1);
+    double s5[5] = {0, 0, 0, 0, 0};
+    const int Gcg = (A.N + kCgBlock - 1) / kCgBlock;
+    for (int k = threadIdx.x; k < Ggam; k += blockDim.x) {
+        s5[0] += A.part[(2 * par) * A.G + k];
+        s5[1] += A.part[(2 * par + 1) * A.G + k];
+        s5[2] += A.part[(6 + par) * A.G + k];
+    }
+    for (int k = threadIdx.x; k < Gcg; k += blockDim.x) {
+        s5[3] += A.part[4 * A.G + k];
+        s5[4] += A.part[5 * A.G + k];
+    }
+    hc_block_sum<5>(s5, red);
+    const double2 gam = cx(s5[0], s5[1]), del = cx(s5[3], s5[4]);
+    const double rr = s5[2];
+    double bb;
+    if (it == 0) {
+        double sb[1] = {0};
+        for (int k = threadIdx.x; k < Gcg; k += blockDim.x) sb[0] += A.part[8 * A.G + k];
+        hc_block_sum<1>(sb, red);
+        bb = sb[0];
+    } else {
+        bb = S->bb;
+    }
+    double2 beta = cx(0, 0), alpha;
+    if (it == 0) {
+        alpha = cdiv(gam, del);
+    } else {
+        const double2 gp = cx(S->gam[(it - 1) & 1][0], S->gam[(it - 1) & 1][1]);
+        const double2 ap = cx(S->alp[(it - 1) & 1][0], S->alp[(it - 1) & 1][1]);
+        beta = cdiv(gam, gp);
+        alpha = cdiv(gam, csub(del, cdiv(cmul(beta, gam), ap)));
+    }
+    const double er = (bb == 0.0) ? 0.0 : sqrt(rr / bb);
+    const bool stop = (bb == 0.0) || (it >= 1 && er <= S->tol);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (it == 0) S->bb = bb;
+        S->er = er;
+        S->iters = it;
+        if (stop) S->done = 1;
+        S->gam[it & 1][0] = gam.x;
+        S->gam[it & 1][1] = gam.y;
+        S->alp[it & 1][0] = alpha.x;
+        S->alp[it & 1][1] = alpha.y;
+    }
+    if (stop) return;
+    double g[3] = {0, 0, 0};
+    for (int i = blockIdx.x * kHcAxBlock + threadIdx.x; i < A.N; i += gridDim.x * kHcAxBlock) {
+        const double2 z = cadd(A.w[i], cmul(beta, A.z[i]));
+        const double2 pp = cadd(A.u[i], cmul(beta, A.p[i]));
+        const double2 rn = csub(A.r[i], cmul(alpha, z));
+        const double2 u = cmul(A.dinv[i], rn);
+        A.x[i] = cadd(A.x[i], cmul(alpha, pp));
+        A.z[i] = z;
+        A.p[i] = pp;
+        A.r[i] = rn;
+        A.u[i] = u;
+        const double2 gg = cmul(rn, u);
+        g[0] += gg.x;
+        g[1] += gg.y;
+        g[2] += rn.x * rn.x + rn.y * rn.y;
+    }
+    hc_block_sum<3>(g, red);
+    if (threadIdx.x == 0) {
+        const int np = (int)((it + 1) & 1);
+        A.part[(2 * np) * A.G + blockIdx.x] = g[0];
+        A.part[(2 * np + 1) * A.G + blockIdx.x] = g[1];
+        A.part[(6 + np) * A.G + blockIdx.x] = g[2];
+    }
+}
+
+inline int nb256(long long n) { return (int)((n + kBlock - 1) / kBlock); }
+int hc_axpy_grid(int N)
+{
+    int g = (N + kHcAxBlock - 1) / kHcAxBlock;
+    return g < 1 ? 1 : (g < kHcAxGrid ? g : kHcAxGrid);
+}
+
+// ---- host: effective permeability and boundary constants (harmonic2d.cpp) ----
+using hcx = std::complex<double>;
+inline double2 h2(hcx z) { return cx(z.real(), z.imag()); }
+inline hcx hc(double2 z) { return hcx(z.x, z.y); }
+
+DevBlockAC effective_block(const xfk_block_desc &b, const xfk_block_ac_desc &ac, double w)
+{
+    // harmonic2d.cpp:190-235 with femmcomplex.cpp's exp / tanh / quotient formulas
+    DevBlockAC o{};
+    const double2 deg45 = cx(1, 1);
+    double2 m0, m1;
+    if (b.LamType == 0) {
+        m0 = cscale(cexp_(cx(-0.0 * ac.Theta_hx * kDEG, -ac.Theta_hx * kDEG)), b.mu_x);
+        m1 = cscale(cexp_(cx(-0.0 * ac.Theta_hy * kDEG, -ac.Theta_hy * kDEG)), b.mu_y);
+        if (ac.Lam_d != 0) {
+            if (b.Cduct != 0) {
+                double2 halflag = cexp_(cx(-0.0 * ac.Theta_hx * kDEG / 2., -ac.Theta_hx * kDEG / 2.));
+                double ds = sqrt(2. / (0.4 * kPI * w * b.Cduct * b.mu_x));
+                double2 K = cscale(cscale(cmul(halflag, deg45), ac.Lam_d), 0.001);
+                K = cx(K.x / (2. * ds), K.y / (2. * ds));
+                m0 = cscale(cdiv(cmul(m0, ctanh_(K)), K), b.LamFill);
+                m0.x += (1. - b.LamFill);
+                halflag = cexp_(cx(-0.0 * ac.Theta_hy * kDEG / 2., -ac.Theta_hy * kDEG / 2.));
+                ds = sqrt(2. / (0.4 * kPI * w * b.Cduct * b.mu_y));
+                K = cscale(cscale(cmul(halflag, deg45), ac.Lam_d), 0.001);
+                K = cx(K.x / (2. * ds), K.y / (2. * ds));
+                m1 = cscale(cdiv(cmul(m1, ctanh_(K)), K), b.LamFill);
+                m1.x += (1. - b.LamFill);
+            } else {
+                m0 = cscale(m0, b.LamFill);
+                m0.x += (1. - b.LamFill);
+                m1 = cscale(m1, b.LamFill);
+                m1.x += (1. - b.LamFill);
+            }
+        }
+    } else {
+        m0 = cx(1, 0);
+        m1 = cx(1, 0);
+    }
+    o.mu1 = m0;
+    o.mu2 = m1;
+    o.J = cx(b.J_re, ac.J_im);
+    o.Cduct = b.Cduct;
+    o.eddy = !((b.LamType == 0) && (ac.Lam_d > 0));
+    return o;
+}
+
+}  // namespace
+
+}  // namespace xfk
+
+using namespace xfk;
+
+namespace {
+
+int harmonic_validate(const xfk_problem_desc *d, const xfk_harmonic_desc *ac)
+{
+    XFK_REQUIRE(ac && ac->frequency > 0, XFK_ERR_ARG, "harmonic problems need a frequency > 0");
+    XFK_REQUIRE(d->n_blocks == 0 || ac->blocks, XFK_ERR_ARG, "missing AC block table");
+    XFK_REQUIRE(d->n_lines == 0 || ac->lines, XFK_ERR_ARG, "missing AC boundary table");
+    XFK_REQUIRE(d->n_circs == 0 || ac->circs, XFK_ERR_ARG, "missing AC circuit table");
+    for (int k = 0; k < d->n_blocks; ++k) {
+        XFK_REQUIRE(d->blocks[k].BHpoints == 0, XFK_ERR_UNSUPPORTED,
+                    "nonlinear (B-H) materials in harmonic problems are not supported by this build");
+        XFK_REQUIRE(d->blocks[k].LamType != 1 && d->blocks[k].LamType != 2, XFK_ERR_UNSUPPORTED,
+                    "On-edge lamination not supported in AC analyses");   // harmonic2d.cpp:76-85
+        XFK_REQUIRE(d->blocks[k].LamType <= 2, XFK_ERR_UNSUPPORTED,
+                    "wound regions with AC proximity effects (LamType > 2) are not supported by this build");
+    }
+    return XFK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_desc *ac, int device,
+                                xfk_problem **out)
+{
+    XFK_REQUIRE(d && out, XFK_ERR_ARG, "null argument");
+    *out = nullptr;
+    int rc = validate_desc(d);
+    if (rc == XFK_OK) rc = harmonic_validate(d, ac);
+    if (rc == XFK_OK) rc = check_device(device);
+    if (rc != XFK_OK) return rc;
+    const int N = d->n_nodes, NE = d->n_elems;
+    const double c = kC, w = ac->frequency * 2. * kPI;
+    const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
+    GlobalPrep G;
+    prepare_global(d, G);
+
+    // blocks, lines
+    std::vector<DevBlockAC> blk(std::max(1, d->n_blocks));
+    for (int k = 0; k < d->n_blocks; ++k) blk[k] = effective_block(d->blocks[k], ac->blocks[k], w);
+    std::vector<DevLineAC> lin(std::max(1, d->n_lines));
+    for (int k = 0; k < d->n_lines; ++k) {
+        DevLineAC &o = lin[k];
+        const xfk_line_desc &l = d->lines[k];
+        o.format = l.format;
+        o.c0 = cx(l.c0, ac->lines[k].c0_im);
+        o.c1 = cx(l.c1, ac->lines[k].c1_im);
+        o.zs = cx(0, 0);
+        if (l.format == 1) {   // harmonic2d.cpp:424-437
+            const double Mu = ac->lines[k].Mu, Sig = ac->lines[k].Sig;
+            XFK_REQUIRE(Mu > 0 && Sig > 0, XFK_ERR_ARG, "small-skin-depth boundary needs Mu > 0 and Sig > 0");
+            const double ds = sqrt(2. / (0.4 * kPI * w * Sig * Mu));
+            const double den = -ds * Mu * 100.;
+            o.zs = cx(1. / den, 1. / den);
+        }
+    }
+    // circuits (harmonic2d.cpp:86-170)
+    std::vector<DevCircAC> circ(std::max(1, d->n_circs));
+    if (d->n_circs > 0) {
+        std::vector<hcx> I1(d->n_circs), I2(d->n_circs), I3(d->n_circs);
+        for (int i = 0; i < NE; ++i) {
+            const DevLabel &L = G.lab[d->lbl[i]];
+            if (L.in_circuit == -1) continue;
+            const int *n = d->p + 3LL * i;
+            double p0 = d->y[n[1]] - d->y[n[2]], p1 = d->y[n[2]] - d->y[n[0]];
+            double q0 = d->x[n[2]] - d->x[n[1]], q1 = d->x[n[0]] - d->x[n[2]];
+            double a = (p0 * q1 - p1 * q0) / 2.;
+            double Cduct = d->blocks[L.blk].Cduct;
+            if (L.is_wound) Cduct = 0;
+            I1[L.in_circuit] += a;
+            I2[L.in_circuit] += a * Cduct;
+            I3[L.in_circuit] += hc(blk[L.blk].J) * a * 100.;
+        }
+        for (int k = 0; k < d->n_circs; ++k) {
+            DevCircAC &C = circ[k];
+            C.J = cx(0, 0);
+            C.dV = cx(0, 0);
+            if (d->circs[k].type == 0) {
+                XFK_REQUIRE(I2[k] == 0.0, XFK_ERR_UNSUPPORTED,
+                            "circuits with a specified current in a conducting region (Case 2: extra unknowns) "
+                            "are not supported by this build");
+                C.ccase = 1;
+                if (I1[k] != 0.0) {
+                    const hcx amps(d->circs[k].amps_re, ac->circs[k].amps_im);
+                    C.J = cdiv(h2(0.01 * (amps - I3[k])), h2(I1[k]));
+                }
+            } else {
+                C.ccase = 0;
+                C.dV = cx(d->circs[k].dvolts_re, ac->circs[k].dvolts_im);
+            }
+        }
+    }
+    // point currents and complex Dirichlet values, in SetValue order
+    std::vector<int> pt_nodes;
+    std::vector<double> pt_J;
+    std::vector<unsigned char> fixed(N, 0);
+    std::vector<double> first(2 * (size_t)N, 0.0), last(2 * (size_t)N, 0.0);
+    auto set_value = [&](int i, hcx x) {
+        if (!fixed[i]) {
+            first[2 * i] = x.real();
+            first[2 * i + 1] = x.imag();
+        }
+        fixed[i] = 1;
+        last[2 * i] = x.real();
+        last[2 * i + 1] = x.imag();
+    };
+    auto marker = [&](int i) { return d->marker ? d->marker[i] : -1; };
+    for (int i = 0; i < N; ++i) {
+        int m = marker(i);
+        if (m >= 0 && (d->points[m].J_re != 0 || d->points[m].J_im != 0)) {   // harmonic2d.cpp:634-641
+            pt_nodes.push_back(i);
+            pt_J.push_back(-0.01 * d->points[m].J_re);
+            pt_J.push_back(-0.01 * d->points[m].J_im);
+        }
+    }
+    for (int i = 0; i < N; ++i) {
+        int m = marker(i);
+        if (m >= 0 && d->points[m].J_re == 0 && d->points[m].J_im == 0)
+            set_value(i, hcx(d->points[m].A_re, d->points[m].A_im) / c);
+    }
+    auto edge = [&](long long k) { return d->e ? d->e[k] : -1; };
+    for (int i = 0; i < NE; ++i)
+        for (int j = 0; j < 3; ++j) {
+            int k = (j + 1) % 3;
+            int sgi = edge(3LL * i + j);
+            if (sgi < 0 || d->lines[sgi].format != 0) continue;
+            const xfk_line_desc &ln = d->lines[sgi];
+            int nodes2[2] = {d->p[3LL * i + j], d->p[3LL * i + k]};
+            for (int m = 0; m < 2; ++m) {
+                double x = d->x[nodes2[m]], y = d->y[nodes2[m]], a;
+                if (d->coords == 0) {
+                    x /= units[d->length_units];
+                    y /= units[d->length_units];
+                    a = ln.A0 + x * ln.A1 + y * ln.A2;
+                } else {
+                    double r = sqrt(x * x + y * y), t;
+                    if ((x == 0) && (y == 0)) t = 0;
+                    else t = atan2(y, x) / kDEG;
+                    r /= units[d->length_units];
+                    a = ln.A0 + r * ln.A1 + t * ln.A2;
+                }
+                const double2 e = cexp_(cx(0.0 * ln.phi * kDEG, ln.phi * kDEG));
+                set_value(nodes2[m], hcx((a / c) * e.x, (a / c) * e.y));   // harmonic2d.cpp:664-730
+            }
+        }
+    for (int i = 0; i < N; ++i)
+        XFK_REQUIRE((fixed[i] != 0) == (G.fixed[i] != 0), XFK_ERR_ARG, "internal: Dirichlet node sets differ");
+
+    xfk_problem *P = nullptr;
+    rc = build_local(d, G, nullptr, device, nullptr, &P);
+    if (rc != XFK_OK) return rc;
+    P->harmonic = true;
+    P->omega = w;
+    P->any_nonlinear = false;
+    P->hcircs = circ;
+    P->nhpt = (int)pt_nodes.size();
+    hipStream_t s = P->stream;
+    hipError_t e = hipSuccess;
+#define UP(buf, ptr, n) if (e == hipSuccess) e = upload(buf, ptr, n, s)
+    UP(P->blocks_ac, blk.data(), blk.size());
+    UP(P->lines_ac, lin.data(), lin.size());
+    UP(P->circs_ac, circ.data(), circ.size());
+    UP(P->hpt_nodes, pt_nodes.data(), pt_nodes.size());
+    UP(P->hpt_J, pt_J.data(), pt_J.size());
+    UP(P->hfix_first, first.data(), first.size());
+    UP(P->hfix_last, last.data(), last.size());
+#undef UP
+    if (e == hipSuccess) e = hipHostMalloc((void **)&P->hc_host, sizeof(CcgState));
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        set_error(std::string("upload failed: ") + hipGetErrorString(e));
+        xfk_problem_destroy(P);
+        return XFK_ERR_HIP;
+    }
+    *out = P;
+    return XFK_OK;
+}
+
+int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
+{
+    XFK_REQUIRE(P && P->harmonic, XFK_ERR_ARG, "not a harmonic problem (xfk_problem_create_harmonic)");
+    XFK_CHECK(hipSetDevice(P->device));
+    hipStream_t s = P->stream;
+    hipEvent_t e0, e1, e2;
+    XFK_CHECK(hipEventCreate(&e0));
+    XFK_CHECK(hipEventCreate(&e1));
+    XFK_CHECK(hipEventCreate(&e2));
+    xfk_result R{};
+    float ms = 0;
+    XFK_CHECK(hipEventRecord(e0, s));
+    if (!P->symbolic_ready || (flags & XFK_REBUILD_SYMBOLIC)) {
+        P->symbolic_ready = false;
+        int rc = build_symbolic(P);
+        if (rc != XFK_OK) return rc;
+    }
+    XFK_CHECK(hipEventRecord(e1, s));
+    XFK_CHECK(hipEventSynchronize(e1));
+    XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    R.ms_symbolic = ms;
+
+    const int N = P->N;
+    const long long nnz = P->nnz;
+    XFK_CHECK(hipEventRecord(e0, s));
+    XFK_CHECK(P->val.alloc((size_t)nnz));
+    XFK_CHECK(P->val_im.alloc((size_t)nnz));
+    XFK_CHECK(P->b.alloc((size_t)N));
+    XFK_CHECK(P->b_im.alloc((size_t)N));
+    XFK_CHECK(hipMemsetAsync(P->val.p, 0, sizeof(double) * nnz, s));
+    XFK_CHECK(hipMemsetAsync(P->val_im.p, 0, sizeof(double) * nnz, s));
+    XFK_CHECK(hipMemsetAsync(P->b.p, 0, sizeof(double) * N, s));
+    XFK_CHECK(hipMemsetAsync(P->b_im.p, 0, sizeof(double) * N, s));
+    HarmArgs A;
+    A.erec = P->erec.p;
+    A.ebits = P->ebits.p;
+    A.slot = P->slot.p;
+    A.x = P->x.p;
+    A.y = P->y.p;
+    A.labels = P->labels.p;
+    A.blocks = P->blocks_ac.p;
+    A.lines = P->lines_ac.p;
+    A.circs = P->circs_ac.p;
+    A.val = P->val.p;
+    A.val_im = P->val_im.p;
+    A.b = P->b.p;
+    A.b_im = P->b_im.p;
+    A.w = P->omega;
+    for (int cl = 0; cl < P->ncolors; ++cl) {
+        const int n = P->color_off[cl + 1] - P->color_off[cl];
+        if (n > 0) k_hassemble_color<<<nb256(n), kBlock, 0, s>>>(P->color_off[cl], P->color_off[cl + 1], A);
+    }
+    if (P->nhpt > 0) k_hpoint<<<nb256(P->nhpt), kBlock, 0, s>>>(P->nhpt, P->hpt_nodes.p, P->hpt_J.p, P->b.p, P->b_im.p);
+    if (P->nfix_cols > 0) {
+        // rows that are not fixed but couple to a fixed node: k_hdir_cols walks those rows
+        k_hdir_cols<<<nb256(P->nfix_cols), kBlock, 0, s>>>(P->nfix_cols, P->fix_cols_row.p, P->rowptr.p,
+                                                           P->col.p, P->fixed.p, P->hfix_first.p, P->val.p,
+                                                           P->val_im.p, P->b.p, P->b_im.p);
+    }
+    if (P->nfix_rows > 0)
+        k_hdir_rows<<<nb256(P->nfix_rows), kBlock, 0, s>>>(P->nfix_rows, P->fix_rows.p, P->rowptr.p, P->diag.p,
+                                                           P->val.p, P->val_im.p, P->b.p, P->b_im.p,
+                                                           P->hfix_last.p);
+    launch_map(s, P->pm_n, P->pm_dst.p, P->pm_ptr.p, P->pm_src.p, P->pm_w.p, P->val.p, P->pm_tmp.p);
+    launch_map(s, P->pm_n, P->pm_dst.p, P->pm_ptr.p, P->pm_src.p, P->pm_w.p, P->val_im.p, P->pm_tmp.p);
+    launch_map(s, P->pb_n, P->pb_dst.p, P->pb_ptr.p, P->pb_src.p, P->pb_w.p, P->b.p, P->pb_tmp.p);
+    launch_map(s, P->pb_n, P->pb_dst.p, P->pb_ptr.p, P->pb_src.p, P->pb_w.p, P->b_im.p, P->pb_tmp.p);
+    XFK_CHECK(hipGetLastError());
+    XFK_CHECK(hipEventRecord(e1, s));
+
+    // COCG (Jacobi), Chronopoulos-Gear arrangement
+    const int Gcg = (N + kCgBlock - 1) / kCgBlock, Gax = hc_axpy_grid(N);
+    const int G = std::max(Gcg, Gax);
+    XFK_CHECK(P->hc_vec.alloc(7 * (size_t)N));
+    XFK_CHECK(P->hc_part.alloc((size_t)kHcParts * G));
+    XFK_CHECK(P->hc_state.alloc(1));
+    XFK_CHECK(hipMemsetAsync(P->hc_part.p, 0, sizeof(double) * kHcParts * G, s));
+    CcgState init{};
+    init.tol = P->precision;
+    XFK_CHECK(hipMemcpyAsync(P->hc_state.p, &init, sizeof(CcgState), hipMemcpyHostToDevice, s));
+    HcArgs H;
+    H.N = N;
+    H.rowptr = P->rowptr.p;
+    H.col = P->col.p;
+    H.val = P->val.p;
+    H.val_im = P->val_im.p;
+    double2 *v = P->hc_vec.p;
+    H.x = v;
+    H.r = v + N;
+    H.u = v + 2 * (size_t)N;
+    H.w = v + 3 * (size_t)N;
+    H.z = v + 4 * (size_t)N;
+    H.p = v + 5 * (size_t)N;
+    double2 *dinv = v + 6 * (size_t)N;
+    H.dinv = dinv;
+    H.part = P->hc_part.p;
+    H.G = G;
+    H.S = P->hc_state.p;
+    k_hdiag_inv<<<nb256(N), kBlock, 0, s>>>(N, P->diag.p, P->val.p, P->val_im.p, dinv, P->hc_state.p);
+    XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
+    XFK_CHECK(hipStreamSynchronize(s));
+    if (P->hc_host->singular) {
+        set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
+        return XFK_ERR_SINGULAR;
+    }
+    k_hc_init<<<Gcg, kCgBlock, 0, s>>>(H, P->b.p, P->b_im.p);
+    k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H);
+    long long it = 0;
+    int batch = 32;
+    const long long cap = std::max<long long>(100000, 20LL * N);
+    for (;;) {
+        for (int k = 0; k < batch; ++k, ++it) {
+            k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, it == 0 ? Gcg : Gax);
+            k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H);
+        }
+        XFK_CHECK(hipGetLastError());
+        XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
+        XFK_CHECK(hipStreamSynchronize(s));
+        const CcgState &S = *P->hc_host;
+        if (S.done) break;
+        if (it >= cap) {
+            set_error("COCG did not converge within the iteration cap");
+            return XFK_ERR_NOCONV;
+        }
+        double rate = (S.iters > 0 && S.er > 0 && S.er < 1) ? std::log(S.er) / (double)S.iters : 0.0;
+        long long rem = rate < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / rate) : 2 * batch;
+        batch = (int)std::max<long long>(8, std::min<long long>(rem + 2, 512));
+    }
+    XFK_CHECK(hipEventRecord(e2, s));
+    XFK_CHECK(hipEventSynchronize(e2));
+    XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    R.ms_assemble = ms;
+    XFK_CHECK(hipEventElapsedTime(&ms, e1, e2));
+    R.ms_solve = ms;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(e2);
+    R.newton_iters = 1;
+    R.cg_iters = P->hc_host->iters;
+    R.final_er = P->hc_host->er;
+    R.nnz = P->nnz;
+    R.ncolors = P->ncolors;
+    R.color_rounds = P->color_rounds;
+    R.precond = XFK_PRECOND_JACOBI;
+    P->last = R;
+    if (res) *res = R;
+    return XFK_OK;
+}
+
+int xfk_get_solution_complex(xfk_problem *P, double *A)
+{
+    XFK_REQUIRE(P && A && P->harmonic, XFK_ERR_ARG, "null argument or not a harmonic problem");
+    XFK_REQUIRE(P->symbolic_ready && P->hc_vec.p, XFK_ERR_ARG, "no solution yet");
+    XFK_CHECK(hipSetDevice(P->device));
+    XFK_CHECK(d2h(A, P->hc_vec.p, sizeof(double2) * P->N, P->stream));
+    for (int i = 0; i < 2 * P->N; ++i) A[i] *= kC;   // harmonic2d.cpp:783
+    return XFK_OK;
+}
+
+int xfk_get_circuits_complex(xfk_problem *P, int *ccase, double *J, double *dV)
+{
+    XFK_REQUIRE(P && P->harmonic, XFK_ERR_ARG, "not a harmonic problem");
+    for (int k = 0; k < P->ncircs; ++k) {
+        const DevCircAC &C = P->hcircs[k];
+        if (ccase) ccase[k] = C.ccase;
+        if (J) { J[2 * k] = C.J.x; J[2 * k + 1] = C.J.y; }
+        if (dV) { dV[2 * k] = C.dV.x; dV[2 * k + 1] = C.dV.y; }
+    }
+    return XFK_OK;
+}
+
+int xfk_get_csr_complex(xfk_problem *P, int *rowptr, int *col, double *val, double *b)
+{
+    XFK_REQUIRE(P && P->harmonic && P->symbolic_ready && P->val_im.p, XFK_ERR_ARG, "no assembled harmonic system");
+    XFK_CHECK(hipSetDevice(P->device));
+    hipStream_t s = P->stream;
+    XFK_CHECK(hipStreamSynchronize(s));
+    if (rowptr) XFK_CHECK(d2h(rowptr, P->rowptr.p, sizeof(int) * (P->N + 1), s));
+    if (col) XFK_CHECK(d2h(col, P->col.p, sizeof(int) * P->nnz, s));
+    if (val) {
+        std::vector<double> re(P->nnz), im(P->nnz);
+        XFK_CHECK(d2h(re.data(), P->val.p, sizeof(double) * P->nnz, s));
+        XFK_CHECK(d2h(im.data(), P->val_im.p, sizeof(double) * P->nnz, s));
+        for (long long k = 0; k < P->nnz; ++k) {
+            val[2 * k] = re[k];
+            val[2 * k + 1] = im[k];
+        }
+    }
+    if (b) {
+        std::vector<double> re(P->N), im(P->N);
+        XFK_CHECK(d2h(re.data(), P->b.p, sizeof(double) * P->N, s));
+        XFK_CHECK(d2h(im.data(), P->b_im.p, sizeof(double) * P->N, s));
+        for (int i = 0; i < P->N; ++i) {
+            b[2 * i] = re[i];
+            b[2 * i + 1] = im[i];
+        }
+    }
+    return XFK_OK;
+}
+
+}  // extern "C"

@@ -109,6 +109,37 @@ struct CgState {
     long long iters;
 };
 
+// Time-harmonic tables (xfk_harmonic.hip): complex values as double2 {re, im}.
+struct DevBlockAC {
+    double2 mu1, mu2;   // effective permeabilities Mu[k][0], Mu[k][1] (harmonic2d.cpp:190-235)
+    double2 J;          // source current density
+    double Cduct;
+    int eddy;           // 0: laminated (Lam_d > 0) blocks carry no bulk eddy current (harmonic2d.cpp:392-394)
+    int pad;
+};
+
+struct DevLineAC {
+    double2 c0, c1;     // mixed BC
+    double2 zs;         // small-skin-depth BC: (1+I) / (-ds Mu 100) (harmonic2d.cpp:424-437), times l/6 per edge
+    int format, pad;
+};
+
+struct DevCircAC {
+    double2 J;          // Case 1: applied current density
+    double2 dV;         // Case 0: voltage gradient
+    int ccase, pad;
+};
+
+// State of the complex-symmetric Chronopoulos-Gear COCG (xfk_harmonic.hip)
+struct CcgState {
+    double bb;            // |b|^2
+    double gam[2][2];     // gamma_i = r.u (unconjugated), parity rings, {re, im}
+    double alp[2][2];
+    double er, tol;
+    int done, singular;
+    long long iters;
+};
+
 struct NewtonScalars {
     double dx2;       // sum (V - Vold)^2
     double v2;        // sum V^2
@@ -249,6 +280,23 @@ struct xfk_problem {
     xfk::Amg *amg = nullptr;         // hierarchy of the current matrix (xfk_amg.hip)
     int pc_used = XFK_PRECOND_JACOBI;  // preconditioner of the running solve
 
+    // time-harmonic problem (xfk_problem_create_harmonic, xfk_harmonic.hip)
+    bool harmonic = false;
+    double omega = 0;                  // 2 pi f
+    xfk::DBuf<xfk::DevBlockAC> blocks_ac;
+    xfk::DBuf<xfk::DevLineAC> lines_ac;
+    xfk::DBuf<xfk::DevCircAC> circs_ac;
+    std::vector<xfk::DevCircAC> hcircs;          // host copy (circuit results)
+    xfk::DBuf<double> val_im, b_im;              // imaginary parts of val, b
+    xfk::DBuf<double> hfix_first, hfix_last;     // 2 per node {re, im}
+    xfk::DBuf<int> hpt_nodes;
+    xfk::DBuf<double> hpt_J;                     // 2 per point node: -0.01 J
+    int nhpt = 0;
+    xfk::DBuf<double2> hc_vec;                   // COCG vectors: x, r, u, w, z, p, dinv (N each)
+    xfk::DBuf<double> hc_part;                   // per-block partials, 9 arrays
+    xfk::DBuf<xfk::CcgState> hc_state;
+    xfk::CcgState *hc_host = nullptr;            // pinned mirror
+
     // live SpMV launch timing (XFK_TIME_SPMV)
     bool time_spmv = false;
     std::vector<hipEvent_t> spmv_ev;   // pairs
@@ -257,3 +305,43 @@ struct xfk_problem {
     // last-solve statistics
     xfk_result last{};
 };
+
+// Host-side helpers shared by the static (xfk_api.hip) and harmonic
+// (xfk_harmonic.hip) drivers.
+namespace xfk {
+
+// Everything Static2D derives from the GLOBAL problem before the mesh is split
+// (so a sharded solve sees the same boundary values, point currents and
+// circuit currents as the single-device one).
+struct GlobalPrep {
+    std::vector<DevBlock> blk;
+    std::vector<double> hB, hH, hS;
+    std::vector<DevLabel> lab;
+    std::vector<DevLine> lin;
+    std::vector<DevCirc> circ;
+    std::vector<int> ebits;              // per element: 3 x 10-bit boundary-prop index + 1
+    std::vector<int> pt_nodes;           // nodes with a point current, ascending
+    std::vector<double> pt_J;            // 0.01 * J of each
+    std::vector<unsigned char> fixed;    // per node: Dirichlet value set
+    std::vector<double> first, last;     // first / last value set (CBigLinProb::SetValue order)
+    bool any_nonlinear = false;
+};
+
+int validate_desc(const xfk_problem_desc *d);
+int check_device(int device);
+void prepare_global(const xfk_problem_desc *d, GlobalPrep &G);
+// the device problem of one rank (plan == nullptr: the whole mesh)
+int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *plan, int device, xfk_comm *comm,
+                xfk_problem **out);
+int build_symbolic(xfk_problem *P);
+hipError_t d2h(void *dst, const void *src, size_t bytes, hipStream_t s);
+// host -> device copy into a (re)allocated buffer, ordered on `s`
+template <class T>
+inline hipError_t upload(DBuf<T> &d, const T *h, size_t n, hipStream_t s)
+{
+    hipError_t e = d.alloc(n ? n : 1);
+    if (e != hipSuccess || n == 0) return e;
+    return hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, s);
+}
+
+}  // namespace xfk

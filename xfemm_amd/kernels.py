@@ -34,6 +34,8 @@ EXPORTED = (
     "xfk_last_error", "xfk_device_count", "xfk_problem_create", "xfk_problem_destroy",
     "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz",
     "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_solve_csr_pc", "xfk_pcg_time", "xfk_set_option",
+    "xfk_problem_create_harmonic", "xfk_harmonic2d", "xfk_get_solution_complex", "xfk_get_circuits_complex",
+    "xfk_get_csr_complex",
     "xfk_comm_unique_id", "xfk_comm_create_rccl", "xfk_comm_create_local", "xfk_comm_destroy",
     "xfk_comm_rank", "xfk_comm_size", "xfk_partition_plan", "xfk_problem_create_dist", "xfk_dist_get_info",
 )
@@ -131,6 +133,11 @@ def load_library(path: str = KERNELS_SO):
                                        C.c_int, C.POINTER(C.c_longlong), dptr]
     L.xfk_pcg_time.argtypes = [C.c_void_p, C.c_int, dptr, dptr]
     L.xfk_set_option.argtypes = [C.c_void_p, C.c_int, C.c_double]
+    L.xfk_problem_create_harmonic.argtypes = [C.POINTER(ProblemDesc), C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+    L.xfk_harmonic2d.argtypes = [C.c_void_p, C.c_int, C.POINTER(Result)]
+    L.xfk_get_solution_complex.argtypes = [C.c_void_p, dptr]
+    L.xfk_get_circuits_complex.argtypes = [C.c_void_p, iptr, dptr, dptr]
+    L.xfk_get_csr_complex.argtypes = [C.c_void_p, iptr, iptr, dptr, dptr]
     vp = C.c_void_p
     L.xfk_comm_unique_id.argtypes = [C.c_char_p, C.c_int]
     L.xfk_comm_create_rccl.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
@@ -167,6 +174,64 @@ class _Keep(list):
         return a.ctypes.data_as(iptr)
 
 
+def _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision, length_units,
+               coords, relax):
+    """xfk_problem_desc of plain arrays / dicts (see Static2DProblem); returns
+    (desc, keep) where keep holds every buffer the descriptor points into."""
+    keep = _Keep()
+    nb = max(1, len(blocks))
+    bl = (BlockDesc * nb)()
+    for k, b in enumerate(blocks):
+        o = bl[k]
+        o.mu_x, o.mu_y = b.get("mu_x", 1.0), b.get("mu_y", 1.0)
+        o.H_c, o.J_re, o.Cduct = b.get("H_c", 0.0), b.get("J_re", 0.0), b.get("Cduct", 0.0)
+        o.LamFill, o.LamType = b.get("LamFill", 1.0), b.get("LamType", 0)
+        n = len(b.get("B", ()))
+        o.BHpoints = n
+        if n:
+            o.B, o.H, o.slope = keep.d(b["B"]), keep.d(b["H"]), keep.d(b["slope"])
+    lb = (LabelDesc * max(1, len(labels)))()
+    for k, l in enumerate(labels):
+        lb[k].block, lb[k].in_circuit = l["block"], l.get("in_circuit", -1)
+        lb[k].mag_dir, lb[k].is_wound = l.get("mag_dir", 0.0), int(l.get("is_wound", 0))
+    ln = (LineDesc * max(1, len(lines)))()
+    for k, l in enumerate(lines):
+        o = ln[k]
+        o.format = l.get("format", 0)
+        o.A0, o.A1, o.A2, o.phi = l.get("A0", 0.0), l.get("A1", 0.0), l.get("A2", 0.0), l.get("phi", 0.0)
+        o.c0, o.c1 = l.get("c0", 0.0), l.get("c1", 0.0)
+    pt = (PointDesc * max(1, len(points)))()
+    for k, q in enumerate(points):
+        pt[k].A_re, pt[k].A_im = q.get("A_re", 0.0), q.get("A_im", 0.0)
+        pt[k].J_re, pt[k].J_im = q.get("J_re", 0.0), q.get("J_im", 0.0)
+    ci = (CircuitDesc * max(1, len(circuits)))()
+    for k, q in enumerate(circuits):
+        ci[k].type, ci[k].amps_re, ci[k].dvolts_re = q.get("type", 0), q.get("amps_re", 0.0), q.get("dvolts_re", 0.0)
+    D = ProblemDesc()
+    x = np.asarray(x, dtype=np.float64)
+    D.n_nodes = len(x)
+    D.x, D.y = keep.d(x), keep.d(y)
+    D.marker = keep.i(marker) if marker is not None else None
+    p = np.asarray(p, dtype=np.int32).reshape(-1)
+    D.n_elems = len(p) // 3
+    D.p = keep.i(p)
+    D.e = keep.i(np.asarray(e, dtype=np.int32).reshape(-1)) if e is not None else None
+    D.lbl = keep.i(lbl)
+    D.n_blocks, D.blocks = len(blocks), bl
+    D.n_labels, D.labels = len(labels), lb
+    D.n_lines, D.lines = len(lines), ln
+    D.n_points, D.points = len(points), pt
+    D.n_circs, D.circs = len(circuits), ci
+    if pbc is not None and len(pbc):
+        pb = np.asarray(pbc, dtype=np.int32).reshape(-1)
+        D.n_pbc, D.pbc = len(pb) // 3, keep.i(pb)
+    else:
+        D.n_pbc, D.pbc = 0, None
+    D.precision, D.length_units, D.coords, D.relax = precision, length_units, coords, relax
+    keep.extend([bl, lb, ln, pt, ci])
+    return D, keep
+
+
 class Static2DProblem:
     """One device-resident static 2-D magnetostatic problem (FSolver::Static2D).
 
@@ -177,61 +242,18 @@ class Static2DProblem:
                  lines: Sequence[dict] = (), points: Sequence[dict] = (), circuits: Sequence[dict] = (),
                  marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0,
                  device=0, comm: Optional["Comm"] = None, precond: str = "amg", amg_sweeps: Optional[int] = None,
-                 amg_theta: Optional[float] = None):
+                 amg_theta: Optional[float] = None, frequency: float = 0.0):
         """comm: shard the mesh by row blocks over this communicator (every rank
         passes the same global problem; solve() and solution() are collective).
         precond: "amg" (smoothed-aggregation V-cycle, default) or "jacobi"."""
+        if frequency:
+            raise XfkError("frequency != 0: use Harmonic2DProblem")
         L = load_library()
-        keep = _Keep()
-        nb = max(1, len(blocks))
-        bl = (BlockDesc * nb)()
-        for k, b in enumerate(blocks):
-            o = bl[k]
-            o.mu_x, o.mu_y = b.get("mu_x", 1.0), b.get("mu_y", 1.0)
-            o.H_c, o.J_re, o.Cduct = b.get("H_c", 0.0), b.get("J_re", 0.0), b.get("Cduct", 0.0)
-            o.LamFill, o.LamType = b.get("LamFill", 1.0), b.get("LamType", 0)
-            n = len(b.get("B", ()))
-            o.BHpoints = n
-            if n:
-                o.B, o.H, o.slope = keep.d(b["B"]), keep.d(b["H"]), keep.d(b["slope"])
-        lb = (LabelDesc * max(1, len(labels)))()
-        for k, l in enumerate(labels):
-            lb[k].block, lb[k].in_circuit = l["block"], l.get("in_circuit", -1)
-            lb[k].mag_dir, lb[k].is_wound = l.get("mag_dir", 0.0), int(l.get("is_wound", 0))
-        ln = (LineDesc * max(1, len(lines)))()
-        for k, l in enumerate(lines):
-            o = ln[k]
-            o.format = l.get("format", 0)
-            o.A0, o.A1, o.A2, o.phi = l.get("A0", 0.0), l.get("A1", 0.0), l.get("A2", 0.0), l.get("phi", 0.0)
-            o.c0, o.c1 = l.get("c0", 0.0), l.get("c1", 0.0)
-        pt = (PointDesc * max(1, len(points)))()
-        for k, q in enumerate(points):
-            pt[k].A_re, pt[k].A_im = q.get("A_re", 0.0), q.get("A_im", 0.0)
-            pt[k].J_re, pt[k].J_im = q.get("J_re", 0.0), q.get("J_im", 0.0)
-        ci = (CircuitDesc * max(1, len(circuits)))()
-        for k, q in enumerate(circuits):
-            ci[k].type, ci[k].amps_re, ci[k].dvolts_re = q.get("type", 0), q.get("amps_re", 0.0), q.get("dvolts_re", 0.0)
-        D = ProblemDesc()
-        x = np.asarray(x, dtype=np.float64)
-        self.n_nodes = D.n_nodes = len(x)
-        D.x, D.y = keep.d(x), keep.d(y)
-        D.marker = keep.i(marker) if marker is not None else None
-        p = np.asarray(p, dtype=np.int32).reshape(-1)
-        self.n_elems = D.n_elems = len(p) // 3
-        D.p = keep.i(p)
-        D.e = keep.i(np.asarray(e, dtype=np.int32).reshape(-1)) if e is not None else None
-        D.lbl = keep.i(lbl)
-        D.n_blocks, D.blocks = len(blocks), bl
-        D.n_labels, D.labels = len(labels), lb
-        D.n_lines, D.lines = len(lines), ln
-        D.n_points, D.points = len(points), pt
-        D.n_circs, D.circs = len(circuits), ci
-        if pbc is not None and len(pbc):
-            pb = np.asarray(pbc, dtype=np.int32).reshape(-1)
-            D.n_pbc, D.pbc = len(pb) // 3, keep.i(pb)
-        else:
-            D.n_pbc, D.pbc = 0, None
-        D.precision, D.length_units, D.coords, D.relax = precision, length_units, coords, relax
+        D, keep = _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision,
+                             length_units, coords, relax)
+        self._keep = keep
+        self.n_nodes = D.n_nodes
+        self.n_elems = D.n_elems
         self.n_circs = len(circuits)
         h = C.c_void_p()
         self.comm = comm
@@ -304,6 +326,99 @@ class Static2DProblem:
         ms_iter = C.c_double()
         _check(_lib.xfk_pcg_time(self._h, iters, C.byref(ms_spmv), C.byref(ms_iter)))
         return ms_spmv.value, ms_iter.value
+
+
+class BlockAcDesc(C.Structure):
+    _fields_ = [("J_im", C.c_double), ("Theta_hx", C.c_double), ("Theta_hy", C.c_double), ("Lam_d", C.c_double)]
+
+
+class LineAcDesc(C.Structure):
+    _fields_ = [("c0_im", C.c_double), ("c1_im", C.c_double), ("Mu", C.c_double), ("Sig", C.c_double)]
+
+
+class CircuitAcDesc(C.Structure):
+    _fields_ = [("amps_im", C.c_double), ("dvolts_im", C.c_double)]
+
+
+class HarmonicDesc(C.Structure):
+    _fields_ = [("frequency", C.c_double), ("blocks", C.POINTER(BlockAcDesc)), ("lines", C.POINTER(LineAcDesc)),
+                ("circs", C.POINTER(CircuitAcDesc))]
+
+
+class Harmonic2DProblem:
+    """One device-resident time-harmonic planar problem (FSolver::Harmonic2D).
+    Same keyword arguments as Static2DProblem plus ``frequency`` (Hz) and the
+    AC fields: blocks J_im, Theta_hx, Theta_hy, Lam_d; lines c0_im, c1_im, Mu,
+    Sig (BdryFormat 1); circuits amps_im, dvolts_im."""
+
+    def __init__(self, *, x, y, p, lbl, blocks: Sequence[dict], labels: Sequence[dict], frequency: float,
+                 lines: Sequence[dict] = (), points: Sequence[dict] = (), circuits: Sequence[dict] = (),
+                 marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0, device=0):
+        L = load_library()
+        D, keep = _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision,
+                             length_units, coords, relax)
+        ba = (BlockAcDesc * max(1, len(blocks)))()
+        for k, b in enumerate(blocks):
+            ba[k].J_im, ba[k].Lam_d = b.get("J_im", 0.0), b.get("Lam_d", 0.0)
+            ba[k].Theta_hx, ba[k].Theta_hy = b.get("Theta_hx", 0.0), b.get("Theta_hy", 0.0)
+        la = (LineAcDesc * max(1, len(lines)))()
+        for k, l in enumerate(lines):
+            la[k].c0_im, la[k].c1_im, la[k].Mu, la[k].Sig = (l.get("c0_im", 0.0), l.get("c1_im", 0.0),
+                                                             l.get("Mu", 0.0), l.get("Sig", 0.0))
+        ca = (CircuitAcDesc * max(1, len(circuits)))()
+        for k, q in enumerate(circuits):
+            ca[k].amps_im, ca[k].dvolts_im = q.get("amps_im", 0.0), q.get("dvolts_im", 0.0)
+        H = HarmonicDesc(frequency, ba, la, ca)
+        keep.extend([ba, la, ca])
+        self._keep = keep
+        self.n_nodes = D.n_nodes
+        self.n_circs = len(circuits)
+        self.n_rows = self.n_nodes
+        h = C.c_void_p()
+        _check(L.xfk_problem_create_harmonic(C.byref(D), C.byref(H), device, C.byref(h)))
+        self._h = h
+        self.result: Optional[Result] = None
+
+    def solve(self, rebuild_symbolic: bool = False) -> dict:
+        r = Result()
+        _check(_lib.xfk_harmonic2d(self._h, XFK_REBUILD_SYMBOLIC if rebuild_symbolic else 0, C.byref(r)))
+        self.result = r
+        return r.as_dict()
+
+    def solution(self) -> np.ndarray:
+        A = np.zeros(2 * self.n_nodes)
+        _check(_lib.xfk_get_solution_complex(self._h, A.ctypes.data_as(dptr)))
+        return A[0::2] + 1j * A[1::2]
+
+    def circuits(self):
+        n = self.n_circs
+        cc = np.zeros(max(1, n), np.int32)
+        J = np.zeros(2 * max(1, n))
+        dV = np.zeros(2 * max(1, n))
+        _check(_lib.xfk_get_circuits_complex(self._h, cc.ctypes.data_as(iptr), J.ctypes.data_as(dptr),
+                                             dV.ctypes.data_as(dptr)))
+        return cc[:n], (J[0::2] + 1j * J[1::2])[:n], (dV[0::2] + 1j * dV[1::2])[:n]
+
+    def csr(self):
+        nnz = _lib.xfk_get_nnz(self._h)
+        rp = np.zeros(self.n_nodes + 1, np.int32)
+        col = np.zeros(nnz, np.int32)
+        val = np.zeros(2 * nnz)
+        b = np.zeros(2 * self.n_nodes)
+        _check(_lib.xfk_get_csr_complex(self._h, rp.ctypes.data_as(iptr), col.ctypes.data_as(iptr),
+                                        val.ctypes.data_as(dptr), b.ctypes.data_as(dptr)))
+        return rp, col, val[0::2] + 1j * val[1::2], b[0::2] + 1j * b[1::2]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().xfk_problem_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def pcg_solve_csr(rowptr, col, val, b, V0=None, flag=0, precision=1e-8, device=0, precond="jacobi"):
