@@ -106,3 +106,42 @@ def test_harmonic_repeatable():
     A2 = P.solution()
     P.close()
     assert np.array_equal(A1, A2)
+
+
+def _read_harmonic_ans(path):
+    """Nodes (x, y, A re, A im, marker) and elements (p, lbl, e) of a
+    WriteHarmonic2D .ans (harmonic2d.cpp:793-960)."""
+    lines = open(path).read().splitlines()
+    k = lines.index("[Solution]") + 1
+    n = int(lines[k])
+    nodes = np.array([[float(v) for v in ln.split()] for ln in lines[k + 1:k + 1 + n]])
+    k += 1 + n
+    ne = int(lines[k])
+    els = np.array([[int(v) for v in ln.split()] for ln in lines[k + 1:k + 1 + ne]])
+    return nodes, els
+
+
+def test_harmonic_file_interface_end_to_end(tmp_path):
+    """.fem (Frequency > 0) + fmesher files -> FSolver on the GPU -> harmonic .ans."""
+    import os
+    from oracle import femfile
+    from xfemm_amd import fsolver
+    kw = synth.harmonic(18, circuits=False)
+    kw["marker"] = None
+    kw["points"] = []
+    base = str(tmp_path / "h")
+    synth.write_problem(base, kw)
+    pr, mesh = femfile.load_problem(base)
+    assert pr.Frequency == kw["frequency"]
+    Ao, _, _ = oh.solve(pr, mesh)
+    fs = fsolver.FSolver()
+    fs.PathName = base
+    assert fs.LoadProblemFile()
+    assert fs.runSolver(False), fs.last_error()
+    nodes, els = _read_harmonic_ans(base + ".ans")
+    A = nodes[:, 2] + 1j * nodes[:, 3]
+    M, b = oh.system(pr, mesh)
+    exact = sla.spsolve(M.tocsc(), b) * C_ANS
+    assert rel_err(A, Ao) <= max(TOL_A, 2.0 * rel_err(Ao, exact))
+    assert np.array_equal(els[:, :3], mesh.p) and np.array_equal(els[:, 3], mesh.lbl)
+    assert open(base + ".ans").read().startswith(open(base + ".fem").read())

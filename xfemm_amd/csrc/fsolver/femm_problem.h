@@ -65,9 +65,10 @@ struct CMCircuit {
     double Amps_re = 0, Amps_im = 0;
     double dVolts_re = 0, dVolts_im = 0;
     int OrigCirc = 0;
-    // outputs of Static2D
+    // outputs of Static2D / Harmonic2D (imaginary parts: Harmonic2D only)
     int Case = 0;
     double J = 0, dV = 0;
+    double J_im = 0, dV_im = 0;
 };
 
 struct CMBlockLabel {

@@ -346,7 +346,19 @@ void FSolver::GetFillFactor(int lbl)
     bl.bIsWound = (std::abs(bl.Turns) > 1) || (lt > 2);
 }
 
-int FSolver::Static2D()
+// the C-ABI descriptor of the current problem and the arrays it points into
+struct FSolver::DescStore {
+    std::vector<xfk_block_desc> blk;
+    std::vector<xfk_label_desc> lab;
+    std::vector<xfk_line_desc> lin;
+    std::vector<xfk_point_desc> pts;
+    std::vector<xfk_circuit_desc> cir;
+    std::vector<double> x, y;
+    std::vector<int> marker, p, e, lbl, pbc;
+    xfk_problem_desc d{};
+};
+
+bool FSolver::make_desc(DescStore &ds)
 {
     for (int i = 0; i < (int)labellist.size(); i++) GetFillFactor(i);
     for (auto &lb : labellist)
@@ -354,46 +366,51 @@ int FSolver::Static2D()
             warn("Lua magnetisation-direction functions are not supported by this solver build\n");
             return false;
         }
-    // property tables -> C-ABI descriptors
-    std::vector<xfk_block_desc> blk(blockproplist.size());
+    ds.blk.resize(blockproplist.size());
     for (size_t k = 0; k < blockproplist.size(); k++) {
         const CMSolverMaterialProp &m = blockproplist[k];
-        xfk_block_desc &d = blk[k];
+        xfk_block_desc &d = ds.blk[k];
         d.mu_x = m.mu_x; d.mu_y = m.mu_y; d.H_c = m.H_c; d.J_re = m.J_re; d.Cduct = m.Cduct;
         d.LamFill = m.LamFill; d.LamType = m.LamType; d.BHpoints = m.BHpoints;
         d.B = m.Bdata.empty() ? nullptr : m.Bdata.data();
         d.H = m.Hdata.empty() ? nullptr : m.Hdata.data();
         d.slope = m.slope.empty() ? nullptr : m.slope.data();
     }
-    if (blk.empty()) {
+    if (ds.blk.empty()) {
         warn("no block properties defined\n");
         return false;
     }
-    std::vector<xfk_label_desc> lab(labellist.size());
+    ds.lab.resize(labellist.size());
     for (size_t k = 0; k < labellist.size(); k++) {
-        lab[k].block = labellist[k].BlockType >= 0 ? labellist[k].BlockType : 0;
-        lab[k].in_circuit = labellist[k].InCircuit;
-        lab[k].mag_dir = labellist[k].MagDir;
-        lab[k].is_wound = labellist[k].bIsWound ? 1 : 0;
+        ds.lab[k].block = labellist[k].BlockType >= 0 ? labellist[k].BlockType : 0;
+        ds.lab[k].in_circuit = labellist[k].InCircuit;
+        ds.lab[k].mag_dir = labellist[k].MagDir;
+        ds.lab[k].is_wound = labellist[k].bIsWound ? 1 : 0;
     }
-    std::vector<xfk_line_desc> lin(lineproplist.size());
+    ds.lin.resize(lineproplist.size());
     for (size_t k = 0; k < lineproplist.size(); k++) {
         const CMBoundaryProp &b = lineproplist[k];
-        lin[k] = xfk_line_desc{b.BdryFormat, b.A0, b.A1, b.A2, b.phi, b.c0_re, b.c1_re};
+        ds.lin[k] = xfk_line_desc{b.BdryFormat, b.A0, b.A1, b.A2, b.phi, b.c0_re, b.c1_re};
     }
-    std::vector<xfk_point_desc> pts(nodeproplist.size());
+    ds.pts.resize(nodeproplist.size());
     for (size_t k = 0; k < nodeproplist.size(); k++)
-        pts[k] = xfk_point_desc{nodeproplist[k].A_re, nodeproplist[k].A_im, nodeproplist[k].J_re, nodeproplist[k].J_im};
-    std::vector<xfk_circuit_desc> cir(circproplist.size());
+        ds.pts[k] = xfk_point_desc{nodeproplist[k].A_re, nodeproplist[k].A_im, nodeproplist[k].J_re,
+                                   nodeproplist[k].J_im};
+    ds.cir.resize(circproplist.size());
     for (size_t k = 0; k < circproplist.size(); k++)
-        cir[k] = xfk_circuit_desc{circproplist[k].CircType, circproplist[k].Amps_re, circproplist[k].dVolts_re};
-    std::vector<double> x(NumNodes), y(NumNodes);
-    std::vector<int> marker(NumNodes), p(3LL * NumEls), e(3LL * NumEls), lbl(NumEls), pbc(3LL * NumPBCs);
+        ds.cir[k] = xfk_circuit_desc{circproplist[k].CircType, circproplist[k].Amps_re, circproplist[k].dVolts_re};
+    ds.x.resize(NumNodes);
+    ds.y.resize(NumNodes);
+    ds.marker.resize(NumNodes);
+    ds.p.resize(3LL * NumEls);
+    ds.e.resize(3LL * NumEls);
+    ds.lbl.resize(NumEls);
+    ds.pbc.resize(3LL * NumPBCs);
     for (int i = 0; i < NumNodes; i++) {
-        x[i] = meshnode[i].x;
-        y[i] = meshnode[i].y;
-        marker[i] = meshnode[i].BoundaryMarker;
-        if (marker[i] >= (int)nodeproplist.size()) marker[i] = -1;
+        ds.x[i] = meshnode[i].x;
+        ds.y[i] = meshnode[i].y;
+        ds.marker[i] = meshnode[i].BoundaryMarker;
+        if (ds.marker[i] >= (int)nodeproplist.size()) ds.marker[i] = -1;
     }
     for (int i = 0; i < NumEls; i++) {
         if (labellist[meshele[i].lbl].BlockType < 0) {
@@ -401,33 +418,39 @@ int FSolver::Static2D()
             return false;
         }
         for (int q = 0; q < 3; q++) {
-            p[3LL * i + q] = meshele[i].p[q];
+            ds.p[3LL * i + q] = meshele[i].p[q];
             int eq = meshele[i].e[q];
-            e[3LL * i + q] = (eq >= 0 && eq < (int)lineproplist.size()) ? eq : -1;
+            ds.e[3LL * i + q] = (eq >= 0 && eq < (int)lineproplist.size()) ? eq : -1;
         }
-        lbl[i] = meshele[i].lbl;
+        ds.lbl[i] = meshele[i].lbl;
     }
     for (int k = 0; k < NumPBCs; k++) {
-        pbc[3 * k] = pbclist[k].x;
-        pbc[3 * k + 1] = pbclist[k].y;
-        pbc[3 * k + 2] = pbclist[k].t;
+        ds.pbc[3 * k] = pbclist[k].x;
+        ds.pbc[3 * k + 1] = pbclist[k].y;
+        ds.pbc[3 * k + 2] = pbclist[k].t;
     }
-    xfk_problem_desc d{};
-    d.n_nodes = NumNodes; d.x = x.data(); d.y = y.data(); d.marker = marker.data();
-    d.n_elems = NumEls; d.p = p.data(); d.e = e.data(); d.lbl = lbl.data();
-    d.n_blocks = (int)blk.size(); d.blocks = blk.data();
-    d.n_labels = (int)lab.size(); d.labels = lab.data();
-    d.n_lines = (int)lin.size(); d.lines = lin.empty() ? nullptr : lin.data();
-    d.n_points = (int)pts.size(); d.points = pts.empty() ? nullptr : pts.data();
-    d.n_circs = (int)cir.size(); d.circs = cir.empty() ? nullptr : cir.data();
-    d.n_pbc = NumPBCs; d.pbc = NumPBCs ? pbc.data() : nullptr;
+    xfk_problem_desc &d = ds.d;
+    d.n_nodes = NumNodes; d.x = ds.x.data(); d.y = ds.y.data(); d.marker = ds.marker.data();
+    d.n_elems = NumEls; d.p = ds.p.data(); d.e = ds.e.data(); d.lbl = ds.lbl.data();
+    d.n_blocks = (int)ds.blk.size(); d.blocks = ds.blk.data();
+    d.n_labels = (int)ds.lab.size(); d.labels = ds.lab.data();
+    d.n_lines = (int)ds.lin.size(); d.lines = ds.lin.empty() ? nullptr : ds.lin.data();
+    d.n_points = (int)ds.pts.size(); d.points = ds.pts.empty() ? nullptr : ds.pts.data();
+    d.n_circs = (int)ds.cir.size(); d.circs = ds.cir.empty() ? nullptr : ds.cir.data();
+    d.n_pbc = NumPBCs; d.pbc = NumPBCs ? ds.pbc.data() : nullptr;
     d.precision = Precision;
     d.length_units = (int)LengthUnits;
     d.coords = (int)Coords;
     d.relax = Relax;
+    return true;
+}
 
+int FSolver::Static2D()
+{
+    DescStore ds;
+    if (!make_desc(ds)) return false;
     xfk_problem *prob = nullptr;
-    int rc = xfk_problem_create(&d, device, &prob);
+    int rc = xfk_problem_create(&ds.d, device, &prob);
     if (rc == XFK_OK) rc = xfk_static2d(prob, 0, &stats);
     if (rc == XFK_OK) {
         A.assign(NumNodes, 0.0);
@@ -441,6 +464,59 @@ int FSolver::Static2D()
             circproplist[k].Case = cc[k];
             circproplist[k].J = J[k];
             circproplist[k].dV = dV[k];
+        }
+    }
+    if (rc != XFK_OK) warn(std::string("GPU solver error: ") + xfk_last_error() + "\n");
+    if (prob) xfk_problem_destroy(prob);
+    return rc == XFK_OK;
+}
+
+int FSolver::Harmonic2D()
+{
+    DescStore ds;
+    if (!make_desc(ds)) return false;
+    std::vector<xfk_block_ac_desc> bac(blockproplist.size());
+    for (size_t k = 0; k < blockproplist.size(); k++) {
+        const CMSolverMaterialProp &m = blockproplist[k];
+        bac[k] = xfk_block_ac_desc{m.J_im, m.Theta_hx, m.Theta_hy, m.Lam_d};
+    }
+    std::vector<xfk_line_ac_desc> lac(lineproplist.size());
+    for (size_t k = 0; k < lineproplist.size(); k++) {
+        const CMBoundaryProp &b = lineproplist[k];
+        lac[k] = xfk_line_ac_desc{b.c0_im, b.c1_im, b.Mu, b.Sig};
+    }
+    std::vector<xfk_circuit_ac_desc> cac(circproplist.size());
+    for (size_t k = 0; k < circproplist.size(); k++)
+        cac[k] = xfk_circuit_ac_desc{circproplist[k].Amps_im, circproplist[k].dVolts_im};
+    xfk_harmonic_desc ac{Frequency, bac.data(), lac.empty() ? nullptr : lac.data(),
+                         cac.empty() ? nullptr : cac.data()};
+    xfk_problem *prob = nullptr;
+    int rc = xfk_problem_create_harmonic(&ds.d, &ac, device, &prob);
+    if (rc == XFK_OK) rc = xfk_harmonic2d(prob, 0, &stats);
+    std::vector<double> Ac;
+    if (rc == XFK_OK) {
+        Ac.assign(2 * (size_t)NumNodes, 0.0);
+        rc = xfk_get_solution_complex(prob, Ac.data());
+    }
+    if (rc == XFK_OK) {
+        A.resize(NumNodes);
+        A_im.resize(NumNodes);
+        for (int i = 0; i < NumNodes; i++) {
+            A[i] = Ac[2 * i];
+            A_im[i] = Ac[2 * i + 1];
+        }
+    }
+    if (rc == XFK_OK && !circproplist.empty()) {
+        const size_t nc = circproplist.size();
+        std::vector<int> cc(nc);
+        std::vector<double> J(2 * nc), dV(2 * nc);
+        rc = xfk_get_circuits_complex(prob, cc.data(), J.data(), dV.data());
+        for (size_t k = 0; rc == XFK_OK && k < nc; k++) {
+            circproplist[k].Case = cc[k];
+            circproplist[k].J = J[2 * k];
+            circproplist[k].J_im = J[2 * k + 1];
+            circproplist[k].dV = dV[2 * k];
+            circproplist[k].dV_im = dV[2 * k + 1];
         }
     }
     if (rc != XFK_OK) warn(std::string("GPU solver error: ") + xfk_last_error() + "\n");
@@ -491,6 +567,54 @@ int FSolver::WriteStatic2D()
     return true;
 }
 
+int FSolver::WriteHarmonic2D()
+{
+    // harmonic2d.cpp:793-960: echo the .fem, then nodes (x, y, A re, A im,
+    // marker), elements (p, label, edge markers), circuit data per label,
+    // periodic pairs, air-gap elements
+    const double unitconv[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
+    std::string fin = PathName + ".fem", fout = PathName + ".ans";
+    FILE *fz = fopen(fin.c_str(), "rt");
+    if (!fz) {
+        warn("Couldn't open " + fin + "\n");
+        return false;
+    }
+    FILE *fp = fopen(fout.c_str(), "wt");
+    if (!fp) {
+        fclose(fz);
+        warn("Couldn't write to " + fout + "\n");
+        return false;
+    }
+    char c[1024];
+    while (fgets(c, 1024, fz) != nullptr) fputs(c, fp);
+    fclose(fz);
+    fprintf(fp, "[Solution]\n");
+    const double cf = unitconv[LengthUnits];
+    fprintf(fp, "%i\n", NumNodes);
+    for (int i = 0; i < NumNodes; i++)
+        fprintf(fp, "%.17g\t%.17g\t%.17g\t%.17g\t%i\n", meshnode[i].x / cf, meshnode[i].y / cf, A[i], A_im[i],
+                meshnode[i].BoundaryMarker);
+    fprintf(fp, "%i\n", NumEls);
+    for (int i = 0; i < NumEls; i++)
+        fprintf(fp, "%i\t%i\t%i\t%i\t%i\t%i\t%i\n", meshele[i].p[0], meshele[i].p[1], meshele[i].p[2],
+                meshele[i].lbl, meshele[i].e[0], meshele[i].e[1], meshele[i].e[2]);
+    fprintf(fp, "%i\n", (int)labellist.size());
+    for (size_t k = 0; k < labellist.size(); k++) {
+        int i = labellist[k].InCircuit;
+        if (i < 0) fprintf(fp, "1\t0\t0\n");
+        else {
+            const CMCircuit &C = circproplist[i];
+            if (C.Case == 0) fprintf(fp, "0\t%.17g\t%.17g\n", C.dV, C.dV_im);
+            if (C.Case == 1) fprintf(fp, "1\t%.17g\t%.17g\n", C.J, C.J_im);
+        }
+    }
+    fprintf(fp, "%i\n", NumPBCs);
+    for (int k = 0; k < NumPBCs; k++) fprintf(fp, "%i  %i %i\n", pbclist[k].x, pbclist[k].y, pbclist[k].t);
+    fprintf(fp, "%i\n", NumAirGapElems);
+    fclose(fp);
+    return true;
+}
+
 bool FSolver::runSolver(bool verbose)
 {
     LoadMeshErr err = LoadMesh(deleteMeshFiles);
@@ -509,13 +633,22 @@ bool FSolver::runSolver(bool verbose)
         PrintMessage("solving...\n");
         PrintMessage("Problem Statistics:\n%i nodes\n%i elements\nPrecision: %f\n", NumNodes, NumEls, Precision);
     }
-    if (Frequency != 0) {
-        warn("harmonic (Frequency != 0) problems are not supported by this solver build\n");
-        return false;
-    }
     if (ProblemTypeV != PLANAR) {
         warn("axisymmetric problems are not supported by this solver build\n");
         return false;
+    }
+    if (Frequency != 0) {
+        if (!Harmonic2D()) {
+            warn("Couldn't solve the problem\n");
+            return false;
+        }
+        if (verbose) PrintMessage("Harmonic 2-D problem solved\n");
+        if (!WriteHarmonic2D()) {
+            warn("couldn't write results to disk\n");
+            return false;
+        }
+        if (verbose) PrintMessage("results written to disk\n");
+        return true;
     }
     if (!Static2D()) {
         warn("Couldn't solve the problem\n");

@@ -50,17 +50,22 @@ public:
     bool runSolver(bool verbose = false);                // fsolver.cpp:1213-1338
     int Static2D();                                      // static2d.cpp:53-1033 (on the GPU)
     int WriteStatic2D();                                 // static2d.cpp:1038-1195
+    int Harmonic2D();                                    // harmonic2d.cpp:36-790 (on the GPU, linear)
+    int WriteHarmonic2D();                               // harmonic2d.cpp:793-960
     void GetFillFactor(int lbl);                         // fsolver.cpp:1083-1105 (static)
     static std::string getErrorString(LoadMeshErr err);
 
-    // result of the last Static2D: A (= V*c) per node, in meshnode order
-    std::vector<double> A;
+    // result of the last Static2D: A (= V*c) per node, in meshnode order;
+    // Harmonic2D: A holds the real parts and A_im the imaginary parts
+    std::vector<double> A, A_im;
     xfk_result stats{};
     std::string lastError;
 
 private:
     std::vector<std::array<int, 3>> edges_;   // .edge content: n0, n1, marker
     void warn(const std::string &msg);
+    struct DescStore;                         // property tables + mesh arrays behind an xfk_problem_desc
+    bool make_desc(DescStore &ds);
 };
 
 }  // namespace xfemm

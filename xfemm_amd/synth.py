@@ -112,25 +112,30 @@ def magnetostatic(n: int, nonlinear: bool = False, L: float = 10.0, J: float = 2
                 lines=lines, points=[], circuits=[], precision=precision, length_units=2, coords=0, relax=1.0)
 
 
-def fem_text(blocks, lines, precision=1e-8, units="centimeters") -> str:
+def fem_text(blocks, lines, precision=1e-8, units="centimeters", frequency=0.0) -> str:
     """A .fem header carrying the property tables (no geometry: meshes are given)."""
-    out = ["[Format]      =  4.0", "[Frequency]   =  0", "[Precision]   =  %.17g" % precision,
+    out = ["[Format]      =  4.0", "[Frequency]   =  %.17g" % frequency, "[Precision]   =  %.17g" % precision,
            "[MinAngle]    =  30", "[Depth]       =  1", "[LengthUnits] =  %s" % units,
            "[ProblemType] =  planar", "[Coordinates] =  cartesian", "[ACSolver]    =  0",
            '[PrevSoln]    = ""', "[PrevType]    =  0", '[Comment]     =  "synthetic"',
            "[PointProps]   = 0", "[BdryProps]   = %d" % len(lines)]
     for k, ln in enumerate(lines):
         out += ["  <BeginBdry>", '    <BdryName> = "b%d"' % k, "    <BdryType> = %d" % ln.get("format", 0),
-                "    <A_0> = %.17g" % ln.get("A0", 0.0), "    <A_1> = 0", "    <A_2> = 0", "    <Phi> = 0",
-                "    <c0> = %.17g" % ln.get("c0", 0.0), "    <c0i> = 0", "    <c1> = %.17g" % ln.get("c1", 0.0),
-                "    <c1i> = 0", "    <Mu_ssd> = 0", "    <Sigma_ssd> = 0", "  <EndBdry>"]
+                "    <A_0> = %.17g" % ln.get("A0", 0.0), "    <A_1> = %.17g" % ln.get("A1", 0.0),
+                "    <A_2> = %.17g" % ln.get("A2", 0.0), "    <Phi> = %.17g" % ln.get("phi", 0.0),
+                "    <c0> = %.17g" % ln.get("c0", 0.0), "    <c0i> = %.17g" % ln.get("c0_im", 0.0),
+                "    <c1> = %.17g" % ln.get("c1", 0.0), "    <c1i> = %.17g" % ln.get("c1_im", 0.0),
+                "    <Mu_ssd> = %.17g" % ln.get("Mu", 0.0), "    <Sigma_ssd> = %.17g" % ln.get("Sig", 0.0),
+                "  <EndBdry>"]
     out.append("[BlockProps]  = %d" % len(blocks))
     for k, b in enumerate(blocks):
         out += ["  <BeginBlock>", '    <BlockName> = "m%d"' % k, "    <Mu_x> = %.17g" % b.get("mu_x", 1.0),
                 "    <Mu_y> = %.17g" % b.get("mu_y", 1.0), "    <H_c> = %.17g" % b.get("H_c", 0.0),
-                "    <H_cAngle> = 0", "    <J_re> = %.17g" % b.get("J_re", 0.0), "    <J_im> = 0",
-                "    <Sigma> = %.17g" % b.get("Cduct", 0.0), "    <d_lam> = 0", "    <Phi_h> = 0",
-                "    <Phi_hx> = 0", "    <Phi_hy> = 0", "    <LamType> = %d" % b.get("LamType", 0),
+                "    <H_cAngle> = 0", "    <J_re> = %.17g" % b.get("J_re", 0.0),
+                "    <J_im> = %.17g" % b.get("J_im", 0.0), "    <Sigma> = %.17g" % b.get("Cduct", 0.0),
+                "    <d_lam> = %.17g" % b.get("Lam_d", 0.0), "    <Phi_h> = 0",
+                "    <Phi_hx> = %.17g" % b.get("Theta_hx", 0.0), "    <Phi_hy> = %.17g" % b.get("Theta_hy", 0.0),
+                "    <LamType> = %d" % b.get("LamType", 0),
                 "    <LamFill> = %.17g" % b.get("LamFill", 1.0), "    <NStrands> = 0", "    <WireD> = 0"]
         if b.get("bh") == "M19":
             B, H = m19_curve()
@@ -148,7 +153,7 @@ def write_problem(base: str, kw: dict, label_xy: Optional[np.ndarray] = None) ->
     synthetic problem runs through the file-based FSolver path."""
     x, y, p, lbl, e = kw["x"], kw["y"], kw["p"], kw["lbl"], kw["e"]
     conv = 1.0   # centimeters
-    text = fem_text(kw["blocks"], kw["lines"], kw["precision"])
+    text = fem_text(kw["blocks"], kw["lines"], kw["precision"], frequency=kw.get("frequency", 0.0))
     labels = kw["labels"]
     text += "[NumPoints] = 0\n[NumSegments] = 0\n[NumArcSegments] = 0\n[NumHoles] = 0\n"
     text += "[NumBlockLabels] = %d\n" % len(labels)
