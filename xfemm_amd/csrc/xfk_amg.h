@@ -77,11 +77,13 @@ struct Amg {
     AmgStats stats;
 
     // setup scratch (reused across setups)
-    DBuf<double> absd, dfinv;
+    DBuf<double> absd, dfinv, rho_part;
     DBuf<unsigned char> sflag;
     DBuf<unsigned long long> key, t1;
     DBuf<int> cnt, agg1, agg, flag, cursor;
     DBuf<int> ap_row, ap_col;
+    DBuf<int> pad_col;                // single-pass SpGEMM: padded rows
+    DBuf<double> pad_val;
     DBuf<double> ap_val;
     DBuf<int> dev_int;                // small device scalars (undecided flag, overflow flag)
     int *host_int = nullptr;          // pinned mirror

@@ -56,13 +56,55 @@ __device__ __forceinline__ double rho_of(const unsigned long long *p)
     return __longlong_as_double((long long)*p);
 }
 
-// max of non-negative doubles over the wave, one atomic per wave (bit patterns
-// of non-negative doubles order like the values)
-__device__ __forceinline__ void wave_atomic_max(unsigned long long *dst, double v)
+// max of two values over the workgroup (kB threads), result in thread 0
+__device__ __forceinline__ void block_max2(double &a, double &b, double *red)
 {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
-    if ((threadIdx.x & 63) == 0 && v > 0.0) atomicMax(dst, (unsigned long long)__double_as_longlong(v));
+    for (int off = 32; off > 0; off >>= 1) {
+        a = fmax(a, __shfl_xor(a, off, 64));
+        b = fmax(b, __shfl_xor(b, off, 64));
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[2 * wid] = a;
+        red[2 * wid + 1] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int w = 1; w < kB / 64; ++w) {
+            a = fmax(a, red[2 * w]);
+            b = fmax(b, red[2 * w + 1]);
+        }
+}
+
+// per-block maxima (2 arrays of nblk) -> rho[0..1] as ordered bit patterns
+__global__ void __launch_bounds__(1024) k_max_reduce(int nblk, const double *__restrict__ part,
+                                                     unsigned long long *rho)
+{
+    __shared__ double red[2 * 16];
+    double a = 0.0, b = 0.0;
+    for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
+        a = fmax(a, part[i]);
+        b = fmax(b, part[nblk + i]);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a = fmax(a, __shfl_xor(a, off, 64));
+        b = fmax(b, __shfl_xor(b, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[2 * (threadIdx.x >> 6)] = a;
+        red[2 * (threadIdx.x >> 6) + 1] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            a = fmax(a, red[2 * w]);
+            b = fmax(b, red[2 * w + 1]);
+        }
+        rho[0] = (unsigned long long)__double_as_longlong(a);
+        rho[1] = (unsigned long long)__double_as_longlong(b);
+    }
 }
 
 // --------------------------------------------------------------------------
@@ -91,8 +133,9 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
                                                      const int *__restrict__ col, const double *__restrict__ val,
                                                      const double *__restrict__ absd,
                                                      unsigned char *__restrict__ sflag, int *__restrict__ sdeg,
-                                                     double *__restrict__ dfinv, unsigned long long *rho)
+                                                     double *__restrict__ dfinv, double *__restrict__ rho_part)
 {
+    __shared__ double red[2 * (kB / 64)];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     double rA = 0.0, rF = 0.0;
     if (i < n) {
@@ -124,8 +167,11 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
         if (aii != 0.0) rA = (fabs(aii) + sumA) / fabs(aii);
         if (dF != 0.0) rF = (fabs(dF) + sumS) / fabs(dF);
     }
-    wave_atomic_max(&rho[0], rA);
-    wave_atomic_max(&rho[1], rF);
+    block_max2(rA, rF, red);
+    if (threadIdx.x == 0) {
+        rho_part[blockIdx.x] = rA;
+        rho_part[gridDim.x + blockIdx.x] = rF;
+    }
 }
 
 // --------------------------------------------------------------------------
@@ -546,14 +592,12 @@ __global__ void k_spgemm_nprod(int nrows, SgX X, SgY Y, int *__restrict__ nprod)
     nprod[row] = c;
 }
 
-// Sub-wave SpGEMM for rows of at most 64 products (the fine levels: A P,
-// the prolongator): G lanes per row, 64 / G rows per wavefront, the same
-// enumeration / hash / ordered accumulation as k_spgemm within each group.
-// Groups of one wavefront advance independently; their LDS regions are
-// private, and LDS traffic inside a wavefront is ordered, so no workgroup
-// barriers are needed (wave_barrier keeps the compiler from reordering).
-constexpr int kSwCap = 64;
-constexpr int kSwHash = 2 * kSwCap;
+// Sub-wave SpGEMM (the fine levels: A P, the prolongator): G lanes per row,
+// 64 / G rows per wavefront.  Groups of one wavefront advance independently;
+// their LDS regions are private, and LDS traffic inside a wavefront is
+// ordered, so no workgroup barriers are needed (wave_barrier keeps the
+// compiler from reordering).
+constexpr int kSwCap = 64;            // rows of at most this many products
 
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -562,43 +606,41 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <bool FILL, bool PMODE, int G>
-__global__ void __launch_bounds__(64) k_spgemm_sw(int nrows, SgX X, SgY Y, int *__restrict__ cnt_out,
-                                                  const int *__restrict__ crow, int *__restrict__ ccol,
-                                                  double *__restrict__ cval)
+// Single-pass sub-wave SpGEMM for rows of at most CAP products: each group of
+// G lanes enumerates its row's products once into LDS (key, value), builds
+// the distinct-column set in an LDS hash, ranks the columns, and lane l sums
+// the products of ranks l, l+G, ... in enumeration order (deterministic).
+// The row is written padded (row * CAP) with its length; k_spgemm_compact
+// moves it to its CSR place after the length scan.
+template <bool PMODE, int G, int CAP>
+__global__ void __launch_bounds__(64) k_spgemm_sw1(int nrows, SgX X, SgY Y, int *__restrict__ cnt_out,
+                                                   int *__restrict__ pcol, double *__restrict__ pval)
 {
     constexpr int W = 64 / G;
-    constexpr int kShift = 32 - ilog2(kSwHash);
-    __shared__ int hk_all[W][kSwHash];
-    __shared__ int hr_all[FILL ? W : 1][kSwHash];
-    __shared__ int lst_all[FILL ? W : 1][kSwCap];
-    __shared__ int lslot_all[FILL ? W : 1][kSwCap];
-    __shared__ double acc_all[FILL ? W : 1][kSwCap];
+    constexpr int H = 2 * CAP;
+    constexpr int kShift = 32 - ilog2(H);
+    __shared__ int hk_all[W][H];
+    __shared__ int hr_all[W][H];
+    __shared__ int lst_all[W][CAP], lslot_all[W][CAP];
+    __shared__ int pk_all[W][CAP];
+    __shared__ double pv_all[W][CAP];
     __shared__ int c_off_all[W][G], c_ys_all[W][G];
     __shared__ double c_xv_all[W][G];
-    __shared__ int s_rank_all[W][G];
-    __shared__ double s_val_all[W][G];
-    __shared__ int s_cnt_all[W], s_m_all[W];
+    __shared__ int s_cnt_all[W], s_np_all[W];
 
     const int g = threadIdx.x / G, l = threadIdx.x % G;
     const int row = blockIdx.x * W + g;
-    const bool active = row < nrows;
-    int *hk = hk_all[g];
-    int *hr = hr_all[FILL ? g : 0];
-    int *lst = lst_all[FILL ? g : 0];
-    int *lslot = lslot_all[FILL ? g : 0];
-    double *acc = acc_all[FILL ? g : 0];
+    int *hk = hk_all[g], *hr = hr_all[g], *lst = lst_all[g], *lslot = lslot_all[g], *pk = pk_all[g];
+    double *pv = pv_all[g];
     int *c_off = c_off_all[g], *c_ys = c_ys_all[g];
     double *c_xv = c_xv_all[g];
-    int *s_rank = s_rank_all[g];
-    double *s_val = s_val_all[g];
-    for (int t = l; t < kSwHash; t += G) hk[t] = -1;
+    for (int t = l; t < H; t += G) hk[t] = -1;
     if (l == 0) {
         s_cnt_all[g] = 0;
-        s_m_all[g] = 0;
+        s_np_all[g] = 0;
     }
     wave_lds_sync();
-    if (!active) return;
+    if (row >= nrows) return;
     const int xs = X.rowptr[row], xe = X.rowptr[row + 1];
     double omega = 0.0, dfi = 0.0;
     if (PMODE) {
@@ -606,25 +648,9 @@ __global__ void __launch_bounds__(64) k_spgemm_sw(int nrows, SgX X, SgY Y, int *
         omega = rF > 0.0 ? (4.0 / 3.0) / rF : 0.0;
         dfi = X.dfinv[row];
     }
-    auto insert = [&](int key) {
-        unsigned h = ((unsigned)key * 2654435761u) >> kShift;
-        for (;;) {   // at most 64 keys in 128 slots: a free slot always exists
-            const int old = atomicCAS(&hk[h], -1, key);
-            if (old == -1) {
-                atomicAdd(&s_cnt_all[g], 1);
-                return;
-            }
-            if (old == key) return;
-            h = (h + 1) & (kSwHash - 1);
-        }
-    };
-    auto lookup = [&](int key) -> int {
-        unsigned h = ((unsigned)key * 2654435761u) >> kShift;
-        while (hk[h] != key) h = (h + 1) & (kSwHash - 1);
-        return (int)h;
-    };
-    // stage G X entries of [e0, xe) (group-wide prefix sum of their Y-row lengths)
-    auto stage = [&](int e0) -> int {
+    // enumerate products into LDS, in the fixed order
+    int np = 0;
+    for (int e0 = xs; e0 < xe; e0 += G) {
         const int e = e0 + l;
         int len = 0, ys = 0;
         double xv = 0.0;
@@ -656,85 +682,83 @@ __global__ void __launch_bounds__(64) k_spgemm_sw(int nrows, SgX X, SgY Y, int *
         c_ys[l] = ys;
         c_xv[l] = xv;
         wave_lds_sync();
-        return total;
-    };
-    auto product = [&](int p, int &key, double &v) {
-        int lo = 0, hi = G - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (c_off[mid] <= p) lo = mid;
-            else hi = mid - 1;
-        }
-        if (PMODE) {
-            key = Y.agg[c_ys[lo]];
-            v = c_xv[lo];
-        } else {
-            const int q = c_ys[lo] + (p - c_off[lo]);
-            key = Y.col[q];
-            if (FILL) v = c_xv[lo] * Y.val[q];
-        }
-    };
-    for (int e0 = xs; e0 < xe; e0 += G) {
-        const int total = stage(e0);
         for (int p = l; p < total; p += G) {
+            int lo = 0, hi = G - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (c_off[mid] <= p) lo = mid;
+                else hi = mid - 1;
+            }
             int key;
             double v;
-            product(p, key, v);
-            insert(key);
+            if (PMODE) {
+                key = Y.agg[c_ys[lo]];
+                v = c_xv[lo];
+            } else {
+                const int q = c_ys[lo] + (p - c_off[lo]);
+                key = Y.col[q];
+                v = c_xv[lo] * Y.val[q];
+            }
+            pk[np + p] = key;
+            pv[np + p] = v;
+            unsigned h = ((unsigned)key * 2654435761u) >> kShift;
+            for (;;) {   // <= CAP keys in 2 CAP slots: a free slot always exists
+                const int old = atomicCAS(&hk[h], -1, key);
+                if (old == -1) {
+                    atomicAdd(&s_cnt_all[g], 1);
+                    break;
+                }
+                if (old == key) break;
+                h = (h + 1) & (H - 1);
+            }
         }
+        np += total;
         wave_lds_sync();
     }
-    if (!FILL) {
-        if (l == 0) cnt_out[row] = s_cnt_all[g];
-        return;
-    }
-    for (int t = l; t < kSwHash; t += G)
+    // rank the distinct columns
+    for (int t = l; t < H; t += G)
         if (hk[t] != -1) {
-            const int m = atomicAdd(&s_m_all[g], 1);
+            const int m = atomicAdd(&s_np_all[g], 1);
             lst[m] = hk[t];
             lslot[m] = t;
         }
     wave_lds_sync();
-    const int cnt = s_m_all[g];
-    const int cb = crow[row];
+    const int cnt = s_np_all[g];
     for (int m = l; m < cnt; m += G) {
         const int key = lst[m];
         int rank = 0;
         for (int q = 0; q < cnt; ++q) rank += lst[q] < key;
         hr[lslot[m]] = rank;
-        ccol[cb + rank] = key;
-        acc[rank] = 0.0;
+        pcol[(size_t)row * CAP + rank] = key;
     }
     wave_lds_sync();
-    for (int e0 = xs; e0 < xe; e0 += G) {
-        const int total = stage(e0);
-        for (int p0 = 0; p0 < total; p0 += G) {
-            const int p = p0 + l;
-            int rank = -1;
-            double v = 0.0;
-            if (p < total) {
-                int key;
-                product(p, key, v);
-                rank = hr[lookup(key)];
-            }
-            s_rank[l] = rank;
-            s_val[l] = v;
-            wave_lds_sync();
-            if (rank >= 0) {
-                bool leader = true;
-                double sum = 0.0;
-#pragma unroll
-                for (int m = 0; m < G; ++m)
-                    if (s_rank[m] == rank) {
-                        leader &= !(m < l);
-                        sum += s_val[m];
-                    }
-                if (leader) acc[rank] += sum;
-            }
-            wave_lds_sync();
-        }
+    // product ranks, then ordered sums per owned rank
+    for (int p = l; p < np; p += G) {
+        unsigned h = ((unsigned)pk[p] * 2654435761u) >> kShift;
+        while (hk[h] != pk[p]) h = (h + 1) & (H - 1);
+        pk[p] = hr[h];
     }
-    for (int m = l; m < cnt; m += G) cval[cb + m] = acc[m];
+    wave_lds_sync();
+    for (int m = l; m < cnt; m += G) {
+        double sum = 0.0;
+        for (int p = 0; p < np; ++p)
+            if (pk[p] == m) sum += pv[p];
+        pval[(size_t)row * CAP + m] = sum;
+    }
+    if (l == 0) cnt_out[row] = cnt;
+}
+
+// padded rows (row * cap) -> CSR
+__global__ void k_spgemm_compact(int nrows, int cap, const int *__restrict__ crow, const int *__restrict__ pcol,
+                                 const double *__restrict__ pval, int *__restrict__ ccol, double *__restrict__ cval)
+{
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= nrows) return;
+    const int b = crow[row], n = crow[row + 1] - b;
+    for (int m = 0; m < n; ++m) {
+        ccol[b + m] = pcol[(size_t)row * cap + m];
+        cval[b + m] = pval[(size_t)row * cap + m];
+    }
 }
 
 // --------------------------------------------------------------------------
@@ -971,17 +995,33 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
         int rc = read_flag(M, s, 3, maxprod);
         if (rc != XFK_OK) return rc;
     }
-    const bool sub = maxprod <= kSwCap;
-    const int gsw = (nrows + 64 / G - 1) / (64 / G);
-    AMG_CHECK(hipMemsetAsync(M.dev_int.p + 2, 0, 2 * sizeof(int), s));
-    if (nrows > 0) {
-        if (sub)
-            k_spgemm_sw<false, PMODE, G><<<gsw, 64, 0, s>>>(nrows, X, Y, M.cnt.p, nullptr, nullptr, nullptr);
-        else
-            k_spgemm<false, PMODE, kSgMax><<<nrows, 64, 0, s>>>(nrows, X, Y, M.cnt.p, nullptr, nullptr, nullptr,
-                                                                M.dev_int.p + 2);
+    if (maxprod <= kSwCap) {
+        // single pass into padded rows, then scan + compaction
+        const int cap = maxprod <= 16 ? 16 : (maxprod <= 32 ? 32 : 64);
+        const int gsw = (nrows + 64 / G - 1) / (64 / G);
+        AMG_CHECK(M.pad_col.alloc((size_t)nrows * cap));
+        AMG_CHECK(M.pad_val.alloc((size_t)nrows * cap));
+        if (nrows > 0) {
+            if (cap == 16)
+                k_spgemm_sw1<PMODE, G, 16><<<gsw, 64, 0, s>>>(nrows, X, Y, M.cnt.p, M.pad_col.p, M.pad_val.p);
+            else if (cap == 32)
+                k_spgemm_sw1<PMODE, G, 32><<<gsw, 64, 0, s>>>(nrows, X, Y, M.cnt.p, M.pad_col.p, M.pad_val.p);
+            else
+                k_spgemm_sw1<PMODE, G, 64><<<gsw, 64, 0, s>>>(nrows, X, Y, M.cnt.p, M.pad_col.p, M.pad_val.p);
+        }
+        int rc = scan_total(M, s, M.cnt.p, crow.p, nrows, cnnz);
+        if (rc != XFK_OK) return rc;
+        AMG_CHECK(ccol.alloc((size_t)std::max(1LL, cnnz)));
+        AMG_CHECK(cval.alloc((size_t)std::max(1LL, cnnz)));
+        if (nrows > 0)
+            k_spgemm_compact<<<nb(nrows), kB, 0, s>>>(nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p);
+        return XFK_OK;
     }
-    if (nrows > 0 && !sub) {   // longest row -> LDS capacity of the FILL pass
+    AMG_CHECK(hipMemsetAsync(M.dev_int.p + 2, 0, 2 * sizeof(int), s));
+    if (nrows > 0)
+        k_spgemm<false, PMODE, kSgMax><<<nrows, 64, 0, s>>>(nrows, X, Y, M.cnt.p, nullptr, nullptr, nullptr,
+                                                            M.dev_int.p + 2);
+    if (nrows > 0) {   // longest row -> LDS capacity of the FILL pass
         size_t bytes = 0;
         AMG_CHECK(hipcub::DeviceReduce::Max(nullptr, bytes, M.cnt.p, M.dev_int.p + 3, nrows, s));
         AMG_CHECK(M.cub_tmp.alloc(bytes ? bytes : 1));
@@ -990,7 +1030,7 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     AMG_CHECK(hipMemcpyAsync(M.host_int + 2, M.dev_int.p + 2, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     int rc = scan_total(M, s, M.cnt.p, crow.p, nrows, cnnz);   // synchronises
     if (rc != XFK_OK) return rc;
-    const int ovf = sub ? 0 : M.host_int[2], maxrow = sub ? maxprod : M.host_int[3];
+    const int ovf = M.host_int[2], maxrow = M.host_int[3];
     if (ovf) {
         set_error("AMG: a SpGEMM row exceeds the LDS hash capacity");
         return XFK_ERR_UNSUPPORTED;
@@ -999,9 +1039,7 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     AMG_CHECK(cval.alloc((size_t)std::max(1LL, cnnz)));
     if (nrows > 0) {
         int *of = M.dev_int.p + 2;
-        if (sub)
-            k_spgemm_sw<true, PMODE, G><<<gsw, 64, 0, s>>>(nrows, X, Y, nullptr, crow.p, ccol.p, cval.p);
-        else if (maxrow <= 32)
+        if (maxrow <= 32)
             k_spgemm<true, PMODE, 32><<<nrows, 64, 0, s>>>(nrows, X, Y, nullptr, crow.p, ccol.p, cval.p, of);
         else if (maxrow <= 128)
             k_spgemm<true, PMODE, 128><<<nrows, 64, 0, s>>>(nrows, X, Y, nullptr, crow.p, ccol.p, cval.p, of);
@@ -1067,8 +1105,10 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
             break;
         }
         AMG_CHECK(sflag.alloc((size_t)A.nnz));
+        AMG_CHECK(rho_part.alloc(2 * (size_t)nb(n)));
         k_amg_strength<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
-                                            dfinv.p, rho.p + 2 * l);
+                                            dfinv.p, rho_part.p);
+        k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, rho.p + 2 * l);
         if (l == kAmgMaxLevels - 1) break;   // smoother-only coarsest level
         // MIS-2
         AMG_CHECK(key.alloc(n));
