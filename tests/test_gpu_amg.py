@@ -38,7 +38,7 @@ def _solve_vs(kw, Ao, tol, **opt):
     return A, r, t
 
 
-@pytest.mark.parametrize("cells,nonlinear", [(60, False), (40, True)])
+@pytest.mark.parametrize("cells,nonlinear", [(60, False), (50, True)])
 def test_amg_matches_oracle(cells, nonlinear):
     pr, mesh, kw = synth_to_oracle(synth.magnetostatic(cells, nonlinear=nonlinear))
     Ao, st, _ = oracle.solve(pr, mesh)
@@ -144,6 +144,19 @@ def test_standalone_amg_pcg(n):
         assert it <= 2
 
 
+@pytest.mark.parametrize("n", [30, 45])
+def test_dense_coarsest_blocked_inverse(n):
+    """n*n <= 2048 rows: the whole matrix is the dense coarsest level, inverted
+    by blocked Gauss-Jordan (several 64-wide block columns, ragged last block):
+    PCG converges in one step to the direct solution."""
+    M = _laplace_random(n, 7)
+    b = np.random.default_rng(2).standard_normal(M.shape[0])
+    V, it, er = kernels.pcg_solve_csr(M.indptr, M.indices, M.data, b, precision=1e-12, precond="amg")
+    Vd = sla.spsolve(M.tocsc(), b)
+    assert it <= 2
+    assert rel_err(V, Vd) <= 1e-10
+
+
 def test_amg_without_couplings_uses_smoother_only():
     N = 1000
     rp = np.arange(N + 1, dtype=np.int32)
@@ -161,4 +174,21 @@ def test_precond_option_validation():
         P.set_option(kernels.XFK_OPT_PRECOND, 7)
     with pytest.raises(kernels.XfkError):
         P.set_option(kernels.XFK_OPT_AMG_SWEEPS, 0)
+    for bad in (0.0, 2.0):   # the cycle is SPD only for 0 < omega < 2
+        with pytest.raises(kernels.XfkError):
+            P.set_option(kernels.XFK_OPT_AMG_OMEGA, bad)
     P.close()
+
+
+@pytest.mark.parametrize("omega", [1.0, 1.9])
+def test_jacobi_weight_factor(omega):
+    """Any weight factor in (0, 2) gives an SPD cycle: same answer, within the
+    solver tolerance of the oracle."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(40))
+    Ao, _, _ = oracle.solve(pr, mesh)
+    P = kernels.Static2DProblem(**kw, amg_omega=omega)
+    P.solve()
+    A = P.solution()
+    tol = solver_tolerance(TOL_LINEAR, Ao, P)
+    P.close()
+    assert rel_err(A, Ao) <= tol

@@ -149,7 +149,12 @@ def test_solve_is_deterministic():
 
 def test_large_mesh_residual_property():
     """At bench-like sizes the oracle is too slow: check the size-independent
-    property that the returned A solves the assembled system."""
+    properties that the returned A solves the assembled system -- against a
+    sparse direct solve of that system (1e-6 of max|A|, the linear parity
+    tolerance) and by its residual.  The PCG stops on the residual weighted by
+    its own preconditioner (the reference's test, spars.cpp:313), so the
+    Jacobi-weighted residual checked here is bounded loosely (10 x Precision)."""
+    import scipy.sparse.linalg as spla
     kw = synth.magnetostatic(400)
     P = kernels.Static2DProblem(**kw)
     r = P.solve()
@@ -159,7 +164,9 @@ def test_large_mesh_residual_property():
     d = G.diagonal()
     res = b - G @ V
     er = np.sqrt(np.dot(res / d, res) / np.dot(b / d, b))
-    assert er <= 2 * kw["precision"], (er, r)
+    assert er <= 10 * kw["precision"], (er, r)
+    Vx = spla.spsolve(G.tocsc(), b)
+    assert np.abs(V - Vx).max() <= 1e-6 * np.abs(Vx).max(), (np.abs(V - Vx).max() / np.abs(Vx).max(), r)
     assert np.allclose(G.data, (G.T).tocsr().data) or abs(G - G.T).max() == 0.0
 
 

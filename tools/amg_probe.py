@@ -13,11 +13,19 @@ from xfemm_amd import kernels, synth  # noqa: E402
 cells = [int(a) for a in sys.argv[1:] if not a.startswith("-")] or [100, 1000]
 nonlin = "--nonlinear" in sys.argv
 sweeps = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--sweeps=")] or [2]
+omegas = [float(a.split("=")[1]) for a in sys.argv if a.startswith("--omega=")] or [None]
+nojac = "--no-jacobi" in sys.argv
 for n in cells:
     kw = synth.magnetostatic(n, nonlinear=nonlin)
     sols = {}
-    for pc in ["jacobi"] + ["amg%d" % k for k in sweeps]:
-        opt = dict(precond="jacobi") if pc == "jacobi" else dict(precond="amg", amg_sweeps=int(pc[3:]))
+    cases = ([] if nojac else ["jacobi"]) + ["amg%d" % k + ("" if w is None else "w%g" % w)
+                                            for k in sweeps for w in omegas]
+    for pc in cases:
+        if pc == "jacobi":
+            opt = dict(precond="jacobi")
+        else:
+            k, _, w = pc[3:].partition("w")
+            opt = dict(precond="amg", amg_sweeps=int(k), amg_omega=float(w) if w else None)
         P = kernels.Static2DProblem(device=0, **opt, **kw)
         r = P.solve()
         t0 = time.perf_counter()
@@ -31,6 +39,7 @@ for n in cells:
               % (n, pc, dt * 1e3, r["newton_iters"], r["cg_iters"], r["ms_symbolic"], r["ms_assemble"],
                  r["ms_solve"], r["ms_amg_setup"], r["amg_levels"], r["amg_op_complexity"]), flush=True)
         P.close()
+    ref = sols[cases[0]]
     for k in sols:
-        d = np.abs(sols[k] - sols["jacobi"]).max() / np.abs(sols["jacobi"]).max()
+        d = np.abs(sols[k] - ref).max() / np.abs(ref).max()
         print("   %s: max|A - A_jac|/max|A| = %.3e" % (k, d), flush=True)

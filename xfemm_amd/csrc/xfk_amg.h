@@ -18,10 +18,11 @@
 //   A_{l+1}     R (A P), two wave-per-row SpGEMMs with LDS hash tables and an
 //               ordered per-product accumulation (bit-reproducible)
 // until the level has <= kAmgDenseMax rows, whose dense inverse is formed by
-// single-workgroup Gauss-Jordan.
+// blocked Gauss-Jordan (64-wide block columns, tile GEMM updates).
 //
-// V-cycle: nu damped-Jacobi sweeps (omega = 1 / rho_A, Gershgorin) before and
-// after the coarse correction; the first sweep starts from x = 0 implicitly.
+// V-cycle: nu damped-Jacobi sweeps (weight omega / rho_A, rho_A the Gershgorin
+// bound of D^-1 A, default nu = 1, omega = 1.75) before and after the coarse
+// correction; the first sweep starts from x = 0 implicitly.
 // With equal pre/post sweeps and R = P^T the cycle is a symmetric positive
 // definite operator, as CG requires.
 #pragma once
@@ -35,7 +36,7 @@
 
 namespace xfk {
 
-constexpr int kAmgDenseMax = 128;     // coarsest level solved by its dense inverse (LDS Gauss-Jordan)
+constexpr int kAmgDenseMax = 2048;    // coarsest level solved by its dense inverse (blocked Gauss-Jordan)
 constexpr int kAmgMaxLevels = 16;
 
 struct AmgLevel {
@@ -67,12 +68,16 @@ struct AmgStats {
 struct Amg {
     // parameters
     double theta = 0.08;              // strength threshold
-    int sweeps = 2;                   // Jacobi sweeps before and after the coarse correction
+    int sweeps = 1;                   // Jacobi sweeps before and after the coarse correction
+    double omega = 1.75;              // Jacobi weight = omega / rho_A (rho_A: Gershgorin bound of D^-1 A);
+                                      // omega < 2 keeps the cycle SPD since rho_A >= rho(D^-1 A)
 
     std::vector<std::unique_ptr<AmgLevel>> L;
     int nlev = 0;
     bool dense_coarse = false;
-    DBuf<double> cinv;                // dense inverse of the coarsest level (row major)
+    DBuf<double> cinv;                // dense inverse of the coarsest level (row major, padded)
+    int cinv_ld = 0;
+    DBuf<double> bgj_tmp;             // blocked Gauss-Jordan panels
     DBuf<unsigned long long> rho;     // per level {rho_A, rho_F} as ordered bit patterns
     AmgStats stats;
 

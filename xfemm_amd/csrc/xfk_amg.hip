@@ -77,8 +77,10 @@ __device__ __forceinline__ void block_max2(double &a, double &b, double *red)
         }
 }
 
-// per-block maxima (2 arrays of nblk) -> rho[0..1] as ordered bit patterns
-__global__ void __launch_bounds__(1024) k_max_reduce(int nblk, const double *__restrict__ part,
+// per-block maxima (2 arrays of nblk) -> rho[0..1] as ordered bit patterns;
+// rho[0] (read only by the smoothers, weight 1 / rho[0]) is divided by the
+// Jacobi weight factor omega
+__global__ void __launch_bounds__(1024) k_max_reduce(int nblk, const double *__restrict__ part, double omega,
                                                      unsigned long long *rho)
 {
     __shared__ double red[2 * 16];
@@ -102,7 +104,7 @@ __global__ void __launch_bounds__(1024) k_max_reduce(int nblk, const double *__r
             a = fmax(a, red[2 * w]);
             b = fmax(b, red[2 * w + 1]);
         }
-        rho[0] = (unsigned long long)__double_as_longlong(a);
+        rho[0] = (unsigned long long)__double_as_longlong(a / omega);
         rho[1] = (unsigned long long)__double_as_longlong(b);
     }
 }
@@ -765,60 +767,253 @@ __global__ void k_spgemm_compact(int nrows, int cap, const int *__restrict__ cro
 // setup: coarsest level, dense inverse
 // --------------------------------------------------------------------------
 
-__global__ void k_dense_scatter(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
-                                const double *__restrict__ val, double *__restrict__ M)
+// The coarsest level (<= kAmgDenseMax rows) becomes a dense matrix padded to
+// a multiple of kBj with an identity tail (ld = padded size), inverted in
+// place by blocked Gauss-Jordan without pivoting (the level operators are
+// symmetric positive semi-definite).  Step k of kBj-wide block columns:
+//     D  = inv(M_kk)                      k_bgj_diag   (one workgroup, LDS)
+//     T_kj = D M_kj          (j != k)     k_bgj_row
+//     M_kj = T_kj, M_kk = D, C = M_:k      (snapshot of the old column)
+//     M_ij -= C_i T_kj       (i, j != k)  k_bgj_update (tile GEMMs)
+//     M_ik = -C_i D          (i != k)
+// The matrix is first scaled symmetrically to unit diagonal and the inverse
+// unscaled at the end.  A pivot that vanishes relative to the largest scaled
+// diagonal entry marks a null direction: its row and column are zeroed
+// (generalised inverse on the range).
+constexpr int kBj = 64;
+
+// the matrix has been zeroed (hipMemsetAsync); entries of row i, identity tail
+// symmetric diagonal scaling sc_i = 1 / sqrt(a_ii) (1 for a zero diagonal
+// and the identity tail): the scaled matrix has unit diagonal, so every
+// Gauss-Jordan pivot (a Schur-complement diagonal) lies in (0, 1]
+__global__ void k_dense_dscale(int n, int ld, const int *__restrict__ rowptr, const int *__restrict__ col,
+                               const double *__restrict__ val, double *__restrict__ sc)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    for (int j = 0; j < n; ++j) M[(size_t)i * n + j] = 0.0;
+    if (i >= ld) return;
+    double d = 0.0;
+    if (i < n)
+        for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
+            if (col[k] == i) d += val[k];
+    sc[i] = d > 0.0 ? 1.0 / sqrt(d) : 1.0;
+}
+__global__ void k_dense_scatter(int n, int ld, const int *__restrict__ rowptr, const int *__restrict__ col,
+                                const double *__restrict__ val, const double *__restrict__ sc, double *__restrict__ M)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ld) return;
+    if (i >= n) {
+        M[(size_t)i * ld + i] = 1.0;
+        return;
+    }
     for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
-        if (col[k] < n) M[(size_t)i * n + col[k]] += val[k];
+        if (col[k] < n) M[(size_t)i * ld + col[k]] += val[k] * sc[i] * sc[col[k]];
+}
+// inv(A) = S inv(S A S) S
+__global__ void k_dense_unscale(int ld, double *__restrict__ M, const double *__restrict__ sc)
+{
+    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // double2 index
+    const size_t half = (size_t)ld * ld / 2;
+    if (e >= half) return;
+    const int i = (int)(2 * e / ld), j = (int)(2 * e % ld);
+    double2 *p = reinterpret_cast<double2 *>(M) + e;
+    double2 v = *p;
+    v.x *= sc[i] * sc[j];
+    v.y *= sc[i] * sc[j + 1];
+    *p = v;
 }
 
-// In-place Gauss-Jordan inversion in LDS without pivoting (the level
-// operators are symmetric positive semi-definite).  A pivot that vanishes
-// relative to the largest diagonal entry marks a null direction: its row and
-// column are zeroed, so the result is a generalised inverse on the range.
-__global__ void __launch_bounds__(1024) k_gauss_jordan(int n, double *__restrict__ Mg)
+__global__ void __launch_bounds__(1024) k_dense_maxdiag(int n, int ld, const double *__restrict__ M,
+                                                        double *__restrict__ maxd)
 {
-    __shared__ double M[kAmgDenseMax * kAmgDenseMax];
-    __shared__ double rowk[kAmgDenseMax], colk[kAmgDenseMax];
-    __shared__ double s_maxd;
-    const int tid = threadIdx.x;
-    const int nn = n * n;
-    for (int idx = tid; idx < nn; idx += blockDim.x) M[idx] = Mg[idx];
+    __shared__ double red[16];
+    double m = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmax(m, fabs(M[(size_t)i * ld + i]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
-    if (tid == 0) {
-        double m = 0.0;
-        for (int i = 0; i < n; ++i) m = fmax(m, fabs(M[i * n + i]));
-        s_maxd = m;
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = fmax(m, red[w]);
+        *maxd = m;
     }
-    __syncthreads();
-    for (int k = 0; k < n; ++k) {
-        const double piv = M[k * n + k];
-        if (!(fabs(piv) > 1e-13 * s_maxd)) {
-            __syncthreads();
-            for (int j = tid; j < n; j += blockDim.x) {
-                M[k * n + j] = 0.0;
-                M[j * n + k] = 0.0;
-            }
-            __syncthreads();
+}
+
+// D = inv(M_kk) by in-place Gauss-Jordan: 256 threads, thread t keeps the 16
+// entries (rows 16 (t >> 6) + m, column t & 63) in registers for the whole
+// inversion.  Pivot p is one uniform rank-1 update a_ij -= c_i r_j with
+//     c_i = a_ip (i != p),  c_p = a_pp - 1,
+//     r_j = a_pj / a_pp (j != p),  r_p = 1 + 1 / a_pp,
+// which leaves a_pj / a_pp in row p, -a_ip / a_pp in column p and 1 / a_pp at
+// the pivot; it is cancellation-free because the scaled pivots lie in (0, 1].
+// Row p and column p go through LDS, double-buffered: one barrier per pivot.
+__global__ void __launch_bounds__(256) k_bgj_diag(int k, int ld, const double *__restrict__ M,
+                                                  const double *__restrict__ maxd, double *__restrict__ D)
+{
+    __shared__ double rowk[2][kBj];
+    __shared__ __attribute__((aligned(16))) double colk[2][kBj];
+    const int tid = threadIdx.x;
+    const int j = tid & 63, w = tid >> 6;
+    const size_t base = (size_t)k * kBj * ld + (size_t)k * kBj;
+    double a[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) a[m] = M[base + (size_t)(16 * w + m) * ld + j];
+    const double thr = 1e-13 * (*maxd);
+    for (int p = 0; p < kBj; ++p) {
+        const int buf = p & 1, mp = p & 15;
+        if (w == (p >> 4)) {   // this wave holds row p
+            double own = a[0];
+#pragma unroll
+            for (int m = 1; m < 16; ++m)
+                if (m == mp) own = a[m];
+            rowk[buf][j] = own;
+        }
+        if (j == p) {   // this lane holds column p
+            double2 *cw = reinterpret_cast<double2 *>(&colk[buf][16 * w]);
+#pragma unroll
+            for (int m = 0; m < 16; m += 2) cw[m / 2] = make_double2(a[m], a[m + 1]);
+            if (w == (p >> 4)) colk[buf][p] = a[mp] - 1.0;
+        }
+        __syncthreads();
+        const double piv = rowk[buf][p];
+        if (!(fabs(piv) > thr)) {   // null direction: zero row p and column p
+#pragma unroll
+            for (int m = 0; m < 16; ++m)
+                if (16 * w + m == p || j == p) a[m] = 0.0;
             continue;
         }
         const double ip = 1.0 / piv;
-        for (int j = tid; j < n; j += blockDim.x) {
-            rowk[j] = (j == k ? 1.0 : M[k * n + j]) * ip;
-            colk[j] = M[j * n + k];
+        const double r = j == p ? 1.0 + ip : rowk[buf][j] * ip;
+        const double2 *cr = reinterpret_cast<const double2 *>(&colk[buf][16 * w]);
+#pragma unroll
+        for (int m = 0; m < 16; m += 2) {
+            const double2 c = cr[m / 2];
+            a[m] -= c.x * r;
+            a[m + 1] -= c.y * r;
         }
-        __syncthreads();
-        for (int idx = tid; idx < nn; idx += blockDim.x) {
-            const int i = idx / n, j = idx - i * n;
-            if (i == k) M[idx] = rowk[j];
-            else M[idx] = (j == k ? 0.0 : M[idx]) - colk[i] * rowk[j];
-        }
-        __syncthreads();
     }
-    for (int idx = tid; idx < nn; idx += blockDim.x) Mg[idx] = M[idx];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) D[(16 * w + m) * kBj + j] = a[m];
+}
+
+// C = X Y for 64 x 64 blocks staged in LDS on the f64 matrix cores: 4 waves,
+// wave w computes the 32 x 32 quadrant (w >> 1, w & 1) as 2 x 2 tiles of
+// v_mfma_f64_16x16x4_f64 (A[l & 15][k = l >> 4], B[k = l >> 4][l & 15];
+// C/D col = l & 15, row = (l >> 4) + 4 r).  c[ti][tj][r] is element
+// (32 (w >> 1) + 16 ti + (l >> 4) + 4 r, 32 (w & 1) + 16 tj + (l & 15)).
+// LDS row strides (doubles) that make the operand reads conflict-free: a
+// 32-lane half reads 16 rows x 2 k of X (stride 66 -> banks 4 li + 2 lk) and
+// 2 k-rows x 16 columns of Y (stride 80 -> the two rows 32 banks apart).
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr int kXs = 66, kYs = 80;
+
+__device__ __forceinline__ void bgj_mm(const double *__restrict__ Xs, const double *__restrict__ Ys, dbl4 (&c)[2][2])
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = 32 * (w >> 1), c0 = 32 * (w & 1);
+    const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) c[ti][tj] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int s = 0; s < kBj / 4; ++s) {
+        double a[2], b[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            a[t] = Xs[(r0 + 16 * t + li) * kXs + 4 * s + lk];
+            b[t] = Ys[(4 * s + lk) * kYs + c0 + 16 * t + li];
+        }
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj)
+                c[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], c[ti][tj], 0, 0, 0);
+    }
+}
+
+// (row, col) of element r of tile (ti, tj) of this thread
+__device__ __forceinline__ int bgj_row(int ti, int r) { return 32 * ((threadIdx.x >> 6) >> 1) + 16 * ti + ((threadIdx.x & 63) >> 4) + 4 * r; }
+__device__ __forceinline__ int bgj_col(int tj) { return 32 * ((threadIdx.x >> 6) & 1) + 16 * tj + (threadIdx.x & 15); }
+
+template <int S>
+__device__ __forceinline__ void bgj_load(double *__restrict__ dst, const double *__restrict__ src, size_t ld)
+{
+    // 2048 double2 per tile, 8 per thread, all issued before the first use
+    double2 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int e = threadIdx.x + 256 * q, r = e >> 5, c = 2 * (e & 31);
+        v[q] = *reinterpret_cast<const double2 *>(src + (size_t)r * ld + c);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int e = threadIdx.x + 256 * q, r = e >> 5, c = 2 * (e & 31);
+        dst[r * S + c] = v[q].x;
+        dst[r * S + c + 1] = v[q].y;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_bgj_row(int k, int ld, double *__restrict__ M, const double *__restrict__ D,
+                                                 double *__restrict__ Trow, double *__restrict__ Csnap)
+{
+    const int j = blockIdx.x;
+    if (j == k) {
+        for (int idx = threadIdx.x; idx < kBj * kBj; idx += blockDim.x)
+            M[(size_t)(k * kBj + idx / kBj) * ld + k * kBj + idx % kBj] = D[idx];
+        return;
+    }
+    __shared__ double Xs[kBj * kXs], Ys[kBj * kYs];
+    bgj_load<kXs>(Xs, D, kBj);
+    bgj_load<kYs>(Ys, M + (size_t)k * kBj * ld + (size_t)j * kBj, ld);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int e = threadIdx.x + 256 * q, r = e >> 5, c = 2 * (e & 31);
+        *reinterpret_cast<double2 *>(Csnap + (size_t)j * kBj * kBj + r * kBj + c) =
+            *reinterpret_cast<const double2 *>(M + (size_t)(j * kBj + r) * ld + k * kBj + c);
+    }
+    __syncthreads();
+    dbl4 c[2][2];
+    bgj_mm(Xs, Ys, c);
+    double *T = Trow + (size_t)j * kBj * kBj;
+    double *Mk = M + (size_t)k * kBj * ld + (size_t)j * kBj;
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = bgj_row(ti, r), col = bgj_col(tj);
+                T[row * kBj + col] = c[ti][tj][r];
+                Mk[(size_t)row * ld + col] = c[ti][tj][r];
+            }
+}
+
+// M_ij -= C_i T_kj (i, j != k) and M_ik = -C_i D (i != k), C_i the snapshot
+// of the old column block
+__global__ void __launch_bounds__(256) k_bgj_update(int k, int nbk, int ld, double *__restrict__ M,
+                                                    const double *__restrict__ D, const double *__restrict__ Trow,
+                                                    const double *__restrict__ Csnap)
+{
+    const int i = blockIdx.x / nbk, j = blockIdx.x % nbk;
+    if (i == k) return;
+    __shared__ double Xs[kBj * kXs], Ys[kBj * kYs];
+    bgj_load<kXs>(Xs, Csnap + (size_t)i * kBj * kBj, kBj);
+    bgj_load<kYs>(Ys, j == k ? D : Trow + (size_t)j * kBj * kBj, kBj);
+    __syncthreads();
+    dbl4 c[2][2];
+    bgj_mm(Xs, Ys, c);
+    double *Mij = M + (size_t)i * kBj * ld + (size_t)j * kBj;
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double *e = &Mij[(size_t)bgj_row(ti, r) * ld + bgj_col(tj)];
+                if (j == k) *e = -c[ti][tj][r];
+                else *e -= c[ti][tj][r];
+            }
 }
 
 // --------------------------------------------------------------------------
@@ -918,17 +1113,38 @@ __global__ void __launch_bounds__(256) k_csr_mv_g(int n, const int *__restrict__
     if (i < n && (threadIdx.x & (G - 1)) == 0) y[i] = ACC ? y[i] + s : s;
 }
 
-// x = M b, one wavefront per row of the dense coarsest inverse
-__global__ void __launch_bounds__(256) k_dense_mv(int n, const double *__restrict__ M, const double *__restrict__ b,
-                                                  double *__restrict__ x, const int *done)
+// x = M b, one wavefront per row of the dense coarsest inverse (ld is a
+// multiple of 64 and the padding columns are zero): double2 loads, four in
+// flight per lane
+__global__ void __launch_bounds__(256) k_dense_mv(int n, int ld, const double *__restrict__ M,
+                                                  const double *__restrict__ b, double *__restrict__ x, const int *done)
 {
     if (done && *done) return;
     const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (i >= n) return;
-    double s = 0.0;
-    for (int j = lane; j < n; j += 64) s += M[(size_t)i * n + j] * b[j];
-    s = cg_wave_sum(s);
+    const double2 *Mi = reinterpret_cast<const double2 *>(M + (size_t)i * ld);
+    const int n2 = ld >> 1;
+    double s0 = 0.0, s1 = 0.0;
+    int j = lane;
+    for (; j + 192 < n2; j += 256) {
+        double2 m[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m[q] = Mi[j + 64 * q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = 2 * (j + 64 * q);
+            s0 += m[q].x * (c < n ? b[c] : 0.0);
+            s1 += m[q].y * (c + 1 < n ? b[c + 1] : 0.0);
+        }
+    }
+    for (; j < n2; j += 64) {
+        const double2 m = Mi[j];
+        const int c = 2 * j;
+        s0 += m.x * (c < n ? b[c] : 0.0);
+        s1 += m.y * (c + 1 < n ? b[c + 1] : 0.0);
+    }
+    const double s = cg_wave_sum(s0 + s1);
     if (lane == 0) x[i] = s;
 }
 
@@ -1108,7 +1324,7 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
         AMG_CHECK(rho_part.alloc(2 * (size_t)nb(n)));
         k_amg_strength<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
                                             dfinv.p, rho_part.p);
-        k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, rho.p + 2 * l);
+        k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, omega, rho.p + 2 * l);
         if (l == kAmgMaxLevels - 1) break;   // smoother-only coarsest level
         // MIS-2
         AMG_CHECK(key.alloc(n));
@@ -1191,9 +1407,22 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
     }
     if (dense_coarse) {
         AmgLevel &C = *L[nlev - 1];
-        AMG_CHECK(cinv.alloc((size_t)C.n * C.n));
-        k_dense_scatter<<<nb(C.n), kB, 0, s>>>(C.n, C.rowptr, C.col, C.val, cinv.p);
-        k_gauss_jordan<<<1, 1024, 0, s>>>(C.n, cinv.p);
+        const int nbk = (C.n + kBj - 1) / kBj, ld = nbk * kBj;
+        cinv_ld = ld;
+        AMG_CHECK(cinv.alloc((size_t)ld * ld));
+        AMG_CHECK(bgj_tmp.alloc(2 * (size_t)nbk * kBj * kBj + kBj * kBj + 1 + ld));
+        double *Trow = bgj_tmp.p, *Tcol = Trow + (size_t)nbk * kBj * kBj, *D = Tcol + (size_t)nbk * kBj * kBj;
+        double *maxd = D + kBj * kBj, *sc = maxd + 1;
+        AMG_CHECK(hipMemsetAsync(cinv.p, 0, sizeof(double) * (size_t)ld * ld, s));
+        k_dense_dscale<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, sc);
+        k_dense_scatter<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, sc, cinv.p);
+        k_dense_maxdiag<<<1, 1024, 0, s>>>(C.n, ld, cinv.p, maxd);
+        for (int k = 0; k < nbk; ++k) {
+            k_bgj_diag<<<1, 256, 0, s>>>(k, ld, cinv.p, maxd, D);
+            k_bgj_row<<<nbk, 256, 0, s>>>(k, ld, cinv.p, D, Trow, Tcol);
+            if (nbk > 1) k_bgj_update<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, D, Trow, Tcol);
+        }
+        k_dense_unscale<<<(unsigned)(((size_t)ld * ld / 2 + 255) / 256), 256, 0, s>>>(ld, cinv.p, sc);
     }
     AMG_CHECK(hipGetLastError());
     AMG_CHECK(hipStreamSynchronize(s));
@@ -1249,7 +1478,7 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     if (l == M.nlev - 1) {
         double *dst = (l == 0) ? out0 : A.xa.p;
         if (M.dense_coarse) {
-            k_dense_mv<<<(A.n * 64 + 255) / 256, 256, 0, s>>>(A.n, M.cinv.p, b, dst, done);
+            k_dense_mv<<<(A.n * 64 + 255) / 256, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv.p, b, dst, done);
             return dst;
         }
         // smoother-only coarsest level: 2 nu sweeps from zero

@@ -542,6 +542,7 @@ static int amg_setup(xfk_problem *P)
     if (!P->amg) P->amg = new Amg();
     P->amg->theta = P->amg_theta;
     P->amg->sweeps = P->amg_sweeps;
+    P->amg->omega = P->amg_omega;
     hipEvent_t e0, e1;
     XFK_CHECK(hipEventCreate(&e0));
     XFK_CHECK(hipEventCreate(&e1));
@@ -1305,6 +1306,10 @@ int xfk_set_option(xfk_problem *P, int option, double value)
     case XFK_OPT_AMG_THETA:
         XFK_REQUIRE(value >= 0.0 && value < 1.0, XFK_ERR_ARG, "AMG strength threshold must be in [0, 1)");
         P->amg_theta = value;
+        return XFK_OK;
+    case XFK_OPT_AMG_OMEGA:
+        XFK_REQUIRE(value > 0.0 && value < 2.0, XFK_ERR_ARG, "AMG Jacobi weight factor must be in (0, 2)");
+        P->amg_omega = value;
         return XFK_OK;
     default:
         set_error("unknown option");

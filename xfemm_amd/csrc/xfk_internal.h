@@ -275,8 +275,9 @@ struct xfk_problem {
 
     // preconditioner (xfk_set_option): XFK_PRECOND_AMG (default) or XFK_PRECOND_JACOBI
     int precond = XFK_PRECOND_AMG;
-    int amg_sweeps = 2;
+    int amg_sweeps = 1;
     double amg_theta = 0.08;
+    double amg_omega = 1.75;
     xfk::Amg *amg = nullptr;         // hierarchy of the current matrix (xfk_amg.hip)
     int pc_used = XFK_PRECOND_JACOBI;  // preconditioner of the running solve
 
