@@ -85,6 +85,21 @@ def test_sharded_linear_matches_oracle(nranks):
     assert np.array_equal(outs[0][1], outs[-1][1])             # same gathered solution everywhere
 
 
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_sharded_amg_iterations_match_single_device(nranks):
+    """The sharded hierarchy (rank-local aggregation, Galerkin product over the
+    full rows with the peers' P rows, global replicated coarse levels) keeps
+    every inter-rank coupling: the PCG needs about as many iterations as on
+    one device, not the growth of a block preconditioner."""
+    kw = synth.magnetostatic(120)
+    r1, A1, _ = single(kw)
+    outs = run_sharded(kw, nranks)
+    res, A, _, _ = outs[0]
+    assert res["precond"] == kernels.XFK_PRECOND_AMG
+    assert res["cg_iters"] <= 1.25 * r1["cg_iters"] + 2, (res["cg_iters"], r1["cg_iters"])
+    assert rel_err(A, A1) <= TOL_LINEAR
+
+
 def test_sharded_nonlinear_matches_oracle():
     pr, mesh, kw = synth_to_oracle(synth.magnetostatic(32, nonlinear=True))
     Ao, st, _ = oracle.solve(pr, mesh)

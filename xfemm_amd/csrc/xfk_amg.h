@@ -33,6 +33,9 @@
 #include <vector>
 
 #include "xfk_internal.h"
+#include "xfk_partition.h"
+
+struct xfk_comm;
 
 namespace xfk {
 
@@ -42,7 +45,8 @@ constexpr int kAmgMaxLevels = 16;
 struct AmgLevel {
     int n = 0;                        // rows
     long long nnz = 0;
-    int ncol_lim = 0;                 // columns >= ncol_lim are ignored (sharded level 0: halo)
+    int ncol_lim = 0;                 // columns >= ncol_lim are ignored by the coarsening (sharded level 0: halo)
+    int ncol_smooth = 0;              // columns the smoother and residual read (sharded level 0: owned + halo)
     const int *rowptr = nullptr, *col = nullptr;
     const double *val = nullptr;
     DBuf<int> rowptr_o, col_o;        // storage of levels >= 1
@@ -94,14 +98,48 @@ struct Amg {
     int *host_int = nullptr;          // pinned mirror
     DBuf<char> cub_tmp;
 
+    // sharded level 0 (setup_dist): every rank aggregates its own rows, the
+    // coarse levels are global and replicated on every rank
+    bool dist = false;
+    xfk_comm *comm = nullptr;
+    const HaloPlan *halo = nullptr;   // level-0 halo exchange (the problem's node plan)
+    int nranks = 1, rank = 0;
+    std::vector<int> c0;              // global coarse offset of each rank's aggregates (nranks + 1)
+    int ncmax = 0;                    // largest per-rank aggregate count (all-gather stride)
+    DBuf<int> c0_dev;
+    DBuf<double> cb_loc, cb_all;      // restricted residual: own aggregates, all-gathered (padded)
+    DBuf<int> pe_row, pe_col;         // P extended by the halo nodes' rows (global coarse columns)
+    DBuf<double> pe_val, ebuf;
+    DBuf<int> l_row, l_col, s_col;    // this rank's coarse rows (s_: padded send copy)
+    DBuf<double> l_val, s_val;
+    DBuf<int> g_row, g_col;           // all-gathered coarse rows (padded per rank)
+    DBuf<double> g_val;
+    DBuf<int> e0_dev;
+    int *host_big = nullptr;          // pinned scratch for small device -> host reads
+    int host_big_n = 0;
+
     ~Amg();
     // Build the hierarchy for the n x n CSR on `s` (host-synchronising).
     // Columns >= ncol_lim (sharded halo) are ignored.  Returns XFK_OK, or
     // XFK_ERR_UNSUPPORTED when a SpGEMM row exceeds the LDS hash capacity.
     int setup(hipStream_t s, int n, int ncol_lim, const int *rowptr, const int *col, const double *val,
               long long nnz);
-    // u = M^-1 r (owned rows of level 0); kernels return early once *done != 0
-    void vcycle(hipStream_t s, const double *r, double *u, const int *done);
+    // Sharded level 0: n owned rows, nh halo columns (local ids n.., filled by
+    // comm->exchange(halo)).  Aggregation and P use the owned block; the
+    // Galerkin product uses the full rows with the peers' P rows for the halo,
+    // so the coarse operator carries every inter-rank coupling.  Collective.
+    int setup_dist(hipStream_t s, xfk_comm *comm, const HaloPlan &halo, int n, int nh, const int *rowptr,
+                   const int *col, const double *val, long long nnz);
+    // u = M^-1 r (owned rows of level 0); kernels return early once *done != 0.
+    // Sharded: collective (halo exchanges, one all-gather).
+    int vcycle(hipStream_t s, const double *r, double *u, const int *done);
+
+  private:
+    int init(hipStream_t s);
+    int build(hipStream_t s, int l0);
+    int aggregate(hipStream_t s, int l, long long &nc, bool allow_stop);
+    int galerkin_dist(hipStream_t s, int st);
+    int host_ints(int count);
 };
 
 }  // namespace xfk

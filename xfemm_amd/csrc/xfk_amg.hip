@@ -12,10 +12,12 @@
 // afterwards).
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <climits>
 #include <cmath>
 
 #include "xfk_amg.h"
+#include "xfk_comm.h"
 #include "xfk_spmv.h"
 
 namespace xfk {
@@ -151,7 +153,12 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
             if (j == i) {
                 aii = a;
                 f = 2;   // the diagonal: not a neighbour, but kept by the prolongator smoothing
-            } else if (j < ncl) {
+            } else if (j >= ncl) {
+                // halo column: read by the smoother; for the rank-local P it is
+                // lumped like a weak entry, so P keeps reproducing constants
+                sumA += fabs(a);
+                lump += a;
+            } else {
                 sumA += fabs(a);
                 if (a != 0.0 && fabs(a) > theta * sqrt(ai * absd[j])) {
                     f = 1;
@@ -1148,6 +1155,76 @@ __global__ void __launch_bounds__(256) k_dense_mv(int n, int ld, const double *_
     if (lane == 0) x[i] = s;
 }
 
+// --------------------------------------------------------------------------
+// sharded level 0: helpers of the distributed Galerkin product and V-cycle
+// --------------------------------------------------------------------------
+
+// x = w D^-1 b: the first Jacobi sweep from zero, written out (its halo is
+// exchanged before the residual)
+__global__ void k_jacobi_first(int n, const unsigned long long *rho, const double *__restrict__ dinv,
+                               const double *__restrict__ b, double *__restrict__ x, const int *done)
+{
+    if (done && *done) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double ra = rho_of(rho);
+    x[i] = (ra > 0.0 ? 1.0 / ra : 0.0) * dinv[i] * b[i];
+}
+__global__ void k_row_len_d(int n, const int *__restrict__ rowptr, double *__restrict__ len)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) len[i] = (double)(rowptr[i + 1] - rowptr[i]);
+}
+__global__ void k_dbl2int(long long n, const double *__restrict__ a, int *__restrict__ b)
+{
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i < n) b[i] = (int)a[i];
+}
+__global__ void k_int2dbl(long long n, const int *__restrict__ a, double *__restrict__ b)
+{
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i < n) b[i] = (double)a[i];
+}
+__global__ void k_add_int(long long n, int *__restrict__ a, int v)
+{
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i < n) a[i] += v;
+}
+// row pointer of P extended by the halo rows: owned rows, then pnnz + hrow
+__global__ void k_pe_row(int n, int nh, long long pnnz, const int *__restrict__ prow, const int *__restrict__ hrow,
+                         int *__restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) out[i] = prow[i];
+    else if (i <= n + nh) out[i] = (int)pnnz + hrow[i - n];
+}
+// global coarse row pointer from the all-gathered per-rank row pointers
+// (stride ld per rank); c0 / e0: first row / entry of each rank (nranks + 1)
+__global__ void k_concat_rowptr(int NC, int nranks, const int *__restrict__ c0, const int *__restrict__ e0,
+                                const int *__restrict__ grow, int ld, int *__restrict__ out)
+{
+    const int I = blockIdx.x * blockDim.x + threadIdx.x;
+    if (I > NC) return;
+    if (I == NC) {
+        out[I] = e0[nranks];
+        return;
+    }
+    int q = 0;
+    while (c0[q + 1] <= I) ++q;
+    out[I] = e0[q] + grow[(size_t)q * ld + (I - c0[q])];
+}
+// global coarse vector from the padded all-gather (stride ld per rank)
+__global__ void k_unpad(int NC, int nranks, const int *__restrict__ c0, const double *__restrict__ all, int ld,
+                        double *__restrict__ out, const int *done)
+{
+    if (done && *done) return;
+    const int I = blockIdx.x * blockDim.x + threadIdx.x;
+    if (I >= NC) return;
+    int q = 0;
+    while (c0[q + 1] <= I) ++q;
+    out[I] = all[(size_t)q * ld + (I - c0[q])];
+}
+
 }  // namespace
 
 // --------------------------------------------------------------------------
@@ -1157,6 +1234,7 @@ __global__ void __launch_bounds__(256) k_dense_mv(int n, int ld, const double *_
 Amg::~Amg()
 {
     if (host_int) (void)hipHostFree(host_int);
+    if (host_big) (void)hipHostFree(host_big);
 }
 
 #define AMG_CHECK(call)                                                          \
@@ -1285,26 +1363,116 @@ void launch_mv(hipStream_t s, int n, const int *rowptr, const int *col, const do
 
 }  // namespace
 
-int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *col0, const double *val0,
-               long long nnz0)
+int Amg::host_ints(int count)
+{
+    if (host_big_n >= count) return XFK_OK;
+    if (host_big) (void)hipHostFree(host_big);
+    host_big = nullptr;
+    host_big_n = 0;
+    AMG_CHECK(hipHostMalloc((void **)&host_big, sizeof(int) * std::max(count, 1)));
+    host_big_n = count;
+    return XFK_OK;
+}
+
+int Amg::init(hipStream_t s)
 {
     if (!host_int) AMG_CHECK(hipHostMalloc((void **)&host_int, 4 * sizeof(int)));
     AMG_CHECK(dev_int.alloc(4));
     AMG_CHECK(rho.alloc(2 * kAmgMaxLevels));
     AMG_CHECK(hipMemsetAsync(rho.p, 0, sizeof(unsigned long long) * 2 * kAmgMaxLevels, s));
     if (L.empty()) L.emplace_back(new AmgLevel());
-    {
-        AmgLevel &F = *L[0];
-        F.n = n0;
-        F.nnz = nnz0;
-        F.ncol_lim = ncl0;
-        F.rowptr = rowptr0;
-        F.col = col0;
-        F.val = val0;
-    }
     stats = AmgStats();
     dense_coarse = false;
-    int l = 0;
+    return XFK_OK;
+}
+
+int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *col0, const double *val0,
+               long long nnz0)
+{
+    dist = false;
+    comm = nullptr;
+    halo = nullptr;
+    int rc = init(s);
+    if (rc != XFK_OK) return rc;
+    AmgLevel &F = *L[0];
+    F.n = n0;
+    F.nnz = nnz0;
+    F.ncol_lim = ncl0;
+    F.ncol_smooth = ncl0;
+    F.rowptr = rowptr0;
+    F.col = col0;
+    F.val = val0;
+    return build(s, 0);
+}
+
+// MIS-2 aggregation of level l, P = (I - omega D_F^-1 A_F) P_tent and R = P^T
+// (strength flags and rho_F already computed).  nc = 0 when the level does
+// not coarsen usefully (allow_stop) or has no aggregate.
+int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
+{
+    AmgLevel &A = *L[l];
+    const int n = A.n;
+    nc = 0;
+    A.nc = 0;
+    AMG_CHECK(key.alloc(n));
+    AMG_CHECK(t1.alloc(n));
+    k_mis_init<<<nb(n), kB, 0, s>>>(n, cnt.p, key.p);
+    int rounds = 0;
+    for (int batch = 6;; batch = 2) {
+        for (int b = 0; b < batch; ++b, ++rounds) {
+            k_mis_max<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, dev_int.p);
+            k_mis_update<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, dev_int.p);
+        }
+        int und = 0;
+        int rc = read_flag(*this, s, 0, und);
+        if (rc != XFK_OK) return rc;
+        if (!und) break;
+        if (rounds > 4096) {
+            set_error("AMG: MIS-2 aggregation did not terminate");
+            return XFK_ERR_NOCONV;
+        }
+    }
+    stats.mis_rounds[l] = rounds;
+    AMG_CHECK(flag.alloc((size_t)n + 1));
+    AMG_CHECK(cursor.alloc((size_t)n + 1));
+    k_agg_roots<<<nb(n), kB, 0, s>>>(n, key.p, flag.p);
+    int rc = scan_total(*this, s, flag.p, cursor.p, n, nc);   // cursor = root ids
+    if (rc != XFK_OK) return rc;
+    if (allow_stop && (nc == 0 || nc > (long long)(0.9 * n))) {   // no useful coarsening: smoother-only coarsest
+        nc = 0;
+        return XFK_OK;
+    }
+    AMG_CHECK(agg1.alloc(n));
+    AMG_CHECK(agg.alloc(n));
+    k_agg_join1<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, cursor.p, agg1.p);
+    k_agg_join2<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, agg1.p, agg.p);
+    // P = (I - omega D_F^-1 A_F) P_tent
+    SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, rho.p + 2 * l + 1};
+    SgY YT{nullptr, nullptr, nullptr, agg.p};
+    if ((rc = spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz)) != XFK_OK) return rc;
+    A.nc = (int)nc;
+    // R = P^T
+    AMG_CHECK(cnt.alloc((size_t)std::max<long long>(n, nc) + 1));
+    AMG_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * (nc + 1), s));
+    k_rt_count<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, cnt.p);
+    AMG_CHECK(A.rrow.alloc((size_t)nc + 1));
+    long long rnnz = 0;
+    if ((rc = scan_total(*this, s, cnt.p, A.rrow.p, (int)nc, rnnz)) != XFK_OK) return rc;
+    AMG_CHECK(A.rcol.alloc((size_t)std::max(1LL, rnnz)));
+    AMG_CHECK(A.rval.alloc((size_t)std::max(1LL, rnnz)));
+    AMG_CHECK(hipMemsetAsync(cursor.p, 0, sizeof(int) * (nc + 1), s));
+    k_rt_fill<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, A.rrow.p, cursor.p, A.rcol.p);
+    if (nc > 0)
+        k_rt_sort_vals<<<(int)((nc * 64 + 255) / 256), 256, 0, s>>>((int)nc, A.rrow.p, A.rcol.p, A.prow.p, A.pcol.p,
+                                                                   A.pval.p, A.rval.p);
+    return XFK_OK;
+}
+
+// levels l0.. of the hierarchy (L[l0] set up by the caller), then the
+// smoother vectors and the dense coarsest inverse
+int Amg::build(hipStream_t s, int l0)
+{
+    int l = l0;
     for (;; ++l) {
         AmgLevel &A = *L[l];
         const int n = A.n;
@@ -1326,55 +1494,10 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
                                             dfinv.p, rho_part.p);
         k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, omega, rho.p + 2 * l);
         if (l == kAmgMaxLevels - 1) break;   // smoother-only coarsest level
-        // MIS-2
-        AMG_CHECK(key.alloc(n));
-        AMG_CHECK(t1.alloc(n));
-        k_mis_init<<<nb(n), kB, 0, s>>>(n, cnt.p, key.p);
-        int rounds = 0;
-        for (int batch = 6;; batch = 2) {
-            for (int b = 0; b < batch; ++b, ++rounds) {
-                k_mis_max<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, dev_int.p);
-                k_mis_update<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, dev_int.p);
-            }
-            int und = 0;
-            int rc = read_flag(*this, s, 0, und);
-            if (rc != XFK_OK) return rc;
-            if (!und) break;
-            if (rounds > 4096) {
-                set_error("AMG: MIS-2 aggregation did not terminate");
-                return XFK_ERR_NOCONV;
-            }
-        }
-        stats.mis_rounds[l] = rounds;
-        AMG_CHECK(flag.alloc((size_t)n + 1));
-        AMG_CHECK(cursor.alloc((size_t)n + 1));
-        k_agg_roots<<<nb(n), kB, 0, s>>>(n, key.p, flag.p);
         long long nc = 0;
-        int rc = scan_total(*this, s, flag.p, cursor.p, n, nc);   // cursor = root ids
+        int rc = aggregate(s, l, nc, true);
         if (rc != XFK_OK) return rc;
-        if (nc == 0 || nc > (long long)(0.9 * n)) break;   // no useful coarsening: smoother-only coarsest
-        AMG_CHECK(agg1.alloc(n));
-        AMG_CHECK(agg.alloc(n));
-        k_agg_join1<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, cursor.p, agg1.p);
-        k_agg_join2<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, agg1.p, agg.p);
-        // P = (I - omega D_F^-1 A_F) P_tent
-        SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, rho.p + 2 * l + 1};
-        SgY YT{nullptr, nullptr, nullptr, agg.p};
-        if ((rc = spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz)) != XFK_OK) return rc;
-        A.nc = (int)nc;
-        // R = P^T
-        AMG_CHECK(cnt.alloc((size_t)std::max<long long>(n, nc) + 1));
-        AMG_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * (nc + 1), s));
-        k_rt_count<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, cnt.p);
-        AMG_CHECK(A.rrow.alloc((size_t)nc + 1));
-        long long rnnz = 0;
-        if ((rc = scan_total(*this, s, cnt.p, A.rrow.p, (int)nc, rnnz)) != XFK_OK) return rc;
-        AMG_CHECK(A.rcol.alloc((size_t)std::max(1LL, rnnz)));
-        AMG_CHECK(A.rval.alloc((size_t)std::max(1LL, rnnz)));
-        AMG_CHECK(hipMemsetAsync(cursor.p, 0, sizeof(int) * (nc + 1), s));
-        k_rt_fill<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, A.rrow.p, cursor.p, A.rcol.p);
-        k_rt_sort_vals<<<(int)((nc * 64 + 255) / 256), 256, 0, s>>>((int)nc, A.rrow.p, A.rcol.p, A.prow.p, A.pcol.p,
-                                                                   A.pval.p, A.rval.p);
+        if (nc == 0) break;
         // AP = A P, then A_c = R (A P)
         SgX XA{A.rowptr, A.col, A.val, A.ncol_lim, nullptr, nullptr, nullptr};
         SgY YP{A.prow.p, A.pcol.p, A.pval.p, nullptr};
@@ -1389,6 +1512,7 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
         C.n = (int)nc;
         C.nnz = cnnz;
         C.ncol_lim = (int)nc;
+        C.ncol_smooth = (int)nc;
         C.rowptr = C.rowptr_o.p;
         C.col = C.col_o.p;
         C.val = C.val_o.p;
@@ -1397,13 +1521,14 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
     stats.levels = nlev;
     double tot = 0;
     for (int k = 0; k < nlev; ++k) tot += (double)stats.nnz[k];
-    stats.op_complexity = nnz0 > 0 ? tot / (double)nnz0 : 0.0;
+    stats.op_complexity = stats.nnz[0] > 0 ? tot / (double)stats.nnz[0] : 0.0;
     for (int k = 0; k < nlev; ++k) {
         AmgLevel &A = *L[k];
-        AMG_CHECK(A.xa.alloc((size_t)A.n));
-        AMG_CHECK(A.xb.alloc((size_t)A.n));
-        AMG_CHECK(A.r.alloc((size_t)A.n));
-        if (k > 0) AMG_CHECK(A.b.alloc((size_t)A.n));
+        const size_t nv = (size_t)std::max(1, std::max(A.n, A.ncol_smooth));
+        AMG_CHECK(A.xa.alloc(nv));
+        AMG_CHECK(A.xb.alloc(nv));
+        AMG_CHECK(A.r.alloc((size_t)std::max(1, A.n)));
+        if (k > 0) AMG_CHECK(A.b.alloc((size_t)std::max(1, A.n)));
     }
     if (dense_coarse) {
         AmgLevel &C = *L[nlev - 1];
@@ -1429,6 +1554,228 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
     return XFK_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// sharded level 0
+// ---------------------------------------------------------------------------
+
+namespace {
+
+// every rank's k doubles -> host (rank-major); collective
+int gather_host(Amg &M, xfk_comm *comm, hipStream_t s, const double *vals, int k, std::vector<double> &out)
+{
+    DBuf<double> d;
+    AMG_CHECK(d.alloc((size_t)k * (comm->size + 1)));
+    AMG_CHECK(hipMemcpyAsync(d.p, vals, sizeof(double) * k, hipMemcpyHostToDevice, s));
+    int rc = comm->allgather(d.p, d.p + k, (size_t)k, s);
+    if (rc != XFK_OK) return rc;
+    out.assign((size_t)k * comm->size, 0.0);
+    AMG_CHECK(hipMemcpyAsync(out.data(), d.p + k, sizeof(double) * k * comm->size, hipMemcpyDeviceToHost, s));
+    AMG_CHECK(hipStreamSynchronize(s));
+    (void)M;
+    return XFK_OK;
+}
+
+}  // namespace
+
+int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n, int nh, const int *rowptr,
+                    const int *col, const double *val, long long nnz)
+{
+    dist = true;
+    comm = comm_;
+    halo = &halo_;
+    nranks = comm->size;
+    rank = comm->rank;
+    int rc = init(s);
+    if (rc != XFK_OK) return rc;
+    AmgLevel &A = *L[0];
+    A.n = n;
+    A.nnz = nnz;
+    A.ncol_lim = n;            // aggregation and P: the owned block
+    A.ncol_smooth = n + nh;    // smoother and residual: the full rows
+    A.rowptr = rowptr;
+    A.col = col;
+    A.val = val;
+    stats.n[0] = n;
+    stats.nnz[0] = nnz;
+    AMG_CHECK(A.dinv.alloc(n));
+    AMG_CHECK(absd.alloc(n));
+    AMG_CHECK(dfinv.alloc(n));
+    AMG_CHECK(cnt.alloc((size_t)n + 1));
+    AMG_CHECK(sflag.alloc((size_t)std::max(1LL, nnz)));
+    AMG_CHECK(rho_part.alloc(2 * (size_t)nb(n)));
+    k_amg_diag<<<nb(n), kB, 0, s>>>(n, rowptr, col, val, absd.p, A.dinv.p);
+    k_amg_strength<<<nb(n), kB, 0, s>>>(n, n, theta, rowptr, col, val, absd.p, sflag.p, cnt.p, dfinv.p, rho_part.p);
+    k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, omega, rho.p);
+    long long nc = 0;
+    rc = aggregate(s, 0, nc, false);
+    if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
+    if ((rc = galerkin_dist(s, rc == XFK_OK ? 0 : 1)) != XFK_OK) return rc;
+    return build(s, 1);
+}
+
+// A_1 = R (A P_ext) on every rank for its aggregates, all-gathered into the
+// global level 1.  st: this rank's status so far (every rank makes the same
+// collective calls whatever its status).
+int Amg::galerkin_dist(hipStream_t s, int st)
+{
+    AmgLevel &A = *L[0];
+    const int n = A.n, nh = A.ncol_smooth - A.n;
+    const int nc = st ? 0 : A.nc;
+    std::vector<double> all;
+    // 1. aggregate counts and status of every rank
+    {
+        const double mine[2] = {(double)nc, (double)st};
+        int rc = gather_host(*this, comm, s, mine, 2, all);
+        if (rc != XFK_OK) return rc;
+    }
+    c0.assign(nranks + 1, 0);
+    ncmax = 1;
+    bool fail = false;
+    for (int q = 0; q < nranks; ++q) {
+        c0[q + 1] = c0[q] + (int)all[2 * q];
+        ncmax = std::max(ncmax, (int)all[2 * q]);
+        fail |= all[2 * q + 1] != 0.0;
+    }
+    const int NC = c0[nranks];
+    if (fail || NC == 0) {
+        set_error("AMG: a rank could not aggregate its rows");
+        return XFK_ERR_UNSUPPORTED;
+    }
+    AMG_CHECK(c0_dev.alloc(nranks + 1));
+    AMG_CHECK(hipMemcpyAsync(c0_dev.p, c0.data(), sizeof(int) * (nranks + 1), hipMemcpyHostToDevice, s));
+    // 2. P rows of the halo nodes: lengths through the node plan, then the
+    //    entries through a plan over the P arrays (a peer's rows for my halo
+    //    range are one contiguous run of its P entries)
+    const long long pnnz = A.pnnz;
+    const int ncl = n + nh;
+    AMG_CHECK(ebuf.alloc((size_t)ncl));
+    k_row_len_d<<<nb(n), kB, 0, s>>>(n, A.prow.p, ebuf.p);
+    int rc = comm->exchange(*halo, ebuf.p, s);
+    if (rc != XFK_OK) return rc;
+    AMG_CHECK(cnt.alloc((size_t)std::max(n, nh) + 1));
+    AMG_CHECK(flag.alloc((size_t)nh + 1));
+    if (nh > 0) k_dbl2int<<<nb(nh), kB, 0, s>>>(nh, ebuf.p + n, cnt.p);
+    long long nhe = 0;
+    if ((rc = scan_total(*this, s, cnt.p, flag.p, nh, nhe)) != XFK_OK) return rc;   // flag = halo row pointer
+    AMG_CHECK(pe_row.alloc((size_t)ncl + 1));
+    k_pe_row<<<nb(ncl + 1), kB, 0, s>>>(n, nh, pnnz, A.prow.p, flag.p, pe_row.p);
+    const int nsr = (int)(halo->send.size() + halo->recv.size());
+    if ((rc = host_ints(2 * nsr)) != XFK_OK) return rc;
+    {
+        int k = 0;
+        for (const HaloRange &t : halo->send) {
+            AMG_CHECK(hipMemcpyAsync(host_big + k++, A.prow.p + t.off, sizeof(int), hipMemcpyDeviceToHost, s));
+            AMG_CHECK(hipMemcpyAsync(host_big + k++, A.prow.p + t.off + t.len, sizeof(int), hipMemcpyDeviceToHost, s));
+        }
+        for (const HaloRange &r : halo->recv) {
+            AMG_CHECK(hipMemcpyAsync(host_big + k++, flag.p + (r.off - n), sizeof(int), hipMemcpyDeviceToHost, s));
+            AMG_CHECK(hipMemcpyAsync(host_big + k++, flag.p + (r.off - n) + r.len, sizeof(int),
+                                     hipMemcpyDeviceToHost, s));
+        }
+        AMG_CHECK(hipStreamSynchronize(s));
+    }
+    HaloPlan ep;
+    {
+        int k = 0;
+        for (const HaloRange &t : halo->send) {
+            const int b0 = host_big[k++], b1 = host_big[k++];
+            ep.send.push_back(HaloRange{t.peer, b0, b1 - b0, t.g0});
+        }
+        for (const HaloRange &r : halo->recv) {
+            const int b0 = host_big[k++], b1 = host_big[k++];
+            ep.recv.push_back(HaloRange{r.peer, (int)pnnz + b0, b1 - b0, r.g0});
+        }
+    }
+    const size_t ne = (size_t)std::max(1LL, pnnz + nhe);
+    // values
+    AMG_CHECK(pe_val.alloc(ne));
+    if (pnnz > 0)
+        AMG_CHECK(hipMemcpyAsync(pe_val.p, A.pval.p, sizeof(double) * pnnz, hipMemcpyDeviceToDevice, s));
+    if ((rc = comm->exchange(ep, pe_val.p, s)) != XFK_OK) return rc;
+    // columns: P goes to global coarse numbering (R = P^T is built already)
+    if (pnnz > 0) k_add_int<<<nb(pnnz), kB, 0, s>>>(pnnz, A.pcol.p, c0[rank]);
+    AMG_CHECK(ebuf.alloc(ne));
+    if (pnnz > 0) k_int2dbl<<<nb(pnnz), kB, 0, s>>>(pnnz, A.pcol.p, ebuf.p);
+    if ((rc = comm->exchange(ep, ebuf.p, s)) != XFK_OK) return rc;
+    AMG_CHECK(pe_col.alloc(ne));
+    if (pnnz > 0)
+        AMG_CHECK(hipMemcpyAsync(pe_col.p, A.pcol.p, sizeof(int) * pnnz, hipMemcpyDeviceToDevice, s));
+    if (nhe > 0) k_dbl2int<<<nb(nhe), kB, 0, s>>>(nhe, ebuf.p + pnnz, pe_col.p + pnnz);
+    // 3. AP over the full rows, then this rank's coarse rows R (AP)
+    long long lnnz = 0;
+    AMG_CHECK(l_row.alloc((size_t)ncmax + 1));
+    {
+        SgX XA{A.rowptr, A.col, A.val, ncl, nullptr, nullptr, nullptr};
+        SgY YP{pe_row.p, pe_col.p, pe_val.p, nullptr};
+        long long apnnz = 0;
+        rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, apnnz);
+        if (rc == XFK_OK) {
+            SgX XR{A.rrow.p, A.rcol.p, A.rval.p, INT_MAX, nullptr, nullptr, nullptr};
+            SgY YAP{ap_row.p, ap_col.p, ap_val.p, nullptr};
+            rc = spgemm<false>(*this, s, nc, XR, YAP, l_row, l_col, l_val, lnnz);
+        }
+        if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
+    }
+    // 4. entry counts and status of every rank
+    {
+        const double mine[2] = {(double)lnnz, rc == XFK_OK ? 0.0 : 1.0};
+        int rc2 = gather_host(*this, comm, s, mine, 2, all);
+        if (rc2 != XFK_OK) return rc2;
+    }
+    std::vector<int> e0(nranks + 1, 0);
+    long long nnzmax = 1;
+    for (int q = 0; q < nranks; ++q) {
+        e0[q + 1] = e0[q] + (int)all[2 * q];
+        nnzmax = std::max(nnzmax, (long long)all[2 * q]);
+        fail |= all[2 * q + 1] != 0.0;
+    }
+    if (fail) {
+        set_error("AMG: a SpGEMM row exceeds the LDS hash capacity");
+        return XFK_ERR_UNSUPPORTED;
+    }
+    // 5. all-gather the coarse rows (padded per rank) into the global level 1
+    AMG_CHECK(s_col.alloc((size_t)nnzmax));
+    AMG_CHECK(s_val.alloc((size_t)nnzmax));
+    if (lnnz > 0) {
+        AMG_CHECK(hipMemcpyAsync(s_col.p, l_col.p, sizeof(int) * lnnz, hipMemcpyDeviceToDevice, s));
+        AMG_CHECK(hipMemcpyAsync(s_val.p, l_val.p, sizeof(double) * lnnz, hipMemcpyDeviceToDevice, s));
+    }
+    AMG_CHECK(g_row.alloc((size_t)nranks * (ncmax + 1)));
+    AMG_CHECK(g_col.alloc((size_t)nranks * nnzmax));
+    AMG_CHECK(g_val.alloc((size_t)nranks * nnzmax));
+    if ((rc = comm->allgather_bytes(l_row.p, g_row.p, sizeof(int) * (ncmax + 1), s)) != XFK_OK) return rc;
+    if ((rc = comm->allgather_bytes(s_col.p, g_col.p, sizeof(int) * nnzmax, s)) != XFK_OK) return rc;
+    if ((rc = comm->allgather(s_val.p, g_val.p, (size_t)nnzmax, s)) != XFK_OK) return rc;
+    if ((int)L.size() <= 1) L.emplace_back(new AmgLevel());
+    AmgLevel &C = *L[1];
+    const long long NNZ = e0[nranks];
+    AMG_CHECK(C.rowptr_o.alloc((size_t)NC + 1));
+    AMG_CHECK(C.col_o.alloc((size_t)std::max(1LL, NNZ)));
+    AMG_CHECK(C.val_o.alloc((size_t)std::max(1LL, NNZ)));
+    AMG_CHECK(e0_dev.alloc(nranks + 1));
+    AMG_CHECK(hipMemcpyAsync(e0_dev.p, e0.data(), sizeof(int) * (nranks + 1), hipMemcpyHostToDevice, s));
+    k_concat_rowptr<<<nb(NC + 1), kB, 0, s>>>(NC, nranks, c0_dev.p, e0_dev.p, g_row.p, ncmax + 1, C.rowptr_o.p);
+    for (int q = 0; q < nranks; ++q) {
+        const long long cq = e0[q + 1] - e0[q];
+        if (cq == 0) continue;
+        AMG_CHECK(hipMemcpyAsync(C.col_o.p + e0[q], g_col.p + (size_t)q * nnzmax, sizeof(int) * cq,
+                                 hipMemcpyDeviceToDevice, s));
+        AMG_CHECK(hipMemcpyAsync(C.val_o.p + e0[q], g_val.p + (size_t)q * nnzmax, sizeof(double) * cq,
+                                 hipMemcpyDeviceToDevice, s));
+    }
+    C.n = NC;
+    C.nnz = NNZ;
+    C.ncol_lim = NC;
+    C.ncol_smooth = NC;
+    C.rowptr = C.rowptr_o.p;
+    C.col = C.col_o.p;
+    C.val = C.val_o.p;
+    AMG_CHECK(cb_loc.alloc((size_t)ncmax));
+    AMG_CHECK(cb_all.alloc((size_t)nranks * ncmax));
+    return XFK_OK;
+}
+
 namespace {
 
 template <int MODE>
@@ -1437,20 +1784,20 @@ void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned lon
 {
     if (l == 0) {
         const int g = (A.n + kCgBlock - 1) / kCgBlock;
-        k_amg_smooth<MODE><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
+        k_amg_smooth<MODE><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
                                                   rout, done);
         return;
     }
     const int G = lanes_for(A.n > 0 ? (double)A.nnz / A.n : 1.0);
     const int g = (int)(((long long)A.n * G + 255) / 256);
     if (G == 4)
-        k_amg_smooth_g<MODE, 4><<<g, 256, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
+        k_amg_smooth_g<MODE, 4><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
                                                  rout, done);
     else if (G == 8)
-        k_amg_smooth_g<MODE, 8><<<g, 256, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
+        k_amg_smooth_g<MODE, 8><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
                                                  rout, done);
     else
-        k_amg_smooth_g<MODE, 16><<<g, 256, 0, s>>>(A.n, A.ncol_lim, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
+        k_amg_smooth_g<MODE, 16><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
                                                   out, rout, done);
 }
 
@@ -1519,9 +1866,42 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     return cur;
 }
 
-void Amg::vcycle(hipStream_t s, const double *r, double *u, const int *done)
+int Amg::vcycle(hipStream_t s, const double *r, double *u, const int *done)
 {
-    vcycle_level(*this, s, 0, r, u, done);
+    if (!dist) {
+        vcycle_level(*this, s, 0, r, u, done);
+        return XFK_OK;
+    }
+    // sharded level 0: every sweep reads the peers' halo values of the iterate
+    AmgLevel &A = *L[0];
+    const unsigned long long *rh = rho.p;
+    double *cur = A.xa.p, *oth = A.xb.p;
+    int rc;
+    k_jacobi_first<<<nb(A.n), kB, 0, s>>>(A.n, rh, A.dinv.p, r, cur, done);
+    for (int k = 1; k < sweeps; ++k) {
+        if ((rc = comm->exchange(*halo, cur, s)) != XFK_OK) return rc;
+        launch_smooth(s, kSweep, 0, A, rh, r, cur, oth, nullptr, done);
+        std::swap(cur, oth);
+    }
+    if ((rc = comm->exchange(*halo, cur, s)) != XFK_OK) return rc;
+    launch_smooth(s, kResid, 0, A, rh, r, cur, nullptr, A.r.p, done);
+    // restriction to the own aggregates, gathered into the global level 1
+    launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, cb_loc.p, false,
+              lanes_for(A.nc > 0 ? (double)A.pnnz / A.nc : 1.0), done);
+    if ((rc = comm->allgather(cb_loc.p, cb_all.p, (size_t)ncmax, s)) != XFK_OK) return rc;
+    AmgLevel &C = *L[1];
+    k_unpad<<<nb(C.n), kB, 0, s>>>(C.n, nranks, c0_dev.p, cb_all.p, ncmax, C.b.p, done);
+    const double *xc = vcycle_level(*this, s, 1, C.b.p, nullptr, done);
+    launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)A.pnnz / A.n), done);
+    for (int k = 0; k < sweeps; ++k) {
+        if ((rc = comm->exchange(*halo, cur, s)) != XFK_OK) return rc;
+        double *nx = (k == sweeps - 1) ? u : oth;
+        launch_smooth(s, kSweep, 0, A, rh, r, cur, nx, nullptr, done);
+        oth = cur;
+        cur = nx;
+    }
+    AMG_CHECK(hipGetLastError());
+    return XFK_OK;
 }
 
 }  // namespace xfk

@@ -547,7 +547,11 @@ static int amg_setup(xfk_problem *P)
     XFK_CHECK(hipEventCreate(&e0));
     XFK_CHECK(hipEventCreate(&e1));
     XFK_CHECK(hipEventRecord(e0, s));
-    int rc = P->amg->setup(s, P->N, P->N, P->rowptr.p, P->col.p, P->val.p, P->nnz);
+    // sharded: rank-local aggregation, global coarse levels (Amg::setup_dist)
+    int rc = (P->comm && P->comm->size > 1)
+                 ? P->amg->setup_dist(s, P->comm, P->halo, P->N, P->NL - P->N, P->rowptr.p, P->col.p, P->val.p,
+                                      P->nnz)
+                 : P->amg->setup(s, P->N, P->N, P->rowptr.p, P->col.p, P->val.p, P->nnz);
     XFK_CHECK(hipEventRecord(e1, s));
     XFK_CHECK(hipEventSynchronize(e1));
     float ms = 0;
@@ -593,9 +597,9 @@ static int pcg_start(xfk_problem *P, int flag)
                      P->part_loc.p + 3 * G, P->part_loc.p);
     if (P->pc_used == XFK_PRECOND_AMG) {
         // u0 = M^-1 r0; res_o = (M^-1 b).b (one more V-cycle when x0 != 0)
-        P->amg->vcycle(s, A0.R, A0.U, nullptr);
+        if ((rc = P->amg->vcycle(s, A0.R, A0.U, nullptr)) != XFK_OK) return rc;
         if (flag) {
-            P->amg->vcycle(s, P->b.p, P->W2.p, nullptr);
+            if ((rc = P->amg->vcycle(s, P->b.p, P->W2.p, nullptr)) != XFK_OK) return rc;
             launch_cg_dot(s, N, P->b.p, P->W2.p, P->part_loc.p + 3 * G);
         } else {
             launch_cg_dot(s, N, P->b.p, A0.U, P->part_loc.p + 3 * G);
@@ -618,8 +622,9 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
     const CgAxpyArgs A = cg_args(P, it);
     const size_t G = (size_t)P->Gpart;
     launch_cg_axpy(s, A);
-    if (A.amg) P->amg->vcycle(s, A.R, A.U, &P->pcg.p->done);
-    int rc = exchange(P, A.U);
+    int rc;
+    if (A.amg && (rc = P->amg->vcycle(s, A.R, A.U, &P->pcg.p->done)) != XFK_OK) return rc;
+    rc = exchange(P, A.U);
     if (rc != XFK_OK) return rc;
     if (stamp) XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used], s));
     if (A.amg)

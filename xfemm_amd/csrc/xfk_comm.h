@@ -24,5 +24,7 @@ struct xfk_comm {
     virtual int exchange(const xfk::HaloPlan &h, double *vec, hipStream_t s) = 0;
     // recv[q * n + i] = send_q[i]
     virtual int allgather(const double *send, double *recv, size_t n, hipStream_t s) = 0;
+    // the same for raw bytes (integer arrays): recv[q * bytes + i] = send_q[i]
+    virtual int allgather_bytes(const void *send, void *recv, size_t bytes, hipStream_t s) = 0;
     virtual const char *kind() const = 0;
 };

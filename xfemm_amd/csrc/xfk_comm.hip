@@ -50,6 +50,11 @@ struct RcclComm final : xfk_comm {
         XFK_NCCL(ncclAllGather(send, recv, n, ncclDouble, comm, s));
         return XFK_OK;
     }
+    int allgather_bytes(const void *send, void *recv, size_t bytes, hipStream_t s) override
+    {
+        XFK_NCCL(ncclAllGather(send, recv, bytes, ncclChar, comm, s));
+        return XFK_OK;
+    }
     const char *kind() const override { return "rccl"; }
 };
 
@@ -186,6 +191,15 @@ struct LocalComm final : xfk_comm {
         return collective(send, nullptr, s, "allgather", [&]() -> int {
             for (int q = 0; q < size; ++q)
                 XFK_CHECK(hipMemcpyAsync(recv + (size_t)q * n, hub->src[q], sizeof(double) * n,
+                                         hipMemcpyDeviceToDevice, s));
+            return XFK_OK;
+        });
+    }
+    int allgather_bytes(const void *send, void *recv, size_t bytes, hipStream_t s) override
+    {
+        return collective(static_cast<const double *>(send), nullptr, s, "allgather", [&]() -> int {
+            for (int q = 0; q < size; ++q)
+                XFK_CHECK(hipMemcpyAsync(static_cast<char *>(recv) + (size_t)q * bytes, hub->src[q], bytes,
                                          hipMemcpyDeviceToDevice, s));
             return XFK_OK;
         });
