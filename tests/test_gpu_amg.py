@@ -88,9 +88,10 @@ def test_amg_is_deterministic():
     assert np.array_equal(A1, A2) and np.array_equal(A1, A3)
 
 
-def _laplace_random(n, seed):
+def _laplace_random(n, seed, shift=1.0):
     """5-point operator with random positive conductances and a Dirichlet-like
-    diagonal shift on the first row of nodes (SPD)."""
+    diagonal shift on the first row of nodes (SPD; shift = 0: pure Neumann,
+    constants are the null space)."""
     rng = np.random.default_rng(seed)
     N = n * n
     idx = np.arange(N).reshape(n, n)
@@ -105,7 +106,7 @@ def _laplace_random(n, seed):
         vals += [-c, -c]
         np.add.at(diag, a, c)
         np.add.at(diag, b, c)
-    diag[idx[0]] += 1.0
+    diag[idx[0]] += shift
     rows.append(np.arange(N))
     cols.append(np.arange(N))
     vals.append(diag)
@@ -155,6 +156,20 @@ def test_dense_coarsest_blocked_inverse(n):
     Vd = sla.spsolve(M.tocsc(), b)
     assert it <= 2
     assert rel_err(V, Vd) <= 1e-10
+
+
+def test_dense_coarsest_null_direction():
+    """A pure-Neumann operator (no Dirichlet shift: constants are its null
+    space) with a consistent right-hand side: the Gauss-Jordan inverse meets
+    a vanishing pivot, zeroes that direction (generalised inverse on the
+    range) and the PCG still solves the system."""
+    M = _laplace_random(30, 11, shift=0.0)
+    n = M.shape[0]
+    b = np.random.default_rng(5).standard_normal(n)
+    b -= b.mean()
+    V, it, er = kernels.pcg_solve_csr(M.indptr, M.indices, M.data, b, precision=1e-10, precond="amg")
+    assert np.all(np.isfinite(V))
+    assert np.linalg.norm(M @ V - b) <= 1e-8 * np.linalg.norm(b)
 
 
 def test_amg_without_couplings_uses_smoother_only():

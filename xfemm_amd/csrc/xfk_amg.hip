@@ -784,9 +784,10 @@ __global__ void k_spgemm_compact(int nrows, int cap, const int *__restrict__ cro
 //     M_ij -= C_i T_kj       (i, j != k)  k_bgj_update (tile GEMMs)
 //     M_ik = -C_i D          (i != k)
 // The matrix is first scaled symmetrically to unit diagonal and the inverse
-// unscaled at the end.  A pivot that vanishes relative to the largest scaled
-// diagonal entry marks a null direction: its row and column are zeroed
-// (generalised inverse on the range).
+// unscaled at the end.  A pivot below 1e-11 of the (unit) scaled diagonal
+// marks a null direction -- roundoff leaves the exact null pivot of a
+// pure-Neumann operator near 1e-13 (tools/lab/gj_emul.py) -- and its row and
+// column are zeroed (generalised inverse on the range).
 constexpr int kBj = 64;
 
 // the matrix has been zeroed (hipMemsetAsync); entries of row i, identity tail
@@ -848,56 +849,127 @@ __global__ void __launch_bounds__(1024) k_dense_maxdiag(int n, int ld, const dou
 
 // D = inv(M_kk) by in-place Gauss-Jordan: 256 threads, thread t keeps the 16
 // entries (rows 16 (t >> 6) + m, column t & 63) in registers for the whole
-// inversion.  Pivot p is one uniform rank-1 update a_ij -= c_i r_j with
-//     c_i = a_ip (i != p),  c_p = a_pp - 1,
-//     r_j = a_pj / a_pp (j != p),  r_p = 1 + 1 / a_pp,
-// which leaves a_pj / a_pp in row p, -a_ip / a_pp in column p and 1 / a_pp at
-// the pivot; it is cancellation-free because the scaled pivots lie in (0, 1].
-// Row p and column p go through LDS, double-buffered: one barrier per pivot.
+// inversion.  Pivots are taken four at a time: with P = {p0 .. p0+3},
+// Dinv = inv(A_PP) (every thread inverts the 4 x 4 block in registers) and
+//     c_i = A_iP,  r_j = Dinv A_Pj (j not in P),  r_j = e_t + Dinv[:, t] (j = p0 + t),
+// one uniform rank-4 update a_ij -= c_i . r_j followed by a_sj += r_j[s] on
+// the rows of P leaves Dinv A_Pj in rows P, -A_iP Dinv in columns P and Dinv
+// in the pivot block; the scaled pivots lie in (0, 1], so no step cancels
+// more than a few bits.  A pivot block with a vanishing pivot is eliminated
+// by four scalar steps instead, which zero the row and column of a null
+// direction.  Rows P and columns P go through LDS, double-buffered: one
+// barrier per step.
+__device__ __forceinline__ void gj_scalar_step(int p, double (&a)[16], double thr, double *slab, double *colk)
+{
+    const int j = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (w == (p >> 4))   // the wave holding row p publishes its slab
+#pragma unroll
+        for (int m = 0; m < 16; ++m) slab[m * kBj + j] = a[m];
+    if (j == p)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) colk[16 * w + m] = a[m];
+    __syncthreads();
+    const double *rowp = slab + (p & 15) * kBj;
+    const double piv = rowp[p];
+    if (!(fabs(piv) > thr)) {   // null direction: zero row p and column p
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            if (16 * w + m == p || j == p) a[m] = 0.0;
+        return;
+    }
+    const double ip = 1.0 / piv;
+    const double r = j == p ? 1.0 + ip : rowp[j] * ip;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) a[m] -= (colk[16 * w + m] - (16 * w + m == p ? 1.0 : 0.0)) * r;
+}
+
 __global__ void __launch_bounds__(256) k_bgj_diag(int k, int ld, const double *__restrict__ M,
                                                   const double *__restrict__ maxd, double *__restrict__ D)
 {
-    __shared__ double rowk[2][kBj];
-    __shared__ __attribute__((aligned(16))) double colk[2][kBj];
+    __shared__ __attribute__((aligned(16))) double rowb[2][16 * kBj];  // the 16-row slab holding P: [m][j]
+    __shared__ __attribute__((aligned(16))) double colb[2][kBj * 4];   // columns P: [i][t]
     const int tid = threadIdx.x;
     const int j = tid & 63, w = tid >> 6;
     const size_t base = (size_t)k * kBj * ld + (size_t)k * kBj;
     double a[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) a[m] = M[base + (size_t)(16 * w + m) * ld + j];
-    const double thr = 1e-13 * (*maxd);
-    for (int p = 0; p < kBj; ++p) {
-        const int buf = p & 1, mp = p & 15;
-        if (w == (p >> 4)) {   // this wave holds row p
-            double own = a[0];
+    const double thr = 1e-11 * (*maxd);
+    int phase = 0;
+    for (int p0 = 0; p0 < kBj; p0 += 4) {
+        const int buf = phase & 1;
+        const int mb = p0 & 15, wp = p0 >> 4;
+        double *R4 = rowb[buf], *C4 = colb[buf];
+        if (w == wp)   // this wave holds rows P: publish its whole slab (no dynamic register index)
 #pragma unroll
-            for (int m = 1; m < 16; ++m)
-                if (m == mp) own = a[m];
-            rowk[buf][j] = own;
-        }
-        if (j == p) {   // this lane holds column p
-            double2 *cw = reinterpret_cast<double2 *>(&colk[buf][16 * w]);
+            for (int m = 0; m < 16; ++m) R4[m * kBj + j] = a[m];
+        R4 += mb * kBj;   // rows P = slab rows mb .. mb+3
+        if (j >= p0 && j < p0 + 4)   // these lanes hold columns P
 #pragma unroll
-            for (int m = 0; m < 16; m += 2) cw[m / 2] = make_double2(a[m], a[m + 1]);
-            if (w == (p >> 4)) colk[buf][p] = a[mp] - 1.0;
-        }
+            for (int m = 0; m < 16; ++m) C4[(16 * w + m) * 4 + (j - p0)] = a[m];
         __syncthreads();
-        const double piv = rowk[buf][p];
-        if (!(fabs(piv) > thr)) {   // null direction: zero row p and column p
+        ++phase;
+        // Dinv = inv(A_PP), in-place Gauss-Jordan in registers
+        double Dv[4][4];
 #pragma unroll
-            for (int m = 0; m < 16; ++m)
-                if (16 * w + m == p || j == p) a[m] = 0.0;
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Dv[s2][t] = R4[s2 * kBj + p0 + t];
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const double piv = Dv[q][q];
+            ok = ok && (fabs(piv) > thr);
+            const double ip = 1.0 / piv;
+            Dv[q][q] = 1.0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Dv[q][t] *= ip;
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                if (s2 == q) continue;
+                const double f = Dv[s2][q];
+                Dv[s2][q] = 0.0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) Dv[s2][t] -= f * Dv[q][t];
+            }
+        }
+        if (!ok) {   // a (near) null direction inside the block: scalar steps
+            for (int p = p0; p < p0 + 4; ++p) {
+                const int b2 = phase & 1;
+                gj_scalar_step(p, a, thr, rowb[b2], colb[b2]);
+                ++phase;
+            }
             continue;
         }
-        const double ip = 1.0 / piv;
-        const double r = j == p ? 1.0 + ip : rowk[buf][j] * ip;
-        const double2 *cr = reinterpret_cast<const double2 *>(&colk[buf][16 * w]);
+        double r[4];
+        if (j >= p0 && j < p0 + 4) {
+            const int t = j - p0;
 #pragma unroll
-        for (int m = 0; m < 16; m += 2) {
-            const double2 c = cr[m / 2];
-            a[m] -= c.x * r;
-            a[m + 1] -= c.y * r;
+            for (int s2 = 0; s2 < 4; ++s2) {
+                double d = Dv[s2][0];
+#pragma unroll
+                for (int tt = 1; tt < 4; ++tt)
+                    if (tt == t) d = Dv[s2][tt];
+                r[s2] = (s2 == t ? 1.0 : 0.0) + d;
+            }
+        } else {
+            const double x0 = R4[j], x1 = R4[kBj + j], x2 = R4[2 * kBj + j], x3 = R4[3 * kBj + j];
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) r[s2] = Dv[s2][0] * x0 + Dv[s2][1] * x1 + Dv[s2][2] * x2 + Dv[s2][3] * x3;
         }
+        const double4 *cr = reinterpret_cast<const double4 *>(&C4[16 * w * 4]);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const double4 c = cr[m];
+            a[m] -= c.x * r[0] + c.y * r[1] + c.z * r[2] + c.w * r[3];
+        }
+        if (w == wp)
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const int s2 = m - mb;
+                a[m] += (s2 == 0 ? r[0] : 0.0) + (s2 == 1 ? r[1] : 0.0) + (s2 == 2 ? r[2] : 0.0) +
+                        (s2 == 3 ? r[3] : 0.0);
+            }
     }
 #pragma unroll
     for (int m = 0; m < 16; ++m) D[(16 * w + m) * kBj + j] = a[m];
@@ -1048,9 +1120,10 @@ __device__ __forceinline__ void smooth_finish(int i, double ax, double w, const 
     if constexpr (MODE == kResidFromZero) out[i] = xi;
 }
 
-// level 0: CSR-stream tile SpMV (the PCG's kernel shape)
-template <int MODE>
-__global__ void __launch_bounds__(kCgBlock) k_amg_smooth(int n, int ncl, const int *__restrict__ rowptr,
+// CSR-stream tile SpMV (the PCG's kernel shape): B = 1024 on level 0, 256 on
+// large coarse levels (more workgroups than CUs)
+template <int MODE, int B>
+__global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__restrict__ rowptr,
                                                          const int *__restrict__ col, const double *__restrict__ val,
                                                          const double *__restrict__ dinv,
                                                          const unsigned long long *rho, const double *__restrict__ b,
@@ -1058,16 +1131,17 @@ __global__ void __launch_bounds__(kCgBlock) k_amg_smooth(int n, int ncl, const i
                                                          double *__restrict__ rout, const int *done)
 {
     if (done && *done) return;
-    __shared__ __attribute__((aligned(16))) double lds[kCgCap];
+    __shared__ __attribute__((aligned(16))) double lds[8 * B];
     const double ra = rho_of(rho);
     const double w = ra > 0.0 ? 1.0 / ra : 0.0;
-    const int r0 = blockIdx.x * kCgBlock;
+    const int r0 = xcd_tile(blockIdx.x, gridDim.x) * B;
     constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
     double ax;
     if constexpr (implicit)
-        ax = cg_tile_spmv(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; }, lds);
+        ax = cg_tile_spmv<B>(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; },
+                             lds);
     else
-        ax = cg_tile_spmv(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; }, lds);
+        ax = cg_tile_spmv<B>(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; }, lds);
     const int i = r0 + threadIdx.x;
     if (i < n) smooth_finish<MODE>(i, ax, w, dinv, b, x, out, rout);
 }
@@ -1106,6 +1180,20 @@ __global__ void __launch_bounds__(256) k_amg_smooth_g(int n, int ncl, const int 
     else
         ax = group_row_dot<G>(i, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; });
     if (i < n && (threadIdx.x & (G - 1)) == 0) smooth_finish<MODE>(i, ax, w, dinv, b, x, out, rout);
+}
+
+// y = M x (ACC: y += M x), tile form (large transfer operators)
+template <int B, bool ACC>
+__global__ void __launch_bounds__(B) k_csr_mv_tile(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                   const double *__restrict__ val, const double *__restrict__ x,
+                                                   double *__restrict__ y, const int *done)
+{
+    if (done && *done) return;
+    __shared__ __attribute__((aligned(16))) double lds[8 * B];
+    const int r0 = xcd_tile(blockIdx.x, gridDim.x) * B;
+    const double s = cg_tile_spmv<B>(r0, n, rowptr, col, val, [&](int j) { return x[j]; }, lds);
+    const int i = r0 + threadIdx.x;
+    if (i < n) y[i] = ACC ? y[i] + s : s;
 }
 
 // y = M x (ACC: y += M x), G lanes per row (restriction R r, prolongation x += P xc)
@@ -1343,6 +1431,9 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     return XFK_OK;
 }
 
+// levels / transfer operators with at least this many rows use the tile kernels
+constexpr int kTileMinRows = 16384;
+
 // lanes per row for a CSR with this many nonzeros per row on average
 int lanes_for(double per_row)
 {
@@ -1353,6 +1444,12 @@ void launch_mv(hipStream_t s, int n, const int *rowptr, const int *col, const do
                bool acc, int G, const int *done)
 {
     if (n <= 0) return;
+    if (n >= kTileMinRows && G <= 8) {
+        const int g = (n + 255) / 256;
+        if (acc) k_csr_mv_tile<256, true><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+        else k_csr_mv_tile<256, false><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+        return;
+    }
     const int g = (int)(((long long)n * G + 255) / 256);
 #define XFK_MV(GG)                                                                                        \
     if (acc) k_csr_mv_g<GG, true><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);                    \
@@ -1784,8 +1881,14 @@ void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned lon
 {
     if (l == 0) {
         const int g = (A.n + kCgBlock - 1) / kCgBlock;
-        k_amg_smooth<MODE><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
-                                                  rout, done);
+        k_amg_smooth<MODE, kCgBlock><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p,
+                                                            rho, b, x, out, rout, done);
+        return;
+    }
+    if (A.n >= kTileMinRows) {
+        const int g = (A.n + 255) / 256;
+        k_amg_smooth<MODE, 256><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
+                                                  out, rout, done);
         return;
     }
     const int G = lanes_for(A.n > 0 ? (double)A.nnz / A.n : 1.0);

@@ -80,7 +80,8 @@ __global__ void __launch_bounds__(kCgBlock) k_cg_spmv(int N, const int *__restri
     if (S && S->done) return;
     __shared__ __attribute__((aligned(16))) double lds[kCgCap];
     __shared__ double red[2 * (kCgBlock / 64)];
-    const int r0 = blockIdx.x * kCgBlock;
+    const int t = xcd_tile(blockIdx.x, gridDim.x);
+    const int r0 = t * kCgBlock;
     const double w = cg_tile_spmv(r0, N, rowptr, col, val, [&](int j) { return U[j]; }, lds);
     const int r = r0 + threadIdx.x;
     double d = 0.0, g = 0.0;
@@ -92,8 +93,8 @@ __global__ void __launch_bounds__(kCgBlock) k_cg_spmv(int N, const int *__restri
     }
     cg_block_sum2(d, g, red);
     if (threadIdx.x == 0) {
-        part_del[blockIdx.x] = d;
-        if (R) part_gam[blockIdx.x] = g;
+        part_del[t] = d;
+        if (R) part_gam[t] = g;
     }
 }
 
@@ -101,12 +102,24 @@ __global__ void __launch_bounds__(kCgBlock) k_cg_spmv(int N, const int *__restri
 __device__ __forceinline__ void cg_reduce2(const double *__restrict__ pa, int Ga, const double *__restrict__ pb,
                                            int Gb, double &a, double &b, double *red)
 {
-    double sa = 0.0, sb = 0.0;
-    for (int i = threadIdx.x; i < Ga; i += blockDim.x) sa += pa[i];
-    for (int i = threadIdx.x; i < Gb; i += blockDim.x) sb += pb[i];
-    cg_block_sum2(sa, sb, red);
-    a = sa;
-    b = sb;
+    // four independent accumulators per array so the loads overlap (a fixed
+    // order: every block, every run gets the same bits)
+    double sa[4] = {0.0, 0.0, 0.0, 0.0}, sb[4] = {0.0, 0.0, 0.0, 0.0};
+    const int st = blockDim.x;
+    int i = threadIdx.x;
+    for (; i + 3 * st < Ga; i += 4 * st)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) sa[m] += pa[i + m * st];
+    for (; i < Ga; i += st) sa[0] += pa[i];
+    i = threadIdx.x;
+    for (; i + 3 * st < Gb; i += 4 * st)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) sb[m] += pb[i + m * st];
+    for (; i < Gb; i += st) sb[0] += pb[i];
+    double ra = (sa[0] + sa[1]) + (sa[2] + sa[3]), rb = (sb[0] + sb[1]) + (sb[2] + sb[3]);
+    cg_block_sum2(ra, rb, red);
+    a = ra;
+    b = rb;
 }
 
 // CgAxpyArgs: xfk_kernels.h

@@ -6,7 +6,7 @@
 
 namespace xfk {
 
-constexpr int kCgBlock = 1024;            // 16 waves; one row tile per workgroup
+constexpr int kCgBlock = 512;             // 8 waves; one row tile per workgroup
 constexpr int kCgCap = 8 * kCgBlock;      // products staged per LDS pass (64 KiB)
 
 __device__ __forceinline__ double cg_wave_sum(double v)
@@ -52,30 +52,44 @@ __device__ __forceinline__ void cg_reduce_partials(const double *__restrict__ pa
     b = sb;
 }
 
-// y = sum_k val[k] * X(col[k]) for the rows of one tile; CSR-stream through LDS
-template <class XF>
+// XCD-aware tile order: workgroup b is dispatched to XCD b % 8, so XCD x gets
+// the contiguous run of tiles [x q + min(x, r), ...) (q = nb / 8, r = nb % 8)
+// and its L2 serves the x-vector reuse between neighbouring tiles of a banded
+// matrix instead of every XCD fetching every tile's halo of x
+__device__ __forceinline__ int xcd_tile(int b, int nb)
+{
+    const int q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
+    return x * q + min(x, r) + k;
+}
+
+// y = sum_k val[k] * X(col[k]) for the B rows of one tile (B threads, one
+// row each); CSR-stream: the tile's products are staged through LDS (8 B
+// doubles per pass) by coalesced reads of col / val, then each thread sums
+// its own row
+template <int B = kCgBlock, class XF>
 __device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restrict__ rowptr,
                                                const int *__restrict__ col, const double *__restrict__ val,
                                                XF X, double *lds)
 {
+    constexpr int CAP = 8 * B;
     const int r = r0 + threadIdx.x;
-    const int rend = min(r0 + kCgBlock, N);
+    const int rend = min(r0 + B, N);
     const int s = rowptr[r0], e = rowptr[rend];
     const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
     double acc = 0.0;
-    for (int c0 = s; c0 < e; c0 += kCgCap) {
-        const int c1 = min(e, c0 + kCgCap);
+    for (int c0 = s; c0 < e; c0 += CAP) {
+        const int c1 = min(e, c0 + CAP);
         int cidx[8];
         double v[8];
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
-            const int k = c0 + threadIdx.x + m * kCgBlock;
+            const int k = c0 + threadIdx.x + m * B;
             cidx[m] = (k < c1) ? col[k] : -1;
             v[m] = (k < c1) ? val[k] : 0.0;
         }
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
-            const int k = c0 + threadIdx.x + m * kCgBlock;
+            const int k = c0 + threadIdx.x + m * B;
             if (cidx[m] >= 0) lds[k - c0] = v[m] * X(cidx[m]);
         }
         __syncthreads();
