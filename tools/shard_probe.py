@@ -5,12 +5,24 @@ sys.path.insert(0, R)
 import numpy as np
 from xfemm_amd import kernels, synth
 cells = int(sys.argv[1]) if len(sys.argv) > 1 else 400
+ranks = [int(a) for a in sys.argv[2:] if not a.startswith("--")] or [2, 4, 8]
+opt = {}
+for a in sys.argv[2:]:
+    if a.startswith("--omega="):
+        opt["amg_omega"] = float(a.split("=")[1])
+    if a.startswith("--sweeps="):
+        opt["amg_sweeps"] = int(a.split("=")[1])
+    if a.startswith("--theta="):
+        opt["amg_theta"] = float(a.split("=")[1])
+    if a == "--single-only":
+        ranks = []
 kw = synth.magnetostatic(cells)
-P = kernels.Static2DProblem(**kw); r1 = P.solve(); A1 = P.solution(); P.close()
-print("single: iters %d levels %d" % (r1["cg_iters"], r1["amg_levels"]), flush=True)
-for n in [2, 4, 8]:
+P = kernels.Static2DProblem(**kw, **opt); r1 = P.solve(); A1 = P.solution(); P.close()
+print("single: iters %d levels %d setup %.1f ms solve %.1f ms" % (r1["cg_iters"], r1["amg_levels"],
+      r1["ms_amg_setup"], r1["ms_solve"]), flush=True)
+for n in ranks:
     comms = kernels.Comm.local_group(n)
-    probs = [kernels.Static2DProblem(**kw, comm=comms[q]) for q in range(n)]
+    probs = [kernels.Static2DProblem(**kw, comm=comms[q], **opt) for q in range(n)]
     out = [None] * n
     def work(q):
         out[q] = (probs[q].solve(), probs[q].solution())
@@ -19,6 +31,7 @@ for n in [2, 4, 8]:
     [t.start() for t in th]; [t.join() for t in th]
     dt = time.time() - t0
     r, A = out[0]
-    print("ranks %d: iters %d precond %d levels %d err vs single %.2e (%.2f s)" % (
-        n, r["cg_iters"], r["precond"], r["amg_levels"], np.abs(A - A1).max() / np.abs(A1).max(), dt), flush=True)
+    print("ranks %d: iters %d precond %d levels %d err vs single %.2e (%.2f s; rank 0: setup %.1f ms solve %.1f ms)" % (
+        n, r["cg_iters"], r["precond"], r["amg_levels"], np.abs(A - A1).max() / np.abs(A1).max(), dt,
+        r["ms_amg_setup"], r["ms_solve"]), flush=True)
     [p.close() for p in probs]; [c.close() for c in comms]

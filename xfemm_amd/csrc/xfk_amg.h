@@ -12,8 +12,9 @@
 //   MIS-2       parallel maximal distance-2 independent set of the strength
 //               graph, keys (state, hash(i), i), two max-propagation sweeps per round
 //   aggregates  roots, then distance-1 and distance-2 joins (max-key neighbour)
-//   P           (I - omega D_F^-1 A_F) P_tent, A_F = strong part + weak entries lumped
-//               onto the diagonal, omega = 4 / (3 rho_F), rho_F Gershgorin bound
+//   P           (I - W D_F^-1 A_F) P_tent, A_F = strong part + weak entries lumped
+//               onto the diagonal, W_ii = 4 / (3 max(rho_i, 2)), rho_i the row's
+//               Gershgorin bound of D_F^-1 A_F
 //   R = P^T     counting transpose, rows sorted, values looked up in P
 //   A_{l+1}     R (A P), two wave-per-row SpGEMMs with LDS hash tables and an
 //               ordered per-product accumulation (bit-reproducible)
@@ -86,7 +87,7 @@ struct Amg {
     AmgStats stats;
 
     // setup scratch (reused across setups)
-    DBuf<double> absd, dfinv, rho_part;
+    DBuf<double> absd, dfinv, wF, rho_part;
     DBuf<unsigned char> sflag;
     DBuf<unsigned long long> key, t1;
     DBuf<int> cnt, agg1, agg, flag, cursor;

@@ -15,6 +15,9 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 
 #include "xfk_amg.h"
 #include "xfk_comm.h"
@@ -137,7 +140,8 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
                                                      const int *__restrict__ col, const double *__restrict__ val,
                                                      const double *__restrict__ absd,
                                                      unsigned char *__restrict__ sflag, int *__restrict__ sdeg,
-                                                     double *__restrict__ dfinv, double *__restrict__ rho_part)
+                                                     double *__restrict__ dfinv, double *__restrict__ wF,
+                                                     double *__restrict__ rho_part)
 {
     __shared__ double red[2 * (kB / 64)];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -145,7 +149,7 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
     if (i < n) {
         const double ai = absd[i];
         double aii = 0.0, lump = 0.0, sumS = 0.0, sumA = 0.0;
-        int deg = 0;
+        int deg = 0, hdeg = 0;
         for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
             const int j = col[k];
             const double a = val[k];
@@ -156,8 +160,11 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
             } else if (j >= ncl) {
                 // halo column: read by the smoother; for the rank-local P it is
                 // lumped like a weak entry, so P keeps reproducing constants
+                // (strong by the one-sided test |a_ij| > theta |a_ii|: the
+                // peer's diagonal is not known here)
                 sumA += fabs(a);
                 lump += a;
+                hdeg += (fabs(a) > theta * ai);
             } else {
                 sumA += fabs(a);
                 if (a != 0.0 && fabs(a) > theta * sqrt(ai * absd[j])) {
@@ -171,10 +178,18 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
             sflag[k] = f;
         }
         const double dF = aii + lump;
-        dfinv[i] = (dF != 0.0) ? 1.0 / dF : 0.0;
-        sdeg[i] = deg;
+        // -1: every strong coupling crosses to a peer -> a singleton aggregate
+        sdeg[i] = (deg == 0 && hdeg > 0) ? -1 : deg;
         if (aii != 0.0) rA = (fabs(aii) + sumA) / fabs(aii);
         if (dF != 0.0) rF = (fabs(dF) + sumS) / fabs(dF);
+        // prolongator smoothing weight per row, 4 / (3 max(rho_i, 2)) with
+        // rho_i the row's Gershgorin bound of D_F^-1 A_F: one row whose
+        // filtered diagonal nearly cancels no longer shrinks the weight of
+        // every row of the level (a global Gershgorin maximum of 100-200 was
+        // measured on coarse levels of the steel / air problem)
+        // rows without strong couplings keep the tentative (injection) row
+        dfinv[i] = (dF != 0.0) ? 1.0 / dF : 0.0;
+        wF[i] = (dF != 0.0 && deg > 0) ? (4.0 / 3.0) / fmax(rF, 2.0) : 0.0;
     }
     block_max2(rA, rF, red);
     if (threadIdx.x == 0) {
@@ -190,7 +205,7 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
 __global__ void k_mis_init(int n, const int *__restrict__ sdeg, unsigned long long *__restrict__ key)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) key[i] = mis_key(sdeg[i] > 0 ? kStUnd : 0ull, i);
+    if (i < n) key[i] = mis_key(sdeg[i] > 0 ? kStUnd : (sdeg[i] < 0 ? kStIn : 0ull), i);
 }
 
 __global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
@@ -233,6 +248,32 @@ __global__ void k_agg_roots(int n, const unsigned long long *__restrict__ key, i
 
 // distance 1: roots keep their aggregate, neighbours of roots join the root
 // with the largest key
+// rows left out that have (weak) couplings to aggregated owned rows join the
+// aggregate of the largest |a_ij| (ties: larger j); their P row is the
+// tentative injection (no strong couplings -> smoothing weight 0)
+__global__ void k_agg_join3(int n, int ncl, const int *__restrict__ rowptr, const int *__restrict__ col,
+                            const double *__restrict__ val, const int *__restrict__ agg2, int *__restrict__ agg)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int a = agg2[i];
+    if (a < 0) {
+        double best = 0.0;
+        int bj = -1;
+        for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+            const int j = col[k];
+            if (j == i || j >= ncl || agg2[j] < 0) continue;
+            const double v = fabs(val[k]);
+            if (v > best || (v == best && v > 0.0 && j > bj)) {
+                best = v;
+                bj = j;
+            }
+        }
+        if (bj >= 0) a = agg2[bj];
+    }
+    agg[i] = a;
+}
+
 __global__ void k_agg_join1(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
                             const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ key,
                             const int *__restrict__ rootid, int *__restrict__ agg1)
@@ -385,8 +426,8 @@ struct SgX {
     const double *val;
     int col_lim;                   // X columns >= col_lim are skipped (sharded halo)
     const unsigned char *mask;     // PMODE: sflag (1 strong, 2 diagonal)
-    const double *dfinv;           // PMODE
-    const unsigned long long *rhoF;   // PMODE
+    const double *dfinv;           // PMODE: D_F^-1
+    const double *wF;              // PMODE: per-row smoothing weight
 };
 struct SgY {
     const int *rowptr, *col;
@@ -427,8 +468,7 @@ __global__ void __launch_bounds__(64) k_spgemm(int nrows, SgX X, SgY Y, int *__r
     const int xs = X.rowptr[row], xe = X.rowptr[row + 1];
     double omega = 0.0, dfi = 0.0;
     if (PMODE) {
-        const double rF = rho_of(X.rhoF);
-        omega = rF > 0.0 ? (4.0 / 3.0) / rF : 0.0;
+        omega = X.wF[row];
         dfi = X.dfinv[row];
     }
 
@@ -653,8 +693,7 @@ __global__ void __launch_bounds__(64) k_spgemm_sw1(int nrows, SgX X, SgY Y, int 
     const int xs = X.rowptr[row], xe = X.rowptr[row + 1];
     double omega = 0.0, dfi = 0.0;
     if (PMODE) {
-        const double rF = rho_of(X.rhoF);
-        omega = rF > 0.0 ? (4.0 / 3.0) / rF : 0.0;
+        omega = X.wF[row];
         dfi = X.dfinv[row];
     }
     // enumerate products into LDS, in the fixed order
@@ -1243,6 +1282,18 @@ __global__ void __launch_bounds__(256) k_dense_mv(int n, int ld, const double *_
     if (lane == 0) x[i] = s;
 }
 
+// diagnostics (XFK_AMG_DEBUG): rows left without an aggregate, split by
+// whether they have strong (owned) couplings / any off-diagonal coupling
+__global__ void k_debug_unagg(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+                              const int *__restrict__ sdeg, const int *__restrict__ agg, int *out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || agg[i] >= 0) return;
+    int offd = 0;
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) offd += (col[k] != i);
+    atomicAdd(&out[sdeg[i] > 0 ? 0 : (offd > 0 ? 1 : 2)], 1);
+}
+
 // --------------------------------------------------------------------------
 // sharded level 0: helpers of the distributed Galerkin product and V-cycle
 // --------------------------------------------------------------------------
@@ -1543,8 +1594,28 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     AMG_CHECK(agg.alloc(n));
     k_agg_join1<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, cursor.p, agg1.p);
     k_agg_join2<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, agg1.p, agg.p);
+    k_agg_join3<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, A.rowptr, A.col, A.val, agg.p, agg1.p);
+    std::swap(agg.p, agg1.p);   // agg = the joined map
+    std::swap(agg.n, agg1.n);
+    if (std::getenv("XFK_AMG_DEBUG")) {
+        DBuf<int> d;
+        AMG_CHECK(d.alloc(3));
+        AMG_CHECK(hipMemsetAsync(d.p, 0, 3 * sizeof(int), s));
+        k_debug_unagg<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, cnt.p, agg.p, d.p);
+        int h[3];
+        unsigned long long r2[2];
+        AMG_CHECK(hipMemcpyAsync(h, d.p, sizeof(h), hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipMemcpyAsync(r2, rho.p + 2 * l, sizeof(r2), hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipStreamSynchronize(s));
+        double ra, rf;
+        std::memcpy(&ra, &r2[0], 8);
+        std::memcpy(&rf, &r2[1], 8);
+        std::fprintf(stderr, "[amg] rank %d level %d n %d nnz %lld nc %lld unaggregated: strong %d weak-only %d isolated %d "
+                     "rhoA/omega %.4g rhoF %.4g mis_rounds %d\n", dist ? rank : 0, l, n, A.nnz, nc, h[0], h[1], h[2],
+                     ra, rf, rounds);
+    }
     // P = (I - omega D_F^-1 A_F) P_tent
-    SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, rho.p + 2 * l + 1};
+    SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, wF.p};
     SgY YT{nullptr, nullptr, nullptr, agg.p};
     if ((rc = spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz)) != XFK_OK) return rc;
     A.nc = (int)nc;
@@ -1579,6 +1650,7 @@ int Amg::build(hipStream_t s, int l0)
         AMG_CHECK(A.dinv.alloc(n));
         AMG_CHECK(absd.alloc(n));
         AMG_CHECK(dfinv.alloc(n));
+        AMG_CHECK(wF.alloc(n));
         AMG_CHECK(cnt.alloc((size_t)n + 1));
         k_amg_diag<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
         if (n <= kAmgDenseMax) {
@@ -1588,7 +1660,7 @@ int Amg::build(hipStream_t s, int l0)
         AMG_CHECK(sflag.alloc((size_t)A.nnz));
         AMG_CHECK(rho_part.alloc(2 * (size_t)nb(n)));
         k_amg_strength<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
-                                            dfinv.p, rho_part.p);
+                                            dfinv.p, wF.p, rho_part.p);
         k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, omega, rho.p + 2 * l);
         if (l == kAmgMaxLevels - 1) break;   // smoother-only coarsest level
         long long nc = 0;
@@ -1698,11 +1770,13 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
     AMG_CHECK(A.dinv.alloc(n));
     AMG_CHECK(absd.alloc(n));
     AMG_CHECK(dfinv.alloc(n));
+    AMG_CHECK(wF.alloc(n));
     AMG_CHECK(cnt.alloc((size_t)n + 1));
     AMG_CHECK(sflag.alloc((size_t)std::max(1LL, nnz)));
     AMG_CHECK(rho_part.alloc(2 * (size_t)nb(n)));
     k_amg_diag<<<nb(n), kB, 0, s>>>(n, rowptr, col, val, absd.p, A.dinv.p);
-    k_amg_strength<<<nb(n), kB, 0, s>>>(n, n, theta, rowptr, col, val, absd.p, sflag.p, cnt.p, dfinv.p, rho_part.p);
+    k_amg_strength<<<nb(n), kB, 0, s>>>(n, n, theta, rowptr, col, val, absd.p, sflag.p, cnt.p, dfinv.p, wF.p,
+                                        rho_part.p);
     k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, omega, rho.p);
     long long nc = 0;
     rc = aggregate(s, 0, nc, false);
@@ -1773,6 +1847,14 @@ int Amg::galerkin_dist(hipStream_t s, int st)
         AMG_CHECK(hipStreamSynchronize(s));
     }
     HaloPlan ep;
+    if (std::getenv("XFK_AMG_DEBUG")) {
+        for (const HaloRange &t : halo->send)
+            std::fprintf(stderr, "[amg] rank %d n %d nh %d send peer %d off %d len %d g0 %d\n", rank, n, nh, t.peer,
+                         t.off, t.len, t.g0);
+        for (const HaloRange &r : halo->recv)
+            std::fprintf(stderr, "[amg] rank %d n %d nh %d recv peer %d off %d len %d g0 %d\n", rank, n, nh, r.peer,
+                         r.off, r.len, r.g0);
+    }
     {
         int k = 0;
         for (const HaloRange &t : halo->send) {
@@ -1868,6 +1950,36 @@ int Amg::galerkin_dist(hipStream_t s, int st)
     C.rowptr = C.rowptr_o.p;
     C.col = C.col_o.p;
     C.val = C.val_o.p;
+    if (std::getenv("XFK_AMG_DEBUG") && rank == 0) {   // symmetry of the gathered A_1
+        std::vector<int> hr(NC + 1), hc(NNZ);
+        std::vector<double> hv(NNZ);
+        AMG_CHECK(hipMemcpyAsync(hr.data(), C.rowptr, sizeof(int) * (NC + 1), hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipMemcpyAsync(hc.data(), C.col, sizeof(int) * NNZ, hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipMemcpyAsync(hv.data(), C.val, sizeof(double) * NNZ, hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipStreamSynchronize(s));
+        std::vector<std::pair<int, double>> row;
+        std::vector<std::vector<std::pair<int, double>>> R(NC);
+        double amax = 0, dmax = 0;
+        long long missing = 0;
+        for (int i = 0; i < NC; ++i) {
+            for (int k = hr[i]; k < hr[i + 1]; ++k) R[i].push_back({hc[k], hv[k]});
+            std::sort(R[i].begin(), R[i].end());
+        }
+        for (int i = 0; i < NC; ++i)
+            for (auto &e : R[i]) {
+                amax = std::max(amax, std::fabs(e.second));
+                auto &Rj = R[e.first];
+                auto it = std::lower_bound(Rj.begin(), Rj.end(), std::make_pair(i, -1e300));
+                if (it == Rj.end() || it->first != i) {
+                    ++missing;
+                    dmax = std::max(dmax, std::fabs(e.second));
+                } else {
+                    dmax = std::max(dmax, std::fabs(e.second - it->second));
+                }
+            }
+        std::fprintf(stderr, "[amg] A_1 %d rows %lld nnz: max|A - A^T| / max|A| = %.3e, %lld entries without a mirror\n",
+                     NC, NNZ, dmax / amax, missing);
+    }
     AMG_CHECK(cb_loc.alloc((size_t)ncmax));
     AMG_CHECK(cb_all.alloc((size_t)nranks * ncmax));
     return XFK_OK;
