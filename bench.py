@@ -234,8 +234,10 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": "configs[%d]: synthetic %d-tri square-domain magnetostatic, %s, tol %g%s" % (
-                4 if sharded else (3 if args.nonlinear else 2), 2 * cells ** 2,
+            "workload": "%s: synthetic %d-tri square-domain magnetostatic, %s, tol %g%s" % (
+                "configs[4]" if (sharded or cells == 3162) else (
+                    ("configs[3]" if args.nonlinear else "configs[2]") if cells == 1000 else "custom size"),
+                2 * cells ** 2,
                 "nonlinear M-19 B-H (Newton)" if args.nonlinear else "linear mu",
                 kw["precision"], (", row-block sharded over %d GPU(s), RCCL halo + all-reduce" % world)
                 if sharded else (", one independent problem per GPU" if world > 1 else "")),
