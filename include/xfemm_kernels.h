@@ -140,7 +140,9 @@ enum {
     XFK_OPT_PRECOND = 1,        /* XFK_PRECOND_* */
     XFK_OPT_AMG_SWEEPS = 2,     /* Jacobi sweeps before and after the coarse correction (1..8, default 1) */
     XFK_OPT_AMG_THETA = 3,      /* strength threshold (0..1, default 0.08) */
-    XFK_OPT_AMG_OMEGA = 4       /* Jacobi weight factor: weight = omega / rho(D^-1 A) (0..2, default 1.75) */
+    XFK_OPT_AMG_OMEGA = 4,      /* Jacobi weight factor: weight = omega / rho(D^-1 A) (0..2, default 1.75) */
+    XFK_OPT_AMG_REPLICATE = 5   /* sharded solve: coarse levels of at most this many global rows are
+                                   replicated on every rank, larger ones stay sharded (default 250000) */
 };
 int xfk_set_option(xfk_problem *prob, int option, double value);
 

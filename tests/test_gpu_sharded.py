@@ -28,9 +28,9 @@ TOL_LINEAR = 1e-6
 TOL_NONLINEAR = 1e-5
 
 
-def run_sharded(kw, nranks):
+def run_sharded(kw, nranks, **opt):
     comms = kernels.Comm.local_group(nranks)
-    probs = [kernels.Static2DProblem(**kw, comm=comms[r]) for r in range(nranks)]
+    probs = [kernels.Static2DProblem(**kw, comm=comms[r], **opt) for r in range(nranks)]
     out = [None] * nranks
     err = [None] * nranks
 
@@ -98,6 +98,23 @@ def test_sharded_amg_iterations_match_single_device(nranks):
     assert res["precond"] == kernels.XFK_PRECOND_AMG
     assert res["cg_iters"] <= 1.25 * r1["cg_iters"] + 2, (res["cg_iters"], r1["cg_iters"])
     assert rel_err(A, A1) <= TOL_LINEAR
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4])
+def test_sharded_coarse_levels(nranks):
+    """A low replication threshold keeps several coarse levels sharded (each
+    with its own halo plan over the peers' aggregate ids) before the global
+    replicated tail: same answer, iterations as on one device."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(48))
+    Ao, _, _ = oracle.solve(pr, mesh)
+    r1, A1, _ = single(kw)
+    outs = run_sharded(kw, nranks, amg_replicate=40)
+    for res, A, _, _ in outs:
+        assert res["precond"] == kernels.XFK_PRECOND_AMG
+        assert rel_err(A, Ao) <= TOL_LINEAR
+        assert rel_err(A, A1) <= TOL_LINEAR
+        assert res["cg_iters"] <= 1.25 * r1["cg_iters"] + 2, (res["cg_iters"], r1["cg_iters"])
+    assert np.array_equal(outs[0][1], outs[-1][1])
 
 
 def test_sharded_nonlinear_matches_oracle():

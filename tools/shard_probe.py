@@ -14,6 +14,8 @@ for a in sys.argv[2:]:
         opt["amg_sweeps"] = int(a.split("=")[1])
     if a.startswith("--theta="):
         opt["amg_theta"] = float(a.split("=")[1])
+    if a.startswith("--rep="):
+        opt["amg_replicate"] = int(a.split("=")[1])
     if a == "--single-only":
         ranks = []
 kw = synth.magnetostatic(cells)

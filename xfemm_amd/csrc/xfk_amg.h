@@ -60,6 +60,11 @@ struct AmgLevel {
     DBuf<double> pval, rval;
     // V-cycle vectors: b (right-hand side, levels >= 1), two iterate buffers, residual
     DBuf<double> b, xa, xb, r;
+    // sharded level: rows owned by this rank, halo columns n .. ncol_smooth-1
+    // filled by exchanges over `plan` (level 0: the problem's node plan;
+    // coarser: spans of the peers' aggregate ids)
+    bool dist = false;
+    HaloPlan plan;
 };
 
 struct AmgStats {
@@ -99,15 +104,19 @@ struct Amg {
     int *host_int = nullptr;          // pinned mirror
     DBuf<char> cub_tmp;
 
-    // sharded level 0 (setup_dist): every rank aggregates its own rows, the
-    // coarse levels are global and replicated on every rank
+    // sharded hierarchy (setup_dist): levels 0 .. lrep-1 are sharded (each rank
+    // aggregates its own rows; the Galerkin product uses the peers' P rows),
+    // levels lrep.. are global and replicated on every rank once the global
+    // level has <= rep_rows rows
     bool dist = false;
+    int rep_rows = 250000;
+    int lrep = 0;
     xfk_comm *comm = nullptr;
-    const HaloPlan *halo = nullptr;   // level-0 halo exchange (the problem's node plan)
     int nranks = 1, rank = 0;
-    std::vector<int> c0;              // global coarse offset of each rank's aggregates (nranks + 1)
-    int ncmax = 0;                    // largest per-rank aggregate count (all-gather stride)
+    std::vector<int> c0;              // first row of each rank's aggregates on level lrep (nranks + 1)
+    int ncmax = 0;                    // largest per-rank aggregate count there (all-gather stride)
     DBuf<int> c0_dev;
+    DBuf<int> span_dev, map_dev;      // peer spans of a sharded coarse level (setup scratch)
     DBuf<double> cb_loc, cb_all;      // restricted residual: own aggregates, all-gathered (padded)
     DBuf<int> pe_row, pe_col;         // P extended by the halo nodes' rows (global coarse columns)
     DBuf<double> pe_val, ebuf;
@@ -139,7 +148,8 @@ struct Amg {
     int init(hipStream_t s);
     int build(hipStream_t s, int l0);
     int aggregate(hipStream_t s, int l, long long &nc, bool allow_stop);
-    int galerkin_dist(hipStream_t s, int st);
+    int galerkin_dist(hipStream_t s, int l, int st, bool &rep);
+    double *vc_dist(hipStream_t s, int l, const double *b, double *out, const int *done, int &rc);
     int host_ints(int count);
 };
 

@@ -1529,6 +1529,10 @@ int Amg::init(hipStream_t s)
     AMG_CHECK(rho.alloc(2 * kAmgMaxLevels));
     AMG_CHECK(hipMemsetAsync(rho.p, 0, sizeof(unsigned long long) * 2 * kAmgMaxLevels, s));
     if (L.empty()) L.emplace_back(new AmgLevel());
+    for (auto &lv : L) {   // levels are rebuilt: none sharded until setup_dist says so
+        lv->dist = false;
+        lv->plan = HaloPlan();
+    }
     stats = AmgStats();
     dense_coarse = false;
     return XFK_OK;
@@ -1539,7 +1543,7 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
 {
     dist = false;
     comm = nullptr;
-    halo = nullptr;
+    lrep = 0;
     int rc = init(s);
     if (rc != XFK_OK) return rc;
     AmgLevel &F = *L[0];
@@ -1752,45 +1756,98 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
 {
     dist = true;
     comm = comm_;
-    halo = &halo_;
     nranks = comm->size;
     rank = comm->rank;
     int rc = init(s);
     if (rc != XFK_OK) return rc;
-    AmgLevel &A = *L[0];
-    A.n = n;
-    A.nnz = nnz;
-    A.ncol_lim = n;            // aggregation and P: the owned block
-    A.ncol_smooth = n + nh;    // smoother and residual: the full rows
-    A.rowptr = rowptr;
-    A.col = col;
-    A.val = val;
-    stats.n[0] = n;
-    stats.nnz[0] = nnz;
-    AMG_CHECK(A.dinv.alloc(n));
-    AMG_CHECK(absd.alloc(n));
-    AMG_CHECK(dfinv.alloc(n));
-    AMG_CHECK(wF.alloc(n));
-    AMG_CHECK(cnt.alloc((size_t)n + 1));
-    AMG_CHECK(sflag.alloc((size_t)std::max(1LL, nnz)));
-    AMG_CHECK(rho_part.alloc(2 * (size_t)nb(n)));
-    k_amg_diag<<<nb(n), kB, 0, s>>>(n, rowptr, col, val, absd.p, A.dinv.p);
-    k_amg_strength<<<nb(n), kB, 0, s>>>(n, n, theta, rowptr, col, val, absd.p, sflag.p, cnt.p, dfinv.p, wF.p,
-                                        rho_part.p);
-    k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, omega, rho.p);
-    long long nc = 0;
-    rc = aggregate(s, 0, nc, false);
-    if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
-    if ((rc = galerkin_dist(s, rc == XFK_OK ? 0 : 1)) != XFK_OK) return rc;
-    return build(s, 1);
+    {
+        AmgLevel &A = *L[0];
+        A.n = n;
+        A.nnz = nnz;
+        A.ncol_lim = n;            // aggregation and P: the owned block
+        A.ncol_smooth = n + nh;    // smoother and residual: the full rows
+        A.rowptr = rowptr;
+        A.col = col;
+        A.val = val;
+        A.dist = true;
+        A.plan = halo_;
+    }
+    for (int l = 0;; ++l) {
+        AmgLevel &A = *L[l];
+        const int nl = A.n;
+        stats.n[l] = nl;
+        stats.nnz[l] = A.nnz;
+        AMG_CHECK(A.dinv.alloc(std::max(1, nl)));
+        AMG_CHECK(absd.alloc(std::max(1, nl)));
+        AMG_CHECK(dfinv.alloc(std::max(1, nl)));
+        AMG_CHECK(wF.alloc(std::max(1, nl)));
+        AMG_CHECK(cnt.alloc((size_t)nl + 1));
+        AMG_CHECK(sflag.alloc((size_t)std::max(1LL, A.nnz)));
+        AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb(nl))));
+        k_amg_diag<<<nb(nl), kB, 0, s>>>(nl, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
+        k_amg_strength<<<nb(nl), kB, 0, s>>>(nl, nl, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p, dfinv.p,
+                                             wF.p, rho_part.p);
+        k_max_reduce<<<1, 1024, 0, s>>>(nb(nl), rho_part.p, omega, rho.p + 2 * l);
+        long long nc = 0;
+        rc = aggregate(s, l, nc, false);
+        if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
+        bool rep = false;
+        if ((rc = galerkin_dist(s, l, rc == XFK_OK ? 0 : 1, rep)) != XFK_OK) return rc;
+        if (rep) {
+            lrep = l + 1;
+            return build(s, l + 1);
+        }
+    }
 }
 
-// A_1 = R (A P_ext) on every rank for its aggregates, all-gathered into the
-// global level 1.  st: this rank's status so far (every rank makes the same
-// collective calls whatever its status).
-int Amg::galerkin_dist(hipStream_t s, int st)
+namespace {
+
+// per peer: the smallest and largest of its ids this rank's columns reference
+__global__ void k_peer_span(long long nnz, const int *__restrict__ col, int own0, int own1,
+                            const int *__restrict__ c0, int nranks, int *lo, int *hi)
 {
-    AmgLevel &A = *L[0];
+    const long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (e >= nnz) return;
+    const int J = col[e];
+    if (J >= own0 && J < own1) return;
+    int q = 0;
+    while (c0[q + 1] <= J) ++q;
+    atomicMin(&lo[q], J);
+    atomicMax(&hi[q], J);
+}
+// global ids -> local: own rows first, then the peers' spans in peer order
+__global__ void k_localize(long long nnz, int *__restrict__ col, int own0, int own1, int n,
+                           const int *__restrict__ c0, int nranks, const int *__restrict__ lo,
+                           const int *__restrict__ off)
+{
+    const long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (e >= nnz) return;
+    const int J = col[e];
+    if (J >= own0 && J < own1) {
+        col[e] = J - own0;
+        return;
+    }
+    int q = 0;
+    while (c0[q + 1] <= J) ++q;
+    col[e] = n + off[q] + (J - lo[q]);
+}
+__global__ void k_fill_int(int n, int *a, int v)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = v;
+}
+
+}  // namespace
+
+// A_{l+1} = R (A P_ext) on every rank for its own aggregates (P_ext: P plus
+// the peers' P rows of the halo nodes, global coarse ids).  The result either
+// stays sharded (own rows, halo spans and an exchange plan built here) or, once
+// the global level has <= rep_rows rows, is all-gathered into the replicated
+// level l+1 (rep = true).  st: this rank's status so far -- every rank makes
+// the same collective calls whatever its status.
+int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
+{
+    AmgLevel &A = *L[l];
     const int n = A.n, nh = A.ncol_smooth - A.n;
     const int nc = st ? 0 : A.nc;
     std::vector<double> all;
@@ -1800,29 +1857,32 @@ int Amg::galerkin_dist(hipStream_t s, int st)
         int rc = gather_host(*this, comm, s, mine, 2, all);
         if (rc != XFK_OK) return rc;
     }
-    c0.assign(nranks + 1, 0);
-    ncmax = 1;
+    std::vector<int> cn(nranks + 1, 0);
+    int cmax = 1, cmin = INT_MAX;
     bool fail = false;
     for (int q = 0; q < nranks; ++q) {
-        c0[q + 1] = c0[q] + (int)all[2 * q];
-        ncmax = std::max(ncmax, (int)all[2 * q]);
+        cn[q + 1] = cn[q] + (int)all[2 * q];
+        cmax = std::max(cmax, (int)all[2 * q]);
+        cmin = std::min(cmin, (int)all[2 * q]);
         fail |= all[2 * q + 1] != 0.0;
     }
-    const int NC = c0[nranks];
+    const int NC = cn[nranks];
     if (fail || NC == 0) {
         set_error("AMG: a rank could not aggregate its rows");
         return XFK_ERR_UNSUPPORTED;
     }
+    // replicate small levels (and never leave a rank without rows)
+    rep = NC <= rep_rows || cmin == 0 || l + 2 >= kAmgMaxLevels;
     AMG_CHECK(c0_dev.alloc(nranks + 1));
-    AMG_CHECK(hipMemcpyAsync(c0_dev.p, c0.data(), sizeof(int) * (nranks + 1), hipMemcpyHostToDevice, s));
-    // 2. P rows of the halo nodes: lengths through the node plan, then the
-    //    entries through a plan over the P arrays (a peer's rows for my halo
+    AMG_CHECK(hipMemcpyAsync(c0_dev.p, cn.data(), sizeof(int) * (nranks + 1), hipMemcpyHostToDevice, s));
+    // 2. P rows of the halo nodes: lengths through the level's plan, then the
+    //    entries through a plan over the P arrays (a peer's rows for one halo
     //    range are one contiguous run of its P entries)
     const long long pnnz = A.pnnz;
     const int ncl = n + nh;
-    AMG_CHECK(ebuf.alloc((size_t)ncl));
-    k_row_len_d<<<nb(n), kB, 0, s>>>(n, A.prow.p, ebuf.p);
-    int rc = comm->exchange(*halo, ebuf.p, s);
+    AMG_CHECK(ebuf.alloc((size_t)std::max(1, ncl)));
+    if (n > 0) k_row_len_d<<<nb(n), kB, 0, s>>>(n, A.prow.p, ebuf.p);
+    int rc = comm->exchange(A.plan, ebuf.p, s);
     if (rc != XFK_OK) return rc;
     AMG_CHECK(cnt.alloc((size_t)std::max(n, nh) + 1));
     AMG_CHECK(flag.alloc((size_t)nh + 1));
@@ -1831,15 +1891,16 @@ int Amg::galerkin_dist(hipStream_t s, int st)
     if ((rc = scan_total(*this, s, cnt.p, flag.p, nh, nhe)) != XFK_OK) return rc;   // flag = halo row pointer
     AMG_CHECK(pe_row.alloc((size_t)ncl + 1));
     k_pe_row<<<nb(ncl + 1), kB, 0, s>>>(n, nh, pnnz, A.prow.p, flag.p, pe_row.p);
-    const int nsr = (int)(halo->send.size() + halo->recv.size());
+    const HaloPlan &hp = A.plan;
+    const int nsr = (int)(hp.send.size() + hp.recv.size());
     if ((rc = host_ints(2 * nsr)) != XFK_OK) return rc;
     {
         int k = 0;
-        for (const HaloRange &t : halo->send) {
+        for (const HaloRange &t : hp.send) {
             AMG_CHECK(hipMemcpyAsync(host_big + k++, A.prow.p + t.off, sizeof(int), hipMemcpyDeviceToHost, s));
             AMG_CHECK(hipMemcpyAsync(host_big + k++, A.prow.p + t.off + t.len, sizeof(int), hipMemcpyDeviceToHost, s));
         }
-        for (const HaloRange &r : halo->recv) {
+        for (const HaloRange &r : hp.recv) {
             AMG_CHECK(hipMemcpyAsync(host_big + k++, flag.p + (r.off - n), sizeof(int), hipMemcpyDeviceToHost, s));
             AMG_CHECK(hipMemcpyAsync(host_big + k++, flag.p + (r.off - n) + r.len, sizeof(int),
                                      hipMemcpyDeviceToHost, s));
@@ -1847,43 +1908,36 @@ int Amg::galerkin_dist(hipStream_t s, int st)
         AMG_CHECK(hipStreamSynchronize(s));
     }
     HaloPlan ep;
-    if (std::getenv("XFK_AMG_DEBUG")) {
-        for (const HaloRange &t : halo->send)
-            std::fprintf(stderr, "[amg] rank %d n %d nh %d send peer %d off %d len %d g0 %d\n", rank, n, nh, t.peer,
-                         t.off, t.len, t.g0);
-        for (const HaloRange &r : halo->recv)
-            std::fprintf(stderr, "[amg] rank %d n %d nh %d recv peer %d off %d len %d g0 %d\n", rank, n, nh, r.peer,
-                         r.off, r.len, r.g0);
-    }
     {
         int k = 0;
-        for (const HaloRange &t : halo->send) {
+        for (const HaloRange &t : hp.send) {
             const int b0 = host_big[k++], b1 = host_big[k++];
             ep.send.push_back(HaloRange{t.peer, b0, b1 - b0, t.g0});
         }
-        for (const HaloRange &r : halo->recv) {
+        for (const HaloRange &r : hp.recv) {
             const int b0 = host_big[k++], b1 = host_big[k++];
             ep.recv.push_back(HaloRange{r.peer, (int)pnnz + b0, b1 - b0, r.g0});
         }
     }
     const size_t ne = (size_t)std::max(1LL, pnnz + nhe);
-    // values
     AMG_CHECK(pe_val.alloc(ne));
     if (pnnz > 0)
         AMG_CHECK(hipMemcpyAsync(pe_val.p, A.pval.p, sizeof(double) * pnnz, hipMemcpyDeviceToDevice, s));
     if ((rc = comm->exchange(ep, pe_val.p, s)) != XFK_OK) return rc;
-    // columns: P goes to global coarse numbering (R = P^T is built already)
-    if (pnnz > 0) k_add_int<<<nb(pnnz), kB, 0, s>>>(pnnz, A.pcol.p, c0[rank]);
-    AMG_CHECK(ebuf.alloc(ne));
-    if (pnnz > 0) k_int2dbl<<<nb(pnnz), kB, 0, s>>>(pnnz, A.pcol.p, ebuf.p);
-    if ((rc = comm->exchange(ep, ebuf.p, s)) != XFK_OK) return rc;
+    // columns in global coarse ids (A.pcol itself stays rank-local: the
+    // prolongation reads the own aggregates only)
     AMG_CHECK(pe_col.alloc(ne));
-    if (pnnz > 0)
+    if (pnnz > 0) {
         AMG_CHECK(hipMemcpyAsync(pe_col.p, A.pcol.p, sizeof(int) * pnnz, hipMemcpyDeviceToDevice, s));
+        k_add_int<<<nb(pnnz), kB, 0, s>>>(pnnz, pe_col.p, cn[rank]);
+    }
+    AMG_CHECK(ebuf.alloc(ne));
+    if (pnnz > 0) k_int2dbl<<<nb(pnnz), kB, 0, s>>>(pnnz, pe_col.p, ebuf.p);
+    if ((rc = comm->exchange(ep, ebuf.p, s)) != XFK_OK) return rc;
     if (nhe > 0) k_dbl2int<<<nb(nhe), kB, 0, s>>>(nhe, ebuf.p + pnnz, pe_col.p + pnnz);
     // 3. AP over the full rows, then this rank's coarse rows R (AP)
     long long lnnz = 0;
-    AMG_CHECK(l_row.alloc((size_t)ncmax + 1));
+    AMG_CHECK(l_row.alloc((size_t)cmax + 1));
     {
         SgX XA{A.rowptr, A.col, A.val, ncl, nullptr, nullptr, nullptr};
         SgY YP{pe_row.p, pe_col.p, pe_val.p, nullptr};
@@ -1913,7 +1967,72 @@ int Amg::galerkin_dist(hipStream_t s, int st)
         set_error("AMG: a SpGEMM row exceeds the LDS hash capacity");
         return XFK_ERR_UNSUPPORTED;
     }
-    // 5. all-gather the coarse rows (padded per rank) into the global level 1
+    if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
+    AmgLevel &C = *L[l + 1];
+    if (!rep) {
+        // 5a. stay sharded: own rows with local columns, halo spans per peer
+        const int own0 = cn[rank], own1 = cn[rank + 1];
+        AMG_CHECK(span_dev.alloc(2 * (size_t)nranks));
+        k_fill_int<<<1, 64, 0, s>>>(nranks, span_dev.p, INT_MAX);
+        k_fill_int<<<1, 64, 0, s>>>(nranks, span_dev.p + nranks, -1);
+        if (lnnz > 0)
+            k_peer_span<<<nb(lnnz), kB, 0, s>>>(lnnz, l_col.p, own0, own1, c0_dev.p, nranks, span_dev.p,
+                                                 span_dev.p + nranks);
+        std::vector<int> span(2 * nranks);
+        AMG_CHECK(hipMemcpyAsync(span.data(), span_dev.p, sizeof(int) * 2 * nranks, hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipStreamSynchronize(s));
+        // every rank's spans: what each peer needs from me
+        DBuf<int> sp_all;
+        AMG_CHECK(sp_all.alloc(2 * (size_t)nranks * (nranks + 1)));
+        AMG_CHECK(hipMemcpyAsync(sp_all.p, span.data(), sizeof(int) * 2 * nranks, hipMemcpyHostToDevice, s));
+        if ((rc = comm->allgather_bytes(sp_all.p, sp_all.p + 2 * nranks, sizeof(int) * 2 * nranks, s)) != XFK_OK)
+            return rc;
+        std::vector<int> spa(2 * (size_t)nranks * nranks);
+        AMG_CHECK(hipMemcpyAsync(spa.data(), sp_all.p + 2 * nranks, sizeof(int) * spa.size(), hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipStreamSynchronize(s));
+        HaloPlan cp;
+        std::vector<int> off(nranks, 0);
+        int nhc = 0;
+        for (int q = 0; q < nranks; ++q) {
+            if (q == rank || span[q] > span[nranks + q]) continue;
+            const int len = span[nranks + q] - span[q] + 1;
+            off[q] = nhc;
+            cp.recv.push_back(HaloRange{q, nc + nhc, len, span[q]});
+            nhc += len;
+        }
+        for (int r = 0; r < nranks; ++r) {
+            if (r == rank) continue;
+            const int lo = spa[2 * (size_t)nranks * r + rank], hi = spa[2 * (size_t)nranks * r + nranks + rank];
+            if (lo > hi) continue;
+            cp.send.push_back(HaloRange{r, lo - own0, hi - lo + 1, lo});
+        }
+        AMG_CHECK(map_dev.alloc(nranks));
+        AMG_CHECK(hipMemcpyAsync(map_dev.p, off.data(), sizeof(int) * nranks, hipMemcpyHostToDevice, s));
+        AMG_CHECK(C.rowptr_o.alloc((size_t)nc + 1));
+        AMG_CHECK(C.col_o.alloc((size_t)std::max(1LL, lnnz)));
+        AMG_CHECK(C.val_o.alloc((size_t)std::max(1LL, lnnz)));
+        AMG_CHECK(hipMemcpyAsync(C.rowptr_o.p, l_row.p, sizeof(int) * (nc + 1), hipMemcpyDeviceToDevice, s));
+        if (lnnz > 0) {
+            AMG_CHECK(hipMemcpyAsync(C.col_o.p, l_col.p, sizeof(int) * lnnz, hipMemcpyDeviceToDevice, s));
+            AMG_CHECK(hipMemcpyAsync(C.val_o.p, l_val.p, sizeof(double) * lnnz, hipMemcpyDeviceToDevice, s));
+            k_localize<<<nb(lnnz), kB, 0, s>>>(lnnz, C.col_o.p, own0, own1, nc, c0_dev.p, nranks, span_dev.p,
+                                                map_dev.p);
+        }
+        C.n = nc;
+        C.nnz = lnnz;
+        C.ncol_lim = nc;
+        C.ncol_smooth = nc + nhc;
+        C.rowptr = C.rowptr_o.p;
+        C.col = C.col_o.p;
+        C.val = C.val_o.p;
+        C.dist = true;
+        C.plan = cp;
+        AMG_CHECK(hipStreamSynchronize(s));
+        return XFK_OK;
+    }
+    // 5b. all-gather the coarse rows (padded per rank) into the replicated level
+    c0 = cn;
+    ncmax = cmax;
     AMG_CHECK(s_col.alloc((size_t)nnzmax));
     AMG_CHECK(s_val.alloc((size_t)nnzmax));
     if (lnnz > 0) {
@@ -1926,8 +2045,6 @@ int Amg::galerkin_dist(hipStream_t s, int st)
     if ((rc = comm->allgather_bytes(l_row.p, g_row.p, sizeof(int) * (ncmax + 1), s)) != XFK_OK) return rc;
     if ((rc = comm->allgather_bytes(s_col.p, g_col.p, sizeof(int) * nnzmax, s)) != XFK_OK) return rc;
     if ((rc = comm->allgather(s_val.p, g_val.p, (size_t)nnzmax, s)) != XFK_OK) return rc;
-    if ((int)L.size() <= 1) L.emplace_back(new AmgLevel());
-    AmgLevel &C = *L[1];
     const long long NNZ = e0[nranks];
     AMG_CHECK(C.rowptr_o.alloc((size_t)NC + 1));
     AMG_CHECK(C.col_o.alloc((size_t)std::max(1LL, NNZ)));
@@ -1950,6 +2067,8 @@ int Amg::galerkin_dist(hipStream_t s, int st)
     C.rowptr = C.rowptr_o.p;
     C.col = C.col_o.p;
     C.val = C.val_o.p;
+    C.dist = false;
+    C.plan = HaloPlan();
     if (std::getenv("XFK_AMG_DEBUG") && rank == 0) {   // symmetry of the gathered A_1
         std::vector<int> hr(NC + 1), hc(NNZ);
         std::vector<double> hv(NNZ);
@@ -2081,40 +2200,58 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     return cur;
 }
 
+// sharded level l: every sweep reads the peers' halo values of the iterate;
+// the restriction / prolongation stay rank-local (P rows reference the own
+// aggregates only).  Returns the buffer holding the result (`out` if given).
+double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const int *done, int &rc)
+{
+    AmgLevel &A = *L[l];
+    const unsigned long long *rh = rho.p + 2 * l;
+    double *cur = A.xa.p, *oth = A.xb.p;
+    rc = XFK_OK;
+    if (A.n > 0) k_jacobi_first<<<nb(A.n), kB, 0, s>>>(A.n, rh, A.dinv.p, b, cur, done);
+    for (int k = 1; k < sweeps; ++k) {
+        if ((rc = comm->exchange(A.plan, cur, s)) != XFK_OK) return nullptr;
+        launch_smooth(s, kSweep, l, A, rh, b, cur, oth, nullptr, done);
+        std::swap(cur, oth);
+    }
+    if ((rc = comm->exchange(A.plan, cur, s)) != XFK_OK) return nullptr;
+    launch_smooth(s, kResid, l, A, rh, b, cur, nullptr, A.r.p, done);
+    AmgLevel &C = *L[l + 1];
+    const int GR = lanes_for(A.nc > 0 ? (double)A.pnnz / A.nc : 1.0);
+    const double *xc;
+    if (C.dist) {
+        launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false, GR, done);
+        xc = vc_dist(s, l + 1, C.b.p, nullptr, done, rc);
+        if (rc != XFK_OK) return nullptr;
+    } else {
+        // the replicated levels: gather the global right-hand side, solve the
+        // same coarse problem on every rank, read the own aggregates back
+        launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, cb_loc.p, false, GR, done);
+        if ((rc = comm->allgather(cb_loc.p, cb_all.p, (size_t)ncmax, s)) != XFK_OK) return nullptr;
+        k_unpad<<<nb(C.n), kB, 0, s>>>(C.n, nranks, c0_dev.p, cb_all.p, ncmax, C.b.p, done);
+        xc = vcycle_level(*this, s, l + 1, C.b.p, nullptr, done) + c0[rank];
+    }
+    if (A.n > 0) launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)A.pnnz / A.n), done);
+    for (int k = 0; k < sweeps; ++k) {
+        if ((rc = comm->exchange(A.plan, cur, s)) != XFK_OK) return nullptr;
+        double *nx = (k == sweeps - 1 && out) ? out : oth;
+        launch_smooth(s, kSweep, l, A, rh, b, cur, nx, nullptr, done);
+        oth = cur;
+        cur = nx;
+    }
+    return cur;
+}
+
 int Amg::vcycle(hipStream_t s, const double *r, double *u, const int *done)
 {
     if (!dist) {
         vcycle_level(*this, s, 0, r, u, done);
         return XFK_OK;
     }
-    // sharded level 0: every sweep reads the peers' halo values of the iterate
-    AmgLevel &A = *L[0];
-    const unsigned long long *rh = rho.p;
-    double *cur = A.xa.p, *oth = A.xb.p;
-    int rc;
-    k_jacobi_first<<<nb(A.n), kB, 0, s>>>(A.n, rh, A.dinv.p, r, cur, done);
-    for (int k = 1; k < sweeps; ++k) {
-        if ((rc = comm->exchange(*halo, cur, s)) != XFK_OK) return rc;
-        launch_smooth(s, kSweep, 0, A, rh, r, cur, oth, nullptr, done);
-        std::swap(cur, oth);
-    }
-    if ((rc = comm->exchange(*halo, cur, s)) != XFK_OK) return rc;
-    launch_smooth(s, kResid, 0, A, rh, r, cur, nullptr, A.r.p, done);
-    // restriction to the own aggregates, gathered into the global level 1
-    launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, cb_loc.p, false,
-              lanes_for(A.nc > 0 ? (double)A.pnnz / A.nc : 1.0), done);
-    if ((rc = comm->allgather(cb_loc.p, cb_all.p, (size_t)ncmax, s)) != XFK_OK) return rc;
-    AmgLevel &C = *L[1];
-    k_unpad<<<nb(C.n), kB, 0, s>>>(C.n, nranks, c0_dev.p, cb_all.p, ncmax, C.b.p, done);
-    const double *xc = vcycle_level(*this, s, 1, C.b.p, nullptr, done);
-    launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)A.pnnz / A.n), done);
-    for (int k = 0; k < sweeps; ++k) {
-        if ((rc = comm->exchange(*halo, cur, s)) != XFK_OK) return rc;
-        double *nx = (k == sweeps - 1) ? u : oth;
-        launch_smooth(s, kSweep, 0, A, rh, r, cur, nx, nullptr, done);
-        oth = cur;
-        cur = nx;
-    }
+    int rc = XFK_OK;
+    vc_dist(s, 0, r, u, done, rc);
+    if (rc != XFK_OK) return rc;
     AMG_CHECK(hipGetLastError());
     return XFK_OK;
 }

@@ -543,6 +543,7 @@ static int amg_setup(xfk_problem *P)
     P->amg->theta = P->amg_theta;
     P->amg->sweeps = P->amg_sweeps;
     P->amg->omega = P->amg_omega;
+    P->amg->rep_rows = P->amg_replicate;
     hipEvent_t e0, e1;
     XFK_CHECK(hipEventCreate(&e0));
     XFK_CHECK(hipEventCreate(&e1));
@@ -1315,6 +1316,11 @@ int xfk_set_option(xfk_problem *P, int option, double value)
     case XFK_OPT_AMG_OMEGA:
         XFK_REQUIRE(value > 0.0 && value < 2.0, XFK_ERR_ARG, "AMG Jacobi weight factor must be in (0, 2)");
         P->amg_omega = value;
+        return XFK_OK;
+    case XFK_OPT_AMG_REPLICATE:
+        XFK_REQUIRE(value >= 0 && value <= 2e9 && value == (int)value, XFK_ERR_ARG,
+                    "AMG replication threshold must be a row count");
+        P->amg_replicate = (int)value;
         return XFK_OK;
     default:
         set_error("unknown option");

@@ -278,6 +278,7 @@ struct xfk_problem {
     int amg_sweeps = 1;
     double amg_theta = 0.08;
     double amg_omega = 1.75;
+    int amg_replicate = 250000;
     xfk::Amg *amg = nullptr;         // hierarchy of the current matrix (xfk_amg.hip)
     int pc_used = XFK_PRECOND_JACOBI;  // preconditioner of the running solve
 
