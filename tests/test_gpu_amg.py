@@ -195,6 +195,22 @@ def test_precond_option_validation():
     P.close()
 
 
+@pytest.mark.parametrize("reuse", [False, True])
+def test_newton_hierarchy_reuse(reuse):
+    """Later Newton iterations keep the hierarchy of the first (fine-level
+    smoother refreshed) or rebuild it: both reach the oracle's answer within
+    the solver tolerance; reuse builds it once."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(32, nonlinear=True))
+    Ao, st, _ = oracle.solve(pr, mesh)
+    P = kernels.Static2DProblem(**kw, amg_reuse=reuse)
+    r = P.solve()
+    A = P.solution()
+    tol = solver_tolerance(TOL_NONLINEAR, Ao, P)
+    P.close()
+    assert r["newton_iters"] >= 3
+    assert rel_err(A, Ao) <= tol
+
+
 @pytest.mark.parametrize("omega", [1.0, 1.9])
 def test_jacobi_weight_factor(omega):
     """Any weight factor in (0, 2) gives an SPD cycle: same answer, within the

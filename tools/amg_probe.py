@@ -14,6 +14,7 @@ cells = [int(a) for a in sys.argv[1:] if not a.startswith("-")] or [100, 1000]
 nonlin = "--nonlinear" in sys.argv
 sweeps = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--sweeps=")] or [2]
 omegas = [float(a.split("=")[1]) for a in sys.argv if a.startswith("--omega=")] or [None]
+reuse = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--reuse=")]
 nojac = "--no-jacobi" in sys.argv
 for n in cells:
     kw = synth.magnetostatic(n, nonlinear=nonlin)
@@ -26,6 +27,8 @@ for n in cells:
         else:
             k, _, w = pc[3:].partition("w")
             opt = dict(precond="amg", amg_sweeps=int(k), amg_omega=float(w) if w else None)
+            if reuse:
+                opt["amg_reuse"] = bool(reuse[0])
         P = kernels.Static2DProblem(device=0, **opt, **kw)
         r = P.solve()
         t0 = time.perf_counter()

@@ -143,6 +143,9 @@ struct Amg {
     // u = M^-1 r (owned rows of level 0); kernels return early once *done != 0.
     // Sharded: collective (halo exchanges, one all-gather).
     int vcycle(hipStream_t s, const double *r, double *u, const int *done);
+    // New values in the level-0 matrix (same pattern): refresh the fine-level
+    // smoother (D^-1, rho_A); the coarse levels are kept
+    int refresh(hipStream_t s);
 
   private:
     int init(hipStream_t s);

@@ -2243,6 +2243,26 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
     return cur;
 }
 
+int Amg::refresh(hipStream_t s)
+{
+    AmgLevel &A = *L[0];
+    const int n = A.n;
+    AMG_CHECK(absd.alloc(std::max(1, n)));
+    AMG_CHECK(dfinv.alloc(std::max(1, n)));
+    AMG_CHECK(wF.alloc(std::max(1, n)));
+    AMG_CHECK(cnt.alloc((size_t)n + 1));
+    AMG_CHECK(sflag.alloc((size_t)std::max(1LL, A.nnz)));
+    AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb(n))));
+    if (n > 0) {
+        k_amg_diag<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
+        k_amg_strength<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
+                                            dfinv.p, wF.p, rho_part.p);
+        k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, omega, rho.p);
+    }
+    AMG_CHECK(hipGetLastError());
+    return XFK_OK;
+}
+
 int Amg::vcycle(hipStream_t s, const double *r, double *u, const int *done)
 {
     if (!dist) {

@@ -536,9 +536,22 @@ static int allreduce_partials(xfk_problem *P, int narrays)
 // back to Jacobi for this solve when the hierarchy cannot be built
 static int amg_setup(xfk_problem *P)
 {
+    const bool was_amg = P->pc_used == XFK_PRECOND_AMG;
     P->pc_used = XFK_PRECOND_JACOBI;
+    P->amg_fresh = false;
     if (P->precond != XFK_PRECOND_AMG) return XFK_OK;
     hipStream_t s = P->stream;
+    // later Newton iterations: same pattern, new values -> keep the hierarchy
+    // while the PCG stays within 2x the iterations of the last fresh build
+    // (the decision reads iteration counts every rank shares)
+    if (P->amg_reuse && P->amg_reusable && was_amg && P->amg &&
+        P->amg_last_iters <= std::max(2 * P->amg_fresh_iters, P->amg_fresh_iters + 8)) {
+        int rc = P->amg->refresh(s);
+        if (rc != XFK_OK) return rc;
+        P->pc_used = XFK_PRECOND_AMG;
+        return XFK_OK;
+    }
+    P->amg_reusable = false;
     if (!P->amg) P->amg = new Amg();
     P->amg->theta = P->amg_theta;
     P->amg->sweeps = P->amg_sweeps;
@@ -566,6 +579,8 @@ static int amg_setup(xfk_problem *P)
     if (rc2 != XFK_OK) return rc2;
     if (ok == 0.0) {
         P->pc_used = XFK_PRECOND_AMG;
+        P->amg_fresh = true;
+        P->amg_reusable = true;
         P->last.amg_levels = P->amg->stats.levels;
         P->last.amg_op_complexity = P->amg->stats.op_complexity;
     }
@@ -1148,6 +1163,8 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     int Iter = 0;
     bool LinearFlag = !P->any_nonlinear;
     const long long cap = std::max<long long>(100000, 20LL * N);
+    P->amg_reusable = false;   // a hierarchy is reused only inside one solve
+    P->pc_used = XFK_PRECOND_JACOBI;
     for (;;) {
         XFK_CHECK(hipEventRecord(e0, s));
         if (Iter > 0 && (rc = exchange(P, P->V.p)) != XFK_OK) return rc;   // halo of V for the element B
@@ -1165,6 +1182,8 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
         R.ms_solve += ms;
         R.cg_iters += P->pcg_host->iters;
         R.final_er = P->pcg_host->er;
+        P->amg_last_iters = P->pcg_host->iters;
+        if (P->amg_fresh) P->amg_fresh_iters = P->pcg_host->iters;
 
         if (!LinearFlag) {
             launch_newton_res(s, N, P->V.p, P->Vold.p, P->partials.p, P->counters.p + 3, P->nws.p);
@@ -1321,6 +1340,10 @@ int xfk_set_option(xfk_problem *P, int option, double value)
         XFK_REQUIRE(value >= 0 && value <= 2e9 && value == (int)value, XFK_ERR_ARG,
                     "AMG replication threshold must be a row count");
         P->amg_replicate = (int)value;
+        return XFK_OK;
+    case XFK_OPT_AMG_REUSE:
+        XFK_REQUIRE(value == 0 || value == 1, XFK_ERR_ARG, "AMG reuse is 0 or 1");
+        P->amg_reuse = (int)value;
         return XFK_OK;
     default:
         set_error("unknown option");

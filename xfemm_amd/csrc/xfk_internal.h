@@ -279,6 +279,10 @@ struct xfk_problem {
     double amg_theta = 0.08;
     double amg_omega = 1.75;
     int amg_replicate = 250000;
+    int amg_reuse = 1;
+    bool amg_reusable = false;        // the hierarchy belongs to this solve's matrix pattern
+    bool amg_fresh = false;           // built from scratch for the running PCG solve
+    long long amg_fresh_iters = 0, amg_last_iters = 0;
     xfk::Amg *amg = nullptr;         // hierarchy of the current matrix (xfk_amg.hip)
     int pc_used = XFK_PRECOND_JACOBI;  // preconditioner of the running solve
 

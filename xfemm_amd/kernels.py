@@ -30,6 +30,7 @@ XFK_OPT_AMG_SWEEPS = 2
 XFK_OPT_AMG_THETA = 3
 XFK_OPT_AMG_OMEGA = 4
 XFK_OPT_AMG_REPLICATE = 5
+XFK_OPT_AMG_REUSE = 6
 
 # every symbol include/xfemm_kernels.h declares
 EXPORTED = (
@@ -245,7 +246,7 @@ class Static2DProblem:
                  marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0,
                  device=0, comm: Optional["Comm"] = None, precond: str = "amg", amg_sweeps: Optional[int] = None,
                  amg_theta: Optional[float] = None, frequency: float = 0.0, amg_omega: Optional[float] = None,
-                 amg_replicate: Optional[int] = None):
+                 amg_replicate: Optional[int] = None, amg_reuse: Optional[bool] = None):
         """comm: shard the mesh by row blocks over this communicator (every rank
         passes the same global problem; solve() and solution() are collective).
         precond: "amg" (smoothed-aggregation V-cycle, default) or "jacobi"."""
@@ -274,6 +275,8 @@ class Static2DProblem:
             self.set_option(XFK_OPT_AMG_OMEGA, amg_omega)
         if amg_replicate is not None:
             self.set_option(XFK_OPT_AMG_REPLICATE, amg_replicate)
+        if amg_reuse is not None:
+            self.set_option(XFK_OPT_AMG_REUSE, int(bool(amg_reuse)))
         self.n_rows = self.dist_info()["n_own"] if comm is not None else self.n_nodes
         self.result: Optional[Result] = None
 
