@@ -1109,12 +1109,15 @@ __global__ void __launch_bounds__(256) k_bgj_row(int k, int ld, double *__restri
 
 // M_ij -= C_i T_kj (i, j != k) and M_ik = -C_i D (i != k), C_i the snapshot
 // of the old column block
+// jsel >= 0: only block column jsel (grid nbk); else every block column but
+// jskip (grid nbk^2; -1: all)
 __global__ void __launch_bounds__(256) k_bgj_update(int k, int nbk, int ld, double *__restrict__ M,
                                                     const double *__restrict__ D, const double *__restrict__ Trow,
-                                                    const double *__restrict__ Csnap)
+                                                    const double *__restrict__ Csnap, int jsel, int jskip)
 {
-    const int i = blockIdx.x / nbk, j = blockIdx.x % nbk;
-    if (i == k) return;
+    const int i = jsel >= 0 ? (int)blockIdx.x : (int)blockIdx.x / nbk;
+    const int j = jsel >= 0 ? jsel : (int)blockIdx.x % nbk;
+    if (i == k || j == jskip) return;
     __shared__ double Xs[kBj * kXs], Ys[kBj * kYs];
     bgj_load<kXs>(Xs, Csnap + (size_t)i * kBj * kBj, kBj);
     bgj_load<kYs>(Ys, j == k ? D : Trow + (size_t)j * kBj * kBj, kBj);
@@ -1708,17 +1711,22 @@ int Amg::build(hipStream_t s, int l0)
         const int nbk = (C.n + kBj - 1) / kBj, ld = nbk * kBj;
         cinv_ld = ld;
         AMG_CHECK(cinv.alloc((size_t)ld * ld));
-        AMG_CHECK(bgj_tmp.alloc(2 * (size_t)nbk * kBj * kBj + kBj * kBj + 1 + ld));
-        double *Trow = bgj_tmp.p, *Tcol = Trow + (size_t)nbk * kBj * kBj, *D = Tcol + (size_t)nbk * kBj * kBj;
-        double *maxd = D + kBj * kBj, *sc = maxd + 1;
+        AMG_CHECK(bgj_tmp.alloc(2 * (size_t)nbk * kBj * kBj + 2 * kBj * kBj + 1 + ld));
+        double *Trow = bgj_tmp.p, *Tcol = Trow + (size_t)nbk * kBj * kBj, *Dbuf = Tcol + (size_t)nbk * kBj * kBj;
+        double *maxd = Dbuf + 2 * kBj * kBj, *sc = maxd + 1;
         AMG_CHECK(hipMemsetAsync(cinv.p, 0, sizeof(double) * (size_t)ld * ld, s));
         k_dense_dscale<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, sc);
         k_dense_scatter<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, sc, cinv.p);
         k_dense_maxdiag<<<1, 1024, 0, s>>>(C.n, ld, cinv.p, maxd);
+        // (a lookahead variant -- block column k+1 first, its pivot block
+        // inverted on a second stream during the rest of the update -- was
+        // measured slower: the two cross-stream waits cost ~15 us per step,
+        // more than the 25 us pivot-block inversion it hides)
         for (int k = 0; k < nbk; ++k) {
+            double *D = Dbuf;
             k_bgj_diag<<<1, 256, 0, s>>>(k, ld, cinv.p, maxd, D);
             k_bgj_row<<<nbk, 256, 0, s>>>(k, ld, cinv.p, D, Trow, Tcol);
-            if (nbk > 1) k_bgj_update<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, D, Trow, Tcol);
+            if (nbk > 1) k_bgj_update<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, D, Trow, Tcol, -1, -1);
         }
         k_dense_unscale<<<(unsigned)(((size_t)ld * ld / 2 + 255) / 256), 256, 0, s>>>(ld, cinv.p, sc);
     }
