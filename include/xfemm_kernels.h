@@ -55,6 +55,7 @@ typedef struct {
     int in_circuit;             /* -1 = none */
     double mag_dir;             /* magnetisation direction, degrees */
     int is_wound;
+    int is_external;            /* axisymmetric: conformally mapped exterior region ([IsExternal]) */
 } xfk_label_desc;
 
 /* CMBoundaryProp (CBoundaryProp.h). */
@@ -94,7 +95,12 @@ typedef struct {
     int length_units;           /* femm::LengthUnit */
     int coords;                 /* 0 cartesian, 1 polar */
     double relax;               /* FSolver::Relax, 1.0 */
+    int problem_type;           /* [ProblemType]: XFK_PLANAR (Static2D) or XFK_AXISYMMETRIC
+                                   (FSolver::StaticAxisymmetric, staticaxi.cpp:45-794: x is r, y is z) */
+    double ext_zo, ext_ro, ext_ri;   /* [extZo] [extRo] [extRi]: axisymmetric exterior region, user units */
 } xfk_problem_desc;
+
+enum { XFK_PLANAR = 0, XFK_AXISYMMETRIC = 1 };
 
 typedef struct {
     int newton_iters;           /* linear solves performed */

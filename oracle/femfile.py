@@ -143,6 +143,9 @@ class FemProblem:
     labels: List[BlockLabel] = field(default_factory=list)
     NumCircPropsOrig: int = 0
     Relax: float = 1.0
+    extZo: float = 0.0          # axisymmetric exterior region (feasolver.cpp:306-326)
+    extRo: float = 0.0
+    extRi: float = 0.0
 
 
 # --------------------------------------------------------------------------
@@ -423,7 +426,13 @@ def parse_fem(path: str) -> FemProblem:
                 pr.ProblemType = 0
             if u == "axisymmetric":
                 pr.ProblemType = 1
-        elif tok in ("[extzo]", "[extro]", "[extri]", "[forcemaxmesh]", "[dosmartmesh]"):
+        elif tok == "[extzo]":
+            pr.extZo = _stod(r)
+        elif tok == "[extro]":
+            pr.extRo = _stod(r)
+        elif tok == "[extri]":
+            pr.extRi = _stod(r)
+        elif tok in ("[forcemaxmesh]", "[dosmartmesh]"):
             pass
         elif tok == "[comment]":
             pr.Comment = _parse_string(r)

@@ -34,7 +34,7 @@ class OraBlock(C.Structure):
 
 
 class OraLabel(C.Structure):
-    _fields_ = [("InCircuit", C.c_int), ("MagDir", C.c_double), ("bIsWound", C.c_int)]
+    _fields_ = [("InCircuit", C.c_int), ("MagDir", C.c_double), ("bIsWound", C.c_int), ("IsExternal", C.c_int)]
 
 
 class OraLine(C.Structure):
@@ -62,7 +62,8 @@ class OraProblem(C.Structure):
                 ("n_circs", C.c_int), ("circs", C.POINTER(OraCirc)),
                 ("n_pbc", C.c_int), ("pbc", iptr),
                 ("precision", C.c_double), ("length_units", C.c_int), ("coords", C.c_int),
-                ("bandwidth", C.c_int), ("relax", C.c_double)]
+                ("bandwidth", C.c_int), ("relax", C.c_double),
+                ("axisymmetric", C.c_int), ("ext_ro", C.c_double), ("ext_ri", C.c_double), ("ext_zo", C.c_double)]
 
 
 class OraStats(C.Structure):
@@ -196,6 +197,7 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
         if lb.MagDirFctn:
             raise NotImplementedError("Lua magnetisation-direction functions are out of scope")
         labels[k].InCircuit, labels[k].MagDir, labels[k].bIsWound = lb.InCircuit, lb.MagDir, int(lb.bIsWound)
+        labels[k].IsExternal = int(lb.IsExternal)
     lines = (OraLine * max(1, len(pr.bdrys)))()
     for k, bd in enumerate(pr.bdrys):
         l = lines[k]
@@ -220,6 +222,8 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
     P.pbc = keep.i(mesh.pbc.reshape(-1) if len(mesh.pbc) else np.zeros(3, np.int32))
     P.precision, P.length_units, P.coords = pr.Precision, pr.LengthUnits, pr.Coords
     P.bandwidth, P.relax = mesh.bandwidth, pr.Relax
+    P.axisymmetric = int(pr.ProblemType == 1)
+    P.ext_ro, P.ext_ri, P.ext_zo = pr.extRo, pr.extRi, pr.extZo
     keep.items.extend([blocks, labels, lines, points, circs])
     return P, keep, circs
 

@@ -349,7 +349,12 @@ static void ora_circuits(ora_problem *pr)
                 if (pr->labels[lb].bIsWound) Cduct = 0;
                 int ic = pr->labels[lb].InCircuit;
                 CI1[ic] += a;
-                CI2[ic] += a * Cduct;
+                if (pr->axisymmetric) {   /* staticaxi.cpp:96-104 */
+                    double r = (pr->x[n[0]] + pr->x[n[1]] + pr->x[n[2]]) / 3.;
+                    CI2[ic] += 100. * a * Cduct / r;
+                } else {
+                    CI2[ic] += a * Cduct;
+                }
                 CI3[ic] += bp->J_re * a * 100.;
             }
         }
@@ -613,6 +618,306 @@ static void ora_assemble(ora_problem *pr, const ora_linprob_ops *ops, void *L, i
     *LinearFlag_io = LinearFlag;
 }
 
+/* one Newton iteration of FSolver::StaticAxisymmetric (staticaxi.cpp:146-697):
+ * x is r, y is z (cm) */
+static void ora_assemble_axi(ora_problem *pr, const ora_linprob_ops *ops, void *L, int Iter,
+                             double *mu1, double *mu2, double *v12, int *LinearFlag_io)
+{
+    const double c = ORA_PI * 4.e-05;
+    const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
+    const int NN = pr->n_nodes, NE = pr->n_elems;
+    const double extRo = pr->ext_ro * units[pr->length_units];   /* staticaxi.cpp:70-72 */
+    const double extRi = pr->ext_ri * units[pr->length_units];
+    const double extZo = pr->ext_zo * units[pr->length_units];
+    int LinearFlag = *LinearFlag_io;
+    double *b = ops->b(L);
+    double *Vv = ops->V(L);
+    const double *X = pr->x, *Y = pr->y;
+
+    for (int i = 0; i < NE; i++) {
+        double Me[3][3], be[3], Mx[3][3], My[3][3], Mxy[3][3], Mn[3][3];
+        double l[3], p[3], q[3], g[3], v[3], u[3], rn[3];
+        int n[3];
+        double a, K, t = 0., r, B, mu, dv, R, a_hat, vol, R_hat = 0.;
+        for (int j = 0; j < 3; j++) {
+            for (int k = 0; k < 3; k++) {
+                Me[j][k] = 0.; Mx[j][k] = 0.; My[j][k] = 0.; Mxy[j][k] = 0.; Mn[j][k] = 0.;
+            }
+            be[j] = 0.;
+        }
+        for (int k = 0; k < 3; k++) {
+            n[k] = pr->p[3 * i + k];
+            rn[k] = X[n[k]];
+        }
+        p[0] = Y[n[1]] - Y[n[2]];
+        p[1] = Y[n[2]] - Y[n[0]];
+        p[2] = Y[n[0]] - Y[n[1]];
+        q[0] = X[n[2]] - X[n[1]];
+        q[1] = X[n[0]] - X[n[2]];
+        q[2] = X[n[1]] - X[n[0]];
+        g[0] = (X[n[2]] + X[n[1]]) / 2.;
+        g[1] = (X[n[0]] + X[n[2]]) / 2.;
+        g[2] = (X[n[1]] + X[n[0]]) / 2.;
+        for (int j = 0, k = 1; j < 3; k++, j++) {
+            if (k == 3) k = 0;
+            l[j] = sqrt(pow(X[n[k]] - X[n[j]], 2.) + pow(Y[n[k]] - Y[n[j]], 2.));
+        }
+        a = (p[0] * q[1] - p[1] * q[0]) / 2.;
+        R = (X[n[0]] + X[n[1]] + X[n[2]]) / 3.;
+        a_hat = 0;
+        for (int j = 0; j < 3; j++) a_hat += (rn[j] * rn[j] * p[j] / (4. * R));
+        vol = 2. * R * a_hat;
+
+        /* R_hat: the element's 1/r-weighted mean radius (staticaxi.cpp:208-254) */
+        int flag = 0;
+        for (int j = 0; j < 3; j++)
+            if (rn[j] < 1.e-06) flag++;
+        if (flag == 2) {
+            R_hat = R;
+        } else if (flag == 1) {
+            if (rn[0] < 1.e-06) {
+                if (fabs(rn[1] - rn[2]) < 1.e-06) R_hat = rn[2] / 2.;
+                else R_hat = (rn[1] - rn[2]) / (2. * log(rn[1]) - 2. * log(rn[2]));
+            }
+            if (rn[1] < 1.e-06) {
+                if (fabs(rn[2] - rn[0]) < 1.e-06) R_hat = rn[0] / 2.;
+                else R_hat = (rn[2] - rn[0]) / (2. * log(rn[2]) - 2. * log(rn[0]));
+            }
+            if (rn[2] < 1.e-06) {
+                if (fabs(rn[0] - rn[1]) < 1.e-06) R_hat = rn[1] / 2.;
+                else R_hat = (rn[0] - rn[1]) / (2. * log(rn[0]) - 2. * log(rn[1]));
+            }
+        } else {
+            if (fabs(q[0]) < 1.e-06)
+                R_hat = (q[1] * q[1]) / (2. * (-q[1] + rn[0] * log(rn[0] / rn[2])));
+            else if (fabs(q[1]) < 1.e-06)
+                R_hat = (q[2] * q[2]) / (2. * (-q[2] + rn[1] * log(rn[1] / rn[0])));
+            else if (fabs(q[2]) < 1.e-06)
+                R_hat = (q[0] * q[0]) / (2. * (-q[0] + rn[2] * log(rn[2] / rn[1])));
+            else
+                R_hat = -(q[0] * q[1] * q[2]) /
+                        (2. * (q[0] * rn[0] * log(rn[0]) + q[1] * rn[1] * log(rn[1]) + q[2] * rn[2] * log(rn[2])));
+        }
+
+        /* Mr, Mz, Mrz (staticaxi.cpp:256-296) */
+        K = (-1. / (2. * a_hat * R));
+        for (int j = 0; j < 3; j++)
+            for (int k = j; k < 3; k++) Mx[j][k] += K * p[j] * rn[j] * p[k] * rn[k];
+        for (int j = 0; j < 3; j++)
+            if (rn[j] < 1.e-06) Mx[j][j] += Mx[0][0] + Mx[1][1] + Mx[2][2];
+        K = (-1. / (2. * a_hat * R_hat));
+        for (int j = 0; j < 3; j++)
+            for (int k = j; k < 3; k++) My[j][k] += K * (q[j] * rn[j]) * (q[k] * rn[k]) * (g[j] / R) * (g[k] / R);
+        for (int j = 0; j < 3; j++)
+            for (int k = j; k < 3; k++)
+                Mxy[j][k] += K * ((q[j] * rn[j]) * (g[j] / R)) * (p[k] * rn[k]) +
+                             K * ((q[k] * rn[k]) * (g[k] / R)) * (p[j] * rn[j]);
+        Mx[1][0] = Mx[0][1]; Mx[2][0] = Mx[0][2]; Mx[2][1] = Mx[1][2];
+        My[1][0] = My[0][1]; My[2][0] = My[0][2]; My[2][1] = My[1][2];
+        Mxy[1][0] = Mxy[0][1]; Mxy[2][0] = Mxy[0][2]; Mxy[2][1] = Mxy[1][2];
+
+        /* mixed boundary conditions, r-weighted (staticaxi.cpp:298-320) */
+        for (int j = 0; j < 3; j++) {
+            int ej = pr->e[3 * i + j];
+            if (ej >= 0 && pr->lines[ej].BdryFormat == 2) {
+                int k = j + 1;
+                if (k == 3) k = 0;
+                r = (X[n[j]] + X[n[k]]) / 2.;
+                K = -0.0001 * c * 2. * r * pr->lines[ej].c0 * l[j] / 6.;
+                Me[j][j] += K * 2.;
+                Me[k][k] += K * 2.;
+                Me[j][k] += K;
+                Me[k][j] += K;
+                K = (pr->lines[ej].c1 * l[j] / 2.) * 0.0001 * 2 * r;
+                be[j] += K;
+                be[k] += K;
+            }
+        }
+
+        const ora_label *lab = &pr->labels[pr->lbl[i]];
+        const ora_block *bp = &pr->blocks[pr->blk[i]];
+        /* source current density (staticaxi.cpp:322-337) */
+        for (int j = 0; j < 3; j++) {
+            if (lab->InCircuit >= 0) {
+                const ora_circ *cp = &pr->circs[lab->InCircuit];
+                if (cp->Case == 1) t = cp->J;
+                if (cp->Case == 0) t = -100. * cp->dV * bp->Cduct / R;
+            } else {
+                t = 0;
+            }
+            K = -2. * R * (bp->J_re + t) * a / 3.;
+            be[j] += K;
+        }
+        /* magnetization, r-weighted (staticaxi.cpp:339-407; no Lua directions) */
+        t = lab->MagDir;
+        for (int j = 0; j < 3; j++) {
+            int k = j + 1;
+            if (k == 3) k = 0;
+            r = (X[n[j]] + X[n[k]]) / 2.;
+            K = -0.0001 * r * bp->H_c *
+                (cos(t * ORA_PI / 180.) * (X[n[k]] - X[n[j]]) + sin(t * ORA_PI / 180.) * (Y[n[k]] - Y[n[j]]));
+            be[j] += K;
+            be[k] += K;
+        }
+
+        /* permeability (staticaxi.cpp:409-623; no incremental problems) */
+        if (Iter == 0) {
+            if (bp->LamType == 0) {
+                mu = bp->LamFill;
+                mu1[i] = bp->mu_x * mu;
+                mu2[i] = bp->mu_y * mu;
+            }
+            if (bp->LamType == 1) {
+                mu = bp->LamFill;
+                K = bp->mu_x;
+                mu1[i] = K * mu + (1. - mu);
+                mu2[i] = K / (mu + K * (1. - mu));
+            }
+            if (bp->LamType == 2) {
+                mu = bp->LamFill;
+                K = bp->mu_y;
+                mu1[i] = K * mu + (1. - mu);
+                mu2[i] = K / (mu + K * (1. - mu));
+            }
+            if (bp->LamType > 2) { mu1[i] = 1; mu2[i] = 1; }
+            if (bp->BHpoints != 0) LinearFlag = 0;
+        } else {
+            if ((bp->LamType == 0) && (mu1[i] == mu2[i]) && (bp->BHpoints > 0)) {
+                /* B directly from the energy */
+                v[0] = 0; v[1] = 0; v[2] = 0;
+                for (int j = 0; j < 3; j++)
+                    for (int w = 0; w < 3; w++) v[j] += (Mx[j][w] + My[j][w]) * Vv[n[w]];
+                dv = 0;
+                for (int j = 0; j < 3; j++) dv += Vv[n[j]] * v[j];
+                dv *= (10000. * c * c / vol);
+                B = sqrt(fabs(dv));
+                ora_get_bh_props(bp, B, &mu, &dv);
+                mu = 1. / (ORA_MUO * mu);
+                mu1[i] = mu;
+                mu2[i] = mu;
+                for (int j = 0; j < 3; j++) {
+                    v[j] = 0;
+                    for (int w = 0; w < 3; w++) v[j] += (Mx[j][w] + My[j][w]) * Vv[n[w]];
+                }
+                K = -200. * c * c * c * dv / vol;
+                for (int j = 0; j < 3; j++)
+                    for (int w = 0; w < 3; w++) Mn[j][w] = K * v[j] * v[w];
+            }
+            if ((bp->LamType == 1) && (bp->BHpoints > 0)) {
+                t = bp->LamFill;
+                v[0] = 0; v[1] = 0; v[2] = 0;
+                for (int j = 0; j < 3; j++)
+                    for (int w = 0; w < 3; w++) v[j] += (Mx[j][w] + My[j][w] / (t * t)) * Vv[n[w]];
+                dv = 0;
+                for (int j = 0; j < 3; j++) dv += Vv[n[j]] * v[j];
+                dv *= (10000. * c * c / vol);
+                B = sqrt(fabs(dv));
+                ora_get_bh_props(bp, B, &mu, &dv);
+                mu = 1. / (ORA_MUO * mu);
+                mu1[i] = mu * t;
+                mu2[i] = mu / (t + mu * (1. - t));
+                for (int j = 0; j < 3; j++) {
+                    v[j] = 0; u[j] = 0;
+                    for (int w = 0; w < 3; w++) {
+                        v[j] += (My[j][w] / t + Mx[j][w]) * Vv[n[w]];
+                        u[j] += (My[j][w] / t + t * Mx[j][w]) * Vv[n[w]];
+                    }
+                }
+                K = -100. * c * c * c * dv / (vol);
+                for (int j = 0; j < 3; j++)
+                    for (int w = 0; w < 3; w++) Mn[j][w] = K * (v[j] * u[w] + v[w] * u[j]);
+            }
+            if ((bp->LamType == 2) && (bp->BHpoints > 0)) {
+                t = bp->LamFill;
+                v[0] = 0; v[1] = 0; v[2] = 0;
+                for (int j = 0; j < 3; j++)
+                    for (int w = 0; w < 3; w++) v[j] += (Mx[j][w] / (t * t) + My[j][w]) * Vv[n[w]];
+                dv = 0;
+                for (int j = 0; j < 3; j++) dv += Vv[n[j]] * v[j];
+                dv *= (10000. * c * c / vol);
+                B = sqrt(fabs(dv));
+                ora_get_bh_props(bp, B, &mu, &dv);
+                mu = 1. / (ORA_MUO * mu);
+                mu2[i] = mu * t;
+                mu1[i] = mu / (t + mu * (1. - t));
+                for (int j = 0; j < 3; j++) {
+                    v[j] = 0; u[j] = 0;
+                    for (int w = 0; w < 3; w++) {
+                        v[j] += (Mx[j][w] / t + My[j][w]) * Vv[n[w]];
+                        u[j] += (Mx[j][w] / t + t * My[j][w]) * Vv[n[w]];
+                    }
+                }
+                K = -100. * c * c * c * dv / (vol);
+                for (int j = 0; j < 3; j++)
+                    for (int w = 0; w < 3; w++) Mn[j][w] = K * (v[j] * u[w] + v[w] * u[j]);
+            }
+        }
+
+        /* the conformally mapped exterior region (staticaxi.cpp:625-632) */
+        if (lab->IsExternal && (Iter == 0)) {
+            double Z = (Y[n[0]] + Y[n[1]] + Y[n[2]]) / 3. - extZo;
+            double kludge = (R * R + Z * Z) * extRi / (extRo * extRo * extRo);
+            mu1[i] /= kludge;
+            mu2[i] /= kludge;
+        }
+
+        for (int j = 0; j < 3; j++)
+            for (int k = 0; k < 3; k++) {
+                Me[j][k] += (Mx[j][k] / mu2[i] + My[j][k] / mu1[i] + Mxy[j][k] * v12[i] + Mn[j][k]);
+                be[j] += Mn[j][k] * Vv[n[k]];
+            }
+        for (int j = 0; j < 3; j++) {
+            for (int k = j; k < 3; k++) ops->addto(L, -Me[j][k], n[j], n[k]);
+            b[n[j]] -= be[j];
+        }
+    }
+
+    /* point currents (staticaxi.cpp:644-650) */
+    for (int i = 0; i < NN; i++)
+        if (pr->marker[i] >= 0) b[i] += (0.01 * pr->points[pr->marker[i]].J_re * 2. * X[i]);
+    /* A = 0 on the axis, fixed A at points (staticaxi.cpp:652-659) */
+    for (int i = 0; i < NN; i++) {
+        if (fabs(X[i]) < (units[pr->length_units] * 1.e-06)) {
+            ops->setvalue(L, i, 0.);
+        } else if (pr->marker[i] >= 0) {
+            const ora_point *pp = &pr->points[pr->marker[i]];
+            if ((pp->J_re == 0) && (pp->J_im == 0)) ops->setvalue(L, i, pp->A_re / c);
+        }
+    }
+    /* fixed A along segments, skipped on the axis (staticaxi.cpp:661-728) */
+    for (int i = 0; i < NE; i++)
+        for (int j = 0; j < 3; j++) {
+            int k = j + 1;
+            if (k == 3) k = 0;
+            int s = pr->e[3 * i + j];
+            if (s >= 0 && pr->lines[s].BdryFormat == 0) {
+                const ora_line *ln = &pr->lines[s];
+                int nodes2[2] = {pr->p[3 * i + j], pr->p[3 * i + k]};
+                for (int m = 0; m < 2; m++) {
+                    double x = X[nodes2[m]], y = Y[nodes2[m]], av;
+                    if (pr->coords == 0) {
+                        x /= units[pr->length_units];
+                        y /= units[pr->length_units];
+                        av = ln->A0 + x * ln->A1 + y * ln->A2;
+                    } else {
+                        double rr = sqrt(x * x + y * y), tt;
+                        if ((x == 0) && (y == 0)) tt = 0;
+                        else tt = atan2(y, x) / ORA_DEG;
+                        rr /= units[pr->length_units];
+                        av = ln->A0 + rr * ln->A1 + tt * ln->A2;
+                    }
+                    av *= cos(ln->phi * ORA_DEG);
+                    if (x != 0) ops->setvalue(L, nodes2[m], av / c);
+                }
+            }
+        }
+    for (int k = 0; k < pr->n_pbc; k++) {
+        if (pr->pbc[3 * k + 2] == 0) ops->periodicity(L, pr->pbc[3 * k], pr->pbc[3 * k + 1]);
+        if (pr->pbc[3 * k + 2] == 1) ops->antiperiodicity(L, pr->pbc[3 * k], pr->pbc[3 * k + 1]);
+    }
+    *LinearFlag_io = LinearFlag;
+}
+
 int ora_static2d(ora_problem *pr, const ora_linprob_ops *ops, double *A_out, ora_stats *stats)
 {
     if (!ops) ops = &k_builtin;
@@ -633,7 +938,8 @@ int ora_static2d(ora_problem *pr, const ora_linprob_ops *ops, double *A_out, ora
 
     do {
         if (Iter > 0) ops->wipe(L);
-        ora_assemble(pr, ops, L, Iter, mu1, mu2, v12, &LinearFlag);
+        if (pr->axisymmetric) ora_assemble_axi(pr, ops, L, Iter, mu1, mu2, v12, &LinearFlag);
+        else ora_assemble(pr, ops, L, Iter, mu1, mu2, v12, &LinearFlag);
         double *Vv;
         Vv = ops->V(L);
         for (int j = 0; j < NN; j++) V_old[j] = Vv[j];
@@ -666,6 +972,8 @@ int ora_static2d(ora_problem *pr, const ora_linprob_ops *ops, double *A_out, ora
 
     double *Vv = ops->V(L);
     for (int i = 0; i < NN; i++) A_out[i] = Vv[i] * c;
+    if (pr->axisymmetric)   /* Webers: 2 pi r A (staticaxi.cpp:774-779) */
+        for (int i = 0; i < NN; i++) A_out[i] *= (pr->x[i] * 0.01 * 2 * ORA_PI);
     if (stats) {
         stats->newton_iters = Iter;
         stats->cg_iters = cg_total;
@@ -687,7 +995,8 @@ int ora_static2d_system(ora_problem *pr, int *rows, int *cols, double *vals, lon
     double *v12 = (double *)calloc(NE, sizeof(double));
     /* circuits are computed by ora_static2d; do the same prologue here */
     ora_circuits(pr);
-    ora_assemble(pr, &k_builtin, L, 0, mu1, mu2, v12, &LinearFlag);
+    if (pr->axisymmetric) ora_assemble_axi(pr, &k_builtin, L, 0, mu1, mu2, v12, &LinearFlag);
+    else ora_assemble(pr, &k_builtin, L, 0, mu1, mu2, v12, &LinearFlag);
     *nnz_out = ora_lp_export_upper(L, rows, cols, vals, cap);
     for (int i = 0; i < NN; i++) b_out[i] = ((ora_lp *)L)->b[i];
     ora_lp_destroy(L);

@@ -9,6 +9,9 @@
  *       cfemm/libfemm/spars.cpp:35-495, spars.h:38-83
  *   FSolver::Static2D (element assembly, BCs, nonlinear B-H Newton loop)
  *       cfemm/fsolver/static2d.cpp:53-1033
+ *   FSolver::StaticAxisymmetric (r-weighted element matrices with the
+ *       logarithmic R_hat, r-weighted sources, A = 0 on the axis, output
+ *       converted to flux 2 pi r A)  cfemm/fsolver/staticaxi.cpp:45-794
  *   CMSolverMaterialProp::GetBHProps (cubic Hermite B-H interpolation)
  *       cfemm/libfemm/CMaterialProp.cpp:997-1057
  *
@@ -42,6 +45,7 @@ typedef struct {
     int InCircuit;          /* -1 if none */
     double MagDir;          /* degrees */
     int bIsWound;
+    int IsExternal;         /* axisymmetric: conformally mapped exterior region */
 } ora_label;
 
 typedef struct {
@@ -83,6 +87,8 @@ typedef struct {
     int coords;                 /* 0 cartesian, 1 polar */
     int bandwidth;              /* CBigLinProb bdw (0 = full scan) */
     double relax;               /* FSolver::Relax (1.0 after LoadProblemFile) */
+    int axisymmetric;           /* ProblemType: 0 planar (Static2D), 1 axisymmetric */
+    double ext_ro, ext_ri, ext_zo;   /* exterior-region parameters (user units) */
 } ora_problem;
 
 typedef struct {
@@ -107,7 +113,8 @@ typedef struct {
 /* The built-in CBigLinProb restatement. */
 const ora_linprob_ops *ora_builtin_linprob(void);
 
-/* FSolver::Static2D; A_out[i] = V[i] * c (the value written to .ans). */
+/* FSolver::Static2D / StaticAxisymmetric (pr->axisymmetric); A_out[i] is
+ * the value written to .ans: V[i] * c, times 2 pi r (m) when axisymmetric. */
 int ora_static2d(ora_problem *pr, const ora_linprob_ops *ops, double *A_out,
                  ora_stats *stats);
 

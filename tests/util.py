@@ -21,7 +21,7 @@ def kernel_kwargs(pr: femfile.FemProblem, mesh: femfile.Mesh) -> dict:
             b.update(B=np.array(m.Bdata), H=np.array(m.Hdata), slope=np.array(m.slope))
         blocks.append(b)
     labels = [dict(block=max(lb.BlockType, 0), in_circuit=lb.InCircuit, mag_dir=lb.MagDir,
-                   is_wound=int(lb.bIsWound)) for lb in pr.labels]
+                   is_wound=int(lb.bIsWound), is_external=int(lb.IsExternal)) for lb in pr.labels]
     lines = [dict(format=b.BdryFormat, A0=b.A0, A1=b.A1, A2=b.A2, phi=b.phi, c0=b.c0, c1=b.c1, c0_im=b.c0i,
                   c1_im=b.c1i, Mu=b.Mu, Sig=b.Sig) for b in pr.bdrys]
     points = [dict(A_re=q.A_re, A_im=q.A_im, J_re=q.J_re, J_im=q.J_im) for q in pr.points]
@@ -30,7 +30,8 @@ def kernel_kwargs(pr: femfile.FemProblem, mesh: femfile.Mesh) -> dict:
     return dict(x=mesh.x, y=mesh.y, p=mesh.p, lbl=mesh.lbl, marker=mesh.marker, e=mesh.e,
                 pbc=mesh.pbc if len(mesh.pbc) else None, blocks=blocks, labels=labels, lines=lines,
                 points=points, circuits=circuits, precision=pr.Precision, length_units=pr.LengthUnits,
-                coords=pr.Coords, relax=pr.Relax, frequency=pr.Frequency)
+                coords=pr.Coords, relax=pr.Relax, frequency=pr.Frequency, problem_type=pr.ProblemType,
+                ext_zo=pr.extZo, ext_ro=pr.extRo, ext_ri=pr.extRi)
 
 
 def synth_to_oracle(kw: dict):
@@ -42,6 +43,8 @@ def synth_to_oracle(kw: dict):
     pr.LengthUnits = kw["length_units"]
     pr.Relax = 1.0
     pr.Frequency = kw.get("frequency", 0.0)
+    pr.ProblemType = kw.get("problem_type", 0)
+    pr.extZo, pr.extRo, pr.extRi = kw.get("ext_zo", 0.0), kw.get("ext_ro", 0.0), kw.get("ext_ri", 0.0)
     for b in kw["blocks"]:
         m = femfile.BlockProp(mu_x=b.get("mu_x", 1.0), mu_y=b.get("mu_y", 1.0), H_c=b.get("H_c", 0.0),
                               J_re=b.get("J_re", 0.0), Cduct=b.get("Cduct", 0.0),
@@ -55,7 +58,8 @@ def synth_to_oracle(kw: dict):
         pr.blocks.append(m)
     for lb in kw["labels"]:
         pr.labels.append(femfile.BlockLabel(BlockType=lb["block"], InCircuit=lb.get("in_circuit", -1),
-                                            MagDir=lb.get("mag_dir", 0.0), Turns=2 if lb.get("is_wound", 0) else 1))
+                                            MagDir=lb.get("mag_dir", 0.0), Turns=2 if lb.get("is_wound", 0) else 1,
+                                            IsExternal=bool(lb.get("is_external", 0))))
     for ln in kw["lines"]:
         pr.bdrys.append(femfile.BdryProp(BdryFormat=ln.get("format", 0), A0=ln.get("A0", 0.0),
                                          A1=ln.get("A1", 0.0), A2=ln.get("A2", 0.0), phi=ln.get("phi", 0.0),
@@ -91,7 +95,7 @@ def rel_err(a, b):
 C_ANS = 3.141592653589793238462643383 * 4.0e-5   # A = V * c (static2d.cpp:66, 1018-1021)
 
 
-def solver_tolerance(tol, A_ref, P):
+def solver_tolerance(tol, A_ref, P, r=None):
     """Tolerance for comparing the device's A with the reference's.
 
     The reference stops its SSOR-PCG at sqrt(z.r / z0.b) <= Precision
@@ -107,4 +111,6 @@ def solver_tolerance(tol, A_ref, P):
     n = len(rp) - 1
     M = sp.csr_matrix((val, col, rp), shape=(n, n))
     exact = spla.spsolve(M.tocsc(), b) * C_ANS
+    if r is not None:   # axisymmetric answers are the flux 2 pi r A (staticaxi.cpp:774-779)
+        exact = exact * (np.asarray(r) * 0.01 * 2 * np.pi)
     return max(tol, 2.0 * rel_err(A_ref, exact))

@@ -271,9 +271,11 @@ bool ParseFemFile(const std::string &path, FemmProblemData &pr, std::string &err
             std::string u = first_token(rest);
             if (u == "planar") pr.ProblemTypeV = PLANAR;
             if (u == "axisymmetric") pr.ProblemTypeV = AXISYMMETRIC;
-        } else if (tok == "[extzo]" || tok == "[extro]" || tok == "[extri]" || tok == "[forcemaxmesh]" ||
-                   tok == "[dosmartmesh]") {
-            // geometry/meshing options, unused by the solver
+        } else if (tok == "[extzo]") ok = parse_double(rest, pr.extZo);   // feasolver.cpp:306-326
+        else if (tok == "[extro]") ok = parse_double(rest, pr.extRo);
+        else if (tok == "[extri]") ok = parse_double(rest, pr.extRi);
+        else if (tok == "[forcemaxmesh]" || tok == "[dosmartmesh]") {
+            // meshing options, unused by the solver
         } else if (tok == "[comment]") ok = parse_string(rest, pr.comment);
         else if (tok == "[acsolver]") ok = parse_int(rest, pr.ACSolver);
         else if (tok == "[prevtype]") ok = parse_int(rest, pr.PrevType);

@@ -109,6 +109,7 @@ struct FemmProblemData {
     LengthUnit LengthUnits = LengthInches;
     CoordsType Coords = CART;
     ProblemType ProblemTypeV = PLANAR;
+    double extZo = 0, extRo = 0, extRi = 0;   // axisymmetric exterior region, user units
     int ACSolver = 0;
     int PrevType = 0;
     std::string previousSolutionFile;

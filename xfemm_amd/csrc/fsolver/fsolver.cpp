@@ -386,6 +386,7 @@ bool FSolver::make_desc(DescStore &ds)
         ds.lab[k].in_circuit = labellist[k].InCircuit;
         ds.lab[k].mag_dir = labellist[k].MagDir;
         ds.lab[k].is_wound = labellist[k].bIsWound ? 1 : 0;
+        ds.lab[k].is_external = labellist[k].IsExternal ? 1 : 0;
     }
     ds.lin.resize(lineproplist.size());
     for (size_t k = 0; k < lineproplist.size(); k++) {
@@ -442,6 +443,10 @@ bool FSolver::make_desc(DescStore &ds)
     d.length_units = (int)LengthUnits;
     d.coords = (int)Coords;
     d.relax = Relax;
+    d.problem_type = ProblemTypeV == AXISYMMETRIC ? XFK_AXISYMMETRIC : XFK_PLANAR;
+    d.ext_zo = extZo;
+    d.ext_ro = extRo;
+    d.ext_ri = extRi;
     return true;
 }
 
@@ -633,8 +638,8 @@ bool FSolver::runSolver(bool verbose)
         PrintMessage("solving...\n");
         PrintMessage("Problem Statistics:\n%i nodes\n%i elements\nPrecision: %f\n", NumNodes, NumEls, Precision);
     }
-    if (ProblemTypeV != PLANAR) {
-        warn("axisymmetric problems are not supported by this solver build\n");
+    if (ProblemTypeV != PLANAR && Frequency != 0) {
+        warn("harmonic axisymmetric problems are not supported by this solver build\n");
         return false;
     }
     if (Frequency != 0) {
@@ -654,7 +659,8 @@ bool FSolver::runSolver(bool verbose)
         warn("Couldn't solve the problem\n");
         return false;
     }
-    if (verbose) PrintMessage("Static 2-D problem solved\n");
+    if (verbose)
+        PrintMessage(ProblemTypeV == AXISYMMETRIC ? "Static axisymmetric problem solved\n" : "Static 2-D problem solved\n");
     if (!WriteStatic2D()) {
         warn("couldn't write results to disk\n");
         return false;

@@ -442,6 +442,10 @@ static int assemble(xfk_problem *P, int iter)
     A.val = P->val.p;
     A.b = P->b.p;
     A.iter = iter;
+    A.axi = P->axi ? 1 : 0;
+    A.ext_ro = P->ext_ro;
+    A.ext_ri = P->ext_ri;
+    A.ext_zo = P->ext_zo;
     for (int c = 0; c < P->ncolors; ++c) launch_assemble_color(s, P->color_off[c], P->color_off[c + 1], A);
     launch_point_currents(s, P->npt, P->pt_nodes.p, P->pt_J.p, P->b.p);
     launch_dirichlet(s, P->nfix_rows, P->fix_rows.p, P->nfix_cols, P->fix_cols_row.p, P->rowptr.p, P->col.p,
@@ -738,6 +742,8 @@ int validate_desc(const xfk_problem_desc *d)
     XFK_REQUIRE(d->n_pbc == 0 || d->pbc, XFK_ERR_ARG, "missing pbc table");
     XFK_REQUIRE(d->n_lines < 1023, XFK_ERR_UNSUPPORTED, "at most 1022 boundary properties");
     XFK_REQUIRE(d->length_units >= 0 && d->length_units < 6, XFK_ERR_ARG, "bad length units");
+    XFK_REQUIRE(d->problem_type == XFK_PLANAR || d->problem_type == XFK_AXISYMMETRIC, XFK_ERR_ARG,
+                "problem type must be planar or axisymmetric");
     const int N = d->n_nodes, NE = d->n_elems;
     for (long long i = 0; i < 3LL * NE; ++i)
         XFK_REQUIRE(d->p[i] >= 0 && d->p[i] < N, XFK_ERR_ARG, "element node index out of range");
@@ -747,6 +753,8 @@ int validate_desc(const xfk_problem_desc *d)
         XFK_REQUIRE(d->labels[k].block >= 0 && d->labels[k].block < d->n_blocks, XFK_ERR_ARG,
                     "label block index out of range");
         XFK_REQUIRE(d->labels[k].in_circuit < d->n_circs, XFK_ERR_ARG, "label circuit index out of range");
+        XFK_REQUIRE(!(d->problem_type == XFK_AXISYMMETRIC && d->labels[k].is_external) || d->ext_ro > 0, XFK_ERR_ARG,
+                    "exterior region needs [extRo] > 0");
     }
     for (int k = 0; k < d->n_blocks; ++k) {
         const xfk_block_desc &b = d->blocks[k];
@@ -804,7 +812,7 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
         G.lab[k].blk = l.block;
         G.lab[k].in_circuit = l.in_circuit;
         G.lab[k].is_wound = l.is_wound;
-        G.lab[k].pad = 0;
+        G.lab[k].external = l.is_external;
     }
     G.lin.assign(std::max(1, d->n_lines), DevLine{});
     for (int k = 0; k < d->n_lines; ++k) {
@@ -813,6 +821,10 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
         G.lin[k].format = d->lines[k].format;
         G.lin[k].pad = 0;
     }
+    G.axi = d->problem_type == XFK_AXISYMMETRIC;
+    G.ext_ro = d->ext_ro * units[d->length_units];   // staticaxi.cpp:70-72
+    G.ext_ri = d->ext_ri * units[d->length_units];
+    G.ext_zo = d->ext_zo * units[d->length_units];
     // which elements are nonlinear -> LinearFlag (static2d.cpp:633-639)
     for (int i = 0; i < NE && !G.any_nonlinear; ++i)
         if (G.blk[G.lab[d->lbl[i]].blk].BHpoints != 0) G.any_nonlinear = true;
@@ -831,7 +843,8 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
             double Cduct = G.blk[L.blk].Cduct;
             if (L.is_wound) Cduct = 0;
             I1[L.in_circuit] += a;
-            I2[L.in_circuit] += a * Cduct;
+            if (G.axi) I2[L.in_circuit] += 100. * a * Cduct / ((d->x[n[0]] + d->x[n[1]] + d->x[n[2]]) / 3.);
+            else I2[L.in_circuit] += a * Cduct;   // staticaxi.cpp:96-104 / static2d.cpp:108-118
             I3[L.in_circuit] += G.blk[L.blk].J_re * a * 100.;
         }
         for (int k = 0; k < d->n_circs; ++k) {
@@ -878,12 +891,16 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
         int m = marker(i);
         if (m >= 0 && d->points[m].J_re != 0.0) {
             G.pt_nodes.push_back(i);
-            G.pt_J.push_back(0.01 * d->points[m].J_re);
+            // axisymmetric: 0.01 J 2 r (staticaxi.cpp:644-650)
+            G.pt_J.push_back(G.axi ? 0.01 * d->points[m].J_re * 2. * d->x[i] : 0.01 * d->points[m].J_re);
         }
     }
     for (int i = 0; i < N; ++i) {
         int m = marker(i);
-        if (m >= 0 && d->points[m].J_re == 0 && d->points[m].J_im == 0) set_value(i, d->points[m].A_re / c);
+        if (G.axi && fabs(d->x[i]) < units[d->length_units] * 1.e-06)
+            set_value(i, 0.);   // A = 0 on the axis (staticaxi.cpp:652-659)
+        else if (m >= 0 && d->points[m].J_re == 0 && d->points[m].J_im == 0)
+            set_value(i, d->points[m].A_re / c);
     }
     for (int i = 0; i < NE; ++i)
         for (int j = 0; j < 3; ++j) {
@@ -906,7 +923,7 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
                     a = ln.A0 + r * ln.A1 + t * ln.A2;
                 }
                 a *= cos(ln.phi * kDEG);
-                set_value(nodes2[m], a / c);
+                if (!G.axi || x != 0) set_value(nodes2[m], a / c);   // staticaxi.cpp:681, 694, 712, 726
             }
         }
 }
@@ -940,6 +957,11 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     P->relax = d->relax;
     P->length_units = d->length_units;
     P->coords = d->coords;
+    P->axi = G.axi;
+    if (G.axi) P->axi_x.assign(d->x, d->x + d->n_nodes);
+    P->ext_ro = G.ext_ro;
+    P->ext_ri = G.ext_ri;
+    P->ext_zo = G.ext_zo;
     P->any_nonlinear = G.any_nonlinear;
     if (plan) {
         P->comm = comm;
@@ -1253,6 +1275,8 @@ int xfk_get_solution(xfk_problem *P, double *A)
     if (!P->comm) {
         XFK_CHECK(d2h(A, P->V.p, sizeof(double) * P->N, s));
         for (int i = 0; i < P->N; ++i) A[i] = A[i] * kC;   // L.b[i] = L.V[i]*c (static2d.cpp:1018-1021)
+        if (P->axi)   // flux 2 pi r A, Webers (staticaxi.cpp:774-779)
+            for (int i = 0; i < P->N; ++i) A[i] *= (P->axi_x[i] * 0.01 * 2 * kPI);
         return XFK_OK;
     }
     // sharded: all-gather the owned rows (padded to the largest block)
@@ -1272,6 +1296,8 @@ int xfk_get_solution(xfk_problem *P, double *A)
         const long long r0 = row_begin(P->N_global, q, R), r1 = row_begin(P->N_global, q + 1, R);
         for (long long i = r0; i < r1; ++i) A[i] = h[(size_t)q * maxn + (i - r0)] * kC;
     }
+    if (P->axi)
+        for (int i = 0; i < P->N_global; ++i) A[i] *= (P->axi_x[i] * 0.01 * 2 * kPI);
     return XFK_OK;
 }
 

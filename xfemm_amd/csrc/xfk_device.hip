@@ -428,6 +428,174 @@ __device__ void get_bh_props(const DevBlock &m, const double *__restrict__ Bt, c
         }
 }
 
+// FSolver::StaticAxisymmetric element (staticaxi.cpp:172-636): x is r, y is
+// z.  Flux-formulation matrices with the logarithmic mean radius R_hat, r-
+// weighted sources and boundary terms, B from the element energy, the
+// exterior-region permeability warp.  Me / be are the element's contribution
+// before the sign of the global assembly (as in the planar path).
+__device__ void axi_element(int i, const AssembleArgs &A, const int (&n)[3], const double (&X)[3],
+                            const double (&Y)[3], const DevLabel &lab, const DevBlock &bp, double (&Me)[3][3],
+                            double (&be)[3])
+{
+    double p[3], q[3], g[3], rn[3], Mx[3][3], My[3][3], Mn[3][3];
+    p[0] = Y[1] - Y[2]; p[1] = Y[2] - Y[0]; p[2] = Y[0] - Y[1];
+    q[0] = X[2] - X[1]; q[1] = X[0] - X[2]; q[2] = X[1] - X[0];
+    g[0] = (X[2] + X[1]) / 2.; g[1] = (X[0] + X[2]) / 2.; g[2] = (X[1] + X[0]) / 2.;
+    rn[0] = X[0]; rn[1] = X[1]; rn[2] = X[2];
+    const double a = (p[0] * q[1] - p[1] * q[0]) / 2.;
+    const double R = (X[0] + X[1] + X[2]) / 3.;
+    double a_hat = 0;
+    for (int j = 0; j < 3; ++j) a_hat += (rn[j] * rn[j] * p[j] / (4. * R));
+    const double vol = 2. * R * a_hat;
+    int flag = 0;
+    for (int j = 0; j < 3; ++j) flag += (rn[j] < 1.e-06);
+    double R_hat = 0.;
+    if (flag == 2) {
+        R_hat = R;
+    } else if (flag == 1) {
+        if (rn[0] < 1.e-06)
+            R_hat = (fabs(rn[1] - rn[2]) < 1.e-06) ? rn[2] / 2. : (rn[1] - rn[2]) / (2. * log(rn[1]) - 2. * log(rn[2]));
+        if (rn[1] < 1.e-06)
+            R_hat = (fabs(rn[2] - rn[0]) < 1.e-06) ? rn[0] / 2. : (rn[2] - rn[0]) / (2. * log(rn[2]) - 2. * log(rn[0]));
+        if (rn[2] < 1.e-06)
+            R_hat = (fabs(rn[0] - rn[1]) < 1.e-06) ? rn[1] / 2. : (rn[0] - rn[1]) / (2. * log(rn[0]) - 2. * log(rn[1]));
+    } else {
+        if (fabs(q[0]) < 1.e-06)
+            R_hat = (q[1] * q[1]) / (2. * (-q[1] + rn[0] * log(rn[0] / rn[2])));
+        else if (fabs(q[1]) < 1.e-06)
+            R_hat = (q[2] * q[2]) / (2. * (-q[2] + rn[1] * log(rn[1] / rn[0])));
+        else if (fabs(q[2]) < 1.e-06)
+            R_hat = (q[0] * q[0]) / (2. * (-q[0] + rn[2] * log(rn[2] / rn[1])));
+        else
+            R_hat = -(q[0] * q[1] * q[2]) /
+                    (2. * (q[0] * rn[0] * log(rn[0]) + q[1] * rn[1] * log(rn[1]) + q[2] * rn[2] * log(rn[2])));
+    }
+    // Mr, Mz (staticaxi.cpp:256-276); Mrz only enters with v12 (incremental problems)
+    double K = (-1. / (2. * a_hat * R));
+    for (int j = 0; j < 3; ++j)
+        for (int k = j; k < 3; ++k) Mx[j][k] = K * p[j] * rn[j] * p[k] * rn[k];
+    for (int j = 0; j < 3; ++j)
+        if (rn[j] < 1.e-06) Mx[j][j] += Mx[0][0] + Mx[1][1] + Mx[2][2];
+    K = (-1. / (2. * a_hat * R_hat));
+    for (int j = 0; j < 3; ++j)
+        for (int k = j; k < 3; ++k) My[j][k] = K * (q[j] * rn[j]) * (q[k] * rn[k]) * (g[j] / R) * (g[k] / R);
+    Mx[1][0] = Mx[0][1]; Mx[2][0] = Mx[0][2]; Mx[2][1] = Mx[1][2];
+    My[1][0] = My[0][1]; My[2][0] = My[0][2]; My[2][1] = My[1][2];
+    for (int j = 0; j < 3; ++j) {
+        for (int k = 0; k < 3; ++k) { Me[j][k] = 0.; Mn[j][k] = 0.; }
+        be[j] = 0.;
+    }
+    // mixed boundary conditions (staticaxi.cpp:298-320)
+    const int eb = A.ebits[i];
+    if (eb)
+        for (int j = 0; j < 3; ++j) {
+            const int ej = ((eb >> (10 * j)) & 1023) - 1;
+            if (ej < 0) continue;
+            const DevLine ln = A.lines[ej];
+            if (ln.format != 2) continue;
+            const int k = (j + 1) % 3;
+            const double lj = sqrt(pow(X[k] - X[j], 2.) + pow(Y[k] - Y[j], 2.));
+            const double r = (X[j] + X[k]) / 2.;
+            double Kb = -0.0001 * kC * 2. * r * ln.c0 * lj / 6.;
+            Me[j][j] += Kb * 2.;
+            Me[k][k] += Kb * 2.;
+            Me[j][k] += Kb;
+            Me[k][j] += Kb;
+            Kb = (ln.c1 * lj / 2.) * 0.0001 * 2 * r;
+            be[j] += Kb;
+            be[k] += Kb;
+        }
+    // source current density (staticaxi.cpp:322-337)
+    double t = 0;
+    if (lab.in_circuit >= 0) {
+        const DevCirc C = A.circs[lab.in_circuit];
+        if (C.ccase == 1) t = C.J;
+        if (C.ccase == 0) t = -100. * C.dV * bp.Cduct / R;
+    }
+    const double Ks = -2. * R * (bp.J_re + t) * a / 3.;
+    be[0] += Ks; be[1] += Ks; be[2] += Ks;
+    // magnetisation (staticaxi.cpp:396-407)
+    if (bp.H_c != 0.0)
+        for (int j = 0; j < 3; ++j) {
+            const int k = (j + 1) % 3;
+            const double r = (X[j] + X[k]) / 2.;
+            const double Km = -0.0001 * r * bp.H_c * (lab.cos_m * (X[k] - X[j]) + lab.sin_m * (Y[k] - Y[j]));
+            be[j] += Km;
+            be[k] += Km;
+        }
+    // permeability (staticaxi.cpp:409-632)
+    double m1, m2;
+    const double Vn[3] = {A.V[n[0]], A.V[n[1]], A.V[n[2]]};
+    if (A.iter == 0) {
+        const double f = bp.LamFill;
+        if (bp.LamType == 0) { m1 = bp.mu_x * f; m2 = bp.mu_y * f; }
+        else if (bp.LamType == 1) { m1 = bp.mu_x * f + (1. - f); m2 = bp.mu_x / (f + bp.mu_x * (1. - f)); }
+        else if (bp.LamType == 2) { m1 = bp.mu_y * f + (1. - f); m2 = bp.mu_y / (f + bp.mu_y * (1. - f)); }
+        else { m1 = 1; m2 = 1; }
+        if (lab.external) {
+            const double Z = (Y[0] + Y[1] + Y[2]) / 3. - A.ext_zo;
+            const double kludge = (R * R + Z * Z) * A.ext_ri / (A.ext_ro * A.ext_ro * A.ext_ro);
+            m1 /= kludge;
+            m2 /= kludge;
+        }
+        A.mu1[i] = m1;
+        A.mu2[i] = m2;
+    } else {
+        m1 = A.mu1[i];
+        m2 = A.mu2[i];
+        if (bp.BHpoints > 0 && bp.LamType <= 2 && (bp.LamType != 0 || m1 == m2)) {
+            const double f = bp.LamFill;
+            const double sx = (bp.LamType == 2) ? 1. / (f * f) : 1., sy = (bp.LamType == 1) ? 1. / (f * f) : 1.;
+            double v[3], u[3], dv = 0;
+            for (int j = 0; j < 3; ++j) {
+                v[j] = 0;
+                for (int w = 0; w < 3; ++w) v[j] += (Mx[j][w] * sx + My[j][w] * sy) * Vn[w];
+            }
+            for (int j = 0; j < 3; ++j) dv += Vn[j] * v[j];
+            dv *= (10000. * kC * kC / vol);
+            const double B = sqrt(fabs(dv));
+            double mu = 0;
+            get_bh_props(bp, A.bhB, A.bhH, A.bhS, B, mu, dv);
+            mu = 1. / (kMUO * mu);
+            if (bp.LamType == 0) {
+                m1 = mu; m2 = mu;
+                for (int j = 0; j < 3; ++j) {
+                    v[j] = 0;
+                    for (int w = 0; w < 3; ++w) v[j] += (Mx[j][w] + My[j][w]) * Vn[w];
+                }
+                const double Kn = -200. * kC * kC * kC * dv / vol;
+                for (int j = 0; j < 3; ++j)
+                    for (int w = 0; w < 3; ++w) Mn[j][w] = Kn * v[j] * v[w];
+            } else {
+                if (bp.LamType == 1) { m1 = mu * f; m2 = mu / (f + mu * (1. - f)); }
+                else { m2 = mu * f; m1 = mu / (f + mu * (1. - f)); }
+                for (int j = 0; j < 3; ++j) {
+                    v[j] = 0; u[j] = 0;
+                    for (int w = 0; w < 3; ++w) {
+                        if (bp.LamType == 1) {
+                            v[j] += (My[j][w] / f + Mx[j][w]) * Vn[w];
+                            u[j] += (My[j][w] / f + f * Mx[j][w]) * Vn[w];
+                        } else {
+                            v[j] += (Mx[j][w] / f + My[j][w]) * Vn[w];
+                            u[j] += (Mx[j][w] / f + f * My[j][w]) * Vn[w];
+                        }
+                    }
+                }
+                const double Kn = -100. * kC * kC * kC * dv / (vol);
+                for (int j = 0; j < 3; ++j)
+                    for (int w = 0; w < 3; ++w) Mn[j][w] = Kn * (v[j] * u[w] + v[w] * u[j]);
+            }
+            A.mu1[i] = m1;
+            A.mu2[i] = m2;
+        }
+    }
+    for (int j = 0; j < 3; ++j)
+        for (int k = 0; k < 3; ++k) {
+            Me[j][k] += (Mx[j][k] / m2 + My[j][k] / m1 + Mn[j][k]);
+            be[j] += Mn[j][k] * Vn[k];
+        }
+}
+
 // AssembleArgs: see xfk_kernels.h
 
 __global__ void __launch_bounds__(kBlock) k_assemble_color(int begin, int end, AssembleArgs A)
@@ -452,6 +620,17 @@ __global__ void __launch_bounds__(kBlock) k_assemble_color(int begin, int end, A
     const DevBlock bp = A.blocks[lab.blk];
     const double X[3] = {A.x[n[0]], A.x[n[1]], A.x[n[2]]};
     const double Y[3] = {A.y[n[0]], A.y[n[1]], A.y[n[2]]};
+    const int *sl = &s_slot[li * 9 + (li >> 3)];
+    if (A.axi) {
+        double Me[3][3], be[3];
+        axi_element(i, A, n, X, Y, lab, bp, Me, be);
+        for (int j = 0; j < 3; ++j) {
+            if (sl[3 * j] < 0) continue;
+            for (int k = 0; k < 3; ++k) A.val[sl[3 * j + k]] -= (k >= j) ? Me[j][k] : Me[k][j];
+            A.b[n[j]] -= be[j];
+        }
+        return;
+    }
 
     double p[3], q[3];
     p[0] = Y[1] - Y[2]; p[1] = Y[2] - Y[0]; p[2] = Y[0] - Y[1];
@@ -587,7 +766,6 @@ __global__ void __launch_bounds__(kBlock) k_assemble_color(int begin, int end, A
 
     // colour-exclusive scatter: no other element of this launch touches n[*];
     // rows of halo nodes (slot -1) belong to another rank
-    const int *sl = &s_slot[li * 9 + (li >> 3)];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         if (sl[3 * j] < 0) continue;

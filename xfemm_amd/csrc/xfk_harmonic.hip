@@ -543,6 +543,10 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     XFK_REQUIRE(d && out, XFK_ERR_ARG, "null argument");
     *out = nullptr;
     int rc = validate_desc(d);
+    if (rc == XFK_OK && d->problem_type != XFK_PLANAR) {
+        set_error("HarmonicAxisymmetric (harmonicaxi.cpp) is not implemented on the device");
+        rc = XFK_ERR_UNSUPPORTED;
+    }
     if (rc == XFK_OK) rc = harmonic_validate(d, ac);
     if (rc == XFK_OK) rc = check_device(device);
     if (rc != XFK_OK) return rc;

@@ -67,7 +67,7 @@ struct DevBlock {
 // host exactly as static2d.cpp:593-595 does (cos/sin of MagDir*PI/180).
 struct DevLabel {
     double cos_m, sin_m;
-    int blk, in_circuit, is_wound, pad;
+    int blk, in_circuit, is_wound, external;
 };
 
 struct DevLine {
@@ -196,6 +196,9 @@ struct xfk_problem {
     // host copies kept for host-side setup (periodic maps)
     std::vector<int> hp, hpbc;
     int length_units = 0, coords = 0;
+    bool axi = false;                // StaticAxisymmetric (x is r)
+    std::vector<double> axi_x;       // global node radii (cm): the answer is 2 pi r A
+    double ext_ro = 0, ext_ri = 0, ext_zo = 0;   // exterior region, cm
     double precision = 1e-8, relax = 1.0;
     bool any_nonlinear = false;
 
@@ -331,6 +334,8 @@ struct GlobalPrep {
     std::vector<unsigned char> fixed;    // per node: Dirichlet value set
     std::vector<double> first, last;     // first / last value set (CBigLinProb::SetValue order)
     bool any_nonlinear = false;
+    bool axi = false;                    // FSolver::StaticAxisymmetric
+    double ext_ro = 0, ext_ri = 0, ext_zo = 0;   // exterior region, cm
 };
 
 int validate_desc(const xfk_problem_desc *d);

@@ -19,6 +19,8 @@ struct AssembleArgs {
     const double *V;
     double *val, *b;
     int iter;
+    int axi;                      // StaticAxisymmetric element matrices (staticaxi.cpp:172-632)
+    double ext_ro, ext_ri, ext_zo;   // exterior region (cm)
 };
 
 int grid_reduce(int N);

@@ -53,7 +53,7 @@ class BlockDesc(C.Structure):
 
 class LabelDesc(C.Structure):
     _fields_ = [("block", C.c_int), ("in_circuit", C.c_int), ("mag_dir", C.c_double),
-                ("is_wound", C.c_int)]
+                ("is_wound", C.c_int), ("is_external", C.c_int)]
 
 
 class LineDesc(C.Structure):
@@ -80,7 +80,12 @@ class ProblemDesc(C.Structure):
                 ("n_circs", C.c_int), ("circs", C.POINTER(CircuitDesc)),
                 ("n_pbc", C.c_int), ("pbc", iptr),
                 ("precision", C.c_double), ("length_units", C.c_int), ("coords", C.c_int),
-                ("relax", C.c_double)]
+                ("relax", C.c_double), ("problem_type", C.c_int), ("ext_zo", C.c_double),
+                ("ext_ro", C.c_double), ("ext_ri", C.c_double)]
+
+
+XFK_PLANAR = 0
+XFK_AXISYMMETRIC = 1
 
 
 class Result(C.Structure):
@@ -178,7 +183,7 @@ class _Keep(list):
 
 
 def _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision, length_units,
-               coords, relax):
+               coords, relax, problem_type=0, ext=(0.0, 0.0, 0.0)):
     """xfk_problem_desc of plain arrays / dicts (see Static2DProblem); returns
     (desc, keep) where keep holds every buffer the descriptor points into."""
     keep = _Keep()
@@ -197,6 +202,7 @@ def _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e,
     for k, l in enumerate(labels):
         lb[k].block, lb[k].in_circuit = l["block"], l.get("in_circuit", -1)
         lb[k].mag_dir, lb[k].is_wound = l.get("mag_dir", 0.0), int(l.get("is_wound", 0))
+        lb[k].is_external = int(l.get("is_external", 0))
     ln = (LineDesc * max(1, len(lines)))()
     for k, l in enumerate(lines):
         o = ln[k]
@@ -231,6 +237,8 @@ def _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e,
     else:
         D.n_pbc, D.pbc = 0, None
     D.precision, D.length_units, D.coords, D.relax = precision, length_units, coords, relax
+    D.problem_type = int(problem_type)
+    D.ext_zo, D.ext_ro, D.ext_ri = ext
     keep.extend([bl, lb, ln, pt, ci])
     return D, keep
 
@@ -246,15 +254,18 @@ class Static2DProblem:
                  marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0,
                  device=0, comm: Optional["Comm"] = None, precond: str = "amg", amg_sweeps: Optional[int] = None,
                  amg_theta: Optional[float] = None, frequency: float = 0.0, amg_omega: Optional[float] = None,
-                 amg_replicate: Optional[int] = None, amg_reuse: Optional[bool] = None):
+                 amg_replicate: Optional[int] = None, amg_reuse: Optional[bool] = None, problem_type: int = 0,
+                 ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0):
         """comm: shard the mesh by row blocks over this communicator (every rank
         passes the same global problem; solve() and solution() are collective).
-        precond: "amg" (smoothed-aggregation V-cycle, default) or "jacobi"."""
+        precond: "amg" (smoothed-aggregation V-cycle, default) or "jacobi".
+        problem_type: XFK_PLANAR (Static2D) or XFK_AXISYMMETRIC
+        (StaticAxisymmetric: x is r, y is z; solution() is the flux 2 pi r A)."""
         if frequency:
             raise XfkError("frequency != 0: use Harmonic2DProblem")
         L = load_library()
         D, keep = _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision,
-                             length_units, coords, relax)
+                             length_units, coords, relax, problem_type, (ext_zo, ext_ro, ext_ri))
         self._keep = keep
         self.n_nodes = D.n_nodes
         self.n_elems = D.n_elems
@@ -363,10 +374,11 @@ class Harmonic2DProblem:
 
     def __init__(self, *, x, y, p, lbl, blocks: Sequence[dict], labels: Sequence[dict], frequency: float,
                  lines: Sequence[dict] = (), points: Sequence[dict] = (), circuits: Sequence[dict] = (),
-                 marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0, device=0):
+                 marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0, device=0,
+                 problem_type: int = 0, ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0):
         L = load_library()
         D, keep = _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision,
-                             length_units, coords, relax)
+                             length_units, coords, relax, problem_type, (ext_zo, ext_ro, ext_ri))
         ba = (BlockAcDesc * max(1, len(blocks)))()
         for k, b in enumerate(blocks):
             ba[k].J_im, ba[k].Lam_d = b.get("J_im", 0.0), b.get("Lam_d", 0.0)

@@ -112,11 +112,14 @@ def magnetostatic(n: int, nonlinear: bool = False, L: float = 10.0, J: float = 2
                 lines=lines, points=[], circuits=[], precision=precision, length_units=2, coords=0, relax=1.0)
 
 
-def fem_text(blocks, lines, precision=1e-8, units="centimeters", frequency=0.0) -> str:
+def fem_text(blocks, lines, precision=1e-8, units="centimeters", frequency=0.0, problem_type=0,
+             ext=(0.0, 0.0, 0.0)) -> str:
     """A .fem header carrying the property tables (no geometry: meshes are given)."""
     out = ["[Format]      =  4.0", "[Frequency]   =  %.17g" % frequency, "[Precision]   =  %.17g" % precision,
            "[MinAngle]    =  30", "[Depth]       =  1", "[LengthUnits] =  %s" % units,
-           "[ProblemType] =  planar", "[Coordinates] =  cartesian", "[ACSolver]    =  0",
+           "[ProblemType] =  %s" % ("axisymmetric" if problem_type == 1 else "planar"),
+           "[Coordinates] =  cartesian", "[ACSolver]    =  0",
+           "[extZo] = %.17g" % ext[0], "[extRo] = %.17g" % ext[1], "[extRi] = %.17g" % ext[2],
            '[PrevSoln]    = ""', "[PrevType]    =  0", '[Comment]     =  "synthetic"',
            "[PointProps]   = 0", "[BdryProps]   = %d" % len(lines)]
     for k, ln in enumerate(lines):
@@ -153,13 +156,15 @@ def write_problem(base: str, kw: dict, label_xy: Optional[np.ndarray] = None) ->
     synthetic problem runs through the file-based FSolver path."""
     x, y, p, lbl, e = kw["x"], kw["y"], kw["p"], kw["lbl"], kw["e"]
     conv = 1.0   # centimeters
-    text = fem_text(kw["blocks"], kw["lines"], kw["precision"], frequency=kw.get("frequency", 0.0))
+    text = fem_text(kw["blocks"], kw["lines"], kw["precision"], frequency=kw.get("frequency", 0.0),
+                    problem_type=kw.get("problem_type", 0),
+                    ext=(kw.get("ext_zo", 0.0), kw.get("ext_ro", 0.0), kw.get("ext_ri", 0.0)))
     labels = kw["labels"]
     text += "[NumPoints] = 0\n[NumSegments] = 0\n[NumArcSegments] = 0\n[NumHoles] = 0\n"
     text += "[NumBlockLabels] = %d\n" % len(labels)
     for k, lb in enumerate(labels):
-        text += "0\t0\t%d\t-1\t%d\t%.17g\t0\t1\t0\n" % (lb["block"] + 1, lb.get("in_circuit", -1) + 1,
-                                                        lb.get("mag_dir", 0.0))
+        text += "0\t0\t%d\t-1\t%d\t%.17g\t0\t1\t%d\n" % (lb["block"] + 1, lb.get("in_circuit", -1) + 1,
+                                                        lb.get("mag_dir", 0.0), int(lb.get("is_external", 0)))
     with open(base + ".fem", "w") as fh:
         fh.write(text)
     with open(base + ".node", "w") as fh:
@@ -184,6 +189,75 @@ def write_problem(base: str, kw: dict, label_xy: Optional[np.ndarray] = None) ->
             fh.write("%d\t%d\t%d\t%d\n" % (n, k[0], k[1], mk))
     with open(base + ".pbc", "w") as fh:
         fh.write("0\n0\n")
+
+
+def axisymmetric(n: int, nonlinear: bool = False, L: float = 10.0, J: float = 2.0, mu_steel: float = 1000.0,
+                 precision: float = 1e-8, mixed: bool = True, circuit: bool = False, external: bool = False):
+    """Keyword arguments of an axisymmetric (StaticAxisymmetric) problem on the
+    n x n-cell square r in [0, L], z in [0, L] (cm): a steel pot core around a
+    coil ring, a radially thin NdFeB ring magnetised along +z, A = 0 on the
+    outer radius and the bottom, a mixed (c0, c1) condition on the top unless
+    `mixed` is off; the axis r = 0 takes A = 0 by the solver's own rule.
+    `circuit`: the coil carries a series circuit current instead of J;
+    `external`: the outer band r > 0.8 L is a conformally mapped exterior
+    region (IsExternal, extRo = 0.8 L, extRi = 0.7 L, extZo = L / 2)."""
+    x, y, p = square_mesh(n, L)
+    cx = (x[p[:, 0]] + x[p[:, 1]] + x[p[:, 2]]) / 3.0
+    cy = (y[p[:, 0]] + y[p[:, 1]] + y[p[:, 2]]) / 3.0
+    u, v = cx / L, cy / L
+    lbl = np.zeros(len(p), dtype=np.int32)                                      # 0: air
+    pot = (u < 0.45) & (v > 0.25) & (v < 0.75)
+    cavity = (u > 0.12) & (u < 0.38) & (v > 0.32) & (v < 0.68)
+    lbl[pot & ~cavity] = 1                                                      # 1: steel
+    lbl[(u > 0.16) & (u < 0.32) & (v > 0.36) & (v < 0.64)] = 2                  # 2: coil
+    lbl[(u > 0.55) & (u < 0.6) & (v > 0.42) & (v < 0.58)] = 3                   # 3: magnet ring
+    if external:
+        lbl[(u > 0.8) & (lbl == 0)] = 4                                         # 4: exterior air
+    blocks = [dict(mu_x=1.0, mu_y=1.0),
+              dict(mu_x=mu_steel, mu_y=mu_steel, LamFill=1.0),
+              dict(mu_x=1.0, mu_y=1.0, J_re=0.0 if circuit else J, Cduct=58.0 if circuit else 0.0),
+              dict(mu_x=1.049, mu_y=1.049, H_c=979000.0, Cduct=0.667)]
+    if nonlinear:
+        blocks[1] = dict(mu_x=1.0, mu_y=1.0, LamFill=0.98, LamType=0, bh="M19")
+    labels = [dict(block=0), dict(block=1), dict(block=2, in_circuit=0 if circuit else -1, is_wound=1),
+              dict(block=3, mag_dir=90.0)]
+    if external:
+        labels.append(dict(block=0, is_external=1))
+    for b in blocks:
+        if b.get("bh") == "M19":
+            from .fsolver import bh_get_slopes
+            Bc, Hc, Sc, mu = bh_get_slopes(*m19_curve(), lam_type=b.get("LamType", 0),
+                                           lam_fill=b.get("LamFill", 1.0))
+            b.update(B=Bc, H=Hc, slope=Sc, mu_x=mu, mu_y=mu)
+    tol = 1e-9 * L
+    e = _boundary_edges(p, x, y, L, tol)
+    lines = [dict(format=0)]
+    if mixed:   # top edge: c0 A + dA/dn = c1
+        lines.append(dict(format=2, c0=2.0e5, c1=0.5))
+        for j in range(3):
+            a, b2 = p[:, j], p[:, (j + 1) % 3]
+            top = (np.abs(y[a] - L) < tol) & (np.abs(y[b2] - L) < tol)
+            e[top & (e[:, j] >= 0), j] = 1
+    circuits = [dict(type=0, amps_re=4000.0)] if circuit else []
+    kw = dict(x=x, y=y, p=p, lbl=lbl, e=e, marker=None, pbc=None, blocks=blocks, labels=labels, lines=lines,
+              points=[], circuits=circuits, precision=precision, length_units=2, coords=0, relax=1.0,
+              problem_type=1)
+    if external:
+        kw.update(ext_zo=L / 2, ext_ro=0.8 * L, ext_ri=0.7 * L)
+    return kw
+
+
+def axisymmetric_uniform(n: int, B0: float = 1.0, L: float = 10.0, precision: float = 1e-12):
+    """Air-filled axisymmetric box with A = B0 r / 2 imposed on the outer
+    boundary (A1 = B0 / 2 per metre of r, the mesh in cm): the solution is the
+    uniform axial field, flux 2 pi r A = pi B0 r^2 (Wb, r in m) -- inside the
+    formulation's c0 + c1 r^2 + c2 z flux space, so reproduced to roundoff."""
+    x, y, p = square_mesh(n, L)
+    e = _boundary_edges(p, x, y, L, 1e-9 * L)
+    lines = [dict(format=0, A1=0.5 * B0 * 0.01)]
+    return dict(x=x, y=y, p=p, lbl=np.zeros(len(p), dtype=np.int32), e=e, marker=None, pbc=None,
+                blocks=[dict(mu_x=1.0, mu_y=1.0)], labels=[dict(block=0)], lines=lines, points=[], circuits=[],
+                precision=precision, length_units=2, coords=0, relax=1.0, problem_type=1)
 
 
 def bc_showcase(n: int, anti: bool = False, nonlinear: bool = False, L: float = 10.0):
