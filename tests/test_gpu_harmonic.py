@@ -8,7 +8,8 @@ Tolerances (f64 / complex f64):
   * A at every node: max |dA| <= max(1e-6, 2 x the reference's own error) *
     max |A|, the reference's own error being its distance from the exact
     solution of the assembled system (both stop at |r| / |b| <= Precision,
-    the reference preconditioning COCG with SSOR, the device with Jacobi)
+    the reference preconditioning COCG with SSOR, the device with the AMG
+    V-cycle of the real surrogate Re A +- Im A, or complex Jacobi)
   * the device solution solves its own system: |b - A V| / |b| <= 2 Precision
 """
 import numpy as np
@@ -95,6 +96,27 @@ def test_harmonic_unsupported_cases_are_reported():
     kw = synth.magnetostatic(10)
     with pytest.raises(kernels.XfkError):
         kernels.Harmonic2DProblem(**dict(kw, frequency=0.0))
+
+
+@pytest.mark.parametrize("frequency", [60.0, 2000.0])
+def test_harmonic_amg_preconditioner(frequency):
+    """The V-cycle preconditioner reaches the same answer as complex Jacobi in
+    a mesh-independent handful of iterations (the surrogate's sign follows Im A)."""
+    kw = synth.harmonic(150, frequency=frequency, circuits=False)
+    res = {}
+    for pc in ("amg", "jacobi"):
+        P = kernels.Harmonic2DProblem(**kw, precond=pc)
+        r = P.solve()
+        rp, col, val, b = P.csr()
+        G = sp.csr_matrix((val, col, rp), shape=(len(rp) - 1,) * 2)
+        V = P.solution() / C_ANS
+        assert np.linalg.norm(b - G @ V) / np.linalg.norm(b) <= 2 * kw["precision"]
+        res[pc] = (r, P.solution())
+        P.close()
+    ra, rj = res["amg"][0], res["jacobi"][0]
+    assert ra["amg_levels"] >= 2 and rj["amg_levels"] == 0
+    assert ra["cg_iters"] <= 80 and ra["cg_iters"] * 4 < rj["cg_iters"]
+    assert rel_err(res["amg"][1], res["jacobi"][1]) <= 1e-6
 
 
 def test_harmonic_repeatable():

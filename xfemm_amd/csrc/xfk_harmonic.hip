@@ -13,13 +13,15 @@
 // UNCONJUGATED bilinear form x.y, for complex-symmetric A -- stopping at
 // |r| / |b| <= Precision (cspars.cpp:822-895).  Here it runs in the
 // Chronopoulos-Gear arrangement of xfk_pcg.hip (two launches per iteration,
-// every inner product from one reduction phase) with a complex Jacobi
-// preconditioner in place of the sequential SSOR sweep; the three CGNE
+// every inner product from one reduction phase) preconditioned by the
+// smoothed-aggregation V-cycle of a real SPD surrogate (or complex Jacobi) in
+// place of the sequential SSOR sweep; the three CGNE
 // start-up iterations of PCGSQStart (cspars.cpp:764-820) are not needed by it
 // and are omitted (the answer is the solution to the same tolerance).
 #include <cmath>
 #include <complex>
 
+#include "xfk_amg.h"
 #include "xfk_kernels.h"
 #include "xfk_spmv.h"
 
@@ -289,6 +291,36 @@ __device__ __forceinline__ double2 hc_tile_spmv(int r0, int N, const int *__rest
     return acc;
 }
 
+// the same with X given as split real / imaginary arrays
+__device__ __forceinline__ double2 hc_tile_spmv_split(int r0, int N, const int *__restrict__ rowptr,
+                                                      const int *__restrict__ col, const double *__restrict__ val,
+                                                      const double *__restrict__ val_im,
+                                                      const double *__restrict__ Xr, const double *__restrict__ Xi,
+                                                      double2 *lds)
+{
+    const int r = r0 + threadIdx.x;
+    const int rend = min(r0 + kCgBlock, N);
+    const int s = rowptr[r0], e = rowptr[rend];
+    const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
+    double2 acc = cx(0, 0);
+    for (int c0 = s; c0 < e; c0 += kHcCap) {
+        const int c1 = min(e, c0 + kHcCap);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int k = c0 + threadIdx.x + m * kCgBlock;
+            if (k < c1) {
+                const int j = col[k];
+                lds[k - c0] = cmul(cx(val[k], val_im[k]), cx(Xr[j], Xi[j]));
+            }
+        }
+        __syncthreads();
+        const int a = max(my_s, c0), z = min(my_e, c1);
+        for (int k = a; k < z; ++k) acc = cadd(acc, lds[k - c0]);
+        __syncthreads();
+    }
+    return acc;
+}
+
 // sums of NV values over the workgroup, broadcast
 template <int NV>
 __device__ __forceinline__ void hc_block_sum(double (&v)[NV], double *red)
@@ -319,6 +351,11 @@ struct HcArgs {
     double *part;     // kHcParts arrays of G
     int G;
     CcgState *S;
+    // AMG mode: the real V-cycle preconditions real and imaginary parts; r is
+    // also written split (r_re, r_im), u comes back split (u_re, u_im)
+    int amg;
+    double *r_re, *r_im;
+    const double *u_re, *u_im;
 };
 
 // r = b - A x0 (x0 = 0), u = M^-1 r, z = p = 0; partials gamma_0, |r0|^2, |b|^2
@@ -330,47 +367,73 @@ __global__ void __launch_bounds__(kCgBlock) k_hc_init(HcArgs A, const double *__
     double v[4] = {0, 0, 0, 0};
     if (i < A.N) {
         const double2 rr = cx(b[i], b_im[i]);
-        const double2 u = cmul(A.dinv[i], rr);
         A.x[i] = cx(0, 0);
         A.r[i] = rr;
-        A.u[i] = u;
         A.z[i] = cx(0, 0);
         A.p[i] = cx(0, 0);
-        const double2 g = cmul(rr, u);
-        v[0] = g.x;
-        v[1] = g.y;
+        if (A.amg) {   // u and gamma_0 come from the V-cycle and the SpMV
+            A.r_re[i] = rr.x;
+            A.r_im[i] = rr.y;
+        } else {
+            const double2 u = cmul(A.dinv[i], rr);
+            A.u[i] = u;
+            const double2 g = cmul(rr, u);
+            v[0] = g.x;
+            v[1] = g.y;
+        }
         v[2] = rr.x * rr.x + rr.y * rr.y;
     }
     double s3[3] = {v[0], v[1], v[2]};
     hc_block_sum<3>(s3, red);
     if (threadIdx.x == 0) {
-        A.part[0 * A.G + blockIdx.x] = s3[0];
-        A.part[1 * A.G + blockIdx.x] = s3[1];
+        if (!A.amg) {
+            A.part[0 * A.G + blockIdx.x] = s3[0];
+            A.part[1 * A.G + blockIdx.x] = s3[1];
+        }
         A.part[6 * A.G + blockIdx.x] = s3[2];
         A.part[8 * A.G + blockIdx.x] = s3[2];   // |b|^2 = |r0|^2 (x0 = 0)
     }
 }
 
-// w = A u; partials delta = u.w (unconjugated)
-__global__ void __launch_bounds__(kCgBlock) k_hc_spmv(HcArgs A)
+// w = A u; partials delta = u.w (unconjugated).  AMG mode: u is gathered from
+// the V-cycle's split output (and stored interleaved for the update kernel),
+// and gamma = r.u goes to the partial arrays of parity gpar
+__global__ void __launch_bounds__(kCgBlock) k_hc_spmv(HcArgs A, int gpar)
 {
     if (A.S->done) return;
     __shared__ __attribute__((aligned(16))) double2 lds[kHcCap];
-    __shared__ double red[2 * (kCgBlock / 64)];
+    __shared__ double red[4 * (kCgBlock / 64)];
     const int r0 = blockIdx.x * kCgBlock;
-    const double2 w = hc_tile_spmv(r0, A.N, A.rowptr, A.col, A.val, A.val_im, A.u, lds);
     const int i = r0 + threadIdx.x;
-    double s2[2] = {0, 0};
+    double2 w;
+    if (A.amg) {
+        const double *ur = A.u_re, *ui = A.u_im;
+        w = hc_tile_spmv_split(r0, A.N, A.rowptr, A.col, A.val, A.val_im, ur, ui, lds);
+    } else {
+        w = hc_tile_spmv(r0, A.N, A.rowptr, A.col, A.val, A.val_im, A.u, lds);
+    }
+    double s4[4] = {0, 0, 0, 0};
     if (i < A.N) {
         A.w[i] = w;
-        const double2 d = cmul(A.u[i], w);
-        s2[0] = d.x;
-        s2[1] = d.y;
+        const double2 u = A.amg ? cx(A.u_re[i], A.u_im[i]) : A.u[i];
+        if (A.amg) A.u[i] = u;
+        const double2 d = cmul(u, w);
+        s4[0] = d.x;
+        s4[1] = d.y;
+        if (A.amg) {
+            const double2 g = cmul(A.r[i], u);
+            s4[2] = g.x;
+            s4[3] = g.y;
+        }
     }
-    hc_block_sum<2>(s2, red);
+    hc_block_sum<4>(s4, red);
     if (threadIdx.x == 0) {
-        A.part[4 * A.G + blockIdx.x] = s2[0];
-        A.part[5 * A.G + blockIdx.x] = s2[1];
+        A.part[4 * A.G + blockIdx.x] = s4[0];
+        A.part[5 * A.G + blockIdx.x] = s4[1];
+        if (A.amg) {
+            A.part[(2 * gpar) * A.G + blockIdx.x] = s4[2];
+            A.part[(2 * gpar + 1) * A.G + blockIdx.x] = s4[3];
+        }
     }
 }
 
@@ -378,7 +441,7 @@ __global__ void __launch_bounds__(kCgBlock) k_hc_spmv(HcArgs A)
 // beta, the reference's stop test |r| / |b| <= Precision; then
 // z = w + beta z, p = u + beta p, x += alpha p, r -= alpha z, u = M^-1 r,
 // partials gamma_it+1, |r_it+1|^2
-__global__ void __launch_bounds__(kHcAxBlock) k_hc_axpy(HcArgs A, long long it, int Ggam)
+__global__ void __launch_bounds__(kHcAxBlock) k_hc_axpy(HcArgs A, long long it, int Ggam, int Grr)
 {
     __shared__ double red[5 * (kHcAxBlock / 64)];
     CcgState *S = A.S;
@@ -389,8 +452,8 @@ __global__ void __launch_bounds__(kHcAxBlock) k_hc_axpy(HcArgs A, long long it, 
     for (int k = threadIdx.x; k < Ggam; k += blockDim.x) {
         s5[0] += A.part[(2 * par) * A.G + k];
         s5[1] += A.part[(2 * par + 1) * A.G + k];
-        s5[2] += A.part[(6 + par) * A.G + k];
     }
+    for (int k = threadIdx.x; k < Grr; k += blockDim.x) s5[2] += A.part[(6 + par) * A.G + k];
     for (int k = threadIdx.x; k < Gcg; k += blockDim.x) {
         s5[3] += A.part[4 * A.G + k];
         s5[4] += A.part[5 * A.G + k];
@@ -430,6 +493,23 @@ __global__ void __launch_bounds__(kHcAxBlock) k_hc_axpy(HcArgs A, long long it, 
     }
     if (stop) return;
     double g[3] = {0, 0, 0};
+    if (A.amg) {   // u = M^-1 r by the V-cycle after this launch: r also split
+        for (int i = blockIdx.x * kHcAxBlock + threadIdx.x; i < A.N; i += gridDim.x * kHcAxBlock) {
+            const double2 z = cadd(A.w[i], cmul(beta, A.z[i]));
+            const double2 pp = cadd(A.u[i], cmul(beta, A.p[i]));
+            const double2 rn = csub(A.r[i], cmul(alpha, z));
+            A.x[i] = cadd(A.x[i], cmul(alpha, pp));
+            A.z[i] = z;
+            A.p[i] = pp;
+            A.r[i] = rn;
+            A.r_re[i] = rn.x;
+            A.r_im[i] = rn.y;
+            g[2] += rn.x * rn.x + rn.y * rn.y;
+        }
+        hc_block_sum<3>(g, red);
+        if (threadIdx.x == 0) A.part[(6 + (int)((it + 1) & 1)) * A.G + blockIdx.x] = g[2];
+        return;
+    }
     for (int i = blockIdx.x * kHcAxBlock + threadIdx.x; i < A.N; i += gridDim.x * kHcAxBlock) {
         const double2 z = cadd(A.w[i], cmul(beta, A.z[i]));
         const double2 pp = cadd(A.u[i], cmul(beta, A.p[i]));
@@ -452,6 +532,48 @@ __global__ void __launch_bounds__(kHcAxBlock) k_hc_axpy(HcArgs A, long long it, 
         A.part[(2 * np + 1) * A.G + blockIdx.x] = g[1];
         A.part[(6 + np) * A.G + blockIdx.x] = g[2];
     }
+}
+
+// the real SPD surrogate the AMG hierarchy is built on: Re A + sgn Im A with
+// the sign that makes the imaginary part (eddy-current mass, loss terms)
+// positive semi-definite, so that the surrogate is spectrally equivalent to A
+__global__ void k_hc_surrogate(int N, double sgn, const int *__restrict__ rowptr, const int *__restrict__ col,
+                               const double *__restrict__ val, const double *__restrict__ val_im,
+                               double *__restrict__ out)
+{
+    // positive off-diagonal parts of sgn Im A (the consistent eddy-current
+    // mass) are lumped onto the diagonal: B stays SPD, within a factor of two
+    // of the unlumped surrogate, and keeps the M-matrix sign pattern the
+    // aggregation's strength test and the Jacobi smoother expect
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    double lump = 0;
+    int kd = -1;
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        const double m = sgn * val_im[k];
+        if (col[k] == i) {
+            kd = k;
+            out[k] = val[k] + m;
+        } else if (m > 0) {
+            lump += m;
+            out[k] = val[k];
+        } else {
+            out[k] = val[k] + m;
+        }
+    }
+    if (kd >= 0) out[kd] += lump;
+}
+// per-block sums of the imaginary diagonal (its sign picks sgn above)
+__global__ void __launch_bounds__(256) k_hc_diag_im(int N, const int *__restrict__ diag,
+                                                    const double *__restrict__ val_im, double *__restrict__ part)
+{
+    __shared__ double red[4];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    double v = (i < N) ? val_im[diag[i]] : 0.0;
+    v = cg_wave_sum(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 inline int nb256(long long n) { return (int)((n + kBlock - 1) / kBlock); }
@@ -767,7 +889,41 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     XFK_CHECK(hipGetLastError());
     XFK_CHECK(hipEventRecord(e1, s));
 
-    // COCG (Jacobi), Chronopoulos-Gear arrangement
+    // COCG, Chronopoulos-Gear arrangement; preconditioner: the AMG V-cycle of
+    // the real surrogate B = Re A + sgn Im A applied to real and imaginary
+    // parts (a real symmetric M keeps COCG's complex-symmetric structure; with
+    // K_r, K_i both positive semi-definite, the eigenvalues of B^-1 (K_r + i K_i)
+    // lie in the box [0,1] x [0,1] away from 0, so the iteration count is the
+    // V-cycle's, not the mesh's), or complex Jacobi
+    bool amg = false;
+    float ms_setup = 0;
+    if (P->precond == XFK_PRECOND_AMG) {
+        const int nbd = nb256(N);
+        XFK_CHECK(P->hc_bval.alloc((size_t)std::max<long long>(P->nnz, nbd)));
+        k_hc_diag_im<<<nbd, 256, 0, s>>>(N, P->diag.p, P->val_im.p, P->hc_bval.p);
+        std::vector<double> hp(nbd);
+        XFK_CHECK(d2h(hp.data(), P->hc_bval.p, sizeof(double) * nbd, s));
+        double sdi = 0;
+        for (double v : hp) sdi += v;
+        k_hc_surrogate<<<nb256(N), kBlock, 0, s>>>(N, sdi >= 0 ? 1.0 : -1.0, P->rowptr.p, P->col.p, P->val.p,
+                                                   P->val_im.p, P->hc_bval.p);
+        if (!P->amg) P->amg = new Amg();
+        P->amg->theta = P->amg_theta;
+        P->amg->sweeps = P->amg_sweeps;
+        P->amg->omega = P->amg_omega;
+        hipEvent_t a0, a1;
+        XFK_CHECK(hipEventCreate(&a0));
+        XFK_CHECK(hipEventCreate(&a1));
+        XFK_CHECK(hipEventRecord(a0, s));
+        const int arc = P->amg->setup(s, N, N, P->rowptr.p, P->col.p, P->hc_bval.p, P->nnz);
+        XFK_CHECK(hipEventRecord(a1, s));
+        XFK_CHECK(hipEventSynchronize(a1));
+        XFK_CHECK(hipEventElapsedTime(&ms_setup, a0, a1));
+        (void)hipEventDestroy(a0);
+        (void)hipEventDestroy(a1);
+        if (arc != XFK_OK && arc != XFK_ERR_UNSUPPORTED) return arc;
+        amg = arc == XFK_OK;
+    }
     const int Gcg = (N + kCgBlock - 1) / kCgBlock, Gax = hc_axpy_grid(N);
     const int G = std::max(Gcg, Gax);
     XFK_CHECK(P->hc_vec.alloc(7 * (size_t)N));
@@ -795,6 +951,19 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     H.part = P->hc_part.p;
     H.G = G;
     H.S = P->hc_state.p;
+    H.amg = amg ? 1 : 0;
+    XFK_CHECK(P->hc_split.alloc(4 * (size_t)N));
+    H.r_re = P->hc_split.p;
+    H.r_im = P->hc_split.p + N;
+    double *u_re = P->hc_split.p + 2 * (size_t)N, *u_im = P->hc_split.p + 3 * (size_t)N;
+    H.u_re = u_re;
+    H.u_im = u_im;
+    const int *done = &P->hc_state.p->done;
+    auto precondition = [&]() -> int {
+        int rc = P->amg->vcycle(s, H.r_re, u_re, done);
+        if (rc == XFK_OK) rc = P->amg->vcycle(s, H.r_im, u_im, done);
+        return rc;
+    };
     k_hdiag_inv<<<nb256(N), kBlock, 0, s>>>(N, P->diag.p, P->val.p, P->val_im.p, dinv, P->hc_state.p);
     XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
     XFK_CHECK(hipStreamSynchronize(s));
@@ -803,14 +972,21 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
         return XFK_ERR_SINGULAR;
     }
     k_hc_init<<<Gcg, kCgBlock, 0, s>>>(H, P->b.p, P->b_im.p);
-    k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H);
+    int prc;
+    if (amg && (prc = precondition()) != XFK_OK) return prc;
+    k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, 0);
     long long it = 0;
-    int batch = 32;
+    int batch = amg ? 8 : 32;
     const long long cap = std::max<long long>(100000, 20LL * N);
     for (;;) {
         for (int k = 0; k < batch; ++k, ++it) {
-            k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, it == 0 ? Gcg : Gax);
-            k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H);
+            if (amg) {
+                k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, Gcg, it == 0 ? Gcg : Gax);
+                if ((prc = precondition()) != XFK_OK) return prc;
+            } else {
+                k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, it == 0 ? Gcg : Gax, it == 0 ? Gcg : Gax);
+            }
+            k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, (int)((it + 1) & 1));
         }
         XFK_CHECK(hipGetLastError());
         XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
@@ -840,7 +1016,12 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     R.nnz = P->nnz;
     R.ncolors = P->ncolors;
     R.color_rounds = P->color_rounds;
-    R.precond = XFK_PRECOND_JACOBI;
+    R.precond = amg ? XFK_PRECOND_AMG : XFK_PRECOND_JACOBI;
+    if (amg) {
+        R.amg_levels = P->amg->stats.levels;
+        R.amg_op_complexity = P->amg->stats.op_complexity;
+        R.ms_amg_setup = ms_setup;
+    }
     P->last = R;
     if (res) *res = R;
     return XFK_OK;

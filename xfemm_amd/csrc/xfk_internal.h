@@ -302,6 +302,8 @@ struct xfk_problem {
     xfk::DBuf<double> hpt_J;                     // 2 per point node: -0.01 J
     int nhpt = 0;
     xfk::DBuf<double2> hc_vec;                   // COCG vectors: x, r, u, w, z, p, dinv (N each)
+    xfk::DBuf<double> hc_split;                  // AMG: r and u split into real / imaginary parts
+    xfk::DBuf<double> hc_bval;                   // AMG: values of the real surrogate Re A + |Im A|
     xfk::DBuf<double> hc_part;                   // per-block partials, 9 arrays
     xfk::DBuf<xfk::CcgState> hc_state;
     xfk::CcgState *hc_host = nullptr;            // pinned mirror

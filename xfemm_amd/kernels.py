@@ -375,7 +375,11 @@ class Harmonic2DProblem:
     def __init__(self, *, x, y, p, lbl, blocks: Sequence[dict], labels: Sequence[dict], frequency: float,
                  lines: Sequence[dict] = (), points: Sequence[dict] = (), circuits: Sequence[dict] = (),
                  marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0, device=0,
-                 problem_type: int = 0, ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0):
+                 problem_type: int = 0, ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0,
+                 precond: str = "amg"):
+        """precond: "amg" (V-cycle of the real SPD surrogate Re A +- Im A, the
+        sign making Im A positive semi-definite, applied to the real and
+        imaginary parts; default) or "jacobi" (complex Jacobi)."""
         L = load_library()
         D, keep = _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision,
                              length_units, coords, relax, problem_type, (ext_zo, ext_ro, ext_ri))
@@ -399,6 +403,7 @@ class Harmonic2DProblem:
         h = C.c_void_p()
         _check(L.xfk_problem_create_harmonic(C.byref(D), C.byref(H), device, C.byref(h)))
         self._h = h
+        _check(L.xfk_set_option(self._h, XFK_OPT_PRECOND, float(PRECONDS[precond])))
         self.result: Optional[Result] = None
 
     def solve(self, rebuild_symbolic: bool = False) -> dict:
