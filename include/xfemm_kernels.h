@@ -149,9 +149,11 @@ enum {
     XFK_OPT_AMG_OMEGA = 4,      /* Jacobi weight factor: weight = omega / rho(D^-1 A) (0..2, default 1.75) */
     XFK_OPT_AMG_REPLICATE = 5,  /* sharded solve: coarse levels of at most this many global rows are
                                    replicated on every rank, larger ones stay sharded (default 250000) */
-    XFK_OPT_AMG_REUSE = 6       /* 1 (default): later Newton iterations of one solve keep the hierarchy
+    XFK_OPT_AMG_REUSE = 6,      /* 1 (default): later Newton iterations of one solve keep the hierarchy
                                    and refresh only the fine-level smoother, rebuilt when the PCG needs
                                    2x the iterations of the last fresh build; 0: rebuild every time */
+    XFK_OPT_AMG_DENSE = 7       /* coarsening stops at a level of at most this many rows, which is
+                                   solved by its dense inverse (16..2048, default 2048) */
 };
 int xfk_set_option(xfk_problem *prob, int option, double value);
 

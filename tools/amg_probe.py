@@ -16,17 +16,21 @@ sweeps = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--sweeps=")] o
 omegas = [float(a.split("=")[1]) for a in sys.argv if a.startswith("--omega=")] or [None]
 reuse = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--reuse=")]
 nojac = "--no-jacobi" in sys.argv
+denses = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--dense=")] or [None]
 for n in cells:
     kw = synth.magnetostatic(n, nonlinear=nonlin)
     sols = {}
     cases = ([] if nojac else ["jacobi"]) + ["amg%d" % k + ("" if w is None else "w%g" % w)
-                                            for k in sweeps for w in omegas]
+                                            + ("" if d is None else "d%d" % d)
+                                            for k in sweeps for w in omegas for d in denses]
     for pc in cases:
         if pc == "jacobi":
             opt = dict(precond="jacobi")
         else:
-            k, _, w = pc[3:].partition("w")
-            opt = dict(precond="amg", amg_sweeps=int(k), amg_omega=float(w) if w else None)
+            k, _, d = pc[3:].partition("d")
+            k, _, w = k.partition("w")
+            opt = dict(precond="amg", amg_sweeps=int(k), amg_omega=float(w) if w else None,
+                       amg_dense=int(d) if d else None)
             if reuse:
                 opt["amg_reuse"] = bool(reuse[0])
         P = kernels.Static2DProblem(device=0, **opt, **kw)

@@ -110,6 +110,7 @@ struct Amg {
     // level has <= rep_rows rows
     bool dist = false;
     int rep_rows = 250000;
+    int dense_max = kAmgDenseMax;     // coarsest level: dense inverse at <= dense_max rows
     int lrep = 0;
     xfk_comm *comm = nullptr;
     int nranks = 1, rank = 0;

@@ -817,7 +817,8 @@ __global__ void k_spgemm_compact(int nrows, int cap, const int *__restrict__ cro
 // a multiple of kBj with an identity tail (ld = padded size), inverted in
 // place by blocked Gauss-Jordan without pivoting (the level operators are
 // symmetric positive semi-definite).  Step k of kBj-wide block columns:
-//     D  = inv(M_kk)                      k_bgj_diag   (one workgroup, LDS)
+//     D  = inv(M_kk)                      k_bgj_diag for k = 0, else workgroup 0
+//                                         of update k-1 (once its tile is final)
 //     T_kj = D M_kj          (j != k)     k_bgj_row
 //     M_kj = T_kj, M_kk = D, C = M_:k      (snapshot of the old column)
 //     M_ij -= C_i T_kj       (i, j != k)  k_bgj_update (tile GEMMs)
@@ -922,23 +923,20 @@ __device__ __forceinline__ void gj_scalar_step(int p, double (&a)[16], double th
     for (int m = 0; m < 16; ++m) a[m] -= (colk[16 * w + m] - (16 * w + m == p ? 1.0 : 0.0)) * r;
 }
 
-__global__ void __launch_bounds__(256) k_bgj_diag(int k, int ld, const double *__restrict__ M,
-                                                  const double *__restrict__ maxd, double *__restrict__ D)
+// lds: 2 * 16 * kBj + 2 * 4 * kBj doubles (16-byte aligned): the double-
+// buffered 16-row slab holding P ([m][j]) and columns P ([i][t])
+constexpr int kBjDiagLds = 2 * 16 * kBj + 2 * 4 * kBj;
+__device__ __forceinline__ void bgj_diag_inv(double (&a)[16], double thr, double *lds)
 {
-    __shared__ __attribute__((aligned(16))) double rowb[2][16 * kBj];  // the 16-row slab holding P: [m][j]
-    __shared__ __attribute__((aligned(16))) double colb[2][kBj * 4];   // columns P: [i][t]
     const int tid = threadIdx.x;
     const int j = tid & 63, w = tid >> 6;
-    const size_t base = (size_t)k * kBj * ld + (size_t)k * kBj;
-    double a[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) a[m] = M[base + (size_t)(16 * w + m) * ld + j];
-    const double thr = 1e-11 * (*maxd);
+    // (buffer pointers by arithmetic on lds: a runtime-indexed pointer array
+    // would hide the LDS address space and turn every access into a flat op)
     int phase = 0;
     for (int p0 = 0; p0 < kBj; p0 += 4) {
         const int buf = phase & 1;
         const int mb = p0 & 15, wp = p0 >> 4;
-        double *R4 = rowb[buf], *C4 = colb[buf];
+        double *R4 = lds + buf * 16 * kBj, *C4 = lds + 32 * kBj + buf * 4 * kBj;
         if (w == wp)   // this wave holds rows P: publish its whole slab (no dynamic register index)
 #pragma unroll
             for (int m = 0; m < 16; ++m) R4[m * kBj + j] = a[m];
@@ -975,7 +973,7 @@ __global__ void __launch_bounds__(256) k_bgj_diag(int k, int ld, const double *_
         if (!ok) {   // a (near) null direction inside the block: scalar steps
             for (int p = p0; p < p0 + 4; ++p) {
                 const int b2 = phase & 1;
-                gj_scalar_step(p, a, thr, rowb[b2], colb[b2]);
+                gj_scalar_step(p, a, thr, lds + b2 * 16 * kBj, lds + 32 * kBj + b2 * 4 * kBj);
                 ++phase;
             }
             continue;
@@ -1010,6 +1008,18 @@ __global__ void __launch_bounds__(256) k_bgj_diag(int k, int ld, const double *_
                         (s2 == 3 ? r[3] : 0.0);
             }
     }
+}
+
+__global__ void __launch_bounds__(256) k_bgj_diag(int k, int ld, const double *__restrict__ M,
+                                                  const double *__restrict__ maxd, double *__restrict__ D)
+{
+    __shared__ __attribute__((aligned(16))) double lds[kBjDiagLds];
+    const int j = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const size_t base = (size_t)k * kBj * ld + (size_t)k * kBj;
+    double a[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) a[m] = M[base + (size_t)(16 * w + m) * ld + j];
+    bgj_diag_inv(a, 1e-11 * (*maxd), lds);
 #pragma unroll
     for (int m = 0; m < 16; ++m) D[(16 * w + m) * kBj + j] = a[m];
 }
@@ -1108,23 +1118,29 @@ __global__ void __launch_bounds__(256) k_bgj_row(int k, int ld, double *__restri
 }
 
 // M_ij -= C_i T_kj (i, j != k) and M_ik = -C_i D (i != k), C_i the snapshot
-// of the old column block
-// jsel >= 0: only block column jsel (grid nbk); else every block column but
-// jskip (grid nbk^2; -1: all)
+// of the old column block.  Workgroup 0 takes tile (k+1, k+1) -- the next
+// pivot block, final after this update -- and, once it is written, inverts it
+// into Dnext while the other workgroups are still updating: the next step
+// needs no separate pivot-block launch on its critical path.
 __global__ void __launch_bounds__(256) k_bgj_update(int k, int nbk, int ld, double *__restrict__ M,
                                                     const double *__restrict__ D, const double *__restrict__ Trow,
-                                                    const double *__restrict__ Csnap, int jsel, int jskip)
+                                                    const double *__restrict__ Csnap, const double *__restrict__ maxd,
+                                                    double *__restrict__ Dnext)
 {
-    const int i = jsel >= 0 ? (int)blockIdx.x : (int)blockIdx.x / nbk;
-    const int j = jsel >= 0 ? jsel : (int)blockIdx.x % nbk;
-    if (i == k || j == jskip) return;
-    __shared__ double Xs[kBj * kXs], Ys[kBj * kYs];
+    const int nt = nbk * nbk, kn = k + 1 < nbk ? k + 1 : 0;
+    const int b = (int)((blockIdx.x + (unsigned)(kn * nbk + kn)) % (unsigned)nt);
+    const int i = b / nbk, j = b % nbk;
+    if (i == k) return;
+    const bool piv = k + 1 < nbk && blockIdx.x == 0;
+    __shared__ __attribute__((aligned(16))) double Xs[kBj * kXs];
+    __shared__ __attribute__((aligned(16))) double Ys[kBj * kYs];
     bgj_load<kXs>(Xs, Csnap + (size_t)i * kBj * kBj, kBj);
     bgj_load<kYs>(Ys, j == k ? D : Trow + (size_t)j * kBj * kBj, kBj);
     __syncthreads();
     dbl4 c[2][2];
     bgj_mm(Xs, Ys, c);
     double *Mij = M + (size_t)i * kBj * ld + (size_t)j * kBj;
+    if (piv) __syncthreads();   // Xs / Ys are reused below
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -1132,9 +1148,19 @@ __global__ void __launch_bounds__(256) k_bgj_update(int k, int nbk, int ld, doub
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 double *e = &Mij[(size_t)bgj_row(ti, r) * ld + bgj_col(tj)];
-                if (j == k) *e = -c[ti][tj][r];
-                else *e -= c[ti][tj][r];
+                const double v = j == k ? -c[ti][tj][r] : *e - c[ti][tj][r];
+                *e = v;
+                if (piv) Xs[bgj_row(ti, r) * kBj + bgj_col(tj)] = v;
             }
+    if (!piv) return;
+    __syncthreads();
+    const int jl = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double a[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) a[m] = Xs[(16 * w + m) * kBj + jl];
+    bgj_diag_inv(a, 1e-11 * (*maxd), Ys);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) Dnext[(16 * w + m) * kBj + jl] = a[m];
 }
 
 // --------------------------------------------------------------------------
@@ -1660,7 +1686,7 @@ int Amg::build(hipStream_t s, int l0)
         AMG_CHECK(wF.alloc(n));
         AMG_CHECK(cnt.alloc((size_t)n + 1));
         k_amg_diag<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
-        if (n <= kAmgDenseMax) {
+        if (n <= dense_max) {
             dense_coarse = true;
             break;
         }
@@ -1722,11 +1748,12 @@ int Amg::build(hipStream_t s, int l0)
         // inverted on a second stream during the rest of the update -- was
         // measured slower: the two cross-stream waits cost ~15 us per step,
         // more than the 25 us pivot-block inversion it hides)
+        // pivot block 0 by itself; pivot block k+1 inverted inside update k
+        k_bgj_diag<<<1, 256, 0, s>>>(0, ld, cinv.p, maxd, Dbuf);
         for (int k = 0; k < nbk; ++k) {
-            double *D = Dbuf;
-            k_bgj_diag<<<1, 256, 0, s>>>(k, ld, cinv.p, maxd, D);
+            double *D = Dbuf + (size_t)(k & 1) * kBj * kBj, *Dn = Dbuf + (size_t)((k + 1) & 1) * kBj * kBj;
             k_bgj_row<<<nbk, 256, 0, s>>>(k, ld, cinv.p, D, Trow, Tcol);
-            if (nbk > 1) k_bgj_update<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, D, Trow, Tcol, -1, -1);
+            if (nbk > 1) k_bgj_update<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, D, Trow, Tcol, maxd, Dn);
         }
         k_dense_unscale<<<(unsigned)(((size_t)ld * ld / 2 + 255) / 256), 256, 0, s>>>(ld, cinv.p, sc);
     }

@@ -561,6 +561,7 @@ static int amg_setup(xfk_problem *P)
     P->amg->sweeps = P->amg_sweeps;
     P->amg->omega = P->amg_omega;
     P->amg->rep_rows = P->amg_replicate;
+    P->amg->dense_max = P->amg_dense;
     hipEvent_t e0, e1;
     XFK_CHECK(hipEventCreate(&e0));
     XFK_CHECK(hipEventCreate(&e1));
@@ -1370,6 +1371,11 @@ int xfk_set_option(xfk_problem *P, int option, double value)
     case XFK_OPT_AMG_REUSE:
         XFK_REQUIRE(value == 0 || value == 1, XFK_ERR_ARG, "AMG reuse is 0 or 1");
         P->amg_reuse = (int)value;
+        return XFK_OK;
+    case XFK_OPT_AMG_DENSE:
+        XFK_REQUIRE(value >= 16 && value <= kAmgDenseMax && value == (int)value, XFK_ERR_ARG,
+                    "AMG dense coarsest size must be 16..2048 rows");
+        P->amg_dense = (int)value;
         return XFK_OK;
     default:
         set_error("unknown option");

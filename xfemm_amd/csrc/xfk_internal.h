@@ -282,6 +282,7 @@ struct xfk_problem {
     double amg_theta = 0.08;
     double amg_omega = 1.75;
     int amg_replicate = 250000;
+    int amg_dense = 2048;
     int amg_reuse = 1;
     bool amg_reusable = false;        // the hierarchy belongs to this solve's matrix pattern
     bool amg_fresh = false;           // built from scratch for the running PCG solve

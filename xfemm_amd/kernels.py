@@ -31,6 +31,7 @@ XFK_OPT_AMG_THETA = 3
 XFK_OPT_AMG_OMEGA = 4
 XFK_OPT_AMG_REPLICATE = 5
 XFK_OPT_AMG_REUSE = 6
+XFK_OPT_AMG_DENSE = 7
 
 # every symbol include/xfemm_kernels.h declares
 EXPORTED = (
@@ -255,7 +256,7 @@ class Static2DProblem:
                  device=0, comm: Optional["Comm"] = None, precond: str = "amg", amg_sweeps: Optional[int] = None,
                  amg_theta: Optional[float] = None, frequency: float = 0.0, amg_omega: Optional[float] = None,
                  amg_replicate: Optional[int] = None, amg_reuse: Optional[bool] = None, problem_type: int = 0,
-                 ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0):
+                 ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0, amg_dense: Optional[int] = None):
         """comm: shard the mesh by row blocks over this communicator (every rank
         passes the same global problem; solve() and solution() are collective).
         precond: "amg" (smoothed-aggregation V-cycle, default) or "jacobi".
@@ -288,6 +289,8 @@ class Static2DProblem:
             self.set_option(XFK_OPT_AMG_REPLICATE, amg_replicate)
         if amg_reuse is not None:
             self.set_option(XFK_OPT_AMG_REUSE, int(bool(amg_reuse)))
+        if amg_dense is not None:
+            self.set_option(XFK_OPT_AMG_DENSE, amg_dense)
         self.n_rows = self.dist_info()["n_own"] if comm is not None else self.n_nodes
         self.result: Optional[Result] = None
 
