@@ -208,17 +208,21 @@ __global__ void k_mis_init(int n, const int *__restrict__ sdeg, unsigned long lo
     if (i < n) key[i] = mis_key(sdeg[i] > 0 ? kStUnd : (sdeg[i] < 0 ? kStIn : 0ull), i);
 }
 
+// Rounds are launched in batches without a host check in between: the
+// undecided flag is double-buffered by round parity (prev = the last round's
+// result, cur = this round's), and once a round leaves nothing undecided the
+// later rounds of the batch exit at once (passing the 0 on).
 __global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
                           const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ in,
-                          unsigned long long *__restrict__ out, int *undecided)
+                          unsigned long long *__restrict__ out, const int *prev, int *cur)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i == 0) *cur = 0;   // k_mis_update of this round runs after this launch
+    if (i >= n || *prev == 0) return;
     unsigned long long m = in[i];
     for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
         if (sflag[k] == 1) m = max(m, in[col[k]]);
     out[i] = m;
-    if (i == 0) *undecided = 0;   // k_mis_update of this round runs after this launch
 }
 
 // second max sweep fused with the state update: an undecided node whose
@@ -226,10 +230,10 @@ __global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__re
 // within distance 2 leaves
 __global__ void k_mis_update(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
                              const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ t1,
-                             unsigned long long *__restrict__ key, int *__restrict__ undecided)
+                             unsigned long long *__restrict__ key, const int *prev, int *undecided)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i >= n || *prev == 0) return;
     const unsigned long long k = key[i];
     if (key_st(k) != kStUnd) return;
     unsigned long long m = t1[i];
@@ -641,12 +645,12 @@ __global__ void k_spgemm_nprod(int nrows, SgX X, SgY Y, int *__restrict__ nprod)
     nprod[row] = c;
 }
 
-// Sub-wave SpGEMM (the fine levels: A P, the prolongator): G lanes per row,
-// 64 / G rows per wavefront.  Groups of one wavefront advance independently;
-// their LDS regions are private, and LDS traffic inside a wavefront is
-// ordered, so no workgroup barriers are needed (wave_barrier keeps the
-// compiler from reordering).
-constexpr int kSwCap = 64;            // rows of at most this many products
+// Sub-wave SpGEMM (the fine levels: A P, the prolongator, R (A P)): G lanes
+// per row, 64 / G rows per wavefront.  Groups of one wavefront advance
+// independently; their LDS regions are private, and LDS traffic inside a
+// wavefront is ordered, so no workgroup barriers are needed (wave_barrier
+// keeps the compiler from reordering).
+constexpr int kSortCap = 256;         // k_spgemm_sort: rows of at most this many products
 
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -655,155 +659,198 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Single-pass sub-wave SpGEMM for rows of at most CAP products: each group of
-// G lanes enumerates its row's products once into LDS (key, value), builds
-// the distinct-column set in an LDS hash, ranks the columns, and lane l sums
-// the products of ranks l, l+G, ... in enumeration order (deterministic).
+// Sort-based single-pass SpGEMM for rows of at most CAP products: a group of
+// G lanes per row (64 / G rows per wavefront).  Lane l expands X entries
+// l, l + G, ... (its Y row) into the row's product list in LDS -- the fixed
+// enumeration order -- then the list is loaded as CAP virtual slots, S = CAP / G
+// consecutive slots per lane in registers, and sorted by column with a bitonic
+// network (in-lane compare-exchanges for distances < S, shuffles across the
+// group for the others).  A segmented inclusive scan then sums each column's
+// products and counts the distinct columns; the last slot of each column
+// writes it at its rank.  The network and the scan are fixed, so the sums
+// are the same bits on every run.  Only the product list (12 B per product)
+// lives in LDS: several times more rows in flight than the hash kernels.
 // The row is written padded (row * CAP) with its length; k_spgemm_compact
 // moves it to its CSR place after the length scan.
 template <bool PMODE, int G, int CAP>
-__global__ void __launch_bounds__(64) k_spgemm_sw1(int nrows, SgX X, SgY Y, int *__restrict__ cnt_out,
-                                                   int *__restrict__ pcol, double *__restrict__ pval)
+__global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int *__restrict__ cnt_out,
+                                                    int *__restrict__ pcol, double *__restrict__ pval)
 {
     constexpr int W = 64 / G;
-    constexpr int H = 2 * CAP;
-    constexpr int kShift = 32 - ilog2(H);
-    __shared__ int hk_all[W][H];
-    __shared__ int hr_all[W][H];
-    __shared__ int lst_all[W][CAP], lslot_all[W][CAP];
+    constexpr int S = CAP / G;
+    static_assert(S >= 1 && S * G == CAP, "CAP must be a multiple of G");
     __shared__ int pk_all[W][CAP];
     __shared__ double pv_all[W][CAP];
-    __shared__ int c_off_all[W][G], c_ys_all[W][G];
-    __shared__ double c_xv_all[W][G];
-    __shared__ int s_cnt_all[W], s_np_all[W];
-
     const int g = threadIdx.x / G, l = threadIdx.x % G;
     const int row = blockIdx.x * W + g;
-    int *hk = hk_all[g], *hr = hr_all[g], *lst = lst_all[g], *lslot = lslot_all[g], *pk = pk_all[g];
+    int *pk = pk_all[g];
     double *pv = pv_all[g];
-    int *c_off = c_off_all[g], *c_ys = c_ys_all[g];
-    double *c_xv = c_xv_all[g];
-    for (int t = l; t < H; t += G) hk[t] = -1;
-    if (l == 0) {
-        s_cnt_all[g] = 0;
-        s_np_all[g] = 0;
-    }
-    wave_lds_sync();
-    if (row >= nrows) return;
-    const int xs = X.rowptr[row], xe = X.rowptr[row + 1];
-    double omega = 0.0, dfi = 0.0;
-    if (PMODE) {
-        omega = X.wF[row];
-        dfi = X.dfinv[row];
-    }
-    // enumerate products into LDS, in the fixed order
+    const bool live = row < nrows;
     int np = 0;
-    for (int e0 = xs; e0 < xe; e0 += G) {
-        const int e = e0 + l;
-        int len = 0, ys = 0;
-        double xv = 0.0;
-        if (e < xe) {
-            const int k = X.col[e];
-            if (k < X.col_lim) {
-                if (PMODE) {
-                    const unsigned char f = X.mask[e];
-                    if (f != 0 && Y.agg[k] >= 0) {
-                        ys = k;
-                        len = 1;
-                        xv = (f == 2) ? 1.0 - omega : -omega * dfi * X.val[e];
+    if (live) {
+        const int xs = X.rowptr[row], xe = X.rowptr[row + 1];
+        double omega = 0.0, dfi = 0.0;
+        if (PMODE) {
+            omega = X.wF[row];
+            dfi = X.dfinv[row];
+        }
+        for (int e0 = xs; e0 < xe; e0 += G) {
+            const int e = e0 + l;
+            int len = 0, ys = 0;
+            double xv = 0.0;
+            if (e < xe) {
+                const int k = X.col[e];
+                if (k < X.col_lim) {
+                    if (PMODE) {
+                        const unsigned char f = X.mask[e];
+                        if (f != 0 && Y.agg[k] >= 0) {
+                            ys = Y.agg[k];
+                            len = 1;
+                            xv = (f == 2) ? 1.0 - omega : -omega * dfi * X.val[e];
+                        }
+                    } else {
+                        ys = Y.rowptr[k];
+                        len = Y.rowptr[k + 1] - ys;
+                        xv = X.val[e];
                     }
-                } else {
-                    ys = Y.rowptr[k];
-                    len = Y.rowptr[k + 1] - ys;
-                    xv = X.val[e];
                 }
             }
-        }
-        int incl = len;
+            int incl = len;
 #pragma unroll
-        for (int off = 1; off < G; off <<= 1) {
-            const int t = __shfl_up(incl, off, G);
-            if (l >= off) incl += t;
-        }
-        const int total = __shfl(incl, G - 1, G);
-        c_off[l] = incl - len;
-        c_ys[l] = ys;
-        c_xv[l] = xv;
-        wave_lds_sync();
-        for (int p = l; p < total; p += G) {
-            int lo = 0, hi = G - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (c_off[mid] <= p) lo = mid;
-                else hi = mid - 1;
+            for (int off = 1; off < G; off <<= 1) {
+                const int t = __shfl_up(incl, off, G);
+                if (l >= off) incl += t;
             }
-            int key;
-            double v;
+            const int total = __shfl(incl, G - 1, G);
+            const int o = np + incl - len;
             if (PMODE) {
-                key = Y.agg[c_ys[lo]];
-                v = c_xv[lo];
-            } else {
-                const int q = c_ys[lo] + (p - c_off[lo]);
-                key = Y.col[q];
-                v = c_xv[lo] * Y.val[q];
-            }
-            pk[np + p] = key;
-            pv[np + p] = v;
-            unsigned h = ((unsigned)key * 2654435761u) >> kShift;
-            for (;;) {   // <= CAP keys in 2 CAP slots: a free slot always exists
-                const int old = atomicCAS(&hk[h], -1, key);
-                if (old == -1) {
-                    atomicAdd(&s_cnt_all[g], 1);
-                    break;
+                if (len) {
+                    pk[o] = ys;
+                    pv[o] = xv;
                 }
-                if (old == key) break;
-                h = (h + 1) & (H - 1);
+            } else {
+                for (int q = 0; q < len; ++q) {
+                    pk[o + q] = Y.col[ys + q];
+                    pv[o + q] = xv * Y.val[ys + q];
+                }
+            }
+            np += total;
+        }
+    }
+    wave_lds_sync();
+    int key[S];
+    double val[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int v = l * S + s;
+        key[s] = v < np ? pk[v] : INT_MAX;
+        val[s] = v < np ? pv[v] : 0.0;
+    }
+    // bitonic sort of the CAP slots (slot v = l * S + s) by key
+#pragma unroll
+    for (int k = 2; k <= CAP; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j < S) {
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const int t = s ^ j;
+                    if (t > s) {
+                        const bool up = ((l * S + s) & k) == 0;
+                        if ((key[s] > key[t]) == up && key[s] != key[t]) {
+                            const int tk = key[s];
+                            key[s] = key[t];
+                            key[t] = tk;
+                            const double tv = val[s];
+                            val[s] = val[t];
+                            val[t] = tv;
+                        }
+                    }
+                }
+            } else {
+                const int lm = j / S;
+                const bool lower = (l & lm) == 0;
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const int ok = __shfl_xor(key[s], lm, G);
+                    const double ov = __shfl_xor(val[s], lm, G);
+                    const bool up = ((l * S + s) & k) == 0;
+                    // the lower slot of an ascending pair keeps the smaller key
+                    const bool take = (lower == up) ? (ok < key[s]) : (ok > key[s]);
+                    if (take) {
+                        key[s] = ok;
+                        val[s] = ov;
+                    }
+                }
             }
         }
-        np += total;
-        wave_lds_sync();
     }
-    // rank the distinct columns
-    for (int t = l; t < H; t += G)
-        if (hk[t] != -1) {
-            const int m = atomicAdd(&s_np_all[g], 1);
-            lst[m] = hk[t];
-            lslot[m] = t;
+    // segmented inclusive scan: head = first slot of a column
+    const int prev_last = __shfl_up(key[S - 1], 1, G);
+    int head[S], nh = 0;
+    double run[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int pk_ = s > 0 ? key[s - 1] : (l > 0 ? prev_last : -1);
+        head[s] = (key[s] != INT_MAX && key[s] != pk_) ? 1 : 0;
+        run[s] = (s > 0 && !head[s]) ? run[s - 1] + val[s] : val[s];
+        nh += head[s];
+    }
+    // carry from earlier lanes into this lane's leading (headless) slots
+    int seg_open = 1;   // no head in this lane yet: the lane continues the previous segment
+#pragma unroll
+    for (int s = 0; s < S; ++s) seg_open &= !head[s];
+    double carry = run[S - 1];   // this lane's trailing partial
+    int hpre = nh;
+    int open = seg_open;
+#pragma unroll
+    for (int off = 1; off < G; off <<= 1) {
+        const double oc = __shfl_up(carry, off, G);
+        const int oo = __shfl_up(open, off, G);
+        const int oh = __shfl_up(hpre, off, G);
+        if (l >= off) {
+            if (open) carry = oc + carry;
+            open = open && oo;
+            hpre += oh;
         }
-    wave_lds_sync();
-    const int cnt = s_np_all[g];
-    for (int m = l; m < cnt; m += G) {
-        const int key = lst[m];
-        int rank = 0;
-        for (int q = 0; q < cnt; ++q) rank += lst[q] < key;
-        hr[lslot[m]] = rank;
-        pcol[(size_t)row * CAP + rank] = key;
     }
-    wave_lds_sync();
-    // product ranks, then ordered sums per owned rank
-    for (int p = l; p < np; p += G) {
-        unsigned h = ((unsigned)pk[p] * 2654435761u) >> kShift;
-        while (hk[h] != pk[p]) h = (h + 1) & (H - 1);
-        pk[p] = hr[h];
+    // carry / head count of the lanes before this one
+    double cin = __shfl_up(carry, 1, G);
+    int hin = __shfl_up(hpre, 1, G);
+    if (l == 0) {
+        cin = 0.0;
+        hin = 0;
     }
-    wave_lds_sync();
-    for (int m = l; m < cnt; m += G) {
-        double sum = 0.0;
-        for (int p = 0; p < np; ++p)
-            if (pk[p] == m) sum += pv[p];
-        pval[(size_t)row * CAP + m] = sum;
+    const int cnt = __shfl(hpre, G - 1, G);
+    if (!live) return;
+    int h = hin;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        bool lead = true;   // slots before this lane's first head continue the incoming segment
+#pragma unroll
+        for (int q = 0; q <= s; ++q) lead = lead && !head[q];
+        const double tot = lead ? cin + run[s] : run[s];
+        h += head[s];
+        const int nk = s + 1 < S ? key[s + 1] : __shfl_down(key[0], 1, G);
+        const bool tail = key[s] != INT_MAX && (nk != key[s] || (s + 1 == S && l == G - 1));
+        if (tail) {
+            pcol[(size_t)row * CAP + h - 1] = key[s];
+            pval[(size_t)row * CAP + h - 1] = tot;
+        }
     }
     if (l == 0) cnt_out[row] = cnt;
 }
 
-// padded rows (row * cap) -> CSR
+// padded rows (row * cap) -> CSR; 16 lanes per row, so a row's reads and
+// writes are contiguous runs
 __global__ void k_spgemm_compact(int nrows, int cap, const int *__restrict__ crow, const int *__restrict__ pcol,
                                  const double *__restrict__ pval, int *__restrict__ ccol, double *__restrict__ cval)
 {
-    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    const int row = (int)(t >> 4), l = (int)(t & 15);
     if (row >= nrows) return;
     const int b = crow[row], n = crow[row + 1] - b;
-    for (int m = 0; m < n; ++m) {
+    for (int m = l; m < n; m += 16) {
         ccol[b + m] = pcol[(size_t)row * cap + m];
         cval[b + m] = pval[(size_t)row * cap + m];
     }
@@ -1443,7 +1490,6 @@ template <bool PMODE>
 int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<int> &crow, DBuf<int> &ccol,
            DBuf<double> &cval, long long &cnnz)
 {
-    constexpr int G = 8;
     AMG_CHECK(M.cnt.alloc((size_t)nrows + 1));
     AMG_CHECK(crow.alloc((size_t)nrows + 1));
     // longest product list -> sub-wave (<= 64 products per row) or wave-per-row kernels
@@ -1457,26 +1503,34 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
         int rc = read_flag(M, s, 3, maxprod);
         if (rc != XFK_OK) return rc;
     }
-    if (maxprod <= kSwCap) {
-        // single pass into padded rows, then scan + compaction
-        const int cap = maxprod <= 16 ? 16 : (maxprod <= 32 ? 32 : 64);
-        const int gsw = (nrows + 64 / G - 1) / (64 / G);
+    if (maxprod <= kSortCap) {
+        // single pass into padded rows (sort-based), then scan + compaction
+        const int cap = maxprod <= 16 ? 16 : maxprod <= 32 ? 32 : maxprod <= 64 ? 64 : maxprod <= 128 ? 128 : 256;
         AMG_CHECK(M.pad_col.alloc((size_t)nrows * cap));
         AMG_CHECK(M.pad_val.alloc((size_t)nrows * cap));
+        int *pc = M.pad_col.p;
+        double *pv = M.pad_val.p;
         if (nrows > 0) {
+            // few lanes per row, 4-8 sorted slots per lane: many rows per
+            // wavefront to overlap their dependent gathers
             if (cap == 16)
-                k_spgemm_sw1<PMODE, G, 16><<<gsw, 64, 0, s>>>(nrows, X, Y, M.cnt.p, M.pad_col.p, M.pad_val.p);
+                k_spgemm_sort<PMODE, 4, 16><<<(nrows + 15) / 16, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv);
             else if (cap == 32)
-                k_spgemm_sw1<PMODE, G, 32><<<gsw, 64, 0, s>>>(nrows, X, Y, M.cnt.p, M.pad_col.p, M.pad_val.p);
+                k_spgemm_sort<PMODE, 8, 32><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv);
+            else if (cap == 64)
+                k_spgemm_sort<PMODE, 8, 64><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv);
+            else if (cap == 128)
+                k_spgemm_sort<PMODE, 16, 128><<<(nrows + 3) / 4, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv);
             else
-                k_spgemm_sw1<PMODE, G, 64><<<gsw, 64, 0, s>>>(nrows, X, Y, M.cnt.p, M.pad_col.p, M.pad_val.p);
+                k_spgemm_sort<PMODE, 32, 256><<<(nrows + 1) / 2, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv);
         }
         int rc = scan_total(M, s, M.cnt.p, crow.p, nrows, cnnz);
         if (rc != XFK_OK) return rc;
         AMG_CHECK(ccol.alloc((size_t)std::max(1LL, cnnz)));
         AMG_CHECK(cval.alloc((size_t)std::max(1LL, cnnz)));
         if (nrows > 0)
-            k_spgemm_compact<<<nb(nrows), kB, 0, s>>>(nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p);
+            k_spgemm_compact<<<(unsigned)(((long long)nrows * 16 + kB - 1) / kB), kB, 0, s>>>(
+                nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p);
         return XFK_OK;
     }
     AMG_CHECK(hipMemsetAsync(M.dev_int.p + 2, 0, 2 * sizeof(int), s));
@@ -1554,7 +1608,7 @@ int Amg::host_ints(int count)
 int Amg::init(hipStream_t s)
 {
     if (!host_int) AMG_CHECK(hipHostMalloc((void **)&host_int, 4 * sizeof(int)));
-    AMG_CHECK(dev_int.alloc(4));
+    AMG_CHECK(dev_int.alloc(6));
     AMG_CHECK(rho.alloc(2 * kAmgMaxLevels));
     AMG_CHECK(hipMemsetAsync(rho.p, 0, sizeof(unsigned long long) * 2 * kAmgMaxLevels, s));
     if (L.empty()) L.emplace_back(new AmgLevel());
@@ -1599,13 +1653,17 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     AMG_CHECK(t1.alloc(n));
     k_mis_init<<<nb(n), kB, 0, s>>>(n, cnt.p, key.p);
     int rounds = 0;
-    for (int batch = 6;; batch = 2) {
+    int *und2 = dev_int.p + 4;   // undecided flag of rounds of parity 0 / 1
+    AMG_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(und2 + 1), 1, 1, s));
+    // (level sizes here need 10-16 rounds: one host check for most levels)
+    for (int batch = 12;; batch = 4) {
         for (int b = 0; b < batch; ++b, ++rounds) {
-            k_mis_max<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, dev_int.p);
-            k_mis_update<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, dev_int.p);
+            int *cur = und2 + (rounds & 1), *prev = und2 + ((rounds + 1) & 1);
+            k_mis_max<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur);
+            k_mis_update<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, prev, cur);
         }
         int und = 0;
-        int rc = read_flag(*this, s, 0, und);
+        int rc = read_flag(*this, s, 4 + ((rounds - 1) & 1), und);
         if (rc != XFK_OK) return rc;
         if (!und) break;
         if (rounds > 4096) {
