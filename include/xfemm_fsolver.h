@@ -64,6 +64,15 @@ const char *xfemm_fsolver_last_error(xfemm_fsolver *s);
  * initial relative permeability in *mu_x.  1 on success. */
 int xfemm_bh_get_slopes(int n, double *B, double *H, double *slope, int lam_type, double lam_fill,
                         double *mu_x);
+/* CMMaterialProp::GetSlopes(omega > 0) with CMSolverMaterialProp::LaminatedBH
+ * (CMaterialProp.cpp:127-348, 1060-1160): the harmonic solver's complex curve.
+ * B, H in place (H gets its real part, H_im the imaginary part), complex knot
+ * slopes in slope / slope_im; *mu_x the initial relative permeability, *mu_max
+ * MuMax.  theta_hn: hysteresis lag (deg); lam_d (mm) and cduct (MS/m) drive
+ * the lamination eddy-current correction.  1 on success. */
+int xfemm_bh_get_slopes_ac(int n, double *B, double *H, double *H_im, double *slope, double *slope_im,
+                           double omega, int lam_type, double lam_fill, double theta_hn, double lam_d,
+                           double cduct, double *mu_x, double *mu_max);
 
 #ifdef __cplusplus
 }

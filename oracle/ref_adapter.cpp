@@ -65,6 +65,48 @@ int ref_block_slopes(const char *block_text, double *B, double *H, double *slope
     return n;
 }
 
+// GetSlopes(omega) (omega > 0: the harmonic solver's complex curve); returns
+// BHpoints (or -1), the complex H and slopes split into re / im arrays.
+int ref_block_slopes_ac(const char *block_text, double omega, double *B, double *Hr, double *Hi, double *Sr,
+                        double *Si, int cap, double *mu_x, double *mu_max)
+{
+    std::istringstream in(block_text);
+    std::ostringstream err;
+    femm::CMSolverMaterialProp prop = femm::CMSolverMaterialProp::fromStream(in, err);
+    if (prop.BHpoints > 0) prop.GetSlopes(omega);
+    int n = prop.BHpoints;
+    if (n > cap) return -1;
+    for (int i = 0; i < n; i++) {
+        B[i] = prop.Bdata[i];
+        Hr[i] = prop.Hdata[i].re;
+        Hi[i] = prop.Hdata[i].im;
+        Sr[i] = prop.slope[i].re;
+        Si[i] = prop.slope[i].im;
+    }
+    *mu_x = prop.mu_x;
+    *mu_max = prop.MuMax;
+    return n;
+}
+
+// Get_v(B) and GetdHdB(B) of the AC-processed block (what the harmonic
+// nonlinear update evaluates, harmonic2d.cpp:648-650), for a batch of B.
+int ref_block_acprops(const char *block_text, double omega, const double *Bq, int nq, double *vr, double *vi,
+                      double *dr, double *di)
+{
+    std::istringstream in(block_text);
+    std::ostringstream err;
+    femm::CMSolverMaterialProp prop = femm::CMSolverMaterialProp::fromStream(in, err);
+    if (prop.BHpoints > 0) prop.GetSlopes(omega);
+    for (int i = 0; i < nq; i++) {
+        CComplex v = prop.Get_v(Bq[i]), d = prop.GetdHdB(Bq[i]);
+        vr[i] = v.re;
+        vi[i] = v.im;
+        dr[i] = d.re;
+        di[i] = d.im;
+    }
+    return prop.BHpoints;
+}
+
 // GetBHProps(B) of the processed block, for a batch of flux densities.
 int ref_block_bhprops(const char *block_text, const double *Bq, int nq, double *v, double *dv)
 {

@@ -165,4 +165,31 @@ int xfemm_bh_get_slopes(int n, double *B, double *H, double *slope, int lam_type
     return 1;
 }
 
+int xfemm_bh_get_slopes_ac(int n, double *B, double *H, double *H_im, double *slope, double *slope_im, double omega,
+                           int lam_type, double lam_fill, double theta_hn, double lam_d, double cduct, double *mu_x,
+                           double *mu_max)
+{
+    if (n < 2 || !B || !H || !H_im || !slope || !slope_im || !(omega >= 0)) return 0;
+    xfemm::CMSolverMaterialProp m;
+    m.BHpoints = n;
+    m.Bdata.assign(B, B + n);
+    m.Hdata.assign(H, H + n);
+    m.LamType = lam_type;
+    m.LamFill = lam_fill;
+    m.Theta_hn = theta_hn;
+    m.Lam_d = lam_d;
+    m.Cduct = cduct;
+    if (!m.GetSlopesAC(omega)) return 0;
+    for (int i = 0; i < n; i++) {
+        B[i] = m.Bdata[i];
+        H[i] = m.Hdata[i];
+        H_im[i] = m.Hdata_im[i];
+        slope[i] = m.slope[i];
+        slope_im[i] = m.slope_im[i];
+    }
+    if (mu_x) *mu_x = m.mu_x;
+    if (mu_max) *mu_max = m.MuMax;
+    return 1;
+}
+
 }  // extern "C"

@@ -53,10 +53,17 @@ struct CMSolverMaterialProp {
     int BHpoints = 0;
     std::vector<double> Bdata, Hdata;   // H real parts (static problems)
     std::vector<double> slope;
+    std::vector<double> Hdata_im, slope_im;   // imaginary parts (GetSlopesAC)
     double MuMax = 0;
 
     // CMMaterialProp::GetSlopes(omega = 0) (CMaterialProp.cpp:127-348)
     bool GetSlopes();
+    // CMMaterialProp::GetSlopes(omega > 0) with CMSolverMaterialProp::LaminatedBH
+    // (CMaterialProp.cpp:127-348, 1060-1160): the effective B-H curve for a
+    // sinusoidal H, the hysteresis-lag kludge, the 1-D lamination eddy-current
+    // solve per curve point, the lamination fill.  Complex H and slopes come
+    // back in Hdata / Hdata_im and slope / slope_im; MuMax is set.
+    bool GetSlopesAC(double omega);
 };
 
 struct CMCircuit {

@@ -63,6 +63,8 @@ def load_library(path: str = FSOLVER_SO):
     L.xfemm_fsolver_last_error.argtypes = [vp]
     L.xfemm_fsolver_last_error.restype = C.c_char_p
     L.xfemm_bh_get_slopes.argtypes = [C.c_int, dptr, dptr, dptr, C.c_int, C.c_double, dptr]
+    L.xfemm_bh_get_slopes_ac.argtypes = [C.c_int, dptr, dptr, dptr, dptr, dptr, C.c_double, C.c_int, C.c_double,
+                                         C.c_double, C.c_double, C.c_double, dptr, dptr]
     _lib = L
     return L
 
@@ -78,6 +80,22 @@ def bh_get_slopes(B, H, lam_type=0, lam_fill=1.0):
                                  S.ctypes.data_as(dptr), lam_type, lam_fill, C.byref(mu)):
         raise ValueError("bad B-H curve")
     return B, H, S, mu.value
+
+
+def bh_get_slopes_ac(B, H, omega, lam_type=0, lam_fill=1.0, theta_hn=0.0, lam_d=0.0, cduct=0.0):
+    """CMMaterialProp::GetSlopes(omega > 0) on a B-H table (the harmonic
+    solver's curve: effective sinusoidal-H amplitude, hysteresis lag,
+    laminations) -> (B, H complex, slope complex, mu_x, MuMax)."""
+    L = load_library()
+    B = np.array(B, dtype=np.float64)
+    H = np.array(H, dtype=np.float64)
+    Hi, S, Si = np.zeros_like(B), np.zeros_like(B), np.zeros_like(B)
+    mu, mm = C.c_double(), C.c_double()
+    if not L.xfemm_bh_get_slopes_ac(len(B), B.ctypes.data_as(dptr), H.ctypes.data_as(dptr), Hi.ctypes.data_as(dptr),
+                                    S.ctypes.data_as(dptr), Si.ctypes.data_as(dptr), omega, lam_type, lam_fill,
+                                    theta_hn, lam_d, cduct, C.byref(mu), C.byref(mm)):
+        raise ValueError("bad B-H curve")
+    return B, H + 1j * Hi, S + 1j * Si, mu.value, mm.value
 
 
 class FSolver:
