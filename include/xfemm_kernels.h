@@ -225,16 +225,27 @@ int xfk_dist_get_info(const xfk_problem *prob, xfk_dist_info *info);
  * (cspars.cpp:822-895, 1062-1081) as the solver.
  *
  * The base descriptor carries the real parts; these arrays (same lengths as
- * desc->blocks / lines / circs) carry what the AC formulation adds.  Linear
- * problems: BHpoints must be 0 and LamType 0 (the reference itself rejects
- * LamType 1/2 in AC analyses; wound regions with proximity effects, LamType
- * > 2, and Case-2 circuits -- specified current in a conducting region,
- * which adds unknowns -- return XFK_ERR_UNSUPPORTED).  Single device.
+ * desc->blocks / lines / circs) carry what the AC formulation adds.  Blocks
+ * with a B-H curve run the reference's successive-approximation loop
+ * (ACSolver 0: averaged secant / incremental permeability per element,
+ * residual correction on the right-hand side, relaxation after 5 iterations,
+ * stop at |dV| / |V| < 100 Precision).  The reference itself rejects LamType
+ * 1/2 in AC analyses; wound regions with proximity effects (LamType > 2),
+ * Case-2 circuits -- specified current in a conducting region, which adds
+ * unknowns -- and the Newton AC solver (ACSolver 1) return
+ * XFK_ERR_UNSUPPORTED.  Single device.
  * ------------------------------------------------------------------------- */
 typedef struct {
     double J_im;                /* imaginary part of the source current density, MA/m^2 */
     double Theta_hx, Theta_hy;  /* hysteresis lag, degrees */
     double Lam_d;               /* lamination thickness, mm */
+    /* nonlinear blocks (desc->blocks[k].BHpoints > 0, LamType 0): the curve
+     * processed by GetSlopes(omega) (xfemm_bh_get_slopes_ac) -- B and the real
+     * parts of H and slope in desc->blocks[k], the imaginary parts here; mu_x /
+     * mu_y there are the curve's initial permeability, Theta_hx / Theta_hy
+     * its Theta_hn.  NULL for linear blocks. */
+    const double *H_im;
+    const double *slope_im;
 } xfk_block_ac_desc;
 
 typedef struct {

@@ -19,7 +19,8 @@ from .oracle import OraPoint, OraStats, _Keep, dptr, iptr, lib, ref
 class OrhBlock(C.Structure):
     _fields_ = [("mu_x", C.c_double), ("mu_y", C.c_double), ("Theta_hx", C.c_double), ("Theta_hy", C.c_double),
                 ("Lam_d", C.c_double), ("LamFill", C.c_double), ("J_re", C.c_double), ("J_im", C.c_double),
-                ("Cduct", C.c_double), ("LamType", C.c_int), ("BHpoints", C.c_int)]
+                ("Cduct", C.c_double), ("LamType", C.c_int), ("BHpoints", C.c_int),
+                ("B", dptr), ("H_re", dptr), ("H_im", dptr), ("S_re", dptr), ("S_im", dptr)]
 
 
 class OrhLabel(C.Structure):
@@ -60,12 +61,13 @@ _GETV = C.CFUNCTYPE(dptr, C.c_void_p)
 _SETVAL = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_double, C.c_double)
 _PAIR = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int)
 _SOLVE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int)
+_WIPE = C.CFUNCTYPE(None, C.c_void_p)
 
 
 class OrhOps(C.Structure):
     _fields_ = [("create", _CREATE), ("destroy", _DESTROY), ("addto", _ADDTO), ("get", _GET), ("put", _PUT),
                 ("b", _GETV), ("V", _GETV), ("setvalue", _SETVAL), ("periodicity", _PAIR),
-                ("antiperiodicity", _PAIR), ("solve", _SOLVE)]
+                ("antiperiodicity", _PAIR), ("solve", _SOLVE), ("wipe", _WIPE)]
 
 
 def _hlib():
@@ -76,6 +78,7 @@ def _hlib():
         L.orh_harmonic2d_system.argtypes = [C.POINTER(OrhProblem), iptr, iptr, dptr, C.c_longlong, dptr,
                                             C.POINTER(C.c_longlong)]
         L.orh_harmonic2d_system.restype = C.c_int
+        L.orh_acprops.argtypes = [C.POINTER(OrhBlock), dptr, C.c_int, dptr, dptr]
         L._orh_ready = True
     return L
 
@@ -91,7 +94,7 @@ def _ref_ops() -> OrhOps:
     return OrhOps(f(_CREATE, "ref_clp_create"), f(_DESTROY, "ref_clp_destroy"), f(_ADDTO, "ref_clp_addto"),
                   f(_GET, "ref_clp_get"), f(_PUT, "ref_clp_put"), f(_GETV, "ref_clp_b"), f(_GETV, "ref_clp_V"),
                   f(_SETVAL, "ref_clp_setvalue"), f(_PAIR, "ref_clp_periodicity"),
-                  f(_PAIR, "ref_clp_antiperiodicity"), f(_SOLVE, "ref_clp_solve"))
+                  f(_PAIR, "ref_clp_antiperiodicity"), f(_SOLVE, "ref_clp_solve"), f(_WIPE, "ref_clp_wipe"))
 
 
 def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
@@ -102,6 +105,10 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
         b.mu_x, b.mu_y, b.Theta_hx, b.Theta_hy = m.mu_x, m.mu_y, m.Theta_hx, m.Theta_hy
         b.Lam_d, b.LamFill, b.J_re, b.J_im, b.Cduct = m.Lam_d, m.LamFill, m.J_re, m.J_im, m.Cduct
         b.LamType, b.BHpoints = m.LamType, m.BHpoints
+        if m.BHpoints:   # the GetSlopes(omega) curve, complex (an input of the restated loop)
+            H, S = np.asarray(m.Hdata, dtype=complex), np.asarray(m.slope, dtype=complex)
+            b.B, b.H_re, b.H_im = keep.d(np.asarray(m.Bdata, float)), keep.d(H.real), keep.d(H.imag)
+            b.S_re, b.S_im = keep.d(S.real), keep.d(S.imag)
     labels = (OrhLabel * max(1, len(pr.labels)))()
     for k, lb in enumerate(pr.labels):
         labels[k].InCircuit, labels[k].bIsWound = lb.InCircuit, int(lb.bIsWound)
@@ -137,7 +144,9 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
 
 
 def solve(pr: femfile.FemProblem, mesh: femfile.Mesh, linprob: str = "oracle"):
-    """Restated linear Harmonic2D.  Returns (A complex per node, stats,
+    """Restated Harmonic2D (linear, or the successive approximation of
+    nonlinear blocks whose femfile.BlockProp carries the GetSlopes(omega)
+    curve: Bdata, complex Hdata / slope).  Returns (A complex per node, stats,
     circuits[(Case, J, dV)] with complex J / dV)."""
     L = _hlib()
     P, keep, circs = make_problem(pr, mesh)

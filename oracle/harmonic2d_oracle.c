@@ -121,6 +121,15 @@ static void *clp_create(int n, int bw, int nodes, double precision)
     return L;
 }
 
+static void clp_wipe(void *lp)
+{   /* cspars.cpp:539-555 */
+    clp *L = (clp *)lp;
+    for (int i = 0; i < L->n; i++) {
+        L->b[i] = C(0, 0);
+        for (int k = 0; k < L->M[i].len; k++) L->M[i].x[k] = C(0, 0);
+    }
+}
+
 static void clp_destroy(void *lp)
 {
     clp *L = (clp *)lp;
@@ -386,7 +395,7 @@ static int clp_solve(void *lp, int flag)
 
 static const orh_linprob_ops g_builtin = {clp_create, clp_destroy, clp_addto, clp_get, clp_put,
                                           clp_b, clp_V, clp_setvalue, clp_periodicity,
-                                          clp_antiperiodicity, clp_solve};
+                                          clp_antiperiodicity, clp_solve, clp_wipe};
 
 const orh_linprob_ops *orh_builtin_linprob(void) { return &g_builtin; }
 
@@ -397,6 +406,77 @@ const orh_linprob_ops *orh_builtin_linprob(void) { return &g_builtin; }
 typedef struct {
     cx mu0, mu1;
 } effmu;
+
+#define ORH_MUO 1.2566370614359173e-6
+
+/* abs(CComplex) (femmcomplex.cpp:749-757) */
+static double cx_abs(cx x)
+{
+    if ((x.re == 0) && (x.im == 0)) return 0.;
+    if (fabs(x.re) > fabs(x.im)) return fabs(x.re) * sqrt(1. + (x.im / x.re) * (x.im / x.re));
+    return fabs(x.im) * sqrt(1. + (x.re / x.im) * (x.re / x.im));
+}
+
+/* ---- the complex curve of a nonlinear block ---- */
+static cx bh_H(const orh_block *b, int i) { return C(b->H_re[i], b->H_im[i]); }
+static cx bh_S(const orh_block *b, int i) { return C(b->S_re[i], b->S_im[i]); }
+
+/* CMMaterialProp::GetH(CComplex) (CMaterialProp.cpp:493-518) for x = B >= 0 */
+static cx bh_geth(const orh_block *m, double B)
+{
+    const int n = m->BHpoints;
+    const double b = B;                 /* abs(CComplex(B)) */
+    if (b == 0) return C(0, 0);
+    const cx pp = cdivd(C(B, 0), b);    /* p = x / b */
+    if (b > m->B[n - 1]) return cmul(pp, cadd(bh_H(m, n - 1), cmuld(bh_S(m, n - 1), b - m->B[n - 1])));
+    for (int i = 0; i < n - 1; i++)
+        if ((b >= m->B[i]) && (b <= m->B[i + 1])) {
+            double l = m->B[i + 1] - m->B[i], z = (b - m->B[i]) / l, z2 = z * z;
+            cx h = dmulc(1. - 3. * z2 + 2. * z2 * z, bh_H(m, i));
+            h = cadd(h, dmulc(z * (1. - 2. * z + z2) * l, bh_S(m, i)));
+            h = cadd(h, dmulc(z2 * (3. - 2. * z), bh_H(m, i + 1)));
+            h = cadd(h, dmulc(z2 * (z - 1.) * l, bh_S(m, i + 1)));
+            return cmul(pp, h);
+        }
+    return C(0, 0);
+}
+
+/* Get_v(B) (CMaterialProp.cpp:899-903): the base-class GetH(double) is the
+ * real part of GetH(CComplex) (:488-491) */
+static cx bh_getv(const orh_block *m, double B)
+{
+    if (B == 0) return bh_S(m, 0);
+    return C(bh_geth(m, B).re / B, 0);
+}
+
+/* GetdHdB(B) (CMaterialProp.cpp:461-486) */
+static cx bh_dhdb(const orh_block *m, double B)
+{
+    const int n = m->BHpoints;
+    const double b = fabs(B);
+    if (b > m->B[n - 1]) return bh_S(m, n - 1);
+    for (int i = 0; i < n - 1; i++)
+        if ((b >= m->B[i]) && (b <= m->B[i + 1])) {
+            double l = m->B[i + 1] - m->B[i], z = (b - m->B[i]) / l;
+            cx h = cdivd(dmulc(6. * z * (z - 1.), bh_H(m, i)), l);
+            h = cadd(h, dmulc(1. - 4. * z + 3. * z * z, bh_S(m, i)));
+            h = cadd(h, cdivd(dmulc(6. * z * (1. - z), bh_H(m, i + 1)), l));
+            h = cadd(h, dmulc(z * (3. * z - 2.), bh_S(m, i + 1)));
+            return h;
+        }
+    return C(0, 0);
+}
+
+void orh_acprops(const orh_block *b, const double *Bq, int nq, double *v, double *dhdb)
+{
+    for (int i = 0; i < nq; i++) {
+        cx a = bh_getv(b, Bq[i]), d = bh_dhdb(b, Bq[i]);
+        v[2 * i] = a.re;
+        v[2 * i + 1] = a.im;
+        dhdb[2 * i] = d.re;
+        dhdb[2 * i + 1] = d.im;
+    }
+}
 
 /* effective permeability of each block (harmonic2d.cpp:190-235) */
 static void effective_mu(const orh_problem *pr, double w, effmu *Mu)
@@ -478,7 +558,8 @@ static void circuits(orh_problem *pr)
     free(I1); free(I2); free(I3);
 }
 
-static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L, const effmu *Mu, double w)
+static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L, const effmu *Mu, double w,
+                           int Iter)
 {
     const double c = ORA_PI * 4.e-05;
     const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
@@ -594,8 +675,27 @@ static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L,
             cx v = cadd(C(gr, gi), Kc);
             ops->put(L, v.re, v.im, cr, cr);
         }
-        /* element permeability (Iter == 0, linear: :481-486) and the global matrices (:600-630) */
+        /* element permeability: Iter 0 / linear blocks the block's (:557-563);
+         * later passes, nonlinear LamType-0 blocks: successive approximation
+         * (:588-660, ACSolver 0) */
         cx mu1 = Mu[pr->blk[i]].mu0, mu2 = Mu[pr->blk[i]].mu1, v12 = C(0, 0);
+        if (Iter > 0 && blk->LamType == 0 && blk->BHpoints > 0 && mu1.re == mu2.re && mu1.im == mu2.im) {
+            cx B1 = C(0, 0), B2 = C(0, 0);
+            for (int j = 0; j < 3; j++) {
+                B1 = cadd(B1, cmuld(VL[n[j]], q[j]));
+                B2 = cadd(B2, cmuld(VL[n[j]], p[j]));
+            }
+            cx s1 = cmul(B1, cconj(B1)), s2 = cmul(B2, cconj(B2));
+            double B = c * sqrt(cx_abs(s1) + cx_abs(s2)) / (0.02 * a);
+            cx murel = ddivc(1., cmuld(bh_getv(blk, B), ORH_MUO));   /* muo * Get_v: CComplex * double */
+            cx muinc = ddivc(1., cmuld(bh_dhdb(blk, B), ORH_MUO));
+            cx K = cdiv(cmul(dmulc(2., murel), muinc), cadd(murel, muinc));
+            mu1 = K;
+            mu2 = K;
+            K = cneg(csub(ddivc(1., murel), ddivc(1., K)));
+            for (int j = 0; j < 3; j++)
+                for (int k = 0; k < 3; k++) Mn[j][k] = cmul(K, cadd(Mx[j][k], My[j][k]));
+        }
         for (int j = 0; j < 3; j++)
             for (int k = 0; k < 3; k++) {
                 Me[j][k] = cadd(Me[j][k], cadd(cadd(cdiv(Mx[j][k], mu2), cdiv(My[j][k], mu1)), cmul(Mxy[j][k], v12)));
@@ -669,7 +769,9 @@ static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L,
 static int check_linear(const orh_problem *pr)
 {
     for (int k = 0; k < pr->n_blocks; k++) {
-        if (pr->blocks[k].BHpoints != 0) return 0;
+        if (pr->blocks[k].BHpoints != 0 && !(pr->blocks[k].B && pr->blocks[k].H_re && pr->blocks[k].H_im &&
+                                             pr->blocks[k].S_re && pr->blocks[k].S_im))
+            return 0;
         if (pr->blocks[k].LamType == 1 || pr->blocks[k].LamType == 2 || pr->blocks[k].LamType > 2) return 0;
     }
     return 1;
@@ -686,9 +788,48 @@ int orh_harmonic2d(orh_problem *pr, const orh_linprob_ops *ops, double *A_out, o
     circuits(pr);
     effective_mu(pr, w, Mu);
     void *L = ops->create(n, pr->bandwidth, NN, pr->precision);
-    assemble_and_bc(pr, ops, L, Mu, w);
-    g_iters = -1;
-    int ok = ops->solve(L, 0);
+    /* LinearFlag = false when any element lies in a B-H block (:559-569) */
+    int linear = 1;
+    for (int i = 0; i < pr->n_elems && linear; i++) linear = pr->blocks[pr->blk[i]].BHpoints == 0;
+    cx *Vold = (cx *)calloc(n, sizeof(cx));
+    double res = 0, lastres = 0, Relax = 1.;   /* FSolver::Relax (fsolver.cpp:210) */
+    int Iter = 0, ok = 0;
+    long long iters_total = 0;
+    do {   /* :219-873 */
+        if (Iter > 0) ops->wipe(L);
+        assemble_and_bc(pr, ops, L, Mu, w, Iter);
+        cx *VL = (cx *)ops->V(L);
+        for (int j = 0; j < n; j++) Vold[j] = VL[j];
+        g_iters = -1;
+        ok = ops->solve(L, Iter);
+        if (!ok) break;
+        if (g_iters > 0) iters_total += g_iters;
+        VL = (cx *)ops->V(L);
+        if (!linear) {
+            double x = 0, y = 0;
+            for (int j = 0; j < NN; j++) {
+                x += cmul(csub(VL[j], Vold[j]), cconj(csub(VL[j], Vold[j]))).re;
+                y += cmul(VL[j], cconj(VL[j])).re;
+            }
+            if (y == 0) linear = 1;
+            else {
+                lastres = res;
+                res = sqrt(x / y);
+            }
+            if (Iter > 5) {
+                if ((res > lastres) && (Relax > 0.1)) Relax /= 2.;
+                else Relax += 0.1 * (1. - Relax);
+                for (int j = 0; j < n; j++) VL[j] = cadd(dmulc(Relax, VL[j]), dmulc(1.0 - Relax, Vold[j]));
+            }
+        }
+        if ((res < 100. * pr->precision) && Iter > 0) linear = 1;
+        Iter++;
+        if (Iter > 1000) {
+            ok = 0;
+            break;
+        }
+    } while (!linear);
+    free(Vold);
     if (ok) {
         const cx *V = (const cx *)ops->V(L);
         for (int i = 0; i < NN; i++) {
@@ -703,9 +844,9 @@ int orh_harmonic2d(orh_problem *pr, const orh_linprob_ops *ops, double *A_out, o
             }
     }
     if (stats) {
-        stats->newton_iters = 1;
-        stats->cg_iters = (ops == orh_builtin_linprob()) ? g_iters : -1;
-        stats->last_res = 0;
+        stats->newton_iters = Iter;
+        stats->cg_iters = (ops == orh_builtin_linprob()) ? iters_total : -1;
+        stats->last_res = res;
     }
     ops->destroy(L);
     free(Mu);
@@ -722,7 +863,7 @@ int orh_harmonic2d_system(orh_problem *pr, int *rows, int *cols, double *vals, l
     circuits(pr);
     effective_mu(pr, w, Mu);
     clp *L = (clp *)clp_create(n, pr->bandwidth, NN, pr->precision);
-    assemble_and_bc(pr, orh_builtin_linprob(), L, Mu, w);
+    assemble_and_bc(pr, orh_builtin_linprob(), L, Mu, w, 0);
     long long k = 0;
     for (int i = 0; i < NN; i++) {
         const crow *r = &L->M[i];

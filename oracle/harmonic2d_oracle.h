@@ -8,10 +8,16 @@
  *   CBigComplexLinProb                cfemm/libfemm/cspars.cpp:40-1081
  *     (upper-triangular linked rows, complex-symmetric MultA, SSOR MultPC,
  *      SetValue, (Anti)Periodicity, PCGSQStart + PBCGSolve = PBCGSolveMod)
- *   FSolver::Harmonic2D, linear       cfemm/fsolver/harmonic2d.cpp:36-790
+ *   FSolver::Harmonic2D               cfemm/fsolver/harmonic2d.cpp:36-873
  *     (effective permeabilities with hysteresis lag and laminations, eddy
  *      currents, mixed and small-skin-depth boundaries, complex sources,
- *      circuits of Case 0 / 1 / 2, point currents, Dirichlet, periodicity)
+ *      circuits of Case 0 / 1 / 2, point currents, Dirichlet, periodicity;
+ *      nonlinear blocks: the successive approximation of ACSolver 0 --
+ *      averaged permeability from Get_v / GetdHdB, the Mn V correction,
+ *      relaxation -- on the complex curve GetSlopes(omega) produced, which is
+ *      an INPUT here: the host restatement of that preprocessing is pinned
+ *      separately against the reference's CMaterialProp.cpp,
+ *      tests/test_oracle_acslopes.py)
  *
  * As for the static oracle, the linear algebra is reached through
  * orh_linprob_ops so the restated element loop can drive either the restated
@@ -35,7 +41,9 @@ typedef struct {
     double J_re, J_im;          /* MA/m^2 */
     double Cduct;               /* MS/m */
     int LamType;
-    int BHpoints;               /* must be 0: the oracle restates the linear path */
+    int BHpoints;               /* 0 = linear */
+    /* BHpoints > 0: the curve processed by GetSlopes(omega) (B, complex H, complex slope) */
+    const double *B, *H_re, *H_im, *S_re, *S_im;
 } orh_block;
 
 typedef struct {
@@ -89,13 +97,18 @@ typedef struct {
     void (*periodicity)(void *L, int i, int j);
     void (*antiperiodicity)(void *L, int i, int j);
     int (*solve)(void *L, int flag);   /* PBCGSolveMod(flag, false) */
+    void (*wipe)(void *L);             /* Wipe(): matrix and b to zero, V kept */
 } orh_linprob_ops;
 
 const orh_linprob_ops *orh_builtin_linprob(void);
 
-/* FSolver::Harmonic2D (linear problems); A = V * c (the values written to
- * .ans), interleaved re/im per node; circuit results in pr->circs. */
+/* FSolver::Harmonic2D; A = V * c (the values written to .ans), interleaved
+ * re/im per node; circuit results in pr->circs. */
 int orh_harmonic2d(orh_problem *pr, const orh_linprob_ops *ops, double *A_out, ora_stats *stats);
+
+/* Get_v(B) and GetdHdB(B) of a nonlinear block's complex curve
+ * (CMaterialProp.cpp:461-486, 899-903), interleaved re/im, for nq values. */
+void orh_acprops(const orh_block *b, const double *Bq, int nq, double *v, double *dhdb);
 
 /* The assembled system after all boundary conditions (node rows only), as
  * upper-triangular COO (interleaved complex values) plus b. */

@@ -149,5 +149,6 @@ void ref_clp_setvalue(void *L, int i, double xr, double xi) { CL(L)->SetValue(i,
 void ref_clp_periodicity(void *L, int i, int j) { CL(L)->Periodicity(i, j); }
 void ref_clp_antiperiodicity(void *L, int i, int j) { CL(L)->AntiPeriodicity(i, j); }
 int ref_clp_solve(void *L, int flag) { return CL(L)->PBCGSolveMod(flag, false) ? 1 : 0; }
+void ref_clp_wipe(void *L) { CL(L)->Wipe(); }
 
 }  // extern "C"

@@ -167,3 +167,52 @@ def test_harmonic_file_interface_end_to_end(tmp_path):
     assert rel_err(A, Ao) <= max(TOL_A, 2.0 * rel_err(Ao, exact))
     assert np.array_equal(els[:, :3], mesh.p) and np.array_equal(els[:, 3], mesh.lbl)
     assert open(base + ".ans").read().startswith(open(base + ".fem").read())
+
+
+@pytest.mark.parametrize("cells", [10, 20, 40])
+def test_harmonic_nonlinear_matches_oracle(cells):
+    """Successive approximation of a nonlinear AC problem (M-19 steel on its
+    GetSlopes(omega) curve: hysteresis lag, lamination eddy currents): A at
+    every node vs the oracle (whose loop is bit-identical to the reference's
+    cspars.cpp solver), within 1e-5 of max |A| -- both loops stop at
+    |dV| / |V| < 100 Precision, from COCG solves that each stop at Precision
+    with different preconditioners."""
+    kw = synth.harmonic(cells, nonlinear=True)
+    pr, mesh, kk = _problem(kw)
+    Ao, st, _ = oh.solve(pr, mesh)
+    P = kernels.Harmonic2DProblem(**kk)
+    r = P.solve()
+    A = P.solution()
+    P.close()
+    assert st["newton_iters"] > 1 and r["newton_iters"] > 1
+    assert rel_err(A, Ao) <= 1e-5
+    assert abs(r["newton_iters"] - st["newton_iters"]) <= max(3, st["newton_iters"] // 5)
+
+
+def test_harmonic_nonlinear_file_interface_end_to_end(tmp_path):
+    """.fem with a nonlinear laminated lossy steel (raw M-19 points, Sigma,
+    d_lam, Phi_h) -> FSolver (GetSlopes(omega) on the host, successive
+    approximation on the GPU) -> .ans, against the oracle."""
+    from xfemm_amd import fsolver
+    kw = synth.harmonic(16, circuits=False, nonlinear=True)
+    kw["marker"] = None
+    kw["points"] = []
+    base = str(tmp_path / "hn")
+    synth.write_problem(base, kw)
+    from oracle import femfile
+    pr, mesh = femfile.load_problem(base)   # the files' node order (as in the .ans)
+    for m in pr.blocks:
+        if m.BHpoints:   # the harmonic curve of the raw points (GetSlopes(omega))
+            B, H, S, mu, _ = fsolver.bh_get_slopes_ac(*synth.m19_curve(), 2 * np.pi * pr.Frequency, m.LamType,
+                                                      m.LamFill, m.Theta_hn, m.Lam_d, m.Cduct)
+            m.Bdata, m.Hdata, m.slope, m.mu_x, m.mu_y = list(B), list(H), list(S), mu, mu
+            m.Theta_hx = m.Theta_hy = m.Theta_hn
+    Ao, st, _ = oh.solve(pr, mesh)
+    assert st["newton_iters"] > 1
+    fs = fsolver.FSolver()
+    fs.PathName = base
+    assert fs.LoadProblemFile()
+    assert fs.runSolver(False), fs.last_error()
+    nodes, _ = _read_harmonic_ans(base + ".ans")
+    A = nodes[:, 2] + 1j * nodes[:, 3]
+    assert rel_err(A, Ao) <= 1e-5

@@ -51,7 +51,11 @@ def synth_to_oracle(kw: dict):
                               LamFill=b.get("LamFill", 1.0), LamType=b.get("LamType", 0),
                               J_im=b.get("J_im", 0.0), Theta_hx=b.get("Theta_hx", 0.0),
                               Theta_hy=b.get("Theta_hy", 0.0), Lam_d=b.get("Lam_d", 0.0))
-        if b.get("bh") == "M19":
+        if len(b.get("B", ())) and np.iscomplexobj(b["H"]):
+            # harmonic: the GetSlopes(omega) curve (host restatement, pinned
+            # against the reference by tests/test_oracle_acslopes.py)
+            m.BHpoints, m.Bdata, m.Hdata, m.slope = len(b["B"]), list(b["B"]), list(b["H"]), list(b["slope"])
+        elif b.get("bh") == "M19":
             B, H = synth.m19_curve()
             m.BHpoints, m.Bdata, m.Hdata = len(B), list(B), list(H)
             femfile.get_slopes(m)

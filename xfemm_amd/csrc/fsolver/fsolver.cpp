@@ -57,9 +57,12 @@ bool FSolver::LoadProblemFile()
         warn("previous-solution (incremental/frozen permeability) problems are not supported by this solver build\n");
         return false;
     }
+    // B-H curves: GetSlopes(Frequency * 2 pi) (fsolver.cpp:241-276; the
+    // harmonic curve is complex: effective sinusoidal-H amplitude, hysteresis
+    // lag, lamination eddy currents)
     for (auto &prop : blockproplist)
         if (prop.BHpoints > 0) {
-            if (!prop.GetSlopes()) {
+            if (!(Frequency != 0 ? prop.GetSlopesAC(Frequency * 2. * kPi) : prop.GetSlopes())) {
                 warn("bad B-H curve in material " + prop.BlockName + "\n");
                 return false;
             }
@@ -481,9 +484,18 @@ int FSolver::Harmonic2D()
     DescStore ds;
     if (!make_desc(ds)) return false;
     std::vector<xfk_block_ac_desc> bac(blockproplist.size());
+    bool nonlinear = false;
     for (size_t k = 0; k < blockproplist.size(); k++) {
         const CMSolverMaterialProp &m = blockproplist[k];
-        bac[k] = xfk_block_ac_desc{m.J_im, m.Theta_hx, m.Theta_hy, m.Lam_d};
+        const bool bh = m.BHpoints > 0;
+        nonlinear = nonlinear || bh;
+        bac[k] = xfk_block_ac_desc{m.J_im, m.Theta_hx, m.Theta_hy, m.Lam_d, bh ? m.Hdata_im.data() : nullptr,
+                                   bh ? m.slope_im.data() : nullptr};
+    }
+    if (nonlinear && ACSolver == 1) {
+        warn("the Newton AC solver ([ACSolver] = 1) is not supported by this solver build; "
+             "use successive approximation ([ACSolver] = 0)\n");
+        return false;
     }
     std::vector<xfk_line_ac_desc> lac(lineproplist.size());
     for (size_t k = 0; k < lineproplist.size(); k++) {

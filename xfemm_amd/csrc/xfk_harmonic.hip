@@ -80,11 +80,60 @@ struct HarmArgs {
     const DevCircAC *circs;
     double *val, *val_im, *b, *b_im;
     double w;
+    // successive approximation (nonlinear blocks, iter > 0)
+    int iter;
+    const double2 *V;                  // the current iterate
+    const double *bhB;                 // complex B-H curves (DevBlockAC::bh_off / bh_n)
+    const double2 *bhH, *bhS;
 };
 
-// One colour of the element loop (harmonic2d.cpp:352-630, linear: Iter == 0,
-// Mn == 0, v12 == 0): element matrices, eddy-current and boundary terms,
-// sources, colour-exclusive scatter into the complex CSR.
+// Get_v(B) of the harmonic solver's curve (CMaterialProp.cpp:899-903): the
+// base-class GetH(double), i.e. the REAL part of the Hermite interpolant
+// (CMaterialProp.cpp:488-518), over B; slope[0] at B = 0
+__device__ double2 hbh_v(double Bq, int n, const double *__restrict__ B, const double2 *__restrict__ H,
+                         const double2 *__restrict__ S)
+{
+    if (Bq == 0) return S[0];
+    const double b = fabs(Bq);
+    double h = 0.0;
+    if (b > B[n - 1]) {
+        h = H[n - 1].x + S[n - 1].x * (b - B[n - 1]);
+    } else {
+        for (int i = 0; i < n - 1; i++)
+            if ((b >= B[i]) && (b <= B[i + 1])) {
+                const double l = B[i + 1] - B[i], z = (b - B[i]) / l, z2 = z * z;
+                h = (1. - 3. * z2 + 2. * z2 * z) * H[i].x + z * (1. - 2. * z + z2) * l * S[i].x +
+                    z2 * (3. - 2. * z) * H[i + 1].x + z2 * (z - 1.) * l * S[i + 1].x;
+                break;
+            }
+    }
+    return cx(h / Bq, 0.0);
+}
+
+// GetdHdB(B) on the complex curve (CMaterialProp.cpp:461-486)
+__device__ double2 hbh_dhdb(double Bq, int n, const double *__restrict__ B, const double2 *__restrict__ H,
+                            const double2 *__restrict__ S)
+{
+    const double b = fabs(Bq);
+    if (b > B[n - 1]) return S[n - 1];
+    for (int i = 0; i < n - 1; i++)
+        if ((b >= B[i]) && (b <= B[i + 1])) {
+            const double l = B[i + 1] - B[i], z = (b - B[i]) / l;
+            const double c0 = 6. * z * (z - 1.), c1 = 1. - 4. * z + 3. * z * z, c2 = 6. * z * (1. - z),
+                         c3 = z * (3. * z - 2.);
+            double2 h = cx(c0 * H[i].x / l, c0 * H[i].y / l);
+            h = cadd(h, cscale(S[i], c1));
+            h = cadd(h, cx(c2 * H[i + 1].x / l, c2 * H[i + 1].y / l));
+            return cadd(h, cscale(S[i + 1], c3));
+        }
+    return cx(0, 0);
+}
+
+// One colour of the element loop (harmonic2d.cpp:352-700; v12 == 0):
+// element matrices, eddy-current and boundary terms, sources, for nonlinear
+// blocks after the first pass the averaged permeability of the element's
+// flux density and the residual correction Mn V (successive approximation,
+// harmonic2d.cpp:616-660), colour-exclusive scatter into the complex CSR.
 __global__ void __launch_bounds__(kBlock) k_hassemble_color(int begin, int end, HarmArgs A)
 {
     __shared__ int s_slot[kBlock * 9 + kBlock / 8];
@@ -167,14 +216,39 @@ __global__ void __launch_bounds__(kBlock) k_hassemble_color(int begin, int end, 
     be[0] = cadd(be[0], Ks);
     be[1] = cadd(be[1], Ks);
     be[2] = cadd(be[2], Ks);
-    // Mx / mu2 + My / mu1 (harmonic2d.cpp:600-612)
-    const double2 r1 = crecip(bp.mu1), r2 = crecip(bp.mu2);
+    double2 mu1 = bp.mu1, mu2 = bp.mu2;
+    double2 Kn = cx(0, 0);
+    const bool nl = bp.bh_n > 0 && A.iter > 0;
+    if (nl) {
+        // flux density of the element from the current iterate
+        double2 B1 = cx(0, 0), B2 = cx(0, 0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const double2 v = A.V[n[j]];
+            B1 = cadd(B1, cscale(v, q[j]));
+            B2 = cadd(B2, cscale(v, p[j]));
+        }
+        const double s1 = B1.x * B1.x - B1.y * (-B1.y), s2 = B2.x * B2.x - B2.y * (-B2.y);
+        const double B = kC * sqrt(fabs(s1) + fabs(s2)) / (0.02 * a);
+        const double *cb = A.bhB + bp.bh_off;
+        const double2 *ch = A.bhH + bp.bh_off, *cs = A.bhS + bp.bh_off;
+        const double2 gv = hbh_v(B, bp.bh_n, cb, ch, cs), gd = hbh_dhdb(B, bp.bh_n, cb, ch, cs);
+        const double2 murel = crecip(cscale(gv, kMUO)), muinc = crecip(cscale(gd, kMUO));
+        const double2 Ka = cdiv(cmul(cscale(murel, 2.), muinc), cadd(murel, muinc));   // averaged
+        mu1 = Ka;
+        mu2 = Ka;
+        const double2 d = csub(crecip(murel), crecip(Ka));
+        Kn = cx(-d.x, -d.y);
+    }
+    // Mx / mu2 + My / mu1 (+ Mn, the correction moved to the right-hand side)
+    const double2 r1 = crecip(mu1), r2 = crecip(mu2);
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const double mx = K * p[j] * p[k], my = K * q[j] * q[k];
             Me[j][k] = cadd(Me[j][k], cadd(cscale(r2, mx), cscale(r1, my)));
+            if (nl) be[j] = cadd(be[j], cmul(cscale(Kn, mx + my), A.V[n[k]]));
         }
     const int *sl = &s_slot[li * 9 + (li >> 3)];
 #pragma unroll
@@ -358,16 +432,25 @@ struct HcArgs {
     const double *u_re, *u_im;
 };
 
-// r = b - A x0 (x0 = 0), u = M^-1 r, z = p = 0; partials gamma_0, |r0|^2, |b|^2
+// r = b - A x0, u = M^-1 r, z = p = 0; partials gamma_0, |r0|^2, |b|^2.
+// WARM: x0 is the current iterate (later passes of the nonlinear loop:
+// PBCGSolveMod(Iter > 0) keeps V), else x0 = 0
+template <bool WARM>
 __global__ void __launch_bounds__(kCgBlock) k_hc_init(HcArgs A, const double *__restrict__ b,
                                                       const double *__restrict__ b_im)
 {
-    __shared__ double red[3 * (kCgBlock / 64) + 3];
+    __shared__ double red[4 * (kCgBlock / 64) + 4];
+    __shared__ double2 lds[WARM ? kHcCap : 1];
     const int i = blockIdx.x * kCgBlock + threadIdx.x;
+    double2 ax = cx(0, 0);
+    if (WARM) ax = hc_tile_spmv(blockIdx.x * kCgBlock, A.N, A.rowptr, A.col, A.val, A.val_im, A.x, lds);
     double v[4] = {0, 0, 0, 0};
+    double bb = 0;
     if (i < A.N) {
-        const double2 rr = cx(b[i], b_im[i]);
-        A.x[i] = cx(0, 0);
+        const double2 bi = cx(b[i], b_im[i]);
+        const double2 rr = WARM ? csub(bi, ax) : bi;
+        bb = bi.x * bi.x + bi.y * bi.y;
+        if (!WARM) A.x[i] = cx(0, 0);
         A.r[i] = rr;
         A.z[i] = cx(0, 0);
         A.p[i] = cx(0, 0);
@@ -383,16 +466,42 @@ __global__ void __launch_bounds__(kCgBlock) k_hc_init(HcArgs A, const double *__
         }
         v[2] = rr.x * rr.x + rr.y * rr.y;
     }
-    double s3[3] = {v[0], v[1], v[2]};
-    hc_block_sum<3>(s3, red);
+    double s4[4] = {v[0], v[1], v[2], bb};
+    hc_block_sum<4>(s4, red);
     if (threadIdx.x == 0) {
         if (!A.amg) {
-            A.part[0 * A.G + blockIdx.x] = s3[0];
-            A.part[1 * A.G + blockIdx.x] = s3[1];
+            A.part[0 * A.G + blockIdx.x] = s4[0];
+            A.part[1 * A.G + blockIdx.x] = s4[1];
         }
-        A.part[6 * A.G + blockIdx.x] = s3[2];
-        A.part[8 * A.G + blockIdx.x] = s3[2];   // |b|^2 = |r0|^2 (x0 = 0)
+        A.part[6 * A.G + blockIdx.x] = s4[2];
+        A.part[8 * A.G + blockIdx.x] = s4[3];
     }
+}
+
+// nonlinear loop: sum |V - V_old|^2 and |V|^2 over the nodes (harmonic2d.cpp:831-845)
+__global__ void __launch_bounds__(256) k_hres(int N, const double2 *__restrict__ V, const double2 *__restrict__ Vo,
+                                              double *__restrict__ part)
+{
+    __shared__ double red[2 * 4 + 2];
+    double s2[2] = {0, 0};
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < N; i += gridDim.x * 256) {
+        const double2 d = csub(V[i], Vo[i]), v = V[i];
+        s2[0] += d.x * d.x - d.y * (-d.y);
+        s2[1] += v.x * v.x - v.y * (-v.y);
+    }
+    hc_block_sum<2>(s2, red);
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = s2[0];
+        part[gridDim.x + blockIdx.x] = s2[1];
+    }
+}
+// V = Relax V + (1 - Relax) V_old (harmonic2d.cpp:851)
+__global__ void k_hrelax(int N, double relax, double2 *__restrict__ V, const double2 *__restrict__ Vo)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const double2 v = V[i], o = Vo[i];
+    V[i] = cx(relax * v.x + (1.0 - relax) * o.x, relax * v.y + (1.0 - relax) * o.y);
 }
 
 // w = A u; partials delta = u.w (unconjugated).  AMG mode: u is gathered from
@@ -645,8 +754,11 @@ int harmonic_validate(const xfk_problem_desc *d, const xfk_harmonic_desc *ac)
     XFK_REQUIRE(d->n_lines == 0 || ac->lines, XFK_ERR_ARG, "missing AC boundary table");
     XFK_REQUIRE(d->n_circs == 0 || ac->circs, XFK_ERR_ARG, "missing AC circuit table");
     for (int k = 0; k < d->n_blocks; ++k) {
-        XFK_REQUIRE(d->blocks[k].BHpoints == 0, XFK_ERR_UNSUPPORTED,
-                    "nonlinear (B-H) materials in harmonic problems are not supported by this build");
+        if (d->blocks[k].BHpoints > 0) {
+            XFK_REQUIRE(ac->blocks[k].H_im && ac->blocks[k].slope_im && d->blocks[k].B && d->blocks[k].H &&
+                            d->blocks[k].slope && d->blocks[k].BHpoints >= 2,
+                        XFK_ERR_ARG, "nonlinear harmonic block needs its complex B-H curve (GetSlopes(omega))");
+        }
         XFK_REQUIRE(d->blocks[k].LamType != 1 && d->blocks[k].LamType != 2, XFK_ERR_UNSUPPORTED,
                     "On-edge lamination not supported in AC analyses");   // harmonic2d.cpp:76-85
         XFK_REQUIRE(d->blocks[k].LamType <= 2, XFK_ERR_UNSUPPORTED,
@@ -680,7 +792,30 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
 
     // blocks, lines
     std::vector<DevBlockAC> blk(std::max(1, d->n_blocks));
-    for (int k = 0; k < d->n_blocks; ++k) blk[k] = effective_block(d->blocks[k], ac->blocks[k], w);
+    std::vector<double> bhB;
+    std::vector<double2> bhH, bhS;
+    for (int k = 0; k < d->n_blocks; ++k) {
+        blk[k] = effective_block(d->blocks[k], ac->blocks[k], w);
+        const xfk_block_desc &b = d->blocks[k];
+        if (b.BHpoints > 0) {   // the complex curve of GetSlopes(omega)
+            blk[k].bh_n = b.BHpoints;
+            blk[k].bh_off = (int)bhB.size();
+            for (int i = 0; i < b.BHpoints; ++i) {
+                bhB.push_back(b.B[i]);
+                bhH.push_back(cx(b.H[i], ac->blocks[k].H_im[i]));
+                bhS.push_back(cx(b.slope[i], ac->blocks[k].slope_im[i]));
+            }
+        }
+    }
+    // the reference starts its successive approximation when any element
+    // lies in a block with a B-H curve (harmonic2d.cpp:559-569)
+    bool nonlin = false;
+    for (int i = 0; i < NE && !nonlin; ++i) nonlin = blk[G.lab[d->lbl[i]].blk].bh_n > 0;
+    if (bhB.empty()) {
+        bhB.push_back(0.0);
+        bhH.push_back(cx(0, 0));
+        bhS.push_back(cx(0, 0));
+    }
     std::vector<DevLineAC> lin(std::max(1, d->n_lines));
     for (int k = 0; k < d->n_lines; ++k) {
         DevLineAC &o = lin[k];
@@ -794,7 +929,7 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     if (rc != XFK_OK) return rc;
     P->harmonic = true;
     P->omega = w;
-    P->any_nonlinear = false;
+    P->any_nonlinear = nonlin;
     P->hcircs = circ;
     P->nhpt = (int)pt_nodes.size();
     hipStream_t s = P->stream;
@@ -807,6 +942,9 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     UP(P->hpt_J, pt_J.data(), pt_J.size());
     UP(P->hfix_first, first.data(), first.size());
     UP(P->hfix_last, last.data(), last.size());
+    UP(P->hbh_B, bhB.data(), bhB.size());
+    UP(P->hbh_H, bhH.data(), bhH.size());
+    UP(P->hbh_S, bhS.data(), bhS.size());
 #undef UP
     if (e == hipSuccess) e = hipHostMalloc((void **)&P->hc_host, sizeof(CcgState));
     if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -843,15 +981,23 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
 
     const int N = P->N;
     const long long nnz = P->nnz;
-    XFK_CHECK(hipEventRecord(e0, s));
     XFK_CHECK(P->val.alloc((size_t)nnz));
     XFK_CHECK(P->val_im.alloc((size_t)nnz));
     XFK_CHECK(P->b.alloc((size_t)N));
     XFK_CHECK(P->b_im.alloc((size_t)N));
-    XFK_CHECK(hipMemsetAsync(P->val.p, 0, sizeof(double) * nnz, s));
-    XFK_CHECK(hipMemsetAsync(P->val_im.p, 0, sizeof(double) * nnz, s));
-    XFK_CHECK(hipMemsetAsync(P->b.p, 0, sizeof(double) * N, s));
-    XFK_CHECK(hipMemsetAsync(P->b_im.p, 0, sizeof(double) * N, s));
+    const int Gcg = (N + kCgBlock - 1) / kCgBlock, Gax = hc_axpy_grid(N);
+    const int G = std::max(Gcg, Gax);
+    XFK_CHECK(P->hc_vec.alloc(7 * (size_t)N));
+    XFK_CHECK(P->hc_part.alloc((size_t)kHcParts * G));
+    XFK_CHECK(P->hc_state.alloc(1));
+    XFK_CHECK(P->hc_split.alloc(4 * (size_t)N));
+    double2 *v = P->hc_vec.p;
+    const bool nonlin = P->any_nonlinear;
+    constexpr int kResGrid = 256;
+    if (nonlin) {
+        XFK_CHECK(P->hV_old.alloc((size_t)N));
+        XFK_CHECK(P->hres_part.alloc(2 * kResGrid));
+    }
     HarmArgs A;
     A.erec = P->erec.p;
     A.ebits = P->ebits.p;
@@ -867,79 +1013,16 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     A.b = P->b.p;
     A.b_im = P->b_im.p;
     A.w = P->omega;
-    for (int cl = 0; cl < P->ncolors; ++cl) {
-        const int n = P->color_off[cl + 1] - P->color_off[cl];
-        if (n > 0) k_hassemble_color<<<nb256(n), kBlock, 0, s>>>(P->color_off[cl], P->color_off[cl + 1], A);
-    }
-    if (P->nhpt > 0) k_hpoint<<<nb256(P->nhpt), kBlock, 0, s>>>(P->nhpt, P->hpt_nodes.p, P->hpt_J.p, P->b.p, P->b_im.p);
-    if (P->nfix_cols > 0) {
-        // rows that are not fixed but couple to a fixed node: k_hdir_cols walks those rows
-        k_hdir_cols<<<nb256(P->nfix_cols), kBlock, 0, s>>>(P->nfix_cols, P->fix_cols_row.p, P->rowptr.p,
-                                                           P->col.p, P->fixed.p, P->hfix_first.p, P->val.p,
-                                                           P->val_im.p, P->b.p, P->b_im.p);
-    }
-    if (P->nfix_rows > 0)
-        k_hdir_rows<<<nb256(P->nfix_rows), kBlock, 0, s>>>(P->nfix_rows, P->fix_rows.p, P->rowptr.p, P->diag.p,
-                                                           P->val.p, P->val_im.p, P->b.p, P->b_im.p,
-                                                           P->hfix_last.p);
-    launch_map(s, P->pm_n, P->pm_dst.p, P->pm_ptr.p, P->pm_src.p, P->pm_w.p, P->val.p, P->pm_tmp.p);
-    launch_map(s, P->pm_n, P->pm_dst.p, P->pm_ptr.p, P->pm_src.p, P->pm_w.p, P->val_im.p, P->pm_tmp.p);
-    launch_map(s, P->pb_n, P->pb_dst.p, P->pb_ptr.p, P->pb_src.p, P->pb_w.p, P->b.p, P->pb_tmp.p);
-    launch_map(s, P->pb_n, P->pb_dst.p, P->pb_ptr.p, P->pb_src.p, P->pb_w.p, P->b_im.p, P->pb_tmp.p);
-    XFK_CHECK(hipGetLastError());
-    XFK_CHECK(hipEventRecord(e1, s));
-
-    // COCG, Chronopoulos-Gear arrangement; preconditioner: the AMG V-cycle of
-    // the real surrogate B = Re A + sgn Im A applied to real and imaginary
-    // parts (a real symmetric M keeps COCG's complex-symmetric structure; with
-    // K_r, K_i both positive semi-definite, the eigenvalues of B^-1 (K_r + i K_i)
-    // lie in the box [0,1] x [0,1] away from 0, so the iteration count is the
-    // V-cycle's, not the mesh's), or complex Jacobi
-    bool amg = false;
-    float ms_setup = 0;
-    if (P->precond == XFK_PRECOND_AMG) {
-        const int nbd = nb256(N);
-        XFK_CHECK(P->hc_bval.alloc((size_t)std::max<long long>(P->nnz, nbd)));
-        k_hc_diag_im<<<nbd, 256, 0, s>>>(N, P->diag.p, P->val_im.p, P->hc_bval.p);
-        std::vector<double> hp(nbd);
-        XFK_CHECK(d2h(hp.data(), P->hc_bval.p, sizeof(double) * nbd, s));
-        double sdi = 0;
-        for (double v : hp) sdi += v;
-        k_hc_surrogate<<<nb256(N), kBlock, 0, s>>>(N, sdi >= 0 ? 1.0 : -1.0, P->rowptr.p, P->col.p, P->val.p,
-                                                   P->val_im.p, P->hc_bval.p);
-        if (!P->amg) P->amg = new Amg();
-        P->amg->theta = P->amg_theta;
-        P->amg->sweeps = P->amg_sweeps;
-        P->amg->omega = P->amg_omega;
-        hipEvent_t a0, a1;
-        XFK_CHECK(hipEventCreate(&a0));
-        XFK_CHECK(hipEventCreate(&a1));
-        XFK_CHECK(hipEventRecord(a0, s));
-        const int arc = P->amg->setup(s, N, N, P->rowptr.p, P->col.p, P->hc_bval.p, P->nnz);
-        XFK_CHECK(hipEventRecord(a1, s));
-        XFK_CHECK(hipEventSynchronize(a1));
-        XFK_CHECK(hipEventElapsedTime(&ms_setup, a0, a1));
-        (void)hipEventDestroy(a0);
-        (void)hipEventDestroy(a1);
-        if (arc != XFK_OK && arc != XFK_ERR_UNSUPPORTED) return arc;
-        amg = arc == XFK_OK;
-    }
-    const int Gcg = (N + kCgBlock - 1) / kCgBlock, Gax = hc_axpy_grid(N);
-    const int G = std::max(Gcg, Gax);
-    XFK_CHECK(P->hc_vec.alloc(7 * (size_t)N));
-    XFK_CHECK(P->hc_part.alloc((size_t)kHcParts * G));
-    XFK_CHECK(P->hc_state.alloc(1));
-    XFK_CHECK(hipMemsetAsync(P->hc_part.p, 0, sizeof(double) * kHcParts * G, s));
-    CcgState init{};
-    init.tol = P->precision;
-    XFK_CHECK(hipMemcpyAsync(P->hc_state.p, &init, sizeof(CcgState), hipMemcpyHostToDevice, s));
+    A.V = v;
+    A.bhB = P->hbh_B.p;
+    A.bhH = P->hbh_H.p;
+    A.bhS = P->hbh_S.p;
     HcArgs H;
     H.N = N;
     H.rowptr = P->rowptr.p;
     H.col = P->col.p;
     H.val = P->val.p;
     H.val_im = P->val_im.p;
-    double2 *v = P->hc_vec.p;
     H.x = v;
     H.r = v + N;
     H.u = v + 2 * (size_t)N;
@@ -951,67 +1034,175 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     H.part = P->hc_part.p;
     H.G = G;
     H.S = P->hc_state.p;
-    H.amg = amg ? 1 : 0;
-    XFK_CHECK(P->hc_split.alloc(4 * (size_t)N));
     H.r_re = P->hc_split.p;
     H.r_im = P->hc_split.p + N;
     double *u_re = P->hc_split.p + 2 * (size_t)N, *u_im = P->hc_split.p + 3 * (size_t)N;
     H.u_re = u_re;
     H.u_im = u_im;
     const int *done = &P->hc_state.p->done;
-    auto precondition = [&]() -> int {
-        int rc = P->amg->vcycle(s, H.r_re, u_re, done);
-        if (rc == XFK_OK) rc = P->amg->vcycle(s, H.r_im, u_im, done);
-        return rc;
-    };
-    k_hdiag_inv<<<nb256(N), kBlock, 0, s>>>(N, P->diag.p, P->val.p, P->val_im.p, dinv, P->hc_state.p);
-    XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
-    XFK_CHECK(hipStreamSynchronize(s));
-    if (P->hc_host->singular) {
-        set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
-        return XFK_ERR_SINGULAR;
-    }
-    k_hc_init<<<Gcg, kCgBlock, 0, s>>>(H, P->b.p, P->b_im.p);
-    int prc;
-    if (amg && (prc = precondition()) != XFK_OK) return prc;
-    k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, 0);
-    long long it = 0;
-    int batch = amg ? 8 : 32;
-    const long long cap = std::max<long long>(100000, 20LL * N);
-    for (;;) {
-        for (int k = 0; k < batch; ++k, ++it) {
-            if (amg) {
-                k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, Gcg, it == 0 ? Gcg : Gax);
-                if ((prc = precondition()) != XFK_OK) return prc;
-            } else {
-                k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, it == 0 ? Gcg : Gax, it == 0 ? Gcg : Gax);
-            }
-            k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, (int)((it + 1) & 1));
+
+    // successive approximation (harmonic2d.cpp:219-873; a single pass for
+    // linear problems): assemble from the current iterate, solve warm-started,
+    // relax, stop at |dV| / |V| < 100 Precision
+    double Relax = P->relax, resn = 0, lastres = 0;
+    long long cg_total = 0;
+    float ms_asm = 0, ms_sol = 0, ms_setup = 0;
+    bool amg = false;
+    int iter = 0;
+    for (;; ++iter) {
+        XFK_CHECK(hipEventRecord(e0, s));
+        XFK_CHECK(hipMemsetAsync(P->val.p, 0, sizeof(double) * nnz, s));
+        XFK_CHECK(hipMemsetAsync(P->val_im.p, 0, sizeof(double) * nnz, s));
+        XFK_CHECK(hipMemsetAsync(P->b.p, 0, sizeof(double) * N, s));
+        XFK_CHECK(hipMemsetAsync(P->b_im.p, 0, sizeof(double) * N, s));
+        A.iter = iter;
+        for (int cl = 0; cl < P->ncolors; ++cl) {
+            const int n = P->color_off[cl + 1] - P->color_off[cl];
+            if (n > 0) k_hassemble_color<<<nb256(n), kBlock, 0, s>>>(P->color_off[cl], P->color_off[cl + 1], A);
         }
+        if (P->nhpt > 0)
+            k_hpoint<<<nb256(P->nhpt), kBlock, 0, s>>>(P->nhpt, P->hpt_nodes.p, P->hpt_J.p, P->b.p, P->b_im.p);
+        if (P->nfix_cols > 0) {
+            // rows that are not fixed but couple to a fixed node: k_hdir_cols walks those rows
+            k_hdir_cols<<<nb256(P->nfix_cols), kBlock, 0, s>>>(P->nfix_cols, P->fix_cols_row.p, P->rowptr.p,
+                                                               P->col.p, P->fixed.p, P->hfix_first.p, P->val.p,
+                                                               P->val_im.p, P->b.p, P->b_im.p);
+        }
+        if (P->nfix_rows > 0)
+            k_hdir_rows<<<nb256(P->nfix_rows), kBlock, 0, s>>>(P->nfix_rows, P->fix_rows.p, P->rowptr.p,
+                                                               P->diag.p, P->val.p, P->val_im.p, P->b.p,
+                                                               P->b_im.p, P->hfix_last.p);
+        launch_map(s, P->pm_n, P->pm_dst.p, P->pm_ptr.p, P->pm_src.p, P->pm_w.p, P->val.p, P->pm_tmp.p);
+        launch_map(s, P->pm_n, P->pm_dst.p, P->pm_ptr.p, P->pm_src.p, P->pm_w.p, P->val_im.p, P->pm_tmp.p);
+        launch_map(s, P->pb_n, P->pb_dst.p, P->pb_ptr.p, P->pb_src.p, P->pb_w.p, P->b.p, P->pb_tmp.p);
+        launch_map(s, P->pb_n, P->pb_dst.p, P->pb_ptr.p, P->pb_src.p, P->pb_w.p, P->b_im.p, P->pb_tmp.p);
+        if (nonlin) XFK_CHECK(hipMemcpyAsync(P->hV_old.p, v, sizeof(double2) * N, hipMemcpyDeviceToDevice, s));
         XFK_CHECK(hipGetLastError());
+        XFK_CHECK(hipEventRecord(e1, s));
+
+        // COCG, Chronopoulos-Gear arrangement; preconditioner: the AMG V-cycle of
+        // the real surrogate B = Re A + sgn Im A applied to real and imaginary
+        // parts (a real symmetric M keeps COCG's complex-symmetric structure; with
+        // K_r, K_i both positive semi-definite, the eigenvalues of B^-1 (K_r + i K_i)
+        // lie in the box [0,1] x [0,1] away from 0, so the iteration count is the
+        // V-cycle's, not the mesh's), or complex Jacobi
+        amg = false;
+        if (P->precond == XFK_PRECOND_AMG) {
+            const int nbd = nb256(N);
+            XFK_CHECK(P->hc_bval.alloc((size_t)std::max<long long>(P->nnz, nbd)));
+            k_hc_diag_im<<<nbd, 256, 0, s>>>(N, P->diag.p, P->val_im.p, P->hc_bval.p);
+            std::vector<double> hp(nbd);
+            XFK_CHECK(d2h(hp.data(), P->hc_bval.p, sizeof(double) * nbd, s));
+            double sdi = 0;
+            for (double q : hp) sdi += q;
+            k_hc_surrogate<<<nb256(N), kBlock, 0, s>>>(N, sdi >= 0 ? 1.0 : -1.0, P->rowptr.p, P->col.p, P->val.p,
+                                                       P->val_im.p, P->hc_bval.p);
+            if (!P->amg) P->amg = new Amg();
+            P->amg->theta = P->amg_theta;
+            P->amg->sweeps = P->amg_sweeps;
+            P->amg->omega = P->amg_omega;
+            hipEvent_t a0, a1;
+            XFK_CHECK(hipEventCreate(&a0));
+            XFK_CHECK(hipEventCreate(&a1));
+            XFK_CHECK(hipEventRecord(a0, s));
+            const int arc = P->amg->setup(s, N, N, P->rowptr.p, P->col.p, P->hc_bval.p, P->nnz);
+            XFK_CHECK(hipEventRecord(a1, s));
+            XFK_CHECK(hipEventSynchronize(a1));
+            float mss = 0;
+            XFK_CHECK(hipEventElapsedTime(&mss, a0, a1));
+            ms_setup += mss;
+            (void)hipEventDestroy(a0);
+            (void)hipEventDestroy(a1);
+            if (arc != XFK_OK && arc != XFK_ERR_UNSUPPORTED) return arc;
+            amg = arc == XFK_OK;
+        }
+        H.amg = amg ? 1 : 0;
+        auto precondition = [&]() -> int {
+            int rc = P->amg->vcycle(s, H.r_re, u_re, done);
+            if (rc == XFK_OK) rc = P->amg->vcycle(s, H.r_im, u_im, done);
+            return rc;
+        };
+        XFK_CHECK(hipMemsetAsync(P->hc_part.p, 0, sizeof(double) * kHcParts * G, s));
+        CcgState init{};
+        init.tol = P->precision;
+        XFK_CHECK(hipMemcpyAsync(P->hc_state.p, &init, sizeof(CcgState), hipMemcpyHostToDevice, s));
+        k_hdiag_inv<<<nb256(N), kBlock, 0, s>>>(N, P->diag.p, P->val.p, P->val_im.p, dinv, P->hc_state.p);
         XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
         XFK_CHECK(hipStreamSynchronize(s));
-        const CcgState &S = *P->hc_host;
-        if (S.done) break;
-        if (it >= cap) {
-            set_error("COCG did not converge within the iteration cap");
+        if (P->hc_host->singular) {
+            set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
+            return XFK_ERR_SINGULAR;
+        }
+        if (iter > 0) k_hc_init<true><<<Gcg, kCgBlock, 0, s>>>(H, P->b.p, P->b_im.p);
+        else k_hc_init<false><<<Gcg, kCgBlock, 0, s>>>(H, P->b.p, P->b_im.p);
+        int prc;
+        if (amg && (prc = precondition()) != XFK_OK) return prc;
+        k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, 0);
+        long long it = 0;
+        int batch = amg ? 8 : 32;
+        const long long cap = std::max<long long>(100000, 20LL * N);
+        for (;;) {
+            for (int k = 0; k < batch; ++k, ++it) {
+                if (amg) {
+                    k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, Gcg, it == 0 ? Gcg : Gax);
+                    if ((prc = precondition()) != XFK_OK) return prc;
+                } else {
+                    k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, it == 0 ? Gcg : Gax, it == 0 ? Gcg : Gax);
+                }
+                k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, (int)((it + 1) & 1));
+            }
+            XFK_CHECK(hipGetLastError());
+            XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
+            XFK_CHECK(hipStreamSynchronize(s));
+            const CcgState &S = *P->hc_host;
+            if (S.done) break;
+            if (it >= cap) {
+                set_error("COCG did not converge within the iteration cap");
+                return XFK_ERR_NOCONV;
+            }
+            double rate = (S.iters > 0 && S.er > 0 && S.er < 1) ? std::log(S.er) / (double)S.iters : 0.0;
+            long long rem = rate < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / rate) : 2 * batch;
+            batch = (int)std::max<long long>(8, std::min<long long>(rem + 2, 512));
+        }
+        cg_total += P->hc_host->iters;
+        XFK_CHECK(hipEventRecord(e2, s));
+        XFK_CHECK(hipEventSynchronize(e2));
+        float ms = 0;
+        XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        ms_asm += ms;
+        XFK_CHECK(hipEventElapsedTime(&ms, e1, e2));
+        ms_sol += ms;
+        if (!nonlin) break;
+        // the change of this pass (harmonic2d.cpp:829-852)
+        k_hres<<<kResGrid, 256, 0, s>>>(N, v, P->hV_old.p, P->hres_part.p);
+        std::vector<double> hp(2 * kResGrid);
+        XFK_CHECK(d2h(hp.data(), P->hres_part.p, sizeof(double) * hp.size(), s));
+        double sx = 0, sy = 0;
+        for (int k = 0; k < kResGrid; ++k) {
+            sx += hp[k];
+            sy += hp[kResGrid + k];
+        }
+        if (sy == 0) break;
+        lastres = resn;
+        resn = std::sqrt(sx / sy);
+        if (iter > 5) {
+            if ((resn > lastres) && (Relax > 0.1)) Relax /= 2.;
+            else Relax += 0.1 * (1. - Relax);
+            k_hrelax<<<nb256(N), kBlock, 0, s>>>(N, Relax, v, P->hV_old.p);
+        }
+        if ((resn < 100. * P->precision) && iter > 0) break;
+        if (iter >= 10000) {
+            set_error("harmonic successive approximation did not converge within the iteration cap");
             return XFK_ERR_NOCONV;
         }
-        double rate = (S.iters > 0 && S.er > 0 && S.er < 1) ? std::log(S.er) / (double)S.iters : 0.0;
-        long long rem = rate < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / rate) : 2 * batch;
-        batch = (int)std::max<long long>(8, std::min<long long>(rem + 2, 512));
     }
-    XFK_CHECK(hipEventRecord(e2, s));
-    XFK_CHECK(hipEventSynchronize(e2));
-    XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
-    R.ms_assemble = ms;
-    XFK_CHECK(hipEventElapsedTime(&ms, e1, e2));
-    R.ms_solve = ms;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipEventDestroy(e2);
-    R.newton_iters = 1;
-    R.cg_iters = P->hc_host->iters;
+    R.ms_assemble = ms_asm;
+    R.ms_solve = ms_sol;
+    R.newton_iters = iter + 1;
+    R.cg_iters = cg_total;
     R.final_er = P->hc_host->er;
     R.nnz = P->nnz;
     R.ncolors = P->ncolors;

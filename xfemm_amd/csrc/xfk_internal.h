@@ -115,6 +115,8 @@ struct DevBlockAC {
     double2 J;          // source current density
     double Cduct;
     int eddy;           // 0: laminated (Lam_d > 0) blocks carry no bulk eddy current (harmonic2d.cpp:392-394)
+    int bh_n;           // nonlinear: knots of the complex B-H curve (0: linear)
+    int bh_off;         // first knot in the problem's curve tables
     int pad;
 };
 
@@ -304,7 +306,12 @@ struct xfk_problem {
     int nhpt = 0;
     xfk::DBuf<double2> hc_vec;                   // COCG vectors: x, r, u, w, z, p, dinv (N each)
     xfk::DBuf<double> hc_split;                  // AMG: r and u split into real / imaginary parts
-    xfk::DBuf<double> hc_bval;                   // AMG: values of the real surrogate Re A + |Im A|
+    xfk::DBuf<double> hc_bval;                   // AMG: values of the real surrogate Re A +- Im A
+    // nonlinear harmonic (successive approximation, harmonic2d.cpp:616-660, 826-873)
+    xfk::DBuf<double> hbh_B;                     // complex B-H curves of all nonlinear blocks
+    xfk::DBuf<double2> hbh_H, hbh_S;
+    xfk::DBuf<double2> hV_old;                   // the iterate before the solve
+    xfk::DBuf<double> hres_part;                 // residual partial sums
     xfk::DBuf<double> hc_part;                   // per-block partials, 9 arrays
     xfk::DBuf<xfk::CcgState> hc_state;
     xfk::CcgState *hc_host = nullptr;            // pinned mirror

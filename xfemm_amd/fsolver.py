@@ -24,7 +24,7 @@ EXPORTED = (
     "xfemm_fsolver_get_pbcs", "xfemm_fsolver_num_pbcs", "xfemm_fsolver_bandwidth",
     "xfemm_fsolver_get_block_bh", "xfemm_fsolver_num_nodes", "xfemm_fsolver_num_elements",
     "xfemm_fsolver_get_solution", "xfemm_fsolver_get_elements", "xfemm_fsolver_get_stats",
-    "xfemm_fsolver_last_error", "xfemm_bh_get_slopes",
+    "xfemm_fsolver_last_error", "xfemm_bh_get_slopes", "xfemm_bh_get_slopes_ac",
 )
 
 _lib = None

@@ -198,7 +198,8 @@ def _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e,
         n = len(b.get("B", ()))
         o.BHpoints = n
         if n:
-            o.B, o.H, o.slope = keep.d(b["B"]), keep.d(b["H"]), keep.d(b["slope"])
+            # (harmonic blocks may carry the complex curve: real parts here)
+            o.B, o.H, o.slope = keep.d(b["B"]), keep.d(np.real(b["H"])), keep.d(np.real(b["slope"]))
     lb = (LabelDesc * max(1, len(labels)))()
     for k, l in enumerate(labels):
         lb[k].block, lb[k].in_circuit = l["block"], l.get("in_circuit", -1)
@@ -353,7 +354,8 @@ class Static2DProblem:
 
 
 class BlockAcDesc(C.Structure):
-    _fields_ = [("J_im", C.c_double), ("Theta_hx", C.c_double), ("Theta_hy", C.c_double), ("Lam_d", C.c_double)]
+    _fields_ = [("J_im", C.c_double), ("Theta_hx", C.c_double), ("Theta_hy", C.c_double), ("Lam_d", C.c_double),
+                ("H_im", dptr), ("slope_im", dptr)]
 
 
 class LineAcDesc(C.Structure):
@@ -390,6 +392,9 @@ class Harmonic2DProblem:
         for k, b in enumerate(blocks):
             ba[k].J_im, ba[k].Lam_d = b.get("J_im", 0.0), b.get("Lam_d", 0.0)
             ba[k].Theta_hx, ba[k].Theta_hy = b.get("Theta_hx", 0.0), b.get("Theta_hy", 0.0)
+            if len(b.get("B", ())):   # nonlinear: the complex curve of bh_get_slopes_ac
+                ba[k].H_im = keep.d(np.imag(np.asarray(b["H"])))
+                ba[k].slope_im = keep.d(np.imag(np.asarray(b["slope"])))
         la = (LineAcDesc * max(1, len(lines)))()
         for k, l in enumerate(lines):
             la[k].c0_im, la[k].c1_im, la[k].Mu, la[k].Sig = (l.get("c0_im", 0.0), l.get("c1_im", 0.0),

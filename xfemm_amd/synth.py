@@ -136,7 +136,7 @@ def fem_text(blocks, lines, precision=1e-8, units="centimeters", frequency=0.0, 
                 "    <Mu_y> = %.17g" % b.get("mu_y", 1.0), "    <H_c> = %.17g" % b.get("H_c", 0.0),
                 "    <H_cAngle> = 0", "    <J_re> = %.17g" % b.get("J_re", 0.0),
                 "    <J_im> = %.17g" % b.get("J_im", 0.0), "    <Sigma> = %.17g" % b.get("Cduct", 0.0),
-                "    <d_lam> = %.17g" % b.get("Lam_d", 0.0), "    <Phi_h> = 0",
+                "    <d_lam> = %.17g" % b.get("Lam_d", 0.0), "    <Phi_h> = %.17g" % b.get("Theta_hn", 0.0),
                 "    <Phi_hx> = %.17g" % b.get("Theta_hx", 0.0), "    <Phi_hy> = %.17g" % b.get("Theta_hy", 0.0),
                 "    <LamType> = %d" % b.get("LamType", 0),
                 "    <LamFill> = %.17g" % b.get("LamFill", 1.0), "    <NStrands> = 0", "    <WireD> = 0"]
@@ -318,7 +318,7 @@ def bc_chain(n: int, L: float = 10.0):
 
 
 def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float = 1e-8, periodic: bool = False,
-             circuits: bool = True):
+             circuits: bool = True, nonlinear: bool = False):
     """Keyword arguments of a linear time-harmonic planar problem
     (FSolver::Harmonic2D, cfemm/fsolver/harmonic2d.cpp) on the magnetostatic
     square: laminated lossy steel (lamination thickness with conductivity,
@@ -327,7 +327,10 @@ def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float 
     side with phase, a mixed side with complex c0/c1, a small-skin-depth side,
     a complex point current and point value; optionally bottom/top periodic
     pairs and circuits (a wound coil with specified current -> Case 1, the
-    plate driven by a specified voltage gradient -> Case 0)."""
+    plate driven by a specified voltage gradient -> Case 0).  `nonlinear`:
+    the steel follows the M-19 curve processed for the frequency
+    (GetSlopes(omega): hysteresis lag, lamination eddy currents, fill), which
+    starts the reference's successive approximation."""
     kw = magnetostatic(n, L=L, precision=precision)
     x, y, p = kw["x"], kw["y"], kw["p"]
     tol = 1e-9 * L
@@ -358,6 +361,14 @@ def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float 
         dict(mu_x=1.0, mu_y=1.0, Cduct=35.0),                                        # aluminium plate
         dict(mu_x=50.0, mu_y=5.0, Lam_d=0.5, LamFill=0.9),                           # anisotropic, no conduction
     ]
+    if nonlinear:
+        from .fsolver import bh_get_slopes_ac
+        b1 = kw["blocks"][1]
+        Bc, Hc, Sc, mu, _ = bh_get_slopes_ac(*m19_curve(), 2 * np.pi * frequency, lam_type=0,
+                                             lam_fill=b1["LamFill"], theta_hn=b1["Theta_hx"], lam_d=b1["Lam_d"],
+                                             cduct=b1["Cduct"])
+        # (bh / Theta_hn: what a .fem of this problem carries -- the raw curve)
+        b1.update(B=Bc, H=Hc, slope=Sc, mu_x=mu, mu_y=mu, bh="M19", Theta_hn=b1["Theta_hx"])
     lbl = kw["lbl"]
     cx = (x[p[:, 0]] + x[p[:, 1]] + x[p[:, 2]]) / (3.0 * L)
     cy = (y[p[:, 0]] + y[p[:, 1]] + y[p[:, 2]]) / (3.0 * L)
