@@ -266,10 +266,13 @@ typedef struct {
 
 int xfk_problem_create_harmonic(const xfk_problem_desc *desc, const xfk_harmonic_desc *ac, int device,
                                 xfk_problem **out);
-/* FSolver::Harmonic2D on the device (complex-symmetric COCG, the reference's
- * stopping test |r| / |b| <= Precision).  flags as for xfk_static2d. */
+/* FSolver::Harmonic2D, or HarmonicAxisymmetric (harmonicaxi.cpp:1-800) when
+ * desc->problem_type is XFK_AXISYMMETRIC, on the device (complex-symmetric
+ * COCG, the reference's stopping test |r| / |b| <= Precision).  flags as for
+ * xfk_static2d. */
 int xfk_harmonic2d(xfk_problem *prob, int flags, xfk_result *res);
-/* A = V * c at every node, interleaved (re, im). */
+/* A = V * c at every node, interleaved (re, im); axisymmetric problems: the
+ * flux V * c * 2 pi r * 0.01 (harmonicaxi.cpp:790). */
 int xfk_get_solution_complex(xfk_problem *prob, double *A_host);
 /* Circuit results: case, J and dV interleaved (re, im) per circuit. */
 int xfk_get_circuits_complex(xfk_problem *prob, int *ccase, double *J, double *dV);

@@ -24,7 +24,7 @@ class OrhBlock(C.Structure):
 
 
 class OrhLabel(C.Structure):
-    _fields_ = [("InCircuit", C.c_int), ("bIsWound", C.c_int)]
+    _fields_ = [("InCircuit", C.c_int), ("bIsWound", C.c_int), ("IsExternal", C.c_int)]
 
 
 class OrhLine(C.Structure):
@@ -49,7 +49,8 @@ class OrhProblem(C.Structure):
                 ("n_circs", C.c_int), ("circs", C.POINTER(OrhCirc)),
                 ("n_pbc", C.c_int), ("pbc", iptr),
                 ("precision", C.c_double), ("frequency", C.c_double), ("length_units", C.c_int),
-                ("coords", C.c_int), ("bandwidth", C.c_int)]
+                ("coords", C.c_int), ("bandwidth", C.c_int), ("problem_type", C.c_int),
+                ("extZo", C.c_double), ("extRo", C.c_double), ("extRi", C.c_double)]
 
 
 _CREATE = C.CFUNCTYPE(C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double)
@@ -112,6 +113,7 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
     labels = (OrhLabel * max(1, len(pr.labels)))()
     for k, lb in enumerate(pr.labels):
         labels[k].InCircuit, labels[k].bIsWound = lb.InCircuit, int(lb.bIsWound)
+        labels[k].IsExternal = int(lb.IsExternal)
     lines = (OrhLine * max(1, len(pr.bdrys)))()
     for k, bd in enumerate(pr.bdrys):
         l = lines[k]
@@ -139,6 +141,7 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
     P.pbc = keep.i(mesh.pbc.reshape(-1) if len(mesh.pbc) else np.zeros(3, np.int32))
     P.precision, P.frequency = pr.Precision, pr.Frequency
     P.length_units, P.coords, P.bandwidth = pr.LengthUnits, pr.Coords, mesh.bandwidth
+    P.problem_type, P.extZo, P.extRo, P.extRi = pr.ProblemType, pr.extZo, pr.extRo, pr.extRi
     keep.items.extend([blocks, labels, lines, points, circs])
     return P, keep, circs
 

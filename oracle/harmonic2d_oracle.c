@@ -479,21 +479,29 @@ void orh_acprops(const orh_block *b, const double *Bq, int nq, double *v, double
 }
 
 /* effective permeability of each block (harmonic2d.cpp:190-235) */
+/* -I Theta DEG (harmonic2d.cpp) or -I Theta PI / 180 (harmonicaxi.cpp:133-151), halved for the half-lag */
+static cx lagarg(double th, int axi, int half)
+{
+    if (axi) return cdivd(cmuld(cmuld(cneg(I), th), ORA_PI), half ? 360. : 180.);
+    return half ? cdivd(cmuld(cmuld(cneg(I), th), ORA_DEG), 2.) : cmuld(cmuld(cneg(I), th), ORA_DEG);
+}
+
 static void effective_mu(const orh_problem *pr, double w, effmu *Mu)
 {
     const cx deg45 = C(1, 1);
+    const int axi = pr->problem_type == 1;
     for (int k = 0; k < pr->n_blocks; k++) {
         const orh_block *b = &pr->blocks[k];
         if (b->LamType == 0) {
-            Mu[k].mu0 = dmulc(b->mu_x, cx_exp(cmuld(cmuld(cneg(I), b->Theta_hx), ORA_DEG)));
-            Mu[k].mu1 = dmulc(b->mu_y, cx_exp(cmuld(cmuld(cneg(I), b->Theta_hy), ORA_DEG)));
+            Mu[k].mu0 = dmulc(b->mu_x, cx_exp(lagarg(b->Theta_hx, axi, 0)));
+            Mu[k].mu1 = dmulc(b->mu_y, cx_exp(lagarg(b->Theta_hy, axi, 0)));
             if (b->Lam_d != 0) {
                 if (b->Cduct != 0) {
-                    cx halflag = cx_exp(cdivd(cmuld(cmuld(cneg(I), b->Theta_hx), ORA_DEG), 2.));
+                    cx halflag = cx_exp(lagarg(b->Theta_hx, axi, 1));
                     double ds = sqrt(2. / (0.4 * ORA_PI * w * b->Cduct * b->mu_x));
                     cx K = cdivd(cmuld(cmuld(cmul(halflag, deg45), b->Lam_d), 0.001), 2. * ds);
                     Mu[k].mu0 = cplusd(cmuld(cdiv(cmul(Mu[k].mu0, cx_tanh(K)), K), b->LamFill), 1. - b->LamFill);
-                    halflag = cx_exp(cdivd(cmuld(cmuld(cneg(I), b->Theta_hy), ORA_DEG), 2.));
+                    halflag = cx_exp(lagarg(b->Theta_hy, axi, 1));
                     ds = sqrt(2. / (0.4 * ORA_PI * w * b->Cduct * b->mu_y));
                     K = cdivd(cmuld(cmuld(cmul(halflag, deg45), b->Lam_d), 0.001), 2. * ds);
                     Mu[k].mu1 = cplusd(cmuld(cdiv(cmul(Mu[k].mu1, cx_tanh(K)), K), b->LamFill), 1. - b->LamFill);
@@ -528,7 +536,12 @@ static void circuits(orh_problem *pr)
         if (lb->bIsWound) Cduct = 0;
         int k = lb->InCircuit;
         I1[k] = cplusd(I1[k], a);
-        I2[k] = cplusd(I2[k], a * Cduct);
+        if (pr->problem_type == 1) {   /* conductivity / R (harmonicaxi.cpp:86-87) */
+            double r = (pr->x[n[0]] + pr->x[n[1]] + pr->x[n[2]]) / 3.;
+            I2[k] = cplusd(I2[k], a * Cduct / (0.01 * r));
+        } else {
+            I2[k] = cplusd(I2[k], a * Cduct);
+        }
         I3[k] = cadd(I3[k], cmuld(cmuld(dplusc(b->J_re, cmuld(I, b->J_im)), a), 100.));
     }
     for (int k = 0; k < nc; k++) {
@@ -558,6 +571,182 @@ static void circuits(orh_problem *pr)
     free(I1); free(I2); free(I3);
 }
 
+/* one element of HarmonicAxisymmetric (harmonicaxi.cpp:215-605) */
+static void axi_element(orh_problem *pr, const orh_linprob_ops *ops, void *L, const effmu *Mu, double w, int Iter,
+                        int i, cx *VL, cx *bL)
+{
+    const double c = ORA_PI * 4.e-05;
+    const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
+    const cx deg45 = C(1, 1);
+    const int NN = pr->n_nodes;
+    cx Me[3][3], be[3], Mx[3][3], My[3][3], Mn[3][3], K;
+    double p[3], q[3], g[3], rn[3], l[3];
+    int n[3];
+    for (int j = 0; j < 3; j++) {
+        for (int k = 0; k < 3; k++) Me[j][k] = Mx[j][k] = My[j][k] = Mn[j][k] = C(0, 0);
+        be[j] = C(0, 0);
+    }
+    for (int k = 0; k < 3; k++) {
+        n[k] = pr->p[3 * i + k];
+        rn[k] = pr->x[n[k]];
+    }
+    p[0] = pr->y[n[1]] - pr->y[n[2]];
+    p[1] = pr->y[n[2]] - pr->y[n[0]];
+    p[2] = pr->y[n[0]] - pr->y[n[1]];
+    q[0] = pr->x[n[2]] - pr->x[n[1]];
+    q[1] = pr->x[n[0]] - pr->x[n[2]];
+    q[2] = pr->x[n[1]] - pr->x[n[0]];
+    g[0] = (pr->x[n[2]] + pr->x[n[1]]) / 2.;
+    g[1] = (pr->x[n[0]] + pr->x[n[2]]) / 2.;
+    g[2] = (pr->x[n[1]] + pr->x[n[0]]) / 2.;
+    for (int j = 0, k = 1; j < 3; k++, j++) {
+        if (k == 3) k = 0;
+        l[j] = sqrt(pow(pr->x[n[k]] - pr->x[n[j]], 2.) + pow(pr->y[n[k]] - pr->y[n[j]], 2.));
+    }
+    const double a = (p[0] * q[1] - p[1] * q[0]) / 2.;
+    const double R = (pr->x[n[0]] + pr->x[n[1]] + pr->x[n[2]]) / 3.;
+    double a_hat = 0, R_hat = 0;
+    for (int j = 0; j < 3; j++) a_hat += (rn[j] * rn[j] * p[j] / (4. * R));
+    const double vol = 2. * R * a_hat;
+    int flag = 0;
+    for (int j = 0; j < 3; j++)
+        if (rn[j] < 1.e-06) flag++;
+    if (flag == 2) {
+        R_hat = R;
+    } else if (flag == 1) {
+        if (rn[0] < 1.e-06)
+            R_hat = (fabs(rn[1] - rn[2]) < 1.e-06) ? rn[2] / 2. : (rn[1] - rn[2]) / (2. * log(rn[1]) - 2. * log(rn[2]));
+        if (rn[1] < 1.e-06)
+            R_hat = (fabs(rn[2] - rn[0]) < 1.e-06) ? rn[0] / 2. : (rn[2] - rn[0]) / (2. * log(rn[2]) - 2. * log(rn[0]));
+        if (rn[2] < 1.e-06)
+            R_hat = (fabs(rn[0] - rn[1]) < 1.e-06) ? rn[1] / 2. : (rn[0] - rn[1]) / (2. * log(rn[0]) - 2. * log(rn[1]));
+    } else {
+        if (fabs(q[0]) < 1.e-06) R_hat = (q[1] * q[1]) / (2. * (-q[1] + rn[0] * log(rn[0] / rn[2])));
+        else if (fabs(q[1]) < 1.e-06) R_hat = (q[2] * q[2]) / (2. * (-q[2] + rn[1] * log(rn[1] / rn[0])));
+        else if (fabs(q[2]) < 1.e-06) R_hat = (q[0] * q[0]) / (2. * (-q[0] + rn[2] * log(rn[2] / rn[1])));
+        else
+            R_hat = -(q[0] * q[1] * q[2]) /
+                    (2. * (q[0] * rn[0] * log(rn[0]) + q[1] * rn[1] * log(rn[1]) + q[2] * rn[2] * log(rn[2])));
+    }
+    /* Mr, Mz (:293-321) */
+    K = C(-1. / (2. * a_hat * R), 0);
+    for (int j = 0; j < 3; j++)
+        for (int k = j; k < 3; k++) Mx[j][k] = cadd(Mx[j][k], cmuld(cmuld(cmuld(cmuld(K, p[j]), rn[j]), p[k]), rn[k]));
+    for (int j = 0; j < 3; j++)
+        if (rn[j] < 1.e-06) Mx[j][j] = cadd(Mx[j][j], cadd(cadd(Mx[0][0], Mx[1][1]), Mx[2][2]));
+    K = C(-1. / (2. * a_hat * R_hat), 0);
+    for (int j = 0; j < 3; j++)
+        for (int k = j; k < 3; k++)
+            My[j][k] = cadd(My[j][k], cmuld(cmuld(cmuld(cmuld(K, q[j] * rn[j]), q[k] * rn[k]), g[j] / R), g[k] / R));
+    Mx[1][0] = Mx[0][1]; Mx[2][0] = Mx[0][2]; Mx[2][1] = Mx[1][2];
+    My[1][0] = My[0][1]; My[2][0] = My[0][2]; My[2][1] = My[1][2];
+    const orh_block *blk = &pr->blocks[pr->blk[i]];
+    const orh_label *lab = &pr->labels[pr->lbl[i]];
+    /* eddy currents (:333-347) */
+    K = cdivd(cmuld(cmuld(cmuld(cmuld(cmuld(cneg(I), R), a), w), blk->Cduct), c), 6.);
+    if ((blk->LamType == 0) && (blk->Lam_d > 0)) K = C(0, 0);
+    if (lab->bIsWound) K = C(0, 0);
+    for (int j = 0; j < 3; j++)
+        for (int k = 0; k < 3; k++) Me[j][k] = cadd(Me[j][k], cdivd(cmuld(K, 4.), 3.));
+    /* derivative boundary conditions (:349-383) */
+    for (int j = 0; j < 3; j++) {
+        int k = j + 1;
+        if (k == 3) k = 0;
+        double r = (pr->x[n[j]] + pr->x[n[k]]) / 2.;
+        int ej = pr->e ? pr->e[3 * i + j] : -1;
+        if (ej < 0) continue;
+        const orh_line *ln = &pr->lines[ej];
+        if (ln->BdryFormat == 2) {
+            K = cdivd(cmuld(dmulc(-0.0001 * c * 2. * r, C(ln->c0_re, ln->c0_im)), l[j]), 6.);
+            Me[j][j] = cadd(Me[j][j], dmulc(2.0, K));
+            Me[k][k] = cadd(Me[k][k], dmulc(2.0, K));
+            Me[j][k] = cadd(Me[j][k], K);
+            Me[k][j] = cadd(Me[k][j], K);
+            K = cmuld(cmuld(cmuld(cdivd(cmuld(C(ln->c1_re, ln->c1_im), l[j]), 2.), 2.), r), 0.0001);
+            be[j] = cadd(be[j], K);
+            be[k] = cadd(be[k], K);
+        }
+        if (ln->BdryFormat == 1) {
+            double ds = sqrt(2. / (0.4 * ORA_PI * w * ln->Sig * ln->Mu));
+            K = cdivd(deg45, -ds * ln->Mu * 100.);
+            K = cmuld(K, 2. * r * l[j] / 6.);
+            Me[j][j] = cadd(Me[j][j], dmulc(2.0, K));
+            Me[k][k] = cadd(Me[k][k], dmulc(2.0, K));
+            Me[j][k] = cadd(Me[j][k], K);
+            Me[k][j] = cadd(Me[k][j], K);
+        }
+    }
+    /* sources (:385-405) */
+    for (int j = 0; j < 3; j++) {
+        cx Jv = C(0, 0);
+        if (lab->InCircuit >= 0) {
+            const orh_circ *cc = &pr->circs[lab->InCircuit];
+            if (cc->Case == 1) Jv = C(cc->J_re, cc->J_im);
+            if (cc->Case == 0) Jv = cdivd(cmuld(dmulc(-100., C(cc->dV_re, cc->dV_im)), blk->Cduct), R);
+        }
+        K = cdivd(cmuld(dmulc(-2. * R, cadd(dplusc(blk->J_re, cmuld(I, blk->J_im)), Jv)), a), 3.);
+        be[j] = cadd(be[j], K);
+        if (lab->InCircuit >= 0 && pr->circs[lab->InCircuit].Case == 2) {
+            int row = NN + lab->InCircuit;
+            bL[row] = cadd(bL[row], cdivd(K, R));
+        }
+    }
+    /* Case 2 circuit couplings (:407-417) */
+    if (lab->InCircuit >= 0 && pr->circs[lab->InCircuit].Case == 2) {
+        int cr = NN + lab->InCircuit;
+        cx Kc = cmuld(cmuld(cmuld(cmuld(dmulc(-2., I), a), w), blk->Cduct), c);
+        for (int j = 0; j < 3; j++) {
+            double gr, gi;
+            ops->get(L, n[j], cr, &gr, &gi);
+            cx v = cadd(C(gr, gi), cdivd(Kc, 3.));
+            ops->put(L, v.re, v.im, n[j], cr);
+        }
+        double gr, gi;
+        ops->get(L, cr, cr, &gr, &gi);
+        cx v = cadd(C(gr, gi), cdivd(Kc, R));
+        ops->put(L, v.re, v.im, cr, cr);
+    }
+    /* permeability: the block's / successive approximation with B from the
+     * element energy (:425-560) / the exterior warp (:567-574) */
+    cx mu1 = Mu[pr->blk[i]].mu0, mu2 = Mu[pr->blk[i]].mu1;
+    int updated = 0;
+    if (Iter > 0 && blk->LamType == 0 && blk->BHpoints > 0 && mu1.re == mu2.re && mu1.im == mu2.im) {
+        cx v[3], dv = C(0, 0);
+        for (int j = 0; j < 3; j++) {
+            v[j] = C(0, 0);
+            for (int ww = 0; ww < 3; ww++) v[j] = cadd(v[j], cmul(cadd(Mx[j][ww], My[j][ww]), VL[n[ww]]));
+        }
+        for (int j = 0; j < 3; j++) dv = cadd(dv, cmul(cconj(VL[n[j]]), v[j]));
+        dv = cmuld(dv, (10000. * c * c / vol));
+        double B = sqrt(cx_abs(dv));
+        cx murel = ddivc(1., cmuld(bh_getv(blk, B), ORH_MUO));
+        cx muinc = ddivc(1., cmuld(bh_dhdb(blk, B), ORH_MUO));
+        K = cdiv(cmul(dmulc(2., murel), muinc), cadd(murel, muinc));
+        mu1 = K;
+        mu2 = K;
+        K = cneg(csub(ddivc(1., murel), ddivc(1., K)));
+        for (int j = 0; j < 3; j++)
+            for (int k = 0; k < 3; k++) Mn[j][k] = cmul(K, cadd(Mx[j][k], My[j][k]));
+        updated = 1;
+    }
+    if (lab->IsExternal && !updated) {   /* set at Iter 0 and kept by linear elements */
+        double u = units[pr->length_units];
+        double Z = (pr->y[n[0]] + pr->y[n[1]] + pr->y[n[2]]) / 3. - pr->extZo * u;
+        double kludge = (R * R + Z * Z) * (pr->extRi * u) / ((pr->extRo * u) * (pr->extRo * u) * (pr->extRo * u));
+        mu1 = cdivd(mu1, kludge);
+        mu2 = cdivd(mu2, kludge);
+    }
+    for (int j = 0; j < 3; j++)
+        for (int k = 0; k < 3; k++) {
+            Me[j][k] = cadd(Me[j][k], cadd(cdiv(Mx[j][k], mu2), cdiv(My[j][k], mu1)));
+            be[j] = cadd(be[j], cmul(Mn[j][k], VL[n[k]]));
+        }
+    for (int j = 0; j < 3; j++) {
+        for (int k = j; k < 3; k++) ops->addto(L, Me[j][k].re, Me[j][k].im, n[j], n[k]);
+        bL[n[j]] = cadd(bL[n[j]], be[j]);
+    }
+}
+
 static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L, const effmu *Mu, double w,
                            int Iter)
 {
@@ -567,7 +756,12 @@ static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L,
     const int NN = pr->n_nodes;
     cx *bL = (cx *)ops->b(L);
     cx *VL = (cx *)ops->V(L);
+    const int axi = pr->problem_type == 1;
     for (int i = 0; i < pr->n_elems; i++) {
+        if (axi) {
+            axi_element(pr, ops, L, Mu, w, Iter, i, VL, bL);
+            continue;
+        }
         cx Me[3][3], be[3], Mx[3][3], My[3][3], Mxy[3][3], Mn[3][3];
         double p[3], q[3], l[3];
         int n[3];
@@ -709,18 +903,23 @@ static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L,
     /* point currents (:634-641) */
     for (int i = 0; i < NN; i++) {
         int m = pr->marker ? pr->marker[i] : -1;
-        if (m >= 0) {
-            cx K = dmulc(0.01, dplusc(pr->points[m].J_re, cmuld(I, pr->points[m].J_im)));
-            bL[i] = cadd(bL[i], cneg(K));
+        if (m >= 0) {   /* axisymmetric: (2 r 0.01) J (harmonicaxi.cpp:610-617) */
+            cx K = dmulc(axi ? (2. * pr->x[i] * 0.01) : 0.01, dplusc(pr->points[m].J_re, cmuld(I, pr->points[m].J_im)));
+            bL[i] = axi ? csub(bL[i], K) : cadd(bL[i], cneg(K));
         }
     }
     /* Case 2 total current constraints (:644-650) */
     for (int i = 0; i < pr->n_circs; i++)
         if (pr->circs[i].Case == 2)
-            bL[NN + i] = cadd(bL[NN + i], dmulc(0.01, dplusc(pr->circs[i].Amps_re, cmuld(I, pr->circs[i].Amps_im))));
+            bL[NN + i] = cadd(bL[NN + i], dmulc(axi ? 2. * 0.01 : 0.01,
+                                                dplusc(pr->circs[i].Amps_re, cmuld(I, pr->circs[i].Amps_im))));
     /* fixed points (:653-661) */
     for (int i = 0; i < NN; i++) {
         int m = pr->marker ? pr->marker[i] : -1;
+        if (axi && pr->x[i] < (units[pr->length_units] * 1.e-06)) {   /* A = 0 on the axis (:626-631) */
+            ops->setvalue(L, i, 0., 0.);
+            continue;
+        }
         if (m >= 0 && pr->points[m].J_re == 0 && pr->points[m].J_im == 0) {
             cx K = cdivd(dplusc(pr->points[m].A_re, cmuld(I, pr->points[m].A_im)), c);
             ops->setvalue(L, i, K.re, K.im);
@@ -833,12 +1032,19 @@ int orh_harmonic2d(orh_problem *pr, const orh_linprob_ops *ops, double *A_out, o
     if (ok) {
         const cx *V = (const cx *)ops->V(L);
         for (int i = 0; i < NN; i++) {
-            A_out[2 * i] = V[i].re * c;
-            A_out[2 * i + 1] = V[i].im * c;
+            if (pr->problem_type == 1) {   /* the flux (harmonicaxi.cpp:790) */
+                cx f = cmuld(cmuld(cmuld(cmuld(cmuld(V[i], c), 2.), ORA_PI), pr->x[i]), 0.01);
+                A_out[2 * i] = f.re;
+                A_out[2 * i + 1] = f.im;
+            } else {
+                A_out[2 * i] = V[i].re * c;
+                A_out[2 * i + 1] = V[i].im * c;
+            }
         }
         for (int i = 0; i < pr->n_circs; i++)
             if (pr->circs[i].Case == 2) {   /* L.b[NumNodes+i] = I*c*w*V (:784) and .ans writes it as dV */
-                cx dv = cmul(cmuld(cmuld(I, c), w), V[NN + i]);
+                cx dv = pr->problem_type == 1 ? cmul(cmuld(cmuld(cmuld(I, w), c), 0.01), V[NN + i])   /* :791 */
+                                              : cmul(cmuld(cmuld(I, c), w), V[NN + i]);
                 pr->circs[i].dV_re = dv.re;
                 pr->circs[i].dV_im = dv.im;
             }

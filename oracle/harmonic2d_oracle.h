@@ -9,6 +9,11 @@
  *     (upper-triangular linked rows, complex-symmetric MultA, SSOR MultPC,
  *      SetValue, (Anti)Periodicity, PCGSQStart + PBCGSolve = PBCGSolveMod)
  *   FSolver::Harmonic2D               cfemm/fsolver/harmonic2d.cpp:36-873
+ *   FSolver::HarmonicAxisymmetric     cfemm/fsolver/harmonicaxi.cpp:1-800
+ *     (r-weighted flux formulation, eddy current lumped to the element mean,
+ *      r-weighted boundary terms / sources / point currents / circuits, A = 0
+ *      on the axis, B from the element energy, exterior-region warp; answers
+ *      are the flux 2 pi r A)
  *     (effective permeabilities with hysteresis lag and laminations, eddy
  *      currents, mixed and small-skin-depth boundaries, complex sources,
  *      circuits of Case 0 / 1 / 2, point currents, Dirichlet, periodicity;
@@ -49,6 +54,7 @@ typedef struct {
 typedef struct {
     int InCircuit;
     int bIsWound;
+    int IsExternal;             /* exterior region (axisymmetric) */
 } orh_label;
 
 typedef struct {
@@ -83,6 +89,8 @@ typedef struct {
     int length_units;
     int coords;
     int bandwidth;              /* CBigComplexLinProb bdw (0 = full scan) */
+    int problem_type;           /* 0 planar (Harmonic2D), 1 axisymmetric (HarmonicAxisymmetric) */
+    double extZo, extRo, extRi; /* exterior region (axisymmetric), length units of the file */
 } orh_problem;
 
 typedef struct {

@@ -118,13 +118,6 @@ def test_sharded_axisymmetric():
         assert rel_err(A, A1) <= TOL_LINEAR
 
 
-def test_harmonic_axisymmetric_is_rejected():
-    kw = synth.axisymmetric(8)
-    kw = dict(kw)
-    with pytest.raises(kernels.XfkError, match="HarmonicAxisymmetric"):
-        kernels.Harmonic2DProblem(**kw, frequency=60.0)
-
-
 def test_fem_file_interface(tmp_path):
     """.fem with [ProblemType] = axisymmetric through the C++ FSolver host:
     the .ans carries the oracle's flux 2 pi r A (same Cuthill-McKee order)."""

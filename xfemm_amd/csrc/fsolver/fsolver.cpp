@@ -650,16 +650,14 @@ bool FSolver::runSolver(bool verbose)
         PrintMessage("solving...\n");
         PrintMessage("Problem Statistics:\n%i nodes\n%i elements\nPrecision: %f\n", NumNodes, NumEls, Precision);
     }
-    if (ProblemTypeV != PLANAR && Frequency != 0) {
-        warn("harmonic axisymmetric problems are not supported by this solver build\n");
-        return false;
-    }
-    if (Frequency != 0) {
+    if (Frequency != 0) {   // Harmonic2D / HarmonicAxisymmetric, one .ans layout (fsolver.cpp:1312-1336)
         if (!Harmonic2D()) {
             warn("Couldn't solve the problem\n");
             return false;
         }
-        if (verbose) PrintMessage("Harmonic 2-D problem solved\n");
+        if (verbose)
+            PrintMessage(ProblemTypeV == AXISYMMETRIC ? "Harmonic axisymmetric problem solved\n"
+                                                      : "Harmonic 2-D problem solved\n");
         if (!WriteHarmonic2D()) {
             warn("couldn't write results to disk\n");
             return false;

@@ -11,6 +11,7 @@
 // sc1-store / relaxed-ticket / sc1-load form of cdna_hip_programming.md
 // Guideline 16 (no L2 write-back fences on the hot path).
 #include "xfk_kernels.h"
+#include "xfk_axi.h"
 
 namespace xfk {
 
@@ -437,50 +438,12 @@ __device__ void axi_element(int i, const AssembleArgs &A, const int (&n)[3], con
                             const double (&Y)[3], const DevLabel &lab, const DevBlock &bp, double (&Me)[3][3],
                             double (&be)[3])
 {
-    double p[3], q[3], g[3], rn[3], Mx[3][3], My[3][3], Mn[3][3];
-    p[0] = Y[1] - Y[2]; p[1] = Y[2] - Y[0]; p[2] = Y[0] - Y[1];
-    q[0] = X[2] - X[1]; q[1] = X[0] - X[2]; q[2] = X[1] - X[0];
-    g[0] = (X[2] + X[1]) / 2.; g[1] = (X[0] + X[2]) / 2.; g[2] = (X[1] + X[0]) / 2.;
-    rn[0] = X[0]; rn[1] = X[1]; rn[2] = X[2];
-    const double a = (p[0] * q[1] - p[1] * q[0]) / 2.;
-    const double R = (X[0] + X[1] + X[2]) / 3.;
-    double a_hat = 0;
-    for (int j = 0; j < 3; ++j) a_hat += (rn[j] * rn[j] * p[j] / (4. * R));
-    const double vol = 2. * R * a_hat;
-    int flag = 0;
-    for (int j = 0; j < 3; ++j) flag += (rn[j] < 1.e-06);
-    double R_hat = 0.;
-    if (flag == 2) {
-        R_hat = R;
-    } else if (flag == 1) {
-        if (rn[0] < 1.e-06)
-            R_hat = (fabs(rn[1] - rn[2]) < 1.e-06) ? rn[2] / 2. : (rn[1] - rn[2]) / (2. * log(rn[1]) - 2. * log(rn[2]));
-        if (rn[1] < 1.e-06)
-            R_hat = (fabs(rn[2] - rn[0]) < 1.e-06) ? rn[0] / 2. : (rn[2] - rn[0]) / (2. * log(rn[2]) - 2. * log(rn[0]));
-        if (rn[2] < 1.e-06)
-            R_hat = (fabs(rn[0] - rn[1]) < 1.e-06) ? rn[1] / 2. : (rn[0] - rn[1]) / (2. * log(rn[0]) - 2. * log(rn[1]));
-    } else {
-        if (fabs(q[0]) < 1.e-06)
-            R_hat = (q[1] * q[1]) / (2. * (-q[1] + rn[0] * log(rn[0] / rn[2])));
-        else if (fabs(q[1]) < 1.e-06)
-            R_hat = (q[2] * q[2]) / (2. * (-q[2] + rn[1] * log(rn[1] / rn[0])));
-        else if (fabs(q[2]) < 1.e-06)
-            R_hat = (q[0] * q[0]) / (2. * (-q[0] + rn[2] * log(rn[2] / rn[1])));
-        else
-            R_hat = -(q[0] * q[1] * q[2]) /
-                    (2. * (q[0] * rn[0] * log(rn[0]) + q[1] * rn[1] * log(rn[1]) + q[2] * rn[2] * log(rn[2])));
-    }
-    // Mr, Mz (staticaxi.cpp:256-276); Mrz only enters with v12 (incremental problems)
-    double K = (-1. / (2. * a_hat * R));
-    for (int j = 0; j < 3; ++j)
-        for (int k = j; k < 3; ++k) Mx[j][k] = K * p[j] * rn[j] * p[k] * rn[k];
-    for (int j = 0; j < 3; ++j)
-        if (rn[j] < 1.e-06) Mx[j][j] += Mx[0][0] + Mx[1][1] + Mx[2][2];
-    K = (-1. / (2. * a_hat * R_hat));
-    for (int j = 0; j < 3; ++j)
-        for (int k = j; k < 3; ++k) My[j][k] = K * (q[j] * rn[j]) * (q[k] * rn[k]) * (g[j] / R) * (g[k] / R);
-    Mx[1][0] = Mx[0][1]; Mx[2][0] = Mx[0][2]; Mx[2][1] = Mx[1][2];
-    My[1][0] = My[0][1]; My[2][0] = My[0][2]; My[2][1] = My[1][2];
+    AxiGeom Gm;
+    axi_geometry(X, Y, Gm);
+    double Mn[3][3];
+    const double(&Mx)[3][3] = Gm.Mx;
+    const double(&My)[3][3] = Gm.My;
+    const double a = Gm.a, R = Gm.R, vol = Gm.vol;
     for (int j = 0; j < 3; ++j) {
         for (int k = 0; k < 3; ++k) { Me[j][k] = 0.; Mn[j][k] = 0.; }
         be[j] = 0.;

@@ -22,6 +22,7 @@
 #include <complex>
 
 #include "xfk_amg.h"
+#include "xfk_axi.h"
 #include "xfk_kernels.h"
 #include "xfk_spmv.h"
 
@@ -80,6 +81,9 @@ struct HarmArgs {
     const DevCircAC *circs;
     double *val, *val_im, *b, *b_im;
     double w;
+    // HarmonicAxisymmetric (x is r, y is z; exterior-region warp in cm)
+    int axi;
+    double ext_ro, ext_ri, ext_zo;
     // successive approximation (nonlinear blocks, iter > 0)
     int iter;
     const double2 *V;                  // the current iterate
@@ -129,6 +133,140 @@ __device__ double2 hbh_dhdb(double Bq, int n, const double *__restrict__ B, cons
     return cx(0, 0);
 }
 
+// the averaged permeability of successive approximation at flux density B
+// (harmonic2d.cpp:648-656, harmonicaxi.cpp:543-553): mu = K, correction Kn
+__device__ __forceinline__ void hbh_update(double B, const DevBlockAC &bp, const HarmArgs &A, double2 &mu,
+                                           double2 &Kn)
+{
+    const double *cb = A.bhB + bp.bh_off;
+    const double2 *ch = A.bhH + bp.bh_off, *cs = A.bhS + bp.bh_off;
+    const double2 gv = hbh_v(B, bp.bh_n, cb, ch, cs), gd = hbh_dhdb(B, bp.bh_n, cb, ch, cs);
+    const double2 murel = crecip(cscale(gv, kMUO)), muinc = crecip(cscale(gd, kMUO));
+    mu = cdiv(cmul(cscale(murel, 2.), muinc), cadd(murel, muinc));
+    const double2 d = csub(crecip(murel), crecip(mu));
+    Kn = cx(-d.x, -d.y);
+}
+
+// femmcomplex abs (femmcomplex.cpp:749-757)
+__device__ __forceinline__ double cabs_(double2 x)
+{
+    if ((x.x == 0) && (x.y == 0)) return 0.;
+    if (fabs(x.x) > fabs(x.y)) return fabs(x.x) * sqrt(1. + (x.y / x.x) * (x.y / x.x));
+    return fabs(x.y) * sqrt(1. + (x.x / x.y) * (x.x / x.y));
+}
+
+// HarmonicAxisymmetric element (harmonicaxi.cpp:215-605): the r-weighted flux
+// formulation of xfk_axi.h, eddy currents lumped to the element mean, r-weighted
+// boundary terms and sources, B from the element energy, the exterior warp
+__device__ void hax_element(int i, const HarmArgs &A, const int (&n)[3], const double (&X)[3],
+                            const double (&Y)[3], const DevLabel &lab, const DevBlockAC &bp, double2 (&Me)[3][3],
+                            double2 (&be)[3])
+{
+    AxiGeom Gm;
+    axi_geometry(X, Y, Gm);
+    const double R = Gm.R, a = Gm.a;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) Me[j][k] = cx(0, 0);
+        be[j] = cx(0, 0);
+    }
+    // eddy currents, induced current constant over the element (:333-347)
+    if (bp.eddy && !lab.is_wound) {
+        double2 Ke = cx(-0.0 * R, -R);
+        Ke = cx(Ke.x * a, Ke.y * a);
+        Ke = cx(Ke.x * A.w, Ke.y * A.w);
+        Ke = cx(Ke.x * bp.Cduct, Ke.y * bp.Cduct);
+        Ke = cx(Ke.x * kC / 6., Ke.y * kC / 6.);
+        Ke = cx(Ke.x * 4. / 3., Ke.y * 4. / 3.);
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) Me[j][k] = cadd(Me[j][k], Ke);
+    }
+    // derivative boundary conditions (:349-383)
+    const int eb = A.ebits[i];
+    if (eb) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int ej = ((eb >> (10 * j)) & 1023) - 1;
+            if (ej < 0) continue;
+            const DevLineAC ln = A.lines[ej];
+            if (ln.format != 1 && ln.format != 2) continue;
+            const int k = (j + 1) % 3;
+            const double r = (X[j] + X[k]) / 2.;
+            const double lj = sqrt(pow(X[k] - X[j], 2.) + pow(Y[k] - Y[j], 2.));
+            double2 Kb;
+            if (ln.format == 2) {
+                const double s = -0.0001 * kC * 2. * r;
+                Kb = cscale(ln.c0, s);
+                Kb = cx(Kb.x * lj / 6., Kb.y * lj / 6.);
+                const double2 Kc = cx(ln.c1.x * lj / 2. * 2. * r * 0.0001, ln.c1.y * lj / 2. * 2. * r * 0.0001);
+                be[j] = cadd(be[j], Kc);
+                be[k] = cadd(be[k], Kc);
+            } else {
+                Kb = cscale(ln.zs, (2. * r * lj / 6.));
+            }
+            Me[j][j] = cadd(Me[j][j], cscale(Kb, 2.));
+            Me[k][k] = cadd(Me[k][k], cscale(Kb, 2.));
+            Me[j][k] = cadd(Me[j][k], Kb);
+            Me[k][j] = cadd(Me[k][j], Kb);
+        }
+    }
+    // source current density (:385-405)
+    double2 Jv = cx(0, 0);
+    if (lab.in_circuit >= 0) {
+        const DevCircAC C = A.circs[lab.in_circuit];
+        if (C.ccase == 1) Jv = C.J;
+        if (C.ccase == 0) Jv = cx(-100. * C.dV.x * bp.Cduct / R, -100. * C.dV.y * bp.Cduct / R);
+    }
+    {
+        const double2 Jt = cadd(bp.J, Jv);
+        const double s = -2. * R;
+        const double2 Ks = cx(s * Jt.x * a / 3., s * Jt.y * a / 3.);
+        be[0] = cadd(be[0], Ks);
+        be[1] = cadd(be[1], Ks);
+        be[2] = cadd(be[2], Ks);
+    }
+    // permeability: the block's (+ the exterior warp), or successive
+    // approximation with B derived from the element energy (:468-560)
+    double2 mu1 = bp.mu1, mu2 = bp.mu2, Kn = cx(0, 0);
+    const bool nl = bp.bh_n > 0 && A.iter > 0;
+    if (nl) {
+        double2 v[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            v[j] = cx(0, 0);
+#pragma unroll
+            for (int w = 0; w < 3; ++w) v[j] = cadd(v[j], cscale(A.V[n[w]], Gm.Mx[j][w] + Gm.My[j][w]));
+        }
+        double2 dv = cx(0, 0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const double2 vn = A.V[n[j]];
+            dv = cadd(dv, cmul(cx(vn.x, -vn.y), v[j]));
+        }
+        const double s = (10000. * kC * kC / Gm.vol);
+        dv = cx(dv.x * s, dv.y * s);
+        hbh_update(sqrt(cabs_(dv)), bp, A, mu1, Kn);
+        mu2 = mu1;
+    } else if (lab.external) {
+        const double Z = (Y[0] + Y[1] + Y[2]) / 3. - A.ext_zo;
+        const double kludge = (R * R + Z * Z) * A.ext_ri / (A.ext_ro * A.ext_ro * A.ext_ro);
+        mu1 = cx(mu1.x / kludge, mu1.y / kludge);
+        mu2 = cx(mu2.x / kludge, mu2.y / kludge);
+    }
+    const double2 r1 = crecip(mu1), r2 = crecip(mu2);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double mx = Gm.Mx[j][k], my = Gm.My[j][k];
+            Me[j][k] = cadd(Me[j][k], cadd(cscale(r2, mx), cscale(r1, my)));
+            if (nl) be[j] = cadd(be[j], cmul(cscale(Kn, mx + my), A.V[n[k]]));
+        }
+}
+
 // One colour of the element loop (harmonic2d.cpp:352-700; v12 == 0):
 // element matrices, eddy-current and boundary terms, sources, for nonlinear
 // blocks after the first pass the averaged permeability of the element's
@@ -154,6 +292,22 @@ __global__ void __launch_bounds__(kBlock) k_hassemble_color(int begin, int end, 
     const DevBlockAC bp = A.blocks[lab.blk];
     const double X[3] = {A.x[n[0]], A.x[n[1]], A.x[n[2]]};
     const double Y[3] = {A.y[n[0]], A.y[n[1]], A.y[n[2]]};
+    if (A.axi) {
+        double2 Me[3][3], be[3];
+        hax_element(i, A, n, X, Y, lab, bp, Me, be);
+        const int *sl = &s_slot[li * 9 + (li >> 3)];
+        for (int j = 0; j < 3; ++j) {
+            if (sl[3 * j] < 0) continue;
+            for (int k = 0; k < 3; ++k) {
+                const double2 m = (k >= j) ? Me[j][k] : Me[k][j];
+                A.val[sl[3 * j + k]] += m.x;
+                A.val_im[sl[3 * j + k]] += m.y;
+            }
+            A.b[n[j]] += be[j].x;
+            A.b_im[n[j]] += be[j].y;
+        }
+        return;
+    }
     double p[3], q[3];
     p[0] = Y[1] - Y[2]; p[1] = Y[2] - Y[0]; p[2] = Y[0] - Y[1];
     q[0] = X[2] - X[1]; q[1] = X[0] - X[2]; q[2] = X[1] - X[0];
@@ -230,15 +384,8 @@ __global__ void __launch_bounds__(kBlock) k_hassemble_color(int begin, int end, 
         }
         const double s1 = B1.x * B1.x - B1.y * (-B1.y), s2 = B2.x * B2.x - B2.y * (-B2.y);
         const double B = kC * sqrt(fabs(s1) + fabs(s2)) / (0.02 * a);
-        const double *cb = A.bhB + bp.bh_off;
-        const double2 *ch = A.bhH + bp.bh_off, *cs = A.bhS + bp.bh_off;
-        const double2 gv = hbh_v(B, bp.bh_n, cb, ch, cs), gd = hbh_dhdb(B, bp.bh_n, cb, ch, cs);
-        const double2 murel = crecip(cscale(gv, kMUO)), muinc = crecip(cscale(gd, kMUO));
-        const double2 Ka = cdiv(cmul(cscale(murel, 2.), muinc), cadd(murel, muinc));   // averaged
-        mu1 = Ka;
-        mu2 = Ka;
-        const double2 d = csub(crecip(murel), crecip(Ka));
-        Kn = cx(-d.x, -d.y);
+        hbh_update(B, bp, A, mu1, Kn);   // averaged secant / incremental permeability
+        mu2 = mu1;
     }
     // Mx / mu2 + My / mu1 (+ Mn, the correction moved to the right-hand side)
     const double2 r1 = crecip(mu1), r2 = crecip(mu2);
@@ -697,24 +844,33 @@ using hcx = std::complex<double>;
 inline double2 h2(hcx z) { return cx(z.real(), z.imag()); }
 inline hcx hc(double2 z) { return hcx(z.x, z.y); }
 
-DevBlockAC effective_block(const xfk_block_desc &b, const xfk_block_ac_desc &ac, double w)
+// the lag angle argument -I Theta DEG (harmonic2d.cpp) or -I Theta PI / 180
+// (harmonicaxi.cpp:133-151), halved for the lamination half-lag
+double2 lag_arg(double theta, bool axi, bool half)
 {
-    // harmonic2d.cpp:190-235 with femmcomplex.cpp's exp / tanh / quotient formulas
+    if (axi) return half ? cx(-0.0 * theta * kPI / 360., -theta * kPI / 360.) : cx(-0.0 * theta * kPI / 180., -theta * kPI / 180.);
+    return half ? cx(-0.0 * theta * kDEG / 2., -theta * kDEG / 2.) : cx(-0.0 * theta * kDEG, -theta * kDEG);
+}
+
+DevBlockAC effective_block(const xfk_block_desc &b, const xfk_block_ac_desc &ac, double w, bool axi)
+{
+    // harmonic2d.cpp:190-235 / harmonicaxi.cpp:128-170 with femmcomplex.cpp's
+    // exp / tanh / quotient formulas
     DevBlockAC o{};
     const double2 deg45 = cx(1, 1);
     double2 m0, m1;
     if (b.LamType == 0) {
-        m0 = cscale(cexp_(cx(-0.0 * ac.Theta_hx * kDEG, -ac.Theta_hx * kDEG)), b.mu_x);
-        m1 = cscale(cexp_(cx(-0.0 * ac.Theta_hy * kDEG, -ac.Theta_hy * kDEG)), b.mu_y);
+        m0 = cscale(cexp_(lag_arg(ac.Theta_hx, axi, false)), b.mu_x);
+        m1 = cscale(cexp_(lag_arg(ac.Theta_hy, axi, false)), b.mu_y);
         if (ac.Lam_d != 0) {
             if (b.Cduct != 0) {
-                double2 halflag = cexp_(cx(-0.0 * ac.Theta_hx * kDEG / 2., -ac.Theta_hx * kDEG / 2.));
+                double2 halflag = cexp_(lag_arg(ac.Theta_hx, axi, true));
                 double ds = sqrt(2. / (0.4 * kPI * w * b.Cduct * b.mu_x));
                 double2 K = cscale(cscale(cmul(halflag, deg45), ac.Lam_d), 0.001);
                 K = cx(K.x / (2. * ds), K.y / (2. * ds));
                 m0 = cscale(cdiv(cmul(m0, ctanh_(K)), K), b.LamFill);
                 m0.x += (1. - b.LamFill);
-                halflag = cexp_(cx(-0.0 * ac.Theta_hy * kDEG / 2., -ac.Theta_hy * kDEG / 2.));
+                halflag = cexp_(lag_arg(ac.Theta_hy, axi, true));
                 ds = sqrt(2. / (0.4 * kPI * w * b.Cduct * b.mu_y));
                 K = cscale(cscale(cmul(halflag, deg45), ac.Lam_d), 0.001);
                 K = cx(K.x / (2. * ds), K.y / (2. * ds));
@@ -777,10 +933,6 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     XFK_REQUIRE(d && out, XFK_ERR_ARG, "null argument");
     *out = nullptr;
     int rc = validate_desc(d);
-    if (rc == XFK_OK && d->problem_type != XFK_PLANAR) {
-        set_error("HarmonicAxisymmetric (harmonicaxi.cpp) is not implemented on the device");
-        rc = XFK_ERR_UNSUPPORTED;
-    }
     if (rc == XFK_OK) rc = harmonic_validate(d, ac);
     if (rc == XFK_OK) rc = check_device(device);
     if (rc != XFK_OK) return rc;
@@ -789,13 +941,14 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
     GlobalPrep G;
     prepare_global(d, G);
+    const bool axi = G.axi;   // HarmonicAxisymmetric (harmonicaxi.cpp)
 
     // blocks, lines
     std::vector<DevBlockAC> blk(std::max(1, d->n_blocks));
     std::vector<double> bhB;
     std::vector<double2> bhH, bhS;
     for (int k = 0; k < d->n_blocks; ++k) {
-        blk[k] = effective_block(d->blocks[k], ac->blocks[k], w);
+        blk[k] = effective_block(d->blocks[k], ac->blocks[k], w, axi);
         const xfk_block_desc &b = d->blocks[k];
         if (b.BHpoints > 0) {   // the complex curve of GetSlopes(omega)
             blk[k].bh_n = b.BHpoints;
@@ -846,7 +999,12 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
             double Cduct = d->blocks[L.blk].Cduct;
             if (L.is_wound) Cduct = 0;
             I1[L.in_circuit] += a;
-            I2[L.in_circuit] += a * Cduct;
+            if (axi) {   // conductivity / R (harmonicaxi.cpp:86-87)
+                const double r = (d->x[n[0]] + d->x[n[1]] + d->x[n[2]]) / 3.;
+                I2[L.in_circuit] += a * Cduct / (0.01 * r);
+            } else {
+                I2[L.in_circuit] += a * Cduct;
+            }
             I3[L.in_circuit] += hc(blk[L.blk].J) * a * 100.;
         }
         for (int k = 0; k < d->n_circs; ++k) {
@@ -887,12 +1045,17 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
         int m = marker(i);
         if (m >= 0 && (d->points[m].J_re != 0 || d->points[m].J_im != 0)) {   // harmonic2d.cpp:634-641
             pt_nodes.push_back(i);
-            pt_J.push_back(-0.01 * d->points[m].J_re);
-            pt_J.push_back(-0.01 * d->points[m].J_im);
+            const double s = axi ? (2. * d->x[i] * 0.01) : 0.01;   // harmonicaxi.cpp:610-617
+            pt_J.push_back(-(s * d->points[m].J_re));
+            pt_J.push_back(-(s * d->points[m].J_im));
         }
     }
     for (int i = 0; i < N; ++i) {
         int m = marker(i);
+        if (axi && d->x[i] < (units[d->length_units] * 1.e-06)) {   // A = 0 on the axis (harmonicaxi.cpp:626-631)
+            set_value(i, hcx(0, 0));
+            continue;
+        }
         if (m >= 0 && d->points[m].J_re == 0 && d->points[m].J_im == 0)
             set_value(i, hcx(d->points[m].A_re, d->points[m].A_im) / c);
     }
@@ -930,6 +1093,11 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     P->harmonic = true;
     P->omega = w;
     P->any_nonlinear = nonlin;
+    P->axi = axi;
+    if (axi) P->axi_x.assign(d->x, d->x + N);
+    P->ext_ro = G.ext_ro;
+    P->ext_ri = G.ext_ri;
+    P->ext_zo = G.ext_zo;
     P->hcircs = circ;
     P->nhpt = (int)pt_nodes.size();
     hipStream_t s = P->stream;
@@ -1013,6 +1181,10 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     A.b = P->b.p;
     A.b_im = P->b_im.p;
     A.w = P->omega;
+    A.axi = P->axi ? 1 : 0;
+    A.ext_ro = P->ext_ro;
+    A.ext_ri = P->ext_ri;
+    A.ext_zo = P->ext_zo;
     A.V = v;
     A.bhB = P->hbh_B.p;
     A.bhH = P->hbh_H.p;
@@ -1238,7 +1410,12 @@ int xfk_get_solution_complex(xfk_problem *P, double *A)
     XFK_REQUIRE(P->symbolic_ready && P->hc_vec.p, XFK_ERR_ARG, "no solution yet");
     XFK_CHECK(hipSetDevice(P->device));
     XFK_CHECK(d2h(A, P->hc_vec.p, sizeof(double2) * P->N, P->stream));
-    for (int i = 0; i < 2 * P->N; ++i) A[i] *= kC;   // harmonic2d.cpp:783
+    if (P->axi) {   // the flux 2 pi r A (harmonicaxi.cpp:790)
+        for (int i = 0; i < P->N; ++i)
+            for (int q = 0; q < 2; ++q) A[2 * i + q] = A[2 * i + q] * kC * 2. * kPI * P->axi_x[i] * 0.01;
+    } else {
+        for (int i = 0; i < 2 * P->N; ++i) A[i] *= kC;   // harmonic2d.cpp:783
+    }
     return XFK_OK;
 }
 

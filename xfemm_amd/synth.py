@@ -260,6 +260,73 @@ def axisymmetric_uniform(n: int, B0: float = 1.0, L: float = 10.0, precision: fl
                 precision=precision, length_units=2, coords=0, relax=1.0, problem_type=1)
 
 
+def harmonic_axisymmetric(n: int, L: float = 10.0, frequency: float = 60.0, precision: float = 1e-8,
+                          circuits: bool = True, nonlinear: bool = False, external: bool = False):
+    """Keyword arguments of a time-harmonic axisymmetric problem
+    (FSolver::HarmonicAxisymmetric, cfemm/fsolver/harmonicaxi.cpp) on the
+    n x n-cell square r in [0, L], z in [0, L] (cm): a laminated lossy steel
+    pot core (hysteresis lag) around a coil with a complex current density, an
+    aluminium ring below it (eddy currents), A with a phase on the outer
+    radius, a complex mixed condition on the top, a small-skin-depth bottom, a
+    complex point current; the axis takes A = 0 by the solver's rule.
+    `circuits`: the coil is a wound specified-current circuit (Case 1) and the
+    ring is driven by a voltage gradient (Case 0); `nonlinear`: the steel
+    follows the M-19 curve processed for the frequency; `external`: the outer
+    band r > 0.8 L is a mapped exterior region."""
+    x, y, p = square_mesh(n, L)
+    cxm = (x[p[:, 0]] + x[p[:, 1]] + x[p[:, 2]]) / (3.0 * L)
+    cym = (y[p[:, 0]] + y[p[:, 1]] + y[p[:, 2]]) / (3.0 * L)
+    lbl = np.zeros(len(p), dtype=np.int32)                                          # 0: air
+    pot = (cxm < 0.45) & (cym > 0.25) & (cym < 0.75)
+    cavity = (cxm > 0.12) & (cxm < 0.38) & (cym > 0.32) & (cym < 0.68)
+    lbl[pot & ~cavity] = 1                                                          # 1: steel
+    lbl[(cxm > 0.16) & (cxm < 0.32) & (cym > 0.36) & (cym < 0.64)] = 2              # 2: coil
+    lbl[(cxm > 0.1) & (cxm < 0.5) & (cym > 0.08) & (cym < 0.16)] = 3                # 3: aluminium ring
+    if external:
+        lbl[(cxm > 0.8) & (lbl == 0)] = 4                                           # 4: exterior air
+    blocks = [dict(mu_x=1.0, mu_y=1.0),
+              dict(mu_x=900.0, mu_y=900.0, Lam_d=0.35, LamFill=0.96, Cduct=2.0, Theta_hx=10.0, Theta_hy=10.0),
+              dict(mu_x=1.0, mu_y=1.0, J_re=0.0 if circuits else 2.0, J_im=0.0 if circuits else 0.7),
+              dict(mu_x=1.0, mu_y=1.0, Cduct=35.0)]
+    if nonlinear:
+        from .fsolver import bh_get_slopes_ac
+        b1 = blocks[1]
+        Bc, Hc, Sc, mu, _ = bh_get_slopes_ac(*m19_curve(), 2 * np.pi * frequency, lam_type=0,
+                                             lam_fill=b1["LamFill"], theta_hn=b1["Theta_hx"], lam_d=b1["Lam_d"],
+                                             cduct=b1["Cduct"])
+        b1.update(B=Bc, H=Hc, slope=Sc, mu_x=mu, mu_y=mu, bh="M19", Theta_hn=b1["Theta_hx"])
+    labels = [dict(block=0), dict(block=1), dict(block=2), dict(block=3)]
+    circs = []
+    if circuits:
+        labels[2] = dict(block=2, in_circuit=0, is_wound=1)
+        labels[3] = dict(block=3, in_circuit=1)
+        circs = [dict(type=0, amps_re=3000.0, amps_im=800.0), dict(type=1, dvolts_re=0.02, dvolts_im=-0.01)]
+    if external:
+        labels.append(dict(block=0, is_external=1))
+    tol = 1e-9 * L
+    e = -np.ones(p.shape, dtype=np.int32)
+    for j in range(3):
+        a, b2 = p[:, j], p[:, (j + 1) % 3]
+        right = (np.abs(x[a] - L) < tol) & (np.abs(x[b2] - L) < tol)
+        bot = (np.abs(y[a]) < tol) & (np.abs(y[b2]) < tol)
+        top = (np.abs(y[a] - L) < tol) & (np.abs(y[b2] - L) < tol)
+        e[right, j] = 0
+        e[top, j] = 1
+        e[bot, j] = 2
+    lines = [dict(format=0, A0=2e-4, A1=1e-5, phi=20.0),
+             dict(format=2, c0=2.0e5, c0_im=3.0e4, c1=0.5, c1_im=-0.2),
+             dict(format=1, Mu=1.0, Sig=5.8)]
+    m = n + 1
+    marker = -np.ones(len(x), dtype=np.int32)
+    marker[(m // 2) * m + (2 * m) // 3] = 0
+    kw = dict(x=x, y=y, p=p, lbl=lbl, e=e, marker=marker, pbc=None, blocks=blocks, labels=labels, lines=lines,
+              points=[dict(J_re=4.0, J_im=1.5)], circuits=circs, precision=precision, length_units=2, coords=0,
+              relax=1.0, problem_type=1, frequency=frequency)
+    if external:
+        kw.update(ext_zo=L / 2, ext_ro=0.8 * L, ext_ri=0.7 * L)
+    return kw
+
+
 def bc_showcase(n: int, anti: bool = False, nonlinear: bool = False, L: float = 10.0):
     """Every static boundary-condition path of Static2D on one square mesh:
     left side prescribed A = (A0 + A1*y)*cos(phi) (BdryFormat 0, static2d.cpp:840-926),
