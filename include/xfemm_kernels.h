@@ -229,11 +229,13 @@ int xfk_dist_get_info(const xfk_problem *prob, xfk_dist_info *info);
  * with a B-H curve run the reference's successive-approximation loop
  * (ACSolver 0: averaged secant / incremental permeability per element,
  * residual correction on the right-hand side, relaxation after 5 iterations,
- * stop at |dV| / |V| < 100 Precision).  The reference itself rejects LamType
- * 1/2 in AC analyses; wound regions with proximity effects (LamType > 2),
- * Case-2 circuits -- specified current in a conducting region, which adds
- * unknowns -- and the Newton AC solver (ACSolver 1) return
- * XFK_ERR_UNSUPPORTED.  Single device.
+ * stop at |dV| / |V| < 100 Precision).  Case-2 circuits -- a specified
+ * current in a conducting region, whose voltage gradient is an extra
+ * unknown -- are solved through the Schur complement of the bordered system
+ * (one extra COCG solve per such circuit; not with periodic boundaries).
+ * The reference itself rejects LamType 1/2 in AC analyses; wound regions
+ * with proximity effects (LamType > 2) and the Newton AC solver (ACSolver 1)
+ * return XFK_ERR_UNSUPPORTED.  Single device.
  * ------------------------------------------------------------------------- */
 typedef struct {
     double J_im;                /* imaginary part of the source current density, MA/m^2 */

@@ -99,3 +99,18 @@ def test_harmonic_axi_file_interface_end_to_end(tmp_path):
     nodes, _ = _read_harmonic_ans(base + ".ans")
     A = nodes[:, 2] + 1j * nodes[:, 3]
     assert rel_err(A, Ao) <= 1e-6
+
+
+def test_harmonic_axi_case2_circuit_matches_oracle():
+    kw = synth.harmonic_axisymmetric(20)
+    kw["circuits"][1] = dict(type=0, amps_re=500.0, amps_im=-100.0)   # the ring: specified current
+    pr, mesh, kk = synth_to_oracle(kw)
+    Ao, _, circ_o = oh.solve(pr, mesh)
+    assert circ_o[1][0] == 2
+    P = kernels.Harmonic2DProblem(**kk)
+    P.solve()
+    A = P.solution()
+    cc, J, dV = P.circuits()
+    P.close()
+    assert rel_err(A, Ao) <= 1e-6
+    assert cc[1] == 2 and abs(dV[1] - circ_o[1][2]) <= 1e-6 * abs(circ_o[1][2])

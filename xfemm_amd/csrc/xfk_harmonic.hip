@@ -642,6 +642,34 @@ __global__ void __launch_bounds__(256) k_hres(int N, const double2 *__restrict__
         part[gridDim.x + blockIdx.x] = s2[1];
     }
 }
+// Case-2 border: per-block partials of C . y (unconjugated, C split re / im)
+__global__ void __launch_bounds__(256) k_hc_cdot(int N, const double *__restrict__ cr, const double *__restrict__ ci,
+                                                 const double2 *__restrict__ y, double *__restrict__ part)
+{
+    __shared__ double red[2 * 4 + 2];
+    double s2[2] = {0, 0};
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < N; i += gridDim.x * 256) {
+        const double2 t = cmul(cx(cr[i], ci[i]), y[i]);
+        s2[0] += t.x;
+        s2[1] += t.y;
+    }
+    hc_block_sum<2>(s2, red);
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = s2[0];
+        part[gridDim.x + blockIdx.x] = s2[1];
+    }
+}
+// x = y0 - sum_q Y_q u_q
+__global__ void k_hc_border_combine(int N, int nc2, const double2 *__restrict__ y0, const double2 *__restrict__ Y,
+                                    const double2 *__restrict__ u, double2 *__restrict__ x)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    double2 v = y0[i];
+    for (int q = 0; q < nc2; ++q) v = csub(v, cmul(Y[(size_t)q * N + i], u[q]));
+    x[i] = v;
+}
+
 // V = Relax V + (1 - Relax) V_old (harmonic2d.cpp:851)
 __global__ void k_hrelax(int N, double relax, double2 *__restrict__ V, const double2 *__restrict__ Vo)
 {
@@ -1012,9 +1040,13 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
             C.J = cx(0, 0);
             C.dV = cx(0, 0);
             if (d->circs[k].type == 0) {
-                XFK_REQUIRE(I2[k] == 0.0, XFK_ERR_UNSUPPORTED,
-                            "circuits with a specified current in a conducting region (Case 2: extra unknowns) "
-                            "are not supported by this build");
+                if (I2[k] != 0.0) {   // Case 2: the voltage gradient is an extra unknown
+                    XFK_REQUIRE(d->n_pbc == 0, XFK_ERR_UNSUPPORTED,
+                                "Case-2 circuits (specified current in a conducting region) together with "
+                                "periodic boundaries are not supported by this build");
+                    C.ccase = 2;
+                    continue;
+                }
                 C.ccase = 1;
                 if (I1[k] != 0.0) {
                     const hcx amps(d->circs[k].amps_re, ac->circs[k].amps_im);
@@ -1087,11 +1119,74 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     for (int i = 0; i < N; ++i)
         XFK_REQUIRE((fixed[i] != 0) == (G.fixed[i] != 0), XFK_ERR_ARG, "internal: Dirichlet node sets differ");
 
+    // Case-2 circuits: the border of the system (harmonic2d.cpp:441-472, 644-650;
+    // harmonicaxi.cpp:385-417, 619-623) -- column C_k over the nodes of the
+    // circuit's region, diagonal D_k, right-hand side f_k -- depends only on the
+    // geometry, so it is built here once; SetValue moves the fixed nodes'
+    // column entries (first value) to f_k
+    std::vector<int> c2;   // circuit index of each bordered unknown
+    for (int k = 0; k < d->n_circs; ++k)
+        if (circ[k].ccase == 2) c2.push_back(k);
+    const int nc2 = (int)c2.size();
+    std::vector<double> Cb(2 * (size_t)nc2 * N, 0.0);   // per unknown: N re, then N im
+    std::vector<double2> Db(nc2, cx(0, 0)), fb(nc2, cx(0, 0));
+    if (nc2 > 0) {
+        std::vector<int> slot(std::max(1, d->n_circs), -1);
+        for (int q = 0; q < nc2; ++q) slot[c2[q]] = q;
+        for (int i = 0; i < NE; ++i) {
+            const DevLabel &L = G.lab[d->lbl[i]];
+            if (L.in_circuit < 0 || circ[L.in_circuit].ccase != 2) continue;
+            const int q = slot[L.in_circuit];
+            const int *n = d->p + 3LL * i;
+            const double p0 = d->y[n[1]] - d->y[n[2]], p1 = d->y[n[2]] - d->y[n[0]];
+            const double q0 = d->x[n[2]] - d->x[n[1]], q1 = d->x[n[0]] - d->x[n[2]];
+            const double a = (p0 * q1 - p1 * q0) / 2.;
+            const double R = (d->x[n[0]] + d->x[n[1]] + d->x[n[2]]) / 3.;
+            const double Cd = d->blocks[L.blk].Cduct;
+            const double2 Jb = blk[L.blk].J;
+            // source of the element, added once per node to the circuit row
+            double2 Ks;
+            if (axi) {
+                const double s = -2. * R;
+                Ks = cx(s * Jb.x * a / 3., s * Jb.y * a / 3.);
+                Ks = cx(Ks.x / R, Ks.y / R);
+            } else {
+                Ks = cx((-Jb.x * a) / 3., (-Jb.y * a) / 3.);
+            }
+            for (int j = 0; j < 3; ++j) fb[q] = cadd(fb[q], Ks);
+            // coupling -I a w sigma c (axi: -2 I a w sigma c)
+            double2 Kc = axi ? cx(-2. * 0.0, -2. * 1.0) : cx(-0.0, -1.0);
+            Kc = cx(Kc.x * a * w * Cd * c, Kc.y * a * w * Cd * c);
+            for (int j = 0; j < 3; ++j) {
+                double *cr = &Cb[2 * (size_t)q * N], *ci = cr + N;
+                cr[n[j]] += Kc.x / 3.;
+                ci[n[j]] += Kc.y / 3.;
+            }
+            Db[q] = cadd(Db[q], axi ? cx(Kc.x / R, Kc.y / R) : Kc);
+        }
+        for (int q = 0; q < nc2; ++q) {
+            const int k = c2[q];
+            const double s = axi ? 2. * 0.01 : 0.01;
+            fb[q] = cadd(fb[q], cx(s * d->circs[k].amps_re, s * ac->circs[k].amps_im));
+            double *cr = &Cb[2 * (size_t)q * N], *ci = cr + N;
+            for (int i = 0; i < N; ++i)
+                if (fixed[i] && (cr[i] != 0 || ci[i] != 0)) {
+                    fb[q] = csub(fb[q], cmul(cx(cr[i], ci[i]), cx(first[2 * i], first[2 * i + 1])));
+                    cr[i] = 0;
+                    ci[i] = 0;
+                }
+        }
+    }
+
     xfk_problem *P = nullptr;
     rc = build_local(d, G, nullptr, device, nullptr, &P);
     if (rc != XFK_OK) return rc;
     P->harmonic = true;
     P->omega = w;
+    P->hc2_circ = c2;
+    P->hc2_D = Db;
+    P->hc2_f = fb;
+    P->hc2_u.assign(nc2, cx(0, 0));
     P->any_nonlinear = nonlin;
     P->axi = axi;
     if (axi) P->axi_x.assign(d->x, d->x + N);
@@ -1111,6 +1206,7 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     UP(P->hfix_first, first.data(), first.size());
     UP(P->hfix_last, last.data(), last.size());
     UP(P->hbh_B, bhB.data(), bhB.size());
+    if (nc2 > 0) UP(P->hc2_C, Cb.data(), Cb.size());
     UP(P->hbh_H, bhH.data(), bhH.size());
     UP(P->hbh_S, bhS.data(), bhS.size());
 #undef UP
@@ -1306,49 +1402,129 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
             if (rc == XFK_OK) rc = P->amg->vcycle(s, H.r_im, u_im, done);
             return rc;
         };
-        XFK_CHECK(hipMemsetAsync(P->hc_part.p, 0, sizeof(double) * kHcParts * G, s));
-        CcgState init{};
-        init.tol = P->precision;
-        XFK_CHECK(hipMemcpyAsync(P->hc_state.p, &init, sizeof(CcgState), hipMemcpyHostToDevice, s));
-        k_hdiag_inv<<<nb256(N), kBlock, 0, s>>>(N, P->diag.p, P->val.p, P->val_im.p, dinv, P->hc_state.p);
-        XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
-        XFK_CHECK(hipStreamSynchronize(s));
-        if (P->hc_host->singular) {
-            set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
-            return XFK_ERR_SINGULAR;
-        }
-        if (iter > 0) k_hc_init<true><<<Gcg, kCgBlock, 0, s>>>(H, P->b.p, P->b_im.p);
-        else k_hc_init<false><<<Gcg, kCgBlock, 0, s>>>(H, P->b.p, P->b_im.p);
-        int prc;
-        if (amg && (prc = precondition()) != XFK_OK) return prc;
-        k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, 0);
-        long long it = 0;
-        int batch = amg ? 8 : 32;
-        const long long cap = std::max<long long>(100000, 20LL * N);
-        for (;;) {
-            for (int k = 0; k < batch; ++k, ++it) {
-                if (amg) {
-                    k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, Gcg, it == 0 ? Gcg : Gax);
-                    if ((prc = precondition()) != XFK_OK) return prc;
-                } else {
-                    k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, it == 0 ? Gcg : Gax, it == 0 ? Gcg : Gax);
-                }
-                k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, (int)((it + 1) & 1));
-            }
-            XFK_CHECK(hipGetLastError());
+        // one COCG solve A x = b (warm: from the current x)
+        auto solve_one = [&](double2 *xv, const double *bre, const double *bim, bool warm) -> int {
+            H.x = xv;
+            XFK_CHECK(hipMemsetAsync(P->hc_part.p, 0, sizeof(double) * kHcParts * G, s));
+            CcgState init{};
+            init.tol = P->precision;
+            XFK_CHECK(hipMemcpyAsync(P->hc_state.p, &init, sizeof(CcgState), hipMemcpyHostToDevice, s));
+            k_hdiag_inv<<<nb256(N), kBlock, 0, s>>>(N, P->diag.p, P->val.p, P->val_im.p, dinv, P->hc_state.p);
             XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
             XFK_CHECK(hipStreamSynchronize(s));
-            const CcgState &S = *P->hc_host;
-            if (S.done) break;
-            if (it >= cap) {
-                set_error("COCG did not converge within the iteration cap");
-                return XFK_ERR_NOCONV;
+            if (P->hc_host->singular) {
+                set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
+                return XFK_ERR_SINGULAR;
             }
-            double rate = (S.iters > 0 && S.er > 0 && S.er < 1) ? std::log(S.er) / (double)S.iters : 0.0;
-            long long rem = rate < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / rate) : 2 * batch;
-            batch = (int)std::max<long long>(8, std::min<long long>(rem + 2, 512));
+            if (warm) k_hc_init<true><<<Gcg, kCgBlock, 0, s>>>(H, bre, bim);
+            else k_hc_init<false><<<Gcg, kCgBlock, 0, s>>>(H, bre, bim);
+            int prc;
+            if (amg && (prc = precondition()) != XFK_OK) return prc;
+            k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, 0);
+            long long it = 0;
+            int batch = amg ? 8 : 32;
+            const long long cap = std::max<long long>(100000, 20LL * N);
+            for (;;) {
+                for (int k = 0; k < batch; ++k, ++it) {
+                    if (amg) {
+                        k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, Gcg, it == 0 ? Gcg : Gax);
+                        if ((prc = precondition()) != XFK_OK) return prc;
+                    } else {
+                        k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, it == 0 ? Gcg : Gax, it == 0 ? Gcg : Gax);
+                    }
+                    k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, (int)((it + 1) & 1));
+                }
+                XFK_CHECK(hipGetLastError());
+                XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
+                XFK_CHECK(hipStreamSynchronize(s));
+                const CcgState &S = *P->hc_host;
+                if (S.done) break;
+                if (it >= cap) {
+                    set_error("COCG did not converge within the iteration cap");
+                    return XFK_ERR_NOCONV;
+                }
+                double rate = (S.iters > 0 && S.er > 0 && S.er < 1) ? std::log(S.er) / (double)S.iters : 0.0;
+                long long rem = rate < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / rate) : 2 * batch;
+                batch = (int)std::max<long long>(8, std::min<long long>(rem + 2, 512));
+            }
+            cg_total += P->hc_host->iters;
+            return XFK_OK;
+        };
+        const int nc2 = (int)P->hc2_circ.size();
+        int src;
+        if (nc2 == 0) {
+            if ((src = solve_one(v, P->b.p, P->b_im.p, iter > 0)) != XFK_OK) return src;
+        } else {
+            // bordered system [A C; C^T D][V; u] = [b; f] through the Schur
+            // complement: Y = A^-1 C, y0 = A^-1 b, (D - C^T Y) u = f - C^T y0,
+            // V = y0 - Y u (one COCG solve per Case-2 circuit and one for b)
+            if (iter == 0) {
+                XFK_CHECK(P->hc2_Y.alloc((size_t)nc2 * N));
+                XFK_CHECK(P->hc2_y0.alloc((size_t)N));
+                XFK_CHECK(P->hres_part.alloc(2 * kResGrid));
+            }
+            const double *Cb = P->hc2_C.p;
+            for (int q = 0; q < nc2; ++q)
+                if ((src = solve_one(P->hc2_Y.p + (size_t)q * N, Cb + 2 * (size_t)q * N,
+                                     Cb + 2 * (size_t)q * N + N, iter > 0)) != XFK_OK)
+                    return src;
+            if ((src = solve_one(P->hc2_y0.p, P->b.p, P->b_im.p, iter > 0)) != XFK_OK) return src;
+            auto cdot = [&](int q, const double2 *y, hcx &out) -> int {
+                k_hc_cdot<<<kResGrid, 256, 0, s>>>(N, Cb + 2 * (size_t)q * N, Cb + 2 * (size_t)q * N + N, y,
+                                                   P->hres_part.p);
+                std::vector<double> hp(2 * kResGrid);
+                XFK_CHECK(d2h(hp.data(), P->hres_part.p, sizeof(double) * hp.size(), s));
+                double re = 0, im = 0;
+                for (int k = 0; k < kResGrid; ++k) {
+                    re += hp[k];
+                    im += hp[kResGrid + k];
+                }
+                out = hcx(re, im);
+                return XFK_OK;
+            };
+            std::vector<hcx> S((size_t)nc2 * nc2), g(nc2);
+            for (int q = 0; q < nc2; ++q) {
+                hcx t;
+                if ((src = cdot(q, P->hc2_y0.p, t)) != XFK_OK) return src;
+                g[q] = hc(P->hc2_f[q]) - t;
+                for (int r = 0; r < nc2; ++r) {
+                    if ((src = cdot(q, P->hc2_Y.p + (size_t)r * N, t)) != XFK_OK) return src;
+                    S[(size_t)q * nc2 + r] = (q == r ? hc(P->hc2_D[q]) : hcx(0, 0)) - t;
+                }
+            }
+            // small dense complex solve, partial pivoting
+            for (int k = 0; k < nc2; ++k) {
+                int pv = k;
+                for (int r = k + 1; r < nc2; ++r)
+                    if (std::abs(S[(size_t)r * nc2 + k]) > std::abs(S[(size_t)pv * nc2 + k])) pv = r;
+                if (std::abs(S[(size_t)pv * nc2 + k]) == 0.0) {
+                    set_error("singular circuit system (Case-2 circuits)");
+                    return XFK_ERR_SINGULAR;
+                }
+                if (pv != k) {
+                    for (int c2 = 0; c2 < nc2; ++c2) std::swap(S[(size_t)k * nc2 + c2], S[(size_t)pv * nc2 + c2]);
+                    std::swap(g[k], g[pv]);
+                }
+                for (int r = k + 1; r < nc2; ++r) {
+                    const hcx f = S[(size_t)r * nc2 + k] / S[(size_t)k * nc2 + k];
+                    for (int c2 = k; c2 < nc2; ++c2) S[(size_t)r * nc2 + c2] -= f * S[(size_t)k * nc2 + c2];
+                    g[r] -= f * g[k];
+                }
+            }
+            std::vector<double2> u(nc2);
+            for (int k = nc2 - 1; k >= 0; --k) {
+                hcx t = g[k];
+                for (int c2 = k + 1; c2 < nc2; ++c2) t -= S[(size_t)k * nc2 + c2] * hc(u[c2]);
+                u[k] = h2(t / S[(size_t)k * nc2 + k]);
+            }
+            P->hc2_u_old = P->hc2_u;
+            P->hc2_u = u;
+            DBuf<double2> ud;
+            XFK_CHECK(ud.alloc((size_t)nc2));
+            XFK_CHECK(hipMemcpyAsync(ud.p, u.data(), sizeof(double2) * nc2, hipMemcpyHostToDevice, s));
+            k_hc_border_combine<<<nb256(N), kBlock, 0, s>>>(N, nc2, P->hc2_y0.p, P->hc2_Y.p, ud.p, v);
+            XFK_CHECK(hipStreamSynchronize(s));
         }
-        cg_total += P->hc_host->iters;
         last_iters = P->hc_host->iters;
         if (fresh) fresh_iters = last_iters;
         XFK_CHECK(hipEventRecord(e2, s));
@@ -1375,6 +1551,10 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
             if ((resn > lastres) && (Relax > 0.1)) Relax /= 2.;
             else Relax += 0.1 * (1. - Relax);
             k_hrelax<<<nb256(N), kBlock, 0, s>>>(N, Relax, v, P->hV_old.p);
+            for (size_t q = 0; q < P->hc2_u.size(); ++q) {   // the circuit unknowns relax alike
+                const double2 a2 = P->hc2_u[q], o = P->hc2_u_old[q];
+                P->hc2_u[q] = cx(Relax * a2.x + (1.0 - Relax) * o.x, Relax * a2.y + (1.0 - Relax) * o.y);
+            }
         }
         if ((resn < 100. * P->precision) && iter > 0) break;
         if (iter >= 10000) {
@@ -1385,6 +1565,13 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipEventDestroy(e2);
+    // Case-2 circuits: the voltage gradient from the bordered unknown
+    // (harmonic2d.cpp:784-785: I c w V[N+k]; harmonicaxi.cpp:791: I w c 0.01 V[N+k])
+    for (size_t q = 0; q < P->hc2_circ.size(); ++q) {
+        const double2 f = P->axi ? cx(0.0 * P->omega * kC * 0.01, P->omega * kC * 0.01)
+                                 : cx(0.0 * kC * P->omega, kC * P->omega);
+        P->hcircs[P->hc2_circ[q]].dV = cmul(f, P->hc2_u[q]);
+    }
     R.ms_assemble = ms_asm;
     R.ms_solve = ms_sol;
     R.newton_iters = iter + 1;

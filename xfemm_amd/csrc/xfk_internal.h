@@ -312,6 +312,12 @@ struct xfk_problem {
     xfk::DBuf<double2> hbh_H, hbh_S;
     xfk::DBuf<double2> hV_old;                   // the iterate before the solve
     xfk::DBuf<double> hres_part;                 // residual partial sums
+    // Case-2 circuits: bordered unknowns solved through their Schur complement
+    std::vector<int> hc2_circ;                   // circuit of each bordered unknown
+    std::vector<double2> hc2_D, hc2_f, hc2_u;    // diagonal, right-hand side, solution (u: V[N + k])
+    std::vector<double2> hc2_u_old;
+    xfk::DBuf<double> hc2_C;                     // border columns, per unknown N re then N im
+    xfk::DBuf<double2> hc2_Y, hc2_y0;            // A^-1 C_k and A^-1 b
     xfk::DBuf<double> hc_part;                   // per-block partials, 9 arrays
     xfk::DBuf<xfk::CcgState> hc_state;
     xfk::CcgState *hc_host = nullptr;            // pinned mirror
