@@ -103,7 +103,7 @@ def pmc_traffic(algo_bytes, kernel="k_cg_spmv"):
     Only a summary of the same workload counts: its traffic must lie within
     [0.8, 2] x this launch's algorithmic bytes."""
     import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), key=os.path.getmtime)
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))  # tag order: r01 < r01b < ...
     for path in reversed(paths):
         try:
             with open(path) as f:

@@ -1,0 +1,15 @@
+# rocprofv3 kernel trace (+ --stats) of the bench, then separate PMC passes
+# (FETCH_SIZE, WRITE_SIZE; never combined with tracing domains) over the PCG
+# kernels.  Usage: bash tools/profile.sh TAG [extra bench args]
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+TAG=${1:-r01}
+shift || true
+OUT=gpurun_out/prof_$TAG
+REGEX='k_cg_spmv|k_cg_axpy|k_amg_smooth<'
+mkdir -p $OUT
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -T -f csv -d $OUT/trace -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $OUT/bench_trace.json 2> $OUT/trace.err && \
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -T -f csv --kernel-include-regex "$REGEX" -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@" > $OUT/bench_fetch.json 2> $OUT/fetch.err && \
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -T -f csv --kernel-include-regex "$REGEX" -d $OUT/pmc_write -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@" > $OUT/bench_write.json 2> $OUT/write.err && \
+python3 tools/pmc_summary.py $OUT > $OUT/pmc_summary.json
