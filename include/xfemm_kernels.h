@@ -77,6 +77,20 @@ typedef struct {
     double dvolts_re;
 } xfk_circuit_desc;
 
+/* CAirGapElement (cfemm/libfemm/CAirGapElement.h) as FSolver::LoadMesh reads it
+ * from the .pbc file (fsolver.cpp:425-515): an unmeshed annulus between two
+ * rings of equally spaced boundary nodes, coupled by totalArcElements
+ * "air-gap elements" (static2d.cpp:191-344, harmonic2d.cpp:227-380). */
+typedef struct {
+    int format;                 /* BdryFormat: 0 periodic, 1 antiperiodic copies */
+    double ri, ro;              /* inner / outer radius */
+    double total_arc_length;    /* degrees spanned by the AGE */
+    double inner_shift, outer_shift;   /* InnerShift / OuterShift, in arc elements */
+    int n_arc;                  /* totalArcElements */
+    const int *qn;              /* 4 * (n_arc + 1): quadNode[k].n0 n1 n2 n3 */
+    const double *qw;           /* 4 * (n_arc + 1): quadNode[k].w0 w1 w2 w3 */
+} xfk_age_desc;
+
 typedef struct {
     int n_nodes;
     const double *x, *y;        /* node coordinates, cm */
@@ -98,6 +112,8 @@ typedef struct {
     int problem_type;           /* [ProblemType]: XFK_PLANAR (Static2D) or XFK_AXISYMMETRIC
                                    (FSolver::StaticAxisymmetric, staticaxi.cpp:45-794: x is r, y is z) */
     double ext_zo, ext_ro, ext_ri;   /* [extZo] [extRo] [extRi]: axisymmetric exterior region, user units */
+    int n_ages;  const xfk_age_desc *ages;   /* air-gap elements (planar; ignored when axisymmetric,
+                                                as StaticAxisymmetric / HarmonicAxisymmetric do) */
 } xfk_problem_desc;
 
 enum { XFK_PLANAR = 0, XFK_AXISYMMETRIC = 1 };
@@ -296,6 +312,12 @@ int xfk_pcg_solve_csr(int n, const int *rowptr, const int *col, const double *va
 int xfk_pcg_solve_csr_pc(int n, const int *rowptr, const int *col, const double *val,
                          const double *b, double *V, int flag, double precision,
                          int device, int precond, long long *iters, double *er);
+
+/* Air-gap element matrix of one arc element (host math, no device needed):
+ * MG (10 x 10, row-major) for the reduced ring shifts ci, co and
+ * K = dr / (R dtheta), Ki = 1 / K.  Replaces the closed form of
+ * cfemm/fsolver/static2d.cpp:209-263 (harmonic2d.cpp:245-300). */
+int xfk_age_element_matrix(double ci, double co, double K, double Ki, double *MG);
 
 /* Timing probe of the CG kernels (profiles / roofline): run `iters` PCG
  * iterations on the assembled system without a convergence stop; returns the

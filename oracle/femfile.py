@@ -30,6 +30,8 @@ import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
+import dataclasses
+
 import numpy as np
 
 MUO = 1.2566370614359173e-6          # femmconstants.h
@@ -641,6 +643,9 @@ class Mesh:
     pbc: np.ndarray          # (npbc,3) x,y,t
     bandwidth: int = 0
     edges: Optional[np.ndarray] = None   # (nedge,3) n0,n1,marker (raw .edge content)
+    # air-gap elements (CAirGapElement): dicts format, ri, ro, total_arc_length,
+    # inner_shift, outer_shift, qn / qw ((n_arc + 1) x 4)
+    ages: list = dataclasses.field(default_factory=list)
 
 
 def _read_ints_floats(path):
@@ -667,9 +672,19 @@ def load_mesh(base: str, pr: FemProblem) -> Mesh:
     for i in range(npbc):
         f = plines[1 + i].split()
         pbc[i] = (int(f[1]), int(f[2]), int(f[3]))
+    # air-gap elements (fsolver.cpp:425-515): name line, parameter line,
+    # totalArcElements + 1 quadNode lines
     nage = int(plines[1 + npbc].split()[0]) if len(plines) > 1 + npbc else 0
-    if nage != 0:
-        raise NotImplementedError("air-gap elements are not restated by this oracle")
+    ages, ln = [], 2 + npbc
+    for _ in range(nage):
+        f = plines[ln + 1].split()
+        n = int(f[8])
+        q = [plines[ln + 2 + k].split() for k in range(n + 1)]
+        ages.append(dict(format=int(f[0]), ri=float(f[3]), ro=float(f[4]), total_arc_length=float(f[5]),
+                         inner_shift=float(f[9]), outer_shift=float(f[10]),
+                         qn=np.array([[int(r[0]), int(r[2]), int(r[4]), int(r[6])] for r in q], np.int32),
+                         qw=np.array([[float(r[1]), float(r[3]), float(r[5]), float(r[7])] for r in q])))
+        ln += n + 3
 
     tok = _read_ints_floats(base + ".ele")
     ne = int(tok[0])
@@ -709,7 +724,7 @@ def load_mesh(base: str, pr: FemProblem) -> Mesh:
                     e[el, 1] = j
                 if (c == n0 and a == n1) or (c == n1 and a == n0):
                     e[el, 2] = j
-    return Mesh(x=x, y=y, marker=marker, p=p, e=e, lbl=lbl, blk=blk, pbc=pbc, edges=edges)
+    return Mesh(x=x, y=y, marker=marker, p=p, e=e, lbl=lbl, blk=blk, pbc=pbc, edges=edges, ages=ages)
 
 
 def cuthill(mesh: Mesh) -> np.ndarray:
@@ -777,7 +792,9 @@ def cuthill(mesh: Mesh) -> np.ndarray:
         if n >= nn:
             break
     newnum_a = np.array(newnum, dtype=np.int64)
-    # remap pbcs
+    # remap air-gap quadNodes (cuthill.cpp:321-330) and pbcs
+    for a in mesh.ages:
+        a["qn"] = newnum_a[a["qn"]].astype(np.int32)
     if len(mesh.pbc):
         mesh.pbc[:, 0] = newnum_a[mesh.pbc[:, 0]]
         mesh.pbc[:, 1] = newnum_a[mesh.pbc[:, 1]]

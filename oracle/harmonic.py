@@ -39,6 +39,26 @@ class OrhCirc(C.Structure):
                 ("J_re", C.c_double), ("J_im", C.c_double), ("dV_re", C.c_double), ("dV_im", C.c_double)]
 
 
+class OraAge(C.Structure):
+    """ora_age (static2d_oracle.h): one air-gap element."""
+    _fields_ = [("BdryFormat", C.c_int), ("ri", C.c_double), ("ro", C.c_double), ("totalArcLength", C.c_double),
+                ("InnerShift", C.c_double), ("OuterShift", C.c_double), ("totalArcElements", C.c_int),
+                ("qn", iptr), ("qw", dptr)]
+
+
+def make_ages(mesh, keep):
+    ages = (OraAge * max(1, len(mesh.ages)))()
+    for k, a in enumerate(mesh.ages):
+        o = ages[k]
+        o.BdryFormat, o.ri, o.ro = int(a.get("format", 0)), a["ri"], a["ro"]
+        o.totalArcLength, o.InnerShift, o.OuterShift = a["total_arc_length"], a["inner_shift"], a["outer_shift"]
+        qn = np.asarray(a["qn"], np.int32).reshape(-1, 4)
+        o.totalArcElements = len(qn) - 1
+        o.qn, o.qw = keep.i(qn.reshape(-1)), keep.d(np.asarray(a["qw"], float).reshape(-1))
+    keep.items.append(ages)
+    return len(mesh.ages), ages
+
+
 class OrhProblem(C.Structure):
     _fields_ = [("n_nodes", C.c_int), ("x", dptr), ("y", dptr), ("marker", iptr),
                 ("n_elems", C.c_int), ("p", iptr), ("e", iptr), ("lbl", iptr), ("blk", iptr),
@@ -50,7 +70,8 @@ class OrhProblem(C.Structure):
                 ("n_pbc", C.c_int), ("pbc", iptr),
                 ("precision", C.c_double), ("frequency", C.c_double), ("length_units", C.c_int),
                 ("coords", C.c_int), ("bandwidth", C.c_int), ("problem_type", C.c_int),
-                ("extZo", C.c_double), ("extRo", C.c_double), ("extRi", C.c_double)]
+                ("extZo", C.c_double), ("extRo", C.c_double), ("extRi", C.c_double),
+                ("n_ages", C.c_int), ("ages", C.POINTER(OraAge))]
 
 
 _CREATE = C.CFUNCTYPE(C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double)
@@ -142,6 +163,7 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
     P.precision, P.frequency = pr.Precision, pr.Frequency
     P.length_units, P.coords, P.bandwidth = pr.LengthUnits, pr.Coords, mesh.bandwidth
     P.problem_type, P.extZo, P.extRo, P.extRi = pr.ProblemType, pr.extZo, pr.extRo, pr.extRi
+    P.n_ages, P.ages = make_ages(mesh, keep)
     keep.items.extend([blocks, labels, lines, points, circs])
     return P, keep, circs
 

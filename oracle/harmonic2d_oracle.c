@@ -747,6 +747,12 @@ static void axi_element(orh_problem *pr, const orh_linprob_ops *ops, void *L, co
     }
 }
 
+static void hage_emit(void *ctx, double v, int p, int q)
+{
+    struct hage_ctx { const orh_linprob_ops *ops; void *L; } *a = ctx;
+    a->ops->addto(a->L, -v, 0.0, p, q);   /* opposite sign to Static2D (harmonic2d.cpp:382) */
+}
+
 static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L, const effmu *Mu, double w,
                            int Iter)
 {
@@ -757,6 +763,10 @@ static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L,
     cx *bL = (cx *)ops->b(L);
     cx *VL = (cx *)ops->V(L);
     const int axi = pr->problem_type == 1;
+    if (!axi) {   /* air-gap elements first (harmonic2d.cpp:227-380), real entries */
+        struct hage_ctx { const orh_linprob_ops *ops; void *L; } actx = {ops, L};
+        ora_age_assemble(pr->n_ages, pr->ages, hage_emit, &actx);
+    }
     for (int i = 0; i < pr->n_elems; i++) {
         if (axi) {
             axi_element(pr, ops, L, Mu, w, Iter, i, VL, bL);

@@ -91,6 +91,7 @@ typedef struct {
     int bandwidth;              /* CBigComplexLinProb bdw (0 = full scan) */
     int problem_type;           /* 0 planar (Harmonic2D), 1 axisymmetric (HarmonicAxisymmetric) */
     double extZo, extRo, extRi; /* exterior region (axisymmetric), length units of the file */
+    int n_ages;  const ora_age *ages;   /* air-gap elements (planar only) */
 } orh_problem;
 
 typedef struct {

@@ -52,6 +52,26 @@ class OraCirc(C.Structure):
                 ("Case", C.c_int), ("J", C.c_double), ("dV", C.c_double)]
 
 
+class OraAge(C.Structure):
+    """ora_age (static2d_oracle.h): one air-gap element."""
+    _fields_ = [("BdryFormat", C.c_int), ("ri", C.c_double), ("ro", C.c_double), ("totalArcLength", C.c_double),
+                ("InnerShift", C.c_double), ("OuterShift", C.c_double), ("totalArcElements", C.c_int),
+                ("qn", iptr), ("qw", dptr)]
+
+
+def make_ages(mesh, keep):
+    ages = (OraAge * max(1, len(mesh.ages)))()
+    for k, a in enumerate(mesh.ages):
+        o = ages[k]
+        o.BdryFormat, o.ri, o.ro = int(a.get("format", 0)), a["ri"], a["ro"]
+        o.totalArcLength, o.InnerShift, o.OuterShift = a["total_arc_length"], a["inner_shift"], a["outer_shift"]
+        qn = np.asarray(a["qn"], np.int32).reshape(-1, 4)
+        o.totalArcElements = len(qn) - 1
+        o.qn, o.qw = keep.i(qn.reshape(-1)), keep.d(np.asarray(a["qw"], float).reshape(-1))
+    keep.items.append(ages)
+    return len(mesh.ages), ages
+
+
 class OraProblem(C.Structure):
     _fields_ = [("n_nodes", C.c_int), ("x", dptr), ("y", dptr), ("marker", iptr),
                 ("n_elems", C.c_int), ("p", iptr), ("e", iptr), ("lbl", iptr), ("blk", iptr),
@@ -63,7 +83,8 @@ class OraProblem(C.Structure):
                 ("n_pbc", C.c_int), ("pbc", iptr),
                 ("precision", C.c_double), ("length_units", C.c_int), ("coords", C.c_int),
                 ("bandwidth", C.c_int), ("relax", C.c_double),
-                ("axisymmetric", C.c_int), ("ext_ro", C.c_double), ("ext_ri", C.c_double), ("ext_zo", C.c_double)]
+                ("axisymmetric", C.c_int), ("ext_ro", C.c_double), ("ext_ri", C.c_double), ("ext_zo", C.c_double),
+                ("n_ages", C.c_int), ("ages", C.POINTER(OraAge))]
 
 
 class OraStats(C.Structure):
@@ -224,6 +245,7 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
     P.bandwidth, P.relax = mesh.bandwidth, pr.Relax
     P.axisymmetric = int(pr.ProblemType == 1)
     P.ext_ro, P.ext_ri, P.ext_zo = pr.extRo, pr.extRi, pr.extZo
+    P.n_ages, P.ages = make_ages(mesh, keep)
     keep.items.extend([blocks, labels, lines, points, circs])
     return P, keep, circs
 

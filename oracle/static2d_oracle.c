@@ -380,6 +380,12 @@ static void ora_circuits(ora_problem *pr)
 }
 
 /* one Newton iteration's assembly + boundary conditions (static2d.cpp:186-940) */
+static void age_emit(void *ctx, double v, int p, int q)
+{
+    struct age_ctx { const ora_linprob_ops *ops; void *L; } *a = ctx;
+    a->ops->addto(a->L, v, p, q);
+}
+
 static void ora_assemble(ora_problem *pr, const ora_linprob_ops *ops, void *L, int Iter,
                          double *mu1, double *mu2, double *v12, int *LinearFlag_io)
 {
@@ -389,6 +395,10 @@ static void ora_assemble(ora_problem *pr, const ora_linprob_ops *ops, void *L, i
     int LinearFlag = *LinearFlag_io;
         double *b = ops->b(L);
         double *Vv = ops->V(L);
+
+        /* air-gap elements first (static2d.cpp:191-344) */
+        struct age_ctx { const ora_linprob_ops *ops; void *L; } actx = {ops, L};
+        ora_age_assemble(pr->n_ages, pr->ages, age_emit, &actx);
 
         for (int i = 0; i < NE; i++) {
             double Me[3][3], be[3], Mx[3][3], My[3][3], Mxy[3][3], Mn[3][3];

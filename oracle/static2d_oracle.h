@@ -67,6 +67,22 @@ typedef struct {
     double dV;              /* out */
 } ora_circ;
 
+/* CAirGapElement after FSolver::LoadMesh (fsolver.cpp:425-515). */
+typedef struct {
+    int BdryFormat;             /* 0 periodic, 1 antiperiodic copies */
+    double ri, ro, totalArcLength, InnerShift, OuterShift;
+    int totalArcElements;
+    const int *qn;              /* quadNode[k].n0..n3 at 4k+0..3, k = 0..totalArcElements */
+    const double *qw;           /* quadNode[k].w0..w3 */
+} ora_age;
+
+typedef void (*ora_age_emit)(void *ctx, double v, int p, int q);
+/* MG of one arc element (row-major 10x10), static2d.cpp:209-263. */
+void ora_age_matrix(double ci, double co, double K, double Ki, double *MG);
+/* Every air-gap contribution as AddTo(v, p, q) calls in the reference's order
+ * (static2d.cpp:191-344). */
+void ora_age_assemble(int n_ages, const ora_age *ages, ora_age_emit emit, void *ctx);
+
 typedef struct {
     int n_nodes;
     const double *x, *y;        /* cm */
@@ -89,6 +105,7 @@ typedef struct {
     double relax;               /* FSolver::Relax (1.0 after LoadProblemFile) */
     int axisymmetric;           /* ProblemType: 0 planar (Static2D), 1 axisymmetric */
     double ext_ro, ext_ri, ext_zo;   /* exterior-region parameters (user units) */
+    int n_ages;  const ora_age *ages;   /* air-gap elements (planar only, as the reference) */
 } ora_problem;
 
 typedef struct {

@@ -1,0 +1,129 @@
+"""Air-gap elements on the GPU (static and time-harmonic planar) vs the oracle.
+
+The host reduces every AGE contribution (static2d.cpp:191-344,
+harmonic2d.cpp:227-380) once per problem to one value per matrix entry; the
+entries join the CSR pattern as fill-in and the GPU adds them after the
+element scatter.  Checked here: the assembled system after all boundary
+conditions (<= 1e-12 of max |entry|), A at every node (<= 1e-6 linear,
+<= 1e-5 nonlinear, relative to max |A|), the antiperiodic half machine, the
+sharded path's refusal and the .fem/.pbc file path through FSolver.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import harmonic as oh
+from oracle import oracle
+from util import rel_err, solver_tolerance, synth_to_oracle
+from xfemm_amd import kernels, synth
+
+pytestmark = pytest.mark.gpu
+
+TOL_SYSTEM = 1e-12
+TOL_LINEAR = 1e-6
+TOL_NONLINEAR = 1e-5
+
+
+def _csr(P):
+    rp, col, val, b = P.csr()
+    n = len(rp) - 1
+    return sp.csr_matrix((val, col, rp), shape=(n, n)), b
+
+
+@pytest.mark.parametrize("half,angle", [(False, 0.0), (False, 2.3), (True, 9.0)])
+def test_static_system_matches_oracle(half, angle):
+    pr, mesh, kk = synth_to_oracle(synth.age_motor(48, 4, half=half, rotor_angle=angle))
+    P = kernels.Static2DProblem(**kk)
+    P.solve()
+    G, b = _csr(P)
+    Go, bo = oracle.system(pr, mesh)
+    assert abs(G - Go).max() <= TOL_SYSTEM * abs(Go).max()
+    assert np.abs(b - bo).max() <= TOL_SYSTEM * np.abs(bo).max()
+    P.close()
+
+
+@pytest.mark.parametrize("half,angle,precond", [(False, 2.3, "amg"), (True, 9.0, "amg"), (False, 5.0, "jacobi")])
+def test_static_solution_matches_oracle(half, angle, precond):
+    pr, mesh, kk = synth_to_oracle(synth.age_motor(64, 6, half=half, rotor_angle=angle))
+    P = kernels.Static2DProblem(precond=precond, **kk)
+    P.solve()
+    A = P.solution()
+    Ao, _, _ = oracle.solve(pr, mesh)
+    assert rel_err(A, Ao) <= solver_tolerance(TOL_LINEAR, Ao, P)
+    P.close()
+
+
+def test_static_nonlinear_matches_oracle():
+    pr, mesh, kk = synth_to_oracle(synth.age_motor(48, 4, rotor_angle=3.1, nonlinear=True))
+    Ao, st, _ = oracle.solve(pr, mesh)
+    P = kernels.Static2DProblem(**kk)
+    r = P.solve()
+    A = P.solution()
+    P.close()
+    assert st["newton_iters"] > 1 and r["newton_iters"] > 1
+    assert rel_err(A, Ao) <= TOL_NONLINEAR
+
+
+def test_gpu_full_machine_equals_half():
+    nth = 64
+    sol = {}
+    for half in (False, True):
+        kw = synth.age_motor(nth, 5, half=half, rotor_angle=4.4, precision=1e-12)
+        P = kernels.Static2DProblem(**synth_to_oracle(kw)[2])
+        P.solve()
+        sol[half] = P.solution().reshape(-1, nth // 2 + 1 if half else nth)
+        P.close()
+    F, H = sol[False], sol[True]
+    assert np.abs(F[:, :nth // 2 + 1] - H).max() <= 1e-8 * np.abs(F).max()
+
+
+def test_sharded_solve_refuses_air_gaps():
+    kk = synth_to_oracle(synth.age_motor(24, 3))[2]
+    kk.pop("pbc", None)
+    comms = kernels.Comm.local_group(1)
+    try:
+        with pytest.raises(kernels.XfkError):
+            kernels.Static2DProblem(comm=comms[0], **kk)
+    finally:
+        for c in comms:
+            c.close()
+
+
+def _harmonic_kw(half=False, angle=2.3, nonlinear=False):
+    kw = synth.age_motor(48, 4, half=half, rotor_angle=angle, nonlinear=nonlinear)
+    kw["frequency"] = 60.0
+    kw["blocks"][1]["Cduct"] = 2.0          # conducting rotor / stator steel: eddy currents
+    kw["blocks"][3]["J_im"] = 1.0
+    return kw
+
+
+@pytest.mark.parametrize("half", [False, True])
+def test_harmonic_matches_oracle(half):
+    pr, mesh, kk = synth_to_oracle(_harmonic_kw(half=half))
+    P = kernels.Harmonic2DProblem(**kk)
+    P.solve()
+    G, b = _csr(P)
+    Go, bo = oh.system(pr, mesh)
+    assert abs(G - Go).max() <= TOL_SYSTEM * abs(Go).max()
+    A = P.solution()
+    Ao, _, _ = oh.solve(pr, mesh)
+    assert rel_err(A, Ao) <= TOL_LINEAR
+    P.close()
+
+
+def test_static_file_interface(tmp_path):
+    """.fem + .pbc with an air-gap element section -> C++ FSolver -> .ans."""
+    from oracle import femfile
+    from xfemm_amd import fsolver
+    kw = synth.age_motor(48, 4, half=True, rotor_angle=2.3)
+    base = str(tmp_path / "age")
+    synth.write_problem(base, kw)
+    pr, mesh = femfile.load_problem(base)
+    assert len(mesh.ages) == 1
+    Ao, _, _ = oracle.solve(pr, mesh)
+    fs = fsolver.FSolver()
+    fs.PathName = base
+    assert fs.LoadProblemFile()
+    assert fs.runSolver(False), fs.last_error()
+    ans = femfile.read_ans(base + ".ans")
+    assert rel_err(ans.A, Ao) <= TOL_LINEAR

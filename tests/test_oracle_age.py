@@ -1,0 +1,125 @@
+"""Air-gap elements on the CPU: the element matrix tables and the oracle.
+
+* Both monomial tables of the AGE matrix (the product host's, reached through
+  the C-ABI xfk_age_element_matrix, and the oracle's) reproduce the
+  reference's closed form (cfemm/fsolver/static2d.cpp:209-263), evaluated
+  exactly at sample points by tools/gen_age_table.py into
+  tests/golden/age_mg.json.
+* The oracle's AGE assembly (oracle/age_oracle.c, static2d.cpp:191-344) is
+  pinned by a property of the operator itself: a full-circle machine and its
+  antiperiodic half (AGE BdryFormat 1: signed ring copies, sign fixes at the
+  slice ends, plus antiperiodic pbc pairs) give the same A on the shared half,
+  for rotor angles that put the rings off-grid (ci != co).  No golden .ans of
+  the reference has an air gap (its fmesher is needed to make one), so this is
+  the pin beside the table check.
+* .pbc parsing of the AGE section, Cuthill-McKee remapping of the quadNodes.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import femfile, oracle
+from util import synth_to_oracle
+from xfemm_amd import kernels, synth
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "age_mg.json")
+
+
+def _points():
+    with open(GOLD) as f:
+        return json.load(f)["points"]
+
+
+@pytest.mark.parametrize("k", range(6))
+def test_host_age_matrix_matches_reference_closed_form(k):
+    pt = _points()[k]
+    M = kernels.age_element_matrix(pt["ci"], pt["co"], pt["K"], pt["Ki"])
+    R = np.array(pt["MG"])
+    assert np.abs(M - R).max() <= 1e-13 * np.abs(R).max()
+
+
+@pytest.mark.parametrize("k", range(6))
+def test_oracle_age_matrix_matches_reference_closed_form(k):
+    import ctypes as C
+    pt = _points()[k]
+    L = oracle.lib()
+    L.ora_age_matrix.argtypes = [C.c_double] * 4 + [C.POINTER(C.c_double)]
+    M = np.zeros(100)
+    L.ora_age_matrix(pt["ci"], pt["co"], pt["K"], pt["Ki"], M.ctypes.data_as(C.POINTER(C.c_double)))
+    R = np.array(pt["MG"])
+    assert np.abs(M.reshape(10, 10) - R).max() <= 1e-13 * np.abs(R).max()
+
+
+def test_age_matrix_is_psd_with_constant_null_space():
+    """Properties of a stiffness matrix: symmetric, positive semi-definite,
+    constants in the null space (rows sum to zero)."""
+    for ci, co in [(1.0, 1.0), (0.15, 0.0), (0.5, 0.0), (0.93, 1.0)]:
+        M = kernels.age_element_matrix(ci, co, 0.07, 1 / 0.07)
+        assert np.allclose(M, M.T, rtol=0, atol=1e-14 * np.abs(M).max())
+        assert np.linalg.eigvalsh(M).min() >= -1e-12 * np.abs(M).max()
+        assert np.abs(M.sum(1)).max() <= 1e-12 * np.abs(M).max()
+
+
+@pytest.mark.parametrize("angle", [0.0, 2.3, 9.0])
+def test_oracle_full_machine_equals_antiperiodic_half(angle):
+    nth = 24
+    sol = {}
+    for half in (False, True):
+        kw = synth.age_motor(nth, 3, half=half, rotor_angle=angle, precision=1e-12)
+        pr, mesh, _ = synth_to_oracle(kw)
+        A, st, _ = oracle.solve(pr, mesh)
+        sol[half] = A.reshape(-1, nth // 2 + 1 if half else nth)
+    F, H = sol[False], sol[True]
+    scale = np.abs(F).max()
+    assert scale > 1e-3
+    assert np.abs(F[:, :nth // 2 + 1] - H).max() <= 1e-9 * scale
+    assert np.abs(F[:, :nth // 2] + F[:, nth // 2:]).max() <= 1e-9 * scale   # the machine is antiperiodic
+
+
+def test_rotor_angle_changes_the_field():
+    kw0 = synth.age_motor(24, 3, rotor_angle=0.0)
+    kw1 = synth.age_motor(24, 3, rotor_angle=7.5)
+    A0 = oracle.solve(*synth_to_oracle(kw0)[:2])[0]
+    A1 = oracle.solve(*synth_to_oracle(kw1)[:2])[0]
+    assert np.abs(A0 - A1).max() > 1e-3 * np.abs(A0).max()
+
+
+def test_pbc_file_age_section_roundtrip(tmp_path):
+    kw = synth.age_motor(24, 3, half=True, rotor_angle=2.3)
+    base = str(tmp_path / "m")
+    synth.write_problem(base, kw)
+    pr, mesh = femfile.load_problem(base)
+    assert len(mesh.ages) == 1 and len(mesh.pbc) == len(kw["pbc"])
+    a, g = mesh.ages[0], kw["ages"][0]
+    assert a["format"] == 1 and a["total_arc_length"] == 180.0
+    assert a["inner_shift"] == g["inner_shift"] and a["outer_shift"] == g["outer_shift"]
+    assert np.array_equal(a["qw"], g["qw"])
+    # quadNodes follow the Cuthill-McKee renumbering: same coordinates
+    for q_new, q_old in zip(a["qn"].reshape(-1), np.asarray(g["qn"]).reshape(-1)):
+        assert mesh.x[q_new] == pytest.approx(kw["x"][q_old]) and mesh.y[q_new] == pytest.approx(kw["y"][q_old])
+    # and the renumbered problem gives the same field
+    A_file, _, _ = oracle.solve(pr, mesh)
+    A_mem, _, _ = oracle.solve(*synth_to_oracle(kw)[:2])
+    order = np.lexsort((np.round(mesh.y, 9), np.round(mesh.x, 9)))
+    order0 = np.lexsort((np.round(kw["y"], 9), np.round(kw["x"], 9)))
+    assert np.abs(A_file[order] - A_mem[order0]).max() <= 1e-6 * np.abs(A_mem).max()
+
+
+def test_harmonic_oracle_full_machine_equals_antiperiodic_half():
+    """Harmonic2D adds the AGE matrix with the opposite sign
+    (harmonic2d.cpp:382); the antiperiodic half still equals the full machine."""
+    from oracle import harmonic as oh
+    nth = 24
+    sol = {}
+    for half in (False, True):
+        kw = synth.age_motor(nth, 3, half=half, rotor_angle=4.0, precision=1e-12)
+        kw["frequency"] = 60.0
+        kw["blocks"][1]["Cduct"] = 2.0
+        pr, mesh, _ = synth_to_oracle(kw)
+        A, _, _ = oh.solve(pr, mesh)
+        sol[half] = A.reshape(-1, nth // 2 + 1 if half else nth)
+    F, H = sol[False], sol[True]
+    assert np.isfinite(F).all() and np.abs(F).max() > 1e-4
+    assert np.abs(F[:, :nth // 2 + 1] - H).max() <= 1e-9 * np.abs(F).max()

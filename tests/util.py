@@ -31,7 +31,7 @@ def kernel_kwargs(pr: femfile.FemProblem, mesh: femfile.Mesh) -> dict:
                 pbc=mesh.pbc if len(mesh.pbc) else None, blocks=blocks, labels=labels, lines=lines,
                 points=points, circuits=circuits, precision=pr.Precision, length_units=pr.LengthUnits,
                 coords=pr.Coords, relax=pr.Relax, frequency=pr.Frequency, problem_type=pr.ProblemType,
-                ext_zo=pr.extZo, ext_ro=pr.extRo, ext_ri=pr.extRi)
+                ext_zo=pr.extZo, ext_ro=pr.extRo, ext_ri=pr.extRi, ages=list(mesh.ages))
 
 
 def synth_to_oracle(kw: dict):
@@ -85,7 +85,8 @@ def synth_to_oracle(kw: dict):
                         p=np.asarray(kw["p"], np.int32),
                         e=np.asarray(kw["e"], np.int32), lbl=np.asarray(kw["lbl"], np.int32),
                         blk=np.array([kw["labels"][l]["block"] for l in kw["lbl"]], np.int32),
-                        pbc=np.zeros((0, 3), np.int32) if pbc is None else np.asarray(pbc, np.int32))
+                        pbc=np.zeros((0, 3), np.int32) if pbc is None else np.asarray(pbc, np.int32),
+                        ages=list(kw.get("ages", [])))
     return pr, mesh, kernel_kwargs(pr, mesh)
 
 

@@ -39,7 +39,7 @@ std::string FSolver::getErrorString(LoadMeshErr err)
     case MISSINGMATPROPS: return "problem loading mesh:\nMaterial properties have not been defined for all regions.\n";
     case ELMLABELTOOBIG:
         return "problem loading mesh:\nElemnet label number was greater than the number of labels in the problem.\n";
-    case UNSUPPORTEDMESH: return "problem loading mesh:\nair-gap elements are not supported by this solver build.\n";
+    case UNSUPPORTEDMESH: return "problem loading mesh:\nmalformed air-gap element data.\n";
     }
     return std::string();
 }
@@ -138,10 +138,36 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
         }
         pbclist.push_back(pbc);
     }
+    // air-gap elements: name, parameter line, totalArcElements + 1 quadNodes
     NumAirGapElems = 0;
     if (fgets(s, 1024, fp)) sscanf(s, "%i", &NumAirGapElems);
+    agelist.clear();
+    for (int i = 0; i < NumAirGapElems; i++) {
+        AirGap g;
+        bool ok = fgets(s, 1024, fp) != nullptr;
+        g.name = s;
+        ok = ok && fgets(s, 1024, fp) &&
+             sscanf(s, "%i %lf %lf %lf %lf %lf %lf %lf %i %lf %lf", &g.format, &g.inner_angle, &g.outer_angle,
+                    &g.ri, &g.ro, &g.arc, &g.agc_re, &g.agc_im, &g.n_arc, &g.inner_shift, &g.outer_shift) == 11;
+        ok = ok && g.n_arc > 0;
+        for (int k = 0; ok && k <= g.n_arc; k++) {
+            int n[4];
+            double w[4];
+            ok = fgets(s, 1024, fp) && sscanf(s, "%i %lf %i %lf %i %lf %i %lf", &n[0], &w[0], &n[1], &w[1], &n[2],
+                                              &w[2], &n[3], &w[3]) == 8;
+            for (int m = 0; ok && m < 4; m++) {
+                ok = n[m] >= 0 && n[m] < NumNodes;   // negative quadNode: the reference rejects the file too
+                g.qn.push_back(n[m]);
+                g.qw.push_back(w[m]);
+            }
+        }
+        if (!ok) {
+            fclose(fp);
+            return BADPBCFILE;
+        }
+        agelist.push_back(g);
+    }
     fclose(fp);
-    if (NumAirGapElems != 0) return UNSUPPORTEDMESH;
 
     infile = PathName + ".ele";
     fp = fopen(infile.c_str(), "rt");
@@ -327,6 +353,8 @@ int FSolver::Cuthill(bool deleteFiles)
         p.x = newnum[p.x];
         p.y = newnum[p.y];
     }
+    for (auto &g : agelist)   // cuthill.cpp:321-330
+        for (int &q : g.qn) q = newnum[q];
     int newwide = 0;
     for (int a = 0; a < NumNodes; a++)
         for (int c : ocon[a]) newwide = std::max(newwide, std::abs(newnum[a] - newnum[c]));
@@ -358,6 +386,7 @@ struct FSolver::DescStore {
     std::vector<xfk_circuit_desc> cir;
     std::vector<double> x, y;
     std::vector<int> marker, p, e, lbl, pbc;
+    std::vector<xfk_age_desc> age;
     xfk_problem_desc d{};
 };
 
@@ -442,6 +471,15 @@ bool FSolver::make_desc(DescStore &ds)
     d.n_points = (int)ds.pts.size(); d.points = ds.pts.empty() ? nullptr : ds.pts.data();
     d.n_circs = (int)ds.cir.size(); d.circs = ds.cir.empty() ? nullptr : ds.cir.data();
     d.n_pbc = NumPBCs; d.pbc = NumPBCs ? ds.pbc.data() : nullptr;
+    ds.age.clear();
+    for (const AirGap &g : agelist) {
+        xfk_age_desc a{};
+        a.format = g.format; a.ri = g.ri; a.ro = g.ro; a.total_arc_length = g.arc;
+        a.inner_shift = g.inner_shift; a.outer_shift = g.outer_shift; a.n_arc = g.n_arc;
+        a.qn = g.qn.data(); a.qw = g.qw.data();
+        ds.age.push_back(a);
+    }
+    d.n_ages = (int)ds.age.size(); d.ages = ds.age.empty() ? nullptr : ds.age.data();
     d.precision = Precision;
     d.length_units = (int)LengthUnits;
     d.coords = (int)Coords;

@@ -35,6 +35,16 @@ public:
     std::vector<CNode> meshnode;
     std::vector<CMElement> meshele;
     std::vector<CCommonPoint> pbclist;
+    // CAirGapElement as read from the .pbc file (fsolver.cpp:425-515)
+    struct AirGap {
+        std::string name;
+        int format = 0, n_arc = 0;
+        double inner_angle = 0, outer_angle = 0, ri = 0, ro = 0, arc = 0, agc_re = 0, agc_im = 0;
+        double inner_shift = 0, outer_shift = 0;
+        std::vector<int> qn;       // 4 per quadNode
+        std::vector<double> qw;
+    };
+    std::vector<AirGap> agelist;
 
     int (*WarnMessage)(const char *, ...);
     int (*PrintMessage)(const char *, ...);

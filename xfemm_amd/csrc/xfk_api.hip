@@ -21,6 +21,7 @@
 #include <type_traits>
 #include <unordered_map>
 
+#include "xfk_age.h"
 #include "xfk_comm.h"
 #include "xfk_kernels.h"
 #include "xfk_partition.h"
@@ -71,6 +72,14 @@ static int build_pbc_map(xfk_problem *P)
             for (int m = 0; m < 3; ++m)
                 if (m != j) it->second.insert(P->hp[3 * e + m]);
         }
+    for (long long k : P->age_key) {   // air-gap couplings are entries of the matrix too
+        const int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
+        if (r == c) continue;
+        auto it = N0.find(r);
+        if (it != N0.end()) it->second.insert(c);
+        it = N0.find(c);
+        if (it != N0.end()) it->second.insert(r);
+    }
     std::unordered_map<int, std::set<int>> Ncur = N0;
     std::unordered_map<long long, Terms> E;
     std::unordered_map<int, Terms> Eb;
@@ -156,6 +165,31 @@ static int build_pbc_map(xfk_problem *P)
     return XFK_OK;
 }
 
+
+// Air-gap couplings that no triangle provides join the CSR pattern through the
+// fill-in list (merged with the periodic fill-in).
+static void add_age_fill(xfk_problem *P)
+{
+    if (P->age_key.empty()) return;
+    std::unordered_map<int, std::set<int>> adj;
+    for (long long k : P->age_key) {
+        const int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
+        if (r != c) { adj[r]; adj[c]; }
+    }
+    for (int e = 0; e < P->NE; ++e)
+        for (int j = 0; j < 3; ++j) {
+            auto it = adj.find(P->hp[3 * e + j]);
+            if (it == adj.end()) continue;
+            for (int m = 0; m < 3; ++m)
+                if (m != j) it->second.insert(P->hp[3 * e + m]);
+        }
+    std::set<long long> fill(P->pbc_fill.begin(), P->pbc_fill.end());
+    for (long long k : P->age_key) {
+        const int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
+        if (r != c && !adj[r].count(c)) fill.insert(k);
+    }
+    P->pbc_fill.assign(fill.begin(), fill.end());
+}
 
 // device -> host read-back ordered on the problem's (non-blocking) stream
 hipError_t d2h(void *dst, const void *src, size_t bytes, hipStream_t s)
@@ -340,6 +374,28 @@ int build_symbolic(xfk_problem *P)
     XFK_CHECK(P->mu1.alloc(NE));
     XFK_CHECK(P->mu2.alloc(NE));
 
+    // air-gap entries -> CSR slots (full storage: both triangles)
+    P->age_n = 0;
+    if (!P->age_key.empty()) {
+        std::vector<int> rc;
+        std::vector<double> v;
+        for (size_t m = 0; m < P->age_key.size(); ++m) {
+            const int r = (int)(P->age_key[m] >> 32), c = (int)(P->age_key[m] & 0xffffffff);
+            rc.push_back(r); rc.push_back(c); v.push_back(P->age_val[m]);
+            if (r != c) { rc.push_back(c); rc.push_back(r); v.push_back(P->age_val[m]); }
+        }
+        const int na = (int)v.size();
+        DBuf<int> d_rc;
+        XFK_CHECK(upload(d_rc, rc.data(), rc.size(), s));
+        XFK_CHECK(upload(P->age_v, v.data(), v.size(), s));
+        XFK_CHECK(P->age_slot.alloc(na));
+        launch_lookup_slots(s, na, d_rc.p, P->rowptr.p, P->col.p, P->age_slot.p);
+        std::vector<int> chk(na);
+        XFK_CHECK(d2h(chk.data(), P->age_slot.p, sizeof(int) * na, s));
+        for (int x : chk) XFK_REQUIRE(x >= 0, XFK_ERR_HIP, "internal: air-gap slot missing from the CSR pattern");
+        P->age_n = na;
+    }
+
     // periodic averaging maps -> CSR slots
     P->pm_n = 0;
     P->pb_n = 0;
@@ -447,6 +503,7 @@ static int assemble(xfk_problem *P, int iter)
     A.ext_ri = P->ext_ri;
     A.ext_zo = P->ext_zo;
     for (int c = 0; c < P->ncolors; ++c) launch_assemble_color(s, P->color_off[c], P->color_off[c + 1], A);
+    launch_add_at_slots(s, P->age_n, P->age_slot.p, P->age_v.p, P->val.p);   // air-gap elements
     launch_point_currents(s, P->npt, P->pt_nodes.p, P->pt_J.p, P->b.p);
     launch_dirichlet(s, P->nfix_rows, P->fix_rows.p, P->nfix_cols, P->fix_cols_row.p, P->rowptr.p, P->col.p,
                      P->diag.p, P->fixed.p, P->fix_first.p, P->fix_last.p, P->val.p, P->b.p);
@@ -741,6 +798,7 @@ int validate_desc(const xfk_problem_desc *d)
     XFK_REQUIRE(d->n_points == 0 || d->points, XFK_ERR_ARG, "missing point table");
     XFK_REQUIRE(d->n_circs == 0 || d->circs, XFK_ERR_ARG, "missing circuit table");
     XFK_REQUIRE(d->n_pbc == 0 || d->pbc, XFK_ERR_ARG, "missing pbc table");
+    XFK_REQUIRE(d->n_ages >= 0 && (d->n_ages == 0 || d->ages), XFK_ERR_ARG, "missing air-gap element table");
     XFK_REQUIRE(d->n_lines < 1023, XFK_ERR_UNSUPPORTED, "at most 1022 boundary properties");
     XFK_REQUIRE(d->length_units >= 0 && d->length_units < 6, XFK_ERR_ARG, "bad length units");
     XFK_REQUIRE(d->problem_type == XFK_PLANAR || d->problem_type == XFK_AXISYMMETRIC, XFK_ERR_ARG,
@@ -1029,8 +1087,13 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     P->npt = (int)pt_nodes.size();
     P->nfix_rows = (int)fix_rows.size();
 
+    if (!plan) {
+        P->age_key = G.age_key;
+        P->age_val = G.age_val;
+    }
     int rc = build_pbc_map(P);
     if (rc != XFK_OK) return fail(rc);
+    add_age_fill(P);
 
     hipStream_t s = P->stream;
     hipError_t e = hipSuccess;
@@ -1082,6 +1145,8 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
     if (rc != XFK_OK) return rc;
     GlobalPrep G;
     prepare_global(d, G);
+    rc = age_entries(d, 1.0, G.age_key, G.age_val);
+    if (rc != XFK_OK) return rc;
     return build_local(d, G, nullptr, device, nullptr, out);
 }
 
@@ -1124,6 +1189,8 @@ int xfk_problem_create_dist(const xfk_problem_desc *d, int device, xfk_comm *com
     if (rc == XFK_OK) rc = check_device(device);
     if (rc != XFK_OK) return rc;
     XFK_REQUIRE(d->n_pbc == 0, XFK_ERR_UNSUPPORTED, "periodic boundaries are not supported in the sharded solve");
+    XFK_REQUIRE(d->n_ages == 0 || d->problem_type != XFK_PLANAR, XFK_ERR_UNSUPPORTED,
+                "air-gap elements are not supported in the sharded solve");
     PartPlan plan;
     XFK_REQUIRE(plan_partition(d->n_nodes, d->n_elems, d->p, comm->rank, comm->size, plan), XFK_ERR_ARG,
                 "bad partition: fewer nodes than ranks");

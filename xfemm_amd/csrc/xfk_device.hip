@@ -800,6 +800,14 @@ __global__ void k_map_gather(int n, const int *__restrict__ ptr, const int *__re
     tmp[i] = s;
 }
 
+// air-gap element values at their CSR slots (one thread per unique slot)
+__global__ void k_add_at_slots(int n, const int *__restrict__ slot, const double *__restrict__ v,
+                               double *__restrict__ data)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) data[slot[i]] += v[i];
+}
+
 __global__ void k_map_scatter(int n, const int *__restrict__ dst, const double *__restrict__ tmp,
                               double *__restrict__ data)
 {
@@ -950,6 +958,10 @@ void launch_dirichlet(hipStream_t s, int nrows, const int *rows, int nadj, const
 {
     if (nadj) k_dirichlet_cols<<<nblk(nadj), kBlock, 0, s>>>(nadj, adj, rowptr, col, fixed, fix_first, val, b);
     if (nrows) k_dirichlet_rows<<<nblk(nrows), kBlock, 0, s>>>(nrows, rows, rowptr, diag, val, b, fix_last);
+}
+void launch_add_at_slots(hipStream_t s, int n, const int *slot, const double *v, double *data)
+{
+    if (n) k_add_at_slots<<<nblk(n), kBlock, 0, s>>>(n, slot, v, data);
 }
 void launch_map(hipStream_t s, int n, const int *dst, const int *ptr, const int *src, const double *w,
                 double *data, double *tmp)

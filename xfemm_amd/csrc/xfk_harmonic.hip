@@ -21,6 +21,7 @@
 #include <cmath>
 #include <complex>
 
+#include "xfk_age.h"
 #include "xfk_amg.h"
 #include "xfk_axi.h"
 #include "xfk_kernels.h"
@@ -969,6 +970,8 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
     GlobalPrep G;
     prepare_global(d, G);
+    rc = age_entries(d, -1.0, G.age_key, G.age_val);   // air-gap elements, negated (harmonic2d.cpp:227-382)
+    if (rc != XFK_OK) return rc;
     const bool axi = G.axi;   // HarmonicAxisymmetric (harmonicaxi.cpp)
 
     // blocks, lines
@@ -1329,6 +1332,7 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
             const int n = P->color_off[cl + 1] - P->color_off[cl];
             if (n > 0) k_hassemble_color<<<nb256(n), kBlock, 0, s>>>(P->color_off[cl], P->color_off[cl + 1], A);
         }
+        launch_add_at_slots(s, P->age_n, P->age_slot.p, P->age_v.p, P->val.p);   // air-gap elements (real)
         if (P->nhpt > 0)
             k_hpoint<<<nb256(P->nhpt), kBlock, 0, s>>>(P->nhpt, P->hpt_nodes.p, P->hpt_J.p, P->b.p, P->b_im.p);
         if (P->nfix_cols > 0) {

@@ -253,7 +253,12 @@ struct xfk_problem {
     xfk::DBuf<double> pb_w, pb_tmp;
     int pb_n = 0;
     // fill-in entries requested by the periodic map (row, col) -> pattern
-    std::vector<long long> pbc_fill;   // packed (row<<32)|col
+    std::vector<long long> pbc_fill;   // packed (row<<32)|col: periodic fill-in and air-gap couplings
+    std::vector<long long> age_key;    // air-gap element entries (r <= c), xfk_age.h
+    std::vector<double> age_val;
+    xfk::DBuf<int> age_slot;           // CSR slot of every full-storage air-gap entry
+    xfk::DBuf<double> age_v;
+    int age_n = 0;
     std::vector<std::vector<std::pair<long long, double>>> pbc_entry_terms;  // host form
     std::vector<long long> pbc_entry_key;
     std::vector<std::vector<std::pair<int, double>>> pbc_b_terms;
@@ -352,6 +357,8 @@ struct GlobalPrep {
     bool any_nonlinear = false;
     bool axi = false;                    // FSolver::StaticAxisymmetric
     double ext_ro = 0, ext_ri = 0, ext_zo = 0;   // exterior region, cm
+    std::vector<long long> age_key;      // air-gap element entries, (r << 32) | c with r <= c
+    std::vector<double> age_val;
 };
 
 int validate_desc(const xfk_problem_desc *d);

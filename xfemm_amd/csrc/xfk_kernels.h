@@ -71,6 +71,8 @@ void launch_build_erec(hipStream_t s, int NE, const int *perm, const int *p, con
                        int4 *erec, int *ebits, int *iperm);
 void launch_build_slots(hipStream_t s, int NE, int nrows, const int *p, const int *iperm, const int *rowptr,
                         const int *col, int *slot, int *bad);
+// data[slot[i]] += v[i] (unique slots: race-free)
+void launch_add_at_slots(hipStream_t s, int n, const int *slot, const double *v, double *data);
 void launch_lookup_slots(hipStream_t s, int n, const int *rc, const int *rowptr, const int *col, int *out);
 void launch_mark_fix_adj(hipStream_t s, int N, const int *rowptr, const int *col, const unsigned char *fixed,
                          int *flag);

@@ -35,7 +35,7 @@ XFK_OPT_AMG_DENSE = 7
 
 # every symbol include/xfemm_kernels.h declares
 EXPORTED = (
-    "xfk_last_error", "xfk_device_count", "xfk_problem_create", "xfk_problem_destroy",
+    "xfk_last_error", "xfk_age_element_matrix", "xfk_device_count", "xfk_problem_create", "xfk_problem_destroy",
     "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz",
     "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_solve_csr_pc", "xfk_pcg_time", "xfk_set_option",
     "xfk_problem_create_harmonic", "xfk_harmonic2d", "xfk_get_solution_complex", "xfk_get_circuits_complex",
@@ -71,6 +71,13 @@ class CircuitDesc(C.Structure):
     _fields_ = [("type", C.c_int), ("amps_re", C.c_double), ("dvolts_re", C.c_double)]
 
 
+class AgeDesc(C.Structure):
+    """xfk_age_desc: one CAirGapElement as read from the .pbc file."""
+    _fields_ = [("format", C.c_int), ("ri", C.c_double), ("ro", C.c_double), ("total_arc_length", C.c_double),
+                ("inner_shift", C.c_double), ("outer_shift", C.c_double), ("n_arc", C.c_int),
+                ("qn", iptr), ("qw", dptr)]
+
+
 class ProblemDesc(C.Structure):
     _fields_ = [("n_nodes", C.c_int), ("x", dptr), ("y", dptr), ("marker", iptr),
                 ("n_elems", C.c_int), ("p", iptr), ("e", iptr), ("lbl", iptr),
@@ -82,7 +89,8 @@ class ProblemDesc(C.Structure):
                 ("n_pbc", C.c_int), ("pbc", iptr),
                 ("precision", C.c_double), ("length_units", C.c_int), ("coords", C.c_int),
                 ("relax", C.c_double), ("problem_type", C.c_int), ("ext_zo", C.c_double),
-                ("ext_ro", C.c_double), ("ext_ri", C.c_double)]
+                ("ext_ro", C.c_double), ("ext_ri", C.c_double),
+                ("n_ages", C.c_int), ("ages", C.POINTER(AgeDesc))]
 
 
 XFK_PLANAR = 0
@@ -147,6 +155,7 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_get_solution_complex.argtypes = [C.c_void_p, dptr]
     L.xfk_get_circuits_complex.argtypes = [C.c_void_p, iptr, dptr, dptr]
     L.xfk_get_csr_complex.argtypes = [C.c_void_p, iptr, iptr, dptr, dptr]
+    L.xfk_age_element_matrix.argtypes = [C.c_double, C.c_double, C.c_double, C.c_double, dptr]
     vp = C.c_void_p
     L.xfk_comm_unique_id.argtypes = [C.c_char_p, C.c_int]
     L.xfk_comm_create_rccl.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
@@ -184,7 +193,7 @@ class _Keep(list):
 
 
 def _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision, length_units,
-               coords, relax, problem_type=0, ext=(0.0, 0.0, 0.0)):
+               coords, relax, problem_type=0, ext=(0.0, 0.0, 0.0), ages=()):
     """xfk_problem_desc of plain arrays / dicts (see Static2DProblem); returns
     (desc, keep) where keep holds every buffer the descriptor points into."""
     keep = _Keep()
@@ -241,8 +250,30 @@ def _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e,
     D.precision, D.length_units, D.coords, D.relax = precision, length_units, coords, relax
     D.problem_type = int(problem_type)
     D.ext_zo, D.ext_ro, D.ext_ri = ext
-    keep.extend([bl, lb, ln, pt, ci])
+    # air-gap elements: dicts with format, ri, ro, total_arc_length, inner_shift,
+    # outer_shift and the quadNode table qn / qw ((n_arc + 1) x 4 each)
+    ag = (AgeDesc * max(1, len(ages)))()
+    for k, a in enumerate(ages):
+        o = ag[k]
+        o.format, o.ri, o.ro = int(a.get("format", 0)), a["ri"], a["ro"]
+        o.total_arc_length, o.inner_shift, o.outer_shift = a["total_arc_length"], a["inner_shift"], a["outer_shift"]
+        qn = np.asarray(a["qn"], dtype=np.int32).reshape(-1, 4)
+        o.n_arc = len(qn) - 1
+        o.qn, o.qw = keep.i(qn), keep.d(np.asarray(a["qw"], dtype=np.float64).reshape(-1, 4))
+    D.n_ages, D.ages = len(ages), ag
+    keep.extend([bl, lb, ln, pt, ci, ag])
     return D, keep
+
+
+def age_element_matrix(ci: float, co: float, K: float, Ki: float) -> np.ndarray:
+    """10 x 10 matrix of one air-gap arc element (host math of the C-ABI,
+    cfemm/fsolver/static2d.cpp:209-263)."""
+    L = load_library()
+    out = np.zeros(100)
+    rc = L.xfk_age_element_matrix(ci, co, K, Ki, out.ctypes.data_as(dptr))
+    if rc != 0:
+        raise XfkError("xfk_age_element_matrix failed (%d)" % rc)
+    return out.reshape(10, 10)
 
 
 class Static2DProblem:
@@ -257,7 +288,8 @@ class Static2DProblem:
                  device=0, comm: Optional["Comm"] = None, precond: str = "amg", amg_sweeps: Optional[int] = None,
                  amg_theta: Optional[float] = None, frequency: float = 0.0, amg_omega: Optional[float] = None,
                  amg_replicate: Optional[int] = None, amg_reuse: Optional[bool] = None, problem_type: int = 0,
-                 ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0, amg_dense: Optional[int] = None):
+                 ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0, amg_dense: Optional[int] = None,
+                 ages: Sequence[dict] = ()):
         """comm: shard the mesh by row blocks over this communicator (every rank
         passes the same global problem; solve() and solution() are collective).
         precond: "amg" (smoothed-aggregation V-cycle, default) or "jacobi".
@@ -267,7 +299,7 @@ class Static2DProblem:
             raise XfkError("frequency != 0: use Harmonic2DProblem")
         L = load_library()
         D, keep = _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision,
-                             length_units, coords, relax, problem_type, (ext_zo, ext_ro, ext_ri))
+                             length_units, coords, relax, problem_type, (ext_zo, ext_ro, ext_ri), ages)
         self._keep = keep
         self.n_nodes = D.n_nodes
         self.n_elems = D.n_elems
@@ -381,13 +413,13 @@ class Harmonic2DProblem:
                  lines: Sequence[dict] = (), points: Sequence[dict] = (), circuits: Sequence[dict] = (),
                  marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0, device=0,
                  problem_type: int = 0, ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0,
-                 precond: str = "amg"):
+                 precond: str = "amg", ages: Sequence[dict] = ()):
         """precond: "amg" (V-cycle of the real SPD surrogate Re A +- Im A, the
         sign making Im A positive semi-definite, applied to the real and
         imaginary parts; default) or "jacobi" (complex Jacobi)."""
         L = load_library()
         D, keep = _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision,
-                             length_units, coords, relax, problem_type, (ext_zo, ext_ro, ext_ri))
+                             length_units, coords, relax, problem_type, (ext_zo, ext_ro, ext_ri), ages)
         ba = (BlockAcDesc * max(1, len(blocks)))()
         for k, b in enumerate(blocks):
             ba[k].J_im, ba[k].Lam_d = b.get("J_im", 0.0), b.get("Lam_d", 0.0)

@@ -187,8 +187,25 @@ def write_problem(base: str, kw: dict, label_xy: Optional[np.ndarray] = None) ->
         fh.write("%d\t1\n" % len(edges))
         for n, (k, mk) in enumerate(sorted(edges.items())):
             fh.write("%d\t%d\t%d\t%d\n" % (n, k[0], k[1], mk))
+    # .pbc: periodic pairs, then the air-gap elements (writepoly.cpp:1836-1966)
+    pbc = kw.get("pbc")
+    pbc = np.zeros((0, 3), np.int32) if pbc is None else np.asarray(pbc).reshape(-1, 3)
     with open(base + ".pbc", "w") as fh:
-        fh.write("0\n0\n")
+        fh.write("%d\n" % len(pbc))
+        for k, (a, b, t) in enumerate(pbc):
+            fh.write("%d\t%d\t%d\t%d\n" % (k, a, b, t))
+        ages = kw.get("ages", [])
+        fh.write("%d\n" % len(ages))
+        for k, a in enumerate(ages):
+            qn, qw = np.asarray(a["qn"]), np.asarray(a["qw"])
+            c = a.get("center", (0.0, 0.0))
+            fh.write('"age%d"\n' % k)
+            fh.write("%d %.17g %.17g %.17g %.17g %.17g %.17g %.17g %d %.17g %.17g\n" % (
+                a.get("format", 0), a.get("inner_angle", 0.0), a.get("outer_angle", 0.0), a["ri"], a["ro"],
+                a["total_arc_length"], c[0], c[1], len(qn) - 1, a["inner_shift"], a["outer_shift"]))
+            for i in range(len(qn)):
+                fh.write("%d %g %d %g %d %g %d %g\n" % (qn[i, 0], qw[i, 0], qn[i, 1], qw[i, 1], qn[i, 2], qw[i, 2],
+                                                        qn[i, 3], qw[i, 3]))
 
 
 def axisymmetric(n: int, nonlinear: bool = False, L: float = 10.0, J: float = 2.0, mu_steel: float = 1000.0,
@@ -458,3 +475,117 @@ def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float 
         top = (m - 1) * m + np.arange(m)
         kw["pbc"] = np.stack([bottom, top, np.zeros(m)], 1).astype(np.int32)
     return kw
+
+
+def age_rings(inner_nodes, outer_nodes, x, y, total_arc_length: float, fmt: int = 0, inner_angle: float = 0.0,
+              outer_angle: float = 0.0, ri: float = 1.0, ro: float = 1.0, center=(0.0, 0.0)) -> dict:
+    """One air-gap element as fmesher writes it into the .pbc file
+    (cfemm/fmesher/writepoly.cpp:1852-1966): the slice's ring nodes are copied
+    round the full circle (antiperiodic copies signed -1 when fmt == 1), placed
+    by angle in arc-element units, sorted, and each quadNode k lists the ring
+    nodes either side of arc position k with their signs."""
+    n = len(inner_nodes)
+    dtta = total_arc_length / n
+    n0 = int(round(360.0 / dtta))
+    n1 = int(round(360.0 / total_arc_length))
+    agc = complex(*center)
+
+    def ring(nodes, angle):
+        out = []
+        for j in range(n1):
+            dL = -1.0 if (fmt == 1 and j % 2 != 0) else 1.0
+            a = np.exp(1j * (j * total_arc_length + angle) * np.pi / 180.0)
+            for nd in nodes:
+                z = a * (complex(x[nd], y[nd]) - agc)
+                deg = np.angle(z) if z.imag >= 0 else np.angle(z) + 2.0 * np.pi
+                out.append((int(nd), deg * 180.0 / np.pi / dtta, dL))
+        return sorted(out, key=lambda t: t[1])   # the reference's bubble sort is stable too
+
+    IR, OR = ring(inner_nodes, inner_angle), ring(outer_nodes, outer_angle)
+    qn = np.zeros((n + 1, 4), np.int32)
+    qw = np.zeros((n + 1, 4))
+    for i in range(n + 1):
+        p1 = 0 if i == n0 else i
+        p0 = p1 - 1 if p1 > 0 else n0 - 1
+        qn[i] = (IR[p0][0], IR[p1][0], OR[p0][0], OR[p1][0])
+        qw[i] = (IR[p0][2], IR[p1][2], OR[p0][2], OR[p1][2])
+    return dict(format=fmt, inner_angle=inner_angle, outer_angle=outer_angle, ri=ri, ro=ro,
+                total_arc_length=total_arc_length, inner_shift=IR[0][1], outer_shift=OR[0][1], qn=qn, qw=qw,
+                center=center)
+
+
+def age_motor(n_theta: int = 48, n_r: int = 4, half: bool = False, rotor_angle: float = 0.0,
+              nonlinear: bool = False, precision: float = 1e-8, J: float = 3.0, gap: float = 0.1):
+    """Two-pole permanent-magnet machine with an air-gap element between rotor
+    and stator: a rotor annulus (shaft hole, steel core, x-magnetised ring) and
+    a stator annulus (steel with a +-J winding sector), each a structured polar
+    mesh with n_theta nodes per full ring; the unmeshed gap between radii
+    ri = 2 and ro = 2 + gap is bridged by one AGE.  half: the 0..180 degree
+    slice with antiperiodic sides (AGE BdryFormat 1).  rotor_angle rotates the
+    rotor through the AGE's InnerAngle (degrees, no remeshing)."""
+    r_shaft, ri, ro, r_out = 0.5, 2.0, 2.0 + gap, 4.0
+    nt = n_theta // 2 if half else n_theta
+    na = nt + 1 if half else nt                 # nodes per ring
+    radii_rotor = np.linspace(r_shaft, ri, n_r + 1)
+    radii_stator = np.linspace(ro, r_out, n_r + 1)
+    dth = 2.0 * np.pi / n_theta
+    xs, ys, rings = [], [], []
+    for r in list(radii_rotor) + list(radii_stator):
+        idx = []
+        for m in range(na):
+            idx.append(len(xs))
+            xs.append(r * np.cos(m * dth))
+            ys.append(r * np.sin(m * dth))
+        rings.append(idx)
+    x, y = np.array(xs), np.array(ys)
+    p, lbl, e = [], [], []
+    nseg = nt                                  # angular cells per ring pair
+    for part, off in ((0, 0), (1, n_r + 1)):
+        for j in range(n_r):
+            a_r, b_r = rings[off + j], rings[off + j + 1]
+            for m in range(nseg):
+                m1 = (m + 1) % na
+                th = (m + 0.5) * dth * 180.0 / np.pi
+                if part == 0:
+                    lab = 2 if j == n_r - 1 else 1          # magnet ring outside a steel core
+                else:
+                    lab = 1
+                    if j == 1 and (30.0 < th < 60.0):
+                        lab = 3
+                    elif j == 1 and (210.0 < th < 240.0):
+                        lab = 4
+                # counter-clockwise, as Triangle writes them
+                for k, tri in enumerate(((a_r[m], b_r[m1], a_r[m1]), (a_r[m], b_r[m], b_r[m1]))):
+                    p.append(tri)
+                    lbl.append(lab)
+                    ee = [-1, -1, -1]
+                    # Dirichlet A = 0 on the shaft and the stator's outer rim
+                    if part == 0 and j == 0 and k == 0:
+                        ee[2] = 0        # edge a_r[m1] -> a_r[m]
+                    if part == 1 and j == n_r - 1 and k == 1:
+                        ee[1] = 0        # edge b_r[m] -> b_r[m1]
+                    e.append(ee)
+    p = np.array(p, np.int32)
+    blocks = [
+        dict(mu_x=1.0, mu_y=1.0),
+        dict(mu_x=800.0, mu_y=800.0, LamFill=1.0),
+        dict(mu_x=1.049, mu_y=1.049, H_c=979000.0),
+        dict(mu_x=1.0, mu_y=1.0, J_re=J),
+        dict(mu_x=1.0, mu_y=1.0, J_re=-J),
+    ]
+    if nonlinear:
+        from .fsolver import bh_get_slopes
+        Bc, Hc, Sc, mu = bh_get_slopes(*m19_curve(), lam_type=0, lam_fill=0.98)
+        blocks[1] = dict(mu_x=mu, mu_y=mu, LamFill=0.98, LamType=0, bh="M19", B=Bc, H=Hc, slope=Sc)
+    labels = [dict(block=0), dict(block=1), dict(block=2, mag_dir=0.0), dict(block=3), dict(block=4)]
+    inner, outer = rings[n_r], rings[n_r + 1]
+    if half:
+        inner, outer = inner[:nt], outer[:nt]
+    age = age_rings(inner, outer, x, y, 180.0 if half else 360.0, fmt=1 if half else 0,
+                    inner_angle=rotor_angle, ri=ri, ro=ro)
+    pbc = None
+    if half:   # antiperiodic sides: the 0 and 180 degree nodes of every ring
+        pbc = np.array([(rg[0], rg[-1], 1) for k, rg in enumerate(rings)], np.int32)
+    return dict(x=x, y=y, p=p, lbl=np.array(lbl, np.int32), e=np.array(e, np.int32), marker=None, pbc=pbc,
+                blocks=blocks, labels=labels, lines=[dict(format=0)], points=[], circuits=[], precision=precision,
+                length_units=2, coords=0, relax=1.0, ages=[age])
