@@ -127,3 +127,24 @@ def test_static_file_interface(tmp_path):
     assert fs.runSolver(False), fs.last_error()
     ans = femfile.read_ans(base + ".ans")
     assert rel_err(ans.A, Ao) <= TOL_LINEAR
+
+
+def test_harmonic_nonlinear_matches_oracle():
+    """Successive approximation (ACSolver 0) over M-19 on its GetSlopes(omega)
+    curve with the air gap in the loop."""
+    from xfemm_amd import fsolver
+    kw = _harmonic_kw(angle=3.1, nonlinear=True)
+    b = kw["blocks"][1]
+    b.update(Theta_hx=10.0, Theta_hy=10.0, Lam_d=0.0)
+    Bc, Hc, Sc, mu, _ = fsolver.bh_get_slopes_ac(*synth.m19_curve(), 2 * np.pi * kw["frequency"], lam_type=0,
+                                                 lam_fill=b["LamFill"], theta_hn=10.0, lam_d=0.0,
+                                                 cduct=b["Cduct"])
+    b.update(B=Bc, H=Hc, slope=Sc, mu_x=mu, mu_y=mu, bh="M19", Theta_hn=10.0)
+    pr, mesh, kk = synth_to_oracle(kw)
+    Ao, st, _ = oh.solve(pr, mesh)
+    P = kernels.Harmonic2DProblem(**kk)
+    r = P.solve()
+    A = P.solution()
+    P.close()
+    assert st["newton_iters"] > 1 and r["newton_iters"] > 1
+    assert rel_err(A, Ao) <= TOL_NONLINEAR
