@@ -675,16 +675,7 @@ def load_mesh(base: str, pr: FemProblem) -> Mesh:
     # air-gap elements (fsolver.cpp:425-515): name line, parameter line,
     # totalArcElements + 1 quadNode lines
     nage = int(plines[1 + npbc].split()[0]) if len(plines) > 1 + npbc else 0
-    ages, ln = [], 2 + npbc
-    for _ in range(nage):
-        f = plines[ln + 1].split()
-        n = int(f[8])
-        q = [plines[ln + 2 + k].split() for k in range(n + 1)]
-        ages.append(dict(format=int(f[0]), ri=float(f[3]), ro=float(f[4]), total_arc_length=float(f[5]),
-                         inner_shift=float(f[9]), outer_shift=float(f[10]),
-                         qn=np.array([[int(r[0]), int(r[2]), int(r[4]), int(r[6])] for r in q], np.int32),
-                         qw=np.array([[float(r[1]), float(r[3]), float(r[5]), float(r[7])] for r in q])))
-        ln += n + 3
+    ages, _ = _parse_age_blocks(plines, 2 + npbc, nage)
 
     tok = _read_ints_floats(base + ".ele")
     ne = int(tok[0])
@@ -860,6 +851,27 @@ class AnsSolution:
     p: np.ndarray
     lbl: np.ndarray
     circ: List[tuple]
+    pbc: Optional[np.ndarray] = None
+    ages: list = dataclasses.field(default_factory=list)   # as Mesh.ages, renumbered node ids
+
+
+def _parse_age_blocks(lines, i, nage):
+    """AGE blocks as FSolver::LoadMesh reads them from the .pbc and
+    WriteStatic2D writes them to the .ans (fsolver.cpp:425-515,
+    static2d.cpp:1161-1190): name, parameter line, n_arc + 1 quadNodes."""
+    ages = []
+    for _ in range(nage):
+        name = lines[i].strip().strip('"')
+        f = lines[i + 1].split()
+        n = int(f[8])
+        q = [lines[i + 2 + k].split() for k in range(n + 1)]
+        ages.append(dict(name=name, format=int(f[0]), inner_angle=float(f[1]), outer_angle=float(f[2]),
+                         ri=float(f[3]), ro=float(f[4]), total_arc_length=float(f[5]),
+                         inner_shift=float(f[9]), outer_shift=float(f[10]),
+                         qn=np.array([[int(r[0]), int(r[2]), int(r[4]), int(r[6])] for r in q], np.int32),
+                         qw=np.array([[float(r[1]), float(r[3]), float(r[5]), float(r[7])] for r in q])))
+        i += n + 3
+    return ages, i
 
 
 def read_ans(path: str) -> AnsSolution:
@@ -882,8 +894,17 @@ def read_ans(path: str) -> AnsSolution:
     for j in range(nl):
         f = lines[i + j].split()
         circ.append((int(f[0]), float(f[1])))
+    i += nl
+    pbc, ages = None, []
+    if i < len(lines) and lines[i].strip():       # periodic pairs + air-gap elements (static2d.cpp:1152-1190)
+        npbc = int(lines[i]); i += 1
+        pbc = np.array([[int(v) for v in lines[i + j].split()[:3]] for j in range(npbc)], dtype=np.int32)
+        i += npbc
+        if i < len(lines) and lines[i].strip():
+            nage = int(lines[i]); i += 1
+            ages, i = _parse_age_blocks(lines, i, nage)
     return AnsSolution(x=x, y=y, A=A, marker=marker, p=ele[:, :3].astype(np.int32),
-                       lbl=ele[:, 3].astype(np.int32), circ=circ)
+                       lbl=ele[:, 3].astype(np.int32), circ=circ, pbc=pbc, ages=ages)
 
 
 def load_problem(base: str, renumber: bool = True):

@@ -765,7 +765,7 @@ static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L,
     const int axi = pr->problem_type == 1;
     if (!axi) {   /* air-gap elements first (harmonic2d.cpp:227-380), real entries */
         struct hage_ctx { const orh_linprob_ops *ops; void *L; } actx = {ops, L};
-        ora_age_assemble(pr->n_ages, pr->ages, hage_emit, &actx);
+        ora_age_assemble(pr->n_ages, pr->ages, 1, hage_emit, &actx);
     }
     for (int i = 0; i < pr->n_elems; i++) {
         if (axi) {

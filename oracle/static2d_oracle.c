@@ -398,7 +398,7 @@ static void ora_assemble(ora_problem *pr, const ora_linprob_ops *ops, void *L, i
 
         /* air-gap elements first (static2d.cpp:191-344) */
         struct age_ctx { const ora_linprob_ops *ops; void *L; } actx = {ops, L};
-        ora_age_assemble(pr->n_ages, pr->ages, age_emit, &actx);
+        ora_age_assemble(pr->n_ages, pr->ages, 0, age_emit, &actx);
 
         for (int i = 0; i < NE; i++) {
             double Me[3][3], be[3], Mx[3][3], My[3][3], Mxy[3][3], Mn[3][3];

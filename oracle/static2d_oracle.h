@@ -81,7 +81,7 @@ typedef void (*ora_age_emit)(void *ctx, double v, int p, int q);
 void ora_age_matrix(double ci, double co, double K, double Ki, double *MG);
 /* Every air-gap contribution as AddTo(v, p, q) calls in the reference's order
  * (static2d.cpp:191-344). */
-void ora_age_assemble(int n_ages, const ora_age *ages, ora_age_emit emit, void *ctx);
+void ora_age_assemble(int n_ages, const ora_age *ages, int harmonic, ora_age_emit emit, void *ctx);
 
 typedef struct {
     int n_nodes;

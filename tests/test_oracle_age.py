@@ -1,10 +1,13 @@
 """Air-gap elements on the CPU: the element matrix tables and the oracle.
 
-* Both monomial tables of the AGE matrix (the product host's, reached through
-  the C-ABI xfk_age_element_matrix, and the oracle's) reproduce the
-  reference's closed form (cfemm/fsolver/static2d.cpp:209-263), evaluated
-  exactly at sample points by tools/gen_age_table.py into
-  tests/golden/age_mg.json.
+* The AGE matrix three ways: the product host's monomial table (reached
+  through the C-ABI xfk_age_element_matrix, generated from the reference's
+  closed form cfemm/fsolver/static2d.cpp:218-268 by tools/gen_age_table.py),
+  the reference's closed form evaluated exactly at sample points
+  (tests/golden/age_mg.json), and the oracle's INDEPENDENT construction of the
+  element (oracle/age_oracle.c: Catmull-Rom ring interpolation of the corner
+  values of an annulus rectangle, mean of bilinear and two-triangle stiffness)
+  -- no shared table or text between the oracle and the product.
 * The oracle's AGE assembly (oracle/age_oracle.c, static2d.cpp:191-344) is
   pinned by a property of the operator itself: a full-circle machine and its
   antiperiodic half (AGE BdryFormat 1: signed ring copies, sign fixes at the
@@ -107,9 +110,14 @@ def test_pbc_file_age_section_roundtrip(tmp_path):
     assert np.abs(A_file[order] - A_mem[order0]).max() <= 1e-6 * np.abs(A_mem).max()
 
 
-def test_harmonic_oracle_full_machine_equals_antiperiodic_half():
+def test_harmonic_oracle_antiperiodic_half_keeps_reference_quirk():
     """Harmonic2D adds the AGE matrix with the opposite sign
-    (harmonic2d.cpp:382); the antiperiodic half still equals the full machine."""
+    (harmonic2d.cpp:382) and, unlike Static2D, never applies the antiperiodic
+    sign fix of the last arc element (harmonic2d.cpp:373 tests
+    k == totalArcElements).  The oracle and the product reproduce the
+    reference's answers, so for an antiperiodic air gap the harmonic half
+    machine is NOT the full machine (the static one is, test above); the
+    difference is pinned here so that a silent 'fix' shows up."""
     from oracle import harmonic as oh
     nth = 24
     sol = {}
@@ -122,4 +130,5 @@ def test_harmonic_oracle_full_machine_equals_antiperiodic_half():
         sol[half] = A.reshape(-1, nth // 2 + 1 if half else nth)
     F, H = sol[False], sol[True]
     assert np.isfinite(F).all() and np.abs(F).max() > 1e-4
-    assert np.abs(F[:, :nth // 2 + 1] - H).max() <= 1e-9 * np.abs(F).max()
+    d = np.abs(F[:, :nth // 2 + 1] - H).max() / np.abs(F).max()
+    assert d > 1e-3, d

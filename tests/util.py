@@ -100,22 +100,32 @@ def rel_err(a, b):
 C_ANS = 3.141592653589793238462643383 * 4.0e-5   # A = V * c (static2d.cpp:66, 1018-1021)
 
 
-def solver_tolerance(tol, A_ref, P, r=None):
-    """Tolerance for comparing the device's A with the reference's.
+CONVERGED_PRECISION = 1e-13
+
+
+def converged(pr, mesh, solve=None):
+    """The oracle run to convergence: the reference's own algorithm (restated
+    Static2D / Harmonic2D with SSOR-PCG / COCG) at Precision 1e-13 instead of
+    the problem's.  The parity contract of the AMG path is
+
+        max|A_gpu - A_converged| <= tol * max|A_converged|   (tol fixed per test)
 
     The reference stops its SSOR-PCG at sqrt(z.r / z0.b) <= Precision
-    (spars.cpp:259/313); on ill-conditioned systems (steel at mu_r ~ 1e3-1e4,
-    condition ~1e5-1e6) that leaves an error in the slowest modes larger than
-    `tol` -- the Jacobi-PCG carries the same error, the AMG-PCG (same test,
-    a preconditioner that resolves those modes) does not.  The reference's own
-    error is measured against the exact solution of the final assembled
-    system (P's, single device) and twice that is allowed."""
-    import scipy.sparse as sp
-    import scipy.sparse.linalg as spla
-    rp, col, val, b = P.csr()
-    n = len(rp) - 1
-    M = sp.csr_matrix((val, col, rp), shape=(n, n))
-    exact = spla.spsolve(M.tocsc(), b) * C_ANS
-    if r is not None:   # axisymmetric answers are the flux 2 pi r A (staticaxi.cpp:774-779)
-        exact = exact * (np.asarray(r) * 0.01 * 2 * np.pi)
-    return max(tol, 2.0 * rel_err(A_ref, exact))
+    (spars.cpp:259/313); on ill-conditioned steel problems that leaves slow-mode
+    error (2.6e-5 of max|A| on bc_showcase(24, nonlinear) at Precision 1e-8)
+    which the AMG-PCG, stopping on the same test, resolves.  The target is built
+    from the oracle alone, so it cannot move with the device's result; the
+    plain distance to the oracle at the problem's Precision is reported next to
+    it (``parity_message``).  Measured: the oracle at 1e-13 is within 7e-14 of a
+    direct solve of its own system (linear) and within 2e-12 of its 1e-15 run
+    (nonlinear)."""
+    import copy
+    from oracle import oracle
+    pr2 = copy.deepcopy(pr)
+    pr2.Precision = CONVERGED_PRECISION
+    return (solve or oracle.solve)(pr2, mesh)[0]
+
+
+def parity_message(A, Ao, Ac, tol):
+    return ("max|dA|/max|A|: vs converged oracle %.3e (tol %.1e), vs oracle at the problem Precision %.3e"
+            % (rel_err(A, Ac), tol, rel_err(A, Ao)))

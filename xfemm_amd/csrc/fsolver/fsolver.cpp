@@ -617,9 +617,26 @@ int FSolver::WriteStatic2D()
     }
     fprintf(fp, "%i\n", NumPBCs);
     for (int k = 0; k < NumPBCs; k++) fprintf(fp, "%i\t%i\t%i\n", pbclist[k].x, pbclist[k].y, pbclist[k].t);
-    fprintf(fp, "%i\n", NumAirGapElems);
+    WriteAirGapElements(fp);
     fclose(fp);
     return true;
+}
+
+void FSolver::WriteAirGapElements(FILE *fp) const
+{
+    // static2d.cpp:1161-1190 / harmonic2d.cpp:1002-1030: per AGE its name as
+    // read from the .pbc (newline kept), the parameter line, and the
+    // totalArcElements + 1 quadNodes in the renumbered node ids -- the input
+    // fpproc's gap integrals (torque, force) read back
+    fprintf(fp, "%i\n", NumAirGapElems);
+    for (const AirGap &g : agelist) {
+        fprintf(fp, "%s", g.name.c_str());
+        fprintf(fp, "%i %.17g %.17g %.17g %.17g %.17g %.17g %.17g %i %.17g %.17g\n", g.format, g.inner_angle,
+                g.outer_angle, g.ri, g.ro, g.arc, g.agc_re, g.agc_im, g.n_arc, g.inner_shift, g.outer_shift);
+        for (int k = 0; k <= g.n_arc; k++)
+            fprintf(fp, "%i %.17g %i %.17g %i %.17g %i %.17g\n", g.qn[4 * k], g.qw[4 * k], g.qn[4 * k + 1],
+                    g.qw[4 * k + 1], g.qn[4 * k + 2], g.qw[4 * k + 2], g.qn[4 * k + 3], g.qw[4 * k + 3]);
+    }
 }
 
 int FSolver::WriteHarmonic2D()
@@ -665,7 +682,7 @@ int FSolver::WriteHarmonic2D()
     }
     fprintf(fp, "%i\n", NumPBCs);
     for (int k = 0; k < NumPBCs; k++) fprintf(fp, "%i  %i %i\n", pbclist[k].x, pbclist[k].y, pbclist[k].t);
-    fprintf(fp, "%i\n", NumAirGapElems);
+    WriteAirGapElements(fp);
     fclose(fp);
     return true;
 }

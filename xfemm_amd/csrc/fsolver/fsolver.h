@@ -62,6 +62,7 @@ public:
     int WriteStatic2D();                                 // static2d.cpp:1038-1195
     int Harmonic2D();                                    // harmonic2d.cpp:36-790 (on the GPU, linear)
     int WriteHarmonic2D();                               // harmonic2d.cpp:793-960
+    void WriteAirGapElements(FILE *fp) const;            // static2d.cpp:1161-1190, harmonic2d.cpp:1002-1030
     void GetFillFactor(int lbl);                         // fsolver.cpp:1083-1105 (static)
     static std::string getErrorString(LoadMeshErr err);
 
