@@ -67,11 +67,23 @@ class stdout_to_stderr:
         os.close(self.saved)
 
 
+def host_cpu():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(n_cells, nonlinear):
-    """Reference CPU solver on a bounded sample of the same workload family:
-    the reference's own CBigLinProb (spars.cpp: linked-list matrix, SSOR-PCG,
-    SetValue) compiled into oracle/_ref, driven by the restated Static2D
-    element loop (oracle/static2d_oracle.c).  Single thread."""
+    """Reference CPU solver on the same workload as the GPU line (configs[2]:
+    the 1000 x 1000-cell, 2M-triangle mesh by default): the reference's own
+    CBigLinProb (spars.cpp: linked-list matrix, SSOR-PCG, SetValue) compiled
+    into oracle/_ref, driven by the restated Static2D element loop
+    (oracle/static2d_oracle.c).  Single thread, as the reference runs."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle import oracle
     from util import synth_to_oracle
@@ -90,10 +102,37 @@ def cpu_baseline(n_cells, nonlinear):
         "unit": "DoF/s",
         "cores": 1,
         "kind": kind,
-        "sample": "%dx%d-cell square (%d tri, %d DoF)%s: full Static2D (assembly + SSOR-PCG to 1e-8%s) "
-                  "in %.1f s; smaller than the GPU workload, so fewer iterations per DoF (favours the CPU)"
-                  % (n_cells, n_cells, 2 * n_cells * n_cells, dof, " M-19" if nonlinear else "", iters, dt),
+        "host_cpu": host_cpu(),
+        "sample": "%dx%d-cell square (%d tri, %d DoF)%s: one full Static2D (assembly + SSOR-PCG to 1e-8%s) "
+                  "in %.1f s on one core of the GPU box's host%s"
+                  % (n_cells, n_cells, 2 * n_cells * n_cells, dof, " M-19" if nonlinear else "", iters, dt,
+                     "; the same mesh as the GPU line" if n_cells == 1000 else "; a smaller mesh than the GPU line"),
     }
+
+
+def nonlinear_secondary(device, args):
+    """BASELINE configs[3] (the same 2M-tri mesh with M-19 B-H steel, full
+    Newton loop with re-assembly every iteration) measured after the main
+    timed region, same step definition (symbolic phase included)."""
+    from xfemm_amd import kernels, synth
+    kw = synth.magnetostatic(args.cells, nonlinear=True)
+    P = kernels.Static2DProblem(device=device, precond=args.precond, amg_sweeps=args.amg_sweeps,
+                                amg_omega=args.amg_omega, **kw)
+    P.solve(rebuild_symbolic=True)
+    _hip_sync()
+    t0 = time.perf_counter()
+    res = [P.solve(rebuild_symbolic=True) for _ in range(args.secondary_steps)]
+    _hip_sync()
+    dt = (time.perf_counter() - t0) / args.secondary_steps
+    n = P.n_nodes
+    P.close()
+    r = res[-1]
+    return {"workload": "configs[3]: synthetic %d-tri square-domain magnetostatic, nonlinear M-19 B-H "
+                        "(Newton, re-assembly every iteration), tol %g" % (2 * args.cells ** 2, kw["precision"]),
+            "metric": "solved DoF/s", "value": n / dt, "unit": "DoF/s", "ms_per_step": 1e3 * dt,
+            "steps": args.secondary_steps, "warmup": 1, "newton_iters": r["newton_iters"],
+            "pcg_iters": r["cg_iters"], "ms_amg_setup": r["ms_amg_setup"], "ms_assemble": r["ms_assemble"],
+            "ms_symbolic": r["ms_symbolic"], "ms_solve": r["ms_solve"]}
 
 
 def pmc_traffic(algo_bytes, kernel="k_cg_spmv"):
@@ -122,7 +161,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cells", type=int, default=1000, help="cells per side (2*cells^2 triangles)")
     ap.add_argument("--nonlinear", action="store_true", help="M-19 B-H steel (configs[3])")
-    ap.add_argument("--cpu-cells", type=int, default=700)
+    ap.add_argument("--cpu-cells", type=int, default=1000,
+                    help="cells per side of the CPU-baseline sample (1000: the GPU line's own 2M-tri mesh)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the configs[3] (nonlinear M-19) secondary measurement")
+    ap.add_argument("--secondary-steps", type=int, default=3)
     ap.add_argument("--precond", choices=["amg", "jacobi"], default="amg",
                     help="device preconditioner of the PCG (the reference uses SSOR)")
     ap.add_argument("--amg-sweeps", type=int, default=1, help="Jacobi sweeps before/after the coarse correction")
@@ -277,6 +320,8 @@ def main():
     }
     if same_mesh is not None:
         out["config"]["same_mesh_1gpu"] = same_mesh
+    if rank == 0 and world == 1 and not sharded and not args.nonlinear and not args.no_secondary:
+        out["secondary"] = nonlinear_secondary(local, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_cells, args.nonlinear)
     if rank == 0:
