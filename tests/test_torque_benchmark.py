@@ -28,14 +28,26 @@ def _have_triangle():
     return os.path.exists(os.path.join(os.path.dirname(mesher.__file__), "_ref", "libtriangle.so"))
 
 
+def _edge_set(path):
+    with open(path) as fh:
+        rows = [ln.split() for ln in fh.read().splitlines()[1:] if ln.strip()]
+    return {(min(int(r[1]), int(r[2])), max(int(r[1]), int(r[2])), int(r[3])) for r in rows}
+
+
 @pytest.mark.skipif(not _have_triangle(), reason="oracle/_ref/libtriangle.so not built (reference absent)")
 def test_mesher_reproduces_committed_fixture(tmp_path):
     res = mesher.mesh_problem(mesher.parse_geometry(os.path.join(GOLDEN, "TorqueBenchmark.fem")))
     base = str(tmp_path / "tb")
     mesher.write_mesh(res, base, {"AGE": (30.0, 0.0)})
-    for ext in (".node", ".ele", ".edge"):
-        assert open(base + ext).read() == open(os.path.join(TORQUE_DIR, "TorqueBenchmark" + ext)).read(), ext
-    assert open(base + ".pbc").read() == open(os.path.join(TORQUE_DIR, "TorqueBenchmark_30.pbc")).read()
+    for ext, ref in ((".node", "TorqueBenchmark.node"), (".ele", "TorqueBenchmark.ele"),
+                     (".pbc", "TorqueBenchmark_30.pbc")):
+        got, exp = open(base + ext).read(), open(os.path.join(TORQUE_DIR, ref)).read()
+        same = got == exp      # (no assert on the strings: pytest's diff of 200 kB texts takes minutes)
+        assert same, "%s differs: %d vs %d lines" % (ext, got.count("\n"), exp.count("\n"))
+    # Triangle numbers edges by comparing triangle addresses (triangle.c
+    # writeedges: `trisym.tri < triangleloop.tri`), so the .edge ORDER depends
+    # on the heap; the set of (edge, marker) does not
+    assert _edge_set(base + ".edge") == _edge_set(os.path.join(TORQUE_DIR, "TorqueBenchmark.edge"))
     assert res.switches == "-pPq33.000000eAazQIY"       # MinAngle 30 + MINANGLE_BUMP, exterior Steiner points off
 
 

@@ -315,9 +315,13 @@ int build_symbolic(xfk_problem *P)
     XFK_CHECK(P->diag.alloc(N));
     launch_row_copy(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, T.rowtmp, P->rowptr.p, P->col.p, P->diag.p);
 
-    // Jones-Plassmann colouring of elements (shared node = conflict) over
-    // full-array sweeps (kernels in xfk_device.hip); the host checks for
-    // completion every kSyncRounds rounds.
+    // The static path assembles by rows (k_assemble_rows): no colouring.  The
+    // time-harmonic path still scatters by colour: Jones-Plassmann colouring
+    // of elements (shared node = conflict) over full-array sweeps (kernels in
+    // xfk_device.hip); the host checks for completion every kSyncRounds rounds.
+    P->ncolors = 0;
+    P->color_rounds = 0;
+    if (P->harmonic) {
     XFK_CHECK(P->color.alloc(NE));
     XFK_CHECK(hipMemsetAsync(P->color.p, 0xff, sizeof(int) * NE, s));
     constexpr int kSyncRounds = 6;
@@ -362,6 +366,7 @@ int build_symbolic(xfk_problem *P)
     XFK_CHECK(P->slot.alloc(9 * (size_t)NE));
     launch_build_erec(s, NE, P->perm.p, P->p_raw.p, P->lbl_raw.p, P->ebits_raw.p, P->erec.p, P->ebits.p, T.iperm);
     launch_build_slots(s, NE, N, P->p_raw.p, T.iperm, P->rowptr.p, P->col.p, P->slot.p, T.cnt);
+    }
 
     // rows adjacent to fixed nodes
     launch_mark_fix_adj(s, N, P->rowptr.p, P->col.p, P->fixed.p, T.flag);
@@ -373,6 +378,10 @@ int build_symbolic(xfk_problem *P)
     P->nfix_cols = hc[1];
     XFK_CHECK(P->mu1.alloc(NE));
     XFK_CHECK(P->mu2.alloc(NE));
+    if (!P->harmonic) {
+        XFK_CHECK(P->mu1b.alloc(NE));
+        XFK_CHECK(P->mu2b.alloc(NE));
+    }
 
     // air-gap entries -> CSR slots (full storage: both triangles)
     P->age_n = 0;
@@ -477,9 +486,7 @@ int build_symbolic(xfk_problem *P)
 static int assemble(xfk_problem *P, int iter)
 {
     hipStream_t s = P->stream;
-    XFK_CHECK(hipMemsetAsync(P->val.p, 0, sizeof(double) * P->nnz, s));
-    XFK_CHECK(hipMemsetAsync(P->b.p, 0, sizeof(double) * P->N, s));
-    AssembleArgs A;
+    AssembleArgs A = {};
     A.erec = P->erec.p;
     A.ebits = P->ebits.p;
     A.slot = P->slot.p;
@@ -502,7 +509,20 @@ static int assemble(xfk_problem *P, int iter)
     A.ext_ro = P->ext_ro;
     A.ext_ri = P->ext_ri;
     A.ext_zo = P->ext_zo;
-    for (int c = 0; c < P->ncolors; ++c) launch_assemble_color(s, P->color_off[c], P->color_off[c + 1], A);
+    A.p_raw = P->p_raw.p;
+    A.lbl_raw = P->lbl_raw.p;
+    A.ebits_raw = P->ebits_raw.p;
+    A.n2e_ptr = P->n2e_ptr.p;
+    A.n2e = P->n2e.p;
+    A.rowptr = P->rowptr.p;
+    A.col = P->col.p;
+    A.mu1_out = P->mu1b.p;
+    A.mu2_out = P->mu2b.p;
+    launch_assemble_rows(s, P->N, A);   // writes every entry of val and b
+    std::swap(P->mu1.p, P->mu1b.p);     // the state just written is read next iteration
+    std::swap(P->mu1.n, P->mu1b.n);
+    std::swap(P->mu2.p, P->mu2b.p);
+    std::swap(P->mu2.n, P->mu2b.n);
     launch_add_at_slots(s, P->age_n, P->age_slot.p, P->age_v.p, P->val.p);   // air-gap elements
     launch_point_currents(s, P->npt, P->pt_nodes.p, P->pt_J.p, P->b.p);
     launch_dirichlet(s, P->nfix_rows, P->fix_rows.p, P->nfix_cols, P->fix_cols_row.p, P->rowptr.p, P->col.p,

@@ -434,9 +434,10 @@ __device__ void get_bh_props(const DevBlock &m, const double *__restrict__ Bt, c
 // weighted sources and boundary terms, B from the element energy, the
 // exterior-region permeability warp.  Me / be are the element's contribution
 // before the sign of the global assembly (as in the planar path).
-__device__ void axi_element(int i, const AssembleArgs &A, const int (&n)[3], const double (&X)[3],
-                            const double (&Y)[3], const DevLabel &lab, const DevBlock &bp, double (&Me)[3][3],
-                            double (&be)[3])
+template <bool FIRST>
+__device__ __forceinline__ void axi_element(int eb, const AssembleArgs &A, const int (&n)[3], const double (&X)[3],
+                            const double (&Y)[3], const DevLabel &lab, const DevBlock &bp, double &m1, double &m2,
+                            double (&Me)[3][3], double (&be)[3])
 {
     AxiGeom Gm;
     axi_geometry(X, Y, Gm);
@@ -449,7 +450,6 @@ __device__ void axi_element(int i, const AssembleArgs &A, const int (&n)[3], con
         be[j] = 0.;
     }
     // mixed boundary conditions (staticaxi.cpp:298-320)
-    const int eb = A.ebits[i];
     if (eb)
         for (int j = 0; j < 3; ++j) {
             const int ej = ((eb >> (10 * j)) & 1023) - 1;
@@ -486,10 +486,10 @@ __device__ void axi_element(int i, const AssembleArgs &A, const int (&n)[3], con
             be[j] += Km;
             be[k] += Km;
         }
-    // permeability (staticaxi.cpp:409-632)
-    double m1, m2;
+    // permeability (staticaxi.cpp:409-632); m1 / m2 in: the element's Newton
+    // state (iter > 0), out: its new state
     const double Vn[3] = {A.V[n[0]], A.V[n[1]], A.V[n[2]]};
-    if (A.iter == 0) {
+    if (FIRST) {   // iter == 0: the blocks' linear permeabilities
         const double f = bp.LamFill;
         if (bp.LamType == 0) { m1 = bp.mu_x * f; m2 = bp.mu_y * f; }
         else if (bp.LamType == 1) { m1 = bp.mu_x * f + (1. - f); m2 = bp.mu_x / (f + bp.mu_x * (1. - f)); }
@@ -501,11 +501,7 @@ __device__ void axi_element(int i, const AssembleArgs &A, const int (&n)[3], con
             m1 /= kludge;
             m2 /= kludge;
         }
-        A.mu1[i] = m1;
-        A.mu2[i] = m2;
     } else {
-        m1 = A.mu1[i];
-        m2 = A.mu2[i];
         if (bp.BHpoints > 0 && bp.LamType <= 2 && (bp.LamType != 0 || m1 == m2)) {
             const double f = bp.LamFill;
             const double sx = (bp.LamType == 2) ? 1. / (f * f) : 1., sy = (bp.LamType == 1) ? 1. / (f * f) : 1.;
@@ -548,8 +544,6 @@ __device__ void axi_element(int i, const AssembleArgs &A, const int (&n)[3], con
                 for (int j = 0; j < 3; ++j)
                     for (int w = 0; w < 3; ++w) Mn[j][w] = Kn * (v[j] * u[w] + v[w] * u[j]);
             }
-            A.mu1[i] = m1;
-            A.mu2[i] = m2;
         }
     }
     for (int j = 0; j < 3; ++j)
@@ -559,48 +553,20 @@ __device__ void axi_element(int i, const AssembleArgs &A, const int (&n)[3], con
         }
 }
 
-// AssembleArgs: see xfk_kernels.h
-
-__global__ void __launch_bounds__(kBlock) k_assemble_color(int begin, int end, AssembleArgs A)
+// FSolver::Static2D element (static2d.cpp:352-805): Me / be before the sign
+// of the global assembly, m1 / m2 the element's permeability state.
+template <bool FIRST>
+__device__ __forceinline__ void planar_element(int eb, const AssembleArgs &A, const int (&n)[3],
+                                               const double (&X)[3], const double (&Y)[3], const DevLabel &lab,
+                                               const DevBlock &bp, double &m1, double &m2, double (&Me)[3][3],
+                                               double (&be)[3])
 {
-    // LDS-staged element -> CSR slot maps: the tile's 9-int records are one
-    // contiguous span, loaded coalesced and read back per element.
-    __shared__ int s_slot[kBlock * 9 + kBlock / 8];
-    const int tile0 = begin + blockIdx.x * kBlock;
-    const int ntile = min(kBlock, end - tile0);
-    if (ntile <= 0) return;
-    for (int k = threadIdx.x; k < ntile * 9; k += kBlock) {
-        int e = k / 9;
-        s_slot[k + (e >> 3)] = A.slot[(size_t)tile0 * 9 + k];   // pad one int per 8 records
-    }
-    __syncthreads();
-    const int li = threadIdx.x;
-    if (li >= ntile) return;
-    const int i = tile0 + li;
-    const int4 r = A.erec[i];
-    const int n[3] = {r.x, r.y, r.z};
-    const DevLabel lab = A.labels[r.w];
-    const DevBlock bp = A.blocks[lab.blk];
-    const double X[3] = {A.x[n[0]], A.x[n[1]], A.x[n[2]]};
-    const double Y[3] = {A.y[n[0]], A.y[n[1]], A.y[n[2]]};
-    const int *sl = &s_slot[li * 9 + (li >> 3)];
-    if (A.axi) {
-        double Me[3][3], be[3];
-        axi_element(i, A, n, X, Y, lab, bp, Me, be);
-        for (int j = 0; j < 3; ++j) {
-            if (sl[3 * j] < 0) continue;
-            for (int k = 0; k < 3; ++k) A.val[sl[3 * j + k]] -= (k >= j) ? Me[j][k] : Me[k][j];
-            A.b[n[j]] -= be[j];
-        }
-        return;
-    }
-
     double p[3], q[3];
     p[0] = Y[1] - Y[2]; p[1] = Y[2] - Y[0]; p[2] = Y[0] - Y[1];
     q[0] = X[2] - X[1]; q[1] = X[0] - X[2]; q[2] = X[1] - X[0];
     const double a = (p[0] * q[1] - p[1] * q[0]) / 2.;
     const double K = (-1. / (4. * a));
-    double Mx[3][3], My[3][3], Me[3][3], Mn[3][3], be[3];
+    double Mx[3][3], My[3][3], Mn[3][3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
 #pragma unroll
@@ -614,7 +580,6 @@ __global__ void __launch_bounds__(kBlock) k_assemble_color(int begin, int end, A
     }
 
     // mixed boundary conditions on the element's edges (static2d.cpp:459-480)
-    const int eb = A.ebits[i];
     if (eb) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -656,20 +621,16 @@ __global__ void __launch_bounds__(kBlock) k_assemble_color(int begin, int end, A
         }
     }
 
-    // permeability (static2d.cpp:600-797)
-    double m1, m2;
+    // permeability (static2d.cpp:600-797); m1 / m2 in: the element's Newton
+    // state (iter > 0), out: its new state
     const double Vn[3] = {A.V[n[0]], A.V[n[1]], A.V[n[2]]};
-    if (A.iter == 0) {
+    if (FIRST) {   // iter == 0: the blocks' linear permeabilities
         const double f = bp.LamFill;
         if (bp.LamType == 0) { m1 = bp.mu_x * f + (1. - f); m2 = bp.mu_y * f + (1. - f); }
         else if (bp.LamType == 1) { m1 = bp.mu_x * f + (1. - f); m2 = bp.mu_x / (f + bp.mu_x * (1. - f)); }
         else if (bp.LamType == 2) { m2 = bp.mu_y * f + (1. - f); m1 = bp.mu_y / (f + bp.mu_y * (1. - f)); }
         else { m1 = 1; m2 = 1; }
-        A.mu1[i] = m1;
-        A.mu2[i] = m2;
     } else {
-        m1 = A.mu1[i];
-        m2 = A.mu2[i];
         if (bp.BHpoints > 0 && bp.LamType <= 2 && (bp.LamType != 0 || m1 == m2)) {
             const double f = bp.LamFill;
             double B1 = 0., B2 = 0.;
@@ -713,8 +674,6 @@ __global__ void __launch_bounds__(kBlock) k_assemble_color(int begin, int end, A
                 for (int j = 0; j < 3; ++j)
                     for (int w = 0; w < 3; ++w) Mn[j][w] = Kn * (v[j] * u[w] + v[w] * u[j]);
             }
-            A.mu1[i] = m1;
-            A.mu2[i] = m2;
         }
     }
 
@@ -727,18 +686,74 @@ __global__ void __launch_bounds__(kBlock) k_assemble_color(int begin, int end, A
             be[j] += Mn[j][k] * Vn[k];
         }
 
-    // colour-exclusive scatter: no other element of this launch touches n[*];
-    // rows of halo nodes (slot -1) belong to another rank
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        if (sl[3 * j] < 0) continue;
+}
+
+// Row-gather assembly (static planar / axisymmetric): one thread per owned CSR
+// row i sums the contributions of the elements incident on node i, in
+// ascending element order -- the order the reference's AddTo accumulates each
+// entry in -- so no colouring, no element -> slot maps and no zeroing pass are
+// needed, and every row is written exactly once.  Each element is evaluated
+// once per vertex (3x the arithmetic of a scatter, none of its random
+// read-modify-writes).  Rows of <= kRowAcc entries accumulate in LDS, longer
+// ones (air-gap rings, periodic corners) in place in val (the row is private
+// to its thread).  The element's permeability state is read from mu*_in and
+// written to mu*_out by the thread of its first owned vertex.
+constexpr int kRowBlock = 128;
+constexpr int kRowAcc = 12;
+
+template <bool AXI, bool FIRST>
+__global__ void __launch_bounds__(kRowBlock) k_assemble_rows(int N, AssembleArgs A)
+{
+    __shared__ double s_acc[kRowAcc * kRowBlock];
+    __shared__ int s_col[kRowAcc * kRowBlock];
+    const int i = blockIdx.x * kRowBlock + threadIdx.x;
+    if (i >= N) return;
+    const int rs = A.rowptr[i], L = A.rowptr[i + 1] - rs;
+    const bool lds = L <= kRowAcc;
+    double *acc = lds ? s_acc + threadIdx.x : A.val + rs;
+    const int stride = lds ? kRowBlock : 1;
+    const int *cols = lds ? s_col + threadIdx.x : A.col + rs;
+    for (int k = 0; k < L; ++k) {
+        acc[k * stride] = 0.;
+        if (lds) s_col[k * kRowBlock + threadIdx.x] = A.col[rs + k];
+    }
+    double bi = 0.;
+    const int t1 = A.n2e_ptr[i + 1];
+    for (int t = A.n2e_ptr[i]; t < t1; ++t) {
+        const int e = A.n2e[t];
+        const int n[3] = {A.p_raw[3 * e], A.p_raw[3 * e + 1], A.p_raw[3 * e + 2]};
+        const int j = (n[0] == i) ? 0 : ((n[1] == i) ? 1 : 2);
+        const DevLabel lab = A.labels[A.lbl_raw[e]];
+        const DevBlock bp = A.blocks[lab.blk];
+        const double X[3] = {A.x[n[0]], A.x[n[1]], A.x[n[2]]};
+        const double Y[3] = {A.y[n[0]], A.y[n[1]], A.y[n[2]]};
+        double m1 = 0., m2 = 0., Me[3][3], be[3];
+        if (!FIRST) {
+            m1 = A.mu1[e];
+            m2 = A.mu2[e];
+        }
+        if (AXI) axi_element<FIRST>(A.ebits_raw[e], A, n, X, Y, lab, bp, m1, m2, Me, be);
+        else planar_element<FIRST>(A.ebits_raw[e], A, n, X, Y, lab, bp, m1, m2, Me, be);
+        const int w = (n[0] < N) ? 0 : ((n[1] < N) ? 1 : 2);
+        if (w == j) {
+            A.mu1_out[e] = m1;
+            A.mu2_out[e] = m2;
+        }
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const double m = (k >= j) ? Me[j][k] : Me[k][j];   // upper value, exact symmetry
-            A.val[sl[3 * j + k]] -= m;
+            // row j of Me, upper values (exact symmetry), selected without
+            // dynamic register indexing
+            const double m = (j == 0) ? Me[0][k] : ((j == 1) ? ((k >= 1) ? Me[1][k] : Me[0][1])
+                                                             : ((k == 2) ? Me[2][2] : Me[k][2]));
+            int pos = 0;
+            while (pos < L - 1 && cols[pos * stride] != n[k]) ++pos;
+            acc[pos * stride] -= m;
         }
-        A.b[n[j]] -= be[j];
+        bi -= (j == 0) ? be[0] : ((j == 1) ? be[1] : be[2]);
     }
+    if (lds)
+        for (int k = 0; k < L; ++k) A.val[rs + k] = s_acc[k * kRowBlock + threadIdx.x];
+    A.b[i] = bi;
 }
 
 // point currents (static2d.cpp:818-825)
@@ -944,10 +959,19 @@ void launch_compact_flags(hipStream_t s, int N, const int *flag, int *cursor, in
 {
     if (N) k_compact_flags<<<nblk(N), kBlock, 0, s>>>(N, flag, cursor, out);
 }
-void launch_assemble_color(hipStream_t s, int begin, int end, const AssembleArgs &A)
+void launch_assemble_rows(hipStream_t s, int N, const AssembleArgs &A)
 {
-    if (end > begin) k_assemble_color<<<nblk(end - begin), kBlock, 0, s>>>(begin, end, A);
+    if (N <= 0) return;
+    const int g = (N + kRowBlock - 1) / kRowBlock;
+    if (A.axi) {
+        if (A.iter == 0) k_assemble_rows<true, true><<<g, kRowBlock, 0, s>>>(N, A);
+        else k_assemble_rows<true, false><<<g, kRowBlock, 0, s>>>(N, A);
+    } else {
+        if (A.iter == 0) k_assemble_rows<false, true><<<g, kRowBlock, 0, s>>>(N, A);
+        else k_assemble_rows<false, false><<<g, kRowBlock, 0, s>>>(N, A);
+    }
 }
+
 void launch_point_currents(hipStream_t s, int n, const int *nodes, const double *J, double *b)
 {
     if (n) k_point_currents<<<nblk(n), kBlock, 0, s>>>(n, nodes, J, b);

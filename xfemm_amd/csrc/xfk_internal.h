@@ -231,7 +231,8 @@ struct xfk_problem {
     xfk::DBuf<int4> erec;            // colour order
     xfk::DBuf<int> ebits;            // colour order
     xfk::DBuf<int> slot;             // colour order, 9 per element
-    xfk::DBuf<double> mu1, mu2;      // colour order
+    xfk::DBuf<double> mu1, mu2;      // element permeability state (colour order: harmonic; raw order: static)
+    xfk::DBuf<double> mu1b, mu2b;    // static row-gather assembly: the state written by the current assembly
 
     // boundary conditions
     xfk::DBuf<int> pt_nodes;         // nodes with a point current / fixed point value

@@ -21,6 +21,10 @@ struct AssembleArgs {
     int iter;
     int axi;                      // StaticAxisymmetric element matrices (staticaxi.cpp:172-632)
     double ext_ro, ext_ri, ext_zo;   // exterior region (cm)
+    // row-gather assembly (k_assemble_rows): raw-order element data, node ->
+    // element lists, the CSR pattern, permeability state out (mu1 / mu2 in)
+    const int *p_raw, *lbl_raw, *ebits_raw, *n2e_ptr, *n2e, *rowptr, *col;
+    double *mu1_out, *mu2_out;
 };
 
 int grid_reduce(int N);
@@ -77,7 +81,8 @@ void launch_lookup_slots(hipStream_t s, int n, const int *rc, const int *rowptr,
 void launch_mark_fix_adj(hipStream_t s, int N, const int *rowptr, const int *col, const unsigned char *fixed,
                          int *flag);
 void launch_compact_flags(hipStream_t s, int N, const int *flag, int *cursor, int *out);
-void launch_assemble_color(hipStream_t s, int begin, int end, const AssembleArgs &A);
+// one thread per owned row, contributions of the incident elements in element order
+void launch_assemble_rows(hipStream_t s, int N, const AssembleArgs &A);
 void launch_point_currents(hipStream_t s, int n, const int *nodes, const double *J, double *b);
 void launch_dirichlet(hipStream_t s, int nrows, const int *rows, int nadj, const int *adj, const int *rowptr,
                       const int *col, const int *diag, const unsigned char *fixed, const double *fix_first,
