@@ -117,7 +117,7 @@ def nonlinear_secondary(device, args):
     from xfemm_amd import kernels, synth
     kw = synth.magnetostatic(args.cells, nonlinear=True)
     P = kernels.Static2DProblem(device=device, precond=args.precond, amg_sweeps=args.amg_sweeps,
-                                amg_omega=args.amg_omega, **kw)
+                                amg_omega=args.amg_omega, amg_dense=args.amg_dense, **kw)
     P.solve(rebuild_symbolic=True)
     _hip_sync()
     t0 = time.perf_counter()
@@ -170,6 +170,7 @@ def main():
                     help="device preconditioner of the PCG (the reference uses SSOR)")
     ap.add_argument("--amg-sweeps", type=int, default=1, help="Jacobi sweeps before/after the coarse correction")
     ap.add_argument("--amg-omega", type=float, default=1.75, help="Jacobi weight factor (weight omega / rho)")
+    ap.add_argument("--amg-dense", type=int, default=None, help="dense coarsest level of at most this many rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per SpMV launch from a PMC pass (profiles/), if measured")
@@ -205,13 +206,13 @@ def main():
         with stdout_to_stderr():
             comm = kernels.Comm.rccl(uid, rank, world, local)
         P = kernels.Static2DProblem(device=local, comm=comm, precond=args.precond, amg_sweeps=args.amg_sweeps,
-                                    amg_omega=args.amg_omega, **kw)
+                                    amg_omega=args.amg_omega, amg_dense=args.amg_dense, **kw)
         n_dof = P.n_nodes                       # global DoF of the sharded mesh
     else:
         cells = args.cells
         kw = synth.magnetostatic(cells, nonlinear=args.nonlinear)
         P = kernels.Static2DProblem(device=local, precond=args.precond, amg_sweeps=args.amg_sweeps,
-                                    amg_omega=args.amg_omega, **kw)
+                                    amg_omega=args.amg_omega, amg_dense=args.amg_dense, **kw)
         n_dof = P.n_nodes
 
     def barrier():
@@ -253,7 +254,7 @@ def main():
         P.close()
         if rank == 0:
             Q = kernels.Static2DProblem(device=local, precond=args.precond, amg_sweeps=args.amg_sweeps,
-                                        amg_omega=args.amg_omega, **kw)
+                                        amg_omega=args.amg_omega, amg_dense=args.amg_dense, **kw)
             Q.solve(rebuild_symbolic=True)
             t1 = time.perf_counter()
             r1 = Q.solve(rebuild_symbolic=True)

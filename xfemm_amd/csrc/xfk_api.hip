@@ -24,6 +24,8 @@
 #include "xfk_age.h"
 #include "xfk_comm.h"
 #include "xfk_kernels.h"
+#include <cstdio>
+#include <cstdlib>
 #include "xfk_partition.h"
 
 namespace xfk {
@@ -1013,6 +1015,11 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
 {
     xfk_problem *P = new xfk_problem();
     P->device = device;
+    if (std::getenv("XFK_SPIN_WAIT")) {   // experiment: host waits spin instead of yielding
+        hipError_t e = hipSetDevice(device);
+        if (e == hipSuccess) e = hipSetDeviceFlags(hipDeviceScheduleSpin);
+        std::fprintf(stderr, "[xfk] hipDeviceScheduleSpin: %s\n", hipGetErrorString(e));
+    }
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking) != hipSuccess) {
         set_error("cannot initialise the HIP device/stream");
         delete P;
