@@ -23,6 +23,10 @@
         }                                                                                  \
     } while (0)
 
+typedef int nt_i4 __attribute__((ext_vector_type(4)));
+typedef int nt_i2 __attribute__((ext_vector_type(2)));
+typedef double nt_d2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ int xcd_tile(int b, int nb)
 {
     const int q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
@@ -163,6 +167,100 @@ __global__ void __launch_bounds__(B) k_v4(int N, const int *__restrict__ rowptr,
     if (r < N) y[r] = acc;
 }
 
+// V5: 4 entries per lane-slot: one 16-B int4 load of col + two 16-B double2
+// loads of val (the tile's stream realigned to 4 entries), PER slots per lane
+template <int B, int PER, bool NT>
+__global__ void __launch_bounds__(B) k_v5(int N, const int *__restrict__ rowptr, const int *__restrict__ col,
+                                          const double *__restrict__ val, const double *__restrict__ x,
+                                          double *__restrict__ y)
+{
+    constexpr int CAP = 4 * PER * B;
+    __shared__ double lds[CAP];
+    const int t = xcd_tile(blockIdx.x, gridDim.x);
+    const int r0 = t * B;
+    const int r = r0 + threadIdx.x;
+    const int rend = min(r0 + B, N);
+    const int s = rowptr[r0], e = rowptr[rend];
+    const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
+    double acc = 0.0;
+    const int s4 = s & ~3;
+    for (int c0 = s4; c0 < e; c0 += CAP) {
+        const int c1 = min(e, c0 + CAP);
+#pragma unroll
+        for (int m = 0; m < PER; ++m) {
+            const int k = c0 + 4 * (threadIdx.x + m * B);
+            if (k + 3 < c1 && k >= s) {
+                int4 c;
+                double2 v0, v1;
+                if (NT) {
+                    const nt_i4 ci = __builtin_nontemporal_load(reinterpret_cast<const nt_i4 *>(col + k));
+                    const nt_d2 a0 = __builtin_nontemporal_load(reinterpret_cast<const nt_d2 *>(val + k));
+                    const nt_d2 a1 = __builtin_nontemporal_load(reinterpret_cast<const nt_d2 *>(val + k + 2));
+                    c = make_int4(ci.x, ci.y, ci.z, ci.w);
+                    v0 = make_double2(a0.x, a0.y);
+                    v1 = make_double2(a1.x, a1.y);
+                } else {
+                    c = *reinterpret_cast<const int4 *>(col + k);
+                    v0 = *reinterpret_cast<const double2 *>(val + k);
+                    v1 = *reinterpret_cast<const double2 *>(val + k + 2);
+                }
+                lds[k - c0] = v0.x * x[c.x];
+                lds[k + 1 - c0] = v0.y * x[c.y];
+                lds[k + 2 - c0] = v1.x * x[c.z];
+                lds[k + 3 - c0] = v1.y * x[c.w];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (k + q >= s && k + q < c1) lds[k + q - c0] = val[k + q] * x[col[k + q]];
+            }
+        }
+        __syncthreads();
+        const int a = max(my_s, c0), z = min(my_e, c1);
+        for (int k = a; k < z; ++k) acc += lds[k - c0];
+        __syncthreads();
+    }
+    if (r < N) y[r] = acc;
+}
+
+// V6: V4 (pairs) with nontemporal matrix loads
+template <int B>
+__global__ void __launch_bounds__(B) k_v6(int N, const int *__restrict__ rowptr, const int *__restrict__ col,
+                                          const double *__restrict__ val, const double *__restrict__ x,
+                                          double *__restrict__ y)
+{
+    constexpr int CAP = 8 * B;
+    __shared__ double lds[CAP];
+    const int t = xcd_tile(blockIdx.x, gridDim.x);
+    const int r0 = t * B;
+    const int r = r0 + threadIdx.x;
+    const int rend = min(r0 + B, N);
+    const int s = rowptr[r0], e = rowptr[rend];
+    const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
+    double acc = 0.0;
+    const int s2 = s & ~1;
+    for (int c0 = s2; c0 < e; c0 += CAP) {
+        const int c1 = min(e, c0 + CAP);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int k = c0 + 2 * (threadIdx.x + m * B);
+            if (k + 1 < c1 && k >= s) {
+                const nt_d2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_d2 *>(val + k));
+                const nt_i2 c = __builtin_nontemporal_load(reinterpret_cast<const nt_i2 *>(col + k));
+                lds[k - c0] = v.x * x[c.x];
+                lds[k + 1 - c0] = v.y * x[c.y];
+            } else {
+                if (k >= s && k < c1) lds[k - c0] = val[k] * x[col[k]];
+                if (k + 1 >= s && k + 1 < c1) lds[k + 1 - c0] = val[k + 1] * x[col[k + 1]];
+            }
+        }
+        __syncthreads();
+        const int a = max(my_s, c0), z = min(my_e, c1);
+        for (int k = a; k < z; ++k) acc += lds[k - c0];
+        __syncthreads();
+    }
+    if (r < N) y[r] = acc;
+}
+
 int main(int argc, char **argv)
 {
     const char *path = argc > 1 ? argv[1] : "/tmp/csr.bin";
@@ -235,6 +333,9 @@ int main(int argc, char **argv)
         run("V0 tile512 x8 (product)", by12, [&] { k_v0<512, 8><<<g, 512>>>(n, d_rp, d_col, d_val, d_x, d_y); });
         run("V1 tile512 x8 int16 offsets", by10, [&] { k_v1<512, 8><<<g, 512>>>(n, d_rp, d_off, d_val, d_x, d_y); });
         run("V4 tile512 16-B val/col pairs", by12, [&] { k_v4<512><<<g, 512>>>(n, d_rp, d_col, d_val, d_x, d_y); });
+        run("V5 tile512 int4+2xdouble2 x2", by12, [&] { k_v5<512, 2, false><<<g, 512>>>(n, d_rp, d_col, d_val, d_x, d_y); });
+        run("V5nt tile512 int4+2xdouble2 x2 NT", by12, [&] { k_v5<512, 2, true><<<g, 512>>>(n, d_rp, d_col, d_val, d_x, d_y); });
+        run("V6 tile512 pairs NT", by12, [&] { k_v6<512><<<g, 512>>>(n, d_rp, d_col, d_val, d_x, d_y); });
     }
     {
         const int g = (n + 255) / 256;
@@ -242,11 +343,15 @@ int main(int argc, char **argv)
         run("V2b tile256 x8", by12, [&] { k_v0<256, 8><<<g, 256>>>(n, d_rp, d_col, d_val, d_x, d_y); });
         run("V1b tile256 x16 int16 offsets", by10, [&] { k_v1<256, 16><<<g, 256>>>(n, d_rp, d_off, d_val, d_x, d_y); });
         run("V3 row per lane", by12, [&] { k_v3<<<g, 256>>>(n, d_rp, d_col, d_val, d_x, d_y); });
+        run("V4b tile256 pairs", by12, [&] { k_v4<256><<<g, 256>>>(n, d_rp, d_col, d_val, d_x, d_y); });
+        run("V5b tile256 int4 x2", by12, [&] { k_v5<256, 2, false><<<g, 256>>>(n, d_rp, d_col, d_val, d_x, d_y); });
     }
     {
         const int g = (n + 1023) / 1024;
         run("V2c tile1024 x8", by12, [&] { k_v0<1024, 8><<<g, 1024>>>(n, d_rp, d_col, d_val, d_x, d_y); });
         run("V1c tile1024 x8 int16", by10, [&] { k_v1<1024, 8><<<g, 1024>>>(n, d_rp, d_off, d_val, d_x, d_y); });
+        run("V4c tile1024 pairs", by12, [&] { k_v4<1024><<<g, 1024>>>(n, d_rp, d_col, d_val, d_x, d_y); });
+        run("V5c tile1024 int4 x2", by12, [&] { k_v5<1024, 2, false><<<g, 1024>>>(n, d_rp, d_col, d_val, d_x, d_y); });
     }
     return 0;
 }

@@ -63,9 +63,13 @@ __device__ __forceinline__ int xcd_tile(int b, int nb)
 }
 
 // y = sum_k val[k] * X(col[k]) for the B rows of one tile (B threads, one
-// row each); CSR-stream: the tile's products are staged through LDS (8 B
-// doubles per pass) by coalesced reads of col / val, then each thread sums
-// its own row
+// row each); CSR-stream: the tile's products are staged through LDS by
+// coalesced 16-B reads -- each lane takes 4 consecutive nonzeros per slot (one
+// int4 of col, two double2 of val; the stream realigned to 4 entries, the
+// partial quads at its ends read per entry), 2 slots per lane per pass -- then
+// each thread sums its own row in order.  Measured on the configs[2] matrix
+// (tools/lab/spmv_lab.hip): 16.5 us vs 19.9 us for one 4/8-B entry per lane,
+// bit-identical sums.  col / val must be 16-B aligned (hipMalloc'd arrays).
 template <int B = kCgBlock, class XF>
 __device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restrict__ rowptr,
                                                const int *__restrict__ col, const double *__restrict__ val,
@@ -77,20 +81,24 @@ __device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restr
     const int s = rowptr[r0], e = rowptr[rend];
     const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
     double acc = 0.0;
-    for (int c0 = s; c0 < e; c0 += CAP) {
+    for (int c0 = s & ~3; c0 < e; c0 += CAP) {
         const int c1 = min(e, c0 + CAP);
-        int cidx[8];
-        double v[8];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const int k = c0 + threadIdx.x + m * B;
-            cidx[m] = (k < c1) ? col[k] : -1;
-            v[m] = (k < c1) ? val[k] : 0.0;
-        }
+        for (int m = 0; m < 2; ++m) {
+            const int k = c0 + 4 * (threadIdx.x + m * B);
+            if (k >= s && k + 3 < c1) {
+                const int4 c = *reinterpret_cast<const int4 *>(col + k);
+                const double2 v0 = *reinterpret_cast<const double2 *>(val + k);
+                const double2 v1 = *reinterpret_cast<const double2 *>(val + k + 2);
+                lds[k - c0] = v0.x * X(c.x);
+                lds[k + 1 - c0] = v0.y * X(c.y);
+                lds[k + 2 - c0] = v1.x * X(c.z);
+                lds[k + 3 - c0] = v1.y * X(c.w);
+            } else {
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const int k = c0 + threadIdx.x + m * B;
-            if (cidx[m] >= 0) lds[k - c0] = v[m] * X(cidx[m]);
+                for (int q = 0; q < 4; ++q)
+                    if (k + q >= s && k + q < c1) lds[k + q - c0] = val[k + q] * X(col[k + q]);
+            }
         }
         __syncthreads();
         const int a = max(my_s, c0), z = min(my_e, c1);
