@@ -71,7 +71,7 @@ class OrhProblem(C.Structure):
                 ("precision", C.c_double), ("frequency", C.c_double), ("length_units", C.c_int),
                 ("coords", C.c_int), ("bandwidth", C.c_int), ("problem_type", C.c_int),
                 ("extZo", C.c_double), ("extRo", C.c_double), ("extRi", C.c_double),
-                ("n_ages", C.c_int), ("ages", C.POINTER(OraAge))]
+                ("n_ages", C.c_int), ("ages", C.POINTER(OraAge)), ("ac_solver", C.c_int)]
 
 
 _CREATE = C.CFUNCTYPE(C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double)
@@ -84,12 +84,17 @@ _SETVAL = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_double, C.c_double)
 _PAIR = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int)
 _SOLVE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int)
 _WIPE = C.CFUNCTYPE(None, C.c_void_p)
+_PUTK = C.CFUNCTYPE(None, C.c_void_p, C.c_double, C.c_double, C.c_int, C.c_int, C.c_int)
+_GETK = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_int, dptr, dptr)
+_NEWTON = C.CFUNCTYPE(C.c_int, C.c_void_p)
+_SETPREC = C.CFUNCTYPE(None, C.c_void_p, C.c_double)
 
 
 class OrhOps(C.Structure):
     _fields_ = [("create", _CREATE), ("destroy", _DESTROY), ("addto", _ADDTO), ("get", _GET), ("put", _PUT),
                 ("b", _GETV), ("V", _GETV), ("setvalue", _SETVAL), ("periodicity", _PAIR),
-                ("antiperiodicity", _PAIR), ("solve", _SOLVE), ("wipe", _WIPE)]
+                ("antiperiodicity", _PAIR), ("solve", _SOLVE), ("wipe", _WIPE), ("put_k", _PUTK),
+                ("get_k", _GETK), ("newton", _NEWTON), ("set_precision", _SETPREC)]
 
 
 def _hlib():
@@ -116,7 +121,9 @@ def _ref_ops() -> OrhOps:
     return OrhOps(f(_CREATE, "ref_clp_create"), f(_DESTROY, "ref_clp_destroy"), f(_ADDTO, "ref_clp_addto"),
                   f(_GET, "ref_clp_get"), f(_PUT, "ref_clp_put"), f(_GETV, "ref_clp_b"), f(_GETV, "ref_clp_V"),
                   f(_SETVAL, "ref_clp_setvalue"), f(_PAIR, "ref_clp_periodicity"),
-                  f(_PAIR, "ref_clp_antiperiodicity"), f(_SOLVE, "ref_clp_solve"), f(_WIPE, "ref_clp_wipe"))
+                  f(_PAIR, "ref_clp_antiperiodicity"), f(_SOLVE, "ref_clp_solve"), f(_WIPE, "ref_clp_wipe"),
+                  f(_PUTK, "ref_clp_put_k"), f(_GETK, "ref_clp_get_k"), f(_NEWTON, "ref_clp_newton"),
+                  f(_SETPREC, "ref_clp_set_precision"))
 
 
 def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
@@ -164,6 +171,7 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
     P.length_units, P.coords, P.bandwidth = pr.LengthUnits, pr.Coords, mesh.bandwidth
     P.problem_type, P.extZo, P.extRo, P.extRi = pr.ProblemType, pr.extZo, pr.extRo, pr.extRi
     P.n_ages, P.ages = make_ages(mesh, keep)
+    P.ac_solver = int(getattr(pr, "ACSolver", 0))
     keep.items.extend([blocks, labels, lines, points, circs])
     return P, keep, circs
 

@@ -85,6 +85,11 @@ typedef struct {
     double precision, lambda;
     crow *M;
     cx *b, *V, *P, *R, *U, *Z;
+    /* Newton AC solver (cspars.cpp:58, 160-184): auxiliary matrices, allocated
+       by the first Put with k > 0 */
+    int bnewton;
+    crow *Mh, *Ms, *Ma;
+    cx *uu, *vv;
 } clp;
 
 static void crow_reserve(crow *r, int cap)
@@ -121,13 +126,45 @@ static void *clp_create(int n, int bw, int nodes, double precision)
     return L;
 }
 
+static crow *crows_new(int n)
+{
+    crow *M = (crow *)calloc(n, sizeof(crow));
+    for (int i = 0; i < n; i++) {
+        crow_reserve(&M[i], 8);
+        M[i].len = 1;
+        M[i].c[0] = i;
+        M[i].x[0] = C(0, 0);
+    }
+    return M;
+}
+
+static void crows_free(crow *M, int n)
+{
+    if (!M) return;
+    for (int i = 0; i < n; i++) {
+        free(M[i].c);
+        free(M[i].x);
+    }
+    free(M);
+}
+
+static void crows_zero(crow *M, int n)
+{
+    for (int i = 0; i < n; i++)
+        for (int k = 0; k < M[i].len; k++) M[i].x[k] = C(0, 0);
+}
+
 static void clp_wipe(void *lp)
-{   /* cspars.cpp:539-555 */
+{   /* cspars.cpp:539-590 */
     clp *L = (clp *)lp;
     for (int i = 0; i < L->n; i++) {
         L->b[i] = C(0, 0);
         for (int k = 0; k < L->M[i].len; k++) L->M[i].x[k] = C(0, 0);
     }
+    if (!L->bnewton) return;
+    crows_zero(L->Mh, L->n);
+    crows_zero(L->Ma, L->n);
+    crows_zero(L->Ms, L->n);
 }
 
 static void clp_destroy(void *lp)
@@ -139,8 +176,61 @@ static void clp_destroy(void *lp)
         free(L->M[i].x);
     }
     free(L->M);
+    crows_free(L->Mh, L->n);
+    crows_free(L->Ms, L->n);
+    crows_free(L->Ma, L->n);
     free(L->b); free(L->V); free(L->P); free(L->R); free(L->U); free(L->Z);
+    free(L->uu); free(L->vv);
     free(L);
+}
+
+static crow *lp_mat(clp *L, int k)
+{
+    return k == 1 ? L->Mh : (k == 2 ? L->Ms : (k == 3 ? L->Ma : L->M));
+}
+
+static void lp_putk(clp *L, cx v, int p, int q, int k)
+{   /* cspars.cpp:147-233 */
+    if (q < p) {
+        int t = p; p = q; q = t;
+        if (k == 1) v = cconj(v);           /* hermitian matrix */
+        if (k == 3) v = cneg(cconj(v));     /* antihermitian matrix */
+    }
+    if (k > 0 && !L->bnewton) {             /* allocate the auxiliary matrices on first use */
+        L->bnewton = 1;
+        L->Mh = crows_new(L->n);
+        L->Ma = crows_new(L->n);
+        L->Ms = crows_new(L->n);
+        L->uu = (cx *)calloc(L->n, sizeof(cx));
+        L->vv = (cx *)calloc(L->n, sizeof(cx));
+    }
+    crow *r = &lp_mat(L, k)[p];
+    int t = 0;
+    while (t < r->len && r->c[t] < q) t++;
+    if (t < r->len && r->c[t] == q) { r->x[t] = v; return; }
+    crow_reserve(r, r->len + 1);
+    memmove(r->c + t + 1, r->c + t, sizeof(int) * (r->len - t));
+    memmove(r->x + t + 1, r->x + t, sizeof(cx) * (r->len - t));
+    r->c[t] = q;
+    r->x[t] = v;
+    r->len++;
+}
+
+static cx lp_getk(clp *L, int p, int q, int k)
+{   /* cspars.cpp:235-283 */
+    int flip = 0;
+    if (q < p) { int t = p; p = q; q = t; flip = 1; }
+    if (k > 0 && !L->bnewton) return C(0, 0);
+    const crow *r = &lp_mat(L, k)[p];
+    for (int t = 0; t < r->len; t++) {
+        if (r->c[t] == q) {
+            if (flip && k == 1) return cconj(r->x[t]);
+            if (flip && k == 3) return cneg(cconj(r->x[t]));
+            return r->x[t];
+        }
+        if (r->c[t] > q) break;
+    }
+    return C(0, 0);
 }
 
 static void lp_put(clp *L, cx v, int p, int q)
@@ -208,6 +298,23 @@ static void clp_setvalue(void *lp, int i, double xr, double xi)
             L->b[k] = csub(L->b[k], cmul(z, x));
             if (i != k) lp_put(L, C(0, 0), k, i);
         }
+        if (L->bnewton) {   /* cspars.cpp:511-534 (Ma, like Ms, acts on conj(x) here) */
+            z = lp_getk(L, k, i, 1);
+            if (cnz(z)) {
+                if (i != k) L->b[k] = csub(L->b[k], cmul(z, x));
+                lp_putk(L, C(0, 0), k, i, 1);
+            }
+            z = lp_getk(L, k, i, 2);
+            if (cnz(z)) {
+                if (i != k) L->b[k] = csub(L->b[k], cmul(z, cconj(x)));
+                lp_putk(L, C(0, 0), k, i, 2);
+            }
+            z = lp_getk(L, k, i, 3);
+            if (cnz(z)) {
+                if (i != k) L->b[k] = csub(L->b[k], cmul(z, cconj(x)));
+                lp_putk(L, C(0, 0), k, i, 3);
+            }
+        }
     }
     L->b[i] = cmul(lp_get(L, i, i), x);
 }
@@ -255,6 +362,40 @@ static void clp_pair(clp *L, int i, int j, int anti)
         c = dmulc(0.5, cadd(L->b[i], L->b[j]));
         L->b[i] = c;
         L->b[j] = c;
+    }
+    if (!L->bnewton) return;
+    for (int h = 1; h <= 3; h++) {   /* cspars.cpp:648-671 / 732-755 */
+        for (int k = fst; k < L->n; k++) {
+            if ((k != i) && (k != j)) {
+                cx v1 = lp_getk(L, k, i, h), v2 = lp_getk(L, k, j, h);
+                if (cnz(v1) || cnz(v2)) {
+                    if (anti) {
+                        cx cc = cdivd(csub(v1, v2), 2.);
+                        lp_putk(L, cc, k, i, h);
+                        lp_putk(L, cneg(cc), k, j, h);
+                    } else {
+                        cx cc = cdivd(cadd(v1, v2), 2.);
+                        lp_putk(L, cc, k, i, h);
+                        lp_putk(L, cc, k, j, h);
+                    }
+                }
+            }
+            if ((k == i + L->bdw) && (k < j - L->bdw) && (L->bdw != 0)) k = j - L->bdw;
+            else if (k == lst) k = L->nodes;
+        }
+        if (anti) {
+            cx cc = cdivd(cadd(csub(csub(lp_getk(L, i, i, h), lp_getk(L, i, j, h)), lp_getk(L, j, i, h)),
+                               lp_getk(L, j, j, h)), 4.);
+            lp_putk(L, cc, i, i, h);
+            lp_putk(L, cneg(cc), i, j, h);
+            lp_putk(L, cc, j, j, h);
+        } else {
+            cx cc = cdivd(cadd(cadd(cadd(lp_getk(L, i, i, h), lp_getk(L, i, j, h)), lp_getk(L, j, i, h)),
+                               lp_getk(L, j, j, h)), 4.);
+            lp_putk(L, cc, i, i, h);
+            lp_putk(L, cc, i, j, h);
+            lp_putk(L, cc, j, j, h);
+        }
     }
 }
 
@@ -385,17 +526,123 @@ static int lp_pbcgsolve(clp *L, int flag)
     return 1;
 }
 
+/* Y = M_k X for k = 1 (hermitian), 2 (complex symmetric), 3 (antihermitian)
+   stored as their upper triangles (cspars.cpp:290-360) */
+static void lp_multA_k(clp *L, const cx *X, cx *Y, int k)
+{
+    const crow *M = lp_mat(L, k);
+    for (int i = 0; i < L->n; i++) Y[i] = C(0, 0);
+    for (int i = 0; i < L->n; i++) {
+        const crow *r = &M[i];
+        Y[i] = cadd(Y[i], cmul(r->x[0], X[i]));
+        for (int t = 1; t < r->len; t++) {
+            const int c = r->c[t];
+            Y[i] = cadd(Y[i], cmul(r->x[t], X[c]));
+            if (k == 1) Y[c] = cadd(Y[c], cmul(cconj(r->x[t]), X[i]));
+            else if (k == 3) Y[c] = cadd(Y[c], cmul(cneg(cconj(r->x[t])), X[i]));
+            else Y[c] = cadd(Y[c], cmul(r->x[t], X[i]));
+        }
+    }
+}
+
+/* Y = conj(M_2) X (cspars.cpp:362-404, k = 2: the complex-symmetric branch) */
+static void lp_multconjA_2(clp *L, const cx *X, cx *Y)
+{
+    const crow *M = L->Ms;
+    for (int i = 0; i < L->n; i++) Y[i] = C(0, 0);
+    for (int i = 0; i < L->n; i++) {
+        const crow *r = &M[i];
+        Y[i] = cadd(Y[i], cmul(cconj(r->x[0]), X[i]));
+        for (int t = 1; t < r->len; t++) {
+            const int c = r->c[t];
+            Y[i] = cadd(Y[i], cmul(cconj(r->x[t]), X[c]));
+            Y[c] = cadd(Y[c], cmul(cconj(r->x[t]), X[i]));
+        }
+    }
+}
+
+/* the full Newton operator, MultA(X, Y, -1) (cspars.cpp:303-312):
+   Y = M X + Mh X + Ms conj(X) + Ma X */
+static void lp_multA_full(clp *L, const cx *X, cx *Y)
+{
+    lp_multA(L, X, Y);
+    lp_multA_k(L, X, L->uu, 1);
+    for (int i = 0; i < L->n; i++) Y[i] = cadd(Y[i], L->uu[i]);
+    lp_multconjA_2(L, X, L->uu);
+    lp_multA_k(L, X, L->vv, 3);
+    for (int i = 0; i < L->n; i++) Y[i] = cadd(cadd(Y[i], cconj(L->uu[i])), L->vv[i]);
+}
+
+/* CBigComplexLinProb::KludgeSolve (cspars.cpp:983-1059): outer iterations on
+   the non-complex-linear Newton system, each a complex-symmetric PBCGSolve of
+   the main matrix against the RHS moved by the auxiliary matrices at the
+   current V, then a least-squares step length along the update */
+static int lp_kludgesolve(clp *L, int flag)
+{
+    const int n = L->n;
+    cx *borig = (cx *)calloc(n, sizeof(cx)), *v = (cx *)calloc(n, sizeof(cx)), *r = (cx *)calloc(n, sizeof(cx));
+    if (flag == 0)
+        for (int i = 0; i < n; i++) L->V[i] = C(0, 0);
+    const double normb = lp_nrm(L->b, n);
+    for (int i = 0; i < n; i++) {
+        borig[i] = L->b[i];
+        v[i] = L->V[i];
+    }
+    lp_multA_full(L, L->V, r);
+    for (int i = 0; i < n; i++) r[i] = csub(L->b[i], r[i]);
+    double er = lp_nrm(r, n) / normb;
+    long long its = 0;
+    if (!(er < L->precision)) {
+        for (int k = 0; k < 10; k++) {
+            lp_multA_k(L, L->V, L->P, 1);
+            lp_multconjA_2(L, L->V, L->U);
+            lp_multA_k(L, L->V, L->R, 3);
+            for (int i = 0; i < n; i++)
+                L->b[i] = csub(csub(csub(borig[i], L->P[i]), cconj(L->U[i])), L->R[i]);
+            lp_pbcgsolve(L, 1);
+            its += g_iters;
+            for (int i = 0; i < n; i++) L->P[i] = csub(L->V[i], v[i]);
+            lp_multA_full(L, L->P, L->U);
+            const double cstep = lp_conjdot(r, L->U, n).re / lp_conjdot(L->U, L->U, n).re;
+            for (int i = 0; i < n; i++) {
+                L->V[i] = cadd(v[i], dmulc(cstep, L->P[i]));
+                r[i] = csub(r[i], dmulc(cstep, L->U[i]));
+                v[i] = L->V[i];
+            }
+            er = lp_nrm(r, n) / normb;
+            if (er < L->precision * 10.) break;
+        }
+    }
+    g_iters = its;
+    free(borig);
+    free(v);
+    free(r);
+    return 1;
+}
+
 static int clp_solve(void *lp, int flag)
-{   /* cspars.cpp:1062-1081 (bNewton false) */
+{   /* cspars.cpp:1062-1081 */
     clp *L = (clp *)lp;
+    if (L->bnewton) return lp_kludgesolve(L, flag);
     if (flag == 0)
         if (lp_pcgsqstart(L) == 0) return 0;
     return lp_pbcgsolve(L, 2);
 }
 
+static void clp_put_k(void *lp, double vr, double vi, int p, int q, int k) { lp_putk((clp *)lp, C(vr, vi), p, q, k); }
+static void clp_get_k(void *lp, int p, int q, int k, double *vr, double *vi)
+{
+    cx z = lp_getk((clp *)lp, p, q, k);
+    *vr = z.re;
+    *vi = z.im;
+}
+static int clp_newton(void *lp) { return ((clp *)lp)->bnewton; }
+static void clp_set_precision(void *lp, double p) { ((clp *)lp)->precision = p; }
+
 static const orh_linprob_ops g_builtin = {clp_create, clp_destroy, clp_addto, clp_get, clp_put,
                                           clp_b, clp_V, clp_setvalue, clp_periodicity,
-                                          clp_antiperiodicity, clp_solve, clp_wipe};
+                                          clp_antiperiodicity, clp_solve, clp_wipe,
+                                          clp_put_k, clp_get_k, clp_newton, clp_set_precision};
 
 const orh_linprob_ops *orh_builtin_linprob(void) { return &g_builtin; }
 
@@ -465,6 +712,69 @@ static cx bh_dhdb(const orh_block *m, double B)
             return h;
         }
     return C(0, 0);
+}
+
+/* CMSolverMaterialProp::GetBHProps(double, CComplex&, CComplex&) (CMaterialProp.cpp:1008-1057) */
+static void bh_getbhprops(const orh_block *m, double B, cx *v, cx *dv)
+{
+    const double b = fabs(B);
+    const int n = m->BHpoints;
+    if (b == 0) {
+        *v = bh_S(m, 0);
+        *dv = C(0, 0);
+        return;
+    }
+    if (b > m->B[n - 1]) {
+        const cx h = cadd(bh_H(m, n - 1), cmuld(bh_S(m, n - 1), b - m->B[n - 1]));
+        const cx dh = bh_S(m, n - 1);
+        *v = cdivd(h, b);
+        *dv = dmulc(0.5, csub(cdivd(dh, b * b), cdivd(h, b * b * b)));
+        return;
+    }
+    for (int i = 0; i < n - 1; i++)
+        if ((b >= m->B[i]) && (b <= m->B[i + 1])) {
+            const double l = m->B[i + 1] - m->B[i], z = (b - m->B[i]) / l, z2 = z * z;
+            cx h = dmulc(1. - 3. * z2 + 2. * z2 * z, bh_H(m, i));
+            h = cadd(h, dmulc(z * (1. - 2. * z + z2) * l, bh_S(m, i)));
+            h = cadd(h, dmulc(z2 * (3. - 2. * z), bh_H(m, i + 1)));
+            h = cadd(h, dmulc(z2 * (z - 1.) * l, bh_S(m, i + 1)));
+            cx dh = cdivd(dmulc(6. * z * (z - 1.), bh_H(m, i)), l);
+            dh = cadd(dh, dmulc(1. - 4. * z + 3. * z * z, bh_S(m, i)));
+            dh = cadd(dh, cdivd(dmulc(6. * z * (1. - z), bh_H(m, i + 1)), l));
+            dh = cadd(dh, dmulc(z * (3. * z - 2.), bh_S(m, i + 1)));
+            *v = cdivd(h, b);
+            *dv = dmulc(0.5, csub(cdivd(dh, b * b), cdivd(h, b * b * b)));
+            return;
+        }
+}
+
+/* Newton terms of one nonlinear element (harmonic2d.cpp:610-639,
+   harmonicaxi.cpp:519-545): mu from GetBHProps, v = (Mx + My) V, K =
+   -200 c^3 dv / a (a: area, or the r-weighted volume of the axisymmetric
+   element), Mn = K Re(v v^H), Mnh / Mna the Hermitian / anti-Hermitian
+   remainders of 0.5 Re(K) v v^H / 0.5 I Im(K) v v^H, Mns = 0.5 K v v^T */
+static void newton_terms(const orh_block *blk, double B, double c, double a, const cx (*Mx)[3], const cx (*My)[3],
+                         const cx *Vn, cx *mu_out, cx (*Mn)[3], cx (*Mnh)[3], cx (*Mna)[3], cx (*Mns)[3])
+{
+    cx mu, dv, v[3];
+    bh_getbhprops(blk, B, &mu, &dv);
+    mu = ddivc(1., cmuld(mu, ORH_MUO));   /* 1./(muo*mu): double * CComplex */
+    *mu_out = mu;
+    for (int j = 0; j < 3; j++) {
+        v[j] = C(0, 0);
+        for (int w = 0; w < 3; w++) v[j] = cadd(v[j], cmul(cadd(Mx[j][w], My[j][w]), Vn[w]));
+    }
+    const cx K = cdivd(dmulc(-200. * c * c * c, dv), a);
+    const cx half_im = cmuld(cmuld(I, 0.5), K.im);   /* I*0.5*Im(K) */
+    for (int j = 0; j < 3; j++)
+        for (int w = 0; w < 3; w++) {
+            const cx vv = cmul(v[j], cconj(v[w]));
+            Mn[j][w] = cmuld(K, vv.re);
+            Mnh[j][w] = C(cmul(dmulc(0.5 * K.re, v[j]), cconj(v[w])).re - Mn[j][w].re,
+                          cmul(dmulc(0.5 * K.re, v[j]), cconj(v[w])).im);
+            Mna[j][w] = csub(cmul(cmul(half_im, v[j]), cconj(v[w])), cmuld(I, Mn[j][w].im));
+            Mns[j][w] = cmul(cmul(dmulc(0.5, K), v[j]), v[w]);
+        }
 }
 
 void orh_acprops(const orh_block *b, const double *Bq, int nq, double *v, double *dhdb)
@@ -572,6 +882,55 @@ static void circuits(orh_problem *pr)
 }
 
 /* one element of HarmonicAxisymmetric (harmonicaxi.cpp:215-605) */
+/* Element matrices into the system (harmonic2d.cpp:671-705, harmonicaxi.cpp:588-623).
+   ACSolver 0: Me += Mx/mu2 + My/mu1 (+ Mxy v12 planar), be += Mn V.
+   ACSolver 1 (every element, Newton terms zero unless it is nonlinear): Me +=
+   Mx/mu2 + My/mu1 + Mn, be += (Mnh + Mna + Mn) V + Mns conj(V), and the nonzero
+   upper-triangle Newton terms accumulate into the auxiliary matrices 1, 2, 3
+   (Put(Get(k) + m, k)). */
+static void element_to_system(const orh_problem *pr, const orh_linprob_ops *ops, void *L, const int *n, cx (*Me)[3],
+                              cx *be, cx (*Mx)[3], cx (*My)[3], cx (*Mxy)[3], cx v12, cx (*Mn)[3], cx (*Mnh)[3],
+                              cx (*Mna)[3], cx (*Mns)[3], cx mu1, cx mu2, const cx *VL, cx *bL, int planar)
+{
+    static const cx Z3[3][3];
+    const int ac1 = pr->ac_solver == 1;
+    if (ac1 && !Mnh) {   /* linear element of a Newton problem: the zeroed Mnh / Mna / Mns (:399-404) */
+        Mnh = (cx(*)[3])Z3;
+        Mna = (cx(*)[3])Z3;
+        Mns = (cx(*)[3])Z3;
+    }
+    for (int j = 0; j < 3; j++)
+        for (int k = 0; k < 3; k++) {
+            if (ac1) {
+                Me[j][k] = cadd(Me[j][k], cadd(cadd(cdiv(Mx[j][k], mu2), cdiv(My[j][k], mu1)), Mn[j][k]));
+                be[j] = cadd(be[j], cmul(cadd(cadd(Mnh[j][k], Mna[j][k]), Mn[j][k]), VL[n[k]]));
+                be[j] = cadd(be[j], cmul(Mns[j][k], cconj(VL[n[k]])));
+            } else if (planar) {
+                Me[j][k] = cadd(Me[j][k], cadd(cadd(cdiv(Mx[j][k], mu2), cdiv(My[j][k], mu1)), cmul(Mxy[j][k], v12)));
+                be[j] = cadd(be[j], cmul(Mn[j][k], VL[n[k]]));
+            } else {
+                Me[j][k] = cadd(Me[j][k], cadd(cdiv(Mx[j][k], mu2), cdiv(My[j][k], mu1)));
+                be[j] = cadd(be[j], cmul(Mn[j][k], VL[n[k]]));
+            }
+        }
+    for (int j = 0; j < 3; j++) {
+        for (int k = j; k < 3; k++) {
+            ops->addto(L, Me[j][k].re, Me[j][k].im, n[j], n[k]);
+            if (ac1) {
+                const cx *aux[3] = {&Mnh[j][k], &Mns[j][k], &Mna[j][k]};
+                for (int m = 0; m < 3; m++) {
+                    if (aux[m]->re == 0 && aux[m]->im == 0) continue;
+                    double gr, gi;
+                    ops->get_k(L, n[j], n[k], m + 1, &gr, &gi);
+                    const cx s = cadd(C(gr, gi), *aux[m]);
+                    ops->put_k(L, s.re, s.im, n[j], n[k], m + 1);
+                }
+            }
+        }
+        bL[n[j]] = cadd(bL[n[j]], be[j]);
+    }
+}
+
 static void axi_element(orh_problem *pr, const orh_linprob_ops *ops, void *L, const effmu *Mu, double w, int Iter,
                         int i, cx *VL, cx *bL)
 {
@@ -709,7 +1068,8 @@ static void axi_element(orh_problem *pr, const orh_linprob_ops *ops, void *L, co
     /* permeability: the block's / successive approximation with B from the
      * element energy (:425-560) / the exterior warp (:567-574) */
     cx mu1 = Mu[pr->blk[i]].mu0, mu2 = Mu[pr->blk[i]].mu1;
-    int updated = 0;
+    cx Mnh[3][3], Mna[3][3], Mns[3][3];
+    int updated = 0, newton = 0;
     if (Iter > 0 && blk->LamType == 0 && blk->BHpoints > 0 && mu1.re == mu2.re && mu1.im == mu2.im) {
         cx v[3], dv = C(0, 0);
         for (int j = 0; j < 3; j++) {
@@ -719,6 +1079,13 @@ static void axi_element(orh_problem *pr, const orh_linprob_ops *ops, void *L, co
         for (int j = 0; j < 3; j++) dv = cadd(dv, cmul(cconj(VL[n[j]]), v[j]));
         dv = cmuld(dv, (10000. * c * c / vol));
         double B = sqrt(cx_abs(dv));
+        if (pr->ac_solver == 1) {   /* Newton (harmonicaxi.cpp:520-547): K over vol */
+            const cx Vn[3] = {VL[n[0]], VL[n[1]], VL[n[2]]};
+            newton_terms(blk, B, c, vol, (const cx(*)[3])Mx, (const cx(*)[3])My, Vn, &mu1, Mn, Mnh, Mna, Mns);
+            mu2 = mu1;
+            newton = 1;
+            updated = 1;
+        } else {
         cx murel = ddivc(1., cmuld(bh_getv(blk, B), ORH_MUO));
         cx muinc = ddivc(1., cmuld(bh_dhdb(blk, B), ORH_MUO));
         K = cdiv(cmul(dmulc(2., murel), muinc), cadd(murel, muinc));
@@ -728,6 +1095,7 @@ static void axi_element(orh_problem *pr, const orh_linprob_ops *ops, void *L, co
         for (int j = 0; j < 3; j++)
             for (int k = 0; k < 3; k++) Mn[j][k] = cmul(K, cadd(Mx[j][k], My[j][k]));
         updated = 1;
+        }
     }
     if (lab->IsExternal && !updated) {   /* set at Iter 0 and kept by linear elements */
         double u = units[pr->length_units];
@@ -736,15 +1104,8 @@ static void axi_element(orh_problem *pr, const orh_linprob_ops *ops, void *L, co
         mu1 = cdivd(mu1, kludge);
         mu2 = cdivd(mu2, kludge);
     }
-    for (int j = 0; j < 3; j++)
-        for (int k = 0; k < 3; k++) {
-            Me[j][k] = cadd(Me[j][k], cadd(cdiv(Mx[j][k], mu2), cdiv(My[j][k], mu1)));
-            be[j] = cadd(be[j], cmul(Mn[j][k], VL[n[k]]));
-        }
-    for (int j = 0; j < 3; j++) {
-        for (int k = j; k < 3; k++) ops->addto(L, Me[j][k].re, Me[j][k].im, n[j], n[k]);
-        bL[n[j]] = cadd(bL[n[j]], be[j]);
-    }
+    element_to_system(pr, ops, L, n, Me, be, Mx, My, NULL, C(0, 0), Mn, newton ? Mnh : NULL, Mna, Mns, mu1, mu2, VL,
+                      bL, 0);
 }
 
 static void hage_emit(void *ctx, double v, int p, int q)
@@ -883,6 +1244,8 @@ static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L,
          * later passes, nonlinear LamType-0 blocks: successive approximation
          * (:588-660, ACSolver 0) */
         cx mu1 = Mu[pr->blk[i]].mu0, mu2 = Mu[pr->blk[i]].mu1, v12 = C(0, 0);
+        cx Mnh[3][3], Mna[3][3], Mns[3][3];
+        int newton = 0;
         if (Iter > 0 && blk->LamType == 0 && blk->BHpoints > 0 && mu1.re == mu2.re && mu1.im == mu2.im) {
             cx B1 = C(0, 0), B2 = C(0, 0);
             for (int j = 0; j < 3; j++) {
@@ -891,6 +1254,12 @@ static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L,
             }
             cx s1 = cmul(B1, cconj(B1)), s2 = cmul(B2, cconj(B2));
             double B = c * sqrt(cx_abs(s1) + cx_abs(s2)) / (0.02 * a);
+            if (pr->ac_solver == 1) {   /* Newton (:611-639) */
+                const cx Vn[3] = {VL[n[0]], VL[n[1]], VL[n[2]]};
+                newton_terms(blk, B, c, a, (const cx(*)[3])Mx, (const cx(*)[3])My, Vn, &mu1, Mn, Mnh, Mna, Mns);
+                mu2 = mu1;
+                newton = 1;
+            } else {
             cx murel = ddivc(1., cmuld(bh_getv(blk, B), ORH_MUO));   /* muo * Get_v: CComplex * double */
             cx muinc = ddivc(1., cmuld(bh_dhdb(blk, B), ORH_MUO));
             cx K = cdiv(cmul(dmulc(2., murel), muinc), cadd(murel, muinc));
@@ -899,16 +1268,10 @@ static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L,
             K = cneg(csub(ddivc(1., murel), ddivc(1., K)));
             for (int j = 0; j < 3; j++)
                 for (int k = 0; k < 3; k++) Mn[j][k] = cmul(K, cadd(Mx[j][k], My[j][k]));
-        }
-        for (int j = 0; j < 3; j++)
-            for (int k = 0; k < 3; k++) {
-                Me[j][k] = cadd(Me[j][k], cadd(cadd(cdiv(Mx[j][k], mu2), cdiv(My[j][k], mu1)), cmul(Mxy[j][k], v12)));
-                be[j] = cadd(be[j], cmul(Mn[j][k], VL[n[k]]));
             }
-        for (int j = 0; j < 3; j++) {
-            for (int k = j; k < 3; k++) ops->addto(L, Me[j][k].re, Me[j][k].im, n[j], n[k]);
-            bL[n[j]] = cadd(bL[n[j]], be[j]);
         }
+        element_to_system(pr, ops, L, n, Me, be, Mx, My, Mxy, v12, Mn, newton ? Mnh : NULL, Mna, Mns, mu1, mu2, VL,
+                          bL, 1);
     }
     /* point currents (:634-641) */
     for (int i = 0; i < NN; i++) {
@@ -1009,6 +1372,11 @@ int orh_harmonic2d(orh_problem *pr, const orh_linprob_ops *ops, double *A_out, o
         assemble_and_bc(pr, ops, L, Mu, w, Iter);
         cx *VL = (cx *)ops->V(L);
         for (int j = 0; j < n; j++) Vold[j] = VL[j];
+        if (ops->newton(L)) {   /* :821-825 */
+            double lp = 1.e-4 < 0.001 * res ? 1.e-4 : 0.001 * res;
+            if (lp < pr->precision) lp = pr->precision;
+            ops->set_precision(L, lp);
+        }
         g_iters = -1;
         ok = ops->solve(L, Iter);
         if (!ok) break;

@@ -92,6 +92,7 @@ typedef struct {
     int problem_type;           /* 0 planar (Harmonic2D), 1 axisymmetric (HarmonicAxisymmetric) */
     double extZo, extRo, extRi; /* exterior region (axisymmetric), length units of the file */
     int n_ages;  const ora_age *ages;   /* air-gap elements (planar only) */
+    int ac_solver;              /* [ACSolver]: 0 successive approximation, 1 Newton (KludgeSolve) */
 } orh_problem;
 
 typedef struct {
@@ -107,6 +108,12 @@ typedef struct {
     void (*antiperiodicity)(void *L, int i, int j);
     int (*solve)(void *L, int flag);   /* PBCGSolveMod(flag, false) */
     void (*wipe)(void *L);             /* Wipe(): matrix and b to zero, V kept */
+    /* Newton AC solver: the auxiliary matrices k = 1 (Hermitian Mh), 2 (symmetric
+     * Ms, applied to conj(x)), 3 (anti-Hermitian Ma) of Put / Get (cspars.cpp:147-283) */
+    void (*put_k)(void *L, double vr, double vi, int p, int q, int k);
+    void (*get_k)(void *L, int p, int q, int k, double *vr, double *vi);
+    int (*newton)(void *L);            /* bNewton */
+    void (*set_precision)(void *L, double precision);
 } orh_linprob_ops;
 
 const orh_linprob_ops *orh_builtin_linprob(void);

@@ -150,5 +150,14 @@ void ref_clp_periodicity(void *L, int i, int j) { CL(L)->Periodicity(i, j); }
 void ref_clp_antiperiodicity(void *L, int i, int j) { CL(L)->AntiPeriodicity(i, j); }
 int ref_clp_solve(void *L, int flag) { return CL(L)->PBCGSolveMod(flag, false) ? 1 : 0; }
 void ref_clp_wipe(void *L) { CL(L)->Wipe(); }
+void ref_clp_put_k(void *L, double vr, double vi, int p, int q, int k) { CL(L)->Put(CComplex(vr, vi), p, q, k); }
+void ref_clp_get_k(void *L, int p, int q, int k, double *vr, double *vi)
+{
+    CComplex v = CL(L)->Get(p, q, k);
+    *vr = v.re;
+    *vi = v.im;
+}
+int ref_clp_newton(void *L) { return CL(L)->bNewton ? 1 : 0; }
+void ref_clp_set_precision(void *L, double precision) { CL(L)->Precision = precision; }
 
 }  // extern "C"

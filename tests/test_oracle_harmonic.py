@@ -45,3 +45,37 @@ def test_oracle_solves_its_system(kind):
     assert np.linalg.norm(b - M @ V) / np.linalg.norm(b) <= 2 * pr.Precision
     exact = sla.spsolve(M.tocsc(), b)
     assert np.abs(V - exact).max() / np.abs(exact).max() <= 1e-4
+
+
+def _newton_case(kind):
+    if kind == "axi":
+        kw = synth.harmonic_axisymmetric(12, nonlinear=True)
+    elif kind == "axi_ext":
+        kw = synth.harmonic_axisymmetric(12, nonlinear=True, external=True)
+    elif kind == "periodic":
+        kw = synth.harmonic(14, nonlinear=True, periodic=True)
+    elif kind == "hf":
+        kw = synth.harmonic(14, nonlinear=True, frequency=5000.0)
+    else:
+        kw = synth.harmonic(14, nonlinear=True)
+    kw["ac_solver"] = 1
+    return kw
+
+
+@pytest.mark.skipif(not oracle.ref_available(), reason="reference build (oracle/_ref) absent")
+@pytest.mark.parametrize("kind", ["planar", "periodic", "hf", "axi", "axi_ext"])
+def test_newton_ac_solver_is_bit_identical_to_reference(kind):
+    """[ACSolver] = 1: the element Newton terms (harmonic2d.cpp:611-639 /
+    harmonicaxi.cpp:520-547) into the auxiliary matrices and KludgeSolve
+    (cspars.cpp), the restated linprob against the compiled one."""
+    kw = _newton_case(kind)
+    pr, mesh, _ = synth_to_oracle(kw)
+    A1, st1, c1 = oh.solve(pr, mesh, "oracle")
+    A2, st2, c2 = oh.solve(pr, mesh, "reference")
+    assert np.array_equal(A1, A2)
+    assert c1 == c2 and st1["newton_iters"] == st2["newton_iters"]
+    # the Newton path is taken: a different iteration and answer than ACSolver 0
+    kw["ac_solver"] = 0
+    pr0, mesh0, _ = synth_to_oracle(kw)
+    A0, st0, _ = oh.solve(pr0, mesh0, "oracle")
+    assert st0["newton_iters"] != st1["newton_iters"] and not np.array_equal(A0, A1)

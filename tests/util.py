@@ -44,6 +44,7 @@ def synth_to_oracle(kw: dict):
     pr.Relax = 1.0
     pr.Frequency = kw.get("frequency", 0.0)
     pr.ProblemType = kw.get("problem_type", 0)
+    pr.ACSolver = kw.get("ac_solver", 0)
     pr.extZo, pr.extRo, pr.extRi = kw.get("ext_zo", 0.0), kw.get("ext_ro", 0.0), kw.get("ext_ri", 0.0)
     for b in kw["blocks"]:
         m = femfile.BlockProp(mu_x=b.get("mu_x", 1.0), mu_y=b.get("mu_y", 1.0), H_c=b.get("H_c", 0.0),

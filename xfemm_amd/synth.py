@@ -113,12 +113,12 @@ def magnetostatic(n: int, nonlinear: bool = False, L: float = 10.0, J: float = 2
 
 
 def fem_text(blocks, lines, precision=1e-8, units="centimeters", frequency=0.0, problem_type=0,
-             ext=(0.0, 0.0, 0.0)) -> str:
+             ext=(0.0, 0.0, 0.0), ac_solver=0) -> str:
     """A .fem header carrying the property tables (no geometry: meshes are given)."""
     out = ["[Format]      =  4.0", "[Frequency]   =  %.17g" % frequency, "[Precision]   =  %.17g" % precision,
            "[MinAngle]    =  30", "[Depth]       =  1", "[LengthUnits] =  %s" % units,
            "[ProblemType] =  %s" % ("axisymmetric" if problem_type == 1 else "planar"),
-           "[Coordinates] =  cartesian", "[ACSolver]    =  0",
+           "[Coordinates] =  cartesian", "[ACSolver]    =  %d" % ac_solver,
            "[extZo] = %.17g" % ext[0], "[extRo] = %.17g" % ext[1], "[extRi] = %.17g" % ext[2],
            '[PrevSoln]    = ""', "[PrevType]    =  0", '[Comment]     =  "synthetic"',
            "[PointProps]   = 0", "[BdryProps]   = %d" % len(lines)]
@@ -158,7 +158,8 @@ def write_problem(base: str, kw: dict, label_xy: Optional[np.ndarray] = None) ->
     conv = 1.0   # centimeters
     text = fem_text(kw["blocks"], kw["lines"], kw["precision"], frequency=kw.get("frequency", 0.0),
                     problem_type=kw.get("problem_type", 0),
-                    ext=(kw.get("ext_zo", 0.0), kw.get("ext_ro", 0.0), kw.get("ext_ri", 0.0)))
+                    ext=(kw.get("ext_zo", 0.0), kw.get("ext_ro", 0.0), kw.get("ext_ri", 0.0)),
+                    ac_solver=kw.get("ac_solver", 0))
     labels = kw["labels"]
     text += "[NumPoints] = 0\n[NumSegments] = 0\n[NumArcSegments] = 0\n[NumHoles] = 0\n"
     text += "[NumBlockLabels] = %d\n" % len(labels)
