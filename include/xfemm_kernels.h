@@ -249,9 +249,18 @@ int xfk_dist_get_info(const xfk_problem *prob, xfk_dist_info *info);
  * current in a conducting region, whose voltage gradient is an extra
  * unknown -- are solved through the Schur complement of the bordered system
  * (one extra COCG solve per such circuit; not with periodic boundaries).
+ * ac_solver = 1 selects the reference's Newton AC solver instead
+ * (harmonic2d.cpp:611-639, harmonicaxi.cpp:520-547): after the first pass the
+ * nonlinear elements add their Newton terms -- Mn to the matrix, the
+ * Hermitian / conj-symmetric / anti-Hermitian remainders to three auxiliary
+ * matrices -- and every pass solves M V + Mh V + Ms conj(V) + Ma V = b by the
+ * reference's KludgeSolve (cspars.cpp:1000-1060: at most 10 COCG solves on M
+ * with the auxiliary terms moved to the right-hand side, each followed by a
+ * line search on the true residual) at the adaptive precision
+ * min(1e-4, 0.001 res) >= Precision (harmonic2d.cpp:821-825).
  * The reference itself rejects LamType 1/2 in AC analyses; wound regions
- * with proximity effects (LamType > 2) and the Newton AC solver (ACSolver 1)
- * return XFK_ERR_UNSUPPORTED.  Single device.
+ * with proximity effects (LamType > 2) return XFK_ERR_UNSUPPORTED.  Single
+ * device.
  * ------------------------------------------------------------------------- */
 typedef struct {
     double J_im;                /* imaginary part of the source current density, MA/m^2 */
@@ -280,6 +289,7 @@ typedef struct {
     const xfk_block_ac_desc *blocks;
     const xfk_line_ac_desc *lines;      /* may be NULL when n_lines == 0 */
     const xfk_circuit_ac_desc *circs;   /* may be NULL when n_circs == 0 */
+    int ac_solver;              /* [ACSolver]: 0 successive approximation, 1 Newton */
 } xfk_harmonic_desc;
 
 int xfk_problem_create_harmonic(const xfk_problem_desc *desc, const xfk_harmonic_desc *ac, int device,

@@ -610,6 +610,8 @@ static int lp_kludgesolve(clp *L, int flag)
                 v[i] = L->V[i];
             }
             er = lp_nrm(r, n) / normb;
+            if (getenv("ORACLE_TRACE_NONLINEAR"))
+                fprintf(stderr, "  kludge %d: c %.6e er %.6e (cocg %lld)\n", k, cstep, er, (long long)g_iters);
             if (er < L->precision * 10.) break;
         }
     }
@@ -1393,6 +1395,7 @@ int orh_harmonic2d(orh_problem *pr, const orh_linprob_ops *ops, double *A_out, o
                 lastres = res;
                 res = sqrt(x / y);
             }
+            if (getenv("ORACLE_TRACE_NONLINEAR")) fprintf(stderr, "pass %d: res %.6e relax %.4f\n", Iter, res, Relax);
             if (Iter > 5) {
                 if ((res > lastres) && (Relax > 0.1)) Relax /= 2.;
                 else Relax += 0.1 * (1. - Relax);

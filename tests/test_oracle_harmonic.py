@@ -56,6 +56,8 @@ def _newton_case(kind):
         kw = synth.harmonic(14, nonlinear=True, periodic=True)
     elif kind == "hf":
         kw = synth.harmonic(14, nonlinear=True, frequency=5000.0)
+    elif kind == "stiff":   # KludgeSolve stagnates (line-search step -> 0): the reference's path, bit for bit
+        kw = synth.harmonic(24, nonlinear=True)
     else:
         kw = synth.harmonic(14, nonlinear=True)
     kw["ac_solver"] = 1
@@ -63,7 +65,7 @@ def _newton_case(kind):
 
 
 @pytest.mark.skipif(not oracle.ref_available(), reason="reference build (oracle/_ref) absent")
-@pytest.mark.parametrize("kind", ["planar", "periodic", "hf", "axi", "axi_ext"])
+@pytest.mark.parametrize("kind", ["planar", "periodic", "hf", "stiff", "axi", "axi_ext"])
 def test_newton_ac_solver_is_bit_identical_to_reference(kind):
     """[ACSolver] = 1: the element Newton terms (harmonic2d.cpp:611-639 /
     harmonicaxi.cpp:520-547) into the auxiliary matrices and KludgeSolve

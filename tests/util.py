@@ -31,7 +31,7 @@ def kernel_kwargs(pr: femfile.FemProblem, mesh: femfile.Mesh) -> dict:
                 pbc=mesh.pbc if len(mesh.pbc) else None, blocks=blocks, labels=labels, lines=lines,
                 points=points, circuits=circuits, precision=pr.Precision, length_units=pr.LengthUnits,
                 coords=pr.Coords, relax=pr.Relax, frequency=pr.Frequency, problem_type=pr.ProblemType,
-                ext_zo=pr.extZo, ext_ro=pr.extRo, ext_ri=pr.extRi, ages=list(mesh.ages))
+                ext_zo=pr.extZo, ext_ro=pr.extRo, ext_ri=pr.extRi, ages=list(mesh.ages), ac_solver=pr.ACSolver)
 
 
 def synth_to_oracle(kw: dict):

@@ -522,18 +522,11 @@ int FSolver::Harmonic2D()
     DescStore ds;
     if (!make_desc(ds)) return false;
     std::vector<xfk_block_ac_desc> bac(blockproplist.size());
-    bool nonlinear = false;
     for (size_t k = 0; k < blockproplist.size(); k++) {
         const CMSolverMaterialProp &m = blockproplist[k];
         const bool bh = m.BHpoints > 0;
-        nonlinear = nonlinear || bh;
         bac[k] = xfk_block_ac_desc{m.J_im, m.Theta_hx, m.Theta_hy, m.Lam_d, bh ? m.Hdata_im.data() : nullptr,
                                    bh ? m.slope_im.data() : nullptr};
-    }
-    if (nonlinear && ACSolver == 1) {
-        warn("the Newton AC solver ([ACSolver] = 1) is not supported by this solver build; "
-             "use successive approximation ([ACSolver] = 0)\n");
-        return false;
     }
     std::vector<xfk_line_ac_desc> lac(lineproplist.size());
     for (size_t k = 0; k < lineproplist.size(); k++) {
@@ -544,7 +537,7 @@ int FSolver::Harmonic2D()
     for (size_t k = 0; k < circproplist.size(); k++)
         cac[k] = xfk_circuit_ac_desc{circproplist[k].Amps_im, circproplist[k].dVolts_im};
     xfk_harmonic_desc ac{Frequency, bac.data(), lac.empty() ? nullptr : lac.data(),
-                         cac.empty() ? nullptr : cac.data()};
+                         cac.empty() ? nullptr : cac.data(), ACSolver};
     xfk_problem *prob = nullptr;
     int rc = xfk_problem_create_harmonic(&ds.d, &ac, device, &prob);
     if (rc == XFK_OK) rc = xfk_harmonic2d(prob, 0, &stats);

@@ -41,6 +41,8 @@ static inline long long ukey(int r, int c)
     return ((long long)r << 32) | (unsigned)c;
 }
 
+static inline long long okey(int r, int c) { return ((long long)r << 32) | (unsigned)c; }
+
 static Terms lin2(double a, const Terms &x, double b, const Terms &y)
 {
     std::map<long long, double> m;
@@ -101,6 +103,16 @@ static int build_pbc_map(xfk_problem *P)
         if (is_orig(r, c)) return Terms{{k, 1.0}};
         return Terms{};
     };
+    // auxiliary matrices of the Newton AC solver: ordered entries
+    std::unordered_map<long long, Terms> Ea;
+    std::set<long long> afill;
+    auto geta = [&](int r, int c) -> Terms {
+        long long k = okey(r, c);
+        auto it = Ea.find(k);
+        if (it != Ea.end()) return it->second;
+        if (is_orig(r, c)) return Terms{{k, 1.0}};
+        return Terms{};
+    };
     auto getb = [&](int i) -> Terms {
         auto it = Eb.find(i);
         if (it != Eb.end()) return it->second;
@@ -125,6 +137,13 @@ static int build_pbc_map(xfk_problem *P)
             Terms c = lin2(0.5, v1, 0.5 * sg, v2);
             E[ukey(k, i)] = c;
             E[ukey(k, j)] = (sg > 0) ? c : lin2(-1.0, c, 0.0, Terms{});
+            // row k and, by the Hermitian / anti-Hermitian flip of Put, column k
+            Terms ca = lin2(0.5, geta(k, i), 0.5 * sg, geta(k, j));
+            Terms ct = lin2(0.5, geta(i, k), 0.5 * sg, geta(j, k));
+            Ea[okey(k, i)] = ca;
+            Ea[okey(k, j)] = lin2(sg, ca, 0.0, Terms{});
+            Ea[okey(i, k)] = ct;
+            Ea[okey(j, k)] = lin2(sg, ct, 0.0, Terms{});
             for (int m : {i, j})
                 if (!is_orig(k, m)) fill.insert(ukey(k, m));
             Ncur[i].insert(k);
@@ -138,6 +157,13 @@ static int build_pbc_map(xfk_problem *P)
         Terms d = lin2(0.5, get(i, i), 0.5, get(j, j));
         E[ukey(i, i)] = d;
         E[ukey(j, j)] = d;
+        // auxiliary (i, j) block: c = (ii +- ij +- ji + jj) / 4 at ii, jj and +-c at ij, ji
+        Terms da = lin2(0.25, lin2(1.0, geta(i, i), sg, geta(i, j)), 0.25, lin2(sg, geta(j, i), 1.0, geta(j, j)));
+        Ea[okey(i, i)] = da;
+        Ea[okey(j, j)] = da;
+        Ea[okey(i, j)] = lin2(sg, da, 0.0, Terms{});
+        Ea[okey(j, i)] = lin2(sg, da, 0.0, Terms{});
+        if (!is_orig(i, j) && !fill.count(ukey(i, j))) afill.insert(ukey(i, j));
         Terms bi = getb(i), bj = getb(j);
         Terms c = lin2(0.5, bi, 0.5 * sg, bj);
         Eb[i] = c;
@@ -153,6 +179,18 @@ static int build_pbc_map(xfk_problem *P)
         P->pbc_entry_key.push_back(k);
         P->pbc_entry_terms.push_back(E[k]);
     }
+    P->pbca_entry_key.clear();
+    P->pbca_entry_terms.clear();
+    keys.clear();
+    for (auto &kv : Ea) keys.push_back(kv.first);
+    std::sort(keys.begin(), keys.end());
+    for (long long k : keys) {
+        P->pbca_entry_key.push_back(k);
+        P->pbca_entry_terms.push_back(Ea[k]);
+    }
+    P->pbca_fill.clear();
+    for (long long k : afill)
+        if (!fill.count(k)) P->pbca_fill.push_back(k);
     P->pbc_b_key.clear();
     P->pbc_b_terms.clear();
     std::vector<int> bk;
@@ -269,7 +307,10 @@ int build_symbolic(xfk_problem *P)
     hipStream_t s = P->stream;
     const int N = P->N, NL = P->NL, NE = P->NE;   // owned rows, local nodes, local elements
     SymTmp T;
-    const int nfill = 2 * (int)P->pbc_fill.size();
+    // periodic fill-in (+ the auxiliary matrices' (i, j) entries of the Newton AC solver)
+    std::vector<long long> fillv = P->pbc_fill;
+    if (P->harmonic && P->ac_solver == 1) fillv.insert(fillv.end(), P->pbca_fill.begin(), P->pbca_fill.end());
+    const int nfill = 2 * (int)fillv.size();
     T.carve(nullptr, NL, NE, nfill);
     XFK_CHECK(P->sym_tmp.alloc(T.bytes));
     T.carve(P->sym_tmp.p, NL, NE, nfill);
@@ -285,9 +326,9 @@ int build_symbolic(xfk_problem *P)
 
     // periodic fill-in entries, CSR by row
     const int *fp = nullptr, *fc = nullptr;
-    if (!P->pbc_fill.empty()) {
+    if (!fillv.empty()) {
         std::vector<std::vector<int>> rows(N);
-        for (long long k : P->pbc_fill) {
+        for (long long k : fillv) {
             int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
             rows[r].push_back(c);
             rows[c].push_back(r);
@@ -467,6 +508,41 @@ int build_symbolic(xfk_problem *P)
         XFK_CHECK(P->pb_tmp.alloc(bd.size()));
         XFK_CHECK(hipStreamSynchronize(s));
         P->pb_n = (int)bd.size();
+    }
+
+    // the auxiliary matrices' map (Newton AC solver): ordered entries, one gather per slot
+    P->pa_n = 0;
+    if (P->harmonic && P->ac_solver == 1 && !P->pbca_entry_key.empty()) {
+        std::vector<int> rc_dst, src_rc, ptr{0};
+        std::vector<double> w;
+        for (size_t m = 0; m < P->pbca_entry_key.size(); ++m) {
+            const long long k = P->pbca_entry_key[m];
+            rc_dst.push_back((int)(k >> 32));
+            rc_dst.push_back((int)(k & 0xffffffff));
+            for (auto &t : P->pbca_entry_terms[m]) {
+                src_rc.push_back((int)(t.first >> 32));
+                src_rc.push_back((int)(t.first & 0xffffffff));
+                w.push_back(t.second);
+            }
+            ptr.push_back((int)w.size());
+        }
+        const int nd = (int)rc_dst.size() / 2, ns = (int)w.size();
+        DBuf<int> d_rc, s_rc;
+        XFK_CHECK(upload(d_rc, rc_dst.data(), rc_dst.size(), s));
+        XFK_CHECK(upload(s_rc, src_rc.data(), src_rc.size(), s));
+        XFK_CHECK(P->pa_dst.alloc(nd));
+        XFK_CHECK(P->pa_src.alloc(ns ? ns : 1));
+        launch_lookup_slots(s, nd, d_rc.p, P->rowptr.p, P->col.p, P->pa_dst.p);
+        launch_lookup_slots(s, ns, s_rc.p, P->rowptr.p, P->col.p, P->pa_src.p);
+        XFK_CHECK(upload(P->pa_ptr, ptr.data(), ptr.size(), s));
+        XFK_CHECK(upload(P->pa_w, w.data(), w.size(), s));
+        XFK_CHECK(P->pa_tmp.alloc(nd));
+        std::vector<int> chk(nd), chk2(ns);
+        XFK_CHECK(d2h(chk.data(), P->pa_dst.p, sizeof(int) * nd, s));
+        if (ns) XFK_CHECK(d2h(chk2.data(), P->pa_src.p, sizeof(int) * ns, s));
+        for (int v : chk) XFK_REQUIRE(v >= 0, XFK_ERR_HIP, "internal: auxiliary periodic map slot missing");
+        for (int v : chk2) XFK_REQUIRE(v >= 0, XFK_ERR_HIP, "internal: auxiliary periodic map source slot missing");
+        P->pa_n = nd;
     }
 
     // vectors and reduction scratch

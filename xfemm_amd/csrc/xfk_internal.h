@@ -264,6 +264,16 @@ struct xfk_problem {
     std::vector<long long> pbc_entry_key;
     std::vector<std::vector<std::pair<int, double>>> pbc_b_terms;
     std::vector<int> pbc_b_key;
+    // the same composition for the Newton AC solver's auxiliary matrices
+    // (cspars.cpp:648-670, 732-754): ordered (row, col) entries -- they are
+    // Hermitian / anti-Hermitian, not symmetric -- whose (i, j) block of each
+    // pair is the mean of its four entries; the entries (i, j) it creates
+    std::vector<std::vector<std::pair<long long, double>>> pbca_entry_terms;
+    std::vector<long long> pbca_entry_key;
+    std::vector<long long> pbca_fill;
+    xfk::DBuf<int> pa_dst, pa_ptr, pa_src;
+    xfk::DBuf<double> pa_w, pa_tmp;
+    int pa_n = 0;
 
     // numeric: V (the PCG iterate x) and U (= M^-1 r) span the NL local
     // nodes, their halo slices filled by exchanges; the rest span N rows
@@ -324,6 +334,12 @@ struct xfk_problem {
     std::vector<double2> hc2_u_old;
     xfk::DBuf<double> hc2_C;                     // border columns, per unknown N re then N im
     xfk::DBuf<double2> hc2_Y, hc2_y0;            // A^-1 C_k and A^-1 b
+    // Newton AC solver (ac_solver == 1): Mh, Ms, Ma over the CSR pattern as
+    // six arrays of nnz (re, im of each), the KludgeSolve vectors
+    int ac_solver = 0;
+    xfk::DBuf<double> haux;
+    xfk::DBuf<double2> hk_vec;                   // borig, v, r, P(dir), U (N each)
+    xfk::DBuf<double> hk_b;                      // b' split: re, im (N each)
     xfk::DBuf<double> hc_part;                   // per-block partials, 9 arrays
     xfk::DBuf<xfk::CcgState> hc_state;
     xfk::CcgState *hc_host = nullptr;            // pinned mirror

@@ -289,8 +289,9 @@ class Static2DProblem:
                  amg_theta: Optional[float] = None, frequency: float = 0.0, amg_omega: Optional[float] = None,
                  amg_replicate: Optional[int] = None, amg_reuse: Optional[bool] = None, problem_type: int = 0,
                  ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0, amg_dense: Optional[int] = None,
-                 ages: Sequence[dict] = ()):
-        """comm: shard the mesh by row blocks over this communicator (every rank
+                 ages: Sequence[dict] = (), ac_solver: int = 0):
+        """ac_solver: [ACSolver], read by the harmonic solvers only (ignored here).
+        comm: shard the mesh by row blocks over this communicator (every rank
         passes the same global problem; solve() and solution() are collective).
         precond: "amg" (smoothed-aggregation V-cycle, default) or "jacobi".
         problem_type: XFK_PLANAR (Static2D) or XFK_AXISYMMETRIC
@@ -400,7 +401,7 @@ class CircuitAcDesc(C.Structure):
 
 class HarmonicDesc(C.Structure):
     _fields_ = [("frequency", C.c_double), ("blocks", C.POINTER(BlockAcDesc)), ("lines", C.POINTER(LineAcDesc)),
-                ("circs", C.POINTER(CircuitAcDesc))]
+                ("circs", C.POINTER(CircuitAcDesc)), ("ac_solver", C.c_int)]
 
 
 class Harmonic2DProblem:
@@ -413,10 +414,11 @@ class Harmonic2DProblem:
                  lines: Sequence[dict] = (), points: Sequence[dict] = (), circuits: Sequence[dict] = (),
                  marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0, device=0,
                  problem_type: int = 0, ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0,
-                 precond: str = "amg", ages: Sequence[dict] = ()):
+                 precond: str = "amg", ages: Sequence[dict] = (), ac_solver: int = 0):
         """precond: "amg" (V-cycle of the real SPD surrogate Re A +- Im A, the
         sign making Im A positive semi-definite, applied to the real and
-        imaginary parts; default) or "jacobi" (complex Jacobi)."""
+        imaginary parts; default) or "jacobi" (complex Jacobi).  ac_solver:
+        [ACSolver], 0 successive approximation, 1 Newton (KludgeSolve)."""
         L = load_library()
         D, keep = _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision,
                              length_units, coords, relax, problem_type, (ext_zo, ext_ro, ext_ri), ages)
@@ -434,7 +436,7 @@ class Harmonic2DProblem:
         ca = (CircuitAcDesc * max(1, len(circuits)))()
         for k, q in enumerate(circuits):
             ca[k].amps_im, ca[k].dvolts_im = q.get("amps_im", 0.0), q.get("dvolts_im", 0.0)
-        H = HarmonicDesc(frequency, ba, la, ca)
+        H = HarmonicDesc(frequency, ba, la, ca, int(ac_solver))
         keep.extend([ba, la, ca])
         self._keep = keep
         self.n_nodes = D.n_nodes
