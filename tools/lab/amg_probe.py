@@ -1,12 +1,12 @@
 """GPU probe: Jacobi vs AMG PCG on synthetic magnetostatic problems (iterations,
-timings, hierarchy, agreement).  Usage: python tools/amg_probe.py [cells ...]"""
+timings, hierarchy, agreement).  Usage: python tools/lab/amg_probe.py [cells ...]"""
 import os
 import sys
 import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from xfemm_amd import kernels, synth  # noqa: E402
 

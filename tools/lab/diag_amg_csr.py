@@ -1,6 +1,6 @@
 """Diagnostic: AMG-PCG vs direct solve on assembled oracle systems (true residual)."""
 import os, sys
-R = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+R = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path.insert(0, R); sys.path.insert(0, os.path.join(R, "tests"))
 import numpy as np
 import scipy.sparse.linalg as sla

@@ -1,5 +1,5 @@
 # Full GPU pass: gpu tests, default bench (with CPU baseline), rocprof trace + PMC passes.
-# Usage: bash tools/gpu_full.sh TAG
+# Usage: bash tools/lab/gpu_full.sh TAG
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 TAG=${1:-r01}

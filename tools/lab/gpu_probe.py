@@ -1,5 +1,5 @@
 """Quick GPU probe: HIP path vs oracle on the golden problems + synthetic ones.
-Run on the GPU box:  python tools/gpu_probe.py"""
+Run on the GPU box:  python tools/lab/gpu_probe.py"""
 import os
 import sys
 import time
@@ -7,7 +7,7 @@ import time
 import numpy as np
 import scipy.sparse as sp
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 

@@ -1,6 +1,6 @@
 """In-process sharded solve (N ranks on one GPU) vs single device: iterations, agreement."""
 import os, sys, threading, time
-R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, R)
 import numpy as np
 from xfemm_amd import kernels, synth

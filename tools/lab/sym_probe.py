@@ -1,7 +1,7 @@
 """Symbolic-phase timing probe: rebuild the 2M-tri problem's symbolic data a
-few times (tools/timeline.py reads the kernel trace of this under rocprofv3)."""
+few times (tools/lab/timeline.py reads the kernel trace of this under rocprofv3)."""
 import os, sys, time
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from xfemm_amd import kernels, synth
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1000

@@ -1,7 +1,7 @@
 """Print the kernel timeline (duration, gap to the previous kernel) of the
 k-th occurrence of a phase in a rocprofv3 kernel-trace CSV.
 
-usage: python tools/timeline.py TRACE.csv START_KERNEL END_KERNEL [OCCURRENCE]
+usage: python tools/lab/timeline.py TRACE.csv START_KERNEL END_KERNEL [OCCURRENCE]
 """
 import csv, sys
 
