@@ -585,10 +585,26 @@ def get_slopes(m: BlockProp) -> None:
 # FSolver::LoadProblemFile post-processing (fsolver.cpp:202-348)
 # --------------------------------------------------------------------------
 
+class PrevSolnError(ValueError):
+    """A previous-solution problem the reference refuses, or on which its
+    behaviour is undefined (message says which)."""
+
+
 def prepare_problem(pr: FemProblem) -> FemProblem:
     pr.Relax = 1.0
     if pr.PrevSoln:
-        raise NotImplementedError("previous-solution (incremental) problems are out of scope")
+        # fsolver.cpp:224-238: with a previous solution LoadProblemFile returns
+        # right after loadPreviousSolution, before the B-H precomputation
+        # (GetSlopes) and the serial-circuit expansion.  A B-H block then has
+        # no slopes (Get_v / GetdHdB index empty vectors) and a serial circuit
+        # keeps CircType 1: undefined in the reference, refused here.
+        if any(m.BHpoints > 0 for m in pr.blocks):
+            raise PrevSolnError("B-H curves with a previous solution: the reference never computes their "
+                                "slopes (fsolver.cpp:224-238)")
+        if any(c.CircType == 1 for c in pr.circuits):
+            raise PrevSolnError("serial circuits with a previous solution: the reference skips their "
+                                "expansion (fsolver.cpp:224-238)")
+        return pr
     for m in pr.blocks:
         if m.BHpoints > 0:
             get_slopes(m)
@@ -907,11 +923,118 @@ def read_ans(path: str) -> AnsSolution:
                        lbl=ele[:, 3].astype(np.int32), circ=circ, pbc=pbc, ages=ages)
 
 
-def load_problem(base: str, renumber: bool = True):
-    """Convenience: parse + prepare + mesh (+ Cuthill) like FSolver::runSolver."""
+@dataclass
+class PrevSolution:
+    """What FSolver::loadPreviousSolution keeps: the mesh and, for PrevType != 0,
+    A of the previous (DC) solution per node; Jprev per element."""
+    mesh: Mesh
+    Aprev: Optional[np.ndarray]
+    Jprev: np.ndarray
+
+
+def _scan(fields, conv):
+    """sscanf over whitespace fields with the given converters: the values up
+    to the first field that is missing or does not convert."""
+    out = []
+    for f, c in zip(fields, conv):
+        try:
+            out.append(c(f))
+        except ValueError:
+            break
+    return out
+
+
+def _c_int(tok: str) -> int:
+    """%i of sscanf: the leading integer of the token ("-10.5" -> -10)."""
+    import re
+    m = re.match(r"[+-]?(0[xX][0-9a-fA-F]+|0[0-7]*|[1-9][0-9]*)", tok)
+    if not m:
+        raise ValueError(tok)
+    return int(m.group(0), 0)
+
+
+def load_previous_solution(pr: FemProblem, path: str, load_aprev: bool) -> PrevSolution:
+    """FSolver::loadPreviousSolution (fsolver.cpp:990-1081) with
+    LoadMeshNodesFromSolution (:801-840), LoadMeshElementsFromSolution
+    (:842-880), LoadPBCFromSolution (:882-909), LoadAGEsFromSolution (:911-988).
+
+    Reproduced as the reference reads a WriteStatic2D .ans: element lines
+    carry p0 p1 p2 lbl only, so the sscanf of 8 fields leaves e[] and Jprev at
+    the CMElement defaults -- e = {0, 0, 0} (CElement.cpp:30-39): EVERY edge of
+    every element carries boundary property 0 -- and Jprev = 0.  Node
+    coordinates come back through x / unitconv * 100 LengthConvMeters."""
+    if not os.path.exists(path):
+        raise PrevSolnError("Failed to open the specified previous solution file, file path was:\n%s\n" % path)
+    with open(path, "r") as fh:
+        lines = fh.read().split("\n")
+    i, has = 0, False
+    while i < len(lines):
+        toks = lines[i].split()
+        q = toks[0].lower() if toks else ""
+        if q.startswith("[frequency]"):
+            v = lines[i].split("=", 1)[1] if "=" in lines[i] else ""
+            f = _scan(v.split(), [float])
+            if f and f[0] != 0:
+                raise PrevSolnError("Previous solution file (%s) appears to be an AC problem, only DC previous "
+                                    "solutions are presently supported\n" % path)
+        i += 1
+        if q.startswith("[solution]"):
+            has = True
+            break
+    if not has:
+        raise PrevSolnError("No solution was found in previous solution file, file path was:\n%s\n" % path)
+    conv = 100.0 * LENGTH_CONV_METERS[pr.LengthUnits]
+    nn = _c_int(lines[i].split()[0]); i += 1
+    x, y, A, mk = np.zeros(nn), np.zeros(nn), np.zeros(nn), np.zeros(nn, np.int32)
+    for j in range(nn):
+        v = _scan(lines[i + j].split(), [float, float, float, _c_int])
+        x[j], y[j], A[j], mk[j] = v[0] * conv, v[1] * conv, v[2], v[3]
+    i += nn
+    ne = _c_int(lines[i].split()[0]); i += 1
+    p = np.zeros((ne, 3), np.int32)
+    lbl = np.zeros(ne, np.int32)
+    e = np.zeros((ne, 3), np.int32)      # CElement() default, not -1
+    Jprev = np.zeros(ne)
+    for j in range(ne):
+        v = _scan(lines[i + j].split(), [_c_int] * 7 + [float])
+        p[j], lbl[j] = v[0:3], v[3]
+        for q in range(3):
+            if len(v) > 4 + q:
+                e[j, q] = v[4 + q]
+        if len(v) > 7:
+            Jprev[j] = v[7]
+    i += ne
+    blk = np.array([pr.labels[l].BlockType for l in lbl], np.int32)
+    nlab = _c_int(lines[i].split()[0]); i += 1 + nlab      # block-label circuit lines: skipped
+    npbc = _c_int(lines[i].split()[0]) if i < len(lines) and lines[i].split() else 0
+    i += 1
+    pbc = np.zeros((npbc, 3), np.int32)
+    for j in range(npbc):
+        pbc[j] = _scan(lines[i + j].split(), [_c_int] * 3)
+    i += npbc
+    nage = _c_int(lines[i].split()[0]) if i < len(lines) and lines[i].split() else 0
+    ages, _ = _parse_age_blocks(lines, i + 1, nage)
+    mesh = Mesh(x=x, y=y, marker=mk, p=p, e=e, lbl=lbl, blk=blk, pbc=pbc, bandwidth=0, ages=ages)
+    return PrevSolution(mesh=mesh, Aprev=A if load_aprev else None, Jprev=Jprev)
+
+
+def load_problem(base: str, renumber: bool = True, with_prev: bool = False):
+    """Convenience: parse + prepare + mesh (+ Cuthill) like FSolver::runSolver.
+    With [PrevSoln] the mesh is the previous solution's (no Cuthill,
+    fsolver.cpp:1224); ``with_prev`` also returns the PrevSolution."""
     pr = prepare_problem(parse_fem(base + ".fem"))
-    mesh = load_mesh(base, pr)
-    if renumber:
-        cuthill(mesh)
+    prev = None
+    if pr.PrevSoln:
+        # FSolver::runSolver (fsolver.cpp:1245-1320)
+        if pr.Frequency == 0 and pr.PrevType != 0:
+            raise PrevSolnError("Cannot handle incremental permeability problems with frequency 0.\n")
+        if pr.Frequency != 0 and pr.ProblemType == 1:
+            raise PrevSolnError("Cannot handle harmonic axisymmetric incremental problems.\n")
+        prev = load_previous_solution(pr, pr.PrevSoln, pr.PrevType != 0)
+        mesh = prev.mesh
+    else:
+        mesh = load_mesh(base, pr)
+        if renumber:
+            cuthill(mesh)
     get_fill_factor(pr)
-    return pr, mesh
+    return (pr, mesh, prev) if with_prev else (pr, mesh)

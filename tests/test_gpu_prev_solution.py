@@ -1,0 +1,135 @@
+"""Previous-solution problems ([PrevSoln] / [PrevType]) through FSolver on the
+GPU (libxfemm_fsolver.so), against the oracle's restatement of
+fsolver.cpp:202-238, 801-1081, 1224-1320 (tests/test_prev_solution.py).
+
+  * TorqueBenchmark, PrevType 0: the GPU's own .ans as [PrevSoln].  The mesh,
+    periodic pairs and air gap come back from the .ans, every element edge
+    carries boundary property 0 ("pbc1", inert): the re-solve equals the first
+    solve and the converged oracle on the same mesh (<= 1e-6), and passes the
+    reference's torque check.
+  * Harmonic planar, PrevType 1 (incremental; linear blocks -- on B-H blocks
+    the reference reads uncomputed slopes and is refused): the DC .ans of the
+    same mesh as [PrevSoln]; the mixed boundary property 0 then applies to
+    every element edge, as in the reference.  A vs the converged harmonic
+    oracle on that mesh (<= 1e-6); the .ans carries the Aprev column (the DC
+    A) and the Jprev column (0: a WriteStatic2D .ans has none).
+  * The reference's refusals, through the C++ host.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import ansfile
+from oracle import femfile, gaptorque, oracle
+from oracle import harmonic as oh
+from torque import torque_ok, write_case
+from util import converged, parity_message, rel_err
+from xfemm_amd import fsolver, synth
+
+pytestmark = pytest.mark.gpu
+
+TOL_A = 1e-6
+
+
+def _run(base, ok=True):
+    fs = fsolver.FSolver(delete_mesh_files=False)
+    fs.PathName = base
+    good = fs.LoadProblemFile() and fs.runSolver(False)
+    assert good == ok, fs.last_error()
+    return fs
+
+
+def _ans_columns(path):
+    lines = open(path).read().splitlines()
+    k = lines.index("[Solution]") + 1
+    n = int(lines[k])
+    nodes = [ln.split("\t") for ln in lines[k + 1:k + 1 + n]]
+    ne = int(lines[k + 1 + n])
+    els = [ln.split("\t") for ln in lines[k + 2 + n:k + 2 + n + ne]]
+    return nodes, els
+
+
+def test_prev_torque_benchmark_resolve(tmp_path):
+    deg = 40
+    base = write_case(tmp_path, deg)
+    _run(base)
+    first = femfile.read_ans(base + ".ans")
+    base2 = str(tmp_path / "again")
+    with open(base2 + ".fem", "w") as fh:
+        fh.write(ansfile.with_prev(open(base + ".fem").read(), base + ".ans", 0))
+    pr2, mesh2 = femfile.load_problem(base2)
+    assert (mesh2.e == 0).all()
+    _run(base2)
+    again = femfile.read_ans(base2 + ".ans")
+    assert np.array_equal(again.p, first.p) and np.array_equal(again.x, first.x)
+    assert rel_err(again.A, first.A) <= 1e-12
+    Ao, _, _ = oracle.solve(pr2, mesh2)
+    Ac = converged(pr2, mesh2)
+    assert rel_err(again.A, Ac) <= TOL_A, parity_message(again.A, Ao, Ac, TOL_A)
+    tq = gaptorque.gap_dc_torque(again.ages[0], again.A, pr2.Depth, pr2.LengthUnits)
+    assert torque_ok(tq, deg)[0], tq
+
+
+def _harmonic_kw():
+    kw = synth.harmonic(16, circuits=False)
+    # boundary property 0 is the mixed one (it lands on every edge of a
+    # previous-solution mesh); the others keep their roles
+    order = [1, 0, 2, 3]
+    kw["lines"] = [kw["lines"][k] for k in order]
+    inv = {old: new for new, old in enumerate(order)}
+    e = kw["e"].copy()
+    for old, new in inv.items():
+        e[kw["e"] == old] = new
+    kw["e"] = e
+    kw["marker"] = None
+    kw["points"] = []
+    return kw
+
+
+def test_prev_harmonic_incremental_linear(tmp_path):
+    kw = _harmonic_kw()
+    dc = str(tmp_path / "dc")
+    synth.write_problem(dc, dict(kw, frequency=0.0))
+    _run(dc)
+    dc_ans = femfile.read_ans(dc + ".ans")
+    ac = str(tmp_path / "ac")
+    synth.write_problem(ac, kw)
+    with open(ac + ".fem") as fh:
+        text = fh.read()
+    with open(ac + ".fem", "w") as fh:
+        fh.write(ansfile.with_prev(text, dc + ".ans", 1))
+    pr, mesh, prev = femfile.load_problem(ac, with_prev=True)
+    assert prev.Aprev is not None and (mesh.e == 0).all()
+    _run(ac)
+    nodes, els = _ans_columns(ac + ".ans")
+    A = np.array([float(r[2]) + 1j * float(r[3]) for r in nodes])
+    Aprev = np.array([float(r[5]) for r in nodes])
+    Jprev = np.array([float(r[7]) for r in els])
+    assert np.array_equal(Aprev, dc_ans.A) and not Jprev.any()
+    Ao, _, _ = oh.solve(pr, mesh)
+    Ac = converged(pr, mesh, oh.solve)
+    assert rel_err(A, Ac) <= TOL_A, parity_message(A, Ao, Ac, TOL_A)
+
+
+def test_prev_refusals_through_fsolver(tmp_path):
+    base = write_case(tmp_path, 0)
+    _run(base)
+    text = open(base + ".fem").read()
+    b2 = str(tmp_path / "r")
+    for txt, msg in [(ansfile.with_prev(text, base + ".ans", 1), "incremental permeability problems with frequency 0"),
+                     (ansfile.with_prev(text, base + ".missing", 0), "Failed to open")]:
+        with open(b2 + ".fem", "w") as fh:
+            fh.write(txt)
+        fs = _run(b2, ok=False)
+        assert msg in fs.last_error()
+    # a nonlinear block with a previous solution (slopes never computed by the reference)
+    kw = synth.harmonic(8, circuits=False, nonlinear=True)
+    h = str(tmp_path / "hn")
+    synth.write_problem(h, kw)
+    with open(h + ".fem") as fh:
+        t = fh.read()
+    with open(h + ".fem", "w") as fh:
+        fh.write(ansfile.with_prev(t, base + ".ans", 1))
+    fs = _run(h, ok=False)
+    assert "slopes" in fs.last_error()

@@ -100,6 +100,7 @@ struct CMElement {
     int p[3] = {0, 0, 0};
     int e[3] = {-1, -1, -1};
     int blk = 0, lbl = 0;
+    double Jprev = 0;   // previous-solution problems: the element's J column of the .ans
 };
 
 struct CCommonPoint {

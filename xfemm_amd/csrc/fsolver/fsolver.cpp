@@ -1,6 +1,7 @@
 // FSolver host logic over the MI355X kernels (see fsolver.h).
 #include "fsolver.h"
 
+#include <cctype>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -53,9 +54,26 @@ bool FSolver::LoadProblemFile()
         warn(err);
         return false;
     }
+    meshLoadedFromPrevSolution = false;
     if (!previousSolutionFile.empty()) {
-        warn("previous-solution (incremental/frozen permeability) problems are not supported by this solver build\n");
-        return false;
+        // fsolver.cpp:224-238: the mesh (and A, for PrevType != 0) come from
+        // the previous solution, and LoadProblemFile returns right there --
+        // before GetSlopes and the serial-circuit expansion below.  On a B-H
+        // block or a serial circuit the reference then runs on uncomputed
+        // slopes / an unexpanded circuit (undefined); refused here.
+        for (auto &prop : blockproplist)
+            if (prop.BHpoints > 0) {
+                warn("B-H curves with a previous solution: the reference never computes their slopes "
+                     "(fsolver.cpp:224-238)\n");
+                return false;
+            }
+        for (auto &c : circproplist)
+            if (c.CircType == 1) {
+                warn("serial circuits with a previous solution: the reference skips their expansion "
+                     "(fsolver.cpp:224-238)\n");
+                return false;
+            }
+        return loadPreviousSolution(PrevType != 0);
     }
     // B-H curves: GetSlopes(Frequency * 2 pi) (fsolver.cpp:241-276; the
     // harmonic curve is complex: effective sinusoidal-H amplitude, hysteresis
@@ -97,8 +115,139 @@ bool FSolver::LoadProblemFile()
     return true;
 }
 
+// FSolver::loadPreviousSolution (fsolver.cpp:990-1081) and its readers
+// (:801-988).  A WriteStatic2D .ans has p0 p1 p2 lbl per element, so the
+// 8-field scan leaves e[] and Jprev at the CMElement defaults of the
+// reference -- e = {0, 0, 0} (CElement.cpp:30-39): every edge carries boundary
+// property 0 -- and Jprev = 0.
+bool FSolver::loadPreviousSolution(bool loadAprev)
+{
+    if (previousSolutionFile.empty()) return false;
+    FILE *fp = fopen(previousSolutionFile.c_str(), "rt");
+    if (!fp) {
+        warn("Failed to open the specified previous solution file, file path was:\n" + previousSolutionFile + "\n");
+        return false;
+    }
+    char s[1024];
+    bool hasSolution = false;
+    while (fgets(s, 1024, fp) != nullptr) {
+        char q[256] = {0};
+        sscanf(s, "%255s", q);
+        std::string key(q);
+        for (auto &ch : key) ch = (char)tolower((unsigned char)ch);
+        if (key.compare(0, 11, "[frequency]") == 0) {
+            double prevFreq = 0;
+            const char *v = strchr(s, '=');
+            if (v) sscanf(v + 1, "%lf", &prevFreq);
+            if (prevFreq != 0) {
+                fclose(fp);
+                warn("Previous solution file (" + previousSolutionFile +
+                     ") appears to be an AC problem, only DC previous solutions are presently supported\n");
+                return false;
+            }
+        }
+        if (key.compare(0, 10, "[solution]") == 0) {
+            hasSolution = true;
+            break;
+        }
+    }
+    if (!hasSolution) {
+        fclose(fp);
+        warn("No solution was found in previous solution file, file path was:\n" + previousSolutionFile + "\n");
+        return false;
+    }
+    auto fail = [&](const char *what) {
+        fclose(fp);
+        warn(std::string("malformed previous solution file (") + what + "): " + previousSolutionFile + "\n");
+        return false;
+    };
+    // nodes: x y A marker, lengths back to cm (fsolver.cpp:801-840)
+    if (!fgets(s, 1024, fp) || sscanf(s, "%i", &NumNodes) != 1 || NumNodes < 0) return fail("node count");
+    Aprev.clear();
+    meshnode.assign(NumNodes, CNode());
+    const double conv = 100 * kLengthConvMeters[LengthUnits];
+    for (int i = 0; i < NumNodes; i++) {
+        CNode node;
+        double a = 0;
+        if (!fgets(s, 1024, fp) || sscanf(s, "%lf %lf %lf %i", &node.x, &node.y, &a, &node.BoundaryMarker) < 3)
+            return fail("node line");
+        node.x *= conv;
+        node.y *= conv;
+        if (loadAprev) Aprev.push_back(a);
+        meshnode[i] = node;
+    }
+    // elements: p0 p1 p2 lbl [e0 e1 e2 Jprev] (fsolver.cpp:842-880)
+    if (!fgets(s, 1024, fp) || sscanf(s, "%i", &NumEls) != 1 || NumEls < 0) return fail("element count");
+    meshele.assign(NumEls, CMElement());
+    for (int i = 0; i < NumEls; i++) {
+        CMElement elm;
+        elm.e[0] = elm.e[1] = elm.e[2] = 0;
+        if (!fgets(s, 1024, fp) ||
+            sscanf(s, "%i %i %i %i %i %i %i %lf", &elm.p[0], &elm.p[1], &elm.p[2], &elm.lbl, &elm.e[0], &elm.e[1],
+                   &elm.e[2], &elm.Jprev) < 4)
+            return fail("element line");
+        if (elm.lbl < 0 || elm.lbl >= (int)labellist.size()) return fail("element label");
+        for (int q = 0; q < 3; q++)
+            if (elm.p[q] < 0 || elm.p[q] >= NumNodes) return fail("element node");
+        elm.blk = labellist[elm.lbl].BlockType;
+        meshele[i] = elm;
+    }
+    // block-label circuit lines: skipped
+    int numLabels = 0;
+    if (!fgets(s, 1024, fp) || sscanf(s, "%i", &numLabels) != 1) return fail("label count");
+    for (int i = 0; i < numLabels; i++)
+        if (!fgets(s, 1024, fp)) return fail("label line");
+    // periodic pairs (fsolver.cpp:882-909)
+    NumPBCs = 0;
+    pbclist.clear();
+    if (fgets(s, 1024, fp) != nullptr) {
+        sscanf(s, "%i", &NumPBCs);
+        for (int i = 0; i < NumPBCs; i++) {
+            CCommonPoint pbc;
+            if (!fgets(s, 1024, fp) || sscanf(s, "%i %i %i", &pbc.x, &pbc.y, &pbc.t) != 3) return fail("pbc line");
+            pbclist.push_back(pbc);
+        }
+    }
+    // air-gap elements (fsolver.cpp:911-988): name (80 characters), parameters, quadNodes
+    NumAirGapElems = 0;
+    agelist.clear();
+    if (fgets(s, 1024, fp) != nullptr) sscanf(s, "%i", &NumAirGapElems);
+    for (int i = 0; i < NumAirGapElems; i++) {
+        AirGap g;
+        if (!fgets(s, 80, fp)) return fail("air-gap name");
+        g.name = s;
+        if (!fgets(s, 1024, fp) ||
+            sscanf(s, "%i %lf %lf %lf %lf %lf %lf %lf %i %lf %lf", &g.format, &g.inner_angle, &g.outer_angle, &g.ri,
+                   &g.ro, &g.arc, &g.agc_re, &g.agc_im, &g.n_arc, &g.inner_shift, &g.outer_shift) != 11 ||
+            g.n_arc <= 0)
+            return fail("air-gap parameters");
+        for (int k = 0; k <= g.n_arc; k++) {
+            int n[4];
+            double w[4];
+            if (!fgets(s, 1024, fp) ||
+                sscanf(s, "%i %lf %i %lf %i %lf %i %lf", &n[0], &w[0], &n[1], &w[1], &n[2], &w[2], &n[3], &w[3]) != 8)
+                return fail("air-gap quadNode");
+            for (int m = 0; m < 4; m++) {
+                if (n[m] < 0 || n[m] >= NumNodes) {
+                    fclose(fp);
+                    warn("An error occured while reading pbc file, quadNode has negative node number.\n");
+                    return false;
+                }
+                g.qn.push_back(n[m]);
+                g.qw.push_back(w[m]);
+            }
+        }
+        agelist.push_back(g);
+    }
+    fclose(fp);
+    BandWidth = 0;
+    meshLoadedFromPrevSolution = true;
+    return true;
+}
+
 LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
 {
+    if (meshLoadedFromPrevSolution) return NOERROR;   // fsolver.cpp:357-360
     char s[1024];
     std::string infile = PathName + ".node";
     FILE *fp = fopen(infile.c_str(), "rt");
@@ -593,9 +742,13 @@ int FSolver::WriteStatic2D()
     fprintf(fp, "[Solution]\n");
     const double cf = unitconv[LengthUnits];
     fprintf(fp, "%i\n", NumNodes);
-    for (int i = 0; i < NumNodes; i++)
-        fprintf(fp, "%.17g\t%.17g\t%.17g\t%i\n", meshnode[i].x / cf, meshnode[i].y / cf, A[i],
+    for (int i = 0; i < NumNodes; i++) {
+        fprintf(fp, "%.17g\t%.17g\t%.17g\t%i", meshnode[i].x / cf, meshnode[i].y / cf, A[i],
                 meshnode[i].BoundaryMarker);
+        // static2d.cpp:1093-1101: Aprev follows the marker with no separator
+        if (!Aprev.empty()) fprintf(fp, "%.17g\n", Aprev[i]);
+        else fprintf(fp, "\n");
+    }
     fprintf(fp, "%i\n", NumEls);
     for (int i = 0; i < NumEls; i++)
         fprintf(fp, "%i\t%i\t%i\t%i\n", meshele[i].p[0], meshele[i].p[1], meshele[i].p[2], meshele[i].lbl);
@@ -656,13 +809,21 @@ int FSolver::WriteHarmonic2D()
     fprintf(fp, "[Solution]\n");
     const double cf = unitconv[LengthUnits];
     fprintf(fp, "%i\n", NumNodes);
-    for (int i = 0; i < NumNodes; i++)
-        fprintf(fp, "%.17g\t%.17g\t%.17g\t%.17g\t%i\n", meshnode[i].x / cf, meshnode[i].y / cf, A[i], A_im[i],
+    // incremental problems add A of the previous solution per node and J per
+    // element (harmonic2d.cpp:929-949)
+    for (int i = 0; i < NumNodes; i++) {
+        fprintf(fp, "%.17g\t%.17g\t%.17g\t%.17g\t%i", meshnode[i].x / cf, meshnode[i].y / cf, A[i], A_im[i],
                 meshnode[i].BoundaryMarker);
+        if (!Aprev.empty()) fprintf(fp, "\t%.17g\n", Aprev[i]);
+        else fprintf(fp, "\n");
+    }
     fprintf(fp, "%i\n", NumEls);
-    for (int i = 0; i < NumEls; i++)
-        fprintf(fp, "%i\t%i\t%i\t%i\t%i\t%i\t%i\n", meshele[i].p[0], meshele[i].p[1], meshele[i].p[2],
+    for (int i = 0; i < NumEls; i++) {
+        fprintf(fp, "%i\t%i\t%i\t%i\t%i\t%i\t%i", meshele[i].p[0], meshele[i].p[1], meshele[i].p[2],
                 meshele[i].lbl, meshele[i].e[0], meshele[i].e[1], meshele[i].e[2]);
+        if (!Aprev.empty()) fprintf(fp, "\t%.17g\n", meshele[i].Jprev);
+        else fprintf(fp, "\n");
+    }
     fprintf(fp, "%i\n", (int)labellist.size());
     for (size_t k = 0; k < labellist.size(); k++) {
         int i = labellist[k].InCircuit;
@@ -693,6 +854,18 @@ bool FSolver::runSolver(bool verbose)
             warn("problem renumbering node points\n");
             return false;
         }
+    }
+    if (!previousSolutionFile.empty()) {   // fsolver.cpp:1245-1320
+        if (Frequency == 0 && PrevType != 0) {
+            warn("Cannot handle incremental permeability problems with frequency 0.\n");
+            return false;
+        }
+        if (Frequency != 0 && ProblemTypeV == AXISYMMETRIC) {
+            warn("Cannot handle harmonic axisymmetric incremental problems.\n");
+            return false;
+        }
+        if (Frequency != 0)
+            warn("Harmonic planar incremental permeability problems are work in progress. RESULTS WON'T BE VALID!\n");
     }
     if (verbose) {
         PrintMessage("solving...\n");

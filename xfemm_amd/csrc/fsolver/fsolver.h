@@ -54,6 +54,7 @@ public:
     bool deleteMeshFiles = true;
 
     bool LoadProblemFile();                              // fsolver.cpp:202-348
+    bool loadPreviousSolution(bool loadAprev);           // fsolver.cpp:990-1081
     LoadMeshErr LoadMesh(bool deleteFiles = true);       // fsolver.cpp:350-718
     int Cuthill(bool deleteFiles = true);                // cuthill.cpp:88-390
     int SortElements();                                  // cuthill.cpp:39-86
@@ -69,6 +70,10 @@ public:
     // result of the last Static2D: A (= V*c) per node, in meshnode order;
     // Harmonic2D: A holds the real parts and A_im the imaginary parts
     std::vector<double> A, A_im;
+    // previous-solution problems ([PrevSoln]): A of the previous solution
+    // (PrevType != 0), and whether the mesh came from it (fsolver.h:149)
+    std::vector<double> Aprev;
+    bool meshLoadedFromPrevSolution = false;
     xfk_result stats{};
     std::string lastError;
 
