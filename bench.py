@@ -172,6 +172,7 @@ def main():
     ap.add_argument("--amg-omega", type=float, default=1.75, help="Jacobi weight factor (weight omega / rho)")
     ap.add_argument("--amg-dense", type=int, default=None, help="dense coarsest level of at most this many rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-phases", action="store_true", help="skip the per-phase table")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per SpMV launch from a PMC pass (profiles/), if measured")
     ap.add_argument("--mode", choices=["sharded", "replicas"], default="sharded",
@@ -248,6 +249,22 @@ def main():
     value = (1 if sharded else world) * n_dof * args.steps / elapsed
     pcg_iters = results[-1]["cg_iters"]
 
+    # per-phase table (outside the timed region): the AMG setup steps and every
+    # launch of one PCG iteration, HIP events on the solve stream
+    phases = None
+    if amg and not sharded and world == 1 and not args.no_phases:
+        iters = max(1, pcg_iters)
+        phases = []
+        for ph in P.phase_profile(iters=iters, setup=True):
+            setup = ph["name"].startswith("setup")
+            row = {"phase": ph["name"], "launches_per_%s" % ("setup" if setup else "iteration"):
+                   ph["calls"] if setup else ph["calls"] / iters, "us_per_launch": ph["us_per_call"]}
+            if ph["bytes_per_call"] > 0:
+                gbs = ph["bytes_per_call"] / (ph["us_per_call"] * 1e-6) / 1e9
+                row.update({"bytes_per_launch": ph["bytes_per_call"], "achieved_GBps": gbs,
+                            "frac": gbs / HBM_PEAK_GBS, "bound": "hbm"})
+            phases.append(row)
+
     same_mesh = None
     if sharded and world > 1 and not args.no_same_mesh_1gpu:
         # strong-scaling reference: rank 0 alone on the same mesh (after the timed region)
@@ -319,6 +336,15 @@ def main():
             "launches_sampled": sum(r["spmv_samples"] for r in results),
         },
     }
+    if phases is not None:
+        it_phases = [p for p in phases if "launches_per_iteration" in p]
+        out["roofline"]["phases"] = phases
+        out["roofline"]["phases_note"] = (
+            "xfk_phase_profile after the timed region: AMG setup rebuilt once, then %d PCG iterations; "
+            "us per launch from HIP events; algorithmic bytes per launch (matrix stream 12 B/nnz + 4 B/row, each "
+            "vector once); peak %g GB/s; one PCG iteration = %.1f us of phases" % (
+                max(1, pcg_iters), HBM_PEAK_GBS,
+                sum(p["us_per_launch"] * p["launches_per_iteration"] for p in it_phases)))
     if same_mesh is not None:
         out["config"]["same_mesh_1gpu"] = same_mesh
     if rank == 0 and world == 1 and not sharded and not args.nonlinear and not args.no_secondary:

@@ -334,6 +334,23 @@ int xfk_age_element_matrix(double ci, double co, double K, double Ki, double *MG
  * mean device time (ms) of the SpMV kernel and of one whole iteration. */
 int xfk_pcg_time(xfk_problem *prob, int iters, double *ms_spmv, double *ms_iter);
 
+/* Per-phase profile of a solved static problem (single device, AMG
+ * preconditioner): with XFK_PROFILE_SETUP the AMG hierarchy is rebuilt for the
+ * assembled matrix, then `iters` PCG iterations run without a convergence stop;
+ * every phase -- setup steps per level, each V-cycle launch per level, the
+ * PCG SpMV and update -- is bracketed by HIP events on the problem's stream.
+ * Phases come back in first-seen order, aggregated by name: launches, total
+ * device time, algorithmic bytes per launch (0 where the phase is not a
+ * streaming kernel).  *count = phases written (<= cap). */
+typedef struct {
+    char name[64];
+    int calls;
+    double ms_total;
+    double bytes_per_call;
+} xfk_phase;
+enum { XFK_PROFILE_SETUP = 1 };
+int xfk_phase_profile(xfk_problem *prob, int iters, int flags, xfk_phase *out, int cap, int *count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1566,7 +1566,16 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
 }
 
 // levels / transfer operators with at least this many rows use the tile kernels
-constexpr int kTileMinRows = 16384;
+// (XFK_TILE_MIN_ROWS overrides, for experiments)
+static int tile_min_rows()
+{
+    static const int v = [] {
+        const char *e = std::getenv("XFK_TILE_MIN_ROWS");
+        return e ? std::atoi(e) : 16384;
+    }();
+    return v;
+}
+#define kTileMinRows tile_min_rows()
 
 // lanes per row for a CSR with this many nonzeros per row on average
 int lanes_for(double per_row)
@@ -1651,6 +1660,8 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     A.nc = 0;
     AMG_CHECK(key.alloc(n));
     AMG_CHECK(t1.alloc(n));
+    const std::string lv = g_prof ? "setup L" + std::to_string(l) + " " : std::string();
+    if (g_prof) g_prof->begin(lv + "MIS-2 aggregation", 0.0);
     k_mis_init<<<nb(n), kB, 0, s>>>(n, cnt.p, key.p);
     int rounds = 0;
     int *und2 = dev_int.p + 4;   // undecided flag of rounds of parity 0 / 1
@@ -1688,6 +1699,7 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     k_agg_join3<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, A.rowptr, A.col, A.val, agg.p, agg1.p);
     std::swap(agg.p, agg1.p);   // agg = the joined map
     std::swap(agg.n, agg1.n);
+    if (g_prof) g_prof->end();
     if (std::getenv("XFK_AMG_DEBUG")) {
         DBuf<int> d;
         AMG_CHECK(d.alloc(3));
@@ -1708,8 +1720,10 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     // P = (I - omega D_F^-1 A_F) P_tent
     SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, wF.p};
     SgY YT{nullptr, nullptr, nullptr, agg.p};
+    if (g_prof) g_prof->begin(lv + "P = (I - w D^-1 A) P_tent, R = P^T", 0.0);
     if ((rc = spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz)) != XFK_OK) return rc;
     A.nc = (int)nc;
+    if (std::getenv("XFK_AMG_DEBUG")) std::fprintf(stderr, "[amg] level %d P nnz %lld\n", l, A.pnnz);
     // R = P^T
     AMG_CHECK(cnt.alloc((size_t)std::max<long long>(n, nc) + 1));
     AMG_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * (nc + 1), s));
@@ -1724,6 +1738,7 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     if (nc > 0)
         k_rt_sort_vals<<<(int)((nc * 64 + 255) / 256), 256, 0, s>>>((int)nc, A.rrow.p, A.rcol.p, A.prow.p, A.pcol.p,
                                                                    A.pval.p, A.rval.p);
+    if (g_prof) g_prof->end();
     return XFK_OK;
 }
 
@@ -1743,8 +1758,11 @@ int Amg::build(hipStream_t s, int l0)
         AMG_CHECK(dfinv.alloc(n));
         AMG_CHECK(wF.alloc(n));
         AMG_CHECK(cnt.alloc((size_t)n + 1));
+        const std::string lv = g_prof ? "setup L" + std::to_string(l) + " " : std::string();
+        if (g_prof) g_prof->begin(lv + "diagonal, strength, rho", 0.0);
         k_amg_diag<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
         if (n <= dense_max) {
+            if (g_prof) g_prof->end();
             dense_coarse = true;
             break;
         }
@@ -1753,6 +1771,7 @@ int Amg::build(hipStream_t s, int l0)
         k_amg_strength<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
                                             dfinv.p, wF.p, rho_part.p);
         k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, omega, rho.p + 2 * l);
+        if (g_prof) g_prof->end();
         if (l == kAmgMaxLevels - 1) break;   // smoother-only coarsest level
         long long nc = 0;
         int rc = aggregate(s, l, nc, true);
@@ -1762,13 +1781,19 @@ int Amg::build(hipStream_t s, int l0)
         SgX XA{A.rowptr, A.col, A.val, A.ncol_lim, nullptr, nullptr, nullptr};
         SgY YP{A.prow.p, A.pcol.p, A.pval.p, nullptr};
         long long apnnz = 0;
-        if ((rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, apnnz)) != XFK_OK) return rc;
+        if (g_prof) g_prof->begin(lv + "SpGEMM A P", 0.0);
+        rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, apnnz);
+        if (g_prof) g_prof->end();
+        if (rc != XFK_OK) return rc;
         if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
         AmgLevel &C = *L[l + 1];
         SgX XR{A.rrow.p, A.rcol.p, A.rval.p, INT_MAX, nullptr, nullptr, nullptr};
         SgY YAP{ap_row.p, ap_col.p, ap_val.p, nullptr};
         long long cnnz = 0;
-        if ((rc = spgemm<false>(*this, s, (int)nc, XR, YAP, C.rowptr_o, C.col_o, C.val_o, cnnz)) != XFK_OK) return rc;
+        if (g_prof) g_prof->begin(lv + "SpGEMM R (A P)", 0.0);
+        rc = spgemm<false>(*this, s, (int)nc, XR, YAP, C.rowptr_o, C.col_o, C.val_o, cnnz);
+        if (g_prof) g_prof->end();
+        if (rc != XFK_OK) return rc;
         C.n = (int)nc;
         C.nnz = cnnz;
         C.ncol_lim = (int)nc;
@@ -1793,6 +1818,7 @@ int Amg::build(hipStream_t s, int l0)
     if (dense_coarse) {
         AmgLevel &C = *L[nlev - 1];
         const int nbk = (C.n + kBj - 1) / kBj, ld = nbk * kBj;
+        if (g_prof) g_prof->begin("setup L" + std::to_string(nlev - 1) + " dense inverse (blocked Gauss-Jordan)", 0.0);
         cinv_ld = ld;
         AMG_CHECK(cinv.alloc((size_t)ld * ld));
         AMG_CHECK(bgj_tmp.alloc(2 * (size_t)nbk * kBj * kBj + 2 * kBj * kBj + 1 + ld));
@@ -1814,6 +1840,7 @@ int Amg::build(hipStream_t s, int l0)
             if (nbk > 1) k_bgj_update<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, D, Trow, Tcol, maxd, Dn);
         }
         k_dense_unscale<<<(unsigned)(((size_t)ld * ld / 2 + 255) / 256), 256, 0, s>>>(ld, cinv.p, sc);
+        if (g_prof) g_prof->end();
     }
     AMG_CHECK(hipGetLastError());
     AMG_CHECK(hipStreamSynchronize(s));
@@ -2241,6 +2268,37 @@ void launch_smooth(hipStream_t s, int mode, int l, const AmgLevel &A, const unsi
 
 }  // namespace
 
+// algorithmic bytes of one smoother launch (mode as launch_smooth): the
+// matrix stream, the gathered operand once, b / D^-1, the written vectors
+static double smooth_bytes(const AmgLevel &A, int mode)
+{
+    const double n = A.n, base = 12.0 * (double)A.nnz + 4.0 * (n + 1);
+    const bool implicit = mode == kSweepFromZero || mode == kResidFromZero;
+    const double rd = (implicit ? 2.0 : 3.0) * 8.0 * n;
+    const double wr = (mode == kResidFromZero ? 2.0 : 1.0) * 8.0 * n;
+    return base + rd + wr;
+}
+
+static const char *smooth_name(int mode)
+{
+    switch (mode) {
+    case kResidFromZero: return "sweep from 0 + residual";
+    case kSweepFromZero: return "sweep from 0";
+    case kResid: return "residual";
+    default: return "sweep";
+    }
+}
+
+static void smooth_ph(hipStream_t s, int mode, int l, const AmgLevel &A, const unsigned long long *rho,
+                      const double *b, const double *x, double *out, double *rout, const int *done)
+{
+    if (g_prof)
+        XFK_PHASE("L" + std::to_string(l) + " " + smooth_name(mode), smooth_bytes(A, mode),
+                  launch_smooth(s, mode, l, A, rho, b, x, out, rout, done));
+    else
+        launch_smooth(s, mode, l, A, rho, b, x, out, rout, done);
+}
+
 // Symmetric V-cycle; returns the buffer holding the level's result.  Level 0
 // writes its result to `out0`.
 static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, double *out0, const int *done)
@@ -2249,18 +2307,20 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     const unsigned long long *rho = M.rho.p + 2 * l;
     const int nu = M.sweeps;
     auto other = [&](double *c) { return c == A.xa.p ? A.xb.p : A.xa.p; };
+    const std::string lv = g_prof ? "L" + std::to_string(l) + " " : std::string();
     if (l == M.nlev - 1) {
         double *dst = (l == 0) ? out0 : A.xa.p;
         if (M.dense_coarse) {
-            k_dense_mv<<<(A.n * 64 + 255) / 256, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv.p, b, dst, done);
+            XFK_PHASE(lv + "dense inverse x b", 8.0 * A.n * M.cinv_ld + 8.0 * (M.cinv_ld + A.n),
+                      (k_dense_mv<<<(A.n * 64 + 255) / 256, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv.p, b, dst, done)));
             return dst;
         }
         // smoother-only coarsest level: 2 nu sweeps from zero
         double *cur = A.xa.p;
-        launch_smooth(s, kSweepFromZero, l, A, rho, b, nullptr, cur, nullptr, done);
+        smooth_ph(s, kSweepFromZero, l, A, rho, b, nullptr, cur, nullptr, done);
         for (int k = 2; k < 2 * nu; ++k) {
             double *nx = (k == 2 * nu - 1 && l == 0) ? out0 : other(cur);
-            launch_smooth(s, kSweep, l, A, rho, b, cur, nx, nullptr, done);
+            smooth_ph(s, kSweep, l, A, rho, b, cur, nx, nullptr, done);
             cur = nx;
         }
         if (l == 0 && cur != out0)
@@ -2270,24 +2330,27 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     // pre-smoothing (nu sweeps from zero) and residual
     double *cur = A.xa.p;
     if (nu == 1) {
-        launch_smooth(s, kResidFromZero, l, A, rho, b, nullptr, cur, A.r.p, done);
+        smooth_ph(s, kResidFromZero, l, A, rho, b, nullptr, cur, A.r.p, done);
     } else {
-        launch_smooth(s, kSweepFromZero, l, A, rho, b, nullptr, cur, nullptr, done);
+        smooth_ph(s, kSweepFromZero, l, A, rho, b, nullptr, cur, nullptr, done);
         for (int k = 2; k < nu; ++k) {
             double *nx = other(cur);
-            launch_smooth(s, kSweep, l, A, rho, b, cur, nx, nullptr, done);
+            smooth_ph(s, kSweep, l, A, rho, b, cur, nx, nullptr, done);
             cur = nx;
         }
-        launch_smooth(s, kResid, l, A, rho, b, cur, nullptr, A.r.p, done);
+        smooth_ph(s, kResid, l, A, rho, b, cur, nullptr, A.r.p, done);
     }
     AmgLevel &C = *M.L[l + 1];
     const long long rnnz = A.pnnz;
-    launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false, lanes_for((double)rnnz / A.nc), done);
+    XFK_PHASE(lv + "restriction R r", 12.0 * rnnz + 4.0 * (A.nc + 1) + 8.0 * A.n + 8.0 * A.nc,
+              launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false, lanes_for((double)rnnz / A.nc),
+                        done));
     const double *xc = vcycle_level(M, s, l + 1, C.b.p, nullptr, done);
-    launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)rnnz / A.n), done);
+    XFK_PHASE(lv + "prolongation x += P xc", 12.0 * rnnz + 4.0 * (A.n + 1) + 8.0 * A.nc + 16.0 * A.n,
+              launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)rnnz / A.n), done));
     for (int k = 0; k < nu; ++k) {
         double *nx = (k == nu - 1 && l == 0) ? out0 : other(cur);
-        launch_smooth(s, kSweep, l, A, rho, b, cur, nx, nullptr, done);
+        smooth_ph(s, kSweep, l, A, rho, b, cur, nx, nullptr, done);
         cur = nx;
     }
     return cur;

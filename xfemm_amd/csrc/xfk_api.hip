@@ -31,6 +31,7 @@
 namespace xfk {
 
 static thread_local std::string g_err;
+thread_local PhaseProf *g_prof = nullptr;
 void set_error(const std::string &msg) { g_err = msg; }
 
 using Terms = std::vector<std::pair<long long, double>>;
@@ -797,17 +798,24 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
     hipStream_t s = P->stream;
     const CgAxpyArgs A = cg_args(P, it);
     const size_t G = (size_t)P->Gpart;
-    launch_cg_axpy(s, A);
+    const double N = P->N;
+    // algorithmic bytes: the update streams 10 vectors (AMG: w z p x r u read,
+    // z p x r written); the SpMV the matrix, u, r and w
+    XFK_PHASE("PCG update (Chronopoulos-Gear axpy)", 80.0 * N, launch_cg_axpy(s, A));
     int rc;
     if (A.amg && (rc = P->amg->vcycle(s, A.R, A.U, &P->pcg.p->done)) != XFK_OK) return rc;
     rc = exchange(P, A.U);
     if (rc != XFK_OK) return rc;
     if (stamp) XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used], s));
+    const double spmv_bytes = 12.0 * (double)P->nnz + 4.0 * (N + 1) + 24.0 * N;
     if (A.amg)
-        launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G, P->pcg.p, A.R,
-                       P->part_loc.p + (size_t)((it + 1) & 1) * G);
+        XFK_PHASE("PCG SpMV w = A u", spmv_bytes,
+                  launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G,
+                                 P->pcg.p, A.R, P->part_loc.p + (size_t)((it + 1) & 1) * G));
     else
-        launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G, P->pcg.p);
+        XFK_PHASE("PCG SpMV w = A u", spmv_bytes,
+                  launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G,
+                                 P->pcg.p));
     if (stamp) {
         XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used + 1], s));
         P->spmv_used += 2;
@@ -1609,6 +1617,56 @@ int xfk_pcg_solve_csr_pc(int n, const int *rowptr, const int *col, const double 
     }
     xfk_problem_destroy(P);
     return rc;
+}
+
+int xfk_phase_profile(xfk_problem *P, int iters, int flags, xfk_phase *out, int cap, int *count)
+{
+    XFK_REQUIRE(P && P->symbolic_ready && iters > 0 && out && count, XFK_ERR_ARG, "no assembled system");
+    XFK_REQUIRE(!P->harmonic && !P->comm, XFK_ERR_UNSUPPORTED, "phase profile: single-device static problems only");
+    XFK_REQUIRE(P->amg && P->pc_used == XFK_PRECOND_AMG, XFK_ERR_ARG, "phase profile: solve with the AMG first");
+    XFK_CHECK(hipSetDevice(P->device));
+    hipStream_t s = P->stream;
+    PhaseProf prof;
+    prof.s = s;
+    g_prof = &prof;
+    int rc = XFK_OK;
+    if (flags & XFK_PROFILE_SETUP)
+        rc = P->amg->setup(s, P->N, P->N, P->rowptr.p, P->col.p, P->val.p, P->nnz);
+    if (rc == XFK_OK) {
+        const double tol = P->precision;
+        P->precision = 0.0;   // never converges: fixed iteration count
+        rc = pcg_start(P, 1);
+        P->precision = tol;
+        for (int k = 0; rc == XFK_OK && k < iters; ++k) rc = pcg_iteration(P, k, false);
+    }
+    g_prof = nullptr;
+    if (rc != XFK_OK) return rc;
+    XFK_CHECK(hipStreamSynchronize(s));
+    std::vector<std::string> order;
+    std::map<std::string, xfk_phase> agg;
+    for (const auto &r : prof.recs) {
+        if (r.ev0 < 0 || r.ev1 < 0) continue;
+        float ms = 0;
+        XFK_CHECK(hipEventElapsedTime(&ms, prof.ev[r.ev0], prof.ev[r.ev1]));
+        auto it = agg.find(r.name);
+        if (it == agg.end()) {
+            xfk_phase ph{};
+            std::snprintf(ph.name, sizeof ph.name, "%s", r.name.c_str());
+            it = agg.emplace(r.name, ph).first;
+            order.push_back(r.name);
+        }
+        xfk_phase &ph = it->second;
+        ph.bytes_per_call = (ph.bytes_per_call * ph.calls + r.bytes) / (ph.calls + 1);
+        ph.calls += 1;
+        ph.ms_total += ms;
+    }
+    int k = 0;
+    for (const auto &nm : order) {
+        if (k >= cap) break;
+        out[k++] = agg[nm];
+    }
+    *count = k;
+    return XFK_OK;
 }
 
 int xfk_pcg_time(xfk_problem *P, int iters, double *ms_spmv, double *ms_iter)

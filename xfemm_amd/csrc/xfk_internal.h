@@ -357,6 +357,54 @@ struct xfk_problem {
 // (xfk_harmonic.hip) drivers.
 namespace xfk {
 
+// Per-phase timing for xfk_phase_profile: while g_prof is set, the PCG and
+// V-cycle launch sites bracket each launch with a pair of HIP events on the
+// launch stream, tagged with the phase name and its algorithmic bytes.
+struct PhaseProf {
+    hipStream_t s = nullptr;
+    struct Rec {
+        std::string name;
+        double bytes;
+        int ev0, ev1;   // begin / end events (ev1 < 0: never closed, ignored)
+    };
+    std::vector<hipEvent_t> ev;
+    int used = 0;
+    std::vector<Rec> recs;
+    hipError_t record()
+    {
+        if (used == (int)ev.size()) {
+            hipEvent_t e;
+            hipError_t r = hipEventCreate(&e);
+            if (r != hipSuccess) return r;
+            ev.push_back(e);
+        }
+        return hipEventRecord(ev[used++], s);
+    }
+    void begin(const std::string &name, double bytes)
+    {
+        if (!recs.empty() && recs.back().ev1 < 0) recs.back().ev0 = -1;   // an unclosed phase: dropped
+        recs.push_back({name, bytes, used, -1});
+        (void)record();
+    }
+    void end()
+    {
+        if (recs.empty() || recs.back().ev1 >= 0 || recs.back().ev0 < 0) return;
+        recs.back().ev1 = used;
+        (void)record();
+    }
+    ~PhaseProf()
+    {
+        for (auto &e : ev) (void)hipEventDestroy(e);
+    }
+};
+extern thread_local PhaseProf *g_prof;
+#define XFK_PHASE(name, bytes, ...)                       \
+    do {                                                  \
+        if (::xfk::g_prof) ::xfk::g_prof->begin(name, bytes); \
+        __VA_ARGS__;                                      \
+        if (::xfk::g_prof) ::xfk::g_prof->end();          \
+    } while (0)
+
 // Everything Static2D derives from the GLOBAL problem before the mesh is split
 // (so a sharded solve sees the same boundary values, point currents and
 // circuit currents as the single-device one).

@@ -37,7 +37,8 @@ XFK_OPT_AMG_DENSE = 7
 EXPORTED = (
     "xfk_last_error", "xfk_age_element_matrix", "xfk_device_count", "xfk_problem_create", "xfk_problem_destroy",
     "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz",
-    "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_solve_csr_pc", "xfk_pcg_time", "xfk_set_option",
+    "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_solve_csr_pc", "xfk_pcg_time", "xfk_phase_profile",
+    "xfk_set_option",
     "xfk_problem_create_harmonic", "xfk_harmonic2d", "xfk_get_solution_complex", "xfk_get_circuits_complex",
     "xfk_get_csr_complex",
     "xfk_comm_unique_id", "xfk_comm_create_rccl", "xfk_comm_create_local", "xfk_comm_destroy",
@@ -149,6 +150,7 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_pcg_solve_csr_pc.argtypes = [C.c_int, iptr, iptr, dptr, dptr, dptr, C.c_int, C.c_double, C.c_int,
                                        C.c_int, C.POINTER(C.c_longlong), dptr]
     L.xfk_pcg_time.argtypes = [C.c_void_p, C.c_int, dptr, dptr]
+    L.xfk_phase_profile.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     L.xfk_set_option.argtypes = [C.c_void_p, C.c_int, C.c_double]
     L.xfk_problem_create_harmonic.argtypes = [C.POINTER(ProblemDesc), C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
     L.xfk_harmonic2d.argtypes = [C.c_void_p, C.c_int, C.POINTER(Result)]
@@ -384,6 +386,28 @@ class Static2DProblem:
         ms_iter = C.c_double()
         _check(_lib.xfk_pcg_time(self._h, iters, C.byref(ms_spmv), C.byref(ms_iter)))
         return ms_spmv.value, ms_iter.value
+
+    def phase_profile(self, iters: int = 10, setup: bool = True):
+        """Per-phase HIP-event profile (xfk_phase_profile): list of dicts
+        name, calls, ms_total, us_per_call, bytes_per_call."""
+        cap = 256
+        buf = (Phase * cap)()
+        n = C.c_int()
+        _check(_lib.xfk_phase_profile(self._h, iters, XFK_PROFILE_SETUP if setup else 0, C.cast(buf, C.c_void_p),
+                                      cap, C.byref(n)))
+        out = []
+        for k in range(n.value):
+            ph = buf[k]
+            out.append(dict(name=ph.name.decode(), calls=ph.calls, ms_total=ph.ms_total,
+                            us_per_call=1e3 * ph.ms_total / max(1, ph.calls), bytes_per_call=ph.bytes_per_call))
+        return out
+
+
+class Phase(C.Structure):
+    _fields_ = [("name", C.c_char * 64), ("calls", C.c_int), ("ms_total", C.c_double), ("bytes_per_call", C.c_double)]
+
+
+XFK_PROFILE_SETUP = 1
 
 
 class BlockAcDesc(C.Structure):
