@@ -222,6 +222,7 @@ typedef struct {
     int n_halo;                 /* halo nodes (local ids n_own .. n_own + n_halo - 1) */
     int n_elems;                /* local (owned + ghost) elements */
     int n_send, n_recv;         /* halo ranges */
+    int n_extra;                /* coupled nodes owned elsewhere, assembled here (local ids n_own ..) */
 } xfk_dist_info;
 
 /* Host-only partition plan (no device needed).  Call once with null arrays to
@@ -230,6 +231,13 @@ typedef struct {
  * global row} per range). */
 int xfk_partition_plan(int n_nodes, int n_elems, const int *p, int rank, int nranks, xfk_dist_info *info,
                        int *l2g, int *elems, int *recv, int *send);
+/* The same with coupled nodes (periodic pairs, air-gap quad nodes): every
+ * element touching one is local on every rank, the coupled nodes owned
+ * elsewhere are the first n_extra halo nodes (assembled rows), and a peer may
+ * send several ranges (coupled nodes first).  xfk_problem_create_dist plans
+ * this way for problems with periodic boundaries or air gaps. */
+int xfk_partition_plan_coupled(int n_nodes, int n_elems, const int *p, int rank, int nranks, int n_coupled,
+                               const int *coupled, xfk_dist_info *info, int *l2g, int *elems, int *recv, int *send);
 
 /* This rank's part of the global problem `desc` on `device`. */
 int xfk_problem_create_dist(const xfk_problem_desc *desc, int device, xfk_comm *comm, xfk_problem **out);

@@ -6,7 +6,7 @@ entries join the CSR pattern as fill-in and the GPU adds them after the
 element scatter.  Checked here: the assembled system after all boundary
 conditions (<= 1e-12 of max |entry|), A at every node (<= 1e-6 linear,
 <= 1e-5 nonlinear, relative to max |A|), the antiperiodic half machine, the
-sharded path's refusal and the .fem/.pbc file path through FSolver.
+sharded solve (3 ranks) and the .fem/.pbc file path through FSolver.
 """
 import numpy as np
 import pytest
@@ -81,16 +81,24 @@ def test_gpu_full_machine_equals_half():
     assert np.abs(F[:, :nth // 2 + 1] - H).max() <= 1e-8 * np.abs(F).max()
 
 
-def test_sharded_solve_refuses_air_gaps():
-    kk = synth_to_oracle(synth.age_motor(24, 3))[2]
-    kk.pop("pbc", None)
-    comms = kernels.Comm.local_group(1)
-    try:
-        with pytest.raises(kernels.XfkError):
-            kernels.Static2DProblem(comm=comms[0], **kk)
-    finally:
-        for c in comms:
-            c.close()
+def test_sharded_air_gap_matches_oracle():
+    """Air-gap machine (full and antiperiodic half) sharded over 3 ranks: every
+    rank assembles the rows of the air-gap / periodic nodes itself
+    (xfk_partition.h) -- same answer as one device and the oracle."""
+    from test_gpu_sharded import run_sharded
+    for half in (False, True):
+        pr, mesh, kk = synth_to_oracle(synth.age_motor(64, 6, half=half, rotor_angle=2.3))
+        Ao, _, _ = oracle.solve(pr, mesh)
+        Ac = converged(pr, mesh)
+        P = kernels.Static2DProblem(**kk)
+        P.solve()
+        A1 = P.solution()
+        P.close()
+        outs = run_sharded(kk, 3)
+        assert any(o[3]["n_extra"] > 0 for o in outs)
+        for res, A, _, info in outs:
+            assert rel_err(A, Ac) <= TOL_LINEAR, parity_message(A, Ao, Ac, TOL_LINEAR)
+            assert rel_err(A, A1) <= TOL_LINEAR
 
 
 def _harmonic_kw(half=False, angle=2.3, nonlinear=False):

@@ -171,13 +171,50 @@ def test_sharded_circuit_and_point_current():
         assert np.array_equal(c[1], c1[1])
 
 
-def test_sharded_rejects_periodic_boundaries():
-    kw = synth.bc_showcase(12)
-    comms = kernels.Comm.local_group(2)
-    with pytest.raises(kernels.XfkError, match="periodic"):
-        kernels.Static2DProblem(**kw, comm=comms[0])
-    for c in comms:
-        c.close()
+@pytest.mark.parametrize("anti,nranks", [(False, 2), (True, 3), (False, 4)])
+def test_sharded_periodic_matches_oracle(anti, nranks):
+    """Periodic / antiperiodic pairs across rank blocks: the coupled nodes'
+    rows are assembled on every rank (extra rows), so each rank's periodic
+    averaging map (the reference's sequential Periodicity / AntiPeriodicity)
+    reads every pre-map entry locally."""
+    pr, mesh, kw = synth_to_oracle(synth.bc_showcase(24, anti=anti))
+    Ao, _, _ = oracle.solve(pr, mesh)
+    Ac = converged(pr, mesh)
+    r1, A1, _ = single(kw)
+    outs = run_sharded(kw, nranks)
+    assert any(o[3]["n_extra"] > 0 for o in outs)
+    for res, A, _, info in outs:
+        assert rel_err(A, Ac) <= TOL_LINEAR, parity_message(A, Ao, Ac, TOL_LINEAR)
+        assert rel_err(A, A1) <= TOL_LINEAR
+    assert np.array_equal(outs[0][1], outs[-1][1])
+
+
+def test_sharded_periodic_nonlinear():
+    pr, mesh, kw = synth_to_oracle(synth.bc_showcase(20, nonlinear=True))
+    Ao, _, _ = oracle.solve(pr, mesh)
+    Ac = converged(pr, mesh)
+    for res, A, _, _ in run_sharded(kw, 3):
+        assert rel_err(A, Ac) <= TOL_NONLINEAR, parity_message(A, Ao, Ac, TOL_NONLINEAR)
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_sharded_torque_benchmark(tmp_path, nranks):
+    """configs[0] (TorqueBenchmark: periodic pbc1/pbc2 + air gap + magnets)
+    sharded: A vs the converged oracle and the reference's torque check."""
+    from oracle import femfile, gaptorque
+    from torque import torque_ok, write_case
+    from util import kernel_kwargs
+    deg = 30
+    pr, mesh = femfile.load_problem(write_case(tmp_path, deg))
+    kw = kernel_kwargs(pr, mesh)
+    Ao, _, _ = oracle.solve(pr, mesh)
+    Ac = converged(pr, mesh)
+    outs = run_sharded(kw, nranks)
+    assert any(o[3]["n_extra"] > 0 for o in outs)
+    for res, A, _, info in outs:
+        assert rel_err(A, Ac) <= TOL_LINEAR, parity_message(A, Ao, Ac, TOL_LINEAR)
+        tq = gaptorque.gap_dc_torque(mesh.ages[0], A, pr.Depth, pr.LengthUnits)
+        assert torque_ok(tq, deg)[0], tq
 
 
 def test_rccl_single_rank_is_bit_identical():

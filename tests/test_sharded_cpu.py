@@ -70,6 +70,55 @@ def test_partition_plan_scrambled_numbering():
     assert all(len(pl["recv"]) == 2 for pl in plans)
 
 
+def _check_coupled(N, p, X, plans):
+    """Coupled-node plans: every element touching a coupled node is local on
+    every rank, the coupled nodes owned elsewhere are the first n_extra halo
+    nodes, and each peer sends the ranges a rank receives from it in the same
+    order (coupled ranges first)."""
+    p = np.asarray(p).reshape(-1, 3)
+    world = len(plans)
+    isx = np.zeros(N, bool)
+    isx[X] = True
+    owner = np.zeros(N, int)
+    for q, pl in enumerate(plans):
+        owner[pl["row0"]:pl["row0"] + pl["n_own"]] = q
+    for q, pl in enumerate(plans):
+        touch = np.where((owner[p] == q).any(axis=1) | isx[p].any(axis=1))[0]
+        assert np.array_equal(np.sort(pl["elems"]), touch)
+        l2g = pl["l2g"]
+        assert len(set(l2g.tolist())) == len(l2g)
+        assert set(np.unique(p[touch])) <= set(l2g.tolist())
+        n0, ne = pl["n_own"], pl["n_extra"]
+        extra = set(np.where(isx & (owner != q))[0].tolist())
+        assert set(l2g[n0:n0 + ne].tolist()) == extra
+        off = n0
+        for peer, loff, ln, g0 in pl["recv"]:
+            assert loff == off and (owner[g0:g0 + ln] == peer).all()
+            assert np.array_equal(l2g[loff:loff + ln], np.arange(g0, g0 + ln))
+            off += ln
+        assert off == n0 + pl["n_halo"]
+        for peer in range(world):
+            if peer == q:
+                continue
+            mine = [(int(r[2]), int(r[3])) for r in pl["recv"] if r[0] == peer]
+            theirs = [(int(t[2]), int(t[3])) for t in plans[peer]["send"] if t[0] == q]
+            assert mine == theirs
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_partition_plan_coupled_nodes(world):
+    kw = synth.bc_showcase(12)
+    N = len(kw["x"])
+    X = np.unique(np.asarray(kw["pbc"]).reshape(-1, 3)[:, :2])
+    plans = [kernels.partition_plan(N, kw["p"], r, world, coupled=X) for r in range(world)]
+    _check_coupled(N, kw["p"], X, plans)
+    assert sum(pl["n_extra"] for pl in plans) == (world - 1) * len(X)
+    # without coupled nodes the plan is the ordinary one
+    plain = _plans(N, kw["p"], world)
+    _check_plans(N, kw["p"], plain)
+    assert all(pl["n_extra"] == 0 for pl in plain)
+
+
 def test_partition_plan_rejects_bad_sizes():
     kw = synth.magnetostatic(4)
     with pytest.raises(kernels.XfkError):

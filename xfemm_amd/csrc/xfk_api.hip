@@ -122,7 +122,7 @@ static int build_pbc_map(xfk_problem *P)
     for (int q = 0; q < npbc; ++q) {
         int i = P->hpbc[3 * q], j = P->hpbc[3 * q + 1], t = P->hpbc[3 * q + 2];
         if (t != 0 && t != 1) continue;  // static2d.cpp:932-939 only handles 0 and 1
-        if (i < 0 || j < 0 || i >= P->N || j >= P->N) {
+        if (i < 0 || j < 0 || i >= P->NL || j >= P->NL) {
             set_error("pbc node index out of range");
             return XFK_ERR_ARG;
         }
@@ -306,7 +306,7 @@ struct SymTmp {
 int build_symbolic(xfk_problem *P)
 {
     hipStream_t s = P->stream;
-    const int N = P->N, NL = P->NL, NE = P->NE;   // owned rows, local nodes, local elements
+    const int N = P->NR, NL = P->NL, NE = P->NE;   // assembled rows, local nodes, local elements
     SymTmp T;
     // periodic fill-in (+ the auxiliary matrices' (i, j) entries of the Newton AC solver)
     std::vector<long long> fillv = P->pbc_fill;
@@ -331,8 +331,8 @@ int build_symbolic(xfk_problem *P)
         std::vector<std::vector<int>> rows(N);
         for (long long k : fillv) {
             int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
-            rows[r].push_back(c);
-            rows[c].push_back(r);
+            if (r < N) rows[r].push_back(c);   // rows beyond the assembled ones do not exist
+            if (c < N) rows[c].push_back(r);
         }
         std::vector<int> hptr(N + 1, 0), hcol;
         for (int r = 0; r < N; ++r) {
@@ -351,9 +351,11 @@ int build_symbolic(xfk_problem *P)
     XFK_CHECK(P->rowptr.alloc(N + 1));
     launch_row_build(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, T.rowtmp, T.rowcnt);
     XFK_CHECK(exclusive_scan(P, T.rowcnt, P->rowptr.p, N));
-    int nnz = 0;
+    int nnz = 0, nnz_own = 0;
     XFK_CHECK(d2h(&nnz, P->rowptr.p + N, sizeof(int), s));
+    XFK_CHECK(d2h(&nnz_own, P->rowptr.p + P->N, sizeof(int), s));
     P->nnz = nnz;
+    P->nnz_own = nnz_own;
     XFK_CHECK(P->col.alloc(nnz));
     XFK_CHECK(P->val.alloc(nnz));
     XFK_CHECK(P->diag.alloc(N));
@@ -459,14 +461,20 @@ int build_symbolic(xfk_problem *P)
             long long k = P->pbc_entry_key[m];
             int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
             const Terms &tt = P->pbc_entry_terms[m];
-            // one gather entry per destination slot (both triangles)
+            // one gather entry per destination slot (both triangles) in an
+            // assembled row; a source (symmetric before the map) is read in
+            // whichever orientation lies in an assembled row -- one of its
+            // indices is always a coupled node (assembled on every rank)
             int ndst = (r == c) ? 1 : 2;
             for (int d = 0; d < ndst; ++d) {
-                rc_dst.push_back(d == 0 ? r : c);
-                rc_dst.push_back(d == 0 ? c : r);
+                const int dr = d == 0 ? r : c, dc = d == 0 ? c : r;
+                if (dr >= N) continue;
+                rc_dst.push_back(dr);
+                rc_dst.push_back(dc);
                 for (auto &t : tt) {
-                    src_rc.push_back((int)(t.first >> 32));
-                    src_rc.push_back((int)(t.first & 0xffffffff));
+                    const int a = (int)(t.first >> 32), b2 = (int)(t.first & 0xffffffff);
+                    src_rc.push_back(a < N ? a : b2);
+                    src_rc.push_back(a < N ? b2 : a);
                     w.push_back(t.second);
                 }
                 ptr.push_back((int)w.size());
@@ -547,7 +555,7 @@ int build_symbolic(xfk_problem *P)
     }
 
     // vectors and reduction scratch
-    for (DBuf<double> *v : {&P->b, &P->P, &P->dinv}) XFK_CHECK(v->alloc(N));
+    for (DBuf<double> *v : {&P->b, &P->P, &P->dinv}) XFK_CHECK(v->alloc(N));   // (N = assembled rows here)
     for (DBuf<double> *v : {&P->V, &P->Vold}) XFK_CHECK(v->alloc(NL));
     XFK_CHECK(P->partials.alloc(2 * kRedGrid));
     XFK_CHECK(P->counters.alloc(8));
@@ -597,7 +605,7 @@ static int assemble(xfk_problem *P, int iter)
     A.col = P->col.p;
     A.mu1_out = P->mu1b.p;
     A.mu2_out = P->mu2b.p;
-    launch_assemble_rows(s, P->N, A);   // writes every entry of val and b
+    launch_assemble_rows(s, P->NR, A);   // writes every entry of val and b (assembled rows)
     std::swap(P->mu1.p, P->mu1b.p);     // the state just written is read next iteration
     std::swap(P->mu1.n, P->mu1b.n);
     std::swap(P->mu2.p, P->mu2b.p);
@@ -725,8 +733,8 @@ static int amg_setup(xfk_problem *P)
     // sharded: rank-local aggregation, global coarse levels (Amg::setup_dist)
     int rc = (P->comm && P->comm->size > 1)
                  ? P->amg->setup_dist(s, P->comm, P->halo, P->N, P->NL - P->N, P->rowptr.p, P->col.p, P->val.p,
-                                      P->nnz)
-                 : P->amg->setup(s, P->N, P->N, P->rowptr.p, P->col.p, P->val.p, P->nnz);
+                                      P->nnz_own)
+                 : P->amg->setup(s, P->N, P->N, P->rowptr.p, P->col.p, P->val.p, P->nnz_own);
     XFK_CHECK(hipEventRecord(e1, s));
     XFK_CHECK(hipEventSynchronize(e1));
     float ms = 0;
@@ -807,7 +815,7 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
     rc = exchange(P, A.U);
     if (rc != XFK_OK) return rc;
     if (stamp) XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used], s));
-    const double spmv_bytes = 12.0 * (double)P->nnz + 4.0 * (N + 1) + 24.0 * N;
+    const double spmv_bytes = 12.0 * (double)P->nnz_own + 4.0 * (N + 1) + 24.0 * N;
     if (A.amg)
         XFK_PHASE("PCG SpMV w = A u", spmv_bytes,
                   launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G,
@@ -1115,11 +1123,13 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     };
     const int Ng = d->n_nodes, NEg = d->n_elems;
     const int N = plan ? plan->n_own : Ng;                  // owned rows
+    const int NR = plan ? plan->n_own + plan->n_extra : Ng; // assembled rows (+ coupled nodes owned elsewhere)
     const int NL = plan ? plan->n_own + plan->n_halo : Ng;  // local nodes
     const int NE = plan ? (int)plan->elems.size() : NEg;
     auto gnode = [&](int l) { return plan ? plan->l2g[l] : l; };
     auto gelem = [&](int l) { return plan ? plan->elems[l] : l; };
     P->N = N;
+    P->NR = NR;
     P->NL = NL;
     P->NE = NE;
     P->N_global = Ng;
@@ -1150,14 +1160,18 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
         y[l] = d->y[gnode(l)];
     }
     std::vector<int> pl(3LL * NE), lbl(NE), ebits(NE);
+    // global -> local: owned, or inside a receive range
+    std::unordered_map<int, int> g2l_halo;
+    if (plan)
+        for (const HaloRange &r : plan->halo.recv)
+            for (int k = 0; k < r.len; ++k) g2l_halo[r.g0 + k] = r.off + k;
+    auto g2l = [&](int g) -> int {
+        if (!plan) return g;
+        if (g >= plan->row0 && g < plan->row0 + plan->n_own) return g - plan->row0;
+        auto it = g2l_halo.find(g);
+        return it == g2l_halo.end() ? -1 : it->second;
+    };
     if (plan) {
-        // global -> local for the nodes of local elements: owned, or inside a receive range
-        auto g2l = [&](int g) {
-            if (g >= plan->row0 && g < plan->row0 + plan->n_own) return g - plan->row0;
-            for (const HaloRange &r : plan->halo.recv)
-                if (g >= r.g0 && g < r.g0 + r.len) return r.off + (g - r.g0);
-            return -1;
-        };
         for (int l = 0; l < NE; ++l) {
             const int e = gelem(l);
             for (int j = 0; j < 3; ++j) {
@@ -1174,7 +1188,17 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
         ebits[l] = G.ebits[gelem(l)];
     }
     P->hp = pl;
-    if (!plan && d->n_pbc) P->hpbc.assign(d->pbc, d->pbc + 3LL * d->n_pbc);
+    if (d->n_pbc) {   // periodic pairs in local numbering (sharded: every coupled node is local)
+        P->hpbc.assign(d->pbc, d->pbc + 3LL * d->n_pbc);
+        for (int k = 0; k < d->n_pbc; ++k)
+            for (int m = 0; m < 2; ++m) {
+                const int g = d->pbc[3 * k + m];
+                if (g < 0 || g >= Ng) continue;   // reported by build_pbc_map
+                const int v = g2l(g);
+                XFK_REQUIRE(v >= 0 && v < NR, fail(XFK_ERR_ARG), "internal: periodic node is not an assembled row");
+                P->hpbc[3 * k + m] = v;
+            }
+    }
 
     // boundary data of the local nodes (global values), owned rows only for rows
     std::vector<unsigned char> fixed(NL);
@@ -1187,13 +1211,12 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     std::vector<int> pt_nodes, fix_rows;
     std::vector<double> pt_J;
     for (size_t k = 0; k < G.pt_nodes.size(); ++k) {
-        const int g = G.pt_nodes[k];
-        const int l = plan ? g - plan->row0 : g;
-        if (l < 0 || l >= N) continue;
+        const int l = g2l(G.pt_nodes[k]);
+        if (l < 0 || l >= NR) continue;
         pt_nodes.push_back(l);
         pt_J.push_back(G.pt_J[k]);
     }
-    for (int l = 0; l < N; ++l)
+    for (int l = 0; l < NR; ++l)
         if (fixed[l]) fix_rows.push_back(l);
     P->npt = (int)pt_nodes.size();
     P->nfix_rows = (int)fix_rows.size();
@@ -1201,6 +1224,15 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     if (!plan) {
         P->age_key = G.age_key;
         P->age_val = G.age_val;
+    } else {   // air-gap entries of the assembled rows, local numbering (r <= c kept as a key order)
+        for (size_t m = 0; m < G.age_key.size(); ++m) {
+            int r = g2l((int)(G.age_key[m] >> 32)), c = g2l((int)(G.age_key[m] & 0xffffffff));
+            XFK_REQUIRE(r >= 0 && c >= 0 && r < NR && c < NR, fail(XFK_ERR_ARG),
+                        "internal: air-gap node is not an assembled row");
+            if (c < r) std::swap(r, c);
+            P->age_key.push_back(((long long)r << 32) | (unsigned)c);
+            P->age_val.push_back(G.age_val[m]);
+        }
     }
     int rc = build_pbc_map(P);
     if (rc != XFK_OK) return fail(rc);
@@ -1264,10 +1296,21 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
 int xfk_partition_plan(int n_nodes, int n_elems, const int *p, int rank, int nranks, xfk_dist_info *info,
                        int *l2g, int *elems, int *recv, int *send)
 {
+    return xfk_partition_plan_coupled(n_nodes, n_elems, p, rank, nranks, 0, nullptr, info, l2g, elems, recv, send);
+}
+
+int xfk_partition_plan_coupled(int n_nodes, int n_elems, const int *p, int rank, int nranks, int n_coupled,
+                               const int *coupled, xfk_dist_info *info, int *l2g, int *elems, int *recv, int *send)
+{
     XFK_REQUIRE(p && info && n_nodes > 0 && n_elems > 0, XFK_ERR_ARG, "null argument");
+    XFK_REQUIRE(n_coupled == 0 || coupled, XFK_ERR_ARG, "null coupled-node list");
+    std::vector<int> cpl(coupled, coupled + n_coupled);
+    std::sort(cpl.begin(), cpl.end());
+    cpl.erase(std::unique(cpl.begin(), cpl.end()), cpl.end());
     PartPlan plan;
-    XFK_REQUIRE(plan_partition(n_nodes, n_elems, p, rank, nranks, plan), XFK_ERR_ARG,
+    XFK_REQUIRE(plan_partition(n_nodes, n_elems, p, rank, nranks, plan, &cpl), XFK_ERR_ARG,
                 "bad partition: rank / size out of range or fewer nodes than ranks");
+    info->n_extra = plan.n_extra;
     info->rank = rank;
     info->nranks = nranks;
     info->n_global = n_nodes;
@@ -1299,14 +1342,25 @@ int xfk_problem_create_dist(const xfk_problem_desc *d, int device, xfk_comm *com
     int rc = validate_desc(d);
     if (rc == XFK_OK) rc = check_device(device);
     if (rc != XFK_OK) return rc;
-    XFK_REQUIRE(d->n_pbc == 0, XFK_ERR_UNSUPPORTED, "periodic boundaries are not supported in the sharded solve");
-    XFK_REQUIRE(d->n_ages == 0 || d->problem_type != XFK_PLANAR, XFK_ERR_UNSUPPORTED,
-                "air-gap elements are not supported in the sharded solve");
-    PartPlan plan;
-    XFK_REQUIRE(plan_partition(d->n_nodes, d->n_elems, d->p, comm->rank, comm->size, plan), XFK_ERR_ARG,
-                "bad partition: fewer nodes than ranks");
     GlobalPrep G;
     prepare_global(d, G);
+    rc = age_entries(d, 1.0, G.age_key, G.age_val);
+    if (rc != XFK_OK) return rc;
+    // coupled nodes: periodic pairs and air-gap quad nodes (assembled on every rank)
+    std::vector<int> coupled;
+    for (int k = 0; k < d->n_pbc; ++k) {
+        coupled.push_back(d->pbc[3 * k]);
+        coupled.push_back(d->pbc[3 * k + 1]);
+    }
+    for (long long k : G.age_key) {
+        coupled.push_back((int)(k >> 32));
+        coupled.push_back((int)(k & 0xffffffff));
+    }
+    std::sort(coupled.begin(), coupled.end());
+    coupled.erase(std::unique(coupled.begin(), coupled.end()), coupled.end());
+    PartPlan plan;
+    XFK_REQUIRE(plan_partition(d->n_nodes, d->n_elems, d->p, comm->rank, comm->size, plan, &coupled), XFK_ERR_ARG,
+                "bad partition: fewer nodes than ranks");
     return build_local(d, G, &plan, device, comm, out);
 }
 
@@ -1319,6 +1373,7 @@ int xfk_dist_get_info(const xfk_problem *P, xfk_dist_info *info)
     info->row0 = P->row0;
     info->n_own = P->N;
     info->n_halo = P->NL - P->N;
+    info->n_extra = P->NR - P->N;
     info->n_elems = P->NE;
     info->n_send = (int)P->halo.send.size();
     info->n_recv = (int)P->halo.recv.size();
@@ -1433,7 +1488,7 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     }
     R.newton_iters = Iter;
     R.last_res = resn;
-    R.nnz = P->nnz;
+    R.nnz = P->nnz_own;
     R.ncolors = P->ncolors;
     R.color_rounds = P->color_rounds;
     R.precond = P->pc_used;
@@ -1494,7 +1549,7 @@ int xfk_get_circuits(xfk_problem *P, int *ccase, double *J, double *dV)
     return XFK_OK;
 }
 
-long long xfk_get_nnz(xfk_problem *P) { return P ? P->nnz : -1; }
+long long xfk_get_nnz(xfk_problem *P) { return P ? P->nnz_own : -1; }
 
 int xfk_get_csr(xfk_problem *P, int *rowptr, int *col, double *val, double *b)
 {
@@ -1502,8 +1557,8 @@ int xfk_get_csr(xfk_problem *P, int *rowptr, int *col, double *val, double *b)
     XFK_CHECK(hipSetDevice(P->device));
     XFK_CHECK(hipStreamSynchronize(P->stream));
     if (rowptr) XFK_CHECK(d2h(rowptr, P->rowptr.p, sizeof(int) * (P->N + 1), P->stream));
-    if (col) XFK_CHECK(d2h(col, P->col.p, sizeof(int) * P->nnz, P->stream));
-    if (val) XFK_CHECK(d2h(val, P->val.p, sizeof(double) * P->nnz, P->stream));
+    if (col) XFK_CHECK(d2h(col, P->col.p, sizeof(int) * P->nnz_own, P->stream));
+    if (val) XFK_CHECK(d2h(val, P->val.p, sizeof(double) * P->nnz_own, P->stream));
     if (b) XFK_CHECK(d2h(b, P->b.p, sizeof(double) * P->N, P->stream));
     return XFK_OK;
 }
@@ -1577,6 +1632,8 @@ int xfk_pcg_solve_csr_pc(int n, const int *rowptr, const int *col, const double 
     P->N = n;
     P->NL = n;
     P->nnz = rowptr[n];
+    P->nnz_own = P->nnz;
+    P->NR = n;
     P->precision = precision;
     P->precond = precond;
     int rc = XFK_OK;
@@ -1631,7 +1688,7 @@ int xfk_phase_profile(xfk_problem *P, int iters, int flags, xfk_phase *out, int 
     g_prof = &prof;
     int rc = XFK_OK;
     if (flags & XFK_PROFILE_SETUP)
-        rc = P->amg->setup(s, P->N, P->N, P->rowptr.p, P->col.p, P->val.p, P->nnz);
+        rc = P->amg->setup(s, P->N, P->N, P->rowptr.p, P->col.p, P->val.p, P->nnz_own);
     if (rc == XFK_OK) {
         const double tol = P->precision;
         P->precision = 0.0;   // never converges: fixed iteration count

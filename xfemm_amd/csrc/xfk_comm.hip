@@ -174,8 +174,8 @@ struct LocalComm final : xfk_comm {
             for (const HaloRange &r : h.recv) {
                 const HaloPlan *peer = hub->plan[r.peer];
                 const HaloRange *t = nullptr;
-                for (const HaloRange &c : peer->send)
-                    if (c.peer == rank) t = &c;
+                for (const HaloRange &c : peer->send)   // (a peer may send several ranges: match by start)
+                    if (c.peer == rank && c.g0 == r.g0) t = &c;
                 if (!t || t->len != r.len || t->g0 != r.g0) {
                     set_error("local communicator: halo ranges of two ranks disagree");
                     return XFK_ERR_ARG;

@@ -183,7 +183,11 @@ struct xfk_problem {
     // sizes: N owned rows (= all nodes unless sharded), NL local nodes
     // (owned rows first, then the halo), NE local elements
     int N = 0, NL = 0, NE = 0;
-    long long nnz = 0;
+    // rows assembled: the owned rows, then (sharded periodic / air-gap
+    // problems) the extra rows of coupled nodes owned elsewhere (xfk_partition.h)
+    int NR = 0;
+    long long nnz = 0;       // entries of the assembled rows (NR)
+    long long nnz_own = 0;   // entries of the owned rows (N): the solved matrix
     int ncolors = 0;
     std::vector<int> color_off;      // ncolors + 1 (host)
 

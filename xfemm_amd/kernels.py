@@ -42,7 +42,7 @@ EXPORTED = (
     "xfk_problem_create_harmonic", "xfk_harmonic2d", "xfk_get_solution_complex", "xfk_get_circuits_complex",
     "xfk_get_csr_complex",
     "xfk_comm_unique_id", "xfk_comm_create_rccl", "xfk_comm_create_local", "xfk_comm_destroy",
-    "xfk_comm_rank", "xfk_comm_size", "xfk_partition_plan", "xfk_problem_create_dist", "xfk_dist_get_info",
+    "xfk_comm_rank", "xfk_comm_size", "xfk_partition_plan", "xfk_partition_plan_coupled", "xfk_problem_create_dist", "xfk_dist_get_info",
 )
 
 
@@ -113,7 +113,7 @@ class Result(C.Structure):
 class DistInfo(C.Structure):
     _fields_ = [("rank", C.c_int), ("nranks", C.c_int), ("n_global", C.c_int), ("row0", C.c_int),
                 ("n_own", C.c_int), ("n_halo", C.c_int), ("n_elems", C.c_int), ("n_send", C.c_int),
-                ("n_recv", C.c_int)]
+                ("n_recv", C.c_int), ("n_extra", C.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -167,6 +167,8 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_comm_size.argtypes = [vp]
     L.xfk_partition_plan.argtypes = [C.c_int, C.c_int, iptr, C.c_int, C.c_int, C.POINTER(DistInfo),
                                      iptr, iptr, iptr, iptr]
+    L.xfk_partition_plan_coupled.argtypes = [C.c_int, C.c_int, iptr, C.c_int, C.c_int, C.c_int, iptr,
+                                             C.POINTER(DistInfo), iptr, iptr, iptr, iptr]
     L.xfk_problem_create_dist.argtypes = [C.POINTER(ProblemDesc), C.c_int, vp, C.POINTER(vp)]
     L.xfk_dist_get_info.argtypes = [vp, C.POINTER(DistInfo)]
     _lib = L
@@ -571,20 +573,26 @@ class Comm:
             pass
 
 
-def partition_plan(n_nodes: int, p, rank: int, nranks: int) -> dict:
-    """Host-only row-block partition plan of xfk_problem_create_dist (no device)."""
+def partition_plan(n_nodes: int, p, rank: int, nranks: int, coupled=None) -> dict:
+    """Host-only row-block partition plan of xfk_problem_create_dist (no device);
+    ``coupled``: periodic / air-gap nodes (xfk_partition_plan_coupled)."""
     L = load_library()
     p = np.ascontiguousarray(np.asarray(p, dtype=np.int32).reshape(-1))
     ne = len(p) // 3
     info = DistInfo()
     pp = p.ctypes.data_as(iptr)
-    _check(L.xfk_partition_plan(n_nodes, ne, pp, rank, nranks, C.byref(info), None, None, None, None))
+    cp = np.ascontiguousarray(np.asarray([] if coupled is None else coupled, dtype=np.int32).reshape(-1))
+    nc = len(cp)
+    cpp = cp.ctypes.data_as(iptr) if nc else None
+    _check(L.xfk_partition_plan_coupled(n_nodes, ne, pp, rank, nranks, nc, cpp, C.byref(info), None, None, None,
+                                        None))
     l2g = np.zeros(info.n_own + info.n_halo, np.int32)
     elems = np.zeros(max(1, info.n_elems), np.int32)
     recv = np.zeros(4 * max(1, info.n_recv), np.int32)
     send = np.zeros(4 * max(1, info.n_send), np.int32)
-    _check(L.xfk_partition_plan(n_nodes, ne, pp, rank, nranks, C.byref(info), l2g.ctypes.data_as(iptr),
-                                elems.ctypes.data_as(iptr), recv.ctypes.data_as(iptr), send.ctypes.data_as(iptr)))
+    _check(L.xfk_partition_plan_coupled(n_nodes, ne, pp, rank, nranks, nc, cpp, C.byref(info),
+                                        l2g.ctypes.data_as(iptr), elems.ctypes.data_as(iptr),
+                                        recv.ctypes.data_as(iptr), send.ctypes.data_as(iptr)))
     d = info.as_dict()
     d["l2g"] = l2g
     d["elems"] = elems[:info.n_elems]
