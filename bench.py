@@ -48,9 +48,10 @@ def spmv_bytes(n_rows, nnz, amg=False):
     """Algorithmic HBM bytes of one CSR SpMV launch of the PCG (k_cg_spmv,
     xfemm_amd/csrc/xfk_pcg.hip): val 8 B + col 4 B per nonzero, rowptr 4 B per
     row (+1), u read once 8 B per row, w written 8 B per row (the fused u.w
-    partial re-reads u from cache); with the AMG preconditioner the launch
-    also reads r (8 B per row) for the fused r.u partial."""
-    return 12 * nnz + 4 * (n_rows + 1) + (24 if amg else 16) * n_rows
+    partial re-reads u from cache).  With the AMG preconditioner the r.u
+    partial comes from the V-cycle's last level-0 sweep (which holds r and
+    u), so the SpMV does not read r either."""
+    return 12 * nnz + 4 * (n_rows + 1) + 16 * n_rows
 
 
 class stdout_to_stderr:

@@ -128,6 +128,7 @@ struct Amg {
     DBuf<int> e0_dev;
     int *host_big = nullptr;          // pinned scratch for small device -> host reads
     int host_big_n = 0;
+    double *part_gam_ = nullptr;      // vcycle's gamma partials, for vc_dist
 
     ~Amg();
     // Build the hierarchy for the n x n CSR on `s` (host-synchronising).
@@ -143,7 +144,10 @@ struct Amg {
                    const int *col, const double *val, long long nnz);
     // u = M^-1 r (owned rows of level 0); kernels return early once *done != 0.
     // Sharded: collective (halo exchanges, one all-gather).
-    int vcycle(hipStream_t s, const double *r, double *u, const int *done);
+    // part_gam: the PCG's gamma = r.u partials (k_cg_spmv layout), produced by
+    // the last level-0 sweep when the cycle's shape allows (gamma_done)
+    int vcycle(hipStream_t s, const double *r, double *u, const int *done, double *part_gam = nullptr);
+    bool gamma_done = false;
     // New values in the level-0 matrix (same pattern): refresh the fine-level
     // smoother (D^-1, rho_A); the coarse levels are kept
     int refresh(hipStream_t s);

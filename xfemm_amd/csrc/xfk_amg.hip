@@ -1237,19 +1237,24 @@ __device__ __forceinline__ void smooth_finish(int i, double ax, double w, const 
 
 // CSR-stream tile SpMV (the PCG's kernel shape): B = 1024 on level 0, 256 on
 // large coarse levels (more workgroups than CUs)
+// part_gam (the PCG's last level-0 sweep only): per-tile partials of
+// b . out, i.e. gamma = r . u of the CG, in the layout and summation order of
+// k_cg_spmv's (same tiles, same workgroup sum), so the SpMV need not read r
 template <int MODE, int B>
 __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__restrict__ rowptr,
                                                          const int *__restrict__ col, const double *__restrict__ val,
                                                          const double *__restrict__ dinv,
                                                          const unsigned long long *rho, const double *__restrict__ b,
                                                          const double *__restrict__ x, double *__restrict__ out,
-                                                         double *__restrict__ rout, const int *done)
+                                                         double *__restrict__ rout, const int *done,
+                                                         double *__restrict__ part_gam)
 {
     if (done && *done) return;
     __shared__ __attribute__((aligned(16))) double lds[8 * B];
     const double ra = rho_of(rho);
     const double w = ra > 0.0 ? 1.0 / ra : 0.0;
-    const int r0 = xcd_tile(blockIdx.x, gridDim.x) * B;
+    const int t = xcd_tile(blockIdx.x, gridDim.x);
+    const int r0 = t * B;
     constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
     double ax;
     if constexpr (implicit)
@@ -1259,6 +1264,15 @@ __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__r
         ax = cg_tile_spmv<B>(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; }, lds);
     const int i = r0 + threadIdx.x;
     if (i < n) smooth_finish<MODE>(i, ax, w, dinv, b, x, out, rout);
+    if constexpr (MODE == kSweep) {
+        if (part_gam) {   // uniform per launch
+            __shared__ double red[2 * (B / 64)];
+            double g = 0.0, zero = 0.0;
+            if (i < n) g = b[i] * out[i];
+            cg_block_sum2(zero, g, red);
+            if (threadIdx.x == 0) part_gam[t] = g;
+        }
+    }
 }
 
 // G lanes per row, strided over the row, butterfly sum inside the group
@@ -2228,18 +2242,18 @@ namespace {
 
 template <int MODE>
 void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
-                     const double *x, double *out, double *rout, const int *done)
+                     const double *x, double *out, double *rout, const int *done, double *part_gam)
 {
     if (l == 0) {
         const int g = (A.n + kCgBlock - 1) / kCgBlock;
         k_amg_smooth<MODE, kCgBlock><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p,
-                                                            rho, b, x, out, rout, done);
+                                                            rho, b, x, out, rout, done, part_gam);
         return;
     }
     if (A.n >= kTileMinRows) {
         const int g = (A.n + 255) / 256;
         k_amg_smooth<MODE, 256><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
-                                                  out, rout, done);
+                                                  out, rout, done, nullptr);
         return;
     }
     const int G = lanes_for(A.n > 0 ? (double)A.nnz / A.n : 1.0);
@@ -2256,13 +2270,13 @@ void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned lon
 }
 
 void launch_smooth(hipStream_t s, int mode, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
-                   const double *x, double *out, double *rout, const int *done)
+                   const double *x, double *out, double *rout, const int *done, double *part_gam = nullptr)
 {
     switch (mode) {
-    case kSweepFromZero: launch_smooth_t<kSweepFromZero>(s, l, A, rho, b, x, out, rout, done); break;
-    case kSweep: launch_smooth_t<kSweep>(s, l, A, rho, b, x, out, rout, done); break;
-    case kResid: launch_smooth_t<kResid>(s, l, A, rho, b, x, out, rout, done); break;
-    default: launch_smooth_t<kResidFromZero>(s, l, A, rho, b, x, out, rout, done); break;
+    case kSweepFromZero: launch_smooth_t<kSweepFromZero>(s, l, A, rho, b, x, out, rout, done, nullptr); break;
+    case kSweep: launch_smooth_t<kSweep>(s, l, A, rho, b, x, out, rout, done, part_gam); break;
+    case kResid: launch_smooth_t<kResid>(s, l, A, rho, b, x, out, rout, done, nullptr); break;
+    default: launch_smooth_t<kResidFromZero>(s, l, A, rho, b, x, out, rout, done, nullptr); break;
     }
 }
 
@@ -2290,18 +2304,20 @@ static const char *smooth_name(int mode)
 }
 
 static void smooth_ph(hipStream_t s, int mode, int l, const AmgLevel &A, const unsigned long long *rho,
-                      const double *b, const double *x, double *out, double *rout, const int *done)
+                      const double *b, const double *x, double *out, double *rout, const int *done,
+                      double *part_gam = nullptr)
 {
     if (g_prof)
-        XFK_PHASE("L" + std::to_string(l) + " " + smooth_name(mode), smooth_bytes(A, mode),
-                  launch_smooth(s, mode, l, A, rho, b, x, out, rout, done));
+        XFK_PHASE("L" + std::to_string(l) + " " + smooth_name(mode) + (part_gam ? " (+ r.u partials)" : ""),
+                  smooth_bytes(A, mode), launch_smooth(s, mode, l, A, rho, b, x, out, rout, done, part_gam));
     else
-        launch_smooth(s, mode, l, A, rho, b, x, out, rout, done);
+        launch_smooth(s, mode, l, A, rho, b, x, out, rout, done, part_gam);
 }
 
 // Symmetric V-cycle; returns the buffer holding the level's result.  Level 0
 // writes its result to `out0`.
-static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, double *out0, const int *done)
+static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, double *out0, const int *done,
+                            double *part_gam = nullptr)
 {
     AmgLevel &A = *M.L[l];
     const unsigned long long *rho = M.rho.p + 2 * l;
@@ -2349,8 +2365,10 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     XFK_PHASE(lv + "prolongation x += P xc", 12.0 * rnnz + 4.0 * (A.n + 1) + 8.0 * A.nc + 16.0 * A.n,
               launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)rnnz / A.n), done));
     for (int k = 0; k < nu; ++k) {
-        double *nx = (k == nu - 1 && l == 0) ? out0 : other(cur);
-        smooth_ph(s, kSweep, l, A, rho, b, cur, nx, nullptr, done);
+        const bool last0 = k == nu - 1 && l == 0;
+        double *nx = last0 ? out0 : other(cur);
+        smooth_ph(s, kSweep, l, A, rho, b, cur, nx, nullptr, done, last0 ? part_gam : nullptr);
+        if (last0 && part_gam) M.gamma_done = true;
         cur = nx;
     }
     return cur;
@@ -2391,8 +2409,10 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
     if (A.n > 0) launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)A.pnnz / A.n), done);
     for (int k = 0; k < sweeps; ++k) {
         if ((rc = comm->exchange(A.plan, cur, s)) != XFK_OK) return nullptr;
+        const bool last0 = k == sweeps - 1 && out && l == 0;
         double *nx = (k == sweeps - 1 && out) ? out : oth;
-        launch_smooth(s, kSweep, l, A, rh, b, cur, nx, nullptr, done);
+        launch_smooth(s, kSweep, l, A, rh, b, cur, nx, nullptr, done, last0 ? part_gam_ : nullptr);
+        if (last0 && part_gam_) gamma_done = true;
         oth = cur;
         cur = nx;
     }
@@ -2419,14 +2439,17 @@ int Amg::refresh(hipStream_t s)
     return XFK_OK;
 }
 
-int Amg::vcycle(hipStream_t s, const double *r, double *u, const int *done)
+int Amg::vcycle(hipStream_t s, const double *r, double *u, const int *done, double *part_gam)
 {
+    gamma_done = false;
     if (!dist) {
-        vcycle_level(*this, s, 0, r, u, done);
+        vcycle_level(*this, s, 0, r, u, done, part_gam);
         return XFK_OK;
     }
     int rc = XFK_OK;
+    part_gam_ = part_gam;
     vc_dist(s, 0, r, u, done, rc);
+    part_gam_ = nullptr;
     if (rc != XFK_OK) return rc;
     AMG_CHECK(hipGetLastError());
     return XFK_OK;

@@ -811,15 +811,17 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
     // z p x r written); the SpMV the matrix, u, r and w
     XFK_PHASE("PCG update (Chronopoulos-Gear axpy)", 80.0 * N, launch_cg_axpy(s, A));
     int rc;
-    if (A.amg && (rc = P->amg->vcycle(s, A.R, A.U, &P->pcg.p->done)) != XFK_OK) return rc;
+    double *pgam = P->part_loc.p + (size_t)((it + 1) & 1) * G;
+    if (A.amg && (rc = P->amg->vcycle(s, A.R, A.U, &P->pcg.p->done, pgam)) != XFK_OK) return rc;
+    const bool gam = A.amg && !P->amg->gamma_done;   // the SpMV forms r.u itself (reads r)
     rc = exchange(P, A.U);
     if (rc != XFK_OK) return rc;
     if (stamp) XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used], s));
-    const double spmv_bytes = 12.0 * (double)P->nnz_own + 4.0 * (N + 1) + 24.0 * N;
+    const double spmv_bytes = 12.0 * (double)P->nnz_own + 4.0 * (N + 1) + (gam ? 24.0 : 16.0) * N;
     if (A.amg)
         XFK_PHASE("PCG SpMV w = A u", spmv_bytes,
                   launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G,
-                                 P->pcg.p, A.R, P->part_loc.p + (size_t)((it + 1) & 1) * G));
+                                 P->pcg.p, gam ? A.R : nullptr, gam ? pgam : nullptr));
     else
         XFK_PHASE("PCG SpMV w = A u", spmv_bytes,
                   launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G,
