@@ -30,6 +30,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <map>
 #include <memory>
 #include <vector>
 
@@ -100,7 +101,8 @@ struct Amg {
     DBuf<int> pad_col;                // single-pass SpGEMM: padded rows
     DBuf<double> pad_val;
     DBuf<double> ap_val;
-    DBuf<int> dev_int;                // small device scalars (undecided flag, overflow flag)
+    DBuf<int> dev_int;                // small device scalars (undecided flag, overflow flags)
+    std::map<int, int> cap_hint;      // SpGEMM slot capacity of each call site in the last setup
     int *host_int = nullptr;          // pinned mirror
     DBuf<char> cub_tmp;
 

@@ -674,7 +674,7 @@ __device__ __forceinline__ void wave_lds_sync()
 // moves it to its CSR place after the length scan.
 template <bool PMODE, int G, int CAP>
 __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int *__restrict__ cnt_out,
-                                                    int *__restrict__ pcol, double *__restrict__ pval)
+                                                    int *__restrict__ pcol, double *__restrict__ pval, int *ovf)
 {
     constexpr int W = 64 / G;
     constexpr int S = CAP / G;
@@ -724,17 +724,23 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
             const int total = __shfl(incl, G - 1, G);
             const int o = np + incl - len;
             if (PMODE) {
-                if (len) {
+                if (len && o < CAP) {
                     pk[o] = ys;
                     pv[o] = xv;
                 }
             } else {
-                for (int q = 0; q < len; ++q) {
+                for (int q = 0; q < len && o + q < CAP; ++q) {
                     pk[o + q] = Y.col[ys + q];
                     pv[o + q] = xv * Y.val[ys + q];
                 }
             }
             np += total;
+        }
+        // more products than slots (a capacity taken from an earlier setup):
+        // the row is garbage, the host redoes the product with a measured capacity
+        if (np > CAP) {
+            if (l == 0) *ovf = 1;
+            np = CAP;
         }
     }
     wave_lds_sync();
@@ -1491,6 +1497,17 @@ int scan_total(Amg &A, hipStream_t s, const int *in, int *out, int n, long long 
     return XFK_OK;
 }
 
+// the same without reading the total back (no host synchronisation)
+int scan_only(Amg &A, hipStream_t s, const int *in, int *out, int n)
+{
+    size_t bytes = 0;
+    AMG_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out + 1, n, s));
+    AMG_CHECK(A.cub_tmp.alloc(bytes ? bytes : 1));
+    AMG_CHECK(hipMemsetAsync(out, 0, sizeof(int), s));
+    if (n > 0) AMG_CHECK(hipcub::DeviceScan::InclusiveSum(A.cub_tmp.p, bytes, in, out + 1, n, s));
+    return XFK_OK;
+}
+
 int read_flag(Amg &A, hipStream_t s, int idx, int &v)
 {
     AMG_CHECK(hipMemcpyAsync(A.host_int + 1, A.dev_int.p + idx, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1502,10 +1519,59 @@ int read_flag(Amg &A, hipStream_t s, int idx, int &v)
 // C = X Y (rowptr/col/val allocated here); XFK_ERR_UNSUPPORTED on LDS overflow
 template <bool PMODE>
 int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<int> &crow, DBuf<int> &ccol,
-           DBuf<double> &cval, long long &cnnz)
+           DBuf<double> &cval, long long &cnnz, int key = -1)
 {
     AMG_CHECK(M.cnt.alloc((size_t)nrows + 1));
     AMG_CHECK(crow.alloc((size_t)nrows + 1));
+    // single pass into padded rows of `cap` slots (sort-based), then scan +
+    // compaction; returns the overflow flag (rows with more products than
+    // slots), read back with the scan's own synchronisation
+    int *sovf = M.dev_int.p + 6;
+    auto sort_pass = [&](int cap, bool &overflow) -> int {
+        AMG_CHECK(M.pad_col.alloc((size_t)nrows * cap));
+        AMG_CHECK(M.pad_val.alloc((size_t)nrows * cap));
+        int *pc = M.pad_col.p;
+        double *pv = M.pad_val.p;
+        AMG_CHECK(hipMemsetAsync(sovf, 0, sizeof(int), s));
+        if (nrows > 0) {
+            // few lanes per row, 4-8 sorted slots per lane: many rows per
+            // wavefront to overlap their dependent gathers
+            if (cap == 16)
+                k_spgemm_sort<PMODE, 4, 16><<<(nrows + 15) / 16, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, sovf);
+            else if (cap == 32)
+                k_spgemm_sort<PMODE, 8, 32><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, sovf);
+            else if (cap == 64)
+                k_spgemm_sort<PMODE, 8, 64><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, sovf);
+            else if (cap == 128)
+                k_spgemm_sort<PMODE, 16, 128><<<(nrows + 3) / 4, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, sovf);
+            else
+                k_spgemm_sort<PMODE, 32, 256><<<(nrows + 1) / 2, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, sovf);
+        }
+        AMG_CHECK(hipMemcpyAsync(M.host_int + 4, sovf, sizeof(int), hipMemcpyDeviceToHost, s));
+        int rc = scan_total(M, s, M.cnt.p, crow.p, nrows, cnnz);   // synchronises
+        if (rc != XFK_OK) return rc;
+        overflow = M.host_int[4] != 0;
+        if (overflow) return XFK_OK;
+        AMG_CHECK(ccol.alloc((size_t)std::max(1LL, cnnz)));
+        AMG_CHECK(cval.alloc((size_t)std::max(1LL, cnnz)));
+        if (nrows > 0)
+            k_spgemm_compact<<<(unsigned)(((long long)nrows * 16 + kB - 1) / kB), kB, 0, s>>>(
+                nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p);
+        return XFK_OK;
+    };
+    // the slot capacity this product needed in the previous setup (same
+    // call site): taken without measuring the longest product list first
+    // (one launch pair and one host synchronisation fewer); an overflow is
+    // detected by the kernel and the product redone with a measured capacity
+    if (key >= 0) {
+        auto hint = M.cap_hint.find(key);
+        if (hint != M.cap_hint.end()) {
+            bool overflow = false;
+            int rc = sort_pass(hint->second, overflow);
+            if (rc != XFK_OK || !overflow) return rc;
+            M.cap_hint.erase(hint);
+        }
+    }
     // longest product list -> sub-wave (<= 64 products per row) or wave-per-row kernels
     int maxprod = 0;
     if (nrows > 0) {
@@ -1518,33 +1584,15 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
         if (rc != XFK_OK) return rc;
     }
     if (maxprod <= kSortCap) {
-        // single pass into padded rows (sort-based), then scan + compaction
         const int cap = maxprod <= 16 ? 16 : maxprod <= 32 ? 32 : maxprod <= 64 ? 64 : maxprod <= 128 ? 128 : 256;
-        AMG_CHECK(M.pad_col.alloc((size_t)nrows * cap));
-        AMG_CHECK(M.pad_val.alloc((size_t)nrows * cap));
-        int *pc = M.pad_col.p;
-        double *pv = M.pad_val.p;
-        if (nrows > 0) {
-            // few lanes per row, 4-8 sorted slots per lane: many rows per
-            // wavefront to overlap their dependent gathers
-            if (cap == 16)
-                k_spgemm_sort<PMODE, 4, 16><<<(nrows + 15) / 16, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv);
-            else if (cap == 32)
-                k_spgemm_sort<PMODE, 8, 32><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv);
-            else if (cap == 64)
-                k_spgemm_sort<PMODE, 8, 64><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv);
-            else if (cap == 128)
-                k_spgemm_sort<PMODE, 16, 128><<<(nrows + 3) / 4, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv);
-            else
-                k_spgemm_sort<PMODE, 32, 256><<<(nrows + 1) / 2, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv);
-        }
-        int rc = scan_total(M, s, M.cnt.p, crow.p, nrows, cnnz);
+        bool overflow = false;
+        int rc = sort_pass(cap, overflow);
         if (rc != XFK_OK) return rc;
-        AMG_CHECK(ccol.alloc((size_t)std::max(1LL, cnnz)));
-        AMG_CHECK(cval.alloc((size_t)std::max(1LL, cnnz)));
-        if (nrows > 0)
-            k_spgemm_compact<<<(unsigned)(((long long)nrows * 16 + kB - 1) / kB), kB, 0, s>>>(
-                nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p);
+        if (overflow) {
+            set_error("AMG: internal SpGEMM capacity error");
+            return XFK_ERR_HIP;
+        }
+        if (key >= 0) M.cap_hint[key] = cap;
         return XFK_OK;
     }
     AMG_CHECK(hipMemsetAsync(M.dev_int.p + 2, 0, 2 * sizeof(int), s));
@@ -1630,8 +1678,8 @@ int Amg::host_ints(int count)
 
 int Amg::init(hipStream_t s)
 {
-    if (!host_int) AMG_CHECK(hipHostMalloc((void **)&host_int, 4 * sizeof(int)));
-    AMG_CHECK(dev_int.alloc(6));
+    if (!host_int) AMG_CHECK(hipHostMalloc((void **)&host_int, 8 * sizeof(int)));
+    AMG_CHECK(dev_int.alloc(8));
     AMG_CHECK(rho.alloc(2 * kAmgMaxLevels));
     AMG_CHECK(hipMemsetAsync(rho.p, 0, sizeof(unsigned long long) * 2 * kAmgMaxLevels, s));
     if (L.empty()) L.emplace_back(new AmgLevel());
@@ -1735,7 +1783,8 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, wF.p};
     SgY YT{nullptr, nullptr, nullptr, agg.p};
     if (g_prof) g_prof->begin(lv + "P = (I - w D^-1 A) P_tent, R = P^T", 0.0);
-    if ((rc = spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz)) != XFK_OK) return rc;
+    if ((rc = spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz, dist ? -1 : 4 * l)) != XFK_OK)
+        return rc;
     A.nc = (int)nc;
     if (std::getenv("XFK_AMG_DEBUG")) std::fprintf(stderr, "[amg] level %d P nnz %lld\n", l, A.pnnz);
     // R = P^T
@@ -1743,8 +1792,8 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     AMG_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * (nc + 1), s));
     k_rt_count<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, cnt.p);
     AMG_CHECK(A.rrow.alloc((size_t)nc + 1));
-    long long rnnz = 0;
-    if ((rc = scan_total(*this, s, cnt.p, A.rrow.p, (int)nc, rnnz)) != XFK_OK) return rc;
+    const long long rnnz = A.pnnz;   // R = P^T: as many entries as P (no read-back of the scan)
+    if ((rc = scan_only(*this, s, cnt.p, A.rrow.p, (int)nc)) != XFK_OK) return rc;
     AMG_CHECK(A.rcol.alloc((size_t)std::max(1LL, rnnz)));
     AMG_CHECK(A.rval.alloc((size_t)std::max(1LL, rnnz)));
     AMG_CHECK(hipMemsetAsync(cursor.p, 0, sizeof(int) * (nc + 1), s));
@@ -1796,7 +1845,7 @@ int Amg::build(hipStream_t s, int l0)
         SgY YP{A.prow.p, A.pcol.p, A.pval.p, nullptr};
         long long apnnz = 0;
         if (g_prof) g_prof->begin(lv + "SpGEMM A P", 0.0);
-        rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, apnnz);
+        rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, apnnz, 4 * l + 1);
         if (g_prof) g_prof->end();
         if (rc != XFK_OK) return rc;
         if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
@@ -1805,7 +1854,7 @@ int Amg::build(hipStream_t s, int l0)
         SgY YAP{ap_row.p, ap_col.p, ap_val.p, nullptr};
         long long cnnz = 0;
         if (g_prof) g_prof->begin(lv + "SpGEMM R (A P)", 0.0);
-        rc = spgemm<false>(*this, s, (int)nc, XR, YAP, C.rowptr_o, C.col_o, C.val_o, cnnz);
+        rc = spgemm<false>(*this, s, (int)nc, XR, YAP, C.rowptr_o, C.col_o, C.val_o, cnnz, 4 * l + 2);
         if (g_prof) g_prof->end();
         if (rc != XFK_OK) return rc;
         C.n = (int)nc;
