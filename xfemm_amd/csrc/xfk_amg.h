@@ -66,6 +66,7 @@ struct AmgLevel {
     // coarser: spans of the peers' aggregate ids)
     bool dist = false;
     HaloPlan plan;
+    TileSplit ts;                     // sharded level run by the tile kernels: exchange overlap
 };
 
 struct AmgStats {
@@ -131,6 +132,7 @@ struct Amg {
     int *host_big = nullptr;          // pinned scratch for small device -> host reads
     int host_big_n = 0;
     double *part_gam_ = nullptr;      // vcycle's gamma partials, for vc_dist
+    SideStream side;                  // sharded: halo exchanges overlapped with interior tiles
 
     ~Amg();
     // Build the hierarchy for the n x n CSR on `s` (host-synchronising).

@@ -869,13 +869,13 @@ __global__ void k_spgemm_compact(int nrows, int cap, const int *__restrict__ cro
 // The coarsest level (<= kAmgDenseMax rows) becomes a dense matrix padded to
 // a multiple of kBj with an identity tail (ld = padded size), inverted in
 // place by blocked Gauss-Jordan without pivoting (the level operators are
-// symmetric positive semi-definite).  Step k of kBj-wide block columns:
+// symmetric positive semi-definite).  Step k of kBj-wide block columns
+// (k_bgj_step, one launch):
 //     D  = inv(M_kk)                      k_bgj_diag for k = 0, else workgroup 0
-//                                         of update k-1 (once its tile is final)
-//     T_kj = D M_kj          (j != k)     k_bgj_row
-//     M_kj = T_kj, M_kk = D, C = M_:k      (snapshot of the old column)
-//     M_ij -= C_i T_kj       (i, j != k)  k_bgj_update (tile GEMMs)
-//     M_ik = -C_i D          (i != k)
+//                                         of step k-1 (once its tile is final)
+//     M_kj = D M_kj          (j != k),    M_kk = D
+//     M_ij -= M_ik (D M_kj)  (i, j != k)
+//     M_ik = -M_ik D         (i != k)     (old values of row k / column k)
 // The matrix is first scaled symmetrically to unit diagonal and the inverse
 // unscaled at the end.  A pivot below 1e-11 of the (unit) scaled diagonal
 // marks a null direction -- roundoff leaves the exact null pivot of a
@@ -1135,29 +1135,103 @@ __device__ __forceinline__ void bgj_load(double *__restrict__ dst, const double 
     }
 }
 
-__global__ void __launch_bounds__(256) k_bgj_row(int k, int ld, double *__restrict__ M, const double *__restrict__ D,
-                                                 double *__restrict__ Trow, double *__restrict__ Csnap)
+// One launch per block step k.
+// Step k reads only snapshots written by step k-1 (or the prologue), so every
+// tile is finalised in the same launch with no ordering between workgroups:
+//     D    = inv(M_kk)                               Dk
+//     R[j] = M_kj after step k-1 (row k, unscaled)    Rk + j T2
+//     C[i] = M_ik after step k-1 (column k)           Ck + i T2
+// tile (i, j):  i == k:  M_kj = D R[j]          (j == k: M_kk = D)
+//               j == k:  M_ik = -C[i] D
+//               else:    M_ij -= C[i] (D R[j])  (T_kj = D R[j] recomputed per
+//                                                tile: no row launch, no wait)
+// Row k+1 of the result goes to Rn, column k+1 to Cn; workgroup 0 takes tile
+// (k+1, k+1) -- the next pivot block -- and inverts it into Dn once written.
+// The chain per step is one launch: the pivot workgroup's two tile GEMMs and
+// the 64 x 64 inversion.
+__global__ void __launch_bounds__(256) k_bgj_snap0(int nbk, int ld, const double *__restrict__ M,
+                                                   double *__restrict__ R0, double *__restrict__ C0)
 {
-    const int j = blockIdx.x;
-    if (j == k) {
-        for (int idx = threadIdx.x; idx < kBj * kBj; idx += blockDim.x)
-            M[(size_t)(k * kBj + idx / kBj) * ld + k * kBj + idx % kBj] = D[idx];
-        return;
-    }
-    __shared__ double Xs[kBj * kXs], Ys[kBj * kYs];
-    bgj_load<kXs>(Xs, D, kBj);
-    bgj_load<kYs>(Ys, M + (size_t)k * kBj * ld + (size_t)j * kBj, ld);
+    const int t = blockIdx.x % nbk;
+    const bool row = blockIdx.x < nbk;
+    const double *src = row ? M + (size_t)t * kBj : M + (size_t)t * kBj * ld;   // tile (0, t) or (t, 0)
+    double *dst = (row ? R0 : C0) + (size_t)t * kBj * kBj;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int e = threadIdx.x + 256 * q, r = e >> 5, c = 2 * (e & 31);
-        *reinterpret_cast<double2 *>(Csnap + (size_t)j * kBj * kBj + r * kBj + c) =
-            *reinterpret_cast<const double2 *>(M + (size_t)(j * kBj + r) * ld + k * kBj + c);
+        *reinterpret_cast<double2 *>(dst + r * kBj + c) = *reinterpret_cast<const double2 *>(src + (size_t)r * ld + c);
     }
-    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_bgj_step(int k, int nbk, int ld, double *__restrict__ M,
+                                                  const double *__restrict__ Dk, const double *__restrict__ Rk,
+                                                  const double *__restrict__ Ck, double *__restrict__ Dn,
+                                                  double *__restrict__ Rn, double *__restrict__ Cn,
+                                                  const double *__restrict__ maxd)
+{
+    const int nt = nbk * nbk, kn = k + 1 < nbk ? k + 1 : 0;
+    const int b = (int)((blockIdx.x + (unsigned)(kn * nbk + kn)) % (unsigned)nt);
+    const int i = b / nbk, j = b % nbk;
+    const bool piv = k + 1 < nbk && blockIdx.x == 0;
+    const size_t T2 = (size_t)kBj * kBj;
+    __shared__ __attribute__((aligned(16))) double Xs[kBj * kXs];
+    __shared__ __attribute__((aligned(16))) double Ys[kBj * kYs];
+    double *Mij = M + (size_t)i * kBj * ld + (size_t)j * kBj;
+    if (i == k && j == k) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = threadIdx.x + 256 * q, r = e >> 5, c = 2 * (e & 31);
+            *reinterpret_cast<double2 *>(Mij + (size_t)r * ld + c) = *reinterpret_cast<const double2 *>(Dk + r * kBj + c);
+        }
+        return;
+    }
     dbl4 c[2][2];
-    bgj_mm(Xs, Ys, c);
-    double *T = Trow + (size_t)j * kBj * kBj;
-    double *Mk = M + (size_t)k * kBj * ld + (size_t)j * kBj;
+    double sgn = 1.0;
+    bool rmw = false;
+    if (i == k) {   // T = D R[j]
+        bgj_load<kXs>(Xs, Dk, kBj);
+        bgj_load<kYs>(Ys, Rk + j * T2, kBj);
+        __syncthreads();
+        bgj_mm(Xs, Ys, c);
+    } else if (j == k) {   // -C[i] D
+        bgj_load<kXs>(Xs, Ck + i * T2, kBj);
+        bgj_load<kYs>(Ys, Dk, kBj);
+        __syncthreads();
+        bgj_mm(Xs, Ys, c);
+        sgn = -1.0;
+    } else {   // M_ij - C[i] (D R[j])
+        double2 pre[8];   // C[i], in flight during the first product
+        const double *Ci = Ck + i * T2;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = threadIdx.x + 256 * q, r = e >> 5, cc = 2 * (e & 31);
+            pre[q] = *reinterpret_cast<const double2 *>(Ci + r * kBj + cc);
+        }
+        bgj_load<kXs>(Xs, Dk, kBj);
+        bgj_load<kYs>(Ys, Rk + j * T2, kBj);
+        __syncthreads();
+        bgj_mm(Xs, Ys, c);
+        __syncthreads();
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Ys[bgj_row(ti, r) * kYs + bgj_col(tj)] = c[ti][tj][r];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = threadIdx.x + 256 * q, r = e >> 5, cc = 2 * (e & 31);
+            Xs[r * kXs + cc] = pre[q].x;
+            Xs[r * kXs + cc + 1] = pre[q].y;
+        }
+        __syncthreads();
+        bgj_mm(Xs, Ys, c);
+        sgn = -1.0;
+        rmw = true;
+    }
+    double *rn = (i == k + 1) ? Rn + j * T2 : nullptr;
+    double *cn = (j == k + 1) ? Cn + i * T2 : nullptr;
+    if (piv) __syncthreads();   // Xs is reused below
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -1165,45 +1239,12 @@ __global__ void __launch_bounds__(256) k_bgj_row(int k, int ld, double *__restri
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = bgj_row(ti, r), col = bgj_col(tj);
-                T[row * kBj + col] = c[ti][tj][r];
-                Mk[(size_t)row * ld + col] = c[ti][tj][r];
-            }
-}
-
-// M_ij -= C_i T_kj (i, j != k) and M_ik = -C_i D (i != k), C_i the snapshot
-// of the old column block.  Workgroup 0 takes tile (k+1, k+1) -- the next
-// pivot block, final after this update -- and, once it is written, inverts it
-// into Dnext while the other workgroups are still updating: the next step
-// needs no separate pivot-block launch on its critical path.
-__global__ void __launch_bounds__(256) k_bgj_update(int k, int nbk, int ld, double *__restrict__ M,
-                                                    const double *__restrict__ D, const double *__restrict__ Trow,
-                                                    const double *__restrict__ Csnap, const double *__restrict__ maxd,
-                                                    double *__restrict__ Dnext)
-{
-    const int nt = nbk * nbk, kn = k + 1 < nbk ? k + 1 : 0;
-    const int b = (int)((blockIdx.x + (unsigned)(kn * nbk + kn)) % (unsigned)nt);
-    const int i = b / nbk, j = b % nbk;
-    if (i == k) return;
-    const bool piv = k + 1 < nbk && blockIdx.x == 0;
-    __shared__ __attribute__((aligned(16))) double Xs[kBj * kXs];
-    __shared__ __attribute__((aligned(16))) double Ys[kBj * kYs];
-    bgj_load<kXs>(Xs, Csnap + (size_t)i * kBj * kBj, kBj);
-    bgj_load<kYs>(Ys, j == k ? D : Trow + (size_t)j * kBj * kBj, kBj);
-    __syncthreads();
-    dbl4 c[2][2];
-    bgj_mm(Xs, Ys, c);
-    double *Mij = M + (size_t)i * kBj * ld + (size_t)j * kBj;
-    if (piv) __syncthreads();   // Xs / Ys are reused below
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-        for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                double *e = &Mij[(size_t)bgj_row(ti, r) * ld + bgj_col(tj)];
-                const double v = j == k ? -c[ti][tj][r] : *e - c[ti][tj][r];
+                double *e = &Mij[(size_t)row * ld + col];
+                const double v = rmw ? *e - c[ti][tj][r] : sgn * c[ti][tj][r];
                 *e = v;
-                if (piv) Xs[bgj_row(ti, r) * kBj + bgj_col(tj)] = v;
+                if (rn) rn[row * kBj + col] = v;
+                if (cn) cn[row * kBj + col] = v;
+                if (piv) Xs[row * kBj + col] = v;
             }
     if (!piv) return;
     __syncthreads();
@@ -1213,7 +1254,7 @@ __global__ void __launch_bounds__(256) k_bgj_update(int k, int nbk, int ld, doub
     for (int m = 0; m < 16; ++m) a[m] = Xs[(16 * w + m) * kBj + jl];
     bgj_diag_inv(a, 1e-11 * (*maxd), Ys);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) Dnext[(16 * w + m) * kBj + jl] = a[m];
+    for (int m = 0; m < 16; ++m) Dn[(16 * w + m) * kBj + jl] = a[m];
 }
 
 // --------------------------------------------------------------------------
@@ -1253,13 +1294,13 @@ __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__r
                                                          const unsigned long long *rho, const double *__restrict__ b,
                                                          const double *__restrict__ x, double *__restrict__ out,
                                                          double *__restrict__ rout, const int *done,
-                                                         double *__restrict__ part_gam)
+                                                         double *__restrict__ part_gam, const int *__restrict__ tl)
 {
     if (done && *done) return;
     __shared__ __attribute__((aligned(16))) double lds[8 * B];
     const double ra = rho_of(rho);
     const double w = ra > 0.0 ? 1.0 / ra : 0.0;
-    const int t = xcd_tile(blockIdx.x, gridDim.x);
+    const int t = tl ? tl[xcd_tile(blockIdx.x, gridDim.x)] : xcd_tile(blockIdx.x, gridDim.x);
     const int r0 = t * B;
     constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
     double ax;
@@ -1665,6 +1706,69 @@ void launch_mv(hipStream_t s, int n, const int *rowptr, const int *col, const do
 
 }  // namespace
 
+// tile t reads a halo column (>= n) in one of its rows
+__global__ void k_tile_halo_flags(int n, int B, const int *__restrict__ rowptr, const int *__restrict__ col,
+                                  int *__restrict__ flag)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    bool h = false;
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) h = h || col[k] >= n;
+    if (h) flag[i / B] = 1;   // benign race: every writer stores 1
+}
+
+int build_tile_split(hipStream_t s, int n, int B, const int *rowptr, const int *col, TileSplit &ts)
+{
+    const int nt = (n + B - 1) / B;
+    ts.B = 0;
+    ts.n_in = ts.n_bd = 0;
+    if (nt == 0) {
+        ts.B = B;
+        return XFK_OK;
+    }
+    DBuf<int> flag;
+    AMG_CHECK(flag.alloc(nt));
+    AMG_CHECK(hipMemsetAsync(flag.p, 0, sizeof(int) * nt, s));
+    k_tile_halo_flags<<<nb(n), kB, 0, s>>>(n, B, rowptr, col, flag.p);
+    std::vector<int> h(nt), list;
+    list.reserve(nt);
+    AMG_CHECK(hipMemcpyAsync(h.data(), flag.p, sizeof(int) * nt, hipMemcpyDeviceToHost, s));
+    AMG_CHECK(hipStreamSynchronize(s));
+    for (int t = 0; t < nt; ++t)
+        if (!h[t]) list.push_back(t);
+    ts.n_in = (int)list.size();
+    for (int t = 0; t < nt; ++t)
+        if (h[t]) list.push_back(t);
+    ts.n_bd = nt - ts.n_in;
+    AMG_CHECK(ts.tiles.alloc(nt));
+    AMG_CHECK(hipMemcpyAsync(ts.tiles.p, list.data(), sizeof(int) * nt, hipMemcpyHostToDevice, s));
+    AMG_CHECK(hipStreamSynchronize(s));   // `list` is a host temporary
+    ts.B = B;
+    return XFK_OK;
+}
+
+int SideStream::init()
+{
+    if (cs) return XFK_OK;
+    AMG_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    AMG_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    AMG_CHECK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    return XFK_OK;
+}
+
+SideStream::~SideStream()
+{
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+    if (cs) (void)hipStreamDestroy(cs);
+}
+
+bool overlap_enabled()
+{
+    const char *e = std::getenv("XFK_NO_OVERLAP");
+    return !(e && std::atoi(e) != 0);
+}
+
 int Amg::host_ints(int count)
 {
     if (host_big_n >= count) return XFK_OK;
@@ -1686,6 +1790,7 @@ int Amg::init(hipStream_t s)
     for (auto &lv : L) {   // levels are rebuilt: none sharded until setup_dist says so
         lv->dist = false;
         lv->plan = HaloPlan();
+        lv->ts.B = 0;
     }
     stats = AmgStats();
     dense_coarse = false;
@@ -1884,9 +1989,12 @@ int Amg::build(hipStream_t s, int l0)
         if (g_prof) g_prof->begin("setup L" + std::to_string(nlev - 1) + " dense inverse (blocked Gauss-Jordan)", 0.0);
         cinv_ld = ld;
         AMG_CHECK(cinv.alloc((size_t)ld * ld));
-        AMG_CHECK(bgj_tmp.alloc(2 * (size_t)nbk * kBj * kBj + 2 * kBj * kBj + 1 + ld));
-        double *Trow = bgj_tmp.p, *Tcol = Trow + (size_t)nbk * kBj * kBj, *Dbuf = Tcol + (size_t)nbk * kBj * kBj;
-        double *maxd = Dbuf + 2 * kBj * kBj, *sc = maxd + 1;
+        const size_t T2 = (size_t)kBj * kBj;
+        AMG_CHECK(bgj_tmp.alloc(4 * (size_t)nbk * T2 + 2 * T2 + 1 + ld));
+        double *Rs[2] = {bgj_tmp.p, bgj_tmp.p + (size_t)nbk * T2};
+        double *Cs[2] = {bgj_tmp.p + 2 * (size_t)nbk * T2, bgj_tmp.p + 3 * (size_t)nbk * T2};
+        double *Dbuf = bgj_tmp.p + 4 * (size_t)nbk * T2;
+        double *maxd = Dbuf + 2 * T2, *sc = maxd + 1;
         AMG_CHECK(hipMemsetAsync(cinv.p, 0, sizeof(double) * (size_t)ld * ld, s));
         k_dense_dscale<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, sc);
         k_dense_scatter<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, sc, cinv.p);
@@ -1894,13 +2002,15 @@ int Amg::build(hipStream_t s, int l0)
         // (a lookahead variant -- block column k+1 first, its pivot block
         // inverted on a second stream during the rest of the update -- was
         // measured slower: the two cross-stream waits cost ~15 us per step,
-        // more than the 25 us pivot-block inversion it hides)
-        // pivot block 0 by itself; pivot block k+1 inverted inside update k
+        // more than the 25 us pivot-block inversion it hides.  The separate
+        // row launch of T_k = D_k M_k: is gone: every tile recomputes its
+        // T_kj, 1130 -> 1070 us at 1600 rows, tools/lab/gj_lab.hip)
+        k_bgj_snap0<<<2 * nbk, 256, 0, s>>>(nbk, ld, cinv.p, Rs[0], Cs[0]);
         k_bgj_diag<<<1, 256, 0, s>>>(0, ld, cinv.p, maxd, Dbuf);
         for (int k = 0; k < nbk; ++k) {
-            double *D = Dbuf + (size_t)(k & 1) * kBj * kBj, *Dn = Dbuf + (size_t)((k + 1) & 1) * kBj * kBj;
-            k_bgj_row<<<nbk, 256, 0, s>>>(k, ld, cinv.p, D, Trow, Tcol);
-            if (nbk > 1) k_bgj_update<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, D, Trow, Tcol, maxd, Dn);
+            const int p = k & 1, q = (k + 1) & 1;
+            k_bgj_step<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, Dbuf + p * T2, Rs[p], Cs[p], Dbuf + q * T2, Rs[q],
+                                                 Cs[q], maxd);
         }
         k_dense_unscale<<<(unsigned)(((size_t)ld * ld / 2 + 255) / 256), 256, 0, s>>>(ld, cinv.p, sc);
         if (g_prof) g_prof->end();
@@ -2289,20 +2399,28 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
 
 namespace {
 
+// which: 0 every row; 1 / 2 the interior / boundary tiles of A.ts (tile levels)
 template <int MODE>
 void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
-                     const double *x, double *out, double *rout, const int *done, double *part_gam)
+                     const double *x, double *out, double *rout, const int *done, double *part_gam, int which)
 {
+    const int *tl = nullptr;
+    int nt = 0;
+    if (which) {
+        tl = A.ts.tiles.p + (which == 2 ? A.ts.n_in : 0);
+        nt = which == 1 ? A.ts.n_in : A.ts.n_bd;
+        if (nt == 0) return;
+    }
     if (l == 0) {
-        const int g = (A.n + kCgBlock - 1) / kCgBlock;
+        const int g = tl ? nt : (A.n + kCgBlock - 1) / kCgBlock;
         k_amg_smooth<MODE, kCgBlock><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p,
-                                                            rho, b, x, out, rout, done, part_gam);
+                                                            rho, b, x, out, rout, done, part_gam, tl);
         return;
     }
     if (A.n >= kTileMinRows) {
-        const int g = (A.n + 255) / 256;
+        const int g = tl ? nt : (A.n + 255) / 256;
         k_amg_smooth<MODE, 256><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
-                                                  out, rout, done, nullptr);
+                                                  out, rout, done, nullptr, tl);
         return;
     }
     const int G = lanes_for(A.n > 0 ? (double)A.nnz / A.n : 1.0);
@@ -2319,15 +2437,19 @@ void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned lon
 }
 
 void launch_smooth(hipStream_t s, int mode, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
-                   const double *x, double *out, double *rout, const int *done, double *part_gam = nullptr)
+                   const double *x, double *out, double *rout, const int *done, double *part_gam = nullptr,
+                   int which = 0)
 {
     switch (mode) {
-    case kSweepFromZero: launch_smooth_t<kSweepFromZero>(s, l, A, rho, b, x, out, rout, done, nullptr); break;
-    case kSweep: launch_smooth_t<kSweep>(s, l, A, rho, b, x, out, rout, done, part_gam); break;
-    case kResid: launch_smooth_t<kResid>(s, l, A, rho, b, x, out, rout, done, nullptr); break;
-    default: launch_smooth_t<kResidFromZero>(s, l, A, rho, b, x, out, rout, done, nullptr); break;
+    case kSweepFromZero: launch_smooth_t<kSweepFromZero>(s, l, A, rho, b, x, out, rout, done, nullptr, which); break;
+    case kSweep: launch_smooth_t<kSweep>(s, l, A, rho, b, x, out, rout, done, part_gam, which); break;
+    case kResid: launch_smooth_t<kResid>(s, l, A, rho, b, x, out, rout, done, nullptr, which); break;
+    default: launch_smooth_t<kResidFromZero>(s, l, A, rho, b, x, out, rout, done, nullptr, which); break;
     }
 }
+
+// tile size of the level's smoother launches (0: sub-wave kernels, no split)
+int smooth_tile(int l, const AmgLevel &A) { return l == 0 ? kCgBlock : (A.n >= kTileMinRows ? 256 : 0); }
 
 }  // namespace
 
@@ -2432,14 +2554,32 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
     const unsigned long long *rh = rho.p + 2 * l;
     double *cur = A.xa.p, *oth = A.xb.p;
     rc = XFK_OK;
+    // tile levels: the halo exchange of the iterate overlaps the interior tiles
+    const int B = smooth_tile(l, A);
+    const bool ov = B > 0 && overlap_enabled();
+    if (ov && !A.ts.ready()) {
+        if ((rc = side.init()) != XFK_OK) return nullptr;
+        if ((rc = build_tile_split(s, A.n, B, A.rowptr, A.col, A.ts)) != XFK_OK) return nullptr;
+    }
+    // halo of x, then mode over the level's rows (interior tiles during the exchange)
+    auto smooth_after_exchange = [&](int mode, double *x, double *o, double *ro, double *pg) -> int {
+        if (!ov) {
+            const int r = comm->exchange(A.plan, x, s);
+            if (r != XFK_OK) return r;
+            launch_smooth(s, mode, l, A, rh, b, x, o, ro, done, pg);
+            return XFK_OK;
+        }
+        return exchange_overlapped(
+            s, side, [&](hipStream_t cs) { return comm->exchange(A.plan, x, cs); },
+            [&] { launch_smooth(s, mode, l, A, rh, b, x, o, ro, done, pg, 1); },
+            [&] { launch_smooth(s, mode, l, A, rh, b, x, o, ro, done, pg, 2); });
+    };
     if (A.n > 0) k_jacobi_first<<<nb(A.n), kB, 0, s>>>(A.n, rh, A.dinv.p, b, cur, done);
     for (int k = 1; k < sweeps; ++k) {
-        if ((rc = comm->exchange(A.plan, cur, s)) != XFK_OK) return nullptr;
-        launch_smooth(s, kSweep, l, A, rh, b, cur, oth, nullptr, done);
+        if ((rc = smooth_after_exchange(kSweep, cur, oth, nullptr, nullptr)) != XFK_OK) return nullptr;
         std::swap(cur, oth);
     }
-    if ((rc = comm->exchange(A.plan, cur, s)) != XFK_OK) return nullptr;
-    launch_smooth(s, kResid, l, A, rh, b, cur, nullptr, A.r.p, done);
+    if ((rc = smooth_after_exchange(kResid, cur, nullptr, A.r.p, nullptr)) != XFK_OK) return nullptr;
     AmgLevel &C = *L[l + 1];
     const int GR = lanes_for(A.nc > 0 ? (double)A.pnnz / A.nc : 1.0);
     const double *xc;
@@ -2457,10 +2597,10 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
     }
     if (A.n > 0) launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)A.pnnz / A.n), done);
     for (int k = 0; k < sweeps; ++k) {
-        if ((rc = comm->exchange(A.plan, cur, s)) != XFK_OK) return nullptr;
         const bool last0 = k == sweeps - 1 && out && l == 0;
         double *nx = (k == sweeps - 1 && out) ? out : oth;
-        launch_smooth(s, kSweep, l, A, rh, b, cur, nx, nullptr, done, last0 ? part_gam_ : nullptr);
+        if ((rc = smooth_after_exchange(kSweep, cur, nx, nullptr, last0 ? part_gam_ : nullptr)) != XFK_OK)
+            return nullptr;
         if (last0 && part_gam_) gamma_done = true;
         oth = cur;
         cur = nx;

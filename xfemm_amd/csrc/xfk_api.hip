@@ -11,6 +11,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "xfk_amg.h"
+#include "xfk_spmv.h"
 
 #include <algorithm>
 #include <chrono>
@@ -306,6 +307,7 @@ struct SymTmp {
 int build_symbolic(xfk_problem *P)
 {
     hipStream_t s = P->stream;
+    P->ts.B = 0;   // the exchange-overlap tile split follows the pattern
     const int N = P->NR, NL = P->NL, NE = P->NE;   // assembled rows, local nodes, local elements
     SymTmp T;
     // periodic fill-in (+ the auxiliary matrices' (i, j) entries of the Newton AC solver)
@@ -726,9 +728,9 @@ static int amg_setup(xfk_problem *P)
     P->amg->omega = P->amg_omega;
     P->amg->rep_rows = P->amg_replicate;
     P->amg->dense_max = P->amg_dense;
-    hipEvent_t e0, e1;
-    XFK_CHECK(hipEventCreate(&e0));
-    XFK_CHECK(hipEventCreate(&e1));
+    ScopedEvents<2> ev;
+    XFK_CHECK(ev.create());
+    hipEvent_t e0 = ev[0], e1 = ev[1];
     XFK_CHECK(hipEventRecord(e0, s));
     // sharded: rank-local aggregation, global coarse levels (Amg::setup_dist)
     int rc = (P->comm && P->comm->size > 1)
@@ -739,8 +741,6 @@ static int amg_setup(xfk_problem *P)
     XFK_CHECK(hipEventSynchronize(e1));
     float ms = 0;
     XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     P->last.ms_amg_setup += ms;
     double ok = (rc == XFK_OK) ? 0.0 : 1.0;   // every rank must take the same preconditioner
     if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
@@ -814,18 +814,36 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
     double *pgam = P->part_loc.p + (size_t)((it + 1) & 1) * G;
     if (A.amg && (rc = P->amg->vcycle(s, A.R, A.U, &P->pcg.p->done, pgam)) != XFK_OK) return rc;
     const bool gam = A.amg && !P->amg->gamma_done;   // the SpMV forms r.u itself (reads r)
+    const double *Rg = A.amg && gam ? A.R : nullptr;
+    double *pg = A.amg && gam ? pgam : nullptr;
+    const CgState *St = P->pcg.p;
+    if (P->comm && P->comm->size > 1 && overlap_enabled()) {
+        // sharded: the halo of u travels on the side stream while the tiles
+        // without halo columns multiply (bit-identical to the single launch)
+        if (!P->ts.ready()) {
+            if ((rc = P->side.init()) != XFK_OK) return rc;
+            if ((rc = build_tile_split(s, P->N, kCgBlock, P->rowptr.p, P->col.p, P->ts)) != XFK_OK) return rc;
+        }
+        rc = exchange_overlapped(
+            s, P->side, [&](hipStream_t cs) { return P->comm->exchange(P->halo, A.U, cs); },
+            [&] {
+                launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G, St, Rg,
+                               pg, P->ts.tiles.p, P->ts.n_in);
+            },
+            [&] {
+                launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G, St, Rg,
+                               pg, P->ts.tiles.p + P->ts.n_in, P->ts.n_bd);
+            });
+        if (rc != XFK_OK) return rc;
+        return allreduce_partials(P, 3);
+    }
     rc = exchange(P, A.U);
     if (rc != XFK_OK) return rc;
     if (stamp) XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used], s));
     const double spmv_bytes = 12.0 * (double)P->nnz_own + 4.0 * (N + 1) + (gam ? 24.0 : 16.0) * N;
-    if (A.amg)
-        XFK_PHASE("PCG SpMV w = A u", spmv_bytes,
-                  launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G,
-                                 P->pcg.p, gam ? A.R : nullptr, gam ? pgam : nullptr));
-    else
-        XFK_PHASE("PCG SpMV w = A u", spmv_bytes,
-                  launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G,
-                                 P->pcg.p));
+    XFK_PHASE("PCG SpMV w = A u", spmv_bytes,
+              launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G, St, Rg,
+                             pg));
     if (stamp) {
         XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used + 1], s));
         P->spmv_used += 2;
@@ -1388,10 +1406,9 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     XFK_REQUIRE(!P->harmonic, XFK_ERR_ARG, "harmonic problem: use xfk_harmonic2d");
     XFK_CHECK(hipSetDevice(P->device));
     hipStream_t s = P->stream;
-    hipEvent_t e0, e1, e2;
-    XFK_CHECK(hipEventCreate(&e0));
-    XFK_CHECK(hipEventCreate(&e1));
-    XFK_CHECK(hipEventCreate(&e2));
+    ScopedEvents<3> ev;
+    XFK_CHECK(ev.create());
+    hipEvent_t e0 = ev[0], e1 = ev[1], e2 = ev[2];
     xfk_result R{};
     int rc = XFK_OK;
     float ms = 0;
@@ -1475,9 +1492,6 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
         }
     }
     XFK_CHECK(hipStreamSynchronize(s));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipEventDestroy(e2);
     if (P->time_spmv && P->spmv_used > 0) {
         double sum = 0;
         for (int k = 0; k < P->spmv_used; k += 2) {
@@ -1743,9 +1757,9 @@ int xfk_pcg_time(xfk_problem *P, int iters, double *ms_spmv, double *ms_iter)
         P->spmv_ev.resize(2 * iters);
         for (auto &ev : P->spmv_ev) XFK_CHECK(hipEventCreate(&ev));
     }
-    hipEvent_t t0, t1;
-    XFK_CHECK(hipEventCreate(&t0));
-    XFK_CHECK(hipEventCreate(&t1));
+    ScopedEvents<2> ev;
+    XFK_CHECK(ev.create());
+    hipEvent_t t0 = ev[0], t1 = ev[1];
     P->spmv_used = 0;
     XFK_CHECK(hipEventRecord(t0, s));
     for (int k = 0; k < iters; ++k) {
@@ -1762,8 +1776,6 @@ int xfk_pcg_time(xfk_problem *P, int iters, double *ms_spmv, double *ms_iter)
     }
     float tot = 0;
     XFK_CHECK(hipEventElapsedTime(&tot, t0, t1));
-    (void)hipEventDestroy(t0);
-    (void)hipEventDestroy(t1);
     if (ms_spmv) *ms_spmv = sum / (P->spmv_used / 2);
     if (ms_iter) *ms_iter = tot / iters;
     P->spmv_used = 0;

@@ -1481,10 +1481,9 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     XFK_REQUIRE(P && P->harmonic, XFK_ERR_ARG, "not a harmonic problem (xfk_problem_create_harmonic)");
     XFK_CHECK(hipSetDevice(P->device));
     hipStream_t s = P->stream;
-    hipEvent_t e0, e1, e2;
-    XFK_CHECK(hipEventCreate(&e0));
-    XFK_CHECK(hipEventCreate(&e1));
-    XFK_CHECK(hipEventCreate(&e2));
+    ScopedEvents<3> ev;
+    XFK_CHECK(ev.create());
+    hipEvent_t e0 = ev[0], e1 = ev[1], e2 = ev[2];
     xfk_result R{};
     float ms = 0;
     XFK_CHECK(hipEventRecord(e0, s));
@@ -1645,9 +1644,9 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
             P->amg->theta = P->amg_theta;
             P->amg->sweeps = P->amg_sweeps;
             P->amg->omega = P->amg_omega;
-            hipEvent_t a0, a1;
-            XFK_CHECK(hipEventCreate(&a0));
-            XFK_CHECK(hipEventCreate(&a1));
+            ScopedEvents<2> aev;
+            XFK_CHECK(aev.create());
+            hipEvent_t a0 = aev[0], a1 = aev[1];
             XFK_CHECK(hipEventRecord(a0, s));
             // later passes of the nonlinear loop keep the hierarchy (fine-level
             // smoother refreshed) while COCG stays within 1.25x + 1 the
@@ -1665,8 +1664,6 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
             float mss = 0;
             XFK_CHECK(hipEventElapsedTime(&mss, a0, a1));
             ms_setup += mss;
-            (void)hipEventDestroy(a0);
-            (void)hipEventDestroy(a1);
             if (arc != XFK_OK && arc != XFK_ERR_UNSUPPORTED) return arc;
             amg = arc == XFK_OK;
             reusable = amg;
@@ -1900,9 +1897,6 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
             return XFK_ERR_NOCONV;
         }
     }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipEventDestroy(e2);
     // Case-2 circuits: the voltage gradient from the bordered unknown
     // (harmonic2d.cpp:784-785: I c w V[N+k]; harmonicaxi.cpp:791: I w c 0.01 V[N+k])
     for (size_t q = 0; q < P->hc2_circ.size(); ++q) {

@@ -47,6 +47,24 @@ constexpr double kC = kPI * 4.e-05;  // static2d.cpp:66
         }                                                                        \
     } while (0)
 
+// hipEvents owned by one function: destroyed on every return path
+template <int N>
+struct ScopedEvents {
+    hipEvent_t e[N] = {};
+    hipError_t create()
+    {
+        for (auto &x : e)
+            if (hipError_t r = hipEventCreate(&x); r != hipSuccess) return r;
+        return hipSuccess;
+    }
+    hipEvent_t operator[](int i) const { return e[i]; }
+    ~ScopedEvents()
+    {
+        for (auto &x : e)
+            if (x) (void)hipEventDestroy(x);
+    }
+};
+
 #define XFK_REQUIRE(cond, code, msg)  \
     do {                              \
         if (!(cond)) {                \
@@ -173,6 +191,44 @@ struct DBuf {
     }
 };
 
+// Halo exchange overlapped with computation on a sharded operator.  Tiles of
+// B rows (the tile kernels' workgroups) are split once per operator into the
+// interior tiles -- every column owned (< n) -- and the boundary tiles that
+// read a halo column.  The exchange runs on a side stream while the interior
+// tiles run on the main stream; the boundary tiles follow the exchange.
+// Every tile computes exactly what the unsplit launch computes (same tile
+// ids, same partial-sum slots), so the split changes no bit of the result.
+struct TileSplit {
+    DBuf<int> tiles;                  // interior tile ids, then boundary tile ids (ascending)
+    int B = 0, n_in = 0, n_bd = 0;
+    bool ready() const { return B > 0; }
+};
+// host-synchronising (once per operator)
+int build_tile_split(hipStream_t s, int n, int B, const int *rowptr, const int *col, TileSplit &ts);
+struct SideStream {
+    hipStream_t cs = nullptr;
+    hipEvent_t a = nullptr, b = nullptr;
+    int init();
+    ~SideStream();
+};
+// XFK_NO_OVERLAP=1 turns the overlap off (exchange, then one launch)
+bool overlap_enabled();
+// exch(side stream) once the main stream's work so far is done; interior()
+// meanwhile on s; boundary() on s after the exchange
+template <class Ex, class In, class Bd>
+int exchange_overlapped(hipStream_t s, SideStream &ss, Ex &&exch, In &&interior, Bd &&boundary)
+{
+    XFK_CHECK(hipEventRecord(ss.a, s));
+    XFK_CHECK(hipStreamWaitEvent(ss.cs, ss.a, 0));
+    const int rc = exch(ss.cs);
+    if (rc != XFK_OK) return rc;
+    XFK_CHECK(hipEventRecord(ss.b, ss.cs));
+    interior();
+    XFK_CHECK(hipStreamWaitEvent(s, ss.b, 0));
+    boundary();
+    return XFK_OK;
+}
+
 }  // namespace xfk
 
 // The opaque problem handle of the C-ABI.
@@ -198,6 +254,8 @@ struct xfk_problem {
     std::vector<int> l2g;            // local node -> global node
     xfk::HaloPlan halo;              // slices of the node vectors exchanged with peers
     int Gpart = 0;                   // length of each per-block partial array (agreed by all ranks)
+    xfk::TileSplit ts;               // sharded PCG SpMV: interior / boundary tiles (exchange overlap)
+    xfk::SideStream side;
 
     // host copies kept for host-side setup (periodic maps)
     std::vector<int> hp, hpbc;

@@ -54,7 +54,7 @@ void launch_cg_axpy(hipStream_t s, const CgAxpyArgs &A);
 // w = A u, partials of u.w (and of r.u into part_gam when R != nullptr)
 void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *U,
                     double *W, double *part_del, const CgState *S, const double *R = nullptr,
-                    double *part_gam = nullptr);
+                    double *part_gam = nullptr, const int *tiles = nullptr, int ntiles = 0);
 void launch_cg_dot(hipStream_t s, int N, const double *a, const double *b, double *part);
 
 void launch_count_incidence(hipStream_t s, int NE, const int *p, int *deg);

@@ -75,12 +75,13 @@ __global__ void __launch_bounds__(kCgBlock) k_cg_spmv(int N, const int *__restri
                                                       const int *__restrict__ col, const double *__restrict__ val,
                                                       const double *__restrict__ U, double *__restrict__ W,
                                                       double *__restrict__ part_del, const CgState *S,
-                                                      const double *__restrict__ R, double *__restrict__ part_gam)
+                                                      const double *__restrict__ R, double *__restrict__ part_gam,
+                                                      const int *__restrict__ tl)
 {
     if (S && S->done) return;
     __shared__ __attribute__((aligned(16))) double lds[kCgCap];
     __shared__ double red[2 * (kCgBlock / 64)];
-    const int t = xcd_tile(blockIdx.x, gridDim.x);
+    const int t = tl ? tl[xcd_tile(blockIdx.x, gridDim.x)] : xcd_tile(blockIdx.x, gridDim.x);
     const int r0 = t * kCgBlock;
     const double w = cg_tile_spmv(r0, N, rowptr, col, val, [&](int j) { return U[j]; }, lds);
     const int r = r0 + threadIdx.x;
@@ -241,9 +242,12 @@ void launch_cg_axpy(hipStream_t s, const CgAxpyArgs &A)
 }
 
 void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *U,
-                    double *W, double *part_del, const CgState *S, const double *R, double *part_gam)
+                    double *W, double *part_del, const CgState *S, const double *R, double *part_gam,
+                    const int *tiles, int ntiles)
 {
-    k_cg_spmv<<<cg_grid(N), kCgBlock, 0, s>>>(N, rowptr, col, val, U, W, part_del, S, R, part_gam);
+    if (tiles && ntiles == 0) return;
+    k_cg_spmv<<<tiles ? ntiles : cg_grid(N), kCgBlock, 0, s>>>(N, rowptr, col, val, U, W, part_del, S, R, part_gam,
+                                                               tiles);
 }
 
 // partials of a.b over the cg_grid(N) layout (the AMG start: (M^-1 b).b)
