@@ -96,7 +96,7 @@ struct Amg {
     // setup scratch (reused across setups)
     DBuf<double> absd, dfinv, wF, rho_part;
     DBuf<unsigned char> sflag;
-    DBuf<unsigned long long> key, t1;
+    DBuf<unsigned> key, t1;           // MIS-2 keys (state:2 | priority:30)
     DBuf<int> cnt, agg1, agg, flag, cursor;
     DBuf<int> ap_row, ap_col;
     DBuf<int> pad_col;                // single-pass SpGEMM: padded rows
@@ -104,6 +104,7 @@ struct Amg {
     DBuf<double> ap_val;
     DBuf<int> dev_int;                // small device scalars (undecided flag, overflow flags)
     std::map<int, int> cap_hint;      // SpGEMM slot capacity of each call site in the last setup
+    std::map<int, int> mis_hint;      // MIS-2 rounds each level needed in the last setup
     int *host_int = nullptr;          // pinned mirror
     DBuf<char> cub_tmp;
 

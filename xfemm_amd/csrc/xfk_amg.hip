@@ -34,27 +34,29 @@ namespace {
 constexpr int kB = 256;
 inline int nb(long long n) { return (int)((n + kB - 1) / kB); }
 
-constexpr unsigned long long kStIn = 2ull, kStUnd = 1ull;   // OUT = 0
+// MIS key: (state:2 | perm(i):30), perm a bijection of [0, 2^30) (odd
+// multipliers and xor-shifts): unique per node, so the max over a
+// neighbourhood picks an IN node first, then the undecided node of the
+// largest pseudo-random priority -- 4-byte keys halve the gathers of the two
+// max sweeps of every round
+using MisKey = unsigned;
+constexpr MisKey kStIn = 2u, kStUnd = 1u;   // OUT = 0
+constexpr MisKey kKeyMask = 0x3FFFFFFFu;
 
-__device__ __forceinline__ unsigned mix32(unsigned x)
+__device__ __forceinline__ MisKey perm30(unsigned x)
 {
-    x ^= x >> 16;
-    x *= 0x7feb352dU;
+    x &= kKeyMask;
+    x = (x * 0x2C1B3C6Du) & kKeyMask;
     x ^= x >> 15;
-    x *= 0x846ca68bU;
-    x ^= x >> 16;
+    x = (x * 0x297A2D39u) & kKeyMask;
+    x ^= x >> 12;
+    x = (x * 0x7FEB352Du) & kKeyMask;
+    x ^= x >> 15;
     return x;
 }
-
-// MIS key: (state:2 | hash(i):30 | i:32); max over a neighbourhood picks an
-// IN node first, then the undecided node with the largest (hash, index)
-__device__ __forceinline__ unsigned long long mis_key(unsigned long long st, int i)
-{
-    return (st << 62) | ((unsigned long long)(mix32((unsigned)i) & 0x3FFFFFFFu) << 32) | (unsigned)i;
-}
-__device__ __forceinline__ int key_idx(unsigned long long k) { return (int)(unsigned)(k & 0xFFFFFFFFull); }
-__device__ __forceinline__ unsigned long long key_st(unsigned long long k) { return k >> 62; }
-__device__ __forceinline__ unsigned long long key_low(unsigned long long k) { return k & ((1ull << 62) - 1); }
+__device__ __forceinline__ MisKey mis_key(MisKey st, int i) { return (st << 30) | perm30((unsigned)i); }
+__device__ __forceinline__ MisKey key_st(MisKey k) { return k >> 30; }
+__device__ __forceinline__ MisKey key_low(MisKey k) { return k & kKeyMask; }
 
 __device__ __forceinline__ double rho_of(const unsigned long long *p)
 {
@@ -202,10 +204,17 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
 // setup: MIS-2 aggregation
 // --------------------------------------------------------------------------
 
-__global__ void k_mis_init(int n, const int *__restrict__ sdeg, unsigned long long *__restrict__ key)
+// also arms the round bookkeeping: "undecided" for the round before the
+// first, no round run yet
+__global__ void k_mis_init(int n, const int *__restrict__ sdeg, MisKey *__restrict__ key, int *und_prev,
+                           int *run)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) key[i] = mis_key(sdeg[i] > 0 ? kStUnd : (sdeg[i] < 0 ? kStIn : 0ull), i);
+    if (i == 0) {
+        *und_prev = 1;
+        *run = 0;
+    }
+    if (i < n) key[i] = mis_key(sdeg[i] > 0 ? kStUnd : (sdeg[i] < 0 ? kStIn : 0u), i);
 }
 
 // Rounds are launched in batches without a host check in between: the
@@ -213,13 +222,16 @@ __global__ void k_mis_init(int n, const int *__restrict__ sdeg, unsigned long lo
 // result, cur = this round's), and once a round leaves nothing undecided the
 // later rounds of the batch exit at once (passing the 0 on).
 __global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
-                          const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ in,
-                          unsigned long long *__restrict__ out, const int *prev, int *cur)
+                          const unsigned char *__restrict__ sflag, const MisKey *__restrict__ in,
+                          MisKey *__restrict__ out, const int *prev, int *cur, int *run)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) *cur = 0;   // k_mis_update of this round runs after this launch
+    if (i == 0) {   // k_mis_update of this round runs after this launch
+        if (*prev != 0) *run += 1;   // rounds that did work (the next setup's batch size)
+        *cur = 0;
+    }
     if (i >= n || *prev == 0) return;
-    unsigned long long m = in[i];
+    MisKey m = in[i];
     for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
         if (sflag[k] == 1) m = max(m, in[col[k]]);
     out[i] = m;
@@ -229,22 +241,22 @@ __global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__re
 // distance-2 maximum is itself joins the set; one that sees a set member
 // within distance 2 leaves
 __global__ void k_mis_update(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
-                             const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ t1,
-                             unsigned long long *__restrict__ key, const int *prev, int *undecided)
+                             const unsigned char *__restrict__ sflag, const MisKey *__restrict__ t1,
+                             MisKey *__restrict__ key, const int *prev, int *undecided)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || *prev == 0) return;
-    const unsigned long long k = key[i];
+    const MisKey k = key[i];
     if (key_st(k) != kStUnd) return;
-    unsigned long long m = t1[i];
+    MisKey m = t1[i];
     for (int q = rowptr[i]; q < rowptr[i + 1]; ++q)
         if (sflag[q] == 1) m = max(m, t1[col[q]]);
-    if (key_idx(m) == i) key[i] = (kStIn << 62) | key_low(k);
+    if (key_low(m) == perm30((unsigned)i)) key[i] = (kStIn << 30) | key_low(k);
     else if (key_st(m) == kStIn) key[i] = key_low(k);
     else *undecided = 1;   // benign race: every writer stores 1
 }
 
-__global__ void k_agg_roots(int n, const unsigned long long *__restrict__ key, int *__restrict__ flag)
+__global__ void k_agg_roots(int n, const MisKey *__restrict__ key, int *__restrict__ flag)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) flag[i] = key_st(key[i]) == kStIn;
@@ -279,7 +291,7 @@ __global__ void k_agg_join3(int n, int ncl, const int *__restrict__ rowptr, cons
 }
 
 __global__ void k_agg_join1(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
-                            const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ key,
+                            const unsigned char *__restrict__ sflag, const MisKey *__restrict__ key,
                             const int *__restrict__ rootid, int *__restrict__ agg1)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -289,11 +301,11 @@ __global__ void k_agg_join1(int n, const int *__restrict__ rowptr, const int *__
         return;
     }
     int bj = -1;
-    unsigned long long best = 0;
+    MisKey best = 0;
     for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
         if (sflag[k] != 1) continue;
         const int j = col[k];
-        const unsigned long long kj = key[j];
+        const MisKey kj = key[j];
         if (key_st(kj) == kStIn && (bj < 0 || key_low(kj) > best)) {
             best = key_low(kj);
             bj = j;
@@ -305,7 +317,7 @@ __global__ void k_agg_join1(int n, const int *__restrict__ rowptr, const int *__
 // distance 2: the rest join the aggregate of their largest-key neighbour
 // that joined at distance 1
 __global__ void k_agg_join2(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
-                            const unsigned char *__restrict__ sflag, const unsigned long long *__restrict__ key,
+                            const unsigned char *__restrict__ sflag, const MisKey *__restrict__ key,
                             const int *__restrict__ agg1, int *__restrict__ agg)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -316,12 +328,12 @@ __global__ void k_agg_join2(int n, const int *__restrict__ rowptr, const int *__
         return;
     }
     int bj = -1;
-    unsigned long long best = 0;
+    MisKey best = 0;
     for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
         if (sflag[k] != 1) continue;
         const int j = col[k];
         if (agg1[j] < 0) continue;
-        const unsigned long long kl = key_low(key[j]);
+        const MisKey kl = key_low(key[j]);
         if (bj < 0 || kl > best) {
             best = kl;
             bj = j;
@@ -341,14 +353,16 @@ __global__ void k_rt_count(int n, const int *__restrict__ prow, const int *__res
     for (int k = prow[i]; k < prow[i + 1]; ++k) atomicAdd(&rcnt[pcol[k]], 1);
 }
 
+// the counts left by k_rt_count count down to each row's free slot (no
+// zeroed cursor array needed)
 __global__ void k_rt_fill(int n, const int *__restrict__ prow, const int *__restrict__ pcol,
-                          const int *__restrict__ rrow, int *__restrict__ cursor, int *__restrict__ rcol)
+                          const int *__restrict__ rrow, int *__restrict__ cnt, int *__restrict__ rcol)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     for (int k = prow[i]; k < prow[i + 1]; ++k) {
         const int J = pcol[k];
-        rcol[rrow[J] + atomicAdd(&cursor[J], 1)] = i;
+        rcol[rrow[J] + atomicSub(&cnt[J], 1) - 1] = i;
     }
 }
 
@@ -1829,32 +1843,41 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     AMG_CHECK(t1.alloc(n));
     const std::string lv = g_prof ? "setup L" + std::to_string(l) + " " : std::string();
     if (g_prof) g_prof->begin(lv + "MIS-2 aggregation", 0.0);
-    k_mis_init<<<nb(n), kB, 0, s>>>(n, cnt.p, key.p);
     int rounds = 0;
     int *und2 = dev_int.p + 4;   // undecided flag of rounds of parity 0 / 1
-    AMG_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(und2 + 1), 1, 1, s));
-    // (level sizes here need 10-16 rounds: one host check for most levels)
-    for (int batch = 12;; batch = 4) {
+    int *run = dev_int.p + 7;    // rounds that did work
+    k_mis_init<<<std::max(1, nb(n)), kB, 0, s>>>(n, cnt.p, key.p, und2 + 1, run);
+    AMG_CHECK(flag.alloc((size_t)n + 1));
+    AMG_CHECK(cursor.alloc((size_t)n + 1));
+    // Batches of rounds without a host check; the first batch is the round
+    // count this level needed in the last setup (the same matrix family
+    // needs the same count: one host check in the usual case, no idle
+    // rounds), 12 without one.  Roots and their numbering are formed
+    // speculatively after each batch and read back in the same host check.
+    auto hint = mis_hint.find(l);
+    for (int batch = hint != mis_hint.end() ? std::max(1, hint->second) : 12;; batch = 2) {
         for (int b = 0; b < batch; ++b, ++rounds) {
             int *cur = und2 + (rounds & 1), *prev = und2 + ((rounds + 1) & 1);
-            k_mis_max<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur);
+            k_mis_max<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur, run);
             k_mis_update<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, prev, cur);
         }
-        int und = 0;
-        int rc = read_flag(*this, s, 4 + ((rounds - 1) & 1), und);
+        k_agg_roots<<<nb(n), kB, 0, s>>>(n, key.p, flag.p);
+        int rc = scan_only(*this, s, flag.p, cursor.p, n);   // cursor = root ids
         if (rc != XFK_OK) return rc;
-        if (!und) break;
+        AMG_CHECK(hipMemcpyAsync(host_int + 1, und2 + ((rounds - 1) & 1), sizeof(int), hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipMemcpyAsync(host_int + 5, run, sizeof(int), hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipMemcpyAsync(host_int, cursor.p + n, sizeof(int), hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipStreamSynchronize(s));
+        if (!host_int[1]) break;
         if (rounds > 4096) {
             set_error("AMG: MIS-2 aggregation did not terminate");
             return XFK_ERR_NOCONV;
         }
     }
-    stats.mis_rounds[l] = rounds;
-    AMG_CHECK(flag.alloc((size_t)n + 1));
-    AMG_CHECK(cursor.alloc((size_t)n + 1));
-    k_agg_roots<<<nb(n), kB, 0, s>>>(n, key.p, flag.p);
-    int rc = scan_total(*this, s, flag.p, cursor.p, n, nc);   // cursor = root ids
-    if (rc != XFK_OK) return rc;
+    mis_hint[l] = host_int[5];
+    nc = host_int[0];
+    stats.mis_rounds[l] = host_int[5];
+    int rc = XFK_OK;
     if (allow_stop && (nc == 0 || nc > (long long)(0.9 * n))) {   // no useful coarsening: smoother-only coarsest
         nc = 0;
         return XFK_OK;
@@ -1901,8 +1924,7 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     if ((rc = scan_only(*this, s, cnt.p, A.rrow.p, (int)nc)) != XFK_OK) return rc;
     AMG_CHECK(A.rcol.alloc((size_t)std::max(1LL, rnnz)));
     AMG_CHECK(A.rval.alloc((size_t)std::max(1LL, rnnz)));
-    AMG_CHECK(hipMemsetAsync(cursor.p, 0, sizeof(int) * (nc + 1), s));
-    k_rt_fill<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, A.rrow.p, cursor.p, A.rcol.p);
+    k_rt_fill<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, A.rrow.p, cnt.p, A.rcol.p);
     if (nc > 0)
         k_rt_sort_vals<<<(int)((nc * 64 + 255) / 256), 256, 0, s>>>((int)nc, A.rrow.p, A.rcol.p, A.prow.p, A.pcol.p,
                                                                    A.pval.p, A.rval.p);
