@@ -145,11 +145,15 @@ def test_standalone_amg_pcg(n):
         assert it <= 2
 
 
-@pytest.mark.parametrize("n", [30, 45])
-def test_dense_coarsest_blocked_inverse(n):
+@pytest.mark.parametrize("n,nd", [(20, True), (30, True), (45, True), (45, False)])
+def test_dense_coarsest_blocked_inverse(monkeypatch, n, nd):
     """n*n <= 2048 rows: the whole matrix is the dense coarsest level, inverted
     by blocked Gauss-Jordan (several 64-wide block columns, ragged last block):
-    PCG converges in one step to the direct solution."""
+    PCG converges in one step to the direct solution.  From 512 rows on the
+    level is reordered by nested dissection (two parts eliminated side by
+    side, then the separator); XFK_NO_ND=1 keeps the plain order."""
+    if not nd:
+        monkeypatch.setenv("XFK_NO_ND", "1")
     M = _laplace_random(n, 7)
     b = np.random.default_rng(2).standard_normal(M.shape[0])
     V, it, er = kernels.pcg_solve_csr(M.indptr, M.indices, M.data, b, precision=1e-12, precond="amg")

@@ -256,7 +256,7 @@ int main()
         double *Rs[2] = {tmp, tmp + (size_t)nbk * T2}, *Cs[2] = {tmp + 2 * (size_t)nbk * T2, tmp + 3 * (size_t)nbk * T2};
         auto new_gj = [&] {
             reset();
-            k_bgj_snap0<<<2 * nbk, 256, 0, s>>>(nbk, ld, dM, Rs[0], Cs[0]);
+            k_bgj_snap<<<2 * nbk, 256, 0, s>>>(0, nbk, ld, dM, Rs[0], Cs[0]);
             k_bgj_diag<<<1, 256, 0, s>>>(0, ld, dM, maxd, Dbuf);
             for (int k = 0; k < nbk; ++k) {
                 const int p = k & 1, q = (k + 1) & 1;

@@ -89,6 +89,9 @@ struct Amg {
     bool dense_coarse = false;
     DBuf<double> cinv;                // dense inverse of the coarsest level (row major, padded)
     int cinv_ld = 0;
+    DBuf<double> cinv_o;              // nested-dissection order: the other buffer of the unpermute
+    DBuf<int> cinv_perm, cinv_iperm, nd_tiles;
+    int nd_ntiles = 0;
     DBuf<double> bgj_tmp;             // blocked Gauss-Jordan panels
     DBuf<unsigned long long> rho;     // per level {rho_A, rho_F} as ordered bit patterns
     AmgStats stats;
@@ -164,6 +167,7 @@ struct Amg {
     int galerkin_dist(hipStream_t s, int l, int st, bool &rep);
     double *vc_dist(hipStream_t s, int l, const double *b, double *out, const int *done, int &rc);
     int host_ints(int count);
+    int nd_order(hipStream_t s, const AmgLevel &C, int &nbh, int &ld);
 };
 
 }  // namespace xfk

@@ -898,31 +898,39 @@ __global__ void k_spgemm_compact(int nrows, int cap, const int *__restrict__ cro
 constexpr int kBj = 64;
 
 // the matrix has been zeroed (hipMemsetAsync); entries of row i, identity tail
-// symmetric diagonal scaling sc_i = 1 / sqrt(a_ii) (1 for a zero diagonal
-// and the identity tail): the scaled matrix has unit diagonal, so every
-// Gauss-Jordan pivot (a Schur-complement diagonal) lies in (0, 1]
+// symmetric diagonal scaling sc_q = 1 / sqrt(a_qq) (1 for a zero diagonal
+// and the padding rows): the scaled matrix has unit diagonal, so every
+// Gauss-Jordan pivot (a Schur-complement diagonal) lies in (0, 1].
+// perm / iperm (nested-dissection order, nullptr: identity): dense index of
+// coarse row r is perm[r]; iperm[q] the coarse row of dense index q (-1: padding)
 __global__ void k_dense_dscale(int n, int ld, const int *__restrict__ rowptr, const int *__restrict__ col,
-                               const double *__restrict__ val, double *__restrict__ sc)
+                               const double *__restrict__ val, const int *__restrict__ iperm, double *__restrict__ sc)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= ld) return;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= ld) return;
+    const int i = iperm ? iperm[q] : (q < n ? q : -1);
     double d = 0.0;
-    if (i < n)
+    if (i >= 0)
         for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
             if (col[k] == i) d += val[k];
-    sc[i] = d > 0.0 ? 1.0 / sqrt(d) : 1.0;
+    sc[q] = d > 0.0 ? 1.0 / sqrt(d) : 1.0;
 }
 __global__ void k_dense_scatter(int n, int ld, const int *__restrict__ rowptr, const int *__restrict__ col,
-                                const double *__restrict__ val, const double *__restrict__ sc, double *__restrict__ M)
+                                const double *__restrict__ val, const int *__restrict__ perm,
+                                const int *__restrict__ iperm, const double *__restrict__ sc, double *__restrict__ M)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= ld) return;
-    if (i >= n) {
-        M[(size_t)i * ld + i] = 1.0;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= ld) return;
+    const int i = iperm ? iperm[q] : (q < n ? q : -1);
+    if (i < 0) {
+        M[(size_t)q * ld + q] = 1.0;
         return;
     }
-    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
-        if (col[k] < n) M[(size_t)i * ld + col[k]] += val[k] * sc[i] * sc[col[k]];
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        if (col[k] >= n) continue;
+        const int c = perm ? perm[col[k]] : col[k];
+        M[(size_t)q * ld + c] += val[k] * sc[q] * sc[c];
+    }
 }
 // inv(A) = S inv(S A S) S
 __global__ void k_dense_unscale(int ld, double *__restrict__ M, const double *__restrict__ sc)
@@ -936,6 +944,25 @@ __global__ void k_dense_unscale(int ld, double *__restrict__ M, const double *__
     v.x *= sc[i] * sc[j];
     v.y *= sc[i] * sc[j + 1];
     *p = v;
+}
+
+// nested-dissection order back to the coarse numbering, unscaled:
+// out[iperm q][iperm r] = M[q][r] sc_q sc_r (out: n rows of ldo, the padding
+// columns n .. ldo-1 zero), so the V-cycle's apply reads plain rows
+__global__ void __launch_bounds__(256) k_dense_unperm(int n, int ld, int ldo, const double *__restrict__ M,
+                                                      const double *__restrict__ sc, const int *__restrict__ iperm,
+                                                      double *__restrict__ out)
+{
+    const int q = blockIdx.x;
+    const int i = iperm[q];
+    if (i < 0) return;
+    const double sq = sc[q];
+    double *o = out + (size_t)i * ldo;
+    for (int r = threadIdx.x; r < ld; r += blockDim.x) {
+        const int j = iperm[r];
+        if (j >= 0) o[j] = M[(size_t)q * ld + r] * sq * sc[r];
+    }
+    for (int c = n + threadIdx.x; c < ldo; c += blockDim.x) o[c] = 0.0;
 }
 
 __global__ void __launch_bounds__(1024) k_dense_maxdiag(int n, int ld, const double *__restrict__ M,
@@ -1102,15 +1129,17 @@ __global__ void __launch_bounds__(256) k_bgj_diag(int k, int ld, const double *_
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 constexpr int kXs = 66, kYs = 80;
 
+template <bool ZERO = true>
 __device__ __forceinline__ void bgj_mm(const double *__restrict__ Xs, const double *__restrict__ Ys, dbl4 (&c)[2][2])
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r0 = 32 * (w >> 1), c0 = 32 * (w & 1);
     const int li = lane & 15, lk = lane >> 4;
+    if (ZERO)
 #pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
+        for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
-        for (int tj = 0; tj < 2; ++tj) c[ti][tj] = dbl4{0.0, 0.0, 0.0, 0.0};
+            for (int tj = 0; tj < 2; ++tj) c[ti][tj] = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
     for (int s = 0; s < kBj / 4; ++s) {
         double a[2], b[2];
@@ -1163,13 +1192,14 @@ __device__ __forceinline__ void bgj_load(double *__restrict__ dst, const double 
 // (k+1, k+1) -- the next pivot block -- and inverts it into Dn once written.
 // The chain per step is one launch: the pivot workgroup's two tile GEMMs and
 // the 64 x 64 inversion.
-__global__ void __launch_bounds__(256) k_bgj_snap0(int nbk, int ld, const double *__restrict__ M,
-                                                   double *__restrict__ R0, double *__restrict__ C0)
+// snapshots of row k (R[j] = M_kj) and column k (C[i] = M_ik) before step k
+__global__ void __launch_bounds__(256) k_bgj_snap(int k, int nbk, int ld, const double *__restrict__ M,
+                                                  double *__restrict__ R, double *__restrict__ C)
 {
     const int t = blockIdx.x % nbk;
     const bool row = blockIdx.x < nbk;
-    const double *src = row ? M + (size_t)t * kBj : M + (size_t)t * kBj * ld;   // tile (0, t) or (t, 0)
-    double *dst = (row ? R0 : C0) + (size_t)t * kBj * kBj;
+    const double *src = row ? M + (size_t)k * kBj * ld + (size_t)t * kBj : M + (size_t)t * kBj * ld + (size_t)k * kBj;
+    double *dst = (row ? R : C) + (size_t)t * kBj * kBj;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int e = threadIdx.x + 256 * q, r = e >> 5, c = 2 * (e & 31);
@@ -1269,6 +1299,142 @@ __global__ void __launch_bounds__(256) k_bgj_step(int k, int nbk, int ld, double
     bgj_diag_inv(a, 1e-11 * (*maxd), Ys);
 #pragma unroll
     for (int m = 0; m < 16; ++m) Dn[(16 * w + m) * kBj + jl] = a[m];
+}
+
+// Nested-dissection steps.  The coarsest operator, reordered as [part 1 |
+// part 2 | separator] (blocks [0, nb), [nb, 2 nb), [2 nb, nbk)), has no entry
+// between the two parts, and Gauss-Jordan keeps it so: eliminating a block
+// column of part 1 touches only tiles of (part 1 + separator)^2, one of part 2
+// only (part 2 + separator)^2, and the two updates commute.  Step t
+// eliminates blocks t and nb + t in one launch -- two pivot chains side by
+// side, half the chain length -- each tile applying the update of every
+// chain whose region holds it (separator tiles: both, summed on the MFMA in
+// chain order).  The separator's blocks then follow with k_bgj_step.
+struct BgjChain {
+    int k;                       // pivot block of this step
+    int nx;                      // next pivot block of the chain (-1: none)
+    const double *D, *R, *C;     // inv(M_kk), row / column snapshots of step k
+    double *Dn, *Rn, *Cn;        // the same for the next pivot
+};
+
+__global__ void __launch_bounds__(256, 2) k_bgj_dual(int nb, int nbk, int ld, double *__restrict__ M, BgjChain c1,
+                                                  BgjChain c2, const int *__restrict__ tiles, const double *maxd)
+{
+    const size_t T2 = (size_t)kBj * kBj;
+    // workgroups 0 (and 1) finalise the next pivot blocks and invert them
+    const int np = (c1.nx >= 0) + (c2.nx >= 0 && c2.nx != c1.nx);
+    int i, j;
+    double *Dpiv = nullptr;
+    if ((int)blockIdx.x < np) {
+        const bool first = blockIdx.x == 0 && c1.nx >= 0;
+        i = j = first ? c1.nx : c2.nx;
+        Dpiv = first ? c1.Dn : c2.Dn;
+    } else {
+        const int t = tiles[blockIdx.x - np];
+        i = t / nbk;
+        j = t % nbk;
+        if ((i == j) && (i == c1.nx || i == c2.nx)) return;   // taken by a pivot workgroup
+    }
+    const bool a1 = (i < nb || i >= 2 * nb) && (j < nb || j >= 2 * nb);
+    const bool a2 = i >= nb && j >= nb;
+    __shared__ __attribute__((aligned(16))) double Xs[kBj * kXs];
+    __shared__ __attribute__((aligned(16))) double Ys[kBj * kYs];
+    double *Mij = M + (size_t)i * kBj * ld + (size_t)j * kBj;
+    // (chain fields selected into scalars: a pointer to a by-value kernel
+    // argument would put the arguments in scratch memory)
+    const bool p1 = a1 && (i == c1.k || j == c1.k), p2 = !p1 && a2 && (i == c2.k || j == c2.k);
+    const int pk = p1 ? c1.k : c2.k;
+    const double *pD = p1 ? c1.D : c2.D, *pR = p1 ? c1.R : c2.R, *pC = p1 ? c1.C : c2.C;
+    if ((p1 || p2) && i == pk && j == pk) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = threadIdx.x + 256 * q, r = e >> 5, c = 2 * (e & 31);
+            *reinterpret_cast<double2 *>(Mij + (size_t)r * ld + c) = *reinterpret_cast<const double2 *>(pD + r * kBj + c);
+        }
+        return;
+    }
+    dbl4 acc[2][2];
+    double sgn = 1.0;
+    bool rmw = false;
+    if ((p1 || p2) && i == pk) {   // row of a pivot: D R[j]
+        bgj_load<kXs>(Xs, pD, kBj);
+        bgj_load<kYs>(Ys, pR + j * T2, kBj);
+        __syncthreads();
+        bgj_mm(Xs, Ys, acc);
+    } else if (p1 || p2) {         // column of a pivot: -C[i] D
+        bgj_load<kXs>(Xs, pC + i * T2, kBj);
+        bgj_load<kYs>(Ys, pD, kBj);
+        __syncthreads();
+        bgj_mm(Xs, Ys, acc);
+        sgn = -1.0;
+    } else {                       // M_ij - sum over the chains holding the tile of C[i] (D R[j])
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = dbl4{0.0, 0.0, 0.0, 0.0};
+        for (int q = 0; q < 2; ++q) {
+            if (!(q == 0 ? a1 : a2)) continue;
+            const double *chD = q == 0 ? c1.D : c2.D, *chR = q == 0 ? c1.R : c2.R;
+            double2 pre[8];
+            const double *Ci = (q == 0 ? c1.C : c2.C) + i * T2;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = threadIdx.x + 256 * u, r = e >> 5, cc = 2 * (e & 31);
+                pre[u] = *reinterpret_cast<const double2 *>(Ci + r * kBj + cc);
+            }
+            __syncthreads();   // LDS of the previous chain's product is free
+            bgj_load<kXs>(Xs, chD, kBj);
+            bgj_load<kYs>(Ys, chR + j * T2, kBj);
+            __syncthreads();
+            dbl4 t[2][2];
+            bgj_mm(Xs, Ys, t);
+            __syncthreads();
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) Ys[bgj_row(ti, r) * kYs + bgj_col(tj)] = t[ti][tj][r];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = threadIdx.x + 256 * u, r = e >> 5, cc = 2 * (e & 31);
+                Xs[r * kXs + cc] = pre[u].x;
+                Xs[r * kXs + cc + 1] = pre[u].y;
+            }
+            __syncthreads();
+            bgj_mm<false>(Xs, Ys, acc);
+        }
+        rmw = true;
+    }
+    double *r1 = (i == c1.nx) ? c1.Rn + j * T2 : nullptr, *k1 = (j == c1.nx) ? c1.Cn + i * T2 : nullptr;
+    const bool own2 = c2.nx != c1.nx;
+    double *r2 = (own2 && i == c2.nx) ? c2.Rn + j * T2 : nullptr, *k2 = (own2 && j == c2.nx) ? c2.Cn + i * T2 : nullptr;
+    if (Dpiv) __syncthreads();   // Xs is reused below
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = bgj_row(ti, r), col = bgj_col(tj);
+                double *e = &Mij[(size_t)row * ld + col];
+                const double v = rmw ? *e - acc[ti][tj][r] : sgn * acc[ti][tj][r];
+                *e = v;
+                if (r1) r1[row * kBj + col] = v;
+                if (k1) k1[row * kBj + col] = v;
+                if (r2) r2[row * kBj + col] = v;
+                if (k2) k2[row * kBj + col] = v;
+                if (Dpiv) Xs[row * kBj + col] = v;
+            }
+    if (!Dpiv) return;
+    __syncthreads();
+    const int jl = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double a[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) a[m] = Xs[(16 * w + m) * kBj + jl];
+    bgj_diag_inv(a, 1e-11 * (*maxd), Ys);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) Dpiv[(16 * w + m) * kBj + jl] = a[m];
 }
 
 // --------------------------------------------------------------------------
@@ -1932,6 +2098,60 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     return XFK_OK;
 }
 
+// Nested-dissection order of the coarsest level for the dense inverse: part 1
+// = rows [0, m), part 2 = rows >= m without a column < m, separator = rows >=
+// m with one (the levels are numbered along the fine level's Cuthill-McKee
+// order, so the coupling across m is a band of about one grid line).  Parts
+// padded to nbh blocks each, the separator to whole blocks; padding rows are
+// identity rows.  nbh = 0 keeps the plain order (small levels, or a
+// separator of more than a quarter of the rows).  Host-synchronising.
+int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &nbh, int &ld)
+{
+    const int n = C.n;
+    nbh = 0;
+    ld = ((n + kBj - 1) / kBj) * kBj;
+    if (n < 8 * kBj || std::getenv("XFK_NO_ND")) return XFK_OK;
+    std::vector<int> rp(n + 1), cl((size_t)C.nnz);
+    AMG_CHECK(hipMemcpyAsync(rp.data(), C.rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost, s));
+    AMG_CHECK(hipMemcpyAsync(cl.data(), C.col, sizeof(int) * C.nnz, hipMemcpyDeviceToHost, s));
+    AMG_CHECK(hipStreamSynchronize(s));
+    const int m = kBj * std::max(1, (int)std::lround(n / (2.0 * kBj)));
+    std::vector<int> part2, sepr;
+    for (int r = m; r < n; ++r) {
+        bool cross = false;
+        for (int k = rp[r]; k < rp[r + 1] && !cross; ++k) cross = cl[k] < m;
+        (cross ? sepr : part2).push_back(r);
+    }
+    const int m2 = (int)part2.size(), ms = (int)sepr.size();
+    if (m2 == 0 || 4 * ms > n) return XFK_OK;
+    nbh = (std::max(m, m2) + kBj - 1) / kBj;
+    const int P = nbh * kBj;
+    ld = 2 * P + ((ms + kBj - 1) / kBj) * kBj;
+    std::vector<int> perm(n), iperm(ld, -1);
+    for (int r = 0; r < m; ++r) perm[r] = r;
+    for (int t = 0; t < m2; ++t) perm[part2[t]] = P + t;
+    for (int t = 0; t < ms; ++t) perm[sepr[t]] = 2 * P + t;
+    for (int r = 0; r < n; ++r) iperm[perm[r]] = r;
+    AMG_CHECK(cinv_perm.alloc(n));
+    AMG_CHECK(cinv_iperm.alloc(ld));
+    AMG_CHECK(hipMemcpyAsync(cinv_perm.p, perm.data(), sizeof(int) * n, hipMemcpyHostToDevice, s));
+    AMG_CHECK(hipMemcpyAsync(cinv_iperm.p, iperm.data(), sizeof(int) * ld, hipMemcpyHostToDevice, s));
+    // the tiles of (part 1 + separator)^2 and (part 2 + separator)^2
+    const int nbk = ld / kBj;
+    std::vector<int> tl;
+    for (int i = 0; i < nbk; ++i)
+        for (int j = 0; j < nbk; ++j) {
+            const bool a1 = (i < nbh || i >= 2 * nbh) && (j < nbh || j >= 2 * nbh);
+            const bool a2 = i >= nbh && j >= nbh;
+            if (a1 || a2) tl.push_back(i * nbk + j);
+        }
+    nd_ntiles = (int)tl.size();
+    AMG_CHECK(nd_tiles.alloc(tl.size()));
+    AMG_CHECK(hipMemcpyAsync(nd_tiles.p, tl.data(), sizeof(int) * tl.size(), hipMemcpyHostToDevice, s));
+    AMG_CHECK(hipStreamSynchronize(s));   // host vectors go out of scope
+    return XFK_OK;
+}
+
 // levels l0.. of the hierarchy (L[l0] set up by the caller), then the
 // smoother vectors and the dense coarsest inverse
 int Amg::build(hipStream_t s, int l0)
@@ -2007,34 +2227,70 @@ int Amg::build(hipStream_t s, int l0)
     }
     if (dense_coarse) {
         AmgLevel &C = *L[nlev - 1];
-        const int nbk = (C.n + kBj - 1) / kBj, ld = nbk * kBj;
         if (g_prof) g_prof->begin("setup L" + std::to_string(nlev - 1) + " dense inverse (blocked Gauss-Jordan)", 0.0);
+        int nbh = 0, ld = 0;   // nested dissection: blocks per part (0: plain order)
+        int rc = nd_order(s, C, nbh, ld);
+        if (rc != XFK_OK) return rc;
+        const int nbk = ld / kBj;
         cinv_ld = ld;
         AMG_CHECK(cinv.alloc((size_t)ld * ld));
         const size_t T2 = (size_t)kBj * kBj;
-        AMG_CHECK(bgj_tmp.alloc(4 * (size_t)nbk * T2 + 2 * T2 + 1 + ld));
-        double *Rs[2] = {bgj_tmp.p, bgj_tmp.p + (size_t)nbk * T2};
-        double *Cs[2] = {bgj_tmp.p + 2 * (size_t)nbk * T2, bgj_tmp.p + 3 * (size_t)nbk * T2};
-        double *Dbuf = bgj_tmp.p + 4 * (size_t)nbk * T2;
-        double *maxd = Dbuf + 2 * T2, *sc = maxd + 1;
+        // per chain: double-buffered row / column snapshots and pivot inverses
+        AMG_CHECK(bgj_tmp.alloc(8 * (size_t)nbk * T2 + 4 * T2 + 1 + ld));
+        double *Rs[2][2], *Cs[2][2], *Ds[2][2];
+        for (int c = 0; c < 2; ++c)
+            for (int q = 0; q < 2; ++q) {
+                Rs[c][q] = bgj_tmp.p + (size_t)(4 * c + q) * nbk * T2;
+                Cs[c][q] = bgj_tmp.p + (size_t)(4 * c + 2 + q) * nbk * T2;
+                Ds[c][q] = bgj_tmp.p + 8 * (size_t)nbk * T2 + (size_t)(2 * c + q) * T2;
+            }
+        double *maxd = bgj_tmp.p + 8 * (size_t)nbk * T2 + 4 * T2, *sc = maxd + 1;
+        const int *pm = nbh ? cinv_perm.p : nullptr, *ipm = nbh ? cinv_iperm.p : nullptr;
         AMG_CHECK(hipMemsetAsync(cinv.p, 0, sizeof(double) * (size_t)ld * ld, s));
-        k_dense_dscale<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, sc);
-        k_dense_scatter<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, sc, cinv.p);
-        k_dense_maxdiag<<<1, 1024, 0, s>>>(C.n, ld, cinv.p, maxd);
+        k_dense_dscale<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, ipm, sc);
+        k_dense_scatter<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, pm, ipm, sc, cinv.p);
+        k_dense_maxdiag<<<1, 1024, 0, s>>>(ld, ld, cinv.p, maxd);
         // (a lookahead variant -- block column k+1 first, its pivot block
         // inverted on a second stream during the rest of the update -- was
         // measured slower: the two cross-stream waits cost ~15 us per step,
-        // more than the 25 us pivot-block inversion it hides.  The separate
-        // row launch of T_k = D_k M_k: is gone: every tile recomputes its
-        // T_kj, 1130 -> 1070 us at 1600 rows, tools/lab/gj_lab.hip)
-        k_bgj_snap0<<<2 * nbk, 256, 0, s>>>(nbk, ld, cinv.p, Rs[0], Cs[0]);
-        k_bgj_diag<<<1, 256, 0, s>>>(0, ld, cinv.p, maxd, Dbuf);
-        for (int k = 0; k < nbk; ++k) {
-            const int p = k & 1, q = (k + 1) & 1;
-            k_bgj_step<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, Dbuf + p * T2, Rs[p], Cs[p], Dbuf + q * T2, Rs[q],
-                                                 Cs[q], maxd);
+        // more than the 25 us pivot-block inversion it hides)
+        int k0 = 0, par = 0;   // first single-chain step, its buffer parity
+        if (nbh) {
+            // the two parts side by side: steps t = 0 .. nbh-1 eliminate blocks t and nbh + t
+            k_bgj_snap<<<2 * nbk, 256, 0, s>>>(0, nbk, ld, cinv.p, Rs[0][0], Cs[0][0]);
+            k_bgj_snap<<<2 * nbk, 256, 0, s>>>(nbh, nbk, ld, cinv.p, Rs[1][0], Cs[1][0]);
+            k_bgj_diag<<<1, 256, 0, s>>>(0, ld, cinv.p, maxd, Ds[0][0]);
+            k_bgj_diag<<<1, 256, 0, s>>>(nbh, ld, cinv.p, maxd, Ds[1][0]);
+            const int sep = 2 * nbh < nbk ? 2 * nbh : -1;   // first separator block
+            for (int t = 0; t < nbh; ++t) {
+                const int p = t & 1, q = (t + 1) & 1;
+                const bool last = t + 1 == nbh;
+                BgjChain c1{t, last ? sep : t + 1, Ds[0][p], Rs[0][p], Cs[0][p], Ds[0][q], Rs[0][q], Cs[0][q]};
+                BgjChain c2{nbh + t, last ? sep : nbh + t + 1, Ds[1][p], Rs[1][p], Cs[1][p], Ds[1][q], Rs[1][q], Cs[1][q]};
+                const int np = (c1.nx >= 0) + (c2.nx >= 0 && c2.nx != c1.nx);
+                k_bgj_dual<<<nd_ntiles + np, 256, 0, s>>>(nbh, nbk, ld, cinv.p, c1, c2, nd_tiles.p, maxd);
+            }
+            k0 = 2 * nbh;
+            par = nbh & 1;   // the separator's first snapshots are chain 1's of parity nbh & 1
+        } else {
+            k_bgj_snap<<<2 * nbk, 256, 0, s>>>(0, nbk, ld, cinv.p, Rs[0][0], Cs[0][0]);
+            k_bgj_diag<<<1, 256, 0, s>>>(0, ld, cinv.p, maxd, Ds[0][0]);
         }
-        k_dense_unscale<<<(unsigned)(((size_t)ld * ld / 2 + 255) / 256), 256, 0, s>>>(ld, cinv.p, sc);
+        for (int k = k0; k < nbk; ++k) {
+            const int p = (par + k - k0) & 1, q = (par + k - k0 + 1) & 1;
+            k_bgj_step<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, Ds[0][p], Rs[0][p], Cs[0][p], Ds[0][q],
+                                                 Rs[0][q], Cs[0][q], maxd);
+        }
+        if (nbh) {
+            const int ldo = ((C.n + kBj - 1) / kBj) * kBj;
+            AMG_CHECK(cinv_o.alloc((size_t)ldo * ldo));
+            k_dense_unperm<<<ld, 256, 0, s>>>(C.n, ld, ldo, cinv.p, sc, cinv_iperm.p, cinv_o.p);
+            std::swap(cinv.p, cinv_o.p);
+            std::swap(cinv.n, cinv_o.n);
+            cinv_ld = ldo;
+        } else {
+            k_dense_unscale<<<(unsigned)(((size_t)ld * ld / 2 + 255) / 256), 256, 0, s>>>(ld, cinv.p, sc);
+        }
         if (g_prof) g_prof->end();
     }
     AMG_CHECK(hipGetLastError());
