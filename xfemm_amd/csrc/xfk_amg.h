@@ -91,7 +91,13 @@ struct Amg {
     int cinv_ld = 0;
     DBuf<double> cinv_o;              // nested-dissection order: the other buffer of the unpermute
     DBuf<int> cinv_perm, cinv_iperm, nd_tiles;
-    int nd_ntiles = 0;
+    DBuf<unsigned char> nd_mask;
+    struct NdPhase {                  // one tree level of the nested-dissection order
+        int nch = 0, steps = 0;       // pivot chains (<= 4) and their block steps
+        int base[4] = {}, next_slot[4] = {};
+        int tiles_off = 0, ntiles = 0;
+    };
+    std::vector<NdPhase> nd_phases;
     DBuf<double> bgj_tmp;             // blocked Gauss-Jordan panels
     DBuf<unsigned long long> rho;     // per level {rho_A, rho_F} as ordered bit patterns
     AmgStats stats;
@@ -167,7 +173,7 @@ struct Amg {
     int galerkin_dist(hipStream_t s, int l, int st, bool &rep);
     double *vc_dist(hipStream_t s, int l, const double *b, double *out, const int *done, int &rc);
     int host_ints(int count);
-    int nd_order(hipStream_t s, const AmgLevel &C, int &nbh, int &ld);
+    int nd_order(hipStream_t s, const AmgLevel &C, int &ld);
 };
 
 }  // namespace xfk

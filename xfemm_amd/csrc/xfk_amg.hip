@@ -1301,51 +1301,69 @@ __global__ void __launch_bounds__(256) k_bgj_step(int k, int nbk, int ld, double
     for (int m = 0; m < 16; ++m) Dn[(16 * w + m) * kBj + jl] = a[m];
 }
 
-// Nested-dissection steps.  The coarsest operator, reordered as [part 1 |
-// part 2 | separator] (blocks [0, nb), [nb, 2 nb), [2 nb, nbk)), has no entry
-// between the two parts, and Gauss-Jordan keeps it so: eliminating a block
-// column of part 1 touches only tiles of (part 1 + separator)^2, one of part 2
-// only (part 2 + separator)^2, and the two updates commute.  Step t
-// eliminates blocks t and nb + t in one launch -- two pivot chains side by
-// side, half the chain length -- each tile applying the update of every
-// chain whose region holds it (separator tiles: both, summed on the MFMA in
-// chain order).  The separator's blocks then follow with k_bgj_step.
-struct BgjChain {
-    int k;                       // pivot block of this step
-    int nx;                      // next pivot block of the chain (-1: none)
-    const double *D, *R, *C;     // inv(M_kk), row / column snapshots of step k
-    double *Dn, *Rn, *Cn;        // the same for the next pivot
+// Nested-dissection steps.  The coarsest operator is reordered by a
+// recursive bisection: leaves (parts that share no entry), then their
+// separators, the top separator last.  Gauss-Jordan keeps distinct leaves
+// decoupled: eliminating a block column of a leaf touches only the tiles of
+// its region -- the leaf plus its ancestor separators -- and the updates of
+// different leaves commute.  So the leaves' block columns are eliminated side
+// by side, one pivot chain per leaf in each launch (up to four), then the
+// separators of the next tree level the same way (region: their subtree plus
+// ancestors), the top separator last.  Each tile applies the update of every
+// chain whose region holds it (separator tiles: several, summed on the MFMA
+// in chain order); per block, bit c of `mask` marks chain c's region.
+constexpr int kNdChains = 4;
+struct BgjStep {
+    int n;                                             // chains of this step
+    int k[kNdChains];                                  // their pivot blocks
+    const double *D[kNdChains], *R[kNdChains], *C[kNdChains];   // inv(M_kk), row / column snapshots
+    int nn;                                            // distinct next pivot blocks
+    int nx[kNdChains];
+    double *Dn[kNdChains], *Rn[kNdChains], *Cn[kNdChains];
 };
 
-__global__ void __launch_bounds__(256, 2) k_bgj_dual(int nb, int nbk, int ld, double *__restrict__ M, BgjChain c1,
-                                                  BgjChain c2, const int *__restrict__ tiles, const double *maxd)
+// (chain fields are selected by unrolled comparisons: a dynamically indexed
+// by-value kernel argument would be placed in scratch memory)
+__global__ void __launch_bounds__(256, 2) k_bgj_multi(int nbk, int ld, double *__restrict__ M, BgjStep st,
+                                                      const unsigned char *__restrict__ mask,
+                                                      const int *__restrict__ tiles, const double *maxd)
 {
     const size_t T2 = (size_t)kBj * kBj;
-    // workgroups 0 (and 1) finalise the next pivot blocks and invert them
-    const int np = (c1.nx >= 0) + (c2.nx >= 0 && c2.nx != c1.nx);
     int i, j;
     double *Dpiv = nullptr;
-    if ((int)blockIdx.x < np) {
-        const bool first = blockIdx.x == 0 && c1.nx >= 0;
-        i = j = first ? c1.nx : c2.nx;
-        Dpiv = first ? c1.Dn : c2.Dn;
+    if ((int)blockIdx.x < st.nn) {   // workgroups 0 .. nn-1 finalise and invert the next pivot blocks
+#pragma unroll
+        for (int t = 0; t < kNdChains; ++t)
+            if (t == (int)blockIdx.x) {
+                i = j = st.nx[t];
+                Dpiv = st.Dn[t];
+            }
     } else {
-        const int t = tiles[blockIdx.x - np];
+        const int t = tiles[blockIdx.x - st.nn];
         i = t / nbk;
         j = t % nbk;
-        if ((i == j) && (i == c1.nx || i == c2.nx)) return;   // taken by a pivot workgroup
+        if (i == j)
+#pragma unroll
+            for (int u = 0; u < kNdChains; ++u)
+                if (u < st.nn && st.nx[u] == i) return;   // taken by a pivot workgroup
     }
-    const bool a1 = (i < nb || i >= 2 * nb) && (j < nb || j >= 2 * nb);
-    const bool a2 = i >= nb && j >= nb;
+    const unsigned act = (unsigned)mask[i] & (unsigned)mask[j];
+    int pc = -1;
+    const double *pD = nullptr, *pR = nullptr, *pC = nullptr;
+    int pk = -1;
+#pragma unroll
+    for (int c = 0; c < kNdChains; ++c)
+        if (c < st.n && ((act >> c) & 1u) && (i == st.k[c] || j == st.k[c])) {
+            pc = c;
+            pk = st.k[c];
+            pD = st.D[c];
+            pR = st.R[c];
+            pC = st.C[c];
+        }
     __shared__ __attribute__((aligned(16))) double Xs[kBj * kXs];
     __shared__ __attribute__((aligned(16))) double Ys[kBj * kYs];
     double *Mij = M + (size_t)i * kBj * ld + (size_t)j * kBj;
-    // (chain fields selected into scalars: a pointer to a by-value kernel
-    // argument would put the arguments in scratch memory)
-    const bool p1 = a1 && (i == c1.k || j == c1.k), p2 = !p1 && a2 && (i == c2.k || j == c2.k);
-    const int pk = p1 ? c1.k : c2.k;
-    const double *pD = p1 ? c1.D : c2.D, *pR = p1 ? c1.R : c2.R, *pC = p1 ? c1.C : c2.C;
-    if ((p1 || p2) && i == pk && j == pk) {
+    if (pc >= 0 && i == pk && j == pk) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int e = threadIdx.x + 256 * q, r = e >> 5, c = 2 * (e & 31);
@@ -1356,35 +1374,35 @@ __global__ void __launch_bounds__(256, 2) k_bgj_dual(int nb, int nbk, int ld, do
     dbl4 acc[2][2];
     double sgn = 1.0;
     bool rmw = false;
-    if ((p1 || p2) && i == pk) {   // row of a pivot: D R[j]
+    if (pc >= 0 && i == pk) {   // row of a pivot: D R[j]
         bgj_load<kXs>(Xs, pD, kBj);
         bgj_load<kYs>(Ys, pR + j * T2, kBj);
         __syncthreads();
         bgj_mm(Xs, Ys, acc);
-    } else if (p1 || p2) {         // column of a pivot: -C[i] D
+    } else if (pc >= 0) {       // column of a pivot: -C[i] D
         bgj_load<kXs>(Xs, pC + i * T2, kBj);
         bgj_load<kYs>(Ys, pD, kBj);
         __syncthreads();
         bgj_mm(Xs, Ys, acc);
         sgn = -1.0;
-    } else {                       // M_ij - sum over the chains holding the tile of C[i] (D R[j])
+    } else {                    // M_ij - sum over the chains holding the tile of C[i] (D R[j])
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
             for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = dbl4{0.0, 0.0, 0.0, 0.0};
-        for (int q = 0; q < 2; ++q) {
-            if (!(q == 0 ? a1 : a2)) continue;
-            const double *chD = q == 0 ? c1.D : c2.D, *chR = q == 0 ? c1.R : c2.R;
+#pragma unroll
+        for (int c = 0; c < kNdChains; ++c) {
+            if (!(c < st.n && ((act >> c) & 1u))) continue;
             double2 pre[8];
-            const double *Ci = (q == 0 ? c1.C : c2.C) + i * T2;
+            const double *Ci = st.C[c] + i * T2;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int e = threadIdx.x + 256 * u, r = e >> 5, cc = 2 * (e & 31);
                 pre[u] = *reinterpret_cast<const double2 *>(Ci + r * kBj + cc);
             }
-            __syncthreads();   // LDS of the previous chain's product is free
-            bgj_load<kXs>(Xs, chD, kBj);
-            bgj_load<kYs>(Ys, chR + j * T2, kBj);
+            __syncthreads();   // the LDS of the previous chain's product is free
+            bgj_load<kXs>(Xs, st.D[c], kBj);
+            bgj_load<kYs>(Ys, st.R[c] + j * T2, kBj);
             __syncthreads();
             dbl4 t[2][2];
             bgj_mm(Xs, Ys, t);
@@ -1406,9 +1424,13 @@ __global__ void __launch_bounds__(256, 2) k_bgj_dual(int nb, int nbk, int ld, do
         }
         rmw = true;
     }
-    double *r1 = (i == c1.nx) ? c1.Rn + j * T2 : nullptr, *k1 = (j == c1.nx) ? c1.Cn + i * T2 : nullptr;
-    const bool own2 = c2.nx != c1.nx;
-    double *r2 = (own2 && i == c2.nx) ? c2.Rn + j * T2 : nullptr, *k2 = (own2 && j == c2.nx) ? c2.Cn + i * T2 : nullptr;
+    // row / column snapshots of the next pivot blocks this tile belongs to
+    double *rs[kNdChains], *cs[kNdChains];
+#pragma unroll
+    for (int t = 0; t < kNdChains; ++t) {
+        rs[t] = (t < st.nn && i == st.nx[t]) ? st.Rn[t] + j * T2 : nullptr;
+        cs[t] = (t < st.nn && j == st.nx[t]) ? st.Cn[t] + i * T2 : nullptr;
+    }
     if (Dpiv) __syncthreads();   // Xs is reused below
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
@@ -1420,10 +1442,11 @@ __global__ void __launch_bounds__(256, 2) k_bgj_dual(int nb, int nbk, int ld, do
                 double *e = &Mij[(size_t)row * ld + col];
                 const double v = rmw ? *e - acc[ti][tj][r] : sgn * acc[ti][tj][r];
                 *e = v;
-                if (r1) r1[row * kBj + col] = v;
-                if (k1) k1[row * kBj + col] = v;
-                if (r2) r2[row * kBj + col] = v;
-                if (k2) k2[row * kBj + col] = v;
+#pragma unroll
+                for (int t = 0; t < kNdChains; ++t) {
+                    if (rs[t]) rs[t][row * kBj + col] = v;
+                    if (cs[t]) cs[t][row * kBj + col] = v;
+                }
                 if (Dpiv) Xs[row * kBj + col] = v;
             }
     if (!Dpiv) return;
@@ -1435,6 +1458,51 @@ __global__ void __launch_bounds__(256, 2) k_bgj_dual(int nb, int nbk, int ld, do
     bgj_diag_inv(a, 1e-11 * (*maxd), Ys);
 #pragma unroll
     for (int m = 0; m < 16; ++m) Dpiv[(16 * w + m) * kBj + jl] = a[m];
+}
+
+// first step of the first phase: pivot-block inverses (workgroups 0 .. n-1)
+// and row / column snapshots of the chains' first pivot blocks
+__global__ void __launch_bounds__(256) k_bgj_init(int nbk, int ld, const double *__restrict__ M, BgjStep st,
+                                                  const double *__restrict__ maxd)
+{
+    const int b = blockIdx.x;
+    if (b < st.nn) {
+        __shared__ __attribute__((aligned(16))) double lds[kBjDiagLds];
+        int k = 0;
+        double *D = nullptr;
+#pragma unroll
+        for (int t = 0; t < kNdChains; ++t)
+            if (t == b) {
+                k = st.nx[t];
+                D = st.Dn[t];
+            }
+        const int jl = threadIdx.x & 63, w = threadIdx.x >> 6;
+        const size_t base = (size_t)k * kBj * ld + (size_t)k * kBj;
+        double a[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) a[m] = M[base + (size_t)(16 * w + m) * ld + jl];
+        bgj_diag_inv(a, 1e-11 * (*maxd), lds);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) D[(16 * w + m) * kBj + jl] = a[m];
+        return;
+    }
+    const int e0 = b - st.nn, ch = e0 / (2 * nbk), rem = e0 % (2 * nbk);
+    const int t = rem % nbk;
+    const bool row = rem < nbk;
+    int k = 0;
+    double *dst = nullptr;
+#pragma unroll
+    for (int u = 0; u < kNdChains; ++u)
+        if (u == ch) {
+            k = st.nx[u];
+            dst = (row ? st.Rn[u] : st.Cn[u]) + (size_t)t * kBj * kBj;
+        }
+    const double *src = row ? M + (size_t)k * kBj * ld + (size_t)t * kBj : M + (size_t)t * kBj * ld + (size_t)k * kBj;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int e = threadIdx.x + 256 * q, r = e >> 5, c = 2 * (e & 31);
+        *reinterpret_cast<double2 *>(dst + r * kBj + c) = *reinterpret_cast<const double2 *>(src + (size_t)r * ld + c);
+    }
 }
 
 // --------------------------------------------------------------------------
@@ -2098,55 +2166,122 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     return XFK_OK;
 }
 
-// Nested-dissection order of the coarsest level for the dense inverse: part 1
-// = rows [0, m), part 2 = rows >= m without a column < m, separator = rows >=
-// m with one (the levels are numbered along the fine level's Cuthill-McKee
-// order, so the coupling across m is a band of about one grid line).  Parts
-// padded to nbh blocks each, the separator to whole blocks; padding rows are
-// identity rows.  nbh = 0 keeps the plain order (small levels, or a
-// separator of more than a quarter of the rows).  Host-synchronising.
-int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &nbh, int &ld)
+// Nested-dissection order of the coarsest level for the dense inverse: a
+// recursive bisection -- left = the first half of the rows (the levels are
+// numbered along the fine level's Cuthill-McKee order, so the halves are
+// banded slabs), right = the other rows without an entry in the left half,
+// separator = those with one (about one grid line).  Two tree levels give
+// four leaves (four pivot chains per launch), then their two separators,
+// then the top separator; one level two leaves.  Groups are padded with
+// identity rows to whole blocks, the groups of one phase to equal block
+// counts.  Falls back to one level, then to the plain order, when a
+// separator would be empty or hold more than a quarter of the rows.
+// Host-synchronising (the coarsest level has <= dense_max rows).
+namespace {
+void nd_bisect(const std::vector<int> &rp, const std::vector<int> &cl, const std::vector<int> &rows,
+               std::vector<char> &inl, std::vector<int> &L, std::vector<int> &R, std::vector<int> &S)
+{
+    const size_t h = rows.size() / 2;
+    L.assign(rows.begin(), rows.begin() + h);
+    R.clear();
+    S.clear();
+    for (int r : L) inl[r] = 1;
+    for (size_t t = h; t < rows.size(); ++t) {
+        const int r = rows[t];
+        bool cross = false;
+        for (int k = rp[r]; k < rp[r + 1] && !cross; ++k) cross = inl[cl[k]] != 0;
+        (cross ? S : R).push_back(r);
+    }
+    for (int r : L) inl[r] = 0;
+}
+}  // namespace
+
+int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &ld)
 {
     const int n = C.n;
-    nbh = 0;
+    nd_phases.clear();
     ld = ((n + kBj - 1) / kBj) * kBj;
     if (n < 8 * kBj || std::getenv("XFK_NO_ND")) return XFK_OK;
     std::vector<int> rp(n + 1), cl((size_t)C.nnz);
     AMG_CHECK(hipMemcpyAsync(rp.data(), C.rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost, s));
     AMG_CHECK(hipMemcpyAsync(cl.data(), C.col, sizeof(int) * C.nnz, hipMemcpyDeviceToHost, s));
     AMG_CHECK(hipStreamSynchronize(s));
-    const int m = kBj * std::max(1, (int)std::lround(n / (2.0 * kBj)));
-    std::vector<int> part2, sepr;
-    for (int r = m; r < n; ++r) {
-        bool cross = false;
-        for (int k = rp[r]; k < rp[r + 1] && !cross; ++k) cross = cl[k] < m;
-        (cross ? sepr : part2).push_back(r);
+    for (int r = 0; r < n; ++r)   // columns >= n (none on a level built here) are dropped by the scatter
+        for (int k = rp[r]; k < rp[r + 1]; ++k) cl[k] = std::min(cl[k], n);
+    std::vector<char> inl(n + 1, 0);
+    std::vector<int> all(n);
+    for (int r = 0; r < n; ++r) all[r] = r;
+    // groups: rows, phase, slot in the phase, parent separator group, subtree groups
+    struct G {
+        std::vector<int> rows;
+        int phase, slot, parent;
+        std::vector<int> sub;
+    };
+    std::vector<G> g;
+    std::vector<int> A, B, S;
+    nd_bisect(rp, cl, all, inl, A, B, S);
+    if (A.empty() || B.empty() || S.empty() || 4 * S.size() > (size_t)n) return XFK_OK;
+    bool two = n >= 16 * kBj;
+    std::vector<int> A1, A2, SA, B1, B2, SB;
+    if (two) {
+        nd_bisect(rp, cl, A, inl, A1, A2, SA);
+        nd_bisect(rp, cl, B, inl, B1, B2, SB);
+        two = !A1.empty() && !A2.empty() && !SA.empty() && !B1.empty() && !B2.empty() && !SB.empty() &&
+              4 * (S.size() + SA.size() + SB.size()) <= (size_t)n;
     }
-    const int m2 = (int)part2.size(), ms = (int)sepr.size();
-    if (m2 == 0 || 4 * ms > n) return XFK_OK;
-    nbh = (std::max(m, m2) + kBj - 1) / kBj;
-    const int P = nbh * kBj;
-    ld = 2 * P + ((ms + kBj - 1) / kBj) * kBj;
+    if (two) {
+        g = {{A1, 0, 0, 4, {0}}, {A2, 0, 1, 4, {1}}, {B1, 0, 2, 5, {2}}, {B2, 0, 3, 5, {3}},
+             {SA, 1, 0, 6, {0, 1, 4}}, {SB, 1, 1, 6, {2, 3, 5}}, {S, 2, 0, -1, {0, 1, 2, 3, 4, 5, 6}}};
+    } else {
+        g = {{A, 0, 0, 2, {0}}, {B, 0, 1, 2, {1}}, {S, 1, 0, -1, {0, 1, 2}}};
+    }
+    const int nph = g.back().phase + 1;
+    // blocks: each phase's groups padded to the phase's largest group
+    std::vector<int> pblk(nph, 0), b0(g.size());
+    for (const G &x : g) pblk[x.phase] = std::max(pblk[x.phase], (int)((x.rows.size() + kBj - 1) / kBj));
+    int nbk = 0;
+    for (size_t q = 0; q < g.size(); ++q) {
+        b0[q] = nbk;
+        nbk += pblk[g[q].phase];
+    }
+    ld = nbk * kBj;
     std::vector<int> perm(n), iperm(ld, -1);
-    for (int r = 0; r < m; ++r) perm[r] = r;
-    for (int t = 0; t < m2; ++t) perm[part2[t]] = P + t;
-    for (int t = 0; t < ms; ++t) perm[sepr[t]] = 2 * P + t;
-    for (int r = 0; r < n; ++r) iperm[perm[r]] = r;
+    for (size_t q = 0; q < g.size(); ++q)
+        for (size_t t = 0; t < g[q].rows.size(); ++t) {
+            perm[g[q].rows[t]] = b0[q] * kBj + (int)t;
+            iperm[b0[q] * kBj + (int)t] = g[q].rows[t];
+        }
+    // per phase: region masks (bit = slot) and the tiles some chain holds
+    std::vector<unsigned char> mask((size_t)nph * nbk, 0);
+    std::vector<int> tl;
+    for (int ph = 0; ph < nph; ++ph) {
+        unsigned char *m = mask.data() + (size_t)ph * nbk;
+        NdPhase P{};
+        P.steps = pblk[ph];
+        for (size_t q = 0; q < g.size(); ++q) {
+            if (g[q].phase != ph) continue;
+            P.base[g[q].slot] = b0[q];
+            P.nch = std::max(P.nch, g[q].slot + 1);
+            P.next_slot[g[q].slot] = g[q].parent >= 0 ? g[g[q].parent].slot : -1;
+            std::vector<int> reg = g[q].sub;
+            for (int a = g[q].parent; a >= 0; a = g[a].parent) reg.push_back(a);
+            for (int x : reg)
+                for (int bb = 0; bb < pblk[g[x].phase]; ++bb) m[b0[x] + bb] |= (unsigned char)(1u << g[q].slot);
+        }
+        P.tiles_off = (int)tl.size();
+        for (int i = 0; i < nbk; ++i)
+            for (int j = 0; j < nbk; ++j)
+                if (m[i] & m[j]) tl.push_back(i * nbk + j);
+        P.ntiles = (int)tl.size() - P.tiles_off;
+        nd_phases.push_back(P);
+    }
     AMG_CHECK(cinv_perm.alloc(n));
     AMG_CHECK(cinv_iperm.alloc(ld));
+    AMG_CHECK(nd_mask.alloc(mask.size()));
+    AMG_CHECK(nd_tiles.alloc(tl.size()));
     AMG_CHECK(hipMemcpyAsync(cinv_perm.p, perm.data(), sizeof(int) * n, hipMemcpyHostToDevice, s));
     AMG_CHECK(hipMemcpyAsync(cinv_iperm.p, iperm.data(), sizeof(int) * ld, hipMemcpyHostToDevice, s));
-    // the tiles of (part 1 + separator)^2 and (part 2 + separator)^2
-    const int nbk = ld / kBj;
-    std::vector<int> tl;
-    for (int i = 0; i < nbk; ++i)
-        for (int j = 0; j < nbk; ++j) {
-            const bool a1 = (i < nbh || i >= 2 * nbh) && (j < nbh || j >= 2 * nbh);
-            const bool a2 = i >= nbh && j >= nbh;
-            if (a1 || a2) tl.push_back(i * nbk + j);
-        }
-    nd_ntiles = (int)tl.size();
-    AMG_CHECK(nd_tiles.alloc(tl.size()));
+    AMG_CHECK(hipMemcpyAsync(nd_mask.p, mask.data(), mask.size(), hipMemcpyHostToDevice, s));
     AMG_CHECK(hipMemcpyAsync(nd_tiles.p, tl.data(), sizeof(int) * tl.size(), hipMemcpyHostToDevice, s));
     AMG_CHECK(hipStreamSynchronize(s));   // host vectors go out of scope
     return XFK_OK;
@@ -2228,24 +2363,22 @@ int Amg::build(hipStream_t s, int l0)
     if (dense_coarse) {
         AmgLevel &C = *L[nlev - 1];
         if (g_prof) g_prof->begin("setup L" + std::to_string(nlev - 1) + " dense inverse (blocked Gauss-Jordan)", 0.0);
-        int nbh = 0, ld = 0;   // nested dissection: blocks per part (0: plain order)
-        int rc = nd_order(s, C, nbh, ld);
+        int ld = 0;
+        int rc = nd_order(s, C, ld);
         if (rc != XFK_OK) return rc;
+        const bool nd = !nd_phases.empty();
         const int nbk = ld / kBj;
         cinv_ld = ld;
         AMG_CHECK(cinv.alloc((size_t)ld * ld));
         const size_t T2 = (size_t)kBj * kBj;
-        // per chain: double-buffered row / column snapshots and pivot inverses
-        AMG_CHECK(bgj_tmp.alloc(8 * (size_t)nbk * T2 + 4 * T2 + 1 + ld));
-        double *Rs[2][2], *Cs[2][2], *Ds[2][2];
-        for (int c = 0; c < 2; ++c)
-            for (int q = 0; q < 2; ++q) {
-                Rs[c][q] = bgj_tmp.p + (size_t)(4 * c + q) * nbk * T2;
-                Cs[c][q] = bgj_tmp.p + (size_t)(4 * c + 2 + q) * nbk * T2;
-                Ds[c][q] = bgj_tmp.p + 8 * (size_t)nbk * T2 + (size_t)(2 * c + q) * T2;
-            }
-        double *maxd = bgj_tmp.p + 8 * (size_t)nbk * T2 + 4 * T2, *sc = maxd + 1;
-        const int *pm = nbh ? cinv_perm.p : nullptr, *ipm = nbh ? cinv_iperm.p : nullptr;
+        // per chain slot and parity: row / column snapshots and the pivot inverse
+        const size_t per = 2 * (size_t)nbk * T2 + T2;
+        AMG_CHECK(bgj_tmp.alloc(2 * kNdChains * per + 1 + ld));
+        auto Rb = [&](int c, int q) { return bgj_tmp.p + (size_t)(2 * c + q) * per; };
+        auto Cb = [&](int c, int q) { return Rb(c, q) + (size_t)nbk * T2; };
+        auto Db = [&](int c, int q) { return Rb(c, q) + 2 * (size_t)nbk * T2; };
+        double *maxd = bgj_tmp.p + 2 * kNdChains * per, *sc = maxd + 1;
+        const int *pm = nd ? cinv_perm.p : nullptr, *ipm = nd ? cinv_iperm.p : nullptr;
         AMG_CHECK(hipMemsetAsync(cinv.p, 0, sizeof(double) * (size_t)ld * ld, s));
         k_dense_dscale<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, ipm, sc);
         k_dense_scatter<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, pm, ipm, sc, cinv.p);
@@ -2254,34 +2387,62 @@ int Amg::build(hipStream_t s, int l0)
         // inverted on a second stream during the rest of the update -- was
         // measured slower: the two cross-stream waits cost ~15 us per step,
         // more than the 25 us pivot-block inversion it hides)
-        int k0 = 0, par = 0;   // first single-chain step, its buffer parity
-        if (nbh) {
-            // the two parts side by side: steps t = 0 .. nbh-1 eliminate blocks t and nbh + t
-            k_bgj_snap<<<2 * nbk, 256, 0, s>>>(0, nbk, ld, cinv.p, Rs[0][0], Cs[0][0]);
-            k_bgj_snap<<<2 * nbk, 256, 0, s>>>(nbh, nbk, ld, cinv.p, Rs[1][0], Cs[1][0]);
-            k_bgj_diag<<<1, 256, 0, s>>>(0, ld, cinv.p, maxd, Ds[0][0]);
-            k_bgj_diag<<<1, 256, 0, s>>>(nbh, ld, cinv.p, maxd, Ds[1][0]);
-            const int sep = 2 * nbh < nbk ? 2 * nbh : -1;   // first separator block
-            for (int t = 0; t < nbh; ++t) {
-                const int p = t & 1, q = (t + 1) & 1;
-                const bool last = t + 1 == nbh;
-                BgjChain c1{t, last ? sep : t + 1, Ds[0][p], Rs[0][p], Cs[0][p], Ds[0][q], Rs[0][q], Cs[0][q]};
-                BgjChain c2{nbh + t, last ? sep : nbh + t + 1, Ds[1][p], Rs[1][p], Cs[1][p], Ds[1][q], Rs[1][q], Cs[1][q]};
-                const int np = (c1.nx >= 0) + (c2.nx >= 0 && c2.nx != c1.nx);
-                k_bgj_dual<<<nd_ntiles + np, 256, 0, s>>>(nbh, nbk, ld, cinv.p, c1, c2, nd_tiles.p, maxd);
+        if (nd) {
+            int par = 0;
+            BgjStep st{};
+            st.nn = nd_phases[0].nch;
+            for (int c = 0; c < st.nn; ++c) {
+                st.nx[c] = nd_phases[0].base[c];
+                st.Dn[c] = Db(c, 0);
+                st.Rn[c] = Rb(c, 0);
+                st.Cn[c] = Cb(c, 0);
             }
-            k0 = 2 * nbh;
-            par = nbh & 1;   // the separator's first snapshots are chain 1's of parity nbh & 1
+            k_bgj_init<<<st.nn * (1 + 2 * nbk), 256, 0, s>>>(nbk, ld, cinv.p, st, maxd);
+            for (size_t ph = 0; ph < nd_phases.size(); ++ph) {
+                const NdPhase &P = nd_phases[ph];
+                for (int t = 0; t < P.steps; ++t) {
+                    const int pp = par, qq = par ^ 1;
+                    BgjStep x{};
+                    x.n = P.nch;
+                    for (int c = 0; c < P.nch; ++c) {
+                        x.k[c] = P.base[c] + t;
+                        x.D[c] = Db(c, pp);
+                        x.R[c] = Rb(c, pp);
+                        x.C[c] = Cb(c, pp);
+                    }
+                    if (t + 1 < P.steps) {
+                        x.nn = P.nch;
+                        for (int c = 0; c < P.nch; ++c) x.nx[c] = P.base[c] + t + 1;
+                    } else if (ph + 1 < nd_phases.size()) {
+                        const NdPhase &Q = nd_phases[ph + 1];
+                        x.nn = Q.nch;
+                        for (int c = 0; c < Q.nch; ++c) x.nx[c] = Q.base[c];
+                    }
+                    for (int c = 0; c < x.nn; ++c) {
+                        x.Dn[c] = Db(c, qq);
+                        x.Rn[c] = Rb(c, qq);
+                        x.Cn[c] = Cb(c, qq);
+                    }
+                    k_bgj_multi<<<P.ntiles + x.nn, 256, 0, s>>>(nbk, ld, cinv.p, x, nd_mask.p + ph * (size_t)nbk,
+                                                                nd_tiles.p + P.tiles_off, maxd);
+                    par = qq;
+                }
+            }
         } else {
-            k_bgj_snap<<<2 * nbk, 256, 0, s>>>(0, nbk, ld, cinv.p, Rs[0][0], Cs[0][0]);
-            k_bgj_diag<<<1, 256, 0, s>>>(0, ld, cinv.p, maxd, Ds[0][0]);
+            BgjStep st{};
+            st.nn = 1;
+            st.nx[0] = 0;
+            st.Dn[0] = Db(0, 0);
+            st.Rn[0] = Rb(0, 0);
+            st.Cn[0] = Cb(0, 0);
+            k_bgj_init<<<1 + 2 * nbk, 256, 0, s>>>(nbk, ld, cinv.p, st, maxd);
+            for (int k = 0; k < nbk; ++k) {
+                const int p = k & 1, q = (k + 1) & 1;
+                k_bgj_step<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, Db(0, p), Rb(0, p), Cb(0, p), Db(0, q),
+                                                     Rb(0, q), Cb(0, q), maxd);
+            }
         }
-        for (int k = k0; k < nbk; ++k) {
-            const int p = (par + k - k0) & 1, q = (par + k - k0 + 1) & 1;
-            k_bgj_step<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, Ds[0][p], Rs[0][p], Cs[0][p], Ds[0][q],
-                                                 Rs[0][q], Cs[0][q], maxd);
-        }
-        if (nbh) {
+        if (nd) {
             const int ldo = ((C.n + kBj - 1) / kBj) * kBj;
             AMG_CHECK(cinv_o.alloc((size_t)ldo * ldo));
             k_dense_unperm<<<ld, 256, 0, s>>>(C.n, ld, ldo, cinv.p, sc, cinv_iperm.p, cinv_o.p);
