@@ -43,6 +43,7 @@ namespace xfk {
 
 constexpr int kAmgDenseMax = 2048;    // coarsest level solved by its dense inverse (blocked Gauss-Jordan)
 constexpr int kAmgMaxLevels = 16;
+constexpr int kAmgDeferSlots = 64;    // deferred SpGEMM (overflow flag, length) pairs per setup
 
 struct AmgLevel {
     int n = 0;                        // rows
@@ -114,6 +115,10 @@ struct Amg {
     DBuf<int> dev_int;                // small device scalars (undecided flag, overflow flags)
     std::map<int, int> cap_hint;      // SpGEMM slot capacity of each call site in the last setup
     std::map<int, int> mis_hint;      // MIS-2 rounds each level needed in the last setup
+    DBuf<int> def_dev;                // deferred SpGEMM results: (overflow flag, length) pairs
+    int *def_host = nullptr;          // pinned mirror
+    int def_n = 0;
+    long long *def_target[kAmgDeferSlots / 2] = {};
     int *host_int = nullptr;          // pinned mirror
     DBuf<char> cub_tmp;
 
@@ -174,6 +179,8 @@ struct Amg {
     double *vc_dist(hipStream_t s, int l, const double *b, double *out, const int *done, int &rc);
     int host_ints(int count);
     int nd_order(hipStream_t s, const AmgLevel &C, int &ld);
+    int resolve_deferred(hipStream_t s, bool &overflow);
+    long long ap_nnz = 0;
 };
 
 }  // namespace xfk

@@ -863,10 +863,13 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
 
 // padded rows (row * cap) -> CSR; 16 lanes per row, so a row's reads and
 // writes are contiguous runs
+// nnz_out (optional): the product's length, for a deferred host read
 __global__ void k_spgemm_compact(int nrows, int cap, const int *__restrict__ crow, const int *__restrict__ pcol,
-                                 const double *__restrict__ pval, int *__restrict__ ccol, double *__restrict__ cval)
+                                 const double *__restrict__ pval, int *__restrict__ ccol, double *__restrict__ cval,
+                                 int *nnz_out)
 {
     const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (t == 0 && nnz_out) *nnz_out = crow[nrows];
     const int row = (int)(t >> 4), l = (int)(t & 15);
     if (row >= nrows) return;
     const int b = crow[row], n = crow[row + 1] - b;
@@ -1757,6 +1760,7 @@ __global__ void k_unpad(int NC, int nranks, const int *__restrict__ c0, const do
 
 Amg::~Amg()
 {
+    if (def_host) (void)hipHostFree(def_host);
     if (host_int) (void)hipHostFree(host_int);
     if (host_big) (void)hipHostFree(host_big);
 }
@@ -1816,26 +1820,32 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     // compaction; returns the overflow flag (rows with more products than
     // slots), read back with the scan's own synchronisation
     int *sovf = M.dev_int.p + 6;
-    auto sort_pass = [&](int cap, bool &overflow) -> int {
-        AMG_CHECK(M.pad_col.alloc((size_t)nrows * cap));
-        AMG_CHECK(M.pad_val.alloc((size_t)nrows * cap));
+    auto launch_sort = [&](int cap, int *ovf) {
         int *pc = M.pad_col.p;
         double *pv = M.pad_val.p;
-        AMG_CHECK(hipMemsetAsync(sovf, 0, sizeof(int), s));
         if (nrows > 0) {
             // few lanes per row, 4-8 sorted slots per lane: many rows per
             // wavefront to overlap their dependent gathers
             if (cap == 16)
-                k_spgemm_sort<PMODE, 4, 16><<<(nrows + 15) / 16, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, sovf);
+                k_spgemm_sort<PMODE, 4, 16><<<(nrows + 15) / 16, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
             else if (cap == 32)
-                k_spgemm_sort<PMODE, 8, 32><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, sovf);
+                k_spgemm_sort<PMODE, 8, 32><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
             else if (cap == 64)
-                k_spgemm_sort<PMODE, 8, 64><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, sovf);
+                k_spgemm_sort<PMODE, 8, 64><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
             else if (cap == 128)
-                k_spgemm_sort<PMODE, 16, 128><<<(nrows + 3) / 4, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, sovf);
+                k_spgemm_sort<PMODE, 16, 128><<<(nrows + 3) / 4, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
             else
-                k_spgemm_sort<PMODE, 32, 256><<<(nrows + 1) / 2, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, sovf);
+                k_spgemm_sort<PMODE, 32, 256><<<(nrows + 1) / 2, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
         }
+    };
+    // single pass into padded rows of `cap` slots (sort-based), then scan +
+    // compaction; returns the overflow flag (rows with more products than
+    // slots), read back with the scan's own synchronisation
+    auto sort_pass = [&](int cap, bool &overflow) -> int {
+        AMG_CHECK(M.pad_col.alloc((size_t)nrows * cap));
+        AMG_CHECK(M.pad_val.alloc((size_t)nrows * cap));
+        AMG_CHECK(hipMemsetAsync(sovf, 0, sizeof(int), s));
+        launch_sort(cap, sovf);
         AMG_CHECK(hipMemcpyAsync(M.host_int + 4, sovf, sizeof(int), hipMemcpyDeviceToHost, s));
         int rc = scan_total(M, s, M.cnt.p, crow.p, nrows, cnnz);   // synchronises
         if (rc != XFK_OK) return rc;
@@ -1845,16 +1855,38 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
         AMG_CHECK(cval.alloc((size_t)std::max(1LL, cnnz)));
         if (nrows > 0)
             k_spgemm_compact<<<(unsigned)(((long long)nrows * 16 + kB - 1) / kB), kB, 0, s>>>(
-                nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p);
+                nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p, nullptr);
         return XFK_OK;
     };
     // the slot capacity this product needed in the previous setup (same
-    // call site): taken without measuring the longest product list first
-    // (one launch pair and one host synchronisation fewer); an overflow is
-    // detected by the kernel and the product redone with a measured capacity
+    // call site): taken without measuring the longest product list first,
+    // and without any host synchronisation -- the output is sized for
+    // nrows x cap, its length and the kernel's overflow flag land in a
+    // deferred slot that the setup reads once at its end (an overflow there
+    // rebuilds the hierarchy with measured capacities)
     if (key >= 0) {
         auto hint = M.cap_hint.find(key);
         if (hint != M.cap_hint.end()) {
+            if (M.def_n + 2 <= kAmgDeferSlots) {
+                const int cap = hint->second;
+                int *slot = M.def_dev.p + M.def_n;
+                AMG_CHECK(M.pad_col.alloc((size_t)nrows * cap));
+                AMG_CHECK(M.pad_val.alloc((size_t)nrows * cap));
+                AMG_CHECK(ccol.alloc((size_t)std::max(1LL, (long long)nrows * cap)));
+                AMG_CHECK(cval.alloc((size_t)std::max(1LL, (long long)nrows * cap)));
+                launch_sort(cap, slot);
+                int rc = scan_only(M, s, M.cnt.p, crow.p, nrows);
+                if (rc != XFK_OK) return rc;
+                if (nrows > 0)
+                    k_spgemm_compact<<<(unsigned)(((long long)nrows * 16 + kB - 1) / kB), kB, 0, s>>>(
+                        nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p, slot + 1);
+                else
+                    AMG_CHECK(hipMemsetAsync(slot + 1, 0, sizeof(int), s));
+                M.def_target[M.def_n / 2] = &cnnz;
+                M.def_n += 2;
+                cnnz = (long long)nrows * cap;   // an upper bound until the deferred read
+                return XFK_OK;
+            }
             bool overflow = false;
             int rc = sort_pass(hint->second, overflow);
             if (rc != XFK_OK || !overflow) return rc;
@@ -2017,6 +2049,21 @@ bool overlap_enabled()
     return !(e && std::atoi(e) != 0);
 }
 
+int Amg::resolve_deferred(hipStream_t s, bool &overflow)
+{
+    overflow = false;
+    if (def_n == 0) return XFK_OK;
+    AMG_CHECK(hipMemcpyAsync(def_host, def_dev.p, sizeof(int) * def_n, hipMemcpyDeviceToHost, s));
+    AMG_CHECK(hipStreamSynchronize(s));
+    for (int q = 0; q < def_n / 2; ++q) {
+        if (def_host[2 * q]) overflow = true;
+        else *def_target[q] = def_host[2 * q + 1];
+    }
+    def_n = 0;
+    AMG_CHECK(hipMemsetAsync(def_dev.p, 0, sizeof(int) * kAmgDeferSlots, s));
+    return XFK_OK;
+}
+
 int Amg::host_ints(int count)
 {
     if (host_big_n >= count) return XFK_OK;
@@ -2031,7 +2078,11 @@ int Amg::host_ints(int count)
 int Amg::init(hipStream_t s)
 {
     if (!host_int) AMG_CHECK(hipHostMalloc((void **)&host_int, 8 * sizeof(int)));
+    if (!def_host) AMG_CHECK(hipHostMalloc((void **)&def_host, kAmgDeferSlots * sizeof(int)));
     AMG_CHECK(dev_int.alloc(8));
+    AMG_CHECK(def_dev.alloc(kAmgDeferSlots));
+    AMG_CHECK(hipMemsetAsync(def_dev.p, 0, sizeof(int) * kAmgDeferSlots, s));
+    def_n = 0;
     AMG_CHECK(rho.alloc(2 * kAmgMaxLevels));
     AMG_CHECK(hipMemsetAsync(rho.p, 0, sizeof(unsigned long long) * 2 * kAmgMaxLevels, s));
     if (L.empty()) L.emplace_back(new AmgLevel());
@@ -2325,22 +2376,19 @@ int Amg::build(hipStream_t s, int l0)
         // AP = A P, then A_c = R (A P)
         SgX XA{A.rowptr, A.col, A.val, A.ncol_lim, nullptr, nullptr, nullptr};
         SgY YP{A.prow.p, A.pcol.p, A.pval.p, nullptr};
-        long long apnnz = 0;
         if (g_prof) g_prof->begin(lv + "SpGEMM A P", 0.0);
-        rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, apnnz, 4 * l + 1);
+        rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, ap_nnz, 4 * l + 1);
         if (g_prof) g_prof->end();
         if (rc != XFK_OK) return rc;
         if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
         AmgLevel &C = *L[l + 1];
         SgX XR{A.rrow.p, A.rcol.p, A.rval.p, INT_MAX, nullptr, nullptr, nullptr};
         SgY YAP{ap_row.p, ap_col.p, ap_val.p, nullptr};
-        long long cnnz = 0;
         if (g_prof) g_prof->begin(lv + "SpGEMM R (A P)", 0.0);
-        rc = spgemm<false>(*this, s, (int)nc, XR, YAP, C.rowptr_o, C.col_o, C.val_o, cnnz, 4 * l + 2);
+        rc = spgemm<false>(*this, s, (int)nc, XR, YAP, C.rowptr_o, C.col_o, C.val_o, C.nnz, 4 * l + 2);
         if (g_prof) g_prof->end();
         if (rc != XFK_OK) return rc;
         C.n = (int)nc;
-        C.nnz = cnnz;
         C.ncol_lim = (int)nc;
         C.ncol_smooth = (int)nc;
         C.rowptr = C.rowptr_o.p;
@@ -2348,6 +2396,18 @@ int Amg::build(hipStream_t s, int l0)
         C.val = C.val_o.p;
     }
     nlev = l + 1;
+    {
+        // the SpGEMM lengths taken without a host check (capacity hints); an
+        // overflow means a hint was too small: rebuild with measured capacities
+        bool overflow = false;
+        int rc = resolve_deferred(s, overflow);
+        if (rc != XFK_OK) return rc;
+        if (overflow) {
+            cap_hint.clear();
+            return build(s, l0);
+        }
+        for (int k = l0; k < nlev; ++k) stats.nnz[k] = L[k]->nnz;
+    }
     stats.levels = nlev;
     double tot = 0;
     for (int k = 0; k < nlev; ++k) tot += (double)stats.nnz[k];
