@@ -158,8 +158,8 @@ def pmc_traffic(algo_bytes, kernel="k_cg_spmv"):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cells", type=int, default=1000, help="cells per side (2*cells^2 triangles)")
     ap.add_argument("--nonlinear", action="store_true", help="M-19 B-H steel (configs[3])")
     ap.add_argument("--cpu-cells", type=int, default=1000,
