@@ -99,6 +99,11 @@ struct Amg {
         int tiles_off = 0, ntiles = 0;
     };
     std::vector<NdPhase> nd_phases;
+    std::vector<int> nd_key;          // coarsest pattern (rowptr, col) the cached plan was made for
+    std::vector<NdPhase> nd_phases_key;
+    int nd_ld = 0;
+    char *nd_stage = nullptr;         // pinned upload staging of the plan
+    size_t nd_stage_n = 0;
     DBuf<double> bgj_tmp;             // blocked Gauss-Jordan panels
     DBuf<unsigned long long> rho;     // per level {rho_A, rho_F} as ordered bit patterns
     AmgStats stats;

@@ -1760,6 +1760,7 @@ __global__ void k_unpad(int NC, int nranks, const int *__restrict__ c0, const do
 
 Amg::~Amg()
 {
+    if (nd_stage) (void)hipHostFree(nd_stage);
     if (def_host) (void)hipHostFree(def_host);
     if (host_int) (void)hipHostFree(host_int);
     if (host_big) (void)hipHostFree(host_big);
@@ -2253,10 +2254,23 @@ int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &ld)
     nd_phases.clear();
     ld = ((n + kBj - 1) / kBj) * kBj;
     if (n < 8 * kBj || std::getenv("XFK_NO_ND")) return XFK_OK;
-    std::vector<int> rp(n + 1), cl((size_t)C.nnz);
-    AMG_CHECK(hipMemcpyAsync(rp.data(), C.rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost, s));
-    AMG_CHECK(hipMemcpyAsync(cl.data(), C.col, sizeof(int) * C.nnz, hipMemcpyDeviceToHost, s));
+    // the pattern through pinned memory; an unchanged pattern (the next setup
+    // of the same matrix family) keeps the plan and its device arrays
+    const size_t npat = (size_t)n + 1 + (size_t)C.nnz;
+    int rc = host_ints((int)npat);
+    if (rc != XFK_OK) return rc;
+    AMG_CHECK(hipMemcpyAsync(host_big, C.rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost, s));
+    AMG_CHECK(hipMemcpyAsync(host_big + n + 1, C.col, sizeof(int) * C.nnz, hipMemcpyDeviceToHost, s));
     AMG_CHECK(hipStreamSynchronize(s));
+    if (nd_key.size() == npat && std::equal(nd_key.begin(), nd_key.end(), host_big)) {
+        nd_phases = nd_phases_key;
+        ld = nd_ld;
+        return XFK_OK;
+    }
+    nd_key.assign(host_big, host_big + npat);
+    nd_phases_key.clear();
+    nd_ld = ld;
+    std::vector<int> rp(host_big, host_big + n + 1), cl(host_big + n + 1, host_big + npat);
     for (int r = 0; r < n; ++r)   // columns >= n (none on a level built here) are dropped by the scatter
         for (int k = rp[r]; k < rp[r + 1]; ++k) cl[k] = std::min(cl[k], n);
     std::vector<char> inl(n + 1, 0);
@@ -2330,11 +2344,29 @@ int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &ld)
     AMG_CHECK(cinv_iperm.alloc(ld));
     AMG_CHECK(nd_mask.alloc(mask.size()));
     AMG_CHECK(nd_tiles.alloc(tl.size()));
-    AMG_CHECK(hipMemcpyAsync(cinv_perm.p, perm.data(), sizeof(int) * n, hipMemcpyHostToDevice, s));
-    AMG_CHECK(hipMemcpyAsync(cinv_iperm.p, iperm.data(), sizeof(int) * ld, hipMemcpyHostToDevice, s));
-    AMG_CHECK(hipMemcpyAsync(nd_mask.p, mask.data(), mask.size(), hipMemcpyHostToDevice, s));
-    AMG_CHECK(hipMemcpyAsync(nd_tiles.p, tl.data(), sizeof(int) * tl.size(), hipMemcpyHostToDevice, s));
-    AMG_CHECK(hipStreamSynchronize(s));   // host vectors go out of scope
+    // uploads from a pinned staging copy (no host check: the staging buffer
+    // is rewritten only after the next setup's synchronising pattern read)
+    const size_t bytes = sizeof(int) * ((size_t)n + ld + tl.size()) + mask.size();
+    if (nd_stage_n < bytes) {
+        if (nd_stage) (void)hipHostFree(nd_stage);
+        nd_stage = nullptr;
+        nd_stage_n = 0;
+        AMG_CHECK(hipHostMalloc((void **)&nd_stage, bytes));
+        nd_stage_n = bytes;
+    }
+    char *h = nd_stage;
+    std::memcpy(h, perm.data(), sizeof(int) * n);
+    std::memcpy(h + sizeof(int) * n, iperm.data(), sizeof(int) * ld);
+    std::memcpy(h + sizeof(int) * ((size_t)n + ld), tl.data(), sizeof(int) * tl.size());
+    std::memcpy(h + sizeof(int) * ((size_t)n + ld + tl.size()), mask.data(), mask.size());
+    AMG_CHECK(hipMemcpyAsync(cinv_perm.p, h, sizeof(int) * n, hipMemcpyHostToDevice, s));
+    AMG_CHECK(hipMemcpyAsync(cinv_iperm.p, h + sizeof(int) * n, sizeof(int) * ld, hipMemcpyHostToDevice, s));
+    AMG_CHECK(hipMemcpyAsync(nd_tiles.p, h + sizeof(int) * ((size_t)n + ld), sizeof(int) * tl.size(),
+                             hipMemcpyHostToDevice, s));
+    AMG_CHECK(hipMemcpyAsync(nd_mask.p, h + sizeof(int) * ((size_t)n + ld + tl.size()), mask.size(),
+                             hipMemcpyHostToDevice, s));
+    nd_phases_key = nd_phases;
+    nd_ld = ld;
     return XFK_OK;
 }
 
@@ -2514,8 +2546,7 @@ int Amg::build(hipStream_t s, int l0)
         }
         if (g_prof) g_prof->end();
     }
-    AMG_CHECK(hipGetLastError());
-    AMG_CHECK(hipStreamSynchronize(s));
+    AMG_CHECK(hipGetLastError());   // no host check: nothing on the host waits for the device here
     return XFK_OK;
 }
 

@@ -353,9 +353,10 @@ int build_symbolic(xfk_problem *P)
     XFK_CHECK(P->rowptr.alloc(N + 1));
     launch_row_build(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, T.rowtmp, T.rowcnt);
     XFK_CHECK(exclusive_scan(P, T.rowcnt, P->rowptr.p, N));
-    int nnz = 0, nnz_own = 0;
-    XFK_CHECK(d2h(&nnz, P->rowptr.p + N, sizeof(int), s));
-    XFK_CHECK(d2h(&nnz_own, P->rowptr.p + P->N, sizeof(int), s));
+    XFK_CHECK(hipMemcpyAsync(P->hpin, P->rowptr.p + N, sizeof(int), hipMemcpyDeviceToHost, s));
+    XFK_CHECK(hipMemcpyAsync(P->hpin + 1, P->rowptr.p + P->N, sizeof(int), hipMemcpyDeviceToHost, s));
+    XFK_CHECK(hipStreamSynchronize(s));
+    const int nnz = P->hpin[0], nnz_own = P->hpin[1];
     P->nnz = nnz;
     P->nnz_own = nnz_own;
     XFK_CHECK(P->col.alloc(nnz));
@@ -420,8 +421,9 @@ int build_symbolic(xfk_problem *P)
     launch_mark_fix_adj(s, N, P->rowptr.p, P->col.p, P->fixed.p, T.flag);
     XFK_CHECK(P->fix_cols_row.alloc(N));
     launch_compact_flags(s, N, T.flag, T.cnt + 1, P->fix_cols_row.p);
-    int hc[2];
-    XFK_CHECK(d2h(hc, T.cnt, sizeof(int) * 2, s));
+    XFK_CHECK(hipMemcpyAsync(P->hpin + 2, T.cnt, sizeof(int) * 2, hipMemcpyDeviceToHost, s));
+    XFK_CHECK(hipStreamSynchronize(s));
+    const int hc[2] = {P->hpin[2], P->hpin[3]};
     XFK_REQUIRE(hc[0] == 0, XFK_ERR_HIP, "internal: element slot missing from the CSR pattern");
     P->nfix_cols = hc[1];
     XFK_CHECK(P->mu1.alloc(NE));
@@ -728,9 +730,16 @@ static int amg_setup(xfk_problem *P)
     P->amg->omega = P->amg_omega;
     P->amg->rep_rows = P->amg_replicate;
     P->amg->dense_max = P->amg_dense;
-    ScopedEvents<2> ev;
-    XFK_CHECK(ev.create());
-    hipEvent_t e0 = ev[0], e1 = ev[1];
+    // setup time: an event pair per setup, read after the solve's final
+    // synchronisation (no host check here); callers that never read them
+    // recycle the pairs
+    if (P->setup_used >= 64) P->setup_used = 0;
+    if (P->setup_ev.size() < 2 * (P->setup_used + 1)) {
+        P->setup_ev.resize(2 * (P->setup_used + 1), nullptr);
+        for (auto &e : P->setup_ev)
+            if (!e) XFK_CHECK(hipEventCreate(&e));
+    }
+    hipEvent_t e0 = P->setup_ev[2 * P->setup_used], e1 = P->setup_ev[2 * P->setup_used + 1];
     XFK_CHECK(hipEventRecord(e0, s));
     // sharded: rank-local aggregation, global coarse levels (Amg::setup_dist)
     int rc = (P->comm && P->comm->size > 1)
@@ -738,10 +747,7 @@ static int amg_setup(xfk_problem *P)
                                       P->nnz_own)
                  : P->amg->setup(s, P->N, P->N, P->rowptr.p, P->col.p, P->val.p, P->nnz_own);
     XFK_CHECK(hipEventRecord(e1, s));
-    XFK_CHECK(hipEventSynchronize(e1));
-    float ms = 0;
-    XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
-    P->last.ms_amg_setup += ms;
+    ++P->setup_used;
     double ok = (rc == XFK_OK) ? 0.0 : 1.0;   // every rank must take the same preconditioner
     if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
     int rc2 = allreduce_host(P, ok);
@@ -760,20 +766,24 @@ static int pcg_start(xfk_problem *P, int flag)
 {
     hipStream_t s = P->stream;
     const int N = P->N;
-    CgState init{};
-    init.tol = P->precision;
-    XFK_CHECK(hipMemcpyAsync(P->pcg.p, &init, sizeof(CgState), hipMemcpyHostToDevice, s));
+    *P->pcg_host = CgState{};   // pinned: the upload does not stage through the host
+    P->pcg_host->tol = P->precision;
+    XFK_CHECK(hipMemcpyAsync(P->pcg.p, P->pcg_host, sizeof(CgState), hipMemcpyHostToDevice, s));
     if (P->comm) XFK_CHECK(hipMemsetAsync(P->part_loc.p, 0, sizeof(double) * 4 * P->Gpart, s));
     launch_diag_inv(s, N, P->diag.p, P->val.p, P->dinv.p, P->pcg.p);
-    XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(CgState), hipMemcpyDeviceToHost, s));
-    XFK_CHECK(hipStreamSynchronize(s));
-    double singular = P->pcg_host->singular ? 1.0 : 0.0;
-    int rc = allreduce_host(P, singular);
-    if (rc != XFK_OK) return rc;
-    if (singular != 0.0) {
-        set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
-        return XFK_ERR_SINGULAR;
+    int rc = XFK_OK;
+    if (P->comm) {   // every rank must agree before the collective setup
+        XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(CgState), hipMemcpyDeviceToHost, s));
+        XFK_CHECK(hipStreamSynchronize(s));
+        double singular = P->pcg_host->singular ? 1.0 : 0.0;
+        rc = allreduce_host(P, singular);
+        if (rc != XFK_OK) return rc;
+        if (singular != 0.0) {
+            set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
+            return XFK_ERR_SINGULAR;
+        }
     }
+    // (one device: the singular flag is read with the PCG's first poll)
     if ((rc = amg_setup(P)) != XFK_OK) return rc;
     const CgAxpyArgs A0 = cg_args(P, 0);
     const size_t G = (size_t)P->Gpart;
@@ -859,7 +869,12 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
     rc = pcg_start(P, flag);
     if (rc != XFK_OK) return rc;
     long long it = 0;
+    // the first batch: the iterations the first pass of the last solve took
+    // (same problem, same matrix family: one poll), else 8 / 16; an
+    // iteration launched after convergence exits at once but still costs
+    // its launches, so the hint is not padded
     int batch = P->pc_used == XFK_PRECOND_AMG ? 8 : 16;
+    if (flag == 0 && P->pcg_hint0 > 0) batch = P->pcg_hint0;
     for (;;) {
         for (int k = 0; k < batch; ++k, ++it) {
             const bool stamp = P->time_spmv && (it % 16 == 0) && P->spmv_used + 2 <= (int)P->spmv_ev.size();
@@ -870,6 +885,10 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
         XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(CgState), hipMemcpyDeviceToHost, s));
         XFK_CHECK(hipStreamSynchronize(s));
         const CgState &S = *P->pcg_host;
+        if (S.singular) {
+            set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
+            return XFK_ERR_SINGULAR;
+        }
         if (S.done) break;
         if (it >= max_iters) {
             set_error("PCG did not converge within the iteration cap");
@@ -881,6 +900,7 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
         rem = std::max<long long>(8, std::min<long long>(rem + 2, 512));
         batch = (int)rem;
     }
+    if (flag == 0) P->pcg_hint0 = (int)P->pcg_host->iters + 1;   // iteration it = iters detected the stop
     return XFK_OK;
 }
 
@@ -905,7 +925,10 @@ void xfk_problem_destroy(xfk_problem *P)
     (void)hipSetDevice(P->device);
     if (P->stream) (void)hipStreamSynchronize(P->stream);
     for (auto &ev : P->spmv_ev) (void)hipEventDestroy(ev);
+    for (auto &ev : P->setup_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (P->pcg_host) (void)hipHostFree(P->pcg_host);
+    if (P->hpin) (void)hipHostFree(P->hpin);
     if (P->nws_host) (void)hipHostFree(P->nws_host);
     if (P->hc_host) (void)hipHostFree(P->hc_host);
     hipStream_t s = P->stream;
@@ -1281,6 +1304,7 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     UP(P->fix_rows, fix_rows.data(), fix_rows.size());
 #undef UP
     if (e == hipSuccess) e = hipHostMalloc((void **)&P->pcg_host, sizeof(CgState));
+    if (e == hipSuccess) e = hipHostMalloc((void **)&P->hpin, 16 * sizeof(int));
     if (e == hipSuccess) e = hipHostMalloc((void **)&P->nws_host, sizeof(NewtonScalars));
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {
@@ -1421,6 +1445,7 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     P->last.ms_amg_setup = 0;
     P->last.amg_levels = 0;
     P->last.amg_op_complexity = 0;
+    P->setup_used = 0;
     XFK_CHECK(hipEventRecord(e0, s));
     if (!P->symbolic_ready || (flags & XFK_REBUILD_SYMBOLIC)) {
         P->symbolic_ready = false;
@@ -1492,6 +1517,12 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
         }
     }
     XFK_CHECK(hipStreamSynchronize(s));
+    for (int k = 0; k < P->setup_used; ++k) {
+        float m = 0;
+        XFK_CHECK(hipEventElapsedTime(&m, P->setup_ev[2 * k], P->setup_ev[2 * k + 1]));
+        P->last.ms_amg_setup += m;
+    }
+    P->setup_used = 0;
     if (P->time_spmv && P->spmv_used > 0) {
         double sum = 0;
         for (int k = 0; k < P->spmv_used; k += 2) {
@@ -1678,6 +1709,7 @@ int xfk_pcg_solve_csr_pc(int n, const int *rowptr, const int *col, const double 
     if (e == hipSuccess) e = hipMemsetAsync(P->counters.p, 0, sizeof(unsigned) * 8, s);
     if (e == hipSuccess) e = P->pcg.alloc(1);
     if (e == hipSuccess) e = hipHostMalloc((void **)&P->pcg_host, sizeof(CgState));
+    if (e == hipSuccess) e = hipHostMalloc((void **)&P->hpin, 16 * sizeof(int));
     if (e != hipSuccess) {
         set_error(std::string("pcg setup failed: ") + hipGetErrorString(e));
         rc = XFK_ERR_HIP;

@@ -255,6 +255,10 @@ struct xfk_problem {
     xfk::HaloPlan halo;              // slices of the node vectors exchanged with peers
     int Gpart = 0;                   // length of each per-block partial array (agreed by all ranks)
     xfk::TileSplit ts;               // sharded PCG SpMV: interior / boundary tiles (exchange overlap)
+    int *hpin = nullptr;             // pinned scratch for small device -> host reads
+    int pcg_hint0 = 0;               // PCG iterations of the last solve's first pass (first batch)
+    std::vector<hipEvent_t> setup_ev;   // AMG setup event pairs, read after the solve
+    int setup_used = 0;
     xfk::SideStream side;
 
     // host copies kept for host-side setup (periodic maps)
