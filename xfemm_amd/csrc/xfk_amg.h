@@ -90,7 +90,8 @@ struct Amg {
     bool dense_coarse = false;
     DBuf<double> cinv;                // dense inverse of the coarsest level (row major, padded)
     int cinv_ld = 0;
-    DBuf<double> cinv_o;              // nested-dissection order: the other buffer of the unpermute
+    DBuf<double> cinv_o;              // nested-dissection order: the unpermuted inverse
+    const double *cinv_apply = nullptr;   // the inverse the V-cycle applies (cinv or cinv_o)
     DBuf<int> cinv_perm, cinv_iperm, nd_tiles;
     DBuf<unsigned char> nd_mask;
     struct NdPhase {                  // one tree level of the nested-dissection order

@@ -2538,11 +2538,11 @@ int Amg::build(hipStream_t s, int l0)
             const int ldo = ((C.n + kBj - 1) / kBj) * kBj;
             AMG_CHECK(cinv_o.alloc((size_t)ldo * ldo));
             k_dense_unperm<<<ld, 256, 0, s>>>(C.n, ld, ldo, cinv.p, sc, cinv_iperm.p, cinv_o.p);
-            std::swap(cinv.p, cinv_o.p);
-            std::swap(cinv.n, cinv_o.n);
+            cinv_apply = cinv_o.p;   // (two buffers kept apart: no reallocation per setup)
             cinv_ld = ldo;
         } else {
             k_dense_unscale<<<(unsigned)(((size_t)ld * ld / 2 + 255) / 256), 256, 0, s>>>(ld, cinv.p, sc);
+            cinv_apply = cinv.p;
         }
         if (g_prof) g_prof->end();
     }
@@ -3029,7 +3029,7 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
         double *dst = (l == 0) ? out0 : A.xa.p;
         if (M.dense_coarse) {
             XFK_PHASE(lv + "dense inverse x b", 8.0 * A.n * M.cinv_ld + 8.0 * (M.cinv_ld + A.n),
-                      (k_dense_mv<<<(A.n * 64 + 255) / 256, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv.p, b, dst, done)));
+                      (k_dense_mv<<<(A.n * 64 + 255) / 256, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv_apply, b, dst, done)));
             return dst;
         }
         // smoother-only coarsest level: 2 nu sweeps from zero
