@@ -1538,7 +1538,7 @@ __device__ __forceinline__ void smooth_finish(int i, double ax, double w, const 
 // part_gam (the PCG's last level-0 sweep only): per-tile partials of
 // b . out, i.e. gamma = r . u of the CG, in the layout and summation order of
 // k_cg_spmv's (same tiles, same workgroup sum), so the SpMV need not read r
-template <int MODE, int B>
+template <int MODE, int B, int SLOTS = 2>
 __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__restrict__ rowptr,
                                                          const int *__restrict__ col, const double *__restrict__ val,
                                                          const double *__restrict__ dinv,
@@ -1548,7 +1548,7 @@ __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__r
                                                          double *__restrict__ part_gam, const int *__restrict__ tl)
 {
     if (done && *done) return;
-    __shared__ __attribute__((aligned(16))) double lds[8 * B];
+    __shared__ __attribute__((aligned(16))) double lds[4 * SLOTS * B];
     const double ra = rho_of(rho);
     const double w = ra > 0.0 ? 1.0 / ra : 0.0;
     const int t = tl ? tl[xcd_tile(blockIdx.x, gridDim.x)] : xcd_tile(blockIdx.x, gridDim.x);
@@ -1556,10 +1556,10 @@ __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__r
     constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
     double ax;
     if constexpr (implicit)
-        ax = cg_tile_spmv<B>(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; },
+        ax = cg_tile_spmv<B, SLOTS>(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; },
                              lds);
     else
-        ax = cg_tile_spmv<B>(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; }, lds);
+        ax = cg_tile_spmv<B, SLOTS>(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; }, lds);
     const int i = r0 + threadIdx.x;
     if (i < n) smooth_finish<MODE>(i, ax, w, dinv, b, x, out, rout);
     if constexpr (MODE == kSweep) {
@@ -1610,15 +1610,15 @@ __global__ void __launch_bounds__(256) k_amg_smooth_g(int n, int ncl, const int 
 }
 
 // y = M x (ACC: y += M x), tile form (large transfer operators)
-template <int B, bool ACC>
+template <int B, bool ACC, int SLOTS = 2>
 __global__ void __launch_bounds__(B) k_csr_mv_tile(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
                                                    const double *__restrict__ val, const double *__restrict__ x,
                                                    double *__restrict__ y, const int *done)
 {
     if (done && *done) return;
-    __shared__ __attribute__((aligned(16))) double lds[8 * B];
+    __shared__ __attribute__((aligned(16))) double lds[4 * SLOTS * B];
     const int r0 = xcd_tile(blockIdx.x, gridDim.x) * B;
-    const double s = cg_tile_spmv<B>(r0, n, rowptr, col, val, [&](int j) { return x[j]; }, lds);
+    const double s = cg_tile_spmv<B, SLOTS>(r0, n, rowptr, col, val, [&](int j) { return x[j]; }, lds);
     const int i = r0 + threadIdx.x;
     if (i < n) y[i] = ACC ? y[i] + s : s;
 }
@@ -1972,9 +1972,15 @@ void launch_mv(hipStream_t s, int n, const int *rowptr, const int *col, const do
 {
     if (n <= 0) return;
     if (n >= kTileMinRows && G <= 8) {
+        // G = 8: 7..20 entries per row -> 6 slots per lane, one staging pass per tile
         const int g = (n + 255) / 256;
-        if (acc) k_csr_mv_tile<256, true><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
-        else k_csr_mv_tile<256, false><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+        if (G <= 4) {
+            if (acc) k_csr_mv_tile<256, true, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+            else k_csr_mv_tile<256, false, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+        } else {
+            if (acc) k_csr_mv_tile<256, true, 6><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+            else k_csr_mv_tile<256, false, 6><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+        }
         return;
     }
     const int g = (int)(((long long)n * G + 255) / 256);
@@ -2948,9 +2954,14 @@ void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned lon
         return;
     }
     if (A.n >= kTileMinRows) {
+        // coarse levels carry 10-16 entries per row: 4 slots per lane, one pass per tile
         const int g = tl ? nt : (A.n + 255) / 256;
-        k_amg_smooth<MODE, 256><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
-                                                  out, rout, done, nullptr, tl);
+        if ((double)A.nnz <= 8.0 * A.n)
+            k_amg_smooth<MODE, 256, 2><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b,
+                                                         x, out, rout, done, nullptr, tl);
+        else
+            k_amg_smooth<MODE, 256, 4><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b,
+                                                         x, out, rout, done, nullptr, tl);
         return;
     }
     const int G = lanes_for(A.n > 0 ? (double)A.nnz / A.n : 1.0);

@@ -70,12 +70,16 @@ __device__ __forceinline__ int xcd_tile(int b, int nb)
 // each thread sums its own row in order.  Measured on the configs[2] matrix
 // (tools/lab/spmv_lab.hip): 16.5 us vs 19.9 us for one 4/8-B entry per lane,
 // bit-identical sums.  col / val must be 16-B aligned (hipMalloc'd arrays).
-template <int B = kCgBlock, class XF>
+// SLOTS: 4-entry slots per lane per pass (CAP = 4 SLOTS B products staged per
+// pass, lds holds CAP doubles): 2 for the ~7 entries per row of the fine
+// level, more for the longer rows of coarse levels and of R, so that a tile
+// takes one pass (each pass is a load / barrier / sum / barrier round trip)
+template <int B = kCgBlock, int SLOTS = 2, class XF>
 __device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restrict__ rowptr,
                                                const int *__restrict__ col, const double *__restrict__ val,
                                                XF X, double *lds)
 {
-    constexpr int CAP = 8 * B;
+    constexpr int CAP = 4 * SLOTS * B;
     const int r = r0 + threadIdx.x;
     const int rend = min(r0 + B, N);
     const int s = rowptr[r0], e = rowptr[rend];
@@ -84,7 +88,7 @@ __device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restr
     for (int c0 = s & ~3; c0 < e; c0 += CAP) {
         const int c1 = min(e, c0 + CAP);
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
+        for (int m = 0; m < SLOTS; ++m) {
             const int k = c0 + 4 * (threadIdx.x + m * B);
             if (k >= s && k + 3 < c1) {
                 const int4 c = *reinterpret_cast<const int4 *>(col + k);
