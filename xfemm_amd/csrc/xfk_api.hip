@@ -272,7 +272,7 @@ struct SymTmp {
     // zero-initialised block (one memset)
     int *deg, *cursor, *cnt, *hist;
     // uninitialised
-    int *rowcnt, *keys_out, *iota, *flag, *iperm, *rowtmp;
+    int *rowcnt, *keys_out, *iota, *flag, *iperm, *rowtmp, *slot_val, *slot_key;
     unsigned char *active;
     unsigned long long *maxkey, *used;
     size_t zero_bytes = 0, bytes = 0;
@@ -299,6 +299,8 @@ struct SymTmp {
         take(maxkey, N);
         take(used, 2 * (size_t)N);
         take(iperm, NE);
+        take(slot_val, 3 * (size_t)NE);
+        take(slot_key, 3 * (size_t)NE);
         take(rowtmp, (size_t)row_tmp_size(N, NE, nfill));
         bytes = off;
     }
@@ -322,10 +324,23 @@ int build_symbolic(xfk_problem *P)
     // node -> incident elements
     XFK_CHECK(P->n2e_ptr.alloc(NL + 1));
     XFK_CHECK(P->n2e.alloc(3 * (size_t)NE));
-    launch_count_incidence(s, NE, P->p_raw.p, T.deg);
-    XFK_CHECK(exclusive_scan(P, T.deg, P->n2e_ptr.p, NL));
-    launch_fill_n2e(s, NE, P->p_raw.p, P->n2e_ptr.p, T.cursor, P->n2e.p);
-    launch_sort_segments(s, NL, P->n2e_ptr.p, P->n2e.p);
+    // stable radix sort of the element-major incidence slots by node: each
+    // node's elements come out ascending (the reference's AddTo order) with no
+    // atomics and no per-node sort (was: atomic count + fill + insertion sort)
+    launch_slot_elements(s, NE, T.slot_val);
+    {
+        int bits = 1;
+        while (bits < 31 && (1LL << bits) <= NL) ++bits;
+        void *tmp = nullptr;
+        size_t bytes = 0;
+        const int n3 = 3 * NE;
+        XFK_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, P->p_raw.p, T.slot_key, T.slot_val, P->n2e.p, n3, 0,
+                                                     bits, s));
+        XFK_CHECK(cub_scratch(P, bytes, &tmp));
+        XFK_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, P->p_raw.p, T.slot_key, T.slot_val, P->n2e.p, n3, 0,
+                                                     bits, s));
+        launch_n2e_ptr(s, NL, T.slot_key, n3, P->n2e_ptr.p);
+    }
 
     // periodic fill-in entries, CSR by row
     const int *fp = nullptr, *fc = nullptr;

@@ -103,6 +103,29 @@ __global__ void k_fill_n2e(int NE, const int *__restrict__ p, const int *__restr
     }
 }
 
+// Node -> element lists by a stable radix sort of the (node, element)
+// incidence pairs (xfk_api.hip: build_symbolic): values k / 3 of the
+// element-major incidence slots, then each node's first slot by a lower
+// bound in the sorted keys (nodes of no element get an empty range)
+__global__ void k_slot_elements(long long n3, int *__restrict__ v)
+{
+    const long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (k < n3) v[k] = (int)(k / 3);
+}
+
+__global__ void k_n2e_ptr(int NL, const int *__restrict__ keys, int n3, int *__restrict__ ptr)
+{
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n > NL) return;
+    int lo = 0, hi = n3;   // first slot with key >= n
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < n) lo = mid + 1;
+        else hi = mid;
+    }
+    ptr[n] = lo;
+}
+
 // Deterministic order of each node's element list (insertion sort, lists are short).
 __global__ void k_sort_segments(int N, const int *__restrict__ ptr, int *__restrict__ a)
 {
@@ -903,6 +926,15 @@ void launch_count_incidence(hipStream_t s, int NE, const int *p, int *deg)
 void launch_fill_n2e(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e)
 {
     if (NE) k_fill_n2e<<<nblk(NE), kBlock, 0, s>>>(NE, p, ptr, cursor, n2e);
+}
+void launch_slot_elements(hipStream_t s, int NE, int *v)
+{
+    const long long n3 = 3LL * NE;
+    if (NE) k_slot_elements<<<(unsigned)((n3 + kBlock - 1) / kBlock), kBlock, 0, s>>>(n3, v);
+}
+void launch_n2e_ptr(hipStream_t s, int NL, const int *keys, int n3, int *ptr)
+{
+    k_n2e_ptr<<<nblk(NL + 1), kBlock, 0, s>>>(NL, keys, n3, ptr);
 }
 void launch_sort_segments(hipStream_t s, int N, const int *ptr, int *a)
 {
