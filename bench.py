@@ -118,7 +118,7 @@ def nonlinear_secondary(device, args):
     from xfemm_amd import kernels, synth
     kw = synth.magnetostatic(args.cells, nonlinear=True)
     P = kernels.Static2DProblem(device=device, precond=args.precond, amg_sweeps=args.amg_sweeps,
-                                amg_omega=args.amg_omega, amg_dense=args.amg_dense, **kw)
+                                amg_omega=args.amg_omega, amg_dense=args.amg_dense, amg_theta=args.amg_theta, **kw)
     P.solve(rebuild_symbolic=True)
     _hip_sync()
     t0 = time.perf_counter()
@@ -172,6 +172,7 @@ def main():
     ap.add_argument("--amg-sweeps", type=int, default=1, help="Jacobi sweeps before/after the coarse correction")
     ap.add_argument("--amg-omega", type=float, default=1.75, help="Jacobi weight factor (weight omega / rho)")
     ap.add_argument("--amg-dense", type=int, default=None, help="dense coarsest level of at most this many rows")
+    ap.add_argument("--amg-theta", type=float, default=None, help="strength threshold (default 0.08)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phases", action="store_true", help="skip the per-phase table")
     ap.add_argument("--traffic", type=float, default=None,
@@ -208,13 +209,13 @@ def main():
         with stdout_to_stderr():
             comm = kernels.Comm.rccl(uid, rank, world, local)
         P = kernels.Static2DProblem(device=local, comm=comm, precond=args.precond, amg_sweeps=args.amg_sweeps,
-                                    amg_omega=args.amg_omega, amg_dense=args.amg_dense, **kw)
+                                    amg_omega=args.amg_omega, amg_dense=args.amg_dense, amg_theta=args.amg_theta, **kw)
         n_dof = P.n_nodes                       # global DoF of the sharded mesh
     else:
         cells = args.cells
         kw = synth.magnetostatic(cells, nonlinear=args.nonlinear)
         P = kernels.Static2DProblem(device=local, precond=args.precond, amg_sweeps=args.amg_sweeps,
-                                    amg_omega=args.amg_omega, amg_dense=args.amg_dense, **kw)
+                                    amg_omega=args.amg_omega, amg_dense=args.amg_dense, amg_theta=args.amg_theta, **kw)
         n_dof = P.n_nodes
 
     def barrier():
@@ -272,7 +273,7 @@ def main():
         P.close()
         if rank == 0:
             Q = kernels.Static2DProblem(device=local, precond=args.precond, amg_sweeps=args.amg_sweeps,
-                                        amg_omega=args.amg_omega, amg_dense=args.amg_dense, **kw)
+                                        amg_omega=args.amg_omega, amg_dense=args.amg_dense, amg_theta=args.amg_theta, **kw)
             Q.solve(rebuild_symbolic=True)
             t1 = time.perf_counter()
             r1 = Q.solve(rebuild_symbolic=True)
