@@ -863,17 +863,19 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
 
 // padded rows (row * cap) -> CSR; 16 lanes per row, so a row's reads and
 // writes are contiguous runs
-// nnz_out (optional): the product's length, for a deferred host read
+// nnz_out (optional): the product's length, for a deferred host read;
+// L lanes per row (a quarter of the slot capacity: the rows hold about that many)
+template <int L>
 __global__ void k_spgemm_compact(int nrows, int cap, const int *__restrict__ crow, const int *__restrict__ pcol,
                                  const double *__restrict__ pval, int *__restrict__ ccol, double *__restrict__ cval,
                                  int *nnz_out)
 {
     const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (t == 0 && nnz_out) *nnz_out = crow[nrows];
-    const int row = (int)(t >> 4), l = (int)(t & 15);
+    const int row = (int)(t / L), l = (int)(t % L);
     if (row >= nrows) return;
     const int b = crow[row], n = crow[row + 1] - b;
-    for (int m = l; m < n; m += 16) {
+    for (int m = l; m < n; m += L) {
         ccol[b + m] = pcol[(size_t)row * cap + m];
         cval[b + m] = pval[(size_t)row * cap + m];
     }
@@ -1811,6 +1813,20 @@ int read_flag(Amg &A, hipStream_t s, int idx, int &v)
 }
 
 // C = X Y (rowptr/col/val allocated here); XFK_ERR_UNSUPPORTED on LDS overflow
+void launch_compact(hipStream_t s, int nrows, int cap, const int *crow, const int *pc, const double *pv, int *ccol,
+                    double *cval, int *nnz_out)
+{
+    if (cap <= 16)
+        k_spgemm_compact<4><<<(unsigned)(((long long)nrows * 4 + kB - 1) / kB), kB, 0, s>>>(nrows, cap, crow, pc, pv,
+                                                                                             ccol, cval, nnz_out);
+    else if (cap <= 32)
+        k_spgemm_compact<8><<<(unsigned)(((long long)nrows * 8 + kB - 1) / kB), kB, 0, s>>>(nrows, cap, crow, pc, pv,
+                                                                                             ccol, cval, nnz_out);
+    else
+        k_spgemm_compact<16><<<(unsigned)(((long long)nrows * 16 + kB - 1) / kB), kB, 0, s>>>(nrows, cap, crow, pc,
+                                                                                               pv, ccol, cval, nnz_out);
+}
+
 template <bool PMODE>
 int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<int> &crow, DBuf<int> &ccol,
            DBuf<double> &cval, long long &cnnz, int key = -1)
@@ -1855,8 +1871,7 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
         AMG_CHECK(ccol.alloc((size_t)std::max(1LL, cnnz)));
         AMG_CHECK(cval.alloc((size_t)std::max(1LL, cnnz)));
         if (nrows > 0)
-            k_spgemm_compact<<<(unsigned)(((long long)nrows * 16 + kB - 1) / kB), kB, 0, s>>>(
-                nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p, nullptr);
+            launch_compact(s, nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p, nullptr);
         return XFK_OK;
     };
     // the slot capacity this product needed in the previous setup (same
@@ -1879,8 +1894,7 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
                 int rc = scan_only(M, s, M.cnt.p, crow.p, nrows);
                 if (rc != XFK_OK) return rc;
                 if (nrows > 0)
-                    k_spgemm_compact<<<(unsigned)(((long long)nrows * 16 + kB - 1) / kB), kB, 0, s>>>(
-                        nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p, slot + 1);
+                    launch_compact(s, nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p, slot + 1);
                 else
                     AMG_CHECK(hipMemsetAsync(slot + 1, 0, sizeof(int), s));
                 M.def_target[M.def_n / 2] = &cnnz;
