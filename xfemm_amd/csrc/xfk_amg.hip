@@ -138,6 +138,11 @@ __global__ void k_amg_diag(int n, const int *__restrict__ rowptr, const int *__r
 // strong flags per nonzero (1 strong off-diagonal, 2 diagonal, 0 weak or
 // outside the block), strong degree per row, lumped filtered diagonal,
 // Gershgorin bounds of D^-1 A (rho[0]) and D_F^-1 A_F (rho[1])
+// kStrG lanes per row (consecutive entries of a row on consecutive lanes:
+// coalesced col / val reads and flag writes, the row's sums by shuffles)
+constexpr int kStrG = 4;
+inline int nb_str(long long n) { return nb(n * kStrG); }
+
 __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double theta, const int *__restrict__ rowptr,
                                                      const int *__restrict__ col, const double *__restrict__ val,
                                                      const double *__restrict__ absd,
@@ -146,13 +151,14 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
                                                      double *__restrict__ rho_part)
 {
     __shared__ double red[2 * (kB / 64)];
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / kStrG;
+    const int g = threadIdx.x % kStrG;
     double rA = 0.0, rF = 0.0;
+    double aii = 0.0, lump = 0.0, sumS = 0.0, sumA = 0.0;
+    int deg = 0, hdeg = 0;
     if (i < n) {
         const double ai = absd[i];
-        double aii = 0.0, lump = 0.0, sumS = 0.0, sumA = 0.0;
-        int deg = 0, hdeg = 0;
-        for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        for (int k = rowptr[i] + g; k < rowptr[i + 1]; k += kStrG) {
             const int j = col[k];
             const double a = val[k];
             unsigned char f = 0;
@@ -179,6 +185,17 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
             }
             sflag[k] = f;
         }
+    }
+#pragma unroll
+    for (int off = 1; off < kStrG; off <<= 1) {   // fixed butterfly: the same bits on every run
+        aii += __shfl_xor(aii, off, kStrG);
+        lump += __shfl_xor(lump, off, kStrG);
+        sumS += __shfl_xor(sumS, off, kStrG);
+        sumA += __shfl_xor(sumA, off, kStrG);
+        deg += __shfl_xor(deg, off, kStrG);
+        hdeg += __shfl_xor(hdeg, off, kStrG);
+    }
+    if (i < n && g == 0) {
         const double dF = aii + lump;
         // -1: every strong coupling crosses to a peer -> a singleton aggregate
         sdeg[i] = (deg == 0 && hdeg > 0) ? -1 : deg;
@@ -2415,10 +2432,10 @@ int Amg::build(hipStream_t s, int l0)
             break;
         }
         AMG_CHECK(sflag.alloc((size_t)A.nnz));
-        AMG_CHECK(rho_part.alloc(2 * (size_t)nb(n)));
-        k_amg_strength<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
-                                            dfinv.p, wF.p, rho_part.p);
-        k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, omega, rho.p + 2 * l);
+        AMG_CHECK(rho_part.alloc(2 * (size_t)nb_str(n)));
+        k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
+                                                dfinv.p, wF.p, rho_part.p);
+        k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p + 2 * l);
         if (g_prof) g_prof->end();
         if (l == kAmgMaxLevels - 1) break;   // smoother-only coarsest level
         long long nc = 0;
@@ -2626,11 +2643,11 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
         AMG_CHECK(wF.alloc(std::max(1, nl)));
         AMG_CHECK(cnt.alloc((size_t)nl + 1));
         AMG_CHECK(sflag.alloc((size_t)std::max(1LL, A.nnz)));
-        AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb(nl))));
+        AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(nl))));
         k_amg_diag<<<nb(nl), kB, 0, s>>>(nl, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
-        k_amg_strength<<<nb(nl), kB, 0, s>>>(nl, nl, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p, dfinv.p,
-                                             wF.p, rho_part.p);
-        k_max_reduce<<<1, 1024, 0, s>>>(nb(nl), rho_part.p, omega, rho.p + 2 * l);
+        k_amg_strength<<<nb_str(nl), kB, 0, s>>>(nl, nl, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
+                                                 dfinv.p, wF.p, rho_part.p);
+        k_max_reduce<<<1, 1024, 0, s>>>(nb_str(nl), rho_part.p, omega, rho.p + 2 * l);
         long long nc = 0;
         rc = aggregate(s, l, nc, false);
         if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
@@ -3172,12 +3189,12 @@ int Amg::refresh(hipStream_t s)
     AMG_CHECK(wF.alloc(std::max(1, n)));
     AMG_CHECK(cnt.alloc((size_t)n + 1));
     AMG_CHECK(sflag.alloc((size_t)std::max(1LL, A.nnz)));
-    AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb(n))));
+    AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(n))));
     if (n > 0) {
         k_amg_diag<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
-        k_amg_strength<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
-                                            dfinv.p, wF.p, rho_part.p);
-        k_max_reduce<<<1, 1024, 0, s>>>(nb(n), rho_part.p, omega, rho.p);
+        k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
+                                                dfinv.p, wF.p, rho_part.p);
+        k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p);
     }
     AMG_CHECK(hipGetLastError());
     return XFK_OK;
