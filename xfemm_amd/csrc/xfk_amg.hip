@@ -238,36 +238,47 @@ __global__ void k_mis_init(int n, const int *__restrict__ sdeg, MisKey *__restri
 // undecided flag is double-buffered by round parity (prev = the last round's
 // result, cur = this round's), and once a round leaves nothing undecided the
 // later rounds of the batch exit at once (passing the 0 on).
+// G lanes per row (coarse levels, 10-16 entries per row; 1 on the fine level):
+// consecutive strong entries on consecutive lanes, the maximum by a butterfly
+template <int G>
 __global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
                           const unsigned char *__restrict__ sflag, const MisKey *__restrict__ in,
                           MisKey *__restrict__ out, const int *prev, int *cur, int *run)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) {   // k_mis_update of this round runs after this launch
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = t / G, g = t % G;
+    if (t == 0) {   // k_mis_update of this round runs after this launch
         if (*prev != 0) *run += 1;   // rounds that did work (the next setup's batch size)
         *cur = 0;
     }
     if (i >= n || *prev == 0) return;
     MisKey m = in[i];
-    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
+    for (int k = rowptr[i] + g; k < rowptr[i + 1]; k += G)
         if (sflag[k] == 1) m = max(m, in[col[k]]);
-    out[i] = m;
+#pragma unroll
+    for (int off = 1; off < G; off <<= 1) m = max(m, (MisKey)__shfl_xor((int)m, off, G));
+    if (g == 0) out[i] = m;
 }
 
 // second max sweep fused with the state update: an undecided node whose
 // distance-2 maximum is itself joins the set; one that sees a set member
 // within distance 2 leaves
+template <int G>
 __global__ void k_mis_update(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
                              const unsigned char *__restrict__ sflag, const MisKey *__restrict__ t1,
                              MisKey *__restrict__ key, const int *prev, int *undecided)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = t / G, g = t % G;
     if (i >= n || *prev == 0) return;
     const MisKey k = key[i];
-    if (key_st(k) != kStUnd) return;
+    if (key_st(k) != kStUnd) return;   // uniform over the row's lanes
     MisKey m = t1[i];
-    for (int q = rowptr[i]; q < rowptr[i + 1]; ++q)
+    for (int q = rowptr[i] + g; q < rowptr[i + 1]; q += G)
         if (sflag[q] == 1) m = max(m, t1[col[q]]);
+#pragma unroll
+    for (int off = 1; off < G; off <<= 1) m = max(m, (MisKey)__shfl_xor((int)m, off, G));
+    if (g != 0) return;
     if (key_low(m) == perm30((unsigned)i)) key[i] = (kStIn << 30) | key_low(k);
     else if (key_st(m) == kStIn) key[i] = key_low(k);
     else *undecided = 1;   // benign race: every writer stores 1
@@ -2181,8 +2192,13 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     for (int batch = hint != mis_hint.end() ? std::max(1, hint->second) : 12;; batch = 2) {
         for (int b = 0; b < batch; ++b, ++rounds) {
             int *cur = und2 + (rounds & 1), *prev = und2 + ((rounds + 1) & 1);
-            k_mis_max<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur, run);
-            k_mis_update<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, prev, cur);
+            if (A.nnz > 9LL * n) {
+                k_mis_max<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur, run);
+                k_mis_update<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, prev, cur);
+            } else {
+                k_mis_max<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur, run);
+                k_mis_update<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, prev, cur);
+            }
         }
         k_agg_roots<<<nb(n), kB, 0, s>>>(n, key.p, flag.p);
         int rc = scan_only(*this, s, flag.p, cursor.p, n);   // cursor = root ids
