@@ -95,8 +95,8 @@ struct Amg {
     DBuf<int> cinv_perm, cinv_iperm, nd_tiles;
     DBuf<unsigned char> nd_mask;
     struct NdPhase {                  // one tree level of the nested-dissection order
-        int nch = 0, steps = 0;       // pivot chains (<= 4) and their block steps
-        int base[4] = {}, next_slot[4] = {};
+        int nch = 0, steps = 0;       // pivot chains (<= 8) and their block steps
+        int base[8] = {}, next_slot[8] = {};
         int tiles_off = 0, ntiles = 0;
     };
     std::vector<NdPhase> nd_phases;

@@ -1345,7 +1345,7 @@ __global__ void __launch_bounds__(256) k_bgj_step(int k, int nbk, int ld, double
 // ancestors), the top separator last.  Each tile applies the update of every
 // chain whose region holds it (separator tiles: several, summed on the MFMA
 // in chain order); per block, bit c of `mask` marks chain c's region.
-constexpr int kNdChains = 4;
+constexpr int kNdChains = 8;
 struct BgjStep {
     int n;                                             // chains of this step
     int k[kNdChains];                                  // their pivot blocks
@@ -2283,10 +2283,9 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
 // separator would be empty or hold more than a quarter of the rows.
 // Host-synchronising (the coarsest level has <= dense_max rows).
 namespace {
-void nd_bisect(const std::vector<int> &rp, const std::vector<int> &cl, const std::vector<int> &rows,
-               std::vector<char> &inl, std::vector<int> &L, std::vector<int> &R, std::vector<int> &S)
+void nd_split_at(const std::vector<int> &rp, const std::vector<int> &cl, const std::vector<int> &rows, size_t h,
+                 std::vector<char> &inl, std::vector<int> &L, std::vector<int> &R, std::vector<int> &S)
 {
-    const size_t h = rows.size() / 2;
     L.assign(rows.begin(), rows.begin() + h);
     R.clear();
     S.clear();
@@ -2298,6 +2297,15 @@ void nd_bisect(const std::vector<int> &rp, const std::vector<int> &cl, const std
         (cross ? S : R).push_back(r);
     }
     for (int r : L) inl[r] = 0;
+}
+// split position chosen so that the two parts (not counting the separator)
+// come out about equal: the chain length of a phase is its largest part
+void nd_bisect(const std::vector<int> &rp, const std::vector<int> &cl, const std::vector<int> &rows,
+               std::vector<char> &inl, std::vector<int> &L, std::vector<int> &R, std::vector<int> &S)
+{
+    nd_split_at(rp, cl, rows, rows.size() / 2, inl, L, R, S);
+    const size_t h = (rows.size() - S.size()) / 2;
+    if (h > 0 && h != rows.size() / 2) nd_split_at(rp, cl, rows, h, inl, L, R, S);
 }
 }  // namespace
 
@@ -2336,22 +2344,69 @@ int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &ld)
         std::vector<int> sub;
     };
     std::vector<G> g;
-    std::vector<int> A, B, S;
-    nd_bisect(rp, cl, all, inl, A, B, S);
-    if (A.empty() || B.empty() || S.empty() || 4 * S.size() > (size_t)n) return XFK_OK;
-    bool two = n >= 16 * kBj;
-    std::vector<int> A1, A2, SA, B1, B2, SB;
-    if (two) {
-        nd_bisect(rp, cl, A, inl, A1, A2, SA);
-        nd_bisect(rp, cl, B, inl, B1, B2, SB);
-        two = !A1.empty() && !A2.empty() && !SA.empty() && !B1.empty() && !B2.empty() && !SB.empty() &&
-              4 * (S.size() + SA.size() + SB.size()) <= (size_t)n;
+    // the deepest bisection (3, 2, then 1 level) whose groups are all non-empty,
+    // whose separators hold at most a quarter of the rows, and whose leaves
+    // keep >= 1 block; leaves are phase 0 (slots = leaf index), the
+    // separators of bisection level lev are phase D - lev
+    for (int D = n >= 24 * kBj ? 3 : (n >= 16 * kBj ? 2 : 1); D >= 1 && g.empty(); --D) {
+        std::vector<std::vector<int>> sets{all};
+        std::vector<std::vector<std::vector<int>>> seps(D);   // seps[lev][m]
+        bool ok = true;
+        size_t nsep = 0;
+        for (int lev = 0; lev < D && ok; ++lev) {
+            std::vector<std::vector<int>> next;
+            for (const auto &x : sets) {
+                std::vector<int> L, R, S;
+                nd_bisect(rp, cl, x, inl, L, R, S);
+                ok = ok && !L.empty() && !R.empty() && !S.empty();
+                nsep += S.size();
+                next.push_back(std::move(L));
+                next.push_back(std::move(R));
+                seps[lev].push_back(std::move(S));
+            }
+            sets = std::move(next);
+        }
+        if (std::getenv("XFK_AMG_DEBUG")) {
+            std::fprintf(stderr, "[amg] nested dissection depth %d: ok %d separators %zu, sets", D, (int)ok, nsep);
+            for (const auto &x : sets) std::fprintf(stderr, " %zu", x.size());
+            std::fprintf(stderr, "\n");
+        }
+        if (!ok || 3 * nsep > (size_t)n) continue;
+        if (D > 1)
+            for (const auto &x : sets) ok = ok && x.size() >= (size_t)kBj;
+        if (!ok) continue;
+        // group indices: leaves 0 .. 2^D - 1, then separators by level, deepest first
+        const int nl = 1 << D;
+        std::vector<int> sep_at(D);   // first group index of level lev's separators
+        int q = nl;
+        for (int lev = D - 1; lev >= 0; --lev) {
+            sep_at[lev] = q;
+            q += 1 << lev;
+        }
+        g.resize(q);
+        for (int k = 0; k < nl; ++k)
+            g[k] = {sets[k], 0, k, sep_at[D - 1] + (k >> 1), {k}};
+        for (int lev = D - 1; lev >= 0; --lev)
+            for (int m = 0; m < (1 << lev); ++m) {
+                G &x = g[sep_at[lev] + m];
+                x.rows = seps[lev][m];
+                x.phase = D - lev;
+                x.slot = m;
+                x.parent = lev > 0 ? sep_at[lev - 1] + (m >> 1) : -1;
+                // subtree: leaves and deeper separators under this one, and itself
+                for (int k = 0; k < nl; ++k)
+                    if ((k >> (D - lev)) == m) x.sub.push_back(k);
+                for (int l2 = lev + 1; l2 < D; ++l2)
+                    for (int m2 = 0; m2 < (1 << l2); ++m2)
+                        if ((m2 >> (l2 - lev)) == m) x.sub.push_back(sep_at[l2] + m2);
+                x.sub.push_back(sep_at[lev] + m);
+            }
     }
-    if (two) {
-        g = {{A1, 0, 0, 4, {0}}, {A2, 0, 1, 4, {1}}, {B1, 0, 2, 5, {2}}, {B2, 0, 3, 5, {3}},
-             {SA, 1, 0, 6, {0, 1, 4}}, {SB, 1, 1, 6, {2, 3, 5}}, {S, 2, 0, -1, {0, 1, 2, 3, 4, 5, 6}}};
-    } else {
-        g = {{A, 0, 0, 2, {0}}, {B, 0, 1, 2, {1}}, {S, 1, 0, -1, {0, 1, 2}}};
+    if (g.empty()) return XFK_OK;
+    if (std::getenv("XFK_AMG_DEBUG")) {
+        std::fprintf(stderr, "[amg] coarsest %d rows: nested dissection, %d groups:", n, (int)g.size());
+        for (const G &x : g) std::fprintf(stderr, " %d/%d", (int)x.rows.size(), x.phase);
+        std::fprintf(stderr, "\n");
     }
     const int nph = g.back().phase + 1;
     // blocks: each phase's groups padded to the phase's largest group
