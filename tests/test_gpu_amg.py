@@ -88,6 +88,24 @@ def test_amg_is_deterministic():
     assert np.array_equal(A1, A2) and np.array_equal(A1, A3)
 
 
+def test_spgemm_capacity_overflow_rebuilds(monkeypatch):
+    """The SpGEMMs of a setup take their slot capacity from the previous setup
+    of the same call site without a host check; a product that no longer
+    fits is detected in the kernel and the hierarchy is rebuilt with measured
+    capacities.  XFK_AMG_TEST_SMALL_HINT stores too-small capacities, so every
+    later setup overflows and rebuilds: the answer must not change."""
+    kw = synth.magnetostatic(200)
+    P = kernels.Static2DProblem(**kw, precond="amg")
+    P.solve()
+    A1 = P.solution()
+    monkeypatch.setenv("XFK_AMG_TEST_SMALL_HINT", "1")
+    for _ in range(3):
+        r = P.solve(rebuild_symbolic=True)
+        assert np.array_equal(P.solution(), A1)
+    P.close()
+    assert r["precond"] == kernels.XFK_PRECOND_AMG
+
+
 def _laplace_random(n, seed, shift=1.0):
     """5-point operator with random positive conductances and a Dirichlet-like
     diagonal shift on the first row of nodes (SPD; shift = 0: pure Neumann,

@@ -1956,7 +1956,12 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
             set_error("AMG: internal SpGEMM capacity error");
             return XFK_ERR_HIP;
         }
-        if (key >= 0) M.cap_hint[key] = cap;
+        if (key >= 0) {
+            // XFK_AMG_TEST_SMALL_HINT=1 (tests only): store a too-small capacity so
+            // the next setup takes the overflow-and-rebuild path
+            const bool small = std::getenv("XFK_AMG_TEST_SMALL_HINT") != nullptr;
+            M.cap_hint[key] = small ? 16 : cap;   // (16: the smallest capacity the kernels have)
+        }
         return XFK_OK;
     }
     AMG_CHECK(hipMemsetAsync(M.dev_int.p + 2, 0, 2 * sizeof(int), s));
