@@ -106,10 +106,35 @@ def test_newton_ac_file_interface_end_to_end(tmp_path):
     assert rel_err(A, Ac) <= TOL, parity_message(A, Ao, Ac, TOL)
 
 
-def test_newton_ac_case2_is_reported():
-    kw = synth.harmonic(10, nonlinear=True)
-    kw["circuits"][1] = dict(type=0, amps_re=1.0)
-    kw["ac_solver"] = 1
-    _, _, kk = synth_to_oracle(kw)
-    with pytest.raises(kernels.XfkError, match="Case-2"):
-        kernels.Harmonic2DProblem(**kk)
+@pytest.mark.parametrize("n", [14, 20])
+def test_newton_ac_case2_matches_oracle(n):
+    """Newton AC with a Case-2 circuit (specified current in a conducting
+    region): KludgeSolve over the bordered system [V; u] (cspars.cpp:1000-1060
+    on the full unknown vector).  The device's inner solves go through the
+    Schur complement; the answer, the circuit voltage gradient and the
+    circuit current match the oracle at the converged answer."""
+    kw = _case("planar", n)
+    kw["circuits"][1] = dict(type=0, amps_re=2.0, amps_im=0.5)
+    pr, mesh, kk = synth_to_oracle(kw)
+    Ao, st, circ_o = oh.solve(pr, mesh)
+    import copy
+    from util import CONVERGED_PRECISION
+    pr2 = copy.deepcopy(pr)
+    pr2.Precision = CONVERGED_PRECISION
+    Ac, _, circ_c = oh.solve(pr2, mesh)
+    P = kernels.Harmonic2DProblem(**kk)
+    r = P.solve()
+    A = P.solution()
+    cc, J, dV = P.circuits()
+    P.close()
+    assert r["newton_iters"] >= 2
+    assert rel_err(A, Ac) <= TOL, parity_message(A, Ao, Ac, TOL) + " (%d / %d passes)" % (
+        r["newton_iters"], st["newton_iters"])
+    for k, (case, Jo, dVo) in enumerate(circ_c):
+        assert cc[k] == case and abs(J[k] - Jo) <= 1e-12 * max(1.0, abs(Jo))
+        if case == 2:
+            assert abs(dV[k] - dVo) <= 1e-4 * max(1e-12, abs(dVo)), (k, dV[k], dVo)
+    kw0 = dict(kw, ac_solver=0)
+    pr0, mesh0, _ = synth_to_oracle(kw0)
+    A0, _, _ = oh.solve(pr0, mesh0)
+    assert rel_err(A0, Ac) > 10 * TOL

@@ -840,6 +840,20 @@ __global__ void k_hc_border_combine(int N, int nc2, const double2 *__restrict__ 
     x[i] = v;
 }
 
+// y += sign sum_q C_q u_q (the border columns applied to the circuit unknowns)
+__global__ void k_hc_add_cu(int N, int nc2, const double *__restrict__ Cb, const double2 *__restrict__ u,
+                            double sign, double2 *__restrict__ y)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    double2 a = y[i];
+    for (int q = 0; q < nc2; ++q) {
+        const double2 t = cmul(cx(Cb[2 * (size_t)q * N + i], Cb[2 * (size_t)q * N + N + i]), u[q]);
+        a = cx(a.x + sign * t.x, a.y + sign * t.y);
+    }
+    y[i] = a;
+}
+
 // V = Relax V + (1 - Relax) V_old (harmonic2d.cpp:851)
 __global__ void k_hrelax(int N, double relax, double2 *__restrict__ V, const double2 *__restrict__ Vo)
 {
@@ -1437,12 +1451,6 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     P->hc2_u.assign(nc2, cx(0, 0));
     P->any_nonlinear = nonlin;
     P->ac_solver = ac->ac_solver;
-    if (nonlin && ac->ac_solver == 1 && nc2 > 0) {
-        set_error("the Newton AC solver with Case-2 circuits (specified current in a conducting region) is not "
-                  "supported by this build");
-        xfk_problem_destroy(P);
-        return XFK_ERR_UNSUPPORTED;
-    }
     P->axi = axi;
     if (axi) P->axi_x.assign(d->x, d->x + N);
     P->ext_ro = G.ext_ro;
@@ -1781,52 +1789,35 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
             return XFK_OK;
         };
         const int nc2 = (int)P->hc2_circ.size();
-        int src;
-        if (nc2 == 0) {
-            if (A.newton) {
-                if ((src = kludge()) != XFK_OK) return src;
-            } else if ((src = solve_one(v, P->b.p, P->b_im.p, iter > 0)) != XFK_OK) {
-                return src;
+        const double *Cb = P->hc2_C.p;
+        // C_q . y (unconjugated) of the Case-2 border column q
+        auto cdot = [&](int q, const double2 *y, hcx &out) -> int {
+            k_hc_cdot<<<kResGrid, 256, 0, s>>>(N, Cb + 2 * (size_t)q * N, Cb + 2 * (size_t)q * N + N, y,
+                                               P->hres_part.p);
+            std::vector<double> hp(2 * kResGrid);
+            XFK_CHECK(d2h(hp.data(), P->hres_part.p, sizeof(double) * hp.size(), s));
+            double re = 0, im = 0;
+            for (int k = 0; k < kResGrid; ++k) {
+                re += hp[k];
+                im += hp[kResGrid + k];
             }
-        } else {
-            // bordered system [A C; C^T D][V; u] = [b; f] through the Schur
-            // complement: Y = A^-1 C, y0 = A^-1 b, (D - C^T Y) u = f - C^T y0,
-            // V = y0 - Y u (one COCG solve per Case-2 circuit and one for b)
-            if (iter == 0) {
-                XFK_CHECK(P->hc2_Y.alloc((size_t)nc2 * N));
-                XFK_CHECK(P->hc2_y0.alloc((size_t)N));
-                XFK_CHECK(P->hres_part.alloc(2 * kResGrid));
-            }
-            const double *Cb = P->hc2_C.p;
+            out = hcx(re, im);
+            return XFK_OK;
+        };
+        // Schur complement D - C^T Y of this pass's matrix (Y = M^-1 C)
+        auto schur = [&](std::vector<hcx> &Sm) -> int {
+            Sm.assign((size_t)nc2 * nc2, hcx(0, 0));
             for (int q = 0; q < nc2; ++q)
-                if ((src = solve_one(P->hc2_Y.p + (size_t)q * N, Cb + 2 * (size_t)q * N,
-                                     Cb + 2 * (size_t)q * N + N, iter > 0)) != XFK_OK)
-                    return src;
-            if ((src = solve_one(P->hc2_y0.p, P->b.p, P->b_im.p, iter > 0)) != XFK_OK) return src;
-            auto cdot = [&](int q, const double2 *y, hcx &out) -> int {
-                k_hc_cdot<<<kResGrid, 256, 0, s>>>(N, Cb + 2 * (size_t)q * N, Cb + 2 * (size_t)q * N + N, y,
-                                                   P->hres_part.p);
-                std::vector<double> hp(2 * kResGrid);
-                XFK_CHECK(d2h(hp.data(), P->hres_part.p, sizeof(double) * hp.size(), s));
-                double re = 0, im = 0;
-                for (int k = 0; k < kResGrid; ++k) {
-                    re += hp[k];
-                    im += hp[kResGrid + k];
-                }
-                out = hcx(re, im);
-                return XFK_OK;
-            };
-            std::vector<hcx> S((size_t)nc2 * nc2), g(nc2);
-            for (int q = 0; q < nc2; ++q) {
-                hcx t;
-                if ((src = cdot(q, P->hc2_y0.p, t)) != XFK_OK) return src;
-                g[q] = hc(P->hc2_f[q]) - t;
                 for (int r = 0; r < nc2; ++r) {
-                    if ((src = cdot(q, P->hc2_Y.p + (size_t)r * N, t)) != XFK_OK) return src;
-                    S[(size_t)q * nc2 + r] = (q == r ? hc(P->hc2_D[q]) : hcx(0, 0)) - t;
+                    hcx t;
+                    int rc = cdot(q, P->hc2_Y.p + (size_t)r * N, t);
+                    if (rc != XFK_OK) return rc;
+                    Sm[(size_t)q * nc2 + r] = (q == r ? hc(P->hc2_D[q]) : hcx(0, 0)) - t;
                 }
-            }
-            // small dense complex solve, partial pivoting
+            return XFK_OK;
+        };
+        // small dense complex solve S u = g, partial pivoting (S, g by value)
+        auto dense_solve = [&](std::vector<hcx> S, std::vector<hcx> g, std::vector<double2> &u) -> int {
             for (int k = 0; k < nc2; ++k) {
                 int pv = k;
                 for (int r = k + 1; r < nc2; ++r)
@@ -1845,12 +1836,141 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
                     g[r] -= f * g[k];
                 }
             }
-            std::vector<double2> u(nc2);
+            u.assign(nc2, cx(0, 0));
             for (int k = nc2 - 1; k >= 0; --k) {
                 hcx t = g[k];
                 for (int c2 = k + 1; c2 < nc2; ++c2) t -= S[(size_t)k * nc2 + c2] * hc(u[c2]);
                 u[k] = h2(t / S[(size_t)k * nc2 + k]);
             }
+            return XFK_OK;
+        };
+        // KludgeSolve on the bordered system (cspars.cpp:1000-1060 over the
+        // full unknown vector [V; u], harmonic2d.cpp:800-826): the residual,
+        // the step and the line search run over nodes and circuit unknowns
+        // alike (the auxiliary matrices are zero on the border rows); each
+        // inner solve is the bordered [M C; C^T D] solve through the Schur
+        // complement with this pass's Y = M^-1 C
+        auto kludge2 = [&]() -> int {
+            double2 *bo = P->hk_vec.p, *vs = bo + N, *rr = bo + 2 * (size_t)N, *Pd = bo + 3 * (size_t)N,
+                    *U = bo + 4 * (size_t)N;
+            double *bre = P->hk_b.p, *bim = P->hk_b.p + N;
+            const int nbn = nb256(N);
+            int rc;
+            for (int q = 0; q < nc2; ++q)
+                if ((rc = solve_one(P->hc2_Y.p + (size_t)q * N, Cb + 2 * (size_t)q * N, Cb + 2 * (size_t)q * N + N,
+                                    true)) != XFK_OK)
+                    return rc;
+            std::vector<hcx> Sm;
+            if ((rc = schur(Sm)) != XFK_OK) return rc;
+            DBuf<double2> ud;
+            XFK_CHECK(ud.alloc((size_t)nc2));
+            auto put = [&](const std::vector<double2> &w) -> int {
+                XFK_CHECK(hipMemcpyAsync(ud.p, w.data(), sizeof(double2) * nc2, hipMemcpyHostToDevice, s));
+                XFK_CHECK(hipStreamSynchronize(s));
+                return XFK_OK;
+            };
+            std::vector<double2> u = P->hc2_u, un, Pb(nc2);
+            std::vector<hcx> rb(nc2), Ub(nc2), g(nc2);
+            k_hk_join<<<nbn, kBlock, 0, s>>>(N, P->b.p, P->b_im.p, bo);
+            XFK_CHECK(hipMemcpyAsync(vs, v, sizeof(double2) * N, hipMemcpyDeviceToDevice, s));
+            k_hk_apply<<<nbn, 256, 0, s>>>(N, P->rowptr.p, P->col.p, P->val.p, P->val_im.p, aux, nnz, v, bo, 2, rr,
+                                           nullptr, nullptr);
+            if ((rc = put(u)) != XFK_OK) return rc;
+            k_hc_add_cu<<<nbn, kBlock, 0, s>>>(N, nc2, Cb, ud.p, -1.0, rr);
+            double fb2 = 0, rb2 = 0;
+            for (int q = 0; q < nc2; ++q) {
+                hcx t;
+                if ((rc = cdot(q, v, t)) != XFK_OK) return rc;
+                rb[q] = hc(P->hc2_f[q]) - t - hc(P->hc2_D[q]) * hc(u[q]);
+                fb2 += std::norm(hc(P->hc2_f[q]));
+                rb2 += std::norm(rb[q]);
+            }
+            double d3[3];
+            if ((rc = dots(rr, bo, d3)) != XFK_OK) return rc;
+            const double normb = std::sqrt(d3[1] + fb2);
+            if (normb == 0.0) return XFK_OK;
+            double er = std::sqrt(d3[2] + rb2) / normb;
+            if (!(er < lprec)) {
+                for (int k = 0; k < 10; ++k) {
+                    k_hk_apply<<<nbn, 256, 0, s>>>(N, P->rowptr.p, P->col.p, P->val.p, P->val_im.p, aux, nnz, v, bo,
+                                                   1, nullptr, bre, bim);
+                    if ((rc = solve_one(P->hc2_y0.p, bre, bim, true)) != XFK_OK) return rc;
+                    for (int q = 0; q < nc2; ++q) {
+                        hcx t;
+                        if ((rc = cdot(q, P->hc2_y0.p, t)) != XFK_OK) return rc;
+                        g[q] = hc(P->hc2_f[q]) - t;
+                    }
+                    if ((rc = dense_solve(Sm, g, un)) != XFK_OK) return rc;
+                    if ((rc = put(un)) != XFK_OK) return rc;
+                    k_hc_border_combine<<<nbn, kBlock, 0, s>>>(N, nc2, P->hc2_y0.p, P->hc2_Y.p, ud.p, v);
+                    k_hk_diff<<<nbn, kBlock, 0, s>>>(N, v, vs, Pd);
+                    for (int q = 0; q < nc2; ++q) Pb[q] = cx(un[q].x - u[q].x, un[q].y - u[q].y);
+                    k_hk_apply<<<nbn, 256, 0, s>>>(N, P->rowptr.p, P->col.p, P->val.p, P->val_im.p, aux, nnz, Pd,
+                                                   nullptr, 0, U, nullptr, nullptr);
+                    if ((rc = put(Pb)) != XFK_OK) return rc;
+                    k_hc_add_cu<<<nbn, kBlock, 0, s>>>(N, nc2, Cb, ud.p, 1.0, U);
+                    double bn = 0, bd = 0;
+                    for (int q = 0; q < nc2; ++q) {
+                        hcx t;
+                        if ((rc = cdot(q, Pd, t)) != XFK_OK) return rc;
+                        Ub[q] = t + hc(P->hc2_D[q]) * hc(Pb[q]);
+                        bn += (std::conj(rb[q]) * Ub[q]).real();
+                        bd += std::norm(Ub[q]);
+                    }
+                    if ((rc = dots(rr, U, d3)) != XFK_OK) return rc;
+                    const double cstep = (d3[0] + bn) / (d3[1] + bd);
+                    k_hk_update<<<nbn, kBlock, 0, s>>>(N, cstep, v, vs, Pd, rr, U);
+                    rb2 = 0;
+                    for (int q = 0; q < nc2; ++q) {
+                        u[q] = cx(u[q].x + cstep * Pb[q].x, u[q].y + cstep * Pb[q].y);
+                        rb[q] -= cstep * Ub[q];
+                        rb2 += std::norm(rb[q]);
+                    }
+                    if ((rc = dots(rr, rr, d3)) != XFK_OK) return rc;
+                    er = std::sqrt(d3[2] + rb2) / normb;
+                    if (trace) std::fprintf(stderr, "  kludge2 %d: c %.6e er %.6e (cocg %lld)\n", k, cstep, er,
+                                            (long long)P->hc_host->iters);
+                    if (er < lprec * 10.) break;
+                }
+            } else if (trace) {
+                std::fprintf(stderr, "  kludge2: er %.6e < %.3e at start\n", er, lprec);
+            }
+            P->hc2_u_old = P->hc2_u;
+            P->hc2_u = u;
+            return XFK_OK;
+        };
+        int src;
+        if (nc2 == 0) {
+            if (A.newton) {
+                if ((src = kludge()) != XFK_OK) return src;
+            } else if ((src = solve_one(v, P->b.p, P->b_im.p, iter > 0)) != XFK_OK) {
+                return src;
+            }
+        } else if (A.newton) {
+            if ((src = kludge2()) != XFK_OK) return src;
+        } else {
+            // bordered system [A C; C^T D][V; u] = [b; f] through the Schur
+            // complement: Y = A^-1 C, y0 = A^-1 b, (D - C^T Y) u = f - C^T y0,
+            // V = y0 - Y u (one COCG solve per Case-2 circuit and one for b)
+            if (iter == 0) {
+                XFK_CHECK(P->hc2_Y.alloc((size_t)nc2 * N));
+                XFK_CHECK(P->hc2_y0.alloc((size_t)N));
+                XFK_CHECK(P->hres_part.alloc(2 * kResGrid));
+            }
+            for (int q = 0; q < nc2; ++q)
+                if ((src = solve_one(P->hc2_Y.p + (size_t)q * N, Cb + 2 * (size_t)q * N,
+                                     Cb + 2 * (size_t)q * N + N, iter > 0)) != XFK_OK)
+                    return src;
+            if ((src = solve_one(P->hc2_y0.p, P->b.p, P->b_im.p, iter > 0)) != XFK_OK) return src;
+            std::vector<hcx> S, g(nc2);
+            if ((src = schur(S)) != XFK_OK) return src;
+            for (int q = 0; q < nc2; ++q) {
+                hcx t;
+                if ((src = cdot(q, P->hc2_y0.p, t)) != XFK_OK) return src;
+                g[q] = hc(P->hc2_f[q]) - t;
+            }
+            std::vector<double2> u;
+            if ((src = dense_solve(S, g, u)) != XFK_OK) return src;
             P->hc2_u_old = P->hc2_u;
             P->hc2_u = u;
             DBuf<double2> ud;
