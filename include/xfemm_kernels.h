@@ -298,6 +298,11 @@ typedef struct {
     const xfk_line_ac_desc *lines;      /* may be NULL when n_lines == 0 */
     const xfk_circuit_ac_desc *circs;   /* may be NULL when n_circs == 0 */
     int ac_solver;              /* [ACSolver]: 0 successive approximation, 1 Newton */
+    const double *label_prox_mu;   /* 2 per label (re, im): CMBlockLabel::ProximityMu after
+                                      FSolver::GetFillFactor (fsolver.cpp:1083-1193), the relative
+                                      permeability of a wound region of a LamType > 2 block
+                                      (harmonic2d.cpp:664-668); read for those labels only;
+                                      NULL: 1 for every label */
 } xfk_harmonic_desc;
 
 int xfk_problem_create_harmonic(const xfk_problem_desc *desc, const xfk_harmonic_desc *ac, int device,

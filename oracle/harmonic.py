@@ -24,7 +24,8 @@ class OrhBlock(C.Structure):
 
 
 class OrhLabel(C.Structure):
-    _fields_ = [("InCircuit", C.c_int), ("bIsWound", C.c_int), ("IsExternal", C.c_int)]
+    _fields_ = [("InCircuit", C.c_int), ("bIsWound", C.c_int), ("IsExternal", C.c_int),
+                ("ProxMu_re", C.c_double), ("ProxMu_im", C.c_double)]
 
 
 class OrhLine(C.Structure):
@@ -142,6 +143,8 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
     for k, lb in enumerate(pr.labels):
         labels[k].InCircuit, labels[k].bIsWound = lb.InCircuit, int(lb.bIsWound)
         labels[k].IsExternal = int(lb.IsExternal)
+        pm = complex(getattr(lb, "ProximityMu", 1.0))
+        labels[k].ProxMu_re, labels[k].ProxMu_im = pm.real, pm.imag
     lines = (OrhLine * max(1, len(pr.bdrys)))()
     for k, bd in enumerate(pr.bdrys):
         l = lines[k]

@@ -1070,6 +1070,7 @@ static void axi_element(orh_problem *pr, const orh_linprob_ops *ops, void *L, co
     /* permeability: the block's / successive approximation with B from the
      * element energy (:425-560) / the exterior warp (:567-574) */
     cx mu1 = Mu[pr->blk[i]].mu0, mu2 = Mu[pr->blk[i]].mu1;
+    if (blk->LamType > 2) mu1 = mu2 = C(lab->ProxMu_re, lab->ProxMu_im);   /* prox. effects (:571-575) */
     cx Mnh[3][3], Mna[3][3], Mns[3][3];
     int updated = 0, newton = 0;
     if (Iter > 0 && blk->LamType == 0 && blk->BHpoints > 0 && mu1.re == mu2.re && mu1.im == mu2.im) {
@@ -1246,6 +1247,7 @@ static int assemble_and_bc(orh_problem *pr, const orh_linprob_ops *ops, void *L,
          * later passes, nonlinear LamType-0 blocks: successive approximation
          * (:588-660, ACSolver 0) */
         cx mu1 = Mu[pr->blk[i]].mu0, mu2 = Mu[pr->blk[i]].mu1, v12 = C(0, 0);
+        if (blk->LamType > 2) mu1 = mu2 = C(lab->ProxMu_re, lab->ProxMu_im);   /* prox. effects (:664-668) */
         cx Mnh[3][3], Mna[3][3], Mns[3][3];
         int newton = 0;
         if (Iter > 0 && blk->LamType == 0 && blk->BHpoints > 0 && mu1.re == mu2.re && mu1.im == mu2.im) {
@@ -1346,7 +1348,7 @@ static int check_linear(const orh_problem *pr)
         if (pr->blocks[k].BHpoints != 0 && !(pr->blocks[k].B && pr->blocks[k].H_re && pr->blocks[k].H_im &&
                                              pr->blocks[k].S_re && pr->blocks[k].S_im))
             return 0;
-        if (pr->blocks[k].LamType == 1 || pr->blocks[k].LamType == 2 || pr->blocks[k].LamType > 2) return 0;
+        if (pr->blocks[k].LamType == 1 || pr->blocks[k].LamType == 2) return 0;
     }
     return 1;
 }

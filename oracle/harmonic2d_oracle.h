@@ -55,6 +55,7 @@ typedef struct {
     int InCircuit;
     int bIsWound;
     int IsExternal;             /* exterior region (axisymmetric) */
+    double ProxMu_re, ProxMu_im;   /* ProximityMu (GetFillFactor): LamType > 2 wound regions */
 } orh_label;
 
 typedef struct {

@@ -96,6 +96,72 @@ def test_harmonic_unsupported_cases_are_reported():
         kernels.Harmonic2DProblem(**dict(kw, frequency=0.0))
 
 
+@pytest.mark.parametrize("wiretype", [0, 1, 2, 3])
+def test_harmonic_proximity_winding_matches_oracle(wiretype):
+    """Wound region of a LamType 3 + wiretype block at 20 kHz: the element
+    permeability is the label's ProximityMu (FSolver::GetFillFactor,
+    fsolver.cpp:1083-1193; harmonic2d.cpp:664-668) and the region carries no
+    bulk eddy current.  A vs the converged oracle; the winding moves the
+    answer by > 10x the tolerance (the proximity term is exercised)."""
+    kw = synth.harmonic(20, frequency=20000.0, prox=wiretype)
+    pr, mesh, kk = _problem(kw)
+    pm = pr.labels[3].ProximityMu
+    assert abs(pm - 1) > 0.01 and kk["labels"][3]["prox_mu"] == pm
+    P = kernels.Harmonic2DProblem(**kk)
+    P.solve()
+    A = P.solution()
+    P.close()
+    Ao, _, _ = oh.solve(pr, mesh)
+    Ac = converged(pr, mesh, oh.solve)
+    assert rel_err(A, Ac) <= TOL_A, parity_message(A, Ao, Ac, TOL_A)
+    pr0, mesh0, _ = _problem(synth.harmonic(20, frequency=20000.0))
+    A0 = converged(pr0, mesh0, oh.solve)
+    assert rel_err(A0, Ac) > 10 * TOL_A
+
+
+@pytest.mark.parametrize("wiretype", [1, 3])
+def test_harmonic_axisymmetric_proximity_winding_matches_oracle(wiretype):
+    """HarmonicAxisymmetric with the coil (a Case-1 circuit) wound of LamType
+    3 + wiretype wire at 20 kHz (harmonicaxi.cpp:571-575): A vs the converged
+    oracle, and the winding changes the answer."""
+    kw = synth.harmonic_axisymmetric(16, frequency=20000.0, prox=wiretype)
+    pr, mesh, kk = _problem(kw)
+    assert abs(pr.labels[2].ProximityMu - 1) > 0.01
+    P = kernels.Harmonic2DProblem(**kk)
+    P.solve()
+    A = P.solution()
+    P.close()
+    Ao, _, _ = oh.solve(pr, mesh)
+    Ac = converged(pr, mesh, oh.solve)
+    assert rel_err(A, Ac) <= TOL_A, parity_message(A, Ao, Ac, TOL_A)
+    pr0, mesh0, _ = _problem(synth.harmonic_axisymmetric(16, frequency=20000.0))
+    assert rel_err(converged(pr0, mesh0, oh.solve), Ac) > 10 * TOL_A
+
+
+def test_harmonic_proximity_winding_file_interface(tmp_path):
+    """.fem with a stranded-wire winding (LamType 4, WireD, NStrands, Turns)
+    -> FSolver (its own GetFillFactor) on the GPU -> .ans, vs the oracle's
+    restatement loaded from the same files."""
+    from oracle import femfile
+    from xfemm_amd import fsolver
+    kw = synth.harmonic(18, circuits=False, frequency=20000.0, prox=1)
+    kw["marker"] = None
+    kw["points"] = []
+    base = str(tmp_path / "hp")
+    synth.write_problem(base, kw)
+    pr, mesh = femfile.load_problem(base)
+    assert pr.blocks[3].LamType == 4 and pr.labels[3].Turns == 30 and abs(pr.labels[3].ProximityMu - 1) > 0.1
+    Ao, _, _ = oh.solve(pr, mesh)
+    Ac = converged(pr, mesh, oh.solve)
+    fs = fsolver.FSolver()
+    fs.PathName = base
+    assert fs.LoadProblemFile()
+    assert fs.runSolver(False), fs.last_error()
+    nodes, _ = _read_harmonic_ans(base + ".ans")
+    A = nodes[:, 2] + 1j * nodes[:, 3]
+    assert rel_err(A, Ac) <= TOL_A, parity_message(A, Ao, Ac, TOL_A)
+
+
 @pytest.mark.parametrize("frequency", [60.0, 2000.0])
 def test_harmonic_amg_preconditioner(frequency):
     """The V-cycle preconditioner reaches the same answer as complex Jacobi in

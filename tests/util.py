@@ -21,7 +21,8 @@ def kernel_kwargs(pr: femfile.FemProblem, mesh: femfile.Mesh) -> dict:
             b.update(B=np.array(m.Bdata), H=np.array(m.Hdata), slope=np.array(m.slope))
         blocks.append(b)
     labels = [dict(block=max(lb.BlockType, 0), in_circuit=lb.InCircuit, mag_dir=lb.MagDir,
-                   is_wound=int(lb.bIsWound), is_external=int(lb.IsExternal)) for lb in pr.labels]
+                   is_wound=int(lb.bIsWound), is_external=int(lb.IsExternal),
+                   prox_mu=complex(lb.ProximityMu)) for lb in pr.labels]
     lines = [dict(format=b.BdryFormat, A0=b.A0, A1=b.A1, A2=b.A2, phi=b.phi, c0=b.c0, c1=b.c1, c0_im=b.c0i,
                   c1_im=b.c1i, Mu=b.Mu, Sig=b.Sig) for b in pr.bdrys]
     points = [dict(A_re=q.A_re, A_im=q.A_im, J_re=q.J_re, J_im=q.J_im) for q in pr.points]
@@ -51,7 +52,8 @@ def synth_to_oracle(kw: dict):
                               J_re=b.get("J_re", 0.0), Cduct=b.get("Cduct", 0.0),
                               LamFill=b.get("LamFill", 1.0), LamType=b.get("LamType", 0),
                               J_im=b.get("J_im", 0.0), Theta_hx=b.get("Theta_hx", 0.0),
-                              Theta_hy=b.get("Theta_hy", 0.0), Lam_d=b.get("Lam_d", 0.0))
+                              Theta_hy=b.get("Theta_hy", 0.0), Lam_d=b.get("Lam_d", 0.0),
+                              WireD=b.get("WireD", 0.0), NStrands=b.get("NStrands", 0))
         if len(b.get("B", ())) and np.iscomplexobj(b["H"]):
             # harmonic: the GetSlopes(omega) curve (host restatement, pinned
             # against the reference by tests/test_oracle_acslopes.py)
@@ -63,7 +65,8 @@ def synth_to_oracle(kw: dict):
         pr.blocks.append(m)
     for lb in kw["labels"]:
         pr.labels.append(femfile.BlockLabel(BlockType=lb["block"], InCircuit=lb.get("in_circuit", -1),
-                                            MagDir=lb.get("mag_dir", 0.0), Turns=2 if lb.get("is_wound", 0) else 1,
+                                            MagDir=lb.get("mag_dir", 0.0),
+                                            Turns=lb.get("turns", 2 if lb.get("is_wound", 0) else 1),
                                             IsExternal=bool(lb.get("is_external", 0))))
     for ln in kw["lines"]:
         pr.bdrys.append(femfile.BdryProp(BdryFormat=ln.get("format", 0), A0=ln.get("A0", 0.0),
@@ -77,7 +80,6 @@ def synth_to_oracle(kw: dict):
     for q in kw.get("points", []):
         pr.points.append(femfile.PointProp(A_re=q.get("A_re", 0.0), A_im=q.get("A_im", 0.0),
                                            J_re=q.get("J_re", 0.0), J_im=q.get("J_im", 0.0)))
-    femfile.get_fill_factor(pr)
     nn = len(kw["x"])
     marker = kw.get("marker")
     pbc = kw.get("pbc")
@@ -88,6 +90,7 @@ def synth_to_oracle(kw: dict):
                         blk=np.array([kw["labels"][l]["block"] for l in kw["lbl"]], np.int32),
                         pbc=np.zeros((0, 3), np.int32) if pbc is None else np.asarray(pbc, np.int32),
                         ages=list(kw.get("ages", [])))
+    femfile.get_fill_factor(pr, mesh)
     return pr, mesh, kernel_kwargs(pr, mesh)
 
 

@@ -89,6 +89,7 @@ struct CMBlockLabel {
     bool IsDefault = false, IsExternal = false;
     std::string MagDirFctn;
     bool bIsWound = false;
+    double ProxMu_re = 1, ProxMu_im = 0;   // ProximityMu (GetFillFactor, AC wound LamType > 2 regions)
 };
 
 struct CNode {

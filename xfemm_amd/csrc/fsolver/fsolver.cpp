@@ -2,6 +2,7 @@
 #include "fsolver.h"
 
 #include <cctype>
+#include <complex>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -520,10 +521,73 @@ int FSolver::Cuthill(bool deleteFiles)
 
 void FSolver::GetFillFactor(int lbl)
 {
-    // static problems: only bIsWound matters (fsolver.cpp:1096-1105)
+    // bIsWound, and at AC the proximity-effect permeability of a wound
+    // LamType > 2 region (fsolver.cpp:1083-1193): an equivalent-foil model for
+    // rectangular wire, a fitted frequency-dependent permeability for round
+    // wire (magnet, stranded, litz, copper-clad aluminium)
     CMBlockLabel &bl = labellist[lbl];
     const int lt = (bl.BlockType >= 0) ? blockproplist[bl.BlockType].LamType : 0;
     bl.bIsWound = (std::abs(bl.Turns) > 1) || (lt > 2);
+    bl.ProxMu_re = 1;
+    bl.ProxMu_im = 0;
+    if (Frequency == 0 || lt < 3) return;
+    // the region's area, m^2 (ElmArea, fsolver.cpp:1196-1210)
+    double atot = 0;
+    for (const auto &el : meshele) {
+        if (el.lbl != lbl) continue;
+        const CNode &a = meshnode[el.p[0]], &b = meshnode[el.p[1]], &c = meshnode[el.p[2]];
+        const double b0 = b.y - c.y, b1 = c.y - a.y, c0 = c.x - b.x, c1 = a.x - c.x;
+        atot += 0.0001 * (b0 * c1 - b1 * c0) / 2.;
+    }
+    if (atot == 0) return;   // ProximityMu keeps its previous value (1 here)
+    const CMSolverMaterialProp &bp = blockproplist[bl.BlockType];
+    if (bp.Cduct == 0) return;
+    using cd = std::complex<double>;
+    const cd I(0, 1);
+    const double muo = 4.e-7 * kPi;
+    const int wiretype = lt - 3;
+    cd mu;
+    if (wiretype == 3) {   // rectangular wire: equivalent foil
+        const double W = 2. * kPi * Frequency, d = bp.WireD * 0.001;
+        double fill = std::fabs(d * d * (double)bl.Turns / atot);
+        const double pitch = d / std::sqrt(fill);
+        fill = d / pitch;
+        const double o = bp.Cduct * fill * 1.e6;
+        const cd k = std::sqrt(I * W * o * muo) * d / 2.;
+        const cd ufd = muo * std::tanh(k) / k;
+        mu = (fill * ufd + (1. - fill) * muo) / muo;
+    } else {
+        double R = 0, awire = 0;
+        const double turns = (double)bl.Turns, ns = (double)bp.NStrands;
+        if (wiretype == 0 || wiretype == 2) {   // magnet wire, litz: NStrands strands of WireD
+            R = bp.WireD * 0.0005;
+            awire = kPi * R * R * ns * turns;
+        } else if (wiretype == 1) {             // stranded, non-litz: one conductor of the bundle's area
+            R = bp.WireD * 0.0005 * std::sqrt(ns);
+            awire = kPi * R * R * turns;
+        }                                       // CCA (4, 5): the reference leaves R and awire at 0
+        const double fill = std::fabs(awire / atot);
+        const double W = 2. * kPi * Frequency * bp.Cduct * 1.e6 * muo * R * R / 2.;
+        double c1 = 0, c2 = 0;
+        if (wiretype <= 2) {
+            c1 = 0.7756067409818643 + fill * (0.6873854335408803 + fill * (0.06841584481674128 - 0.07143732702512284 * fill));
+            c2 = 1.5 * fill / c1;
+        } else if (wiretype == 4) {
+            c1 = 0.7270741505617485 + 0.8902950067721367 * fill + 0.11894736885885195 * fill * fill -
+                 0.12247276254503957 * fill * fill * fill;
+            c2 = 0.006784920229549677 + 1.8942880489198526 * fill - 1.3631438759519217 * fill * fill +
+                 0.504431701685587 * fill * fill * fill;
+        } else if (wiretype == 5) {
+            c1 = 0.7486913529860821 + 0.9042845510838825 * fill + 0.1361040321433224 * fill * fill -
+                 0.10652380745682069 * fill * fill * fill;
+            c2 = 0.006790468527313965 + 1.8945509985370095 * fill - 1.3643501010185972 * fill * fill +
+                 0.5036765577982594 * fill * fill * fill;
+        }
+        const cd z = std::sqrt(c1 * I * W);
+        mu = c2 * (std::tanh(z) / z) + (1. - c2);
+    }
+    bl.ProxMu_re = mu.real();
+    bl.ProxMu_im = mu.imag();
 }
 
 // the C-ABI descriptor of the current problem and the arrays it points into
@@ -685,8 +749,20 @@ int FSolver::Harmonic2D()
     std::vector<xfk_circuit_ac_desc> cac(circproplist.size());
     for (size_t k = 0; k < circproplist.size(); k++)
         cac[k] = xfk_circuit_ac_desc{circproplist[k].Amps_im, circproplist[k].dVolts_im};
+    std::vector<double> prox(2 * std::max<size_t>(1, labellist.size()), 0.0);
+    for (size_t k = 0; k < labellist.size(); k++) {
+        if (!std::isfinite(labellist[k].ProxMu_re) || !std::isfinite(labellist[k].ProxMu_im)) {
+            // copper-clad aluminium wire (LamType 7, 8): the reference's
+            // GetFillFactor leaves the wire radius at 0, ProximityMu = 0/0
+            warn("copper-clad aluminium windings (LamType 7, 8) have no defined proximity permeability "
+                 "(the reference computes 0/0); not supported\n");
+            return false;
+        }
+        prox[2 * k] = labellist[k].ProxMu_re;
+        prox[2 * k + 1] = labellist[k].ProxMu_im;
+    }
     xfk_harmonic_desc ac{Frequency, bac.data(), lac.empty() ? nullptr : lac.data(),
-                         cac.empty() ? nullptr : cac.data(), ACSolver};
+                         cac.empty() ? nullptr : cac.data(), ACSolver, prox.data()};
     xfk_problem *prob = nullptr;
     int rc = xfk_problem_create_harmonic(&ds.d, &ac, device, &prob);
     if (rc == XFK_OK) rc = xfk_harmonic2d(prob, 0, &stats);

@@ -1668,36 +1668,43 @@ __global__ void __launch_bounds__(256) k_csr_mv_g(int n, const int *__restrict__
 // x = M b, one wavefront per row of the dense coarsest inverse (ld is a
 // multiple of 64 and the padding columns are zero): double2 loads, four in
 // flight per lane
+// x = M b, one 256-thread workgroup per row: every thread issues its (at most
+// kDmvLoads) 16-B loads of the row at once, so the whole inverse is in flight
+// (one wave per row left a 1.6k-row inverse at 2.3 TB/s: 6 waves per CU, each
+// walking its 12.8 KB row in three dependent batches)
+constexpr int kDmvLoads = 4;
 __global__ void __launch_bounds__(256) k_dense_mv(int n, int ld, const double *__restrict__ M,
                                                   const double *__restrict__ b, double *__restrict__ x, const int *done)
 {
     if (done && *done) return;
-    const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    if (i >= n) return;
+    __shared__ double red[4];
+    const int i = blockIdx.x;
     const double2 *Mi = reinterpret_cast<const double2 *>(M + (size_t)i * ld);
     const int n2 = ld >> 1;
     double s0 = 0.0, s1 = 0.0;
-    int j = lane;
-    for (; j + 192 < n2; j += 256) {
-        double2 m[4];
+    for (int j0 = 0; j0 < n2; j0 += 256 * kDmvLoads) {
+        double2 m[kDmvLoads];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) m[q] = Mi[j + 64 * q];
+        for (int q = 0; q < kDmvLoads; ++q) {
+            const int j = j0 + threadIdx.x + 256 * q;
+            m[q] = j < n2 ? Mi[j] : make_double2(0.0, 0.0);
+        }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int c = 2 * (j + 64 * q);
-            s0 += m[q].x * (c < n ? b[c] : 0.0);
-            s1 += m[q].y * (c + 1 < n ? b[c + 1] : 0.0);
+        for (int q = 0; q < kDmvLoads; ++q) {
+            const int c = 2 * (j0 + threadIdx.x + 256 * q);
+            if (c + 1 < n) {
+                const double2 bb = *reinterpret_cast<const double2 *>(b + c);
+                s0 += m[q].x * bb.x;
+                s1 += m[q].y * bb.y;
+            } else if (c < n) {
+                s0 += m[q].x * b[c];
+            }
         }
     }
-    for (; j < n2; j += 64) {
-        const double2 m = Mi[j];
-        const int c = 2 * j;
-        s0 += m.x * (c < n ? b[c] : 0.0);
-        s1 += m.y * (c + 1 < n ? b[c + 1] : 0.0);
-    }
-    const double s = cg_wave_sum(s0 + s1);
-    if (lane == 0) x[i] = s;
+    const double w = cg_wave_sum(s0 + s1);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) x[i] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // diagnostics (XFK_AMG_DEBUG): rows left without an aggregate, split by
@@ -2376,7 +2383,10 @@ int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &ld)
             for (const auto &x : sets) std::fprintf(stderr, " %zu", x.size());
             std::fprintf(stderr, "\n");
         }
-        if (!ok || 3 * nsep > (size_t)n) continue;
+        // (XFK_ND_DEPTH: this depth whatever its separators -- measurement hook)
+        const char *fd = std::getenv("XFK_ND_DEPTH");
+        if (fd && std::atoi(fd) != D) continue;
+        if (!ok || (!fd && 3 * nsep > (size_t)n)) continue;
         if (D > 1)
             for (const auto &x : sets) ok = ok && x.size() >= (size_t)kBj;
         if (!ok) continue;
@@ -3147,7 +3157,7 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
         double *dst = (l == 0) ? out0 : A.xa.p;
         if (M.dense_coarse) {
             XFK_PHASE(lv + "dense inverse x b", 8.0 * A.n * M.cinv_ld + 8.0 * (M.cinv_ld + A.n),
-                      (k_dense_mv<<<(A.n * 64 + 255) / 256, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv_apply, b, dst, done)));
+                      (k_dense_mv<<<A.n, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv_apply, b, dst, done)));
             return dst;
         }
         // smoother-only coarsest level: 2 nu sweeps from zero

@@ -330,6 +330,7 @@ __device__ void hax_element(int i, const HarmArgs &A, const int (&n)[3], const d
     // permeability: the block's (+ the exterior warp), or successive
     // approximation with B derived from the element energy (:468-560)
     double2 mu1 = bp.mu1, mu2 = bp.mu2, Kn = cx(0, 0);
+    if (bp.prox) mu1 = mu2 = lab.prox_mu;   // wound region (harmonicaxi.cpp:571-575), then the warp below
     const bool nl = bp.bh_n > 0 && A.iter > 0;
     if (nl) {
         double2 v[3];
@@ -494,6 +495,7 @@ __global__ void __launch_bounds__(kBlock) k_hassemble_color(int begin, int end, 
     be[1] = cadd(be[1], Ks);
     be[2] = cadd(be[2], Ks);
     double2 mu1 = bp.mu1, mu2 = bp.mu2;
+    if (bp.prox) mu1 = mu2 = lab.prox_mu;   // wound region (harmonic2d.cpp:664-668)
     double2 Kn = cx(0, 0), Kt = cx(0, 0), vn[3];
     const bool nl = bp.bh_n > 0 && A.iter > 0;
     const bool nt = nl && A.newton;
@@ -1179,6 +1181,7 @@ DevBlockAC effective_block(const xfk_block_desc &b, const xfk_block_ac_desc &ac,
     o.J = cx(b.J_re, ac.J_im);
     o.Cduct = b.Cduct;
     o.eddy = !((b.LamType == 0) && (ac.Lam_d > 0));
+    o.prox = b.LamType > 2;
     return o;
 }
 
@@ -1205,8 +1208,6 @@ int harmonic_validate(const xfk_problem_desc *d, const xfk_harmonic_desc *ac)
         }
         XFK_REQUIRE(d->blocks[k].LamType != 1 && d->blocks[k].LamType != 2, XFK_ERR_UNSUPPORTED,
                     "On-edge lamination not supported in AC analyses");   // harmonic2d.cpp:76-85
-        XFK_REQUIRE(d->blocks[k].LamType <= 2, XFK_ERR_UNSUPPORTED,
-                    "wound regions with AC proximity effects (LamType > 2) are not supported by this build");
     }
     return XFK_OK;
 }
@@ -1240,7 +1241,8 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     for (int k = 0; k < d->n_blocks; ++k) {
         blk[k] = effective_block(d->blocks[k], ac->blocks[k], w, axi);
         const xfk_block_desc &b = d->blocks[k];
-        if (b.BHpoints > 0) {   // the complex curve of GetSlopes(omega)
+        // only LamType 0 blocks follow their curve (harmonic2d.cpp:598-600)
+        if (b.BHpoints > 0 && b.LamType == 0) {   // the complex curve of GetSlopes(omega)
             blk[k].bh_n = b.BHpoints;
             blk[k].bh_off = (int)bhB.size();
             for (int i = 0; i < b.BHpoints; ++i) {
@@ -1253,7 +1255,10 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     // the reference starts its successive approximation when any element
     // lies in a block with a B-H curve (harmonic2d.cpp:559-569)
     bool nonlin = false;
-    for (int i = 0; i < NE && !nonlin; ++i) nonlin = blk[G.lab[d->lbl[i]].blk].bh_n > 0;
+    for (int i = 0; i < NE && !nonlin; ++i) nonlin = d->blocks[G.lab[d->lbl[i]].blk].BHpoints > 0;
+    // proximity-effect permeabilities of wound LamType > 2 regions
+    for (size_t k = 0; k < G.lab.size(); ++k)
+        G.lab[k].prox_mu = ac->label_prox_mu ? cx(ac->label_prox_mu[2 * k], ac->label_prox_mu[2 * k + 1]) : cx(1, 0);
     if (bhB.empty()) {
         bhB.push_back(0.0);
         bhH.push_back(cx(0, 0));

@@ -86,6 +86,7 @@ struct DevBlock {
 struct DevLabel {
     double cos_m, sin_m;
     int blk, in_circuit, is_wound, external;
+    double2 prox_mu;    // harmonic: ProximityMu of a LamType > 2 label
 };
 
 struct DevLine {
@@ -135,7 +136,7 @@ struct DevBlockAC {
     int eddy;           // 0: laminated (Lam_d > 0) blocks carry no bulk eddy current (harmonic2d.cpp:392-394)
     int bh_n;           // nonlinear: knots of the complex B-H curve (0: linear)
     int bh_off;         // first knot in the problem's curve tables
-    int pad;
+    int prox;           // LamType > 2: wound region, the label's ProximityMu (harmonic2d.cpp:664-668)
 };
 
 struct DevLineAC {

@@ -427,7 +427,8 @@ class CircuitAcDesc(C.Structure):
 
 class HarmonicDesc(C.Structure):
     _fields_ = [("frequency", C.c_double), ("blocks", C.POINTER(BlockAcDesc)), ("lines", C.POINTER(LineAcDesc)),
-                ("circs", C.POINTER(CircuitAcDesc)), ("ac_solver", C.c_int)]
+                ("circs", C.POINTER(CircuitAcDesc)), ("ac_solver", C.c_int),
+                ("label_prox_mu", C.POINTER(C.c_double))]
 
 
 class Harmonic2DProblem:
@@ -462,7 +463,12 @@ class Harmonic2DProblem:
         ca = (CircuitAcDesc * max(1, len(circuits)))()
         for k, q in enumerate(circuits):
             ca[k].amps_im, ca[k].dvolts_im = q.get("amps_im", 0.0), q.get("dvolts_im", 0.0)
-        H = HarmonicDesc(frequency, ba, la, ca, int(ac_solver))
+        # labels' "prox_mu": ProximityMu after GetFillFactor (wound LamType > 2 regions)
+        prox = np.zeros(2 * max(1, len(labels)))
+        for k, l in enumerate(labels):
+            z = complex(l.get("prox_mu", 1.0))
+            prox[2 * k], prox[2 * k + 1] = z.real, z.imag
+        H = HarmonicDesc(frequency, ba, la, ca, int(ac_solver), keep.d(prox))
         keep.extend([ba, la, ca])
         self._keep = keep
         self.n_nodes = D.n_nodes

@@ -139,7 +139,8 @@ def fem_text(blocks, lines, precision=1e-8, units="centimeters", frequency=0.0, 
                 "    <d_lam> = %.17g" % b.get("Lam_d", 0.0), "    <Phi_h> = %.17g" % b.get("Theta_hn", 0.0),
                 "    <Phi_hx> = %.17g" % b.get("Theta_hx", 0.0), "    <Phi_hy> = %.17g" % b.get("Theta_hy", 0.0),
                 "    <LamType> = %d" % b.get("LamType", 0),
-                "    <LamFill> = %.17g" % b.get("LamFill", 1.0), "    <NStrands> = 0", "    <WireD> = 0"]
+                "    <LamFill> = %.17g" % b.get("LamFill", 1.0), "    <NStrands> = %d" % b.get("NStrands", 0),
+                "    <WireD> = %.17g" % b.get("WireD", 0.0)]
         if b.get("bh") == "M19":
             B, H = m19_curve()
             out.append("    <BHPoints> = %d" % len(B))
@@ -164,8 +165,9 @@ def write_problem(base: str, kw: dict, label_xy: Optional[np.ndarray] = None) ->
     text += "[NumPoints] = 0\n[NumSegments] = 0\n[NumArcSegments] = 0\n[NumHoles] = 0\n"
     text += "[NumBlockLabels] = %d\n" % len(labels)
     for k, lb in enumerate(labels):
-        text += "0\t0\t%d\t-1\t%d\t%.17g\t0\t1\t%d\n" % (lb["block"] + 1, lb.get("in_circuit", -1) + 1,
-                                                        lb.get("mag_dir", 0.0), int(lb.get("is_external", 0)))
+        text += "0\t0\t%d\t-1\t%d\t%.17g\t0\t%d\t%d\n" % (lb["block"] + 1, lb.get("in_circuit", -1) + 1,
+                                                        lb.get("mag_dir", 0.0), int(lb.get("turns", 1)),
+                                                        int(lb.get("is_external", 0)))
     with open(base + ".fem", "w") as fh:
         fh.write(text)
     with open(base + ".node", "w") as fh:
@@ -279,7 +281,8 @@ def axisymmetric_uniform(n: int, B0: float = 1.0, L: float = 10.0, precision: fl
 
 
 def harmonic_axisymmetric(n: int, L: float = 10.0, frequency: float = 60.0, precision: float = 1e-8,
-                          circuits: bool = True, nonlinear: bool = False, external: bool = False):
+                          circuits: bool = True, nonlinear: bool = False, external: bool = False,
+                          prox: Optional[int] = None):
     """Keyword arguments of a time-harmonic axisymmetric problem
     (FSolver::HarmonicAxisymmetric, cfemm/fsolver/harmonicaxi.cpp) on the
     n x n-cell square r in [0, L], z in [0, L] (cm): a laminated lossy steel
@@ -290,7 +293,8 @@ def harmonic_axisymmetric(n: int, L: float = 10.0, frequency: float = 60.0, prec
     `circuits`: the coil is a wound specified-current circuit (Case 1) and the
     ring is driven by a voltage gradient (Case 0); `nonlinear`: the steel
     follows the M-19 curve processed for the frequency; `external`: the outer
-    band r > 0.8 L is a mapped exterior region."""
+    band r > 0.8 L is a mapped exterior region; `prox` (wiretype 0-3): the coil
+    is a copper winding of LamType 3 + prox with AC proximity effects."""
     x, y, p = square_mesh(n, L)
     cxm = (x[p[:, 0]] + x[p[:, 1]] + x[p[:, 2]]) / (3.0 * L)
     cym = (y[p[:, 0]] + y[p[:, 1]] + y[p[:, 2]]) / (3.0 * L)
@@ -319,6 +323,9 @@ def harmonic_axisymmetric(n: int, L: float = 10.0, frequency: float = 60.0, prec
         labels[2] = dict(block=2, in_circuit=0, is_wound=1)
         labels[3] = dict(block=3, in_circuit=1)
         circs = [dict(type=0, amps_re=3000.0, amps_im=800.0), dict(type=1, dvolts_re=0.02, dvolts_im=-0.01)]
+    if prox is not None:
+        blocks[2].update(LamType=3 + prox, Cduct=58.0, WireD=1.0, NStrands=7 if prox in (1, 2) else 1)
+        labels[2] = dict(labels[2], is_wound=1, turns=30)
     if external:
         labels.append(dict(block=0, is_external=1))
     tol = 1e-9 * L
@@ -403,7 +410,7 @@ def bc_chain(n: int, L: float = 10.0):
 
 
 def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float = 1e-8, periodic: bool = False,
-             circuits: bool = True, nonlinear: bool = False):
+             circuits: bool = True, nonlinear: bool = False, prox: Optional[int] = None):
     """Keyword arguments of a linear time-harmonic planar problem
     (FSolver::Harmonic2D, cfemm/fsolver/harmonic2d.cpp) on the magnetostatic
     square: laminated lossy steel (lamination thickness with conductivity,
@@ -415,7 +422,10 @@ def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float 
     plate driven by a specified voltage gradient -> Case 0).  `nonlinear`:
     the steel follows the M-19 curve processed for the frequency
     (GetSlopes(omega): hysteresis lag, lamination eddy currents, fill), which
-    starts the reference's successive approximation."""
+    starts the reference's successive approximation.  `prox` (wiretype 0-3:
+    magnet, stranded, litz, rectangular wire): the coil- region becomes a
+    wound copper winding of LamType 3 + prox with AC proximity effects
+    (FSolver::GetFillFactor's ProximityMu, harmonic2d.cpp:664-668)."""
     kw = magnetostatic(n, L=L, precision=precision)
     x, y, p = kw["x"], kw["y"], kw["p"]
     tol = 1e-9 * L
@@ -461,6 +471,9 @@ def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float 
     lbl[(lbl == 0) & (cx > 0.8) & (cx < 0.95) & (cy > 0.1) & (cy < 0.3)] = 5
     kw["lbl"] = lbl
     labels = [dict(block=0), dict(block=1), dict(block=2), dict(block=3), dict(block=4), dict(block=5)]
+    if prox is not None:
+        kw["blocks"][3].update(LamType=3 + prox, Cduct=58.0, WireD=1.0, NStrands=7 if prox in (1, 2) else 1)
+        labels[3] = dict(block=3, is_wound=1, turns=30)
     if circuits:
         labels[2] = dict(block=2, in_circuit=0, is_wound=1)
         labels[4] = dict(block=4, in_circuit=1)
