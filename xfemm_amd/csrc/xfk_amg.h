@@ -60,6 +60,11 @@ struct AmgLevel {
     long long pnnz = 0;
     DBuf<int> prow, pcol, rrow, rcol;
     DBuf<double> pval, rval;
+    // folded level (xfk_amg.hip: k_fold_pre): P~ = (I - w D^-1 A) P and R~ = P~^T
+    bool fold = false;
+    long long fnnz = 0;
+    DBuf<int> ftrow, ftcol, frrow, frcol;
+    DBuf<double> ftval, frval;
     // V-cycle vectors: b (right-hand side, levels >= 1), two iterate buffers, residual
     DBuf<double> b, xa, xb, r;
     // sharded level: rows owned by this rank, halo columns n .. ncol_smooth-1

@@ -397,6 +397,7 @@ __global__ void k_rt_fill(int n, const int *__restrict__ prow, const int *__rest
 // sort each R row (the atomic fill order is arbitrary), then look the values
 // up in P.  One wavefront per row: rows of <= 64 entries are sorted by a
 // register bitonic network, longer ones by lane 0 (insertion sort).
+constexpr int kRtLdsRow = 1024;
 __global__ void __launch_bounds__(256) k_rt_sort_vals(int nc, const int *__restrict__ rrow, int *__restrict__ rcol,
                                                       const int *__restrict__ prow, const int *__restrict__ pcol,
                                                       const double *__restrict__ pval, double *__restrict__ rval)
@@ -418,6 +419,21 @@ __global__ void __launch_bounds__(256) k_rt_sort_vals(int nc, const int *__restr
             }
         }
         if (lane < len) rcol[s + lane] = v;
+    } else if (len <= kRtLdsRow) {
+        // longer rows (the folded R~ of a coarse level: ~150 entries): the row
+        // in LDS, every entry placed at its rank (the row indices are distinct)
+        __shared__ int buf[4][kRtLdsRow];
+        int *b = buf[threadIdx.x >> 6];
+        for (int a = lane; a < len; a += 64) b[a] = rcol[s + a];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int a = lane; a < len; a += 64) {
+            const int v = b[a];
+            int rk = 0;
+            for (int q = 0; q < len; ++q) rk += b[q] < v;
+            rcol[s + rk] = v;
+        }
     } else if (lane == 0) {
         for (int a = s + 1; a < e; ++a) {
             const int key = rcol[a];
@@ -1665,6 +1681,101 @@ __global__ void __launch_bounds__(256) k_csr_mv_g(int n, const int *__restrict__
     if (i < n && (threadIdx.x & (G - 1)) == 0) y[i] = ACC ? y[i] + s : s;
 }
 
+// Folded coarse level (V(1,1) with one Jacobi sweep, x_pre = w D^-1 b):
+//   pre   y  = x_pre + w D^-1 (b - A x_pre),  b_c = P~^T b
+//   post  x  = y + P~ x_c,                     P~ = (I - w D^-1 A) P
+// equal in exact arithmetic to sweep-from-0 + residual, R r, x += P x_c and
+// the post-sweep (R r' = P^T (I - w A D^-1) b = P~^T b for symmetric A), in
+// two launches instead of four.  P~ is formed over the pattern of A P (which
+// holds P's, the diagonal of A being nonzero).
+// kFoldLanes lanes per row of A P, each entry's P_ij found by a scan of the
+// (short: 2-3 entries) P row
+constexpr int kFoldLanes = 8;
+__global__ void __launch_bounds__(256) k_fold_p(int n, const unsigned long long *rho, const double *__restrict__ dinv,
+                                                const int *__restrict__ aprow, const int *__restrict__ apcol,
+                                                const double *__restrict__ apval, const int *__restrict__ prow,
+                                                const int *__restrict__ pcol, const double *__restrict__ pval,
+                                                int *__restrict__ fcol, double *__restrict__ fval)
+{
+    const int i = (int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) / kFoldLanes);
+    if (i >= n) return;
+    const int g = threadIdx.x & (kFoldLanes - 1);
+    const double ra = rho_of(rho);
+    const double wd = (ra > 0.0 ? 1.0 / ra : 0.0) * dinv[i];
+    const int pb = prow[i], pe = prow[i + 1];
+    for (int k = aprow[i] + g; k < aprow[i + 1]; k += kFoldLanes) {
+        const int c = apcol[k];
+        double pij = 0.0;
+        for (int q = pb; q < pe; ++q)
+            if (pcol[q] == c) pij = pval[q];
+        fcol[k] = c;
+        fval[k] = pij - wd * apval[k];
+    }
+}
+
+// level 0, folded post-step (the pre-step stays sweep-from-0 + residual and
+// R r'): u = x_pre + w D^-1 r' + P~ x_c, i.e. the prolongation and the
+// post-sweep in one pass over P~ instead of P and A.  Tile shape and r.u
+// partials as k_amg_smooth's last sweep (the SpMV's tiles and summation order).
+template <int B, int SLOTS>
+__global__ void __launch_bounds__(B) k_fold_post0(int n, const int *__restrict__ frow, const int *__restrict__ fcol,
+                                                  const double *__restrict__ fval, const double *__restrict__ xc,
+                                                  const double *__restrict__ dinv, const unsigned long long *rho,
+                                                  const double *__restrict__ xpre, const double *__restrict__ rres,
+                                                  const double *__restrict__ b, double *__restrict__ out,
+                                                  const int *done, double *__restrict__ part_gam)
+{
+    if (done && *done) return;
+    __shared__ __attribute__((aligned(16))) double lds[4 * SLOTS * B];
+    const double ra = rho_of(rho);
+    const double w = ra > 0.0 ? 1.0 / ra : 0.0;
+    const int t = xcd_tile(blockIdx.x, gridDim.x);
+    const int r0 = t * B;
+    const double pc = cg_tile_spmv<B, SLOTS>(r0, n, frow, fcol, fval, [&](int j) { return xc[j]; }, lds);
+    const int i = r0 + threadIdx.x;
+    double u = 0.0;
+    if (i < n) {
+        u = (xpre[i] + w * dinv[i] * rres[i]) + pc;
+        out[i] = u;
+    }
+    if (part_gam) {   // uniform per launch
+        __shared__ double red[2 * (B / 64)];
+        double g = 0.0, zero = 0.0;
+        if (i < n) g = b[i] * u;
+        cg_block_sum2(zero, g, red);
+        if (threadIdx.x == 0) part_gam[t] = g;
+    }
+}
+
+// the folded pre-step: workgroups [0, blocks_a) form y (GA lanes per fine
+// row), the rest b_c = P~^T b (GB lanes per coarse row)
+template <int GA, int GB>
+__global__ void __launch_bounds__(256) k_fold_pre(int n, int ncl, const int *__restrict__ rowptr,
+                                                  const int *__restrict__ col, const double *__restrict__ val,
+                                                  const double *__restrict__ dinv, const unsigned long long *rho,
+                                                  const double *__restrict__ b, double *__restrict__ y, int nc,
+                                                  const int *__restrict__ rrow, const int *__restrict__ rcol,
+                                                  const double *__restrict__ rval, double *__restrict__ bc,
+                                                  int blocks_a, const int *done)
+{
+    if (done && *done) return;
+    if ((int)blockIdx.x < blocks_a) {
+        const double ra = rho_of(rho);
+        const double w = ra > 0.0 ? 1.0 / ra : 0.0;
+        const int i = (blockIdx.x * blockDim.x + threadIdx.x) / GA;
+        const double ax =
+            group_row_dot<GA>(i, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; });
+        if (i < n && (threadIdx.x & (GA - 1)) == 0) {
+            const double di = dinv[i], bi = b[i], xi = w * di * bi;
+            y[i] = xi + w * di * (bi - ax);
+        }
+    } else {
+        const int c = ((blockIdx.x - blocks_a) * blockDim.x + threadIdx.x) / GB;
+        const double sc = group_row_dot<GB>(c, nc, rrow, rcol, rval, [&](int j) { return b[j]; });
+        if (c < nc && (threadIdx.x & (GB - 1)) == 0) bc[c] = sc;
+    }
+}
+
 // x = M b, one wavefront per row of the dense coarsest inverse (ld is a
 // multiple of 64 and the padding columns are zero): double2 loads, four in
 // flight per lane
@@ -2015,6 +2126,16 @@ static int tile_min_rows()
 }
 #define kTileMinRows tile_min_rows()
 
+// folded coarse levels (k_fold_pre); XFK_AMG_FOLD=0 keeps the four-launch form
+static bool fold_levels()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_AMG_FOLD");
+        return !e || std::atoi(e) != 0;
+    }();
+    return v;
+}
+
 // lanes per row for a CSR with this many nonzeros per row on average
 int lanes_for(double per_row)
 {
@@ -2179,6 +2300,25 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
 // MIS-2 aggregation of level l, P = (I - omega D_F^-1 A_F) P_tent and R = P^T
 // (strength flags and rho_F already computed).  nc = 0 when the level does
 // not coarsen usefully (allow_stop) or has no aggregate.
+// T = M^T of an n x nc CSR whose rows are sorted by column (T's rows come
+// out sorted by row): counting transpose, the fill counting the row counts
+// back down, rows sorted by a wave bitonic network, values looked up in M.
+// T's arrays hold as many entries as M (no read-back of the scan).
+static int transpose_csr(Amg &M, hipStream_t s, int n, int nc, const int *mrow, const int *mcol, const double *mval,
+                         int *trow, int *tcol, double *tval)
+{
+    AMG_CHECK(M.cnt.alloc((size_t)std::max(n, nc) + 1));
+    AMG_CHECK(hipMemsetAsync(M.cnt.p, 0, sizeof(int) * ((size_t)nc + 1), s));
+    if (n > 0) k_rt_count<<<nb(n), kB, 0, s>>>(n, mrow, mcol, M.cnt.p);
+    int rc = scan_only(M, s, M.cnt.p, trow, nc);
+    if (rc != XFK_OK) return rc;
+    if (n > 0) k_rt_fill<<<nb(n), kB, 0, s>>>(n, mrow, mcol, trow, M.cnt.p, tcol);
+    if (nc > 0)
+        k_rt_sort_vals<<<(int)(((long long)nc * 64 + 255) / 256), 256, 0, s>>>(nc, trow, tcol, mrow, mcol, mval, tval);
+    AMG_CHECK(hipGetLastError());
+    return XFK_OK;
+}
+
 int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
 {
     AmgLevel &A = *L[l];
@@ -2267,18 +2407,11 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     A.nc = (int)nc;
     if (std::getenv("XFK_AMG_DEBUG")) std::fprintf(stderr, "[amg] level %d P nnz %lld\n", l, A.pnnz);
     // R = P^T
-    AMG_CHECK(cnt.alloc((size_t)std::max<long long>(n, nc) + 1));
-    AMG_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * (nc + 1), s));
-    k_rt_count<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, cnt.p);
     AMG_CHECK(A.rrow.alloc((size_t)nc + 1));
-    const long long rnnz = A.pnnz;   // R = P^T: as many entries as P (no read-back of the scan)
-    if ((rc = scan_only(*this, s, cnt.p, A.rrow.p, (int)nc)) != XFK_OK) return rc;
-    AMG_CHECK(A.rcol.alloc((size_t)std::max(1LL, rnnz)));
-    AMG_CHECK(A.rval.alloc((size_t)std::max(1LL, rnnz)));
-    k_rt_fill<<<nb(n), kB, 0, s>>>(n, A.prow.p, A.pcol.p, A.rrow.p, cnt.p, A.rcol.p);
-    if (nc > 0)
-        k_rt_sort_vals<<<(int)((nc * 64 + 255) / 256), 256, 0, s>>>((int)nc, A.rrow.p, A.rcol.p, A.prow.p, A.pcol.p,
-                                                                   A.pval.p, A.rval.p);
+    AMG_CHECK(A.rcol.alloc((size_t)std::max(1LL, A.pnnz)));
+    AMG_CHECK(A.rval.alloc((size_t)std::max(1LL, A.pnnz)));
+    if ((rc = transpose_csr(*this, s, n, (int)nc, A.prow.p, A.pcol.p, A.pval.p, A.rrow.p, A.rcol.p, A.rval.p)) != XFK_OK)
+        return rc;
     if (g_prof) g_prof->end();
     return XFK_OK;
 }
@@ -2543,6 +2676,44 @@ int Amg::build(hipStream_t s, int l0)
         rc = spgemm<false>(*this, s, (int)nc, XR, YAP, C.rowptr_o, C.col_o, C.val_o, C.nnz, 4 * l + 2);
         if (g_prof) g_prof->end();
         if (rc != XFK_OK) return rc;
+        // folded level (l >= 1): P~ from A P before the next level reuses its buffers
+        A.fold = fold_levels() && sweeps == 1 && !A.dist;
+        if (A.fold) {
+            if (g_prof) g_prof->begin(lv + "folded transfer P~ = (I - w D^-1 A) P, R~ = P~^T", 0.0);
+            A.fnnz = ap_nnz;   // an upper bound while the A P length is deferred
+            AMG_CHECK(A.ftrow.alloc((size_t)n + 1));
+            AMG_CHECK(A.ftcol.alloc((size_t)std::max(1LL, ap_nnz)));
+            AMG_CHECK(A.ftval.alloc((size_t)std::max(1LL, ap_nnz)));
+            if (l > 0) {
+                AMG_CHECK(A.frrow.alloc((size_t)nc + 1));
+                AMG_CHECK(A.frcol.alloc((size_t)std::max(1LL, ap_nnz)));
+                AMG_CHECK(A.frval.alloc((size_t)std::max(1LL, ap_nnz)));
+            }
+            AMG_CHECK(hipMemcpyAsync(A.ftrow.p, ap_row.p, sizeof(int) * ((size_t)n + 1), hipMemcpyDeviceToDevice, s));
+            if (n > 0)
+                k_fold_p<<<(int)(((long long)n * kFoldLanes + 255) / 256), 256, 0, s>>>(
+                    n, rho.p + 2 * l, A.dinv.p, ap_row.p, ap_col.p, ap_val.p, A.prow.p, A.pcol.p, A.pval.p, A.ftcol.p,
+                    A.ftval.p);
+            // level 0 folds only its post-step (its pre-step keeps R r'): no R~
+            if (l > 0)
+                rc = transpose_csr(*this, s, n, (int)nc, A.ftrow.p, A.ftcol.p, A.ftval.p, A.frrow.p, A.frcol.p,
+                                   A.frval.p);
+            if (rc != XFK_OK) return rc;
+            // the exact length picks the V-cycle's lanes per row (and so the
+            // summation order): from a deferred slot when A P's length is
+            // deferred too, so hinted and measured setups agree bit for bit
+            if (def_n > 0 && def_n + 2 <= kAmgDeferSlots) {
+                AMG_CHECK(hipMemcpyAsync(def_dev.p + def_n + 1, A.ftrow.p + n, sizeof(int), hipMemcpyDeviceToDevice, s));
+                def_target[def_n / 2] = &A.fnnz;
+                def_n += 2;
+            } else if (def_n > 0) {
+                int len = 0;
+                AMG_CHECK(hipMemcpyAsync(&len, A.ftrow.p + n, sizeof(int), hipMemcpyDeviceToHost, s));
+                AMG_CHECK(hipStreamSynchronize(s));
+                A.fnnz = len;
+            }
+            if (g_prof) g_prof->end();
+        }
         C.n = (int)nc;
         C.ncol_lim = (int)nc;
         C.ncol_smooth = (int)nc;
@@ -3106,6 +3277,42 @@ void launch_smooth(hipStream_t s, int mode, int l, const AmgLevel &A, const unsi
     }
 }
 
+// lanes per row of the long R~ rows (up to one wavefront)
+int lanes_wide(double per_row)
+{
+    return per_row <= 6.0 ? 4 : (per_row <= 20.0 ? 8 : (per_row <= 40.0 ? 16 : (per_row <= 80.0 ? 32 : 64)));
+}
+
+template <int GA>
+void launch_fold_pre_a(hipStream_t s, const AmgLevel &A, const unsigned long long *rho, const double *b, double *y,
+                       double *bc, const int *done)
+{
+    const int GB = lanes_wide(A.nc > 0 ? (double)A.fnnz / A.nc : 1.0);
+    const int ga = (int)(((long long)A.n * GA + 255) / 256);
+    const int gb = (int)(((long long)A.nc * GB + 255) / 256);
+#define XFK_FOLD(GG)                                                                                               \
+    k_fold_pre<GA, GG><<<ga + gb, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, y,   \
+                                               A.nc, A.frrow.p, A.frcol.p, A.frval.p, bc, ga, done)
+    switch (GB) {
+    case 4: XFK_FOLD(4); break;
+    case 8: XFK_FOLD(8); break;
+    case 16: XFK_FOLD(16); break;
+    case 32: XFK_FOLD(32); break;
+    default: XFK_FOLD(64); break;
+    }
+#undef XFK_FOLD
+}
+
+void launch_fold_pre(hipStream_t s, const AmgLevel &A, const unsigned long long *rho, const double *b, double *y,
+                     double *bc, const int *done)
+{
+    if (A.n <= 0) return;
+    const int GA = lanes_for((double)A.nnz / A.n);
+    if (GA == 4) launch_fold_pre_a<4>(s, A, rho, b, y, bc, done);
+    else if (GA == 8) launch_fold_pre_a<8>(s, A, rho, b, y, bc, done);
+    else launch_fold_pre_a<16>(s, A, rho, b, y, bc, done);
+}
+
 // tile size of the level's smoother launches (0: sub-wave kernels, no split)
 int smooth_tile(int l, const AmgLevel &A) { return l == 0 ? kCgBlock : (A.n >= kTileMinRows ? 256 : 0); }
 
@@ -3172,6 +3379,18 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
             (void)hipMemcpyAsync(out0, cur, sizeof(double) * A.n, hipMemcpyDeviceToDevice, s);
         return cur;
     }
+    if (A.fold && l > 0) {
+        // two launches: y and the coarse right-hand side, then x = y + P~ x_c
+        AmgLevel &C = *M.L[l + 1];
+        double *y = A.xa.p;
+        const double n = A.n, nc = A.nc, f = (double)A.fnnz;
+        XFK_PHASE(lv + "folded pre: y, R~ r", 12.0 * A.nnz + 4.0 * (n + 1) + 24.0 * n + 12.0 * f + 4.0 * (nc + 1) + 8.0 * nc,
+                  launch_fold_pre(s, A, rho, b, y, C.b.p, done));
+        const double *xc = vcycle_level(M, s, l + 1, C.b.p, nullptr, done);
+        XFK_PHASE(lv + "folded post: x = y + P~ xc", 12.0 * f + 4.0 * (n + 1) + 8.0 * nc + 16.0 * n,
+                  launch_mv(s, A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xc, y, true, lanes_for(f / n), done));
+        return y;
+    }
     // pre-smoothing (nu sweeps from zero) and residual
     double *cur = A.xa.p;
     if (nu == 1) {
@@ -3191,6 +3410,15 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
               launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false, lanes_for((double)rnnz / A.nc),
                         done));
     const double *xc = vcycle_level(M, s, l + 1, C.b.p, nullptr, done);
+    if (A.fold && l == 0 && nu == 1) {
+        const double n = A.n, f = (double)A.fnnz;
+        XFK_PHASE(lv + "folded post: u = x + w D^-1 r + P~ xc" + (part_gam ? " (+ r.u partials)" : ""),
+                  12.0 * f + 4.0 * (n + 1) + 8.0 * A.nc + (part_gam ? 48.0 : 40.0) * n,
+                  (k_fold_post0<kCgBlock, 2><<<(A.n + kCgBlock - 1) / kCgBlock, kCgBlock, 0, s>>>(
+                      A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xc, A.dinv.p, rho, cur, A.r.p, b, out0, done, part_gam)));
+        if (part_gam) M.gamma_done = true;
+        return out0;
+    }
     XFK_PHASE(lv + "prolongation x += P xc", 12.0 * rnnz + 4.0 * (A.n + 1) + 8.0 * A.nc + 16.0 * A.n,
               launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)rnnz / A.n), done));
     for (int k = 0; k < nu; ++k) {
@@ -3270,6 +3498,7 @@ int Amg::refresh(hipStream_t s)
 {
     AmgLevel &A = *L[0];
     const int n = A.n;
+    A.fold = false;   // level 0's P~ was formed from the previous matrix: plain prolongation + sweep
     AMG_CHECK(absd.alloc(std::max(1, n)));
     AMG_CHECK(dfinv.alloc(std::max(1, n)));
     AMG_CHECK(wF.alloc(std::max(1, n)));

@@ -1750,8 +1750,9 @@ int xfk_phase_profile(xfk_problem *P, int iters, int flags, xfk_phase *out, int 
     prof.s = s;
     g_prof = &prof;
     int rc = XFK_OK;
-    if (flags & XFK_PROFILE_SETUP)
-        rc = P->amg->setup(s, P->N, P->N, P->rowptr.p, P->col.p, P->val.p, P->nnz_own);
+    // a fresh hierarchy built inside pcg_start (as in a solve), not a refresh
+    // of the last one (a refresh runs level 0 unfolded)
+    if (flags & XFK_PROFILE_SETUP) P->amg_reusable = false;
     if (rc == XFK_OK) {
         const double tol = P->precision;
         P->precision = 0.0;   // never converges: fixed iteration count
