@@ -1576,7 +1576,8 @@ __device__ __forceinline__ void smooth_finish(int i, double ax, double w, const 
     const double res = bi - ax;
     if constexpr (MODE == kSweepFromZero || MODE == kSweep) out[i] = xi + w * di * res;
     if constexpr (MODE == kResid || MODE == kResidFromZero) rout[i] = res;
-    if constexpr (MODE == kResidFromZero) out[i] = xi;
+    if constexpr (MODE == kResidFromZero)
+        if (out) out[i] = xi;   // (a folded level-0 post-step recomputes x_pre: not written)
 }
 
 // CSR-stream tile SpMV (the PCG's kernel shape): B = 1024 on level 0, 256 on
@@ -1721,7 +1722,7 @@ template <int B, int SLOTS>
 __global__ void __launch_bounds__(B) k_fold_post0(int n, const int *__restrict__ frow, const int *__restrict__ fcol,
                                                   const double *__restrict__ fval, const double *__restrict__ xc,
                                                   const double *__restrict__ dinv, const unsigned long long *rho,
-                                                  const double *__restrict__ xpre, const double *__restrict__ rres,
+                                                  const double *__restrict__ rres,
                                                   const double *__restrict__ b, double *__restrict__ out,
                                                   const int *done, double *__restrict__ part_gam)
 {
@@ -1735,7 +1736,8 @@ __global__ void __launch_bounds__(B) k_fold_post0(int n, const int *__restrict__
     const int i = r0 + threadIdx.x;
     double u = 0.0;
     if (i < n) {
-        u = (xpre[i] + w * dinv[i] * rres[i]) + pc;
+        const double di = dinv[i];
+        u = (w * di * b[i] + w * di * rres[i]) + pc;
         out[i] = u;
     }
     if (part_gam) {   // uniform per launch
@@ -3325,7 +3327,7 @@ static double smooth_bytes(const AmgLevel &A, int mode)
     const double n = A.n, base = 12.0 * (double)A.nnz + 4.0 * (n + 1);
     const bool implicit = mode == kSweepFromZero || mode == kResidFromZero;
     const double rd = (implicit ? 2.0 : 3.0) * 8.0 * n;
-    const double wr = (mode == kResidFromZero ? 2.0 : 1.0) * 8.0 * n;
+    const double wr = (mode == kResidFromZero && !A.fold ? 2.0 : 1.0) * 8.0 * n;
     return base + rd + wr;
 }
 
@@ -3394,7 +3396,8 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     // pre-smoothing (nu sweeps from zero) and residual
     double *cur = A.xa.p;
     if (nu == 1) {
-        smooth_ph(s, kResidFromZero, l, A, rho, b, nullptr, cur, A.r.p, done);
+        // (a folded level 0 recomputes x_pre = w D^-1 b in its post-step)
+        smooth_ph(s, kResidFromZero, l, A, rho, b, nullptr, (A.fold && l == 0) ? nullptr : cur, A.r.p, done);
     } else {
         smooth_ph(s, kSweepFromZero, l, A, rho, b, nullptr, cur, nullptr, done);
         for (int k = 2; k < nu; ++k) {
@@ -3413,9 +3416,9 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     if (A.fold && l == 0 && nu == 1) {
         const double n = A.n, f = (double)A.fnnz;
         XFK_PHASE(lv + "folded post: u = x + w D^-1 r + P~ xc" + (part_gam ? " (+ r.u partials)" : ""),
-                  12.0 * f + 4.0 * (n + 1) + 8.0 * A.nc + (part_gam ? 48.0 : 40.0) * n,
+                  12.0 * f + 4.0 * (n + 1) + 8.0 * A.nc + 32.0 * n,
                   (k_fold_post0<kCgBlock, 2><<<(A.n + kCgBlock - 1) / kCgBlock, kCgBlock, 0, s>>>(
-                      A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xc, A.dinv.p, rho, cur, A.r.p, b, out0, done, part_gam)));
+                      A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xc, A.dinv.p, rho, A.r.p, b, out0, done, part_gam)));
         if (part_gam) M.gamma_done = true;
         return out0;
     }
