@@ -129,6 +129,26 @@ __global__ void __launch_bounds__(kAxBlock) k_cg_axpy(CgAxpyArgs A)
     __shared__ double red[2 * (kAxBlock / 64)];
     CgState *S = A.S;
     if (S->done) return;
+    // AMG form: the first two row pairs of this thread are loaded before the
+    // partial reduction (they do not depend on alpha, beta), so the stream is
+    // in flight while the partials are summed
+    const int npair = A.N >> 1;
+    const int k0 = blockIdx.x * kAxBlock + threadIdx.x, kst = gridDim.x * kAxBlock;
+    double2 pf[2][6];
+    if (A.amg) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int k = k0 + q * kst;
+            if (k < npair) {
+                pf[q][0] = reinterpret_cast<const double2 *>(A.W)[k];
+                pf[q][1] = reinterpret_cast<const double2 *>(A.Z)[k];
+                pf[q][2] = reinterpret_cast<const double2 *>(A.P)[k];
+                pf[q][3] = reinterpret_cast<const double2 *>(A.V)[k];
+                pf[q][4] = reinterpret_cast<const double2 *>(A.R)[k];
+                pf[q][5] = reinterpret_cast<const double2 *>(A.U)[k];
+            }
+        }
+    }
     double gam, del;
     cg_reduce2(A.gam_in, A.Ggam, A.del_in, A.Gdel, gam, del, red);
     double res_o;
@@ -166,15 +186,17 @@ __global__ void __launch_bounds__(kAxBlock) k_cg_axpy(CgAxpyArgs A)
         double2 *V2 = reinterpret_cast<double2 *>(A.V);
         double2 *R2 = reinterpret_cast<double2 *>(A.R);
         const double2 *W2 = reinterpret_cast<const double2 *>(A.W);
-        for (int k = blockIdx.x * kAxBlock + threadIdx.x; k < (N >> 1); k += gridDim.x * kAxBlock) {
-            const double2 w = W2[k], zo = Z2[k], po = P2[k], x = V2[k], ri = R2[k], u = U2c[k];
+        auto upd = [&](int k, double2 w, double2 zo, double2 po, double2 x, double2 ri, double2 u) {
             double2 z, p, rn, xn;
             z.x = w.x + beta * zo.x;          z.y = w.y + beta * zo.y;
             p.x = u.x + beta * po.x;          p.y = u.y + beta * po.y;
             rn.x = ri.x - alpha * z.x;        rn.y = ri.y - alpha * z.y;
             xn.x = x.x + alpha * p.x;         xn.y = x.y + alpha * p.y;
             Z2[k] = z; P2[k] = p; V2[k] = xn; R2[k] = rn;
-        }
+        };
+        if (k0 < npair) upd(k0, pf[0][0], pf[0][1], pf[0][2], pf[0][3], pf[0][4], pf[0][5]);
+        if (k0 + kst < npair) upd(k0 + kst, pf[1][0], pf[1][1], pf[1][2], pf[1][3], pf[1][4], pf[1][5]);
+        for (int k = k0 + 2 * kst; k < npair; k += kst) upd(k, W2[k], Z2[k], P2[k], V2[k], R2[k], U2c[k]);
         if ((N & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
             const int r = N - 1;
             const double z = A.W[r] + beta * A.Z[r];
@@ -186,7 +208,6 @@ __global__ void __launch_bounds__(kAxBlock) k_cg_axpy(CgAxpyArgs A)
         return;
     }
     double g = 0.0;
-    const int npair = N >> 1;
     const double2 *W2 = reinterpret_cast<const double2 *>(A.W);
     double2 *Z2 = reinterpret_cast<double2 *>(A.Z);
     double2 *P2 = reinterpret_cast<double2 *>(A.P);
