@@ -19,6 +19,7 @@
 // k_cg_axpy first reduces the previous launches' per-block partials itself
 // (identical order in every block -> bit-identical alpha/beta everywhere, no
 // atomics, no fan-in tail).
+#include <cstdlib>
 #include "xfk_kernels.h"
 #include "xfk_spmv.h"
 
@@ -245,8 +246,12 @@ __global__ void __launch_bounds__(kAxBlock) k_cg_axpy(CgAxpyArgs A)
 int cg_grid(int N) { return (N + kCgBlock - 1) / kCgBlock; }
 int cg_axpy_grid(int N)
 {
+    static const int cap = [] {   // XFK_AX_GRID: measurement override of the fixed grid
+        const char *e = std::getenv("XFK_AX_GRID");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : kAxGrid;
+    }();
     int g = (N / 2 + kAxBlock - 1) / kAxBlock;
-    return g < 1 ? 1 : (g < kAxGrid ? g : kAxGrid);
+    return g < 1 ? 1 : (g < cap ? g : cap);
 }
 
 void launch_cg_init_r(hipStream_t s, int N, int flag, const int *rowptr, const int *col, const double *val,
