@@ -136,6 +136,60 @@ def nonlinear_secondary(device, args):
             "ms_symbolic": r["ms_symbolic"], "ms_solve": r["ms_solve"]}
 
 
+def configs4_secondary(device, args):
+    """BASELINE configs[4]'s mesh (3162 x 3162 cells, 20M triangles, 10.0M
+    DoF) solved on ONE GPU: the N = 1 anchor of the strong-scaling curve the
+    sharded N > 1 lines measure on the same mesh.  Same step definition as the
+    main line (symbolic phase included), after one warm-up solve."""
+    from xfemm_amd import kernels, synth
+    kw = synth.magnetostatic(args.shard_cells)
+    P = kernels.Static2DProblem(device=device, precond=args.precond, amg_sweeps=args.amg_sweeps,
+                                amg_omega=args.amg_omega, amg_dense=args.amg_dense, amg_theta=args.amg_theta, **kw)
+    P.solve(rebuild_symbolic=True)
+    _hip_sync()
+    t0 = time.perf_counter()
+    res = [P.solve(rebuild_symbolic=True) for _ in range(args.secondary_steps)]
+    _hip_sync()
+    dt = (time.perf_counter() - t0) / args.secondary_steps
+    n = P.n_nodes
+    P.close()
+    r = res[-1]
+    pcg = r["ms_solve"] - r["ms_amg_setup"]
+    return {"workload": "configs[4] mesh on 1 GPU: synthetic %d-tri square-domain magnetostatic, linear mu, tol %g"
+                        % (2 * args.shard_cells ** 2, kw["precision"]),
+            "metric": "solved DoF/s", "value": n / dt, "unit": "DoF/s", "ms_per_step": 1e3 * dt,
+            "steps": args.secondary_steps, "warmup": 1, "dof": n, "nnz": r["nnz"], "pcg_iters": r["cg_iters"],
+            "ms_per_pcg_iteration": pcg / max(1, r["cg_iters"]), "amg_levels": r["amg_levels"],
+            "ms_amg_setup": r["ms_amg_setup"], "ms_assemble": r["ms_assemble"], "ms_symbolic": r["ms_symbolic"],
+            "ms_solve": r["ms_solve"]}
+
+
+def cold_first_solve(device, args, kw):
+    """A first solve of a fresh problem: new Static2DProblem (host -> HBM
+    upload timed apart), then its first solve() with none of the per-problem
+    hints a re-solve reuses (SpGEMM slot capacities, the nested-dissection plan
+    of the dense coarsest level, MIS round batch sizes, the first PCG batch).
+    The process's code objects are already loaded (it runs after the timed
+    region)."""
+    from xfemm_amd import kernels
+    _hip_sync()
+    t0 = time.perf_counter()
+    P = kernels.Static2DProblem(device=device, precond=args.precond, amg_sweeps=args.amg_sweeps,
+                                amg_omega=args.amg_omega, amg_dense=args.amg_dense, amg_theta=args.amg_theta, **kw)
+    _hip_sync()
+    t1 = time.perf_counter()
+    r = P.solve(rebuild_symbolic=True)
+    _hip_sync()
+    t2 = time.perf_counter()
+    n = P.n_nodes
+    P.close()
+    return {"value": n / (t2 - t1), "unit": "DoF/s", "ms_first_solve": 1e3 * (t2 - t1),
+            "ms_create_upload": 1e3 * (t1 - t0), "pcg_iters": r["cg_iters"], "ms_amg_setup": r["ms_amg_setup"],
+            "ms_symbolic": r["ms_symbolic"], "ms_assemble": r["ms_assemble"], "ms_solve": r["ms_solve"],
+            "note": "fresh problem object, first solve (no re-solve hints); ms_create_upload = host -> HBM "
+                    "upload of the mesh and tables (outside the step)"}
+
+
 def pmc_traffic(algo_bytes, kernel="k_cg_spmv"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*_pmc_summary.json, written by tools/profile.sh from separate
@@ -167,6 +221,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the configs[3] (nonlinear M-19) secondary measurement")
     ap.add_argument("--secondary-steps", type=int, default=3)
+    ap.add_argument("--no-configs4", action="store_true",
+                    help="skip the configs[4] mesh (20M tri) single-GPU secondary measurement")
     ap.add_argument("--precond", choices=["amg", "jacobi"], default="amg",
                     help="device preconditioner of the PCG (the reference uses SSOR)")
     ap.add_argument("--amg-sweeps", type=int, default=1, help="Jacobi sweeps before/after the coarse correction")
@@ -349,8 +405,13 @@ def main():
                 sum(p["us_per_launch"] * p["launches_per_iteration"] for p in it_phases)))
     if same_mesh is not None:
         out["config"]["same_mesh_1gpu"] = same_mesh
+    if rank == 0 and world == 1 and not sharded:
+        out["cold_first_solve"] = cold_first_solve(local, args, kw)
     if rank == 0 and world == 1 and not sharded and not args.nonlinear and not args.no_secondary:
-        out["secondary"] = nonlinear_secondary(local, args)
+        P.close()
+        out["secondary"] = [nonlinear_secondary(local, args)]
+        if not args.no_configs4:
+            out["secondary"].append(configs4_secondary(local, args))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_cells, args.nonlinear)
     if rank == 0:

@@ -747,8 +747,17 @@ static int amg_setup(xfk_problem *P)
     P->amg->dense_max = P->amg_dense;
     // setup time: an event pair per setup, read after the solve's final
     // synchronisation (no host check here); callers that never read them
-    // recycle the pairs
-    if (P->setup_used >= 64) P->setup_used = 0;
+    // recycle the pairs; a full pool (> 64 fresh builds in one solve) is
+    // read out first, so no recorded pair is overwritten unread
+    if (P->setup_used >= 64) {
+        XFK_CHECK(hipStreamSynchronize(s));
+        for (int k = 0; k < P->setup_used; ++k) {
+            float m = 0;
+            XFK_CHECK(hipEventElapsedTime(&m, P->setup_ev[2 * k], P->setup_ev[2 * k + 1]));
+            P->setup_ms_pending += m;
+        }
+        P->setup_used = 0;
+    }
     if (P->setup_ev.size() < 2 * (P->setup_used + 1)) {
         P->setup_ev.resize(2 * (P->setup_used + 1), nullptr);
         for (auto &e : P->setup_ev)
@@ -889,8 +898,11 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
     // iteration launched after convergence exits at once but still costs
     // its launches, so the hint is not padded
     int batch = P->pc_used == XFK_PRECOND_AMG ? 8 : 16;
-    if (flag == 0 && P->pcg_hint0 > 0) batch = P->pcg_hint0;
+    // (clamped like every later batch, and never past the iteration cap, so a
+    // zero-diagonal matrix is still caught at the first poll)
+    if (flag == 0 && P->pcg_hint0 > 0) batch = std::min(P->pcg_hint0, 512);
     for (;;) {
+        batch = (int)std::max<long long>(1, std::min<long long>(batch, max_iters - it));
         for (int k = 0; k < batch; ++k, ++it) {
             const bool stamp = P->time_spmv && (it % 16 == 0) && P->spmv_used + 2 <= (int)P->spmv_ev.size();
             rc = pcg_iteration(P, it, stamp);
@@ -1461,6 +1473,7 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     P->last.amg_levels = 0;
     P->last.amg_op_complexity = 0;
     P->setup_used = 0;
+    P->setup_ms_pending = 0;
     XFK_CHECK(hipEventRecord(e0, s));
     if (!P->symbolic_ready || (flags & XFK_REBUILD_SYMBOLIC)) {
         P->symbolic_ready = false;
@@ -1537,7 +1550,9 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
         XFK_CHECK(hipEventElapsedTime(&m, P->setup_ev[2 * k], P->setup_ev[2 * k + 1]));
         P->last.ms_amg_setup += m;
     }
+    P->last.ms_amg_setup += P->setup_ms_pending;
     P->setup_used = 0;
+    P->setup_ms_pending = 0;
     if (P->time_spmv && P->spmv_used > 0) {
         double sum = 0;
         for (int k = 0; k < P->spmv_used; k += 2) {
@@ -1750,9 +1765,11 @@ int xfk_phase_profile(xfk_problem *P, int iters, int flags, xfk_phase *out, int 
     prof.s = s;
     g_prof = &prof;
     int rc = XFK_OK;
-    // a fresh hierarchy built inside pcg_start (as in a solve), not a refresh
-    // of the last one (a refresh runs level 0 unfolded)
-    if (flags & XFK_PROFILE_SETUP) P->amg_reusable = false;
+    // always a fresh hierarchy built inside pcg_start (as in a solve's first
+    // pass), never a Newton refresh of the last one: a refresh runs level 0
+    // unfolded, which is not the cycle a solve's first pass times.  Without
+    // XFK_PROFILE_SETUP the setup's own phases are dropped from the table.
+    P->amg_reusable = false;
     if (rc == XFK_OK) {
         const double tol = P->precision;
         P->precision = 0.0;   // never converges: fixed iteration count
@@ -1767,6 +1784,7 @@ int xfk_phase_profile(xfk_problem *P, int iters, int flags, xfk_phase *out, int 
     std::map<std::string, xfk_phase> agg;
     for (const auto &r : prof.recs) {
         if (r.ev0 < 0 || r.ev1 < 0) continue;
+        if (!(flags & XFK_PROFILE_SETUP) && r.name.compare(0, 5, "setup") == 0) continue;
         float ms = 0;
         XFK_CHECK(hipEventElapsedTime(&ms, prof.ev[r.ev0], prof.ev[r.ev1]));
         auto it = agg.find(r.name);

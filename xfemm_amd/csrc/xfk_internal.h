@@ -260,6 +260,7 @@ struct xfk_problem {
     int pcg_hint0 = 0;               // PCG iterations of the last solve's first pass (first batch)
     std::vector<hipEvent_t> setup_ev;   // AMG setup event pairs, read after the solve
     int setup_used = 0;
+    double setup_ms_pending = 0;        // pairs read out early when the pool filled
     xfk::SideStream side;
 
     // host copies kept for host-side setup (periodic maps)
