@@ -56,6 +56,10 @@ typedef struct {
     double mag_dir;             /* magnetisation direction, degrees */
     int is_wound;
     int is_external;            /* axisymmetric: conformally mapped exterior region ([IsExternal]) */
+    const char *mag_dir_fctn;   /* MagDirFctn: Lua expression of the element centroid (x y r z theta R)
+                                   giving the direction per element (static2d.cpp:511-581,
+                                   staticaxi.cpp:354-404); NULL or "" = the constant mag_dir.
+                                   Static problems only, as in the reference. */
 } xfk_label_desc;
 
 /* CMBoundaryProp (CBoundaryProp.h). */
@@ -363,6 +367,19 @@ typedef struct {
 } xfk_phase;
 enum { XFK_PROFILE_SETUP = 1 };
 int xfk_phase_profile(xfk_problem *prob, int iters, int flags, xfk_phase *out, int cap, int *count);
+
+/* Magnetisation-direction function of a block label, evaluated for elements
+ * as the reference's element loop does (FSolver::Static2D,
+ * cfemm/fsolver/static2d.cpp:509-583; StaticAxisymmetric staticaxi.cpp:350-406):
+ * the centroid of element i (nodes p[3i..3i+2], coordinates x, y in cm)
+ * in drawing units gives x y r z theta R, and t[i] is the real part of
+ * `fctn` in degrees (mag_dir when the expression returns nothing).  The
+ * expression language is the reference Lua's (complex numbers, the math
+ * library, PI, I), evaluated natively; errors carry the reference's messages
+ * ("Lua error occurred when evaluating: ...", "... does not evaluate to a
+ * numerical value").  Host only: no device is needed. */
+int xfk_magdir_eval(const char *fctn, int n_elems, const int *p, const double *x, const double *y,
+                    int length_units, double mag_dir, double *t);
 
 #ifdef __cplusplus
 }

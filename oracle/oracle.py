@@ -21,6 +21,7 @@ from . import femfile
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 REF_PATH = os.path.join(HERE, "_ref", "libxfemm_ref.so")
+LUA_PATH = os.path.join(HERE, "_ref", "libreflua.so")
 
 dptr = C.POINTER(C.c_double)
 iptr = C.POINTER(C.c_int)
@@ -84,7 +85,7 @@ class OraProblem(C.Structure):
                 ("precision", C.c_double), ("length_units", C.c_int), ("coords", C.c_int),
                 ("bandwidth", C.c_int), ("relax", C.c_double),
                 ("axisymmetric", C.c_int), ("ext_ro", C.c_double), ("ext_ri", C.c_double), ("ext_zo", C.c_double),
-                ("n_ages", C.c_int), ("ages", C.POINTER(OraAge))]
+                ("n_ages", C.c_int), ("ages", C.POINTER(OraAge)), ("elem_magdir", dptr)]
 
 
 class OraStats(C.Structure):
@@ -174,6 +175,39 @@ def ref():
     return _ref
 
 
+_lua = None
+
+
+def ref_lua_available() -> bool:
+    return os.path.exists(LUA_PATH)
+
+
+def ref_magdir(fctn: str, p, x, y, length_units: int, mag_dir: float) -> np.ndarray:
+    """Per-element magnetisation directions of a MagDirFctn label computed by
+    the reference's own Lua interpreter (oracle/_ref/libreflua.so, the element
+    loop of static2d.cpp:509-583).  Raises ValueError with the reference's
+    message when the chunk fails."""
+    global _lua
+    if _lua is None:
+        if not os.path.exists(LUA_PATH):
+            raise FileNotFoundError(LUA_PATH)
+        _lua = C.CDLL(LUA_PATH)
+        _lua.ref_lua_magdir.argtypes = [C.c_char_p, C.c_int, iptr, dptr, dptr, C.c_int, C.c_double, dptr,
+                                        C.c_char_p, C.c_int]
+        _lua.ref_lua_magdir.restype = C.c_int
+    p = _arr(np.asarray(p).reshape(-1), np.int32)
+    x, y = _arr(x, np.float64), _arr(y, np.float64)
+    n = len(p) // 3
+    t = np.zeros(max(1, n))
+    msg = C.create_string_buffer(8192)
+    rc = _lua.ref_lua_magdir(fctn.encode(), n, p.ctypes.data_as(iptr), x.ctypes.data_as(dptr),
+                             y.ctypes.data_as(dptr), int(length_units), float(mag_dir), t.ctypes.data_as(dptr), msg,
+                             len(msg))
+    if rc != 0:
+        raise ValueError(msg.value.decode())
+    return t[:n]
+
+
 def _ref_ops() -> OraOps:
     r = ref()
     return OraOps(_CREATE(("ref_lp_create", r)), _DESTROY(("ref_lp_destroy", r)),
@@ -204,6 +238,21 @@ class _Keep:
         return a.ctypes.data_as(iptr)
 
 
+def element_magdir(pr: femfile.FemProblem, mesh: femfile.Mesh) -> np.ndarray:
+    """Per-element magnetisation direction (degrees): the label's MagDir, or
+    what the reference's Lua makes of its MagDirFctn at the element centroid
+    (ref_magdir).  Static problems only, as the reference."""
+    lbl = np.asarray(mesh.lbl)
+    t = np.array([lb.MagDir for lb in pr.labels], float)[lbl]
+    for k, lb in enumerate(pr.labels):
+        if not lb.MagDirFctn:
+            continue
+        sel = np.where(lbl == k)[0]
+        if len(sel):
+            t[sel] = ref_magdir(lb.MagDirFctn, np.asarray(mesh.p)[sel], mesh.x, mesh.y, pr.LengthUnits, lb.MagDir)
+    return t
+
+
 def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
     keep = _Keep()
     blocks = (OraBlock * max(1, len(pr.blocks)))()
@@ -215,8 +264,6 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
             b.Bdata, b.Hdata, b.slope = keep.d(m.Bdata), keep.d(m.Hdata), keep.d(m.slope)
     labels = (OraLabel * max(1, len(pr.labels)))()
     for k, lb in enumerate(pr.labels):
-        if lb.MagDirFctn:
-            raise NotImplementedError("Lua magnetisation-direction functions are out of scope")
         labels[k].InCircuit, labels[k].MagDir, labels[k].bIsWound = lb.InCircuit, lb.MagDir, int(lb.bIsWound)
         labels[k].IsExternal = int(lb.IsExternal)
     lines = (OraLine * max(1, len(pr.bdrys)))()
@@ -246,6 +293,7 @@ def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):
     P.axisymmetric = int(pr.ProblemType == 1)
     P.ext_ro, P.ext_ri, P.ext_zo = pr.extRo, pr.extRi, pr.extZo
     P.n_ages, P.ages = make_ages(mesh, keep)
+    P.elem_magdir = keep.d(element_magdir(pr, mesh)) if any(lb.MagDirFctn for lb in pr.labels) else None
     keep.items.extend([blocks, labels, lines, points, circs])
     return P, keep, circs
 

@@ -472,8 +472,8 @@ static void ora_assemble(ora_problem *pr, const ora_linprob_ops *ops, void *L, i
                 K = -(bp->J_re + t) * a / 3.;
                 be[j] += K;
             }
-            /* magnetization */
-            t = lab->MagDir;
+            /* magnetization (static2d.cpp:509-598; a MagDirFctn label's direction per element) */
+            t = pr->elem_magdir ? pr->elem_magdir[i] : lab->MagDir;
             for (int j = 0; j < 3; j++) {
                 int k = j + 1;
                 if (k == 3) k = 0;
@@ -758,8 +758,8 @@ static void ora_assemble_axi(ora_problem *pr, const ora_linprob_ops *ops, void *
             K = -2. * R * (bp->J_re + t) * a / 3.;
             be[j] += K;
         }
-        /* magnetization, r-weighted (staticaxi.cpp:339-407; no Lua directions) */
-        t = lab->MagDir;
+        /* magnetization, r-weighted (staticaxi.cpp:339-407) */
+        t = pr->elem_magdir ? pr->elem_magdir[i] : lab->MagDir;
         for (int j = 0; j < 3; j++) {
             int k = j + 1;
             if (k == 3) k = 0;

@@ -106,6 +106,9 @@ typedef struct {
     int axisymmetric;           /* ProblemType: 0 planar (Static2D), 1 axisymmetric */
     double ext_ro, ext_ri, ext_zo;   /* exterior-region parameters (user units) */
     int n_ages;  const ora_age *ages;   /* air-gap elements (planar only, as the reference) */
+    const double *elem_magdir;  /* per element: the direction a label's MagDirFctn gives (degrees,
+                                   from the reference's own Lua, oracle/ref_lua.cpp); NULL = the
+                                   labels' constant MagDir */
 } ora_problem;
 
 typedef struct {

@@ -22,7 +22,7 @@ def kernel_kwargs(pr: femfile.FemProblem, mesh: femfile.Mesh) -> dict:
         blocks.append(b)
     labels = [dict(block=max(lb.BlockType, 0), in_circuit=lb.InCircuit, mag_dir=lb.MagDir,
                    is_wound=int(lb.bIsWound), is_external=int(lb.IsExternal),
-                   prox_mu=complex(lb.ProximityMu)) for lb in pr.labels]
+                   prox_mu=complex(lb.ProximityMu), mag_dir_fctn=lb.MagDirFctn) for lb in pr.labels]
     lines = [dict(format=b.BdryFormat, A0=b.A0, A1=b.A1, A2=b.A2, phi=b.phi, c0=b.c0, c1=b.c1, c0_im=b.c0i,
                   c1_im=b.c1i, Mu=b.Mu, Sig=b.Sig) for b in pr.bdrys]
     points = [dict(A_re=q.A_re, A_im=q.A_im, J_re=q.J_re, J_im=q.J_im) for q in pr.points]
@@ -66,6 +66,7 @@ def synth_to_oracle(kw: dict):
     for lb in kw["labels"]:
         pr.labels.append(femfile.BlockLabel(BlockType=lb["block"], InCircuit=lb.get("in_circuit", -1),
                                             MagDir=lb.get("mag_dir", 0.0),
+                                            MagDirFctn=lb.get("mag_dir_fctn", ""),
                                             Turns=lb.get("turns", 2 if lb.get("is_wound", 0) else 1),
                                             IsExternal=bool(lb.get("is_external", 0))))
     for ln in kw["lines"]:

@@ -606,11 +606,6 @@ struct FSolver::DescStore {
 bool FSolver::make_desc(DescStore &ds)
 {
     for (int i = 0; i < (int)labellist.size(); i++) GetFillFactor(i);
-    for (auto &lb : labellist)
-        if (!lb.MagDirFctn.empty()) {
-            warn("Lua magnetisation-direction functions are not supported by this solver build\n");
-            return false;
-        }
     ds.blk.resize(blockproplist.size());
     for (size_t k = 0; k < blockproplist.size(); k++) {
         const CMSolverMaterialProp &m = blockproplist[k];
@@ -632,6 +627,7 @@ bool FSolver::make_desc(DescStore &ds)
         ds.lab[k].mag_dir = labellist[k].MagDir;
         ds.lab[k].is_wound = labellist[k].bIsWound ? 1 : 0;
         ds.lab[k].is_external = labellist[k].IsExternal ? 1 : 0;
+        ds.lab[k].mag_dir_fctn = labellist[k].MagDirFctn.empty() ? nullptr : labellist[k].MagDirFctn.c_str();
     }
     ds.lin.resize(lineproplist.size());
     for (size_t k = 0; k < lineproplist.size(); k++) {

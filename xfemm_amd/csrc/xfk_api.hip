@@ -25,6 +25,7 @@
 #include "xfk_age.h"
 #include "xfk_comm.h"
 #include "xfk_kernels.h"
+#include "xfk_magdir.h"
 #include <cstdio>
 #include <cstdlib>
 #include "xfk_partition.h"
@@ -1024,6 +1025,46 @@ int check_device(int device)
     return XFK_OK;
 }
 
+int prepare_magdir(const xfk_problem_desc *d, GlobalPrep &G)
+{
+    // Functional magnetisation directions (static2d.cpp:509-583,
+    // staticaxi.cpp:350-406): the reference runs the label's Lua chunk for
+    // every element in every Newton pass; the result depends on the centroid
+    // only, so it is evaluated once here (xfk_magdir.cpp, the same angle to
+    // the bit) and each element of such a label gets a label entry of its own
+    // carrying cos / sin of its angle -- the device kernels are unchanged.
+    std::vector<std::shared_ptr<const MagDirExpr>> ex(d->n_labels);
+    bool any = false;
+    std::string err;
+    for (int k = 0; k < d->n_labels; ++k) {
+        const char *f = d->labels[k].mag_dir_fctn;
+        if (!f || !*f) continue;
+        ex[k] = magdir_parse(f, err);
+        XFK_REQUIRE(ex[k] != nullptr, XFK_ERR_ARG, err.c_str());
+        any = true;
+    }
+    if (!any) return XFK_OK;
+    const int NE = d->n_elems;
+    G.elab.assign(d->lbl, d->lbl + NE);
+    for (int i = 0; i < NE; ++i) {
+        const int l = d->lbl[i];
+        if (!ex[l]) continue;
+        double X[3], Y[3], t = 0;
+        for (int j = 0; j < 3; ++j) {
+            X[j] = d->x[d->p[3LL * i + j]];
+            Y[j] = d->y[d->p[3LL * i + j]];
+        }
+        XFK_REQUIRE(magdir_eval(*ex[l], X, Y, d->length_units, d->labels[l].mag_dir, &t, err), XFK_ERR_ARG,
+                    err.c_str());
+        DevLabel v = G.lab[l];
+        v.cos_m = cos(t * kPI / 180.);   // static2d.cpp:593-595
+        v.sin_m = sin(t * kPI / 180.);
+        G.elab[i] = (int)G.lab.size();
+        G.lab.push_back(v);
+    }
+    return XFK_OK;
+}
+
 void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
 {
     const int N = d->n_nodes, NE = d->n_elems;
@@ -1254,7 +1295,7 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
         pl.assign(d->p, d->p + 3LL * NE);
     }
     for (int l = 0; l < NE; ++l) {
-        lbl[l] = d->lbl[gelem(l)];
+        lbl[l] = G.elab.empty() ? d->lbl[gelem(l)] : G.elab[gelem(l)];
         ebits[l] = G.ebits[gelem(l)];
     }
     P->hp = pl;
@@ -1339,7 +1380,7 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
         return fail(XFK_ERR_HIP);
     }
     P->nblocks = d->n_blocks;
-    P->nlabels = d->n_labels;
+    P->nlabels = (int)G.lab.size();
     P->nlines = d->n_lines;
     P->ncircs = d->n_circs;
     *out = P;
@@ -1359,6 +1400,8 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
     if (rc != XFK_OK) return rc;
     GlobalPrep G;
     prepare_global(d, G);
+    rc = prepare_magdir(d, G);
+    if (rc != XFK_OK) return rc;
     rc = age_entries(d, 1.0, G.age_key, G.age_val);
     if (rc != XFK_OK) return rc;
     return build_local(d, G, nullptr, device, nullptr, out);
@@ -1415,6 +1458,8 @@ int xfk_problem_create_dist(const xfk_problem_desc *d, int device, xfk_comm *com
     if (rc != XFK_OK) return rc;
     GlobalPrep G;
     prepare_global(d, G);
+    rc = prepare_magdir(d, G);
+    if (rc != XFK_OK) return rc;
     rc = age_entries(d, 1.0, G.age_key, G.age_val);
     if (rc != XFK_OK) return rc;
     // coupled nodes: periodic pairs and air-gap quad nodes (assembled on every rank)

@@ -479,7 +479,8 @@ extern thread_local PhaseProf *g_prof;
 struct GlobalPrep {
     std::vector<DevBlock> blk;
     std::vector<double> hB, hH, hS;
-    std::vector<DevLabel> lab;
+    std::vector<DevLabel> lab;           // labels, then one per element of a MagDirFctn label
+    std::vector<int> elab;               // per element: index into lab (empty: the mesh's lbl)
     std::vector<DevLine> lin;
     std::vector<DevCirc> circ;
     std::vector<int> ebits;              // per element: 3 x 10-bit boundary-prop index + 1
@@ -497,6 +498,8 @@ struct GlobalPrep {
 int validate_desc(const xfk_problem_desc *d);
 int check_device(int device);
 void prepare_global(const xfk_problem_desc *d, GlobalPrep &G);
+// static problems: per-element magnetisation directions of MagDirFctn labels
+int prepare_magdir(const xfk_problem_desc *d, GlobalPrep &G);
 // the device problem of one rank (plan == nullptr: the whole mesh)
 int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *plan, int device, xfk_comm *comm,
                 xfk_problem **out);

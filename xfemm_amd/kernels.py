@@ -43,6 +43,7 @@ EXPORTED = (
     "xfk_get_csr_complex",
     "xfk_comm_unique_id", "xfk_comm_create_rccl", "xfk_comm_create_local", "xfk_comm_destroy",
     "xfk_comm_rank", "xfk_comm_size", "xfk_partition_plan", "xfk_partition_plan_coupled", "xfk_problem_create_dist", "xfk_dist_get_info",
+    "xfk_magdir_eval",
 )
 
 
@@ -55,7 +56,7 @@ class BlockDesc(C.Structure):
 
 class LabelDesc(C.Structure):
     _fields_ = [("block", C.c_int), ("in_circuit", C.c_int), ("mag_dir", C.c_double),
-                ("is_wound", C.c_int), ("is_external", C.c_int)]
+                ("is_wound", C.c_int), ("is_external", C.c_int), ("mag_dir_fctn", C.c_char_p)]
 
 
 class LineDesc(C.Structure):
@@ -171,6 +172,7 @@ def load_library(path: str = KERNELS_SO):
                                              C.POINTER(DistInfo), iptr, iptr, iptr, iptr]
     L.xfk_problem_create_dist.argtypes = [C.POINTER(ProblemDesc), C.c_int, vp, C.POINTER(vp)]
     L.xfk_dist_get_info.argtypes = [vp, C.POINTER(DistInfo)]
+    L.xfk_magdir_eval.argtypes = [C.c_char_p, C.c_int, iptr, dptr, dptr, C.c_int, C.c_double, dptr]
     _lib = L
     return L
 
@@ -218,6 +220,11 @@ def _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e,
         lb[k].block, lb[k].in_circuit = l["block"], l.get("in_circuit", -1)
         lb[k].mag_dir, lb[k].is_wound = l.get("mag_dir", 0.0), int(l.get("is_wound", 0))
         lb[k].is_external = int(l.get("is_external", 0))
+        f = l.get("mag_dir_fctn") or ""
+        if f:
+            fb = f.encode()
+            keep.append(fb)
+            lb[k].mag_dir_fctn = fb
     ln = (LineDesc * max(1, len(lines)))()
     for k, l in enumerate(lines):
         o = ln[k]
@@ -267,6 +274,21 @@ def _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e,
     D.n_ages, D.ages = len(ages), ag
     keep.extend([bl, lb, ln, pt, ci, ag])
     return D, keep
+
+
+def magdir_eval(fctn: str, p, x, y, length_units: int = 0, mag_dir: float = 0.0) -> np.ndarray:
+    """Per-element magnetisation direction (degrees) of a label's MagDirFctn
+    (xfk_magdir_eval; host only, no device needed).  Raises XfkError with the
+    reference's message when the expression does not evaluate."""
+    L = load_library()
+    p = np.ascontiguousarray(np.asarray(p, dtype=np.int32).reshape(-1))
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    n = len(p) // 3
+    t = np.zeros(max(1, n))
+    _check(L.xfk_magdir_eval(fctn.encode(), n, p.ctypes.data_as(iptr), x.ctypes.data_as(dptr),
+                             y.ctypes.data_as(dptr), int(length_units), float(mag_dir), t.ctypes.data_as(dptr)))
+    return t[:n]
 
 
 def age_element_matrix(ci: float, co: float, K: float, Ki: float) -> np.ndarray:
