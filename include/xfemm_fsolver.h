@@ -59,6 +59,24 @@ int xfemm_fsolver_get_elements(xfemm_fsolver *s, int *p, int *lbl);
 int xfemm_fsolver_get_stats(xfemm_fsolver *s, xfk_result *out);
 const char *xfemm_fsolver_last_error(xfemm_fsolver *s);
 
+/* femmcli's binding (cfemm/femmcli/LuaMagneticsCommands.cpp:817-842, mi_analyze):
+ * it sets FSolver::previousSolutionFile from the document before
+ * LoadProblemFile (:824) -- kept unless the .fem carries its own [PrevSoln]
+ * line, as FEASolver::CleanUp leaves the member alone (feasolver.cpp:134-172)
+ * -- and then asserts the loaded solver against the document (:830-838):
+ * ACSolver, Frequency and the sizes of the property lists (circuits may grow
+ * by the serial expansion; labels exclude holes).  Getters return -1 (0.0
+ * for the frequency) on a NULL handle. */
+int xfemm_fsolver_set_previous_solution_file(xfemm_fsolver *s, const char *path);   /* fsolver.h previousSolutionFile */
+const char *xfemm_fsolver_previous_solution_file(xfemm_fsolver *s);
+int xfemm_fsolver_ac_solver(xfemm_fsolver *s);               /* FSolver::ACSolver */
+double xfemm_fsolver_frequency(xfemm_fsolver *s);            /* FSolver::Frequency (Hz) */
+int xfemm_fsolver_num_line_props(xfemm_fsolver *s);          /* lineproplist.size() */
+int xfemm_fsolver_num_node_props(xfemm_fsolver *s);          /* nodeproplist.size() */
+int xfemm_fsolver_num_block_props(xfemm_fsolver *s);         /* blockproplist.size() */
+int xfemm_fsolver_num_circ_props(xfemm_fsolver *s);          /* circproplist.size(), after the serial expansion */
+int xfemm_fsolver_num_block_labels(xfemm_fsolver *s);        /* labellist.size() */
+
 /* CMMaterialProp::GetSlopes(0) (libfemm/CMaterialProp.cpp:127): processes a
  * B-H curve in place (B, H: n points) and writes the knot slopes; returns the
  * initial relative permeability in *mu_x.  1 on success. */

@@ -133,3 +133,33 @@ def test_prev_refusals_through_fsolver(tmp_path):
         fh.write(ansfile.with_prev(t, base + ".ans", 1))
     fs = _run(h, ok=False)
     assert "slopes" in fs.last_error()
+
+
+def test_prev_solution_preset_through_the_c_abi(tmp_path):
+    """femmcli's way (LuaMagneticsCommands.cpp:824): previousSolutionFile set
+    through xfemm_fsolver_set_previous_solution_file before LoadProblemFile,
+    on a .fem without a [PrevSoln] line -- the same answer, bit for bit, as the
+    [PrevSoln] line gives (test_prev_torque_benchmark_resolve)."""
+    deg = 40
+    base = write_case(tmp_path, deg)
+    _run(base)
+    fem = open(base + ".fem").read()
+    base_line = str(tmp_path / "line")
+    with open(base_line + ".fem", "w") as fh:
+        fh.write(ansfile.with_prev(fem, base + ".ans", 0))
+    _run(base_line)
+    base_preset = str(tmp_path / "preset")
+    with open(base_preset + ".fem", "w") as fh:
+        fh.write("\n".join(ln for ln in fem.split("\n") if not ln.strip().lower().startswith("[prevsoln]")))
+    fs = fsolver.FSolver(delete_mesh_files=False)
+    fs.PathName = base_preset
+    fs.previousSolutionFile = base + ".ans"
+    assert fs.LoadProblemFile(), fs.last_error()
+    assert fs.ACSolver == 0 and fs.Frequency == 0.0 and fs.NumNodes > 0
+    assert fs.runSolver(False), fs.last_error()
+    a = femfile.read_ans(base_line + ".ans")
+    b = femfile.read_ans(base_preset + ".ans")
+    assert np.array_equal(a.p, b.p) and np.array_equal(a.A, b.A)
+    pr, _ = femfile.load_problem(base)
+    tq = gaptorque.gap_dc_torque(b.ages[0], b.A, pr.Depth, pr.LengthUnits)
+    assert torque_ok(tq, deg)[0], tq

@@ -146,6 +146,32 @@ int xfemm_fsolver_get_stats(xfemm_fsolver *h, xfk_result *out)
 
 const char *xfemm_fsolver_last_error(xfemm_fsolver *h) { return h ? h->s.lastError.c_str() : ""; }
 
+int xfemm_fsolver_set_previous_solution_file(xfemm_fsolver *h, const char *path)
+{
+    if (!h) return 0;
+    h->s.previousSolutionFile = path ? path : "";
+    return 1;
+}
+
+const char *xfemm_fsolver_previous_solution_file(xfemm_fsolver *h)
+{
+    return h ? h->s.previousSolutionFile.c_str() : "";
+}
+
+int xfemm_fsolver_ac_solver(xfemm_fsolver *h) { return h ? h->s.ACSolver : -1; }
+
+double xfemm_fsolver_frequency(xfemm_fsolver *h) { return h ? h->s.Frequency : 0.0; }
+
+int xfemm_fsolver_num_line_props(xfemm_fsolver *h) { return h ? (int)h->s.lineproplist.size() : -1; }
+
+int xfemm_fsolver_num_node_props(xfemm_fsolver *h) { return h ? (int)h->s.nodeproplist.size() : -1; }
+
+int xfemm_fsolver_num_block_props(xfemm_fsolver *h) { return h ? (int)h->s.blockproplist.size() : -1; }
+
+int xfemm_fsolver_num_circ_props(xfemm_fsolver *h) { return h ? (int)h->s.circproplist.size() : -1; }
+
+int xfemm_fsolver_num_block_labels(xfemm_fsolver *h) { return h ? (int)h->s.labellist.size() : -1; }
+
 int xfemm_bh_get_slopes(int n, double *B, double *H, double *slope, int lam_type, double lam_fill, double *mu_x)
 {
     if (n < 2 || !B || !H || !slope) return 0;

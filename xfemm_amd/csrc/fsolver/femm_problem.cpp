@@ -581,7 +581,10 @@ bool ParseFemFile(const std::string &path, FemmProblemData &pr, std::string &err
         } else if (tok == "[comment]") ok = parse_string(rest, pr.comment);
         else if (tok == "[acsolver]") ok = parse_int(rest, pr.ACSolver);
         else if (tok == "[prevtype]") ok = parse_int(rest, pr.PrevType);
-        else if (tok == "[prevsoln]") ok = parse_string(rest, pr.previousSolutionFile);
+        else if (tok == "[prevsoln]") {
+            ok = parse_string(rest, pr.previousSolutionFile);
+            pr.prevSolnInFile = true;
+        }
         else if (tok == "[pointprops]") {
             int k = 0;
             ok = parse_int(rest, k);

@@ -122,6 +122,7 @@ struct FemmProblemData {
     int ACSolver = 0;
     int PrevType = 0;
     std::string previousSolutionFile;
+    bool prevSolnInFile = false;       // the .fem had a [PrevSoln] line
     std::string comment;
     std::vector<CMPointProp> nodeproplist;
     std::vector<CMBoundaryProp> lineproplist;

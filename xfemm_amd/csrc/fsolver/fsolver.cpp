@@ -51,10 +51,16 @@ bool FSolver::LoadProblemFile()
     Relax = 1.;
     std::string err;
     FemmProblemData &base = *this;
+    // a previous-solution file set by the caller survives the parse unless the
+    // .fem names one itself (FEASolver::CleanUp keeps previousSolutionFile,
+    // feasolver.cpp:134-172; femmcli sets it before LoadProblemFile,
+    // LuaMagneticsCommands.cpp:824)
+    const std::string presetPrev = previousSolutionFile;
     if (!ParseFemFile(PathName + ".fem", base, err)) {
         warn(err);
         return false;
     }
+    if (!prevSolnInFile) previousSolutionFile = presetPrev;
     meshLoadedFromPrevSolution = false;
     if (!previousSolutionFile.empty()) {
         // fsolver.cpp:224-238: the mesh (and A, for PrevType != 0) come from

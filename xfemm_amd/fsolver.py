@@ -25,6 +25,9 @@ EXPORTED = (
     "xfemm_fsolver_get_block_bh", "xfemm_fsolver_num_nodes", "xfemm_fsolver_num_elements",
     "xfemm_fsolver_get_solution", "xfemm_fsolver_get_elements", "xfemm_fsolver_get_stats",
     "xfemm_fsolver_last_error", "xfemm_bh_get_slopes", "xfemm_bh_get_slopes_ac",
+    "xfemm_fsolver_set_previous_solution_file", "xfemm_fsolver_previous_solution_file", "xfemm_fsolver_ac_solver",
+    "xfemm_fsolver_frequency", "xfemm_fsolver_num_line_props", "xfemm_fsolver_num_node_props",
+    "xfemm_fsolver_num_block_props", "xfemm_fsolver_num_circ_props", "xfemm_fsolver_num_block_labels",
 )
 
 _lib = None
@@ -61,6 +64,15 @@ def load_library(path: str = FSOLVER_SO):
     L.xfemm_fsolver_get_elements.argtypes = [vp, iptr, iptr]
     L.xfemm_fsolver_get_stats.argtypes = [vp, C.POINTER(kernels.Result)]
     L.xfemm_fsolver_last_error.argtypes = [vp]
+    L.xfemm_fsolver_set_previous_solution_file.argtypes = [vp, C.c_char_p]
+    L.xfemm_fsolver_previous_solution_file.argtypes = [vp]
+    L.xfemm_fsolver_previous_solution_file.restype = C.c_char_p
+    L.xfemm_fsolver_frequency.argtypes = [vp]
+    L.xfemm_fsolver_frequency.restype = C.c_double
+    for nm in ("xfemm_fsolver_ac_solver", "xfemm_fsolver_num_line_props", "xfemm_fsolver_num_node_props",
+               "xfemm_fsolver_num_block_props", "xfemm_fsolver_num_circ_props", "xfemm_fsolver_num_block_labels"):
+        getattr(L, nm).argtypes = [vp]
+        getattr(L, nm).restype = C.c_int
     L.xfemm_fsolver_last_error.restype = C.c_char_p
     L.xfemm_bh_get_slopes.argtypes = [C.c_int, dptr, dptr, dptr, C.c_int, C.c_double, dptr]
     L.xfemm_bh_get_slopes_ac.argtypes = [C.c_int, dptr, dptr, dptr, dptr, dptr, C.c_double, C.c_int, C.c_double,
@@ -124,6 +136,31 @@ class FSolver:
     def PathName(self, p: str):
         self._path = p
         _lib.xfemm_fsolver_set_pathname(self._h, p.encode())
+
+    @property
+    def previousSolutionFile(self) -> str:
+        """FSolver::previousSolutionFile; femmcli sets it before LoadProblemFile
+        (LuaMagneticsCommands.cpp:824), a [PrevSoln] line of the .fem overrides it."""
+        return _lib.xfemm_fsolver_previous_solution_file(self._h).decode()
+
+    @previousSolutionFile.setter
+    def previousSolutionFile(self, p: str):
+        _lib.xfemm_fsolver_set_previous_solution_file(self._h, p.encode())
+
+    @property
+    def ACSolver(self) -> int:
+        return _lib.xfemm_fsolver_ac_solver(self._h)
+
+    @property
+    def Frequency(self) -> float:
+        return _lib.xfemm_fsolver_frequency(self._h)
+
+    def list_sizes(self) -> dict:
+        """The property-list sizes femmcli asserts on (LuaMagneticsCommands.cpp:832-838)."""
+        h = self._h
+        return dict(lineproplist=_lib.xfemm_fsolver_num_line_props(h), nodeproplist=_lib.xfemm_fsolver_num_node_props(h),
+                    blockproplist=_lib.xfemm_fsolver_num_block_props(h),
+                    circproplist=_lib.xfemm_fsolver_num_circ_props(h), labellist=_lib.xfemm_fsolver_num_block_labels(h))
 
     def LoadProblemFile(self) -> bool:
         return bool(_lib.xfemm_fsolver_load_problem_file(self._h))
