@@ -209,6 +209,63 @@ def pmc_traffic(algo_bytes, kernel="k_cg_spmv"):
     return None, None
 
 
+# the kernel family each iteration phase launches (xfk_phase_profile names)
+PHASE_KERNELS = (("PCG update", ("k_cg_axpy",)), ("sweep", ("k_amg_smooth",)),
+                 ("restriction", ("k_csr_mv_tile", "k_csr_mv_g")), ("folded pre", ("k_fold_pre",)),
+                 ("dense inverse x b", ("k_dense_mv",)), ("L0 folded post", ("k_fold_post0",)),
+                 ("folded post", ("k_csr_mv_tile", "k_csr_mv_g")), ("prolongation", ("k_csr_mv_tile", "k_csr_mv_g")),
+                 ("PCG SpMV", ("k_cg_spmv",)))
+
+
+def _phase_rank(name):
+    """Launch order of an iteration phase: update, the V-cycle down (levels
+    ascending), the coarsest solve, back up (levels descending), SpMV."""
+    import re
+    if name.startswith("PCG update"):
+        return (0, 0)
+    if name.startswith("PCG SpMV"):
+        return (9, 0)
+    m = re.match(r"L(\d+) ", name)
+    lvl = int(m.group(1)) if m else 0
+    if "dense" in name:
+        return (2, 0)
+    if "post" in name or "prolongation" in name:
+        return (3, -lvl)
+    return (1, lvl)
+
+
+def annotate_phases(phases):
+    """Per-launch rocprof duration, HBM traffic and bound of the iteration
+    phases from the newest profiles/*_phase_pmc.json (tools/phase_pmc.py: one
+    PCG iteration of the same bench workload in launch order, from a kernel
+    trace and separate FETCH_SIZE / WRITE_SIZE passes).  A launch whose
+    traffic is below half its algorithmic bytes is cache/latency-bound (its
+    operands sit in L2 / MALL), not HBM-bound.  Returns the source file or None."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_phase_pmc.json")))
+    if not paths:
+        return None
+    with open(paths[-1]) as f:
+        seq = json.load(f).get("sequence", [])
+    its = sorted([p for p in phases if p.get("launches_per_iteration", 0) >= 0.5],
+                 key=lambda p: _phase_rank(p["phase"]))
+    if len(its) != len(seq):
+        return None
+    for ph, e in zip(its, seq):
+        fam = next((k for key, k in PHASE_KERNELS if key in ph["phase"]), ())
+        if not e["kernel"].startswith(fam):
+            return None
+    for ph, e in zip(its, seq):
+        ph["rocprof_us"] = e["rocprof_us"]
+        if ph.get("bytes_per_launch") and e.get("traffic_bytes") is not None:
+            ph["traffic_bytes"] = e["traffic_bytes"]
+            ph["traffic_over_algorithmic"] = e["traffic_bytes"] / ph["bytes_per_launch"]
+            ph["achieved_GBps_rocprof"] = ph["bytes_per_launch"] / (e["rocprof_us"] * 1e-6) / 1e9
+            ph["frac_rocprof"] = ph["achieved_GBps_rocprof"] / HBM_PEAK_GBS
+            ph["bound"] = "hbm" if e["traffic_bytes"] >= 0.5 * ph["bytes_per_launch"] else "cache/latency"
+    return os.path.relpath(paths[-1], ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -310,6 +367,7 @@ def main():
     # per-phase table (outside the timed region): the AMG setup steps and every
     # launch of one PCG iteration, HIP events on the solve stream
     phases = None
+    phases_src = None
     if amg and not sharded and world == 1 and not args.no_phases:
         iters = max(1, pcg_iters)
         phases = []
@@ -320,8 +378,9 @@ def main():
             if ph["bytes_per_call"] > 0:
                 gbs = ph["bytes_per_call"] / (ph["us_per_call"] * 1e-6) / 1e9
                 row.update({"bytes_per_launch": ph["bytes_per_call"], "achieved_GBps": gbs,
-                            "frac": gbs / HBM_PEAK_GBS, "bound": "hbm"})
+                            "frac": gbs / HBM_PEAK_GBS, "bound": "unmeasured"})
             phases.append(row)
+        phases_src = annotate_phases(phases)
 
     same_mesh = None
     if sharded and world > 1 and not args.no_same_mesh_1gpu:
@@ -400,9 +459,11 @@ def main():
         out["roofline"]["phases_note"] = (
             "xfk_phase_profile after the timed region: AMG setup rebuilt once, then %d PCG iterations; "
             "us per launch from HIP events; algorithmic bytes per launch (matrix stream 12 B/nnz + 4 B/row, each "
-            "vector once); peak %g GB/s; one PCG iteration = %.1f us of phases" % (
+            "vector once); peak %g GB/s; one PCG iteration = %.1f us of phases. rocprof_us, traffic_bytes and "
+            "bound: one iteration of the same workload from %s (tools/phase_pmc.py: kernel trace + FETCH_SIZE / "
+            "WRITE_SIZE passes; bound 'hbm' when traffic >= 0.5 x algorithmic bytes, else 'cache/latency')" % (
                 max(1, pcg_iters), HBM_PEAK_GBS,
-                sum(p["us_per_launch"] * p["launches_per_iteration"] for p in it_phases)))
+                sum(p["us_per_launch"] * p["launches_per_iteration"] for p in it_phases), phases_src))
     if same_mesh is not None:
         out["config"]["same_mesh_1gpu"] = same_mesh
     if rank == 0 and world == 1 and not sharded:

@@ -172,8 +172,11 @@ enum {
     XFK_OPT_AMG_REUSE = 6,      /* 1 (default): later Newton iterations of one solve keep the hierarchy
                                    and refresh only the fine-level smoother, rebuilt when the PCG needs
                                    2x the iterations of the last fresh build; 0: rebuild every time */
-    XFK_OPT_AMG_DENSE = 7       /* coarsening stops at a level of at most this many rows, which is
+    XFK_OPT_AMG_DENSE = 7,      /* coarsening stops at a level of at most this many rows, which is
                                    solved by its dense inverse (16..2048, default 2048) */
+    XFK_OPT_AMG_FOLD = 8        /* 1 (default, or XFK_AMG_FOLD from the environment): V(1,1) levels
+                                   run folded (one pass over P~ = (I - w D^-1 A) P for prolongation +
+                                   post-sweep, coarse pre-steps with R~ = P~^T); 0: the plain cycle */
 };
 int xfk_set_option(xfk_problem *prob, int option, double value);
 

@@ -245,3 +245,45 @@ def test_jacobi_weight_factor(omega):
     P.close()
     Ac = converged(pr, mesh)
     assert rel_err(A, Ac) <= TOL_LINEAR, parity_message(A, Ao, Ac, TOL_LINEAR)
+
+
+@pytest.mark.parametrize("cells,nonlinear", [(200, False), (60, True)])
+def test_folded_cycle_equals_plain_cycle(cells, nonlinear):
+    """The folded V(1,1) levels (XFK_OPT_AMG_FOLD, default on: one pass over
+    P~ = (I - w D^-1 A) P for prolongation + post-sweep, coarse pre-steps with
+    R~ = P~^T) equal the plain cycle in exact arithmetic.  Both answers meet
+    the parity tolerance against the converged oracle, agree with each other
+    to it, and take the same PCG iterations within one (roundoff only); the
+    nonlinear case also runs the Newton refresh of the hierarchy (which runs
+    level 0 unfolded, P~ belonging to the previous matrix)."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(cells, nonlinear=nonlinear))
+    Ao, _, _ = oracle.solve(pr, mesh)
+    tol = TOL_NONLINEAR if nonlinear else TOL_LINEAR
+    Af, rf, Ac = _solve_vs(kw, pr, mesh, precond="amg", amg_fold=True)
+    Ap, rp = _solve(kw, precond="amg", amg_fold=False)
+    assert rf["precond"] == rp["precond"] == kernels.XFK_PRECOND_AMG
+    assert rel_err(Af, Ac) <= tol, parity_message(Af, Ao, Ac, tol)
+    assert rel_err(Ap, Ac) <= tol, parity_message(Ap, Ao, Ac, tol)
+    assert rel_err(Af, Ap) <= tol
+    assert not np.array_equal(Af, Ap)                      # two different cycles really ran
+    if nonlinear:
+        assert rf["newton_iters"] == rp["newton_iters"] >= 3
+        assert abs(rf["cg_iters"] - rp["cg_iters"]) <= rf["newton_iters"]
+    else:
+        assert abs(rf["cg_iters"] - rp["cg_iters"]) <= 1, (rf["cg_iters"], rp["cg_iters"])
+
+
+def test_amg_is_deterministic_through_newton_refreshes():
+    """Repeated nonlinear solves (fresh builds + Newton refreshes of the
+    hierarchy, folded levels) give the same bits."""
+    kw = synth.magnetostatic(80, nonlinear=True)
+    P = kernels.Static2DProblem(**kw, precond="amg")
+    r1 = P.solve()
+    A1 = P.solution()
+    r2 = P.solve(rebuild_symbolic=True)
+    A2 = P.solution()
+    P.close()
+    A3, r3 = _solve(kw, precond="amg")
+    assert r1["newton_iters"] >= 3
+    assert r1["cg_iters"] == r2["cg_iters"] == r3["cg_iters"]
+    assert np.array_equal(A1, A2) and np.array_equal(A1, A3)

@@ -83,10 +83,6 @@ def test_harmonic_without_circuits_and_high_frequency():
 
 
 def test_harmonic_unsupported_cases_are_reported():
-    kw = synth.harmonic(10, periodic=True)
-    kw["circuits"][1] = dict(type=0, amps_re=1.0)       # Case 2 with periodic boundaries
-    with pytest.raises(kernels.XfkError, match="Case-2"):
-        kernels.Harmonic2DProblem(**kw)
     kw = synth.harmonic(10)
     kw["blocks"][1] = dict(kw["blocks"][1], LamType=1)
     with pytest.raises(kernels.XfkError, match="On-edge lamination"):
@@ -281,16 +277,19 @@ def test_harmonic_nonlinear_file_interface_end_to_end(tmp_path):
     assert rel_err(A, Ao) <= 1e-5
 
 
-@pytest.mark.parametrize("cells,nonlinear", [(20, False), (36, False), (16, True)])
-def test_harmonic_case2_circuit_matches_oracle(cells, nonlinear):
+@pytest.mark.parametrize("cells,nonlinear,periodic", [(20, False, False), (36, False, False), (16, True, False),
+                                                      (20, False, True), (30, False, "anti"), (16, True, True),
+                                                      (16, True, "anti")])
+def test_harmonic_case2_circuit_matches_oracle(cells, nonlinear, periodic):
     """Case-2 circuit (a specified total current in the conducting plate: its
     voltage gradient is an extra unknown, harmonic2d.cpp:441-472): the device
     solves the bordered system through its Schur complement; A and the
     circuit's voltage gradient against the oracle (which assembles the
     bordered system like the reference)."""
-    kw = synth.harmonic(cells, nonlinear=nonlinear)
+    kw = synth.harmonic(cells, nonlinear=nonlinear, periodic=bool(periodic), anti=periodic == "anti")
     kw["circuits"][1] = dict(type=0, amps_re=2.0, amps_im=0.5)
     pr, mesh, kk = _problem(kw)
+    assert len(mesh.pbc) == (cells + 1 if periodic else 0)
     Ao, st, circ_o = oh.solve(pr, mesh)
     assert circ_o[1][0] == 2
     P = kernels.Harmonic2DProblem(**kk)

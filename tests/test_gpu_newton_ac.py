@@ -40,8 +40,8 @@ def _case(kind, n):
         kw = synth.harmonic_axisymmetric(n, nonlinear=True)
     elif kind == "axi_ext":
         kw = synth.harmonic_axisymmetric(n, nonlinear=True, external=True)
-    elif kind == "periodic":
-        kw = synth.harmonic(n, nonlinear=True, periodic=True)
+    elif kind in ("periodic", "anti"):
+        kw = synth.harmonic(n, nonlinear=True, periodic=True, anti=kind == "anti")
     elif kind == "hf":
         kw = synth.harmonic(n, nonlinear=True, frequency=2000.0, circuits=False)
     else:
@@ -106,14 +106,14 @@ def test_newton_ac_file_interface_end_to_end(tmp_path):
     assert rel_err(A, Ac) <= TOL, parity_message(A, Ao, Ac, TOL)
 
 
-@pytest.mark.parametrize("n", [14, 20])
-def test_newton_ac_case2_matches_oracle(n):
+@pytest.mark.parametrize("n,kind", [(14, "planar"), (20, "planar"), (14, "periodic"), (16, "anti")])
+def test_newton_ac_case2_matches_oracle(n, kind):
     """Newton AC with a Case-2 circuit (specified current in a conducting
     region): KludgeSolve over the bordered system [V; u] (cspars.cpp:1000-1060
     on the full unknown vector).  The device's inner solves go through the
     Schur complement; the answer, the circuit voltage gradient and the
     circuit current match the oracle at the converged answer."""
-    kw = _case("planar", n)
+    kw = _case(kind, n)
     kw["circuits"][1] = dict(type=0, amps_re=2.0, amps_im=0.5)
     pr, mesh, kk = synth_to_oracle(kw)
     Ao, st, circ_o = oh.solve(pr, mesh)

@@ -206,3 +206,31 @@ def test_singular_matrix_is_reported():
     val = np.array([1.0, 0.0, 1.0])
     with pytest.raises(kernels.XfkError, match="singular"):
         kernels.pcg_solve_csr(rp, col, val, np.ones(n))
+
+
+def _many_boundary_properties(kw, n_extra=1500):
+    """The problem with n_extra unused boundary properties put in front of its
+    own, so the used ones carry indices > 1022 (the device's 10-bit edge
+    fields index the compacted table of the properties edges use)."""
+    kw = dict(kw)
+    pad = [dict(format=2, c0=float(k), c1=1.0) for k in range(n_extra)]
+    kw["lines"] = pad + list(kw["lines"])
+    e = np.asarray(kw["e"]).copy()
+    e[e >= 0] += n_extra
+    kw["e"] = e
+    return kw
+
+
+def test_more_than_1022_boundary_properties():
+    pr, mesh, kw = synth_to_oracle(_many_boundary_properties(synth.bc_showcase(24)))
+    assert len(pr.bdrys) > 1500 and mesh.e.max() > 1022
+    P = kernels.Static2DProblem(**kw)
+    P.solve()
+    A = P.solution()
+    G, bg = _gpu_system(P)
+    P.close()
+    O, bo = oracle.system(pr, mesh)
+    assert abs(G - O).max() <= TOL_SYSTEM * abs(O).max()
+    Ao, _, _ = oracle.solve(pr, mesh)
+    Ac = converged(pr, mesh)
+    assert rel_err(A, Ac) <= TOL_LINEAR, parity_message(A, Ao, Ac, TOL_LINEAR)

@@ -18,15 +18,15 @@ def _case(kind):
         return synth.harmonic(14)
     if kind == "periodic":
         return synth.harmonic(14, periodic=True)
-    if kind == "case2":
-        kw = synth.harmonic(14)
+    if kind in ("case2", "case2_periodic", "case2_anti"):
+        kw = synth.harmonic(14, periodic=kind != "case2", anti=kind == "case2_anti")
         kw["circuits"][1] = dict(type=0, amps_re=1.5, amps_im=-0.5)
         return kw
     return synth.harmonic(14, frequency=5000.0, circuits=False)
 
 
 @pytest.mark.skipif(not oracle.ref_available(), reason="reference build (oracle/_ref) absent")
-@pytest.mark.parametrize("kind", ["plain", "periodic", "case2", "hf"])
+@pytest.mark.parametrize("kind", ["plain", "periodic", "case2", "case2_periodic", "case2_anti", "hf"])
 def test_restated_complex_linprob_is_bit_identical_to_reference(kind):
     pr, mesh, _ = synth_to_oracle(_case(kind))
     A1, st1, c1 = oh.solve(pr, mesh, "oracle")
@@ -52,8 +52,10 @@ def _newton_case(kind):
         kw = synth.harmonic_axisymmetric(12, nonlinear=True)
     elif kind == "axi_ext":
         kw = synth.harmonic_axisymmetric(12, nonlinear=True, external=True)
-    elif kind == "periodic":
-        kw = synth.harmonic(14, nonlinear=True, periodic=True)
+    elif kind in ("periodic", "case2_periodic", "case2_anti"):
+        kw = synth.harmonic(14, nonlinear=True, periodic=True, anti=kind == "case2_anti")
+        if kind != "periodic":   # a Case-2 circuit together with (anti)periodic pairs (harmonic2d.cpp:157, 811-812)
+            kw["circuits"][1] = dict(type=0, amps_re=1.5, amps_im=-0.5)
     elif kind == "hf":
         kw = synth.harmonic(14, nonlinear=True, frequency=5000.0)
     elif kind == "stiff":   # KludgeSolve stagnates (line-search step -> 0): the reference's path, bit for bit
@@ -65,7 +67,8 @@ def _newton_case(kind):
 
 
 @pytest.mark.skipif(not oracle.ref_available(), reason="reference build (oracle/_ref) absent")
-@pytest.mark.parametrize("kind", ["planar", "periodic", "hf", "stiff", "axi", "axi_ext"])
+@pytest.mark.parametrize("kind", ["planar", "periodic", "case2_periodic", "case2_anti", "hf", "stiff", "axi",
+                                  "axi_ext"])
 def test_newton_ac_solver_is_bit_identical_to_reference(kind):
     """[ACSolver] = 1: the element Newton terms (harmonic2d.cpp:611-639 /
     harmonicaxi.cpp:520-547) into the auxiliary matrices and KludgeSolve

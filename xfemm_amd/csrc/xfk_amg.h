@@ -118,6 +118,7 @@ struct Amg {
     DBuf<double> absd, dfinv, wF, rho_part;
     DBuf<unsigned char> sflag;
     DBuf<unsigned> key, t1;           // MIS-2 keys (state:2 | priority:30)
+    DBuf<unsigned char> act;          // MIS-2: the row's strong neighbourhood still holds an undecided row
     DBuf<int> cnt, agg1, agg, flag, cursor;
     DBuf<int> ap_row, ap_col;
     DBuf<int> pad_col;                // single-pass SpGEMM: padded rows
@@ -140,6 +141,7 @@ struct Amg {
     bool dist = false;
     int rep_rows = 250000;
     int dense_max = kAmgDenseMax;     // coarsest level: dense inverse at <= dense_max rows
+    int fold_on = -1;                 // folded V(1,1) levels: 1 / 0, -1 = the XFK_AMG_FOLD default
     int lrep = 0;
     xfk_comm *comm = nullptr;
     int nranks = 1, rank = 0;

@@ -224,14 +224,17 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
 // also arms the round bookkeeping: "undecided" for the round before the
 // first, no round run yet
 __global__ void k_mis_init(int n, const int *__restrict__ sdeg, MisKey *__restrict__ key, int *und_prev,
-                           int *run)
+                           int *run, unsigned char *__restrict__ act)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) {
         *und_prev = 1;
         *run = 0;
     }
-    if (i < n) key[i] = mis_key(sdeg[i] > 0 ? kStUnd : (sdeg[i] < 0 ? kStIn : 0u), i);
+    if (i < n) {
+        key[i] = mis_key(sdeg[i] > 0 ? kStUnd : (sdeg[i] < 0 ? kStIn : 0u), i);
+        act[i] = 1;
+    }
 }
 
 // Rounds are launched in batches without a host check in between: the
@@ -239,11 +242,15 @@ __global__ void k_mis_init(int n, const int *__restrict__ sdeg, MisKey *__restri
 // result, cur = this round's), and once a round leaves nothing undecided the
 // later rounds of the batch exit at once (passing the 0 on).
 // G lanes per row (coarse levels, 10-16 entries per row; 1 on the fine level):
-// consecutive strong entries on consecutive lanes, the maximum by a butterfly
+// consecutive strong entries on consecutive lanes, the maximum by a butterfly.
+// A row whose strong neighbourhood holds no undecided row any more keeps its
+// maximum for good (decided rows never change): act[i] = 0 then, and later
+// rounds skip the row -- after the first rounds most of the level.
 template <int G>
 __global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
                           const unsigned char *__restrict__ sflag, const MisKey *__restrict__ in,
-                          MisKey *__restrict__ out, const int *prev, int *cur, int *run)
+                          MisKey *__restrict__ out, const int *prev, int *cur, int *run,
+                          unsigned char *__restrict__ act)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = t / G, g = t % G;
@@ -251,13 +258,24 @@ __global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__re
         if (*prev != 0) *run += 1;   // rounds that did work (the next setup's batch size)
         *cur = 0;
     }
-    if (i >= n || *prev == 0) return;
+    if (i >= n || *prev == 0 || act[i] == 0) return;
     MisKey m = in[i];
+    int any = key_st(m) == kStUnd;
     for (int k = rowptr[i] + g; k < rowptr[i + 1]; k += G)
-        if (sflag[k] == 1) m = max(m, in[col[k]]);
+        if (sflag[k] == 1) {
+            const MisKey v = in[col[k]];
+            m = max(m, v);
+            any |= key_st(v) == kStUnd;
+        }
 #pragma unroll
-    for (int off = 1; off < G; off <<= 1) m = max(m, (MisKey)__shfl_xor((int)m, off, G));
-    if (g == 0) out[i] = m;
+    for (int off = 1; off < G; off <<= 1) {
+        m = max(m, (MisKey)__shfl_xor((int)m, off, G));
+        any |= __shfl_xor(any, off, G);
+    }
+    if (g == 0) {
+        out[i] = m;
+        if (!any) act[i] = 0;
+    }
 }
 
 // second max sweep fused with the state update: an undecided node whose
@@ -2144,11 +2162,35 @@ int lanes_for(double per_row)
     return per_row <= 6.0 ? 4 : (per_row <= 20.0 ? 8 : 16);
 }
 
+// lab switch for the long-row transfer operators (R of level 0): 0 = tile of
+// 256 rows with 6 slots (48 KiB LDS), 1 = G lanes per row, 2 = tile of 128
+// rows with 6 slots (24 KiB), 3 = tile of 256 rows with 3 slots (24 KiB)
+static int rmv_mode()
+{
+    static const int v = [] {
+        const char *e = std::getenv("XFK_RMV");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
 void launch_mv(hipStream_t s, int n, const int *rowptr, const int *col, const double *val, const double *x, double *y,
                bool acc, int G, const int *done)
 {
     if (n <= 0) return;
-    if (n >= kTileMinRows && G <= 8) {
+    if (n >= kTileMinRows && G == 8 && rmv_mode() == 2) {
+        const int g = (n + 127) / 128;
+        if (acc) k_csr_mv_tile<128, true, 6><<<g, 128, 0, s>>>(n, rowptr, col, val, x, y, done);
+        else k_csr_mv_tile<128, false, 6><<<g, 128, 0, s>>>(n, rowptr, col, val, x, y, done);
+        return;
+    }
+    if (n >= kTileMinRows && G == 8 && rmv_mode() == 3) {
+        const int g = (n + 255) / 256;
+        if (acc) k_csr_mv_tile<256, true, 3><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+        else k_csr_mv_tile<256, false, 3><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+        return;
+    }
+    if (n >= kTileMinRows && G <= 8 && !(G == 8 && rmv_mode() == 1)) {
         // G = 8: 7..20 entries per row -> 6 slots per lane, one staging pass per tile
         const int g = (n + 255) / 256;
         if (G <= 4) {
@@ -2334,7 +2376,8 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     int rounds = 0;
     int *und2 = dev_int.p + 4;   // undecided flag of rounds of parity 0 / 1
     int *run = dev_int.p + 7;    // rounds that did work
-    k_mis_init<<<std::max(1, nb(n)), kB, 0, s>>>(n, cnt.p, key.p, und2 + 1, run);
+    AMG_CHECK(act.alloc(n));
+    k_mis_init<<<std::max(1, nb(n)), kB, 0, s>>>(n, cnt.p, key.p, und2 + 1, run, act.p);
     AMG_CHECK(flag.alloc((size_t)n + 1));
     AMG_CHECK(cursor.alloc((size_t)n + 1));
     // Batches of rounds without a host check; the first batch is the round
@@ -2347,10 +2390,11 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         for (int b = 0; b < batch; ++b, ++rounds) {
             int *cur = und2 + (rounds & 1), *prev = und2 + ((rounds + 1) & 1);
             if (A.nnz > 9LL * n) {
-                k_mis_max<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur, run);
+                k_mis_max<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur, run,
+                                                         act.p);
                 k_mis_update<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, prev, cur);
             } else {
-                k_mis_max<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur, run);
+                k_mis_max<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur, run, act.p);
                 k_mis_update<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, prev, cur);
             }
         }
@@ -2679,7 +2723,7 @@ int Amg::build(hipStream_t s, int l0)
         if (g_prof) g_prof->end();
         if (rc != XFK_OK) return rc;
         // folded level (l >= 1): P~ from A P before the next level reuses its buffers
-        A.fold = fold_levels() && sweeps == 1 && !A.dist;
+        A.fold = (fold_on < 0 ? fold_levels() : fold_on != 0) && sweeps == 1 && !A.dist;
         if (A.fold) {
             if (g_prof) g_prof->begin(lv + "folded transfer P~ = (I - w D^-1 A) P, R~ = P~^T", 0.0);
             A.fnnz = ap_nnz;   // an upper bound while the A P length is deferred

@@ -746,6 +746,7 @@ static int amg_setup(xfk_problem *P)
     P->amg->omega = P->amg_omega;
     P->amg->rep_rows = P->amg_replicate;
     P->amg->dense_max = P->amg_dense;
+    P->amg->fold_on = P->amg_fold;
     // setup time: an event pair per setup, read after the solve's final
     // synchronisation (no host check here); callers that never read them
     // recycle the pairs; a full pool (> 64 fresh builds in one solve) is
@@ -984,7 +985,6 @@ int validate_desc(const xfk_problem_desc *d)
     XFK_REQUIRE(d->n_circs == 0 || d->circs, XFK_ERR_ARG, "missing circuit table");
     XFK_REQUIRE(d->n_pbc == 0 || d->pbc, XFK_ERR_ARG, "missing pbc table");
     XFK_REQUIRE(d->n_ages >= 0 && (d->n_ages == 0 || d->ages), XFK_ERR_ARG, "missing air-gap element table");
-    XFK_REQUIRE(d->n_lines < 1023, XFK_ERR_UNSUPPORTED, "at most 1022 boundary properties");
     XFK_REQUIRE(d->length_units >= 0 && d->length_units < 6, XFK_ERR_ARG, "bad length units");
     XFK_REQUIRE(d->problem_type == XFK_PLANAR || d->problem_type == XFK_AXISYMMETRIC, XFK_ERR_ARG,
                 "problem type must be planar or axisymmetric");
@@ -1008,9 +1008,21 @@ int validate_desc(const xfk_problem_desc *d)
     if (d->marker)
         for (int i = 0; i < N; ++i)
             XFK_REQUIRE(d->marker[i] < d->n_points, XFK_ERR_ARG, "node point-property index out of range");
-    if (d->e)
-        for (long long i = 0; i < 3LL * NE; ++i)
+    if (d->e) {
+        // the device packs an element's three edge properties in 10-bit fields
+        // of the properties the mesh uses (prepare_global compacts the table):
+        // at most 1022 distinct ones on edges, any number defined
+        std::vector<char> used(std::max(1, d->n_lines), 0);
+        int nused = 0;
+        for (long long i = 0; i < 3LL * NE; ++i) {
             XFK_REQUIRE(d->e[i] < d->n_lines, XFK_ERR_ARG, "edge boundary-property index out of range");
+            if (d->e[i] >= 0 && !used[d->e[i]]) {
+                used[d->e[i]] = 1;
+                ++nused;
+            }
+        }
+        XFK_REQUIRE(nused <= 1022, XFK_ERR_UNSUPPORTED, "at most 1022 distinct boundary properties on element edges");
+    }
     return XFK_OK;
 }
 
@@ -1098,12 +1110,25 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
         G.lab[k].is_wound = l.is_wound;
         G.lab[k].external = l.is_external;
     }
-    G.lin.assign(std::max(1, d->n_lines), DevLine{});
-    for (int k = 0; k < d->n_lines; ++k) {
-        G.lin[k].c0 = d->lines[k].c0;
-        G.lin[k].c1 = d->lines[k].c1;
-        G.lin[k].format = d->lines[k].format;
-        G.lin[k].pad = 0;
+    // boundary properties used on element edges, compacted (the 10-bit edge
+    // fields index this table; validate_desc bounds its size)
+    G.lmap.assign(std::max(1, d->n_lines), -1);
+    G.lin_used.clear();
+    if (d->e)
+        for (long long i = 0; i < 3LL * NE; ++i) {
+            const int k = d->e[i];
+            if (k >= 0 && G.lmap[k] < 0) {
+                G.lmap[k] = (int)G.lin_used.size();
+                G.lin_used.push_back(k);
+            }
+        }
+    G.lin.assign(std::max<size_t>(1, G.lin_used.size()), DevLine{});
+    for (size_t m = 0; m < G.lin_used.size(); ++m) {
+        const xfk_line_desc &l = d->lines[G.lin_used[m]];
+        G.lin[m].c0 = l.c0;
+        G.lin[m].c1 = l.c1;
+        G.lin[m].format = l.format;
+        G.lin[m].pad = 0;
     }
     G.axi = d->problem_type == XFK_AXISYMMETRIC;
     G.ext_ro = d->ext_ro * units[d->length_units];   // staticaxi.cpp:70-72
@@ -1158,7 +1183,7 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
     for (int i = 0; i < NE; ++i)
         for (int j = 0; j < 3; ++j) {
             int ej = edge(3LL * i + j);
-            if (ej >= 0) G.ebits[i] |= (ej + 1) << (10 * j);
+            if (ej >= 0) G.ebits[i] |= (G.lmap[ej] + 1) << (10 * j);
         }
 
     // point currents and Dirichlet values in the reference's SetValue order
@@ -1732,6 +1757,10 @@ int xfk_set_option(xfk_problem *P, int option, double value)
                     "AMG dense coarsest size must be 16..2048 rows");
         P->amg_dense = (int)value;
         return XFK_OK;
+    case XFK_OPT_AMG_FOLD:
+        XFK_REQUIRE(value == 0 || value == 1, XFK_ERR_ARG, "AMG fold is 0 or 1");
+        P->amg_fold = (int)value;
+        return XFK_OK;
     default:
         set_error("unknown option");
         return XFK_ERR_ARG;
@@ -1871,6 +1900,44 @@ int xfk_pcg_time(xfk_problem *P, int iters, double *ms_spmv, double *ms_iter)
     ScopedEvents<2> ev;
     XFK_CHECK(ev.create());
     hipEvent_t t0 = ev[0], t1 = ev[1];
+    if (const char *ge = std::getenv("XFK_PCG_GRAPH")) {
+        // lab: the same iterations launched one by one vs replayed from a
+        // hipGraph of K captured iterations (no events inside); ms_spmv gets
+        // the stream time per iteration, ms_iter the graph time per iteration
+        const int K = std::max(2, std::atoi(ge) & ~1);
+        for (int k = 0; k < 2; ++k)
+            if ((rc = pcg_iteration(P, k, false)) != XFK_OK) return rc;
+        XFK_CHECK(hipEventRecord(t0, s));
+        for (int k = 2; k < 2 + iters; ++k)
+            if ((rc = pcg_iteration(P, k, false)) != XFK_OK) return rc;
+        XFK_CHECK(hipEventRecord(t1, s));
+        XFK_CHECK(hipEventSynchronize(t1));
+        float ts = 0;
+        XFK_CHECK(hipEventElapsedTime(&ts, t0, t1));
+        hipGraph_t g = nullptr;
+        hipGraphExec_t ge2 = nullptr;
+        XFK_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        for (int k = 2; k < 2 + K; ++k)
+            if ((rc = pcg_iteration(P, k, false)) != XFK_OK) {
+                (void)hipStreamEndCapture(s, &g);
+                return rc;
+            }
+        XFK_CHECK(hipStreamEndCapture(s, &g));
+        XFK_CHECK(hipGraphInstantiate(&ge2, g, nullptr, nullptr, 0));
+        XFK_CHECK(hipGraphLaunch(ge2, s));   // warm
+        const int R = std::max(1, iters / K);
+        XFK_CHECK(hipEventRecord(t0, s));
+        for (int q = 0; q < R; ++q) XFK_CHECK(hipGraphLaunch(ge2, s));
+        XFK_CHECK(hipEventRecord(t1, s));
+        XFK_CHECK(hipEventSynchronize(t1));
+        float tg = 0;
+        XFK_CHECK(hipEventElapsedTime(&tg, t0, t1));
+        (void)hipGraphExecDestroy(ge2);
+        (void)hipGraphDestroy(g);
+        if (ms_spmv) *ms_spmv = ts / iters;
+        if (ms_iter) *ms_iter = tg / (R * K);
+        return XFK_OK;
+    }
     P->spmv_used = 0;
     XFK_CHECK(hipEventRecord(t0, s));
     for (int k = 0; k < iters; ++k) {

@@ -1264,9 +1264,10 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
         bhH.push_back(cx(0, 0));
         bhS.push_back(cx(0, 0));
     }
-    std::vector<DevLineAC> lin(std::max(1, d->n_lines));
-    for (int k = 0; k < d->n_lines; ++k) {
-        DevLineAC &o = lin[k];
+    std::vector<DevLineAC> lin(std::max<size_t>(1, G.lin_used.size()));   // compact, as the edge fields
+    for (size_t m = 0; m < G.lin_used.size(); ++m) {
+        const int k = G.lin_used[m];
+        DevLineAC &o = lin[m];
         const xfk_line_desc &l = d->lines[k];
         o.format = l.format;
         o.c0 = cx(l.c0, ac->lines[k].c0_im);
@@ -1308,9 +1309,6 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
             C.dV = cx(0, 0);
             if (d->circs[k].type == 0) {
                 if (I2[k] != 0.0) {   // Case 2: the voltage gradient is an extra unknown
-                    XFK_REQUIRE(d->n_pbc == 0, XFK_ERR_UNSUPPORTED,
-                                "Case-2 circuits (specified current in a conducting region) together with "
-                                "periodic boundaries are not supported by this build");
                     C.ccase = 2;
                     continue;
                 }
@@ -1442,6 +1440,30 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
                     cr[i] = 0;
                     ci[i] = 0;
                 }
+            // then the periodic / antiperiodic pairs, in pbclist order: their
+            // loops over the rows of the whole bordered matrix reach the
+            // circuit's row too (cspars.cpp:677-716 Periodicity, 592-640
+            // AntiPeriodicity: rows k >= NumNodes after the band), averaging
+            // the border column at the pair's two nodes; D_k and f_k stay
+            for (int k2 = 0; k2 < d->n_pbc; ++k2) {
+                int i = d->pbc[3 * k2], j = d->pbc[3 * k2 + 1];
+                const int t = d->pbc[3 * k2 + 2];
+                if (t != 0 && t != 1) continue;
+                if (j < i) std::swap(i, j);
+                const double2 v1 = cx(cr[i], ci[i]), v2 = cx(cr[j], ci[j]);
+                if (v1.x == 0 && v1.y == 0 && v2.x == 0 && v2.y == 0) continue;
+                if (t == 0) {
+                    const double2 h = cx((v1.x + v2.x) / 2., (v1.y + v2.y) / 2.);
+                    cr[i] = cr[j] = h.x;
+                    ci[i] = ci[j] = h.y;
+                } else {
+                    const double2 h = cx((v1.x - v2.x) / 2., (v1.y - v2.y) / 2.);
+                    cr[i] = h.x;
+                    ci[i] = h.y;
+                    cr[j] = -h.x;
+                    ci[j] = -h.y;
+                }
+            }
         }
     }
 

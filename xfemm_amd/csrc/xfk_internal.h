@@ -369,6 +369,7 @@ struct xfk_problem {
     double amg_omega = 1.75;
     int amg_replicate = 250000;
     int amg_dense = 2048;
+    int amg_fold = -1;                // XFK_OPT_AMG_FOLD (-1: the XFK_AMG_FOLD environment default)
     int amg_reuse = 1;
     bool amg_reusable = false;        // the hierarchy belongs to this solve's matrix pattern
     bool amg_fresh = false;           // built from scratch for the running PCG solve
@@ -481,7 +482,8 @@ struct GlobalPrep {
     std::vector<double> hB, hH, hS;
     std::vector<DevLabel> lab;           // labels, then one per element of a MagDirFctn label
     std::vector<int> elab;               // per element: index into lab (empty: the mesh's lbl)
-    std::vector<DevLine> lin;
+    std::vector<DevLine> lin;            // boundary properties used on edges, compacted
+    std::vector<int> lmap, lin_used;     // property -> compact index (-1: unused); compact -> property
     std::vector<DevCirc> circ;
     std::vector<int> ebits;              // per element: 3 x 10-bit boundary-prop index + 1
     std::vector<int> pt_nodes;           // nodes with a point current, ascending

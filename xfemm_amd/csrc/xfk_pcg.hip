@@ -1,10 +1,11 @@
-// Preconditioned conjugate gradient of the fsolver hot path, two launches per
-// iteration.
+// Preconditioned conjugate gradient of the fsolver hot path: two launches per
+// iteration with the Jacobi preconditioner, update + V-cycle + SpMV with the
+// default smoothed-aggregation AMG (xfk_amg.hip).
 //
 // Reference: CBigLinProb::PCGSolve (cfemm/libfemm/spars.cpp:238-316) -- same
 // PCG, same stopping test sqrt(z.r / z0.b) <= Precision, same initial guess
-// semantics (flag), Jacobi preconditioner M = diag(A) instead of the
-// reference's sequential SSOR sweep.
+// semantics (flag); the preconditioner M is the AMG V-cycle (default) or
+// diag(A) (Jacobi) instead of the reference's sequential SSOR sweep.
 //
 // Formulation: the Chronopoulos-Gear arrangement of PCG, in which both inner
 // products of an iteration (gamma = r.u, delta = w.u with u = M^-1 r, w = A u)

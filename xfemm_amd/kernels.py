@@ -32,6 +32,7 @@ XFK_OPT_AMG_OMEGA = 4
 XFK_OPT_AMG_REPLICATE = 5
 XFK_OPT_AMG_REUSE = 6
 XFK_OPT_AMG_DENSE = 7
+XFK_OPT_AMG_FOLD = 8
 
 # every symbol include/xfemm_kernels.h declares
 EXPORTED = (
@@ -315,8 +316,9 @@ class Static2DProblem:
                  amg_theta: Optional[float] = None, frequency: float = 0.0, amg_omega: Optional[float] = None,
                  amg_replicate: Optional[int] = None, amg_reuse: Optional[bool] = None, problem_type: int = 0,
                  ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0, amg_dense: Optional[int] = None,
-                 ages: Sequence[dict] = (), ac_solver: int = 0):
+                 ages: Sequence[dict] = (), ac_solver: int = 0, amg_fold: Optional[bool] = None):
         """ac_solver: [ACSolver], read by the harmonic solvers only (ignored here).
+        amg_fold: folded V(1,1) levels (default on; False: the plain cycle).
         comm: shard the mesh by row blocks over this communicator (every rank
         passes the same global problem; solve() and solution() are collective).
         precond: "amg" (smoothed-aggregation V-cycle, default) or "jacobi".
@@ -351,6 +353,8 @@ class Static2DProblem:
             self.set_option(XFK_OPT_AMG_REUSE, int(bool(amg_reuse)))
         if amg_dense is not None:
             self.set_option(XFK_OPT_AMG_DENSE, amg_dense)
+        if amg_fold is not None:
+            self.set_option(XFK_OPT_AMG_FOLD, int(bool(amg_fold)))
         self.n_rows = self.dist_info()["n_own"] if comm is not None else self.n_nodes
         self.result: Optional[Result] = None
 

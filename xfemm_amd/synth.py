@@ -410,7 +410,7 @@ def bc_chain(n: int, L: float = 10.0):
 
 
 def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float = 1e-8, periodic: bool = False,
-             circuits: bool = True, nonlinear: bool = False, prox: Optional[int] = None):
+             circuits: bool = True, nonlinear: bool = False, prox: Optional[int] = None, anti: bool = False):
     """Keyword arguments of a linear time-harmonic planar problem
     (FSolver::Harmonic2D, cfemm/fsolver/harmonic2d.cpp) on the magnetostatic
     square: laminated lossy steel (lamination thickness with conductivity,
@@ -425,7 +425,8 @@ def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float 
     starts the reference's successive approximation.  `prox` (wiretype 0-3:
     magnet, stranded, litz, rectangular wire): the coil- region becomes a
     wound copper winding of LamType 3 + prox with AC proximity effects
-    (FSolver::GetFillFactor's ProximityMu, harmonic2d.cpp:664-668)."""
+    (FSolver::GetFillFactor's ProximityMu, harmonic2d.cpp:664-668).  `anti`:
+    the bottom/top pairs are antiperiodic (BdryFormat 5) instead."""
     kw = magnetostatic(n, L=L, precision=precision)
     x, y, p = kw["x"], kw["y"], kw["p"]
     tol = 1e-9 * L
@@ -446,7 +447,7 @@ def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float 
     kw["lines"] = [dict(format=0, A0=1e-3, A1=2e-4, A2=0.0, phi=30.0),
                    dict(format=2, c0=3.0, c0_im=1.0, c1=0.5, c1_im=-0.2),
                    dict(format=1, Mu=1.0, Sig=5.8),
-                   dict(format=4)]
+                   dict(format=5 if anti else 4)]
     kw["blocks"] = [
         dict(mu_x=1.0, mu_y=1.0),                                                    # air
         dict(mu_x=800.0, mu_y=800.0, Lam_d=0.35, LamFill=0.96, Cduct=2.0,             # laminated lossy steel
@@ -487,7 +488,7 @@ def harmonic(n: int, L: float = 10.0, frequency: float = 60.0, precision: float 
     if periodic:
         bottom = np.arange(m)
         top = (m - 1) * m + np.arange(m)
-        kw["pbc"] = np.stack([bottom, top, np.zeros(m)], 1).astype(np.int32)
+        kw["pbc"] = np.stack([bottom, top, np.full(m, 1 if anti else 0)], 1).astype(np.int32)
     return kw
 
 
