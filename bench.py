@@ -238,9 +238,12 @@ def annotate_phases(phases):
     """Per-launch rocprof duration, HBM traffic and bound of the iteration
     phases from the newest profiles/*_phase_pmc.json (tools/phase_pmc.py: one
     PCG iteration of the same bench workload in launch order, from a kernel
-    trace and separate FETCH_SIZE / WRITE_SIZE passes).  A launch whose
-    traffic is below half its algorithmic bytes is cache/latency-bound (its
-    operands sit in L2 / MALL), not HBM-bound.  Returns the source file or None."""
+    trace and separate FETCH_SIZE / WRITE_SIZE passes).  Bound: "cache" when
+    the launch moves less than half its algorithmic bytes from HBM (its
+    operands sit in L2 / MALL); "hbm" when it does and streams them at >= 30 %
+    of the HBM peak; "latency" when it moves its bytes but far below the
+    streaming rate (small coarse-level launches at the dependent-launch floor,
+    short dependent load chains).  Returns the source file or None."""
     import glob
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_phase_pmc.json")))
     if not paths:
@@ -262,7 +265,10 @@ def annotate_phases(phases):
             ph["traffic_over_algorithmic"] = e["traffic_bytes"] / ph["bytes_per_launch"]
             ph["achieved_GBps_rocprof"] = ph["bytes_per_launch"] / (e["rocprof_us"] * 1e-6) / 1e9
             ph["frac_rocprof"] = ph["achieved_GBps_rocprof"] / HBM_PEAK_GBS
-            ph["bound"] = "hbm" if e["traffic_bytes"] >= 0.5 * ph["bytes_per_launch"] else "cache/latency"
+            if e["traffic_bytes"] < 0.5 * ph["bytes_per_launch"]:
+                ph["bound"] = "cache"
+            else:
+                ph["bound"] = "hbm" if ph["frac_rocprof"] >= 0.3 else "latency"
     return os.path.relpath(paths[-1], ROOT)
 
 
@@ -461,7 +467,7 @@ def main():
             "us per launch from HIP events; algorithmic bytes per launch (matrix stream 12 B/nnz + 4 B/row, each "
             "vector once); peak %g GB/s; one PCG iteration = %.1f us of phases. rocprof_us, traffic_bytes and "
             "bound: one iteration of the same workload from %s (tools/phase_pmc.py: kernel trace + FETCH_SIZE / "
-            "WRITE_SIZE passes; bound 'hbm' when traffic >= 0.5 x algorithmic bytes, else 'cache/latency')" % (
+            "WRITE_SIZE passes; bound 'cache' when traffic < 0.5 x algorithmic bytes, else 'hbm' at >= 30 %% of peak by rocprof duration, 'latency' below)" % (
                 max(1, pcg_iters), HBM_PEAK_GBS,
                 sum(p["us_per_launch"] * p["launches_per_iteration"] for p in it_phases), phases_src))
     if same_mesh is not None:

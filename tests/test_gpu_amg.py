@@ -159,8 +159,8 @@ def test_standalone_amg_pcg(n):
     Vd = sla.spsolve(M.tocsc(), b)
     assert er <= 1e-12
     assert rel_err(V, Vd) <= 1e-8
-    if n == 8:   # 64 rows: the whole matrix is the dense coarsest level -> exact in one step
-        assert it <= 2
+    if n == 8:   # 64 rows: the whole matrix is the dense coarsest level (applied in f32)
+        assert it <= 3
 
 
 @pytest.mark.parametrize("n,nd", [(20, True), (30, True), (45, True), (45, False)])
@@ -169,14 +169,16 @@ def test_dense_coarsest_blocked_inverse(monkeypatch, n, nd):
     by blocked Gauss-Jordan (several 64-wide block columns, ragged last block):
     PCG converges in one step to the direct solution.  From 512 rows on the
     level is reordered by nested dissection (two parts eliminated side by
-    side, then the separator); XFK_NO_ND=1 keeps the plain order."""
+    side, then the separator); XFK_NO_ND=1 keeps the plain order.  The
+    V-cycle applies the inverse rounded to f32, so each PCG step contracts the
+    error by ~1e-7: three steps reach 1e-12."""
     if not nd:
         monkeypatch.setenv("XFK_NO_ND", "1")
     M = _laplace_random(n, 7)
     b = np.random.default_rng(2).standard_normal(M.shape[0])
     V, it, er = kernels.pcg_solve_csr(M.indptr, M.indices, M.data, b, precision=1e-12, precond="amg")
     Vd = sla.spsolve(M.tocsc(), b)
-    assert it <= 2
+    assert it <= 3
     assert rel_err(V, Vd) <= 1e-10
 
 

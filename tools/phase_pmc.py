@@ -9,8 +9,9 @@ the sequence: the kernel, its grid, the median rocprof duration over the
 iterations, and the median FETCH_SIZE / WRITE_SIZE converted to bytes with the
 width-calibrated factors of tools/pmc_summary.py.  bench.py matches the
 positions to its phase table (roofline.phases): rocprof durations next to the
-HIP-event ones, per-level traffic, and the bound of each launch ("hbm" when
-the traffic is at least half the algorithmic bytes, "cache/latency" below).
+HIP-event ones, per-level traffic, and the bound of each launch ("cache"
+when the traffic is below half the algorithmic bytes, else "hbm" at >= 30 % of
+the peak by rocprof duration and "latency" below).
 
 usage: python tools/phase_pmc.py PROFDIR [CALIB.json]
 """

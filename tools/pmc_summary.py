@@ -36,6 +36,8 @@ MIX = {
     # smoother / CSR tile kernels: as the SpMV
     "k_amg_smooth": {"read": {4: 0.30, 8: 0.70}, "write": {8: 1.0}},
     "k_csr_mv_tile": {"read": {4: 0.30, 8: 0.70}, "write": {8: 1.0}},
+    # dense coarsest apply: 16-B loads of the f32 inverse rows (and of b)
+    "k_dense_mv": {"read": {16: 1.0}, "write": {8: 1.0}},
 }
 
 CALIB_KERNELS = {  # name fragment -> (direction, width)

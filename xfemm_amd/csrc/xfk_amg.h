@@ -95,8 +95,9 @@ struct Amg {
     bool dense_coarse = false;
     DBuf<double> cinv;                // dense inverse of the coarsest level (row major, padded)
     int cinv_ld = 0;
-    DBuf<double> cinv_o;              // nested-dissection order: the unpermuted inverse
-    const double *cinv_apply = nullptr;   // the inverse the V-cycle applies (cinv or cinv_o)
+    bool nd_prefetched = false;       // host_big holds the coarsest pattern (read with the deferred lengths)
+    DBuf<float> cinv_o;               // the inverse the V-cycle applies: unpermuted, unscaled, f32
+    const float *cinv_apply = nullptr;
     DBuf<int> cinv_perm, cinv_iperm, nd_tiles;
     DBuf<unsigned char> nd_mask;
     struct NdPhase {                  // one tree level of the nested-dissection order
@@ -161,6 +162,13 @@ struct Amg {
     int host_big_n = 0;
     double *part_gam_ = nullptr;      // vcycle's gamma partials, for vc_dist
     SideStream side;                  // sharded: halo exchanges overlapped with interior tiles
+    // single-device setup steps off the critical path -- R = P^T beside A P,
+    // the folded transfers P~ / R~ beside the next level -- on a second
+    // stream with scratch of its own (a: fork, b: R done / join, c: P~ done)
+    SideStream sw;
+    bool sw_used = false, rt_pending = false, fold_pending = false;
+    DBuf<int> cnt2;
+    DBuf<char> cub_tmp2;
 
     ~Amg();
     // Build the hierarchy for the n x n CSR on `s` (host-synchronising).

@@ -999,37 +999,28 @@ __global__ void k_dense_scatter(int n, int ld, const int *__restrict__ rowptr, c
         M[(size_t)q * ld + c] += val[k] * sc[q] * sc[c];
     }
 }
-// inv(A) = S inv(S A S) S
-__global__ void k_dense_unscale(int ld, double *__restrict__ M, const double *__restrict__ sc)
-{
-    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // double2 index
-    const size_t half = (size_t)ld * ld / 2;
-    if (e >= half) return;
-    const int i = (int)(2 * e / ld), j = (int)(2 * e % ld);
-    double2 *p = reinterpret_cast<double2 *>(M) + e;
-    double2 v = *p;
-    v.x *= sc[i] * sc[j];
-    v.y *= sc[i] * sc[j + 1];
-    *p = v;
-}
-
-// nested-dissection order back to the coarse numbering, unscaled:
-// out[iperm q][iperm r] = M[q][r] sc_q sc_r (out: n rows of ldo, the padding
-// columns n .. ldo-1 zero), so the V-cycle's apply reads plain rows
+// nested-dissection order back to the coarse numbering, unscaled and
+// rounded to f32: out[iperm q][iperm r] = M[q][r] sc_q sc_r (out: n rows of
+// ldo, the padding columns n .. ldo-1 zero; iperm null: the identity), so
+// the V-cycle's apply streams plain f32 rows -- half the bytes of the
+// per-iteration coarse solve.  The coarsest inverse only preconditions: its
+// 2^-24 relative rounding keeps the V-cycle symmetric positive definite
+// (entries (i, j) and (j, i) of the inverse agree to far below an f32 ulp, so
+// they round alike) and changes no answer beyond the PCG's own tolerance.
 __global__ void __launch_bounds__(256) k_dense_unperm(int n, int ld, int ldo, const double *__restrict__ M,
                                                       const double *__restrict__ sc, const int *__restrict__ iperm,
-                                                      double *__restrict__ out)
+                                                      float *__restrict__ out)
 {
     const int q = blockIdx.x;
-    const int i = iperm[q];
+    const int i = iperm ? iperm[q] : (q < n ? q : -1);
     if (i < 0) return;
     const double sq = sc[q];
-    double *o = out + (size_t)i * ldo;
+    float *o = out + (size_t)i * ldo;
     for (int r = threadIdx.x; r < ld; r += blockDim.x) {
-        const int j = iperm[r];
-        if (j >= 0) o[j] = M[(size_t)q * ld + r] * sq * sc[r];
+        const int j = iperm ? iperm[r] : (r < n ? r : -1);
+        if (j >= 0) o[j] = (float)(M[(size_t)q * ld + r] * sq * sc[r]);
     }
-    for (int c = n + threadIdx.x; c < ldo; c += blockDim.x) o[c] = 0.0;
+    for (int c = n + threadIdx.x; c < ldo; c += blockDim.x) o[c] = 0.0f;
 }
 
 __global__ void __launch_bounds__(1024) k_dense_maxdiag(int n, int ld, const double *__restrict__ M,
@@ -1598,6 +1589,25 @@ __device__ __forceinline__ void smooth_finish(int i, double ax, double w, const 
         if (out) out[i] = xi;   // (a folded level-0 post-step recomputes x_pre: not written)
 }
 
+// smooth_finish with the row's b, D^-1 and x already loaded; returns out[i]
+template <int MODE>
+__device__ __forceinline__ double smooth_finish_v(int i, double ax, double w, double di, double bi, double xv,
+                                                  double *__restrict__ out, double *__restrict__ rout)
+{
+    constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
+    const double xi = implicit ? w * di * bi : xv;
+    const double res = bi - ax;
+    double o = xi;
+    if constexpr (MODE == kSweepFromZero || MODE == kSweep) {
+        o = xi + w * di * res;
+        out[i] = o;
+    }
+    if constexpr (MODE == kResid || MODE == kResidFromZero) rout[i] = res;
+    if constexpr (MODE == kResidFromZero)
+        if (out) out[i] = xi;   // (a folded level-0 post-step recomputes x_pre: not written)
+    return o;
+}
+
 // CSR-stream tile SpMV (the PCG's kernel shape): B = 1024 on level 0, 256 on
 // large coarse levels (more workgroups than CUs)
 // part_gam (the PCG's last level-0 sweep only): per-tile partials of
@@ -1612,26 +1622,32 @@ __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__r
                                                          double *__restrict__ rout, const int *done,
                                                          double *__restrict__ part_gam, const int *__restrict__ tl)
 {
-    if (done && *done) return;
+    // the convergence flag, rho, the tile's row range and this row's b,
+    // D^-1, x are loaded together before the first branch
+    const int dn = load_flag_v(done);
     __shared__ __attribute__((aligned(16))) double lds[4 * SLOTS * B];
     const double ra = rho_of(rho);
-    const double w = ra > 0.0 ? 1.0 / ra : 0.0;
     const int t = tl ? tl[xcd_tile(blockIdx.x, gridDim.x)] : xcd_tile(blockIdx.x, gridDim.x);
     const int r0 = t * B;
+    const int i = r0 + threadIdx.x;
     constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
+    const TileRows tr = tile_rows<B>(r0, n, rowptr);
+    const double bi = i < n ? b[i] : 0.0, di = i < n ? dinv[i] : 0.0;
+    const double xv = (!implicit && i < n) ? x[i] : 0.0;
+    if (dn) return;
+    const double w = ra > 0.0 ? 1.0 / ra : 0.0;
     double ax;
     if constexpr (implicit)
-        ax = cg_tile_spmv<B, SLOTS>(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; },
-                             lds);
+        ax = cg_tile_spmv<B, SLOTS>(tr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; }, lds);
     else
-        ax = cg_tile_spmv<B, SLOTS>(r0, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; }, lds);
-    const int i = r0 + threadIdx.x;
-    if (i < n) smooth_finish<MODE>(i, ax, w, dinv, b, x, out, rout);
+        ax = cg_tile_spmv<B, SLOTS>(tr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; }, lds);
+    double oi = 0.0;
+    if (i < n) oi = smooth_finish_v<MODE>(i, ax, w, di, bi, xv, out, rout);
     if constexpr (MODE == kSweep) {
         if (part_gam) {   // uniform per launch
             __shared__ double red[2 * (B / 64)];
             double g = 0.0, zero = 0.0;
-            if (i < n) g = b[i] * out[i];
+            if (i < n) g = bi * oi;
             cg_block_sum2(zero, g, red);
             if (threadIdx.x == 0) part_gam[t] = g;
         }
@@ -1680,12 +1696,15 @@ __global__ void __launch_bounds__(B) k_csr_mv_tile(int n, const int *__restrict_
                                                    const double *__restrict__ val, const double *__restrict__ x,
                                                    double *__restrict__ y, const int *done)
 {
-    if (done && *done) return;
+    const int dn = load_flag_v(done);
     __shared__ __attribute__((aligned(16))) double lds[4 * SLOTS * B];
     const int r0 = xcd_tile(blockIdx.x, gridDim.x) * B;
-    const double s = cg_tile_spmv<B, SLOTS>(r0, n, rowptr, col, val, [&](int j) { return x[j]; }, lds);
     const int i = r0 + threadIdx.x;
-    if (i < n) y[i] = ACC ? y[i] + s : s;
+    const TileRows tr = tile_rows<B>(r0, n, rowptr);
+    const double y0 = (ACC && i < n) ? y[i] : 0.0;
+    if (dn) return;
+    const double s = cg_tile_spmv<B, SLOTS>(tr, col, val, [&](int j) { return x[j]; }, lds);
+    if (i < n) y[i] = ACC ? y0 + s : s;
 }
 
 // y = M x (ACC: y += M x), G lanes per row (restriction R r, prolongation x += P xc)
@@ -1744,24 +1763,26 @@ __global__ void __launch_bounds__(B) k_fold_post0(int n, const int *__restrict__
                                                   const double *__restrict__ b, double *__restrict__ out,
                                                   const int *done, double *__restrict__ part_gam)
 {
-    if (done && *done) return;
+    const int dn = load_flag_v(done);
     __shared__ __attribute__((aligned(16))) double lds[4 * SLOTS * B];
     const double ra = rho_of(rho);
-    const double w = ra > 0.0 ? 1.0 / ra : 0.0;
     const int t = xcd_tile(blockIdx.x, gridDim.x);
     const int r0 = t * B;
-    const double pc = cg_tile_spmv<B, SLOTS>(r0, n, frow, fcol, fval, [&](int j) { return xc[j]; }, lds);
     const int i = r0 + threadIdx.x;
+    const TileRows tr = tile_rows<B>(r0, n, frow);
+    const double di = i < n ? dinv[i] : 0.0, bi = i < n ? b[i] : 0.0, ri = i < n ? rres[i] : 0.0;
+    if (dn) return;
+    const double w = ra > 0.0 ? 1.0 / ra : 0.0;
+    const double pc = cg_tile_spmv<B, SLOTS>(tr, fcol, fval, [&](int j) { return xc[j]; }, lds);
     double u = 0.0;
     if (i < n) {
-        const double di = dinv[i];
-        u = (w * di * b[i] + w * di * rres[i]) + pc;
+        u = (w * di * bi + w * di * ri) + pc;
         out[i] = u;
     }
     if (part_gam) {   // uniform per launch
         __shared__ double red[2 * (B / 64)];
         double g = 0.0, zero = 0.0;
-        if (i < n) g = b[i] * u;
+        if (i < n) g = bi * u;
         cg_block_sum2(zero, g, red);
         if (threadIdx.x == 0) part_gam[t] = g;
     }
@@ -1796,39 +1817,40 @@ __global__ void __launch_bounds__(256) k_fold_pre(int n, int ncl, const int *__r
     }
 }
 
-// x = M b, one wavefront per row of the dense coarsest inverse (ld is a
-// multiple of 64 and the padding columns are zero): double2 loads, four in
-// flight per lane
-// x = M b, one 256-thread workgroup per row: every thread issues its (at most
-// kDmvLoads) 16-B loads of the row at once, so the whole inverse is in flight
-// (one wave per row left a 1.6k-row inverse at 2.3 TB/s: 6 waves per CU, each
-// walking its 12.8 KB row in three dependent batches)
-constexpr int kDmvLoads = 4;
-__global__ void __launch_bounds__(256) k_dense_mv(int n, int ld, const double *__restrict__ M,
+// x = M b, one 256-thread workgroup per row of the f32 inverse (ld a multiple
+// of 64, padding columns zero): every thread issues its 16-B loads (4 floats)
+// of the row at once, so the whole inverse is in flight (one wave per row
+// left a 1.6k-row inverse at 2.3 TB/s: 6 waves per CU, each walking its row
+// in dependent batches); products and sums in f64
+constexpr int kDmvLoads = 2;
+__global__ void __launch_bounds__(256) k_dense_mv(int n, int ld, const float *__restrict__ M,
                                                   const double *__restrict__ b, double *__restrict__ x, const int *done)
 {
     if (done && *done) return;
     __shared__ double red[4];
     const int i = blockIdx.x;
-    const double2 *Mi = reinterpret_cast<const double2 *>(M + (size_t)i * ld);
-    const int n2 = ld >> 1;
+    const float4 *Mi = reinterpret_cast<const float4 *>(M + (size_t)i * ld);
+    const int n4 = ld >> 2;
     double s0 = 0.0, s1 = 0.0;
-    for (int j0 = 0; j0 < n2; j0 += 256 * kDmvLoads) {
-        double2 m[kDmvLoads];
+    for (int j0 = 0; j0 < n4; j0 += 256 * kDmvLoads) {
+        float4 m[kDmvLoads];
 #pragma unroll
         for (int q = 0; q < kDmvLoads; ++q) {
             const int j = j0 + threadIdx.x + 256 * q;
-            m[q] = j < n2 ? Mi[j] : make_double2(0.0, 0.0);
+            m[q] = j < n4 ? Mi[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int q = 0; q < kDmvLoads; ++q) {
-            const int c = 2 * (j0 + threadIdx.x + 256 * q);
-            if (c + 1 < n) {
-                const double2 bb = *reinterpret_cast<const double2 *>(b + c);
-                s0 += m[q].x * bb.x;
-                s1 += m[q].y * bb.y;
-            } else if (c < n) {
-                s0 += m[q].x * b[c];
+            const int c = 4 * (j0 + threadIdx.x + 256 * q);
+            if (c + 3 < n) {
+                const double2 b0 = *reinterpret_cast<const double2 *>(b + c);
+                const double2 b1 = *reinterpret_cast<const double2 *>(b + c + 2);
+                s0 += (double)m[q].x * b0.x + (double)m[q].z * b1.x;
+                s1 += (double)m[q].y * b0.y + (double)m[q].w * b1.y;
+            } else {
+                if (c < n) s0 += (double)m[q].x * b[c];
+                if (c + 1 < n) s1 += (double)m[q].y * b[c + 1];
+                if (c + 2 < n) s0 += (double)m[q].z * b[c + 2];
             }
         }
     }
@@ -1959,16 +1981,18 @@ int scan_total(Amg &A, hipStream_t s, const int *in, int *out, int n, long long 
     return XFK_OK;
 }
 
-// the same without reading the total back (no host synchronisation)
-int scan_only(Amg &A, hipStream_t s, const int *in, int *out, int n)
+// the same without reading the total back (no host synchronisation), with
+// the given temporary storage
+int scan_only(DBuf<char> &tmp, hipStream_t s, const int *in, int *out, int n)
 {
     size_t bytes = 0;
     AMG_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out + 1, n, s));
-    AMG_CHECK(A.cub_tmp.alloc(bytes ? bytes : 1));
+    AMG_CHECK(tmp.alloc(bytes ? bytes : 1));
     AMG_CHECK(hipMemsetAsync(out, 0, sizeof(int), s));
-    if (n > 0) AMG_CHECK(hipcub::DeviceScan::InclusiveSum(A.cub_tmp.p, bytes, in, out + 1, n, s));
+    if (n > 0) AMG_CHECK(hipcub::DeviceScan::InclusiveSum(tmp.p, bytes, in, out + 1, n, s));
     return XFK_OK;
 }
+int scan_only(Amg &A, hipStream_t s, const int *in, int *out, int n) { return scan_only(A.cub_tmp, s, in, out, n); }
 
 int read_flag(Amg &A, hipStream_t s, int idx, int &v)
 {
@@ -2259,6 +2283,7 @@ int SideStream::init()
     AMG_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     AMG_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
     AMG_CHECK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    AMG_CHECK(hipEventCreateWithFlags(&c, hipEventDisableTiming));
     return XFK_OK;
 }
 
@@ -2266,7 +2291,18 @@ SideStream::~SideStream()
 {
     if (a) (void)hipEventDestroy(a);
     if (b) (void)hipEventDestroy(b);
+    if (c) (void)hipEventDestroy(c);
     if (cs) (void)hipStreamDestroy(cs);
+}
+
+// XFK_NO_SIDE_SETUP=1: every setup step on the main stream
+static bool side_setup_on()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_NO_SIDE_SETUP");
+        return !(e && std::atoi(e) != 0);
+    }();
+    return v;
 }
 
 bool overlap_enabled()
@@ -2348,15 +2384,16 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
 // out sorted by row): counting transpose, the fill counting the row counts
 // back down, rows sorted by a wave bitonic network, values looked up in M.
 // T's arrays hold as many entries as M (no read-back of the scan).
-static int transpose_csr(Amg &M, hipStream_t s, int n, int nc, const int *mrow, const int *mcol, const double *mval,
-                         int *trow, int *tcol, double *tval)
+// cnt / tmp: scratch of the stream it runs on (the setup's side stream has its own)
+static int transpose_csr(DBuf<int> &cnt, DBuf<char> &tmp, hipStream_t s, int n, int nc, const int *mrow,
+                         const int *mcol, const double *mval, int *trow, int *tcol, double *tval)
 {
-    AMG_CHECK(M.cnt.alloc((size_t)std::max(n, nc) + 1));
-    AMG_CHECK(hipMemsetAsync(M.cnt.p, 0, sizeof(int) * ((size_t)nc + 1), s));
-    if (n > 0) k_rt_count<<<nb(n), kB, 0, s>>>(n, mrow, mcol, M.cnt.p);
-    int rc = scan_only(M, s, M.cnt.p, trow, nc);
+    AMG_CHECK(cnt.alloc((size_t)std::max(n, nc) + 1));
+    AMG_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * ((size_t)nc + 1), s));
+    if (n > 0) k_rt_count<<<nb(n), kB, 0, s>>>(n, mrow, mcol, cnt.p);
+    int rc = scan_only(tmp, s, cnt.p, trow, nc);
     if (rc != XFK_OK) return rc;
-    if (n > 0) k_rt_fill<<<nb(n), kB, 0, s>>>(n, mrow, mcol, trow, M.cnt.p, tcol);
+    if (n > 0) k_rt_fill<<<nb(n), kB, 0, s>>>(n, mrow, mcol, trow, cnt.p, tcol);
     if (nc > 0)
         k_rt_sort_vals<<<(int)(((long long)nc * 64 + 255) / 256), 256, 0, s>>>(nc, trow, tcol, mrow, mcol, mval, tval);
     AMG_CHECK(hipGetLastError());
@@ -2452,12 +2489,27 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         return rc;
     A.nc = (int)nc;
     if (std::getenv("XFK_AMG_DEBUG")) std::fprintf(stderr, "[amg] level %d P nnz %lld\n", l, A.pnnz);
-    // R = P^T
+    // R = P^T: on the side stream (single-device levels) while the main
+    // stream forms A P; the Galerkin product R (A P) waits for it
     AMG_CHECK(A.rrow.alloc((size_t)nc + 1));
     AMG_CHECK(A.rcol.alloc((size_t)std::max(1LL, A.pnnz)));
     AMG_CHECK(A.rval.alloc((size_t)std::max(1LL, A.pnnz)));
-    if ((rc = transpose_csr(*this, s, n, (int)nc, A.prow.p, A.pcol.p, A.pval.p, A.rrow.p, A.rcol.p, A.rval.p)) != XFK_OK)
+    const bool off = side_setup_on() && !A.dist && !dist;
+    hipStream_t ts = s;
+    if (off) {
+        if ((rc = sw.init()) != XFK_OK) return rc;
+        AMG_CHECK(hipEventRecord(sw.a, s));
+        AMG_CHECK(hipStreamWaitEvent(sw.cs, sw.a, 0));
+        ts = sw.cs;
+        sw_used = true;
+    }
+    if ((rc = transpose_csr(off ? cnt2 : cnt, off ? cub_tmp2 : cub_tmp, ts, n, (int)nc, A.prow.p, A.pcol.p,
+                            A.pval.p, A.rrow.p, A.rcol.p, A.rval.p)) != XFK_OK)
         return rc;
+    if (off) {
+        AMG_CHECK(hipEventRecord(sw.b, sw.cs));
+        rt_pending = true;
+    }
     if (g_prof) g_prof->end();
     return XFK_OK;
 }
@@ -2509,11 +2561,14 @@ int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &ld)
     // the pattern through pinned memory; an unchanged pattern (the next setup
     // of the same matrix family) keeps the plan and its device arrays
     const size_t npat = (size_t)n + 1 + (size_t)C.nnz;
-    int rc = host_ints((int)npat);
-    if (rc != XFK_OK) return rc;
-    AMG_CHECK(hipMemcpyAsync(host_big, C.rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost, s));
-    AMG_CHECK(hipMemcpyAsync(host_big + n + 1, C.col, sizeof(int) * C.nnz, hipMemcpyDeviceToHost, s));
-    AMG_CHECK(hipStreamSynchronize(s));
+    if (!nd_prefetched || (size_t)C.nnz > C.col_o.n) {   // (else read with the deferred lengths)
+        int rc = host_ints((int)npat);
+        if (rc != XFK_OK) return rc;
+        AMG_CHECK(hipMemcpyAsync(host_big, C.rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipMemcpyAsync(host_big + n + 1, C.col, sizeof(int) * C.nnz, hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipStreamSynchronize(s));
+    }
+    nd_prefetched = false;
     if (nd_key.size() == npat && std::equal(nd_key.begin(), nd_key.end(), host_big)) {
         nd_phases = nd_phases_key;
         ld = nd_ld;
@@ -2710,6 +2765,10 @@ int Amg::build(hipStream_t s, int l0)
         // AP = A P, then A_c = R (A P)
         SgX XA{A.rowptr, A.col, A.val, A.ncol_lim, nullptr, nullptr, nullptr};
         SgY YP{A.prow.p, A.pcol.p, A.pval.p, nullptr};
+        if (fold_pending) {   // the previous level's folded transfer still reads A P's buffers
+            AMG_CHECK(hipStreamWaitEvent(s, sw.c, 0));
+            fold_pending = false;
+        }
         if (g_prof) g_prof->begin(lv + "SpGEMM A P", 0.0);
         rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, ap_nnz, 4 * l + 1);
         if (g_prof) g_prof->end();
@@ -2718,6 +2777,10 @@ int Amg::build(hipStream_t s, int l0)
         AmgLevel &C = *L[l + 1];
         SgX XR{A.rrow.p, A.rcol.p, A.rval.p, INT_MAX, nullptr, nullptr, nullptr};
         SgY YAP{ap_row.p, ap_col.p, ap_val.p, nullptr};
+        if (rt_pending) {   // R = P^T from the side stream
+            AMG_CHECK(hipStreamWaitEvent(s, sw.b, 0));
+            rt_pending = false;
+        }
         if (g_prof) g_prof->begin(lv + "SpGEMM R (A P)", 0.0);
         rc = spgemm<false>(*this, s, (int)nc, XR, YAP, C.rowptr_o, C.col_o, C.val_o, C.nnz, 4 * l + 2);
         if (g_prof) g_prof->end();
@@ -2736,14 +2799,29 @@ int Amg::build(hipStream_t s, int l0)
                 AMG_CHECK(A.frval.alloc((size_t)std::max(1LL, ap_nnz)));
             }
             AMG_CHECK(hipMemcpyAsync(A.ftrow.p, ap_row.p, sizeof(int) * ((size_t)n + 1), hipMemcpyDeviceToDevice, s));
+            // P~ and R~ on the side stream: only the V-cycle reads them; the
+            // next level's A P (which reuses A P's buffers) waits for P~
+            const bool off = side_setup_on();
+            hipStream_t fs = s;
+            if (off) {
+                if ((rc = sw.init()) != XFK_OK) return rc;
+                AMG_CHECK(hipEventRecord(sw.a, s));
+                AMG_CHECK(hipStreamWaitEvent(sw.cs, sw.a, 0));
+                fs = sw.cs;
+                sw_used = true;
+            }
             if (n > 0)
-                k_fold_p<<<(int)(((long long)n * kFoldLanes + 255) / 256), 256, 0, s>>>(
+                k_fold_p<<<(int)(((long long)n * kFoldLanes + 255) / 256), 256, 0, fs>>>(
                     n, rho.p + 2 * l, A.dinv.p, ap_row.p, ap_col.p, ap_val.p, A.prow.p, A.pcol.p, A.pval.p, A.ftcol.p,
                     A.ftval.p);
+            if (off) {
+                AMG_CHECK(hipEventRecord(sw.c, sw.cs));
+                fold_pending = true;
+            }
             // level 0 folds only its post-step (its pre-step keeps R r'): no R~
             if (l > 0)
-                rc = transpose_csr(*this, s, n, (int)nc, A.ftrow.p, A.ftcol.p, A.ftval.p, A.frrow.p, A.frcol.p,
-                                   A.frval.p);
+                rc = transpose_csr(off ? cnt2 : cnt, off ? cub_tmp2 : cub_tmp, fs, n, (int)nc, A.ftrow.p, A.ftcol.p,
+                                   A.ftval.p, A.frrow.p, A.frcol.p, A.frval.p);
             if (rc != XFK_OK) return rc;
             // the exact length picks the V-cycle's lanes per row (and so the
             // summation order): from a deferred slot when A P's length is
@@ -2772,9 +2850,27 @@ int Amg::build(hipStream_t s, int l0)
         // the SpGEMM lengths taken without a host check (capacity hints); an
         // overflow means a hint was too small: rebuild with measured capacities
         bool overflow = false;
+        // the coarsest pattern for the nested-dissection plan rides on the
+        // same host check (its length is deferred too: the whole capacity)
+        nd_prefetched = false;
+        if (dense_coarse && def_n > 0 && nlev - 1 > l0) {
+            AmgLevel &C = *L[nlev - 1];
+            if (C.col == C.col_o.p && C.n >= 8 * kBj) {
+                const size_t cap = C.col_o.n;
+                int rc = host_ints((int)((size_t)C.n + 1 + cap));
+                if (rc != XFK_OK) return rc;
+                AMG_CHECK(hipMemcpyAsync(host_big, C.rowptr, sizeof(int) * ((size_t)C.n + 1), hipMemcpyDeviceToHost, s));
+                AMG_CHECK(hipMemcpyAsync(host_big + C.n + 1, C.col, sizeof(int) * cap, hipMemcpyDeviceToHost, s));
+                nd_prefetched = true;
+            }
+        }
         int rc = resolve_deferred(s, overflow);
         if (rc != XFK_OK) return rc;
         if (overflow) {
+            if (sw_used) {   // nothing of this attempt may still run on the side stream
+                AMG_CHECK(hipStreamSynchronize(sw.cs));
+                sw_used = rt_pending = fold_pending = false;
+            }
             cap_hint.clear();
             return build(s, l0);
         }
@@ -2874,17 +2970,19 @@ int Amg::build(hipStream_t s, int l0)
                                                      Rb(0, q), Cb(0, q), maxd);
             }
         }
-        if (nd) {
+        {
             const int ldo = ((C.n + kBj - 1) / kBj) * kBj;
             AMG_CHECK(cinv_o.alloc((size_t)ldo * ldo));
-            k_dense_unperm<<<ld, 256, 0, s>>>(C.n, ld, ldo, cinv.p, sc, cinv_iperm.p, cinv_o.p);
-            cinv_apply = cinv_o.p;   // (two buffers kept apart: no reallocation per setup)
+            k_dense_unperm<<<ld, 256, 0, s>>>(C.n, ld, ldo, cinv.p, sc, nd ? cinv_iperm.p : nullptr, cinv_o.p);
+            cinv_apply = cinv_o.p;
             cinv_ld = ldo;
-        } else {
-            k_dense_unscale<<<(unsigned)(((size_t)ld * ld / 2 + 255) / 256), 256, 0, s>>>(ld, cinv.p, sc);
-            cinv_apply = cinv.p;
         }
         if (g_prof) g_prof->end();
+    }
+    if (sw_used) {   // the V-cycle reads R, P~, R~: join the side stream (after the dense inverse's launches)
+        AMG_CHECK(hipEventRecord(sw.b, sw.cs));
+        AMG_CHECK(hipStreamWaitEvent(s, sw.b, 0));
+        sw_used = rt_pending = fold_pending = false;
     }
     AMG_CHECK(hipGetLastError());   // no host check: nothing on the host waits for the device here
     return XFK_OK;
@@ -3409,7 +3507,7 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     if (l == M.nlev - 1) {
         double *dst = (l == 0) ? out0 : A.xa.p;
         if (M.dense_coarse) {
-            XFK_PHASE(lv + "dense inverse x b", 8.0 * A.n * M.cinv_ld + 8.0 * (M.cinv_ld + A.n),
+            XFK_PHASE(lv + "dense inverse x b", 4.0 * A.n * M.cinv_ld + 8.0 * (M.cinv_ld + A.n),
                       (k_dense_mv<<<A.n, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv_apply, b, dst, done)));
             return dst;
         }

@@ -208,7 +208,7 @@ struct TileSplit {
 int build_tile_split(hipStream_t s, int n, int B, const int *rowptr, const int *col, TileSplit &ts);
 struct SideStream {
     hipStream_t cs = nullptr;
-    hipEvent_t a = nullptr, b = nullptr;
+    hipEvent_t a = nullptr, b = nullptr, c = nullptr;
     int init();
     ~SideStream();
 };

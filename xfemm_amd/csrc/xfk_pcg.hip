@@ -80,19 +80,23 @@ __global__ void __launch_bounds__(kCgBlock) k_cg_spmv(int N, const int *__restri
                                                       const double *__restrict__ R, double *__restrict__ part_gam,
                                                       const int *__restrict__ tl)
 {
-    if (S && S->done) return;
+    // the convergence flag, the tile's row range and this row's u, r are
+    // loaded together before the first branch (one memory latency, not two)
+    const int dn = load_flag_v(S ? &S->done : nullptr);
     __shared__ __attribute__((aligned(16))) double lds[kCgCap];
     __shared__ double red[2 * (kCgBlock / 64)];
     const int t = tl ? tl[xcd_tile(blockIdx.x, gridDim.x)] : xcd_tile(blockIdx.x, gridDim.x);
     const int r0 = t * kCgBlock;
-    const double w = cg_tile_spmv(r0, N, rowptr, col, val, [&](int j) { return U[j]; }, lds);
     const int r = r0 + threadIdx.x;
+    const TileRows tr = tile_rows(r0, N, rowptr);
+    const double u = r < N ? U[r] : 0.0, rr = (R && r < N) ? R[r] : 0.0;
+    if (dn) return;
+    const double w = cg_tile_spmv(tr, col, val, [&](int j) { return U[j]; }, lds);
     double d = 0.0, g = 0.0;
     if (r < N) {
         W[r] = w;
-        const double u = U[r];
         d = w * u;
-        if (R) g = R[r] * u;
+        if (R) g = rr * u;
     }
     cg_block_sum2(d, g, red);
     if (threadIdx.x == 0) {
@@ -130,10 +134,10 @@ __global__ void __launch_bounds__(kAxBlock) k_cg_axpy(CgAxpyArgs A)
 {
     __shared__ double red[2 * (kAxBlock / 64)];
     CgState *S = A.S;
-    if (S->done) return;
+    const int dn = load_flag_v(&S->done);
     // AMG form: the first two row pairs of this thread are loaded before the
     // partial reduction (they do not depend on alpha, beta), so the stream is
-    // in flight while the partials are summed
+    // in flight while the partials are summed (and while the flag arrives)
     const int npair = A.N >> 1;
     const int k0 = blockIdx.x * kAxBlock + threadIdx.x, kst = gridDim.x * kAxBlock;
     double2 pf[2][6];
@@ -151,6 +155,7 @@ __global__ void __launch_bounds__(kAxBlock) k_cg_axpy(CgAxpyArgs A)
             }
         }
     }
+    if (dn) return;
     double gam, del;
     cg_reduce2(A.gam_in, A.Ggam, A.del_in, A.Gdel, gam, del, red);
     double res_o;

@@ -74,16 +74,54 @@ __device__ __forceinline__ int xcd_tile(int b, int nb)
 // pass, lds holds CAP doubles): 2 for the ~7 entries per row of the fine
 // level, more for the longer rows of coarse levels and of R, so that a tile
 // takes one pass (each pass is a load / barrier / sum / barrier round trip)
-template <int B = kCgBlock, int SLOTS = 2, class XF>
-__device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restrict__ rowptr,
-                                               const int *__restrict__ col, const double *__restrict__ val,
-                                               XF X, double *lds)
+// a device flag read as a per-lane (vector) load: a scalar load would be
+// waited for together with the kernel arguments (the scalar cache's counter
+// is waited to zero), before any other load is issued; as a vector load it
+// is in flight with the tile's first loads and the branch on it waits for it
+// alone.  The empty asm makes the zero index opaque to the compiler.
+// (p == nullptr reads a zero flag; selecting the pointer instead of
+// branching keeps the load in straight-line code: a branch around it would
+// be closed by a wait for it)
+static __device__ int xfk_zero_flag = 0;
+__device__ __forceinline__ int load_flag_v(const int *p)
 {
-    constexpr int CAP = 4 * SLOTS * B;
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    const int *q = p ? p : &xfk_zero_flag;
+    return q[z];
+}
+
+// the tile's row range and this thread's row: loaded first, so a kernel can
+// have them in flight together with its other early loads (the convergence
+// flag, its own row's vector entries) before it branches on any of them
+struct TileRows {
+    int s, e, my_s, my_e;
+};
+// (the tile's bounds are read by vector loads too -- a scalar load would be
+// sunk below the kernel's first branch -- and moved to scalar registers by
+// cg_tile_spmv)
+template <int B = kCgBlock>
+__device__ __forceinline__ TileRows tile_rows(int r0, int N, const int *__restrict__ rowptr)
+{
     const int r = r0 + threadIdx.x;
     const int rend = min(r0 + B, N);
-    const int s = rowptr[r0], e = rowptr[rend];
-    const int my_s = (r < N) ? rowptr[r] : 0, my_e = (r < N) ? rowptr[r + 1] : 0;
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    TileRows t;
+    t.s = rowptr[r0 + z];
+    t.e = rowptr[rend + z];
+    t.my_s = (r < N) ? rowptr[r] : 0;
+    t.my_e = (r < N) ? rowptr[r + 1] : 0;
+    return t;
+}
+
+template <int B = kCgBlock, int SLOTS = 2, class XF>
+__device__ __forceinline__ double cg_tile_spmv(const TileRows &tr, const int *__restrict__ col,
+                                               const double *__restrict__ val, XF X, double *lds)
+{
+    constexpr int CAP = 4 * SLOTS * B;
+    const int s = __builtin_amdgcn_readfirstlane(tr.s), e = __builtin_amdgcn_readfirstlane(tr.e);
+    const int my_s = tr.my_s, my_e = tr.my_e;
     double acc = 0.0;
     for (int c0 = s & ~3; c0 < e; c0 += CAP) {
         const int c1 = min(e, c0 + CAP);
@@ -110,6 +148,14 @@ __device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restr
         __syncthreads();
     }
     return acc;
+}
+
+template <int B = kCgBlock, int SLOTS = 2, class XF>
+__device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restrict__ rowptr,
+                                               const int *__restrict__ col, const double *__restrict__ val,
+                                               XF X, double *lds)
+{
+    return cg_tile_spmv<B, SLOTS>(tile_rows<B>(r0, N, rowptr), col, val, X, lds);
 }
 
 }  // namespace xfk
