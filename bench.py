@@ -1,8 +1,9 @@
 """Bench: solved DoF/s of the fsolver static-2D hot path on MI355X.
 
-One step = FSolver::Static2D from a device-resident mesh: symbolic phase (CSR
-pattern, element colouring, BC maps), element assembly, boundary conditions
-and the PCG solve to the problem's Precision (1e-8), plus the Newton loop for
+One step = FSolver::Static2D from a device-resident mesh: symbolic phase
+(node -> element lists, CSR pattern, Dirichlet row lists), row-gather element
+assembly, boundary conditions, the AMG setup (built fresh every step) and the
+PCG solve to the problem's Precision (1e-8), plus the Newton loop for
 nonlinear problems.  Inputs (mesh + property tables) are uploaded before the
 timed region.
 
@@ -22,9 +23,20 @@ independent 2M-tri problem per GPU (parameter sweep; no collective, "weak").
 The host barrier / max-over-ranks and the RCCL unique-id broadcast use
 torch.distributed (gloo) on scalars only.
 
-Output: one JSON line (rank 0) with roofline (SpMV kernel, HIP-event timing
-inside the timed region) and cpu_baseline (reference spars.cpp via oracle/_ref,
-single core, bounded sample).
+Output: one JSON line (rank 0) with
+  roofline       the PCG SpMV (k_cg_spmv): HIP-event timing inside the timed
+                 region, algorithmic bytes per launch, PMC traffic from the
+                 committed rocprof summary; roofline.phases = every AMG setup
+                 step and every launch of one PCG iteration (xfk_phase_profile,
+                 after the timed region), annotated with the rocprof duration,
+                 the PMC traffic and the bound (cache / hbm / latency) of the
+                 same launch from the newest profiles/*_phase_pmc.json;
+  cpu_baseline   the reference's spars.cpp via oracle/_ref, single core,
+                 bounded sample;
+  secondary      configs[3] (nonlinear M-19, Newton loop) and configs[4] on
+                 one GPU (20M triangles, 10.0M DoF);
+  cold_first_solve  the first solve of a fresh problem object (no capacity or
+                 round-count hints from an earlier setup).
 """
 import argparse
 import ctypes
@@ -44,14 +56,15 @@ def _hip_sync():
     lib.hipDeviceSynchronize()
 
 
-def spmv_bytes(n_rows, nnz, amg=False):
+def spmv_bytes(n_rows, nnz, amg=False, col_bytes=4.0):
     """Algorithmic HBM bytes of one CSR SpMV launch of the PCG (k_cg_spmv,
-    xfemm_amd/csrc/xfk_pcg.hip): val 8 B + col 4 B per nonzero, rowptr 4 B per
-    row (+1), u read once 8 B per row, w written 8 B per row (the fused u.w
-    partial re-reads u from cache).  With the AMG preconditioner the r.u
-    partial comes from the V-cycle's last level-0 sweep (which holds r and
-    u), so the SpMV does not read r either."""
-    return 12 * nnz + 4 * (n_rows + 1) + 16 * n_rows
+    xfemm_amd/csrc/xfk_pcg.hip): val 8 B + the column index per nonzero (4 B,
+    or 2 B with the AMG's 16-bit tile offsets: col_bytes as the library
+    reports it), rowptr 4 B per row (+1), u read once 8 B per row, w written
+    8 B per row (the fused u.w partial re-reads u from cache).  With the AMG
+    preconditioner the r.u partial comes from the V-cycle's last level-0 sweep
+    (which holds r and u), so the SpMV does not read r either."""
+    return (8 + col_bytes) * nnz + 4 * (n_rows + 1) + 16 * n_rows
 
 
 class stdout_to_stderr:
@@ -363,7 +376,8 @@ def main():
     nnz = results[-1]["nnz"]
     rows = P.n_rows
     amg = results[-1]["precond"] == kernels.XFK_PRECOND_AMG
-    algo = spmv_bytes(rows, nnz, amg)
+    col_bytes = P.spmv_col_bytes()
+    algo = spmv_bytes(rows, nnz, amg, col_bytes)
     achieved = algo / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
     ms_step = 1e3 * elapsed / args.steps
     traffic, traffic_src = (args.traffic, "--traffic") if args.traffic is not None else pmc_traffic(algo)
@@ -455,6 +469,7 @@ def main():
             "traffic": traffic,
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": algo,
+            "column_bytes_per_nonzero": col_bytes,
             "launch_us": spmv_ms * 1e3,
             "launches_sampled": sum(r["spmv_samples"] for r in results),
         },
@@ -464,7 +479,7 @@ def main():
         out["roofline"]["phases"] = phases
         out["roofline"]["phases_note"] = (
             "xfk_phase_profile after the timed region: AMG setup rebuilt once, then %d PCG iterations; "
-            "us per launch from HIP events; algorithmic bytes per launch (matrix stream 12 B/nnz + 4 B/row, each "
+            "us per launch from HIP events; algorithmic bytes per launch (matrix stream 12 B/nnz, 10 with 16-bit tile columns, + 4 B/row, each "
             "vector once); peak %g GB/s; one PCG iteration = %.1f us of phases. rocprof_us, traffic_bytes and "
             "bound: one iteration of the same workload from %s (tools/phase_pmc.py: kernel trace + FETCH_SIZE / "
             "WRITE_SIZE passes; bound 'cache' when traffic < 0.5 x algorithmic bytes, else 'hbm' at >= 30 %% of peak by rocprof duration, 'latency' below)" % (

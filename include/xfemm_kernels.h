@@ -174,9 +174,13 @@ enum {
                                    2x the iterations of the last fresh build; 0: rebuild every time */
     XFK_OPT_AMG_DENSE = 7,      /* coarsening stops at a level of at most this many rows, which is
                                    solved by its dense inverse (16..2048, default 2048) */
-    XFK_OPT_AMG_FOLD = 8        /* 1 (default, or XFK_AMG_FOLD from the environment): V(1,1) levels
+    XFK_OPT_AMG_FOLD = 8,       /* 1 (default, or XFK_AMG_FOLD from the environment): V(1,1) levels
                                    run folded (one pass over P~ = (I - w D^-1 A) P for prolongation +
                                    post-sweep, coarse pre-steps with R~ = P~^T); 0: the plain cycle */
+    XFK_OPT_AMG_COL16 = 9       /* 1 (default, unless XFK_NO_COL16 is set): single-device level-0
+                                   operators (the PCG SpMV, the sweeps, P~, R) read 16-bit column
+                                   offsets per row tile (tiles spanning > 65535 columns read the int
+                                   columns); 0: int columns.  The same column indices: the same bits. */
 };
 int xfk_set_option(xfk_problem *prob, int option, double value);
 
@@ -330,6 +334,10 @@ int xfk_get_csr_complex(xfk_problem *prob, int *rowptr, int *col, double *val, d
 /* Device views for the bench / tests (stream-ordered on the problem's stream). */
 int xfk_get_csr(xfk_problem *prob, int *rowptr, int *col, double *val, double *b);
 long long xfk_get_nnz(xfk_problem *prob);
+/* Column-index bytes per nonzero the last solve's PCG SpMV read: 2 with the
+   AMG's 16-bit tile offsets (plus 2 for every nonzero of a tile whose columns
+   span more than 65535), 4 without them; -1 for a null problem. */
+double xfk_spmv_col_bytes(xfk_problem *prob);
 int xfk_get_stream(xfk_problem *prob, void **hip_stream);
 
 /* Stand-alone PCG on a host-supplied full symmetric CSR (testing the solver

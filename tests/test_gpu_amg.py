@@ -11,7 +11,7 @@ import scipy.sparse as sp
 import scipy.sparse.linalg as sla
 
 from oracle import oracle
-from util import converged, parity_message, rel_err, synth_to_oracle
+from util import C_ANS, converged, parity_message, rel_err, synth_to_oracle
 from xfemm_amd import kernels, synth
 
 pytestmark = pytest.mark.gpu
@@ -273,6 +273,40 @@ def test_folded_cycle_equals_plain_cycle(cells, nonlinear):
         assert abs(rf["cg_iters"] - rp["cg_iters"]) <= rf["newton_iters"]
     else:
         assert abs(rf["cg_iters"] - rp["cg_iters"]) <= 1, (rf["cg_iters"], rp["cg_iters"])
+
+
+def test_col16_tiles_are_bit_identical_with_wide_tile_fallback():
+    """Level 0's 16-bit tile columns (XFK_OPT_AMG_COL16, default on) give the
+    same bits as the int columns: once on the banded numbering (every tile
+    fits: 2 B per nonzero) and once with the first half of the nodes in a
+    random order (those tiles span > 65535 columns and read the int array:
+    between 2 and 4 B per nonzero)."""
+    kw = synth.magnetostatic(400)
+    N = len(kw["x"])
+    perm = np.arange(N)
+    perm[: N // 2] = np.random.default_rng(5).permutation(N // 2)
+    inv = np.argsort(perm)
+    kws = dict(kw)
+    kws["x"] = np.asarray(kw["x"])[inv]
+    kws["y"] = np.asarray(kw["y"])[inv]
+    kws["p"] = perm[np.asarray(kw["p"])]
+    for k, lo, hi in ((kw, 2.0, 2.0), (kws, 2.05, 3.95)):
+        out = []
+        for c16 in (True, False):
+            P = kernels.Static2DProblem(**k, precond="amg", amg_col16=c16)
+            r = P.solve()
+            out.append((P.solution(), r["cg_iters"], P.spmv_col_bytes()))
+            if c16:
+                rp, col, val, b = P.csr()
+            P.close()
+        (A1, i1, cb1), (A0, i0, cb0) = out
+        assert lo <= cb1 <= hi, cb1
+        assert cb0 == 4.0
+        assert i1 == i0
+        assert np.array_equal(A1.view(np.int64), A0.view(np.int64))
+        M = sp.csr_matrix((val, col, rp), shape=(len(rp) - 1,) * 2)
+        V = A1 / C_ANS
+        assert np.linalg.norm(M @ V - b) <= 1e-5 * np.linalg.norm(b)
 
 
 def test_amg_is_deterministic_through_newton_refreshes():

@@ -73,6 +73,12 @@ struct AmgLevel {
     bool dist = false;
     HaloPlan plan;
     TileSplit ts;                     // sharded level run by the tile kernels: exchange overlap
+    // 16-bit column offsets per tile (single-device level 0, xfk_spmv.h
+    // k_tile_col16): A and P~ in the 512-row tiles of the SpMV / sweeps /
+    // folded post-step, R in the restriction's 256-row tiles
+    bool has16 = false;
+    DBuf<unsigned short> a16, f16, r16;
+    DBuf<int> a16b, f16b, r16b;
 };
 
 struct AmgStats {
@@ -143,6 +149,7 @@ struct Amg {
     int rep_rows = 250000;
     int dense_max = kAmgDenseMax;     // coarsest level: dense inverse at <= dense_max rows
     int fold_on = -1;                 // folded V(1,1) levels: 1 / 0, -1 = the XFK_AMG_FOLD default
+    int col16 = -1;                   // 16-bit tile columns on level 0: 1 / 0, -1 = on unless XFK_NO_COL16
     int lrep = 0;
     xfk_comm *comm = nullptr;
     int nranks = 1, rank = 0;

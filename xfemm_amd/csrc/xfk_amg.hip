@@ -1620,7 +1620,9 @@ __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__r
                                                          const unsigned long long *rho, const double *__restrict__ b,
                                                          const double *__restrict__ x, double *__restrict__ out,
                                                          double *__restrict__ rout, const int *done,
-                                                         double *__restrict__ part_gam, const int *__restrict__ tl)
+                                                         double *__restrict__ part_gam, const int *__restrict__ tl,
+                                                         const unsigned short *__restrict__ c16 = nullptr,
+                                                         const int *__restrict__ cbase = nullptr)
 {
     // the convergence flag, rho, the tile's row range and this row's b,
     // D^-1, x are loaded together before the first branch
@@ -1632,15 +1634,17 @@ __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__r
     const int i = r0 + threadIdx.x;
     constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
     const TileRows tr = tile_rows<B>(r0, n, rowptr);
+    const int cb = load_col_base(cbase, t);
     const double bi = i < n ? b[i] : 0.0, di = i < n ? dinv[i] : 0.0;
     const double xv = (!implicit && i < n) ? x[i] : 0.0;
     if (dn) return;
     const double w = ra > 0.0 ? 1.0 / ra : 0.0;
     double ax;
     if constexpr (implicit)
-        ax = cg_tile_spmv<B, SLOTS>(tr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; }, lds);
+        ax = cg_tile_spmv16<B, SLOTS>(tr, c16, cb, col, val,
+                                      [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; }, lds);
     else
-        ax = cg_tile_spmv<B, SLOTS>(tr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; }, lds);
+        ax = cg_tile_spmv16<B, SLOTS>(tr, c16, cb, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; }, lds);
     double oi = 0.0;
     if (i < n) oi = smooth_finish_v<MODE>(i, ax, w, di, bi, xv, out, rout);
     if constexpr (MODE == kSweep) {
@@ -1680,7 +1684,7 @@ __global__ void __launch_bounds__(256) k_amg_smooth_g(int n, int ncl, const int 
     if (done && *done) return;
     const double ra = rho_of(rho);
     const double w = ra > 0.0 ? 1.0 / ra : 0.0;
-    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const int i = (xcd_tile(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) / G;
     constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
     double ax;
     if constexpr (implicit)
@@ -1694,16 +1698,20 @@ __global__ void __launch_bounds__(256) k_amg_smooth_g(int n, int ncl, const int 
 template <int B, bool ACC, int SLOTS = 2>
 __global__ void __launch_bounds__(B) k_csr_mv_tile(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
                                                    const double *__restrict__ val, const double *__restrict__ x,
-                                                   double *__restrict__ y, const int *done)
+                                                   double *__restrict__ y, const int *done,
+                                                   const unsigned short *__restrict__ c16 = nullptr,
+                                                   const int *__restrict__ cbase = nullptr)
 {
     const int dn = load_flag_v(done);
     __shared__ __attribute__((aligned(16))) double lds[4 * SLOTS * B];
-    const int r0 = xcd_tile(blockIdx.x, gridDim.x) * B;
+    const int t = xcd_tile(blockIdx.x, gridDim.x);
+    const int r0 = t * B;
     const int i = r0 + threadIdx.x;
     const TileRows tr = tile_rows<B>(r0, n, rowptr);
+    const int cb = load_col_base(cbase, t);
     const double y0 = (ACC && i < n) ? y[i] : 0.0;
     if (dn) return;
-    const double s = cg_tile_spmv<B, SLOTS>(tr, col, val, [&](int j) { return x[j]; }, lds);
+    const double s = cg_tile_spmv16<B, SLOTS>(tr, c16, cb, col, val, [&](int j) { return x[j]; }, lds);
     if (i < n) y[i] = ACC ? y0 + s : s;
 }
 
@@ -1714,7 +1722,7 @@ __global__ void __launch_bounds__(256) k_csr_mv_g(int n, const int *__restrict__
                                                   double *__restrict__ y, const int *done)
 {
     if (done && *done) return;
-    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const int i = (xcd_tile(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) / G;
     const double s = group_row_dot<G>(i, n, rowptr, col, val, [&](int j) { return x[j]; });
     if (i < n && (threadIdx.x & (G - 1)) == 0) y[i] = ACC ? y[i] + s : s;
 }
@@ -1761,7 +1769,9 @@ __global__ void __launch_bounds__(B) k_fold_post0(int n, const int *__restrict__
                                                   const double *__restrict__ dinv, const unsigned long long *rho,
                                                   const double *__restrict__ rres,
                                                   const double *__restrict__ b, double *__restrict__ out,
-                                                  const int *done, double *__restrict__ part_gam)
+                                                  const int *done, double *__restrict__ part_gam,
+                                                  const unsigned short *__restrict__ c16,
+                                                  const int *__restrict__ cbase)
 {
     const int dn = load_flag_v(done);
     __shared__ __attribute__((aligned(16))) double lds[4 * SLOTS * B];
@@ -1770,10 +1780,11 @@ __global__ void __launch_bounds__(B) k_fold_post0(int n, const int *__restrict__
     const int r0 = t * B;
     const int i = r0 + threadIdx.x;
     const TileRows tr = tile_rows<B>(r0, n, frow);
+    const int cb = load_col_base(cbase, t);
     const double di = i < n ? dinv[i] : 0.0, bi = i < n ? b[i] : 0.0, ri = i < n ? rres[i] : 0.0;
     if (dn) return;
     const double w = ra > 0.0 ? 1.0 / ra : 0.0;
-    const double pc = cg_tile_spmv<B, SLOTS>(tr, fcol, fval, [&](int j) { return xc[j]; }, lds);
+    const double pc = cg_tile_spmv16<B, SLOTS>(tr, c16, cb, fcol, fval, [&](int j) { return xc[j]; }, lds);
     double u = 0.0;
     if (i < n) {
         u = (w * di * bi + w * di * ri) + pc;
@@ -1800,10 +1811,12 @@ __global__ void __launch_bounds__(256) k_fold_pre(int n, int ncl, const int *__r
                                                   int blocks_a, const int *done)
 {
     if (done && *done) return;
+    // XCD-contiguous row blocks in each range (blocks_a is a multiple of 8):
+    // an XCD's L2 serves the vector entries its neighbouring rows share
     if ((int)blockIdx.x < blocks_a) {
         const double ra = rho_of(rho);
         const double w = ra > 0.0 ? 1.0 / ra : 0.0;
-        const int i = (blockIdx.x * blockDim.x + threadIdx.x) / GA;
+        const int i = (xcd_tile(blockIdx.x, blocks_a) * blockDim.x + threadIdx.x) / GA;
         const double ax =
             group_row_dot<GA>(i, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; });
         if (i < n && (threadIdx.x & (GA - 1)) == 0) {
@@ -1811,7 +1824,7 @@ __global__ void __launch_bounds__(256) k_fold_pre(int n, int ncl, const int *__r
             y[i] = xi + w * di * (bi - ax);
         }
     } else {
-        const int c = ((blockIdx.x - blocks_a) * blockDim.x + threadIdx.x) / GB;
+        const int c = (xcd_tile(blockIdx.x - blocks_a, gridDim.x - blocks_a) * blockDim.x + threadIdx.x) / GB;
         const double sc = group_row_dot<GB>(c, nc, rrow, rcol, rval, [&](int j) { return b[j]; });
         if (c < nc && (threadIdx.x & (GB - 1)) == 0) bc[c] = sc;
     }
@@ -2198,8 +2211,9 @@ static int rmv_mode()
     return v;
 }
 
+// c16 / cbase: 16-bit column offsets in 256-row tiles (used by the 256-row tile kernels only)
 void launch_mv(hipStream_t s, int n, const int *rowptr, const int *col, const double *val, const double *x, double *y,
-               bool acc, int G, const int *done)
+               bool acc, int G, const int *done, const unsigned short *c16 = nullptr, const int *cbase = nullptr)
 {
     if (n <= 0) return;
     if (n >= kTileMinRows && G == 8 && rmv_mode() == 2) {
@@ -2218,11 +2232,11 @@ void launch_mv(hipStream_t s, int n, const int *rowptr, const int *col, const do
         // G = 8: 7..20 entries per row -> 6 slots per lane, one staging pass per tile
         const int g = (n + 255) / 256;
         if (G <= 4) {
-            if (acc) k_csr_mv_tile<256, true, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
-            else k_csr_mv_tile<256, false, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+            if (acc) k_csr_mv_tile<256, true, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+            else k_csr_mv_tile<256, false, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
         } else {
-            if (acc) k_csr_mv_tile<256, true, 6><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
-            else k_csr_mv_tile<256, false, 6><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done);
+            if (acc) k_csr_mv_tile<256, true, 6><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+            else k_csr_mv_tile<256, false, 6><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
         }
         return;
     }
@@ -2295,6 +2309,16 @@ SideStream::~SideStream()
     if (cs) (void)hipStreamDestroy(cs);
 }
 
+// XFK_NO_COL16=1: level 0 reads 32-bit column indices
+static bool col16_on()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_NO_COL16");
+        return !(e && std::atoi(e) != 0);
+    }();
+    return v;
+}
+
 // XFK_NO_SIDE_SETUP=1: every setup step on the main stream
 static bool side_setup_on()
 {
@@ -2350,6 +2374,7 @@ int Amg::init(hipStream_t s)
     if (L.empty()) L.emplace_back(new AmgLevel());
     for (auto &lv : L) {   // levels are rebuilt: none sharded until setup_dist says so
         lv->dist = false;
+        lv->has16 = false;
         lv->plan = HaloPlan();
         lv->ts.B = 0;
     }
@@ -2396,6 +2421,19 @@ static int transpose_csr(DBuf<int> &cnt, DBuf<char> &tmp, hipStream_t s, int n, 
     if (n > 0) k_rt_fill<<<nb(n), kB, 0, s>>>(n, mrow, mcol, trow, cnt.p, tcol);
     if (nc > 0)
         k_rt_sort_vals<<<(int)(((long long)nc * 64 + 255) / 256), 256, 0, s>>>(nc, trow, tcol, mrow, mcol, mval, tval);
+    AMG_CHECK(hipGetLastError());
+    return XFK_OK;
+}
+
+// 16-bit tile columns (xfk_spmv.h) of an n-row CSR in tiles of B rows, on st
+template <int B>
+static int build_col16(hipStream_t st, int n, const int *rowptr, const int *col, long long nnz,
+                       DBuf<unsigned short> &c16, DBuf<int> &base)
+{
+    const int nt = (n + B - 1) / B;
+    AMG_CHECK(c16.alloc((size_t)std::max(1LL, nnz)));
+    AMG_CHECK(base.alloc((size_t)std::max(1, nt)));
+    if (nt > 0) k_tile_col16<B><<<nt, 256, 0, st>>>(n, rowptr, col, c16.p, base.p);
     AMG_CHECK(hipGetLastError());
     return XFK_OK;
 }
@@ -2505,6 +2543,9 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     }
     if ((rc = transpose_csr(off ? cnt2 : cnt, off ? cub_tmp2 : cub_tmp, ts, n, (int)nc, A.prow.p, A.pcol.p,
                             A.pval.p, A.rrow.p, A.rcol.p, A.rval.p)) != XFK_OK)
+        return rc;
+    if (l == 0 && A.has16 &&
+        (rc = build_col16<256>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)) != XFK_OK)
         return rc;
     if (off) {
         AMG_CHECK(hipEventRecord(sw.b, sw.cs));
@@ -2751,6 +2792,23 @@ int Amg::build(hipStream_t s, int l0)
             dense_coarse = true;
             break;
         }
+        // level 0 (single device): 16-bit tile columns of A for the SpMV and
+        // the sweeps, built off the critical path (they are read from the
+        // first V-cycle on, after the join at the end of the build)
+        A.has16 = l == 0 && !A.dist && !dist && (col16 < 0 ? col16_on() : col16 != 0);
+        if (A.has16) {
+            hipStream_t as = s;
+            if (side_setup_on()) {
+                int rc0 = sw.init();
+                if (rc0 != XFK_OK) return rc0;
+                AMG_CHECK(hipEventRecord(sw.a, s));
+                AMG_CHECK(hipStreamWaitEvent(sw.cs, sw.a, 0));
+                as = sw.cs;
+                sw_used = true;
+            }
+            int rc0 = build_col16<kCgBlock>(as, n, A.rowptr, A.col, A.nnz, A.a16, A.a16b);
+            if (rc0 != XFK_OK) return rc0;
+        }
         AMG_CHECK(sflag.alloc((size_t)A.nnz));
         AMG_CHECK(rho_part.alloc(2 * (size_t)nb_str(n)));
         k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
@@ -2814,6 +2872,9 @@ int Amg::build(hipStream_t s, int l0)
                 k_fold_p<<<(int)(((long long)n * kFoldLanes + 255) / 256), 256, 0, fs>>>(
                     n, rho.p + 2 * l, A.dinv.p, ap_row.p, ap_col.p, ap_val.p, A.prow.p, A.pcol.p, A.pval.p, A.ftcol.p,
                     A.ftval.p);
+            if (l == 0 && A.has16 &&
+                (rc = build_col16<kCgBlock>(fs, n, A.ftrow.p, A.ftcol.p, ap_nnz, A.f16, A.f16b)) != XFK_OK)
+                return rc;
             if (off) {
                 AMG_CHECK(hipEventRecord(sw.c, sw.cs));
                 fold_pending = true;
@@ -3382,7 +3443,8 @@ void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned lon
     if (l == 0) {
         const int g = tl ? nt : (A.n + kCgBlock - 1) / kCgBlock;
         k_amg_smooth<MODE, kCgBlock><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p,
-                                                            rho, b, x, out, rout, done, part_gam, tl);
+                                                            rho, b, x, out, rout, done, part_gam, tl,
+                                                            A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr);
         return;
     }
     if (A.n >= kTileMinRows) {
@@ -3432,7 +3494,9 @@ void launch_fold_pre_a(hipStream_t s, const AmgLevel &A, const unsigned long lon
                        double *bc, const int *done)
 {
     const int GB = lanes_wide(A.nc > 0 ? (double)A.fnnz / A.nc : 1.0);
-    const int ga = (int)(((long long)A.n * GA + 255) / 256);
+    // (the first range padded to whole rounds of the 8 XCDs, so both ranges
+    // take the XCD-contiguous block order)
+    const int ga = (int)(((((long long)A.n * GA + 255) / 256) + 7) & ~7LL);
     const int gb = (int)(((long long)A.nc * GB + 255) / 256);
 #define XFK_FOLD(GG)                                                                                               \
     k_fold_pre<GA, GG><<<ga + gb, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, y,   \
@@ -3466,7 +3530,7 @@ int smooth_tile(int l, const AmgLevel &A) { return l == 0 ? kCgBlock : (A.n >= k
 // matrix stream, the gathered operand once, b / D^-1, the written vectors
 static double smooth_bytes(const AmgLevel &A, int mode)
 {
-    const double n = A.n, base = 12.0 * (double)A.nnz + 4.0 * (n + 1);
+    const double n = A.n, base = (A.has16 ? 10.0 : 12.0) * (double)A.nnz + 4.0 * (n + 1);
     const bool implicit = mode == kSweepFromZero || mode == kResidFromZero;
     const double rd = (implicit ? 2.0 : 3.0) * 8.0 * n;
     const double wr = (mode == kResidFromZero && !A.fold ? 2.0 : 1.0) * 8.0 * n;
@@ -3551,16 +3615,17 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     }
     AmgLevel &C = *M.L[l + 1];
     const long long rnnz = A.pnnz;
-    XFK_PHASE(lv + "restriction R r", 12.0 * rnnz + 4.0 * (A.nc + 1) + 8.0 * A.n + 8.0 * A.nc,
+    XFK_PHASE(lv + "restriction R r", (A.has16 ? 10.0 : 12.0) * rnnz + 4.0 * (A.nc + 1) + 8.0 * A.n + 8.0 * A.nc,
               launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false, lanes_for((double)rnnz / A.nc),
-                        done));
+                        done, A.has16 ? A.r16.p : nullptr, A.has16 ? A.r16b.p : nullptr));
     const double *xc = vcycle_level(M, s, l + 1, C.b.p, nullptr, done);
     if (A.fold && l == 0 && nu == 1) {
         const double n = A.n, f = (double)A.fnnz;
         XFK_PHASE(lv + "folded post: u = x + w D^-1 r + P~ xc" + (part_gam ? " (+ r.u partials)" : ""),
-                  12.0 * f + 4.0 * (n + 1) + 8.0 * A.nc + 32.0 * n,
+                  (A.has16 ? 10.0 : 12.0) * f + 4.0 * (n + 1) + 8.0 * A.nc + 32.0 * n,
                   (k_fold_post0<kCgBlock, 2><<<(A.n + kCgBlock - 1) / kCgBlock, kCgBlock, 0, s>>>(
-                      A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xc, A.dinv.p, rho, A.r.p, b, out0, done, part_gam)));
+                      A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xc, A.dinv.p, rho, A.r.p, b, out0, done, part_gam,
+                      A.has16 ? A.f16.p : nullptr, A.has16 ? A.f16b.p : nullptr)));
         if (part_gam) M.gamma_done = true;
         return out0;
     }

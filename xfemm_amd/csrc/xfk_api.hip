@@ -437,11 +437,17 @@ int build_symbolic(xfk_problem *P)
     launch_mark_fix_adj(s, N, P->rowptr.p, P->col.p, P->fixed.p, T.flag);
     XFK_CHECK(P->fix_cols_row.alloc(N));
     launch_compact_flags(s, N, T.flag, T.cnt + 1, P->fix_cols_row.p);
-    XFK_CHECK(hipMemcpyAsync(P->hpin + 2, T.cnt, sizeof(int) * 2, hipMemcpyDeviceToHost, s));
-    XFK_CHECK(hipStreamSynchronize(s));
-    const int hc[2] = {P->hpin[2], P->hpin[3]};
-    XFK_REQUIRE(hc[0] == 0, XFK_ERR_HIP, "internal: element slot missing from the CSR pattern");
-    P->nfix_cols = hc[1];
+    if (P->harmonic) {   // (its Dirichlet kernels and the slot check read the counts on the host)
+        XFK_CHECK(hipMemcpyAsync(P->hpin + 2, T.cnt, sizeof(int) * 2, hipMemcpyDeviceToHost, s));
+        XFK_CHECK(hipStreamSynchronize(s));
+        const int hc[2] = {P->hpin[2], P->hpin[3]};
+        XFK_REQUIRE(hc[0] == 0, XFK_ERR_HIP, "internal: element slot missing from the CSR pattern");
+        P->nfix_cols = hc[1];
+    } else {             // static paths: the count stays on the device (no host check)
+        XFK_CHECK(P->nfix_dev.alloc(1));
+        XFK_CHECK(hipMemcpyAsync(P->nfix_dev.p, T.cnt + 1, sizeof(int), hipMemcpyDeviceToDevice, s));
+        P->nfix_cols = -1;
+    }
     XFK_CHECK(P->mu1.alloc(NE));
     XFK_CHECK(P->mu2.alloc(NE));
     if (!P->harmonic) {
@@ -584,7 +590,8 @@ int build_symbolic(xfk_problem *P)
     XFK_CHECK(P->nws.alloc(1));
     int rc2 = alloc_cg(P);
     if (rc2 != XFK_OK) return rc2;
-    XFK_CHECK(hipStreamSynchronize(s));
+    // (no host check: the host reads nothing more of this phase; host-side
+    // staging vectors above were uploaded synchronously or checked already)
     P->symbolic_ready = true;
     return XFK_OK;
 }
@@ -632,8 +639,8 @@ static int assemble(xfk_problem *P, int iter)
     std::swap(P->mu2.n, P->mu2b.n);
     launch_add_at_slots(s, P->age_n, P->age_slot.p, P->age_v.p, P->val.p);   // air-gap elements
     launch_point_currents(s, P->npt, P->pt_nodes.p, P->pt_J.p, P->b.p);
-    launch_dirichlet(s, P->nfix_rows, P->fix_rows.p, P->nfix_cols, P->fix_cols_row.p, P->rowptr.p, P->col.p,
-                     P->diag.p, P->fixed.p, P->fix_first.p, P->fix_last.p, P->val.p, P->b.p);
+    launch_dirichlet(s, P->nfix_rows, P->fix_rows.p, P->nfix_cols, P->nfix_dev.p, P->N, P->fix_cols_row.p,
+                     P->rowptr.p, P->col.p, P->diag.p, P->fixed.p, P->fix_first.p, P->fix_last.p, P->val.p, P->b.p);
     launch_map(s, P->pm_n, P->pm_dst.p, P->pm_ptr.p, P->pm_src.p, P->pm_w.p, P->val.p, P->pm_tmp.p);
     launch_map(s, P->pb_n, P->pb_dst.p, P->pb_ptr.p, P->pb_src.p, P->pb_w.p, P->b.p, P->pb_tmp.p);
     XFK_CHECK(hipGetLastError());
@@ -747,6 +754,7 @@ static int amg_setup(xfk_problem *P)
     P->amg->rep_rows = P->amg_replicate;
     P->amg->dense_max = P->amg_dense;
     P->amg->fold_on = P->amg_fold;
+    P->amg->col16 = P->amg_col16;
     // setup time: an event pair per setup, read after the solve's final
     // synchronisation (no host check here); callers that never read them
     // recycle the pairs; a full pool (> 64 fresh builds in one solve) is
@@ -788,6 +796,19 @@ static int amg_setup(xfk_problem *P)
     return XFK_OK;
 }
 
+// the 16-bit tile columns of the operator (built with the AMG hierarchy on a
+// single device: the SpMV reads A's pattern through them), or nulls
+static void spmv_col16(const xfk_problem *P, const unsigned short *&c16, const int *&cbase)
+{
+    c16 = nullptr;
+    cbase = nullptr;
+    if (P->pc_used != XFK_PRECOND_AMG || !P->amg || P->amg->L.empty()) return;
+    const AmgLevel &L0 = *P->amg->L[0];
+    if (!L0.has16 || L0.rowptr != P->rowptr.p || L0.col != P->col.p) return;
+    c16 = L0.a16.p;
+    cbase = L0.a16b.p;
+}
+
 static int pcg_start(xfk_problem *P, int flag)
 {
     hipStream_t s = P->stream;
@@ -826,8 +847,11 @@ static int pcg_start(xfk_problem *P, int flag)
             launch_cg_dot(s, N, P->b.p, A0.U, P->part_loc.p + 3 * G);
         }
         if ((rc = exchange(P, A0.U)) != XFK_OK) return rc;
+        const unsigned short *c16;
+        const int *cbase;
+        spmv_col16(P, c16, cbase);
         launch_cg_spmv(s, N, P->rowptr.p, P->col.p, P->val.p, A0.U, P->W2.p, P->part_loc.p + 2 * G, nullptr, A0.R,
-                       P->part_loc.p);
+                       P->part_loc.p, nullptr, 0, c16, cbase);
         return allreduce_partials(P, 4);
     }
     if ((rc = exchange(P, A0.U)) != XFK_OK) return rc;
@@ -876,10 +900,13 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
     rc = exchange(P, A.U);
     if (rc != XFK_OK) return rc;
     if (stamp) XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used], s));
-    const double spmv_bytes = 12.0 * (double)P->nnz_own + 4.0 * (N + 1) + (gam ? 24.0 : 16.0) * N;
+    const unsigned short *c16;
+    const int *cbase;
+    spmv_col16(P, c16, cbase);
+    const double spmv_bytes = (c16 ? 10.0 : 12.0) * (double)P->nnz_own + 4.0 * (N + 1) + (gam ? 24.0 : 16.0) * N;
     XFK_PHASE("PCG SpMV w = A u", spmv_bytes,
               launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G, St, Rg,
-                             pg));
+                             pg, nullptr, 0, c16, cbase));
     if (stamp) {
         XFK_CHECK(hipEventRecord(P->spmv_ev[P->spmv_used + 1], s));
         P->spmv_used += 2;
@@ -1527,9 +1554,9 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     XFK_REQUIRE(!P->harmonic, XFK_ERR_ARG, "harmonic problem: use xfk_harmonic2d");
     XFK_CHECK(hipSetDevice(P->device));
     hipStream_t s = P->stream;
-    ScopedEvents<3> ev;
+    ScopedEvents<5> ev;
     XFK_CHECK(ev.create());
-    hipEvent_t e0 = ev[0], e1 = ev[1], e2 = ev[2];
+    hipEvent_t e0 = ev[0], e1 = ev[1], e2 = ev[2], es0 = ev[3], es1 = ev[4];
     xfk_result R{};
     int rc = XFK_OK;
     float ms = 0;
@@ -1544,16 +1571,13 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     P->last.amg_op_complexity = 0;
     P->setup_used = 0;
     P->setup_ms_pending = 0;
-    XFK_CHECK(hipEventRecord(e0, s));
+    XFK_CHECK(hipEventRecord(es0, s));
     if (!P->symbolic_ready || (flags & XFK_REBUILD_SYMBOLIC)) {
         P->symbolic_ready = false;
         rc = build_symbolic(P);
         if (rc != XFK_OK) return rc;
     }
-    XFK_CHECK(hipEventRecord(e1, s));
-    XFK_CHECK(hipEventSynchronize(e1));
-    XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
-    R.ms_symbolic = ms;
+    XFK_CHECK(hipEventRecord(es1, s));   // (read after the solve: no host check here)
 
     const int N = P->N;
     XFK_CHECK(hipMemsetAsync(P->V.p, 0, sizeof(double) * P->NL, s));   // CBigLinProb::Create: V = 0
@@ -1615,6 +1639,8 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
         }
     }
     XFK_CHECK(hipStreamSynchronize(s));
+    XFK_CHECK(hipEventElapsedTime(&ms, es0, es1));
+    R.ms_symbolic = ms;
     for (int k = 0; k < P->setup_used; ++k) {
         float m = 0;
         XFK_CHECK(hipEventElapsedTime(&m, P->setup_ev[2 * k], P->setup_ev[2 * k + 1]));
@@ -1698,6 +1724,24 @@ int xfk_get_circuits(xfk_problem *P, int *ccase, double *J, double *dV)
 
 long long xfk_get_nnz(xfk_problem *P) { return P ? P->nnz_own : -1; }
 
+double xfk_spmv_col_bytes(xfk_problem *P)
+{
+    if (!P) return -1.0;
+    const unsigned short *c16;
+    const int *cbase;
+    spmv_col16(P, c16, cbase);
+    if (!c16 || P->nnz_own <= 0) return 4.0;
+    const int N = P->N, nt = (N + kCgBlock - 1) / kCgBlock;
+    std::vector<int> base(nt), rp(N + 1);
+    if (d2h(base.data(), cbase, sizeof(int) * nt, P->stream) != hipSuccess ||
+        d2h(rp.data(), P->rowptr.p, sizeof(int) * (N + 1), P->stream) != hipSuccess)
+        return -1.0;
+    long long wide = 0;
+    for (int t = 0; t < nt; ++t)
+        if (base[t] == kNoColBase) wide += rp[std::min(N, (t + 1) * kCgBlock)] - rp[t * kCgBlock];
+    return (2.0 * (double)P->nnz_own + 2.0 * (double)wide) / (double)P->nnz_own;
+}
+
 int xfk_get_csr(xfk_problem *P, int *rowptr, int *col, double *val, double *b)
 {
     XFK_REQUIRE(P && P->symbolic_ready, XFK_ERR_ARG, "no assembled system");
@@ -1760,6 +1804,10 @@ int xfk_set_option(xfk_problem *P, int option, double value)
     case XFK_OPT_AMG_FOLD:
         XFK_REQUIRE(value == 0 || value == 1, XFK_ERR_ARG, "AMG fold is 0 or 1");
         P->amg_fold = (int)value;
+        return XFK_OK;
+    case XFK_OPT_AMG_COL16:
+        XFK_REQUIRE(value == 0 || value == 1, XFK_ERR_ARG, "AMG 16-bit columns is 0 or 1");
+        P->amg_col16 = (int)value;
         return XFK_OK;
     default:
         set_error("unknown option");

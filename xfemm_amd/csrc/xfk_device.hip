@@ -803,14 +803,11 @@ __global__ void k_dirichlet_rows(int n, const int *__restrict__ rows, const int 
 }
 
 // the column half of SetValue: b[k] -= A(k,i)*x_i, A(k,i) = 0 (first value set)
-__global__ void k_dirichlet_cols(int n, const int *__restrict__ rows, const int *__restrict__ rowptr,
-                                 const int *__restrict__ col, const unsigned char *__restrict__ fixed,
-                                 const double *__restrict__ fix_first, double *__restrict__ val,
-                                 double *__restrict__ b)
+__device__ __forceinline__ void dirichlet_col_row(int r, const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                  const unsigned char *__restrict__ fixed,
+                                                  const double *__restrict__ fix_first, double *__restrict__ val,
+                                                  double *__restrict__ b)
 {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    int r = rows[t];
     double br = b[r];
     for (int k = rowptr[r]; k < rowptr[r + 1]; ++k) {
         int c = col[k];
@@ -823,6 +820,26 @@ __global__ void k_dirichlet_cols(int n, const int *__restrict__ rows, const int 
         }
     }
     b[r] = br;
+}
+__global__ void k_dirichlet_cols(int n, const int *__restrict__ rows, const int *__restrict__ rowptr,
+                                 const int *__restrict__ col, const unsigned char *__restrict__ fixed,
+                                 const double *__restrict__ fix_first, double *__restrict__ val,
+                                 double *__restrict__ b)
+{
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    dirichlet_col_row(rows[t], rowptr, col, fixed, fix_first, val, b);
+}
+// the same with the row count on the device (left there by the symbolic
+// phase: no host read-back), grid-stride
+__global__ void k_dirichlet_cols_d(const int *__restrict__ count, const int *__restrict__ rows,
+                                   const int *__restrict__ rowptr, const int *__restrict__ col,
+                                   const unsigned char *__restrict__ fixed, const double *__restrict__ fix_first,
+                                   double *__restrict__ val, double *__restrict__ b)
+{
+    const int n = *count;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
+        dirichlet_col_row(rows[t], rowptr, col, fixed, fix_first, val, b);
 }
 
 // (anti)periodic averaging map (CBigLinProb::Periodicity / AntiPeriodicity,
@@ -1008,11 +1025,17 @@ void launch_point_currents(hipStream_t s, int n, const int *nodes, const double 
 {
     if (n) k_point_currents<<<nblk(n), kBlock, 0, s>>>(n, nodes, J, b);
 }
-void launch_dirichlet(hipStream_t s, int nrows, const int *rows, int nadj, const int *adj, const int *rowptr,
-                      const int *col, const int *diag, const unsigned char *fixed, const double *fix_first,
-                      const double *fix_last, double *val, double *b)
+void launch_dirichlet(hipStream_t s, int nrows, const int *rows, int nadj, const int *nadj_dev, int nadj_max,
+                      const int *adj, const int *rowptr, const int *col, const int *diag, const unsigned char *fixed,
+                      const double *fix_first, const double *fix_last, double *val, double *b)
 {
-    if (nadj) k_dirichlet_cols<<<nblk(nadj), kBlock, 0, s>>>(nadj, adj, rowptr, col, fixed, fix_first, val, b);
+    if (nadj < 0) {   // count on the device, at most nadj_max
+        if (nadj_max > 0)
+            k_dirichlet_cols_d<<<std::min(nblk(nadj_max), 1024), kBlock, 0, s>>>(nadj_dev, adj, rowptr, col, fixed,
+                                                                              fix_first, val, b);
+    } else if (nadj) {
+        k_dirichlet_cols<<<nblk(nadj), kBlock, 0, s>>>(nadj, adj, rowptr, col, fixed, fix_first, val, b);
+    }
     if (nrows) k_dirichlet_rows<<<nblk(nrows), kBlock, 0, s>>>(nrows, rows, rowptr, diag, val, b, fix_last);
 }
 void launch_add_at_slots(hipStream_t s, int n, const int *slot, const double *v, double *data)

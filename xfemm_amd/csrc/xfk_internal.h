@@ -313,7 +313,8 @@ struct xfk_problem {
     xfk::DBuf<int> fix_cols;         // slots (k, c) with c fixed, k not fixed
     xfk::DBuf<int> fix_cols_node;    // the fixed column c of each such slot
     xfk::DBuf<int> fix_cols_row;     // row k of each such slot
-    int nfix_cols = 0;
+    int nfix_cols = 0;                // -1: the count is on the device (nfix_dev)
+    xfk::DBuf<int> nfix_dev;
     // periodic map: dst <- sum_s w_s * src_s (values), and the same for b
     xfk::DBuf<int> pm_dst, pm_ptr, pm_src;
     xfk::DBuf<double> pm_w, pm_tmp;
@@ -370,6 +371,7 @@ struct xfk_problem {
     int amg_replicate = 250000;
     int amg_dense = 2048;
     int amg_fold = -1;                // XFK_OPT_AMG_FOLD (-1: the XFK_AMG_FOLD environment default)
+    int amg_col16 = -1;               // XFK_OPT_AMG_COL16 (-1: on unless XFK_NO_COL16)
     int amg_reuse = 1;
     bool amg_reusable = false;        // the hierarchy belongs to this solve's matrix pattern
     bool amg_fresh = false;           // built from scratch for the running PCG solve

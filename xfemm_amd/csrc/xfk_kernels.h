@@ -52,9 +52,11 @@ void launch_cg_init_r(hipStream_t s, int N, int flag, const int *rowptr, const i
                       double *part_reso, double *part_gam0);
 void launch_cg_axpy(hipStream_t s, const CgAxpyArgs &A);
 // w = A u, partials of u.w (and of r.u into part_gam when R != nullptr)
+// c16 / cbase: 16-bit column offsets per 512-row tile (AmgLevel::a16), or null
 void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *U,
                     double *W, double *part_del, const CgState *S, const double *R = nullptr,
-                    double *part_gam = nullptr, const int *tiles = nullptr, int ntiles = 0);
+                    double *part_gam = nullptr, const int *tiles = nullptr, int ntiles = 0,
+                    const unsigned short *c16 = nullptr, const int *cbase = nullptr);
 void launch_cg_dot(hipStream_t s, int N, const double *a, const double *b, double *part);
 
 void launch_count_incidence(hipStream_t s, int NE, const int *p, int *deg);
@@ -86,9 +88,10 @@ void launch_compact_flags(hipStream_t s, int N, const int *flag, int *cursor, in
 // one thread per owned row, contributions of the incident elements in element order
 void launch_assemble_rows(hipStream_t s, int N, const AssembleArgs &A);
 void launch_point_currents(hipStream_t s, int n, const int *nodes, const double *J, double *b);
-void launch_dirichlet(hipStream_t s, int nrows, const int *rows, int nadj, const int *adj, const int *rowptr,
-                      const int *col, const int *diag, const unsigned char *fixed, const double *fix_first,
-                      const double *fix_last, double *val, double *b);
+// nadj < 0: the count of rows adjacent to fixed nodes is *nadj_dev (at most nadj_max)
+void launch_dirichlet(hipStream_t s, int nrows, const int *rows, int nadj, const int *nadj_dev, int nadj_max,
+                      const int *adj, const int *rowptr, const int *col, const int *diag, const unsigned char *fixed,
+                      const double *fix_first, const double *fix_last, double *val, double *b);
 void launch_map(hipStream_t s, int n, const int *dst, const int *ptr, const int *src, const double *w,
                 double *data, double *tmp);
 void launch_diag_inv(hipStream_t s, int N, const int *diag, const double *val, double *dinv, CgState *S);

@@ -78,7 +78,8 @@ __global__ void __launch_bounds__(kCgBlock) k_cg_spmv(int N, const int *__restri
                                                       const double *__restrict__ U, double *__restrict__ W,
                                                       double *__restrict__ part_del, const CgState *S,
                                                       const double *__restrict__ R, double *__restrict__ part_gam,
-                                                      const int *__restrict__ tl)
+                                                      const int *__restrict__ tl, const unsigned short *__restrict__ c16,
+                                                      const int *__restrict__ cbase)
 {
     // the convergence flag, the tile's row range and this row's u, r are
     // loaded together before the first branch (one memory latency, not two)
@@ -89,9 +90,10 @@ __global__ void __launch_bounds__(kCgBlock) k_cg_spmv(int N, const int *__restri
     const int r0 = t * kCgBlock;
     const int r = r0 + threadIdx.x;
     const TileRows tr = tile_rows(r0, N, rowptr);
+    const int cb = load_col_base(cbase, t);
     const double u = r < N ? U[r] : 0.0, rr = (R && r < N) ? R[r] : 0.0;
     if (dn) return;
-    const double w = cg_tile_spmv(tr, col, val, [&](int j) { return U[j]; }, lds);
+    const double w = cg_tile_spmv16(tr, c16, cb, col, val, [&](int j) { return U[j]; }, lds);
     double d = 0.0, g = 0.0;
     if (r < N) {
         W[r] = w;
@@ -275,11 +277,11 @@ void launch_cg_axpy(hipStream_t s, const CgAxpyArgs &A)
 
 void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, const double *val, const double *U,
                     double *W, double *part_del, const CgState *S, const double *R, double *part_gam,
-                    const int *tiles, int ntiles)
+                    const int *tiles, int ntiles, const unsigned short *c16, const int *cbase)
 {
     if (tiles && ntiles == 0) return;
     k_cg_spmv<<<tiles ? ntiles : cg_grid(N), kCgBlock, 0, s>>>(N, rowptr, col, val, U, W, part_del, S, R, part_gam,
-                                                               tiles);
+                                                               tiles, c16, cbase);
 }
 
 // partials of a.b over the cg_grid(N) layout (the AMG start: (M^-1 b).b)

@@ -62,18 +62,6 @@ __device__ __forceinline__ int xcd_tile(int b, int nb)
     return x * q + min(x, r) + k;
 }
 
-// y = sum_k val[k] * X(col[k]) for the B rows of one tile (B threads, one
-// row each); CSR-stream: the tile's products are staged through LDS by
-// coalesced 16-B reads -- each lane takes 4 consecutive nonzeros per slot (one
-// int4 of col, two double2 of val; the stream realigned to 4 entries, the
-// partial quads at its ends read per entry), 2 slots per lane per pass -- then
-// each thread sums its own row in order.  Measured on the configs[2] matrix
-// (tools/lab/spmv_lab.hip): 16.5 us vs 19.9 us for one 4/8-B entry per lane,
-// bit-identical sums.  col / val must be 16-B aligned (hipMalloc'd arrays).
-// SLOTS: 4-entry slots per lane per pass (CAP = 4 SLOTS B products staged per
-// pass, lds holds CAP doubles): 2 for the ~7 entries per row of the fine
-// level, more for the longer rows of coarse levels and of R, so that a tile
-// takes one pass (each pass is a load / barrier / sum / barrier round trip)
 // a device flag read as a per-lane (vector) load: a scalar load would be
 // waited for together with the kernel arguments (the scalar cache's counter
 // is waited to zero), before any other load is issued; as a vector load it
@@ -88,6 +76,16 @@ __device__ __forceinline__ int load_flag_v(const int *p)
     int z = 0;
     asm volatile("" : "+v"(z));
     const int *q = p ? p : &xfk_zero_flag;
+    return q[z];
+}
+
+// a tile's column base (kNoColBase without 16-bit offsets), read like a flag
+static __device__ int xfk_no_col_base = -2147483647 - 1;
+__device__ __forceinline__ int load_col_base(const int *base, int t)
+{
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    const int *q = base ? base + t : &xfk_no_col_base;
     return q[z];
 }
 
@@ -115,9 +113,27 @@ __device__ __forceinline__ TileRows tile_rows(int r0, int N, const int *__restri
     return t;
 }
 
-template <int B = kCgBlock, int SLOTS = 2, class XF>
-__device__ __forceinline__ double cg_tile_spmv(const TileRows &tr, const int *__restrict__ col,
-                                               const double *__restrict__ val, XF X, double *lds)
+// y = sum_k val[k] * X(col[k]) for the B rows of one tile (B threads, one
+// row each); CSR-stream: the tile's products are staged through LDS by
+// coalesced 16-B reads -- each lane takes 4 consecutive nonzeros per slot (one
+// int4 of col, two double2 of val; the stream realigned to 4 entries, the
+// partial quads at its ends read per entry), 2 slots per lane per pass -- then
+// each thread sums its own row in order.  Measured on the configs[2] matrix
+// (tools/lab/spmv_lab.hip): 16.5 us vs 19.9 us for one 4/8-B entry per lane,
+// bit-identical sums.  col / val must be 16-B aligned (hipMalloc'd arrays).
+// SLOTS: 4-entry slots per lane per pass (CAP = 4 SLOTS B products staged per
+// pass, lds holds CAP doubles): 2 for the ~7 entries per row of the fine
+// level, more for the longer rows of coarse levels and of R, so that a tile
+// takes one pass (each pass is a load / barrier / sum / barrier round trip)
+// Columns come either as the CSR's int array or as 16-bit offsets from a
+// per-tile base (TileCols16: 2 B instead of 4 B per nonzero, the same column
+// indices, so the same bits); a tile whose columns span more than 65535
+// carries kNoColBase and reads the int array.
+constexpr int kNoColBase = -2147483647 - 1;
+
+template <int B, int SLOTS, class C4, class C1, class XF>
+__device__ __forceinline__ double tile_spmv_impl(const TileRows &tr, C4 cols4, C1 col1,
+                                                 const double *__restrict__ val, XF X, double *lds)
 {
     constexpr int CAP = 4 * SLOTS * B;
     const int s = __builtin_amdgcn_readfirstlane(tr.s), e = __builtin_amdgcn_readfirstlane(tr.e);
@@ -129,7 +145,7 @@ __device__ __forceinline__ double cg_tile_spmv(const TileRows &tr, const int *__
         for (int m = 0; m < SLOTS; ++m) {
             const int k = c0 + 4 * (threadIdx.x + m * B);
             if (k >= s && k + 3 < c1) {
-                const int4 c = *reinterpret_cast<const int4 *>(col + k);
+                const int4 c = cols4(k);
                 const double2 v0 = *reinterpret_cast<const double2 *>(val + k);
                 const double2 v1 = *reinterpret_cast<const double2 *>(val + k + 2);
                 lds[k - c0] = v0.x * X(c.x);
@@ -139,7 +155,7 @@ __device__ __forceinline__ double cg_tile_spmv(const TileRows &tr, const int *__
             } else {
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    if (k + q >= s && k + q < c1) lds[k + q - c0] = val[k + q] * X(col[k + q]);
+                    if (k + q >= s && k + q < c1) lds[k + q - c0] = val[k + q] * X(col1(k + q));
             }
         }
         __syncthreads();
@@ -151,11 +167,73 @@ __device__ __forceinline__ double cg_tile_spmv(const TileRows &tr, const int *__
 }
 
 template <int B = kCgBlock, int SLOTS = 2, class XF>
+__device__ __forceinline__ double cg_tile_spmv(const TileRows &tr, const int *__restrict__ col,
+                                               const double *__restrict__ val, XF X, double *lds)
+{
+    return tile_spmv_impl<B, SLOTS>(
+        tr, [&](int k) { return *reinterpret_cast<const int4 *>(col + k); }, [&](int k) { return col[k]; }, val, X,
+        lds);
+}
+
+// the same with 16-bit column offsets when the tile has a base (cb)
+template <int B = kCgBlock, int SLOTS = 2, class XF>
+__device__ __forceinline__ double cg_tile_spmv16(const TileRows &tr, const unsigned short *__restrict__ c16, int cb,
+                                                 const int *__restrict__ col, const double *__restrict__ val, XF X,
+                                                 double *lds)
+{
+    cb = __builtin_amdgcn_readfirstlane(cb);
+    if (cb == kNoColBase) return cg_tile_spmv<B, SLOTS>(tr, col, val, X, lds);
+    return tile_spmv_impl<B, SLOTS>(
+        tr,
+        [&](int k) {
+            const uint2 u = *reinterpret_cast<const uint2 *>(c16 + k);
+            return make_int4(cb + (int)(u.x & 0xffffu), cb + (int)(u.x >> 16), cb + (int)(u.y & 0xffffu),
+                             cb + (int)(u.y >> 16));
+        },
+        [&](int k) { return cb + (int)c16[k]; }, val, X, lds);
+}
+
+template <int B = kCgBlock, int SLOTS = 2, class XF>
 __device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restrict__ rowptr,
                                                const int *__restrict__ col, const double *__restrict__ val,
                                                XF X, double *lds)
 {
     return cg_tile_spmv<B, SLOTS>(tile_rows<B>(r0, N, rowptr), col, val, X, lds);
+}
+
+// Per-tile 16-bit column offsets of a CSR (tiles of B rows): base[t] = the
+// tile's smallest column, c16[k] = col[k] - base[t]; kNoColBase when the
+// tile's columns span more than 65535.  One workgroup per tile.
+template <int B>
+__global__ void __launch_bounds__(256) k_tile_col16(int n, const int *__restrict__ rowptr,
+                                                    const int *__restrict__ col, unsigned short *__restrict__ c16,
+                                                    int *__restrict__ base)
+{
+    __shared__ int red[2 * 4];
+    const int t = blockIdx.x, r0 = t * B, r1 = min(n, r0 + B);
+    const int s = rowptr[r0], e = rowptr[r1];
+    int lo = 2147483647, hi = -2147483647 - 1;
+    for (int k = s + threadIdx.x; k < e; k += 256) {
+        const int c = col[k];
+        lo = min(lo, c);
+        hi = max(hi, c);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off, 64));
+        hi = max(hi, __shfl_xor(hi, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = lo;
+        red[4 + (threadIdx.x >> 6)] = hi;
+    }
+    __syncthreads();
+    lo = min(min(red[0], red[1]), min(red[2], red[3]));
+    hi = max(max(red[4], red[5]), max(red[6], red[7]));
+    const bool fits = e == s || (long long)hi - lo <= 65535;
+    if (threadIdx.x == 0) base[t] = fits ? (e == s ? 0 : lo) : kNoColBase;
+    if (!fits) return;
+    for (int k = s + threadIdx.x; k < e; k += 256) c16[k] = (unsigned short)(col[k] - lo);
 }
 
 }  // namespace xfk

@@ -33,11 +33,12 @@ XFK_OPT_AMG_REPLICATE = 5
 XFK_OPT_AMG_REUSE = 6
 XFK_OPT_AMG_DENSE = 7
 XFK_OPT_AMG_FOLD = 8
+XFK_OPT_AMG_COL16 = 9
 
 # every symbol include/xfemm_kernels.h declares
 EXPORTED = (
     "xfk_last_error", "xfk_age_element_matrix", "xfk_device_count", "xfk_problem_create", "xfk_problem_destroy",
-    "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz",
+    "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz", "xfk_spmv_col_bytes",
     "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_solve_csr_pc", "xfk_pcg_time", "xfk_phase_profile",
     "xfk_set_option",
     "xfk_problem_create_harmonic", "xfk_harmonic2d", "xfk_get_solution_complex", "xfk_get_circuits_complex",
@@ -146,6 +147,8 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_get_csr.argtypes = [C.c_void_p, iptr, iptr, dptr, dptr]
     L.xfk_get_nnz.argtypes = [C.c_void_p]
     L.xfk_get_nnz.restype = C.c_longlong
+    L.xfk_spmv_col_bytes.argtypes = [C.c_void_p]
+    L.xfk_spmv_col_bytes.restype = C.c_double
     L.xfk_get_stream.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
     L.xfk_pcg_solve_csr.argtypes = [C.c_int, iptr, iptr, dptr, dptr, dptr, C.c_int, C.c_double, C.c_int,
                                     C.POINTER(C.c_longlong), dptr]
@@ -316,9 +319,12 @@ class Static2DProblem:
                  amg_theta: Optional[float] = None, frequency: float = 0.0, amg_omega: Optional[float] = None,
                  amg_replicate: Optional[int] = None, amg_reuse: Optional[bool] = None, problem_type: int = 0,
                  ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0, amg_dense: Optional[int] = None,
-                 ages: Sequence[dict] = (), ac_solver: int = 0, amg_fold: Optional[bool] = None):
+                 ages: Sequence[dict] = (), ac_solver: int = 0, amg_fold: Optional[bool] = None,
+                 amg_col16: Optional[bool] = None):
         """ac_solver: [ACSolver], read by the harmonic solvers only (ignored here).
         amg_fold: folded V(1,1) levels (default on; False: the plain cycle).
+        amg_col16: 16-bit tile column offsets on level 0 (default on; False:
+        int columns; the same bits either way).
         comm: shard the mesh by row blocks over this communicator (every rank
         passes the same global problem; solve() and solution() are collective).
         precond: "amg" (smoothed-aggregation V-cycle, default) or "jacobi".
@@ -355,6 +361,8 @@ class Static2DProblem:
             self.set_option(XFK_OPT_AMG_DENSE, amg_dense)
         if amg_fold is not None:
             self.set_option(XFK_OPT_AMG_FOLD, int(bool(amg_fold)))
+        if amg_col16 is not None:
+            self.set_option(XFK_OPT_AMG_COL16, int(bool(amg_col16)))
         self.n_rows = self.dist_info()["n_own"] if comm is not None else self.n_nodes
         self.result: Optional[Result] = None
 
@@ -397,6 +405,11 @@ class Static2DProblem:
         _check(_lib.xfk_get_circuits(self._h, cc.ctypes.data_as(iptr), J.ctypes.data_as(dptr),
                                      dV.ctypes.data_as(dptr)))
         return cc[:n], J[:n], dV[:n]
+
+    def spmv_col_bytes(self) -> float:
+        """Column-index bytes per nonzero of the last solve's PCG SpMV (2: the
+        AMG's 16-bit tile offsets, 4: int columns)."""
+        return float(_lib.xfk_spmv_col_bytes(self._h))
 
     def csr(self):
         """This rank's rows (all rows unless sharded; sharded columns are local ids)."""
