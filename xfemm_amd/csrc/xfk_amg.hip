@@ -58,6 +58,17 @@ __device__ __forceinline__ MisKey mis_key(MisKey st, int i) { return (st << 30) 
 __device__ __forceinline__ MisKey key_st(MisKey k) { return k >> 30; }
 __device__ __forceinline__ MisKey key_low(MisKey k) { return k & kKeyMask; }
 
+// The columns of a level's CSR as the aggregation reads them: the int array,
+// or (level 0) the 16-bit offsets from the row's 512-row tile base
+// (xfk_spmv.h k_tile_col16; a tile without a base reads the int array)
+struct ColView {
+    const int *col;
+    const unsigned short *c16;   // null: int columns only
+    const int *cbase;
+    __device__ __forceinline__ int base(int i) const { return c16 ? cbase[i / kCgBlock] : kNoColBase; }
+    __device__ __forceinline__ int at(int cb, int k) const { return cb != kNoColBase ? cb + (int)c16[k] : col[k]; }
+};
+
 __device__ __forceinline__ double rho_of(const unsigned long long *p)
 {
     return __longlong_as_double((long long)*p);
@@ -144,7 +155,7 @@ constexpr int kStrG = 4;
 inline int nb_str(long long n) { return nb(n * kStrG); }
 
 __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double theta, const int *__restrict__ rowptr,
-                                                     const int *__restrict__ col, const double *__restrict__ val,
+                                                     ColView cv, const double *__restrict__ val,
                                                      const double *__restrict__ absd,
                                                      unsigned char *__restrict__ sflag, int *__restrict__ sdeg,
                                                      double *__restrict__ dfinv, double *__restrict__ wF,
@@ -158,8 +169,9 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
     int deg = 0, hdeg = 0;
     if (i < n) {
         const double ai = absd[i];
+        const int cb = cv.base(i);
         for (int k = rowptr[i] + g; k < rowptr[i + 1]; k += kStrG) {
-            const int j = col[k];
+            const int j = cv.at(cb, k);
             const double a = val[k];
             unsigned char f = 0;
             if (j == i) {
@@ -247,7 +259,7 @@ __global__ void k_mis_init(int n, const int *__restrict__ sdeg, MisKey *__restri
 // maximum for good (decided rows never change): act[i] = 0 then, and later
 // rounds skip the row -- after the first rounds most of the level.
 template <int G>
-__global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+__global__ void k_mis_max(int n, const int *__restrict__ rowptr, ColView cv,
                           const unsigned char *__restrict__ sflag, const MisKey *__restrict__ in,
                           MisKey *__restrict__ out, const int *prev, int *cur, int *run,
                           unsigned char *__restrict__ act)
@@ -261,9 +273,10 @@ __global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__re
     if (i >= n || *prev == 0 || act[i] == 0) return;
     MisKey m = in[i];
     int any = key_st(m) == kStUnd;
+    const int cb = cv.base(i);
     for (int k = rowptr[i] + g; k < rowptr[i + 1]; k += G)
         if (sflag[k] == 1) {
-            const MisKey v = in[col[k]];
+            const MisKey v = in[cv.at(cb, k)];
             m = max(m, v);
             any |= key_st(v) == kStUnd;
         }
@@ -282,7 +295,7 @@ __global__ void k_mis_max(int n, const int *__restrict__ rowptr, const int *__re
 // distance-2 maximum is itself joins the set; one that sees a set member
 // within distance 2 leaves
 template <int G>
-__global__ void k_mis_update(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+__global__ void k_mis_update(int n, const int *__restrict__ rowptr, ColView cv,
                              const unsigned char *__restrict__ sflag, const MisKey *__restrict__ t1,
                              MisKey *__restrict__ key, const int *prev, int *undecided)
 {
@@ -292,8 +305,9 @@ __global__ void k_mis_update(int n, const int *__restrict__ rowptr, const int *_
     const MisKey k = key[i];
     if (key_st(k) != kStUnd) return;   // uniform over the row's lanes
     MisKey m = t1[i];
+    const int cb = cv.base(i);
     for (int q = rowptr[i] + g; q < rowptr[i + 1]; q += G)
-        if (sflag[q] == 1) m = max(m, t1[col[q]]);
+        if (sflag[q] == 1) m = max(m, t1[cv.at(cb, q)]);
 #pragma unroll
     for (int off = 1; off < G; off <<= 1) m = max(m, (MisKey)__shfl_xor((int)m, off, G));
     if (g != 0) return;
@@ -313,7 +327,7 @@ __global__ void k_agg_roots(int n, const MisKey *__restrict__ key, int *__restri
 // rows left out that have (weak) couplings to aggregated owned rows join the
 // aggregate of the largest |a_ij| (ties: larger j); their P row is the
 // tentative injection (no strong couplings -> smoothing weight 0)
-__global__ void k_agg_join3(int n, int ncl, const int *__restrict__ rowptr, const int *__restrict__ col,
+__global__ void k_agg_join3(int n, int ncl, const int *__restrict__ rowptr, ColView cv,
                             const double *__restrict__ val, const int *__restrict__ agg2, int *__restrict__ agg)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -322,8 +336,9 @@ __global__ void k_agg_join3(int n, int ncl, const int *__restrict__ rowptr, cons
     if (a < 0) {
         double best = 0.0;
         int bj = -1;
+        const int cb = cv.base(i);
         for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
-            const int j = col[k];
+            const int j = cv.at(cb, k);
             if (j == i || j >= ncl || agg2[j] < 0) continue;
             const double v = fabs(val[k]);
             if (v > best || (v == best && v > 0.0 && j > bj)) {
@@ -336,7 +351,7 @@ __global__ void k_agg_join3(int n, int ncl, const int *__restrict__ rowptr, cons
     agg[i] = a;
 }
 
-__global__ void k_agg_join1(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+__global__ void k_agg_join1(int n, const int *__restrict__ rowptr, ColView cv,
                             const unsigned char *__restrict__ sflag, const MisKey *__restrict__ key,
                             const int *__restrict__ rootid, int *__restrict__ agg1)
 {
@@ -348,9 +363,10 @@ __global__ void k_agg_join1(int n, const int *__restrict__ rowptr, const int *__
     }
     int bj = -1;
     MisKey best = 0;
+    const int cb = cv.base(i);
     for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
         if (sflag[k] != 1) continue;
-        const int j = col[k];
+        const int j = cv.at(cb, k);
         const MisKey kj = key[j];
         if (key_st(kj) == kStIn && (bj < 0 || key_low(kj) > best)) {
             best = key_low(kj);
@@ -362,7 +378,7 @@ __global__ void k_agg_join1(int n, const int *__restrict__ rowptr, const int *__
 
 // distance 2: the rest join the aggregate of their largest-key neighbour
 // that joined at distance 1
-__global__ void k_agg_join2(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+__global__ void k_agg_join2(int n, const int *__restrict__ rowptr, ColView cv,
                             const unsigned char *__restrict__ sflag, const MisKey *__restrict__ key,
                             const int *__restrict__ agg1, int *__restrict__ agg)
 {
@@ -375,9 +391,10 @@ __global__ void k_agg_join2(int n, const int *__restrict__ rowptr, const int *__
     }
     int bj = -1;
     MisKey best = 0;
+    const int cb = cv.base(i);
     for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
         if (sflag[k] != 1) continue;
-        const int j = col[k];
+        const int j = cv.at(cb, k);
         if (agg1[j] < 0) continue;
         const MisKey kl = key_low(key[j]);
         if (bj < 0 || kl > best) {
@@ -508,6 +525,8 @@ struct SgX {
     const unsigned char *mask;     // PMODE: sflag (1 strong, 2 diagonal)
     const double *dfinv;           // PMODE: D_F^-1
     const double *wF;              // PMODE: per-row smoothing weight
+    const unsigned short *c16 = nullptr;   // level 0: 16-bit tile columns (k_spgemm_sort reads them)
+    const int *cbase = nullptr;
 };
 struct SgY {
     const int *rowptr, *col;
@@ -765,6 +784,8 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
     int np = 0;
     if (live) {
         const int xs = X.rowptr[row], xe = X.rowptr[row + 1];
+        const ColView xc{X.col, X.c16, X.cbase};
+        const int cb = xc.base(row);
         double omega = 0.0, dfi = 0.0;
         if (PMODE) {
             omega = X.wF[row];
@@ -775,7 +796,7 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
             int len = 0, ys = 0;
             double xv = 0.0;
             if (e < xe) {
-                const int k = X.col[e];
+                const int k = xc.at(cb, e);
                 if (k < X.col_lim) {
                     if (PMODE) {
                         const unsigned char f = X.mask[e];
@@ -2442,6 +2463,7 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
 {
     AmgLevel &A = *L[l];
     const int n = A.n;
+    const ColView cv{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr};
     nc = 0;
     A.nc = 0;
     AMG_CHECK(key.alloc(n));
@@ -2465,12 +2487,12 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         for (int b = 0; b < batch; ++b, ++rounds) {
             int *cur = und2 + (rounds & 1), *prev = und2 + ((rounds + 1) & 1);
             if (A.nnz > 9LL * n) {
-                k_mis_max<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur, run,
+                k_mis_max<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run,
                                                          act.p);
-                k_mis_update<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, prev, cur);
+                k_mis_update<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur);
             } else {
-                k_mis_max<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, t1.p, prev, cur, run, act.p);
-                k_mis_update<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, t1.p, key.p, prev, cur);
+                k_mis_max<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run, act.p);
+                k_mis_update<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur);
             }
         }
         k_agg_roots<<<nb(n), kB, 0, s>>>(n, key.p, flag.p);
@@ -2496,9 +2518,9 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     }
     AMG_CHECK(agg1.alloc(n));
     AMG_CHECK(agg.alloc(n));
-    k_agg_join1<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, cursor.p, agg1.p);
-    k_agg_join2<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, sflag.p, key.p, agg1.p, agg.p);
-    k_agg_join3<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, A.rowptr, A.col, A.val, agg.p, agg1.p);
+    k_agg_join1<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, cursor.p, agg1.p);
+    k_agg_join2<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, agg1.p, agg.p);
+    k_agg_join3<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, A.rowptr, cv, A.val, agg.p, agg1.p);
     std::swap(agg.p, agg1.p);   // agg = the joined map
     std::swap(agg.n, agg1.n);
     if (g_prof) g_prof->end();
@@ -2520,7 +2542,7 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
                      ra, rf, rounds);
     }
     // P = (I - omega D_F^-1 A_F) P_tent
-    SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, wF.p};
+    SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, wF.p, cv.c16, cv.cbase};
     SgY YT{nullptr, nullptr, nullptr, agg.p};
     if (g_prof) g_prof->begin(lv + "P = (I - w D^-1 A) P_tent, R = P^T", 0.0);
     if ((rc = spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz, dist ? -1 : 4 * l)) != XFK_OK)
@@ -2796,22 +2818,15 @@ int Amg::build(hipStream_t s, int l0)
         // the sweeps, built off the critical path (they are read from the
         // first V-cycle on, after the join at the end of the build)
         A.has16 = l == 0 && !A.dist && !dist && (col16 < 0 ? col16_on() : col16 != 0);
-        if (A.has16) {
-            hipStream_t as = s;
-            if (side_setup_on()) {
-                int rc0 = sw.init();
-                if (rc0 != XFK_OK) return rc0;
-                AMG_CHECK(hipEventRecord(sw.a, s));
-                AMG_CHECK(hipStreamWaitEvent(sw.cs, sw.a, 0));
-                as = sw.cs;
-                sw_used = true;
-            }
-            int rc0 = build_col16<kCgBlock>(as, n, A.rowptr, A.col, A.nnz, A.a16, A.a16b);
+        if (A.has16) {   // (on the main stream: the aggregation reads them too)
+            int rc0 = build_col16<kCgBlock>(s, n, A.rowptr, A.col, A.nnz, A.a16, A.a16b);
             if (rc0 != XFK_OK) return rc0;
         }
         AMG_CHECK(sflag.alloc((size_t)A.nnz));
         AMG_CHECK(rho_part.alloc(2 * (size_t)nb_str(n)));
-        k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
+        k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr,
+                                                ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
+                                                A.val, absd.p, sflag.p, cnt.p,
                                                 dfinv.p, wF.p, rho_part.p);
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p + 2 * l);
         if (g_prof) g_prof->end();
@@ -2821,7 +2836,8 @@ int Amg::build(hipStream_t s, int l0)
         if (rc != XFK_OK) return rc;
         if (nc == 0) break;
         // AP = A P, then A_c = R (A P)
-        SgX XA{A.rowptr, A.col, A.val, A.ncol_lim, nullptr, nullptr, nullptr};
+        SgX XA{A.rowptr, A.col, A.val, A.ncol_lim, nullptr, nullptr, nullptr, A.has16 ? A.a16.p : nullptr,
+               A.has16 ? A.a16b.p : nullptr};
         SgY YP{A.prow.p, A.pcol.p, A.pval.p, nullptr};
         if (fold_pending) {   // the previous level's folded transfer still reads A P's buffers
             AMG_CHECK(hipStreamWaitEvent(s, sw.c, 0));
@@ -3107,8 +3123,8 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
         AMG_CHECK(sflag.alloc((size_t)std::max(1LL, A.nnz)));
         AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(nl))));
         k_amg_diag<<<nb(nl), kB, 0, s>>>(nl, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
-        k_amg_strength<<<nb_str(nl), kB, 0, s>>>(nl, nl, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
-                                                 dfinv.p, wF.p, rho_part.p);
+        k_amg_strength<<<nb_str(nl), kB, 0, s>>>(nl, nl, theta, A.rowptr, ColView{A.col, nullptr, nullptr}, A.val,
+                                                 absd.p, sflag.p, cnt.p, dfinv.p, wF.p, rho_part.p);
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(nl), rho_part.p, omega, rho.p + 2 * l);
         long long nc = 0;
         rc = aggregate(s, l, nc, false);
@@ -3717,7 +3733,9 @@ int Amg::refresh(hipStream_t s)
     AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(n))));
     if (n > 0) {
         k_amg_diag<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
-        k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr, A.col, A.val, absd.p, sflag.p, cnt.p,
+        k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr,
+                                                ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
+                                                A.val, absd.p, sflag.p, cnt.p,
                                                 dfinv.p, wF.p, rho_part.p);
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p);
     }
