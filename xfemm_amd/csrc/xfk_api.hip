@@ -1435,6 +1435,10 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     P->nlabels = (int)G.lab.size();
     P->nlines = d->n_lines;
     P->ncircs = d->n_circs;
+    // the AMG object and its setup side stream are resources of the problem,
+    // created with it (a stream's creation is not work of the first solve)
+    P->amg = new Amg();
+    if (P->amg->sw.init() != XFK_OK) return fail(XFK_ERR_HIP);
     *out = P;
     return XFK_OK;
 }
