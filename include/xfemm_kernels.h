@@ -177,10 +177,13 @@ enum {
     XFK_OPT_AMG_FOLD = 8,       /* 1 (default, or XFK_AMG_FOLD from the environment): V(1,1) levels
                                    run folded (one pass over P~ = (I - w D^-1 A) P for prolongation +
                                    post-sweep, coarse pre-steps with R~ = P~^T); 0: the plain cycle */
-    XFK_OPT_AMG_COL16 = 9       /* 1 (default, unless XFK_NO_COL16 is set): single-device level-0
+    XFK_OPT_AMG_COL16 = 9,      /* 1 (default, unless XFK_NO_COL16 is set): single-device level-0
                                    operators (the PCG SpMV, the sweeps, P~, R) read 16-bit column
                                    offsets per row tile (tiles spanning > 65535 columns read the int
                                    columns); 0: int columns.  The same column indices: the same bits. */
+    XFK_OPT_AMG_WLEVEL = 10     /* the folded coarse level that runs a W-cycle (two coarse
+                                   corrections); -2 (default): the level above the last V-cycle
+                                   level (XFK_AMG_W overrides), -1: a plain V-cycle */
 };
 int xfk_set_option(xfk_problem *prob, int option, double value);
 

@@ -309,6 +309,26 @@ def test_col16_tiles_are_bit_identical_with_wide_tile_fallback():
         assert np.linalg.norm(M @ V - b) <= 1e-5 * np.linalg.norm(b)
 
 
+@pytest.mark.parametrize("nonlinear", [False, True])
+def test_w_cycle_level_meets_parity_in_fewer_iterations(nonlinear):
+    """The W-cycle at the level above the last V-cycle level (default:
+    a second coarse correction from the Galerkin coarse residual) is a
+    symmetric preconditioner like the V-cycle: both answers meet the parity
+    tolerance against the converged oracle, and the W-cycle takes no more
+    PCG iterations."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(200, nonlinear=nonlinear))
+    tol = TOL_NONLINEAR if nonlinear else TOL_LINEAR
+    # a 256-row dense coarsest: four levels on this 40k-node mesh
+    Aw, rw, Ac = _solve_vs(kw, pr, mesh, precond="amg", amg_dense=256)
+    Av, rv = _solve(kw, precond="amg", amg_dense=256, amg_wlevel=-1)
+    Ao, _, _ = oracle.solve(pr, mesh)
+    assert rw["amg_levels"] >= 4, rw["amg_levels"]
+    assert rel_err(Aw, Ac) <= tol, parity_message(Aw, Ao, Ac, tol)
+    assert rel_err(Av, Ac) <= tol, parity_message(Av, Ao, Ac, tol)
+    assert not np.array_equal(Aw, Av)
+    assert rw["cg_iters"] <= rv["cg_iters"], (rw["cg_iters"], rv["cg_iters"])
+
+
 def test_amg_is_deterministic_through_newton_refreshes():
     """Repeated nonlinear solves (fresh builds + Newton refreshes of the
     hierarchy, folded levels) give the same bits."""

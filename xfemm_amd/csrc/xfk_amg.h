@@ -93,6 +93,8 @@ struct Amg {
     // parameters
     double theta = 0.08;              // strength threshold
     int sweeps = 1;                   // Jacobi sweeps before and after the coarse correction
+    int wlevel = -2;                  // W-cycle (two coarse corrections) at this folded level (-1: none; -2: XFK_AMG_W)
+    int wcycle_level() const;
     double omega = 1.75;              // Jacobi weight = omega / rho_A (rho_A: Gershgorin bound of D^-1 A);
                                       // omega < 2 keeps the cycle SPD since rho_A >= rho(D^-1 A)
 

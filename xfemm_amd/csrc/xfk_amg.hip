@@ -1829,7 +1829,7 @@ __global__ void __launch_bounds__(256) k_fold_pre(int n, int ncl, const int *__r
                                                   const double *__restrict__ b, double *__restrict__ y, int nc,
                                                   const int *__restrict__ rrow, const int *__restrict__ rcol,
                                                   const double *__restrict__ rval, double *__restrict__ bc,
-                                                  int blocks_a, const int *done)
+                                                  int blocks_a, const int *done, const double *__restrict__ yadd)
 {
     if (done && *done) return;
     // XCD-contiguous row blocks in each range (blocks_a is a multiple of 8):
@@ -1842,7 +1842,8 @@ __global__ void __launch_bounds__(256) k_fold_pre(int n, int ncl, const int *__r
             group_row_dot<GA>(i, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; });
         if (i < n && (threadIdx.x & (GA - 1)) == 0) {
             const double di = dinv[i], bi = b[i], xi = w * di * bi;
-            y[i] = xi + w * di * (bi - ax);
+            const double yi = xi + w * di * (bi - ax);
+            y[i] = yadd ? yadd[i] + yi : yi;   // (a W-cycle's second correction adds onto the first)
         }
     } else {
         const int c = (xcd_tile(blockIdx.x - blocks_a, gridDim.x - blocks_a) * blockDim.x + threadIdx.x) / GB;
@@ -2328,6 +2329,22 @@ SideStream::~SideStream()
     if (b) (void)hipEventDestroy(b);
     if (c) (void)hipEventDestroy(c);
     if (cs) (void)hipStreamDestroy(cs);
+}
+
+// The folded coarse level that runs a W-cycle (two coarse corrections): by
+// default the level above the last V-cycle level (nlev - 3: on configs[2]
+// level 1, whose coarse level of 14k rows costs a few launches per visit;
+// 21 -> 18 PCG iterations), in single-device and replicated hierarchies
+// alike.  wlevel when set (-1: none), else XFK_AMG_W (-1: none).
+int Amg::wcycle_level() const
+{
+    static const int v = [] {
+        const char *e = std::getenv("XFK_AMG_W");
+        return e ? std::atoi(e) : -2;
+    }();
+    const int w = wlevel != -2 ? wlevel : v;
+    if (w != -2) return w;
+    return nlev >= 4 ? nlev - 3 : -1;
 }
 
 // XFK_NO_COL16=1: level 0 reads 32-bit column indices
@@ -3507,7 +3524,7 @@ int lanes_wide(double per_row)
 
 template <int GA>
 void launch_fold_pre_a(hipStream_t s, const AmgLevel &A, const unsigned long long *rho, const double *b, double *y,
-                       double *bc, const int *done)
+                       double *bc, const int *done, const double *yadd)
 {
     const int GB = lanes_wide(A.nc > 0 ? (double)A.fnnz / A.nc : 1.0);
     // (the first range padded to whole rounds of the 8 XCDs, so both ranges
@@ -3516,7 +3533,7 @@ void launch_fold_pre_a(hipStream_t s, const AmgLevel &A, const unsigned long lon
     const int gb = (int)(((long long)A.nc * GB + 255) / 256);
 #define XFK_FOLD(GG)                                                                                               \
     k_fold_pre<GA, GG><<<ga + gb, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, y,   \
-                                               A.nc, A.frrow.p, A.frcol.p, A.frval.p, bc, ga, done)
+                                               A.nc, A.frrow.p, A.frcol.p, A.frval.p, bc, ga, done, yadd)
     switch (GB) {
     case 4: XFK_FOLD(4); break;
     case 8: XFK_FOLD(8); break;
@@ -3528,13 +3545,13 @@ void launch_fold_pre_a(hipStream_t s, const AmgLevel &A, const unsigned long lon
 }
 
 void launch_fold_pre(hipStream_t s, const AmgLevel &A, const unsigned long long *rho, const double *b, double *y,
-                     double *bc, const int *done)
+                     double *bc, const int *done, const double *yadd = nullptr)
 {
     if (A.n <= 0) return;
     const int GA = lanes_for((double)A.nnz / A.n);
-    if (GA == 4) launch_fold_pre_a<4>(s, A, rho, b, y, bc, done);
-    else if (GA == 8) launch_fold_pre_a<8>(s, A, rho, b, y, bc, done);
-    else launch_fold_pre_a<16>(s, A, rho, b, y, bc, done);
+    if (GA == 4) launch_fold_pre_a<4>(s, A, rho, b, y, bc, done, yadd);
+    else if (GA == 8) launch_fold_pre_a<8>(s, A, rho, b, y, bc, done, yadd);
+    else launch_fold_pre_a<16>(s, A, rho, b, y, bc, done, yadd);
 }
 
 // tile size of the level's smoother launches (0: sub-wave kernels, no split)
@@ -3576,8 +3593,10 @@ static void smooth_ph(hipStream_t s, int mode, int l, const AmgLevel &A, const u
 
 // Symmetric V-cycle; returns the buffer holding the level's result.  Level 0
 // writes its result to `out0`.
+// (coarse folded / dense levels: yout = the result buffer instead of xa,
+// yadd = a vector the result is added onto -- the W-cycle's second correction)
 static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, double *out0, const int *done,
-                            double *part_gam = nullptr)
+                            double *part_gam = nullptr, double *yout = nullptr, const double *yadd = nullptr)
 {
     AmgLevel &A = *M.L[l];
     const unsigned long long *rho = M.rho.p + 2 * l;
@@ -3585,7 +3604,7 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     auto other = [&](double *c) { return c == A.xa.p ? A.xb.p : A.xa.p; };
     const std::string lv = g_prof ? "L" + std::to_string(l) + " " : std::string();
     if (l == M.nlev - 1) {
-        double *dst = (l == 0) ? out0 : A.xa.p;
+        double *dst = (l == 0) ? out0 : (yout ? yout : A.xa.p);
         if (M.dense_coarse) {
             XFK_PHASE(lv + "dense inverse x b", 4.0 * A.n * M.cinv_ld + 8.0 * (M.cinv_ld + A.n),
                       (k_dense_mv<<<A.n, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv_apply, b, dst, done)));
@@ -3606,11 +3625,25 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     if (A.fold && l > 0) {
         // two launches: y and the coarse right-hand side, then x = y + P~ x_c
         AmgLevel &C = *M.L[l + 1];
-        double *y = A.xa.p;
+        double *y = yout ? yout : A.xa.p;
         const double n = A.n, nc = A.nc, f = (double)A.fnnz;
-        XFK_PHASE(lv + "folded pre: y, R~ r", 12.0 * A.nnz + 4.0 * (n + 1) + 24.0 * n + 12.0 * f + 4.0 * (nc + 1) + 8.0 * nc,
-                  launch_fold_pre(s, A, rho, b, y, C.b.p, done));
-        const double *xc = vcycle_level(M, s, l + 1, C.b.p, nullptr, done);
+        XFK_PHASE(lv + "folded pre: y, R~ r", 12.0 * A.nnz + 4.0 * (n + 1) + 24.0 * n + 12.0 * f + 4.0 * (nc + 1) +
+                                                   8.0 * nc + (yadd ? 8.0 * n : 0.0),
+                  launch_fold_pre(s, A, rho, b, y, C.b.p, done, yadd));
+        const double *xc;
+        if (l == M.wcycle_level() && l + 1 < M.nlev - 1) {
+            // W-cycle at this level: a second coarse correction from the
+            // coarse residual after the first, b_c' = b_c - A_c x_c (Galerkin:
+            // R (b - A (x_pre + P x_c)) = b_c - A_c x_c), x_c += V(b_c'); the
+            // second visit adds its result onto the first (its folded
+            // pre-step starts from x_c), so the post-step prolongs the sum.
+            // Symmetric like the V-cycle; three launches more than it.
+            const double *x1 = vcycle_level(M, s, l + 1, C.b.p, nullptr, done, nullptr, C.xb.p);
+            smooth_ph(s, kResid, l + 1, C, M.rho.p + 2 * (l + 1), C.b.p, x1, nullptr, C.r.p, done);
+            xc = vcycle_level(M, s, l + 1, C.r.p, nullptr, done, nullptr, C.xa.p, x1);
+        } else {
+            xc = vcycle_level(M, s, l + 1, C.b.p, nullptr, done);
+        }
         XFK_PHASE(lv + "folded post: x = y + P~ xc", 12.0 * f + 4.0 * (n + 1) + 8.0 * nc + 16.0 * n,
                   launch_mv(s, A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xc, y, true, lanes_for(f / n), done));
         return y;

@@ -755,6 +755,7 @@ static int amg_setup(xfk_problem *P)
     P->amg->dense_max = P->amg_dense;
     P->amg->fold_on = P->amg_fold;
     P->amg->col16 = P->amg_col16;
+    P->amg->wlevel = P->amg_wlevel;
     // setup time: an event pair per setup, read after the solve's final
     // synchronisation (no host check here); callers that never read them
     // recycle the pairs; a full pool (> 64 fresh builds in one solve) is
@@ -1812,6 +1813,11 @@ int xfk_set_option(xfk_problem *P, int option, double value)
     case XFK_OPT_AMG_COL16:
         XFK_REQUIRE(value == 0 || value == 1, XFK_ERR_ARG, "AMG 16-bit columns is 0 or 1");
         P->amg_col16 = (int)value;
+        return XFK_OK;
+    case XFK_OPT_AMG_WLEVEL:
+        XFK_REQUIRE(value >= -2 && value < kAmgMaxLevels && value == (int)value, XFK_ERR_ARG,
+                    "AMG W-cycle level must be -2, -1 or a level index");
+        P->amg_wlevel = (int)value;
         return XFK_OK;
     default:
         set_error("unknown option");
