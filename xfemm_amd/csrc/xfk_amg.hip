@@ -2003,13 +2003,67 @@ Amg::~Amg()
 namespace {
 
 // out[0..n] = exclusive scan of in[0..n-1], out[n] = total; returns total
+// Short scans (coarse levels: <= kScanLds entries) in one workgroup, one
+// launch: the input is staged in LDS by coalesced loads, each thread scans
+// 16 consecutive entries there, a workgroup scan adds the thread offsets, and
+// the result leaves by coalesced stores -- one memory round trip each way,
+// instead of hipcub's memset + state init + scan (three launches).
+constexpr int kScanLds = 16384;
+
+// XFK_NO_SCAN_LDS=1: every scan through hipcub
+bool scan_lds_on(int n)
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_NO_SCAN_LDS");
+        return !(e && std::atoi(e) != 0);
+    }();
+    return v && n <= kScanLds;
+}
+
+__global__ void __launch_bounds__(1024) k_scan_lds(int n, const int *__restrict__ in, int *__restrict__ out)
+{
+    __shared__ int buf[kScanLds];
+    __shared__ int wsum[16];
+    for (int i = threadIdx.x; i < n; i += 1024) buf[i] = in[i];
+    __syncthreads();
+    const int b = 16 * threadIdx.x;
+    int loc = 0;
+    for (int q = 0; q < 16 && b + q < n; ++q) loc += buf[b + q];
+    // exclusive scan of the thread sums over the workgroup
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = loc;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(x, off, 64);
+        if (lane >= off) x += t;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    int before = 0;
+    for (int w = 0; w < wid; ++w) before += wsum[w];
+    int run = before + x - loc;
+    __syncthreads();
+    for (int q = 0; q < 16 && b + q < n; ++q) {
+        run += buf[b + q];
+        buf[b + q] = run;   // inclusive prefix in place (own entries only)
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += 1024) out[i + 1] = buf[i];
+    if (threadIdx.x == 0) out[0] = 0;
+}
+
 int scan_total(Amg &A, hipStream_t s, const int *in, int *out, int n, long long &total)
 {
-    size_t bytes = 0;
-    AMG_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out + 1, n, s));
-    AMG_CHECK(A.cub_tmp.alloc(bytes ? bytes : 1));
-    AMG_CHECK(hipMemsetAsync(out, 0, sizeof(int), s));
-    if (n > 0) AMG_CHECK(hipcub::DeviceScan::InclusiveSum(A.cub_tmp.p, bytes, in, out + 1, n, s));
+    if (scan_lds_on(n)) {
+        k_scan_lds<<<1, 1024, 0, s>>>(n, in, out);
+        AMG_CHECK(hipGetLastError());
+    } else {
+        size_t bytes = 0;
+        AMG_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out + 1, n, s));
+        AMG_CHECK(A.cub_tmp.alloc(bytes ? bytes : 1));
+        AMG_CHECK(hipMemsetAsync(out, 0, sizeof(int), s));
+        if (n > 0) AMG_CHECK(hipcub::DeviceScan::InclusiveSum(A.cub_tmp.p, bytes, in, out + 1, n, s));
+    }
     AMG_CHECK(hipMemcpyAsync(A.host_int, out + n, sizeof(int), hipMemcpyDeviceToHost, s));
     AMG_CHECK(hipStreamSynchronize(s));
     total = A.host_int[0];
@@ -2020,6 +2074,11 @@ int scan_total(Amg &A, hipStream_t s, const int *in, int *out, int n, long long 
 // the given temporary storage
 int scan_only(DBuf<char> &tmp, hipStream_t s, const int *in, int *out, int n)
 {
+    if (scan_lds_on(n)) {
+        k_scan_lds<<<1, 1024, 0, s>>>(n, in, out);
+        AMG_CHECK(hipGetLastError());
+        return XFK_OK;
+    }
     size_t bytes = 0;
     AMG_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out + 1, n, s));
     AMG_CHECK(tmp.alloc(bytes ? bytes : 1));
