@@ -193,6 +193,100 @@ __global__ void __launch_bounds__(NT) k_diag_var(int ld, const double *__restric
     for (int m = 0; m < RPT; ++m) D[(RPT * w + m) * kBj + j] = a[m];
 }
 
+// the MFMA-update inverse (bgj_inv_mfma) with ablations: ABL & 1 no MFMA
+// update, & 2 no 4 x 4 inverse, & 4 no barrier, & 8 fast reciprocal
+template <int ABL>
+__global__ void __launch_bounds__(256) k_inv_mfma_var(int ld, const double *__restrict__ M, const double *__restrict__ maxd,
+                                                      double *__restrict__ D)
+{
+    __shared__ __attribute__((aligned(16))) double lds[kBjInvLds];
+    dbl4 c[2][2];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c[ti][tj][r] = M[(size_t)bgj_row(ti, r) * ld + bgj_col(tj)];
+    if constexpr (ABL == 0) {
+        bgj_inv_mfma(c, 1e-11 * (*maxd), lds);
+    } else {
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        const int li = lane & 15, lk = lane >> 4;
+        const int R0 = 32 * (w >> 1), C0 = 32 * (w & 1);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const int p0 = 4 * s;
+            const int tp = (p0 >> 4) & 1, rp = (p0 & 15) >> 2;
+            double *RS = lds + (s & 1) * 8 * kBj;
+            double *CS = RS + 4 * kBj;
+            const bool rowhold = (w >> 1) == (p0 >> 5);
+            if (rowhold)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj) RS[lk * kBj + C0 + 16 * tj + li] = c[tp][tj][rp];
+            if ((w & 1) == (p0 >> 5) && li >= (p0 & 15) && li < (p0 & 15) + 4)
+#pragma unroll
+                for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) CS[(R0 + 16 * ti + lk + 4 * r) * 4 + li - (p0 & 15)] = c[ti][tp][r];
+            if (!(ABL & 4)) __syncthreads();
+            double W[4][4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) W[q][t] = RS[q * kBj + p0 + t];
+            if (!(ABL & 2))
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const double ip = (ABL & 8) ? recip<true>(W[q][q]) : 1.0 / W[q][q];
+                    W[q][q] = 1.0;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) W[q][t] *= ip;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (t == q) continue;
+                        const double f = W[t][q];
+                        W[t][q] = 0.0;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) W[t][u] -= f * W[q][u];
+                    }
+                }
+            double Dk[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Dk[t] = lk == 0 ? W[0][t] : lk == 1 ? W[1][t] : lk == 2 ? W[2][t] : W[3][t];
+            double bop[2], aop[2];
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) {
+                const int jj = C0 + 16 * tj + li, tc = jj - p0;
+                if (tc >= 0 && tc < 4) {
+                    const double d = tc == 0 ? Dk[0] : tc == 1 ? Dk[1] : tc == 2 ? Dk[2] : Dk[3];
+                    bop[tj] = (lk == tc ? 1.0 : 0.0) + d;
+                } else {
+                    bop[tj] = Dk[0] * RS[jj] + Dk[1] * RS[kBj + jj] + Dk[2] * RS[2 * kBj + jj] + Dk[3] * RS[3 * kBj + jj];
+                }
+            }
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti) aop[ti] = -CS[(R0 + 16 * ti + li) * 4 + lk];
+            if (!(ABL & 1))
+#pragma unroll
+                for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                    for (int tj = 0; tj < 2; ++tj)
+                        c[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[ti], bop[tj], c[ti][tj], 0, 0, 0);
+            else
+                c[0][0][0] += aop[0] + aop[1] + bop[0] + bop[1];
+            if (rowhold)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj) c[tp][tj][rp] += bop[tj];
+        }
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) D[bgj_row(ti, r) * kBj + bgj_col(tj)] = c[ti][tj][r];
+}
+
 }  // namespace
 
 int main()
@@ -234,11 +328,19 @@ int main()
         run_var("256 ablate update+inverse", k_diag_var<256, false, 3>, 256);
         run_var("256 ablate all", k_diag_var<256, false, 7>, 256);
         run_var("64 (1 wave) exact", k_diag_var<64, false>, 64);
+        run_var("mfma", k_inv_mfma_var<0>, 256);
+        run_var("mfma (lab copy)", k_inv_mfma_var<16>, 256);
+        run_var("mfma fast recip", k_inv_mfma_var<8>, 256);
+        run_var("mfma ablate update", k_inv_mfma_var<1>, 256);
+        run_var("mfma ablate 4x4 inverse", k_inv_mfma_var<2>, 256);
+        run_var("mfma ablate barrier", k_inv_mfma_var<4>, 256);
+        run_var("mfma ablate all", k_inv_mfma_var<7>, 256);
         (void)hipFree(dM);
         (void)hipFree(dD);
         (void)hipFree(dmax);
     }
     // 2. the whole blocked Gauss-Jordan at the configs[2] coarsest size
+    for (int inv_mode = 0; inv_mode < 2; ++inv_mode)
     for (int n : {64, 128, 1024, 1600}) {
         const int nbk = (n + kBj - 1) / kBj, ld = nbk * kBj;
         const size_t T2 = (size_t)kBj * kBj;
@@ -261,7 +363,7 @@ int main()
             for (int k = 0; k < nbk; ++k) {
                 const int p = k & 1, q = (k + 1) & 1;
                 k_bgj_step<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, dM, Dbuf + p * T2, Rs[p], Cs[p], Dbuf + q * T2, Rs[q],
-                                                     Cs[q], maxd);
+                                                     Cs[q], maxd, inv_mode);
             }
         };
         std::vector<double> X((size_t)ld * ld);
@@ -272,18 +374,19 @@ int main()
         const int k = nbk / 2;
         const float t_step = time_launches(
             [&] {
-                k_bgj_step<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, dM, Dbuf, Rs[0], Cs[0], Dbuf + T2, Rs[1], Cs[1], maxd);
+                k_bgj_step<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, dM, Dbuf, Rs[0], Cs[0], Dbuf + T2, Rs[1], Cs[1], maxd,
+                                                     inv_mode);
             },
             50, s);
         const float t_step_last = time_launches(
             [&] {
                 k_bgj_step<<<nbk * nbk, 256, 0, s>>>(nbk - 1, nbk, ld, dM, Dbuf, Rs[0], Cs[0], Dbuf + T2, Rs[1], Cs[1],
-                                                     maxd);
+                                                     maxd, inv_mode);
             },
             50, s);
-        std::printf("{\"test\": \"bgj n=%d\", \"nbk\": %d, \"us_new\": %.1f, "
+        std::printf("{\"test\": \"bgj n=%d inv_mode %d\", \"nbk\": %d, \"us_new\": %.1f, "
                     "\"res_new\": %.3e, \"us_step\": %.2f, \"us_step_no_pivot\": %.2f}\n",
-                    n, nbk, t_new - t_reset, res_new, t_step, t_step_last);
+                    n, inv_mode, nbk, t_new - t_reset, res_new, t_step, t_step_last);
         (void)hipFree(dA);
         (void)hipFree(dM);
         (void)hipFree(tmp);

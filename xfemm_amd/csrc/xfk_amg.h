@@ -95,6 +95,7 @@ struct Amg {
     int sweeps = 1;                   // Jacobi sweeps before and after the coarse correction
     int wlevel = -2;                  // W-cycle (two coarse corrections) at this folded level (-1: none; -2: XFK_AMG_W)
     int wcycle_level() const;
+    bool w_at(int l) const;
     double omega = 1.75;              // Jacobi weight = omega / rho_A (rho_A: Gershgorin bound of D^-1 A);
                                       // omega < 2 keeps the cycle SPD since rho_A >= rho(D^-1 A)
 
@@ -103,7 +104,6 @@ struct Amg {
     bool dense_coarse = false;
     DBuf<double> cinv;                // dense inverse of the coarsest level (row major, padded)
     int cinv_ld = 0;
-    bool nd_prefetched = false;       // host_big holds the coarsest pattern (read with the deferred lengths)
     DBuf<float> cinv_o;               // the inverse the V-cycle applies: unpermuted, unscaled, f32
     const float *cinv_apply = nullptr;
     DBuf<int> cinv_perm, cinv_iperm, nd_tiles;
@@ -115,6 +115,9 @@ struct Amg {
     };
     std::vector<NdPhase> nd_phases;
     std::vector<int> nd_key;          // coarsest pattern (rowptr, col) the cached plan was made for
+    DBuf<int> nd_key_dev;             // its device copy (compared on the device by the next setup)
+    int nd_key_n = -1;
+    long long nd_key_nnz = 0;
     std::vector<NdPhase> nd_phases_key;
     int nd_ld = 0;
     char *nd_stage = nullptr;         // pinned upload staging of the plan
@@ -140,7 +143,9 @@ struct Amg {
     int *def_host = nullptr;          // pinned mirror
     int def_n = 0;
     long long *def_target[kAmgDeferSlots / 2] = {};
-    int *host_int = nullptr;          // pinned mirror
+    int *host_int = nullptr;          // pinned mirror (16 ints; 8..10: the aggregation's packed check)
+    hipEvent_t ev_host = nullptr;     // host waits for a check while later setup work runs
+    DBuf<int> mis_out;                // packed aggregation check
     DBuf<char> cub_tmp;
 
     // sharded hierarchy (setup_dist): levels 0 .. lrep-1 are sharded (each rank
@@ -205,11 +210,16 @@ struct Amg {
     int init(hipStream_t s);
     int build(hipStream_t s, int l0);
     int aggregate(hipStream_t s, int l, long long &nc, bool allow_stop);
+    int joins_and_p_impl(hipStream_t s, int l);
     int galerkin_dist(hipStream_t s, int l, int st, bool &rep);
     double *vc_dist(hipStream_t s, int l, const double *b, double *out, const int *done, int &rc);
     int host_ints(int count);
     int nd_order(hipStream_t s, const AmgLevel &C, int &ld);
     int resolve_deferred(hipStream_t s, bool &overflow);
+    int fetch_deferred(hipStream_t s);
+    int wait_deferred(hipStream_t s, bool &overflow);
+    int dense_inverse(hipStream_t s, const AmgLevel &C, int ld);
+    int alloc_vectors();
     long long ap_nnz = 0;
 };
 

@@ -322,6 +322,31 @@ __global__ void k_agg_roots(int n, const MisKey *__restrict__ key, int *__restri
     if (i < n) flag[i] = key_st(key[i]) == kStIn;
 }
 
+// the aggregation's host check in one read: {roots, undecided flag, rounds that did work}
+__global__ void k_mis_pack(const int *__restrict__ roots, const int *__restrict__ und, const int *__restrict__ run,
+                           int *__restrict__ out)
+{
+    if (threadIdx.x == 0) {
+        out[0] = *roots;
+        out[1] = *und;
+        out[2] = *run;
+    }
+}
+
+// out = 1 when the pattern (rowptr[0..n], col[0..key_nnz)) differs from the
+// key (rowptr, then col); equal row pointers make the lengths equal, so the
+// first key_nnz columns decide (columns read only below the buffer capacity,
+// checked by the caller)
+__global__ void k_pattern_diff(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+                               const int *__restrict__ key, int key_nnz, int *__restrict__ out)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    bool d = false;
+    if (t <= n) d = rowptr[t] != key[t];
+    if (t < key_nnz) d = d || col[t] != key[n + 1 + t];
+    if (d) out[0] = 1;
+}
+
 // distance 1: roots keep their aggregate, neighbours of roots join the root
 // with the largest key
 // rows left out that have (weak) couplings to aggregated owned rows join the
@@ -1239,6 +1264,108 @@ __device__ __forceinline__ void bgj_mm(const double *__restrict__ Xs, const doub
 __device__ __forceinline__ int bgj_row(int ti, int r) { return 32 * ((threadIdx.x >> 6) >> 1) + 16 * ti + ((threadIdx.x & 63) >> 4) + 4 * r; }
 __device__ __forceinline__ int bgj_col(int tj) { return 32 * ((threadIdx.x >> 6) & 1) + 16 * tj + (threadIdx.x & 15); }
 
+// inv(A) of a 64 x 64 block held in bgj_mm's accumulator layout
+// (c[ti][tj][r] = element (bgj_row(ti, r), bgj_col(tj))), in place: 16
+// rank-4 Gauss-Jordan steps whose updates run on the f64 matrix cores.  Step
+// s publishes rows and columns P = 4s .. 4s+3 to LDS; every lane forms
+// D = inv(A_PP) in registers and its B operand r = D A_Pj (r = I + D on the
+// pivot columns); then c -= A_iP r on the MFMA, and rows P += r -- the update
+// of bgj_diag_inv without its 64 FMAs and 32 LDS reads per lane and step.
+// A (near) null pivot (|piv| <= thr) zeroes its row and column, as there.
+// lds: kBjInvLds doubles (two buffers of a 4 x 64 row slab and a 64 x 4 column slab).
+constexpr int kBjInvLds = 2 * 8 * kBj;
+static_assert(kBjInvLds <= kBjDiagLds && kBjInvLds <= kBj * kYs, "bgj_inv_mfma's LDS exceeds its callers' buffers");
+__device__ __forceinline__ void bgj_inv_mfma(dbl4 (&c)[2][2], double thr, double *lds)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int R0 = 32 * (w >> 1), C0 = 32 * (w & 1);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int p0 = 4 * s;
+        const int tp = (p0 >> 4) & 1, rp = (p0 & 15) >> 2;   // tile / element index of rows (columns) P
+        double *RS = lds + (s & 1) * 8 * kBj;   // RS[t][j] = A(p0 + t, j)
+        double *CS = RS + 4 * kBj;              // CS[i][t] = A(i, p0 + t)
+        const bool rowhold = (w >> 1) == (p0 >> 5);
+        if (rowhold)   // this lane holds row p0 + lk
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) RS[lk * kBj + C0 + 16 * tj + li] = c[tp][tj][rp];
+        if ((w & 1) == (p0 >> 5) && li >= (p0 & 15) && li < (p0 & 15) + 4)   // ... column p0 + li - (p0 & 15)
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) CS[(R0 + 16 * ti + lk + 4 * r) * 4 + li - (p0 & 15)] = c[ti][tp][r];
+        __syncthreads();
+        double W[4][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) W[q][t] = RS[q * kBj + p0 + t];
+        // a null pivot takes ip = 0: its row of D becomes 0 and the
+        // elimination leaves the other rows alone, i.e. D is the inverse on
+        // the other directions; the update then zeroes column p0 + q of the
+        // block by itself (r = e_q there), and row p0 + q is zeroed below
+        unsigned nul = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const double piv = W[q][q];
+            const bool ok = fabs(piv) > thr;
+            nul |= ok ? 0u : 1u << q;
+            double ip = __builtin_amdgcn_rcp(piv);   // 1 / piv: v_rcp_f64 + two Newton steps
+            ip = fma(fma(-piv, ip, 1.0), ip, ip);
+            ip = fma(fma(-piv, ip, 1.0), ip, ip);
+            ip = ok ? ip : 0.0;
+            W[q][q] = 1.0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) W[q][t] *= ip;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (t == q) continue;
+                const double f = W[t][q];
+                W[t][q] = 0.0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) W[t][u] -= f * W[q][u];
+            }
+        }
+        // row lk of D: this lane's B operand row
+        double Dk[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) Dk[t] = lk == 0 ? W[0][t] : lk == 1 ? W[1][t] : lk == 2 ? W[2][t] : W[3][t];
+        double bop[2], aop[2];
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+            const int jj = C0 + 16 * tj + li, tc = jj - p0;
+            if (tc >= 0 && tc < 4) {
+                const double d = tc == 0 ? Dk[0] : tc == 1 ? Dk[1] : tc == 2 ? Dk[2] : Dk[3];
+                bop[tj] = (lk == tc ? 1.0 : 0.0) + d;
+            } else {
+                bop[tj] = Dk[0] * RS[jj] + Dk[1] * RS[kBj + jj] + Dk[2] * RS[2 * kBj + jj] + Dk[3] * RS[3 * kBj + jj];
+            }
+        }
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti) aop[ti] = -CS[(R0 + 16 * ti + li) * 4 + lk];
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) c[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[ti], bop[tj], c[ti][tj], 0, 0, 0);
+        if (rowhold) {
+            const bool zr = (nul >> lk) & 1u;   // row p0 + lk of a null pivot
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) c[tp][tj][rp] = zr ? 0.0 : c[tp][tj][rp] + bop[tj];
+        }
+    }
+}
+
+// XFK_BGJ_INV=0: the pivot-block inverse by bgj_diag_inv (FMA updates)
+static int bgj_inv_mode()
+{
+    static const int v = [] {
+        const char *e = std::getenv("XFK_BGJ_INV");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+
 template <int S>
 __device__ __forceinline__ void bgj_load(double *__restrict__ dst, const double *__restrict__ src, size_t ld)
 {
@@ -1290,7 +1417,7 @@ __global__ void __launch_bounds__(256) k_bgj_step(int k, int nbk, int ld, double
                                                   const double *__restrict__ Dk, const double *__restrict__ Rk,
                                                   const double *__restrict__ Ck, double *__restrict__ Dn,
                                                   double *__restrict__ Rn, double *__restrict__ Cn,
-                                                  const double *__restrict__ maxd)
+                                                  const double *__restrict__ maxd, int inv_mode)
 {
     const int nt = nbk * nbk, kn = k + 1 < nbk ? k + 1 : 0;
     const int b = (int)((blockIdx.x + (unsigned)(kn * nbk + kn)) % (unsigned)nt);
@@ -1354,7 +1481,8 @@ __global__ void __launch_bounds__(256) k_bgj_step(int k, int nbk, int ld, double
     }
     double *rn = (i == k + 1) ? Rn + j * T2 : nullptr;
     double *cn = (j == k + 1) ? Cn + i * T2 : nullptr;
-    if (piv) __syncthreads();   // Xs is reused below
+    const bool fast = piv && inv_mode != 0;
+    if (piv) __syncthreads();   // Xs / Ys are reused below
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -1367,9 +1495,20 @@ __global__ void __launch_bounds__(256) k_bgj_step(int k, int nbk, int ld, double
                 *e = v;
                 if (rn) rn[row * kBj + col] = v;
                 if (cn) cn[row * kBj + col] = v;
-                if (piv) Xs[row * kBj + col] = v;
+                if (fast) c[ti][tj][r] = v;
+                else if (piv) Xs[row * kBj + col] = v;
             }
     if (!piv) return;
+    if (fast) {
+        bgj_inv_mfma(c, 1e-11 * (*maxd), Ys);
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Dn[bgj_row(ti, r) * kBj + bgj_col(tj)] = c[ti][tj][r];
+        return;
+    }
     __syncthreads();
     const int jl = threadIdx.x & 63, w = threadIdx.x >> 6;
     double a[16];
@@ -1405,7 +1544,7 @@ struct BgjStep {
 // by-value kernel argument would be placed in scratch memory)
 __global__ void __launch_bounds__(256, 2) k_bgj_multi(int nbk, int ld, double *__restrict__ M, BgjStep st,
                                                       const unsigned char *__restrict__ mask,
-                                                      const int *__restrict__ tiles, const double *maxd)
+                                                      const int *__restrict__ tiles, const double *maxd, int inv_mode)
 {
     const size_t T2 = (size_t)kBj * kBj;
     int i, j;
@@ -1510,7 +1649,8 @@ __global__ void __launch_bounds__(256, 2) k_bgj_multi(int nbk, int ld, double *_
         rs[t] = (t < st.nn && i == st.nx[t]) ? st.Rn[t] + j * T2 : nullptr;
         cs[t] = (t < st.nn && j == st.nx[t]) ? st.Cn[t] + i * T2 : nullptr;
     }
-    if (Dpiv) __syncthreads();   // Xs is reused below
+    const bool fast = Dpiv && inv_mode != 0;
+    if (Dpiv) __syncthreads();   // Xs / Ys are reused below
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -1526,9 +1666,20 @@ __global__ void __launch_bounds__(256, 2) k_bgj_multi(int nbk, int ld, double *_
                     if (rs[t]) rs[t][row * kBj + col] = v;
                     if (cs[t]) cs[t][row * kBj + col] = v;
                 }
-                if (Dpiv) Xs[row * kBj + col] = v;
+                if (fast) acc[ti][tj][r] = v;
+                else if (Dpiv) Xs[row * kBj + col] = v;
             }
     if (!Dpiv) return;
+    if (fast) {
+        bgj_inv_mfma(acc, 1e-11 * (*maxd), Ys);
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Dpiv[bgj_row(ti, r) * kBj + bgj_col(tj)] = acc[ti][tj][r];
+        return;
+    }
     __syncthreads();
     const int jl = threadIdx.x & 63, w = threadIdx.x >> 6;
     double a[16];
@@ -1542,7 +1693,7 @@ __global__ void __launch_bounds__(256, 2) k_bgj_multi(int nbk, int ld, double *_
 // first step of the first phase: pivot-block inverses (workgroups 0 .. n-1)
 // and row / column snapshots of the chains' first pivot blocks
 __global__ void __launch_bounds__(256) k_bgj_init(int nbk, int ld, const double *__restrict__ M, BgjStep st,
-                                                  const double *__restrict__ maxd)
+                                                  const double *__restrict__ maxd, int inv_mode)
 {
     const int b = blockIdx.x;
     if (b < st.nn) {
@@ -1557,6 +1708,23 @@ __global__ void __launch_bounds__(256) k_bgj_init(int nbk, int ld, const double 
             }
         const int jl = threadIdx.x & 63, w = threadIdx.x >> 6;
         const size_t base = (size_t)k * kBj * ld + (size_t)k * kBj;
+        if (inv_mode != 0) {
+            dbl4 c[2][2];
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) c[ti][tj][r] = M[base + (size_t)bgj_row(ti, r) * ld + bgj_col(tj)];
+            bgj_inv_mfma(c, 1e-11 * (*maxd), lds);
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) D[bgj_row(ti, r) * kBj + bgj_col(tj)] = c[ti][tj][r];
+            return;
+        }
         double a[16];
 #pragma unroll
         for (int m = 0; m < 16; ++m) a[m] = M[base + (size_t)(16 * w + m) * ld + jl];
@@ -1989,6 +2157,7 @@ Amg::~Amg()
     if (def_host) (void)hipHostFree(def_host);
     if (host_int) (void)hipHostFree(host_int);
     if (host_big) (void)hipHostFree(host_big);
+    if (ev_host) (void)hipEventDestroy(ev_host);
 }
 
 #define AMG_CHECK(call)                                                          \
@@ -2004,10 +2173,10 @@ namespace {
 
 // out[0..n] = exclusive scan of in[0..n-1], out[n] = total; returns total
 // Short scans (coarse levels: <= kScanLds entries) in one workgroup, one
-// launch: the input is staged in LDS by coalesced loads, each thread scans
-// 16 consecutive entries there, a workgroup scan adds the thread offsets, and
-// the result leaves by coalesced stores -- one memory round trip each way,
-// instead of hipcub's memset + state init + scan (three launches).
+// launch instead of hipcub's memset + state init + scan: each of 1024 threads
+// loads 16 consecutive entries at once (four 16-B loads), scans them in
+// registers, a workgroup scan of the thread sums gives the offsets, and the
+// prefixes are stored -- one memory round trip each way.
 constexpr int kScanLds = 16384;
 
 // XFK_NO_SCAN_LDS=1: every scan through hipcub
@@ -2022,13 +2191,26 @@ bool scan_lds_on(int n)
 
 __global__ void __launch_bounds__(1024) k_scan_lds(int n, const int *__restrict__ in, int *__restrict__ out)
 {
-    __shared__ int buf[kScanLds];
     __shared__ int wsum[16];
-    for (int i = threadIdx.x; i < n; i += 1024) buf[i] = in[i];
-    __syncthreads();
     const int b = 16 * threadIdx.x;
-    int loc = 0;
-    for (int q = 0; q < 16 && b + q < n; ++q) loc += buf[b + q];
+    int v[16];
+    if (b + 16 <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0) {
+        const int4 *p = reinterpret_cast<const int4 *>(in + b);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int4 x = p[q];
+            v[4 * q] = x.x;
+            v[4 * q + 1] = x.y;
+            v[4 * q + 2] = x.z;
+            v[4 * q + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = b + q < n ? in[b + q] : 0;
+    }
+#pragma unroll
+    for (int q = 1; q < 16; ++q) v[q] += v[q - 1];
+    const int loc = v[15];
     // exclusive scan of the thread sums over the workgroup
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int x = loc;
@@ -2039,16 +2221,13 @@ __global__ void __launch_bounds__(1024) k_scan_lds(int n, const int *__restrict_
     }
     if (lane == 63) wsum[wid] = x;
     __syncthreads();
-    int before = 0;
-    for (int w = 0; w < wid; ++w) before += wsum[w];
-    int run = before + x - loc;
-    __syncthreads();
-    for (int q = 0; q < 16 && b + q < n; ++q) {
-        run += buf[b + q];
-        buf[b + q] = run;   // inclusive prefix in place (own entries only)
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += 1024) out[i + 1] = buf[i];
+    int before = x - loc;
+#pragma unroll
+    for (int w = 0; w < 16; ++w)
+        if (w < wid) before += wsum[w];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+        if (b + q < n) out[b + q + 1] = before + v[q];
     if (threadIdx.x == 0) out[0] = 0;
 }
 
@@ -2406,6 +2585,19 @@ int Amg::wcycle_level() const
     return nlev >= 4 ? nlev - 3 : -1;
 }
 
+// W-cycle at level l: l is the W level, or between XFK_AMG_W_LO and it
+// (experiments with W over several levels; default: the W level alone)
+bool Amg::w_at(int l) const
+{
+    static const int lo_env = [] {
+        const char *e = std::getenv("XFK_AMG_W_LO");
+        return e ? std::atoi(e) : -1;
+    }();
+    const int w = wcycle_level();
+    if (w < 0 || l > w || l + 1 >= nlev - 1) return false;
+    return l == w || (lo_env >= 0 && l >= lo_env);
+}
+
 // XFK_NO_COL16=1: level 0 reads 32-bit column indices
 static bool col16_on()
 {
@@ -2426,6 +2618,16 @@ static bool side_setup_on()
     return v;
 }
 
+// XFK_NO_SPEC=1: no setup work enqueued ahead of a host check
+static bool spec_on()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_NO_SPEC");
+        return !(e && std::atoi(e) != 0);
+    }();
+    return v;
+}
+
 bool overlap_enabled()
 {
     const char *e = std::getenv("XFK_NO_OVERLAP");
@@ -2434,10 +2636,26 @@ bool overlap_enabled()
 
 int Amg::resolve_deferred(hipStream_t s, bool &overflow)
 {
-    overflow = false;
+    int rc = fetch_deferred(s);
+    if (rc != XFK_OK) return rc;
+    return wait_deferred(s, overflow);
+}
+
+// the deferred slots' read, enqueued (the host waits for it in wait_deferred;
+// work enqueued in between runs meanwhile)
+int Amg::fetch_deferred(hipStream_t s)
+{
     if (def_n == 0) return XFK_OK;
     AMG_CHECK(hipMemcpyAsync(def_host, def_dev.p, sizeof(int) * def_n, hipMemcpyDeviceToHost, s));
-    AMG_CHECK(hipStreamSynchronize(s));
+    AMG_CHECK(hipEventRecord(ev_host, s));
+    return XFK_OK;
+}
+
+int Amg::wait_deferred(hipStream_t s, bool &overflow)
+{
+    overflow = false;
+    if (def_n == 0) return XFK_OK;
+    AMG_CHECK(hipEventSynchronize(ev_host));
     for (int q = 0; q < def_n / 2; ++q) {
         if (def_host[2 * q]) overflow = true;
         else *def_target[q] = def_host[2 * q + 1];
@@ -2460,7 +2678,8 @@ int Amg::host_ints(int count)
 
 int Amg::init(hipStream_t s)
 {
-    if (!host_int) AMG_CHECK(hipHostMalloc((void **)&host_int, 8 * sizeof(int)));
+    if (!host_int) AMG_CHECK(hipHostMalloc((void **)&host_int, 16 * sizeof(int)));
+    if (!ev_host) AMG_CHECK(hipEventCreateWithFlags(&ev_host, hipEventDisableTiming));
     if (!def_host) AMG_CHECK(hipHostMalloc((void **)&def_host, kAmgDeferSlots * sizeof(int)));
     AMG_CHECK(dev_int.alloc(8));
     AMG_CHECK(def_dev.alloc(kAmgDeferSlots));
@@ -2559,6 +2778,12 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     // rounds), 12 without one.  Roots and their numbering are formed
     // speculatively after each batch and read back in the same host check.
     auto hint = mis_hint.find(l);
+    // speculative joins and P need a round hint and a hinted (non-synchronising) P
+    const bool spec = spec_on() && !g_prof && !dist && hint != mis_hint.end() && cap_hint.count(4 * l) &&
+                      def_n + 4 <= kAmgDeferSlots && !std::getenv("XFK_AMG_DEBUG");
+    bool joined = false;
+    auto joins_and_p = [&]() { return joins_and_p_impl(s, l); };
+    AMG_CHECK(mis_out.alloc(4));
     for (int batch = hint != mis_hint.end() ? std::max(1, hint->second) : 12;; batch = 2) {
         for (int b = 0; b < batch; ++b, ++rounds) {
             int *cur = und2 + (rounds & 1), *prev = und2 + ((rounds + 1) & 1);
@@ -2574,55 +2799,31 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         k_agg_roots<<<nb(n), kB, 0, s>>>(n, key.p, flag.p);
         int rc = scan_only(*this, s, flag.p, cursor.p, n);   // cursor = root ids
         if (rc != XFK_OK) return rc;
-        AMG_CHECK(hipMemcpyAsync(host_int + 1, und2 + ((rounds - 1) & 1), sizeof(int), hipMemcpyDeviceToHost, s));
-        AMG_CHECK(hipMemcpyAsync(host_int + 5, run, sizeof(int), hipMemcpyDeviceToHost, s));
-        AMG_CHECK(hipMemcpyAsync(host_int, cursor.p + n, sizeof(int), hipMemcpyDeviceToHost, s));
-        AMG_CHECK(hipStreamSynchronize(s));
-        if (!host_int[1]) break;
+        k_mis_pack<<<1, 64, 0, s>>>(cursor.p + n, und2 + ((rounds - 1) & 1), run, mis_out.p);
+        AMG_CHECK(hipMemcpyAsync(host_int + 8, mis_out.p, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipEventRecord(ev_host, s));
+        // while the host waits for the check, the device goes on with the
+        // joins and P (correct when the check finds the MIS complete -- the
+        // usual case with a round hint; otherwise redone after more rounds)
+        joined = spec;
+        if (spec && (rc = joins_and_p()) != XFK_OK) return rc;
+        AMG_CHECK(hipEventSynchronize(ev_host));
+        if (!host_int[9]) break;
+        joined = false;
         if (rounds > 4096) {
             set_error("AMG: MIS-2 aggregation did not terminate");
             return XFK_ERR_NOCONV;
         }
     }
-    mis_hint[l] = host_int[5];
-    nc = host_int[0];
-    stats.mis_rounds[l] = host_int[5];
+    mis_hint[l] = host_int[10];
+    nc = host_int[8];
+    stats.mis_rounds[l] = host_int[10];
     int rc = XFK_OK;
     if (allow_stop && (nc == 0 || nc > (long long)(0.9 * n))) {   // no useful coarsening: smoother-only coarsest
         nc = 0;
         return XFK_OK;
     }
-    AMG_CHECK(agg1.alloc(n));
-    AMG_CHECK(agg.alloc(n));
-    k_agg_join1<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, cursor.p, agg1.p);
-    k_agg_join2<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, agg1.p, agg.p);
-    k_agg_join3<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, A.rowptr, cv, A.val, agg.p, agg1.p);
-    std::swap(agg.p, agg1.p);   // agg = the joined map
-    std::swap(agg.n, agg1.n);
-    if (g_prof) g_prof->end();
-    if (std::getenv("XFK_AMG_DEBUG")) {
-        DBuf<int> d;
-        AMG_CHECK(d.alloc(3));
-        AMG_CHECK(hipMemsetAsync(d.p, 0, 3 * sizeof(int), s));
-        k_debug_unagg<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, cnt.p, agg.p, d.p);
-        int h[3];
-        unsigned long long r2[2];
-        AMG_CHECK(hipMemcpyAsync(h, d.p, sizeof(h), hipMemcpyDeviceToHost, s));
-        AMG_CHECK(hipMemcpyAsync(r2, rho.p + 2 * l, sizeof(r2), hipMemcpyDeviceToHost, s));
-        AMG_CHECK(hipStreamSynchronize(s));
-        double ra, rf;
-        std::memcpy(&ra, &r2[0], 8);
-        std::memcpy(&rf, &r2[1], 8);
-        std::fprintf(stderr, "[amg] rank %d level %d n %d nnz %lld nc %lld unaggregated: strong %d weak-only %d isolated %d "
-                     "rhoA/omega %.4g rhoF %.4g mis_rounds %d\n", dist ? rank : 0, l, n, A.nnz, nc, h[0], h[1], h[2],
-                     ra, rf, rounds);
-    }
-    // P = (I - omega D_F^-1 A_F) P_tent
-    SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, wF.p, cv.c16, cv.cbase};
-    SgY YT{nullptr, nullptr, nullptr, agg.p};
-    if (g_prof) g_prof->begin(lv + "P = (I - w D^-1 A) P_tent, R = P^T", 0.0);
-    if ((rc = spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz, dist ? -1 : 4 * l)) != XFK_OK)
-        return rc;
+    if (!joined && (rc = joins_and_p()) != XFK_OK) return rc;
     A.nc = (int)nc;
     if (std::getenv("XFK_AMG_DEBUG")) std::fprintf(stderr, "[amg] level %d P nnz %lld\n", l, A.pnnz);
     // R = P^T: on the side stream (single-device levels) while the main
@@ -2651,6 +2852,45 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     }
     if (g_prof) g_prof->end();
     return XFK_OK;
+}
+
+// joins of the MIS-2 roots' neighbourhoods (agg), then P = (I - omega D_F^-1 A_F) P_tent
+int Amg::joins_and_p_impl(hipStream_t s, int l)
+{
+    AmgLevel &A = *L[l];
+    const int n = A.n;
+    const ColView cv{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr};
+    const std::string lv = g_prof ? "setup L" + std::to_string(l) + " " : std::string();
+    AMG_CHECK(agg1.alloc(n));
+    AMG_CHECK(agg.alloc(n));
+    k_agg_join1<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, cursor.p, agg1.p);
+    k_agg_join2<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, agg1.p, agg.p);
+    k_agg_join3<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, A.rowptr, cv, A.val, agg.p, agg1.p);
+    std::swap(agg.p, agg1.p);   // agg = the joined map
+    std::swap(agg.n, agg1.n);
+    if (g_prof) g_prof->end();
+    if (std::getenv("XFK_AMG_DEBUG")) {
+        DBuf<int> d;
+        AMG_CHECK(d.alloc(3));
+        AMG_CHECK(hipMemsetAsync(d.p, 0, 3 * sizeof(int), s));
+        k_debug_unagg<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, cnt.p, agg.p, d.p);
+        int h[3];
+        unsigned long long r2[2];
+        AMG_CHECK(hipMemcpyAsync(h, d.p, sizeof(h), hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipMemcpyAsync(r2, rho.p + 2 * l, sizeof(r2), hipMemcpyDeviceToHost, s));
+        AMG_CHECK(hipStreamSynchronize(s));
+        double ra, rf;
+        std::memcpy(&ra, &r2[0], 8);
+        std::memcpy(&rf, &r2[1], 8);
+        std::fprintf(stderr, "[amg] rank %d level %d n %d nnz %lld nc %lld unaggregated: strong %d weak-only %d isolated %d "
+                     "rhoA/omega %.4g rhoF %.4g mis_rounds %d\n", dist ? rank : 0, l, n, A.nnz, (long long)host_int[8], h[0], h[1],
+                     h[2], ra, rf, host_int[10]);
+    }
+    // P = (I - omega D_F^-1 A_F) P_tent
+    SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, wF.p, cv.c16, cv.cbase};
+    SgY YT{nullptr, nullptr, nullptr, agg.p};
+    if (g_prof) g_prof->begin(lv + "P = (I - w D^-1 A) P_tent, R = P^T", 0.0);
+    return spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz, dist ? -1 : 4 * l);
 }
 
 // Nested-dissection order of the coarsest level for the dense inverse: a
@@ -2696,24 +2936,33 @@ int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &ld)
     const int n = C.n;
     nd_phases.clear();
     ld = ((n + kBj - 1) / kBj) * kBj;
-    if (n < 8 * kBj || std::getenv("XFK_NO_ND")) return XFK_OK;
+    if (n < 8 * kBj || std::getenv("XFK_NO_ND")) {
+        nd_key_n = -1;
+        return XFK_OK;
+    }
     // the pattern through pinned memory; an unchanged pattern (the next setup
     // of the same matrix family) keeps the plan and its device arrays
     const size_t npat = (size_t)n + 1 + (size_t)C.nnz;
-    if (!nd_prefetched || (size_t)C.nnz > C.col_o.n) {   // (else read with the deferred lengths)
+    {
         int rc = host_ints((int)npat);
         if (rc != XFK_OK) return rc;
         AMG_CHECK(hipMemcpyAsync(host_big, C.rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost, s));
         AMG_CHECK(hipMemcpyAsync(host_big + n + 1, C.col, sizeof(int) * C.nnz, hipMemcpyDeviceToHost, s));
         AMG_CHECK(hipStreamSynchronize(s));
     }
-    nd_prefetched = false;
     if (nd_key.size() == npat && std::equal(nd_key.begin(), nd_key.end(), host_big)) {
         nd_phases = nd_phases_key;
         ld = nd_ld;
         return XFK_OK;
     }
     nd_key.assign(host_big, host_big + npat);
+    // the device copy of the key: the next setup compares its coarsest
+    // pattern on the device and applies this plan without a host read
+    AMG_CHECK(nd_key_dev.alloc(npat));
+    AMG_CHECK(hipMemcpyAsync(nd_key_dev.p, C.rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToDevice, s));
+    AMG_CHECK(hipMemcpyAsync(nd_key_dev.p + n + 1, C.col, sizeof(int) * C.nnz, hipMemcpyDeviceToDevice, s));
+    nd_key_n = n;
+    nd_key_nnz = C.nnz;
     nd_phases_key.clear();
     nd_ld = ld;
     std::vector<int> rp(host_big, host_big + n + 1), cl(host_big + n + 1, host_big + npat);
@@ -2866,6 +3115,110 @@ int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &ld)
     return XFK_OK;
 }
 
+// the dense coarsest inverse of C in the order nd_phases / cinv_perm give
+// (ld: the padded size of that order)
+int Amg::dense_inverse(hipStream_t s, const AmgLevel &C, int ld)
+{
+    const bool nd = !nd_phases.empty();
+    const int nbk = ld / kBj;
+    cinv_ld = ld;
+    AMG_CHECK(cinv.alloc((size_t)ld * ld));
+    const size_t T2 = (size_t)kBj * kBj;
+    // per chain slot and parity: row / column snapshots and the pivot inverse
+    const size_t per = 2 * (size_t)nbk * T2 + T2;
+    AMG_CHECK(bgj_tmp.alloc(2 * kNdChains * per + 1 + ld));
+    auto Rb = [&](int c, int q) { return bgj_tmp.p + (size_t)(2 * c + q) * per; };
+    auto Cb = [&](int c, int q) { return Rb(c, q) + (size_t)nbk * T2; };
+    auto Db = [&](int c, int q) { return Rb(c, q) + 2 * (size_t)nbk * T2; };
+    double *maxd = bgj_tmp.p + 2 * kNdChains * per, *sc = maxd + 1;
+    const int *pm = nd ? cinv_perm.p : nullptr, *ipm = nd ? cinv_iperm.p : nullptr;
+    AMG_CHECK(hipMemsetAsync(cinv.p, 0, sizeof(double) * (size_t)ld * ld, s));
+    k_dense_dscale<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, ipm, sc);
+    k_dense_scatter<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, pm, ipm, sc, cinv.p);
+    k_dense_maxdiag<<<1, 1024, 0, s>>>(ld, ld, cinv.p, maxd);
+    // (a lookahead variant -- block column k+1 first, its pivot block
+    // inverted on a second stream during the rest of the update -- was
+    // measured slower: the two cross-stream waits cost ~15 us per step,
+    // more than the 25 us pivot-block inversion it hides)
+    if (nd) {
+        int par = 0;
+        BgjStep st{};
+        st.nn = nd_phases[0].nch;
+        for (int c = 0; c < st.nn; ++c) {
+            st.nx[c] = nd_phases[0].base[c];
+            st.Dn[c] = Db(c, 0);
+            st.Rn[c] = Rb(c, 0);
+            st.Cn[c] = Cb(c, 0);
+        }
+        k_bgj_init<<<st.nn * (1 + 2 * nbk), 256, 0, s>>>(nbk, ld, cinv.p, st, maxd, bgj_inv_mode());
+        for (size_t ph = 0; ph < nd_phases.size(); ++ph) {
+            const NdPhase &P = nd_phases[ph];
+            for (int t = 0; t < P.steps; ++t) {
+                const int pp = par, qq = par ^ 1;
+                BgjStep x{};
+                x.n = P.nch;
+                for (int c = 0; c < P.nch; ++c) {
+                    x.k[c] = P.base[c] + t;
+                    x.D[c] = Db(c, pp);
+                    x.R[c] = Rb(c, pp);
+                    x.C[c] = Cb(c, pp);
+                }
+                if (t + 1 < P.steps) {
+                    x.nn = P.nch;
+                    for (int c = 0; c < P.nch; ++c) x.nx[c] = P.base[c] + t + 1;
+                } else if (ph + 1 < nd_phases.size()) {
+                    const NdPhase &Q = nd_phases[ph + 1];
+                    x.nn = Q.nch;
+                    for (int c = 0; c < Q.nch; ++c) x.nx[c] = Q.base[c];
+                }
+                for (int c = 0; c < x.nn; ++c) {
+                    x.Dn[c] = Db(c, qq);
+                    x.Rn[c] = Rb(c, qq);
+                    x.Cn[c] = Cb(c, qq);
+                }
+                k_bgj_multi<<<P.ntiles + x.nn, 256, 0, s>>>(nbk, ld, cinv.p, x, nd_mask.p + ph * (size_t)nbk,
+                                                            nd_tiles.p + P.tiles_off, maxd, bgj_inv_mode());
+                par = qq;
+            }
+        }
+    } else {
+        BgjStep st{};
+        st.nn = 1;
+        st.nx[0] = 0;
+        st.Dn[0] = Db(0, 0);
+        st.Rn[0] = Rb(0, 0);
+        st.Cn[0] = Cb(0, 0);
+        k_bgj_init<<<1 + 2 * nbk, 256, 0, s>>>(nbk, ld, cinv.p, st, maxd, bgj_inv_mode());
+        for (int k = 0; k < nbk; ++k) {
+            const int p = k & 1, q = (k + 1) & 1;
+            k_bgj_step<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, Db(0, p), Rb(0, p), Cb(0, p), Db(0, q),
+                                                 Rb(0, q), Cb(0, q), maxd, bgj_inv_mode());
+        }
+    }
+    {
+        const int ldo = ((C.n + kBj - 1) / kBj) * kBj;
+        AMG_CHECK(cinv_o.alloc((size_t)ldo * ldo));
+        k_dense_unperm<<<ld, 256, 0, s>>>(C.n, ld, ldo, cinv.p, sc, nd ? cinv_iperm.p : nullptr, cinv_o.p);
+        cinv_apply = cinv_o.p;
+        cinv_ld = ldo;
+    }
+    return XFK_OK;
+}
+
+// the V-cycle's per-level vectors
+int Amg::alloc_vectors()
+{
+    for (int k = 0; k < nlev; ++k) {
+        AmgLevel &A = *L[k];
+        const size_t nv = (size_t)std::max(1, std::max(A.n, A.ncol_smooth));
+        AMG_CHECK(A.xa.alloc(nv));
+        AMG_CHECK(A.xb.alloc(nv));
+        AMG_CHECK(A.r.alloc((size_t)std::max(1, A.n)));
+        if (k > 0) AMG_CHECK(A.b.alloc((size_t)std::max(1, A.n)));
+    }
+    return XFK_OK;
+}
+
 // levels l0.. of the hierarchy (L[l0] set up by the caller), then the
 // smoother vectors and the dense coarsest inverse
 int Amg::build(hipStream_t s, int l0)
@@ -3001,23 +3354,33 @@ int Amg::build(hipStream_t s, int l0)
     nlev = l + 1;
     {
         // the SpGEMM lengths taken without a host check (capacity hints); an
-        // overflow means a hint was too small: rebuild with measured capacities
-        bool overflow = false;
-        // the coarsest pattern for the nested-dissection plan rides on the
-        // same host check (its length is deferred too: the whole capacity)
-        nd_prefetched = false;
-        if (dense_coarse && def_n > 0 && nlev - 1 > l0) {
-            AmgLevel &C = *L[nlev - 1];
-            if (C.col == C.col_o.p && C.n >= 8 * kBj) {
-                const size_t cap = C.col_o.n;
-                int rc = host_ints((int)((size_t)C.n + 1 + cap));
-                if (rc != XFK_OK) return rc;
-                AMG_CHECK(hipMemcpyAsync(host_big, C.rowptr, sizeof(int) * ((size_t)C.n + 1), hipMemcpyDeviceToHost, s));
-                AMG_CHECK(hipMemcpyAsync(host_big + C.n + 1, C.col, sizeof(int) * cap, hipMemcpyDeviceToHost, s));
-                nd_prefetched = true;
-            }
+        // overflow means a hint was too small: rebuild with measured capacities.
+        // The dense coarsest inverse needs the nested-dissection plan, which
+        // the host makes from the coarsest pattern; when the pattern equals
+        // the one the cached plan was made for (compared on the device, read
+        // with the deferred lengths), the inverse launched ahead of that read
+        // stands -- otherwise (or on overflow) it is redone
+        AmgLevel &C = *L[nlev - 1];
+        const bool nd_spec = dense_coarse && spec_on() && !g_prof && def_n > 0 && nlev - 1 > l0 &&
+                             C.n >= 8 * kBj && nd_key_n == C.n && C.col == C.col_o.p &&
+                             (size_t)nd_key_nnz <= C.col_o.n && !std::getenv("XFK_NO_ND");
+        if (nd_spec) {
+            AMG_CHECK(mis_out.alloc(4));
+            AMG_CHECK(hipMemsetAsync(mis_out.p + 3, 0, sizeof(int), s));
+            const int nt = (int)std::max((long long)C.n + 1, nd_key_nnz);
+            k_pattern_diff<<<nb(nt), kB, 0, s>>>(C.n, C.rowptr, C.col, nd_key_dev.p, (int)nd_key_nnz, mis_out.p + 3);
+            AMG_CHECK(hipMemcpyAsync(host_int + 11, mis_out.p + 3, sizeof(int), hipMemcpyDeviceToHost, s));
         }
-        int rc = resolve_deferred(s, overflow);
+        int rc = fetch_deferred(s);
+        if (rc != XFK_OK) return rc;
+        if (nd_spec) {
+            rc = alloc_vectors();
+            if (rc != XFK_OK) return rc;
+            nd_phases = nd_phases_key;
+            if ((rc = dense_inverse(s, C, nd_ld)) != XFK_OK) return rc;
+        }
+        bool overflow = false;
+        rc = wait_deferred(s, overflow);
         if (rc != XFK_OK) return rc;
         if (overflow) {
             if (sw_used) {   // nothing of this attempt may still run on the side stream
@@ -3028,109 +3391,19 @@ int Amg::build(hipStream_t s, int l0)
             return build(s, l0);
         }
         for (int k = l0; k < nlev; ++k) stats.nnz[k] = L[k]->nnz;
-    }
-    stats.levels = nlev;
-    double tot = 0;
-    for (int k = 0; k < nlev; ++k) tot += (double)stats.nnz[k];
-    stats.op_complexity = stats.nnz[0] > 0 ? tot / (double)stats.nnz[0] : 0.0;
-    for (int k = 0; k < nlev; ++k) {
-        AmgLevel &A = *L[k];
-        const size_t nv = (size_t)std::max(1, std::max(A.n, A.ncol_smooth));
-        AMG_CHECK(A.xa.alloc(nv));
-        AMG_CHECK(A.xb.alloc(nv));
-        AMG_CHECK(A.r.alloc((size_t)std::max(1, A.n)));
-        if (k > 0) AMG_CHECK(A.b.alloc((size_t)std::max(1, A.n)));
-    }
-    if (dense_coarse) {
-        AmgLevel &C = *L[nlev - 1];
-        if (g_prof) g_prof->begin("setup L" + std::to_string(nlev - 1) + " dense inverse (blocked Gauss-Jordan)", 0.0);
-        int ld = 0;
-        int rc = nd_order(s, C, ld);
+        stats.levels = nlev;
+        double tot = 0;
+        for (int k = 0; k < nlev; ++k) tot += (double)stats.nnz[k];
+        stats.op_complexity = stats.nnz[0] > 0 ? tot / (double)stats.nnz[0] : 0.0;
+        rc = alloc_vectors();
         if (rc != XFK_OK) return rc;
-        const bool nd = !nd_phases.empty();
-        const int nbk = ld / kBj;
-        cinv_ld = ld;
-        AMG_CHECK(cinv.alloc((size_t)ld * ld));
-        const size_t T2 = (size_t)kBj * kBj;
-        // per chain slot and parity: row / column snapshots and the pivot inverse
-        const size_t per = 2 * (size_t)nbk * T2 + T2;
-        AMG_CHECK(bgj_tmp.alloc(2 * kNdChains * per + 1 + ld));
-        auto Rb = [&](int c, int q) { return bgj_tmp.p + (size_t)(2 * c + q) * per; };
-        auto Cb = [&](int c, int q) { return Rb(c, q) + (size_t)nbk * T2; };
-        auto Db = [&](int c, int q) { return Rb(c, q) + 2 * (size_t)nbk * T2; };
-        double *maxd = bgj_tmp.p + 2 * kNdChains * per, *sc = maxd + 1;
-        const int *pm = nd ? cinv_perm.p : nullptr, *ipm = nd ? cinv_iperm.p : nullptr;
-        AMG_CHECK(hipMemsetAsync(cinv.p, 0, sizeof(double) * (size_t)ld * ld, s));
-        k_dense_dscale<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, ipm, sc);
-        k_dense_scatter<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, pm, ipm, sc, cinv.p);
-        k_dense_maxdiag<<<1, 1024, 0, s>>>(ld, ld, cinv.p, maxd);
-        // (a lookahead variant -- block column k+1 first, its pivot block
-        // inverted on a second stream during the rest of the update -- was
-        // measured slower: the two cross-stream waits cost ~15 us per step,
-        // more than the 25 us pivot-block inversion it hides)
-        if (nd) {
-            int par = 0;
-            BgjStep st{};
-            st.nn = nd_phases[0].nch;
-            for (int c = 0; c < st.nn; ++c) {
-                st.nx[c] = nd_phases[0].base[c];
-                st.Dn[c] = Db(c, 0);
-                st.Rn[c] = Rb(c, 0);
-                st.Cn[c] = Cb(c, 0);
-            }
-            k_bgj_init<<<st.nn * (1 + 2 * nbk), 256, 0, s>>>(nbk, ld, cinv.p, st, maxd);
-            for (size_t ph = 0; ph < nd_phases.size(); ++ph) {
-                const NdPhase &P = nd_phases[ph];
-                for (int t = 0; t < P.steps; ++t) {
-                    const int pp = par, qq = par ^ 1;
-                    BgjStep x{};
-                    x.n = P.nch;
-                    for (int c = 0; c < P.nch; ++c) {
-                        x.k[c] = P.base[c] + t;
-                        x.D[c] = Db(c, pp);
-                        x.R[c] = Rb(c, pp);
-                        x.C[c] = Cb(c, pp);
-                    }
-                    if (t + 1 < P.steps) {
-                        x.nn = P.nch;
-                        for (int c = 0; c < P.nch; ++c) x.nx[c] = P.base[c] + t + 1;
-                    } else if (ph + 1 < nd_phases.size()) {
-                        const NdPhase &Q = nd_phases[ph + 1];
-                        x.nn = Q.nch;
-                        for (int c = 0; c < Q.nch; ++c) x.nx[c] = Q.base[c];
-                    }
-                    for (int c = 0; c < x.nn; ++c) {
-                        x.Dn[c] = Db(c, qq);
-                        x.Rn[c] = Rb(c, qq);
-                        x.Cn[c] = Cb(c, qq);
-                    }
-                    k_bgj_multi<<<P.ntiles + x.nn, 256, 0, s>>>(nbk, ld, cinv.p, x, nd_mask.p + ph * (size_t)nbk,
-                                                                nd_tiles.p + P.tiles_off, maxd);
-                    par = qq;
-                }
-            }
-        } else {
-            BgjStep st{};
-            st.nn = 1;
-            st.nx[0] = 0;
-            st.Dn[0] = Db(0, 0);
-            st.Rn[0] = Rb(0, 0);
-            st.Cn[0] = Cb(0, 0);
-            k_bgj_init<<<1 + 2 * nbk, 256, 0, s>>>(nbk, ld, cinv.p, st, maxd);
-            for (int k = 0; k < nbk; ++k) {
-                const int p = k & 1, q = (k + 1) & 1;
-                k_bgj_step<<<nbk * nbk, 256, 0, s>>>(k, nbk, ld, cinv.p, Db(0, p), Rb(0, p), Cb(0, p), Db(0, q),
-                                                     Rb(0, q), Cb(0, q), maxd);
-            }
+        if (dense_coarse && !(nd_spec && host_int[11] == 0)) {
+            if (g_prof) g_prof->begin("setup L" + std::to_string(nlev - 1) + " dense inverse (blocked Gauss-Jordan)", 0.0);
+            int ld = 0;
+            if ((rc = nd_order(s, C, ld)) != XFK_OK) return rc;
+            if ((rc = dense_inverse(s, C, ld)) != XFK_OK) return rc;
+            if (g_prof) g_prof->end();
         }
-        {
-            const int ldo = ((C.n + kBj - 1) / kBj) * kBj;
-            AMG_CHECK(cinv_o.alloc((size_t)ldo * ldo));
-            k_dense_unperm<<<ld, 256, 0, s>>>(C.n, ld, ldo, cinv.p, sc, nd ? cinv_iperm.p : nullptr, cinv_o.p);
-            cinv_apply = cinv_o.p;
-            cinv_ld = ldo;
-        }
-        if (g_prof) g_prof->end();
     }
     if (sw_used) {   // the V-cycle reads R, P~, R~: join the side stream (after the dense inverse's launches)
         AMG_CHECK(hipEventRecord(sw.b, sw.cs));
@@ -3690,7 +3963,7 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
                                                    8.0 * nc + (yadd ? 8.0 * n : 0.0),
                   launch_fold_pre(s, A, rho, b, y, C.b.p, done, yadd));
         const double *xc;
-        if (l == M.wcycle_level() && l + 1 < M.nlev - 1) {
+        if (M.w_at(l)) {
             // W-cycle at this level: a second coarse correction from the
             // coarse residual after the first, b_c' = b_c - A_c x_c (Galerkin:
             // R (b - A (x_pre + P x_c)) = b_c - A_c x_c), x_c += V(b_c'); the
