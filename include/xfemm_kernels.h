@@ -181,9 +181,13 @@ enum {
                                    operators (the PCG SpMV, the sweeps, P~, R) read 16-bit column
                                    offsets per row tile (tiles spanning > 65535 columns read the int
                                    columns); 0: int columns.  The same column indices: the same bits. */
-    XFK_OPT_AMG_WLEVEL = 10     /* the folded coarse level that runs a W-cycle (two coarse
+    XFK_OPT_AMG_WLEVEL = 10,    /* the folded coarse level that runs a W-cycle (two coarse
                                    corrections); -2 (default): the level above the last V-cycle
                                    level (XFK_AMG_W overrides), -1: a plain V-cycle */
+    XFK_OPT_AMG_F32 = 11        /* 1 (default, unless XFK_AMG_F32=0 is set; needs 16-bit columns):
+                                   the V-cycle's level-0 transfers (R, P~) store f32 values,
+                                   products and sums in f64; 0: f64 values.  The sweeps and the
+                                   PCG's own SpMV keep A in f64. */
 };
 int xfk_set_option(xfk_problem *prob, int option, double value);
 

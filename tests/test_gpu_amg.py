@@ -277,7 +277,8 @@ def test_folded_cycle_equals_plain_cycle(cells, nonlinear):
 
 def test_col16_tiles_are_bit_identical_with_wide_tile_fallback():
     """Level 0's 16-bit tile columns (XFK_OPT_AMG_COL16, default on) give the
-    same bits as the int columns: once on the banded numbering (every tile
+    same bits as the int columns (f64 operator values in both, since the f32
+    level-0 operators come with the 16-bit columns): once on the banded numbering (every tile
     fits: 2 B per nonzero) and once with the first half of the nodes in a
     random order (those tiles span > 65535 columns and read the int array:
     between 2 and 4 B per nonzero)."""
@@ -293,7 +294,7 @@ def test_col16_tiles_are_bit_identical_with_wide_tile_fallback():
     for k, lo, hi in ((kw, 2.0, 2.0), (kws, 2.05, 3.95)):
         out = []
         for c16 in (True, False):
-            P = kernels.Static2DProblem(**k, precond="amg", amg_col16=c16)
+            P = kernels.Static2DProblem(**k, precond="amg", amg_col16=c16, amg_f32=False)
             r = P.solve()
             out.append((P.solution(), r["cg_iters"], P.spmv_col_bytes()))
             if c16:
@@ -307,6 +308,30 @@ def test_col16_tiles_are_bit_identical_with_wide_tile_fallback():
         M = sp.csr_matrix((val, col, rp), shape=(len(rp) - 1,) * 2)
         V = A1 / C_ANS
         assert np.linalg.norm(M @ V - b) <= 1e-5 * np.linalg.norm(b)
+
+
+@pytest.mark.parametrize("cells,nonlinear", [(200, False), (60, True)])
+def test_f32_level0_operators_meet_parity(cells, nonlinear):
+    """The V-cycle's level-0 transfers with f32 values (XFK_OPT_AMG_F32,
+    default on: R and P~; products and sums in f64, the sweeps and the PCG's
+    SpMV in f64) change the preconditioner by f32 rounding only: both answers
+    meet the parity tolerance against the converged oracle, agree with each
+    other to it, take the same PCG iterations within one per Newton step, and
+    the f32 path is deterministic (the nonlinear case also runs the Newton
+    refresh of the hierarchy)."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(cells, nonlinear=nonlinear))
+    Ao, _, _ = oracle.solve(pr, mesh)
+    tol = TOL_NONLINEAR if nonlinear else TOL_LINEAR
+    A32, r32, Ac = _solve_vs(kw, pr, mesh, precond="amg", amg_f32=True)
+    A64, r64 = _solve(kw, precond="amg", amg_f32=False)
+    A32b, _ = _solve(kw, precond="amg", amg_f32=True)
+    assert rel_err(A32, Ac) <= tol, parity_message(A32, Ao, Ac, tol)
+    assert rel_err(A64, Ac) <= tol, parity_message(A64, Ao, Ac, tol)
+    assert rel_err(A32, A64) <= tol
+    assert not np.array_equal(A32, A64)                    # the two precisions really ran
+    assert np.array_equal(A32.view(np.int64), A32b.view(np.int64))
+    assert r32["newton_iters"] == r64["newton_iters"]
+    assert abs(r32["cg_iters"] - r64["cg_iters"]) <= r32["newton_iters"], (r32["cg_iters"], r64["cg_iters"])
 
 
 @pytest.mark.parametrize("nonlinear", [False, True])

@@ -79,6 +79,12 @@ struct AmgLevel {
     bool has16 = false;
     DBuf<unsigned short> a16, f16, r16;
     DBuf<int> a16b, f16b, r16b;
+    // level 0 (with has16): the V-cycle's transfers R and P~ with f32 values
+    // (products and sums in f64; A keeps f64 -- a32 only with XFK_AMG_F32_SWEEP=1)
+    bool has32 = false;
+    DBuf<float> a32, r32, f32v;
+    // stored bytes per nonzero of the level's V-cycle transfers (column + value)
+    double nz_bytes() const { return (has16 ? 2.0 : 4.0) + (has32 ? 4.0 : 8.0); }
 };
 
 struct AmgStats {
@@ -157,6 +163,7 @@ struct Amg {
     int dense_max = kAmgDenseMax;     // coarsest level: dense inverse at <= dense_max rows
     int fold_on = -1;                 // folded V(1,1) levels: 1 / 0, -1 = the XFK_AMG_FOLD default
     int col16 = -1;                   // 16-bit tile columns on level 0: 1 / 0, -1 = on unless XFK_NO_COL16
+    int prec32 = -1;                  // f32 values of level 0's V-cycle operators: 1 / 0, -1 = on unless XFK_AMG_F32=0
     int lrep = 0;
     xfk_comm *comm = nullptr;
     int nranks = 1, rank = 0;

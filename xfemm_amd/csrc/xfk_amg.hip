@@ -294,16 +294,21 @@ __global__ void k_mis_max(int n, const int *__restrict__ rowptr, ColView cv,
 // second max sweep fused with the state update: an undecided node whose
 // distance-2 maximum is itself joins the set; one that sees a set member
 // within distance 2 leaves
-template <int G>
+// ROOTS (the last round of a batch): every row also writes its root flag
+// (k_agg_roots folded in: one launch less per level)
+template <int G, bool ROOTS = false>
 __global__ void k_mis_update(int n, const int *__restrict__ rowptr, ColView cv,
                              const unsigned char *__restrict__ sflag, const MisKey *__restrict__ t1,
-                             MisKey *__restrict__ key, const int *prev, int *undecided)
+                             MisKey *__restrict__ key, const int *prev, int *undecided, int *__restrict__ flag = nullptr)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = t / G, g = t % G;
-    if (i >= n || *prev == 0) return;
+    if (i >= n) return;
     const MisKey k = key[i];
-    if (key_st(k) != kStUnd) return;   // uniform over the row's lanes
+    if (*prev == 0 || key_st(k) != kStUnd) {   // uniform over the row's lanes
+        if (ROOTS && g == 0) flag[i] = key_st(k) == kStIn;
+        return;
+    }
     MisKey m = t1[i];
     const int cb = cv.base(i);
     for (int q = rowptr[i] + g; q < rowptr[i + 1]; q += G)
@@ -311,16 +316,18 @@ __global__ void k_mis_update(int n, const int *__restrict__ rowptr, ColView cv,
 #pragma unroll
     for (int off = 1; off < G; off <<= 1) m = max(m, (MisKey)__shfl_xor((int)m, off, G));
     if (g != 0) return;
-    if (key_low(m) == perm30((unsigned)i)) key[i] = (kStIn << 30) | key_low(k);
-    else if (key_st(m) == kStIn) key[i] = key_low(k);
-    else *undecided = 1;   // benign race: every writer stores 1
+    int root = 0;
+    if (key_low(m) == perm30((unsigned)i)) {
+        key[i] = (kStIn << 30) | key_low(k);
+        root = 1;
+    } else if (key_st(m) == kStIn) {
+        key[i] = key_low(k);
+    } else {
+        *undecided = 1;   // benign race: every writer stores 1
+    }
+    if (ROOTS) flag[i] = root;
 }
 
-__global__ void k_agg_roots(int n, const MisKey *__restrict__ key, int *__restrict__ flag)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) flag[i] = key_st(key[i]) == kStIn;
-}
 
 // the aggregation's host check in one read: {roots, undecided flag, rounds that did work}
 __global__ void k_mis_pack(const int *__restrict__ roots, const int *__restrict__ und, const int *__restrict__ run,
@@ -454,10 +461,175 @@ __global__ void k_rt_fill(int n, const int *__restrict__ prow, const int *__rest
     }
 }
 
+// Tiled transpose (XFK_RT_TILE, default on): a workgroup of 256 rows holds
+// its entries' columns in a window [lo, hi] (a banded numbering: a few
+// hundred columns), counts them in LDS and touches
+// the global counts once per (workgroup, column) instead of once per entry.
+// The fill reserves one chunk of each target row per workgroup (returning
+// atomic on the count-down counter), places its entries there through LDS
+// cursors and writes the values with the columns; the row sort restores the
+// order.  A window wider than kRtWin falls back to per-entry atomics.
+constexpr int kRtWin = 4096;
+template <bool FILL>
+__global__ void __launch_bounds__(256) k_rt_tile(int n, const int *__restrict__ mrow, const int *__restrict__ mcol,
+                                                 const double *__restrict__ mval, const int *__restrict__ trow,
+                                                 int *__restrict__ cnt, int *__restrict__ tcol,
+                                                 double *__restrict__ tval)
+{
+    __shared__ int h[kRtWin];
+    __shared__ int cur[FILL ? kRtWin : 1];
+    __shared__ int red[8];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int s = i < n ? mrow[i] : 0, e = i < n ? mrow[i + 1] : 0;
+    int lo = INT_MAX, hi = INT_MIN;   // (every entry: the rows need not be sorted)
+    for (int k = s; k < e; ++k) {
+        const int c = mcol[k];
+        lo = min(lo, c);
+        hi = max(hi, c);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off, 64));
+        hi = max(hi, __shfl_xor(hi, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = lo;
+        red[4 + (threadIdx.x >> 6)] = hi;
+    }
+    __syncthreads();
+    lo = min(min(red[0], red[1]), min(red[2], red[3]));
+    hi = max(max(red[4], red[5]), max(red[6], red[7]));
+    if (hi < lo) return;   // no entries in this tile
+    if ((long long)hi - lo >= kRtWin) {   // wide window: one global atomic per entry
+        for (int k = s; k < e; ++k) {
+            const int J = mcol[k];
+            if (!FILL) {
+                atomicAdd(&cnt[J], 1);
+            } else {
+                const int pos = trow[J] + atomicSub(&cnt[J], 1) - 1;
+                tcol[pos] = i;
+                tval[pos] = mval[k];
+            }
+        }
+        return;
+    }
+    const int w = hi - lo + 1;
+    for (int c = threadIdx.x; c < w; c += 256) {
+        h[c] = 0;
+        if (FILL) cur[c] = 0;
+    }
+    __syncthreads();
+    for (int k = s; k < e; ++k) atomicAdd(&h[mcol[k] - lo], 1);
+    __syncthreads();
+    if (!FILL) {
+        for (int c = threadIdx.x; c < w; c += 256)
+            if (h[c]) atomicAdd(&cnt[lo + c], h[c]);
+        return;
+    }
+    for (int c = threadIdx.x; c < w; c += 256) {
+        const int m = h[c];
+        if (m) h[c] = trow[lo + c] + atomicSub(&cnt[lo + c], m) - m;   // this tile's chunk of row lo + c
+    }
+    __syncthreads();
+    for (int k = s; k < e; ++k) {
+        const int c = mcol[k] - lo;
+        const int pos = h[c] + atomicAdd(&cur[c], 1);
+        tcol[pos] = i;
+        tval[pos] = mval[k];
+    }
+}
+
+// sort each row's (column, value) pairs by column (the rows' entries are
+// distinct).  A wavefront takes 4 consecutive rows: when all hold <= 64
+// entries (the usual case) each 16-lane group ranks its row's columns in
+// wave-private LDS (rank = number of smaller columns, <= 64 broadcast reads
+// per entry) and writes every pair straight to its rank -- no compare-exchange
+// network, values never shuffled; longer rows are taken one at a time by the
+// whole wavefront (<= kRtLdsRow entries in LDS, else lane 0's insertion sort).
+constexpr int kRtLdsRow = 1024;
+__global__ void __launch_bounds__(256) k_rt_sort_pairs(int nc, const int *__restrict__ rrow, int *__restrict__ rcol,
+                                                       double *__restrict__ rval)
+{
+    __shared__ int buf[4][kRtLdsRow];
+    __shared__ double bufv[4][kRtLdsRow];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int J0 = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 4;
+    if (J0 >= nc) return;
+    int *b = buf[wv];
+    double *bv = bufv[wv];
+    auto wsync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // this group's row (groups past nc get an empty one)
+    const int g = lane >> 4, gl = lane & 15, J = J0 + g;
+    const int s = J < nc ? rrow[J] : 0, len = J < nc ? rrow[J + 1] - s : 0;
+    int mx = len;
+#pragma unroll
+    for (int off = 16; off < 64; off <<= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+    if (mx <= 64) {
+        int *gb = b + 64 * g;
+        int kk[4];
+        double vv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int a = gl + 16 * q;
+            kk[q] = a < len ? rcol[s + a] : 0;
+            vv[q] = a < len ? rval[s + a] : 0.0;
+            if (a < len) gb[a] = kk[q];
+        }
+        wsync();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int a = gl + 16 * q;
+            if (a < len) {
+                int rk = 0;
+                for (int t = 0; t < len; ++t) rk += gb[t] < kk[q];
+                rcol[s + rk] = kk[q];
+                rval[s + rk] = vv[q];
+            }
+        }
+        return;
+    }
+    for (int r = 0; r < 4 && J0 + r < nc; ++r) {
+        const int Jr = J0 + r;
+        const int sr = rrow[Jr], er = rrow[Jr + 1], lr = er - sr;
+        if (lr <= 1) continue;
+        if (lr <= kRtLdsRow) {
+            wsync();   // the previous row's reads of b are done
+            for (int a = lane; a < lr; a += 64) {
+                b[a] = rcol[sr + a];
+                bv[a] = rval[sr + a];
+            }
+            wsync();
+            for (int a = lane; a < lr; a += 64) {
+                const int v = b[a];
+                int rk = 0;
+                for (int q = 0; q < lr; ++q) rk += b[q] < v;
+                rcol[sr + rk] = v;
+                rval[sr + rk] = bv[a];
+            }
+        } else if (lane == 0) {
+            for (int a = sr + 1; a < er; ++a) {
+                const int key = rcol[a];
+                const double kv = rval[a];
+                int q = a - 1;
+                while (q >= sr && rcol[q] > key) {
+                    rcol[q + 1] = rcol[q];
+                    rval[q + 1] = rval[q];
+                    --q;
+                }
+                rcol[q + 1] = key;
+                rval[q + 1] = kv;
+            }
+        }
+    }
+}
+
 // sort each R row (the atomic fill order is arbitrary), then look the values
 // up in P.  One wavefront per row: rows of <= 64 entries are sorted by a
 // register bitonic network, longer ones by lane 0 (insertion sort).
-constexpr int kRtLdsRow = 1024;
 __global__ void __launch_bounds__(256) k_rt_sort_vals(int nc, const int *__restrict__ rrow, int *__restrict__ rcol,
                                                       const int *__restrict__ prow, const int *__restrict__ pcol,
                                                       const double *__restrict__ pval, double *__restrict__ rval)
@@ -1802,9 +1974,9 @@ __device__ __forceinline__ double smooth_finish_v(int i, double ax, double w, do
 // part_gam (the PCG's last level-0 sweep only): per-tile partials of
 // b . out, i.e. gamma = r . u of the CG, in the layout and summation order of
 // k_cg_spmv's (same tiles, same workgroup sum), so the SpMV need not read r
-template <int MODE, int B, int SLOTS = 2>
+template <int MODE, int B, int SLOTS = 2, class V = double>
 __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__restrict__ rowptr,
-                                                         const int *__restrict__ col, const double *__restrict__ val,
+                                                         const int *__restrict__ col, const V *__restrict__ val,
                                                          const double *__restrict__ dinv,
                                                          const unsigned long long *rho, const double *__restrict__ b,
                                                          const double *__restrict__ x, double *__restrict__ out,
@@ -1884,9 +2056,9 @@ __global__ void __launch_bounds__(256) k_amg_smooth_g(int n, int ncl, const int 
 }
 
 // y = M x (ACC: y += M x), tile form (large transfer operators)
-template <int B, bool ACC, int SLOTS = 2>
+template <int B, bool ACC, int SLOTS = 2, class V = double>
 __global__ void __launch_bounds__(B) k_csr_mv_tile(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
-                                                   const double *__restrict__ val, const double *__restrict__ x,
+                                                   const V *__restrict__ val, const double *__restrict__ x,
                                                    double *__restrict__ y, const int *done,
                                                    const unsigned short *__restrict__ c16 = nullptr,
                                                    const int *__restrict__ cbase = nullptr)
@@ -1952,9 +2124,9 @@ __global__ void __launch_bounds__(256) k_fold_p(int n, const unsigned long long 
 // R r'): u = x_pre + w D^-1 r' + P~ x_c, i.e. the prolongation and the
 // post-sweep in one pass over P~ instead of P and A.  Tile shape and r.u
 // partials as k_amg_smooth's last sweep (the SpMV's tiles and summation order).
-template <int B, int SLOTS>
+template <int B, int SLOTS, class V>
 __global__ void __launch_bounds__(B) k_fold_post0(int n, const int *__restrict__ frow, const int *__restrict__ fcol,
-                                                  const double *__restrict__ fval, const double *__restrict__ xc,
+                                                  const V *__restrict__ fval, const double *__restrict__ xc,
                                                   const double *__restrict__ dinv, const unsigned long long *rho,
                                                   const double *__restrict__ rres,
                                                   const double *__restrict__ b, double *__restrict__ out,
@@ -2105,6 +2277,15 @@ __global__ void k_int2dbl(long long n, const int *__restrict__ a, double *__rest
     const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i < n) b[i] = (double)a[i];
 }
+// b = (float) a over the rowptr[n] entries of a CSR (the length read on the
+// device: the host may only hold an upper bound); fixed grid, grid-stride
+__global__ void k_d2f(int n, const int *__restrict__ rowptr, const double *__restrict__ a, float *__restrict__ b)
+{
+    const long long m = rowptr[n];
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < m; i += (long long)gridDim.x * blockDim.x)
+        b[i] = (float)a[i];
+}
+
 __global__ void k_add_int(long long n, int *__restrict__ a, int v)
 {
     const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -2471,6 +2652,21 @@ static int rmv_mode()
     return v;
 }
 
+// level 0 with f32 values: the 256-row tile kernels (level 0 always has >= kTileMinRows rows)
+void launch_mv32(hipStream_t s, int n, const int *rowptr, const int *col, const float *val, const double *x,
+                 double *y, bool acc, int G, const int *done, const unsigned short *c16, const int *cbase)
+{
+    if (n <= 0) return;
+    const int g = (n + 255) / 256;
+    if (G <= 4) {
+        if (acc) k_csr_mv_tile<256, true, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+        else k_csr_mv_tile<256, false, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+    } else {
+        if (acc) k_csr_mv_tile<256, true, 6><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+        else k_csr_mv_tile<256, false, 6><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+    }
+}
+
 // c16 / cbase: 16-bit column offsets in 256-row tiles (used by the 256-row tile kernels only)
 void launch_mv(hipStream_t s, int n, const int *rowptr, const int *col, const double *val, const double *x, double *y,
                bool acc, int G, const int *done, const unsigned short *c16 = nullptr, const int *cbase = nullptr)
@@ -2618,6 +2814,35 @@ static bool side_setup_on()
     return v;
 }
 
+// XFK_AMG_F32=0: level 0's V-cycle operators keep f64 values
+static bool f32_on()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_AMG_F32");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+
+// XFK_AMG_F32_SWEEP=1: the level-0 sweeps read the f32 copy of A too (measured
+// slower: the sweep's two gathers per entry, not its value stream, bound it)
+static bool f32_sweep_on()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_AMG_F32_SWEEP");
+        return e && std::atoi(e) != 0;
+    }();
+    return v;
+}
+
+// f32 copy of a CSR's values (cap: an upper bound of its length, for the allocation)
+static int to_f32(hipStream_t s, int n, const int *rowptr, long long cap, const double *a, DBuf<float> &b)
+{
+    if (b.alloc((size_t)std::max(1LL, cap)) != hipSuccess) return XFK_ERR_HIP;
+    if (n > 0) k_d2f<<<2048, 256, 0, s>>>(n, rowptr, a, b.p);
+    return XFK_OK;
+}
+
 // XFK_NO_SPEC=1: no setup work enqueued ahead of a host check
 static bool spec_on()
 {
@@ -2691,6 +2916,7 @@ int Amg::init(hipStream_t s)
     for (auto &lv : L) {   // levels are rebuilt: none sharded until setup_dist says so
         lv->dist = false;
         lv->has16 = false;
+        lv->has32 = false;
         lv->plan = HaloPlan();
         lv->ts.B = 0;
     }
@@ -2726,14 +2952,34 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
 // back down, rows sorted by a wave bitonic network, values looked up in M.
 // T's arrays hold as many entries as M (no read-back of the scan).
 // cnt / tmp: scratch of the stream it runs on (the setup's side stream has its own)
+// XFK_RT_TILE=0: the per-entry transpose (global atomics, values looked up after the sort)
+static bool rt_tile_on()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_RT_TILE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+
 static int transpose_csr(DBuf<int> &cnt, DBuf<char> &tmp, hipStream_t s, int n, int nc, const int *mrow,
                          const int *mcol, const double *mval, int *trow, int *tcol, double *tval)
 {
     AMG_CHECK(cnt.alloc((size_t)std::max(n, nc) + 1));
     AMG_CHECK(hipMemsetAsync(cnt.p, 0, sizeof(int) * ((size_t)nc + 1), s));
-    if (n > 0) k_rt_count<<<nb(n), kB, 0, s>>>(n, mrow, mcol, cnt.p);
+    const bool tiled = rt_tile_on();
+    if (n > 0) {
+        if (tiled) k_rt_tile<false><<<nb(n), 256, 0, s>>>(n, mrow, mcol, mval, trow, cnt.p, tcol, tval);
+        else k_rt_count<<<nb(n), kB, 0, s>>>(n, mrow, mcol, cnt.p);
+    }
     int rc = scan_only(tmp, s, cnt.p, trow, nc);
     if (rc != XFK_OK) return rc;
+    if (tiled) {
+        if (n > 0) k_rt_tile<true><<<nb(n), 256, 0, s>>>(n, mrow, mcol, mval, trow, cnt.p, tcol, tval);
+        if (nc > 0) k_rt_sort_pairs<<<(int)((((long long)nc + 3) / 4 * 64 + 255) / 256), 256, 0, s>>>(nc, trow, tcol, tval);
+        AMG_CHECK(hipGetLastError());
+        return XFK_OK;
+    }
     if (n > 0) k_rt_fill<<<nb(n), kB, 0, s>>>(n, mrow, mcol, trow, cnt.p, tcol);
     if (nc > 0)
         k_rt_sort_vals<<<(int)(((long long)nc * 64 + 255) / 256), 256, 0, s>>>(nc, trow, tcol, mrow, mcol, mval, tval);
@@ -2787,16 +3033,24 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     for (int batch = hint != mis_hint.end() ? std::max(1, hint->second) : 12;; batch = 2) {
         for (int b = 0; b < batch; ++b, ++rounds) {
             int *cur = und2 + (rounds & 1), *prev = und2 + ((rounds + 1) & 1);
+            const bool last = b + 1 == batch;   // its update also writes the root flags
             if (A.nnz > 9LL * n) {
                 k_mis_max<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run,
                                                          act.p);
-                k_mis_update<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur);
+                if (last)
+                    k_mis_update<4, true><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur,
+                                                                      flag.p);
+                else
+                    k_mis_update<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur);
             } else {
                 k_mis_max<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run, act.p);
-                k_mis_update<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur);
+                if (last)
+                    k_mis_update<1, true><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur,
+                                                                flag.p);
+                else
+                    k_mis_update<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur);
             }
         }
-        k_agg_roots<<<nb(n), kB, 0, s>>>(n, key.p, flag.p);
         int rc = scan_only(*this, s, flag.p, cursor.p, n);   // cursor = root ids
         if (rc != XFK_OK) return rc;
         k_mis_pack<<<1, 64, 0, s>>>(cursor.p + n, und2 + ((rounds - 1) & 1), run, mis_out.p);
@@ -2845,6 +3099,10 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         return rc;
     if (l == 0 && A.has16 &&
         (rc = build_col16<256>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)) != XFK_OK)
+        return rc;
+    if (l == 0 && A.has32 &&
+        ((rc = to_f32(ts, (int)nc, A.rrow.p, A.pnnz, A.rval.p, A.r32)) != XFK_OK ||
+         (f32_sweep_on() && (rc = to_f32(ts, n, A.rowptr, A.nnz, A.val, A.a32)) != XFK_OK)))
         return rc;
     if (off) {
         AMG_CHECK(hipEventRecord(sw.b, sw.cs));
@@ -3247,6 +3505,7 @@ int Amg::build(hipStream_t s, int l0)
         // the sweeps, built off the critical path (they are read from the
         // first V-cycle on, after the join at the end of the build)
         A.has16 = l == 0 && !A.dist && !dist && (col16 < 0 ? col16_on() : col16 != 0);
+        A.has32 = A.has16 && (prec32 < 0 ? f32_on() : prec32 != 0);
         if (A.has16) {   // (on the main stream: the aggregation reads them too)
             int rc0 = build_col16<kCgBlock>(s, n, A.rowptr, A.col, A.nnz, A.a16, A.a16b);
             if (rc0 != XFK_OK) return rc0;
@@ -3273,13 +3532,15 @@ int Amg::build(hipStream_t s, int l0)
             fold_pending = false;
         }
         if (g_prof) g_prof->begin(lv + "SpGEMM A P", 0.0);
-        rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, ap_nnz, 4 * l + 1);
+        // A P's row pointers go straight to the level (they are P~'s when it
+        // folds): no copy before the next level reuses the A P buffers
+        rc = spgemm<false>(*this, s, n, XA, YP, A.ftrow, ap_col, ap_val, ap_nnz, 4 * l + 1);
         if (g_prof) g_prof->end();
         if (rc != XFK_OK) return rc;
         if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
         AmgLevel &C = *L[l + 1];
         SgX XR{A.rrow.p, A.rcol.p, A.rval.p, INT_MAX, nullptr, nullptr, nullptr};
-        SgY YAP{ap_row.p, ap_col.p, ap_val.p, nullptr};
+        SgY YAP{A.ftrow.p, ap_col.p, ap_val.p, nullptr};
         if (rt_pending) {   // R = P^T from the side stream
             AMG_CHECK(hipStreamWaitEvent(s, sw.b, 0));
             rt_pending = false;
@@ -3301,7 +3562,6 @@ int Amg::build(hipStream_t s, int l0)
                 AMG_CHECK(A.frcol.alloc((size_t)std::max(1LL, ap_nnz)));
                 AMG_CHECK(A.frval.alloc((size_t)std::max(1LL, ap_nnz)));
             }
-            AMG_CHECK(hipMemcpyAsync(A.ftrow.p, ap_row.p, sizeof(int) * ((size_t)n + 1), hipMemcpyDeviceToDevice, s));
             // P~ and R~ on the side stream: only the V-cycle reads them; the
             // next level's A P (which reuses A P's buffers) waits for P~
             const bool off = side_setup_on();
@@ -3315,11 +3575,12 @@ int Amg::build(hipStream_t s, int l0)
             }
             if (n > 0)
                 k_fold_p<<<(int)(((long long)n * kFoldLanes + 255) / 256), 256, 0, fs>>>(
-                    n, rho.p + 2 * l, A.dinv.p, ap_row.p, ap_col.p, ap_val.p, A.prow.p, A.pcol.p, A.pval.p, A.ftcol.p,
+                    n, rho.p + 2 * l, A.dinv.p, A.ftrow.p, ap_col.p, ap_val.p, A.prow.p, A.pcol.p, A.pval.p, A.ftcol.p,
                     A.ftval.p);
             if (l == 0 && A.has16 &&
                 (rc = build_col16<kCgBlock>(fs, n, A.ftrow.p, A.ftcol.p, ap_nnz, A.f16, A.f16b)) != XFK_OK)
                 return rc;
+            if (l == 0 && A.has32 && (rc = to_f32(fs, n, A.ftrow.p, ap_nnz, A.ftval.p, A.f32v)) != XFK_OK) return rc;
             if (off) {
                 AMG_CHECK(hipEventRecord(sw.c, sw.cs));
                 fold_pending = true;
@@ -3807,9 +4068,16 @@ void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned lon
     }
     if (l == 0) {
         const int g = tl ? nt : (A.n + kCgBlock - 1) / kCgBlock;
-        k_amg_smooth<MODE, kCgBlock><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p,
-                                                            rho, b, x, out, rout, done, part_gam, tl,
-                                                            A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr);
+        if (A.has32 && f32_sweep_on())
+            k_amg_smooth<MODE, kCgBlock><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.a32.p,
+                                                                A.dinv.p, rho, b, x, out, rout, done, part_gam, tl,
+                                                                A.has16 ? A.a16.p : nullptr,
+                                                                A.has16 ? A.a16b.p : nullptr);
+        else
+            k_amg_smooth<MODE, kCgBlock><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p,
+                                                                rho, b, x, out, rout, done, part_gam, tl,
+                                                                A.has16 ? A.a16.p : nullptr,
+                                                                A.has16 ? A.a16b.p : nullptr);
         return;
     }
     if (A.n >= kTileMinRows) {
@@ -3895,7 +4163,8 @@ int smooth_tile(int l, const AmgLevel &A) { return l == 0 ? kCgBlock : (A.n >= k
 // matrix stream, the gathered operand once, b / D^-1, the written vectors
 static double smooth_bytes(const AmgLevel &A, int mode)
 {
-    const double n = A.n, base = (A.has16 ? 10.0 : 12.0) * (double)A.nnz + 4.0 * (n + 1);
+    const double n = A.n, base = ((A.has16 ? 2.0 : 4.0) + (A.has32 && f32_sweep_on() ? 4.0 : 8.0)) * (double)A.nnz +
+                                 4.0 * (n + 1);
     const bool implicit = mode == kSweepFromZero || mode == kResidFromZero;
     const double rd = (implicit ? 2.0 : 3.0) * 8.0 * n;
     const double wr = (mode == kResidFromZero && !A.fold ? 2.0 : 1.0) * 8.0 * n;
@@ -3996,17 +4265,23 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     }
     AmgLevel &C = *M.L[l + 1];
     const long long rnnz = A.pnnz;
-    XFK_PHASE(lv + "restriction R r", (A.has16 ? 10.0 : 12.0) * rnnz + 4.0 * (A.nc + 1) + 8.0 * A.n + 8.0 * A.nc,
-              launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false, lanes_for((double)rnnz / A.nc),
-                        done, A.has16 ? A.r16.p : nullptr, A.has16 ? A.r16b.p : nullptr));
+    XFK_PHASE(lv + "restriction R r", A.nz_bytes() * rnnz + 4.0 * (A.nc + 1) + 8.0 * A.n + 8.0 * A.nc,
+              (A.has32 ? launch_mv32(s, A.nc, A.rrow.p, A.rcol.p, A.r32.p, A.r.p, C.b.p, false,
+                                     lanes_for((double)rnnz / A.nc), done, A.r16.p, A.r16b.p)
+                       : launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false,
+                                   lanes_for((double)rnnz / A.nc), done, A.has16 ? A.r16.p : nullptr,
+                                   A.has16 ? A.r16b.p : nullptr)));
     const double *xc = vcycle_level(M, s, l + 1, C.b.p, nullptr, done);
     if (A.fold && l == 0 && nu == 1) {
         const double n = A.n, f = (double)A.fnnz;
         XFK_PHASE(lv + "folded post: u = x + w D^-1 r + P~ xc" + (part_gam ? " (+ r.u partials)" : ""),
-                  (A.has16 ? 10.0 : 12.0) * f + 4.0 * (n + 1) + 8.0 * A.nc + 32.0 * n,
-                  (k_fold_post0<kCgBlock, 2><<<(A.n + kCgBlock - 1) / kCgBlock, kCgBlock, 0, s>>>(
-                      A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xc, A.dinv.p, rho, A.r.p, b, out0, done, part_gam,
-                      A.has16 ? A.f16.p : nullptr, A.has16 ? A.f16b.p : nullptr)));
+                  A.nz_bytes() * f + 4.0 * (n + 1) + 8.0 * A.nc + 32.0 * n,
+                  (A.has32 ? k_fold_post0<kCgBlock, 2><<<(A.n + kCgBlock - 1) / kCgBlock, kCgBlock, 0, s>>>(
+                                 A.n, A.ftrow.p, A.ftcol.p, A.f32v.p, xc, A.dinv.p, rho, A.r.p, b, out0, done,
+                                 part_gam, A.f16.p, A.f16b.p)
+                           : k_fold_post0<kCgBlock, 2><<<(A.n + kCgBlock - 1) / kCgBlock, kCgBlock, 0, s>>>(
+                                 A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xc, A.dinv.p, rho, A.r.p, b, out0, done,
+                                 part_gam, A.has16 ? A.f16.p : nullptr, A.has16 ? A.f16b.p : nullptr)));
         if (part_gam) M.gamma_done = true;
         return out0;
     }
@@ -4103,6 +4378,10 @@ int Amg::refresh(hipStream_t s)
                                                 A.val, absd.p, sflag.p, cnt.p,
                                                 dfinv.p, wF.p, rho_part.p);
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p);
+    }
+    if (A.has32 && f32_sweep_on()) {   // the sweeps' f32 copy of the new values
+        int rc = to_f32(s, n, A.rowptr, A.nnz, A.val, A.a32);
+        if (rc != XFK_OK) return rc;
     }
     AMG_CHECK(hipGetLastError());
     return XFK_OK;

@@ -755,6 +755,7 @@ static int amg_setup(xfk_problem *P)
     P->amg->dense_max = P->amg_dense;
     P->amg->fold_on = P->amg_fold;
     P->amg->col16 = P->amg_col16;
+    P->amg->prec32 = P->amg_f32;
     P->amg->wlevel = P->amg_wlevel;
     // setup time: an event pair per setup, read after the solve's final
     // synchronisation (no host check here); callers that never read them
@@ -1813,6 +1814,10 @@ int xfk_set_option(xfk_problem *P, int option, double value)
     case XFK_OPT_AMG_COL16:
         XFK_REQUIRE(value == 0 || value == 1, XFK_ERR_ARG, "AMG 16-bit columns is 0 or 1");
         P->amg_col16 = (int)value;
+        return XFK_OK;
+    case XFK_OPT_AMG_F32:
+        XFK_REQUIRE(value == 0 || value == 1, XFK_ERR_ARG, "AMG f32 level-0 operators is 0 or 1");
+        P->amg_f32 = (int)value;
         return XFK_OK;
     case XFK_OPT_AMG_WLEVEL:
         XFK_REQUIRE(value >= -2 && value < kAmgMaxLevels && value == (int)value, XFK_ERR_ARG,

@@ -373,6 +373,7 @@ struct xfk_problem {
     int amg_fold = -1;                // XFK_OPT_AMG_FOLD (-1: the XFK_AMG_FOLD environment default)
     int amg_col16 = -1;               // XFK_OPT_AMG_COL16 (-1: on unless XFK_NO_COL16)
     int amg_wlevel = -2;              // XFK_OPT_AMG_WLEVEL (-2: the default level)
+    int amg_f32 = -1;                 // XFK_OPT_AMG_F32 (-1: on unless XFK_AMG_F32=0)
     int amg_reuse = 1;
     bool amg_reusable = false;        // the hierarchy belongs to this solve's matrix pattern
     bool amg_fresh = false;           // built from scratch for the running PCG solve

@@ -131,9 +131,11 @@ __device__ __forceinline__ TileRows tile_rows(int r0, int N, const int *__restri
 // carries kNoColBase and reads the int array.
 constexpr int kNoColBase = -2147483647 - 1;
 
-template <int B, int SLOTS, class C4, class C1, class XF>
+// V: the stored value type -- double, or float for the AMG's level-0 transfer
+// and smoother operators (products and sums in double either way)
+template <int B, int SLOTS, class V, class C4, class C1, class XF>
 __device__ __forceinline__ double tile_spmv_impl(const TileRows &tr, C4 cols4, C1 col1,
-                                                 const double *__restrict__ val, XF X, double *lds)
+                                                 const V *__restrict__ val, XF X, double *lds)
 {
     constexpr int CAP = 4 * SLOTS * B;
     const int s = __builtin_amdgcn_readfirstlane(tr.s), e = __builtin_amdgcn_readfirstlane(tr.e);
@@ -146,16 +148,24 @@ __device__ __forceinline__ double tile_spmv_impl(const TileRows &tr, C4 cols4, C
             const int k = c0 + 4 * (threadIdx.x + m * B);
             if (k >= s && k + 3 < c1) {
                 const int4 c = cols4(k);
-                const double2 v0 = *reinterpret_cast<const double2 *>(val + k);
-                const double2 v1 = *reinterpret_cast<const double2 *>(val + k + 2);
-                lds[k - c0] = v0.x * X(c.x);
-                lds[k + 1 - c0] = v0.y * X(c.y);
-                lds[k + 2 - c0] = v1.x * X(c.z);
-                lds[k + 3 - c0] = v1.y * X(c.w);
+                if constexpr (sizeof(V) == 8) {
+                    const double2 v0 = *reinterpret_cast<const double2 *>(val + k);
+                    const double2 v1 = *reinterpret_cast<const double2 *>(val + k + 2);
+                    lds[k - c0] = v0.x * X(c.x);
+                    lds[k + 1 - c0] = v0.y * X(c.y);
+                    lds[k + 2 - c0] = v1.x * X(c.z);
+                    lds[k + 3 - c0] = v1.y * X(c.w);
+                } else {
+                    const float4 v = *reinterpret_cast<const float4 *>(val + k);
+                    lds[k - c0] = (double)v.x * X(c.x);
+                    lds[k + 1 - c0] = (double)v.y * X(c.y);
+                    lds[k + 2 - c0] = (double)v.z * X(c.z);
+                    lds[k + 3 - c0] = (double)v.w * X(c.w);
+                }
             } else {
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    if (k + q >= s && k + q < c1) lds[k + q - c0] = val[k + q] * X(col1(k + q));
+                    if (k + q >= s && k + q < c1) lds[k + q - c0] = (double)val[k + q] * X(col1(k + q));
             }
         }
         __syncthreads();
@@ -166,9 +176,9 @@ __device__ __forceinline__ double tile_spmv_impl(const TileRows &tr, C4 cols4, C
     return acc;
 }
 
-template <int B = kCgBlock, int SLOTS = 2, class XF>
+template <int B = kCgBlock, int SLOTS = 2, class V, class XF>
 __device__ __forceinline__ double cg_tile_spmv(const TileRows &tr, const int *__restrict__ col,
-                                               const double *__restrict__ val, XF X, double *lds)
+                                               const V *__restrict__ val, XF X, double *lds)
 {
     return tile_spmv_impl<B, SLOTS>(
         tr, [&](int k) { return *reinterpret_cast<const int4 *>(col + k); }, [&](int k) { return col[k]; }, val, X,
@@ -176,9 +186,9 @@ __device__ __forceinline__ double cg_tile_spmv(const TileRows &tr, const int *__
 }
 
 // the same with 16-bit column offsets when the tile has a base (cb)
-template <int B = kCgBlock, int SLOTS = 2, class XF>
+template <int B = kCgBlock, int SLOTS = 2, class V, class XF>
 __device__ __forceinline__ double cg_tile_spmv16(const TileRows &tr, const unsigned short *__restrict__ c16, int cb,
-                                                 const int *__restrict__ col, const double *__restrict__ val, XF X,
+                                                 const int *__restrict__ col, const V *__restrict__ val, XF X,
                                                  double *lds)
 {
     cb = __builtin_amdgcn_readfirstlane(cb);

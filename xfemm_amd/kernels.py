@@ -35,6 +35,7 @@ XFK_OPT_AMG_DENSE = 7
 XFK_OPT_AMG_FOLD = 8
 XFK_OPT_AMG_COL16 = 9
 XFK_OPT_AMG_WLEVEL = 10
+XFK_OPT_AMG_F32 = 11
 
 # every symbol include/xfemm_kernels.h declares
 EXPORTED = (
@@ -321,13 +322,16 @@ class Static2DProblem:
                  amg_replicate: Optional[int] = None, amg_reuse: Optional[bool] = None, problem_type: int = 0,
                  ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0, amg_dense: Optional[int] = None,
                  ages: Sequence[dict] = (), ac_solver: int = 0, amg_fold: Optional[bool] = None,
-                 amg_col16: Optional[bool] = None, amg_wlevel: Optional[int] = None):
+                 amg_col16: Optional[bool] = None, amg_wlevel: Optional[int] = None,
+                 amg_f32: Optional[bool] = None):
         """ac_solver: [ACSolver], read by the harmonic solvers only (ignored here).
         amg_fold: folded V(1,1) levels (default on; False: the plain cycle).
         amg_col16: 16-bit tile column offsets on level 0 (default on; False:
         int columns; the same bits either way).
         amg_wlevel: the folded coarse level that runs a W-cycle (default: the
         level above the last V-cycle level; -1: a plain V-cycle).
+        amg_f32: f32 values for the V-cycle's level-0 transfers R and P~
+        (default on; False: f64; the sweeps and the PCG SpMV stay f64).
         comm: shard the mesh by row blocks over this communicator (every rank
         passes the same global problem; solve() and solution() are collective).
         precond: "amg" (smoothed-aggregation V-cycle, default) or "jacobi".
@@ -366,6 +370,8 @@ class Static2DProblem:
             self.set_option(XFK_OPT_AMG_FOLD, int(bool(amg_fold)))
         if amg_col16 is not None:
             self.set_option(XFK_OPT_AMG_COL16, int(bool(amg_col16)))
+        if amg_f32 is not None:
+            self.set_option(XFK_OPT_AMG_F32, int(bool(amg_f32)))
         if amg_wlevel is not None:
             self.set_option(XFK_OPT_AMG_WLEVEL, int(amg_wlevel))
         self.n_rows = self.dist_info()["n_own"] if comm is not None else self.n_nodes
