@@ -1023,7 +1023,24 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
                     pv[o] = xv;
                 }
             } else {
-                for (int q = 0; q < len && o + q < CAP; ++q) {
+                // the first U entries of the Y row loaded together (rows of P
+                // hold ~2.5, of A P ~5: one memory latency instead of one per entry)
+                constexpr int U = CAP >= 128 ? 8 : 4;
+                int yc[U];
+                double yv[U];
+#pragma unroll
+                for (int q = 0; q < U; ++q)
+                    if (q < len) {
+                        yc[q] = Y.col[ys + q];
+                        yv[q] = Y.val[ys + q];
+                    }
+#pragma unroll
+                for (int q = 0; q < U; ++q)
+                    if (q < len && o + q < CAP) {
+                        pk[o + q] = yc[q];
+                        pv[o + q] = xv * yv[q];
+                    }
+                for (int q = U; q < len && o + q < CAP; ++q) {
                     pk[o + q] = Y.col[ys + q];
                     pv[o + q] = xv * Y.val[ys + q];
                 }
@@ -2431,7 +2448,9 @@ int scan_total(Amg &A, hipStream_t s, const int *in, int *out, int n, long long 
 }
 
 // the same without reading the total back (no host synchronisation), with
-// the given temporary storage
+// the given temporary storage.  `in` must hold n + 1 readable entries: the
+// long scans are exclusive over n + 1 (out[0] = 0 without a memset; in[n]
+// only fills the unused last slot)
 int scan_only(DBuf<char> &tmp, hipStream_t s, const int *in, int *out, int n)
 {
     if (scan_lds_on(n)) {
@@ -2440,10 +2459,9 @@ int scan_only(DBuf<char> &tmp, hipStream_t s, const int *in, int *out, int n)
         return XFK_OK;
     }
     size_t bytes = 0;
-    AMG_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out + 1, n, s));
+    AMG_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, n + 1, s));
     AMG_CHECK(tmp.alloc(bytes ? bytes : 1));
-    AMG_CHECK(hipMemsetAsync(out, 0, sizeof(int), s));
-    if (n > 0) AMG_CHECK(hipcub::DeviceScan::InclusiveSum(tmp.p, bytes, in, out + 1, n, s));
+    AMG_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, bytes, in, out, n + 1, s));
     return XFK_OK;
 }
 int scan_only(Amg &A, hipStream_t s, const int *in, int *out, int n) { return scan_only(A.cub_tmp, s, in, out, n); }
