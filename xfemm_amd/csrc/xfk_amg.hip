@@ -69,6 +69,10 @@ struct ColView {
     __device__ __forceinline__ int at(int cb, int k) const { return cb != kNoColBase ? cb + (int)c16[k] : col[k]; }
 };
 
+// entries of a row whose loads are issued together in the aggregation sweeps
+// (per row; G lanes take kMisChunk / G each)
+constexpr int kMisChunk = 8;
+
 __device__ __forceinline__ double rho_of(const unsigned long long *p)
 {
     return __longlong_as_double((long long)*p);
@@ -136,12 +140,19 @@ __global__ void k_amg_diag(int n, const int *__restrict__ rowptr, const int *__r
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    double d = 0.0;
-    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
-        if (col[k] == i) {
-            d = val[k];
-            break;
-        }
+    // the row's columns a chunk at a time, loads issued together; the first
+    // match is the diagonal
+    const int s = rowptr[i], e = rowptr[i + 1];
+    int kd = -1;
+    for (int k0 = s; k0 < e && kd < 0; k0 += kMisChunk) {
+        int c[kMisChunk];
+#pragma unroll
+        for (int q = 0; q < kMisChunk; ++q) c[q] = k0 + q < e ? col[k0 + q] : -1;
+#pragma unroll
+        for (int q = kMisChunk - 1; q >= 0; --q)
+            if (c[q] == i) kd = k0 + q;
+    }
+    const double d = kd >= 0 ? val[kd] : 0.0;
     absd[i] = fabs(d);
     dinv[i] = (d != 0.0) ? 1.0 / d : 0.0;
 }
@@ -170,9 +181,29 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
     if (i < n) {
         const double ai = absd[i];
         const int cb = cv.base(i);
-        for (int k = rowptr[i] + g; k < rowptr[i + 1]; k += kStrG) {
-            const int j = cv.at(cb, k);
-            const double a = val[k];
+        const int s = rowptr[i] + g, e = rowptr[i + 1];
+        // a chunk of this lane's entries at a time: columns and values, then
+        // their diagonals, loaded before the first use; the entries are then
+        // taken in the same order as one at a time (same sums, same bits)
+        constexpr int C = kMisChunk / kStrG;
+        for (int k0 = s; k0 < e; k0 += C * kStrG) {
+        int jc[C];
+        double ac[C], dj[C];
+#pragma unroll
+        for (int q = 0; q < C; ++q) {
+            const int k = k0 + q * kStrG;
+            const bool ok = k < e;
+            jc[q] = ok ? cv.at(cb, k) : i;
+            ac[q] = ok ? val[k] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < C; ++q) dj[q] = absd[jc[q] < ncl ? jc[q] : i];
+#pragma unroll
+        for (int q = 0; q < C; ++q) {
+            const int k = k0 + q * kStrG;
+            if (k >= e) break;
+            const int j = jc[q];
+            const double a = ac[q];
             unsigned char f = 0;
             if (j == i) {
                 aii = a;
@@ -187,7 +218,7 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
                 hdeg += (fabs(a) > theta * ai);
             } else {
                 sumA += fabs(a);
-                if (a != 0.0 && fabs(a) > theta * sqrt(ai * absd[j])) {
+                if (a != 0.0 && fabs(a) > theta * sqrt(ai * dj[q])) {
                     f = 1;
                     ++deg;
                     sumS += fabs(a);
@@ -196,6 +227,7 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
                 }
             }
             sflag[k] = f;
+        }
         }
     }
 #pragma unroll
@@ -2254,6 +2286,12 @@ __global__ void __launch_bounds__(256) k_dense_mv(int n, int ld, const float *__
 
 // diagnostics (XFK_AMG_DEBUG): rows left without an aggregate, split by
 // whether they have strong (owned) couplings / any off-diagonal coupling
+__global__ void k_setup_zero(int *__restrict__ a, int na, unsigned long long *__restrict__ b, int nb_)
+{
+    for (int k = threadIdx.x; k < na; k += blockDim.x) a[k] = 0;
+    for (int k = threadIdx.x; k < nb_; k += blockDim.x) b[k] = 0ull;
+}
+
 __global__ void k_debug_unagg(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
                               const int *__restrict__ sdeg, const int *__restrict__ agg, int *out)
 {
@@ -2926,10 +2964,9 @@ int Amg::init(hipStream_t s)
     if (!def_host) AMG_CHECK(hipHostMalloc((void **)&def_host, kAmgDeferSlots * sizeof(int)));
     AMG_CHECK(dev_int.alloc(8));
     AMG_CHECK(def_dev.alloc(kAmgDeferSlots));
-    AMG_CHECK(hipMemsetAsync(def_dev.p, 0, sizeof(int) * kAmgDeferSlots, s));
     def_n = 0;
     AMG_CHECK(rho.alloc(2 * kAmgMaxLevels));
-    AMG_CHECK(hipMemsetAsync(rho.p, 0, sizeof(unsigned long long) * 2 * kAmgMaxLevels, s));
+    k_setup_zero<<<1, 64, 0, s>>>(def_dev.p, kAmgDeferSlots, rho.p, 2 * kAmgMaxLevels);   // (one launch, not two fills)
     if (L.empty()) L.emplace_back(new AmgLevel());
     for (auto &lv : L) {   // levels are rebuilt: none sharded until setup_dist says so
         lv->dist = false;
@@ -3115,6 +3152,10 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     if ((rc = transpose_csr(off ? cnt2 : cnt, off ? cub_tmp2 : cub_tmp, ts, n, (int)nc, A.prow.p, A.pcol.p,
                             A.pval.p, A.rrow.p, A.rcol.p, A.rval.p)) != XFK_OK)
         return rc;
+    if (off) {   // R (A P) waits for R itself; R's V-cycle forms below are joined at the end of the build
+        AMG_CHECK(hipEventRecord(sw.b, sw.cs));
+        rt_pending = true;
+    }
     if (l == 0 && A.has16 &&
         (rc = build_col16<256>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)) != XFK_OK)
         return rc;
@@ -3122,10 +3163,6 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         ((rc = to_f32(ts, (int)nc, A.rrow.p, A.pnnz, A.rval.p, A.r32)) != XFK_OK ||
          (f32_sweep_on() && (rc = to_f32(ts, n, A.rowptr, A.nnz, A.val, A.a32)) != XFK_OK)))
         return rc;
-    if (off) {
-        AMG_CHECK(hipEventRecord(sw.b, sw.cs));
-        rt_pending = true;
-    }
     if (g_prof) g_prof->end();
     return XFK_OK;
 }
@@ -3685,8 +3722,17 @@ int Amg::build(hipStream_t s, int l0)
         }
     }
     if (sw_used) {   // the V-cycle reads R, P~, R~: join the side stream (after the dense inverse's launches)
-        AMG_CHECK(hipEventRecord(sw.b, sw.cs));
-        AMG_CHECK(hipStreamWaitEvent(s, sw.b, 0));
+        // by the time the host gets here (after the deferred read) the side
+        // stream has usually drained: its work is complete and visible, and
+        // the cross-stream wait -- ~15 us of barrier packet on the main
+        // queue between the dense inverse and the PCG -- is skipped
+        const hipError_t q = hipStreamQuery(sw.cs);
+        if (q == hipErrorNotReady) {
+            AMG_CHECK(hipEventRecord(sw.b, sw.cs));
+            AMG_CHECK(hipStreamWaitEvent(s, sw.b, 0));
+        } else {
+            AMG_CHECK(q);
+        }
         sw_used = rt_pending = fold_pending = false;
     }
     AMG_CHECK(hipGetLastError());   // no host check: nothing on the host waits for the device here

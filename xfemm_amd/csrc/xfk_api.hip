@@ -325,11 +325,21 @@ int build_symbolic(xfk_problem *P)
     // node -> incident elements
     XFK_CHECK(P->n2e_ptr.alloc(NL + 1));
     XFK_CHECK(P->n2e.alloc(3 * (size_t)NE));
-    // stable radix sort of the element-major incidence slots by node: each
-    // node's elements come out ascending (the reference's AddTo order) with no
-    // atomics and no per-node sort (was: atomic count + fill + insertion sort)
-    launch_slot_elements(s, NE, T.slot_val);
-    {
+    // counts, scan, fill, per-node register sort (xfk_device.hip k_n2e_*):
+    // each node's elements ascending (the reference's AddTo order);
+    // XFK_N2E_RADIX=1: the stable radix sort of the element-major incidence
+    // slots by node instead (same lists)
+    static const bool n2e_radix = [] {
+        const char *e = std::getenv("XFK_N2E_RADIX");
+        return e && std::atoi(e) != 0;
+    }();
+    if (!n2e_radix) {
+        launch_n2e_count(s, NE, P->p_raw.p, T.deg);
+        XFK_CHECK(exclusive_scan(P, T.deg, P->n2e_ptr.p, NL));
+        launch_n2e_fill(s, NE, P->p_raw.p, P->n2e_ptr.p, T.cursor, P->n2e.p);
+        launch_n2e_sort(s, NL, P->n2e_ptr.p, P->n2e.p);
+    } else {
+        launch_slot_elements(s, NE, T.slot_val);
         int bits = 1;
         while (bits < 31 && (1LL << bits) <= NL) ++bits;
         void *tmp = nullptr;
@@ -817,7 +827,7 @@ static int pcg_start(xfk_problem *P, int flag)
     const int N = P->N;
     *P->pcg_host = CgState{};   // pinned: the upload does not stage through the host
     P->pcg_host->tol = P->precision;
-    XFK_CHECK(hipMemcpyAsync(P->pcg.p, P->pcg_host, sizeof(CgState), hipMemcpyHostToDevice, s));
+    launch_cg_state_init(s, P->pcg.p, P->precision);
     if (P->comm) XFK_CHECK(hipMemsetAsync(P->part_loc.p, 0, sizeof(double) * 4 * P->Gpart, s));
     launch_diag_inv(s, N, P->diag.p, P->val.p, P->dinv.p, P->pcg.p);
     int rc = XFK_OK;
@@ -1598,7 +1608,9 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
         if (Iter > 0 && (rc = exchange(P, P->V.p)) != XFK_OK) return rc;   // halo of V for the element B
         rc = assemble(P, Iter);
         if (rc != XFK_OK) return rc;
-        XFK_CHECK(hipMemcpyAsync(P->Vold.p, P->V.p, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
+        // (the Newton residual and the relaxation read Vold; a linear problem
+        // has neither)
+        if (!LinearFlag) XFK_CHECK(hipMemcpyAsync(P->Vold.p, P->V.p, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
         XFK_CHECK(hipEventRecord(e1, s));
         rc = pcg_solve(P, Iter, cap);
         if (rc != XFK_OK) return rc;

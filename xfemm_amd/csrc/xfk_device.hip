@@ -103,6 +103,69 @@ __global__ void k_fill_n2e(int NE, const int *__restrict__ p, const int *__restr
     }
 }
 
+// Node -> element lists by counting: per-node counts (atomic increments, order-
+// free), an exclusive scan, a fill at atomically taken positions (arbitrary
+// order within a node's list), then every node's short list sorted in
+// registers -- each node's elements come out ascending, the order the radix
+// sort below produced (the reference's AddTo order), in ~1/3 of its time
+// (three 8-bit passes over 3 NE pairs)
+__global__ void k_n2e_count(long long n3, const int *__restrict__ p, int *__restrict__ deg)
+{
+    const long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (k < n3) atomicAdd(&deg[p[k]], 1);
+}
+
+__global__ void k_n2e_fill(long long n3, const int *__restrict__ p, const int *__restrict__ ptr,
+                           int *__restrict__ cursor, int *__restrict__ n2e)
+{
+    const long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (k >= n3) return;
+    const int v = p[k];
+    n2e[ptr[v] + atomicAdd(&cursor[v], 1)] = (int)(k / 3);
+}
+
+// lists of <= 16 elements: a register bitonic network (padding INT_MAX);
+// longer ones (rare high-valence nodes): insertion sort in place
+__global__ void k_n2e_sort(int NL, const int *__restrict__ ptr, int *__restrict__ n2e)
+{
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= NL) return;
+    const int s = ptr[v], e = ptr[v + 1], len = e - s;
+    if (len <= 1) return;
+    if (len <= 16) {
+        int a[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) a[q] = q < len ? n2e[s + q] : INT_MAX;
+#pragma unroll
+        for (int k = 2; k <= 16; k <<= 1)
+#pragma unroll
+            for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int o = q ^ j;
+                    if (o > q) {
+                        const bool up = (q & k) == 0;
+                        const int x = a[q], y = a[o];
+                        a[q] = up ? min(x, y) : max(x, y);
+                        a[o] = up ? max(x, y) : min(x, y);
+                    }
+                }
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (q < len) n2e[s + q] = a[q];
+        return;
+    }
+    for (int i = s + 1; i < e; ++i) {
+        const int key = n2e[i];
+        int j = i - 1;
+        while (j >= s && n2e[j] > key) {
+            n2e[j + 1] = n2e[j];
+            --j;
+        }
+        n2e[j + 1] = key;
+    }
+}
+
 // Node -> element lists by a stable radix sort of the (node, element)
 // incidence pairs (xfk_api.hip: build_symbolic): values k / 3 of the
 // element-major incidence slots, then each node's first slot by a lower
@@ -201,6 +264,153 @@ __global__ void __launch_bounds__(kBlock) k_row_build(int N, RowCands rc, int *_
     if (c != out)
         for (int i = 0; i < u; ++i) out[i] = c[i];
     rowcnt[v] = u;
+}
+
+// Rows of up to kRowRegElems incident elements and no periodic fill-in (all
+// but a few rows of a triangle mesh): the candidates -- v and the two other
+// vertices of each incident element -- are sorted by a register bitonic
+// network of 16 or 32 and de-duplicated there, twice: once for the row
+// length, once (after the scan) writing the row in place.  No temporary rows,
+// no copy pass.  Other rows take k_row_build / k_row_copy's path through tmp.
+constexpr int kRowRegElems = 15;
+
+template <int W>
+__device__ __forceinline__ void bitonic_regs(int (&a)[W])
+{
+#pragma unroll
+    for (int k = 2; k <= W; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                const int o = q ^ j;
+                if (o > q) {
+                    const bool up = (q & k) == 0;
+                    const int x = a[q], y = a[o];
+                    a[q] = up ? min(x, y) : max(x, y);
+                    a[o] = up ? max(x, y) : min(x, y);
+                }
+            }
+}
+
+// candidates of row v (ne incident elements) into a[0 .. W): v, then two per
+// element; unused slots INT_MAX
+template <int W>
+__device__ __forceinline__ void row_regs(int v, int s, int ne, const RowCands &rc, int (&a)[W])
+{
+    a[0] = v;
+    int f[(W - 1) / 2];
+#pragma unroll
+    for (int q = 0; q < (W - 1) / 2; ++q) f[q] = q < ne ? rc.n2e[s + q] : -1;
+#pragma unroll
+    for (int q = 0; q < (W - 1) / 2; ++q) {
+        int x = INT_MAX, y = INT_MAX, z = INT_MAX;
+        if (f[q] >= 0) {
+            x = rc.p[3 * f[q]];
+            y = rc.p[3 * f[q] + 1];
+            z = rc.p[3 * f[q] + 2];
+        }
+        a[1 + 2 * q] = x == v ? y : x;
+        a[2 + 2 * q] = (x == v || y == v) ? z : y;
+    }
+#pragma unroll
+    for (int q = 2 * ((W - 1) / 2) + 1; q < W; ++q) a[q] = INT_MAX;
+    bitonic_regs(a);
+}
+
+__device__ __forceinline__ bool row_reg_ok(const RowCands &rc, int v, int ne)
+{
+    return ne <= kRowRegElems && !(rc.fill_ptr && rc.fill_ptr[v + 1] > rc.fill_ptr[v]);
+}
+
+template <int W>
+__device__ __forceinline__ int row_regs_len(int v, int s, int ne, const RowCands &rc)
+{
+    int a[W];
+    row_regs<W>(v, s, ne, rc, a);
+    int u = 0;
+#pragma unroll
+    for (int q = 0; q < W; ++q) u += (a[q] != INT_MAX && (q == 0 || a[q] != a[q - 1])) ? 1 : 0;
+    return u;
+}
+
+template <int W>
+__device__ __forceinline__ void row_regs_write(int v, int s, int ne, const RowCands &rc, int r0,
+                                               int *__restrict__ col, int *__restrict__ diag)
+{
+    int a[W];
+    row_regs<W>(v, s, ne, rc, a);
+    int u = 0;
+#pragma unroll
+    for (int q = 0; q < W; ++q)
+        if (a[q] != INT_MAX && (q == 0 || a[q] != a[q - 1])) {
+            col[r0 + u] = a[q];
+            if (a[q] == v) diag[v] = r0 + u;
+            ++u;
+        }
+}
+
+__global__ void __launch_bounds__(kBlock) k_row_len_reg(int N, RowCands rc, int *__restrict__ tmp,
+                                                        int *__restrict__ rowcnt)
+{
+    __shared__ int s_c[kBlock * (kRowLds + 1)];
+    const int v = blockIdx.x * kBlock + threadIdx.x;
+    if (v >= N) return;
+    const int s = rc.n2e_ptr[v], ne = rc.n2e_ptr[v + 1] - s;
+    if (row_reg_ok(rc, v, ne)) {
+        rowcnt[v] = ne <= 7 ? row_regs_len<16>(v, s, ne, rc) : row_regs_len<32>(v, s, ne, rc);
+        return;
+    }
+    // long or periodic rows: candidates through LDS / tmp (k_row_build)
+    const int m = rc.count(v);
+    int *out = tmp + rc.base(v);
+    int *c = (m <= kRowLds) ? &s_c[threadIdx.x * (kRowLds + 1)] : out;
+    int k = 0;
+    for (int t = s; t < s + ne; ++t) {
+        const int f = rc.n2e[t];
+        c[k++] = rc.p[3 * f];
+        c[k++] = rc.p[3 * f + 1];
+        c[k++] = rc.p[3 * f + 2];
+    }
+    if (rc.fill_ptr)
+        for (int t = rc.fill_ptr[v]; t < rc.fill_ptr[v + 1]; ++t) c[k++] = rc.fill_col[t];
+    c[k++] = v;
+    for (int i = 1; i < m; ++i) {
+        const int key = c[i];
+        int j = i - 1;
+        while (j >= 0 && c[j] > key) {
+            c[j + 1] = c[j];
+            --j;
+        }
+        c[j + 1] = key;
+    }
+    int u = 0;
+    for (int i = 0; i < m; ++i)
+        if (u == 0 || c[i] != c[u - 1]) c[u++] = c[i];
+    if (c != out)
+        for (int i = 0; i < u; ++i) out[i] = c[i];
+    rowcnt[v] = u;
+}
+
+__global__ void k_row_fill_reg(int N, RowCands rc, const int *__restrict__ tmp, const int *__restrict__ rowptr,
+                               int *__restrict__ col, int *__restrict__ diag)
+{
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= N) return;
+    const int s = rc.n2e_ptr[v], ne = rc.n2e_ptr[v + 1] - s;
+    const int r0 = rowptr[v];
+    if (row_reg_ok(rc, v, ne)) {
+        if (ne <= 7) row_regs_write<16>(v, s, ne, rc, r0, col, diag);
+        else row_regs_write<32>(v, s, ne, rc, r0, col, diag);
+        return;
+    }
+    const int *src = tmp + rc.base(v);
+    const int len = rowptr[v + 1] - r0;
+    for (int i = 0; i < len; ++i) {
+        const int c = src[i];
+        col[r0 + i] = c;
+        if (c == v) diag[v] = r0 + i;
+    }
 }
 
 __global__ void k_row_copy(int N, RowCands rc, const int *__restrict__ tmp, const int *__restrict__ rowptr,
@@ -950,6 +1160,20 @@ void launch_fill_n2e(hipStream_t s, int NE, const int *p, const int *ptr, int *c
 {
     if (NE) k_fill_n2e<<<nblk(NE), kBlock, 0, s>>>(NE, p, ptr, cursor, n2e);
 }
+void launch_n2e_count(hipStream_t s, int NE, const int *p, int *deg)
+{
+    const long long n3 = 3LL * NE;
+    if (NE) k_n2e_count<<<(unsigned)((n3 + kBlock - 1) / kBlock), kBlock, 0, s>>>(n3, p, deg);
+}
+void launch_n2e_fill(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e)
+{
+    const long long n3 = 3LL * NE;
+    if (NE) k_n2e_fill<<<(unsigned)((n3 + kBlock - 1) / kBlock), kBlock, 0, s>>>(n3, p, ptr, cursor, n2e);
+}
+void launch_n2e_sort(hipStream_t s, int NL, const int *ptr, int *n2e)
+{
+    if (NL) k_n2e_sort<<<nblk(NL), kBlock, 0, s>>>(NL, ptr, n2e);
+}
 void launch_slot_elements(hipStream_t s, int NE, int *v)
 {
     const long long n3 = 3LL * NE;
@@ -963,18 +1187,29 @@ void launch_sort_segments(hipStream_t s, int N, const int *ptr, int *a)
 {
     if (N) k_sort_segments<<<nblk(N), kBlock, 0, s>>>(N, ptr, a);
 }
+// XFK_ROW_REG=0: every CSR row through k_row_build / k_row_copy (measurement)
+static bool row_reg_on()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_ROW_REG");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
 long long row_tmp_size(int N, int NE, int nfill) { return 9LL * NE + nfill + N; }
 void launch_row_build(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e, const int *fill_ptr,
                       const int *fill_col, int *tmp, int *rowcnt)
 {
     RowCands rc{p, n2e_ptr, n2e, fill_ptr, fill_col};
-    if (N) k_row_build<<<nblk(N), kBlock, 0, s>>>(N, rc, tmp, rowcnt);
+    if (N && row_reg_on()) k_row_len_reg<<<nblk(N), kBlock, 0, s>>>(N, rc, tmp, rowcnt);
+    else if (N) k_row_build<<<nblk(N), kBlock, 0, s>>>(N, rc, tmp, rowcnt);
 }
 void launch_row_copy(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e, const int *fill_ptr,
                      const int *fill_col, const int *tmp, const int *rowptr, int *col, int *diag)
 {
     RowCands rc{p, n2e_ptr, n2e, fill_ptr, fill_col};
-    if (N) k_row_copy<<<nblk(N), kBlock, 0, s>>>(N, rc, tmp, rowptr, col, diag);
+    if (N && row_reg_on()) k_row_fill_reg<<<nblk(N), kBlock, 0, s>>>(N, rc, tmp, rowptr, col, diag);
+    else if (N) k_row_copy<<<nblk(N), kBlock, 0, s>>>(N, rc, tmp, rowptr, col, diag);
 }
 void launch_jp_round(hipStream_t s, int N, int NE, int round, unsigned char *active, int *pending_round,
                      const int *p, const int *n2e_ptr, const int *n2e, int *color, unsigned long long *maxkey,

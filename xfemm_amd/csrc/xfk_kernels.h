@@ -58,11 +58,15 @@ void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, con
                     double *part_gam = nullptr, const int *tiles = nullptr, int ntiles = 0,
                     const unsigned short *c16 = nullptr, const int *cbase = nullptr);
 void launch_cg_dot(hipStream_t s, int N, const double *a, const double *b, double *part);
+void launch_cg_state_init(hipStream_t s, CgState *S, double tol);
 
 void launch_count_incidence(hipStream_t s, int NE, const int *p, int *deg);
 void launch_fill_n2e(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e);
 void launch_sort_segments(hipStream_t s, int N, const int *ptr, int *a);
 void launch_slot_elements(hipStream_t s, int NE, int *v);
+void launch_n2e_count(hipStream_t s, int NE, const int *p, int *deg);
+void launch_n2e_fill(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e);
+void launch_n2e_sort(hipStream_t s, int NL, const int *ptr, int *n2e);
 void launch_n2e_ptr(hipStream_t s, int NL, const int *keys, int n3, int *ptr);
 long long row_tmp_size(int N, int NE, int nfill);   // ints of the row-build scratch
 void launch_row_build(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e, const int *fill_ptr,

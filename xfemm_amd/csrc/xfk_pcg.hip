@@ -251,6 +251,18 @@ __global__ void __launch_bounds__(kAxBlock) k_cg_axpy(CgAxpyArgs A)
     if (threadIdx.x == 0) A.gam_out[blockIdx.x] = g;
 }
 
+// the PCG state of a new solve (one launch instead of a host -> device copy)
+__global__ void k_cg_state_init(CgState *S, double tol)
+{
+    if (threadIdx.x == 0) {
+        CgState z{};
+        z.tol = tol;
+        *S = z;
+    }
+}
+
+void launch_cg_state_init(hipStream_t s, CgState *S, double tol) { k_cg_state_init<<<1, 64, 0, s>>>(S, tol); }
+
 int cg_grid(int N) { return (N + kCgBlock - 1) / kCgBlock; }
 int cg_axpy_grid(int N)
 {
