@@ -307,6 +307,17 @@ struct SymTmp {
     }
 };
 
+// the CSR lengths of a deferred symbolic phase (build_symbolic), read once
+int xfk_resolve_nnz(xfk_problem *P)
+{
+    if (!P->nnz_pending) return XFK_OK;
+    XFK_CHECK(hipEventSynchronize(P->nnz_ev));
+    P->nnz = P->hpin[0];
+    P->nnz_own = P->hpin[1];
+    P->nnz_pending = false;
+    return XFK_OK;
+}
+
 int build_symbolic(xfk_problem *P)
 {
     hipStream_t s = P->stream;
@@ -381,12 +392,27 @@ int build_symbolic(xfk_problem *P)
     XFK_CHECK(exclusive_scan(P, T.rowcnt, P->rowptr.p, N));
     XFK_CHECK(hipMemcpyAsync(P->hpin, P->rowptr.p + N, sizeof(int), hipMemcpyDeviceToHost, s));
     XFK_CHECK(hipMemcpyAsync(P->hpin + 1, P->rowptr.p + P->N, sizeof(int), hipMemcpyDeviceToHost, s));
-    XFK_CHECK(hipStreamSynchronize(s));
-    const int nnz = P->hpin[0], nnz_own = P->hpin[1];
-    P->nnz = nnz;
-    P->nnz_own = nnz_own;
-    XFK_CHECK(P->col.alloc(nnz));
-    XFK_CHECK(P->val.alloc(nnz));
+    // single-device static problems without air gaps or periodic maps read
+    // the lengths back later (xfk_resolve_nnz, at the preconditioner setup):
+    // the pattern is filled and the matrix assembled into arrays sized for
+    // the bound 6 NE + N + fill-in (a triangle adds at most six off-diagonal
+    // entries), with no host check in between
+    const bool defer = !P->harmonic && !P->comm && P->age_key.empty() && P->pbc_entry_key.empty();
+    long long cap_nnz;
+    if (defer) {
+        if (!P->nnz_ev) XFK_CHECK(hipEventCreateWithFlags(&P->nnz_ev, hipEventDisableTiming));
+        XFK_CHECK(hipEventRecord(P->nnz_ev, s));
+        P->nnz_pending = true;
+        cap_nnz = 6LL * NE + N + nfill;
+    } else {
+        XFK_CHECK(hipStreamSynchronize(s));
+        P->nnz = P->hpin[0];
+        P->nnz_own = P->hpin[1];
+        P->nnz_pending = false;
+        cap_nnz = P->nnz;
+    }
+    XFK_CHECK(P->col.alloc(cap_nnz));
+    XFK_CHECK(P->val.alloc(cap_nnz));
     XFK_CHECK(P->diag.alloc(N));
     launch_row_copy(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, T.rowtmp, P->rowptr.p, P->col.p, P->diag.p);
 
@@ -929,7 +955,9 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
 static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
 {
     hipStream_t s = P->stream;
-    int rc = alloc_cg(P);
+    int rc = xfk_resolve_nnz(P);   // (the assembly is enqueued: no bubble)
+    if (rc != XFK_OK) return rc;
+    rc = alloc_cg(P);
     if (rc != XFK_OK) return rc;
     rc = pcg_start(P, flag);
     if (rc != XFK_OK) return rc;
@@ -997,6 +1025,7 @@ void xfk_problem_destroy(xfk_problem *P)
         if (ev) (void)hipEventDestroy(ev);
     if (P->pcg_host) (void)hipHostFree(P->pcg_host);
     if (P->hpin) (void)hipHostFree(P->hpin);
+    if (P->nnz_ev) (void)hipEventDestroy(P->nnz_ev);
     if (P->nws_host) (void)hipHostFree(P->nws_host);
     if (P->hc_host) (void)hipHostFree(P->hc_host);
     hipStream_t s = P->stream;
@@ -1740,11 +1769,11 @@ int xfk_get_circuits(xfk_problem *P, int *ccase, double *J, double *dV)
     return XFK_OK;
 }
 
-long long xfk_get_nnz(xfk_problem *P) { return P ? P->nnz_own : -1; }
+long long xfk_get_nnz(xfk_problem *P) { return P && xfk_resolve_nnz(P) == XFK_OK ? P->nnz_own : -1; }
 
 double xfk_spmv_col_bytes(xfk_problem *P)
 {
-    if (!P) return -1.0;
+    if (!P || xfk_resolve_nnz(P) != XFK_OK) return -1.0;
     const unsigned short *c16;
     const int *cbase;
     spmv_col16(P, c16, cbase);
@@ -1765,6 +1794,7 @@ int xfk_get_csr(xfk_problem *P, int *rowptr, int *col, double *val, double *b)
     XFK_REQUIRE(P && P->symbolic_ready, XFK_ERR_ARG, "no assembled system");
     XFK_CHECK(hipSetDevice(P->device));
     XFK_CHECK(hipStreamSynchronize(P->stream));
+    if (xfk_resolve_nnz(P) != XFK_OK) return XFK_ERR_HIP;
     if (rowptr) XFK_CHECK(d2h(rowptr, P->rowptr.p, sizeof(int) * (P->N + 1), P->stream));
     if (col) XFK_CHECK(d2h(col, P->col.p, sizeof(int) * P->nnz_own, P->stream));
     if (val) XFK_CHECK(d2h(val, P->val.p, sizeof(double) * P->nnz_own, P->stream));

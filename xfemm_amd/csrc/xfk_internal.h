@@ -257,6 +257,8 @@ struct xfk_problem {
     int Gpart = 0;                   // length of each per-block partial array (agreed by all ranks)
     xfk::TileSplit ts;               // sharded PCG SpMV: interior / boundary tiles (exchange overlap)
     int *hpin = nullptr;             // pinned scratch for small device -> host reads
+    hipEvent_t nnz_ev = nullptr;     // the pattern's lengths landed in hpin[0..1] (deferred read)
+    bool nnz_pending = false;        // nnz / nnz_own not read back yet (xfk_resolve_nnz)
     int pcg_hint0 = 0;               // PCG iterations of the last solve's first pass (first batch)
     std::vector<hipEvent_t> setup_ev;   // AMG setup event pairs, read after the solve
     int setup_used = 0;
