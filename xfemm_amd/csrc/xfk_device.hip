@@ -124,6 +124,82 @@ __global__ void k_n2e_fill(long long n3, const int *__restrict__ p, const int *_
     n2e[ptr[v] + atomicAdd(&cursor[v], 1)] = (int)(k / 3);
 }
 
+// The same counts and fill through LDS: a workgroup of 256 elements touches
+// the nodes of a narrow window (element and node numberings are both banded),
+// counts its incidences there and touches the global counters once per
+// (workgroup, node) instead of once per incidence; the fill reserves one
+// chunk of each node's list per workgroup and places its elements there
+// through LDS cursors (the per-node sort below fixes the order).  A window
+// wider than kN2eWin falls back to one global atomic per incidence.
+constexpr int kN2eWin = 4096;
+template <bool FILL>
+__global__ void __launch_bounds__(256) k_n2e_tile(int NE, const int *__restrict__ p, const int *__restrict__ ptr,
+                                                  int *__restrict__ cnt, int *__restrict__ n2e)
+{
+    __shared__ int h[kN2eWin];
+    __shared__ int cur[FILL ? kN2eWin : 1];
+    __shared__ int red[8];
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    int v[3] = {0, 0, 0};
+    int lo = INT_MAX, hi = INT_MIN;
+    if (e < NE) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            v[j] = p[3 * e + j];
+            lo = min(lo, v[j]);
+            hi = max(hi, v[j]);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off, 64));
+        hi = max(hi, __shfl_xor(hi, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = lo;
+        red[4 + (threadIdx.x >> 6)] = hi;
+    }
+    __syncthreads();
+    lo = min(min(red[0], red[1]), min(red[2], red[3]));
+    hi = max(max(red[4], red[5]), max(red[6], red[7]));
+    if (hi < lo) return;   // no element in this tile
+    if ((long long)hi - lo >= kN2eWin) {   // wide window: one global atomic per incidence
+        if (e < NE)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                if (!FILL) atomicAdd(&cnt[v[j]], 1);
+                else n2e[ptr[v[j]] + atomicAdd(&cnt[v[j]], 1)] = e;
+            }
+        return;
+    }
+    const int w = hi - lo + 1;
+    for (int c = threadIdx.x; c < w; c += 256) {
+        h[c] = 0;
+        if (FILL) cur[c] = 0;
+    }
+    __syncthreads();
+    if (e < NE)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) atomicAdd(&h[v[j] - lo], 1);
+    __syncthreads();
+    if (!FILL) {
+        for (int c = threadIdx.x; c < w; c += 256)
+            if (h[c]) atomicAdd(&cnt[lo + c], h[c]);
+        return;
+    }
+    for (int c = threadIdx.x; c < w; c += 256) {
+        const int m = h[c];
+        if (m) h[c] = ptr[lo + c] + atomicAdd(&cnt[lo + c], m);   // this tile's chunk of node lo + c
+    }
+    __syncthreads();
+    if (e < NE)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int c = v[j] - lo;
+            n2e[h[c] + atomicAdd(&cur[c], 1)] = e;
+        }
+}
+
 // lists of <= 16 elements: a register bitonic network (padding INT_MAX);
 // longer ones (rare high-valence nodes): insertion sort in place
 __global__ void k_n2e_sort(int NL, const int *__restrict__ ptr, int *__restrict__ n2e)
@@ -1160,15 +1236,26 @@ void launch_fill_n2e(hipStream_t s, int NE, const int *p, const int *ptr, int *c
 {
     if (NE) k_fill_n2e<<<nblk(NE), kBlock, 0, s>>>(NE, p, ptr, cursor, n2e);
 }
+// XFK_N2E_TILE=0: one global atomic per incidence (measurement)
+static bool n2e_tile_on()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_N2E_TILE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
 void launch_n2e_count(hipStream_t s, int NE, const int *p, int *deg)
 {
     const long long n3 = 3LL * NE;
-    if (NE) k_n2e_count<<<(unsigned)((n3 + kBlock - 1) / kBlock), kBlock, 0, s>>>(n3, p, deg);
+    if (NE && n2e_tile_on()) k_n2e_tile<false><<<(NE + 255) / 256, 256, 0, s>>>(NE, p, nullptr, deg, nullptr);
+    else if (NE) k_n2e_count<<<(unsigned)((n3 + kBlock - 1) / kBlock), kBlock, 0, s>>>(n3, p, deg);
 }
 void launch_n2e_fill(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e)
 {
     const long long n3 = 3LL * NE;
-    if (NE) k_n2e_fill<<<(unsigned)((n3 + kBlock - 1) / kBlock), kBlock, 0, s>>>(n3, p, ptr, cursor, n2e);
+    if (NE && n2e_tile_on()) k_n2e_tile<true><<<(NE + 255) / 256, 256, 0, s>>>(NE, p, ptr, cursor, n2e);
+    else if (NE) k_n2e_fill<<<(unsigned)((n3 + kBlock - 1) / kBlock), kBlock, 0, s>>>(n3, p, ptr, cursor, n2e);
 }
 void launch_n2e_sort(hipStream_t s, int NL, const int *ptr, int *n2e)
 {
