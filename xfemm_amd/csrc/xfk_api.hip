@@ -899,15 +899,23 @@ static int pcg_start(xfk_problem *P, int flag)
 
 // one PCG iteration: the streaming update then the SpMV (optionally bracketed
 // by HIP events for the live roofline)
-static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
+// the update of iteration it (k_cg_axpy: reductions, convergence test, the
+// streaming update); algorithmic bytes: 10 vectors (AMG: w z p x r u read,
+// z p x r written)
+static void pcg_update(xfk_problem *P, long long it)
+{
+    hipStream_t s = P->stream;
+    const CgAxpyArgs A = cg_args(P, it);
+    XFK_PHASE("PCG update (Chronopoulos-Gear axpy)", 80.0 * (double)P->N, launch_cg_axpy(s, A));
+}
+
+// the rest of iteration it: u = M^-1 r (V-cycle) and w = A u with its partials
+static int pcg_precond_spmv(xfk_problem *P, long long it, bool stamp)
 {
     hipStream_t s = P->stream;
     const CgAxpyArgs A = cg_args(P, it);
     const size_t G = (size_t)P->Gpart;
     const double N = P->N;
-    // algorithmic bytes: the update streams 10 vectors (AMG: w z p x r u read,
-    // z p x r written); the SpMV the matrix, u, r and w
-    XFK_PHASE("PCG update (Chronopoulos-Gear axpy)", 80.0 * N, launch_cg_axpy(s, A));
     int rc;
     double *pgam = P->part_loc.p + (size_t)((it + 1) & 1) * G;
     if (A.amg && (rc = P->amg->vcycle(s, A.R, A.U, &P->pcg.p->done, pgam)) != XFK_OK) return rc;
@@ -952,6 +960,12 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
     return allreduce_partials(P, 3);
 }
 
+static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
+{
+    pcg_update(P, it);
+    return pcg_precond_spmv(P, it, stamp);
+}
+
 static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
 {
     hipStream_t s = P->stream;
@@ -970,12 +984,21 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
     // (clamped like every later batch, and never past the iteration cap, so a
     // zero-diagonal matrix is still caught at the first poll)
     if (flag == 0 && P->pcg_hint0 > 0) batch = std::min(P->pcg_hint0, 512);
+    // Every batch ends with an update, whose convergence test the poll reads:
+    // the V-cycle and SpMV of that iteration open the next batch, so the
+    // converged solve launches no iteration tail that would only exit
+    // (one V-cycle + SpMV, ~14 launches, saved per solve)
+    bool tail = false;   // iteration it - 1's V-cycle + SpMV not launched yet
     for (;;) {
         batch = (int)std::max<long long>(1, std::min<long long>(batch, max_iters - it));
         for (int k = 0; k < batch; ++k, ++it) {
-            const bool stamp = P->time_spmv && (it % 16 == 0) && P->spmv_used + 2 <= (int)P->spmv_ev.size();
-            rc = pcg_iteration(P, it, stamp);
-            if (rc != XFK_OK) return rc;
+            if (tail) {
+                const long long ip = it - 1;
+                const bool stamp = P->time_spmv && (ip % 16 == 0) && P->spmv_used + 2 <= (int)P->spmv_ev.size();
+                if ((rc = pcg_precond_spmv(P, ip, stamp)) != XFK_OK) return rc;
+            }
+            pcg_update(P, it);
+            tail = true;
         }
         XFK_CHECK(hipGetLastError());
         XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(CgState), hipMemcpyDeviceToHost, s));
