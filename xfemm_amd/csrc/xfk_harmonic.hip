@@ -1738,15 +1738,19 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
             long long it = 0;
             int batch = amg ? 8 : 32;
             const long long cap = std::max<long long>(100000, 20LL * N);
+            // batches end with an update (its convergence test is what the
+            // poll reads); that iteration's preconditioner + SpMV open the
+            // next batch, so a converged solve launches no exiting tail
+            bool tail = false;
             for (;;) {
                 for (int k = 0; k < batch; ++k, ++it) {
-                    if (amg) {
-                        k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, Gcg, it == 0 ? Gcg : Gax);
-                        if ((prc = precondition()) != XFK_OK) return prc;
-                    } else {
-                        k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, it == 0 ? Gcg : Gax, it == 0 ? Gcg : Gax);
+                    if (tail) {
+                        if (amg && (prc = precondition()) != XFK_OK) return prc;
+                        k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, (int)(it & 1));   // iteration it - 1's
                     }
-                    k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, (int)((it + 1) & 1));
+                    if (amg) k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, Gcg, it == 0 ? Gcg : Gax);
+                    else k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, it == 0 ? Gcg : Gax, it == 0 ? Gcg : Gax);
+                    tail = true;
                 }
                 XFK_CHECK(hipGetLastError());
                 XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
