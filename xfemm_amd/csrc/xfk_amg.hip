@@ -294,11 +294,14 @@ template <int G>
 __global__ void k_mis_max(int n, const int *__restrict__ rowptr, ColView cv,
                           const unsigned char *__restrict__ sflag, const MisKey *__restrict__ in,
                           MisKey *__restrict__ out, const int *prev, int *cur, int *run,
-                          unsigned char *__restrict__ act)
+                          unsigned char *__restrict__ act, int xcd)
 {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    // xcd: consecutive blocks on one XCD (xcd_tile): a block's neighbour rows
+    // a mesh row away stay in that XCD's L2
+    const int bx = xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int t = bx * blockDim.x + threadIdx.x;
     const int i = t / G, g = t % G;
-    if (t == 0) {   // k_mis_update of this round runs after this launch
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // k_mis_update of this round runs after this launch
         if (*prev != 0) *run += 1;   // rounds that did work (the next setup's batch size)
         *cur = 0;
     }
@@ -331,9 +334,11 @@ __global__ void k_mis_max(int n, const int *__restrict__ rowptr, ColView cv,
 template <int G, bool ROOTS = false>
 __global__ void k_mis_update(int n, const int *__restrict__ rowptr, ColView cv,
                              const unsigned char *__restrict__ sflag, const MisKey *__restrict__ t1,
-                             MisKey *__restrict__ key, const int *prev, int *undecided, int *__restrict__ flag = nullptr)
+                             MisKey *__restrict__ key, const int *prev, int *undecided, int *__restrict__ flag,
+                             int xcd)
 {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int bx = xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int t = bx * blockDim.x + threadIdx.x;
     const int i = t / G, g = t % G;
     if (i >= n) return;
     const MisKey k = key[i];
@@ -2899,6 +2904,16 @@ static int to_f32(hipStream_t s, int n, const int *rowptr, long long cap, const 
     return XFK_OK;
 }
 
+// XFK_MIS_XCD=0: MIS-2 sweeps with round-robin blocks (measurement)
+static bool mis_xcd_on()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_MIS_XCD");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+
 // XFK_NO_SPEC=1: no setup work enqueued ahead of a host check
 static bool spec_on()
 {
@@ -3089,21 +3104,24 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         for (int b = 0; b < batch; ++b, ++rounds) {
             int *cur = und2 + (rounds & 1), *prev = und2 + ((rounds + 1) & 1);
             const bool last = b + 1 == batch;   // its update also writes the root flags
+            const int xc = mis_xcd_on() ? 1 : 0;
             if (A.nnz > 9LL * n) {
                 k_mis_max<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run,
-                                                         act.p);
+                                                         act.p, xc);
                 if (last)
                     k_mis_update<4, true><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur,
-                                                                      flag.p);
+                                                                      flag.p, xc);
                 else
-                    k_mis_update<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur);
+                    k_mis_update<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur,
+                                                                nullptr, xc);
             } else {
-                k_mis_max<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run, act.p);
+                k_mis_max<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run, act.p, xc);
                 if (last)
                     k_mis_update<1, true><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur,
-                                                                flag.p);
+                                                                flag.p, xc);
                 else
-                    k_mis_update<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur);
+                    k_mis_update<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev, cur, nullptr,
+                                                          xc);
             }
         }
         int rc = scan_only(*this, s, flag.p, cursor.p, n);   // cursor = root ids

@@ -348,7 +348,7 @@ int build_symbolic(xfk_problem *P)
         launch_n2e_count(s, NE, P->p_raw.p, T.deg);
         XFK_CHECK(exclusive_scan(P, T.deg, P->n2e_ptr.p, NL));
         launch_n2e_fill(s, NE, P->p_raw.p, P->n2e_ptr.p, T.cursor, P->n2e.p);
-        launch_n2e_sort(s, NL, P->n2e_ptr.p, P->n2e.p);
+        launch_n2e_sort(s, N, NL, P->n2e_ptr.p, P->n2e.p);   // rows < N: sorted by the row-length pass
     } else {
         launch_slot_elements(s, NE, T.slot_val);
         int bits = 1;
@@ -388,7 +388,7 @@ int build_symbolic(xfk_problem *P)
 
     // CSR pattern
     XFK_CHECK(P->rowptr.alloc(N + 1));
-    launch_row_build(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, T.rowtmp, T.rowcnt);
+    launch_row_build(s, N, P->p_raw.p, P->n2e_ptr.p, P->n2e.p, fp, fc, T.rowtmp, T.rowcnt, n2e_radix ? nullptr : P->n2e.p);
     XFK_CHECK(exclusive_scan(P, T.rowcnt, P->rowptr.p, N));
     XFK_CHECK(hipMemcpyAsync(P->hpin, P->rowptr.p + N, sizeof(int), hipMemcpyDeviceToHost, s));
     XFK_CHECK(hipMemcpyAsync(P->hpin + 1, P->rowptr.p + P->N, sizeof(int), hipMemcpyDeviceToHost, s));

@@ -12,6 +12,7 @@
 // Guideline 16 (no L2 write-back fences on the hot path).
 #include "xfk_kernels.h"
 #include "xfk_axi.h"
+#include "xfk_spmv.h"
 
 namespace xfk {
 
@@ -202,11 +203,9 @@ __global__ void __launch_bounds__(256) k_n2e_tile(int NE, const int *__restrict_
 
 // lists of <= 16 elements: a register bitonic network (padding INT_MAX);
 // longer ones (rare high-valence nodes): insertion sort in place
-__global__ void k_n2e_sort(int NL, const int *__restrict__ ptr, int *__restrict__ n2e)
+__device__ __forceinline__ void sort_node_list(int s, int e, int *__restrict__ n2e)
 {
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= NL) return;
-    const int s = ptr[v], e = ptr[v + 1], len = e - s;
+    const int len = e - s;
     if (len <= 1) return;
     if (len <= 16) {
         int a[16];
@@ -240,6 +239,14 @@ __global__ void k_n2e_sort(int NL, const int *__restrict__ ptr, int *__restrict_
         }
         n2e[j + 1] = key;
     }
+}
+
+// nodes v0 <= v < NL (the row-length pass sorts the lists of the rows it builds)
+__global__ void k_n2e_sort(int v0, int NL, const int *__restrict__ ptr, int *__restrict__ n2e)
+{
+    const int v = v0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= NL) return;
+    sort_node_list(ptr[v], ptr[v + 1], n2e);
 }
 
 // Node -> element lists by a stable radix sort of the (node, element)
@@ -427,12 +434,15 @@ __device__ __forceinline__ void row_regs_write(int v, int s, int ne, const RowCa
 }
 
 __global__ void __launch_bounds__(kBlock) k_row_len_reg(int N, RowCands rc, int *__restrict__ tmp,
-                                                        int *__restrict__ rowcnt)
+                                                        int *__restrict__ rowcnt, int *__restrict__ n2e_sort)
 {
     __shared__ int s_c[kBlock * (kRowLds + 1)];
     const int v = blockIdx.x * kBlock + threadIdx.x;
     if (v >= N) return;
     const int s = rc.n2e_ptr[v], ne = rc.n2e_ptr[v + 1] - s;
+    // this row's element list into ascending order (the assembly's summation
+    // order) -- the candidates below do not depend on it
+    if (n2e_sort) sort_node_list(s, s + ne, n2e_sort);
     if (row_reg_ok(rc, v, ne)) {
         rowcnt[v] = ne <= 7 ? row_regs_len<16>(v, s, ne, rc) : row_regs_len<32>(v, s, ne, rc);
         return;
@@ -1016,12 +1026,16 @@ __device__ __forceinline__ void planar_element(int eb, const AssembleArgs &A, co
 constexpr int kRowBlock = 128;
 constexpr int kRowAcc = 12;
 
-template <bool AXI, bool FIRST>
+// XCD: consecutive row blocks on one XCD (xcd_tile), so the coordinates and
+// element data a block shares with the blocks a mesh row away stay in that
+// XCD's L2 (round-robin blocks fetched them once per XCD: 470 MB of HBM
+// traffic per launch for ~100 MB of algorithmic bytes on configs[2])
+template <bool AXI, bool FIRST, bool XCD = true>
 __global__ void __launch_bounds__(kRowBlock) k_assemble_rows(int N, AssembleArgs A)
 {
     __shared__ double s_acc[kRowAcc * kRowBlock];
     __shared__ int s_col[kRowAcc * kRowBlock];
-    const int i = blockIdx.x * kRowBlock + threadIdx.x;
+    const int i = (XCD ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x) * kRowBlock + threadIdx.x;
     if (i >= N) return;
     const int rs = A.rowptr[i], L = A.rowptr[i + 1] - rs;
     const bool lds = L <= kRowAcc;
@@ -1257,9 +1271,9 @@ void launch_n2e_fill(hipStream_t s, int NE, const int *p, const int *ptr, int *c
     if (NE && n2e_tile_on()) k_n2e_tile<true><<<(NE + 255) / 256, 256, 0, s>>>(NE, p, ptr, cursor, n2e);
     else if (NE) k_n2e_fill<<<(unsigned)((n3 + kBlock - 1) / kBlock), kBlock, 0, s>>>(n3, p, ptr, cursor, n2e);
 }
-void launch_n2e_sort(hipStream_t s, int NL, const int *ptr, int *n2e)
+void launch_n2e_sort(hipStream_t s, int v0, int NL, const int *ptr, int *n2e)
 {
-    if (NL) k_n2e_sort<<<nblk(NL), kBlock, 0, s>>>(NL, ptr, n2e);
+    if (NL > v0) k_n2e_sort<<<nblk(NL - v0), kBlock, 0, s>>>(v0, NL, ptr, n2e);
 }
 void launch_slot_elements(hipStream_t s, int NE, int *v)
 {
@@ -1285,10 +1299,11 @@ static bool row_reg_on()
 }
 long long row_tmp_size(int N, int NE, int nfill) { return 9LL * NE + nfill + N; }
 void launch_row_build(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e, const int *fill_ptr,
-                      const int *fill_col, int *tmp, int *rowcnt)
+                      const int *fill_col, int *tmp, int *rowcnt, int *n2e_sort)
 {
+    if (n2e_sort && !row_reg_on()) launch_n2e_sort(s, 0, N, n2e_ptr, n2e_sort);   // (the LDS path sorts nothing)
     RowCands rc{p, n2e_ptr, n2e, fill_ptr, fill_col};
-    if (N && row_reg_on()) k_row_len_reg<<<nblk(N), kBlock, 0, s>>>(N, rc, tmp, rowcnt);
+    if (N && row_reg_on()) k_row_len_reg<<<nblk(N), kBlock, 0, s>>>(N, rc, tmp, rowcnt, n2e_sort);
     else if (N) k_row_build<<<nblk(N), kBlock, 0, s>>>(N, rc, tmp, rowcnt);
 }
 void launch_row_copy(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e, const int *fill_ptr,
@@ -1340,6 +1355,16 @@ void launch_assemble_rows(hipStream_t s, int N, const AssembleArgs &A)
 {
     if (N <= 0) return;
     const int g = (N + kRowBlock - 1) / kRowBlock;
+    // XFK_ASM_XCD=0: round-robin row blocks (measurement)
+    static const bool xcd = [] {
+        const char *e = std::getenv("XFK_ASM_XCD");
+        return !(e && std::atoi(e) == 0);
+    }();
+    if (!xcd && !A.axi) {
+        if (A.iter == 0) k_assemble_rows<false, true, false><<<g, kRowBlock, 0, s>>>(N, A);
+        else k_assemble_rows<false, false, false><<<g, kRowBlock, 0, s>>>(N, A);
+        return;
+    }
     if (A.axi) {
         if (A.iter == 0) k_assemble_rows<true, true><<<g, kRowBlock, 0, s>>>(N, A);
         else k_assemble_rows<true, false><<<g, kRowBlock, 0, s>>>(N, A);

@@ -66,11 +66,12 @@ void launch_sort_segments(hipStream_t s, int N, const int *ptr, int *a);
 void launch_slot_elements(hipStream_t s, int NE, int *v);
 void launch_n2e_count(hipStream_t s, int NE, const int *p, int *deg);
 void launch_n2e_fill(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e);
-void launch_n2e_sort(hipStream_t s, int NL, const int *ptr, int *n2e);
+void launch_n2e_sort(hipStream_t s, int v0, int NL, const int *ptr, int *n2e);
 void launch_n2e_ptr(hipStream_t s, int NL, const int *keys, int n3, int *ptr);
 long long row_tmp_size(int N, int NE, int nfill);   // ints of the row-build scratch
 void launch_row_build(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e, const int *fill_ptr,
-                      const int *fill_col, int *tmp, int *rowcnt);
+                      const int *fill_col, int *tmp, int *rowcnt,
+                      int *n2e_sort = nullptr);
 void launch_row_copy(hipStream_t s, int N, const int *p, const int *n2e_ptr, const int *n2e, const int *fill_ptr,
                      const int *fill_col, const int *tmp, const int *rowptr, int *col, int *diag);
 // one Jones-Plassmann round (node pass + element pass) over the full arrays
