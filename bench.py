@@ -203,6 +203,13 @@ def cold_first_solve(device, args, kw):
                     "upload of the mesh and tables (outside the step)"}
 
 
+def _tag_order(path):
+    """Profile tags in the order they were made: r01 < r01b < ... < r03z <
+    r03aa < r03ab ... (a longer tag of the same round is a later one)."""
+    tag = os.path.basename(path).split("_")[0]
+    return (tag[:3], len(tag), tag)
+
+
 def pmc_traffic(algo_bytes, kernel="k_cg_spmv"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*_pmc_summary.json, written by tools/profile.sh from separate
@@ -210,7 +217,7 @@ def pmc_traffic(algo_bytes, kernel="k_cg_spmv"):
     Only a summary of the same workload counts: its traffic must lie within
     [0.8, 2] x this launch's algorithmic bytes."""
     import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))  # tag order: r01 < r01b < ...
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), key=_tag_order)
     for path in reversed(paths):
         try:
             with open(path) as f:
@@ -223,7 +230,7 @@ def pmc_traffic(algo_bytes, kernel="k_cg_spmv"):
 
 
 # the kernel family each iteration phase launches (xfk_phase_profile names)
-PHASE_KERNELS = (("PCG update", ("k_cg_axpy",)), ("sweep", ("k_amg_smooth",)),
+PHASE_KERNELS = (("PCG update", ("k_cg_axpy",)), ("sweep", ("k_amg_smooth",)), ("residual", ("k_amg_smooth",)),
                  ("restriction", ("k_csr_mv_tile", "k_csr_mv_g")), ("folded pre", ("k_fold_pre",)),
                  ("dense inverse x b", ("k_dense_mv",)), ("L0 folded post", ("k_fold_post0",)),
                  ("folded post", ("k_csr_mv_tile", "k_csr_mv_g")), ("prolongation", ("k_csr_mv_tile", "k_csr_mv_g")),
@@ -258,20 +265,31 @@ def annotate_phases(phases):
     streaming rate (small coarse-level launches at the dependent-launch floor,
     short dependent load chains).  Returns the source file or None."""
     import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_phase_pmc.json")))
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_phase_pmc.json")), key=_tag_order)
     if not paths:
         return None
     with open(paths[-1]) as f:
         seq = json.load(f).get("sequence", [])
     its = sorted([p for p in phases if p.get("launches_per_iteration", 0) >= 0.5],
                  key=lambda p: _phase_rank(p["phase"]))
-    if len(its) != len(seq):
+    # each launch of the profiled iteration goes to the first phase (in
+    # launch-rank order) of its kernel family with launches left: a phase
+    # launched k times per iteration (the W level's coarse visits) takes k
+    left = [max(1, int(round(p["launches_per_iteration"]))) for p in its]
+    if sum(left) != len(seq):
         return None
-    for ph, e in zip(its, seq):
-        fam = next((k for key, k in PHASE_KERNELS if key in ph["phase"]), ())
-        if not e["kernel"].startswith(fam):
+    fams = [next((k for key, k in PHASE_KERNELS if key in p["phase"]), ()) for p in its]
+    got = [[] for _ in its]
+    for e in seq:
+        q = next((q for q in range(len(its)) if left[q] > 0 and fams[q] and e["kernel"].startswith(fams[q])), None)
+        if q is None:
             return None
-    for ph, e in zip(its, seq):
+        left[q] -= 1
+        got[q].append(e)
+    for ph, es in zip(its, got):
+        e = {"rocprof_us": sum(x["rocprof_us"] for x in es) / len(es),
+             "traffic_bytes": (sum(x["traffic_bytes"] for x in es) / len(es)
+                               if all(x.get("traffic_bytes") is not None for x in es) else None)}
         ph["rocprof_us"] = e["rocprof_us"]
         if ph.get("bytes_per_launch") and e.get("traffic_bytes") is not None:
             ph["traffic_bytes"] = e["traffic_bytes"]
