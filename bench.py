@@ -177,6 +177,83 @@ def configs4_secondary(device, args):
             "ms_solve": r["ms_solve"]}
 
 
+def configs4_rank0_of_8(device, args):
+    """One rank of the 8-GPU configs[4] run, compute only: the per-rank lower
+    bound of the sharded step.  The 8 ranks first solve the mesh together
+    through the in-process transport on this GPU (untimed), rank 0 recording
+    every byte it receives (xfk_comm_record mode 2) over a first and a repeated
+    solve; rank 0's problem is then
+    rebuilt on the replay transport (xfk_comm_create_replay) and solved alone:
+    its own kernels on its own 1/8 of the mesh, bit-identical to the recorded
+    run, each collective replaced by a device copy of the recorded bytes.  So
+    the time is rank 0's compute plus device-local copies -- no xGMI
+    transfer, no wait for a peer -- and the replicated coarse levels are timed
+    apart (XFK_TIME_TAIL)."""
+    import threading
+    from xfemm_amd import kernels, synth
+    R = 8
+    kw = synth.magnetostatic(args.shard_cells)
+    opts = dict(device=device, precond=args.precond, amg_sweeps=args.amg_sweeps, amg_omega=args.amg_omega,
+                amg_dense=args.amg_dense, amg_theta=args.amg_theta)
+    comms = kernels.Comm.local_group(R)
+    comms[0].record(2)
+    for c in comms[1:]:
+        c.record(1)
+    probs = [kernels.Static2DProblem(**kw, comm=comms[q], **opts) for q in range(R)]
+    out, err = [None] * R, [None] * R
+
+    def work(q):
+        try:   # a first and a repeated solve: the replay serves each its own segment
+            for _ in range(2):
+                out[q] = probs[q].solve(rebuild_symbolic=True)
+        except Exception as ex:   # surfaced below
+            err[q] = ex
+
+    th = [threading.Thread(target=work, args=(q,)) for q in range(R)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    info0 = probs[0].dist_info()
+    for p in probs:
+        p.close()
+    for e in err:
+        if e is not None:
+            raise e
+    order = kernels.check_comm_logs([c.log() for c in comms])
+    rep = comms[0].replay()
+    for c in comms:
+        c.close()
+    P = kernels.Static2DProblem(**kw, comm=rep, **opts)
+    P.solve(rebuild_symbolic=True)
+    _hip_sync()
+    t0 = time.perf_counter()
+    res = [P.solve(rebuild_symbolic=True) for _ in range(args.secondary_steps)]
+    _hip_sync()
+    dt = (time.perf_counter() - t0) / args.secondary_steps
+    rt = P.solve(rebuild_symbolic=True, time_tail=True)
+    P.close()
+    rep.close()
+    r = res[-1]
+    it = max(1, r["cg_iters"])
+    pcg = r["ms_solve"] - r["ms_amg_setup"]
+    return {"workload": "configs[4] rank 0 of 8, compute only: synthetic %d-tri mesh row-block sharded over 8 "
+                        "ranks, rank 0's solve alone on one GPU with every collective replayed from its recording "
+                        "of the 8-rank run (device copies, no peers)" % (2 * args.shard_cells ** 2),
+            "metric": "per-rank step time (lower bound of the 8-GPU step)", "ms_per_step": 1e3 * dt,
+            "steps": args.secondary_steps, "warmup": 1, "rank0_rows": info0["n_own"], "rank0_halo": info0["n_halo"],
+            "pcg_iters": r["cg_iters"], "pcg_iters_8rank_run": out[0]["cg_iters"],
+            "amg_levels": r["amg_levels"], "ms_symbolic": r["ms_symbolic"], "ms_assemble": r["ms_assemble"],
+            "ms_amg_setup": r["ms_amg_setup"], "ms_per_pcg_iteration": pcg / it,
+            "replicated_tail": {"ms_setup": rt["ms_rep_setup"], "ms_per_vcycle": rt["ms_rep_cycle"] / max(1, rt["rep_cycles"]),
+                                "vcycles": rt["rep_cycles"],
+                                "note": "every rank builds and applies the coarse levels of <= 250k global rows; per "
+                                        "V-cycle: the all-gather of the coarse right-hand side (replayed: a device "
+                                        "copy) + the replicated cycle (HIP events, XFK_TIME_TAIL solve after the "
+                                        "timed ones)"},
+            "collectives_per_solve": order}
+
+
 def cold_first_solve(device, args, kw):
     """A first solve of a fresh problem: new Static2DProblem (host -> HBM
     upload timed apart), then its first solve() with none of the per-problem
@@ -512,6 +589,7 @@ def main():
         out["secondary"] = [nonlinear_secondary(local, args)]
         if not args.no_configs4:
             out["secondary"].append(configs4_secondary(local, args))
+            out["secondary"].append(configs4_rank0_of_8(local, args))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_cells, args.nonlinear)
     if rank == 0:

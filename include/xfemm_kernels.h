@@ -139,6 +139,13 @@ typedef struct {
     int amg_levels;             /* AMG: levels of the last hierarchy */
     double amg_op_complexity;   /* AMG: sum of level nonzeros / fine nonzeros */
     double ms_amg_setup;        /* AMG: device time of the hierarchy setups, ms (inside ms_solve) */
+    /* sharded solves with XFK_TIME_TAIL: device time of the replicated coarse
+     * levels (every rank builds and applies them): the V-cycles' all-gather of
+     * the coarse right-hand side + the replicated cycle, summed over the solve,
+     * and the setup's build of the replicated levels */
+    double ms_rep_cycle;
+    int rep_cycles;             /* V-cycles timed */
+    double ms_rep_setup;
 } xfk_result;
 
 typedef struct xfk_problem xfk_problem;
@@ -150,7 +157,7 @@ int xfk_device_count(void);
 int xfk_problem_create(const xfk_problem_desc *desc, int device, xfk_problem **out);
 void xfk_problem_destroy(xfk_problem *prob);
 
-enum { XFK_REBUILD_SYMBOLIC = 1, XFK_TIME_SPMV = 2 };
+enum { XFK_REBUILD_SYMBOLIC = 1, XFK_TIME_SPMV = 2, XFK_TIME_TAIL = 4 };
 
 /* Solver options.  The reference preconditions its PCG with a sequential
  * SSOR sweep (spars.cpp:186-236, CBigLinProb::MultPC); the device offers
@@ -194,7 +201,9 @@ int xfk_set_option(xfk_problem *prob, int option, double value);
 /* FSolver::Static2D on the device.  flags: XFK_REBUILD_SYMBOLIC rebuilds the
  * CSR pattern, colouring and boundary maps (they are cached otherwise);
  * XFK_TIME_SPMV brackets every 16th SpMV launch with HIP events on the
- * solver stream and reports the mean launch duration. */
+ * solver stream and reports the mean launch duration; XFK_TIME_TAIL (sharded
+ * solves) brackets the replicated coarse levels of every V-cycle and of the
+ * setup (ms_rep_cycle, ms_rep_setup). */
 int xfk_static2d(xfk_problem *prob, int flags, xfk_result *res);
 
 /* A at every node (V * c, the value fsolver writes to .ans), host copy. */
@@ -232,6 +241,47 @@ int xfk_comm_create_local(int nranks, xfk_comm **out_array);
 void xfk_comm_destroy(xfk_comm *comm);
 int xfk_comm_rank(const xfk_comm *comm);
 int xfk_comm_size(const xfk_comm *comm);
+
+/* Issue order and recording.  Every collective of a communicator runs after
+ * the previous one in device order: when a collective is enqueued on another
+ * stream than the previous collective, the communicator first makes that
+ * stream wait for the event recorded after the previous one (RCCL matches
+ * collectives by issue order; the sharded path issues halo exchanges on a side
+ * stream and all-reduces / all-gathers on the main stream).
+ *
+ * xfk_comm_record(comm, mode) starts an empty recording (mode 1: the sequence
+ * of collectives; mode 2: the sequence and every byte the rank receives, kept
+ * in device memory, for xfk_comm_create_replay), or stops it (mode 0; the log
+ * is kept).  xfk_comm_log copies the log: one ALLREDUCE / ALLGATHER / EXCHANGE
+ * record per collective call, each EXCHANGE followed by one SEND / RECV
+ * record per halo range.  Every rank of a correct program produces the same
+ * sequence of calls (op, stream, bytes), and the send of rank a to rank b in
+ * exchange k matches the receive of b from a in the same exchange. */
+enum { XFK_COMM_ALLREDUCE = 1, XFK_COMM_EXCHANGE = 2, XFK_COMM_SEND = 3, XFK_COMM_RECV = 4, XFK_COMM_ALLGATHER = 5 };
+typedef struct {
+    long long seq;              /* collective number since the recording started */
+    int op;                     /* XFK_COMM_* */
+    int stream;                 /* stream index in first-use order (0: the first stream this communicator saw) */
+    int waited;                 /* 1: another stream than the previous collective's; the communicator
+                                   made it wait for that collective's completion event */
+    int peer;                   /* SEND / RECV: the peer rank; -1 otherwise */
+    long long bytes;            /* payload: ALLREDUCE the reduced bytes, ALLGATHER the bytes per rank,
+                                   SEND / RECV the range; EXCHANGE 0 */
+    long long g0;               /* SEND / RECV: the range's first global row; EXCHANGE: its range count */
+} xfk_comm_op;
+int xfk_comm_record(xfk_comm *comm, int mode);
+int xfk_comm_log(const xfk_comm *comm, xfk_comm_op *out, int cap, int *count);
+/* A communicator that replays the recording (mode 2) of `recorded`: same rank
+ * and size, no peers; every collective checks that it is the next one of the
+ * recording (op and sizes, else XFK_ERR_ARG) and copies the recorded received
+ * bytes into place.  The recording is cut into one segment per solve
+ * (xfk_static2d); replayed solve k is served segment k, the last segment
+ * repeating, and must issue exactly that segment's collectives (a first and a
+ * repeated solve differ: the PCG's batching uses the last solve's iteration
+ * count).  It runs one rank of a sharded solve alone on its GPU with the
+ * exact inputs of the recorded run: the per-rank compute time without the
+ * transport. */
+int xfk_comm_create_replay(const xfk_comm *recorded, xfk_comm **out);
 
 typedef struct {
     int rank, nranks;

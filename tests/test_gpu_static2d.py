@@ -50,7 +50,7 @@ def _golden(name):
     return pr, mesh, sol
 
 
-@pytest.mark.parametrize("name", ["Temp", "Temp1"])
+@pytest.mark.parametrize("name", ["Temp", "Temp1", "femmcli_femfile"])
 def test_golden_ans_solution(name):
     pr, mesh, sol = _golden(name)
     P = kernels.Static2DProblem(**kernel_kwargs(pr, mesh))

@@ -3,7 +3,12 @@
 * golden vectors: cfemm/fsolver/test/Temp.ans.check and Temp1.ans.check were
   written by the reference fsolver; the restated Static2D + CBigLinProb must
   reproduce their A column bit for bit (nonlinear steel, 3 Newton iterations,
-  SSOR-PCG, periodic boundaries, serial circuits).
+  SSOR-PCG, periodic boundaries, serial circuits).  The third golden,
+  cfemm/femmcli/test/femmcli_femfile.result.ans.check (femmcli_femfile.lua:
+  the Temp problem through femmcli's own fmesher + fsolver), is read from its
+  own .fem (Windows number formatting: "1e-008") and pinned the same way; its
+  bytes equal Temp1.ans.check's (femmcli meshed the problem exactly as the
+  fsolver test's Temp1 mesh), which the test records.
 * the reference's own spars.cpp / CMaterialProp.cpp compiled into oracle/_ref
   (only where /root/reference was present at build time) must agree bit for
   bit with the restatement.
@@ -28,7 +33,7 @@ def _golden(name):
     return pr, mesh, sol
 
 
-@pytest.mark.parametrize("name", ["Temp", "Temp1"])
+@pytest.mark.parametrize("name", ["Temp", "Temp1", "femmcli_femfile"])
 def test_oracle_reproduces_golden_ans_bit_exact(name):
     pr, mesh, sol = _golden(name)
     A, st, circ = oracle.solve(pr, mesh)
@@ -41,8 +46,20 @@ def test_oracle_reproduces_golden_ans_bit_exact(name):
         assert sol.circ[k][1] == J
 
 
+def test_femmcli_golden_is_the_fsolver_temp1_golden():
+    """femmcli_femfile.result.ans.check (fmesher + fsolver driven by femmcli)
+    is byte for byte the fsolver test's Temp1.ans.check: the third reference
+    golden pins the same mesh and A, reached from a differently formatted
+    .fem (parsed by femfile and by the product's FSolver alike)."""
+    a = open(os.path.join(GOLDEN, "femmcli_femfile.ans.check"), "rb").read()
+    b = open(os.path.join(GOLDEN, "Temp1.ans.check"), "rb").read()
+    assert a == b
+    fa = open(os.path.join(GOLDEN, "femmcli_femfile.fem")).read()
+    assert "1e-008" in fa
+
+
 @needs_ref
-@pytest.mark.parametrize("name", ["Temp", "Temp1"])
+@pytest.mark.parametrize("name", ["Temp", "Temp1", "femmcli_femfile"])
 def test_restated_linprob_matches_reference_spars(name):
     pr, mesh, sol = _golden(name)
     A1, _, _ = oracle.solve(pr, mesh, "oracle")

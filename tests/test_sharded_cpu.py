@@ -141,3 +141,17 @@ def test_sharded_pcg_gloo(world):
         it, err, npeers = open(os.path.join(d, "result.txt")).read().split()
     assert int(npeers) == 1 and int(it) > 10
     assert float(err) <= 1e-6
+
+
+def test_comm_log_checker_rejects_a_mismatched_sequence():
+    """The checker itself: a rank that posts an all-reduce where its peer
+    posts an exchange, or a send without its receive, is reported."""
+    a = [dict(seq=0, op="allreduce", stream=0, waited=0, peer=-1, bytes=8, g0=0)]
+    b = [dict(seq=0, op="exchange", stream=0, waited=0, peer=-1, bytes=0, g0=0)]
+    with pytest.raises(AssertionError):
+        kernels.check_comm_logs([a, b])
+    e0 = [dict(seq=0, op="exchange", stream=1, waited=1, peer=-1, bytes=0, g0=1),
+          dict(seq=0, op="send", stream=1, waited=1, peer=1, bytes=80, g0=5)]
+    e1 = [dict(seq=0, op="exchange", stream=1, waited=1, peer=-1, bytes=0, g0=0)]
+    with pytest.raises(AssertionError):
+        kernels.check_comm_logs([e0, e1])

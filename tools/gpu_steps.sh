@@ -16,7 +16,7 @@ for st in $STEPS; do
     tests) timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread \
              > gpurun_out/gpu_tests_$TAG.log 2>&1; rc=$? ;;
     bench) timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; rc=$? ;;
-    benchq) timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; rc=$? ;;
+    benchq) timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; rc=$? ;;
     prof) bash tools/profile.sh $TAG; rc=$? ;;
     smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;

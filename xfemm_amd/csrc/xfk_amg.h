@@ -183,6 +183,17 @@ struct Amg {
     int host_big_n = 0;
     double *part_gam_ = nullptr;      // vcycle's gamma partials, for vc_dist
     SideStream side;                  // sharded: halo exchanges overlapped with interior tiles
+    // sharded, XFK_TIME_TAIL: event pairs around the replicated tail -- per
+    // V-cycle the all-gather of the coarse right-hand side and the replicated
+    // cycle (kind 0), in the setup the build of the replicated levels (kind 1)
+    bool time_tail = false;
+    std::vector<hipEvent_t> tail_ev;
+    std::vector<char> tail_kind;      // per pair
+    int tail_used = 0;                // events recorded (pairs * 2)
+    int tail_begin(hipStream_t s, int kind);
+    void tail_end(hipStream_t s, int at);
+    // sum the recorded pairs per kind (after the stream is synchronised); resets
+    int tail_read(double &ms_cycle, int &cycles, double &ms_setup);
     // single-device setup steps off the critical path -- R = P^T beside A P,
     // the folded transfers P~ / R~ beside the next level -- on a second
     // stream with scratch of its own (a: fork, b: R done / join, c: P~ done)

@@ -2399,6 +2399,7 @@ Amg::~Amg()
     if (host_int) (void)hipHostFree(host_int);
     if (host_big) (void)hipHostFree(host_big);
     if (ev_host) (void)hipEventDestroy(ev_host);
+    for (hipEvent_t e : tail_ev) (void)hipEventDestroy(e);
 }
 
 #define AMG_CHECK(call)                                                          \
@@ -3174,7 +3175,7 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         AMG_CHECK(hipEventRecord(sw.b, sw.cs));
         rt_pending = true;
     }
-    if (l == 0 && A.has16 &&
+    if (l == 0 && A.has16 && !dist &&
         (rc = build_col16<256>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)) != XFK_OK)
         return rc;
     if (l == 0 && A.has32 &&
@@ -3801,6 +3802,11 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
         A.val = val;
         A.dist = true;
         A.plan = halo_;
+        // 16-bit tile columns of the owned rows (the overlapped PCG SpMV and the
+        // level-0 sweeps read them; a boundary tile reaching the halo ids spans
+        // more than 65535 columns and keeps the int columns, decided per tile)
+        A.has16 = col16 < 0 ? col16_on() : col16 != 0;
+        if (A.has16 && (rc = build_col16<kCgBlock>(s, n, rowptr, col, nnz, A.a16, A.a16b)) != XFK_OK) return rc;
     }
     for (int l = 0;; ++l) {
         AmgLevel &A = *L[l];
@@ -3821,11 +3827,18 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
         long long nc = 0;
         rc = aggregate(s, l, nc, false);
         if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
+        // test hook: this rank reports an aggregation failure at level 0, so
+        // every rank must agree on the Jacobi fallback through the collectives
+        if (const char *fr = std::getenv("XFK_TEST_AMG_FAIL_RANK"))
+            if (l == 0 && std::atoi(fr) == rank) rc = XFK_ERR_UNSUPPORTED;
         bool rep = false;
         if ((rc = galerkin_dist(s, l, rc == XFK_OK ? 0 : 1, rep)) != XFK_OK) return rc;
         if (rep) {
             lrep = l + 1;
-            return build(s, l + 1);
+            const int te = tail_begin(s, 1);
+            rc = build(s, l + 1);
+            tail_end(s, te);
+            return rc;
         }
     }
 }
@@ -4425,9 +4438,11 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
         // the replicated levels: gather the global right-hand side, solve the
         // same coarse problem on every rank, read the own aggregates back
         launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, cb_loc.p, false, GR, done);
+        const int te = tail_begin(s, 0);
         if ((rc = comm->allgather(cb_loc.p, cb_all.p, (size_t)ncmax, s)) != XFK_OK) return nullptr;
         k_unpad<<<nb(C.n), kB, 0, s>>>(C.n, nranks, c0_dev.p, cb_all.p, ncmax, C.b.p, done);
         xc = vcycle_level(*this, s, l + 1, C.b.p, nullptr, done) + c0[rank];
+        tail_end(s, te);
     }
     if (A.n > 0) launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)A.pnnz / A.n), done);
     for (int k = 0; k < sweeps; ++k) {
@@ -4440,6 +4455,45 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
         cur = nx;
     }
     return cur;
+}
+
+int Amg::tail_begin(hipStream_t s, int kind)
+{
+    if (!time_tail) return -1;
+    const int at = tail_used;
+    while ((int)tail_ev.size() < at + 2) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return -1;
+        tail_ev.push_back(e);
+    }
+    if (hipEventRecord(tail_ev[at], s) != hipSuccess) return -1;
+    tail_kind.resize(at / 2 + 1);
+    tail_kind[at / 2] = (char)kind;
+    tail_used = at + 2;
+    return at;
+}
+
+void Amg::tail_end(hipStream_t s, int at)
+{
+    if (at >= 0) (void)hipEventRecord(tail_ev[at + 1], s);
+}
+
+int Amg::tail_read(double &ms_cycle, int &cycles, double &ms_setup)
+{
+    ms_cycle = ms_setup = 0;
+    cycles = 0;
+    for (int k = 0; k + 1 < tail_used; k += 2) {
+        float m = 0;
+        AMG_CHECK(hipEventElapsedTime(&m, tail_ev[k], tail_ev[k + 1]));
+        if (tail_kind[k / 2] == 0) {
+            ms_cycle += m;
+            ++cycles;
+        } else {
+            ms_setup += m;
+        }
+    }
+    tail_used = 0;
+    return XFK_OK;
 }
 
 int Amg::refresh(hipStream_t s)

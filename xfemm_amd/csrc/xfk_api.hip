@@ -930,15 +930,18 @@ static int pcg_precond_spmv(xfk_problem *P, long long it, bool stamp)
             if ((rc = P->side.init()) != XFK_OK) return rc;
             if ((rc = build_tile_split(s, P->N, kCgBlock, P->rowptr.p, P->col.p, P->ts)) != XFK_OK) return rc;
         }
+        const unsigned short *c16;
+        const int *cbase;
+        spmv_col16(P, c16, cbase);   // (boundary tiles reach the halo ids: int columns, decided per tile)
         rc = exchange_overlapped(
             s, P->side, [&](hipStream_t cs) { return P->comm->exchange(P->halo, A.U, cs); },
             [&] {
                 launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G, St, Rg,
-                               pg, P->ts.tiles.p, P->ts.n_in);
+                               pg, P->ts.tiles.p, P->ts.n_in, c16, cbase);
             },
             [&] {
                 launch_cg_spmv(s, P->N, P->rowptr.p, P->col.p, P->val.p, A.U, P->W2.p, P->part_loc.p + 2 * G, St, Rg,
-                               pg, P->ts.tiles.p + P->ts.n_in, P->ts.n_bd);
+                               pg, P->ts.tiles.p + P->ts.n_in, P->ts.n_bd, c16, cbase);
             });
         if (rc != XFK_OK) return rc;
         return allreduce_partials(P, 3);
@@ -1628,8 +1631,13 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     xfk_result R{};
     int rc = XFK_OK;
     float ms = 0;
+    if (P->comm && (rc = P->comm->solve_boundary()) != XFK_OK) return rc;
     P->time_spmv = (flags & XFK_TIME_SPMV) != 0;
     P->spmv_used = 0;
+    if (P->amg) {
+        P->amg->time_tail = (flags & XFK_TIME_TAIL) != 0 && P->comm;
+        P->amg->tail_used = 0;
+    }
     if (P->time_spmv && P->spmv_ev.empty()) {
         P->spmv_ev.resize(2 * 512);
         for (auto &ev : P->spmv_ev) XFK_CHECK(hipEventCreate(&ev));
@@ -1728,6 +1736,10 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
         }
         R.spmv_samples = P->spmv_used / 2;
         R.spmv_ms_avg = sum / R.spmv_samples;
+    }
+    if (P->amg && P->amg->time_tail) {
+        if ((rc = P->amg->tail_read(R.ms_rep_cycle, R.rep_cycles, R.ms_rep_setup)) != XFK_OK) return rc;
+        P->amg->time_tail = false;
     }
     R.newton_iters = Iter;
     R.last_res = resn;

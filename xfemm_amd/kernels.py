@@ -22,6 +22,7 @@ iptr = C.POINTER(C.c_int)
 XFK_OK = 0
 XFK_REBUILD_SYMBOLIC = 1
 XFK_TIME_SPMV = 2
+XFK_TIME_TAIL = 4
 XFK_PRECOND_JACOBI = 0
 XFK_PRECOND_AMG = 1
 PRECONDS = {"jacobi": XFK_PRECOND_JACOBI, "amg": XFK_PRECOND_AMG}
@@ -46,7 +47,8 @@ EXPORTED = (
     "xfk_problem_create_harmonic", "xfk_harmonic2d", "xfk_get_solution_complex", "xfk_get_circuits_complex",
     "xfk_get_csr_complex",
     "xfk_comm_unique_id", "xfk_comm_create_rccl", "xfk_comm_create_local", "xfk_comm_destroy",
-    "xfk_comm_rank", "xfk_comm_size", "xfk_partition_plan", "xfk_partition_plan_coupled", "xfk_problem_create_dist", "xfk_dist_get_info",
+    "xfk_comm_rank", "xfk_comm_size", "xfk_comm_record", "xfk_comm_log", "xfk_comm_create_replay",
+    "xfk_partition_plan", "xfk_partition_plan_coupled", "xfk_problem_create_dist", "xfk_dist_get_info",
     "xfk_magdir_eval",
 )
 
@@ -109,7 +111,8 @@ class Result(C.Structure):
                 ("ms_symbolic", C.c_double), ("ms_assemble", C.c_double), ("ms_solve", C.c_double),
                 ("spmv_ms_avg", C.c_double), ("spmv_samples", C.c_int),
                 ("color_rounds", C.c_int), ("precond", C.c_int), ("amg_levels", C.c_int),
-                ("amg_op_complexity", C.c_double), ("ms_amg_setup", C.c_double)]
+                ("amg_op_complexity", C.c_double), ("ms_amg_setup", C.c_double), ("ms_rep_cycle", C.c_double),
+                ("rep_cycles", C.c_int), ("ms_rep_setup", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -172,6 +175,9 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_comm_destroy.argtypes = [vp]
     L.xfk_comm_rank.argtypes = [vp]
     L.xfk_comm_size.argtypes = [vp]
+    L.xfk_comm_record.argtypes = [vp, C.c_int]
+    L.xfk_comm_log.argtypes = [vp, vp, C.c_int, C.POINTER(C.c_int)]
+    L.xfk_comm_create_replay.argtypes = [vp, C.POINTER(vp)]
     L.xfk_partition_plan.argtypes = [C.c_int, C.c_int, iptr, C.c_int, C.c_int, C.POINTER(DistInfo),
                                      iptr, iptr, iptr, iptr]
     L.xfk_partition_plan_coupled.argtypes = [C.c_int, C.c_int, iptr, C.c_int, C.c_int, C.c_int, iptr,
@@ -396,9 +402,10 @@ class Static2DProblem:
         except Exception:
             pass
 
-    def solve(self, rebuild_symbolic: bool = False, time_spmv: bool = False) -> dict:
+    def solve(self, rebuild_symbolic: bool = False, time_spmv: bool = False, time_tail: bool = False) -> dict:
         r = Result()
-        flags = (XFK_REBUILD_SYMBOLIC if rebuild_symbolic else 0) | (XFK_TIME_SPMV if time_spmv else 0)
+        flags = ((XFK_REBUILD_SYMBOLIC if rebuild_symbolic else 0) | (XFK_TIME_SPMV if time_spmv else 0) |
+                 (XFK_TIME_TAIL if time_tail else 0))
         _check(_lib.xfk_static2d(self._h, flags, C.byref(r)))
         self.result = r
         return r.as_dict()
@@ -589,9 +596,18 @@ def pcg_solve_csr(rowptr, col, val, b, V0=None, flag=0, precision=1e-8, device=0
     return V, it.value, er.value
 
 
+class CommOp(C.Structure):
+    _fields_ = [("seq", C.c_longlong), ("op", C.c_int), ("stream", C.c_int), ("waited", C.c_int),
+                ("peer", C.c_int), ("bytes", C.c_longlong), ("g0", C.c_longlong)]
+
+
+COMM_OPS = {1: "allreduce", 2: "exchange", 3: "send", 4: "recv", 5: "allgather"}
+
+
 class Comm:
     """Communicator of the sharded solve (xfk_comm): RCCL, one process per GPU,
-    or an in-process group of ranks driven by one host thread each."""
+    an in-process group of ranks driven by one host thread each, or the replay
+    of one rank's recording (compute-only runs of a sharded rank)."""
 
     def __init__(self, handle):
         self._h = handle
@@ -617,6 +633,29 @@ class Comm:
         _check(load_library().xfk_comm_create_local(size, hs))
         return [cls(C.c_void_p(hs[q])) for q in range(size)]
 
+    def record(self, mode: int = 1):
+        """Start an empty recording (1: the collective sequence; 2: also every
+        received byte, for replay()); 0 stops it (the log stays readable)."""
+        _check(load_library().xfk_comm_record(self._h, int(mode)))
+
+    def log(self) -> list:
+        """The recorded collectives: dicts seq, op (allreduce / exchange / send /
+        recv / allgather), stream, waited, peer, bytes, g0 (xfk_comm_op)."""
+        L = load_library()
+        n = C.c_int()
+        _check(L.xfk_comm_log(self._h, None, 0, C.byref(n)))
+        buf = (CommOp * max(1, n.value))()
+        _check(L.xfk_comm_log(self._h, C.cast(buf, C.c_void_p), n.value, C.byref(n)))
+        return [dict(seq=o.seq, op=COMM_OPS.get(o.op, str(o.op)), stream=o.stream, waited=o.waited, peer=o.peer,
+                     bytes=o.bytes, g0=o.g0) for o in buf[:n.value]]
+
+    def replay(self) -> "Comm":
+        """A communicator serving this rank's mode-2 recording cyclically
+        (xfk_comm_create_replay): the rank runs alone with the recorded inputs."""
+        h = C.c_void_p()
+        _check(load_library().xfk_comm_create_replay(self._h, C.byref(h)))
+        return Comm(h)
+
     def close(self):
         if getattr(self, "_h", None):
             load_library().xfk_comm_destroy(self._h)
@@ -627,6 +666,58 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+def check_comm_logs(logs) -> dict:
+    """Issue-order check of one recorded program over all ranks (logs[q] =
+    Comm.log() of rank q): every rank made the same sequence of collective
+    calls -- op, stream index, payload bytes of all-reduces and all-gathers --
+    and in every exchange each send of rank a to rank b matches a receive of b
+    from a (length and first global row) in the same exchange, and the reverse.
+    Raises AssertionError naming the first mismatch; returns a summary."""
+    R = len(logs)
+    calls = []
+    for q, lg in enumerate(logs):
+        cs = {}
+        for o in lg:
+            c = cs.setdefault(o["seq"], {"head": None, "send": [], "recv": []})
+            if o["op"] in ("send", "recv"):
+                c[o["op"]].append((o["peer"], o["bytes"], o["g0"]))
+            else:
+                c["head"] = (o["op"], o["stream"], o["bytes"] if o["op"] != "exchange" else 0)
+        calls.append([cs[k] for k in sorted(cs)])
+    n = len(calls[0])
+    for q in range(1, R):
+        assert len(calls[q]) == n, "rank %d made %d collective calls, rank 0 %d" % (q, len(calls[q]), n)
+    waits = 0
+    streams = set()
+    for k in range(n):
+        h0 = calls[0][k]["head"]
+        for q in range(1, R):
+            assert calls[q][k]["head"] == h0, "call %d: rank 0 %s, rank %d %s" % (k, h0, q, calls[q][k]["head"])
+        streams.add(h0[1])
+        if h0[0] != "exchange":
+            continue
+        for a in range(R):
+            for (b, nb, g0) in calls[a][k]["send"]:
+                assert (a, nb, g0) in calls[b][k]["recv"], \
+                    "exchange %d: rank %d sends %d B (row %d) to %d, which posts no such receive" % (k, a, nb, g0, b)
+            for (b, nb, g0) in calls[a][k]["recv"]:
+                assert (a, nb, g0) in calls[b][k]["send"], \
+                    "exchange %d: rank %d expects %d B (row %d) from %d, which sends no such range" % (k, a, nb, g0, b)
+    for lg in logs:
+        prev = None
+        for o in lg:
+            if o["op"] in ("send", "recv"):
+                continue
+            if prev is not None and o["stream"] != prev:
+                assert o["waited"] == 1, "call %d changes stream without the ordering wait" % o["seq"]
+            waits += o["waited"]
+            prev = o["stream"]
+    ops = {}
+    for c in calls[0]:
+        ops[c["head"][0]] = ops.get(c["head"][0], 0) + 1
+    return {"calls": n, "ops": ops, "streams": sorted(streams), "stream_switches": waits}
 
 
 def partition_plan(n_nodes: int, p, rank: int, nranks: int, coupled=None) -> dict:
