@@ -49,6 +49,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+R_OVERRIDE = None       # tools/lab/rank0_probe.py: ranks of the compute-only probe
 
 
 def _hip_sync():
@@ -191,10 +192,10 @@ def configs4_rank0_of_8(device, args):
     apart (XFK_TIME_TAIL)."""
     import threading
     from xfemm_amd import kernels, synth
-    R = 8
+    R = R_OVERRIDE or 8
     kw = synth.magnetostatic(args.shard_cells)
     opts = dict(device=device, precond=args.precond, amg_sweeps=args.amg_sweeps, amg_omega=args.amg_omega,
-                amg_dense=args.amg_dense, amg_theta=args.amg_theta)
+                amg_dense=args.amg_dense, amg_theta=args.amg_theta, amg_replicate=args.amg_replicate)
     comms = kernels.Comm.local_group(R)
     comms[0].record(2)
     for c in comms[1:]:
@@ -400,6 +401,8 @@ def main():
     ap.add_argument("--amg-omega", type=float, default=1.75, help="Jacobi weight factor (weight omega / rho)")
     ap.add_argument("--amg-dense", type=int, default=None, help="dense coarsest level of at most this many rows")
     ap.add_argument("--amg-theta", type=float, default=None, help="strength threshold (default 0.08)")
+    ap.add_argument("--amg-replicate", type=int, default=None,
+                    help="sharded solves: coarse levels of at most this many global rows are replicated")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phases", action="store_true", help="skip the per-phase table")
     ap.add_argument("--traffic", type=float, default=None,
@@ -436,7 +439,8 @@ def main():
         with stdout_to_stderr():
             comm = kernels.Comm.rccl(uid, rank, world, local)
         P = kernels.Static2DProblem(device=local, comm=comm, precond=args.precond, amg_sweeps=args.amg_sweeps,
-                                    amg_omega=args.amg_omega, amg_dense=args.amg_dense, amg_theta=args.amg_theta, **kw)
+                                    amg_omega=args.amg_omega, amg_dense=args.amg_dense, amg_theta=args.amg_theta,
+                                    amg_replicate=args.amg_replicate, **kw)
         n_dof = P.n_nodes                       # global DoF of the sharded mesh
     else:
         cells = args.cells

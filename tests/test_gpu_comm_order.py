@@ -86,9 +86,11 @@ def single(kw, **opt):
 
 
 @pytest.mark.parametrize("nranks", [2, 4, 8])
-def test_linear_sharded_issue_order(nranks):
-    """Overlapped SpMV / level-0 sweeps (two streams), sharded AMG setup with a
-    sharded coarse level (low replication threshold) and the replicated tail."""
+def test_linear_sharded_issue_order(monkeypatch, nranks):
+    """Overlapped SpMV / level-0 sweeps (XFK_OVERLAP=1: exchanges on side
+    streams), sharded AMG setup with a sharded coarse level (low replication
+    threshold) and the replicated tail."""
+    monkeypatch.setenv("XFK_OVERLAP", "1")
     kw = synth.magnetostatic(240)
     res, sols, logs, comms = run_recorded(kw, nranks, amg_replicate=2000)
     close_all(comms)
@@ -101,6 +103,16 @@ def test_linear_sharded_issue_order(nranks):
     r1, A1 = single(kw)
     for A in sols:
         assert rel_err(A, A1) <= TOL_LINEAR
+
+
+@pytest.mark.parametrize("nranks", [2, 8])
+def test_default_sharded_issue_order_one_stream(nranks):
+    """The default (no overlap): every collective on the solve stream."""
+    kw = synth.magnetostatic(240)
+    res, sols, logs, comms = run_recorded(kw, nranks, amg_replicate=2000)
+    close_all(comms)
+    summ = kernels.check_comm_logs(logs)
+    assert len(summ["streams"]) == 1 and summ["stream_switches"] == 0
 
 
 @pytest.mark.parametrize("nranks", [2, 4])

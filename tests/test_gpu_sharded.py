@@ -119,16 +119,16 @@ def test_sharded_coarse_levels(nranks):
 
 @pytest.mark.parametrize("nranks,cells,rep", [(3, 200, 250000), (2, 480, 1000)])
 def test_exchange_overlap_is_bit_identical(monkeypatch, nranks, cells, rep):
-    """The sharded halo exchanges (PCG SpMV, V-cycle sweeps on tile levels)
-    run on a side stream while the tiles without halo columns compute; with
-    XFK_NO_OVERLAP=1 each exchange precedes one launch over every tile.  Same
-    tiles, same partial-sum slots: the same bits and iterations.  The second
-    case keeps a level-1 of > 16k rows per rank sharded (tile kernels there
-    too)."""
+    """With XFK_OVERLAP=1 the sharded halo exchanges (PCG SpMV, V-cycle
+    sweeps on tile levels) run on a side stream while the tiles without halo
+    columns compute; by default each exchange precedes one launch over every
+    tile.  Same tiles, same partial-sum slots: the same bits and iterations.
+    The second case keeps a level-1 of > 16k rows per rank sharded (tile
+    kernels there too)."""
     kw = synth.magnetostatic(cells)
-    on = run_sharded(kw, nranks, amg_replicate=rep)
-    monkeypatch.setenv("XFK_NO_OVERLAP", "1")
     off = run_sharded(kw, nranks, amg_replicate=rep)
+    monkeypatch.setenv("XFK_OVERLAP", "1")
+    on = run_sharded(kw, nranks, amg_replicate=rep)
     for (r_on, A_on, _, _), (r_off, A_off, _, _) in zip(on, off):
         assert r_on["precond"] == kernels.XFK_PRECOND_AMG
         assert r_on["cg_iters"] == r_off["cg_iters"]

@@ -2925,10 +2925,17 @@ static bool spec_on()
     return v;
 }
 
+// Off by default: on MI355X each cross-stream hop (side stream waits for the
+// main stream, main waits for the exchange) costs more than the interior
+// tiles it overlaps -- configs[4] rank 0 of 8, compute only, 469 vs 304 us
+// per PCG iteration (profiles/r04c_rank0_overlap.txt).  XFK_OVERLAP=1 turns
+// it on (XFK_NO_OVERLAP=1 keeps it off).
 bool overlap_enabled()
 {
-    const char *e = std::getenv("XFK_NO_OVERLAP");
-    return !(e && std::atoi(e) != 0);
+    const char *n = std::getenv("XFK_NO_OVERLAP");
+    if (n && std::atoi(n) != 0) return false;
+    const char *e = std::getenv("XFK_OVERLAP");
+    return e && std::atoi(e) != 0;
 }
 
 int Amg::resolve_deferred(hipStream_t s, bool &overflow)
@@ -3726,6 +3733,13 @@ int Amg::build(hipStream_t s, int l0)
             return build(s, l0);
         }
         for (int k = l0; k < nlev; ++k) stats.nnz[k] = L[k]->nnz;
+        if (std::getenv("XFK_AMG_HINTS_PRINT")) {   // lab: the capacities / MIS rounds a setup measured
+            std::fprintf(stderr, "[amg hints] levels %d:", nlev);
+            for (auto &h : cap_hint) std::fprintf(stderr, " cap[%d.%d]=%d", h.first / 4, h.first % 4, h.second);
+            for (auto &h : mis_hint) std::fprintf(stderr, " mis[%d]=%d", h.first, h.second);
+            for (int k = 0; k < nlev; ++k) std::fprintf(stderr, " n%d=%d/%lld", k, L[k]->n, L[k]->nnz);
+            std::fprintf(stderr, "\n");
+        }
         stats.levels = nlev;
         double tot = 0;
         for (int k = 0; k < nlev; ++k) tot += (double)stats.nnz[k];

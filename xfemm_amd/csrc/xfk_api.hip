@@ -30,6 +30,21 @@
 #include <cstdlib>
 #include "xfk_partition.h"
 
+namespace {
+// XFK_TRACE_CREATE=1: host milliseconds of each problem-creation stage on stderr
+struct CreateTrace {
+    bool on = std::getenv("XFK_TRACE_CREATE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char *what)
+    {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[create] %-28s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
+}  // namespace
+
 namespace xfk {
 
 static thread_local std::string g_err;
@@ -489,6 +504,9 @@ int build_symbolic(xfk_problem *P)
     if (!P->harmonic) {
         XFK_CHECK(P->mu1b.alloc(NE));
         XFK_CHECK(P->mu2b.alloc(NE));
+        XFK_CHECK(P->asm_miss.alloc(1));
+        XFK_CHECK(hipMemsetAsync(P->asm_miss.p, 0, sizeof(int), s));
+        P->miss_checked = false;
     }
 
     // air-gap entries -> CSR slots (full storage: both triangles)
@@ -666,8 +684,10 @@ static int assemble(xfk_problem *P, int iter)
     A.n2e = P->n2e.p;
     A.rowptr = P->rowptr.p;
     A.col = P->col.p;
-    A.mu1_out = P->mu1b.p;
-    A.mu2_out = P->mu2b.p;
+    // (a linear problem never reads the permeability state back)
+    A.mu1_out = P->any_nonlinear ? P->mu1b.p : nullptr;
+    A.mu2_out = P->any_nonlinear ? P->mu2b.p : nullptr;
+    A.miss = P->asm_miss.p;
     launch_assemble_rows(s, P->NR, A);   // writes every entry of val and b (assembled rows)
     std::swap(P->mu1.p, P->mu1b.p);     // the state just written is read next iteration
     std::swap(P->mu1.n, P->mu1b.n);
@@ -1005,7 +1025,13 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
         }
         XFK_CHECK(hipGetLastError());
         XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(CgState), hipMemcpyDeviceToHost, s));
+        const bool miss_read = !P->miss_checked && P->asm_miss.p;   // the assembly's slot check, first poll
+        if (miss_read) XFK_CHECK(hipMemcpyAsync(P->hpin + 4, P->asm_miss.p, sizeof(int), hipMemcpyDeviceToHost, s));
         XFK_CHECK(hipStreamSynchronize(s));
+        if (miss_read) {
+            XFK_REQUIRE(P->hpin[4] == 0, XFK_ERR_HIP, "internal: element entry missing from the CSR pattern");
+            P->miss_checked = true;
+        }
         const CgState &S = *P->pcg_host;
         if (S.singular) {
             set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
@@ -1335,6 +1361,7 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
 int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *plan, int device,
                        xfk_comm *comm, xfk_problem **out)
 {
+    CreateTrace tr;
     xfk_problem *P = new xfk_problem();
     P->device = device;
     if (std::getenv("XFK_SPIN_WAIT")) {   // experiment: host waits spin instead of yielding
@@ -1351,6 +1378,7 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
         xfk_problem_destroy(P);
         return code;
     };
+    tr.mark("  device + stream");
     const int Ng = d->n_nodes, NEg = d->n_elems;
     const int N = plan ? plan->n_own : Ng;                  // owned rows
     const int NR = plan ? plan->n_own + plan->n_extra : Ng; // assembled rows (+ coupled nodes owned elsewhere)
@@ -1464,9 +1492,11 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
             P->age_val.push_back(G.age_val[m]);
         }
     }
+    tr.mark("  local mesh + BC arrays");
     int rc = build_pbc_map(P);
     if (rc != XFK_OK) return fail(rc);
     add_age_fill(P);
+    tr.mark("  periodic map + air-gap fill");
 
     hipStream_t s = P->stream;
     hipError_t e = hipSuccess;
@@ -1490,10 +1520,12 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     UP(P->fix_last, last.data(), last.size());
     UP(P->fix_rows, fix_rows.data(), fix_rows.size());
 #undef UP
+    tr.mark("  uploads enqueued");
     if (e == hipSuccess) e = hipHostMalloc((void **)&P->pcg_host, sizeof(CgState));
     if (e == hipSuccess) e = hipHostMalloc((void **)&P->hpin, 16 * sizeof(int));
     if (e == hipSuccess) e = hipHostMalloc((void **)&P->nws_host, sizeof(NewtonScalars));
     if (e == hipSuccess) e = hipStreamSynchronize(s);
+    tr.mark("  pinned mirrors + sync");
     if (e != hipSuccess) {
         set_error(std::string("upload failed: ") + hipGetErrorString(e));
         return fail(XFK_ERR_HIP);
@@ -1506,6 +1538,7 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     // created with it (a stream's creation is not work of the first solve)
     P->amg = new Amg();
     if (P->amg->sw.init() != XFK_OK) return fail(XFK_ERR_HIP);
+    tr.mark("  AMG side stream");
     *out = P;
     return XFK_OK;
 }
@@ -1518,16 +1551,22 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
 {
     XFK_REQUIRE(d && out, XFK_ERR_ARG, "null argument");
     *out = nullptr;
+    CreateTrace tr;
     int rc = validate_desc(d);
     if (rc == XFK_OK) rc = check_device(device);
     if (rc != XFK_OK) return rc;
+    tr.mark("validate + device");
     GlobalPrep G;
     prepare_global(d, G);
+    tr.mark("prepare_global");
     rc = prepare_magdir(d, G);
     if (rc != XFK_OK) return rc;
     rc = age_entries(d, 1.0, G.age_key, G.age_val);
     if (rc != XFK_OK) return rc;
-    return build_local(d, G, nullptr, device, nullptr, out);
+    tr.mark("magdir + air gaps");
+    rc = build_local(d, G, nullptr, device, nullptr, out);
+    tr.mark("build_local");
+    return rc;
 }
 
 int xfk_partition_plan(int n_nodes, int n_elems, const int *p, int rank, int nranks, xfk_dist_info *info,

@@ -433,8 +433,10 @@ __device__ __forceinline__ void row_regs_write(int v, int s, int ne, const RowCa
         }
 }
 
+// n2e_sort is rc.n2e itself (sorted in place, then read through rc.n2e): no
+// __restrict__ on it, so the reads below stay ordered after the sort's stores
 __global__ void __launch_bounds__(kBlock) k_row_len_reg(int N, RowCands rc, int *__restrict__ tmp,
-                                                        int *__restrict__ rowcnt, int *__restrict__ n2e_sort)
+                                                        int *__restrict__ rowcnt, int *n2e_sort)
 {
     __shared__ int s_c[kBlock * (kRowLds + 1)];
     const int v = blockIdx.x * kBlock + threadIdx.x;
@@ -1035,9 +1037,10 @@ __global__ void __launch_bounds__(kRowBlock) k_assemble_rows(int N, AssembleArgs
 {
     __shared__ double s_acc[kRowAcc * kRowBlock];
     __shared__ int s_col[kRowAcc * kRowBlock];
-    const int i = (XCD ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x) * kRowBlock + threadIdx.x;
-    if (i >= N) return;
-    const int rs = A.rowptr[i], L = A.rowptr[i + 1] - rs;
+    const int i0 = (XCD ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x) * kRowBlock;
+    const int i = i0 + threadIdx.x;
+    const bool live = i < N;   // (every thread reaches the barriers below)
+    const int rs = live ? A.rowptr[i] : 0, L = live ? A.rowptr[i + 1] - rs : 0;
     const bool lds = L <= kRowAcc;
     double *acc = lds ? s_acc + threadIdx.x : A.val + rs;
     const int stride = lds ? kRowBlock : 1;
@@ -1047,8 +1050,9 @@ __global__ void __launch_bounds__(kRowBlock) k_assemble_rows(int N, AssembleArgs
         if (lds) s_col[k * kRowBlock + threadIdx.x] = A.col[rs + k];
     }
     double bi = 0.;
-    const int t1 = A.n2e_ptr[i + 1];
-    for (int t = A.n2e_ptr[i]; t < t1; ++t) {
+    bool miss = false;
+    const int t1 = live ? A.n2e_ptr[i + 1] : 0;
+    for (int t = live ? A.n2e_ptr[i] : 0; t < t1; ++t) {
         const int e = A.n2e[t];
         const int n[3] = {A.p_raw[3 * e], A.p_raw[3 * e + 1], A.p_raw[3 * e + 2]};
         const int j = (n[0] == i) ? 0 : ((n[1] == i) ? 1 : 2);
@@ -1064,7 +1068,7 @@ __global__ void __launch_bounds__(kRowBlock) k_assemble_rows(int N, AssembleArgs
         if (AXI) axi_element<FIRST>(A.ebits_raw[e], A, n, X, Y, lab, bp, m1, m2, Me, be);
         else planar_element<FIRST>(A.ebits_raw[e], A, n, X, Y, lab, bp, m1, m2, Me, be);
         const int w = (n[0] < N) ? 0 : ((n[1] < N) ? 1 : 2);
-        if (w == j) {
+        if (w == j && A.mu1_out) {   // (linear problems keep no permeability state)
             A.mu1_out[e] = m1;
             A.mu2_out[e] = m2;
         }
@@ -1076,13 +1080,31 @@ __global__ void __launch_bounds__(kRowBlock) k_assemble_rows(int N, AssembleArgs
                                                              : ((k == 2) ? Me[2][2] : Me[k][2]));
             int pos = 0;
             while (pos < L - 1 && cols[pos * stride] != n[k]) ++pos;
+            miss |= cols[pos * stride] != n[k];
             acc[pos * stride] -= m;
         }
         bi -= (j == 0) ? be[0] : ((j == 1) ? be[1] : be[2]);
     }
-    if (lds)
+    if (miss && A.miss) *A.miss = 1;   // an element entry outside the row's pattern (read with the PCG's first poll)
+    // The block's rows are one contiguous run of val: when every row sat in
+    // LDS, the values are laid out linearly in LDS and written with
+    // consecutive lanes on consecutive entries (whole cache lines), instead of
+    // each lane storing its own row (64 partial lines per store).
+    if (__syncthreads_and(lds)) {
+        double r[kRowAcc];
+#pragma unroll
+        for (int k = 0; k < kRowAcc; ++k) r[k] = k < L ? s_acc[k * kRowBlock + threadIdx.x] : 0.;
+        const int rb0 = A.rowptr[i0], rb1 = A.rowptr[min(i0 + kRowBlock, N)];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kRowAcc; ++k)
+            if (k < L) s_acc[rs - rb0 + k] = r[k];
+        __syncthreads();
+        for (int m = threadIdx.x; m < rb1 - rb0; m += kRowBlock) A.val[rb0 + m] = s_acc[m];
+    } else if (lds) {
         for (int k = 0; k < L; ++k) A.val[rs + k] = s_acc[k * kRowBlock + threadIdx.x];
-    A.b[i] = bi;
+    }
+    if (live) A.b[i] = bi;
 }
 
 // point currents (static2d.cpp:818-825)

@@ -212,7 +212,7 @@ struct SideStream {
     int init();
     ~SideStream();
 };
-// XFK_NO_OVERLAP=1 turns the overlap off (exchange, then one launch)
+// off unless XFK_OVERLAP=1 (otherwise: exchange, then one launch over every tile)
 bool overlap_enabled();
 // exch(side stream) once the main stream's work so far is done; interior()
 // meanwhile on s; boundary() on s after the exchange
@@ -303,6 +303,8 @@ struct xfk_problem {
     xfk::DBuf<int> slot;             // colour order, 9 per element
     xfk::DBuf<double> mu1, mu2;      // element permeability state (colour order: harmonic; raw order: static)
     xfk::DBuf<double> mu1b, mu2b;    // static row-gather assembly: the state written by the current assembly
+    xfk::DBuf<int> asm_miss;         // static assembly: 1 when an element entry found no slot in its row
+    bool miss_checked = false;       // asm_miss read since the last symbolic build
 
     // boundary conditions
     xfk::DBuf<int> pt_nodes;         // nodes with a point current / fixed point value

@@ -24,7 +24,8 @@ struct AssembleArgs {
     // row-gather assembly (k_assemble_rows): raw-order element data, node ->
     // element lists, the CSR pattern, permeability state out (mu1 / mu2 in)
     const int *p_raw, *lbl_raw, *ebits_raw, *n2e_ptr, *n2e, *rowptr, *col;
-    double *mu1_out, *mu2_out;
+    double *mu1_out, *mu2_out;     // null: linear problem, no state kept
+    int *miss;                      // set to 1 when an element entry has no slot in its row
 };
 
 int grid_reduce(int N);
