@@ -146,6 +146,8 @@ typedef struct {
     double ms_rep_cycle;
     int rep_cycles;             /* V-cycles timed */
     double ms_rep_setup;
+    int prec_fallback;          /* 1: a stagnating PCG switched the AMG's f32 parts (level-0 transfers,
+                                   coarsest inverse) to f64 and restarted; kept for the problem's life */
 } xfk_result;
 
 typedef struct xfk_problem xfk_problem;

@@ -368,3 +368,54 @@ def test_amg_is_deterministic_through_newton_refreshes():
     assert r1["newton_iters"] >= 3
     assert r1["cg_iters"] == r2["cg_iters"] == r3["cg_iters"]
     assert np.array_equal(A1, A2) and np.array_equal(A1, A3)
+
+
+def test_high_contrast_f32_matches_f64_iterations():
+    """Steel at mu_r 1e4 with a thin air gap through the core, Precision
+    1e-10 (the coarse levels then carry condition numbers of 1e7 and more):
+    the f32 parts of the V-cycle -- level-0 transfers, and the coarsest
+    inverse rounded from its symmetrised unit-diagonal form -- need no more
+    PCG iterations than the f64 cycle (within 2), both answers meet parity
+    against the converged oracle, and no stagnation fallback is taken."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(160, mu_steel=1e4, precision=1e-10))
+    Ao, _, _ = oracle.solve(pr, mesh)
+    A32, r32, Ac = _solve_vs(kw, pr, mesh, precond="amg", amg_f32=True)
+    A64, r64 = _solve(kw, precond="amg", amg_f32=False)
+    print("mu_r 1e4, 1e-10: f32 %d, f64 %d PCG iterations" % (r32["cg_iters"], r64["cg_iters"]))
+    assert r32["prec_fallback"] == 0 and r64["prec_fallback"] == 0
+    assert r32["cg_iters"] <= r64["cg_iters"] + 2, (r32["cg_iters"], r64["cg_iters"])
+    assert rel_err(A32, Ac) <= TOL_LINEAR, parity_message(A32, Ao, Ac, TOL_LINEAR)
+    assert rel_err(A64, Ac) <= TOL_LINEAR, parity_message(A64, Ao, Ac, TOL_LINEAR)
+
+
+def test_dense_coarsest_high_contrast_f32():
+    """A 1600-row dense-coarsest matrix whose conductances span 1e12: the
+    f32 inverse (symmetrised, unit-diagonal scaled) still converges to the
+    direct solution within four PCG steps."""
+    rng = np.random.default_rng(4)
+    M = _laplace_random(40, 13)
+    d = np.exp(rng.uniform(-14, 14, M.shape[0]))        # diagonal similarity: cond up to ~1e12
+    M = (sp.diags(np.sqrt(d)) @ M @ sp.diags(np.sqrt(d))).tocsr()
+    b = rng.standard_normal(M.shape[0])
+    V, it, er = kernels.pcg_solve_csr(M.indptr, M.indices, M.data, b, precision=1e-12, precond="amg")
+    Vd = sla.spsolve(M.tocsc(), b)
+    assert it <= 4, it
+    assert rel_err(V, Vd) <= 1e-9
+
+
+def test_stagnation_falls_back_to_f64(monkeypatch):
+    """The stagnation guard (XFK_TEST_F64_FALLBACK forces it at the first
+    poll): the hierarchy is rebuilt with f64 transfers and an f64 coarsest
+    inverse, the PCG restarts from its iterate, the answer meets parity and
+    the fallback is reported (and kept for the problem's later solves)."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(120))
+    Ao, _, _ = oracle.solve(pr, mesh)
+    monkeypatch.setenv("XFK_TEST_F64_FALLBACK", "1")
+    P = kernels.Static2DProblem(**kw)
+    r = P.solve()
+    A = P.solution()
+    r2 = P.solve()
+    P.close()
+    Ac = converged(pr, mesh)
+    assert r["prec_fallback"] == 1 and r2["prec_fallback"] == 1
+    assert rel_err(A, Ac) <= TOL_LINEAR, parity_message(A, Ao, Ac, TOL_LINEAR)

@@ -93,3 +93,45 @@ def test_bad_function_is_refused_with_reference_text():
     kw = synth_to_oracle(magnet_problem("nil"))[2]
     with pytest.raises(kernels.XfkError, match='"nil" does not evaluate to a numerical value'):
         kernels.Static2DProblem(**kw)
+
+
+@pytest.mark.parametrize("nranks", [3])
+def test_functional_magnet_sharded(nranks):
+    """Sharded: each rank uploads only the per-element label entries its own
+    elements reference (renumbered); the answer is the single device's."""
+    import threading
+    kw = synth_to_oracle(magnet_problem("atan2(y-5,x-5)*180/PI"))[2]
+    P = kernels.Static2DProblem(**kw)
+    P.solve()
+    A1 = P.solution()
+    P.close()
+    comms = kernels.Comm.local_group(nranks)
+    probs = [kernels.Static2DProblem(**kw, comm=comms[q]) for q in range(nranks)]
+    out = [None] * nranks
+
+    def work(q):
+        probs[q].solve()
+        out[q] = probs[q].solution()
+
+    th = [threading.Thread(target=work, args=(q,)) for q in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for p in probs:
+        p.close()
+    for c in comms:
+        c.close()
+    for A in out:
+        assert A is not None and rel_err(A, A1) <= TOL
+
+
+def test_label_without_elements_is_not_evaluated():
+    """A MagDirFctn on a label that owns no element is never run by the
+    reference (it evaluates per assembled element), so even an expression that
+    would fail does not stop the problem."""
+    kw = magnet_problem("")
+    kw["labels"] = kw["labels"] + [dict(kw["labels"][0], mag_dir_fctn="theta +")]
+    P = kernels.Static2DProblem(**synth_to_oracle(kw)[2])
+    P.solve()
+    P.close()

@@ -117,3 +117,18 @@ def test_magdir_fixture_mesh_elements(tmp_path):
         got = kernels.magdir_eval(lb.MagDirFctn, np.asarray(mesh.p)[sel], mesh.x, mesh.y, pr.LengthUnits, lb.MagDir)
         assert len(sel) > 100
         assert np.array_equal(got.view(np.int64), ref[sel].view(np.int64)), lb.MagDirFctn
+
+
+@needs_lua
+@pytest.mark.parametrize("e", ['tonumber("5")*x', 'strlen("abc")*10', "getn({1,2})*x", "random()*0"])
+def test_magdir_unsupported_lua_is_named(e):
+    """Valid Lua the native evaluator does not restate (library functions,
+    tables): the reference evaluates it, the product refuses it with a
+    message naming the construct -- not a Lua error (INTEGRATION.md lists the
+    unsupported features)."""
+    p, x, y = mesh_sample(4)
+    ref = evaluate(oracle.ref_magdir, e, p, x, y, 0, 0.0)
+    assert not isinstance(ref, str), ref
+    got = evaluate(kernels.magdir_eval, e, p, x, y, 0, 0.0)
+    assert isinstance(got, str) and "not supported by the native expression evaluator" in got, got
+    assert "Lua error occurred" not in got

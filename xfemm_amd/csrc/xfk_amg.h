@@ -110,7 +110,12 @@ struct Amg {
     bool dense_coarse = false;
     DBuf<double> cinv;                // dense inverse of the coarsest level (row major, padded)
     int cinv_ld = 0;
-    DBuf<float> cinv_o;               // the inverse the V-cycle applies: unpermuted, unscaled, f32
+    DBuf<float> cinv_o;               // the inverse the V-cycle applies: unpermuted, symmetrised, scaled M (f32)
+    DBuf<double> cinv_o64;            // the same in f64 (prec32 == 0)
+    DBuf<double> cinv_sc;             // the scale S (original order): A_c^-1 = S M S
+    bool cinv_f64 = false;
+    // the hierarchy applies f32 values somewhere (level-0 transfers or the coarsest inverse)
+    bool f32_active() const { return (dense_coarse && !cinv_f64) || (!L.empty() && L[0]->has32); }
     const float *cinv_apply = nullptr;
     DBuf<int> cinv_perm, cinv_iperm, nd_tiles;
     DBuf<unsigned char> nd_mask;
@@ -145,6 +150,10 @@ struct Amg {
     DBuf<int> dev_int;                // small device scalars (undecided flag, overflow flags)
     std::map<int, int> cap_hint;      // SpGEMM slot capacity of each call site in the last setup
     std::map<int, int> mis_hint;      // MIS-2 rounds each level needed in the last setup
+    int row_max0 = 0;                 // longest row of the fine matrix (the caller's symbolic phase; 0: unknown)
+    // a fresh hierarchy (no setup yet): capacities and MIS rounds from the
+    // longest fine row instead of host-checked measurements
+    void seed_hints();
     DBuf<int> def_dev;                // deferred SpGEMM results: (overflow flag, length) pairs
     int *def_host = nullptr;          // pinned mirror
     int def_n = 0;

@@ -18,6 +18,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
 
 #include "xfk_amg.h"
 #include "xfk_comm.h"
@@ -1271,28 +1274,39 @@ __global__ void k_dense_scatter(int n, int ld, const int *__restrict__ rowptr, c
         M[(size_t)q * ld + c] += val[k] * sc[q] * sc[c];
     }
 }
-// nested-dissection order back to the coarse numbering, unscaled and
-// rounded to f32: out[iperm q][iperm r] = M[q][r] sc_q sc_r (out: n rows of
-// ldo, the padding columns n .. ldo-1 zero; iperm null: the identity), so
-// the V-cycle's apply streams plain f32 rows -- half the bytes of the
-// per-iteration coarse solve.  The coarsest inverse only preconditions: its
-// 2^-24 relative rounding keeps the V-cycle symmetric positive definite
-// (entries (i, j) and (j, i) of the inverse agree to far below an f32 ulp, so
-// they round alike) and changes no answer beyond the PCG's own tolerance.
+
+// The coarsest inverse the V-cycle applies, unpermuted: M is the inverse of
+// the unit-diagonal scaled level (S A_c S)^-1, so A_c^-1 = S M S; the apply
+// keeps S in f64 (osc, original order) and stores M symmetrised -- entries
+// (i, j) and (j, i) both from the one value (M_qr + M_rq) / 2, rounded once --
+// in f32 (V = float, the default: half the bytes of the per-iteration coarse
+// solve) or f64.  Rounding the scaled, symmetrised inverse keeps the coarse
+// correction exactly symmetric; the f32 perturbation is relative to the entries
+// of a unit-diagonal matrix's inverse (not of A_c^-1 itself, whose entries span
+// the coefficient contrast).  One 64 x 64 output tile per block, its mirror
+// tile read through LDS.
+template <class V>
 __global__ void __launch_bounds__(256) k_dense_unperm(int n, int ld, int ldo, const double *__restrict__ M,
                                                       const double *__restrict__ sc, const int *__restrict__ iperm,
-                                                      float *__restrict__ out)
+                                                      V *__restrict__ out, double *__restrict__ osc)
 {
-    const int q = blockIdx.x;
-    const int i = iperm ? iperm[q] : (q < n ? q : -1);
-    if (i < 0) return;
-    const double sq = sc[q];
-    float *o = out + (size_t)i * ldo;
-    for (int r = threadIdx.x; r < ld; r += blockDim.x) {
-        const int j = iperm ? iperm[r] : (r < n ? r : -1);
-        if (j >= 0) o[j] = (float)(M[(size_t)q * ld + r] * sq * sc[r]);
+    __shared__ double t[64][65];
+    const int bq = blockIdx.y * 64, br = blockIdx.x * 64;
+    for (int k = threadIdx.x; k < 64 * 64; k += 256) {   // t[a][b] = M[br + b][bq + a]
+        const int a = k & 63, b = k >> 6;
+        t[a][b] = M[(size_t)(br + b) * ld + bq + a];
     }
-    for (int c = n + threadIdx.x; c < ldo; c += blockDim.x) o[c] = 0.0f;
+    __syncthreads();
+    for (int k = threadIdx.x; k < 64 * 64; k += 256) {
+        const int a = k >> 6, b = k & 63, q = bq + a, r = br + b;
+        const int i = iperm ? iperm[q] : (q < n ? q : -1), j = iperm ? iperm[r] : (r < n ? r : -1);
+        if (i >= 0 && j >= 0) out[(size_t)i * ldo + j] = (V)(0.5 * (M[(size_t)q * ld + r] + t[a][b]));
+    }
+    if (blockIdx.x == 0)
+        for (int a = threadIdx.x; a < 64; a += 256) {
+            const int q = bq + a, i = iperm ? iperm[q] : (q < n ? q : -1);
+            if (i >= 0) osc[i] = sc[q];
+        }
 }
 
 __global__ void __launch_bounds__(1024) k_dense_maxdiag(int n, int ld, const double *__restrict__ M,
@@ -2252,21 +2266,39 @@ __global__ void __launch_bounds__(256) k_fold_pre(int n, int ncl, const int *__r
 // left a 1.6k-row inverse at 2.3 TB/s: 6 waves per CU, each walking its row
 // in dependent batches); products and sums in f64
 constexpr int kDmvLoads = 2;
-__global__ void __launch_bounds__(256) k_dense_mv(int n, int ld, const float *__restrict__ M,
-                                                  const double *__restrict__ b, double *__restrict__ x, const int *done)
+template <class V>
+struct DmvVec;
+template <>
+struct DmvVec<float> {
+    using T = float4;
+};
+template <>
+struct DmvVec<double> {
+    struct T {
+        double x, y, z, w;
+    };
+};
+// x = S M S b: row i of the symmetrised scaled inverse M (f32 or f64), the
+// scale osc in f64, products and sums in f64
+template <class V>
+__global__ void __launch_bounds__(256) k_dense_mv(int n, int ld, const V *__restrict__ M,
+                                                  const double *__restrict__ osc, const double *__restrict__ b,
+                                                  double *__restrict__ x, const int *done)
 {
     if (done && *done) return;
+    using V4 = typename DmvVec<V>::T;
     __shared__ double red[4];
     const int i = blockIdx.x;
-    const float4 *Mi = reinterpret_cast<const float4 *>(M + (size_t)i * ld);
+    const V4 *Mi = reinterpret_cast<const V4 *>(M + (size_t)i * ld);
     const int n4 = ld >> 2;
     double s0 = 0.0, s1 = 0.0;
     for (int j0 = 0; j0 < n4; j0 += 256 * kDmvLoads) {
-        float4 m[kDmvLoads];
+        V4 m[kDmvLoads];
 #pragma unroll
         for (int q = 0; q < kDmvLoads; ++q) {
             const int j = j0 + threadIdx.x + 256 * q;
-            m[q] = j < n4 ? Mi[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (j < n4) m[q] = Mi[j];
+            else m[q] = V4{0, 0, 0, 0};
         }
 #pragma unroll
         for (int q = 0; q < kDmvLoads; ++q) {
@@ -2274,19 +2306,21 @@ __global__ void __launch_bounds__(256) k_dense_mv(int n, int ld, const float *__
             if (c + 3 < n) {
                 const double2 b0 = *reinterpret_cast<const double2 *>(b + c);
                 const double2 b1 = *reinterpret_cast<const double2 *>(b + c + 2);
-                s0 += (double)m[q].x * b0.x + (double)m[q].z * b1.x;
-                s1 += (double)m[q].y * b0.y + (double)m[q].w * b1.y;
+                const double2 c0 = *reinterpret_cast<const double2 *>(osc + c);
+                const double2 c1 = *reinterpret_cast<const double2 *>(osc + c + 2);
+                s0 += (double)m[q].x * (c0.x * b0.x) + (double)m[q].z * (c1.x * b1.x);
+                s1 += (double)m[q].y * (c0.y * b0.y) + (double)m[q].w * (c1.y * b1.y);
             } else {
-                if (c < n) s0 += (double)m[q].x * b[c];
-                if (c + 1 < n) s1 += (double)m[q].y * b[c + 1];
-                if (c + 2 < n) s0 += (double)m[q].z * b[c + 2];
+                if (c < n) s0 += (double)m[q].x * (osc[c] * b[c]);
+                if (c + 1 < n) s1 += (double)m[q].y * (osc[c + 1] * b[c + 1]);
+                if (c + 2 < n) s0 += (double)m[q].z * (osc[c + 2] * b[c + 2]);
             }
         }
     }
     const double w = cg_wave_sum(s0 + s1);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
     __syncthreads();
-    if (threadIdx.x == 0) x[i] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x == 0) x[i] = osc[i] * ((red[0] + red[1]) + (red[2] + red[3]));
 }
 
 // diagnostics (XFK_AMG_DEBUG): rows left without an aggregate, split by
@@ -2809,10 +2843,50 @@ int build_tile_split(hipStream_t s, int n, int B, const int *rowptr, const int *
     return XFK_OK;
 }
 
+namespace {
+std::mutex g_pool_mu;
+std::map<hipStream_t, int> g_pool_dev;                 // every pooled stream -> its device
+std::map<int, std::vector<hipStream_t>> g_pool_free;   // idle streams per device
+}  // namespace
+
+hipError_t stream_acquire(hipStream_t *s)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        auto &f = g_pool_free[dev];
+        if (!f.empty()) {
+            *s = f.back();
+            f.pop_back();
+            return hipSuccess;
+        }
+    }
+    e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        g_pool_dev[*s] = dev;
+    }
+    return e;
+}
+
+void stream_release(hipStream_t s)
+{
+    if (!s) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto it = g_pool_dev.find(s);
+    if (it == g_pool_dev.end()) {
+        (void)hipStreamDestroy(s);
+        return;
+    }
+    g_pool_free[it->second].push_back(s);
+}
+
 int SideStream::init()
 {
     if (cs) return XFK_OK;
-    AMG_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    AMG_CHECK(stream_acquire(&cs));
     AMG_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
     AMG_CHECK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
     AMG_CHECK(hipEventCreateWithFlags(&c, hipEventDisableTiming));
@@ -2824,7 +2898,10 @@ SideStream::~SideStream()
     if (a) (void)hipEventDestroy(a);
     if (b) (void)hipEventDestroy(b);
     if (c) (void)hipEventDestroy(c);
-    if (cs) (void)hipStreamDestroy(cs);
+    if (cs) {
+        (void)hipStreamSynchronize(cs);
+        stream_release(cs);
+    }
 }
 
 // The folded coarse level that runs a W-cycle (two coarse corrections): by
@@ -3003,12 +3080,40 @@ int Amg::init(hipStream_t s)
     return XFK_OK;
 }
 
+// Capacities of a fresh hierarchy, a priori from the longest fine row m
+// (one int read with the pattern's length, no host check per product):
+//   P = (I - W D^-1 A_F) P_tent: one product per entry of A's row -- at most
+//     m on level 0 (exact), taken as 2m on coarse levels (their rows carry the
+//     neighbourhoods of ~9 merged fine rows: 12-20 entries for m = 7);
+//   A P: the P rows of the row's neighbours, 2-4 entries each: 4m on level
+//     0, 8m on coarse levels;  R (A P): 16m on level 0, the sort kernels'
+//     256 on coarse levels;
+//   MIS-2: 12 rounds per level (11-12 measured on configs[1] / configs[2]).
+// Products beyond a capacity are detected in the kernels and the hierarchy is
+// rebuilt with measured capacities (build's deferred check), so a bound that
+// is too small costs time, never correctness.  XFK_AMG_NO_SEED=1: measure.
+void Amg::seed_hints()
+{
+    static const bool off = std::getenv("XFK_AMG_NO_SEED") != nullptr;
+    if (off || row_max0 <= 0 || !cap_hint.empty() || !mis_hint.empty()) return;
+    auto cap = [](long long v) { return v <= 16 ? 16 : v <= 32 ? 32 : v <= 64 ? 64 : v <= 128 ? 128 : 256; };
+    const long long m = row_max0;
+    for (int l = 0; l < kAmgMaxLevels; ++l) {
+        const long long p = l == 0 ? m : 2 * m, ap = l == 0 ? 4 * m : 8 * m, rap = l == 0 ? 16 * m : 256;
+        if (p <= kSortCap) cap_hint[4 * l] = cap(p);
+        if (ap <= kSortCap) cap_hint[4 * l + 1] = cap(ap);
+        if (rap <= kSortCap) cap_hint[4 * l + 2] = cap(rap);
+        mis_hint[l] = 12;
+    }
+}
+
 int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *col0, const double *val0,
                long long nnz0)
 {
     dist = false;
     comm = nullptr;
     lrep = 0;
+    seed_hints();
     int rc = init(s);
     if (rc != XFK_OK) return rc;
     AmgLevel &F = *L[0];
@@ -3536,8 +3641,20 @@ int Amg::dense_inverse(hipStream_t s, const AmgLevel &C, int ld)
     }
     {
         const int ldo = ((C.n + kBj - 1) / kBj) * kBj;
-        AMG_CHECK(cinv_o.alloc((size_t)ldo * ldo));
-        k_dense_unperm<<<ld, 256, 0, s>>>(C.n, ld, ldo, cinv.p, sc, nd ? cinv_iperm.p : nullptr, cinv_o.p);
+        const dim3 g(ld / 64, ld / 64);
+        AMG_CHECK(cinv_sc.alloc((size_t)ldo));
+        cinv_f64 = !(prec32 < 0 ? f32_on() : prec32 != 0);   // (f64 transfers: the f64 inverse too)
+        if (cinv_f64) {
+            AMG_CHECK(cinv_o64.alloc((size_t)ldo * ldo));
+            AMG_CHECK(hipMemsetAsync(cinv_o64.p, 0, sizeof(double) * (size_t)ldo * ldo, s));   // (padding columns)
+            k_dense_unperm<double><<<g, 256, 0, s>>>(C.n, ld, ldo, cinv.p, sc, nd ? cinv_iperm.p : nullptr,
+                                                     cinv_o64.p, cinv_sc.p);
+        } else {
+            AMG_CHECK(cinv_o.alloc((size_t)ldo * ldo));
+            AMG_CHECK(hipMemsetAsync(cinv_o.p, 0, sizeof(float) * (size_t)ldo * ldo, s));
+            k_dense_unperm<float><<<g, 256, 0, s>>>(C.n, ld, ldo, cinv.p, sc, nd ? cinv_iperm.p : nullptr, cinv_o.p,
+                                                    cinv_sc.p);
+        }
         cinv_apply = cinv_o.p;
         cinv_ld = ldo;
     }
@@ -4316,8 +4433,14 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     if (l == M.nlev - 1) {
         double *dst = (l == 0) ? out0 : (yout ? yout : A.xa.p);
         if (M.dense_coarse) {
-            XFK_PHASE(lv + "dense inverse x b", 4.0 * A.n * M.cinv_ld + 8.0 * (M.cinv_ld + A.n),
-                      (k_dense_mv<<<A.n, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv_apply, b, dst, done)));
+            if (M.cinv_f64)
+                XFK_PHASE(lv + "dense inverse x b", 8.0 * A.n * M.cinv_ld + 8.0 * (2 * M.cinv_ld + A.n),
+                          (k_dense_mv<double><<<A.n, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv_o64.p, M.cinv_sc.p, b, dst,
+                                                                  done)));
+            else
+                XFK_PHASE(lv + "dense inverse x b", 4.0 * A.n * M.cinv_ld + 8.0 * (2 * M.cinv_ld + A.n),
+                          (k_dense_mv<float><<<A.n, 256, 0, s>>>(A.n, M.cinv_ld, M.cinv_apply, M.cinv_sc.p, b, dst,
+                                                                 done)));
             return dst;
         }
         // smoother-only coarsest level: 2 nu sweeps from zero

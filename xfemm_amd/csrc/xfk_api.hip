@@ -329,6 +329,7 @@ int xfk_resolve_nnz(xfk_problem *P)
     XFK_CHECK(hipEventSynchronize(P->nnz_ev));
     P->nnz = P->hpin[0];
     P->nnz_own = P->hpin[1];
+    P->row_max = P->hpin[5];
     P->nnz_pending = false;
     return XFK_OK;
 }
@@ -407,22 +408,40 @@ int build_symbolic(xfk_problem *P)
     XFK_CHECK(exclusive_scan(P, T.rowcnt, P->rowptr.p, N));
     XFK_CHECK(hipMemcpyAsync(P->hpin, P->rowptr.p + N, sizeof(int), hipMemcpyDeviceToHost, s));
     XFK_CHECK(hipMemcpyAsync(P->hpin + 1, P->rowptr.p + P->N, sizeof(int), hipMemcpyDeviceToHost, s));
+    // the longest row, read with the lengths: a fresh AMG hierarchy sizes its
+    // SpGEMM capacities from it (Amg::seed_hints) instead of measuring each
+    // product list behind a host check
+    P->hpin[5] = 0;
+    if (!P->harmonic && N > 0 && P->amg && P->amg->cap_hint.empty()) {
+        void *tmp = nullptr;
+        size_t bytes = 0;
+        XFK_CHECK(hipcub::DeviceReduce::Max(tmp, bytes, T.rowcnt, T.cnt + 3, N, s));
+        XFK_CHECK(cub_scratch(P, bytes, &tmp));
+        XFK_CHECK(hipcub::DeviceReduce::Max(tmp, bytes, T.rowcnt, T.cnt + 3, N, s));
+        XFK_CHECK(hipMemcpyAsync(P->hpin + 5, T.cnt + 3, sizeof(int), hipMemcpyDeviceToHost, s));
+    }
     // single-device static problems without air gaps or periodic maps read
     // the lengths back later (xfk_resolve_nnz, at the preconditioner setup):
     // the pattern is filled and the matrix assembled into arrays sized for
     // the bound 6 NE + N + fill-in (a triangle adds at most six off-diagonal
     // entries), with no host check in between
-    const bool defer = !P->harmonic && !P->comm && P->age_key.empty() && P->pbc_entry_key.empty();
+    // (deferred only while the bound's col / val stay within 512 MB: on larger
+    // meshes the one host check is negligible next to the memory the bound
+    // would hold, ~0.7 GB on the configs[4] mesh)
+    const long long bound_nnz = 6LL * NE + N + nfill;
+    const bool defer = !P->harmonic && !P->comm && P->age_key.empty() && P->pbc_entry_key.empty() &&
+                       bound_nnz * 12 <= (512LL << 20);
     long long cap_nnz;
     if (defer) {
         if (!P->nnz_ev) XFK_CHECK(hipEventCreateWithFlags(&P->nnz_ev, hipEventDisableTiming));
         XFK_CHECK(hipEventRecord(P->nnz_ev, s));
         P->nnz_pending = true;
-        cap_nnz = 6LL * NE + N + nfill;
+        cap_nnz = bound_nnz;
     } else {
         XFK_CHECK(hipStreamSynchronize(s));
         P->nnz = P->hpin[0];
         P->nnz_own = P->hpin[1];
+        P->row_max = P->hpin[5];
         P->nnz_pending = false;
         cap_nnz = P->nnz;
     }
@@ -813,6 +832,7 @@ static int amg_setup(xfk_problem *P)
     P->amg->col16 = P->amg_col16;
     P->amg->prec32 = P->amg_f32;
     P->amg->wlevel = P->amg_wlevel;
+    P->amg->row_max0 = P->row_max;
     // setup time: an event pair per setup, read after the solve's final
     // synchronisation (no host check here); callers that never read them
     // recycle the pairs; a full pool (> 64 fresh builds in one solve) is
@@ -989,7 +1009,14 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
     return pcg_precond_spmv(P, it, stamp);
 }
 
-static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
+// the f32 parts of the preconditioner (level-0 transfers, coarsest inverse)
+// are abandoned for f64 when the PCG stagnates: the iterate is not finite, or
+// after this many iterations the residual ratio is still above 1e-4 (a
+// V-cycle preconditioner reaches 1e-8 in 20-30 on the meshes measured)
+constexpr int kF32Guard = 150;
+constexpr int kRetryF64 = 1;   // (internal return code of pcg_solve_once)
+
+static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
 {
     hipStream_t s = P->stream;
     int rc = xfk_resolve_nnz(P);   // (the assembly is enqueued: no bubble)
@@ -1042,6 +1069,11 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
             set_error("PCG did not converge within the iteration cap");
             return XFK_ERR_NOCONV;
         }
+        // (S is the same on every rank: the decision is collective-safe)
+        const bool force = std::getenv("XFK_TEST_F64_FALLBACK") != nullptr;   // test hook (read per poll)
+        if (P->pc_used == XFK_PRECOND_AMG && P->amg && P->amg->f32_active() &&
+            (force || !std::isfinite(S.er) || (S.iters >= kF32Guard && S.er > 1e-4)))
+            return kRetryF64;
         // size the next batch from the observed convergence rate
         double rate = (S.iters > 0 && S.er > 0 && S.er < 1) ? std::log(S.er) / (double)S.iters : 0.0;
         long long rem = rate < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / rate) : 2 * batch;
@@ -1050,6 +1082,31 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
     }
     if (flag == 0) P->pcg_hint0 = (int)P->pcg_host->iters + 1;   // iteration it = iters detected the stop
     return XFK_OK;
+}
+
+static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
+{
+    int rc = pcg_solve_once(P, flag, max_iters);
+    if (rc != kRetryF64) return rc;
+    // f64 transfers and coarsest inverse for the rest of this problem's life,
+    // a fresh hierarchy, and the PCG restarted from the iterate (from zero if
+    // it is not finite)
+    const long long first = P->pcg_host->iters;
+    P->amg_f32 = 0;
+    P->f64_fallback = true;
+    P->amg_reusable = false;
+    int f2 = 1;
+    if (!std::isfinite(P->pcg_host->er)) {
+        XFK_CHECK(hipMemsetAsync(P->V.p, 0, sizeof(double) * P->NL, P->stream));
+        f2 = 0;
+    }
+    rc = pcg_solve_once(P, f2, max_iters);
+    if (rc == kRetryF64) {   // (cannot repeat: no f32 part is left)
+        set_error("internal: f64 fallback requested twice");
+        return XFK_ERR_HIP;
+    }
+    P->pcg_host->iters += first;
+    return rc;
 }
 
 }  // namespace xfk
@@ -1083,7 +1140,7 @@ void xfk_problem_destroy(xfk_problem *P)
     hipStream_t s = P->stream;
     delete P->amg;
     delete P;   // device buffers free themselves (DBuf), on this device
-    if (s) (void)hipStreamDestroy(s);
+    stream_release(s);   // (synchronised above; pooled for the next problem)
 }
 
 }  // extern "C"
@@ -1168,9 +1225,20 @@ int prepare_magdir(const xfk_problem_desc *d, GlobalPrep &G)
     std::vector<std::shared_ptr<const MagDirExpr>> ex(d->n_labels);
     bool any = false;
     std::string err;
+    // only labels that own elements: the reference runs the chunk while
+    // assembling an element, so a label without elements is never evaluated
+    std::vector<char> used(d->n_labels, 0), fctn(d->n_labels, 0);
+    bool any_fctn = false;
     for (int k = 0; k < d->n_labels; ++k) {
         const char *f = d->labels[k].mag_dir_fctn;
-        if (!f || !*f) continue;
+        fctn[k] = (f && *f) ? 1 : 0;
+        any_fctn |= fctn[k] != 0;
+    }
+    if (!any_fctn) return XFK_OK;
+    for (int i = 0; i < d->n_elems; ++i) used[d->lbl[i]] = 1;
+    for (int k = 0; k < d->n_labels; ++k) {
+        const char *f = d->labels[k].mag_dir_fctn;
+        if (!fctn[k] || !used[k]) continue;
         ex[k] = magdir_parse(f, err);
         XFK_REQUIRE(ex[k] != nullptr, XFK_ERR_ARG, err.c_str());
         any = true;
@@ -1369,7 +1437,7 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
         if (e == hipSuccess) e = hipSetDeviceFlags(hipDeviceScheduleSpin);
         std::fprintf(stderr, "[xfk] hipDeviceScheduleSpin: %s\n", hipGetErrorString(e));
     }
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || stream_acquire(&P->stream) != hipSuccess) {
         set_error("cannot initialise the HIP device/stream");
         delete P;
         return XFK_ERR_HIP;
@@ -1410,14 +1478,12 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
         P->l2g = plan->l2g;
     }
 
-    // local mesh
-    std::vector<double> x(NL), y(NL);
-    std::vector<int> g2l_tmp;
-    for (int l = 0; l < NL; ++l) {
-        x[l] = d->x[gnode(l)];
-        y[l] = d->y[gnode(l)];
-    }
-    std::vector<int> pl(3LL * NE), lbl(NE), ebits(NE);
+    // local mesh: a single device uploads the descriptor's (and the global
+    // preparation's) own arrays -- no host copies; a rank gathers its part
+    std::vector<double> xs, ys;
+    std::vector<int> pls, lbls, ebs;
+    const double *xp = d->x, *yp = d->y;
+    const int *plp = d->p, *lblp = G.elab.empty() ? d->lbl : G.elab.data(), *ebp = G.ebits.data();
     // global -> local: owned, or inside a receive range
     std::unordered_map<int, int> g2l_halo;
     if (plan)
@@ -1430,22 +1496,53 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
         return it == g2l_halo.end() ? -1 : it->second;
     };
     if (plan) {
+        xs.resize(NL);
+        ys.resize(NL);
+        for (int l = 0; l < NL; ++l) {
+            xs[l] = d->x[gnode(l)];
+            ys[l] = d->y[gnode(l)];
+        }
+        pls.resize(3LL * NE);
+        lbls.resize(NE);
+        ebs.resize(NE);
         for (int l = 0; l < NE; ++l) {
             const int e = gelem(l);
             for (int j = 0; j < 3; ++j) {
                 const int v = g2l(d->p[3LL * e + j]);
                 XFK_REQUIRE(v >= 0, fail(XFK_ERR_ARG), "internal: element node outside the local halo");
-                pl[3LL * l + j] = v;
+                pls[3LL * l + j] = v;
             }
+            lbls[l] = lblp[e];
+            ebs[l] = ebp[e];
         }
-    } else {
-        pl.assign(d->p, d->p + 3LL * NE);
+        xp = xs.data();
+        yp = ys.data();
+        plp = pls.data();
+        lblp = lbls.data();
+        ebp = ebs.data();
     }
-    for (int l = 0; l < NE; ++l) {
-        lbl[l] = G.elab.empty() ? d->lbl[gelem(l)] : G.elab[gelem(l)];
-        ebits[l] = G.ebits[gelem(l)];
+    // the label table: with MagDirFctn labels it holds one entry per element of
+    // such a label (prepare_magdir), so a rank uploads only the entries its
+    // elements reference, renumbered
+    std::vector<DevLabel> labs;
+    const DevLabel *labp = G.lab.data();
+    size_t nlab = G.lab.size();
+    if (plan && !G.elab.empty()) {
+        std::unordered_map<int, int> lmap;
+        for (int l = 0; l < NE; ++l) {
+            auto it = lmap.find(lbls[l]);
+            if (it == lmap.end()) {
+                it = lmap.emplace(lbls[l], (int)labs.size()).first;
+                labs.push_back(G.lab[lbls[l]]);
+            }
+            lbls[l] = it->second;
+        }
+        if (labs.empty()) labs.push_back(G.lab[0]);
+        labp = labs.data();
+        nlab = labs.size();
     }
-    P->hp = pl;
+    // host element nodes: only the periodic / air-gap maps read them
+    if (d->n_pbc || !G.age_key.empty()) P->hp.assign(plp, plp + 3LL * NE);
     if (d->n_pbc) {   // periodic pairs in local numbering (sharded: every coupled node is local)
         P->hpbc.assign(d->pbc, d->pbc + 3LL * d->n_pbc);
         for (int k = 0; k < d->n_pbc; ++k)
@@ -1459,12 +1556,22 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     }
 
     // boundary data of the local nodes (global values), owned rows only for rows
-    std::vector<unsigned char> fixed(NL);
-    std::vector<double> first(NL), last(NL);
-    for (int l = 0; l < NL; ++l) {
-        fixed[l] = G.fixed[gnode(l)];
-        first[l] = G.first[gnode(l)];
-        last[l] = G.last[gnode(l)];
+    std::vector<unsigned char> fxs;
+    std::vector<double> fsts, lsts;
+    const unsigned char *fixed = G.fixed.data();
+    const double *first = G.first.data(), *last = G.last.data();
+    if (plan) {
+        fxs.resize(NL);
+        fsts.resize(NL);
+        lsts.resize(NL);
+        for (int l = 0; l < NL; ++l) {
+            fxs[l] = G.fixed[gnode(l)];
+            fsts[l] = G.first[gnode(l)];
+            lsts[l] = G.last[gnode(l)];
+        }
+        fixed = fxs.data();
+        first = fsts.data();
+        last = lsts.data();
     }
     std::vector<int> pt_nodes, fix_rows;
     std::vector<double> pt_J;
@@ -1501,13 +1608,13 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     hipStream_t s = P->stream;
     hipError_t e = hipSuccess;
 #define UP(buf, ptr, n) if (e == hipSuccess) e = upload(buf, ptr, n, s)
-    UP(P->x, x.data(), (size_t)NL);
-    UP(P->y, y.data(), (size_t)NL);
-    UP(P->p_raw, pl.data(), 3 * (size_t)NE);
-    UP(P->lbl_raw, lbl.data(), (size_t)NE);
-    UP(P->ebits_raw, ebits.data(), (size_t)NE);
+    UP(P->x, xp, (size_t)NL);
+    UP(P->y, yp, (size_t)NL);
+    UP(P->p_raw, plp, 3 * (size_t)NE);
+    UP(P->lbl_raw, lblp, (size_t)NE);
+    UP(P->ebits_raw, ebp, (size_t)NE);
     UP(P->blocks, G.blk.data(), G.blk.size());
-    UP(P->labels, G.lab.data(), G.lab.size());
+    UP(P->labels, labp, nlab);
     UP(P->lines, G.lin.data(), G.lin.size());
     UP(P->circs, G.circ.data(), G.circ.size());
     UP(P->bhB, G.hB.data(), G.hB.size());
@@ -1515,9 +1622,9 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     UP(P->bhS, G.hS.data(), G.hS.size());
     UP(P->pt_nodes, pt_nodes.data(), pt_nodes.size());
     UP(P->pt_J, pt_J.data(), pt_J.size());
-    UP(P->fixed, fixed.data(), fixed.size());
-    UP(P->fix_first, first.data(), first.size());
-    UP(P->fix_last, last.data(), last.size());
+    UP(P->fixed, fixed, (size_t)NL);
+    UP(P->fix_first, first, (size_t)NL);
+    UP(P->fix_last, last, (size_t)NL);
     UP(P->fix_rows, fix_rows.data(), fix_rows.size());
 #undef UP
     tr.mark("  uploads enqueued");
@@ -1531,7 +1638,7 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
         return fail(XFK_ERR_HIP);
     }
     P->nblocks = d->n_blocks;
-    P->nlabels = (int)G.lab.size();
+    P->nlabels = (int)nlab;
     P->nlines = d->n_lines;
     P->ncircs = d->n_circs;
     // the AMG object and its setup side stream are resources of the problem,
@@ -1780,6 +1887,7 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
         if ((rc = P->amg->tail_read(R.ms_rep_cycle, R.rep_cycles, R.ms_rep_setup)) != XFK_OK) return rc;
         P->amg->time_tail = false;
     }
+    R.prec_fallback = P->f64_fallback ? 1 : 0;
     R.newton_iters = Iter;
     R.last_res = resn;
     R.nnz = P->nnz_own;
@@ -1967,7 +2075,7 @@ int xfk_pcg_solve_csr_pc(int n, const int *rowptr, const int *col, const double 
     P->precision = precision;
     P->precond = precond;
     int rc = XFK_OK;
-    hipError_t e = hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking);
+    hipError_t e = stream_acquire(&P->stream);
     // diagonal positions
     std::vector<int> diag(n, -1);
     for (int i = 0; i < n; ++i)

@@ -206,6 +206,11 @@ struct TileSplit {
 };
 // host-synchronising (once per operator)
 int build_tile_split(hipStream_t s, int n, int B, const int *rowptr, const int *col, TileSplit &ts);
+// Process-wide pool of non-blocking streams on the current device: creating a
+// HIP stream costs ~4 ms on MI355X (a hardware queue), so a problem returns its
+// streams here when it is destroyed and the next problem takes them back.
+hipError_t stream_acquire(hipStream_t *s);
+void stream_release(hipStream_t s);   // idle streams only (the caller synchronised it)
 struct SideStream {
     hipStream_t cs = nullptr;
     hipEvent_t a = nullptr, b = nullptr, c = nullptr;
@@ -245,6 +250,7 @@ struct xfk_problem {
     int NR = 0;
     long long nnz = 0;       // entries of the assembled rows (NR)
     long long nnz_own = 0;   // entries of the owned rows (N): the solved matrix
+    int row_max = 0;         // longest assembled row (0: not measured; read with the lengths)
     int ncolors = 0;
     std::vector<int> color_off;      // ncolors + 1 (host)
 
@@ -378,6 +384,7 @@ struct xfk_problem {
     int amg_col16 = -1;               // XFK_OPT_AMG_COL16 (-1: on unless XFK_NO_COL16)
     int amg_wlevel = -2;              // XFK_OPT_AMG_WLEVEL (-2: the default level)
     int amg_f32 = -1;                 // XFK_OPT_AMG_F32 (-1: on unless XFK_AMG_F32=0)
+    bool f64_fallback = false;        // a stagnating PCG switched the f32 parts of the AMG to f64 (sticky)
     int amg_reuse = 1;
     bool amg_reusable = false;        // the hierarchy belongs to this solve's matrix pattern
     bool amg_fresh = false;           // built from scratch for the running PCG solve

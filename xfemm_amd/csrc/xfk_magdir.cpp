@@ -16,9 +16,10 @@
 //   * the complex number of the xfemm Lua (femmcomplex.cpp), operation by
 //     operation as the C++ overloads resolve there, and the math library
 //     lmathlib.cpp registers (radians; PI, I globals; pow as the ^ tag method).
-// Not supported (the parser refuses them with the reference's error text):
-// strings and `..`, tables, anonymous functions, upvalues, method calls,
-// base-library functions, and random / randomseed (not reproducible).
+// Not supported (refused with a message naming the construct, not a Lua
+// error): tables, field access and indexing, anonymous functions, upvalues,
+// method calls, '...', and the base / string / I/O library functions,
+// random / randomseed included (not reproducible).
 #include "xfk_magdir.h"
 
 #include <cctype>
@@ -315,11 +316,17 @@ struct Parser {
     double num = 0;
     std::string name, str;
     bool ok = true;
+    std::string unsup;   // a construct the reference's Lua accepts and this evaluator does not
     MagDirExpr *E;
 
     explicit Parser(const char *text, MagDirExpr *e) : s(text), E(e) { next(); }
 
     void fail() { ok = false; tok = T_BAD; }
+    void unsupported(const std::string &what)
+    {
+        if (unsup.empty()) unsup = what;
+        fail();
+    }
 
     void next()
     {
@@ -384,7 +391,7 @@ struct Parser {
             return;
         case '.':   // '..' (a lone '.', field access, and '...' are not supported)
             if (d == '.' && s[pos + 1] != '.') { ++pos; tok = T_CONCAT; }
-            else fail();
+            else unsupported(d == '.' ? "'...' (variable arguments)" : "field access ('.')");
             return;
         case '"':
         case '\'':   // read_string (llex.cpp:261-352)
@@ -419,7 +426,7 @@ struct Parser {
             tok = T_STR;
             return;
         case '[':   // [[long string]] (llex.cpp:212-258)
-            if (d != '[') { fail(); return; }
+            if (d != '[') { unsupported("table indexing ('[')"); return; }
             {
                 ++pos;
                 int cont = 0;
@@ -441,7 +448,10 @@ struct Parser {
             }
             tok = T_STR;
             return;
-        default:   // tables, '%', '#', ':', ... : not supported
+        case '{': case '}': unsupported("tables ('{ }')"); return;
+        case '%': unsupported("upvalues ('%')"); return;
+        case ':': unsupported("method calls (':')"); return;
+        default:   // not a Lua 4 token either: the reference's lexer refuses it too
             fail();
             return;
         }
@@ -529,6 +539,24 @@ struct Parser {
                 if (nm == gl[g]) { n.k = K_GLOBAL; n.op = g; }
             for (int f = 0; f < F_COUNT && n.k == K_UNDEF; ++f)
                 if (nm == kBuiltinNames[f]) { n.k = K_FN; n.op = f; }
+            if (n.k == K_UNDEF && tok == '(') {
+                // functions of the reference Lua's base, string and math
+                // libraries this evaluator does not restate (lbaselib.cpp,
+                // lstrlib.cpp, lmathlib.cpp random / randomseed)
+                static const char *const lib[] = {
+                    "assert", "call", "collectgarbage", "copytagmethods", "dofile", "dostring", "error", "foreach",
+                    "foreachi", "getglobal", "getn", "gettagmethod", "globals", "newtag", "next", "print", "rawget",
+                    "rawset", "setglobal", "settag", "settagmethod", "sort", "tag", "tinsert", "tonumber",
+                    "tostring", "tremove", "type", "strlen", "strsub", "strlower", "strupper", "strchar", "strrep",
+                    "ascii", "strbyte", "format", "strfind", "gsub", "random", "randomseed", "rawgettable",
+                    "rawsettable", "read", "write", "date", "clock", "getenv", "execute", "remove", "rename",
+                    "tmpname", "exit", "openfile", "closefile", "readfrom", "writeto", "appendto", "flush", "seek"};
+                for (const char *f : lib)
+                    if (nm == f) {
+                        unsupported("the library function " + nm + "()");
+                        return -1;
+                    }
+            }
             int id = add(n);
             while (ok && tok == '(') {   // call suffix: f(args)
                 next();
@@ -550,7 +578,8 @@ struct Parser {
             }
             return id;
         }
-        fail();   // strings, tables, functions, upvalues: "<expression> expected" or unsupported
+        if (tok == T_KEYWORD && name == "function") unsupported("anonymous functions");
+        else fail();   // "<expression> expected"
         return -1;
     }
 
@@ -821,6 +850,7 @@ std::shared_ptr<const MagDirExpr> magdir_parse(const std::string &fctn, std::str
     Parser P(fctn.c_str(), E.get());
     // retstat (lparser.cpp): an optional expression list unless the block ends
     // or ';' follows, then an optional ';' and the end of the chunk
+    if (P.tok == T_KEYWORD && P.name == "function") P.unsupported("anonymous functions");
     if (P.ok && P.tok != T_EOS && P.tok != ';' && P.tok != T_KEYWORD) {
         for (;;) {
             const int e = P.expr();
@@ -831,6 +861,11 @@ std::shared_ptr<const MagDirExpr> magdir_parse(const std::string &fctn, std::str
         }
     }
     if (P.ok && P.tok == ';') P.next();
+    if (!P.unsup.empty()) {   // valid Lua the native evaluator does not restate: say so
+        err = "MagDirFctn \"" + fctn + "\": " + P.unsup +
+              " not supported by the native expression evaluator (the reference's Lua would evaluate it)";
+        return nullptr;
+    }
     if (!P.ok || P.tok != T_EOS) {
         err = quoted("Lua error occurred when evaluating:\n\"%s\"", fctn);   // static2d.cpp:550-552
         return nullptr;

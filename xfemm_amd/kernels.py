@@ -112,7 +112,7 @@ class Result(C.Structure):
                 ("spmv_ms_avg", C.c_double), ("spmv_samples", C.c_int),
                 ("color_rounds", C.c_int), ("precond", C.c_int), ("amg_levels", C.c_int),
                 ("amg_op_complexity", C.c_double), ("ms_amg_setup", C.c_double), ("ms_rep_cycle", C.c_double),
-                ("rep_cycles", C.c_int), ("ms_rep_setup", C.c_double)]
+                ("rep_cycles", C.c_int), ("ms_rep_setup", C.c_double), ("prec_fallback", C.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
