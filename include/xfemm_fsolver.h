@@ -57,6 +57,11 @@ int xfemm_fsolver_num_elements(xfemm_fsolver *s);
 int xfemm_fsolver_get_solution(xfemm_fsolver *s, double *x, double *y, double *A);
 int xfemm_fsolver_get_elements(xfemm_fsolver *s, int *p, int *lbl);
 int xfemm_fsolver_get_stats(xfemm_fsolver *s, xfk_result *out);
+/* Wall milliseconds of the last runSolver (fsolver.cpp:1213-1340 is the
+ * reference's sequence): ms[0] LoadMesh, ms[1] Cuthill-McKee, ms[2] problem
+ * creation (descriptor, host -> HBM upload), ms[3] solve (device work and the
+ * solution read-back), ms[4] .ans write. */
+int xfemm_fsolver_get_times(xfemm_fsolver *s, double *ms);
 const char *xfemm_fsolver_last_error(xfemm_fsolver *s);
 
 /* femmcli's binding (cfemm/femmcli/LuaMagneticsCommands.cpp:817-842, mi_analyze):

@@ -419,3 +419,23 @@ def test_stagnation_falls_back_to_f64(monkeypatch):
     Ac = converged(pr, mesh)
     assert r["prec_fallback"] == 1 and r2["prec_fallback"] == 1
     assert rel_err(A, Ac) <= TOL_LINEAR, parity_message(A, Ao, Ac, TOL_LINEAR)
+
+
+def test_newton_refresh_refolds_level0(monkeypatch):
+    """A Newton refresh keeps level 0 folded: P~ = (I - w D^-1 A) P re-formed
+    numerically for the new matrix over its own pattern (k_refold_p).  The
+    answer meets the nonlinear parity tolerance, is deterministic, and needs
+    no more PCG iterations than the unfolded refresh (XFK_AMG_REFOLD=0) plus
+    one per Newton step."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(80, nonlinear=True))
+    Ao, _, _ = oracle.solve(pr, mesh)
+    A1, r1, Ac = _solve_vs(kw, pr, mesh, precond="amg")
+    A1b, _ = _solve(kw, precond="amg")
+    monkeypatch.setenv("XFK_AMG_REFOLD", "0")
+    A0, r0 = _solve(kw, precond="amg")
+    print("refold: %d PCG / %d Newton; unfolded refresh: %d / %d"
+          % (r1["cg_iters"], r1["newton_iters"], r0["cg_iters"], r0["newton_iters"]))
+    assert rel_err(A1, Ac) <= TOL_NONLINEAR, parity_message(A1, Ao, Ac, TOL_NONLINEAR)
+    assert rel_err(A0, Ac) <= TOL_NONLINEAR
+    assert np.array_equal(A1.view(np.int64), A1b.view(np.int64))
+    assert r1["cg_iters"] <= r0["cg_iters"] + r1["newton_iters"], (r1["cg_iters"], r0["cg_iters"])

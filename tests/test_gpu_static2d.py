@@ -137,6 +137,16 @@ def test_file_interface_end_to_end(tmp_path):
         assert ans.circ[k] == exp
     txt = open(base + ".ans").read()
     assert txt.startswith(open(os.path.join(GOLDEN, "Temp.fem")).read())
+    # the node / element sections are printf's "%.17g" / "%i" text (the writer
+    # formats them with std::to_chars in parallel chunks): byte for byte
+    sol = txt.split("[Solution]\n", 1)[1].split("\n")
+    nn = int(sol[0])
+    for i in range(nn):
+        x, y, a, m = sol[1 + i].split("\t")
+        assert sol[1 + i] == "%.17g\t%.17g\t%.17g\t%d" % (float(x), float(y), float(a), int(m)), sol[1 + i]
+    ne = int(sol[1 + nn])
+    for i in range(ne):
+        assert sol[2 + nn + i] == "%d\t%d\t%d\t%d" % tuple(int(v) for v in sol[2 + nn + i].split("\t"))
 
 
 def test_solve_is_deterministic():

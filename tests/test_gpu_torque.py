@@ -54,6 +54,8 @@ def _check(base, deg):
     ok, diff, rel = torque_ok(tq, deg)
     assert ok, "GPU torque %.7f at %d deg: diff %.3e (%.4f %%); oracle %.7f" % (tq, deg, diff, rel, tq_ref)
     assert abs(tq - tq_ref) <= 1e-6, (tq, tq_ref)
+    print("TorqueBenchmark %d deg: %d nodes, %d PCG iterations, torque %.7f" % (deg, len(mesh.x), st["cg_iters"], tq))
+    assert st["cg_iters"] <= 40, st["cg_iters"]   # one linear solve (AMG-PCG to 1e-8)
     return st
 
 

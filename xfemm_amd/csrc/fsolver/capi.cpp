@@ -144,6 +144,13 @@ int xfemm_fsolver_get_stats(xfemm_fsolver *h, xfk_result *out)
     return 1;
 }
 
+int xfemm_fsolver_get_times(xfemm_fsolver *h, double *ms)
+{
+    if (!h || !ms) return 0;
+    for (int k = 0; k < 5; ++k) ms[k] = h->s.ms_phase[k];
+    return 1;
+}
+
 const char *xfemm_fsolver_last_error(xfemm_fsolver *h) { return h ? h->s.lastError.c_str() : ""; }
 
 int xfemm_fsolver_set_previous_solution_file(xfemm_fsolver *h, const char *path)

@@ -1,13 +1,17 @@
 // FSolver host logic over the MI355X kernels (see fsolver.h).
 #include "fsolver.h"
 
+#include <algorithm>
 #include <cctype>
+#include <charconv>
+#include <chrono>
 #include <complex>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <utility>
 
 namespace xfemm {
@@ -197,7 +201,6 @@ bool FSolver::loadPreviousSolution(bool loadAprev)
         for (int q = 0; q < 3; q++)
             if (elm.p[q] < 0 || elm.p[q] >= NumNodes) return fail("element node");
         elm.blk = labellist[elm.lbl].BlockType;
-        meshele[i] = elm;
     }
     // block-label circuit lines: skipped
     int numLabels = 0;
@@ -252,36 +255,219 @@ bool FSolver::loadPreviousSolution(bool loadAprev)
     return true;
 }
 
+namespace {
+// XFEMM_TRACE_LOAD=1: host milliseconds of the mesh-loading / renumbering stages on stderr
+struct LoadTrace {
+    bool on = std::getenv("XFEMM_TRACE_LOAD") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char *what)
+    {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[load] %-24s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
+
+// Token readers with fscanf's semantics: "%i" (strtol base 0: decimal, 0x..,
+// leading-0 octal) and "%lf" (strtod).  Digit strings take a direct decimal
+// path (the value strtol gives); everything else goes through strtol /
+// strtod, so every value is the reference's fscanf value to the bit.  `nl`:
+// the token must lie on the current line (line-parallel parsing).
+inline bool ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n' || c == '\v' || c == '\f'; }
+inline bool skip_ws(const char *&p, bool nl)
+{
+    if (nl) {
+        while (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\v' || *p == '\f') ++p;
+        return *p && *p != '\n';
+    }
+    while (ws(*p)) ++p;
+    return *p != 0;
+}
+inline bool read_int(const char *&p, int &v, bool nl)
+{
+    if (!skip_ws(p, nl)) return false;
+    const char *q = p + (*p == '-' || *p == '+');
+    if (*q >= '1' && *q <= '9') {   // plain decimal (no octal / hex prefix)
+        long long a = 0;
+        const char *r = q;
+        while (*r >= '0' && *r <= '9' && r - q < 18) a = 10 * a + (*r++ - '0');
+        if (!(*r >= '0' && *r <= '9') && a <= 2147483648LL) {
+            v = (int)(*p == '-' ? -a : a);
+            p = r;
+            return true;
+        }
+    }
+    char *end = nullptr;
+    const long x = std::strtol(p, &end, 0);
+    if (end == p) return false;
+    v = (int)x;
+    p = end;
+    return true;
+}
+inline bool read_double(const char *&p, double &v, bool nl)
+{
+    if (!skip_ws(p, nl)) return false;
+    char *end = nullptr;
+    v = std::strtod(p, &end);
+    if (end == p) return false;
+    p = end;
+    return true;
+}
+
+// [0, n) split over the host's cores (at most 16), f(begin, end) per part
+template <class F>
+void par_for(long long n, long long min_per_thread, F f)
+{
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int T = (int)std::max<long long>(1, std::min<long long>({(long long)std::min(hw, 16u), n / std::max(1LL, min_per_thread)}));
+    if (T <= 1) {
+        f(0LL, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back([&, t] { f(n * t / T, n * (t + 1) / T); });
+    f(0LL, n / T);
+    for (auto &x : th) x.join();
+}
+
+// A whole mesh file in memory, read as the token stream fscanf sees.
+struct TextBuf {
+    std::vector<char> d;
+    size_t pos = 0;
+    bool load(const std::string &path)
+    {
+        FILE *fp = fopen(path.c_str(), "rb");
+        if (!fp) return false;
+        std::fseek(fp, 0, SEEK_END);
+        const long n = std::ftell(fp);
+        std::fseek(fp, 0, SEEK_SET);
+        d.resize((size_t)std::max(0L, n) + 1);
+        const size_t got = n > 0 ? std::fread(d.data(), 1, (size_t)n, fp) : 0;
+        std::fclose(fp);
+        d.resize(got + 1);
+        d[got] = '\0';
+        pos = 0;
+        return true;
+    }
+    bool next_int(int &v)
+    {
+        const char *p = d.data() + pos;
+        if (!read_int(p, v, false)) return false;
+        pos = (size_t)(p - d.data());
+        return true;
+    }
+    // the first line's leading integer (fgets + sscanf "%i"), then the stream after that line
+    bool header_int(int &v)
+    {
+        const char *nl = std::strchr(d.data(), '\n');
+        std::string line(d.data(), nl ? (size_t)(nl - d.data()) : std::strlen(d.data()));
+        pos = nl ? (size_t)(nl - d.data()) + 1 : d.size() - 1;
+        return std::sscanf(line.c_str(), "%i", &v) == 1;
+    }
+    // `count` records from pos on, rec(p, index, nl) reading one record.
+    // When every record sits on a line of its own (fmesher's layout) the lines
+    // are parsed in parallel chunks -- the same values as the token stream;
+    // any other layout (a record over several lines, extra tokens on a line)
+    // is parsed as one sequential token stream, as fscanf reads it.
+    template <class Rec>
+    bool records(int count, Rec rec)
+    {
+        const char *base = d.data() + pos, *end = d.data() + d.size() - 1;
+        const long long len = end - base;
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const int T = (int)std::max<long long>(1, std::min<long long>(std::min(hw, 16u), len / (1 << 20)));
+        bool ok = T > 1;
+        if (ok) {
+            // chunk starts at line starts; records (non-blank lines) per chunk
+            std::vector<const char *> cs(T + 1);
+            cs[0] = base;
+            cs[T] = end;
+            for (int t = 1; t < T; ++t) {
+                const char *q = base + len * t / T;
+                while (q < end && q[-1] != '\n') ++q;
+                cs[t] = std::max(q, cs[t - 1]);
+            }
+            std::vector<long long> cnt(T + 1, 0);
+            par_for(T, 1, [&](long long a, long long b) {
+                for (long long t = a; t < b; ++t) {
+                    long long c = 0;
+                    bool blank = true;
+                    for (const char *q = cs[t]; q < cs[t + 1]; ++q) {
+                        if (*q == '\n') {
+                            c += !blank;
+                            blank = true;
+                        } else if (!ws(*q)) {
+                            blank = false;
+                        }
+                    }
+                    cnt[t + 1] = c + !blank;
+                }
+            });
+            for (int t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+            ok = cnt[T] >= count;
+            std::vector<char> good(T, 1);
+            if (ok)
+                par_for(T, 1, [&](long long a, long long b) {
+                    for (long long t = a; t < b; ++t) {
+                        long long k = cnt[t];
+                        const char *q = cs[t];
+                        while (q < cs[t + 1] && k < count) {
+                            const char *p = q;
+                            if (!skip_ws(p, true)) {   // blank line
+                                q = p + (*p == '\n');
+                                continue;
+                            }
+                            if (!rec(p, (int)k, true) || skip_ws(p, true)) {   // short record or extra tokens
+                                good[t] = 0;
+                                return;
+                            }
+                            ++k;
+                            q = p + (*p == '\n');
+                        }
+                    }
+                });
+            for (char g : good) ok = ok && g;
+        }
+        if (!ok) {   // the token stream, sequentially
+            const char *p = base;
+            for (int k = 0; k < count; ++k)
+                if (!rec(p, k, false)) return false;
+        }
+        return true;
+    }
+};
+}  // namespace
+
 LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
 {
     if (meshLoadedFromPrevSolution) return NOERROR;   // fsolver.cpp:357-360
+    LoadTrace tr;
     char s[1024];
     std::string infile = PathName + ".node";
-    FILE *fp = fopen(infile.c_str(), "rt");
-    if (!fp) return BADNODEFILE;
+    TextBuf tb;
+    if (!tb.load(infile)) return BADNODEFILE;
     int k = 0, j = 0;
-    if (!fgets(s, 1024, fp) || sscanf(s, "%i", &k) != 1) {
-        fclose(fp);
-        return BADNODEFILE;
-    }
+    if (!tb.header_int(k)) return BADNODEFILE;
     NumNodes = k;
     meshnode.assign(k, CNode());
     const double conv = 100 * kLengthConvMeters[LengthUnits];
-    for (int i = 0; i < k; i++) {
-        CNode node;
-        if (fscanf(fp, "%i %lf %lf %i", &j, &node.x, &node.y, &j) != 4) {
-            fclose(fp);
-            return BADNODEFILE;
-        }
-        node.BoundaryMarker = (j > 1) ? j - 2 : -1;
-        node.x *= conv;   // lengths in cm (fsolver.cpp:386-388)
-        node.y *= conv;
-        meshnode[i] = node;
-    }
-    fclose(fp);
+    if (!tb.records(k, [&](const char *&p, int i, bool nl) {
+            int a, m;
+            CNode &node = meshnode[i];
+            if (!read_int(p, a, nl) || !read_double(p, node.x, nl) || !read_double(p, node.y, nl) ||
+                !read_int(p, m, nl))
+                return false;
+            node.BoundaryMarker = (m > 1) ? m - 2 : -1;
+            node.x *= conv;   // lengths in cm (fsolver.cpp:386-388)
+            node.y *= conv;
+            return true;
+        }))
+        return BADNODEFILE;
+    tr.mark("nodes");
 
     infile = PathName + ".pbc";
-    fp = fopen(infile.c_str(), "rt");
+    FILE *fp = fopen(infile.c_str(), "rt");
     if (!fp) return BADPBCFILE;
     NumPBCs = 0;
     if (fgets(s, 1024, fp)) sscanf(s, "%i", &NumPBCs);
@@ -326,12 +512,8 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
     fclose(fp);
 
     infile = PathName + ".ele";
-    fp = fopen(infile.c_str(), "rt");
-    if (!fp) return BADELEMENTFILE;
-    if (!fgets(s, 1024, fp) || sscanf(s, "%i", &k) != 1) {
-        fclose(fp);
-        return BADELEMENTFILE;
-    }
+    if (!tb.load(infile)) return BADELEMENTFILE;
+    if (!tb.header_int(k)) return BADELEMENTFILE;
     NumEls = k;
     meshele.assign(k, CMElement());
     int defaultLabel = -1;
@@ -340,74 +522,72 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
     auto remove_files = [&]() {
         for (const char *ext : {".ele", ".node", ".pbc", ".poly", ".edge"}) remove((PathName + ext).c_str());
     };
+    if (!tb.records(k, [&](const char *&p, int i, bool nl) {
+            int a;
+            CMElement &elm = meshele[i];
+            return read_int(p, a, nl) && read_int(p, elm.p[0], nl) && read_int(p, elm.p[1], nl) &&
+                   read_int(p, elm.p[2], nl) && read_int(p, elm.lbl, nl);
+        }))
+        return BADELEMENTFILE;
     for (int i = 0; i < k; i++) {
-        CMElement elm;
-        if (fscanf(fp, "%i %i %i %i %i", &j, &elm.p[0], &elm.p[1], &elm.p[2], &elm.lbl) != 5) {
-            fclose(fp);
-            return BADELEMENTFILE;
-        }
+        CMElement &elm = meshele[i];
         elm.lbl--;
         if (elm.lbl < 0) elm.lbl = defaultLabel;
         if (elm.lbl < 0) {
             char buf[256];
             snprintf(buf, sizeof buf, "The element number %i had label %i\n", i, elm.lbl);
             warn(std::string("Material properties have not been defined for all regions.\n") + buf);
-            fclose(fp);
             if (deleteFiles) remove_files();
             return MISSINGMATPROPS;
         }
         if (elm.lbl >= (int)labellist.size()) {
-            fclose(fp);
             if (deleteFiles) remove_files();
             return ELMLABELTOOBIG;
         }
         for (int q = 0; q < 3; q++)
-            if (elm.p[q] < 0 || elm.p[q] >= NumNodes) {
-                fclose(fp);
-                return BADELEMENTFILE;
-            }
+            if (elm.p[q] < 0 || elm.p[q] >= NumNodes) return BADELEMENTFILE;
         elm.blk = labellist[elm.lbl].BlockType;
-        meshele[i] = elm;
     }
-    fclose(fp);
+    tr.mark("elements");
 
-    // node -> element membership (fsolver.cpp:628-657)
-    std::vector<std::vector<int>> mbr(NumNodes);
+    // node -> element membership (fsolver.cpp:628-657), as CSR
+    std::vector<int> mptr(NumNodes + 1, 0), mbr(3 * (size_t)NumEls);
     for (int i = 0; i < NumEls; i++)
-        for (int q = 0; q < 3; q++) mbr[meshele[i].p[q]].push_back(i);
-
-    infile = PathName + ".edge";
-    fp = fopen(infile.c_str(), "rt");
-    if (!fp) return BADEDGEFILE;
-    int nedge = 0, flag = 0;
-    if (fscanf(fp, "%i", &nedge) != 1 || fscanf(fp, "%i", &flag) != 1) {
-        fclose(fp);
-        return BADEDGEFILE;
+        for (int q = 0; q < 3; q++) mptr[meshele[i].p[q] + 1]++;
+    for (int v = 0; v < NumNodes; v++) mptr[v + 1] += mptr[v];
+    {
+        std::vector<int> cur(mptr.begin(), mptr.end() - 1);
+        for (int i = 0; i < NumEls; i++)
+            for (int q = 0; q < 3; q++) mbr[cur[meshele[i].p[q]]++] = i;
     }
-    edges_.clear();
-    edges_.reserve(nedge);
+
+    tr.mark("membership");
+    infile = PathName + ".edge";
+    if (!tb.load(infile)) return BADEDGEFILE;
+    int nedge = 0, flag = 0;
+    if (!tb.next_int(nedge) || !tb.next_int(flag)) return BADEDGEFILE;
+    edges_.assign(std::max(0, nedge), {0, 0, 0});
+    if (nedge > 0 && !tb.records(nedge, [&](const char *&p, int i, bool nl) {
+            int a;
+            auto &e = edges_[i];
+            return read_int(p, a, nl) && read_int(p, e[0], nl) && read_int(p, e[1], nl) && read_int(p, e[2], nl);
+        }))
+        return BADEDGEFILE;
     for (int i = 0; i < nedge; i++) {
-        int n0, n1;
-        if (fscanf(fp, "%i %i %i %i", &j, &n0, &n1, &j) != 4) {
-            fclose(fp);
-            return BADEDGEFILE;
-        }
-        if (n0 < 0 || n1 < 0 || n0 >= NumNodes || n1 >= NumNodes) {
-            fclose(fp);
-            return BADEDGEFILE;
-        }
-        edges_.push_back({n0, n1, j});
+        const int n0 = edges_[i][0], n1 = edges_[i][1];
+        j = edges_[i][2];
+        if (n0 < 0 || n1 < 0 || n0 >= NumNodes || n1 >= NumNodes) return BADEDGEFILE;
         if (j < 0) {
             int bc = -(j + 2);
-            for (int el : mbr[n0]) {
-                CMElement &e = meshele[el];
+            for (int t = mptr[n0]; t < mptr[n0 + 1]; ++t) {
+                CMElement &e = meshele[mbr[t]];
                 if ((e.p[0] == n0 && e.p[1] == n1) || (e.p[0] == n1 && e.p[1] == n0)) e.e[0] = bc;
                 if ((e.p[1] == n0 && e.p[2] == n1) || (e.p[1] == n1 && e.p[2] == n0)) e.e[1] = bc;
                 if ((e.p[2] == n0 && e.p[0] == n1) || (e.p[2] == n1 && e.p[0] == n0)) e.e[2] = bc;
             }
         }
     }
-    fclose(fp);
+    tr.mark("edges");
     if (deleteFiles)
         for (const char *ext : {".ele", ".node", ".pbc", ".poly"}) remove((PathName + ext).c_str());
     return NOERROR;
@@ -415,31 +595,67 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
 
 int FSolver::SortElements()
 {
-    // comb sort on p0+p1+p2 (cuthill.cpp:39-86); not stable, restated exactly
-    std::vector<long long> Score(NumEls);
-    for (int k = 0; k < NumEls; k++) Score[k] = (long long)meshele[k].p[0] + meshele[k].p[1] + meshele[k].p[2];
+    // comb sort on p0+p1+p2 (cuthill.cpp:39-86); not stable, restated exactly:
+    // the same comparisons and swaps, on packed (score, element) keys instead
+    // of the element records, which are permuted once at the end
+    std::vector<unsigned long long> key(NumEls);
+    for (int k = 0; k < NumEls; k++) {
+        const unsigned long long sc = (unsigned long long)((long long)meshele[k].p[0] + meshele[k].p[1] + meshele[k].p[2]);
+        key[k] = (sc << 32) | (unsigned)k;
+    }
+    // A pass with gap g compares (j, j + g) for j ascending: the steps of one
+    // residue class j mod g touch only that class's entries, in ascending
+    // order, so classes are independent -- wide passes run with the classes
+    // split over threads (each class still in ascending order: the same swaps)
     int gap = NumEls, i = 0;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int T = (int)std::min(hw, 16u);
     do {
         if (gap > 1) {
             gap = (gap * 10) / 13;
             if ((gap == 10) || (gap == 9)) gap = 11;
         }
         i = 0;
-        for (int j = 0; (j + gap) < NumEls; j++) {
-            if (Score[j] > Score[j + gap]) {
-                int k = j + gap;
-                std::swap(Score[k], Score[j]);
-                std::swap(meshele[k], meshele[j]);
-                i = 1;
+        if (T > 1 && gap >= 8 * T && NumEls >= (1 << 16)) {
+            std::vector<char> sw(T, 0);
+            std::vector<std::thread> th;
+            const int g = gap;
+            auto part = [&](int t) {
+                const int r0 = (int)((long long)g * t / T), r1 = (int)((long long)g * (t + 1) / T);
+                char any = 0;
+                for (long long b = 0; b + g < NumEls; b += g)
+                    for (int r = r0; r < r1 && b + r + g < NumEls; ++r) {
+                        unsigned long long &x = key[b + r], &y = key[b + r + g];
+                        if ((x >> 32) > (y >> 32)) {
+                            std::swap(x, y);
+                            any = 1;
+                        }
+                    }
+                sw[t] = any;
+            };
+            for (int t = 1; t < T; ++t) th.emplace_back(part, t);
+            part(0);
+            for (auto &x : th) x.join();
+            for (char c : sw) i |= c;
+        } else {
+            for (int j = 0; (j + gap) < NumEls; j++) {
+                if ((key[j] >> 32) > (key[j + gap] >> 32)) {
+                    std::swap(key[j], key[j + gap]);
+                    i = 1;
+                }
             }
         }
     } while ((gap > 1) && (i > 0));
+    std::vector<CMElement> sorted(NumEls);
+    for (int k = 0; k < NumEls; k++) sorted[k] = meshele[(unsigned)(key[k] & 0xffffffffu)];
+    meshele.swap(sorted);
     return true;
 }
 
 int FSolver::Cuthill(bool deleteFiles)
 {
     // reverse-less Cuthill-McKee of cuthill.cpp:88-390, on the .edge connectivity
+    LoadTrace tr;
     const int n_lines = (int)edges_.size();
     std::vector<int> numcon(NumNodes, 0), newnum(NumNodes, -1), nxtnum(NumNodes, -1);
     for (auto &e : edges_) {
@@ -453,6 +669,7 @@ int FSolver::Cuthill(bool deleteFiles)
         ocon[e[1]].push_back(e[0]);
     }
     if (deleteFiles) remove((PathName + ".edge").c_str());
+    tr.mark("adjacency");
     // bubble sort by increasing connectivity
     for (int n0 = 0; n0 < NumNodes; n0++) {
         std::vector<int> &l = ocon[n0];
@@ -461,6 +678,7 @@ int FSolver::Cuthill(bool deleteFiles)
             for (int j = 1; j < m; j++)
                 if (numcon[l[j]] < numcon[l[j - 1]]) std::swap(l[j], l[j - 1]);
     }
+    tr.mark("neighbour sort");
     long long j = numcon[0];
     int n0 = 0;
     for (long long i = 1; i < NumNodes; i++) {
@@ -505,6 +723,7 @@ int FSolver::Cuthill(bool deleteFiles)
             }
         } while (n < NumNodes);
     }
+    tr.mark("numbering");
     for (auto &p : pbclist) {
         p.x = newnum[p.x];
         p.y = newnum[p.y];
@@ -521,7 +740,9 @@ int FSolver::Cuthill(bool deleteFiles)
     std::vector<CNode> sorted(NumNodes);
     for (int i = 0; i < NumNodes; i++) sorted[newnum[i]] = meshnode[i];
     meshnode.swap(sorted);
+    tr.mark("bandwidth + renumber");
     SortElements();
+    tr.mark("SortElements");
     return true;
 }
 
@@ -706,12 +927,24 @@ bool FSolver::make_desc(DescStore &ds)
     return true;
 }
 
+namespace {
+double ms_since(std::chrono::steady_clock::time_point &t)
+{
+    const auto n = std::chrono::steady_clock::now();
+    const double ms = std::chrono::duration<double, std::milli>(n - t).count();
+    t = n;
+    return ms;
+}
+}  // namespace
+
 int FSolver::Static2D()
 {
+    auto t = std::chrono::steady_clock::now();
     DescStore ds;
     if (!make_desc(ds)) return false;
     xfk_problem *prob = nullptr;
     int rc = xfk_problem_create(&ds.d, device, &prob);
+    ms_phase[2] = ms_since(t);
     if (rc == XFK_OK) rc = xfk_static2d(prob, 0, &stats);
     if (rc == XFK_OK) {
         A.assign(NumNodes, 0.0);
@@ -729,11 +962,13 @@ int FSolver::Static2D()
     }
     if (rc != XFK_OK) warn(std::string("GPU solver error: ") + xfk_last_error() + "\n");
     if (prob) xfk_problem_destroy(prob);
+    ms_phase[3] = ms_since(t);
     return rc == XFK_OK;
 }
 
 int FSolver::Harmonic2D()
 {
+    auto t = std::chrono::steady_clock::now();
     DescStore ds;
     if (!make_desc(ds)) return false;
     std::vector<xfk_block_ac_desc> bac(blockproplist.size());
@@ -767,6 +1002,7 @@ int FSolver::Harmonic2D()
                          cac.empty() ? nullptr : cac.data(), ACSolver, prox.data()};
     xfk_problem *prob = nullptr;
     int rc = xfk_problem_create_harmonic(&ds.d, &ac, device, &prob);
+    ms_phase[2] = ms_since(t);
     if (rc == XFK_OK) rc = xfk_harmonic2d(prob, 0, &stats);
     std::vector<double> Ac;
     if (rc == XFK_OK) {
@@ -796,8 +1032,39 @@ int FSolver::Harmonic2D()
     }
     if (rc != XFK_OK) warn(std::string("GPU solver error: ") + xfk_last_error() + "\n");
     if (prob) xfk_problem_destroy(prob);
+    ms_phase[3] = ms_since(t);
     return rc == XFK_OK;
 }
+
+namespace {
+// "%.17g" and "%i" as printf writes them (std::to_chars: the same correctly
+// rounded digits and the same %g form), for the .ans's large sections
+inline char *put_g17(char *p, double v) { return std::to_chars(p, p + 32, v, std::chars_format::general, 17).ptr; }
+inline char *put_i(char *p, int v) { return std::to_chars(p, p + 16, v).ptr; }
+// lines [0, n): line(i, buf) writes line i (at most max_line chars) and returns
+// its end; formatted in parallel chunks, written in order
+template <class F>
+void write_lines(FILE *fp, int n, int max_line, F line)
+{
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int T = (int)std::max(1, std::min<int>((int)std::min(hw, 16u), n / 65536));
+    std::vector<std::vector<char>> buf(T);
+    auto part = [&](int t) {
+        const int a = (int)((long long)n * t / T), b = (int)((long long)n * (t + 1) / T);
+        std::vector<char> &o = buf[t];
+        o.resize((size_t)(b - a) * max_line + 1);
+        char *q = o.data();
+        for (int i = a; i < b; ++i) q = line(i, q);
+        o.resize((size_t)(q - o.data()));
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(part, t);
+    part(0);
+    for (auto &x : th) x.join();
+    for (auto &o : buf)
+        if (!o.empty()) fwrite(o.data(), 1, o.size(), fp);
+}
+}  // namespace
 
 int FSolver::WriteStatic2D()
 {
@@ -820,16 +1087,31 @@ int FSolver::WriteStatic2D()
     fprintf(fp, "[Solution]\n");
     const double cf = unitconv[LengthUnits];
     fprintf(fp, "%i\n", NumNodes);
-    for (int i = 0; i < NumNodes; i++) {
-        fprintf(fp, "%.17g\t%.17g\t%.17g\t%i", meshnode[i].x / cf, meshnode[i].y / cf, A[i],
-                meshnode[i].BoundaryMarker);
+    fflush(fp);
+    write_lines(fp, NumNodes, 128, [&](int i, char *q) {
+        q = put_g17(q, meshnode[i].x / cf);
+        *q++ = '\t';
+        q = put_g17(q, meshnode[i].y / cf);
+        *q++ = '\t';
+        q = put_g17(q, A[i]);
+        *q++ = '\t';
+        q = put_i(q, meshnode[i].BoundaryMarker);
         // static2d.cpp:1093-1101: Aprev follows the marker with no separator
-        if (!Aprev.empty()) fprintf(fp, "%.17g\n", Aprev[i]);
-        else fprintf(fp, "\n");
-    }
+        if (!Aprev.empty()) q = put_g17(q, Aprev[i]);
+        *q++ = '\n';
+        return q;
+    });
     fprintf(fp, "%i\n", NumEls);
-    for (int i = 0; i < NumEls; i++)
-        fprintf(fp, "%i\t%i\t%i\t%i\n", meshele[i].p[0], meshele[i].p[1], meshele[i].p[2], meshele[i].lbl);
+    fflush(fp);
+    write_lines(fp, NumEls, 64, [&](int i, char *q) {
+        for (int m = 0; m < 3; ++m) {
+            q = put_i(q, meshele[i].p[m]);
+            *q++ = '\t';
+        }
+        q = put_i(q, meshele[i].lbl);
+        *q++ = '\n';
+        return q;
+    });
     fprintf(fp, "%i\n", (int)labellist.size());
     for (size_t k = 0; k < labellist.size(); k++) {
         int i = labellist[k].InCircuit;
@@ -889,19 +1171,36 @@ int FSolver::WriteHarmonic2D()
     fprintf(fp, "%i\n", NumNodes);
     // incremental problems add A of the previous solution per node and J per
     // element (harmonic2d.cpp:929-949)
-    for (int i = 0; i < NumNodes; i++) {
-        fprintf(fp, "%.17g\t%.17g\t%.17g\t%.17g\t%i", meshnode[i].x / cf, meshnode[i].y / cf, A[i], A_im[i],
-                meshnode[i].BoundaryMarker);
-        if (!Aprev.empty()) fprintf(fp, "\t%.17g\n", Aprev[i]);
-        else fprintf(fp, "\n");
-    }
+    fflush(fp);
+    write_lines(fp, NumNodes, 160, [&](int i, char *q) {
+        for (double v : {meshnode[i].x / cf, meshnode[i].y / cf, A[i], A_im[i]}) {
+            q = put_g17(q, v);
+            *q++ = '\t';
+        }
+        q = put_i(q, meshnode[i].BoundaryMarker);
+        if (!Aprev.empty()) {
+            *q++ = '\t';
+            q = put_g17(q, Aprev[i]);
+        }
+        *q++ = '\n';
+        return q;
+    });
     fprintf(fp, "%i\n", NumEls);
-    for (int i = 0; i < NumEls; i++) {
-        fprintf(fp, "%i\t%i\t%i\t%i\t%i\t%i\t%i", meshele[i].p[0], meshele[i].p[1], meshele[i].p[2],
-                meshele[i].lbl, meshele[i].e[0], meshele[i].e[1], meshele[i].e[2]);
-        if (!Aprev.empty()) fprintf(fp, "\t%.17g\n", meshele[i].Jprev);
-        else fprintf(fp, "\n");
-    }
+    fflush(fp);
+    write_lines(fp, NumEls, 128, [&](int i, char *q) {
+        const CMElement &e = meshele[i];
+        for (int v : {e.p[0], e.p[1], e.p[2], e.lbl, e.e[0], e.e[1]}) {
+            q = put_i(q, v);
+            *q++ = '\t';
+        }
+        q = put_i(q, e.e[2]);
+        if (!Aprev.empty()) {
+            *q++ = '\t';
+            q = put_g17(q, e.Jprev);
+        }
+        *q++ = '\n';
+        return q;
+    });
     fprintf(fp, "%i\n", (int)labellist.size());
     for (size_t k = 0; k < labellist.size(); k++) {
         int i = labellist[k].InCircuit;
@@ -921,7 +1220,10 @@ int FSolver::WriteHarmonic2D()
 
 bool FSolver::runSolver(bool verbose)
 {
+    for (double &m : ms_phase) m = 0;
+    auto t = std::chrono::steady_clock::now();
     LoadMeshErr err = LoadMesh(deleteMeshFiles);
+    ms_phase[0] = ms_since(t);
     if (err != NOERROR) {
         warn(getErrorString(err));
         return false;
@@ -933,6 +1235,7 @@ bool FSolver::runSolver(bool verbose)
             return false;
         }
     }
+    ms_phase[1] = ms_since(t);
     if (!previousSolutionFile.empty()) {   // fsolver.cpp:1245-1320
         if (Frequency == 0 && PrevType != 0) {
             warn("Cannot handle incremental permeability problems with frequency 0.\n");
@@ -957,10 +1260,12 @@ bool FSolver::runSolver(bool verbose)
         if (verbose)
             PrintMessage(ProblemTypeV == AXISYMMETRIC ? "Harmonic axisymmetric problem solved\n"
                                                       : "Harmonic 2-D problem solved\n");
+        t = std::chrono::steady_clock::now();
         if (!WriteHarmonic2D()) {
             warn("couldn't write results to disk\n");
             return false;
         }
+        ms_phase[4] = ms_since(t);
         if (verbose) PrintMessage("results written to disk\n");
         return true;
     }
@@ -970,10 +1275,12 @@ bool FSolver::runSolver(bool verbose)
     }
     if (verbose)
         PrintMessage(ProblemTypeV == AXISYMMETRIC ? "Static axisymmetric problem solved\n" : "Static 2-D problem solved\n");
+    t = std::chrono::steady_clock::now();
     if (!WriteStatic2D()) {
         warn("couldn't write results to disk\n");
         return false;
     }
+    ms_phase[4] = ms_since(t);
     if (verbose) PrintMessage("results written to disk\n");
     return true;
 }

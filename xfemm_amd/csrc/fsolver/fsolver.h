@@ -75,6 +75,10 @@ public:
     std::vector<double> Aprev;
     bool meshLoadedFromPrevSolution = false;
     xfk_result stats{};
+    // wall milliseconds of the last runSolver: LoadMesh, Cuthill, problem
+    // creation (descriptor + host -> HBM upload), solve (device + solution
+    // read-back), write (.ans)
+    double ms_phase[5] = {};
     std::string lastError;
 
 private:

@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
                                                      const double *__restrict__ absd,
                                                      unsigned char *__restrict__ sflag, int *__restrict__ sdeg,
                                                      double *__restrict__ dfinv, double *__restrict__ wF,
-                                                     double *__restrict__ rho_part)
+                                                     double *__restrict__ rho_part, bool sgnd)
 {
     __shared__ double red[2 * (kB / 64)];
     const int i = (blockIdx.x * blockDim.x + threadIdx.x) / kStrG;
@@ -184,6 +184,14 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
     if (i < n) {
         const double ai = absd[i];
         const int cb = cv.base(i);
+        // signed strength: only couplings of the sign opposite to the
+        // diagonal's are strong (-a_ij for a positive diagonal).  Couplings of
+        // the diagonal's own sign -- the reference's AntiPeriodicity averaging
+        // gives each seam node such couplings to its partner's neighbours, an
+        // air-gap element gives a few -- are weak and lumped, so no aggregate
+        // spans an antiperiodic seam with a constant tentative value.
+        // (the matrices here are SPD: positive diagonals; sgnd == 0: |a_ij|,
+        // the former test, XFK_AMG_ABS_STRENGTH=1)
         const int s = rowptr[i] + g, e = rowptr[i + 1];
         // a chunk of this lane's entries at a time: columns and values, then
         // their diagonals, loaded before the first use; the entries are then
@@ -214,14 +222,14 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
             } else if (j >= ncl) {
                 // halo column: read by the smoother; for the rank-local P it is
                 // lumped like a weak entry, so P keeps reproducing constants
-                // (strong by the one-sided test |a_ij| > theta |a_ii|: the
+                // (strong by the one-sided test -a_ij > theta |a_ii|: the
                 // peer's diagonal is not known here)
                 sumA += fabs(a);
                 lump += a;
-                hdeg += (fabs(a) > theta * ai);
+                hdeg += ((sgnd ? -a : fabs(a)) > theta * ai);
             } else {
                 sumA += fabs(a);
-                if (a != 0.0 && fabs(a) > theta * sqrt(ai * dj[q])) {
+                if (a != 0.0 && (sgnd ? -a : fabs(a)) > theta * sqrt(ai * dj[q])) {
                     f = 1;
                     ++deg;
                     sumS += fabs(a);
@@ -2188,6 +2196,40 @@ __global__ void __launch_bounds__(256) k_fold_p(int n, const unsigned long long 
     }
 }
 
+// A Newton refresh (new level-0 values, same pattern, same P): P~ re-formed
+// numerically over its own pattern, P~_ic = P_ic - w d_i sum_j a_ij P_jc --
+// one lane per P~ entry (kFoldLanes lanes per row), the sum over row i of A in
+// its column order, each P_jc found by a scan of the short P row j; no SpGEMM
+// (the pattern of A P is the pattern of P~, which the setup formed)
+__global__ void __launch_bounds__(256) k_refold_p(int n, const unsigned long long *rho, const double *__restrict__ dinv,
+                                                  const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                  const double *__restrict__ val, const int *__restrict__ prow,
+                                                  const int *__restrict__ pcol, const double *__restrict__ pval,
+                                                  const int *__restrict__ frow, const int *__restrict__ fcol,
+                                                  double *__restrict__ fval)
+{
+    const int i = (int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) / kFoldLanes);
+    if (i >= n) return;
+    const int g = threadIdx.x & (kFoldLanes - 1);
+    const double ra = rho_of(rho);
+    const double wd = (ra > 0.0 ? 1.0 / ra : 0.0) * dinv[i];
+    const int ab = rowptr[i], ae = rowptr[i + 1];
+    for (int k = frow[i] + g; k < frow[i + 1]; k += kFoldLanes) {
+        const int c = fcol[k];
+        double ap = 0.0, pic = 0.0;
+        for (int q = prow[i]; q < prow[i + 1]; ++q)
+            if (pcol[q] == c) pic = pval[q];
+        for (int t = ab; t < ae; ++t) {
+            const int j = col[t];
+            double pjc = 0.0;
+            for (int q = prow[j]; q < prow[j + 1]; ++q)
+                if (pcol[q] == c) pjc = pval[q];
+            ap += val[t] * pjc;
+        }
+        fval[k] = pic - wd * ap;
+    }
+}
+
 // level 0, folded post-step (the pre-step stays sweep-from-0 + residual and
 // R r'): u = x_pre + w D^-1 r' + P~ x_c, i.e. the prolongation and the
 // post-sweep in one pass over P~ instead of P and A.  Tile shape and r.u
@@ -2954,6 +2996,13 @@ static bool side_setup_on()
 }
 
 // XFK_AMG_F32=0: level 0's V-cycle operators keep f64 values
+// signed strength (k_amg_strength); XFK_AMG_ABS_STRENGTH=1: |a_ij|
+static bool signed_strength()
+{
+    static const bool v = std::getenv("XFK_AMG_ABS_STRENGTH") == nullptr;
+    return v;
+}
+
 static bool f32_on()
 {
     static const bool v = [] {
@@ -3713,7 +3762,7 @@ int Amg::build(hipStream_t s, int l0)
         k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr,
                                                 ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
                                                 A.val, absd.p, sflag.p, cnt.p,
-                                                dfinv.p, wF.p, rho_part.p);
+                                                dfinv.p, wF.p, rho_part.p, signed_strength());
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p + 2 * l);
         if (g_prof) g_prof->end();
         if (l == kAmgMaxLevels - 1) break;   // smoother-only coarsest level
@@ -3953,7 +4002,7 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
         AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(nl))));
         k_amg_diag<<<nb(nl), kB, 0, s>>>(nl, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
         k_amg_strength<<<nb_str(nl), kB, 0, s>>>(nl, nl, theta, A.rowptr, ColView{A.col, nullptr, nullptr}, A.val,
-                                                 absd.p, sflag.p, cnt.p, dfinv.p, wF.p, rho_part.p);
+                                                 absd.p, sflag.p, cnt.p, dfinv.p, wF.p, rho_part.p, signed_strength());
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(nl), rho_part.p, omega, rho.p + 2 * l);
         long long nc = 0;
         rc = aggregate(s, l, nc, false);
@@ -4633,11 +4682,21 @@ int Amg::tail_read(double &ms_cycle, int &cycles, double &ms_setup)
     return XFK_OK;
 }
 
+// XFK_AMG_REFOLD=0: a Newton refresh runs level 0 unfolded (the former way)
+static bool refold_on()
+{
+    const char *e = std::getenv("XFK_AMG_REFOLD");   // (read per refresh: tests toggle it)
+    return !(e && std::atoi(e) == 0);
+}
+
 int Amg::refresh(hipStream_t s)
 {
     AmgLevel &A = *L[0];
     const int n = A.n;
-    A.fold = false;   // level 0's P~ was formed from the previous matrix: plain prolongation + sweep
+    // level 0's P~ belongs to the matrix it was formed from: re-formed below
+    // for the new values (k_refold_p), or level 0 runs unfolded
+    const bool refold = A.fold && !dist && refold_on() && A.fnnz > 0;
+    A.fold = refold;
     AMG_CHECK(absd.alloc(std::max(1, n)));
     AMG_CHECK(dfinv.alloc(std::max(1, n)));
     AMG_CHECK(wF.alloc(std::max(1, n)));
@@ -4649,12 +4708,21 @@ int Amg::refresh(hipStream_t s)
         k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr,
                                                 ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
                                                 A.val, absd.p, sflag.p, cnt.p,
-                                                dfinv.p, wF.p, rho_part.p);
+                                                dfinv.p, wF.p, rho_part.p, signed_strength());
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p);
     }
     if (A.has32 && f32_sweep_on()) {   // the sweeps' f32 copy of the new values
         int rc = to_f32(s, n, A.rowptr, A.nnz, A.val, A.a32);
         if (rc != XFK_OK) return rc;
+    }
+    if (refold && n > 0) {   // P~ = (I - w D^-1 A_new) P over its own pattern (new D^-1 and rho above)
+        k_refold_p<<<(int)(((long long)n * kFoldLanes + 255) / 256), 256, 0, s>>>(
+            n, rho.p, A.dinv.p, A.rowptr, A.col, A.val, A.prow.p, A.pcol.p, A.pval.p, A.ftrow.p, A.ftcol.p,
+            A.ftval.p);
+        if (A.has32) {
+            int rc = to_f32(s, n, A.ftrow.p, A.fnnz, A.ftval.p, A.f32v);
+            if (rc != XFK_OK) return rc;
+        }
     }
     AMG_CHECK(hipGetLastError());
     return XFK_OK;

@@ -24,6 +24,7 @@ EXPORTED = (
     "xfemm_fsolver_get_pbcs", "xfemm_fsolver_num_pbcs", "xfemm_fsolver_bandwidth",
     "xfemm_fsolver_get_block_bh", "xfemm_fsolver_num_nodes", "xfemm_fsolver_num_elements",
     "xfemm_fsolver_get_solution", "xfemm_fsolver_get_elements", "xfemm_fsolver_get_stats",
+    "xfemm_fsolver_get_times",
     "xfemm_fsolver_last_error", "xfemm_bh_get_slopes", "xfemm_bh_get_slopes_ac",
     "xfemm_fsolver_set_previous_solution_file", "xfemm_fsolver_previous_solution_file", "xfemm_fsolver_ac_solver",
     "xfemm_fsolver_frequency", "xfemm_fsolver_num_line_props", "xfemm_fsolver_num_node_props",
@@ -63,6 +64,7 @@ def load_library(path: str = FSOLVER_SO):
     L.xfemm_fsolver_get_solution.argtypes = [vp, dptr, dptr, dptr]
     L.xfemm_fsolver_get_elements.argtypes = [vp, iptr, iptr]
     L.xfemm_fsolver_get_stats.argtypes = [vp, C.POINTER(kernels.Result)]
+    L.xfemm_fsolver_get_times.argtypes = [vp, C.POINTER(C.c_double)]
     L.xfemm_fsolver_last_error.argtypes = [vp]
     L.xfemm_fsolver_set_previous_solution_file.argtypes = [vp, C.c_char_p]
     L.xfemm_fsolver_previous_solution_file.argtypes = [vp]
@@ -226,6 +228,14 @@ class FSolver:
                                                A.ctypes.data_as(dptr)):
             raise RuntimeError("no solution")
         return x, y, A
+
+    def times(self) -> dict:
+        """Wall milliseconds of the last runSolver, split as the reference's
+        sequence runs: load_mesh, cuthill, create (descriptor + upload),
+        solve (device + read-back), write (.ans)."""
+        ms = (C.c_double * 5)()
+        _lib.xfemm_fsolver_get_times(self._h, ms)
+        return dict(zip(("ms_load_mesh", "ms_cuthill", "ms_create", "ms_solve", "ms_write"), list(ms)))
 
     def stats(self) -> dict:
         r = kernels.Result()

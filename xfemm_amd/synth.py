@@ -170,26 +170,35 @@ def write_problem(base: str, kw: dict, label_xy: Optional[np.ndarray] = None) ->
                                                         int(lb.get("is_external", 0)))
     with open(base + ".fem", "w") as fh:
         fh.write(text)
+    x = np.asarray(x, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    p = np.asarray(p).reshape(-1, 3)
+    lbl = np.asarray(lbl)
+    e = np.asarray(e).reshape(-1, 3)
     with open(base + ".node", "w") as fh:
         fh.write("%d\t2\t0\t1\n" % len(x))
-        for i in range(len(x)):
-            fh.write("%d\t%.17g\t%.17g\t0\n" % (i, x[i] / conv, y[i] / conv))
+        fh.write("".join("%d\t%.17g\t%.17g\t0\n" % t for t in zip(range(len(x)), (x / conv).tolist(),
+                                                                      (y / conv).tolist())))
     with open(base + ".ele", "w") as fh:
         fh.write("%d\t3\t1\n" % len(p))
-        for i in range(len(p)):
-            fh.write("%d\t%d\t%d\t%d\t%d\n" % (i, p[i, 0], p[i, 1], p[i, 2], lbl[i] + 1))
-    edges = {}
-    for i in range(len(p)):
-        for j in range(3):
-            a, b = int(p[i, j]), int(p[i, (j + 1) % 3])
-            k = (min(a, b), max(a, b))
-            mk = -(int(e[i, j]) + 2) if e[i, j] >= 0 else 0
-            if k not in edges or mk != 0:
-                edges[k] = mk
+        fh.write("".join("%d\t%d\t%d\t%d\t%d\n" % t for t in zip(range(len(p)), p[:, 0].tolist(), p[:, 1].tolist(),
+                                                                    p[:, 2].tolist(), (lbl + 1).tolist())))
+    # every element edge once, sorted by (min, max) node; an edge carrying a
+    # boundary property keeps the marker -(prop + 2) (the last one in element
+    # order when several elements give one), else 0
+    a = p.reshape(-1)
+    b = p[:, [1, 2, 0]].reshape(-1)
+    lo, hi = np.minimum(a, b).astype(np.int64), np.maximum(a, b).astype(np.int64)
+    mk = np.where(e.reshape(-1) >= 0, -(e.reshape(-1).astype(np.int64) + 2), 0)
+    key = lo * (int(hi.max()) + 1 if len(hi) else 1) + hi
+    order = np.lexsort((np.arange(len(key)), mk != 0, key))   # per key: unmarked first, then marked in element order
+    ks = key[order]
+    last = np.r_[ks[1:] != ks[:-1], True]                      # the last entry of each key wins
+    sel = order[last]
     with open(base + ".edge", "w") as fh:
-        fh.write("%d\t1\n" % len(edges))
-        for n, (k, mk) in enumerate(sorted(edges.items())):
-            fh.write("%d\t%d\t%d\t%d\n" % (n, k[0], k[1], mk))
+        fh.write("%d\t1\n" % len(sel))
+        fh.write("".join("%d\t%d\t%d\t%d\n" % t for t in zip(range(len(sel)), lo[sel].tolist(), hi[sel].tolist(),
+                                                               mk[sel].tolist())))
     # .pbc: periodic pairs, then the air-gap elements (writepoly.cpp:1836-1966)
     pbc = kw.get("pbc")
     pbc = np.zeros((0, 3), np.int32) if pbc is None else np.asarray(pbc).reshape(-1, 3)
