@@ -36,7 +36,10 @@ Output: one JSON line (rank 0) with
   secondary      configs[3] (nonlinear M-19, Newton loop) and configs[4] on
                  one GPU (20M triangles, 10.0M DoF);
   cold_first_solve  the first solve of a fresh problem object (no capacity or
-                 round-count hints from an earlier setup).
+                 round-count hints from an earlier setup);
+  fsolver_end_to_end  the product path: FSolver .fem -> .ans wall time on
+                 configs[1] and configs[2], split into LoadMesh / Cuthill /
+                 create / solve / write.
 """
 import argparse
 import ctypes
@@ -255,6 +258,56 @@ def configs4_rank0_of_8(device, args):
             "collectives_per_solve": order}
 
 
+def fsolver_end_to_end(device, args):
+    """The drop-in product path timed whole: FSolver .fem + fmesher files ->
+    .ans (fsolver.cpp:1213-1340's sequence: LoadMesh, Cuthill-McKee, problem
+    creation with the host -> HBM upload, the device solve with the solution
+    read-back, the .ans write), a fresh FSolver per run as femmcli's
+    mi_analyze uses it.  configs[1]: the ~200k-triangle TorqueBenchmark at
+    30 degrees (tests/golden/torque/TorqueBenchmark_fine_30.tgz, made by
+    tools/gen_torque_fixtures.py); configs[2]: the bench's own 2M-triangle
+    mesh written in the fmesher layout (synth.write_problem).  Two runs each,
+    the second reported (the first also loads the process's code objects)."""
+    import shutil
+    import tarfile
+    import tempfile
+    from xfemm_amd import fsolver, synth
+    out = []
+    with tempfile.TemporaryDirectory() as td:
+        with tarfile.open(os.path.join(ROOT, "tests", "golden", "torque", "TorqueBenchmark_fine_30.tgz")) as tf:
+            tf.extractall(td)
+        cases = [("configs[1]: TorqueBenchmark refined (~200k tri, periodic + air gap), 30 deg",
+                  os.path.join(td, "TorqueBenchmark_fine_30"))]
+        b2 = os.path.join(td, "square")
+        synth.write_problem(b2, synth.magnetostatic(args.cells))
+        cases.append(("configs[2]: synthetic %d-tri square" % (2 * args.cells ** 2), b2))
+        for name, base in cases:
+            src = base + "_src"
+            os.makedirs(src, exist_ok=True)
+            for ext in (".fem", ".node", ".ele", ".edge", ".pbc"):
+                shutil.copy(base + ext, os.path.join(src, os.path.basename(base) + ext))
+            rec = None
+            for _ in range(2):
+                for ext in (".node", ".ele", ".edge", ".pbc"):   # (runSolver deletes the mesh files)
+                    shutil.copy(os.path.join(src, os.path.basename(base) + ext), base + ext)
+                _hip_sync()
+                t0 = time.perf_counter()
+                fs = fsolver.FSolver(device=device)
+                fs.PathName = base
+                ok = fs.LoadProblemFile() and fs.runSolver(False)
+                dt = time.perf_counter() - t0
+                if not ok:
+                    raise RuntimeError("FSolver failed on %s: %s" % (name, fs.last_error()))
+                st, tm = fs.stats(), fs.times()
+                rec = {"workload": name, "dof": fs.NumNodes(), "ms_wall": 1e3 * dt,
+                       "dof_per_s_wall": fs.NumNodes() / dt, "pcg_iters": st["cg_iters"],
+                       "ms_device_solve": st["ms_solve"] + st["ms_assemble"] + st["ms_symbolic"]}
+                rec.update(tm)
+                del fs
+            out.append(rec)
+    return out
+
+
 def cold_first_solve(device, args, kw):
     """A first solve of a fresh problem: new Static2DProblem (host -> HBM
     upload timed apart), then its first solve() with none of the per-problem
@@ -404,6 +457,7 @@ def main():
     ap.add_argument("--amg-replicate", type=int, default=None,
                     help="sharded solves: coarse levels of at most this many global rows are replicated")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fsolver", action="store_true", help="skip the FSolver .fem -> .ans end-to-end timing")
     ap.add_argument("--no-phases", action="store_true", help="skip the per-phase table")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per SpMV launch from a PMC pass (profiles/), if measured")
@@ -588,6 +642,8 @@ def main():
         out["config"]["same_mesh_1gpu"] = same_mesh
     if rank == 0 and world == 1 and not sharded:
         out["cold_first_solve"] = cold_first_solve(local, args, kw)
+        if not args.no_fsolver:
+            out["fsolver_end_to_end"] = fsolver_end_to_end(local, args)
     if rank == 0 and world == 1 and not sharded and not args.nonlinear and not args.no_secondary:
         P.close()
         out["secondary"] = [nonlinear_secondary(local, args)]

@@ -16,6 +16,10 @@ test/TorqueBenchmark.fem) and writes
                          machine refined to ~200k triangles (label mesh sizes and
                          boundary-arc side lengths / 6.2, Precision 1e-8); meshed
                          at test time by the same restatement (~1 s)
+  tests/golden/torque/TorqueBenchmark_fine_30.tgz           that mesh at rotor angle
+                         30 (.fem .node .ele .edge .pbc, gzip): bench.py times the
+                         product's FSolver .fem -> .ans on configs[1] from it (the
+                         bench may not run the oracle's mesher)
 
 Run in the dev container:  python tools/gen_torque_fixtures.py
 """
@@ -54,6 +58,16 @@ def main():
             fh.write(mesher.pbc_text(res, {"AGE": (float(deg), 0.0)}))
     with open(base + "_fine.fem", "w") as fh:
         fh.write(fine_fem_text())
+    # configs[1] at 30 degrees, packed for bench.py
+    import tarfile
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from torque import write_fine_case
+    with tempfile.TemporaryDirectory() as td:
+        fb = write_fine_case(td, 30)
+        with tarfile.open(os.path.join(OUT, "TorqueBenchmark_fine_30.tgz"), "w:gz") as tf:
+            for ext in (".fem", ".node", ".ele", ".edge", ".pbc"):
+                tf.add(fb + ext, arcname=os.path.basename(fb) + ext)
     print("TorqueBenchmark: %d nodes, %d triangles, %d periodic pairs, air gap of %d ring nodes (%s)"
           % (len(res.mesh.x), len(res.mesh.tri), len(res.pbc), res.ages[0].nodeNums[0], res.switches))
 
