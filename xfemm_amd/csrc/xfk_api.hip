@@ -1718,6 +1718,34 @@ int xfk_partition_plan_coupled(int n_nodes, int n_elems, const int *p, int rank,
     return XFK_OK;
 }
 
+}  // extern "C"
+
+namespace xfk {
+
+// the row-block plan of this rank; coupled nodes (periodic pairs and air-gap
+// quad nodes) are assembled on every rank
+int plan_rank(const xfk_problem_desc *d, const GlobalPrep &G, xfk_comm *comm, PartPlan &plan)
+{
+    std::vector<int> coupled;
+    for (int k = 0; k < d->n_pbc; ++k) {
+        coupled.push_back(d->pbc[3 * k]);
+        coupled.push_back(d->pbc[3 * k + 1]);
+    }
+    for (long long k : G.age_key) {
+        coupled.push_back((int)(k >> 32));
+        coupled.push_back((int)(k & 0xffffffff));
+    }
+    std::sort(coupled.begin(), coupled.end());
+    coupled.erase(std::unique(coupled.begin(), coupled.end()), coupled.end());
+    XFK_REQUIRE(plan_partition(d->n_nodes, d->n_elems, d->p, comm->rank, comm->size, plan, &coupled), XFK_ERR_ARG,
+                "bad partition: fewer nodes than ranks");
+    return XFK_OK;
+}
+
+}  // namespace xfk
+
+extern "C" {
+
 int xfk_problem_create_dist(const xfk_problem_desc *d, int device, xfk_comm *comm, xfk_problem **out)
 {
     XFK_REQUIRE(d && out && comm, XFK_ERR_ARG, "null argument");
@@ -1731,21 +1759,8 @@ int xfk_problem_create_dist(const xfk_problem_desc *d, int device, xfk_comm *com
     if (rc != XFK_OK) return rc;
     rc = age_entries(d, 1.0, G.age_key, G.age_val);
     if (rc != XFK_OK) return rc;
-    // coupled nodes: periodic pairs and air-gap quad nodes (assembled on every rank)
-    std::vector<int> coupled;
-    for (int k = 0; k < d->n_pbc; ++k) {
-        coupled.push_back(d->pbc[3 * k]);
-        coupled.push_back(d->pbc[3 * k + 1]);
-    }
-    for (long long k : G.age_key) {
-        coupled.push_back((int)(k >> 32));
-        coupled.push_back((int)(k & 0xffffffff));
-    }
-    std::sort(coupled.begin(), coupled.end());
-    coupled.erase(std::unique(coupled.begin(), coupled.end()), coupled.end());
     PartPlan plan;
-    XFK_REQUIRE(plan_partition(d->n_nodes, d->n_elems, d->p, comm->rank, comm->size, plan, &coupled), XFK_ERR_ARG,
-                "bad partition: fewer nodes than ranks");
+    if ((rc = plan_rank(d, G, comm, plan)) != XFK_OK) return rc;
     return build_local(d, G, &plan, device, comm, out);
 }
 

@@ -521,6 +521,8 @@ int prepare_magdir(const xfk_problem_desc *d, GlobalPrep &G);
 int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *plan, int device, xfk_comm *comm,
                 xfk_problem **out);
 int build_symbolic(xfk_problem *P);
+// the row-block plan of comm's rank (coupled nodes assembled on every rank)
+int plan_rank(const xfk_problem_desc *d, const GlobalPrep &G, xfk_comm *comm, PartPlan &plan);
 hipError_t d2h(void *dst, const void *src, size_t bytes, hipStream_t s);
 // host -> device copy into a (re)allocated buffer, ordered on `s`
 template <class T>
