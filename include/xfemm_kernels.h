@@ -377,6 +377,16 @@ typedef struct {
 
 int xfk_problem_create_harmonic(const xfk_problem_desc *desc, const xfk_harmonic_desc *ac, int device,
                                 xfk_problem **out);
+/* The same problem sharded over comm's ranks (row blocks, as
+ * xfk_problem_create_dist): every rank passes the GLOBAL descriptors;
+ * xfk_harmonic2d and xfk_get_solution_complex are collective.  COCG exchanges
+ * the halo of its vectors before every SpMV and all-reduces its per-block
+ * partials once per iteration; the AMG preconditioner is the sharded hierarchy
+ * of the real surrogate (Amg::setup_dist).  Linear problems and the
+ * successive-approximation nonlinear loop (ACSolver 0); Case-2 circuits and
+ * the Newton AC solver return XFK_ERR_UNSUPPORTED (one device). */
+int xfk_problem_create_harmonic_dist(const xfk_problem_desc *desc, const xfk_harmonic_desc *ac, int device,
+                                     xfk_comm *comm, xfk_problem **out);
 /* FSolver::Harmonic2D, or HarmonicAxisymmetric (harmonicaxi.cpp:1-800) when
  * desc->problem_type is XFK_AXISYMMETRIC, on the device (complex-symmetric
  * COCG, the reference's stopping test |r| / |b| <= Precision).  flags as for

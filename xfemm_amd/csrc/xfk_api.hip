@@ -780,7 +780,7 @@ static CgAxpyArgs cg_args(xfk_problem *P, long long it)
 }
 
 // sum of a host scalar over the ranks (setup-time decisions that must agree)
-static int allreduce_host(xfk_problem *P, double &v)
+int allreduce_host(xfk_problem *P, double &v)
 {
     if (!P->comm) return XFK_OK;
     hipStream_t s = P->stream;

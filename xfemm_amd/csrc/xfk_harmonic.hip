@@ -26,6 +26,7 @@
 #include "xfk_age.h"
 #include "xfk_amg.h"
 #include "xfk_axi.h"
+#include "xfk_comm.h"
 #include "xfk_kernels.h"
 #include "xfk_spmv.h"
 
@@ -741,8 +742,10 @@ struct HcArgs {
     const double *val, *val_im;
     double2 *x, *r, *u, *w, *z, *p;
     const double2 *dinv;
-    double *part;     // kHcParts arrays of G
+    double *part;     // kHcParts arrays of G (written)
+    const double *part_rd;   // what the update reads: part, or its sum over the ranks (sharded)
     int G;
+    int Gred;         // partial entries the update reduces (0: the local grids)
     CcgState *S;
     // AMG mode: the real V-cycle preconditions real and imaginary parts; r is
     // also written split (r_re, r_im), u comes back split (u_re, u_im)
@@ -918,15 +921,16 @@ __global__ void __launch_bounds__(kHcAxBlock) k_hc_axpy(HcArgs A, long long it, 
     if (S->done) return;
     const int par = (int)(it & 1);
     double s5[5] = {0, 0, 0, 0, 0};
-    const int Gcg = (A.N + kCgBlock - 1) / kCgBlock;
+    const int Gcg = A.Gred ? A.Gred : (A.N + kCgBlock - 1) / kCgBlock;
+    const double *pr = A.part_rd;
     for (int k = threadIdx.x; k < Ggam; k += blockDim.x) {
-        s5[0] += A.part[(2 * par) * A.G + k];
-        s5[1] += A.part[(2 * par + 1) * A.G + k];
+        s5[0] += pr[(2 * par) * A.G + k];
+        s5[1] += pr[(2 * par + 1) * A.G + k];
     }
-    for (int k = threadIdx.x; k < Grr; k += blockDim.x) s5[2] += A.part[(6 + par) * A.G + k];
+    for (int k = threadIdx.x; k < Grr; k += blockDim.x) s5[2] += pr[(6 + par) * A.G + k];
     for (int k = threadIdx.x; k < Gcg; k += blockDim.x) {
-        s5[3] += A.part[4 * A.G + k];
-        s5[4] += A.part[5 * A.G + k];
+        s5[3] += pr[4 * A.G + k];
+        s5[4] += pr[5 * A.G + k];
     }
     hc_block_sum<5>(s5, red);
     const double2 gam = cx(s5[0], s5[1]), del = cx(s5[3], s5[4]);
@@ -934,7 +938,7 @@ __global__ void __launch_bounds__(kHcAxBlock) k_hc_axpy(HcArgs A, long long it, 
     double bb;
     if (it == 0) {
         double sb[1] = {0};
-        for (int k = threadIdx.x; k < Gcg; k += blockDim.x) sb[0] += A.part[8 * A.G + k];
+        for (int k = threadIdx.x; k < Gcg; k += blockDim.x) sb[0] += pr[8 * A.G + k];
         hc_block_sum<1>(sb, red);
         bb = sb[0];
     } else {
@@ -1214,10 +1218,11 @@ int harmonic_validate(const xfk_problem_desc *d, const xfk_harmonic_desc *ac)
 
 }  // namespace
 
-extern "C" {
+namespace {
 
-int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_desc *ac, int device,
-                                xfk_problem **out)
+// the harmonic problem of one device (comm == nullptr) or of comm's rank
+int create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_desc *ac, int device, xfk_comm *comm,
+                    xfk_problem **out)
 {
     XFK_REQUIRE(d && out, XFK_ERR_ARG, "null argument");
     *out = nullptr;
@@ -1467,8 +1472,40 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
         }
     }
 
+    // sharded: the row-block plan, then the per-node tables in local numbering
+    PartPlan plan;
+    if (comm) {
+        XFK_REQUIRE(nc2 == 0, XFK_ERR_UNSUPPORTED,
+                    "sharded harmonic problems: Case-2 circuits (a specified current in a conducting region) "
+                    "are solved on one device");
+        XFK_REQUIRE(!(nonlin && ac->ac_solver == 1), XFK_ERR_UNSUPPORTED,
+                    "sharded harmonic problems: the Newton AC solver ([ACSolver] = 1) runs on one device");
+        if ((rc = plan_rank(d, G, comm, plan)) != XFK_OK) return rc;
+        const int NL = plan.n_own + plan.n_halo, NR = plan.n_own + plan.n_extra;
+        std::vector<double> f2(2 * (size_t)NL), l2(2 * (size_t)NL);
+        for (int l = 0; l < NL; ++l)
+            for (int q = 0; q < 2; ++q) {
+                f2[2 * (size_t)l + q] = first[2 * (size_t)plan.l2g[l] + q];
+                l2[2 * (size_t)l + q] = last[2 * (size_t)plan.l2g[l] + q];
+            }
+        first.swap(f2);
+        last.swap(l2);
+        std::vector<int> g2l_row(N, -1);   // assembled rows (owned, then the coupled extra rows)
+        for (int l = 0; l < NR; ++l) g2l_row[plan.l2g[l]] = l;
+        std::vector<int> pn;
+        std::vector<double> pj;
+        for (size_t k = 0; k < pt_nodes.size(); ++k) {
+            const int l = g2l_row[pt_nodes[k]];
+            if (l < 0) continue;
+            pn.push_back(l);
+            pj.push_back(pt_J[2 * k]);
+            pj.push_back(pt_J[2 * k + 1]);
+        }
+        pt_nodes.swap(pn);
+        pt_J.swap(pj);
+    }
     xfk_problem *P = nullptr;
-    rc = build_local(d, G, nullptr, device, nullptr, &P);
+    rc = build_local(d, G, comm ? &plan : nullptr, device, comm, &P);
     if (rc != XFK_OK) return rc;
     P->harmonic = true;
     P->omega = w;
@@ -1511,6 +1548,23 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_de
     return XFK_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_desc *ac, int device,
+                                xfk_problem **out)
+{
+    return create_harmonic(d, ac, device, nullptr, out);
+}
+
+int xfk_problem_create_harmonic_dist(const xfk_problem_desc *d, const xfk_harmonic_desc *ac, int device,
+                                     xfk_comm *comm, xfk_problem **out)
+{
+    XFK_REQUIRE(comm, XFK_ERR_ARG, "null communicator");
+    return create_harmonic(d, ac, device, comm, out);
+}
+
 int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
 {
     XFK_REQUIRE(P && P->harmonic, XFK_ERR_ARG, "not a harmonic problem (xfk_problem_create_harmonic)");
@@ -1532,19 +1586,43 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
     R.ms_symbolic = ms;
 
-    const int N = P->N;
+    const int N = P->N, NL = P->NL;   // owned rows; local nodes (owned, then the halo)
     const long long nnz = P->nnz;
+    // sharded (xfk_problem_create_harmonic_dist): row blocks as the static
+    // path -- the halo of x / u exchanged before each SpMV (x: interleaved
+    // complex; u: the V-cycle's split real / imaginary outputs), the
+    // per-block partials all-reduced after each SpMV, the setup-time
+    // decisions and the nonlinear residual summed over the ranks
+    xfk_comm *comm = P->comm;
     XFK_CHECK(P->val.alloc((size_t)nnz));
     XFK_CHECK(P->val_im.alloc((size_t)nnz));
-    XFK_CHECK(P->b.alloc((size_t)N));
-    XFK_CHECK(P->b_im.alloc((size_t)N));
+    const int NR = P->NR;   // assembled rows: owned, then (sharded, periodic) the coupled rows folded in
+    XFK_CHECK(P->b.alloc((size_t)NR));
+    XFK_CHECK(P->b_im.alloc((size_t)NR));
     const int Gcg = (N + kCgBlock - 1) / kCgBlock, Gax = hc_axpy_grid(N);
-    const int G = std::max(Gcg, Gax);
-    XFK_CHECK(P->hc_vec.alloc(7 * (size_t)N));
-    XFK_CHECK(P->hc_part.alloc((size_t)kHcParts * G));
+    int G = std::max(Gcg, Gax);
+    if (comm)   // one partial layout for every rank: the largest block's grids
+        for (int q = 0; q < P->nranks; ++q) {
+            const int nq = (int)(row_begin(P->N_global, q + 1, P->nranks) - row_begin(P->N_global, q, P->nranks));
+            G = std::max(G, std::max((nq + kCgBlock - 1) / kCgBlock, hc_axpy_grid(nq)));
+        }
+    if (comm && P->halo2.send.empty() && P->halo2.recv.empty()) {
+        for (const HaloRange &h : P->halo.send) P->halo2.send.push_back(HaloRange{h.peer, 2 * h.off, 2 * h.len, h.g0});
+        for (const HaloRange &h : P->halo.recv) P->halo2.recv.push_back(HaloRange{h.peer, 2 * h.off, 2 * h.len, h.g0});
+    }
+    XFK_CHECK(P->hc_vec.alloc(7 * (size_t)NL));
+    XFK_CHECK(P->hc_part.alloc((comm ? 2 : 1) * (size_t)kHcParts * G));
     XFK_CHECK(P->hc_state.alloc(1));
-    XFK_CHECK(P->hc_split.alloc(4 * (size_t)N));
+    XFK_CHECK(P->hc_split.alloc(4 * (size_t)NL));
     double2 *v = P->hc_vec.p;
+    auto exch_c = [&](double2 *vec) -> int {   // halo of an interleaved complex node vector
+        return comm ? comm->exchange(P->halo2, reinterpret_cast<double *>(vec), s) : XFK_OK;
+    };
+    auto exch_r = [&](double *vec) -> int { return comm ? comm->exchange(P->halo, vec, s) : XFK_OK; };
+    auto reduce_parts = [&]() -> int {
+        return comm ? comm->allreduce_sum(P->hc_part.p, P->hc_part.p + (size_t)kHcParts * G, (size_t)kHcParts * G, s)
+                    : XFK_OK;
+    };
     const bool nonlin = P->any_nonlinear;
     constexpr int kResGrid = 256;
     // Newton AC solver: auxiliary matrices from the second pass on (the
@@ -1593,19 +1671,21 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     H.val = P->val.p;
     H.val_im = P->val_im.p;
     H.x = v;
-    H.r = v + N;
-    H.u = v + 2 * (size_t)N;
-    H.w = v + 3 * (size_t)N;
-    H.z = v + 4 * (size_t)N;
-    H.p = v + 5 * (size_t)N;
-    double2 *dinv = v + 6 * (size_t)N;
+    H.r = v + NL;
+    H.u = v + 2 * (size_t)NL;
+    H.w = v + 3 * (size_t)NL;
+    H.z = v + 4 * (size_t)NL;
+    H.p = v + 5 * (size_t)NL;
+    double2 *dinv = v + 6 * (size_t)NL;
     H.dinv = dinv;
     H.part = P->hc_part.p;
+    H.part_rd = comm ? P->hc_part.p + (size_t)kHcParts * G : P->hc_part.p;
     H.G = G;
+    H.Gred = comm ? G : 0;
     H.S = P->hc_state.p;
     H.r_re = P->hc_split.p;
-    H.r_im = P->hc_split.p + N;
-    double *u_re = P->hc_split.p + 2 * (size_t)N, *u_im = P->hc_split.p + 3 * (size_t)N;
+    H.r_im = P->hc_split.p + NL;
+    double *u_re = P->hc_split.p + 2 * (size_t)NL, *u_im = P->hc_split.p + 3 * (size_t)NL;
     H.u_re = u_re;
     H.u_im = u_im;
     const int *done = &P->hc_state.p->done;
@@ -1621,10 +1701,14 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     int iter = 0;
     for (;; ++iter) {
         XFK_CHECK(hipEventRecord(e0, s));
+        if (nonlin && iter > 0) {   // the elements' B reads V at their halo nodes
+            const int xrc = exch_c(v);
+            if (xrc != XFK_OK) return xrc;
+        }
         XFK_CHECK(hipMemsetAsync(P->val.p, 0, sizeof(double) * nnz, s));
         XFK_CHECK(hipMemsetAsync(P->val_im.p, 0, sizeof(double) * nnz, s));
-        XFK_CHECK(hipMemsetAsync(P->b.p, 0, sizeof(double) * N, s));
-        XFK_CHECK(hipMemsetAsync(P->b_im.p, 0, sizeof(double) * N, s));
+        XFK_CHECK(hipMemsetAsync(P->b.p, 0, sizeof(double) * NR, s));
+        XFK_CHECK(hipMemsetAsync(P->b_im.p, 0, sizeof(double) * NR, s));
         A.iter = iter;
         A.newton = (ac1 && iter > 0) ? 1 : 0;
         double *aux = A.newton ? P->haux.p : nullptr;
@@ -1673,12 +1757,17 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
             XFK_CHECK(d2h(hp.data(), P->hc_bval.p, sizeof(double) * nbd, s));
             double sdi = 0;
             for (double q : hp) sdi += q;
+            if (comm) {   // the same sign on every rank
+                const int arc0 = allreduce_host(P, sdi);
+                if (arc0 != XFK_OK) return arc0;
+            }
             k_hc_surrogate<<<nb256(N), kBlock, 0, s>>>(N, sdi >= 0 ? 1.0 : -1.0, P->rowptr.p, P->col.p, P->val.p,
                                                        P->val_im.p, P->hc_bval.p);
             if (!P->amg) P->amg = new Amg();
             P->amg->theta = P->amg_theta;
             P->amg->sweeps = P->amg_sweeps;
             P->amg->omega = P->amg_omega;
+            P->amg->rep_rows = P->amg_replicate;
             ScopedEvents<2> aev;
             XFK_CHECK(aev.create());
             hipEvent_t a0 = aev[0], a1 = aev[1];
@@ -1692,22 +1781,39 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
             const bool reuse = P->amg_reuse && reusable && iter > 1 &&
                                4 * last_iters <= 5 * fresh_iters + 4;
             fresh = !reuse;
-            const int arc = reuse ? P->amg->refresh(s) : P->amg->setup(s, N, N, P->rowptr.p, P->col.p, P->hc_bval.p,
-                                                                       P->nnz);
+            const bool sharded = comm && comm->size > 1;   // (one rank: the single-device hierarchy)
+            const int arc = reuse     ? P->amg->refresh(s)
+                            : sharded ? P->amg->setup_dist(s, comm, P->halo, N, NL - N, P->rowptr.p, P->col.p,
+                                                           P->hc_bval.p, P->nnz_own)
+                                      : P->amg->setup(s, N, N, P->rowptr.p, P->col.p, P->hc_bval.p, P->nnz_own);
             XFK_CHECK(hipEventRecord(a1, s));
             XFK_CHECK(hipEventSynchronize(a1));
             float mss = 0;
             XFK_CHECK(hipEventElapsedTime(&mss, a0, a1));
             ms_setup += mss;
             if (arc != XFK_OK && arc != XFK_ERR_UNSUPPORTED) return arc;
-            amg = arc == XFK_OK;
+            double okv = arc == XFK_OK ? 0.0 : 1.0;   // every rank takes the same preconditioner
+            if (comm) {
+                const int arc1 = allreduce_host(P, okv);
+                if (arc1 != XFK_OK) return arc1;
+            }
+            amg = okv == 0.0;
             reusable = amg;
         }
         H.amg = amg ? 1 : 0;
         auto precondition = [&]() -> int {
             int rc = P->amg->vcycle(s, H.r_re, u_re, done);
             if (rc == XFK_OK) rc = P->amg->vcycle(s, H.r_im, u_im, done);
+            if (rc == XFK_OK) rc = exch_r(u_re);   // (the SpMV gathers u at the halo columns)
+            if (rc == XFK_OK) rc = exch_r(u_im);
             return rc;
+        };
+        // the SpMV of the current u, then the partials of every rank summed
+        auto spmv = [&](int gpar) -> int {
+            int rc = amg ? XFK_OK : exch_c(H.u);
+            if (rc != XFK_OK) return rc;
+            k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, gpar);
+            return reduce_parts();
         };
         // one COCG solve A x = b (warm: from the current x)
         // the linear solver's precision: adaptive once the auxiliary matrices
@@ -1719,22 +1825,29 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
         }
         auto solve_one = [&](double2 *xv, const double *bre, const double *bim, bool warm) -> int {
             H.x = xv;
-            XFK_CHECK(hipMemsetAsync(P->hc_part.p, 0, sizeof(double) * kHcParts * G, s));
+            XFK_CHECK(hipMemsetAsync(P->hc_part.p, 0, sizeof(double) * kHcParts * G, s));   // (the written half)
             CcgState init{};
             init.tol = lprec;
             XFK_CHECK(hipMemcpyAsync(P->hc_state.p, &init, sizeof(CcgState), hipMemcpyHostToDevice, s));
             k_hdiag_inv<<<nb256(N), kBlock, 0, s>>>(N, P->diag.p, P->val.p, P->val_im.p, dinv, P->hc_state.p);
             XFK_CHECK(hipMemcpyAsync(P->hc_host, P->hc_state.p, sizeof(CcgState), hipMemcpyDeviceToHost, s));
             XFK_CHECK(hipStreamSynchronize(s));
+            if (comm) {   // every rank must agree before the collective iterations
+                double sg = P->hc_host->singular ? 1.0 : 0.0;
+                const int grc = allreduce_host(P, sg);
+                if (grc != XFK_OK) return grc;
+                P->hc_host->singular = sg != 0.0;
+            }
             if (P->hc_host->singular) {
                 set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
                 return XFK_ERR_SINGULAR;
             }
+            int prc;
+            if (warm && (prc = exch_c(xv)) != XFK_OK) return prc;   // (r = b - A x0 reads x0's halo)
             if (warm) k_hc_init<true><<<Gcg, kCgBlock, 0, s>>>(H, bre, bim);
             else k_hc_init<false><<<Gcg, kCgBlock, 0, s>>>(H, bre, bim);
-            int prc;
             if (amg && (prc = precondition()) != XFK_OK) return prc;
-            k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, 0);
+            if ((prc = spmv(0)) != XFK_OK) return prc;
             long long it = 0;
             int batch = amg ? 8 : 32;
             const long long cap = std::max<long long>(100000, 20LL * N);
@@ -1746,9 +1859,19 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
                 for (int k = 0; k < batch; ++k, ++it) {
                     if (tail) {
                         if (amg && (prc = precondition()) != XFK_OK) return prc;
-                        k_hc_spmv<<<Gcg, kCgBlock, 0, s>>>(H, (int)(it & 1));   // iteration it - 1's
+                        if ((prc = spmv((int)(it & 1))) != XFK_OK) return prc;   // iteration it - 1's
                     }
-                    if (amg) k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, Gcg, it == 0 ? Gcg : Gax);
+                    if (comm) {
+                        // every partial array is read over all G entries (zero
+                        // beyond a rank's grids); the init's gamma / |r|^2 arrays
+                        // (k_hc_init grid) are next written by the update (its own
+                        // grid): cleared once the first update has read them
+                        k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, G, G);
+                        if (it == 0) {
+                            XFK_CHECK(hipMemsetAsync(P->hc_part.p, 0, sizeof(double) * 2 * G, s));
+                            XFK_CHECK(hipMemsetAsync(P->hc_part.p + 6 * (size_t)G, 0, sizeof(double) * G, s));
+                        }
+                    } else if (amg) k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, Gcg, it == 0 ? Gcg : Gax);
                     else k_hc_axpy<<<Gax, kHcAxBlock, 0, s>>>(H, it, it == 0 ? Gcg : Gax, it == 0 ? Gcg : Gax);
                     tail = true;
                 }
@@ -2029,6 +2152,11 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
             sx += hp[k];
             sy += hp[kResGrid + k];
         }
+        if (comm) {   // over every rank's owned rows
+            int rrc = allreduce_host(P, sx);
+            if (rrc == XFK_OK) rrc = allreduce_host(P, sy);
+            if (rrc != XFK_OK) return rrc;
+        }
         if (sy == 0) break;
         lastres = resn;
         resn = std::sqrt(sx / sy);
@@ -2060,7 +2188,7 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     R.newton_iters = iter + 1;
     R.cg_iters = cg_total;
     R.final_er = P->hc_host->er;
-    R.nnz = P->nnz;
+    R.nnz = P->nnz_own;
     R.ncolors = P->ncolors;
     R.color_rounds = P->color_rounds;
     R.precond = amg ? XFK_PRECOND_AMG : XFK_PRECOND_JACOBI;
@@ -2079,12 +2207,33 @@ int xfk_get_solution_complex(xfk_problem *P, double *A)
     XFK_REQUIRE(P && A && P->harmonic, XFK_ERR_ARG, "null argument or not a harmonic problem");
     XFK_REQUIRE(P->symbolic_ready && P->hc_vec.p, XFK_ERR_ARG, "no solution yet");
     XFK_CHECK(hipSetDevice(P->device));
-    XFK_CHECK(d2h(A, P->hc_vec.p, sizeof(double2) * P->N, P->stream));
+    hipStream_t s = P->stream;
+    const int Ng = P->N_global;
+    if (!P->comm) {
+        XFK_CHECK(d2h(A, P->hc_vec.p, sizeof(double2) * P->N, s));
+    } else {   // sharded: all-gather the owned rows (padded to the largest block), collective
+        const int R = P->nranks;
+        size_t maxn = 0;
+        for (int q = 0; q < R; ++q) maxn = std::max<size_t>(maxn, row_begin(Ng, q + 1, R) - row_begin(Ng, q, R));
+        XFK_CHECK(P->gather_buf.alloc(2 * maxn * (1 + R)));
+        double *send = P->gather_buf.p, *recv = P->gather_buf.p + 2 * maxn;
+        XFK_CHECK(hipMemsetAsync(send, 0, sizeof(double) * 2 * maxn, s));
+        XFK_CHECK(hipMemcpyAsync(send, P->hc_vec.p, sizeof(double2) * P->N, hipMemcpyDeviceToDevice, s));
+        const int rc = P->comm->allgather(send, recv, 2 * maxn, s);
+        if (rc != XFK_OK) return rc;
+        std::vector<double> h(2 * maxn * R);
+        XFK_CHECK(d2h(h.data(), recv, sizeof(double) * h.size(), s));
+        for (int q = 0; q < R; ++q) {
+            const long long r0 = row_begin(Ng, q, R), r1 = row_begin(Ng, q + 1, R);
+            for (long long i = r0; i < r1; ++i)
+                for (int c = 0; c < 2; ++c) A[2 * i + c] = h[2 * ((size_t)q * maxn + (i - r0)) + c];
+        }
+    }
     if (P->axi) {   // the flux 2 pi r A (harmonicaxi.cpp:790)
-        for (int i = 0; i < P->N; ++i)
+        for (int i = 0; i < Ng; ++i)
             for (int q = 0; q < 2; ++q) A[2 * i + q] = A[2 * i + q] * kC * 2. * kPI * P->axi_x[i] * 0.01;
     } else {
-        for (int i = 0; i < 2 * P->N; ++i) A[i] *= kC;   // harmonic2d.cpp:783
+        for (long long i = 0; i < 2LL * Ng; ++i) A[i] *= kC;   // harmonic2d.cpp:783
     }
     return XFK_OK;
 }
@@ -2108,12 +2257,12 @@ int xfk_get_csr_complex(xfk_problem *P, int *rowptr, int *col, double *val, doub
     hipStream_t s = P->stream;
     XFK_CHECK(hipStreamSynchronize(s));
     if (rowptr) XFK_CHECK(d2h(rowptr, P->rowptr.p, sizeof(int) * (P->N + 1), s));
-    if (col) XFK_CHECK(d2h(col, P->col.p, sizeof(int) * P->nnz, s));
+    if (col) XFK_CHECK(d2h(col, P->col.p, sizeof(int) * P->nnz_own, s));
     if (val) {
-        std::vector<double> re(P->nnz), im(P->nnz);
-        XFK_CHECK(d2h(re.data(), P->val.p, sizeof(double) * P->nnz, s));
-        XFK_CHECK(d2h(im.data(), P->val_im.p, sizeof(double) * P->nnz, s));
-        for (long long k = 0; k < P->nnz; ++k) {
+        std::vector<double> re(P->nnz_own), im(P->nnz_own);
+        XFK_CHECK(d2h(re.data(), P->val.p, sizeof(double) * P->nnz_own, s));
+        XFK_CHECK(d2h(im.data(), P->val_im.p, sizeof(double) * P->nnz_own, s));
+        for (long long k = 0; k < P->nnz_own; ++k) {
             val[2 * k] = re[k];
             val[2 * k + 1] = im[k];
         }

@@ -260,6 +260,7 @@ struct xfk_problem {
     int N_global = 0, row0 = 0;
     std::vector<int> l2g;            // local node -> global node
     xfk::HaloPlan halo;              // slices of the node vectors exchanged with peers
+    xfk::HaloPlan halo2;             // the same for interleaved complex (double2) node vectors
     int Gpart = 0;                   // length of each per-block partial array (agreed by all ranks)
     xfk::TileSplit ts;               // sharded PCG SpMV: interior / boundary tiles (exchange overlap)
     int *hpin = nullptr;             // pinned scratch for small device -> host reads
@@ -521,6 +522,8 @@ int prepare_magdir(const xfk_problem_desc *d, GlobalPrep &G);
 int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *plan, int device, xfk_comm *comm,
                 xfk_problem **out);
 int build_symbolic(xfk_problem *P);
+// sum of a host scalar over the ranks of P's communicator (no-op on one device)
+int allreduce_host(xfk_problem *P, double &v);
 // the row-block plan of comm's rank (coupled nodes assembled on every rank)
 int plan_rank(const xfk_problem_desc *d, const GlobalPrep &G, xfk_comm *comm, PartPlan &plan);
 hipError_t d2h(void *dst, const void *src, size_t bytes, hipStream_t s);

@@ -44,7 +44,8 @@ EXPORTED = (
     "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz", "xfk_spmv_col_bytes",
     "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_solve_csr_pc", "xfk_pcg_time", "xfk_phase_profile",
     "xfk_set_option",
-    "xfk_problem_create_harmonic", "xfk_harmonic2d", "xfk_get_solution_complex", "xfk_get_circuits_complex",
+    "xfk_problem_create_harmonic", "xfk_problem_create_harmonic_dist", "xfk_harmonic2d",
+    "xfk_get_solution_complex", "xfk_get_circuits_complex",
     "xfk_get_csr_complex",
     "xfk_comm_unique_id", "xfk_comm_create_rccl", "xfk_comm_create_local", "xfk_comm_destroy",
     "xfk_comm_rank", "xfk_comm_size", "xfk_comm_record", "xfk_comm_log", "xfk_comm_create_replay",
@@ -163,6 +164,8 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_phase_profile.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     L.xfk_set_option.argtypes = [C.c_void_p, C.c_int, C.c_double]
     L.xfk_problem_create_harmonic.argtypes = [C.POINTER(ProblemDesc), C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+    L.xfk_problem_create_harmonic_dist.argtypes = [C.POINTER(ProblemDesc), C.c_void_p, C.c_int, C.c_void_p,
+                                                   C.POINTER(C.c_void_p)]
     L.xfk_harmonic2d.argtypes = [C.c_void_p, C.c_int, C.POINTER(Result)]
     L.xfk_get_solution_complex.argtypes = [C.c_void_p, dptr]
     L.xfk_get_circuits_complex.argtypes = [C.c_void_p, iptr, dptr, dptr]
@@ -498,11 +501,14 @@ class Harmonic2DProblem:
                  lines: Sequence[dict] = (), points: Sequence[dict] = (), circuits: Sequence[dict] = (),
                  marker=None, e=None, pbc=None, precision=1e-8, length_units=0, coords=0, relax=1.0, device=0,
                  problem_type: int = 0, ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0,
-                 precond: str = "amg", ages: Sequence[dict] = (), ac_solver: int = 0):
+                 precond: str = "amg", ages: Sequence[dict] = (), ac_solver: int = 0,
+                 comm: Optional["Comm"] = None):
         """precond: "amg" (V-cycle of the real SPD surrogate Re A +- Im A, the
         sign making Im A positive semi-definite, applied to the real and
         imaginary parts; default) or "jacobi" (complex Jacobi).  ac_solver:
-        [ACSolver], 0 successive approximation, 1 Newton (KludgeSolve)."""
+        [ACSolver], 0 successive approximation, 1 Newton (KludgeSolve).
+        comm: shard the rows over this communicator, as Static2DProblem does
+        (xfk_problem_create_harmonic_dist); solution() gathers the whole field."""
         L = load_library()
         D, keep = _make_desc(x, y, p, lbl, blocks, labels, lines, points, circuits, marker, e, pbc, precision,
                              length_units, coords, relax, problem_type, (ext_zo, ext_ro, ext_ri), ages)
@@ -530,11 +536,15 @@ class Harmonic2DProblem:
         self._keep = keep
         self.n_nodes = D.n_nodes
         self.n_circs = len(circuits)
-        self.n_rows = self.n_nodes
         h = C.c_void_p()
-        _check(L.xfk_problem_create_harmonic(C.byref(D), C.byref(H), device, C.byref(h)))
+        self.comm = comm
+        if comm is None:
+            _check(L.xfk_problem_create_harmonic(C.byref(D), C.byref(H), device, C.byref(h)))
+        else:
+            _check(L.xfk_problem_create_harmonic_dist(C.byref(D), C.byref(H), device, comm._h, C.byref(h)))
         self._h = h
         _check(L.xfk_set_option(self._h, XFK_OPT_PRECOND, float(PRECONDS[precond])))
+        self.n_rows = self.dist_info()["n_own"] if comm is not None else self.n_nodes
         self.result: Optional[Result] = None
 
     def solve(self, rebuild_symbolic: bool = False) -> dict:
@@ -542,6 +552,11 @@ class Harmonic2DProblem:
         _check(_lib.xfk_harmonic2d(self._h, XFK_REBUILD_SYMBOLIC if rebuild_symbolic else 0, C.byref(r)))
         self.result = r
         return r.as_dict()
+
+    def dist_info(self) -> dict:
+        info = DistInfo()
+        _check(_lib.xfk_dist_get_info(self._h, C.byref(info)))
+        return info.as_dict()
 
     def solution(self) -> np.ndarray:
         A = np.zeros(2 * self.n_nodes)
@@ -559,10 +574,10 @@ class Harmonic2DProblem:
 
     def csr(self):
         nnz = _lib.xfk_get_nnz(self._h)
-        rp = np.zeros(self.n_nodes + 1, np.int32)
+        rp = np.zeros(self.n_rows + 1, np.int32)
         col = np.zeros(nnz, np.int32)
         val = np.zeros(2 * nnz)
-        b = np.zeros(2 * self.n_nodes)
+        b = np.zeros(2 * self.n_rows)
         _check(_lib.xfk_get_csr_complex(self._h, rp.ctypes.data_as(iptr), col.ctypes.data_as(iptr),
                                         val.ctypes.data_as(dptr), b.ctypes.data_as(dptr)))
         return rp, col, val[0::2] + 1j * val[1::2], b[0::2] + 1j * b[1::2]
