@@ -342,7 +342,10 @@ __global__ void k_mis_max(int n, const int *__restrict__ rowptr, ColView cv,
 // within distance 2 leaves
 // ROOTS (the last round of a batch): every row also writes its root flag
 // (k_agg_roots folded in: one launch less per level)
-template <int G, bool ROOTS = false>
+// PROMOTE (the last round of a capped aggregation, XFK_MIS_CAP): a row still
+// undecided after it becomes a root itself -- its aggregate may then border
+// another root's, the set is no longer distance-2 independent there
+template <int G, bool ROOTS = false, bool PROMOTE = false>
 __global__ void k_mis_update(int n, const int *__restrict__ rowptr, ColView cv,
                              const unsigned char *__restrict__ sflag, const MisKey *__restrict__ t1,
                              MisKey *__restrict__ key, const int *prev, int *undecided, int *__restrict__ flag,
@@ -370,6 +373,9 @@ __global__ void k_mis_update(int n, const int *__restrict__ rowptr, ColView cv,
         root = 1;
     } else if (key_st(m) == kStIn) {
         key[i] = key_low(k);
+    } else if (PROMOTE) {
+        key[i] = (kStIn << 30) | key_low(k);
+        root = 1;
     } else {
         *undecided = 1;   // benign race: every writer stores 1
     }
@@ -2790,11 +2796,38 @@ static int rmv_mode()
     return v;
 }
 
-// level 0 with f32 values: the 256-row tile kernels (level 0 always has >= kTileMinRows rows)
+// rows per tile of level 0's restriction R r (XFK_R0_TILE: 256, 128 or 64):
+// R has ~25 entries per row, so a 256-row tile streams ~6400 of them and the
+// 548 tiles of configs[2] run as one partial round over 256 CUs; smaller
+// tiles give more, shorter workgroups in flight per CU
+static int r0_tile()
+{
+    static const int v = [] {
+        const char *e = std::getenv("XFK_R0_TILE");
+        const int t = e ? std::atoi(e) : 256;
+        return (t == 64 || t == 128) ? t : 256;
+    }();
+    return v;
+}
+
+// level 0 with f32 values: the tile kernels (level 0 always has >= kTileMinRows
+// rows); tb: rows per tile (256; the restriction: r0_tile(), matching its c16 tiles)
 void launch_mv32(hipStream_t s, int n, const int *rowptr, const int *col, const float *val, const double *x,
-                 double *y, bool acc, int G, const int *done, const unsigned short *c16, const int *cbase)
+                 double *y, bool acc, int G, const int *done, const unsigned short *c16, const int *cbase,
+                 int tb = 256)
 {
     if (n <= 0) return;
+    if (tb != 256 && G > 4) {   // 7 slots: one staging pass for rows of up to ~28 entries
+        const int g = (n + tb - 1) / tb;
+        if (tb == 128) {
+            if (acc) k_csr_mv_tile<128, true, 7><<<g, 128, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+            else k_csr_mv_tile<128, false, 7><<<g, 128, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+        } else {
+            if (acc) k_csr_mv_tile<64, true, 7><<<g, 64, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+            else k_csr_mv_tile<64, false, 7><<<g, 64, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+        }
+        return;
+    }
     const int g = (n + 255) / 256;
     if (G <= 4) {
         if (acc) k_csr_mv_tile<256, true, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
@@ -3031,6 +3064,14 @@ static int to_f32(hipStream_t s, int n, const int *rowptr, long long cap, const 
     return XFK_OK;
 }
 
+// XFK_MIS_CAP=k (lab): at most k MIS-2 rounds per level, the rows still
+// undecided after the k-th become roots (0: rounds until the set is maximal)
+static int mis_cap()
+{
+    const char *e = std::getenv("XFK_MIS_CAP");
+    return e ? std::max(0, std::atoi(e)) : 0;
+}
+
 // XFK_MIS_XCD=0: MIS-2 sweeps with round-robin blocks (measurement)
 static bool mis_xcd_on()
 {
@@ -3262,11 +3303,27 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     bool joined = false;
     auto joins_and_p = [&]() { return joins_and_p_impl(s, l); };
     AMG_CHECK(mis_out.alloc(4));
+    const int cap = dist ? 0 : mis_cap();
     for (int batch = hint != mis_hint.end() ? std::max(1, hint->second) : 12;; batch = 2) {
+        if (cap > 0) batch = std::min(batch, cap);
         for (int b = 0; b < batch; ++b, ++rounds) {
             int *cur = und2 + (rounds & 1), *prev = und2 + ((rounds + 1) & 1);
             const bool last = b + 1 == batch;   // its update also writes the root flags
             const int xc = mis_xcd_on() ? 1 : 0;
+            if (last && cap > 0) {   // the capped set's last round promotes what is left
+                if (A.nnz > 9LL * n) {
+                    k_mis_max<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run,
+                                                             act.p, xc);
+                    k_mis_update<4, true, true><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p,
+                                                                            prev, cur, flag.p, xc);
+                } else {
+                    k_mis_max<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run, act.p,
+                                                      xc);
+                    k_mis_update<1, true, true><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev,
+                                                                      cur, flag.p, xc);
+                }
+                continue;
+            }
             if (A.nnz > 9LL * n) {
                 k_mis_max<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run,
                                                          act.p, xc);
@@ -3336,9 +3393,13 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         AMG_CHECK(hipEventRecord(sw.b, sw.cs));
         rt_pending = true;
     }
-    if (l == 0 && A.has16 && !dist &&
-        (rc = build_col16<256>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)) != XFK_OK)
-        return rc;
+    if (l == 0 && A.has16 && !dist) {   // (tiles of the restriction's launch)
+        const int tb = A.has32 ? r0_tile() : 256;
+        rc = tb == 64    ? build_col16<64>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)
+             : tb == 128 ? build_col16<128>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)
+                         : build_col16<256>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b);
+        if (rc != XFK_OK) return rc;
+    }
     if (l == 0 && A.has32 &&
         ((rc = to_f32(ts, (int)nc, A.rrow.p, A.pnnz, A.rval.p, A.r32)) != XFK_OK ||
          (f32_sweep_on() && (rc = to_f32(ts, n, A.rowptr, A.nnz, A.val, A.a32)) != XFK_OK)))
@@ -4548,7 +4609,7 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     const long long rnnz = A.pnnz;
     XFK_PHASE(lv + "restriction R r", A.nz_bytes() * rnnz + 4.0 * (A.nc + 1) + 8.0 * A.n + 8.0 * A.nc,
               (A.has32 ? launch_mv32(s, A.nc, A.rrow.p, A.rcol.p, A.r32.p, A.r.p, C.b.p, false,
-                                     lanes_for((double)rnnz / A.nc), done, A.r16.p, A.r16b.p)
+                                     lanes_for((double)rnnz / A.nc), done, A.r16.p, A.r16b.p, r0_tile())
                        : launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false,
                                    lanes_for((double)rnnz / A.nc), done, A.has16 ? A.r16.p : nullptr,
                                    A.has16 ? A.r16b.p : nullptr)));
