@@ -14,10 +14,12 @@
 #include "xfk_spmv.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <set>
 #include <type_traits>
 #include <unordered_map>
@@ -1151,6 +1153,8 @@ namespace xfk {
 // problem creation: validation, global preparation, local (per-rank) build
 // ----------------------------------------------------------------------------
 
+bool edge_lines_used(const xfk_problem_desc *d, std::vector<char> &used);
+
 int validate_desc(const xfk_problem_desc *d)
 {
     XFK_REQUIRE(d->n_nodes > 0 && d->n_elems > 0, XFK_ERR_ARG, "empty mesh");
@@ -1166,10 +1170,18 @@ int validate_desc(const xfk_problem_desc *d)
     XFK_REQUIRE(d->problem_type == XFK_PLANAR || d->problem_type == XFK_AXISYMMETRIC, XFK_ERR_ARG,
                 "problem type must be planar or axisymmetric");
     const int N = d->n_nodes, NE = d->n_elems;
-    for (long long i = 0; i < 3LL * NE; ++i)
-        XFK_REQUIRE(d->p[i] >= 0 && d->p[i] < N, XFK_ERR_ARG, "element node index out of range");
-    for (int i = 0; i < NE; ++i)
-        XFK_REQUIRE(d->lbl[i] >= 0 && d->lbl[i] < d->n_labels, XFK_ERR_ARG, "element label out of range");
+    // the per-element checks in parallel chunks; failures are reported in the
+    // order of the checks
+    std::atomic<int> bad{0};
+    const int NL = d->n_labels;
+    host_par_for(NE, 1 << 17, [&](long long a, long long b) {
+        bool okp = true, okl = true;
+        for (long long k = 3 * a; k < 3 * b; ++k) okp &= (unsigned)d->p[k] < (unsigned)N;
+        for (long long i = a; i < b; ++i) okl &= (unsigned)d->lbl[i] < (unsigned)NL;
+        if (!okp || !okl) bad |= (okp ? 0 : 1) | (okl ? 0 : 2);
+    });
+    XFK_REQUIRE(!(bad & 1), XFK_ERR_ARG, "element node index out of range");
+    XFK_REQUIRE(!(bad & 2), XFK_ERR_ARG, "element label out of range");
     for (int k = 0; k < d->n_labels; ++k) {
         XFK_REQUIRE(d->labels[k].block >= 0 && d->labels[k].block < d->n_blocks, XFK_ERR_ARG,
                     "label block index out of range");
@@ -1189,18 +1201,38 @@ int validate_desc(const xfk_problem_desc *d)
         // the device packs an element's three edge properties in 10-bit fields
         // of the properties the mesh uses (prepare_global compacts the table):
         // at most 1022 distinct ones on edges, any number defined
-        std::vector<char> used(std::max(1, d->n_lines), 0);
-        int nused = 0;
-        for (long long i = 0; i < 3LL * NE; ++i) {
-            XFK_REQUIRE(d->e[i] < d->n_lines, XFK_ERR_ARG, "edge boundary-property index out of range");
-            if (d->e[i] >= 0 && !used[d->e[i]]) {
-                used[d->e[i]] = 1;
-                ++nused;
-            }
-        }
+        std::vector<char> used;
+        XFK_REQUIRE(edge_lines_used(d, used), XFK_ERR_ARG, "edge boundary-property index out of range");
+        long long nused = 0;
+        for (char u : used) nused += u;
         XFK_REQUIRE(nused <= 1022, XFK_ERR_UNSUPPORTED, "at most 1022 distinct boundary properties on element edges");
     }
     return XFK_OK;
+}
+
+// used[k] = 1 for the boundary properties some element edge carries; false
+// when an edge index is >= n_lines
+bool edge_lines_used(const xfk_problem_desc *d, std::vector<char> &used)
+{
+    const int nl = std::max(1, d->n_lines);
+    const long long n3 = 3LL * d->n_elems;
+    used.assign(nl, 0);
+    if (!d->e) return true;
+    std::mutex mu;
+    std::atomic<bool> ok{true};
+    host_par_for(n3, 1 << 18, [&](long long a, long long b) {
+        std::vector<char> u(nl, 0);
+        bool good = true;
+        for (long long k = a; k < b; ++k) {
+            const int e = d->e[k];
+            good &= e < d->n_lines;
+            if (e >= 0 && e < d->n_lines) u[e] = 1;
+        }
+        if (!good) ok = false;
+        std::lock_guard<std::mutex> g(mu);
+        for (int q = 0; q < nl; ++q) used[q] |= u[q];
+    });
+    return ok;
 }
 
 int check_device(int device)
@@ -1300,16 +1332,18 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
     }
     // boundary properties used on element edges, compacted (the 10-bit edge
     // fields index this table; validate_desc bounds its size)
+    // (ascending property index; validate_desc checked the indices)
     G.lmap.assign(std::max(1, d->n_lines), -1);
     G.lin_used.clear();
-    if (d->e)
-        for (long long i = 0; i < 3LL * NE; ++i) {
-            const int k = d->e[i];
-            if (k >= 0 && G.lmap[k] < 0) {
+    if (d->e) {
+        std::vector<char> used;
+        edge_lines_used(d, used);
+        for (int k = 0; k < (int)used.size(); ++k)
+            if (used[k]) {
                 G.lmap[k] = (int)G.lin_used.size();
                 G.lin_used.push_back(k);
             }
-        }
+    }
     G.lin.assign(std::max<size_t>(1, G.lin_used.size()), DevLine{});
     for (size_t m = 0; m < G.lin_used.size(); ++m) {
         const xfk_line_desc &l = d->lines[G.lin_used[m]];
@@ -1323,8 +1357,18 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
     G.ext_ri = d->ext_ri * units[d->length_units];
     G.ext_zo = d->ext_zo * units[d->length_units];
     // which elements are nonlinear -> LinearFlag (static2d.cpp:633-639)
-    for (int i = 0; i < NE && !G.any_nonlinear; ++i)
-        if (G.blk[G.lab[d->lbl[i]].blk].BHpoints != 0) G.any_nonlinear = true;
+    {
+        std::vector<char> lnl(d->n_labels);
+        bool any = false;
+        for (int k = 0; k < d->n_labels; ++k) any |= (lnl[k] = G.blk[G.lab[k].blk].BHpoints != 0) != 0;
+        std::atomic<bool> hit{false};
+        if (any)
+            host_par_for(NE, 1 << 18, [&](long long a, long long b) {
+                for (long long i = a; i < b && !hit.load(std::memory_order_relaxed); ++i)
+                    if (lnl[d->lbl[i]]) hit = true;
+            });
+        G.any_nonlinear = hit;
+    }
 
     // circuits, element order (static2d.cpp:84-167)
     G.circ.assign(std::max(1, d->n_circs), DevCirc{});
@@ -1368,11 +1412,29 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
     // edges -> packed 3 x 10-bit boundary-property indices
     auto edge = [&](long long k) { return d->e ? d->e[k] : -1; };
     G.ebits.assign(NE, 0);
-    for (int i = 0; i < NE; ++i)
-        for (int j = 0; j < 3; ++j) {
-            int ej = edge(3LL * i + j);
-            if (ej >= 0) G.ebits[i] |= (G.lmap[ej] + 1) << (10 * j);
-        }
+    // elements with a prescribed-A (format 0) edge, in element order (the
+    // SetValue pass below visits only them)
+    std::vector<int> dir_elems;
+    if (d->e) {
+        const int nch = 64;
+        std::vector<std::vector<int>> part(nch);
+        host_par_for(nch, 1, [&](long long a, long long b) {
+            for (long long c = a; c < b; ++c)
+                for (long long i = NE * c / nch; i < NE * (c + 1) / nch; ++i) {
+                    unsigned bits = 0;
+                    bool dir = false;
+                    for (int j = 0; j < 3; ++j) {
+                        const int ej = d->e[3 * i + j];
+                        if (ej < 0) continue;
+                        bits |= (unsigned)(G.lmap[ej] + 1) << (10 * j);
+                        dir |= d->lines[ej].format == 0;
+                    }
+                    G.ebits[i] = (int)bits;
+                    if (dir) part[c].push_back((int)i);
+                }
+        });
+        for (auto &v : part) dir_elems.insert(dir_elems.end(), v.begin(), v.end());
+    }
 
     // point currents and Dirichlet values in the reference's SetValue order
     G.fixed.assign(N, 0);
@@ -1399,7 +1461,7 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
         else if (m >= 0 && d->points[m].J_re == 0 && d->points[m].J_im == 0)
             set_value(i, d->points[m].A_re / c);
     }
-    for (int i = 0; i < NE; ++i)
+    for (int i : dir_elems)
         for (int j = 0; j < 3; ++j) {
             int k = (j + 1) % 3;
             int sgi = edge(3LL * i + j);

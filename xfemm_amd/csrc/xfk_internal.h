@@ -18,8 +18,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/xfemm_kernels.h"
@@ -206,6 +208,23 @@ struct TileSplit {
 };
 // host-synchronising (once per operator)
 int build_tile_split(hipStream_t s, int n, int B, const int *rowptr, const int *col, TileSplit &ts);
+// f(begin, end) over [0, n) in contiguous chunks on up to 16 host threads
+// (one chunk below 2 min_per_thread items); the problem-creation loops over
+// the mesh (validation, boundary preparation) are independent per item
+template <class F>
+void host_par_for(long long n, long long min_per_thread, F f)
+{
+    const long long hw = std::max(1u, std::thread::hardware_concurrency());
+    const int T = (int)std::max(1LL, std::min({std::min(hw, 16LL), n / std::max(1LL, min_per_thread)}));
+    if (T <= 1) {
+        f(0LL, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back([&, t] { f(n * t / T, n * (t + 1) / T); });
+    f(0LL, n / T);
+    for (auto &x : th) x.join();
+}
 // Process-wide pool of non-blocking streams on the current device: creating a
 // HIP stream costs ~4 ms on MI355X (a hardware queue), so a problem returns its
 // streams here when it is destroyed and the next problem takes them back.
