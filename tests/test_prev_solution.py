@@ -47,6 +47,26 @@ def test_prev_mesh_comes_from_the_ans(tmp_path):
     assert pr2.bdrys[0].BdryFormat == 4
 
 
+def test_prev_mesh_native_loader_matches(tmp_path):
+    """The product's FSolver (libxfemm_fsolver.so, host part: no GPU) reads the
+    same mesh back from the .ans as the restatement: nodes, elements with edge
+    property 0, labels, periodic pairs."""
+    from xfemm_amd import fsolver
+    pr, mesh, A, base2 = _prev_case(tmp_path)
+    _, mesh2, _ = femfile.load_problem(base2, with_prev=True)
+    fs = fsolver.FSolver(delete_mesh_files=False)
+    fs.PathName = base2
+    assert fs.LoadProblemFile(), fs.last_error()
+    assert fs.LoadMesh(), fs.last_error()
+    x, y, mk = fs.nodes()
+    p, lbl, e = fs.elements()
+    assert np.array_equal(x, mesh2.x) and np.array_equal(y, mesh2.y) and np.array_equal(mk, mesh2.marker)
+    assert np.array_equal(np.asarray(p).reshape(-1, 3), mesh2.p)
+    assert np.array_equal(lbl, mesh2.lbl)
+    assert np.array_equal(np.asarray(e).reshape(-1, 3), mesh2.e)
+    assert np.array_equal(fs.pbcs(), mesh2.pbc)
+
+
 def test_prev_solve_reproduces_the_machine(tmp_path):
     deg = 30
     pr, mesh, A, base2 = _prev_case(tmp_path, deg)

@@ -201,6 +201,7 @@ bool FSolver::loadPreviousSolution(bool loadAprev)
         for (int q = 0; q < 3; q++)
             if (elm.p[q] < 0 || elm.p[q] >= NumNodes) return fail("element node");
         elm.blk = labellist[elm.lbl].BlockType;
+        meshele[i] = elm;
     }
     // block-label circuit lines: skipped
     int numLabels = 0;

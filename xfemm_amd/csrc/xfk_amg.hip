@@ -171,6 +171,7 @@ inline int nb_str(long long n) { return nb(n * kStrG); }
 __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double theta, const int *__restrict__ rowptr,
                                                      ColView cv, const double *__restrict__ val,
                                                      const double *__restrict__ absd,
+                                                     const double *__restrict__ dinv,
                                                      unsigned char *__restrict__ sflag, int *__restrict__ sdeg,
                                                      double *__restrict__ dfinv, double *__restrict__ wF,
                                                      double *__restrict__ rho_part, bool sgnd)
@@ -190,8 +191,11 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
         // gives each seam node such couplings to its partner's neighbours, an
         // air-gap element gives a few -- are weak and lumped, so no aggregate
         // spans an antiperiodic seam with a constant tentative value.
-        // (the matrices here are SPD: positive diagonals; sgnd == 0: |a_ij|,
-        // the former test, XFK_AMG_ABS_STRENGTH=1)
+        // The test follows the diagonal's sign: the static operators are SPD,
+        // the harmonic surrogate (Re A + s Im A of FEMM's sign convention) is
+        // negative definite -- the diagonal negative, the couplings positive.
+        // (sgnd == 0: |a_ij|, the former test, XFK_AMG_ABS_STRENGTH=1)
+        const double sg = dinv[i] < 0.0 ? -1.0 : 1.0;
         const int s = rowptr[i] + g, e = rowptr[i + 1];
         // a chunk of this lane's entries at a time: columns and values, then
         // their diagonals, loaded before the first use; the entries are then
@@ -226,10 +230,10 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
                 // peer's diagonal is not known here)
                 sumA += fabs(a);
                 lump += a;
-                hdeg += ((sgnd ? -a : fabs(a)) > theta * ai);
+                hdeg += ((sgnd ? -sg * a : fabs(a)) > theta * ai);
             } else {
                 sumA += fabs(a);
-                if (a != 0.0 && (sgnd ? -a : fabs(a)) > theta * sqrt(ai * dj[q])) {
+                if (a != 0.0 && (sgnd ? -sg * a : fabs(a)) > theta * sqrt(ai * dj[q])) {
                     f = 1;
                     ++deg;
                     sumS += fabs(a);
@@ -3822,7 +3826,7 @@ int Amg::build(hipStream_t s, int l0)
         AMG_CHECK(rho_part.alloc(2 * (size_t)nb_str(n)));
         k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr,
                                                 ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
-                                                A.val, absd.p, sflag.p, cnt.p,
+                                                A.val, absd.p, A.dinv.p, sflag.p, cnt.p,
                                                 dfinv.p, wF.p, rho_part.p, signed_strength());
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p + 2 * l);
         if (g_prof) g_prof->end();
@@ -4063,7 +4067,8 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
         AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(nl))));
         k_amg_diag<<<nb(nl), kB, 0, s>>>(nl, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
         k_amg_strength<<<nb_str(nl), kB, 0, s>>>(nl, nl, theta, A.rowptr, ColView{A.col, nullptr, nullptr}, A.val,
-                                                 absd.p, sflag.p, cnt.p, dfinv.p, wF.p, rho_part.p, signed_strength());
+                                                 absd.p, A.dinv.p, sflag.p, cnt.p, dfinv.p, wF.p, rho_part.p,
+                                                 signed_strength());
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(nl), rho_part.p, omega, rho.p + 2 * l);
         long long nc = 0;
         rc = aggregate(s, l, nc, false);
@@ -4768,7 +4773,7 @@ int Amg::refresh(hipStream_t s)
         k_amg_diag<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
         k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr,
                                                 ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
-                                                A.val, absd.p, sflag.p, cnt.p,
+                                                A.val, absd.p, A.dinv.p, sflag.p, cnt.p,
                                                 dfinv.p, wF.p, rho_part.p, signed_strength());
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p);
     }

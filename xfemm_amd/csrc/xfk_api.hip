@@ -804,6 +804,8 @@ static int allreduce_partials(xfk_problem *P, int narrays)
     return P->comm->allreduce_sum(P->part_loc.p, P->part_glob, (size_t)narrays * P->Gpart, P->stream);
 }
 
+static bool trace_newton() { return std::getenv("XFK_TRACE_NEWTON") != nullptr; }
+
 // AMG hierarchy of the assembled matrix (owned block when sharded); falls
 // back to Jacobi for this solve when the hierarchy cannot be built
 static int amg_setup(xfk_problem *P)
@@ -864,6 +866,7 @@ static int amg_setup(xfk_problem *P)
     ++P->setup_used;
     double ok = (rc == XFK_OK) ? 0.0 : 1.0;   // every rank must take the same preconditioner
     if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
+    if (rc != XFK_OK && trace_newton()) std::fprintf(stderr, "[newton] AMG setup declined: %s\n", xfk_last_error());
     int rc2 = allreduce_host(P, ok);
     if (rc2 != XFK_OK) return rc2;
     if (ok == 0.0) {
@@ -1932,6 +1935,11 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
             }
         }
         if ((resn < 100. * P->precision) && (Iter > 0)) LinearFlag = true;
+        if (trace_newton())   // lab: one line per Newton pass
+            std::fprintf(stderr, "[newton] pass %d: pcg %lld (%s%s, levels %d) res %.3e relax %.3f\n", Iter,
+                         (long long)P->pcg_host->iters, P->pc_used == XFK_PRECOND_AMG ? "amg" : "jacobi",
+                         P->pc_used == XFK_PRECOND_AMG ? (P->amg_fresh ? " fresh" : " reused") : "",
+                         (P->pc_used == XFK_PRECOND_AMG && P->amg) ? P->amg->stats.levels : 0, resn, Relax);
         Iter++;
         if (LinearFlag) break;
         if (Iter > 10000) {

@@ -1016,9 +1016,11 @@ __global__ void k_hc_surrogate(int N, double sgn, const int *__restrict__ rowptr
                                double *__restrict__ out)
 {
     // positive off-diagonal parts of sgn Im A (the consistent eddy-current
-    // mass) are lumped onto the diagonal: B stays SPD, within a factor of two
-    // of the unlumped surrogate, and keeps the M-matrix sign pattern the
-    // aggregation's strength test and the Jacobi smoother expect
+    // mass) are lumped onto the diagonal: B stays definite (negative definite
+    // in FEMM's sign convention: Re A has a negative diagonal and positive
+    // couplings), within a factor of two of the unlumped surrogate, and keeps
+    // the sign pattern the aggregation's strength test (relative to the
+    // diagonal's sign) and the Jacobi smoother expect
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     double lump = 0;
