@@ -1019,7 +1019,14 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
 // after this many iterations the residual ratio is still above 1e-4 (a
 // V-cycle preconditioner reaches 1e-8 in 20-30 on the meshes measured)
 constexpr int kF32Guard = 150;
-constexpr int kRetryF64 = 1;   // (internal return code of pcg_solve_once)
+constexpr int kRetryF64 = 1;   // (internal return codes of pcg_solve_once)
+// a hierarchy kept from an earlier Newton pass is abandoned for a fresh one
+// when this solve would take more than 3x + 16 the iterations of the pass that
+// built it (projected from the observed rate at each poll): the first
+// nonlinear pass can change the permeabilities from their initial values
+// enough to make the old hierarchy useless (the antiperiodic magnet machine:
+// 767 iterations on the kept one, 31 on a fresh one)
+constexpr int kRetryFresh = 2;
 
 static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
 {
@@ -1044,8 +1051,12 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
     // converged solve launches no iteration tail that would only exit
     // (one V-cycle + SpMV, ~14 launches, saved per solve)
     bool tail = false;   // iteration it - 1's V-cycle + SpMV not launched yet
+    const long long stale = (P->pc_used == XFK_PRECOND_AMG && !P->amg_fresh && P->amg_fresh_iters > 0)
+                                ? std::max<long long>(3LL * P->amg_fresh_iters, P->amg_fresh_iters + 16)
+                                : -1;
     for (;;) {
         batch = (int)std::max<long long>(1, std::min<long long>(batch, max_iters - it));
+        if (stale > 0 && it < stale) batch = (int)std::min<long long>(batch, stale - it);
         for (int k = 0; k < batch; ++k, ++it) {
             if (tail) {
                 const long long ip = it - 1;
@@ -1082,6 +1093,8 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
         // size the next batch from the observed convergence rate
         double rate = (S.iters > 0 && S.er > 0 && S.er < 1) ? std::log(S.er) / (double)S.iters : 0.0;
         long long rem = rate < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / rate) : 2 * batch;
+        // (S and the counts are the same on every rank: collective-safe)
+        if (stale > 0 && (S.iters >= stale || S.iters + rem > stale)) return kRetryFresh;
         rem = std::max<long long>(8, std::min<long long>(rem + 2, 512));
         batch = (int)rem;
     }
@@ -1091,12 +1104,27 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
 
 static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
 {
+    P->pcg_discarded = 0;
     int rc = pcg_solve_once(P, flag, max_iters);
+    if (rc == kRetryFresh) {   // a fresh hierarchy, the PCG restarted from the iterate
+        P->pcg_discarded = P->pcg_host->iters;
+        P->amg_reusable = false;
+        rc = pcg_solve_once(P, 1, max_iters);
+        if (rc == kRetryFresh) {
+            set_error("internal: fresh hierarchy retried twice");
+            return XFK_ERR_HIP;
+        }
+        if (rc != kRetryF64) {
+            P->pcg_host->iters += P->pcg_discarded;
+            return rc;
+        }
+    }
     if (rc != kRetryF64) return rc;
     // f64 transfers and coarsest inverse for the rest of this problem's life,
     // a fresh hierarchy, and the PCG restarted from the iterate (from zero if
     // it is not finite)
-    const long long first = P->pcg_host->iters;
+    const long long first = P->pcg_host->iters + P->pcg_discarded;
+    P->pcg_discarded = first;
     P->amg_f32 = 0;
     P->f64_fallback = true;
     P->amg_reusable = false;
@@ -1106,7 +1134,7 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
         f2 = 0;
     }
     rc = pcg_solve_once(P, f2, max_iters);
-    if (rc == kRetryF64) {   // (cannot repeat: no f32 part is left)
+    if (rc == kRetryF64 || rc == kRetryFresh) {   // (cannot repeat: no f32 part is left, the hierarchy is fresh)
         set_error("internal: f64 fallback requested twice");
         return XFK_ERR_HIP;
     }
@@ -1908,8 +1936,8 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
         R.ms_solve += ms;
         R.cg_iters += P->pcg_host->iters;
         R.final_er = P->pcg_host->er;
-        P->amg_last_iters = P->pcg_host->iters;
-        if (P->amg_fresh) P->amg_fresh_iters = P->pcg_host->iters;
+        P->amg_last_iters = P->pcg_host->iters - P->pcg_discarded;
+        if (P->amg_fresh) P->amg_fresh_iters = P->pcg_host->iters - P->pcg_discarded;
 
         if (!LinearFlag) {
             launch_newton_res(s, N, P->V.p, P->Vold.p, P->partials.p, P->counters.p + 3, P->nws.p);

@@ -405,6 +405,7 @@ struct xfk_problem {
     int amg_wlevel = -2;              // XFK_OPT_AMG_WLEVEL (-2: the default level)
     int amg_f32 = -1;                 // XFK_OPT_AMG_F32 (-1: on unless XFK_AMG_F32=0)
     bool f64_fallback = false;        // a stagnating PCG switched the f32 parts of the AMG to f64 (sticky)
+    long long pcg_discarded = 0;     // PCG iterations of this solve spent before a restart (stale hierarchy / f64)
     int amg_reuse = 1;
     bool amg_reusable = false;        // the hierarchy belongs to this solve's matrix pattern
     bool amg_fresh = false;           // built from scratch for the running PCG solve
