@@ -448,6 +448,12 @@ typedef struct {
 enum { XFK_PROFILE_SETUP = 1 };
 int xfk_phase_profile(xfk_problem *prob, int iters, int flags, xfk_phase *out, int cap, int *count);
 
+/* Diagnostics: device allocations of the library since the last reset, process
+ * wide -- out[0] hipMalloc calls, out[1] their host ms, out[2] hipFree calls,
+ * out[3] their host ms (a hipFree waits for the device).  reset != 0 zeroes
+ * the counters after reading. */
+int xfk_alloc_stats(double *out4, int reset);
+
 /* Magnetisation-direction function of a block label, evaluated for elements
  * as the reference's element loop does (FSolver::Static2D,
  * cfemm/fsolver/static2d.cpp:509-583; StaticAxisymmetric staticaxi.cpp:350-406):

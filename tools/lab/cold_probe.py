@@ -29,15 +29,22 @@ def main():
                                          kw.get("marker"), kw.get("e"), kw.get("pbc"), kw["precision"],
                                          kw["length_units"], kw.get("coords", 0), kw.get("relax", 1.0))
             t1 = time.perf_counter()
+            kernels.alloc_stats(reset=True)
             P = kernels.Static2DProblem(**kw)
             sync()
+            a_create = kernels.alloc_stats(reset=True)
             t2 = time.perf_counter()
             r1 = P.solve(rebuild_symbolic=True)
             sync()
+            a_first = kernels.alloc_stats(reset=True)
             t3 = time.perf_counter()
             r2 = P.solve(rebuild_symbolic=True)
             sync()
+            a_rep = kernels.alloc_stats(reset=True)
             t4 = time.perf_counter()
+            for tag, a in (("create", a_create), ("first", a_first), ("repeat", a_rep)):
+                print("  allocs %-6s: %d hipMalloc %.2f ms, %d hipFree %.2f ms"
+                      % (tag, a["n_malloc"], a["ms_malloc"], a["n_free"], a["ms_free"]), flush=True)
             print("cells %d rep %d: desc %.1f ms, create %.1f ms (incl. desc), first solve %.2f ms (setup %.2f, "
                   "symbolic %.2f, pcg %d), repeat %.2f ms (setup %.2f)"
                   % (n, rep, 1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (t3 - t2), r1["ms_amg_setup"],

@@ -7,6 +7,8 @@ bash tools/lab/variant_exp.sh r04h XFK_R0_TILE "256 128 64" --no-fsolver --steps
 bash tools/lab/variant_exp.sh r04h XFK_MIS_CAP "0 4 6 8" --no-fsolver --steps 10 --warmup 3 || exit 1
 XFK_MIS_CAP=6 timeout -k 10 300 python -u -m pytest tests/test_gpu_antiperiodic_flux.py tests/test_gpu_torque.py -v -s --timeout 150 --timeout-method thread > gpurun_out/iters_miscap6_r04h.log 2>&1
 echo "miscap6 iters rc=$?"
+XFK_AMG_DEBUG=1 timeout -k 10 120 python tools/lab/amg_probe.py 1000 --no-jacobi > gpurun_out/amgdebug_r04h.txt 2>&1
+echo "amg debug rc=$?"
 # rank 0 of 8 (configs[4]) replayed alone: kernel time per solve inside the timed window
 XFK_LAB_WINDOW=1 timeout -k 10 500 rocprofv3 --kernel-trace -T -f csv -d gpurun_out/prof_rank0_r04h -o run -- python3 tools/lab/rank0_probe.py --child --steps 3 > gpurun_out/rank0_trace_r04h.log 2>&1
 echo "rank0 trace rc=$?"

@@ -11,3 +11,5 @@ rc=$?; echo "anti rc=$rc"
 case $rc in 124|137|134|139) exit $rc;; esac
 timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/bench_r04k.json 2> gpurun_out/bench_r04k.err
 echo "bench rc=$?"
+XFK_TRACE_CREATE=1 timeout -k 10 300 python tools/lab/cold_probe.py 1000 > gpurun_out/cold_r04k.txt 2>&1
+echo "cold rc=$?"

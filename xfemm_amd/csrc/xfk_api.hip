@@ -50,6 +50,32 @@ struct CreateTrace {
 namespace xfk {
 
 static thread_local std::string g_err;
+
+// device allocation counters (xfk_alloc_stats)
+namespace {
+std::atomic<long long> g_nmalloc{0}, g_nfree{0}, g_nsmalloc{0}, g_nsfree{0};
+long long now_ns()
+{
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+}  // namespace
+
+hipError_t dev_malloc(void **p, size_t bytes)
+{
+    const long long t = now_ns();
+    const hipError_t e = hipMalloc(p, bytes);
+    g_nsmalloc += now_ns() - t;
+    ++g_nmalloc;
+    return e;
+}
+void dev_free(void *p)
+{
+    const long long t = now_ns();
+    (void)hipFree(p);
+    g_nsfree += now_ns() - t;
+    ++g_nfree;
+}
 thread_local PhaseProf *g_prof = nullptr;
 void set_error(const std::string &msg) { g_err = msg; }
 
@@ -1149,6 +1175,17 @@ using namespace xfk;
 extern "C" {
 
 const char *xfk_last_error(void) { return g_err.c_str(); }
+
+int xfk_alloc_stats(double *out4, int reset)
+{
+    XFK_REQUIRE(out4, XFK_ERR_ARG, "null argument");
+    out4[0] = (double)g_nmalloc.load();
+    out4[1] = 1e-6 * (double)g_nsmalloc.load();
+    out4[2] = (double)g_nfree.load();
+    out4[3] = 1e-6 * (double)g_nsfree.load();
+    if (reset) g_nmalloc = g_nfree = g_nsmalloc = g_nsfree = 0;
+    return XFK_OK;
+}
 
 int xfk_device_count(void)
 {

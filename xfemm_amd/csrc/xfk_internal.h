@@ -169,6 +169,10 @@ struct NewtonScalars {
 };
 
 // Small device buffer helper.
+// device allocations of the library (counted for xfk_alloc_stats)
+hipError_t dev_malloc(void **p, size_t bytes);
+void dev_free(void *p);
+
 template <class T>
 struct DBuf {
     T *p = nullptr;
@@ -179,16 +183,16 @@ struct DBuf {
     ~DBuf() { free(); }
     hipError_t alloc(size_t count) {
         if (count <= n && p) return hipSuccess;
-        if (p) (void)hipFree(p);
+        if (p) dev_free(p);
         p = nullptr;
         n = 0;
         if (count == 0) return hipSuccess;
-        hipError_t e = hipMalloc(&p, count * sizeof(T));
+        hipError_t e = dev_malloc(reinterpret_cast<void **>(&p), count * sizeof(T));
         if (e == hipSuccess) n = count;
         return e;
     }
     void free() {
-        if (p) (void)hipFree(p);
+        if (p) dev_free(p);
         p = nullptr;
         n = 0;
     }

@@ -43,6 +43,7 @@ EXPORTED = (
     "xfk_last_error", "xfk_age_element_matrix", "xfk_device_count", "xfk_problem_create", "xfk_problem_destroy",
     "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz", "xfk_spmv_col_bytes",
     "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_solve_csr_pc", "xfk_pcg_time", "xfk_phase_profile",
+    "xfk_alloc_stats",
     "xfk_set_option",
     "xfk_problem_create_harmonic", "xfk_problem_create_harmonic_dist", "xfk_harmonic2d",
     "xfk_get_solution_complex", "xfk_get_circuits_complex",
@@ -162,6 +163,7 @@ def load_library(path: str = KERNELS_SO):
                                        C.c_int, C.POINTER(C.c_longlong), dptr]
     L.xfk_pcg_time.argtypes = [C.c_void_p, C.c_int, dptr, dptr]
     L.xfk_phase_profile.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+    L.xfk_alloc_stats.argtypes = [dptr, C.c_int]
     L.xfk_set_option.argtypes = [C.c_void_p, C.c_int, C.c_double]
     L.xfk_problem_create_harmonic.argtypes = [C.POINTER(ProblemDesc), C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
     L.xfk_problem_create_harmonic_dist.argtypes = [C.POINTER(ProblemDesc), C.c_void_p, C.c_int, C.c_void_p,
@@ -195,6 +197,14 @@ def load_library(path: str = KERNELS_SO):
 def _check(rc: int):
     if rc != XFK_OK:
         raise XfkError("xfk error %d: %s" % (rc, _lib.xfk_last_error().decode()))
+
+
+def alloc_stats(reset: bool = False) -> dict:
+    """Device allocations of the library since the last reset (diagnostics):
+    hipMalloc / hipFree calls and their host milliseconds."""
+    out = np.zeros(4)
+    _check(load_library().xfk_alloc_stats(out.ctypes.data_as(dptr), int(reset)))
+    return dict(n_malloc=int(out[0]), ms_malloc=float(out[1]), n_free=int(out[2]), ms_free=float(out[3]))
 
 
 def device_count() -> int:
