@@ -1,12 +1,9 @@
-# A/B: level-0 restriction tile rows, capped MIS-2 rounds (configs[2] bench phases)
+# A/B: level-0 restriction tile rows (configs[2] bench phases)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 bash tools/lab/variant_exp.sh r04h XFK_R0_TILE "256 128 64" --no-fsolver --steps 10 --warmup 3 || exit 1
-bash tools/lab/variant_exp.sh r04h XFK_MIS_CAP "0 4 6 8" --no-fsolver --steps 10 --warmup 3 || exit 1
-XFK_MIS_CAP=6 timeout -k 10 300 python -u -m pytest tests/test_gpu_antiperiodic_flux.py tests/test_gpu_torque.py -v -s --timeout 150 --timeout-method thread > gpurun_out/iters_miscap6_r04h.log 2>&1
-echo "miscap6 iters rc=$?"
 XFK_AMG_DEBUG=1 timeout -k 10 120 python tools/lab/amg_probe.py 1000 --no-jacobi > gpurun_out/amgdebug_r04h.txt 2>&1
 echo "amg debug rc=$?"
 # rank 0 of 8 (configs[4]) replayed alone: kernel time per solve inside the timed window

@@ -346,10 +346,7 @@ __global__ void k_mis_max(int n, const int *__restrict__ rowptr, ColView cv,
 // within distance 2 leaves
 // ROOTS (the last round of a batch): every row also writes its root flag
 // (k_agg_roots folded in: one launch less per level)
-// PROMOTE (the last round of a capped aggregation, XFK_MIS_CAP): a row still
-// undecided after it becomes a root itself -- its aggregate may then border
-// another root's, the set is no longer distance-2 independent there
-template <int G, bool ROOTS = false, bool PROMOTE = false>
+template <int G, bool ROOTS = false>
 __global__ void k_mis_update(int n, const int *__restrict__ rowptr, ColView cv,
                              const unsigned char *__restrict__ sflag, const MisKey *__restrict__ t1,
                              MisKey *__restrict__ key, const int *prev, int *undecided, int *__restrict__ flag,
@@ -377,9 +374,6 @@ __global__ void k_mis_update(int n, const int *__restrict__ rowptr, ColView cv,
         root = 1;
     } else if (key_st(m) == kStIn) {
         key[i] = key_low(k);
-    } else if (PROMOTE) {
-        key[i] = (kStIn << 30) | key_low(k);
-        root = 1;
     } else {
         *undecided = 1;   // benign race: every writer stores 1
     }
@@ -3068,14 +3062,6 @@ static int to_f32(hipStream_t s, int n, const int *rowptr, long long cap, const 
     return XFK_OK;
 }
 
-// XFK_MIS_CAP=k (lab): at most k MIS-2 rounds per level, the rows still
-// undecided after the k-th become roots (0: rounds until the set is maximal)
-static int mis_cap()
-{
-    const char *e = std::getenv("XFK_MIS_CAP");
-    return e ? std::max(0, std::atoi(e)) : 0;
-}
-
 // XFK_MIS_XCD=0: MIS-2 sweeps with round-robin blocks (measurement)
 static bool mis_xcd_on()
 {
@@ -3307,27 +3293,11 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     bool joined = false;
     auto joins_and_p = [&]() { return joins_and_p_impl(s, l); };
     AMG_CHECK(mis_out.alloc(4));
-    const int cap = dist ? 0 : mis_cap();
     for (int batch = hint != mis_hint.end() ? std::max(1, hint->second) : 12;; batch = 2) {
-        if (cap > 0) batch = std::min(batch, cap);
         for (int b = 0; b < batch; ++b, ++rounds) {
             int *cur = und2 + (rounds & 1), *prev = und2 + ((rounds + 1) & 1);
             const bool last = b + 1 == batch;   // its update also writes the root flags
             const int xc = mis_xcd_on() ? 1 : 0;
-            if (last && cap > 0) {   // the capped set's last round promotes what is left
-                if (A.nnz > 9LL * n) {
-                    k_mis_max<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run,
-                                                             act.p, xc);
-                    k_mis_update<4, true, true><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p,
-                                                                            prev, cur, flag.p, xc);
-                } else {
-                    k_mis_max<1><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run, act.p,
-                                                      xc);
-                    k_mis_update<1, true, true><<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, t1.p, key.p, prev,
-                                                                      cur, flag.p, xc);
-                }
-                continue;
-            }
             if (A.nnz > 9LL * n) {
                 k_mis_max<4><<<nb(4LL * n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, t1.p, prev, cur, run,
                                                          act.p, xc);
