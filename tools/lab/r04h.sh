@@ -1,9 +1,13 @@
-# A/B: level-0 restriction tile rows (configs[2] bench phases)
+# A/B: level-0 restriction tile rows (configs[2] bench phases); rank 0 of 8 with / without
+# the sharded f32 transfers; rank-0 kernel trace
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 bash tools/lab/variant_exp.sh r04h XFK_R0_TILE "256 128 64" --no-fsolver --steps 10 --warmup 3 || exit 1
+timeout -k 10 500 python tools/lab/rank0_probe.py '' XFK_AMG_F32=0 > gpurun_out/rank0_f32_r04h.txt 2>&1
+rc=$?; echo "rank0 f32 A/B rc=$rc"
+case $rc in 124|137|134|139) exit $rc;; esac
 XFK_AMG_DEBUG=1 timeout -k 10 120 python tools/lab/amg_probe.py 1000 --no-jacobi > gpurun_out/amgdebug_r04h.txt 2>&1
 echo "amg debug rc=$?"
 # rank 0 of 8 (configs[4]) replayed alone: kernel time per solve inside the timed window

@@ -77,12 +77,14 @@ struct AmgLevel {
     // k_tile_col16): A and P~ in the 512-row tiles of the SpMV / sweeps /
     // folded post-step, R in the restriction's 256-row tiles
     bool has16 = false;
-    DBuf<unsigned short> a16, f16, r16;
-    DBuf<int> a16b, f16b, r16b;
+    DBuf<unsigned short> a16, f16, r16, p16;
+    DBuf<int> a16b, f16b, r16b, p16b;
     // level 0 (with has16): the V-cycle's transfers R and P~ with f32 values
-    // (products and sums in f64; A keeps f64 -- a32 only with XFK_AMG_F32_SWEEP=1)
+    // (products and sums in f64; A keeps f64 -- a32 only with XFK_AMG_F32_SWEEP=1);
+    // a sharded level 0 (unfolded) keeps R and P in f32, P with 16-bit
+    // columns in 256-row tiles (p16)
     bool has32 = false;
-    DBuf<float> a32, r32, f32v;
+    DBuf<float> a32, r32, f32v, p32;
     // stored bytes per nonzero of the level's V-cycle transfers (column + value)
     double nz_bytes() const { return (has16 ? 2.0 : 4.0) + (has32 ? 4.0 : 8.0); }
 };

@@ -3367,8 +3367,8 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         AMG_CHECK(hipEventRecord(sw.b, sw.cs));
         rt_pending = true;
     }
-    if (l == 0 && A.has16 && !dist) {   // (tiles of the restriction's launch)
-        const int tb = A.has32 ? r0_tile() : 256;
+    if (l == 0 && A.has16) {   // (tiles of the restriction's launch)
+        const int tb = (A.has32 && !dist) ? r0_tile() : 256;
         rc = tb == 64    ? build_col16<64>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)
              : tb == 128 ? build_col16<128>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)
                          : build_col16<256>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b);
@@ -3377,6 +3377,10 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     if (l == 0 && A.has32 &&
         ((rc = to_f32(ts, (int)nc, A.rrow.p, A.pnnz, A.rval.p, A.r32)) != XFK_OK ||
          (f32_sweep_on() && (rc = to_f32(ts, n, A.rowptr, A.nnz, A.val, A.a32)) != XFK_OK)))
+        return rc;
+    if (l == 0 && A.has32 && A.dist &&   // the sharded level 0 prolongs through P itself (no fold)
+        ((rc = to_f32(ts, n, A.prow.p, A.pnnz, A.pval.p, A.p32)) != XFK_OK ||
+         (rc = build_col16<256>(ts, n, A.prow.p, A.pcol.p, A.pnnz, A.p16, A.p16b)) != XFK_OK))
         return rc;
     if (g_prof) g_prof->end();
     return XFK_OK;
@@ -4022,6 +4026,8 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
         // more than 65535 columns and keeps the int columns, decided per tile)
         A.has16 = col16 < 0 ? col16_on() : col16 != 0;
         if (A.has16 && (rc = build_col16<kCgBlock>(s, n, rowptr, col, nnz, A.a16, A.a16b)) != XFK_OK) return rc;
+        // f32 restriction / prolongation (converted after the aggregation)
+        A.has32 = A.has16 && (prec32 < 0 ? f32_on() : prec32 != 0);
     }
     for (int l = 0;; ++l) {
         AmgLevel &A = *L[l];
@@ -4652,21 +4658,34 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
     AmgLevel &C = *L[l + 1];
     const int GR = lanes_for(A.nc > 0 ? (double)A.pnnz / A.nc : 1.0);
     const double *xc;
+    // level 0 with f32 transfers: R and P in f32 with 16-bit tile columns
+    auto restrict_to = [&](double *dst) {
+        if (A.has32)
+            launch_mv32(s, A.nc, A.rrow.p, A.rcol.p, A.r32.p, A.r.p, dst, false, GR, done, A.r16.p, A.r16b.p);
+        else
+            launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, dst, false, GR, done);
+    };
     if (C.dist) {
-        launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false, GR, done);
+        restrict_to(C.b.p);
         xc = vc_dist(s, l + 1, C.b.p, nullptr, done, rc);
         if (rc != XFK_OK) return nullptr;
     } else {
         // the replicated levels: gather the global right-hand side, solve the
         // same coarse problem on every rank, read the own aggregates back
-        launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, cb_loc.p, false, GR, done);
+        restrict_to(cb_loc.p);
         const int te = tail_begin(s, 0);
         if ((rc = comm->allgather(cb_loc.p, cb_all.p, (size_t)ncmax, s)) != XFK_OK) return nullptr;
         k_unpad<<<nb(C.n), kB, 0, s>>>(C.n, nranks, c0_dev.p, cb_all.p, ncmax, C.b.p, done);
         xc = vcycle_level(*this, s, l + 1, C.b.p, nullptr, done) + c0[rank];
         tail_end(s, te);
     }
-    if (A.n > 0) launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, lanes_for((double)A.pnnz / A.n), done);
+    if (A.n > 0) {
+        const int GP = lanes_for((double)A.pnnz / A.n);
+        if (A.has32)
+            launch_mv32(s, A.n, A.prow.p, A.pcol.p, A.p32.p, xc, cur, true, GP, done, A.p16.p, A.p16b.p);
+        else
+            launch_mv(s, A.n, A.prow.p, A.pcol.p, A.pval.p, xc, cur, true, GP, done);
+    }
     for (int k = 0; k < sweeps; ++k) {
         const bool last0 = k == sweeps - 1 && out && l == 0;
         double *nx = (k == sweeps - 1 && out) ? out : oth;
