@@ -320,22 +320,38 @@ def cold_first_solve(device, args, kw):
     The process's code objects are already loaded (it runs after the timed
     region)."""
     from xfemm_amd import kernels
-    _hip_sync()
-    t0 = time.perf_counter()
-    P = kernels.Static2DProblem(device=device, precond=args.precond, amg_sweeps=args.amg_sweeps,
-                                amg_omega=args.amg_omega, amg_dense=args.amg_dense, amg_theta=args.amg_theta, **kw)
-    _hip_sync()
-    t1 = time.perf_counter()
-    r = P.solve(rebuild_symbolic=True)
-    _hip_sync()
-    t2 = time.perf_counter()
-    n = P.n_nodes
-    P.close()
-    return {"value": n / (t2 - t1), "unit": "DoF/s", "ms_first_solve": 1e3 * (t2 - t1),
-            "ms_create_upload": 1e3 * (t1 - t0), "pcg_iters": r["cg_iters"], "ms_amg_setup": r["ms_amg_setup"],
-            "ms_symbolic": r["ms_symbolic"], "ms_assemble": r["ms_assemble"], "ms_solve": r["ms_solve"],
-            "note": "fresh problem object, first solve (no re-solve hints); ms_create_upload = host -> HBM "
-                    "upload of the mesh and tables (outside the step)"}
+
+    def one():
+        _hip_sync()
+        kernels.alloc_stats(reset=True)
+        t0 = time.perf_counter()
+        P = kernels.Static2DProblem(device=device, precond=args.precond, amg_sweeps=args.amg_sweeps,
+                                    amg_omega=args.amg_omega, amg_dense=args.amg_dense, amg_theta=args.amg_theta,
+                                    **kw)
+        _hip_sync()
+        t1 = time.perf_counter()
+        a_create = kernels.alloc_stats(reset=True)
+        r = P.solve(rebuild_symbolic=True)
+        _hip_sync()
+        t2 = time.perf_counter()
+        a_solve = kernels.alloc_stats(reset=True)
+        n = P.n_nodes
+        P.close()
+        return {"value": n / (t2 - t1), "unit": "DoF/s", "ms_first_solve": 1e3 * (t2 - t1),
+                "ms_create_upload": 1e3 * (t1 - t0), "pcg_iters": r["cg_iters"], "ms_amg_setup": r["ms_amg_setup"],
+                "ms_symbolic": r["ms_symbolic"], "ms_assemble": r["ms_assemble"], "ms_solve": r["ms_solve"],
+                "hip_malloc_create": a_create["n_malloc"], "hip_malloc_first_solve": a_solve["n_malloc"],
+                "ms_hip_malloc_first_solve": a_solve["ms_malloc"]}
+
+    first = one()
+    first["note"] = ("fresh problem object, first solve (no re-solve hints, no device blocks of a destroyed "
+                     "problem to reuse: the bench's own problem is still alive); ms_create_upload = host -> HBM "
+                     "upload of the mesh and tables (outside the step)")
+    second = one()
+    second["note"] = ("the next fresh problem of the same process (a session's next analysis, the next rotor "
+                      "angle): the previous one was destroyed, its device blocks come from the process cache")
+    first["next_problem_in_process"] = second
+    return first
 
 
 def _tag_order(path):

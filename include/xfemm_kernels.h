@@ -450,8 +450,10 @@ int xfk_phase_profile(xfk_problem *prob, int iters, int flags, xfk_phase *out, i
 
 /* Diagnostics: device allocations of the library since the last reset, process
  * wide -- out[0] hipMalloc calls, out[1] their host ms, out[2] hipFree calls,
- * out[3] their host ms (a hipFree waits for the device).  reset != 0 zeroes
- * the counters after reading. */
+ * out[3] their host ms (a hipFree waits for the device).  Blocks served from
+ * the process cache (what destroyed problems returned: xfk_problem_destroy
+ * keeps their device blocks for the next problem of the process) are not
+ * counted.  reset != 0 zeroes the counters after reading. */
 int xfk_alloc_stats(double *out4, int reset);
 
 /* Magnetisation-direction function of a block label, evaluated for elements

@@ -61,16 +61,108 @@ long long now_ns()
 }
 }  // namespace
 
+// Process-wide cache of device blocks.  A problem being destroyed (its main
+// stream synchronised; every side-stream task was joined into it) returns its
+// blocks here instead of to hipFree, and the next problem of the process --
+// the next rotor angle, the next .fem of a session -- takes them back instead
+// of calling hipMalloc (each call costs host time; each hipFree waits for the
+// device).  Blocks are rounded up to size classes (powers of two up to 64 KiB,
+// then sixteenth steps of the power of two: at most 6.25 % slack) and matched
+// by class and device; at most kPoolCap bytes stay cached.  Any other free (a
+// buffer that grows, a function's scratch) goes straight to hipFree: only the
+// destroy path knows the device no longer reads the block.
+namespace {
+constexpr size_t kPoolCap = 64ull << 30;
+struct BlockPool {
+    std::mutex mu;
+    std::map<std::pair<int, size_t>, std::vector<void *>> free;
+    std::unordered_map<void *, std::pair<int, size_t>> live;   // block -> (device, class bytes)
+    size_t cached = 0;
+};
+BlockPool &block_pool()
+{
+    static BlockPool *p = new BlockPool();   // (never destroyed: blocks outlive static destructors)
+    return *p;
+}
+thread_local bool tl_pool_release = false;
+std::atomic<long long> g_npool{0};
+size_t size_class(size_t b)
+{
+    if (b <= 256) return 256;
+    size_t p2 = 1;
+    while (p2 < b) p2 <<= 1;
+    if (p2 <= (64u << 10)) return p2;
+    const size_t step = (p2 >> 1) >> 4;   // sixteenths of the lower power of two
+    return ((b + step - 1) / step) * step;
+}
+}  // namespace
+
+// blocks freed inside its scope go to the process cache (the caller has
+// synchronised the device work that could read them)
+struct PoolRelease {
+    bool prev = tl_pool_release;
+    PoolRelease() { tl_pool_release = true; }
+    ~PoolRelease() { tl_pool_release = prev; }
+};
+
 hipError_t dev_malloc(void **p, size_t bytes)
 {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const size_t cls = size_class(bytes);
+    BlockPool &bp = block_pool();
+    {
+        std::lock_guard<std::mutex> g(bp.mu);
+        auto it = bp.free.find({dev, cls});
+        if (it != bp.free.end() && !it->second.empty()) {
+            *p = it->second.back();
+            it->second.pop_back();
+            bp.cached -= cls;
+            bp.live[*p] = {dev, cls};
+            ++g_npool;
+            return hipSuccess;
+        }
+    }
     const long long t = now_ns();
-    const hipError_t e = hipMalloc(p, bytes);
+    hipError_t e = hipMalloc(p, cls);
     g_nsmalloc += now_ns() - t;
     ++g_nmalloc;
+    if (e != hipSuccess) {   // out of memory with blocks cached: return them and try once more
+        std::vector<void *> drop;
+        {
+            std::lock_guard<std::mutex> g(bp.mu);
+            for (auto &kv : bp.free)
+                for (void *q : kv.second) drop.push_back(q);
+            bp.free.clear();
+            bp.cached = 0;
+        }
+        if (drop.empty()) return e;
+        for (void *q : drop) (void)hipFree(q);
+        (void)hipGetLastError();
+        e = hipMalloc(p, cls);
+    }
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> g(bp.mu);
+        bp.live[*p] = {dev, cls};
+    }
     return e;
 }
 void dev_free(void *p)
 {
+    BlockPool &bp = block_pool();
+    {
+        std::lock_guard<std::mutex> g(bp.mu);
+        auto it = bp.live.find(p);
+        if (it != bp.live.end()) {
+            const auto key = it->second;
+            bp.live.erase(it);
+            if (tl_pool_release && bp.cached + key.second <= kPoolCap) {
+                bp.free[key].push_back(p);
+                bp.cached += key.second;
+                return;
+            }
+        }
+    }
     const long long t = now_ns();
     (void)hipFree(p);
     g_nsfree += now_ns() - t;
@@ -1183,7 +1275,7 @@ int xfk_alloc_stats(double *out4, int reset)
     out4[1] = 1e-6 * (double)g_nsmalloc.load();
     out4[2] = (double)g_nfree.load();
     out4[3] = 1e-6 * (double)g_nsfree.load();
-    if (reset) g_nmalloc = g_nfree = g_nsmalloc = g_nsfree = 0;
+    if (reset) g_nmalloc = g_nfree = g_nsmalloc = g_nsfree = g_npool = 0;
     return XFK_OK;
 }
 
@@ -1208,8 +1300,11 @@ void xfk_problem_destroy(xfk_problem *P)
     if (P->nws_host) (void)hipHostFree(P->nws_host);
     if (P->hc_host) (void)hipHostFree(P->hc_host);
     hipStream_t s = P->stream;
-    delete P->amg;
-    delete P;   // device buffers free themselves (DBuf), on this device
+    {
+        PoolRelease pr;   // (main stream synchronised above, side-stream work joined into it)
+        delete P->amg;
+        delete P;   // device buffers free themselves (DBuf) into the process cache
+    }
     stream_release(s);   // (synchronised above; pooled for the next problem)
 }
 
