@@ -303,8 +303,8 @@ def fsolver_end_to_end(device, args):
                 if not ok:
                     raise RuntimeError("FSolver failed on %s: %s" % (name, fs.last_error()))
                 st, tm = fs.stats(), fs.times()
-                rec = {"workload": name, "dof": fs.NumNodes(), "ms_wall": 1e3 * dt,
-                       "dof_per_s_wall": fs.NumNodes() / dt, "pcg_iters": st["cg_iters"],
+                rec = {"workload": name, "dof": fs.NumNodes, "ms_wall": 1e3 * dt,
+                       "dof_per_s_wall": fs.NumNodes / dt, "pcg_iters": st["cg_iters"],
                        "ms_device_solve": st["ms_solve"] + st["ms_assemble"] + st["ms_symbolic"]}
                 rec.update(tm)
                 del fs

@@ -16,3 +16,10 @@ echo "rank0 trace rc=$?"
 T=$(find gpurun_out/prof_rank0_r04h -name "*kernel_trace.csv" | head -1)
 python3 tools/lab/trace_window.py "$T" gpurun_out/rank0_trace_r04h.log rank0 > gpurun_out/rank0_window_r04h.txt 2>&1
 rm -f "$T"
+# warm setup timeline (kernel trace of a short bench run): gaps between kernels
+bash tools/lab/trace_only.sh r04h --no-fsolver
+echo "trace rc=$?"
+T=$(find gpurun_out/prof_r04h/trace -name "*kernel_trace.csv" | head -1)
+python3 tools/lab/setup_tl.py "$T" --gaps > gpurun_out/setup_tl_r04h.txt 2>&1
+python3 tools/lab/setup_tl.py "$T" > gpurun_out/setup_tl_full_r04h.txt 2>&1
+echo "tl rc=$?"

@@ -181,9 +181,12 @@ struct DBuf {
     DBuf(const DBuf &) = delete;
     DBuf &operator=(const DBuf &) = delete;
     ~DBuf() { free(); }
+    // growing keeps the old block until the buffer itself is freed: work
+    // still queued may read it, and a hipFree here would wait for the device
+    // in the middle of a solve (the grows of a problem's first setup)
     hipError_t alloc(size_t count) {
         if (count <= n && p) return hipSuccess;
-        if (p) dev_free(p);
+        if (p) retired.push_back(p);
         p = nullptr;
         n = 0;
         if (count == 0) return hipSuccess;
@@ -193,9 +196,12 @@ struct DBuf {
     }
     void free() {
         if (p) dev_free(p);
+        for (T *q : retired) dev_free(q);
+        retired.clear();
         p = nullptr;
         n = 0;
     }
+    std::vector<T *> retired;
 };
 
 // Halo exchange overlapped with computation on a sharded operator.  Tiles of
