@@ -2096,8 +2096,9 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
         }
         if ((resn < 100. * P->precision) && (Iter > 0)) LinearFlag = true;
         if (trace_newton())   // lab: one line per Newton pass
-            std::fprintf(stderr, "[newton] pass %d: pcg %lld (%s%s, levels %d) res %.3e relax %.3f\n", Iter,
-                         (long long)P->pcg_host->iters, P->pc_used == XFK_PRECOND_AMG ? "amg" : "jacobi",
+            std::fprintf(stderr, "[newton] pass %d: pcg %lld (%lld before a restart; %s%s, levels %d) res %.3e relax %.3f\n",
+                         Iter, (long long)P->pcg_host->iters, P->pcg_discarded,
+                         P->pc_used == XFK_PRECOND_AMG ? "amg" : "jacobi",
                          P->pc_used == XFK_PRECOND_AMG ? (P->amg_fresh ? " fresh" : " reused") : "",
                          (P->pc_used == XFK_PRECOND_AMG && P->amg) ? P->amg->stats.levels : 0, resn, Relax);
         Iter++;
