@@ -1139,8 +1139,8 @@ static int pcg_iteration(xfk_problem *P, long long it, bool stamp)
 constexpr int kF32Guard = 150;
 constexpr int kRetryF64 = 1;   // (internal return codes of pcg_solve_once)
 // a hierarchy kept from an earlier Newton pass is abandoned for a fresh one
-// when this solve would take more than 3x + 16 the iterations of the pass that
-// built it (projected from the observed rate at each poll): the first
+// when this solve would take more than max(2x, +8) the iterations of the pass
+// that built it (projected from the observed rate at each poll): the first
 // nonlinear pass can change the permeabilities from their initial values
 // enough to make the old hierarchy useless (the antiperiodic magnet machine:
 // 767 iterations on the kept one, 31 on a fresh one)
@@ -1169,12 +1169,15 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
     // converged solve launches no iteration tail that would only exit
     // (one V-cycle + SpMV, ~14 launches, saved per solve)
     bool tail = false;   // iteration it - 1's V-cycle + SpMV not launched yet
+    // (the bound is the reuse test of amg_setup: a solve that cannot stay
+    // within it would not have kept the hierarchy had its count been known;
+    // polled at least every 16 iterations while the hierarchy is a kept one)
     const long long stale = (P->pc_used == XFK_PRECOND_AMG && !P->amg_fresh && P->amg_fresh_iters > 0)
-                                ? std::max<long long>(3LL * P->amg_fresh_iters, P->amg_fresh_iters + 16)
+                                ? std::max<long long>(2LL * P->amg_fresh_iters, P->amg_fresh_iters + 8)
                                 : -1;
     for (;;) {
         batch = (int)std::max<long long>(1, std::min<long long>(batch, max_iters - it));
-        if (stale > 0 && it < stale) batch = (int)std::min<long long>(batch, stale - it);
+        if (stale > 0 && it < stale) batch = (int)std::min<long long>({(long long)batch, stale - it, 16LL});
         for (int k = 0; k < batch; ++k, ++it) {
             if (tail) {
                 const long long ip = it - 1;
