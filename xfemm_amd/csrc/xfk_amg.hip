@@ -1100,11 +1100,15 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
             np += total;
         }
         // more products than slots (a capacity taken from an earlier setup):
-        // the row is garbage, the host redoes the product with a measured capacity
-        if (np > CAP) {
-            if (l == 0) *ovf = 1;
-            np = CAP;
+        // the row is garbage, the host redoes the product with a measured
+        // capacity (bit 0); a row using more than half the slots sets bit 1 --
+        // without it the next setup takes half the capacity (the flag word is
+        // read first, so once set the rows stop writing it)
+        if (l == 0) {   // (bit 2: more than a quarter)
+            const int b = np > CAP ? 1 : np > CAP / 2 ? 2 : np > CAP / 4 ? 4 : 0;
+            if (b && !(__atomic_load_n(ovf, __ATOMIC_RELAXED) & b)) atomicOr(ovf, b);
         }
+        if (np > CAP) np = CAP;
     }
     wave_lds_sync();
     int key[S];
@@ -2652,7 +2656,7 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
         AMG_CHECK(hipMemcpyAsync(M.host_int + 4, sovf, sizeof(int), hipMemcpyDeviceToHost, s));
         int rc = scan_total(M, s, M.cnt.p, crow.p, nrows, cnnz);   // synchronises
         if (rc != XFK_OK) return rc;
-        overflow = M.host_int[4] != 0;
+        overflow = (M.host_int[4] & 1) != 0;
         if (overflow) return XFK_OK;
         AMG_CHECK(ccol.alloc((size_t)std::max(1LL, cnnz)));
         AMG_CHECK(cval.alloc((size_t)std::max(1LL, cnnz)));
@@ -2684,6 +2688,8 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
                 else
                     AMG_CHECK(hipMemsetAsync(slot + 1, 0, sizeof(int), s));
                 M.def_target[M.def_n / 2] = &cnnz;
+                M.def_key[M.def_n / 2] = key;
+                M.def_cap[M.def_n / 2] = cap;
                 M.def_n += 2;
                 cnnz = (long long)nrows * cap;   // an upper bound until the deferred read
                 return XFK_OK;
@@ -3118,8 +3124,17 @@ int Amg::wait_deferred(hipStream_t s, bool &overflow)
     if (def_n == 0) return XFK_OK;
     AMG_CHECK(hipEventSynchronize(ev_host));
     for (int q = 0; q < def_n / 2; ++q) {
-        if (def_host[2 * q]) overflow = true;
-        else *def_target[q] = def_host[2 * q + 1];
+        if (def_host[2 * q] & 1) {
+            overflow = true;
+            continue;
+        }
+        *def_target[q] = def_host[2 * q + 1];
+        // every row fit in half (a quarter) of the slots: the capacity (seeded
+        // from a priori bounds, or measured on an earlier matrix of the
+        // family) halves (quarters), down to the smallest kernel's 16
+        const int f = def_host[2 * q];
+        if (def_key[q] >= 0 && !(f & 2) && def_cap[q] > 16 && !std::getenv("XFK_AMG_TEST_SMALL_HINT"))
+            cap_hint[def_key[q]] = std::max(16, (f & 4) ? def_cap[q] / 2 : def_cap[q] / 4);
     }
     def_n = 0;
     AMG_CHECK(hipMemsetAsync(def_dev.p, 0, sizeof(int) * kAmgDeferSlots, s));
@@ -3882,6 +3897,7 @@ int Amg::build(hipStream_t s, int l0)
             if (def_n > 0 && def_n + 2 <= kAmgDeferSlots) {
                 AMG_CHECK(hipMemcpyAsync(def_dev.p + def_n + 1, A.ftrow.p + n, sizeof(int), hipMemcpyDeviceToDevice, s));
                 def_target[def_n / 2] = &A.fnnz;
+                def_key[def_n / 2] = -1;
                 def_n += 2;
             } else if (def_n > 0) {
                 int len = 0;
