@@ -56,6 +56,34 @@ def test_host_fsolver_loads_like_the_reference(tmp_path):
     assert mu == pr.blocks[0].mu_x
 
 
+def test_host_fsolver_renumbers_large_scrambled_mesh_like_the_reference(tmp_path):
+    """Cuthill-McKee and SortElements (cuthill.cpp) on an 80k-element mesh with
+    scrambled node and element numbering -- large enough for the parallel
+    comb-sort passes and neighbour ordering -- against the oracle's sequential
+    restatement: the same node order, element order (equal-score elements
+    included) and bandwidth."""
+    from xfemm_amd import synth
+    kw = synth.magnetostatic(200)
+    rng = np.random.default_rng(7)
+    nn, ne = len(kw["x"]), len(kw["p"])
+    perm = rng.permutation(nn)          # node i -> new id perm[i]
+    inv = np.argsort(perm)
+    eperm = rng.permutation(ne)
+    kw = dict(kw, x=kw["x"][inv], y=kw["y"][inv], p=perm[kw["p"]][eperm].astype(np.int32),
+              lbl=kw["lbl"][eperm], e=kw["e"][eperm])
+    base = str(tmp_path / "scr")
+    synth.write_problem(base, kw)
+    fs = fsolver.FSolver(delete_mesh_files=False)
+    fs.PathName = base
+    assert fs.LoadProblemFile() and fs.LoadMesh() and fs.Cuthill(), fs.last_error()
+    pr, mesh = femfile.load_problem(base)
+    x, y, m = fs.nodes()
+    p, lbl, e = fs.elements()
+    assert np.array_equal(x, mesh.x) and np.array_equal(y, mesh.y)
+    assert np.array_equal(p, mesh.p) and np.array_equal(lbl, mesh.lbl) and np.array_equal(e, mesh.e)
+    assert fs.BandWidth == mesh.bandwidth
+
+
 def test_host_fsolver_deletes_mesh_files_like_the_reference(tmp_path):
     base = _copy_case(tmp_path)
     fs = fsolver.FSolver()          # deleteFiles = true, as runSolver's LoadMesh()

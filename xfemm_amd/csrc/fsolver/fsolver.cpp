@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <utility>
 
@@ -599,18 +600,101 @@ int FSolver::SortElements()
     // comb sort on p0+p1+p2 (cuthill.cpp:39-86); not stable, restated exactly:
     // the same comparisons and swaps, on packed (score, element) keys instead
     // of the element records, which are permuted once at the end
-    std::vector<unsigned long long> key(NumEls);
-    for (int k = 0; k < NumEls; k++) {
-        const unsigned long long sc = (unsigned long long)((long long)meshele[k].p[0] + meshele[k].p[1] + meshele[k].p[2]);
-        key[k] = (sc << 32) | (unsigned)k;
-    }
+    LoadTrace tr;
+    std::vector<unsigned long long> key(NumEls), tmp;
+    par_for(NumEls, 1 << 16, [&](long long a, long long b) {
+        for (long long k = a; k < b; k++) {
+            const CMElement &e = meshele[k];
+            const unsigned long long sc = (unsigned long long)((long long)e.p[0] + e.p[1] + e.p[2]);
+            key[k] = (sc << 32) | (unsigned)k;
+        }
+    });
     // A pass with gap g compares (j, j + g) for j ascending: the steps of one
     // residue class j mod g touch only that class's entries, in ascending
-    // order, so classes are independent -- wide passes run with the classes
-    // split over threads (each class still in ascending order: the same swaps)
-    int gap = NumEls, i = 0;
+    // order, so classes are independent.  Wide passes split the classes over
+    // threads.  Narrow passes (few classes) use that a pass over one class is
+    // a bubble pass: the element carried to position k is the prefix
+    // "maximum" c_k = op(c_{k-1}, x_k), op(a, b) = score(a) > score(b) ? a : b
+    // (a swap happens exactly when the carried score exceeds the next one:
+    // ties keep their order), and position k receives
+    // score(c_k) > score(x_{k+1}) ? x_{k+1} : c_k -- an associative scan, so
+    // chunks of rows run in parallel from their classes' carries (computed
+    // from per-chunk reductions): out of place, the same result as the
+    // sequential pass
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const int T = (int)std::min(hw, 16u);
+    auto sc = [](unsigned long long k) { return k >> 32; };
+    auto op = [&](unsigned long long a, unsigned long long b) { return sc(a) > sc(b) ? a : b; };
+    auto scan_pass = [&](int g) -> bool {
+        const long long R = ((long long)NumEls + g - 1) / g;   // rows of g positions
+        const int TT = (int)std::max<long long>(1, std::min<long long>(T, R / 64));
+        std::vector<unsigned long long> red((size_t)TT * g), cin((size_t)TT * g);
+        std::vector<char> has((size_t)TT * g, 0), hin((size_t)TT * g, 0), sw(TT, 0);
+        auto rows = [&](int t, long long &r0, long long &r1) { r0 = R * t / TT; r1 = R * (t + 1) / TT; };
+        std::vector<std::thread> th;
+        auto run = [&](auto fn) {
+            th.clear();
+            for (int t = 1; t < TT; ++t) th.emplace_back(fn, t);
+            fn(0);
+            for (auto &x : th) x.join();
+        };
+        run([&](int t) {   // per chunk and class: the op-reduction of its entries (thread-local, then stored)
+            long long r0, r1;
+            rows(t, r0, r1);
+            std::vector<unsigned long long> rd(g);
+            std::vector<char> h(g, 0);
+            for (long long r = r0; r < r1; ++r)
+                for (int c = 0; c < g; ++c) {
+                    const long long q = r * g + c;
+                    if (q >= NumEls) break;
+                    rd[c] = h[c] ? op(rd[c], key[q]) : key[q];
+                    h[c] = 1;
+                }
+            std::copy(rd.begin(), rd.end(), red.begin() + (size_t)t * g);
+            std::copy(h.begin(), h.end(), has.begin() + (size_t)t * g);
+        });
+        for (int t = 1; t < TT; ++t)   // carries into each chunk
+            for (int c = 0; c < g; ++c) {
+                const size_t a = (size_t)(t - 1) * g + c, b = (size_t)t * g + c;
+                if (hin[a] && has[a]) cin[b] = op(cin[a], red[a]);
+                else if (hin[a]) cin[b] = cin[a];
+                else if (has[a]) cin[b] = red[a];
+                hin[b] = hin[a] || has[a];
+            }
+        tmp.resize(NumEls);
+        run([&](int t) {
+            long long r0, r1;
+            rows(t, r0, r1);
+            std::vector<unsigned long long> car(cin.begin() + (size_t)t * g, cin.begin() + (size_t)(t + 1) * g);
+            std::vector<char> hc(hin.begin() + (size_t)t * g, hin.begin() + (size_t)(t + 1) * g);
+            char any = 0;
+            for (long long r = r0; r < r1; ++r)
+                for (int c = 0; c < g; ++c) {
+                    const long long q = r * g + c;
+                    if (q >= NumEls) break;
+                    const unsigned long long cc = hc[c] ? op(car[c], key[q]) : key[q];   // c_k (x_0 .. x_k)
+                    car[c] = cc;
+                    hc[c] = 1;
+                    if (q + g < NumEls) {
+                        const unsigned long long nx = key[q + g];   // x_{k+1}, as the pass meets it
+                        if (sc(cc) > sc(nx)) {
+                            tmp[q] = nx;
+                            any = 1;
+                        } else {
+                            tmp[q] = cc;
+                        }
+                    } else {
+                        tmp[q] = cc;
+                    }
+                }
+            sw[t] = any;
+        });
+        key.swap(tmp);
+        bool any = false;
+        for (char c : sw) any |= c != 0;
+        return any;
+    };
+    int gap = NumEls, i = 0;
     do {
         if (gap > 1) {
             gap = (gap * 10) / 13;
@@ -638,6 +722,8 @@ int FSolver::SortElements()
             part(0);
             for (auto &x : th) x.join();
             for (char c : sw) i |= c;
+        } else if (T > 1 && NumEls >= (1 << 16)) {   // (narrow passes: few classes)
+            i = scan_pass(gap) ? 1 : 0;
         } else {
             for (int j = 0; (j + gap) < NumEls; j++) {
                 if ((key[j] >> 32) > (key[j + gap] >> 32)) {
@@ -647,8 +733,11 @@ int FSolver::SortElements()
             }
         }
     } while ((gap > 1) && (i > 0));
+    tr.mark("  comb sort");
     std::vector<CMElement> sorted(NumEls);
-    for (int k = 0; k < NumEls; k++) sorted[k] = meshele[(unsigned)(key[k] & 0xffffffffu)];
+    par_for(NumEls, 1 << 16, [&](long long a, long long b) {
+        for (long long k = a; k < b; k++) sorted[k] = meshele[(unsigned)(key[k] & 0xffffffffu)];
+    });
     meshele.swap(sorted);
     return true;
 }
@@ -663,22 +752,34 @@ int FSolver::Cuthill(bool deleteFiles)
         numcon[e[0]]++;
         numcon[e[1]]++;
     }
-    std::vector<std::vector<int>> ocon(NumNodes);
-    for (int i = 0; i < NumNodes; i++) ocon[i].reserve(numcon[i]);
-    for (auto &e : edges_) {
-        ocon[e[0]].push_back(e[1]);
-        ocon[e[1]].push_back(e[0]);
+    // neighbour lists as CSR, each in the order the reference's lists get
+    // their entries (edge order)
+    std::vector<int> aptr((size_t)NumNodes + 1, 0), adj(2 * edges_.size());
+    for (int i = 0; i < NumNodes; i++) aptr[i + 1] = aptr[i] + numcon[i];
+    {
+        std::vector<int> cur(aptr.begin(), aptr.end() - 1);
+        for (auto &e : edges_) {
+            adj[cur[e[0]]++] = e[1];
+            adj[cur[e[1]]++] = e[0];
+        }
     }
     if (deleteFiles) remove((PathName + ".edge").c_str());
     tr.mark("adjacency");
-    // bubble sort by increasing connectivity
-    for (int n0 = 0; n0 < NumNodes; n0++) {
-        std::vector<int> &l = ocon[n0];
-        const int m = (int)l.size();
-        for (int a = 1; a < m; a++)
-            for (int j = 1; j < m; j++)
-                if (numcon[l[j]] < numcon[l[j - 1]]) std::swap(l[j], l[j - 1]);
-    }
+    // bubble sort by increasing connectivity: swaps only on a strict decrease,
+    // so it is the stable sort of the list by numcon -- an insertion sort per
+    // list gives the same order; lists are independent
+    par_for(NumNodes, 1 << 14, [&](long long a, long long b) {
+        for (long long n0 = a; n0 < b; n0++) {
+            int *l = adj.data() + aptr[n0];
+            const int m = aptr[n0 + 1] - aptr[n0];
+            for (int q = 1; q < m; q++) {
+                const int v = l[q], kv = numcon[v];
+                int r = q;
+                for (; r > 0 && numcon[l[r - 1]] > kv; --r) l[r] = l[r - 1];
+                l[r] = v;
+            }
+        }
+    });
     tr.mark("neighbour sort");
     long long j = numcon[0];
     int n0 = 0;
@@ -694,8 +795,8 @@ int FSolver::Cuthill(bool deleteFiles)
     nxtnum[0] = n0;
     if (NumNodes > 1) {
         do {
-            for (int c : ocon[n0])
-                if (newnum[c] < 0) {
+            for (int t = aptr[n0]; t < aptr[n0 + 1]; ++t)
+                if (const int c = adj[t]; newnum[c] < 0) {
                     newnum[c] = n;
                     nxtnum[n] = c;
                     n++;
@@ -732,14 +833,26 @@ int FSolver::Cuthill(bool deleteFiles)
     for (auto &g : agelist)   // cuthill.cpp:321-330
         for (int &q : g.qn) q = newnum[q];
     int newwide = 0;
-    for (int a = 0; a < NumNodes; a++)
-        for (int c : ocon[a]) newwide = std::max(newwide, std::abs(newnum[a] - newnum[c]));
+    {
+        std::mutex mu;
+        par_for(NumNodes, 1 << 16, [&](long long a0, long long a1) {
+            int w = 0;
+            for (long long a = a0; a < a1; a++)
+                for (int t = aptr[a]; t < aptr[a + 1]; ++t) w = std::max(w, std::abs(newnum[a] - newnum[adj[t]]));
+            std::lock_guard<std::mutex> g(mu);
+            newwide = std::max(newwide, w);
+        });
+    }
     BandWidth = newwide + 1;
-    for (auto &e : meshele)
-        for (int q = 0; q < 3; q++) e.p[q] = newnum[e.p[q]];
+    par_for(NumEls, 1 << 16, [&](long long a, long long b) {
+        for (long long k = a; k < b; k++)
+            for (int q = 0; q < 3; q++) meshele[k].p[q] = newnum[meshele[k].p[q]];
+    });
     // SortNodes (fsolver.cpp:1341-1353): node i moves to slot newnum[i]
     std::vector<CNode> sorted(NumNodes);
-    for (int i = 0; i < NumNodes; i++) sorted[newnum[i]] = meshnode[i];
+    par_for(NumNodes, 1 << 16, [&](long long a, long long b) {
+        for (long long k = a; k < b; k++) sorted[newnum[k]] = meshnode[k];
+    });
     meshnode.swap(sorted);
     tr.mark("bandwidth + renumber");
     SortElements();
