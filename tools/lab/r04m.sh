@@ -10,3 +10,5 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-m
 rc=$?; echo "tests rc=$rc"; fatal $rc
 XFK_TRACE_NEWTON=1 XFK_AMG_HINTS_PRINT=1 timeout -k 10 200 python -u tools/lab/anti_probe.py anti > gpurun_out/anti_r04m.txt 2>&1
 echo "anti rc=$?"
+XFK_TRACE_CREATE=1 XFEMM_TRACE_LOAD=1 timeout -k 10 300 python -u tools/lab/fs_probe.py > gpurun_out/fs_probe_r04m.txt 2>&1
+echo "fs probe rc=$?"
