@@ -781,6 +781,7 @@ struct SgY {
     const int *rowptr, *col;
     const double *val;
     const int *agg;                // PMODE: P_tent
+    int ncol = 0;                  // columns of the product (0: unknown -- no capacity-independent sums)
 };
 
 // CAP: distinct columns a row may have (FILL is launched with the smallest
@@ -1018,7 +1019,8 @@ __device__ __forceinline__ void wave_lds_sync()
 // moves it to its CSR place after the length scan.
 template <bool PMODE, int G, int CAP>
 __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int *__restrict__ cnt_out,
-                                                    int *__restrict__ pcol, double *__restrict__ pval, int *ovf)
+                                                    int *__restrict__ pcol, double *__restrict__ pval, int *ovf,
+                                                    int canon)
 {
     constexpr int W = 64 / G;
     constexpr int S = CAP / G;
@@ -1113,10 +1115,16 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
     wave_lds_sync();
     int key[S];
     double val[S];
+    // canon: the sort key is (column, product index) -- the products of a
+    // row are enumerated in the same order whatever the capacity, so equal
+    // columns keep that order and each column's sum (taken left to right
+    // below) has the same bits for every capacity the row may run with (the
+    // setup shrinks capacities between setups: repeated solves stay
+    // bit-identical)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
         const int v = l * S + s;
-        key[s] = v < np ? pk[v] : INT_MAX;
+        key[s] = v < np ? (canon ? pk[v] * CAP + v : pk[v]) : INT_MAX;
         val[s] = v < np ? pv[v] : 0.0;
     }
     // bitonic sort of the CAP slots (slot v = l * S + s) by key
@@ -1158,6 +1166,11 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
             }
         }
     }
+    if (canon) {   // back to columns (the empty slots keep INT_MAX)
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            if (key[s] != INT_MAX) key[s] /= CAP;
+    }
     // segmented inclusive scan: head = first slot of a column
     const int prev_last = __shfl_up(key[S - 1], 1, G);
     int head[S], nh = 0;
@@ -1195,6 +1208,15 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
         hin = 0;
     }
     const int cnt = __shfl(hpre, G - 1, G);
+    if (canon) {   // the sorted row back to LDS: each column summed left to right by its last slot
+        wave_lds_sync();
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            pk[l * S + s] = key[s];
+            pv[l * S + s] = val[s];
+        }
+        wave_lds_sync();
+    }
     if (!live) return;
     int h = hin;
 #pragma unroll
@@ -1202,11 +1224,17 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
         bool lead = true;   // slots before this lane's first head continue the incoming segment
 #pragma unroll
         for (int q = 0; q <= s; ++q) lead = lead && !head[q];
-        const double tot = lead ? cin + run[s] : run[s];
+        double tot = lead ? cin + run[s] : run[s];
         h += head[s];
         const int nk = s + 1 < S ? key[s + 1] : __shfl_down(key[0], 1, G);
         const bool tail = key[s] != INT_MAX && (nk != key[s] || (s + 1 == S && l == G - 1));
         if (tail) {
+            if (canon) {
+                int b = l * S + s;
+                while (b > 0 && pk[b - 1] == key[s]) --b;
+                tot = pv[b];
+                for (int q = b + 1; q <= l * S + s; ++q) tot += pv[q];
+            }
             pcol[(size_t)row * CAP + h - 1] = key[s];
             pval[(size_t)row * CAP + h - 1] = tot;
         }
@@ -2627,6 +2655,8 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     // compaction; returns the overflow flag (rows with more products than
     // slots), read back with the scan's own synchronisation
     int *sovf = M.dev_int.p + 6;
+    // (column, product index) keys fit an int: capacity-independent sums
+    auto canon_for = [&](int cap) { return (Y.ncol > 0 && (long long)Y.ncol * cap < INT_MAX) ? 1 : 0; };
     auto launch_sort = [&](int cap, int *ovf) {
         int *pc = M.pad_col.p;
         double *pv = M.pad_val.p;
@@ -2634,15 +2664,15 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
             // few lanes per row, 4-8 sorted slots per lane: many rows per
             // wavefront to overlap their dependent gathers
             if (cap == 16)
-                k_spgemm_sort<PMODE, 4, 16><<<(nrows + 15) / 16, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
+                k_spgemm_sort<PMODE, 4, 16><<<(nrows + 15) / 16, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, canon_for(16));
             else if (cap == 32)
-                k_spgemm_sort<PMODE, 8, 32><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
+                k_spgemm_sort<PMODE, 8, 32><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, canon_for(32));
             else if (cap == 64)
-                k_spgemm_sort<PMODE, 8, 64><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
+                k_spgemm_sort<PMODE, 8, 64><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, canon_for(64));
             else if (cap == 128)
-                k_spgemm_sort<PMODE, 16, 128><<<(nrows + 3) / 4, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
+                k_spgemm_sort<PMODE, 16, 128><<<(nrows + 3) / 4, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, canon_for(128));
             else
-                k_spgemm_sort<PMODE, 32, 256><<<(nrows + 1) / 2, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
+                k_spgemm_sort<PMODE, 32, 256><<<(nrows + 1) / 2, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, canon_for(256));
         }
     };
     // single pass into padded rows of `cap` slots (sort-based), then scan +
@@ -3435,7 +3465,7 @@ int Amg::joins_and_p_impl(hipStream_t s, int l)
     }
     // P = (I - omega D_F^-1 A_F) P_tent
     SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, wF.p, cv.c16, cv.cbase};
-    SgY YT{nullptr, nullptr, nullptr, agg.p};
+    SgY YT{nullptr, nullptr, nullptr, agg.p, dist ? 0 : n};   // (aggregate ids < n)
     if (g_prof) g_prof->begin(lv + "P = (I - w D^-1 A) P_tent, R = P^T", 0.0);
     return spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz, dist ? -1 : 4 * l);
 }
@@ -3827,7 +3857,7 @@ int Amg::build(hipStream_t s, int l0)
         // AP = A P, then A_c = R (A P)
         SgX XA{A.rowptr, A.col, A.val, A.ncol_lim, nullptr, nullptr, nullptr, A.has16 ? A.a16.p : nullptr,
                A.has16 ? A.a16b.p : nullptr};
-        SgY YP{A.prow.p, A.pcol.p, A.pval.p, nullptr};
+        SgY YP{A.prow.p, A.pcol.p, A.pval.p, nullptr, n};   // (coarse ids < n)
         if (fold_pending) {   // the previous level's folded transfer still reads A P's buffers
             AMG_CHECK(hipStreamWaitEvent(s, sw.c, 0));
             fold_pending = false;
@@ -3841,7 +3871,7 @@ int Amg::build(hipStream_t s, int l0)
         if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
         AmgLevel &C = *L[l + 1];
         SgX XR{A.rrow.p, A.rcol.p, A.rval.p, INT_MAX, nullptr, nullptr, nullptr};
-        SgY YAP{A.ftrow.p, ap_col.p, ap_val.p, nullptr};
+        SgY YAP{A.ftrow.p, ap_col.p, ap_val.p, nullptr, n};
         if (rt_pending) {   // R = P^T from the side stream
             AMG_CHECK(hipStreamWaitEvent(s, sw.b, 0));
             rt_pending = false;
