@@ -160,9 +160,6 @@ struct Amg {
     int *def_host = nullptr;          // pinned mirror
     int def_n = 0;
     long long *def_target[kAmgDeferSlots / 2] = {};
-    // the capacity hint a deferred product ran with (key, capacity; -1: none):
-    // a product whose rows all fit in half of it gets half next time
-    int def_key[kAmgDeferSlots / 2] = {}, def_cap[kAmgDeferSlots / 2] = {};
     int *host_int = nullptr;          // pinned mirror (16 ints; 8..10: the aggregation's packed check)
     hipEvent_t ev_host = nullptr;     // host waits for a check while later setup work runs
     DBuf<int> mis_out;                // packed aggregation check

@@ -781,7 +781,6 @@ struct SgY {
     const int *rowptr, *col;
     const double *val;
     const int *agg;                // PMODE: P_tent
-    int ncol = 0;                  // columns of the product (0: unknown -- no capacity-independent sums)
 };
 
 // CAP: distinct columns a row may have (FILL is launched with the smallest
@@ -1019,8 +1018,7 @@ __device__ __forceinline__ void wave_lds_sync()
 // moves it to its CSR place after the length scan.
 template <bool PMODE, int G, int CAP>
 __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int *__restrict__ cnt_out,
-                                                    int *__restrict__ pcol, double *__restrict__ pval, int *ovf,
-                                                    int canon)
+                                                    int *__restrict__ pcol, double *__restrict__ pval, int *ovf)
 {
     constexpr int W = 64 / G;
     constexpr int S = CAP / G;
@@ -1102,29 +1100,19 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
             np += total;
         }
         // more products than slots (a capacity taken from an earlier setup):
-        // the row is garbage, the host redoes the product with a measured
-        // capacity (bit 0); a row using more than half the slots sets bit 1 --
-        // without it the next setup takes half the capacity (the flag word is
-        // read first, so once set the rows stop writing it)
-        if (l == 0) {   // (bit 2: more than a quarter)
-            const int b = np > CAP ? 1 : np > CAP / 2 ? 2 : np > CAP / 4 ? 4 : 0;
-            if (b && !(__atomic_load_n(ovf, __ATOMIC_RELAXED) & b)) atomicOr(ovf, b);
+        // the row is garbage, the host redoes the product with a measured capacity
+        if (np > CAP) {
+            if (l == 0) *ovf = 1;
+            np = CAP;
         }
-        if (np > CAP) np = CAP;
     }
     wave_lds_sync();
     int key[S];
     double val[S];
-    // canon: the sort key is (column, product index) -- the products of a
-    // row are enumerated in the same order whatever the capacity, so equal
-    // columns keep that order and each column's sum (taken left to right
-    // below) has the same bits for every capacity the row may run with (the
-    // setup shrinks capacities between setups: repeated solves stay
-    // bit-identical)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
         const int v = l * S + s;
-        key[s] = v < np ? (canon ? pk[v] * CAP + v : pk[v]) : INT_MAX;
+        key[s] = v < np ? pk[v] : INT_MAX;
         val[s] = v < np ? pv[v] : 0.0;
     }
     // bitonic sort of the CAP slots (slot v = l * S + s) by key
@@ -1166,11 +1154,6 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
             }
         }
     }
-    if (canon) {   // back to columns (the empty slots keep INT_MAX)
-#pragma unroll
-        for (int s = 0; s < S; ++s)
-            if (key[s] != INT_MAX) key[s] /= CAP;
-    }
     // segmented inclusive scan: head = first slot of a column
     const int prev_last = __shfl_up(key[S - 1], 1, G);
     int head[S], nh = 0;
@@ -1208,15 +1191,6 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
         hin = 0;
     }
     const int cnt = __shfl(hpre, G - 1, G);
-    if (canon) {   // the sorted row back to LDS: each column summed left to right by its last slot
-        wave_lds_sync();
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            pk[l * S + s] = key[s];
-            pv[l * S + s] = val[s];
-        }
-        wave_lds_sync();
-    }
     if (!live) return;
     int h = hin;
 #pragma unroll
@@ -1224,17 +1198,11 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
         bool lead = true;   // slots before this lane's first head continue the incoming segment
 #pragma unroll
         for (int q = 0; q <= s; ++q) lead = lead && !head[q];
-        double tot = lead ? cin + run[s] : run[s];
+        const double tot = lead ? cin + run[s] : run[s];
         h += head[s];
         const int nk = s + 1 < S ? key[s + 1] : __shfl_down(key[0], 1, G);
         const bool tail = key[s] != INT_MAX && (nk != key[s] || (s + 1 == S && l == G - 1));
         if (tail) {
-            if (canon) {
-                int b = l * S + s;
-                while (b > 0 && pk[b - 1] == key[s]) --b;
-                tot = pv[b];
-                for (int q = b + 1; q <= l * S + s; ++q) tot += pv[q];
-            }
             pcol[(size_t)row * CAP + h - 1] = key[s];
             pval[(size_t)row * CAP + h - 1] = tot;
         }
@@ -2655,8 +2623,6 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     // compaction; returns the overflow flag (rows with more products than
     // slots), read back with the scan's own synchronisation
     int *sovf = M.dev_int.p + 6;
-    // (column, product index) keys fit an int: capacity-independent sums
-    auto canon_for = [&](int cap) { return (Y.ncol > 0 && (long long)Y.ncol * cap < INT_MAX) ? 1 : 0; };
     auto launch_sort = [&](int cap, int *ovf) {
         int *pc = M.pad_col.p;
         double *pv = M.pad_val.p;
@@ -2664,15 +2630,15 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
             // few lanes per row, 4-8 sorted slots per lane: many rows per
             // wavefront to overlap their dependent gathers
             if (cap == 16)
-                k_spgemm_sort<PMODE, 4, 16><<<(nrows + 15) / 16, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, canon_for(16));
+                k_spgemm_sort<PMODE, 4, 16><<<(nrows + 15) / 16, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
             else if (cap == 32)
-                k_spgemm_sort<PMODE, 8, 32><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, canon_for(32));
+                k_spgemm_sort<PMODE, 8, 32><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
             else if (cap == 64)
-                k_spgemm_sort<PMODE, 8, 64><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, canon_for(64));
+                k_spgemm_sort<PMODE, 8, 64><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
             else if (cap == 128)
-                k_spgemm_sort<PMODE, 16, 128><<<(nrows + 3) / 4, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, canon_for(128));
+                k_spgemm_sort<PMODE, 16, 128><<<(nrows + 3) / 4, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
             else
-                k_spgemm_sort<PMODE, 32, 256><<<(nrows + 1) / 2, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, canon_for(256));
+                k_spgemm_sort<PMODE, 32, 256><<<(nrows + 1) / 2, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
         }
     };
     // single pass into padded rows of `cap` slots (sort-based), then scan +
@@ -2686,7 +2652,7 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
         AMG_CHECK(hipMemcpyAsync(M.host_int + 4, sovf, sizeof(int), hipMemcpyDeviceToHost, s));
         int rc = scan_total(M, s, M.cnt.p, crow.p, nrows, cnnz);   // synchronises
         if (rc != XFK_OK) return rc;
-        overflow = (M.host_int[4] & 1) != 0;
+        overflow = M.host_int[4] != 0;
         if (overflow) return XFK_OK;
         AMG_CHECK(ccol.alloc((size_t)std::max(1LL, cnnz)));
         AMG_CHECK(cval.alloc((size_t)std::max(1LL, cnnz)));
@@ -2718,8 +2684,6 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
                 else
                     AMG_CHECK(hipMemsetAsync(slot + 1, 0, sizeof(int), s));
                 M.def_target[M.def_n / 2] = &cnnz;
-                M.def_key[M.def_n / 2] = key;
-                M.def_cap[M.def_n / 2] = cap;
                 M.def_n += 2;
                 cnnz = (long long)nrows * cap;   // an upper bound until the deferred read
                 return XFK_OK;
@@ -3154,17 +3118,8 @@ int Amg::wait_deferred(hipStream_t s, bool &overflow)
     if (def_n == 0) return XFK_OK;
     AMG_CHECK(hipEventSynchronize(ev_host));
     for (int q = 0; q < def_n / 2; ++q) {
-        if (def_host[2 * q] & 1) {
-            overflow = true;
-            continue;
-        }
-        *def_target[q] = def_host[2 * q + 1];
-        // every row fit in half (a quarter) of the slots: the capacity (seeded
-        // from a priori bounds, or measured on an earlier matrix of the
-        // family) halves (quarters), down to the smallest kernel's 16
-        const int f = def_host[2 * q];
-        if (def_key[q] >= 0 && !(f & 2) && def_cap[q] > 16 && !std::getenv("XFK_AMG_TEST_SMALL_HINT"))
-            cap_hint[def_key[q]] = std::max(16, (f & 4) ? def_cap[q] / 2 : def_cap[q] / 4);
+        if (def_host[2 * q]) overflow = true;
+        else *def_target[q] = def_host[2 * q + 1];
     }
     def_n = 0;
     AMG_CHECK(hipMemsetAsync(def_dev.p, 0, sizeof(int) * kAmgDeferSlots, s));
@@ -3205,31 +3160,26 @@ int Amg::init(hipStream_t s)
     return XFK_OK;
 }
 
-// Capacities of a fresh hierarchy, a priori from the longest fine row m
-// (one int read with the pattern's length, no host check per product):
-//   P = (I - W D^-1 A_F) P_tent: one product per entry of A's row -- at most
-//     m on level 0 (exact), taken as 2m on coarse levels (their rows carry the
-//     neighbourhoods of ~9 merged fine rows: 12-20 entries for m = 7);
-//   A P: the P rows of the row's neighbours, 2-4 entries each: 4m on level
-//     0, 8m on coarse levels;  R (A P): 16m on level 0, the sort kernels'
-//     256 on coarse levels;
+// Hints of a fresh hierarchy, a priori from the longest fine row m (one int
+// read with the pattern's length, no host check):
+//   P = (I - W D^-1 A_F) P_tent on level 0: one product per entry of A's row,
+//     at most m -- exact, so it is the capacity a measurement would choose;
 //   MIS-2: 12 rounds per level (11-12 measured on configs[1] / configs[2]).
-// Products beyond a capacity are detected in the kernels and the hierarchy is
-// rebuilt with measured capacities (build's deferred check), so a bound that
-// is too small costs time, never correctness.  XFK_AMG_NO_SEED=1: measure.
+// The other products are measured in the first setup (a host check each):
+// an a priori bound for them is 2x oversized, and a capacity carried over
+// from an oversized first setup would stay so (the sort kernels over twice
+// the padded rows: round 4 measured the warm setup 2.24 -> 2.64 ms with
+// seeded A P and R (A P) capacities), while a capacity that changes between
+// setups changes the Galerkin products' summation order, so repeated solves
+// would no longer be bit-identical.  XFK_AMG_NO_SEED=1: measure everything.
+
 void Amg::seed_hints()
 {
     static const bool off = std::getenv("XFK_AMG_NO_SEED") != nullptr;
     if (off || row_max0 <= 0 || !cap_hint.empty() || !mis_hint.empty()) return;
     auto cap = [](long long v) { return v <= 16 ? 16 : v <= 32 ? 32 : v <= 64 ? 64 : v <= 128 ? 128 : 256; };
-    const long long m = row_max0;
-    for (int l = 0; l < kAmgMaxLevels; ++l) {
-        const long long p = l == 0 ? m : 2 * m, ap = l == 0 ? 4 * m : 8 * m, rap = l == 0 ? 16 * m : 256;
-        if (p <= kSortCap) cap_hint[4 * l] = cap(p);
-        if (ap <= kSortCap) cap_hint[4 * l + 1] = cap(ap);
-        if (rap <= kSortCap) cap_hint[4 * l + 2] = cap(rap);
-        mis_hint[l] = 12;
-    }
+    if (row_max0 <= kSortCap) cap_hint[0] = cap(row_max0);
+    for (int l = 0; l < kAmgMaxLevels; ++l) mis_hint[l] = 12;
 }
 
 int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *col0, const double *val0,
@@ -3465,7 +3415,7 @@ int Amg::joins_and_p_impl(hipStream_t s, int l)
     }
     // P = (I - omega D_F^-1 A_F) P_tent
     SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, wF.p, cv.c16, cv.cbase};
-    SgY YT{nullptr, nullptr, nullptr, agg.p, dist ? 0 : n};   // (aggregate ids < n)
+    SgY YT{nullptr, nullptr, nullptr, agg.p};
     if (g_prof) g_prof->begin(lv + "P = (I - w D^-1 A) P_tent, R = P^T", 0.0);
     return spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz, dist ? -1 : 4 * l);
 }
@@ -3857,7 +3807,7 @@ int Amg::build(hipStream_t s, int l0)
         // AP = A P, then A_c = R (A P)
         SgX XA{A.rowptr, A.col, A.val, A.ncol_lim, nullptr, nullptr, nullptr, A.has16 ? A.a16.p : nullptr,
                A.has16 ? A.a16b.p : nullptr};
-        SgY YP{A.prow.p, A.pcol.p, A.pval.p, nullptr, n};   // (coarse ids < n)
+        SgY YP{A.prow.p, A.pcol.p, A.pval.p, nullptr};
         if (fold_pending) {   // the previous level's folded transfer still reads A P's buffers
             AMG_CHECK(hipStreamWaitEvent(s, sw.c, 0));
             fold_pending = false;
@@ -3871,7 +3821,7 @@ int Amg::build(hipStream_t s, int l0)
         if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
         AmgLevel &C = *L[l + 1];
         SgX XR{A.rrow.p, A.rcol.p, A.rval.p, INT_MAX, nullptr, nullptr, nullptr};
-        SgY YAP{A.ftrow.p, ap_col.p, ap_val.p, nullptr, n};
+        SgY YAP{A.ftrow.p, ap_col.p, ap_val.p, nullptr};
         if (rt_pending) {   // R = P^T from the side stream
             AMG_CHECK(hipStreamWaitEvent(s, sw.b, 0));
             rt_pending = false;
@@ -3927,7 +3877,6 @@ int Amg::build(hipStream_t s, int l0)
             if (def_n > 0 && def_n + 2 <= kAmgDeferSlots) {
                 AMG_CHECK(hipMemcpyAsync(def_dev.p + def_n + 1, A.ftrow.p + n, sizeof(int), hipMemcpyDeviceToDevice, s));
                 def_target[def_n / 2] = &A.fnnz;
-                def_key[def_n / 2] = -1;
                 def_n += 2;
             } else if (def_n > 0) {
                 int len = 0;
