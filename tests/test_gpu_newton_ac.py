@@ -2,8 +2,11 @@
 restatement (oracle/harmonic2d_oracle.c, bit-identical to the compiled
 cspars.cpp: tests/test_oracle_harmonic.py::test_newton_ac_solver_is_bit_identical_to_reference).
 
-Tolerance: max |dA| <= 5e-5 max |A| against the oracle re-run at Precision
-1e-13 (util.converged).  Both loops stop when a pass changes V by less than
+Tolerance: max |dA| <= max(1e-5, 2 e_ref) max |A| against the oracle re-run at
+Precision 1e-13 (util.converged), e_ref the distance of the oracle at the
+problem's Precision from that run -- the reference's own stopping error (the
+flat 5e-5 of round 3; measured round 4: 1e-9 .. 1.6e-5 with e_ref up to 8.5e-6,
+the periodic / antiperiodic cases the only ones above 1e-5).  Both loops stop when a pass changes V by less than
 100 Precision (harmonic2d.cpp:868) after KludgeSolve passes that themselves
 stop at the adaptive precision min(1e-4, 0.001 res) (harmonic2d.cpp:821-825),
 so the answer carries the loop's own stopping error: the oracle at the
@@ -32,7 +35,11 @@ from xfemm_amd import kernels, synth
 
 pytestmark = pytest.mark.gpu
 
-TOL = 5e-5
+TOL = 1e-5
+
+
+def _tol(Ao, Ac):
+    return max(TOL, 2.0 * rel_err(Ao, Ac))
 
 
 def _case(kind, n):
@@ -63,14 +70,15 @@ def test_newton_ac_matches_oracle(kind, n):
     cc, J, dV = P.circuits()
     P.close()
     assert r["newton_iters"] >= 2
-    assert rel_err(A, Ac) <= TOL, parity_message(A, Ao, Ac, TOL) + " (%d / %d passes)" % (
+    print("newton AC %s %d: |A - Ac| %.3e, oracle at Precision %.3e" % (kind, n, rel_err(A, Ac), rel_err(Ao, Ac)))
+    assert rel_err(A, Ac) <= _tol(Ao, Ac), parity_message(A, Ao, Ac, _tol(Ao, Ac)) + " (%d / %d passes)" % (
         r["newton_iters"], st["newton_iters"])
     for k, (case, Jo, dVo) in enumerate(circ_o):
         assert cc[k] == case and abs(J[k] - Jo) <= 1e-12 * max(1.0, abs(Jo))
     kw0 = dict(kw, ac_solver=0)
     pr0, mesh0, _ = synth_to_oracle(kw0)
     A0, _, _ = oh.solve(pr0, mesh0)
-    assert rel_err(A0, Ac) > 10 * TOL
+    assert rel_err(A0, Ac) > 50 * TOL
 
 
 def test_newton_ac_file_interface_end_to_end(tmp_path):
@@ -103,7 +111,8 @@ def test_newton_ac_file_interface_end_to_end(tmp_path):
     n = int(lines[k])
     nodes = np.array([[float(v) for v in ln.split()] for ln in lines[k + 1:k + 1 + n]])
     A = nodes[:, 2] + 1j * nodes[:, 3]
-    assert rel_err(A, Ac) <= TOL, parity_message(A, Ao, Ac, TOL)
+    print("newton AC file interface: |A - Ac| %.3e, oracle at Precision %.3e" % (rel_err(A, Ac), rel_err(Ao, Ac)))
+    assert rel_err(A, Ac) <= _tol(Ao, Ac), parity_message(A, Ao, Ac, _tol(Ao, Ac))
 
 
 @pytest.mark.parametrize("n,kind", [(14, "planar"), (20, "planar"), (14, "periodic"), (16, "anti")])
@@ -128,7 +137,8 @@ def test_newton_ac_case2_matches_oracle(n, kind):
     cc, J, dV = P.circuits()
     P.close()
     assert r["newton_iters"] >= 2
-    assert rel_err(A, Ac) <= TOL, parity_message(A, Ao, Ac, TOL) + " (%d / %d passes)" % (
+    print("newton AC %s %d: |A - Ac| %.3e, oracle at Precision %.3e" % (kind, n, rel_err(A, Ac), rel_err(Ao, Ac)))
+    assert rel_err(A, Ac) <= _tol(Ao, Ac), parity_message(A, Ao, Ac, _tol(Ao, Ac)) + " (%d / %d passes)" % (
         r["newton_iters"], st["newton_iters"])
     for k, (case, Jo, dVo) in enumerate(circ_c):
         assert cc[k] == case and abs(J[k] - Jo) <= 1e-12 * max(1.0, abs(Jo))
@@ -137,4 +147,4 @@ def test_newton_ac_case2_matches_oracle(n, kind):
     kw0 = dict(kw, ac_solver=0)
     pr0, mesh0, _ = synth_to_oracle(kw0)
     A0, _, _ = oh.solve(pr0, mesh0)
-    assert rel_err(A0, Ac) > 10 * TOL
+    assert rel_err(A0, Ac) > 50 * TOL

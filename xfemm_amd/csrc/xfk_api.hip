@@ -181,14 +181,29 @@ static inline long long ukey(int r, int c)
 
 static inline long long okey(int r, int c) { return ((long long)r << 32) | (unsigned)c; }
 
+// a x + b y of two combinations sorted by key (every Terms is: the single
+// terms and lin2's own output), merged -- a key in both gets a x + b y, in
+// one a x or b y, as the accumulation into a zeroed map gives; zeros dropped
 static Terms lin2(double a, const Terms &x, double b, const Terms &y)
 {
-    std::map<long long, double> m;
-    for (auto &t : x) m[t.first] += a * t.second;
-    for (auto &t : y) m[t.first] += b * t.second;
     Terms out;
-    for (auto &kv : m)
-        if (kv.second != 0.0) out.push_back(kv);
+    out.reserve(x.size() + y.size());
+    size_t i = 0, j = 0;
+    while (i < x.size() || j < y.size()) {
+        double v;
+        long long k;
+        if (j == y.size() || (i < x.size() && x[i].first < y[j].first)) {
+            k = x[i].first;
+            v = a * x[i++].second;
+        } else if (i == x.size() || y[j].first < x[i].first) {
+            k = y[j].first;
+            v = b * y[j++].second;
+        } else {
+            k = x[i].first;
+            v = a * x[i++].second + b * y[j++].second;
+        }
+        if (v != 0.0) out.push_back({k, v});
+    }
     return out;
 }
 
@@ -198,19 +213,23 @@ static Terms lin2(double a, const Terms &x, double b, const Terms &y)
 // post-Dirichlet values; sets of rows k are structural supersets of the
 // reference's value-based scan, which is exact because averaging zeros gives
 // zero.
-static int build_pbc_map(xfk_problem *P)
+static int build_pbc_map(xfk_problem *P, bool aux)
 {
     const int npbc = (int)P->hpbc.size() / 3;
     if (npbc == 0) return XFK_OK;
     std::unordered_map<int, std::set<int>> N0;  // original neighbours of pbc nodes
-    for (int k = 0; k < npbc; ++k) {
-        N0[P->hpbc[3 * k]];
-        N0[P->hpbc[3 * k + 1]];
-    }
+    std::vector<char> ispbc(std::max(1, P->NL), 0);
+    for (int k = 0; k < npbc; ++k)
+        for (int m = 0; m < 2; ++m) {
+            const int v = P->hpbc[3 * k + m];
+            N0[v];
+            if (v >= 0 && v < P->NL) ispbc[v] = 1;
+        }
     for (int e = 0; e < P->NE; ++e)
         for (int j = 0; j < 3; ++j) {
-            auto it = N0.find(P->hp[3 * e + j]);
-            if (it == N0.end()) continue;
+            const int v = P->hp[3 * e + j];
+            if (v < 0 || v >= P->NL || !ispbc[v]) continue;
+            auto it = N0.find(v);
             for (int m = 0; m < 3; ++m)
                 if (m != j) it->second.insert(P->hp[3 * e + m]);
         }
@@ -275,13 +294,14 @@ static int build_pbc_map(xfk_problem *P)
             Terms c = lin2(0.5, v1, 0.5 * sg, v2);
             E[ukey(k, i)] = c;
             E[ukey(k, j)] = (sg > 0) ? c : lin2(-1.0, c, 0.0, Terms{});
-            // row k and, by the Hermitian / anti-Hermitian flip of Put, column k
-            Terms ca = lin2(0.5, geta(k, i), 0.5 * sg, geta(k, j));
-            Terms ct = lin2(0.5, geta(i, k), 0.5 * sg, geta(j, k));
-            Ea[okey(k, i)] = ca;
-            Ea[okey(k, j)] = lin2(sg, ca, 0.0, Terms{});
-            Ea[okey(i, k)] = ct;
-            Ea[okey(j, k)] = lin2(sg, ct, 0.0, Terms{});
+            if (aux) {   // row k and, by the Hermitian / anti-Hermitian flip of Put, column k
+                Terms ca = lin2(0.5, geta(k, i), 0.5 * sg, geta(k, j));
+                Terms ct = lin2(0.5, geta(i, k), 0.5 * sg, geta(j, k));
+                Ea[okey(k, i)] = ca;
+                Ea[okey(k, j)] = lin2(sg, ca, 0.0, Terms{});
+                Ea[okey(i, k)] = ct;
+                Ea[okey(j, k)] = lin2(sg, ct, 0.0, Terms{});
+            }
             for (int m : {i, j})
                 if (!is_orig(k, m)) fill.insert(ukey(k, m));
             Ncur[i].insert(k);
@@ -295,13 +315,14 @@ static int build_pbc_map(xfk_problem *P)
         Terms d = lin2(0.5, get(i, i), 0.5, get(j, j));
         E[ukey(i, i)] = d;
         E[ukey(j, j)] = d;
-        // auxiliary (i, j) block: c = (ii +- ij +- ji + jj) / 4 at ii, jj and +-c at ij, ji
-        Terms da = lin2(0.25, lin2(1.0, geta(i, i), sg, geta(i, j)), 0.25, lin2(sg, geta(j, i), 1.0, geta(j, j)));
-        Ea[okey(i, i)] = da;
-        Ea[okey(j, j)] = da;
-        Ea[okey(i, j)] = lin2(sg, da, 0.0, Terms{});
-        Ea[okey(j, i)] = lin2(sg, da, 0.0, Terms{});
-        if (!is_orig(i, j) && !fill.count(ukey(i, j))) afill.insert(ukey(i, j));
+        if (aux) {   // auxiliary (i, j) block: c = (ii +- ij +- ji + jj) / 4 at ii, jj and +-c at ij, ji
+            Terms da = lin2(0.25, lin2(1.0, geta(i, i), sg, geta(i, j)), 0.25, lin2(sg, geta(j, i), 1.0, geta(j, j)));
+            Ea[okey(i, i)] = da;
+            Ea[okey(j, j)] = da;
+            Ea[okey(i, j)] = lin2(sg, da, 0.0, Terms{});
+            Ea[okey(j, i)] = lin2(sg, da, 0.0, Terms{});
+            if (!is_orig(i, j) && !fill.count(ukey(i, j))) afill.insert(ukey(i, j));
+        }
         Terms bi = getb(i), bj = getb(j);
         Terms c = lin2(0.5, bi, 0.5 * sg, bj);
         Eb[i] = c;
@@ -350,14 +371,21 @@ static void add_age_fill(xfk_problem *P)
 {
     if (P->age_key.empty()) return;
     std::unordered_map<int, std::set<int>> adj;
+    std::vector<char> isage(std::max(1, P->NL), 0);
     for (long long k : P->age_key) {
         const int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
-        if (r != c) { adj[r]; adj[c]; }
+        if (r != c) {
+            adj[r];
+            adj[c];
+            if (r >= 0 && r < P->NL) isage[r] = 1;
+            if (c >= 0 && c < P->NL) isage[c] = 1;
+        }
     }
     for (int e = 0; e < P->NE; ++e)
         for (int j = 0; j < 3; ++j) {
-            auto it = adj.find(P->hp[3 * e + j]);
-            if (it == adj.end()) continue;
+            const int v = P->hp[3 * e + j];
+            if (v < 0 || v >= P->NL || !isage[v]) continue;
+            auto it = adj.find(v);
             for (int m = 0; m < 3; ++m)
                 if (m != j) it->second.insert(P->hp[3 * e + m]);
         }
@@ -1828,7 +1856,7 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
         }
     }
     tr.mark("  local mesh + BC arrays");
-    int rc = build_pbc_map(P);
+    int rc = build_pbc_map(P, G.pbc_aux);
     if (rc != XFK_OK) return fail(rc);
     add_age_fill(P);
     tr.mark("  periodic map + air-gap fill");

@@ -1237,6 +1237,7 @@ int create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_desc *ac, int 
     const double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
     GlobalPrep G;
     prepare_global(d, G);
+    G.pbc_aux = ac->ac_solver == 1;   // (the Newton AC solver's auxiliary matrices go through the periodic map)
     rc = age_entries(d, -1.0, G.age_key, G.age_val);   // air-gap elements, negated (harmonic2d.cpp:227-382)
     if (rc != XFK_OK) return rc;
     const bool axi = G.axi;   // HarmonicAxisymmetric (harmonicaxi.cpp)

@@ -541,6 +541,7 @@ struct GlobalPrep {
     double ext_ro = 0, ext_ri = 0, ext_zo = 0;   // exterior region, cm
     std::vector<long long> age_key;      // air-gap element entries, (r << 32) | c with r <= c
     std::vector<double> age_val;
+    bool pbc_aux = false;                // compose the periodic map of the Newton AC auxiliary matrices too
 };
 
 int validate_desc(const xfk_problem_desc *d);
