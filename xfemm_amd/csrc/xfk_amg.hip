@@ -2794,38 +2794,13 @@ static int rmv_mode()
     return v;
 }
 
-// rows per tile of level 0's restriction R r (XFK_R0_TILE: 256, 128 or 64):
-// R has ~25 entries per row, so a 256-row tile streams ~6400 of them and the
-// 548 tiles of configs[2] run as one partial round over 256 CUs; smaller
-// tiles give more, shorter workgroups in flight per CU
-static int r0_tile()
-{
-    static const int v = [] {
-        const char *e = std::getenv("XFK_R0_TILE");
-        const int t = e ? std::atoi(e) : 256;
-        return (t == 64 || t == 128) ? t : 256;
-    }();
-    return v;
-}
-
-// level 0 with f32 values: the tile kernels (level 0 always has >= kTileMinRows
-// rows); tb: rows per tile (256; the restriction: r0_tile(), matching its c16 tiles)
+// level 0 with f32 values: the 256-row tile kernels (level 0 always has >= kTileMinRows rows)
+// (128- and 64-row tiles for R's ~25-entry rows were measured slower: 14.4 -> 15.0 / 15.6 us,
+// profiles/r04_experiments/r04h_XFK_R0_TILE_*.json)
 void launch_mv32(hipStream_t s, int n, const int *rowptr, const int *col, const float *val, const double *x,
-                 double *y, bool acc, int G, const int *done, const unsigned short *c16, const int *cbase,
-                 int tb = 256)
+                 double *y, bool acc, int G, const int *done, const unsigned short *c16, const int *cbase)
 {
     if (n <= 0) return;
-    if (tb != 256 && G > 4) {   // 7 slots: one staging pass for rows of up to ~28 entries
-        const int g = (n + tb - 1) / tb;
-        if (tb == 128) {
-            if (acc) k_csr_mv_tile<128, true, 7><<<g, 128, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
-            else k_csr_mv_tile<128, false, 7><<<g, 128, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
-        } else {
-            if (acc) k_csr_mv_tile<64, true, 7><<<g, 64, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
-            else k_csr_mv_tile<64, false, 7><<<g, 64, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
-        }
-        return;
-    }
     const int g = (n + 255) / 256;
     if (G <= 4) {
         if (acc) k_csr_mv_tile<256, true, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
@@ -3362,13 +3337,8 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         AMG_CHECK(hipEventRecord(sw.b, sw.cs));
         rt_pending = true;
     }
-    if (l == 0 && A.has16) {   // (tiles of the restriction's launch)
-        const int tb = (A.has32 && !dist) ? r0_tile() : 256;
-        rc = tb == 64    ? build_col16<64>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)
-             : tb == 128 ? build_col16<128>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)
-                         : build_col16<256>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b);
-        if (rc != XFK_OK) return rc;
-    }
+    if (l == 0 && A.has16 && (rc = build_col16<256>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)) != XFK_OK)
+        return rc;
     if (l == 0 && A.has32 &&
         ((rc = to_f32(ts, (int)nc, A.rrow.p, A.pnnz, A.rval.p, A.r32)) != XFK_OK ||
          (f32_sweep_on() && (rc = to_f32(ts, n, A.rowptr, A.nnz, A.val, A.a32)) != XFK_OK)))
@@ -4585,7 +4555,7 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     const long long rnnz = A.pnnz;
     XFK_PHASE(lv + "restriction R r", A.nz_bytes() * rnnz + 4.0 * (A.nc + 1) + 8.0 * A.n + 8.0 * A.nc,
               (A.has32 ? launch_mv32(s, A.nc, A.rrow.p, A.rcol.p, A.r32.p, A.r.p, C.b.p, false,
-                                     lanes_for((double)rnnz / A.nc), done, A.r16.p, A.r16b.p, r0_tile())
+                                     lanes_for((double)rnnz / A.nc), done, A.r16.p, A.r16b.p)
                        : launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false,
                                    lanes_for((double)rnnz / A.nc), done, A.has16 ? A.r16.p : nullptr,
                                    A.has16 ? A.r16b.p : nullptr)));
