@@ -85,6 +85,9 @@ BlockPool &block_pool()
     return *p;
 }
 thread_local bool tl_pool_release = false;
+thread_local DevArena *tl_arena = nullptr;
+constexpr size_t kArenaChunk = 256ull << 20;
+constexpr size_t kArenaAlign = 256;
 std::atomic<long long> g_npool{0};
 size_t size_class(size_t b)
 {
@@ -105,7 +108,42 @@ struct PoolRelease {
     ~PoolRelease() { tl_pool_release = prev; }
 };
 
+ArenaScope::ArenaScope(DevArena *a) : prev(tl_arena) { tl_arena = a; }
+ArenaScope::~ArenaScope() { tl_arena = prev; }
+
+static hipError_t pool_malloc(void **p, size_t bytes);
+
 hipError_t dev_malloc(void **p, size_t bytes)
+{
+    DevArena *a = tl_arena;
+    if (!a) return pool_malloc(p, bytes);
+    size_t at = (a->off + kArenaAlign - 1) & ~(kArenaAlign - 1);
+    if (a->chunks.empty() || at + bytes > a->chunks.back().second) {
+        // (carving starts one alignment step in: no carved block has its chunk's address)
+        const size_t csz = std::max(kArenaChunk, ((bytes + kArenaAlign - 1) & ~(kArenaAlign - 1)) + kArenaAlign);
+        void *c = nullptr;
+        tl_arena = nullptr;   // (the chunk itself comes from the process cache or hipMalloc)
+        const hipError_t e = pool_malloc(&c, csz);
+        tl_arena = a;
+        if (e != hipSuccess) return e;
+        a->chunks.push_back({static_cast<char *>(c), csz});
+        at = kArenaAlign;
+    }
+    *p = a->chunks.back().first + at;
+    a->off = at + bytes;
+    std::lock_guard<std::mutex> g(block_pool().mu);
+    block_pool().live[*p] = {-1, 0};   // (carved: dev_free leaves it to the arena)
+    return hipSuccess;
+}
+
+void DevArena::release()
+{
+    for (auto &c : chunks) dev_free(c.first);
+    chunks.clear();
+    off = 0;
+}
+
+static hipError_t pool_malloc(void **p, size_t bytes)
 {
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -156,6 +194,7 @@ void dev_free(void *p)
         if (it != bp.live.end()) {
             const auto key = it->second;
             bp.live.erase(it);
+            if (key.second == 0) return;   // carved from an arena: freed with it
             if (tl_pool_release && bp.cached + key.second <= kPoolCap) {
                 bp.free[key].push_back(p);
                 bp.cached += key.second;
@@ -1334,7 +1373,10 @@ void xfk_problem_destroy(xfk_problem *P)
     {
         PoolRelease pr;   // (main stream synchronised above, side-stream work joined into it)
         delete P->amg;
+        P->amg = nullptr;
+        DevArena arena = std::move(P->arena);
         delete P;   // device buffers free themselves (DBuf) into the process cache
+        arena.release();   // (after every buffer carved from it)
     }
     stream_release(s);   // (synchronised above; pooled for the next problem)
 }
@@ -1687,6 +1729,7 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
 {
     CreateTrace tr;
     xfk_problem *P = new xfk_problem();
+    ArenaScope arena_scope(&P->arena);
     P->device = device;
     if (std::getenv("XFK_SPIN_WAIT")) {   // experiment: host waits spin instead of yielding
         hipError_t e = hipSetDevice(device);
@@ -2038,6 +2081,7 @@ int xfk_dist_get_info(const xfk_problem *P, xfk_dist_info *info)
 
 int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
 {
+    ArenaScope arena_scope(P ? &P->arena : nullptr);
     XFK_REQUIRE(P, XFK_ERR_ARG, "null problem");
     XFK_REQUIRE(!P->harmonic, XFK_ERR_ARG, "harmonic problem: use xfk_harmonic2d");
     XFK_CHECK(hipSetDevice(P->device));

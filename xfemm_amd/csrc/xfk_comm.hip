@@ -58,6 +58,7 @@ struct CommRecording {
         const size_t b = (size_t)bytes, a = (b + 255) & ~size_t(255);
         if (chunks.empty() || used + a > chunks.back()->n) {
             chunks.emplace_back(new DBuf<char>());
+            ArenaScope own(nullptr);   // (the recording outlives the problem whose solve it records)
             XFK_CHECK(chunks.back()->alloc(std::max(kChunk, a)));
             used = 0;
         }

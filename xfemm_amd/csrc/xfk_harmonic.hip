@@ -1570,6 +1570,7 @@ int xfk_problem_create_harmonic_dist(const xfk_problem_desc *d, const xfk_harmon
 
 int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
 {
+    ArenaScope arena_scope(P ? &P->arena : nullptr);
     XFK_REQUIRE(P && P->harmonic, XFK_ERR_ARG, "not a harmonic problem (xfk_problem_create_harmonic)");
     XFK_CHECK(hipSetDevice(P->device));
     hipStream_t s = P->stream;

@@ -173,6 +173,22 @@ struct NewtonScalars {
 hipError_t dev_malloc(void **p, size_t bytes);
 void dev_free(void *p);
 
+// A problem's device arena: while an ArenaScope of the problem is active on
+// the calling thread, dev_malloc carves buffers out of chunks of >= 256 MiB
+// (a few hipMalloc per problem instead of one per buffer: ~130 in a first
+// solve, ~1 ms), and dev_free of such a buffer is a no-op; the chunks go back
+// to the process cache when the problem is destroyed.
+struct DevArena {
+    std::vector<std::pair<char *, size_t>> chunks;
+    size_t off = 0;   // used bytes of the last chunk
+    void release();   // (the problem's device work finished)
+};
+struct ArenaScope {
+    DevArena *prev;
+    explicit ArenaScope(DevArena *a);
+    ~ArenaScope();
+};
+
 template <class T>
 struct DBuf {
     T *p = nullptr;
@@ -268,6 +284,7 @@ int exchange_overlapped(hipStream_t s, SideStream &ss, Ex &&exch, In &&interior,
 
 // The opaque problem handle of the C-ABI.
 struct xfk_problem {
+    xfk::DevArena arena;             // (declared first: destroyed after every buffer carved from it)
     int device = 0;
     hipStream_t stream = nullptr;
 
