@@ -1,0 +1,12 @@
+# round-4 measurement pass: full -m gpu suite, smoke, rocprof trace + PMC passes of the bench
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+fatal() { case $1 in 124|137|134|139) exit $1;; esac; }
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests_r04r.log 2>&1
+rc=$?; echo "tests rc=$rc"; fatal $rc
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_r04r.log 2>&1
+rc=$?; echo "smoke rc=$rc"; fatal $rc
+bash tools/profile.sh r04r --no-fsolver
+echo "prof rc=$?"
