@@ -424,13 +424,17 @@ def test_stagnation_falls_back_to_f64(monkeypatch):
 def test_newton_refresh_refolds_level0(monkeypatch):
     """A Newton refresh keeps level 0 folded: P~ = (I - w D^-1 A) P re-formed
     numerically for the new matrix over its own pattern (k_refold_p).  The
-    answer meets the nonlinear parity tolerance, is deterministic, and needs
+    answer meets the nonlinear parity tolerance, is deterministic, is the same
+    bit for bit when no row is staged in LDS (XFK_REFOLD_STAGE=0), and needs
     no more PCG iterations than the unfolded refresh (XFK_AMG_REFOLD=0) plus
     one per Newton step."""
     pr, mesh, kw = synth_to_oracle(synth.magnetostatic(80, nonlinear=True))
     Ao, _, _ = oracle.solve(pr, mesh)
     A1, r1, Ac = _solve_vs(kw, pr, mesh, precond="amg")
     A1b, _ = _solve(kw, precond="amg")
+    monkeypatch.setenv("XFK_REFOLD_STAGE", "0")   # every row's products read from memory, same order
+    A1m, _ = _solve(kw, precond="amg")
+    monkeypatch.delenv("XFK_REFOLD_STAGE")
     monkeypatch.setenv("XFK_AMG_REFOLD", "0")
     A0, r0 = _solve(kw, precond="amg")
     print("refold: %d PCG / %d Newton; unfolded refresh: %d / %d"
@@ -438,4 +442,18 @@ def test_newton_refresh_refolds_level0(monkeypatch):
     assert rel_err(A1, Ac) <= TOL_NONLINEAR, parity_message(A1, Ao, Ac, TOL_NONLINEAR)
     assert rel_err(A0, Ac) <= TOL_NONLINEAR
     assert np.array_equal(A1.view(np.int64), A1b.view(np.int64))
+    assert np.array_equal(A1.view(np.int64), A1m.view(np.int64))
     assert r1["cg_iters"] <= r0["cg_iters"] + r1["newton_iters"], (r1["cg_iters"], r0["cg_iters"])
+
+
+def test_bh_bisection_matches_the_knot_scan(monkeypatch):
+    """The B-H interval lookup bisects non-decreasing tables instead of the
+    reference's first-match scan (CMaterialProp.cpp:1039): the same
+    knot interval for every B, so the nonlinear solve is the same bit for bit
+    as with the scan forced (XFK_BH_SCAN)."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(80, nonlinear=True))
+    A1, r1 = _solve(kw, precond="amg")
+    monkeypatch.setenv("XFK_BH_SCAN", "1")
+    A0, r0 = _solve(kw, precond="amg")
+    assert r1["newton_iters"] == r0["newton_iters"] and r1["cg_iters"] == r0["cg_iters"]
+    assert np.array_equal(A1.view(np.int64), A0.view(np.int64))

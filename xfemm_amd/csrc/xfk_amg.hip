@@ -2201,36 +2201,90 @@ __global__ void __launch_bounds__(256) k_fold_p(int n, const unsigned long long 
 }
 
 // A Newton refresh (new level-0 values, same pattern, same P): P~ re-formed
-// numerically over its own pattern, P~_ic = P_ic - w d_i sum_j a_ij P_jc --
-// one lane per P~ entry (kFoldLanes lanes per row), the sum over row i of A in
-// its column order, each P_jc found by a scan of the short P row j; no SpGEMM
-// (the pattern of A P is the pattern of P~, which the setup formed)
+// numerically over its own pattern, P~_ic = P_ic - w d_i sum_j a_ij P_jc, no
+// SpGEMM (the pattern of A P is the pattern of P~, which the setup formed).
+// kFoldLanes lanes per row: the row's products a_ij x (c, P_jc) -- A's row in
+// column order, each P row j in its stored order -- are staged in LDS once
+// (the lanes' P-row lengths prefix-summed by shuffles); then one lane per P~
+// entry c sums the products of column c in that order (P rows hold a column
+// once, so the sum is the one over j in A's column order).  Rows of more than
+// kRfA entries or kRfP products read A and P from memory in the same order.
+// f32 (optional): the f32 copy of P~ written alongside.  stage = 0 reads
+// every row from memory (XFK_REFOLD_STAGE=0: the test of the staged order).
+constexpr int kRfA = 16, kRfP = 64, kRfRows = 256 / kFoldLanes;
+static_assert(kRfA == 2 * kFoldLanes, "k_refold_p stages two A entries per lane");
 __global__ void __launch_bounds__(256) k_refold_p(int n, const unsigned long long *rho, const double *__restrict__ dinv,
                                                   const int *__restrict__ rowptr, const int *__restrict__ col,
                                                   const double *__restrict__ val, const int *__restrict__ prow,
                                                   const int *__restrict__ pcol, const double *__restrict__ pval,
                                                   const int *__restrict__ frow, const int *__restrict__ fcol,
-                                                  double *__restrict__ fval)
+                                                  double *__restrict__ fval, float *__restrict__ f32, int stage)
 {
-    const int i = (int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) / kFoldLanes);
-    if (i >= n) return;
-    const int g = threadIdx.x & (kFoldLanes - 1);
+    // (rows padded by one element: the 8 rows of a wave read one e at a time)
+    __shared__ int s_pc[kRfRows][kRfP + 1];
+    __shared__ double s_av[kRfRows][kRfP + 1], s_pv[kRfRows][kRfP + 1];
+    const int lr = threadIdx.x / kFoldLanes, g = threadIdx.x & (kFoldLanes - 1);
+    const int i = (int)blockIdx.x * kRfRows + lr;
+    const bool live = i < n;   // (every thread reaches the barrier)
+    const int ab = live ? rowptr[i] : 0, na = live ? rowptr[i + 1] - ab : 0;
+    // lane g: A entries u = g and u = g + kFoldLanes, their P rows
+    int pb[2] = {0, 0}, len[2] = {0, 0};
+    double av[2] = {0.0, 0.0};
+    if (na <= kRfA)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int u = g + h * kFoldLanes;
+            if (u < na) {
+                const int j = col[ab + u];
+                pb[h] = prow[j];
+                len[h] = prow[j + 1] - pb[h];
+                av[h] = val[ab + u];
+            }
+        }
+    int off[2], tot = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // exclusive prefix over u = 0 .. 15
+        int inc = len[h];
+#pragma unroll
+        for (int d = 1; d < kFoldLanes; d <<= 1) {
+            const int v = __shfl_up(inc, d, kFoldLanes);
+            if (g >= d) inc += v;
+        }
+        off[h] = tot + inc - len[h];
+        tot += __shfl(inc, kFoldLanes - 1, kFoldLanes);
+    }
+    const bool staged = stage && na <= kRfA && tot <= kRfP;
+    if (staged)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            for (int q = 0; q < len[h]; ++q) {
+                s_pc[lr][off[h] + q] = pcol[pb[h] + q];
+                s_pv[lr][off[h] + q] = pval[pb[h] + q];
+                s_av[lr][off[h] + q] = av[h];
+            }
+    __syncthreads();
+    if (!live) return;
     const double ra = rho_of(rho);
     const double wd = (ra > 0.0 ? 1.0 / ra : 0.0) * dinv[i];
-    const int ab = rowptr[i], ae = rowptr[i + 1];
+    const int qb = prow[i], qe = prow[i + 1];
     for (int k = frow[i] + g; k < frow[i + 1]; k += kFoldLanes) {
         const int c = fcol[k];
         double ap = 0.0, pic = 0.0;
-        for (int q = prow[i]; q < prow[i + 1]; ++q)
+        for (int q = qb; q < qe; ++q)
             if (pcol[q] == c) pic = pval[q];
-        for (int t = ab; t < ae; ++t) {
-            const int j = col[t];
-            double pjc = 0.0;
-            for (int q = prow[j]; q < prow[j + 1]; ++q)
-                if (pcol[q] == c) pjc = pval[q];
-            ap += val[t] * pjc;
+        if (staged) {
+            for (int e = 0; e < tot; ++e)
+                if (s_pc[lr][e] == c) ap = fma(s_av[lr][e], s_pv[lr][e], ap);
+        } else {
+            for (int t = ab; t < ab + na; ++t) {
+                const int j = col[t];
+                for (int q = prow[j]; q < prow[j + 1]; ++q)
+                    if (pcol[q] == c) ap = fma(val[t], pval[q], ap);
+            }
         }
-        fval[k] = pic - wd * ap;
+        const double v = pic - wd * ap;
+        fval[k] = v;
+        if (f32) f32[k] = (float)v;
     }
 }
 
@@ -4709,6 +4763,12 @@ static bool refold_on()
     return !(e && std::atoi(e) == 0);
 }
 
+static int refold_stage()
+{
+    const char *e = std::getenv("XFK_REFOLD_STAGE");   // (read per refresh: tests toggle it)
+    return (e && std::atoi(e) == 0) ? 0 : 1;
+}
+
 int Amg::refresh(hipStream_t s)
 {
     AmgLevel &A = *L[0];
@@ -4736,13 +4796,10 @@ int Amg::refresh(hipStream_t s)
         if (rc != XFK_OK) return rc;
     }
     if (refold && n > 0) {   // P~ = (I - w D^-1 A_new) P over its own pattern (new D^-1 and rho above)
-        k_refold_p<<<(int)(((long long)n * kFoldLanes + 255) / 256), 256, 0, s>>>(
-            n, rho.p, A.dinv.p, A.rowptr, A.col, A.val, A.prow.p, A.pcol.p, A.pval.p, A.ftrow.p, A.ftcol.p,
-            A.ftval.p);
-        if (A.has32) {
-            int rc = to_f32(s, n, A.ftrow.p, A.fnnz, A.ftval.p, A.f32v);
-            if (rc != XFK_OK) return rc;
-        }
+        if (A.has32) AMG_CHECK(A.f32v.alloc((size_t)std::max(1LL, A.fnnz)));   // (the setup's copy: same pattern)
+        k_refold_p<<<(n + kRfRows - 1) / kRfRows, 256, 0, s>>>(n, rho.p, A.dinv.p, A.rowptr, A.col, A.val, A.prow.p,
+                                                                A.pcol.p, A.pval.p, A.ftrow.p, A.ftcol.p, A.ftval.p,
+                                                                A.has32 ? A.f32v.p : nullptr, refold_stage());
     }
     AMG_CHECK(hipGetLastError());
     return XFK_OK;

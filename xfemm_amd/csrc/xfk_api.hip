@@ -1547,8 +1547,11 @@ void prepare_global(const xfk_problem_desc *d, GlobalPrep &G)
         o.mu_x = b.mu_x; o.mu_y = b.mu_y; o.H_c = b.H_c; o.J_re = b.J_re; o.Cduct = b.Cduct;
         o.LamFill = b.LamFill; o.LamType = b.LamType; o.BHpoints = b.BHpoints;
         o.bh_off = (int)G.hB.size();
-        o.pad = 0;
+        // (XFK_BH_SCAN: the reference's knot scan for every table -- the test
+        // that the bisection finds the same intervals)
+        o.bh_sorted = std::getenv("XFK_BH_SCAN") ? 0 : 1;
         for (int i = 0; i < b.BHpoints; ++i) {
+            if (i > 0 && !(b.B[i] >= b.B[i - 1])) o.bh_sorted = 0;
             G.hB.push_back(b.B[i]);
             G.hH.push_back(b.H[i]);
             G.hS.push_back(b.slope[i]);

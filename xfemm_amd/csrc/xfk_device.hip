@@ -735,19 +735,37 @@ __device__ void get_bh_props(const DevBlock &m, const double *__restrict__ Bt, c
         dv = 0.5 * (dh / (b * b) - h / (b * b * b));
         return;
     }
-    for (int i = 0; i < n - 1; ++i)
-        if ((b >= Bd[i]) && (b <= Bd[i + 1])) {
-            double l = (Bd[i + 1] - Bd[i]);
-            double z = (b - Bd[i]) / l;
-            double z2 = z * z;
-            double h = (1. - 3. * z2 + 2. * z2 * z) * Hd[i] + z * (1. - 2. * z + z2) * l * sl[i] +
-                       z2 * (3. - 2. * z) * Hd[i + 1] + z2 * (z - 1.) * l * sl[i + 1];
-            double dh = 6. * z * (z - 1.) * Hd[i] / l + (1. - 4. * z + 3. * z * z) * sl[i] +
-                        6. * z * (1. - z) * Hd[i + 1] / l + z * (3. * z - 2.) * sl[i + 1];
-            v = h / b;
-            dv = 0.5 * (dh / (b * b) - h / (b * b * b));
-            return;
+    // the first knot interval with Bd[i] <= b <= Bd[i + 1], as the reference's
+    // scan finds it; on a non-decreasing table that is the first i with
+    // Bd[i + 1] >= b (b <= Bd[n - 1] here) if Bd[i] <= b, else none -- found
+    // by bisection (~6 dependent loads instead of a scan of ~25 on M-19)
+    int lo = -1;
+    if (m.bh_sorted) {
+        int l = 0, h = n - 2;
+        while (l < h) {
+            const int mid = (l + h) >> 1;
+            if (Bd[mid + 1] >= b) h = mid;
+            else l = mid + 1;
         }
+        if (b >= Bd[l]) lo = l;
+    } else {
+        for (int i = 0; i < n - 1; ++i)
+            if ((b >= Bd[i]) && (b <= Bd[i + 1])) {
+                lo = i;
+                break;
+            }
+    }
+    if (lo < 0) return;
+    const int i = lo;
+    double l = (Bd[i + 1] - Bd[i]);
+    double z = (b - Bd[i]) / l;
+    double z2 = z * z;
+    double h = (1. - 3. * z2 + 2. * z2 * z) * Hd[i] + z * (1. - 2. * z + z2) * l * sl[i] +
+               z2 * (3. - 2. * z) * Hd[i + 1] + z2 * (z - 1.) * l * sl[i + 1];
+    double dh = 6. * z * (z - 1.) * Hd[i] / l + (1. - 4. * z + 3. * z * z) * sl[i] +
+                6. * z * (1. - z) * Hd[i + 1] / l + z * (3. * z - 2.) * sl[i + 1];
+    v = h / b;
+    dv = 0.5 * (dh / (b * b) - h / (b * b * b));
 }
 
 // FSolver::StaticAxisymmetric element (staticaxi.cpp:172-636): x is r, y is

@@ -80,7 +80,8 @@ void set_error(const std::string &msg);
 // Per-block material parameters, as read by Static2D (CMSolverMaterialProp).
 struct DevBlock {
     double mu_x, mu_y, H_c, J_re, Cduct, LamFill;
-    int LamType, BHpoints, bh_off, pad;
+    int LamType, BHpoints, bh_off;
+    int bh_sorted;   // B knots non-decreasing: the interval lookup may bisect
 };
 
 // Per-label parameters; the magnetisation direction is pre-evaluated on the
