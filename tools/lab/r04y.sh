@@ -1,9 +1,9 @@
-# staged k_refold_p + B-H bisection: targeted GPU tests, configs[3] bench A/B (scan vs bisection), Newton trace
+# staged k_refold_p + B-H bisection + L0 restriction slots: targeted GPU tests, configs[3] bench A/B (scan vs bisection), Newton trace
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_amg.py tests/test_gpu_static2d.py > gpurun_out/tests_r04y.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_amg.py tests/test_gpu_static2d.py tests/test_gpu_antiperiodic_flux.py > gpurun_out/tests_r04y.log 2>&1
 rc=$?; echo "tests rc=$rc"; [ $rc -eq 0 ] || exit $rc
 for k in 1 2; do
   timeout -k 10 300 python bench.py --nonlinear --steps 3 --warmup 1 --no-cpu-baseline --no-fsolver --no-secondary > gpurun_out/nl_new_$k.json 2> gpurun_out/nl_new_$k.err
@@ -11,6 +11,7 @@ for k in 1 2; do
   XFK_BH_SCAN=1 timeout -k 10 300 python bench.py --nonlinear --steps 3 --warmup 1 --no-cpu-baseline --no-fsolver --no-secondary > gpurun_out/nl_scan_$k.json 2> gpurun_out/nl_scan_$k.err
   rc=$?; echo "scan $k rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
+bash tools/lab/variant_exp.sh r04y XFK_R0_SLOTS "6 8 7 6" --no-fsolver --steps 10 --warmup 3 || exit $?
 OUT=gpurun_out/prof_r04y
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d $OUT/trace -o run -- python3 bench.py --nonlinear --steps 1 --warmup 2 --no-cpu-baseline --no-fsolver --no-secondary --no-phases > $OUT/bench_trace.json 2> $OUT/trace.err

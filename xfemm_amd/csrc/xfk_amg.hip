@@ -276,6 +276,40 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
     }
 }
 
+// a Newton refresh (same aggregates, P and weights; new values): only the
+// Gershgorin bound of D^-1 A, summed as k_amg_strength sums it (each lane's
+// entries in order, the same butterfly: the same bits); rho[1] is not used
+// after a setup and is left 0
+__global__ void __launch_bounds__(kB) k_amg_rho(int n, const int *__restrict__ rowptr, ColView cv,
+                                                const double *__restrict__ val, double *__restrict__ rho_part)
+{
+    __shared__ double red[2 * (kB / 64)];
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / kStrG;
+    const int g = threadIdx.x % kStrG;
+    double rA = 0.0, rF = 0.0, aii = 0.0, sumA = 0.0;
+    if (i < n) {
+        const int cb = cv.base(i);
+        const int e = rowptr[i + 1];
+        for (int k = rowptr[i] + g; k < e; k += kStrG) {
+            const int j = cv.at(cb, k);
+            const double a = val[k];
+            if (j == i) aii = a;
+            else sumA += fabs(a);
+        }
+    }
+#pragma unroll
+    for (int off = 1; off < kStrG; off <<= 1) {
+        aii += __shfl_xor(aii, off, kStrG);
+        sumA += __shfl_xor(sumA, off, kStrG);
+    }
+    if (i < n && g == 0 && aii != 0.0) rA = (fabs(aii) + sumA) / fabs(aii);
+    block_max2(rA, rF, red);
+    if (threadIdx.x == 0) {
+        rho_part[blockIdx.x] = rA;
+        rho_part[gridDim.x + blockIdx.x] = rF;
+    }
+}
+
 // --------------------------------------------------------------------------
 // setup: MIS-2 aggregation
 // --------------------------------------------------------------------------
@@ -2851,11 +2885,32 @@ static int rmv_mode()
 // level 0 with f32 values: the 256-row tile kernels (level 0 always has >= kTileMinRows rows)
 // (128- and 64-row tiles for R's ~25-entry rows were measured slower: 14.4 -> 15.0 / 15.6 us,
 // profiles/r04_experiments/r04h_XFK_R0_TILE_*.json)
+// XFK_R0_SLOTS (lab): staging slots per lane for the long rows (6 = 6144
+// products per pass; R's ~27-entry rows fill 256-row tiles with ~6900)
+static int r0_slots()
+{
+    static const int v = [] {
+        const char *e = std::getenv("XFK_R0_SLOTS");
+        return e ? std::atoi(e) : 6;
+    }();
+    return v;
+}
+
 void launch_mv32(hipStream_t s, int n, const int *rowptr, const int *col, const float *val, const double *x,
                  double *y, bool acc, int G, const int *done, const unsigned short *c16, const int *cbase)
 {
     if (n <= 0) return;
     const int g = (n + 255) / 256;
+    if (G > 4 && r0_slots() != 6) {
+        if (r0_slots() == 8) {
+            if (acc) k_csr_mv_tile<256, true, 8><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+            else k_csr_mv_tile<256, false, 8><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+        } else {
+            if (acc) k_csr_mv_tile<256, true, 7><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+            else k_csr_mv_tile<256, false, 7><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+        }
+        return;
+    }
     if (G <= 4) {
         if (acc) k_csr_mv_tile<256, true, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
         else k_csr_mv_tile<256, false, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
@@ -4778,17 +4833,12 @@ int Amg::refresh(hipStream_t s)
     const bool refold = A.fold && !dist && refold_on() && A.fnnz > 0;
     A.fold = refold;
     AMG_CHECK(absd.alloc(std::max(1, n)));
-    AMG_CHECK(dfinv.alloc(std::max(1, n)));
-    AMG_CHECK(wF.alloc(std::max(1, n)));
-    AMG_CHECK(cnt.alloc((size_t)n + 1));
-    AMG_CHECK(sflag.alloc((size_t)std::max(1LL, A.nnz)));
     AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(n))));
     if (n > 0) {
         k_amg_diag<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
-        k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr,
-                                                ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
-                                                A.val, absd.p, A.dinv.p, sflag.p, cnt.p,
-                                                dfinv.p, wF.p, rho_part.p, signed_strength());
+        k_amg_rho<<<nb_str(n), kB, 0, s>>>(n, A.rowptr,
+                                           ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
+                                           A.val, rho_part.p);
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p);
     }
     if (A.has32 && f32_sweep_on()) {   // the sweeps' f32 copy of the new values

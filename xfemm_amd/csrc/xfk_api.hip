@@ -1231,6 +1231,14 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
     // (clamped like every later batch, and never past the iteration cap, so a
     // zero-diagonal matrix is still caught at the first poll)
     if (flag == 0 && P->pcg_hint0 > 0) batch = std::min(P->pcg_hint0, 512);
+    // a warm start (a Newton pass from the last iterate; the restart after a
+    // fresh hierarchy) needs anything from 1 to ~25 iterations: one
+    // iteration, then a batch sized from the residual it left and the rate
+    // of this problem's last solve (an iteration launched after convergence
+    // still costs its ~14 launches: 8 of them in a 1-iteration pass ~0.5 ms)
+    else if (flag != 0 && P->pc_used == XFK_PRECOND_AMG && P->pcg_rate < 0) batch = 1;
+    long long it0 = -1;   // the first poll: iterations and er, for the observed rate
+    double er0 = 0;
     // Every batch ends with an update, whose convergence test the poll reads:
     // the V-cycle and SpMV of that iteration open the next batch, so the
     // converged solve launches no iteration tail that would only exit
@@ -1278,13 +1286,34 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
         if (P->pc_used == XFK_PRECOND_AMG && P->amg && P->amg->f32_active() &&
             (force || !std::isfinite(S.er) || (S.iters >= kF32Guard && S.er > 1e-4)))
             return kRetryF64;
-        // size the next batch from the observed convergence rate
+        // the stale-hierarchy projection: the rate from er = 1 at iteration 0
         double rate = (S.iters > 0 && S.er > 0 && S.er < 1) ? std::log(S.er) / (double)S.iters : 0.0;
         long long rem = rate < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / rate) : 2 * batch;
         // (S and the counts are the same on every rank: collective-safe)
         if (stale > 0 && (S.iters >= stale || S.iters + rem > stale)) return kRetryFresh;
-        rem = std::max<long long>(8, std::min<long long>(rem + 2, 512));
-        batch = (int)rem;
+        // the next batch: the iterations left at the rate observed since the
+        // first poll (else the last solve's, else the one above), not padded --
+        // one more poll (~25 us) costs less than an iteration launched past
+        // convergence (~70 us)
+        double r2 = 0.0;
+        if (it0 >= 0 && S.iters > it0 && S.er > 0 && S.er < er0) r2 = std::log(S.er / er0) / (double)(S.iters - it0);
+        else if (P->pcg_rate < 0) r2 = P->pcg_rate;
+        else r2 = rate;
+        if (it0 < 0 && S.er > 0) {
+            it0 = S.iters;
+            er0 = S.er;
+        }
+        const long long nb = r2 < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / r2) : 2 * batch;
+        batch = (int)std::max<long long>(1, std::min<long long>(nb, 512));
+        // (Jacobi: ~25 us iterations -- padded, at least 8 per poll)
+        if (P->pc_used != XFK_PRECOND_AMG) batch = (int)std::max<long long>(8, std::min<long long>(rem + 2, 512));
+    }
+    {   // this solve's rate, for the next warm start's batches
+        const CgState &S = *P->pcg_host;
+        double r = 0.0;
+        if (it0 >= 0 && S.iters > it0 && S.er > 0 && S.er < er0) r = std::log(S.er / er0) / (double)(S.iters - it0);
+        else if (flag == 0 && S.iters > 0 && S.er > 0 && S.er < 1) r = std::log(S.er) / (double)S.iters;
+        if (r < 0 && P->pc_used == XFK_PRECOND_AMG) P->pcg_rate = r;
     }
     if (flag == 0) P->pcg_hint0 = (int)P->pcg_host->iters + 1;   // iteration it = iters detected the stop
     return XFK_OK;

@@ -314,6 +314,7 @@ struct xfk_problem {
     hipEvent_t nnz_ev = nullptr;     // the pattern's lengths landed in hpin[0..1] (deferred read)
     bool nnz_pending = false;        // nnz / nnz_own not read back yet (xfk_resolve_nnz)
     int pcg_hint0 = 0;               // PCG iterations of the last solve's first pass (first batch)
+    double pcg_rate = 0;             // log(er) per iteration in the last converged solve (< 0; 0: none yet)
     std::vector<hipEvent_t> setup_ev;   // AMG setup event pairs, read after the solve
     int setup_used = 0;
     double setup_ms_pending = 0;        // pairs read out early when the pool filled
