@@ -457,3 +457,31 @@ def test_bh_bisection_matches_the_knot_scan(monkeypatch):
     A0, r0 = _solve(kw, precond="amg")
     assert r1["newton_iters"] == r0["newton_iters"] and r1["cg_iters"] == r0["cg_iters"]
     assert np.array_equal(A1.view(np.int64), A0.view(np.int64))
+
+
+def test_newton_state_pass_matches_per_row_evaluation(monkeypatch):
+    """A planar Newton pass evaluates each element's new state (B, GetBHProps,
+    the permeabilities, dv) once (k_planar_state) for the three rows that
+    gather the element, instead of once per row (XFK_ASM_STATE=0): the same
+    arithmetic, so the same solve bit for bit."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(80, nonlinear=True))
+    A1, r1 = _solve(kw, precond="amg")
+    monkeypatch.setenv("XFK_ASM_STATE", "0")
+    A0, r0 = _solve(kw, precond="amg")
+    assert r1["newton_iters"] == r0["newton_iters"] and r1["cg_iters"] == r0["cg_iters"]
+    assert np.array_equal(A1.view(np.int64), A0.view(np.int64))
+
+
+def test_refold_threshold_unfolds_short_passes(monkeypatch):
+    """A refresh re-forms P~ only when the last Newton pass ran at least
+    XFK_REFOLD_MIN PCG iterations; below it level 0 runs unfolded for the pass.
+    A threshold no pass reaches gives the always-unfolded solve bit for bit
+    (XFK_AMG_REFOLD=0), and the parity tolerance either way."""
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(80, nonlinear=True))
+    monkeypatch.setenv("XFK_REFOLD_MIN", "100000")
+    A1, r1, Ac = _solve_vs(kw, pr, mesh, precond="amg")
+    monkeypatch.delenv("XFK_REFOLD_MIN")
+    monkeypatch.setenv("XFK_AMG_REFOLD", "0")
+    A0, r0 = _solve(kw, precond="amg")
+    assert rel_err(A1, Ac) <= TOL_NONLINEAR
+    assert np.array_equal(A1.view(np.int64), A0.view(np.int64))

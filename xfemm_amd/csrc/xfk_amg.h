@@ -62,6 +62,7 @@ struct AmgLevel {
     DBuf<double> pval, rval;
     // folded level (xfk_amg.hip: k_fold_pre): P~ = (I - w D^-1 A) P and R~ = P~^T
     bool fold = false;
+    bool fold_formed = false;         // the setup formed P~ (a refresh may fold or not)
     long long fnnz = 0;
     DBuf<int> ftrow, ftcol, frrow, frcol;
     DBuf<double> ftval, frval;
@@ -232,8 +233,9 @@ struct Amg {
     int vcycle(hipStream_t s, const double *r, double *u, const int *done, double *part_gam = nullptr);
     bool gamma_done = false;
     // New values in the level-0 matrix (same pattern): refresh the fine-level
-    // smoother (D^-1, rho_A); the coarse levels are kept
-    int refresh(hipStream_t s);
+    // smoother (D^-1, rho_A); the coarse levels are kept.
+    // fold: level 0 stays folded (P~ re-formed for the new values); false: it runs unfolded
+    int refresh(hipStream_t s, bool fold = true);
 
   private:
     int init(hipStream_t s);

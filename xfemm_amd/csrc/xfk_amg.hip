@@ -2886,7 +2886,8 @@ static int rmv_mode()
 // (128- and 64-row tiles for R's ~25-entry rows were measured slower: 14.4 -> 15.0 / 15.6 us,
 // profiles/r04_experiments/r04h_XFK_R0_TILE_*.json)
 // XFK_R0_SLOTS (lab): staging slots per lane for the long rows (6 = 6144
-// products per pass; R's ~27-entry rows fill 256-row tiles with ~6900)
+// products per pass; R's ~27-entry rows fill 256-row tiles with ~6900);
+// 8 / 7 (one pass, 64 / 56 KiB of LDS) measured 20.3 / 20.2 us vs 14.7 us
 static int r0_slots()
 {
     static const int v = [] {
@@ -2901,14 +2902,12 @@ void launch_mv32(hipStream_t s, int n, const int *rowptr, const int *col, const 
 {
     if (n <= 0) return;
     const int g = (n + 255) / 256;
-    if (G > 4 && r0_slots() != 6) {
-        if (r0_slots() == 8) {
-            if (acc) k_csr_mv_tile<256, true, 8><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
-            else k_csr_mv_tile<256, false, 8><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
-        } else {
-            if (acc) k_csr_mv_tile<256, true, 7><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
-            else k_csr_mv_tile<256, false, 7><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
-        }
+    if (G > 4 && r0_slots() != 6 && !acc) {
+        const int v = r0_slots();
+        if (v == 8) k_csr_mv_tile<256, false, 8><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+        else if (v == 4) k_csr_mv_tile<256, false, 4><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+        else if (v == 3) k_csr_mv_tile<256, false, 3><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
+        else k_csr_mv_tile<256, false, 2><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
         return;
     }
     if (G <= 4) {
@@ -3911,6 +3910,7 @@ int Amg::build(hipStream_t s, int l0)
         if (rc != XFK_OK) return rc;
         // folded level (l >= 1): P~ from A P before the next level reuses its buffers
         A.fold = (fold_on < 0 ? fold_levels() : fold_on != 0) && sweeps == 1 && !A.dist;
+        A.fold_formed = A.fold;
         if (A.fold) {
             if (g_prof) g_prof->begin(lv + "folded transfer P~ = (I - w D^-1 A) P, R~ = P~^T", 0.0);
             A.fnnz = ap_nnz;   // an upper bound while the A P length is deferred
@@ -4824,13 +4824,14 @@ static int refold_stage()
     return (e && std::atoi(e) == 0) ? 0 : 1;
 }
 
-int Amg::refresh(hipStream_t s)
+int Amg::refresh(hipStream_t s, bool fold)
 {
     AmgLevel &A = *L[0];
     const int n = A.n;
     // level 0's P~ belongs to the matrix it was formed from: re-formed below
-    // for the new values (k_refold_p), or level 0 runs unfolded
-    const bool refold = A.fold && !dist && refold_on() && A.fnnz > 0;
+    // for the new values (k_refold_p), or level 0 runs unfolded; a refresh
+    // that unfolds keeps P~'s arrays, so a later one may fold again
+    const bool refold = fold && A.fold_formed && !dist && refold_on() && A.fnnz > 0;
     A.fold = refold;
     AMG_CHECK(absd.alloc(std::max(1, n)));
     AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(n))));

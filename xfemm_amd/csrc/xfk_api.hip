@@ -710,6 +710,10 @@ int build_symbolic(xfk_problem *P)
     if (!P->harmonic) {
         XFK_CHECK(P->mu1b.alloc(NE));
         XFK_CHECK(P->mu2b.alloc(NE));
+        if (P->any_nonlinear && !P->axi) {
+            XFK_CHECK(P->dv_el.alloc(NE));
+            XFK_CHECK(P->on_el.alloc(NE));
+        }
         XFK_CHECK(P->asm_miss.alloc(1));
         XFK_CHECK(hipMemsetAsync(P->asm_miss.p, 0, sizeof(int), s));
         P->miss_checked = false;
@@ -894,6 +898,12 @@ static int assemble(xfk_problem *P, int iter)
     A.mu1_out = P->any_nonlinear ? P->mu1b.p : nullptr;
     A.mu2_out = P->any_nonlinear ? P->mu2b.p : nullptr;
     A.miss = P->asm_miss.p;
+    // (XFK_ASM_STATE=0: the Newton state evaluated per row, as before -- measurement / the test)
+    const char *st = std::getenv("XFK_ASM_STATE");
+    const bool pre = P->any_nonlinear && !P->axi && P->dv_el.p && !(st && std::atoi(st) == 0);
+    A.dv_el = pre ? P->dv_el.p : nullptr;
+    A.on_el = pre ? P->on_el.p : nullptr;
+    A.n_el = P->NE;
     launch_assemble_rows(s, P->NR, A);   // writes every entry of val and b (assembled rows)
     std::swap(P->mu1.p, P->mu1b.p);     // the state just written is read next iteration
     std::swap(P->mu1.n, P->mu1b.n);
@@ -991,6 +1001,10 @@ static int allreduce_partials(xfk_problem *P, int narrays)
 
 static bool trace_newton() { return std::getenv("XFK_TRACE_NEWTON") != nullptr; }
 
+// a Newton refresh re-forms level 0's P~ when the last pass ran at least
+// this many PCG iterations (else level 0 runs unfolded for the pass)
+constexpr int kRefoldMinIters = 0;
+
 // AMG hierarchy of the assembled matrix (owned block when sharded); falls
 // back to Jacobi for this solve when the hierarchy cannot be built
 static int amg_setup(xfk_problem *P)
@@ -1005,7 +1019,12 @@ static int amg_setup(xfk_problem *P)
     // (the decision reads iteration counts every rank shares)
     if (P->amg_reuse && P->amg_reusable && was_amg && P->amg &&
         P->amg_last_iters <= std::max(2 * P->amg_fresh_iters, P->amg_fresh_iters + 8)) {
-        int rc = P->amg->refresh(s);
+        // level 0 stays folded when the pass is expected to run long enough to
+        // repay re-forming P~ (k_refold_p): the last pass's count as the guess
+        // (XFK_REFOLD_MIN: that threshold)
+        const char *rm = std::getenv("XFK_REFOLD_MIN");   // (read per refresh: tests set it)
+        const int refold_min = rm ? std::atoi(rm) : kRefoldMinIters;
+        int rc = P->amg->refresh(s, P->amg_last_iters >= refold_min);
         if (rc != XFK_OK) return rc;
         P->pc_used = XFK_PRECOND_AMG;
         return XFK_OK;

@@ -895,18 +895,90 @@ __device__ __forceinline__ void axi_element(int eb, const AssembleArgs &A, const
         }
 }
 
+// The Newton state of a planar element (static2d.cpp:600-640): B from the
+// element's A, GetBHProps, the new permeabilities by lamination type; false
+// (m1 / m2 kept) when the element's material is linear or its state says so.
+// p / q / a: the element's geometry as planar_element forms it.
+__device__ __forceinline__ bool planar_newton_state(const AssembleArgs &A, const DevBlock &bp, const double (&p)[3],
+                                                    const double (&q)[3], double a, const double (&Vn)[3], double &m1,
+                                                    double &m2, double &dv)
+{
+    dv = 0;
+    if (!(bp.BHpoints > 0 && bp.LamType <= 2 && (bp.LamType != 0 || m1 == m2))) return false;
+    const double f = bp.LamFill;
+    double B1 = 0., B2 = 0.;
+    if (bp.LamType == 0) {
+        for (int j = 0; j < 3; ++j) { B1 += Vn[j] * q[j]; B2 += Vn[j] * p[j]; }
+    } else if (bp.LamType == 1) {
+        for (int j = 0; j < 3; ++j) { B1 += Vn[j] * q[j]; B2 += Vn[j] * p[j] / f; }
+    } else {
+        for (int j = 0; j < 3; ++j) { B1 += (Vn[j] * q[j]) / f; B2 += Vn[j] * p[j]; }
+    }
+    const double B = kC * sqrt(B1 * B1 + B2 * B2) / (0.02 * a);
+    double mu = 0;
+    get_bh_props(bp, A.bhB, A.bhH, A.bhS, B, mu, dv);
+    mu = 1. / (kMUO * mu);
+    if (bp.LamType == 0) { m1 = mu; m2 = mu; }
+    else if (bp.LamType == 1) { m1 = mu * f; m2 = mu / (f + mu * (1. - f)); }
+    else { m2 = mu * f; m1 = mu / (f + mu * (1. - f)); }
+    return true;
+}
+
+// the Newton terms Mn of a planar element in the state above (static2d.cpp:640-797)
+__device__ __forceinline__ void planar_newton_terms(const DevBlock &bp, const double (&Mx)[3][3],
+                                                    const double (&My)[3][3], double a, const double (&Vn)[3],
+                                                    double dv, double (&Mn)[3][3])
+{
+    const double f = bp.LamFill;
+    double v[3], u[3];
+    if (bp.LamType == 0) {
+        for (int j = 0; j < 3; ++j) {
+            v[j] = 0;
+            for (int w = 0; w < 3; ++w) v[j] += (Mx[j][w] + My[j][w]) * Vn[w];
+        }
+        const double Kn = -200. * kC * kC * kC * dv / a;
+        for (int j = 0; j < 3; ++j)
+            for (int w = 0; w < 3; ++w) Mn[j][w] = Kn * v[j] * v[w];
+    } else {
+        for (int j = 0; j < 3; ++j) {
+            v[j] = 0; u[j] = 0;
+            for (int w = 0; w < 3; ++w) {
+                if (bp.LamType == 1) {
+                    v[j] += (My[j][w] / f + Mx[j][w]) * Vn[w];
+                    u[j] += (My[j][w] / f + f * Mx[j][w]) * Vn[w];
+                } else {
+                    v[j] += (Mx[j][w] / f + My[j][w]) * Vn[w];
+                    u[j] += (Mx[j][w] / f + f * My[j][w]) * Vn[w];
+                }
+            }
+        }
+        const double Kn = -100. * kC * kC * kC * dv / (a);
+        for (int j = 0; j < 3; ++j)
+            for (int w = 0; w < 3; ++w) Mn[j][w] = Kn * (v[j] * u[w] + v[w] * u[j]);
+    }
+}
+
+// the element geometry of planar_element: p, q and the signed area a
+__device__ __forceinline__ double planar_geometry(const double (&X)[3], const double (&Y)[3], double (&p)[3],
+                                                  double (&q)[3])
+{
+    p[0] = Y[1] - Y[2]; p[1] = Y[2] - Y[0]; p[2] = Y[0] - Y[1];
+    q[0] = X[2] - X[1]; q[1] = X[0] - X[2]; q[2] = X[1] - X[0];
+    return (p[0] * q[1] - p[1] * q[0]) / 2.;
+}
+
 // FSolver::Static2D element (static2d.cpp:352-805): Me / be before the sign
-// of the global assembly, m1 / m2 the element's permeability state.
-template <bool FIRST>
+// of the global assembly, m1 / m2 the element's permeability state.  PRE (a
+// Newton pass, iter > 0): m1 / m2 are already the new state and pre_dv /
+// pre_on its dv and whether the Newton terms apply (k_planar_state).
+template <bool FIRST, bool PRE = false>
 __device__ __forceinline__ void planar_element(int eb, const AssembleArgs &A, const int (&n)[3],
                                                const double (&X)[3], const double (&Y)[3], const DevLabel &lab,
                                                const DevBlock &bp, double &m1, double &m2, double (&Me)[3][3],
-                                               double (&be)[3])
+                                               double (&be)[3], double pre_dv = 0.0, bool pre_on = false)
 {
     double p[3], q[3];
-    p[0] = Y[1] - Y[2]; p[1] = Y[2] - Y[0]; p[2] = Y[0] - Y[1];
-    q[0] = X[2] - X[1]; q[1] = X[0] - X[2]; q[2] = X[1] - X[0];
-    const double a = (p[0] * q[1] - p[1] * q[0]) / 2.;
+    const double a = planar_geometry(X, Y, p, q);
     const double K = (-1. / (4. * a));
     double Mx[3][3], My[3][3], Mn[3][3];
 #pragma unroll
@@ -973,50 +1045,9 @@ __device__ __forceinline__ void planar_element(int eb, const AssembleArgs &A, co
         else if (bp.LamType == 2) { m2 = bp.mu_y * f + (1. - f); m1 = bp.mu_y / (f + bp.mu_y * (1. - f)); }
         else { m1 = 1; m2 = 1; }
     } else {
-        if (bp.BHpoints > 0 && bp.LamType <= 2 && (bp.LamType != 0 || m1 == m2)) {
-            const double f = bp.LamFill;
-            double B1 = 0., B2 = 0.;
-            if (bp.LamType == 0) {
-                for (int j = 0; j < 3; ++j) { B1 += Vn[j] * q[j]; B2 += Vn[j] * p[j]; }
-            } else if (bp.LamType == 1) {
-                for (int j = 0; j < 3; ++j) { B1 += Vn[j] * q[j]; B2 += Vn[j] * p[j] / f; }
-            } else {
-                for (int j = 0; j < 3; ++j) { B1 += (Vn[j] * q[j]) / f; B2 += Vn[j] * p[j]; }
-            }
-            const double B = kC * sqrt(B1 * B1 + B2 * B2) / (0.02 * a);
-            double mu = 0, dv = 0;
-            get_bh_props(bp, A.bhB, A.bhH, A.bhS, B, mu, dv);
-            mu = 1. / (kMUO * mu);
-            double v[3], u[3];
-            if (bp.LamType == 0) {
-                m1 = mu; m2 = mu;
-                for (int j = 0; j < 3; ++j) {
-                    v[j] = 0;
-                    for (int w = 0; w < 3; ++w) v[j] += (Mx[j][w] + My[j][w]) * Vn[w];
-                }
-                const double Kn = -200. * kC * kC * kC * dv / a;
-                for (int j = 0; j < 3; ++j)
-                    for (int w = 0; w < 3; ++w) Mn[j][w] = Kn * v[j] * v[w];
-            } else {
-                if (bp.LamType == 1) { m1 = mu * f; m2 = mu / (f + mu * (1. - f)); }
-                else { m2 = mu * f; m1 = mu / (f + mu * (1. - f)); }
-                for (int j = 0; j < 3; ++j) {
-                    v[j] = 0; u[j] = 0;
-                    for (int w = 0; w < 3; ++w) {
-                        if (bp.LamType == 1) {
-                            v[j] += (My[j][w] / f + Mx[j][w]) * Vn[w];
-                            u[j] += (My[j][w] / f + f * Mx[j][w]) * Vn[w];
-                        } else {
-                            v[j] += (Mx[j][w] / f + My[j][w]) * Vn[w];
-                            u[j] += (Mx[j][w] / f + f * My[j][w]) * Vn[w];
-                        }
-                    }
-                }
-                const double Kn = -100. * kC * kC * kC * dv / (a);
-                for (int j = 0; j < 3; ++j)
-                    for (int w = 0; w < 3; ++w) Mn[j][w] = Kn * (v[j] * u[w] + v[w] * u[j]);
-            }
-        }
+        double dv = pre_dv;
+        const bool on = PRE ? pre_on : planar_newton_state(A, bp, p, q, a, Vn, m1, m2, dv);
+        if (on) planar_newton_terms(bp, Mx, My, a, Vn, dv, Mn);
     }
 
     // element matrix, v12 == 0 outside incremental problems (static2d.cpp:799-805)
@@ -1050,8 +1081,8 @@ constexpr int kRowAcc = 12;
 // element data a block shares with the blocks a mesh row away stay in that
 // XCD's L2 (round-robin blocks fetched them once per XCD: 470 MB of HBM
 // traffic per launch for ~100 MB of algorithmic bytes on configs[2])
-template <bool AXI, bool FIRST, bool XCD = true>
-__global__ void __launch_bounds__(kRowBlock) k_assemble_rows(int N, AssembleArgs A)
+template <bool AXI, bool FIRST, bool XCD, bool PRE>
+__device__ __forceinline__ void assemble_rows(int N, const AssembleArgs &A)
 {
     __shared__ double s_acc[kRowAcc * kRowBlock];
     __shared__ int s_col[kRowAcc * kRowBlock];
@@ -1079,14 +1110,18 @@ __global__ void __launch_bounds__(kRowBlock) k_assemble_rows(int N, AssembleArgs
         const double X[3] = {A.x[n[0]], A.x[n[1]], A.x[n[2]]};
         const double Y[3] = {A.y[n[0]], A.y[n[1]], A.y[n[2]]};
         double m1 = 0., m2 = 0., Me[3][3], be[3];
-        if (!FIRST) {
+        if (PRE) {   // the new state, from k_planar_state
+            m1 = A.mu1_out[e];
+            m2 = A.mu2_out[e];
+        } else if (!FIRST) {
             m1 = A.mu1[e];
             m2 = A.mu2[e];
         }
         if (AXI) axi_element<FIRST>(A.ebits_raw[e], A, n, X, Y, lab, bp, m1, m2, Me, be);
+        else if (PRE) planar_element<false, true>(A.ebits_raw[e], A, n, X, Y, lab, bp, m1, m2, Me, be, A.dv_el[e], A.on_el[e] != 0);
         else planar_element<FIRST>(A.ebits_raw[e], A, n, X, Y, lab, bp, m1, m2, Me, be);
         const int w = (n[0] < N) ? 0 : ((n[1] < N) ? 1 : 2);
-        if (w == j && A.mu1_out) {   // (linear problems keep no permeability state)
+        if (!PRE && w == j && A.mu1_out) {   // (linear problems keep no permeability state)
             A.mu1_out[e] = m1;
             A.mu2_out[e] = m2;
         }
@@ -1123,6 +1158,44 @@ __global__ void __launch_bounds__(kRowBlock) k_assemble_rows(int N, AssembleArgs
         for (int k = 0; k < L; ++k) A.val[rs + k] = s_acc[k * kRowBlock + threadIdx.x];
     }
     if (live) A.b[i] = bi;
+}
+
+template <bool AXI, bool FIRST, bool XCD = true>
+__global__ void __launch_bounds__(kRowBlock) k_assemble_rows(int N, AssembleArgs A)
+{
+    assemble_rows<AXI, FIRST, XCD, false>(N, A);
+}
+
+// the planar Newton pass after k_planar_state: 4 waves per SIMD (132 VGPRs
+// unbounded, 3 waves)
+__global__ void __launch_bounds__(kRowBlock, 4) k_assemble_rows_pre(int N, AssembleArgs A)
+{
+    assemble_rows<false, false, true, true>(N, A);
+}
+
+// A planar Newton pass: each element's new state once (planar_newton_state),
+// for the three rows that gather it (k_assemble_rows<PRE>)
+__global__ void __launch_bounds__(256) k_planar_state(int NE, AssembleArgs A)
+{
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= NE) return;
+    const DevLabel lab = A.labels[A.lbl_raw[e]];
+    const DevBlock bp = A.blocks[lab.blk];
+    double m1 = A.mu1[e], m2 = A.mu2[e], dv = 0;
+    bool on = false;
+    if (bp.BHpoints > 0 && bp.LamType <= 2 && (bp.LamType != 0 || m1 == m2)) {
+        const int n[3] = {A.p_raw[3 * e], A.p_raw[3 * e + 1], A.p_raw[3 * e + 2]};
+        const double X[3] = {A.x[n[0]], A.x[n[1]], A.x[n[2]]};
+        const double Y[3] = {A.y[n[0]], A.y[n[1]], A.y[n[2]]};
+        const double Vn[3] = {A.V[n[0]], A.V[n[1]], A.V[n[2]]};
+        double p[3], q[3];
+        const double a = planar_geometry(X, Y, p, q);
+        on = planar_newton_state(A, bp, p, q, a, Vn, m1, m2, dv);
+    }
+    A.mu1_out[e] = m1;
+    A.mu2_out[e] = m2;
+    A.dv_el[e] = dv;
+    A.on_el[e] = on ? 1 : 0;
 }
 
 // point currents (static2d.cpp:818-825)
@@ -1409,8 +1482,14 @@ void launch_assemble_rows(hipStream_t s, int N, const AssembleArgs &A)
         if (A.iter == 0) k_assemble_rows<true, true><<<g, kRowBlock, 0, s>>>(N, A);
         else k_assemble_rows<true, false><<<g, kRowBlock, 0, s>>>(N, A);
     } else {
-        if (A.iter == 0) k_assemble_rows<false, true><<<g, kRowBlock, 0, s>>>(N, A);
-        else k_assemble_rows<false, false><<<g, kRowBlock, 0, s>>>(N, A);
+        if (A.iter == 0) {
+            k_assemble_rows<false, true><<<g, kRowBlock, 0, s>>>(N, A);
+        } else if (A.dv_el && A.mu1_out) {
+            if (A.n_el > 0) k_planar_state<<<(A.n_el + 255) / 256, 256, 0, s>>>(A.n_el, A);
+            k_assemble_rows_pre<<<g, kRowBlock, 0, s>>>(N, A);
+        } else {
+            k_assemble_rows<false, false><<<g, kRowBlock, 0, s>>>(N, A);
+        }
     }
 }
 

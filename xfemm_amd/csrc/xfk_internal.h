@@ -358,6 +358,8 @@ struct xfk_problem {
     xfk::DBuf<int> slot;             // colour order, 9 per element
     xfk::DBuf<double> mu1, mu2;      // element permeability state (colour order: harmonic; raw order: static)
     xfk::DBuf<double> mu1b, mu2b;    // static row-gather assembly: the state written by the current assembly
+    xfk::DBuf<double> dv_el;         // planar Newton passes: the element's dv (k_planar_state)
+    xfk::DBuf<unsigned char> on_el;  // ... and whether its Newton terms apply
     xfk::DBuf<int> asm_miss;         // static assembly: 1 when an element entry found no slot in its row
     bool miss_checked = false;       // asm_miss read since the last symbolic build
 

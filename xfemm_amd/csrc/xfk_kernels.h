@@ -26,6 +26,12 @@ struct AssembleArgs {
     const int *p_raw, *lbl_raw, *ebits_raw, *n2e_ptr, *n2e, *rowptr, *col;
     double *mu1_out, *mu2_out;     // null: linear problem, no state kept
     int *miss;                      // set to 1 when an element entry has no slot in its row
+    // planar Newton passes (iter > 0): each element's new state evaluated once
+    // by k_planar_state into mu*_out, dv_el (dv of GetBHProps) and on_el (the
+    // Newton terms apply), read by every row of the element; null: per row
+    double *dv_el;
+    unsigned char *on_el;
+    int n_el;                       // elements (the state pass's range)
 };
 
 int grid_reduce(int N);
