@@ -1001,9 +1001,12 @@ static int allreduce_partials(xfk_problem *P, int narrays)
 
 static bool trace_newton() { return std::getenv("XFK_TRACE_NEWTON") != nullptr; }
 
-// a Newton refresh re-forms level 0's P~ when the last pass ran at least
-// this many PCG iterations (else level 0 runs unfolded for the pass)
-constexpr int kRefoldMinIters = 0;
+// a Newton refresh re-forms level 0's P~ (~0.32 ms on configs[3]) when the
+// last pass ran at least this many PCG iterations, else level 0 runs
+// unfolded for the pass; configs[3] per step with 0 / 12 / 16 / 20 / never:
+// 19.32-19.44 / 19.03-19.25 / 19.11-19.13 / 19.06-19.09 / 18.96-19.33 ms
+// (profiles/r04_experiments/r04z4_*) -- within noise of each other
+constexpr int kRefoldMinIters = 16;
 
 // AMG hierarchy of the assembled matrix (owned block when sharded); falls
 // back to Jacobi for this solve when the hierarchy cannot be built
