@@ -2754,28 +2754,28 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     // nrows x cap, its length and the kernel's overflow flag land in a
     // deferred slot that the setup reads once at its end (an overflow there
     // rebuilds the hierarchy with measured capacities)
+    auto deferred_pass = [&](int cap) -> int {
+        int *slot = M.def_dev.p + M.def_n;
+        AMG_CHECK(M.pad_col.alloc((size_t)nrows * cap));
+        AMG_CHECK(M.pad_val.alloc((size_t)nrows * cap));
+        AMG_CHECK(ccol.alloc((size_t)std::max(1LL, (long long)nrows * cap)));
+        AMG_CHECK(cval.alloc((size_t)std::max(1LL, (long long)nrows * cap)));
+        launch_sort(cap, slot);
+        int rc = scan_only(M, s, M.cnt.p, crow.p, nrows);
+        if (rc != XFK_OK) return rc;
+        if (nrows > 0)
+            launch_compact(s, nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p, slot + 1);
+        else
+            AMG_CHECK(hipMemsetAsync(slot + 1, 0, sizeof(int), s));
+        M.def_target[M.def_n / 2] = &cnnz;
+        M.def_n += 2;
+        cnnz = (long long)nrows * cap;   // an upper bound until the deferred read
+        return XFK_OK;
+    };
     if (key >= 0) {
         auto hint = M.cap_hint.find(key);
         if (hint != M.cap_hint.end()) {
-            if (M.def_n + 2 <= kAmgDeferSlots) {
-                const int cap = hint->second;
-                int *slot = M.def_dev.p + M.def_n;
-                AMG_CHECK(M.pad_col.alloc((size_t)nrows * cap));
-                AMG_CHECK(M.pad_val.alloc((size_t)nrows * cap));
-                AMG_CHECK(ccol.alloc((size_t)std::max(1LL, (long long)nrows * cap)));
-                AMG_CHECK(cval.alloc((size_t)std::max(1LL, (long long)nrows * cap)));
-                launch_sort(cap, slot);
-                int rc = scan_only(M, s, M.cnt.p, crow.p, nrows);
-                if (rc != XFK_OK) return rc;
-                if (nrows > 0)
-                    launch_compact(s, nrows, cap, crow.p, M.pad_col.p, M.pad_val.p, ccol.p, cval.p, slot + 1);
-                else
-                    AMG_CHECK(hipMemsetAsync(slot + 1, 0, sizeof(int), s));
-                M.def_target[M.def_n / 2] = &cnnz;
-                M.def_n += 2;
-                cnnz = (long long)nrows * cap;   // an upper bound until the deferred read
-                return XFK_OK;
-            }
+            if (M.def_n + 2 <= kAmgDeferSlots) return deferred_pass(hint->second);
             bool overflow = false;
             int rc = sort_pass(hint->second, overflow);
             if (rc != XFK_OK || !overflow) return rc;
@@ -2795,13 +2795,22 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     }
     if (maxprod <= kSortCap) {
         const int cap = maxprod <= 16 ? 16 : maxprod <= 32 ? 32 : maxprod <= 64 ? 64 : maxprod <= 128 ? 128 : 256;
-        bool overflow = false;
-        int rc = sort_pass(cap, overflow);
-        if (rc != XFK_OK) return rc;
-        if (overflow) {
-            set_error("AMG: internal SpGEMM capacity error");
-            return XFK_ERR_HIP;
+        int rc = XFK_OK;
+        if (key >= 0 && M.def_n + 2 <= kAmgDeferSlots) {
+            // the measured capacity (no overflow possible) through the
+            // deferred slot as a hinted one: the same kernels, so the same
+            // bits, without the host check for the length (~20 us per call
+            // site of a first setup)
+            rc = deferred_pass(cap);
+        } else {
+            bool overflow = false;
+            rc = sort_pass(cap, overflow);
+            if (rc == XFK_OK && overflow) {
+                set_error("AMG: internal SpGEMM capacity error");
+                return XFK_ERR_HIP;
+            }
         }
+        if (rc != XFK_OK) return rc;
         if (key >= 0) {
             // XFK_AMG_TEST_SMALL_HINT=1 (tests only): store a too-small capacity so
             // the next setup takes the overflow-and-rebuild path
@@ -3587,24 +3596,34 @@ int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &ld)
     // whose separators hold at most a quarter of the rows, and whose leaves
     // keep >= 1 block; leaves are phase 0 (slots = leaf index), the
     // separators of bisection level lev are phase D - lev
-    for (int D = n >= 24 * kBj ? 3 : (n >= 16 * kBj ? 2 : 1); D >= 1 && g.empty(); --D) {
-        std::vector<std::vector<int>> sets{all};
-        std::vector<std::vector<std::vector<int>>> seps(D);   // seps[lev][m]
-        bool ok = true;
-        size_t nsep = 0;
-        for (int lev = 0; lev < D && ok; ++lev) {
-            std::vector<std::vector<int>> next;
-            for (const auto &x : sets) {
-                std::vector<int> L, R, S;
-                nd_bisect(rp, cl, x, inl, L, R, S);
-                ok = ok && !L.empty() && !R.empty() && !S.empty();
-                nsep += S.size();
-                next.push_back(std::move(L));
-                next.push_back(std::move(R));
-                seps[lev].push_back(std::move(S));
-            }
-            sets = std::move(next);
+    // The bisection levels are computed once: nd_bisect is a function of its
+    // set, so the first D levels of a deeper bisection are the D-level one and
+    // every depth reads the same splits (no recomputation per depth tried)
+    const int Dmax = n >= 24 * kBj ? 3 : (n >= 16 * kBj ? 2 : 1);
+    std::vector<std::vector<std::vector<int>>> lev_sets(Dmax + 1), lev_seps(Dmax);
+    std::vector<size_t> lev_nsep(Dmax, 0);
+    int lev_done = 0;   // levels computed, each with all its groups non-empty
+    lev_sets[0].push_back(all);
+    for (int lev = 0; lev < Dmax; ++lev) {
+        bool okl = true;
+        for (const auto &x : lev_sets[lev]) {
+            std::vector<int> L, R, S;
+            nd_bisect(rp, cl, x, inl, L, R, S);
+            okl = okl && !L.empty() && !R.empty() && !S.empty();
+            lev_nsep[lev] += S.size();
+            lev_sets[lev + 1].push_back(std::move(L));
+            lev_sets[lev + 1].push_back(std::move(R));
+            lev_seps[lev].push_back(std::move(S));
         }
+        if (!okl) break;
+        lev_done = lev + 1;
+    }
+    for (int D = Dmax; D >= 1 && g.empty(); --D) {
+        bool ok = lev_done >= D;
+        size_t nsep = 0;
+        for (int lev = 0; lev < D && lev < Dmax; ++lev) nsep += lev_nsep[lev];
+        const std::vector<std::vector<int>> &sets = lev_sets[std::min(D, lev_done + 1)];
+        const std::vector<std::vector<std::vector<int>>> &seps = lev_seps;
         if (std::getenv("XFK_AMG_DEBUG")) {
             std::fprintf(stderr, "[amg] nested dissection depth %d: ok %d separators %zu, sets", D, (int)ok, nsep);
             for (const auto &x : sets) std::fprintf(stderr, " %zu", x.size());
