@@ -236,6 +236,9 @@ struct Amg {
     // smoother (D^-1, rho_A); the coarse levels are kept.
     // fold: level 0 stays folded (P~ re-formed for the new values); false: it runs unfolded
     int refresh(hipStream_t s, bool fold = true);
+    // the host read-back / staging buffers, taken when the problem is created
+    // (from the process's pinned cache): a first setup pins no pages
+    int reserve_host();
 
   private:
     int init(hipStream_t s);

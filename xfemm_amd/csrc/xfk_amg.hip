@@ -2562,10 +2562,10 @@ __global__ void k_unpad(int NC, int nranks, const int *__restrict__ c0, const do
 
 Amg::~Amg()
 {
-    if (nd_stage) (void)hipHostFree(nd_stage);
-    if (def_host) (void)hipHostFree(def_host);
-    if (host_int) (void)hipHostFree(host_int);
-    if (host_big) (void)hipHostFree(host_big);
+    pinned_free(nd_stage);   // (to the process cache when the problem is destroyed)
+    pinned_free(def_host);
+    pinned_free(host_int);
+    pinned_free(host_big);
     if (ev_host) (void)hipEventDestroy(ev_host);
     for (hipEvent_t e : tail_ev) (void)hipEventDestroy(e);
 }
@@ -3221,19 +3221,40 @@ int Amg::wait_deferred(hipStream_t s, bool &overflow)
 int Amg::host_ints(int count)
 {
     if (host_big_n >= count) return XFK_OK;
-    if (host_big) (void)hipHostFree(host_big);
+    pinned_free(host_big);   // (outside a destroy: hipHostFree)
     host_big = nullptr;
     host_big_n = 0;
-    AMG_CHECK(hipHostMalloc((void **)&host_big, sizeof(int) * std::max(count, 1)));
+    AMG_CHECK(pinned_malloc((void **)&host_big, sizeof(int) * std::max(count, 1)));
     host_big_n = count;
+    return XFK_OK;
+}
+
+int Amg::reserve_host()
+{
+    if (!host_int) AMG_CHECK(pinned_malloc((void **)&host_int, 16 * sizeof(int)));
+    if (!def_host) AMG_CHECK(pinned_malloc((void **)&def_host, kAmgDeferSlots * sizeof(int)));
+    if (!ev_host) AMG_CHECK(hipEventCreateWithFlags(&ev_host, hipEventDisableTiming));
+    constexpr int kHostBig = 64 << 10;   // ints: a coarsest pattern of ~1600 rows x 40
+    if (host_big_n < kHostBig) {
+        const int rc = host_ints(kHostBig);
+        if (rc != XFK_OK) return rc;
+    }
+    constexpr size_t kStage = 64 << 10;  // bytes: a nested-dissection plan of ~1600 rows
+    if (nd_stage_n < kStage) {
+        pinned_free(nd_stage);
+        nd_stage = nullptr;
+        nd_stage_n = 0;
+        AMG_CHECK(pinned_malloc((void **)&nd_stage, kStage));
+        nd_stage_n = kStage;
+    }
     return XFK_OK;
 }
 
 int Amg::init(hipStream_t s)
 {
-    if (!host_int) AMG_CHECK(hipHostMalloc((void **)&host_int, 16 * sizeof(int)));
+    if (!host_int) AMG_CHECK(pinned_malloc((void **)&host_int, 16 * sizeof(int)));
     if (!ev_host) AMG_CHECK(hipEventCreateWithFlags(&ev_host, hipEventDisableTiming));
-    if (!def_host) AMG_CHECK(hipHostMalloc((void **)&def_host, kAmgDeferSlots * sizeof(int)));
+    if (!def_host) AMG_CHECK(pinned_malloc((void **)&def_host, kAmgDeferSlots * sizeof(int)));
     AMG_CHECK(dev_int.alloc(8));
     AMG_CHECK(def_dev.alloc(kAmgDeferSlots));
     def_n = 0;
@@ -3717,10 +3738,10 @@ int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &ld)
     // is rewritten only after the next setup's synchronising pattern read)
     const size_t bytes = sizeof(int) * ((size_t)n + ld + tl.size()) + mask.size();
     if (nd_stage_n < bytes) {
-        if (nd_stage) (void)hipHostFree(nd_stage);
+        pinned_free(nd_stage);   // (outside a destroy: hipHostFree)
         nd_stage = nullptr;
         nd_stage_n = 0;
-        AMG_CHECK(hipHostMalloc((void **)&nd_stage, bytes));
+        AMG_CHECK(pinned_malloc((void **)&nd_stage, bytes));
         nd_stage_n = bytes;
     }
     char *h = nd_stage;

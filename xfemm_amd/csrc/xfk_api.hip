@@ -207,6 +207,68 @@ void dev_free(void *p)
     g_nsfree += now_ns() - t;
     ++g_nfree;
 }
+// Process-wide cache of pinned host buffers (each hipHostMalloc pins pages,
+// tens of us; hipHostFree may wait for the device): a problem's host mirrors
+// and its AMG's read-back / staging buffers go back here when the problem is
+// destroyed, for the next problem of the process.  Size classes as above; at
+// most kPinCap bytes stay cached.
+namespace {
+constexpr size_t kPinCap = 1ull << 30;
+struct PinPool {
+    std::mutex mu;
+    std::map<size_t, std::vector<void *>> free;
+    std::unordered_map<void *, size_t> live;
+    size_t cached = 0;
+};
+PinPool &pin_pool()
+{
+    static PinPool *p = new PinPool();   // (never destroyed, like the device cache)
+    return *p;
+}
+}  // namespace
+
+hipError_t pinned_malloc(void **p, size_t bytes)
+{
+    const size_t cls = size_class(bytes);
+    PinPool &pp = pin_pool();
+    {
+        std::lock_guard<std::mutex> g(pp.mu);
+        auto it = pp.free.find(cls);
+        if (it != pp.free.end() && !it->second.empty()) {
+            *p = it->second.back();
+            it->second.pop_back();
+            pp.cached -= cls;
+            pp.live[*p] = cls;
+            return hipSuccess;
+        }
+    }
+    const hipError_t e = hipHostMalloc(p, cls);
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> g(pp.mu);
+        pp.live[*p] = cls;
+    }
+    return e;
+}
+void pinned_free(void *p)
+{
+    if (!p) return;
+    PinPool &pp = pin_pool();
+    {
+        std::lock_guard<std::mutex> g(pp.mu);
+        auto it = pp.live.find(p);
+        if (it != pp.live.end()) {
+            const size_t cls = it->second;
+            pp.live.erase(it);
+            if (tl_pool_release && pp.cached + cls <= kPinCap) {
+                pp.free[cls].push_back(p);
+                pp.cached += cls;
+                return;
+            }
+        }
+    }
+    (void)hipHostFree(p);
+}
+
 thread_local PhaseProf *g_prof = nullptr;
 void set_error(const std::string &msg) { g_err = msg; }
 
@@ -1415,14 +1477,14 @@ void xfk_problem_destroy(xfk_problem *P)
     for (auto &ev : P->spmv_ev) (void)hipEventDestroy(ev);
     for (auto &ev : P->setup_ev)
         if (ev) (void)hipEventDestroy(ev);
-    if (P->pcg_host) (void)hipHostFree(P->pcg_host);
-    if (P->hpin) (void)hipHostFree(P->hpin);
     if (P->nnz_ev) (void)hipEventDestroy(P->nnz_ev);
-    if (P->nws_host) (void)hipHostFree(P->nws_host);
-    if (P->hc_host) (void)hipHostFree(P->hc_host);
     hipStream_t s = P->stream;
     {
         PoolRelease pr;   // (main stream synchronised above, side-stream work joined into it)
+        pinned_free(P->pcg_host);
+        pinned_free(P->hpin);
+        pinned_free(P->nws_host);
+        pinned_free(P->hc_host);
         delete P->amg;
         P->amg = nullptr;
         DevArena arena = std::move(P->arena);
@@ -1981,9 +2043,9 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     UP(P->fix_rows, fix_rows.data(), fix_rows.size());
 #undef UP
     tr.mark("  uploads enqueued");
-    if (e == hipSuccess) e = hipHostMalloc((void **)&P->pcg_host, sizeof(CgState));
-    if (e == hipSuccess) e = hipHostMalloc((void **)&P->hpin, 16 * sizeof(int));
-    if (e == hipSuccess) e = hipHostMalloc((void **)&P->nws_host, sizeof(NewtonScalars));
+    if (e == hipSuccess) e = pinned_malloc((void **)&P->pcg_host, sizeof(CgState));
+    if (e == hipSuccess) e = pinned_malloc((void **)&P->hpin, 16 * sizeof(int));
+    if (e == hipSuccess) e = pinned_malloc((void **)&P->nws_host, sizeof(NewtonScalars));
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     tr.mark("  pinned mirrors + sync");
     if (e != hipSuccess) {
@@ -1997,7 +2059,7 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     // the AMG object and its setup side stream are resources of the problem,
     // created with it (a stream's creation is not work of the first solve)
     P->amg = new Amg();
-    if (P->amg->sw.init() != XFK_OK) return fail(XFK_ERR_HIP);
+    if (P->amg->sw.init() != XFK_OK || P->amg->reserve_host() != XFK_OK) return fail(XFK_ERR_HIP);
     tr.mark("  AMG side stream");
     *out = P;
     return XFK_OK;
@@ -2474,8 +2536,8 @@ int xfk_pcg_solve_csr_pc(int n, const int *rowptr, const int *col, const double 
     if (e == hipSuccess) e = P->counters.alloc(8);
     if (e == hipSuccess) e = hipMemsetAsync(P->counters.p, 0, sizeof(unsigned) * 8, s);
     if (e == hipSuccess) e = P->pcg.alloc(1);
-    if (e == hipSuccess) e = hipHostMalloc((void **)&P->pcg_host, sizeof(CgState));
-    if (e == hipSuccess) e = hipHostMalloc((void **)&P->hpin, 16 * sizeof(int));
+    if (e == hipSuccess) e = pinned_malloc((void **)&P->pcg_host, sizeof(CgState));
+    if (e == hipSuccess) e = pinned_malloc((void **)&P->hpin, 16 * sizeof(int));
     if (e != hipSuccess) {
         set_error(std::string("pcg setup failed: ") + hipGetErrorString(e));
         rc = XFK_ERR_HIP;

@@ -1540,7 +1540,7 @@ int create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_desc *ac, int 
     UP(P->hbh_H, bhH.data(), bhH.size());
     UP(P->hbh_S, bhS.data(), bhS.size());
 #undef UP
-    if (e == hipSuccess) e = hipHostMalloc((void **)&P->hc_host, sizeof(CcgState));
+    if (e == hipSuccess) e = pinned_malloc((void **)&P->hc_host, sizeof(CcgState));
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {
         set_error(std::string("upload failed: ") + hipGetErrorString(e));

@@ -173,6 +173,11 @@ struct NewtonScalars {
 // device allocations of the library (counted for xfk_alloc_stats)
 hipError_t dev_malloc(void **p, size_t bytes);
 void dev_free(void *p);
+// pinned host buffers through a process-wide cache: pinned_free returns the
+// buffer to it inside a PoolRelease scope (a problem being destroyed, its
+// device work synchronised), else hipHostFree
+hipError_t pinned_malloc(void **p, size_t bytes);
+void pinned_free(void *p);
 
 // A problem's device arena: while an ArenaScope of the problem is active on
 // the calling thread, dev_malloc carves buffers out of chunks of >= 256 MiB
