@@ -485,3 +485,13 @@ def test_refold_threshold_unfolds_short_passes(monkeypatch):
     A0, r0 = _solve(kw, precond="amg")
     assert rel_err(A1, Ac) <= TOL_NONLINEAR
     assert np.array_equal(A1.view(np.int64), A0.view(np.int64))
+    # a threshold between the passes' counts: refreshes switch between folded
+    # and unfolded level 0 within one Newton loop -- parity, and the same bits
+    # on a repeat
+    monkeypatch.delenv("XFK_AMG_REFOLD")
+    counts = sorted(set([r1["cg_iters"] // max(1, r1["newton_iters"]), 3]))
+    monkeypatch.setenv("XFK_REFOLD_MIN", str(counts[-1]))
+    A2, r2 = _solve(kw, precond="amg")
+    A2b, _ = _solve(kw, precond="amg")
+    assert rel_err(A2, Ac) <= TOL_NONLINEAR
+    assert np.array_equal(A2.view(np.int64), A2b.view(np.int64))
