@@ -45,6 +45,7 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -454,9 +455,59 @@ def annotate_phases(phases):
     return os.path.relpath(paths[-1], ROOT)
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the
+    environment): start the N rank processes here, one per GPU, as torchrun
+    would (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR 127.0.0.1 / a free
+    MASTER_PORT), before anything in this process touches the GPU -- the
+    parent never imports the HIP library, it only waits.  Children are plain
+    subprocesses (no exec of a GPU-initialised process).  If one rank fails,
+    the others are stopped (their exact PIDs) so no rank waits forever in a
+    collective.  Returns the exit code: 0 when every rank succeeded, else the
+    first failing rank's code (never 0)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+        print("[bench] spawned rank %d/%d pid %d" % (r, n, procs[-1].pid), file=sys.stderr, flush=True)
+    code = 0
+    alive = list(range(n))
+    while alive:
+        time.sleep(0.2)
+        for r in list(alive):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            alive.remove(r)
+            print("[bench] rank %d exited with %d" % (r, rc), file=sys.stderr, flush=True)
+            if rc != 0 and code == 0:
+                code = rc if rc > 0 else 128 - rc
+                for q in alive:          # a failed rank: the others would block in its collectives
+                    procs[q].terminate()
+                deadline = time.time() + 20
+                for q in alive:
+                    try:
+                        procs[q].wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        procs[q].kill()
+    return code
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of ONE node; without a launcher's WORLD_SIZE, N > 1 spawns the N rank "
+                         "processes itself (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cells", type=int, default=1000, help="cells per side (2*cells^2 triangles)")
@@ -491,13 +542,25 @@ def main():
                     help="skip rank 0's single-GPU solve of the sharded mesh")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and args.gpus is not None and int(env_world) != args.gpus:
+        print("bench.py: --gpus %d does not match the launcher's WORLD_SIZE=%s" % (args.gpus, env_world),
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        print("[bench] rank %d/%d pid %d up (local rank %s)" % (rank, world, os.getpid(),
+                                                               os.environ.get("LOCAL_RANK", "0")),
+              file=sys.stderr, flush=True)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
-        dist.init_process_group("gloo")
+        with stdout_to_stderr():          # gloo's connection banner goes to stdout
+            dist.init_process_group("gloo")
     sharded = (world > 1 and args.mode == "sharded") or args.force_sharded
 
     from xfemm_amd import kernels, synth
