@@ -456,6 +456,20 @@ int xfk_phase_profile(xfk_problem *prob, int iters, int flags, xfk_phase *out, i
  * counted.  reset != 0 zeroes the counters after reading. */
 int xfk_alloc_stats(double *out4, int reset);
 
+/* Device memory of one problem (diagnostics): out4[0] bytes of the arena
+ * chunks it holds, out4[1] their count, out4[2] bytes carved and live,
+ * out4[3] bytes freed by its solves and kept for reuse by the next ones.  A
+ * problem solved repeatedly stays at the footprint of its largest solve. */
+int xfk_problem_memory(const xfk_problem *prob, long long *out4);
+/* The process-wide caches a destroyed problem leaves for the next one: device
+ * blocks (at most XFK_POOL_CAP_MB, default 64 GiB), pinned host buffers (at
+ * most XFK_PIN_CAP_MB, default 1 GiB) and idle streams.  xfk_cache_stats:
+ * out3[0] cached device bytes, out3[1] cached pinned bytes, out3[2] idle
+ * streams.  xfk_release_cache gives all of them back to HIP (live problems
+ * keep theirs). */
+int xfk_cache_stats(long long *out3);
+int xfk_release_cache(void);
+
 /* Magnetisation-direction function of a block label, evaluated for elements
  * as the reference's element loop does (FSolver::Static2D,
  * cfemm/fsolver/static2d.cpp:509-583; StaticAxisymmetric staticaxi.cpp:350-406):

@@ -215,6 +215,12 @@ struct Amg {
     DBuf<char> cub_tmp2;
 
     ~Amg();
+    // wait for the hierarchy's own streams (overlap, setup side stream)
+    void sync_streams()
+    {
+        if (side.cs) (void)hipStreamSynchronize(side.cs);
+        if (sw.cs) (void)hipStreamSynchronize(sw.cs);
+    }
     // Build the hierarchy for the n x n CSR on `s` (host-synchronising).
     // Columns >= ncol_lim (sharded halo) are ignored.  Returns XFK_OK, or
     // XFK_ERR_UNSUPPORTED when a SpGEMM row exceeds the LDS hash capacity.

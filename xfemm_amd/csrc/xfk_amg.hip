@@ -3048,6 +3048,29 @@ void stream_release(hipStream_t s)
     g_pool_free[it->second].push_back(s);
 }
 
+void stream_pool_drain()
+{
+    std::vector<hipStream_t> idle;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (auto &kv : g_pool_free)
+            for (hipStream_t q : kv.second) {
+                idle.push_back(q);
+                g_pool_dev.erase(q);
+            }
+        g_pool_free.clear();
+    }
+    for (hipStream_t q : idle) (void)hipStreamDestroy(q);
+}
+
+long long stream_pool_idle()
+{
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    long long n = 0;
+    for (auto &kv : g_pool_free) n += (long long)kv.second.size();
+    return n;
+}
+
 int SideStream::init()
 {
     if (cs) return XFK_OK;

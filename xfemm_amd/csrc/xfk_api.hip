@@ -72,7 +72,14 @@ long long now_ns()
 // buffer that grows, a function's scratch) goes straight to hipFree: only the
 // destroy path knows the device no longer reads the block.
 namespace {
-constexpr size_t kPoolCap = 64ull << 30;
+// cap: XFK_POOL_CAP_MB (default 64 GiB; 0 keeps nothing), read once
+size_t env_mb(const char *name, size_t dflt)
+{
+    const char *v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    return (size_t)std::strtoull(v, nullptr, 10) << 20;
+}
+const size_t kPoolCap = env_mb("XFK_POOL_CAP_MB", 64ull << 30);
 struct BlockPool {
     std::mutex mu;
     std::map<std::pair<int, size_t>, std::vector<void *>> free;
@@ -117,10 +124,24 @@ hipError_t dev_malloc(void **p, size_t bytes)
 {
     DevArena *a = tl_arena;
     if (!a) return pool_malloc(p, bytes);
+    const size_t need = (bytes + kArenaAlign - 1) & ~(kArenaAlign - 1);
+    // a block freed in an earlier solve of this problem, if one fits without
+    // wasting more than its own size (a repeated solve asks for the same sizes)
+    auto it = a->reuse.lower_bound(need);
+    if (it != a->reuse.end() && it->first <= 2 * need + (64u << 10)) {
+        char *q = it->second;
+        a->carved[q] = it->first;
+        a->reuse.erase(it);
+        *p = q;
+        std::lock_guard<std::mutex> g(block_pool().mu);
+        block_pool().live[q] = {-1, 0};
+        return hipSuccess;
+    }
     size_t at = (a->off + kArenaAlign - 1) & ~(kArenaAlign - 1);
-    if (a->chunks.empty() || at + bytes > a->chunks.back().second) {
+    if (a->chunks.empty() || at + need > a->chunks.back().second) {
         // (carving starts one alignment step in: no carved block has its chunk's address)
-        const size_t csz = std::max(kArenaChunk, ((bytes + kArenaAlign - 1) & ~(kArenaAlign - 1)) + kArenaAlign);
+        const size_t csz = std::max(a->next_chunk, need + kArenaAlign);
+        a->next_chunk = std::min(kArenaChunk, 2 * a->next_chunk);
         void *c = nullptr;
         tl_arena = nullptr;   // (the chunk itself comes from the process cache or hipMalloc)
         const hipError_t e = pool_malloc(&c, csz);
@@ -130,14 +151,51 @@ hipError_t dev_malloc(void **p, size_t bytes)
         at = kArenaAlign;
     }
     *p = a->chunks.back().first + at;
-    a->off = at + bytes;
+    a->off = at + need;
+    a->carved[*p] = need;
     std::lock_guard<std::mutex> g(block_pool().mu);
     block_pool().live[*p] = {-1, 0};   // (carved: dev_free leaves it to the arena)
     return hipSuccess;
 }
 
+bool DevArena::retire(void *p)
+{
+    auto it = carved.find(p);
+    if (it == carved.end()) return false;
+    pending.push_back({static_cast<char *>(p), it->second});
+    carved.erase(it);
+    std::lock_guard<std::mutex> g(block_pool().mu);
+    block_pool().live.erase(p);
+    return true;
+}
+
+bool arena_retire(void *p)
+{
+    return p && tl_arena && tl_arena->retire(p);
+}
+
+void DevArena::recycle()
+{
+    for (auto &b : pending) reuse.insert({b.second, b.first});
+    pending.clear();
+}
+
+size_t DevArena::chunk_bytes() const
+{
+    size_t t = 0;
+    for (auto &c : chunks) t += c.second;
+    return t;
+}
+
 void DevArena::release()
 {
+    {
+        std::lock_guard<std::mutex> g(block_pool().mu);
+        for (auto &kv : carved) block_pool().live.erase(kv.first);
+    }
+    carved.clear();
+    reuse.clear();
+    pending.clear();
     for (auto &c : chunks) dev_free(c.first);
     chunks.clear();
     off = 0;
@@ -187,6 +245,7 @@ static hipError_t pool_malloc(void **p, size_t bytes)
 }
 void dev_free(void *p)
 {
+    if (arena_retire(p)) return;   // carved from the active arena: reusable after this solve
     BlockPool &bp = block_pool();
     {
         std::lock_guard<std::mutex> g(bp.mu);
@@ -213,7 +272,7 @@ void dev_free(void *p)
 // destroyed, for the next problem of the process.  Size classes as above; at
 // most kPinCap bytes stay cached.
 namespace {
-constexpr size_t kPinCap = 1ull << 30;
+const size_t kPinCap = env_mb("XFK_PIN_CAP_MB", 1ull << 30);   // (XFK_PIN_CAP_MB, default 1 GiB)
 struct PinPool {
     std::mutex mu;
     std::map<size_t, std::vector<void *>> free;
@@ -1352,7 +1411,12 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
         if (miss_read) XFK_CHECK(hipMemcpyAsync(P->hpin + 4, P->asm_miss.p, sizeof(int), hipMemcpyDeviceToHost, s));
         XFK_CHECK(hipStreamSynchronize(s));
         if (miss_read) {
-            XFK_REQUIRE(P->hpin[4] == 0, XFK_ERR_HIP, "internal: element entry missing from the CSR pattern");
+            // (sharded: the flags summed over the ranks -- every rank takes the
+            // same decision, none is left waiting in the next collective; every
+            // rank reads its flag at the same poll, so the calls match)
+            double miss = (double)P->hpin[4];
+            if (P->comm && (rc = allreduce_host(P, miss)) != XFK_OK) return rc;
+            XFK_REQUIRE(miss == 0, XFK_ERR_HIP, "internal: element entry missing from the CSR pattern");
             P->miss_checked = true;
         }
         const CgState &S = *P->pcg_host;
@@ -1410,7 +1474,8 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
     if (rc == kRetryFresh) {   // a fresh hierarchy, the PCG restarted from the iterate
         P->pcg_discarded = P->pcg_host->iters;
         P->amg_reusable = false;
-        rc = pcg_solve_once(P, 1, max_iters);
+        // (the cap covers the whole solve: the discarded iterations count)
+        rc = pcg_solve_once(P, 1, std::max<long long>(1, max_iters - P->pcg_discarded));
         if (rc == kRetryFresh) {
             set_error("internal: fresh hierarchy retried twice");
             return XFK_ERR_HIP;
@@ -1434,7 +1499,7 @@ static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
         XFK_CHECK(hipMemsetAsync(P->V.p, 0, sizeof(double) * P->NL, P->stream));
         f2 = 0;
     }
-    rc = pcg_solve_once(P, f2, max_iters);
+    rc = pcg_solve_once(P, f2, std::max<long long>(1, max_iters - first));
     if (rc == kRetryF64 || rc == kRetryFresh) {   // (cannot repeat: no f32 part is left, the hierarchy is fresh)
         set_error("internal: f64 fallback requested twice");
         return XFK_ERR_HIP;
@@ -1462,6 +1527,67 @@ int xfk_alloc_stats(double *out4, int reset)
     return XFK_OK;
 }
 
+int xfk_release_cache(void)
+{
+    std::vector<void *> dev, pin;
+    {
+        BlockPool &bp = block_pool();
+        std::lock_guard<std::mutex> g(bp.mu);
+        for (auto &kv : bp.free)
+            for (void *q : kv.second) dev.push_back(q);
+        bp.free.clear();
+        bp.cached = 0;
+    }
+    {
+        PinPool &pp = pin_pool();
+        std::lock_guard<std::mutex> g(pp.mu);
+        for (auto &kv : pp.free)
+            for (void *q : kv.second) pin.push_back(q);
+        pp.free.clear();
+        pp.cached = 0;
+    }
+    int rc = XFK_OK;
+    for (void *q : dev)
+        if (hipFree(q) != hipSuccess) rc = XFK_ERR_HIP;
+    for (void *q : pin)
+        if (hipHostFree(q) != hipSuccess) rc = XFK_ERR_HIP;
+    stream_pool_drain();
+    if (rc != XFK_OK) set_error("xfk_release_cache: hipFree failed");
+    return rc;
+}
+
+int xfk_cache_stats(long long *out3)
+{
+    XFK_REQUIRE(out3, XFK_ERR_ARG, "null output");
+    {
+        BlockPool &bp = block_pool();
+        std::lock_guard<std::mutex> g(bp.mu);
+        out3[0] = (long long)bp.cached;
+    }
+    {
+        PinPool &pp = pin_pool();
+        std::lock_guard<std::mutex> g(pp.mu);
+        out3[1] = (long long)pp.cached;
+    }
+    out3[2] = stream_pool_idle();
+    return XFK_OK;
+}
+
+int xfk_problem_memory(const xfk_problem *P, long long *out4)
+{
+    XFK_REQUIRE(P && out4, XFK_ERR_ARG, "null argument");
+    const DevArena &a = P->arena;
+    long long live = 0, reuse = 0;
+    for (auto &kv : a.carved) live += (long long)kv.second;
+    for (auto &kv : a.reuse) reuse += (long long)kv.first;
+    for (auto &b : a.pending) reuse += (long long)b.second;
+    out4[0] = (long long)a.chunk_bytes();
+    out4[1] = (long long)a.chunks.size();
+    out4[2] = live;
+    out4[3] = reuse;
+    return XFK_OK;
+}
+
 int xfk_device_count(void)
 {
     int n = 0;
@@ -1479,8 +1605,13 @@ void xfk_problem_destroy(xfk_problem *P)
         if (ev) (void)hipEventDestroy(ev);
     if (P->nnz_ev) (void)hipEventDestroy(P->nnz_ev);
     hipStream_t s = P->stream;
+    // every stream of the problem idle before its pinned buffers and device
+    // blocks go to the process caches (a failed solve may have left side-stream
+    // copies into them in flight)
+    if (P->side.cs) (void)hipStreamSynchronize(P->side.cs);
+    if (P->amg) P->amg->sync_streams();
     {
-        PoolRelease pr;   // (main stream synchronised above, side-stream work joined into it)
+        PoolRelease pr;
         pinned_free(P->pcg_host);
         pinned_free(P->hpin);
         pinned_free(P->nws_host);
@@ -2195,7 +2326,38 @@ int xfk_dist_get_info(const xfk_problem *P, xfk_dist_info *info)
     return XFK_OK;
 }
 
+}  // extern "C"
+
+namespace xfk {
+// End of a solve: every stream of the problem idle (the main stream, the
+// exchange side stream, the AMG's overlap and setup streams), then the blocks
+// the solve freed become reusable by the next one (DevArena::recycle).
+void problem_recycle(xfk_problem *P)
+{
+    if (!P) return;
+    (void)hipSetDevice(P->device);
+    if (P->stream) (void)hipStreamSynchronize(P->stream);
+    if (P->side.cs) (void)hipStreamSynchronize(P->side.cs);
+    if (P->amg) P->amg->sync_streams();
+    P->arena.recycle();
+}
+static int static2d_run(xfk_problem *P, int flags, xfk_result *res);
+}  // namespace xfk
+
+extern "C" {
+
 int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
+{
+    ArenaScope arena_scope(P ? &P->arena : nullptr);
+    const int rc = static2d_run(P, flags, res);
+    problem_recycle(P);
+    return rc;
+}
+
+}  // extern "C"
+
+namespace xfk {
+static int static2d_run(xfk_problem *P, int flags, xfk_result *res)
 {
     ArenaScope arena_scope(P ? &P->arena : nullptr);
     XFK_REQUIRE(P, XFK_ERR_ARG, "null problem");
@@ -2338,6 +2500,9 @@ int xfk_static2d(xfk_problem *P, int flags, xfk_result *res)
     if (res) *res = R;
     return XFK_OK;
 }
+}  // namespace xfk
+
+extern "C" {
 
 int xfk_get_solution(xfk_problem *P, double *A)
 {

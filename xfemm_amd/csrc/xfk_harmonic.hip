@@ -1553,6 +1553,11 @@ int create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_desc *ac, int 
 
 }  // namespace
 
+namespace xfk {
+static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res);
+void problem_recycle(xfk_problem *P);
+}
+
 extern "C" {
 
 int xfk_problem_create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_desc *ac, int device,
@@ -1569,6 +1574,17 @@ int xfk_problem_create_harmonic_dist(const xfk_problem_desc *d, const xfk_harmon
 }
 
 int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
+{
+    ArenaScope arena_scope(P ? &P->arena : nullptr);
+    const int rc = harmonic2d_run(P, flags, res);
+    problem_recycle(P);
+    return rc;
+}
+
+}  // extern "C"
+
+namespace xfk {
+static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
 {
     ArenaScope arena_scope(P ? &P->arena : nullptr);
     XFK_REQUIRE(P && P->harmonic, XFK_ERR_ARG, "not a harmonic problem (xfk_problem_create_harmonic)");
@@ -2205,6 +2221,10 @@ int xfk_harmonic2d(xfk_problem *P, int flags, xfk_result *res)
     if (res) *res = R;
     return XFK_OK;
 }
+
+}  // namespace xfk
+
+extern "C" {
 
 int xfk_get_solution_complex(xfk_problem *P, double *A)
 {

@@ -20,7 +20,9 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <map>
 #include <string>
+#include <unordered_map>
 #include <thread>
 #include <vector>
 
@@ -180,15 +182,30 @@ hipError_t pinned_malloc(void **p, size_t bytes);
 void pinned_free(void *p);
 
 // A problem's device arena: while an ArenaScope of the problem is active on
-// the calling thread, dev_malloc carves buffers out of chunks of >= 256 MiB
-// (a few hipMalloc per problem instead of one per buffer: ~130 in a first
-// solve, ~1 ms), and dev_free of such a buffer is a no-op; the chunks go back
-// to the process cache when the problem is destroyed.
+// the calling thread, dev_malloc carves buffers out of chunks (32 MiB, then
+// doubling up to 256 MiB: a few hipMalloc per problem instead of one per
+// buffer -- ~130 in a first solve, ~1 ms).  dev_free of a carved buffer (a
+// function's scratch, the old block of a growing DBuf) keeps it `pending`:
+// queued work may still read it.  At the end of every solve, with every
+// stream of the problem idle, recycle() makes the pending blocks reusable,
+// and later carvings take a reusable block of a fitting size before cutting
+// new space, so a problem solved again and again (a rotor-angle loop) stays
+// at the footprint of its largest solve.  The chunks go back to the process
+// cache when the problem is destroyed.
 struct DevArena {
     std::vector<std::pair<char *, size_t>> chunks;
-    size_t off = 0;   // used bytes of the last chunk
+    size_t off = 0;                                   // used bytes of the last chunk
+    size_t next_chunk = 32ull << 20;                  // size of the next chunk (doubling to 256 MiB)
+    std::unordered_map<void *, size_t> carved;        // live carved blocks -> block bytes
+    std::multimap<size_t, char *> reuse;              // freed blocks no device work can read any more
+    std::vector<std::pair<char *, size_t>> pending;   // freed during the current solve
+    size_t chunk_bytes() const;
     void release();   // (the problem's device work finished)
+    void recycle();   // (every stream of the problem idle) pending -> reuse
+    bool retire(void *p);   // p carved here: pending until the next recycle()
 };
+// p carved from the arena active on this thread: retire it there (true)
+bool arena_retire(void *p);
 struct ArenaScope {
     DevArena *prev;
     explicit ArenaScope(DevArena *a);
@@ -203,12 +220,13 @@ struct DBuf {
     DBuf(const DBuf &) = delete;
     DBuf &operator=(const DBuf &) = delete;
     ~DBuf() { free(); }
-    // growing keeps the old block until the buffer itself is freed: work
+    // growing keeps the old block until the buffer itself is freed (or, for a
+    // block carved from the problem's arena, until the solve's end): work
     // still queued may read it, and a hipFree here would wait for the device
     // in the middle of a solve (the grows of a problem's first setup)
     hipError_t alloc(size_t count) {
         if (count <= n && p) return hipSuccess;
-        if (p) retired.push_back(p);
+        if (p && !arena_retire(p)) retired.push_back(p);
         p = nullptr;
         n = 0;
         if (count == 0) return hipSuccess;
@@ -262,6 +280,8 @@ void host_par_for(long long n, long long min_per_thread, F f)
 // streams here when it is destroyed and the next problem takes them back.
 hipError_t stream_acquire(hipStream_t *s);
 void stream_release(hipStream_t s);   // idle streams only (the caller synchronised it)
+void stream_pool_drain();             // destroy the idle pooled streams (xfk_release_cache)
+long long stream_pool_idle();
 struct SideStream {
     hipStream_t cs = nullptr;
     hipEvent_t a = nullptr, b = nullptr, c = nullptr;

@@ -43,7 +43,7 @@ EXPORTED = (
     "xfk_last_error", "xfk_age_element_matrix", "xfk_device_count", "xfk_problem_create", "xfk_problem_destroy",
     "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz", "xfk_spmv_col_bytes",
     "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_solve_csr_pc", "xfk_pcg_time", "xfk_phase_profile",
-    "xfk_alloc_stats",
+    "xfk_alloc_stats", "xfk_problem_memory", "xfk_cache_stats", "xfk_release_cache",
     "xfk_set_option",
     "xfk_problem_create_harmonic", "xfk_problem_create_harmonic_dist", "xfk_harmonic2d",
     "xfk_get_solution_complex", "xfk_get_circuits_complex",
@@ -164,6 +164,8 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_pcg_time.argtypes = [C.c_void_p, C.c_int, dptr, dptr]
     L.xfk_phase_profile.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     L.xfk_alloc_stats.argtypes = [dptr, C.c_int]
+    L.xfk_problem_memory.argtypes = [C.c_void_p, C.POINTER(C.c_longlong)]
+    L.xfk_cache_stats.argtypes = [C.POINTER(C.c_longlong)]
     L.xfk_set_option.argtypes = [C.c_void_p, C.c_int, C.c_double]
     L.xfk_problem_create_harmonic.argtypes = [C.POINTER(ProblemDesc), C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
     L.xfk_problem_create_harmonic_dist.argtypes = [C.POINTER(ProblemDesc), C.c_void_p, C.c_int, C.c_void_p,
@@ -205,6 +207,19 @@ def alloc_stats(reset: bool = False) -> dict:
     out = np.zeros(4)
     _check(load_library().xfk_alloc_stats(out.ctypes.data_as(dptr), int(reset)))
     return dict(n_malloc=int(out[0]), ms_malloc=float(out[1]), n_free=int(out[2]), ms_free=float(out[3]))
+
+
+def cache_stats() -> dict:
+    """The process-wide caches destroyed problems leave for the next one
+    (xfk_cache_stats): device bytes, pinned host bytes, idle streams."""
+    out = (C.c_longlong * 3)()
+    _check(load_library().xfk_cache_stats(out))
+    return dict(device_bytes=int(out[0]), pinned_bytes=int(out[1]), idle_streams=int(out[2]))
+
+
+def release_cache():
+    """Give the process-wide caches back to HIP (xfk_release_cache)."""
+    _check(load_library().xfk_release_cache())
 
 
 def device_count() -> int:
@@ -399,6 +414,13 @@ class Static2DProblem:
     def set_option(self, option: int, value: float):
         _check(_lib.xfk_set_option(self._h, option, float(value)))
 
+    def memory(self) -> dict:
+        """Device memory of this problem (xfk_problem_memory): arena chunk
+        bytes and count, bytes carved and live, bytes kept for reuse."""
+        out = (C.c_longlong * 4)()
+        _check(_lib.xfk_problem_memory(self._h, out))
+        return dict(chunk_bytes=int(out[0]), chunks=int(out[1]), live_bytes=int(out[2]), reuse_bytes=int(out[3]))
+
     def dist_info(self) -> dict:
         info = DistInfo()
         _check(_lib.xfk_dist_get_info(self._h, C.byref(info)))
@@ -562,6 +584,13 @@ class Harmonic2DProblem:
         _check(_lib.xfk_harmonic2d(self._h, XFK_REBUILD_SYMBOLIC if rebuild_symbolic else 0, C.byref(r)))
         self.result = r
         return r.as_dict()
+
+    def memory(self) -> dict:
+        """Device memory of this problem (xfk_problem_memory): arena chunk
+        bytes and count, bytes carved and live, bytes kept for reuse."""
+        out = (C.c_longlong * 4)()
+        _check(_lib.xfk_problem_memory(self._h, out))
+        return dict(chunk_bytes=int(out[0]), chunks=int(out[1]), live_bytes=int(out[2]), reuse_bytes=int(out[3]))
 
     def dist_info(self) -> dict:
         info = DistInfo()
