@@ -158,3 +158,62 @@ def test_product_fails_loudly_without_gpu():
     kw = synth.magnetostatic(4)
     with pytest.raises(kernels.XfkError):
         kernels.Static2DProblem(**kw)
+
+
+def test_host_loadmesh_odd_layouts_fall_back_to_the_token_stream(tmp_path):
+    """Mesh files large enough for the line-parallel parser (> 2 MB) whose
+    layout is not one record per line: a node record split over two lines, a
+    blank line among the element records, an extra token after the last
+    record of .node / .ele / .edge.  Such files are only read correctly by the
+    sequential token stream fscanf sees (the parallel parser must detect them
+    and fall back): the arrays equal the oracle's token-stream restatement of
+    LoadMesh (oracle/femfile.py load_mesh)."""
+    kw = synth.magnetostatic(300)
+    base = str(tmp_path / "odd")
+    synth.write_problem(base, kw)
+
+    def edit(ext, fn):
+        with open(base + ext) as fh:
+            lines = fh.read().split("\n")
+        fn(lines)
+        with open(base + ext, "w") as fh:
+            fh.write("\n".join(lines))
+
+    def node_edit(ls):
+        k = 1 + len(ls) // 2
+        f = ls[k].split()
+        ls[k] = "\t".join(f[:2])               # index and x ...
+        ls.insert(k + 1, "\t".join(f[2:]))     # ... y and marker on the next line
+        ls[-2] += "\t17"                       # a token after the last record
+
+    def ele_edit(ls):
+        ls.insert(1 + len(ls) // 3, "")        # a blank line among the records
+        ls.insert(1 + len(ls) // 3, "   \t ")
+        ls[-2] += " 99"
+
+    def edge_edit(ls):
+        ls[-2] += "\t5"
+
+    edit(".node", node_edit)
+    edit(".ele", ele_edit)
+    edit(".edge", edge_edit)
+    for ext in (".node", ".ele", ".edge"):
+        assert os.path.getsize(base + ext) > (2 << 20), ext
+    fs = fsolver.FSolver(delete_mesh_files=False)
+    fs.PathName = base
+    assert fs.LoadProblemFile() and fs.LoadMesh(), fs.last_error()
+    pr = femfile.prepare_problem(femfile.parse_fem(base + ".fem"))
+    mesh = femfile.load_mesh(base, pr)
+    x, y, m = fs.nodes()
+    p, lbl, e = fs.elements()
+    assert np.array_equal(x, mesh.x) and np.array_equal(y, mesh.y) and np.array_equal(m, mesh.marker)
+    assert np.array_equal(p, mesh.p) and np.array_equal(lbl, mesh.lbl) and np.array_equal(e, mesh.e)
+    # and the plain files parse to the same arrays through the parallel path
+    base2 = str(tmp_path / "plain")
+    synth.write_problem(base2, kw)
+    fs2 = fsolver.FSolver(delete_mesh_files=False)
+    fs2.PathName = base2
+    assert fs2.LoadProblemFile() and fs2.LoadMesh()
+    x2, y2, m2 = fs2.nodes()
+    p2, lbl2, e2 = fs2.elements()
+    assert np.array_equal(x2, x) and np.array_equal(y2, y) and np.array_equal(p2, p) and np.array_equal(e2, e)

@@ -53,6 +53,7 @@ int xfemm_fsolver_load_mesh(xfemm_fsolver *h)
 {
     if (!h) return 0;
     xfemm::LoadMeshErr err = h->s.LoadMesh(h->s.deleteMeshFiles);
+    h->s.join_removals();
     if (err != xfemm::NOERROR) {
         h->s.lastError = xfemm::FSolver::getErrorString(err);
         return 0;
@@ -60,7 +61,13 @@ int xfemm_fsolver_load_mesh(xfemm_fsolver *h)
     return 1;
 }
 
-int xfemm_fsolver_cuthill(xfemm_fsolver *h) { return (h && h->s.Cuthill(h->s.deleteMeshFiles)) ? 1 : 0; }
+int xfemm_fsolver_cuthill(xfemm_fsolver *h)
+{
+    if (!h) return 0;
+    const int ok = h->s.Cuthill(h->s.deleteMeshFiles);
+    h->s.join_removals();
+    return ok ? 1 : 0;
+}
 
 int xfemm_fsolver_get_nodes(xfemm_fsolver *h, double *x, double *y, int *marker)
 {

@@ -2,6 +2,7 @@
 #include "fsolver.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <charconv>
 #include <chrono>
@@ -11,9 +12,22 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <new>
+#include <type_traits>
 #include <thread>
+#include <unordered_map>
 #include <utility>
+
+#include <fcntl.h>
+#include <immintrin.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "fastnum.h"
+#include "hostmem.h"
+#include "hostpool.h"
 
 namespace xfemm {
 
@@ -27,6 +41,24 @@ int PrintWarningMsg(const char *fmt, ...)
 }
 
 FSolver::FSolver() : WarnMessage(&PrintWarningMsg), PrintMessage(&PrintWarningMsg) {}
+
+FSolver::~FSolver() { join_removals(); }
+
+// The mesh files the reference deletes once read (fsolver.cpp:711-716,
+// cuthill.cpp:140): unlinking ~170 MB of page cache costs tens of ms, so it
+// runs beside the rest of runSolver and is joined before runSolver returns.
+void FSolver::remove_async(std::vector<std::string> paths)
+{
+    removers_.emplace_back([paths = std::move(paths)] {
+        for (const auto &p : paths) remove(p.c_str());
+    });
+}
+
+void FSolver::join_removals()
+{
+    for (auto &t : removers_) t.join();
+    removers_.clear();
+}
 
 void FSolver::warn(const std::string &msg)
 {
@@ -310,45 +342,77 @@ inline bool read_int(const char *&p, int &v, bool nl)
 inline bool read_double(const char *&p, double &v, bool nl)
 {
     if (!skip_ws(p, nl)) return false;
-    char *end = nullptr;
-    v = std::strtod(p, &end);
-    if (end == p) return false;
+    const char *end = nullptr;   // (strtod's value and extent, exact fast path: fastnum.h)
+    if (!fastnum::parse_double(p, v, &end)) return false;
     p = end;
     return true;
 }
 
-// [0, n) split over the host's cores (at most 16), f(begin, end) per part
+// [0, n) split over the host's cores (at most 16), f(begin, end) per part,
+// on the persistent pool (hostpool.h)
 template <class F>
 void par_for(long long n, long long min_per_thread, F f)
 {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const int T = (int)std::max<long long>(1, std::min<long long>({(long long)std::min(hw, 16u), n / std::max(1LL, min_per_thread)}));
+    HostPool &pool = HostPool::get();
+    const int T = (int)std::max<long long>(1, std::min<long long>((long long)pool.size(), n / std::max(1LL, min_per_thread)));
     if (T <= 1) {
         f(0LL, n);
         return;
     }
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back([&, t] { f(n * t / T, n * (t + 1) / T); });
-    f(0LL, n / T);
-    for (auto &x : th) x.join();
+    pool.run(T, [&](int t) { f(n * t / T, n * (t + 1) / T); });
 }
 
 // A whole mesh file in memory, read as the token stream fscanf sees.
 struct TextBuf {
-    std::vector<char> d;
+    // the file's bytes + a terminating NUL; not value-initialised (the
+    // parallel reads below fill it, each thread faulting in its own pages),
+    // on huge pages, kept for the next file of the mesh
+    struct Bytes {
+        HugeBuf<char> b;
+        size_t n = 0;   // bytes incl. the NUL
+        char *data() { return b.data(); }
+        const char *data() const { return b.data(); }
+        size_t size() const { return n; }
+        char &operator[](size_t i) { return b[i]; }
+    } d;
     size_t pos = 0;
+    size_t hint = 0;   // bytes to allocate at least (the largest file to come)
     bool load(const std::string &path)
     {
-        FILE *fp = fopen(path.c_str(), "rb");
-        if (!fp) return false;
-        std::fseek(fp, 0, SEEK_END);
-        const long n = std::ftell(fp);
-        std::fseek(fp, 0, SEEK_SET);
-        d.resize((size_t)std::max(0L, n) + 1);
-        const size_t got = n > 0 ? std::fread(d.data(), 1, (size_t)n, fp) : 0;
-        std::fclose(fp);
-        d.resize(got + 1);
-        d[got] = '\0';
+        const int fd = ::open(path.c_str(), O_RDONLY);
+        if (fd < 0) return false;
+        struct stat st;
+        if (::fstat(fd, &st) != 0) {
+            ::close(fd);
+            return false;
+        }
+        const size_t n = (size_t)std::max<off_t>(0, st.st_size);
+        // (sized for the largest mesh file at the first load: .edge > .ele > .node for fmesher output)
+        if (!d.b.allocate(std::max<size_t>(n + 1, hint))) {
+            ::close(fd);
+            return false;
+        }
+        // chunks of >= 4 MiB read side by side (pread: no shared file offset)
+        const int T = (int)std::max<size_t>(1, std::min<size_t>(16, n >> 22));
+        std::vector<size_t> got(T, 0);
+        par_for(T, 1, [&](long long a, long long b) {
+            for (long long t = a; t < b; ++t) {
+                size_t o = n * t / T;
+                const size_t e = n * (t + 1) / T;
+                while (o < e) {
+                    const ssize_t r = ::pread(fd, d.b.data() + o, e - o, (off_t)o);
+                    if (r <= 0) break;
+                    o += (size_t)r;
+                    got[t] += (size_t)r;
+                }
+            }
+        });
+        ::close(fd);
+        size_t tot = 0;
+        for (size_t g : got) tot += g;
+        if (tot != n) return false;
+        d.b[n] = '\0';
+        d.n = n + 1;
         pos = 0;
         return true;
     }
@@ -377,8 +441,7 @@ struct TextBuf {
     {
         const char *base = d.data() + pos, *end = d.data() + d.size() - 1;
         const long long len = end - base;
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        const int T = (int)std::max<long long>(1, std::min<long long>(std::min(hw, 16u), len / (1 << 20)));
+        const int T = (int)std::max<long long>(1, std::min<long long>(HostPool::get().size(), len / (1 << 20)));
         bool ok = T > 1;
         if (ok) {
             // chunk starts at line starts; records (non-blank lines) per chunk
@@ -448,10 +511,17 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
     char s[1024];
     std::string infile = PathName + ".node";
     TextBuf tb;
+    {   // one buffer for the three mesh files: the largest one's size
+        struct stat st;
+        for (const char *ext : {".node", ".ele", ".edge"})
+            if (::stat((PathName + ext).c_str(), &st) == 0) tb.hint = std::max(tb.hint, (size_t)st.st_size + 1);
+    }
     if (!tb.load(infile)) return BADNODEFILE;
+    tr.mark("  .node read");
     int k = 0, j = 0;
     if (!tb.header_int(k)) return BADNODEFILE;
     NumNodes = k;
+    huge_reserve(meshnode, (size_t)std::max(0, k));
     meshnode.assign(k, CNode());
     const double conv = 100 * kLengthConvMeters[LengthUnits];
     if (!tb.records(k, [&](const char *&p, int i, bool nl) {
@@ -515,9 +585,12 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
 
     infile = PathName + ".ele";
     if (!tb.load(infile)) return BADELEMENTFILE;
+    tr.mark("  .ele read");
     if (!tb.header_int(k)) return BADELEMENTFILE;
     NumEls = k;
+    huge_reserve(meshele, (size_t)std::max(0, k));
     meshele.assign(k, CMElement());
+    tr.mark("  element array");
     int defaultLabel = -1;
     for (int i = 0; i < (int)labellist.size(); i++)
         if (labellist[i].IsDefault) defaultLabel = i;
@@ -531,43 +604,60 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
                    read_int(p, elm.p[2], nl) && read_int(p, elm.lbl, nl);
         }))
         return BADELEMENTFILE;
-    for (int i = 0; i < k; i++) {
-        CMElement &elm = meshele[i];
-        elm.lbl--;
-        if (elm.lbl < 0) elm.lbl = defaultLabel;
-        if (elm.lbl < 0) {
-            char buf[256];
-            snprintf(buf, sizeof buf, "The element number %i had label %i\n", i, elm.lbl);
-            warn(std::string("Material properties have not been defined for all regions.\n") + buf);
-            if (deleteFiles) remove_files();
-            return MISSINGMATPROPS;
+    {
+        // labels and node ids checked per element, in parallel; the first
+        // failing element (in file order) decides the error, as the
+        // reference's sequential loop does (fsolver.cpp:593-626)
+        const int nl = (int)labellist.size();
+        const int T = 64;
+        std::vector<int> bad_at(T, -1), bad_code(T, 0);
+        par_for(T, 1, [&](long long t0, long long t1) {
+            for (long long t = t0; t < t1; ++t) {
+                const int a = (int)((long long)k * t / T), b = (int)((long long)k * (t + 1) / T);
+                for (int i = a; i < b; i++) {
+                    CMElement &elm = meshele[i];
+                    elm.lbl--;
+                    if (elm.lbl < 0) elm.lbl = defaultLabel;
+                    int code = 0;
+                    if (elm.lbl < 0) code = 1;
+                    else if (elm.lbl >= nl) code = 2;
+                    else
+                        for (int q = 0; q < 3; q++)
+                            if (elm.p[q] < 0 || elm.p[q] >= NumNodes) code = 3;
+                    if (code) {
+                        bad_at[t] = i;
+                        bad_code[t] = code;
+                        break;
+                    }
+                    elm.blk = labellist[elm.lbl].BlockType;
+                }
+            }
+        });
+        for (int t = 0; t < T; ++t) {
+            if (bad_at[t] < 0) continue;
+            const int i = bad_at[t];
+            if (bad_code[t] == 1) {
+                char buf[256];
+                snprintf(buf, sizeof buf, "The element number %i had label %i\n", i, meshele[i].lbl);
+                warn(std::string("Material properties have not been defined for all regions.\n") + buf);
+                if (deleteFiles) remove_files();
+                return MISSINGMATPROPS;
+            }
+            if (bad_code[t] == 2) {
+                if (deleteFiles) remove_files();
+                return ELMLABELTOOBIG;
+            }
+            return BADELEMENTFILE;
         }
-        if (elm.lbl >= (int)labellist.size()) {
-            if (deleteFiles) remove_files();
-            return ELMLABELTOOBIG;
-        }
-        for (int q = 0; q < 3; q++)
-            if (elm.p[q] < 0 || elm.p[q] >= NumNodes) return BADELEMENTFILE;
-        elm.blk = labellist[elm.lbl].BlockType;
     }
     tr.mark("elements");
 
-    // node -> element membership (fsolver.cpp:628-657), as CSR
-    std::vector<int> mptr(NumNodes + 1, 0), mbr(3 * (size_t)NumEls);
-    for (int i = 0; i < NumEls; i++)
-        for (int q = 0; q < 3; q++) mptr[meshele[i].p[q] + 1]++;
-    for (int v = 0; v < NumNodes; v++) mptr[v + 1] += mptr[v];
-    {
-        std::vector<int> cur(mptr.begin(), mptr.end() - 1);
-        for (int i = 0; i < NumEls; i++)
-            for (int q = 0; q < 3; q++) mbr[cur[meshele[i].p[q]]++] = i;
-    }
-
-    tr.mark("membership");
     infile = PathName + ".edge";
     if (!tb.load(infile)) return BADEDGEFILE;
+    tr.mark("  .edge read");
     int nedge = 0, flag = 0;
     if (!tb.next_int(nedge) || !tb.next_int(flag)) return BADEDGEFILE;
+    huge_reserve(edges_, (size_t)std::max(0, nedge));
     edges_.assign(std::max(0, nedge), {0, 0, 0});
     if (nedge > 0 && !tb.records(nedge, [&](const char *&p, int i, bool nl) {
             int a;
@@ -575,25 +665,222 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
             return read_int(p, a, nl) && read_int(p, e[0], nl) && read_int(p, e[1], nl) && read_int(p, e[2], nl);
         }))
         return BADEDGEFILE;
-    for (int i = 0; i < nedge; i++) {
-        const int n0 = edges_[i][0], n1 = edges_[i][1];
-        j = edges_[i][2];
-        if (n0 < 0 || n1 < 0 || n0 >= NumNodes || n1 >= NumNodes) return BADEDGEFILE;
-        if (j < 0) {
-            int bc = -(j + 2);
-            for (int t = mptr[n0]; t < mptr[n0 + 1]; ++t) {
-                CMElement &e = meshele[mbr[t]];
-                if ((e.p[0] == n0 && e.p[1] == n1) || (e.p[0] == n1 && e.p[1] == n0)) e.e[0] = bc;
-                if ((e.p[1] == n0 && e.p[2] == n1) || (e.p[1] == n1 && e.p[2] == n0)) e.e[1] = bc;
-                if ((e.p[2] == n0 && e.p[0] == n1) || (e.p[2] == n1 && e.p[0] == n0)) e.e[2] = bc;
+    tr.mark("edge records");
+    // boundary-marked edges (marker < 0) set the boundary property of the
+    // element sides they match (fsolver.cpp:660-704: per edge, every element
+    // around its first node whose side k joins the two nodes).  The last such
+    // edge in file order wins a side, so the side takes the property of the
+    // last marked edge with its node pair: a map from the (unordered) pair,
+    // filled in file order, looked up per element side in parallel -- no
+    // node -> element membership lists
+    {
+        const int T = 64;
+        std::vector<char> bad(T, 0);
+        std::vector<std::vector<int>> marked(T);
+        par_for(T, 1, [&](long long t0, long long t1) {
+            for (long long t = t0; t < t1; ++t) {
+                const int a = (int)((long long)nedge * t / T), b = (int)((long long)nedge * (t + 1) / T);
+                for (int i = a; i < b; i++) {
+                    const auto &e = edges_[i];
+                    if (e[0] < 0 || e[1] < 0 || e[0] >= NumNodes || e[1] >= NumNodes) {
+                        bad[t] = 1;
+                        break;
+                    }
+                    if (e[2] < 0) marked[t].push_back(i);
+                }
             }
-        }
+        });
+        for (char c : bad)
+            if (c) return BADEDGEFILE;
+        std::unordered_map<unsigned long long, int> side_bc;
+        std::vector<char> on_marked(NumNodes, 0);
+        auto pair_key = [](int a, int b) {
+            return ((unsigned long long)(unsigned)std::min(a, b) << 32) | (unsigned)std::max(a, b);
+        };
+        for (auto &m : marked)
+            for (int i : m) {
+                const auto &e = edges_[i];
+                side_bc[pair_key(e[0], e[1])] = -(e[2] + 2);
+                on_marked[e[0]] = on_marked[e[1]] = 1;
+            }
+        if (!side_bc.empty())
+            par_for(NumEls, 1 << 15, [&](long long a, long long b) {
+                for (long long i = a; i < b; i++) {
+                    CMElement &el = meshele[i];
+                    for (int q = 0; q < 3; q++) {
+                        const int n0 = el.p[q], n1 = el.p[(q + 1) % 3];
+                        if (!on_marked[n0] || !on_marked[n1]) continue;
+                        auto it = side_bc.find(pair_key(n0, n1));
+                        if (it != side_bc.end()) el.e[q] = it->second;
+                    }
+                }
+            });
     }
     tr.mark("edges");
-    if (deleteFiles)
-        for (const char *ext : {".ele", ".node", ".pbc", ".poly"}) remove((PathName + ext).c_str());
+    if (deleteFiles) remove_async({PathName + ".ele", PathName + ".node", PathName + ".pbc", PathName + ".poly"});
     return NOERROR;
 }
+
+namespace {
+// one run of comb-sort compare-swaps x[i] <-> y[i] (score = high 32 bits,
+// swap on a strict decrease); x and y do not overlap.  Branch-free: a wide
+// pass meets random data, whose swaps mispredict half the time.  Returns
+// nonzero when anything moved.
+__attribute__((target("avx2"))) unsigned long long comb_swap_run_avx2(unsigned long long *__restrict x,
+                                                                       unsigned long long *__restrict y, int n)
+{
+    __m256i anyv = _mm256_setzero_si256();
+    int i = 0;
+    for (; i + 4 <= n; i += 4) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(x + i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(y + i));
+        // (scores < 2^32: the signed 64-bit compare of the shifted keys is the unsigned one)
+        const __m256i m = _mm256_cmpgt_epi64(_mm256_srli_epi64(a, 32), _mm256_srli_epi64(b, 32));
+        _mm256_storeu_si256(reinterpret_cast<__m256i *>(x + i), _mm256_blendv_epi8(a, b, m));
+        _mm256_storeu_si256(reinterpret_cast<__m256i *>(y + i), _mm256_blendv_epi8(b, a, m));
+        anyv = _mm256_or_si256(anyv, m);
+    }
+    unsigned long long any = (unsigned long long)_mm256_movemask_epi8(anyv);
+    for (; i < n; ++i) {
+        const unsigned long long a = x[i], b = y[i];
+        const unsigned long long m = 0ULL - (unsigned long long)((a >> 32) > (b >> 32));
+        x[i] = (a & ~m) | (b & m);
+        y[i] = (b & ~m) | (a & m);
+        any |= m;
+    }
+    return any;
+}
+unsigned long long comb_swap_run_plain(unsigned long long *__restrict x, unsigned long long *__restrict y, int n)
+{
+    unsigned long long any = 0;
+    for (int i = 0; i < n; ++i) {
+        const unsigned long long a = x[i], b = y[i];
+        const unsigned long long m = 0ULL - (unsigned long long)((a >> 32) > (b >> 32));
+        x[i] = (a & ~m) | (b & m);
+        y[i] = (b & ~m) | (a & m);
+        any |= m;
+    }
+    return any;
+}
+unsigned long long comb_swap_run(unsigned long long *x, unsigned long long *y, int n)
+{
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    return avx2 ? comb_swap_run_avx2(x, y, n) : comb_swap_run_plain(x, y, n);
+}
+
+// Narrow comb passes as scans (see SortElements).  op(c, x): the carried
+// entry c stays only on a strictly greater score; the all-zero key (score 0)
+// is its identity from the left, so a class's first entry needs no special
+// case.  Rows of g positions: lane c of a row is class c.
+inline unsigned long long scan_op(unsigned long long c, unsigned long long x)
+{
+    const unsigned long long m = 0ULL - (unsigned long long)((c >> 32) > (x >> 32));
+    return (c & m) | (x & ~m);
+}
+// red[c] = op(red[c], key[r g + c]) over `rows` rows
+__attribute__((target("avx2"))) void scan_reduce_avx2(unsigned long long *red, const unsigned long long *key,
+                                                       long long rows, int g)
+{
+    int c = 0;
+    for (; c + 4 <= g; c += 4) {
+        __m256i r = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(red + c));
+        const unsigned long long *k = key + c;
+        for (long long i = 0; i < rows; ++i, k += g) {
+            const __m256i x = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(k));
+            const __m256i m = _mm256_cmpgt_epi64(_mm256_srli_epi64(r, 32), _mm256_srli_epi64(x, 32));
+            r = _mm256_blendv_epi8(x, r, m);
+        }
+        _mm256_storeu_si256(reinterpret_cast<__m256i *>(red + c), r);
+    }
+    for (; c < g; ++c) {
+        unsigned long long r = red[c];
+        const unsigned long long *k = key + c;
+        for (long long i = 0; i < rows; ++i, k += g) r = scan_op(r, *k);
+        red[c] = r;
+    }
+}
+// car[c] = op(car[c], key[r g + c]) = c_k; out[r g + c] = the smaller-score of
+// c_k and key[(r + 1) g + c] (c_k on ties) -- `rows` rows, each with its
+// next row present; returns nonzero when some position took the next entry
+__attribute__((target("avx2"))) unsigned long long scan_rows_avx2(unsigned long long *car,
+                                                                   const unsigned long long *key,
+                                                                   unsigned long long *out, long long rows, int g)
+{
+    unsigned long long any = 0;
+    int c = 0;
+    __m256i anyv = _mm256_setzero_si256();
+    for (; c + 4 <= g; c += 4) {
+        __m256i cv = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(car + c));
+        const unsigned long long *k = key + c;
+        unsigned long long *o = out + c;
+        for (long long i = 0; i < rows; ++i, k += g, o += g) {
+            const __m256i x = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(k));
+            const __m256i nx = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(k + g));
+            const __m256i m0 = _mm256_cmpgt_epi64(_mm256_srli_epi64(cv, 32), _mm256_srli_epi64(x, 32));
+            cv = _mm256_blendv_epi8(x, cv, m0);
+            const __m256i m = _mm256_cmpgt_epi64(_mm256_srli_epi64(cv, 32), _mm256_srli_epi64(nx, 32));
+            _mm256_storeu_si256(reinterpret_cast<__m256i *>(o), _mm256_blendv_epi8(cv, nx, m));
+            anyv = _mm256_or_si256(anyv, m);
+        }
+        _mm256_storeu_si256(reinterpret_cast<__m256i *>(car + c), cv);
+    }
+    any = (unsigned long long)_mm256_movemask_epi8(anyv);
+    for (; c < g; ++c) {
+        unsigned long long cc = car[c];
+        const unsigned long long *k = key + c;
+        unsigned long long *o = out + c;
+        for (long long i = 0; i < rows; ++i, k += g, o += g) {
+            cc = scan_op(cc, *k);
+            const unsigned long long nx = k[g];
+            const unsigned long long m = 0ULL - (unsigned long long)((cc >> 32) > (nx >> 32));
+            *o = (nx & m) | (cc & ~m);
+            any |= m;
+        }
+        car[c] = cc;
+    }
+    return any;
+}
+void scan_reduce_plain(unsigned long long *red, const unsigned long long *key, long long rows, int g)
+{
+    for (int c = 0; c < g; ++c) {
+        unsigned long long r = red[c];
+        const unsigned long long *k = key + c;
+        for (long long i = 0; i < rows; ++i, k += g) r = scan_op(r, *k);
+        red[c] = r;
+    }
+}
+unsigned long long scan_rows_plain(unsigned long long *car, const unsigned long long *key, unsigned long long *out,
+                                   long long rows, int g)
+{
+    unsigned long long any = 0;
+    for (int c = 0; c < g; ++c) {
+        unsigned long long cc = car[c];
+        const unsigned long long *k = key + c;
+        unsigned long long *o = out + c;
+        for (long long i = 0; i < rows; ++i, k += g, o += g) {
+            cc = scan_op(cc, *k);
+            const unsigned long long nx = k[g];
+            const unsigned long long m = 0ULL - (unsigned long long)((cc >> 32) > (nx >> 32));
+            *o = (nx & m) | (cc & ~m);
+            any |= m;
+        }
+        car[c] = cc;
+    }
+    return any;
+}
+void scan_reduce(unsigned long long *red, const unsigned long long *key, long long rows, int g)
+{
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2 && g >= 4) scan_reduce_avx2(red, key, rows, g);
+    else scan_reduce_plain(red, key, rows, g);
+}
+unsigned long long scan_rows(unsigned long long *car, const unsigned long long *key, unsigned long long *out,
+                             long long rows, int g)
+{
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    return (avx2 && g >= 4) ? scan_rows_avx2(car, key, out, rows, g) : scan_rows_plain(car, key, out, rows, g);
+}
+}  // namespace
 
 int FSolver::SortElements()
 {
@@ -601,7 +888,10 @@ int FSolver::SortElements()
     // the same comparisons and swaps, on packed (score, element) keys instead
     // of the element records, which are permuted once at the end
     LoadTrace tr;
-    std::vector<unsigned long long> key(NumEls), tmp;
+    std::vector<unsigned long long> key, tmp;
+    huge_reserve(key, (size_t)NumEls);
+    huge_reserve(tmp, (size_t)NumEls);
+    key.resize(NumEls);
     par_for(NumEls, 1 << 16, [&](long long a, long long b) {
         for (long long k = a; k < b; k++) {
             const CMElement &e = meshele[k];
@@ -621,73 +911,56 @@ int FSolver::SortElements()
     // chunks of rows run in parallel from their classes' carries (computed
     // from per-chunk reductions): out of place, the same result as the
     // sequential pass
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const int T = (int)std::min(hw, 16u);
-    auto sc = [](unsigned long long k) { return k >> 32; };
-    auto op = [&](unsigned long long a, unsigned long long b) { return sc(a) > sc(b) ? a : b; };
+    HostPool &pool = HostPool::get();
+    const int T = pool.size();
     auto scan_pass = [&](int g) -> bool {
-        const long long R = ((long long)NumEls + g - 1) / g;   // rows of g positions
+        // chunks of whole rows (g positions each); every chunk but the last
+        // holds every class, so the carries need no presence flags
+        const long long n = NumEls;
+        const long long R = (n + g - 1) / g;
         const int TT = (int)std::max<long long>(1, std::min<long long>(T, R / 64));
+        std::vector<long long> q0(TT + 1);
+        for (int t = 0; t <= TT; ++t) q0[t] = std::min(n, (R * t / TT) * g);
         std::vector<unsigned long long> red((size_t)TT * g), cin((size_t)TT * g);
-        std::vector<char> has((size_t)TT * g, 0), hin((size_t)TT * g, 0), sw(TT, 0);
-        auto rows = [&](int t, long long &r0, long long &r1) { r0 = R * t / TT; r1 = R * (t + 1) / TT; };
-        std::vector<std::thread> th;
-        auto run = [&](auto fn) {
-            th.clear();
-            for (int t = 1; t < TT; ++t) th.emplace_back(fn, t);
-            fn(0);
-            for (auto &x : th) x.join();
-        };
-        run([&](int t) {   // per chunk and class: the op-reduction of its entries (thread-local, then stored)
-            long long r0, r1;
-            rows(t, r0, r1);
-            std::vector<unsigned long long> rd(g);
-            std::vector<char> h(g, 0);
-            for (long long r = r0; r < r1; ++r)
-                for (int c = 0; c < g; ++c) {
-                    const long long q = r * g + c;
-                    if (q >= NumEls) break;
-                    rd[c] = h[c] ? op(rd[c], key[q]) : key[q];
-                    h[c] = 1;
-                }
-            std::copy(rd.begin(), rd.end(), red.begin() + (size_t)t * g);
-            std::copy(h.begin(), h.end(), has.begin() + (size_t)t * g);
+        std::vector<char> sw(TT, 0);
+        auto run = [&](auto fn) { pool.run(TT, fn); };
+        run([&](int t) {   // per chunk and class: the op-reduction of its entries (from the identity 0)
+            if (t == TT - 1) return;   // (the last chunk feeds no carry; the others are whole rows)
+            unsigned long long *rd = red.data() + (size_t)t * g;
+            std::fill(rd, rd + g, 0ULL);
+            scan_reduce(rd, key.data() + q0[t], (q0[t + 1] - q0[t]) / g, g);
         });
         for (int t = 1; t < TT; ++t)   // carries into each chunk
             for (int c = 0; c < g; ++c) {
-                const size_t a = (size_t)(t - 1) * g + c, b = (size_t)t * g + c;
-                if (hin[a] && has[a]) cin[b] = op(cin[a], red[a]);
-                else if (hin[a]) cin[b] = cin[a];
-                else if (has[a]) cin[b] = red[a];
-                hin[b] = hin[a] || has[a];
+                const size_t i1 = (size_t)(t - 1) * g + c, i2 = (size_t)t * g + c;
+                cin[i2] = t == 1 ? red[i1] : scan_op(cin[i1], red[i1]);
             }
         tmp.resize(NumEls);
         run([&](int t) {
-            long long r0, r1;
-            rows(t, r0, r1);
-            std::vector<unsigned long long> car(cin.begin() + (size_t)t * g, cin.begin() + (size_t)(t + 1) * g);
-            std::vector<char> hc(hin.begin() + (size_t)t * g, hin.begin() + (size_t)(t + 1) * g);
-            char any = 0;
-            for (long long r = r0; r < r1; ++r)
-                for (int c = 0; c < g; ++c) {
-                    const long long q = r * g + c;
-                    if (q >= NumEls) break;
-                    const unsigned long long cc = hc[c] ? op(car[c], key[q]) : key[q];   // c_k (x_0 .. x_k)
-                    car[c] = cc;
-                    hc[c] = 1;
-                    if (q + g < NumEls) {
-                        const unsigned long long nx = key[q + g];   // x_{k+1}, as the pass meets it
-                        if (sc(cc) > sc(nx)) {
-                            tmp[q] = nx;
-                            any = 1;
-                        } else {
-                            tmp[q] = cc;
-                        }
-                    } else {
-                        tmp[q] = cc;
-                    }
-                }
-            sw[t] = any;
+            const long long a = q0[t], e = q0[t + 1];
+            if (a >= e) return;
+            std::vector<unsigned long long> car(g, 0ULL);   // chunk 0: the identity
+            if (t > 0) std::copy(cin.begin() + (size_t)t * g, cin.begin() + (size_t)(t + 1) * g, car.begin());
+            // whole rows whose next row is complete, then position by position
+            const long long full = std::max(0LL, std::min((e - a) / g, (n - g - a) / g));
+            unsigned long long any = scan_rows(car.data(), key.data() + a, tmp.data() + a, full, g);
+            int c = 0;
+            long long q = a + full * g;
+            const long long lim = std::min(e, n - g);   // positions with a partner one gap on
+            for (; q < lim; ++q) {
+                const unsigned long long cc = scan_op(car[c], key[q]);   // c_k
+                car[c] = cc;
+                const unsigned long long nx = key[q + g];                 // x_{k+1}
+                const unsigned long long m = 0ULL - (unsigned long long)((cc >> 32) > (nx >> 32));
+                tmp[q] = (nx & m) | (cc & ~m);
+                any |= m;
+                if (++c == g) c = 0;
+            }
+            for (; q < e; ++q) {   // the last g positions: the carried entry lands
+                tmp[q] = scan_op(car[c], key[q]);
+                if (++c == g) c = 0;
+            }
+            sw[t] = any != 0;
         });
         key.swap(tmp);
         bool any = false;
@@ -695,7 +968,10 @@ int FSolver::SortElements()
         return any;
     };
     int gap = NumEls, i = 0;
+    double ms_wide = 0, ms_narrow = 0;
+    int n_wide = 0, n_narrow = 0;
     do {
+        const auto tp = std::chrono::steady_clock::now();
         if (gap > 1) {
             gap = (gap * 10) / 13;
             if ((gap == 10) || (gap == 9)) gap = 11;
@@ -703,24 +979,19 @@ int FSolver::SortElements()
         i = 0;
         if (T > 1 && gap >= 8 * T && NumEls >= (1 << 16)) {
             std::vector<char> sw(T, 0);
-            std::vector<std::thread> th;
             const int g = gap;
             auto part = [&](int t) {
                 const int r0 = (int)((long long)g * t / T), r1 = (int)((long long)g * (t + 1) / T);
-                char any = 0;
-                for (long long b = 0; b + g < NumEls; b += g)
-                    for (int r = r0; r < r1 && b + r + g < NumEls; ++r) {
-                        unsigned long long &x = key[b + r], &y = key[b + r + g];
-                        if ((x >> 32) > (y >> 32)) {
-                            std::swap(x, y);
-                            any = 1;
-                        }
-                    }
-                sw[t] = any;
+                unsigned long long any = 0;
+                for (long long b = 0; b + g < NumEls; b += g) {
+                    // (the class range [r0, r1) of this block and its partners one gap on:
+                    // disjoint, so the compare-swaps are independent -- branch-free)
+                    const int re = (int)std::min<long long>(r1, NumEls - g - b);
+                    any |= comb_swap_run(key.data() + b + r0, key.data() + b + r0 + g, re - r0);
+                }
+                sw[t] = any != 0;
             };
-            for (int t = 1; t < T; ++t) th.emplace_back(part, t);
-            part(0);
-            for (auto &x : th) x.join();
+            pool.run(T, part);
             for (char c : sw) i |= c;
         } else if (T > 1 && NumEls >= (1 << 16)) {   // (narrow passes: few classes)
             i = scan_pass(gap) ? 1 : 0;
@@ -732,13 +1003,30 @@ int FSolver::SortElements()
                 }
             }
         }
+        const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
+        if (T > 1 && gap >= 8 * T && NumEls >= (1 << 16)) ms_wide += dt, ++n_wide;
+        else ms_narrow += dt, ++n_narrow;
     } while ((gap > 1) && (i > 0));
+    if (tr.on)
+        std::fprintf(stderr, "[load]   comb passes: %d wide %.1f ms, %d narrow %.1f ms\n", n_wide, ms_wide, n_narrow,
+                     ms_narrow);
     tr.mark("  comb sort");
-    std::vector<CMElement> sorted(NumEls);
-    par_for(NumEls, 1 << 16, [&](long long a, long long b) {
-        for (long long k = a; k < b; k++) sorted[k] = meshele[(unsigned)(key[k] & 0xffffffffu)];
-    });
-    meshele.swap(sorted);
+    // the permutation applied through raw storage (copy-constructed in
+    // parallel, then assigned back): no serial value-initialisation of a
+    // second element array
+    {
+        HugeBuf<char> store;
+        if (!store.allocate(sizeof(CMElement) * (size_t)std::max(1, NumEls))) return false;
+        CMElement *raw = reinterpret_cast<CMElement *>(store.data());
+        par_for(NumEls, 1 << 16, [&](long long a, long long b) {
+            for (long long k = a; k < b; k++) new (raw + k) CMElement(meshele[(unsigned)(key[k] & 0xffffffffu)]);
+        });
+        par_for(NumEls, 1 << 16, [&](long long a, long long b) {
+            for (long long k = a; k < b; k++) meshele[k] = raw[k];
+        });
+        static_assert(std::is_trivially_destructible<CMElement>::value, "raw storage freed without destructors");
+    }
+    tr.mark("  permute");
     return true;
 }
 
@@ -748,22 +1036,52 @@ int FSolver::Cuthill(bool deleteFiles)
     LoadTrace tr;
     const int n_lines = (int)edges_.size();
     std::vector<int> numcon(NumNodes, 0), newnum(NumNodes, -1), nxtnum(NumNodes, -1);
-    for (auto &e : edges_) {
-        numcon[e[0]]++;
-        numcon[e[1]]++;
-    }
     // neighbour lists as CSR, each in the order the reference's lists get
-    // their entries (edge order)
-    std::vector<int> aptr((size_t)NumNodes + 1, 0), adj(2 * edges_.size());
-    for (int i = 0; i < NumNodes; i++) aptr[i + 1] = aptr[i] + numcon[i];
+    // their entries (edge order).  Each thread owns a range of nodes and
+    // scans every edge for the ends it owns -- counts, then the fill -- so
+    // each list is appended in edge order, as the sequential loop does.
+    std::vector<int> aptr, adj;
+    huge_reserve(aptr, (size_t)NumNodes + 1);
+    huge_reserve(adj, 2 * edges_.size());
+    aptr.assign((size_t)NumNodes + 1, 0);
+    adj.resize(2 * edges_.size());
     {
-        std::vector<int> cur(aptr.begin(), aptr.end() - 1);
-        for (auto &e : edges_) {
-            adj[cur[e[0]]++] = e[1];
-            adj[cur[e[1]]++] = e[0];
-        }
+        const int T = (int)std::max<long long>(1, std::min<long long>(HostPool::get().size(), (long long)n_lines / 65536));
+        auto lo = [&](int t) { return (int)((long long)NumNodes * t / T); };
+        std::vector<long long> part(T + 1, 0);
+        par_for(T, 1, [&](long long t0, long long t1) {
+            for (long long t = t0; t < t1; ++t) {
+                const int a = lo((int)t);
+                const unsigned span = (unsigned)(lo((int)t + 1) - a);
+                for (const auto &e : edges_) {
+                    if ((unsigned)(e[0] - a) < span) numcon[e[0]]++;
+                    if ((unsigned)(e[1] - a) < span) numcon[e[1]]++;
+                }
+                long long sum = 0;
+                for (int v = a; v < a + (int)span; ++v) sum += numcon[v];
+                part[t + 1] = sum;
+            }
+        });
+        for (int t = 0; t < T; ++t) part[t + 1] += part[t];
+        par_for(T, 1, [&](long long t0, long long t1) {
+            for (long long t = t0; t < t1; ++t) {
+                const int a = lo((int)t);
+                const unsigned span = (unsigned)(lo((int)t + 1) - a);
+                long long o = part[t];
+                for (int v = a; v < a + (int)span; ++v) {
+                    aptr[v] = (int)o;
+                    o += numcon[v];
+                }
+                std::vector<int> cur(aptr.begin() + a, aptr.begin() + a + span);
+                for (const auto &e : edges_) {
+                    if ((unsigned)(e[0] - a) < span) adj[cur[e[0] - a]++] = e[1];
+                    if ((unsigned)(e[1] - a) < span) adj[cur[e[1] - a]++] = e[0];
+                }
+            }
+        });
+        aptr[NumNodes] = (int)part[T];
     }
-    if (deleteFiles) remove((PathName + ".edge").c_str());
+    if (deleteFiles) remove_async({PathName + ".edge"});
     tr.mark("adjacency");
     // bubble sort by increasing connectivity: swaps only on a strict decrease,
     // so it is the stable sort of the list by numcon -- an insertion sort per
@@ -982,6 +1300,13 @@ bool FSolver::make_desc(DescStore &ds)
     ds.cir.resize(circproplist.size());
     for (size_t k = 0; k < circproplist.size(); k++)
         ds.cir[k] = xfk_circuit_desc{circproplist[k].CircType, circproplist[k].Amps_re, circproplist[k].dVolts_re};
+    // the mesh arrays: huge-page storage, filled in parallel
+    huge_reserve(ds.x, (size_t)NumNodes);
+    huge_reserve(ds.y, (size_t)NumNodes);
+    huge_reserve(ds.marker, (size_t)NumNodes);
+    huge_reserve(ds.p, 3ull * NumEls);
+    huge_reserve(ds.e, 3ull * NumEls);
+    huge_reserve(ds.lbl, (size_t)NumEls);
     ds.x.resize(NumNodes);
     ds.y.resize(NumNodes);
     ds.marker.resize(NumNodes);
@@ -989,23 +1314,31 @@ bool FSolver::make_desc(DescStore &ds)
     ds.e.resize(3LL * NumEls);
     ds.lbl.resize(NumEls);
     ds.pbc.resize(3LL * NumPBCs);
-    for (int i = 0; i < NumNodes; i++) {
-        ds.x[i] = meshnode[i].x;
-        ds.y[i] = meshnode[i].y;
-        ds.marker[i] = meshnode[i].BoundaryMarker;
-        if (ds.marker[i] >= (int)nodeproplist.size()) ds.marker[i] = -1;
-    }
-    for (int i = 0; i < NumEls; i++) {
-        if (labellist[meshele[i].lbl].BlockType < 0) {
-            warn("an element lies in a region without material (hole label)\n");
-            return false;
+    const int nnp = (int)nodeproplist.size(), nlp = (int)lineproplist.size();
+    par_for(NumNodes, 1 << 16, [&](long long a, long long b) {
+        for (long long i = a; i < b; i++) {
+            ds.x[i] = meshnode[i].x;
+            ds.y[i] = meshnode[i].y;
+            const int m = meshnode[i].BoundaryMarker;
+            ds.marker[i] = m >= nnp ? -1 : m;
         }
-        for (int q = 0; q < 3; q++) {
-            ds.p[3LL * i + q] = meshele[i].p[q];
-            int eq = meshele[i].e[q];
-            ds.e[3LL * i + q] = (eq >= 0 && eq < (int)lineproplist.size()) ? eq : -1;
+    });
+    std::atomic<bool> hole{false};
+    par_for(NumEls, 1 << 16, [&](long long a, long long b) {
+        for (long long i = a; i < b; i++) {
+            const CMElement &el = meshele[i];
+            if (labellist[el.lbl].BlockType < 0) hole = true;
+            for (int q = 0; q < 3; q++) {
+                ds.p[3 * i + q] = el.p[q];
+                const int eq = el.e[q];
+                ds.e[3 * i + q] = (eq >= 0 && eq < nlp) ? eq : -1;
+            }
+            ds.lbl[i] = el.lbl;
         }
-        ds.lbl[i] = meshele[i].lbl;
+    });
+    if (hole) {
+        warn("an element lies in a region without material (hole label)\n");
+        return false;
     }
     for (int k = 0; k < NumPBCs; k++) {
         ds.pbc[3 * k] = pbclist[k].x;
@@ -1153,30 +1486,29 @@ int FSolver::Harmonic2D()
 namespace {
 // "%.17g" and "%i" as printf writes them (std::to_chars: the same correctly
 // rounded digits and the same %g form), for the .ans's large sections
-inline char *put_g17(char *p, double v) { return std::to_chars(p, p + 32, v, std::chars_format::general, 17).ptr; }
+inline char *put_g17(char *p, double v) { return fastnum::put_g17(p, v); }   // (exact: fastnum.h)
 inline char *put_i(char *p, int v) { return std::to_chars(p, p + 16, v).ptr; }
 // lines [0, n): line(i, buf) writes line i (at most max_line chars) and returns
-// its end; formatted in parallel chunks, written in order
+// its end; formatted in parallel chunks into huge-page buffers, then written
+// in order by fwrite (one write of ~10 GB/s on the box; a shared mapping of
+// the file was measured 5x slower, tools/lab/io_probe.cpp)
 template <class F>
 void write_lines(FILE *fp, int n, int max_line, F line)
 {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const int T = (int)std::max(1, std::min<int>((int)std::min(hw, 16u), n / 65536));
-    std::vector<std::vector<char>> buf(T);
-    auto part = [&](int t) {
-        const int a = (int)((long long)n * t / T), b = (int)((long long)n * (t + 1) / T);
-        std::vector<char> &o = buf[t];
-        o.resize((size_t)(b - a) * max_line + 1);
-        char *q = o.data();
-        for (int i = a; i < b; ++i) q = line(i, q);
-        o.resize((size_t)(q - o.data()));
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back(part, t);
-    part(0);
-    for (auto &x : th) x.join();
-    for (auto &o : buf)
-        if (!o.empty()) fwrite(o.data(), 1, o.size(), fp);
+    const int T = (int)std::max(1, std::min<int>(HostPool::get().size(), n / 65536));
+    std::vector<HugeBuf<char>> buf(T);
+    std::vector<size_t> len(T, 0);
+    par_for(T, 1, [&](long long t0, long long t1) {
+        for (long long t = t0; t < t1; ++t) {
+            const int a = (int)((long long)n * t / T), b = (int)((long long)n * (t + 1) / T);
+            buf[t].allocate((size_t)(b - a) * max_line + 1);
+            char *q = buf[t].data();
+            for (int i = a; i < b; ++i) q = line(i, q);
+            len[t] = (size_t)(q - buf[t].data());
+        }
+    });
+    for (int t = 0; t < T; ++t)
+        if (len[t]) fwrite(buf[t].data(), 1, len[t], fp);
 }
 }  // namespace
 
@@ -1334,6 +1666,10 @@ int FSolver::WriteHarmonic2D()
 
 bool FSolver::runSolver(bool verbose)
 {
+    struct JoinRemovals {   // the mesh files are gone when runSolver returns, as in the reference
+        FSolver *s;
+        ~JoinRemovals() { s->join_removals(); }
+    } join_at_exit{this};
     for (double &m : ms_phase) m = 0;
     auto t = std::chrono::steady_clock::now();
     LoadMeshErr err = LoadMesh(deleteMeshFiles);

@@ -11,6 +11,7 @@
 
 #include <array>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../../include/xfemm_kernels.h"
@@ -26,7 +27,9 @@ int PrintWarningMsg(const char *fmt, ...);
 class FSolver : public FemmProblemData {
 public:
     FSolver();
-    ~FSolver() = default;
+    ~FSolver();
+    FSolver(const FSolver &) = delete;
+    FSolver &operator=(const FSolver &) = delete;
 
     // General problem attributes (fsolver.h / feasolver.h)
     std::string PathName;
@@ -66,6 +69,7 @@ public:
     void WriteAirGapElements(FILE *fp) const;            // static2d.cpp:1161-1190, harmonic2d.cpp:1002-1030
     void GetFillFactor(int lbl);                         // fsolver.cpp:1083-1105 (static)
     static std::string getErrorString(LoadMeshErr err);
+    void join_removals();   // wait for the mesh-file deletions LoadMesh / Cuthill started
 
     // result of the last Static2D: A (= V*c) per node, in meshnode order;
     // Harmonic2D: A holds the real parts and A_im the imaginary parts
@@ -83,6 +87,8 @@ public:
 
 private:
     std::vector<std::array<int, 3>> edges_;   // .edge content: n0, n1, marker
+    std::vector<std::thread> removers_;       // mesh-file deletions in flight (joined by runSolver)
+    void remove_async(std::vector<std::string> paths);
     void warn(const std::string &msg);
     struct DescStore;                         // property tables + mesh arrays behind an xfk_problem_desc
     bool make_desc(DescStore &ds);
