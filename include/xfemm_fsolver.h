@@ -36,6 +36,17 @@ void xfemm_fsolver_set_message_handlers(xfemm_fsolver *s, xfemm_message_fn warn,
 int xfemm_fsolver_set_pathname(xfemm_fsolver *s, const char *path_without_extension);
 int xfemm_fsolver_set_device(xfemm_fsolver *s, int device);
 int xfemm_fsolver_set_delete_mesh_files(xfemm_fsolver *s, int delete_files);
+/* Sharded solve (north_star: large meshes shard across up to 8 GPUs under the
+ * same FSolver API).  Every rank of `comm` (include/xfemm_kernels.h:
+ * xfk_comm_create_rccl, one process per GPU, or xfk_comm_create_local)
+ * creates its own FSolver on the same PathName and calls
+ * load_problem_file / run_solver; runSolver (reference fsolver.cpp:1213-1340)
+ * then builds the rank's row block with xfk_problem_create_dist /
+ * xfk_problem_create_harmonic_dist, the solve is collective, every rank holds
+ * the global solution afterwards, rank 0 writes the .ans and deletes the mesh
+ * files (after the collective solve, so every rank has read them).  The
+ * communicator stays the caller's.  NULL: one device (the default). */
+int xfemm_fsolver_set_comm(xfemm_fsolver *s, xfk_comm *comm);
 int xfemm_fsolver_load_problem_file(xfemm_fsolver *s);
 int xfemm_fsolver_run_solver(xfemm_fsolver *s, int verbose);
 

@@ -193,10 +193,19 @@ enum {
     XFK_OPT_AMG_WLEVEL = 10,    /* the folded coarse level that runs a W-cycle (two coarse
                                    corrections); -2 (default): the level above the last V-cycle
                                    level (XFK_AMG_W overrides), -1: a plain V-cycle */
-    XFK_OPT_AMG_F32 = 11        /* 1 (default, unless XFK_AMG_F32=0 is set; needs 16-bit columns):
+    XFK_OPT_AMG_F32 = 11,       /* 1 (default, unless XFK_AMG_F32=0 is set; needs 16-bit columns):
                                    the V-cycle's level-0 transfers (R, P~) store f32 values,
                                    products and sums in f64; 0: f64 values.  The sweeps and the
                                    PCG's own SpMV keep A in f64. */
+    XFK_OPT_NEWTON_INEXACT = 12 /* 1 (default, unless XFK_NEWTON_INEXACT=0 is set): the nonlinear
+                                   loop's passes before the last solve their linear system to a
+                                   forcing tolerance (Eisenstat-Walker: eta times the last Newton
+                                   change |dV| / |V|, clamped to [Precision, 1e-3]); a pass that
+                                   meets the loop's stop test (|dV| / |V| < 100 Precision) at a
+                                   tolerance looser than Precision is followed by one more pass
+                                   solved to Precision, so the answer is always that of a pass
+                                   solved to the reference's tolerance.  0: every pass to
+                                   Precision, as the reference (static2d.cpp:997-1008). */
 };
 int xfk_set_option(xfk_problem *prob, int option, double value);
 
@@ -469,6 +478,16 @@ int xfk_problem_memory(const xfk_problem *prob, long long *out4);
  * keep theirs). */
 int xfk_cache_stats(long long *out3);
 int xfk_release_cache(void);
+
+/* FEASolver::SortElements (cfemm/libfemm/cuthill.cpp:39-86; called from
+ * FSolver::Cuthill) on the device: the reference's comb sort -- gap * 10 / 13
+ * (9, 10 -> 11), swap on a strictly greater score, stop after the first pass
+ * without a swap or after the first gap-1 pass (`while ((gap > 1) && (i > 0))`,
+ * so the result need not be fully sorted) -- of the elements by
+ * score[i] = p0 + p1 + p2 of element i, every pass simulated: the reference's
+ * order, equal scores included.  perm[k] = the element at position k after
+ * the sort. */
+int xfk_sort_elements(int n_elems, const unsigned *score, int device, int *perm);
 
 /* Magnetisation-direction function of a block label, evaluated for elements
  * as the reference's element loop does (FSolver::Static2D,

@@ -38,6 +38,13 @@ int xfemm_fsolver_set_device(xfemm_fsolver *h, int device)
     return 1;
 }
 
+int xfemm_fsolver_set_comm(xfemm_fsolver *h, xfk_comm *comm)
+{
+    if (!h) return 0;
+    h->s.comm = comm;
+    return 1;
+}
+
 int xfemm_fsolver_set_delete_mesh_files(xfemm_fsolver *h, int del)
 {
     if (!h) return 0;

@@ -42,7 +42,11 @@ int PrintWarningMsg(const char *fmt, ...)
 
 FSolver::FSolver() : WarnMessage(&PrintWarningMsg), PrintMessage(&PrintWarningMsg) {}
 
-FSolver::~FSolver() { join_removals(); }
+FSolver::~FSolver()
+{
+    if (ele_fmt_.joinable()) ele_fmt_.join();
+    join_removals();
+}
 
 // The mesh files the reference deletes once read (fsolver.cpp:711-716,
 // cuthill.cpp:140): unlinking ~170 MB of page cache costs tens of ms, so it
@@ -52,6 +56,16 @@ void FSolver::remove_async(std::vector<std::string> paths)
     removers_.emplace_back([paths = std::move(paths)] {
         for (const auto &p : paths) remove(p.c_str());
     });
+}
+
+bool FSolver::writes_output() const { return !comm || xfk_comm_rank(comm) == 0; }
+
+void FSolver::remove_mesh_files_after_collective_solve()
+{
+    if (!comm || !deleteMeshFiles || xfk_comm_rank(comm) != 0 || !previousSolutionFile.empty()) return;
+    std::vector<std::string> v;
+    for (const char *ext : {".ele", ".node", ".pbc", ".poly", ".edge"}) v.push_back(PathName + ext);
+    remove_async(std::move(v));
 }
 
 void FSolver::join_removals()
@@ -882,12 +896,53 @@ unsigned long long scan_rows(unsigned long long *car, const unsigned long long *
 }
 }  // namespace
 
+// meshele[k] = the old meshele[src(k)]: through raw storage (copy-constructed
+// in parallel, then assigned back), no serial value-initialisation of a second
+// element array
+template <class Src>
+bool FSolver::permute_elements(Src src)
+{
+    HugeBuf<char> store;
+    if (!store.allocate(sizeof(CMElement) * (size_t)std::max(1, NumEls))) return false;
+    CMElement *raw = reinterpret_cast<CMElement *>(store.data());
+    par_for(NumEls, 1 << 16, [&](long long a, long long b) {
+        for (long long k = a; k < b; k++) new (raw + k) CMElement(meshele[src(k)]);
+    });
+    par_for(NumEls, 1 << 16, [&](long long a, long long b) {
+        for (long long k = a; k < b; k++) meshele[k] = raw[k];
+    });
+    static_assert(std::is_trivially_destructible<CMElement>::value, "raw storage freed without destructors");
+    return true;
+}
+
 int FSolver::SortElements()
 {
     // comb sort on p0+p1+p2 (cuthill.cpp:39-86); not stable, restated exactly:
     // the same comparisons and swaps, on packed (score, element) keys instead
-    // of the element records, which are permuted once at the end
+    // of the element records, which are permuted once at the end.  With a
+    // GPU (the solve needs one anyway) every pass runs on the device
+    // (xfk_sort_elements: ~2 ms instead of ~45 on 16 host cores); without
+    // one, or with XFEMM_HOST_SORT set, on the host below.
     LoadTrace tr;
+    if (NumEls > 1 && !std::getenv("XFEMM_HOST_SORT") && xfk_device_count() > 0) {
+        HugeBuf<unsigned> score;
+        HugeBuf<int> perm;
+        if (!score.allocate((size_t)NumEls) || !perm.allocate((size_t)NumEls)) return false;
+        par_for(NumEls, 1 << 16, [&](long long a, long long b) {
+            for (long long k = a; k < b; k++) {
+                const CMElement &e = meshele[k];
+                score[k] = (unsigned)((long long)e.p[0] + e.p[1] + e.p[2]);
+            }
+        });
+        if (xfk_sort_elements(NumEls, score.data(), device, perm.data()) != XFK_OK) {
+            warn(std::string("device element sort failed: ") + xfk_last_error() + "\n");
+            return false;
+        }
+        tr.mark("  device comb sort");
+        permute_elements([&](long long k) { return perm[k]; });
+        tr.mark("  permute");
+        return true;
+    }
     std::vector<unsigned long long> key, tmp;
     huge_reserve(key, (size_t)NumEls);
     huge_reserve(tmp, (size_t)NumEls);
@@ -1014,18 +1069,7 @@ int FSolver::SortElements()
     // the permutation applied through raw storage (copy-constructed in
     // parallel, then assigned back): no serial value-initialisation of a
     // second element array
-    {
-        HugeBuf<char> store;
-        if (!store.allocate(sizeof(CMElement) * (size_t)std::max(1, NumEls))) return false;
-        CMElement *raw = reinterpret_cast<CMElement *>(store.data());
-        par_for(NumEls, 1 << 16, [&](long long a, long long b) {
-            for (long long k = a; k < b; k++) new (raw + k) CMElement(meshele[(unsigned)(key[k] & 0xffffffffu)]);
-        });
-        par_for(NumEls, 1 << 16, [&](long long a, long long b) {
-            for (long long k = a; k < b; k++) meshele[k] = raw[k];
-        });
-        static_assert(std::is_trivially_destructible<CMElement>::value, "raw storage freed without destructors");
-    }
+    if (!permute_elements([&](long long k) { return (int)(key[k] & 0xffffffffu); })) return false;
     tr.mark("  permute");
     return true;
 }
@@ -1389,8 +1433,12 @@ int FSolver::Static2D()
     auto t = std::chrono::steady_clock::now();
     DescStore ds;
     if (!make_desc(ds)) return false;
+    // the .ans element section depends on the mesh only: formatted while the
+    // device solves (joined by WriteStatic2D, or below on failure)
+    if (ele_fmt_.joinable()) ele_fmt_.join();
+    if (writes_output()) ele_fmt_ = std::thread([this] { ele_text_ = format_static_elements(); });
     xfk_problem *prob = nullptr;
-    int rc = xfk_problem_create(&ds.d, device, &prob);
+    int rc = comm ? xfk_problem_create_dist(&ds.d, device, comm, &prob) : xfk_problem_create(&ds.d, device, &prob);
     ms_phase[2] = ms_since(t);
     if (rc == XFK_OK) rc = xfk_static2d(prob, 0, &stats);
     if (rc == XFK_OK) {
@@ -1407,7 +1455,11 @@ int FSolver::Static2D()
             circproplist[k].dV = dV[k];
         }
     }
-    if (rc != XFK_OK) warn(std::string("GPU solver error: ") + xfk_last_error() + "\n");
+    if (rc != XFK_OK) {
+        warn(std::string("GPU solver error: ") + xfk_last_error() + "\n");
+        if (ele_fmt_.joinable()) ele_fmt_.join();
+        ele_text_ = Formatted();
+    }
     if (prob) xfk_problem_destroy(prob);
     ms_phase[3] = ms_since(t);
     return rc == XFK_OK;
@@ -1448,7 +1500,8 @@ int FSolver::Harmonic2D()
     xfk_harmonic_desc ac{Frequency, bac.data(), lac.empty() ? nullptr : lac.data(),
                          cac.empty() ? nullptr : cac.data(), ACSolver, prox.data()};
     xfk_problem *prob = nullptr;
-    int rc = xfk_problem_create_harmonic(&ds.d, &ac, device, &prob);
+    int rc = comm ? xfk_problem_create_harmonic_dist(&ds.d, &ac, device, comm, &prob)
+                  : xfk_problem_create_harmonic(&ds.d, &ac, device, &prob);
     ms_phase[2] = ms_since(t);
     if (rc == XFK_OK) rc = xfk_harmonic2d(prob, 0, &stats);
     std::vector<double> Ac;
@@ -1493,27 +1546,61 @@ inline char *put_i(char *p, int v) { return std::to_chars(p, p + 16, v).ptr; }
 // in order by fwrite (one write of ~10 GB/s on the box; a shared mapping of
 // the file was measured 5x slower, tools/lab/io_probe.cpp)
 template <class F>
-void write_lines(FILE *fp, int n, int max_line, F line)
+FSolver::Formatted format_lines(int n, int max_line, F line)
 {
     const int T = (int)std::max(1, std::min<int>(HostPool::get().size(), n / 65536));
-    std::vector<HugeBuf<char>> buf(T);
-    std::vector<size_t> len(T, 0);
+    FSolver::Formatted f;
+    f.buf.resize(T);
+    f.len.assign(T, 0);
     par_for(T, 1, [&](long long t0, long long t1) {
         for (long long t = t0; t < t1; ++t) {
             const int a = (int)((long long)n * t / T), b = (int)((long long)n * (t + 1) / T);
-            buf[t].allocate((size_t)(b - a) * max_line + 1);
-            char *q = buf[t].data();
+            f.buf[t].allocate((size_t)(b - a) * max_line + 1);
+            char *q = f.buf[t].data();
             for (int i = a; i < b; ++i) q = line(i, q);
-            len[t] = (size_t)(q - buf[t].data());
+            f.len[t] = (size_t)(q - f.buf[t].data());
         }
     });
-    for (int t = 0; t < T; ++t)
-        if (len[t]) fwrite(buf[t].data(), 1, len[t], fp);
+    return f;
+}
+void write_formatted(FILE *fp, const FSolver::Formatted &f)
+{
+    for (size_t t = 0; t < f.buf.size(); ++t)
+        if (f.len[t]) fwrite(f.buf[t].data(), 1, f.len[t], fp);
+}
+template <class F>
+void write_lines(FILE *fp, int n, int max_line, F line)
+{
+    write_formatted(fp, format_lines(n, max_line, line));
 }
 }  // namespace
 
+FSolver::Formatted FSolver::format_static_elements() const
+{
+    return format_lines(NumEls, 64, [&](int i, char *q) {
+        for (int m = 0; m < 3; ++m) {
+            q = put_i(q, meshele[i].p[m]);
+            *q++ = '\t';
+        }
+        q = put_i(q, meshele[i].lbl);
+        *q++ = '\n';
+        return q;
+    });
+}
+
+// an existing .ans is moved aside and unlinked beside the write (truncating
+// ~130 MB of page cache in fopen costs ~7 ms); the new file is written whole
+void FSolver::clear_old_output(const std::string &path)
+{
+    struct stat st;
+    if (::stat(path.c_str(), &st) != 0 || st.st_size < (1 << 20)) return;
+    const std::string aside = path + ".xfemm-old";
+    if (::rename(path.c_str(), aside.c_str()) == 0) remove_async({aside});
+}
+
 int FSolver::WriteStatic2D()
 {
+    LoadTrace tr;
     const double unitconv[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
     std::string fin = PathName + ".fem", fout = PathName + ".ans";
     FILE *fz = fopen(fin.c_str(), "rt");
@@ -1521,6 +1608,7 @@ int FSolver::WriteStatic2D()
         warn("Couldn't open " + fin + "\n");
         return false;
     }
+    clear_old_output(fout);
     FILE *fp = fopen(fout.c_str(), "wt");
     if (!fp) {
         fclose(fz);
@@ -1530,6 +1618,7 @@ int FSolver::WriteStatic2D()
     char c[1024];
     while (fgets(c, 1024, fz) != nullptr) fputs(c, fp);
     fclose(fz);
+    tr.mark("  .fem echo");
     fprintf(fp, "[Solution]\n");
     const double cf = unitconv[LengthUnits];
     fprintf(fp, "%i\n", NumNodes);
@@ -1547,17 +1636,14 @@ int FSolver::WriteStatic2D()
         *q++ = '\n';
         return q;
     });
+    tr.mark("  .ans nodes");
     fprintf(fp, "%i\n", NumEls);
     fflush(fp);
-    write_lines(fp, NumEls, 64, [&](int i, char *q) {
-        for (int m = 0; m < 3; ++m) {
-            q = put_i(q, meshele[i].p[m]);
-            *q++ = '\t';
-        }
-        q = put_i(q, meshele[i].lbl);
-        *q++ = '\n';
-        return q;
-    });
+    if (ele_fmt_.joinable()) ele_fmt_.join();   // (formatted beside the device solve)
+    else ele_text_ = format_static_elements();
+    write_formatted(fp, ele_text_);
+    ele_text_ = Formatted();
+    tr.mark("  .ans elements");
     fprintf(fp, "%i\n", (int)labellist.size());
     for (size_t k = 0; k < labellist.size(); k++) {
         int i = labellist[k].InCircuit;
@@ -1571,6 +1657,7 @@ int FSolver::WriteStatic2D()
     for (int k = 0; k < NumPBCs; k++) fprintf(fp, "%i\t%i\t%i\n", pbclist[k].x, pbclist[k].y, pbclist[k].t);
     WriteAirGapElements(fp);
     fclose(fp);
+    tr.mark("  .ans close");
     return true;
 }
 
@@ -1672,7 +1759,11 @@ bool FSolver::runSolver(bool verbose)
     } join_at_exit{this};
     for (double &m : ms_phase) m = 0;
     auto t = std::chrono::steady_clock::now();
-    LoadMeshErr err = LoadMesh(deleteMeshFiles);
+    // sharded (set_comm): every rank reads the same mesh files; they are
+    // deleted by rank 0 once the collective solve has run (every rank has
+    // read them by then)
+    const bool delete_now = deleteMeshFiles && !comm;
+    LoadMeshErr err = LoadMesh(delete_now);
     ms_phase[0] = ms_since(t);
     if (err != NOERROR) {
         warn(getErrorString(err));
@@ -1680,7 +1771,7 @@ bool FSolver::runSolver(bool verbose)
     }
     if (previousSolutionFile.empty()) {
         if (verbose) PrintMessage("renumbering nodes using Cuthill-McKee method\n");
-        if (!Cuthill(deleteMeshFiles)) {
+        if (!Cuthill(delete_now)) {
             warn("problem renumbering node points\n");
             return false;
         }
@@ -1703,10 +1794,13 @@ bool FSolver::runSolver(bool verbose)
         PrintMessage("Problem Statistics:\n%i nodes\n%i elements\nPrecision: %f\n", NumNodes, NumEls, Precision);
     }
     if (Frequency != 0) {   // Harmonic2D / HarmonicAxisymmetric, one .ans layout (fsolver.cpp:1312-1336)
-        if (!Harmonic2D()) {
+        const bool solved = Harmonic2D();
+        remove_mesh_files_after_collective_solve();
+        if (!solved) {
             warn("Couldn't solve the problem\n");
             return false;
         }
+        if (!writes_output()) return true;   // (sharded: rank 0 writes the .ans)
         if (verbose)
             PrintMessage(ProblemTypeV == AXISYMMETRIC ? "Harmonic axisymmetric problem solved\n"
                                                       : "Harmonic 2-D problem solved\n");
@@ -1719,10 +1813,13 @@ bool FSolver::runSolver(bool verbose)
         if (verbose) PrintMessage("results written to disk\n");
         return true;
     }
-    if (!Static2D()) {
+    const bool solved = Static2D();
+    remove_mesh_files_after_collective_solve();
+    if (!solved) {
         warn("Couldn't solve the problem\n");
         return false;
     }
+    if (!writes_output()) return true;   // (sharded: rank 0 writes the .ans)
     if (verbose)
         PrintMessage(ProblemTypeV == AXISYMMETRIC ? "Static axisymmetric problem solved\n" : "Static 2-D problem solved\n");
     t = std::chrono::steady_clock::now();

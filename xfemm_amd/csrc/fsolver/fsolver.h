@@ -16,6 +16,7 @@
 
 #include "../../../include/xfemm_kernels.h"
 #include "femm_problem.h"
+#include "hostmem.h"
 
 namespace xfemm {
 
@@ -55,6 +56,11 @@ public:
     // GPU selection and file handling
     int device = 0;
     bool deleteMeshFiles = true;
+    // sharded solve over comm's ranks (xfk_problem_create_dist): every rank
+    // runs its own FSolver on the same files; rank 0 writes the .ans and
+    // deletes the mesh files.  nullptr: one device.
+    xfk_comm *comm = nullptr;
+    bool writes_output() const;
 
     bool LoadProblemFile();                              // fsolver.cpp:202-348
     bool loadPreviousSolution(bool loadAprev);           // fsolver.cpp:990-1081
@@ -70,6 +76,11 @@ public:
     void GetFillFactor(int lbl);                         // fsolver.cpp:1083-1105 (static)
     static std::string getErrorString(LoadMeshErr err);
     void join_removals();   // wait for the mesh-file deletions LoadMesh / Cuthill started
+    // .ans text formatted in parallel chunks (fsolver.cpp: format_lines)
+    struct Formatted {
+        std::vector<HugeBuf<char>> buf;
+        std::vector<size_t> len;
+    };
 
     // result of the last Static2D: A (= V*c) per node, in meshnode order;
     // Harmonic2D: A holds the real parts and A_im the imaginary parts
@@ -89,6 +100,13 @@ private:
     std::vector<std::array<int, 3>> edges_;   // .edge content: n0, n1, marker
     std::vector<std::thread> removers_;       // mesh-file deletions in flight (joined by runSolver)
     void remove_async(std::vector<std::string> paths);
+    template <class Src>
+    bool permute_elements(Src src);
+    std::thread ele_fmt_;                     // the .ans element section, formatted beside the solve
+    Formatted ele_text_;
+    Formatted format_static_elements() const;
+    void clear_old_output(const std::string &path);
+    void remove_mesh_files_after_collective_solve();
     void warn(const std::string &msg);
     struct DescStore;                         // property tables + mesh arrays behind an xfk_problem_desc
     bool make_desc(DescStore &ds);

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <cstdlib>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -66,8 +67,14 @@ class HostPool {
   private:
     HostPool()
     {
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        const int nw = (int)std::min(hw, 16u) - 1;
+        // XFEMM_HOST_THREADS overrides the thread count (1..64; tests)
+        unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        hw = std::min(hw, 16u);
+        if (const char *e = std::getenv("XFEMM_HOST_THREADS")) {
+            const int v = std::atoi(e);
+            if (v >= 1 && v <= 64) hw = (unsigned)v;
+        }
+        const int nw = (int)hw - 1;
         for (int i = 0; i < nw; ++i) workers_.emplace_back([this] { loop(); });
         for (auto &w : workers_) w.detach();
     }

@@ -1121,6 +1121,12 @@ static int allreduce_partials(xfk_problem *P, int narrays)
 }
 
 static bool trace_newton() { return std::getenv("XFK_TRACE_NEWTON") != nullptr; }
+// XFK_NEWTON_INEXACT=0 turns the inexact Newton passes off (XFK_OPT_NEWTON_INEXACT)
+static bool newton_inexact_env()
+{
+    const char *e = std::getenv("XFK_NEWTON_INEXACT");
+    return !(e && e[0] == '0');
+}
 
 // a Newton refresh re-forms level 0's P~ (~0.32 ms on configs[3]) when the
 // last pass ran at least this many PCG iterations, else level 0 runs
@@ -1225,8 +1231,10 @@ static int pcg_start(xfk_problem *P, int flag)
     hipStream_t s = P->stream;
     const int N = P->N;
     *P->pcg_host = CgState{};   // pinned: the upload does not stage through the host
-    P->pcg_host->tol = P->precision;
-    launch_cg_state_init(s, P->pcg.p, P->precision);
+    const double tol = P->pcg_tol > 0 ? P->pcg_tol : P->precision;
+    P->pcg_host->tol = tol;
+    P->pcg_host->tol_rel = P->pcg_tol_rel;
+    launch_cg_state_init(s, P->pcg.p, tol, P->pcg_tol_rel);
     if (P->comm) XFK_CHECK(hipMemsetAsync(P->part_loc.p, 0, sizeof(double) * 4 * P->Gpart, s));
     launch_diag_inv(s, N, P->diag.p, P->val.p, P->dinv.p, P->pcg.p);
     int rc = XFK_OK;
@@ -1436,7 +1444,9 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
             return kRetryF64;
         // the stale-hierarchy projection: the rate from er = 1 at iteration 0
         double rate = (S.iters > 0 && S.er > 0 && S.er < 1) ? std::log(S.er) / (double)S.iters : 0.0;
-        long long rem = rate < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / rate) : 2 * batch;
+        // (the stop level: Precision, or the inexact pass's fraction of er0)
+        const double tol_eff = std::max(S.tol, S.tol_rel * S.er0);
+        long long rem = rate < 0 ? (long long)std::ceil(std::log(tol_eff / S.er) / rate) : 2 * batch;
         // (S and the counts are the same on every rank: collective-safe)
         if (stale > 0 && (S.iters >= stale || S.iters + rem > stale)) return kRetryFresh;
         // the next batch: the iterations left at the rate observed since the
@@ -1451,7 +1461,7 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
             it0 = S.iters;
             er0 = S.er;
         }
-        const long long nb = r2 < 0 ? (long long)std::ceil(std::log(S.tol / S.er) / r2) : 2 * batch;
+        const long long nb = r2 < 0 ? (long long)std::ceil(std::log(tol_eff / S.er) / r2) : 2 * batch;
         batch = (int)std::max<long long>(1, std::min<long long>(nb, 512));
         // (Jacobi: ~25 us iterations -- padded, at least 8 per poll)
         if (P->pc_used != XFK_PRECOND_AMG) batch = (int)std::max<long long>(8, std::min<long long>(rem + 2, 512));
@@ -1524,6 +1534,50 @@ int xfk_alloc_stats(double *out4, int reset)
     out4[2] = (double)g_nfree.load();
     out4[3] = 1e-6 * (double)g_nsfree.load();
     if (reset) g_nmalloc = g_nfree = g_nsmalloc = g_nsfree = g_npool = 0;
+    return XFK_OK;
+}
+
+int xfk_sort_elements(int n_elems, const unsigned *score, int device, int *perm)
+{
+    XFK_REQUIRE(n_elems >= 0 && (n_elems == 0 || (score && perm)), XFK_ERR_ARG, "xfk_sort_elements: bad arguments");
+    if (n_elems <= 1) {
+        if (n_elems == 1) perm[0] = 0;
+        return XFK_OK;
+    }
+    XFK_CHECK(hipSetDevice(device));
+    struct Scratch {   // device blocks back to the process cache once the stream is idle
+        hipStream_t s = nullptr;
+        std::vector<void *> blocks;
+        ~Scratch()
+        {
+            if (s) (void)hipStreamSynchronize(s);
+            PoolRelease pr;
+            for (void *b : blocks) dev_free(b);
+            if (s) stream_release(s);
+        }
+        void *get(size_t bytes)
+        {
+            void *q = nullptr;
+            if (dev_malloc(&q, bytes) != hipSuccess) return nullptr;
+            blocks.push_back(q);
+            return q;
+        }
+    } sc;
+    XFK_CHECK(stream_acquire(&sc.s));
+    const size_t n = (size_t)n_elems, nred = 2 * n + 64;
+    auto *key = static_cast<unsigned long long *>(sc.get(8 * n));
+    auto *tmp = static_cast<unsigned long long *>(sc.get(8 * n));
+    auto *red = static_cast<unsigned long long *>(sc.get(8 * nred));
+    auto *cin = static_cast<unsigned long long *>(sc.get(8 * nred));
+    auto *sd = static_cast<unsigned *>(sc.get(4 * n));
+    auto *flag = static_cast<int *>(sc.get(2 * sizeof(int)));
+    XFK_REQUIRE(key && tmp && red && cin && sd && flag, XFK_ERR_HIP, "xfk_sort_elements: device allocation failed");
+    XFK_CHECK(hipMemcpyAsync(sd, score, 4 * n, hipMemcpyHostToDevice, sc.s));
+    const int rc = sort_elements_device(sc.s, n_elems, sd, reinterpret_cast<int *>(sd), key, tmp, red, cin, flag,
+                                        nullptr);
+    if (rc != XFK_OK) return rc;
+    XFK_CHECK(hipMemcpyAsync(perm, sd, 4 * n, hipMemcpyDeviceToHost, sc.s));
+    XFK_CHECK(hipStreamSynchronize(sc.s));
     return XFK_OK;
 }
 
@@ -2371,6 +2425,8 @@ static int static2d_run(xfk_problem *P, int flags, xfk_result *res)
     int rc = XFK_OK;
     float ms = 0;
     if (P->comm && (rc = P->comm->solve_boundary()) != XFK_OK) return rc;
+    P->pcg_tol = 0;
+    P->pcg_tol_rel = 0;
     P->time_spmv = (flags & XFK_TIME_SPMV) != 0;
     P->spmv_used = 0;
     if (P->amg) {
@@ -2402,7 +2458,28 @@ static int static2d_run(xfk_problem *P, int flags, xfk_result *res)
     const long long cap = std::max<long long>(100000, 20LL * N);
     P->amg_reusable = false;   // a hierarchy is reused only inside one solve
     P->pc_used = XFK_PRECOND_JACOBI;
+    // inexact Newton (XFK_OPT_NEWTON_INEXACT): the pass's PCG tolerance from
+    // the last Newton change (Eisenstat-Walker forcing term eta |dV|/|V|);
+    // the first pass of a nonlinear problem at 1e-4 (its answer moves by
+    // O(1) in the next); a pass solved looser than Precision never ends the
+    // loop -- the next one runs at Precision
+    const bool inexact = !LinearFlag && (P->newton_inexact >= 0 ? P->newton_inexact == 1 : newton_inexact_env());
+    // pass 0 (from V = 0, the initial permeabilities): to kTolFirst of |b|;
+    // later passes while the Newton change is above kExactBelow: until the
+    // linear residual fell by kEta from its start (Eisenstat-Walker's
+    // ||r|| <= eta ||F(x_k)||, the warm start's residual being F(x_k));
+    // then every pass to Precision
+    constexpr double kEta = 0.05, kTolFirst = 1e-4, kExactBelow = 1e-3;
+    double pass_tol = P->precision, pass_rel = 0.0;
     for (;;) {
+        if (inexact) {
+            pass_tol = P->precision;
+            pass_rel = 0.0;
+            if (Iter == 0) pass_tol = std::max(kTolFirst, P->precision);
+            else if (resn >= kExactBelow) pass_rel = kEta;
+        }
+        P->pcg_tol = pass_tol;
+        P->pcg_tol_rel = pass_rel;
         XFK_CHECK(hipEventRecord(e0, s));
         if (Iter > 0 && (rc = exchange(P, P->V.p)) != XFK_OK) return rc;   // halo of V for the element B
         rc = assemble(P, Iter);
@@ -2447,10 +2524,10 @@ static int static2d_run(xfk_problem *P, int flags, xfk_result *res)
                 launch_relax(s, N, Relax, P->V.p, P->Vold.p);
             }
         }
-        if ((resn < 100. * P->precision) && (Iter > 0)) LinearFlag = true;
+        if ((resn < 100. * P->precision) && (Iter > 0) && pass_tol <= P->precision && pass_rel == 0.0) LinearFlag = true;
         if (trace_newton())   // lab: one line per Newton pass
-            std::fprintf(stderr, "[newton] pass %d: pcg %lld (%lld before a restart; %s%s, levels %d) res %.3e relax %.3f\n",
-                         Iter, (long long)P->pcg_host->iters, P->pcg_discarded,
+            std::fprintf(stderr, "[newton] pass %d (tol %.1e rel %.2g): pcg %lld (%lld before a restart; %s%s, levels %d) res %.3e relax %.3f\n",
+                         Iter, pass_tol, pass_rel, (long long)P->pcg_host->iters, P->pcg_discarded,
                          P->pc_used == XFK_PRECOND_AMG ? "amg" : "jacobi",
                          P->pc_used == XFK_PRECOND_AMG ? (P->amg_fresh ? " fresh" : " reused") : "",
                          (P->pc_used == XFK_PRECOND_AMG && P->amg) ? P->amg->stats.levels : 0, resn, Relax);
@@ -2461,6 +2538,8 @@ static int static2d_run(xfk_problem *P, int flags, xfk_result *res)
             return XFK_ERR_NOCONV;
         }
     }
+    P->pcg_tol = 0;
+    P->pcg_tol_rel = 0;
     XFK_CHECK(hipStreamSynchronize(s));
     XFK_CHECK(hipEventElapsedTime(&ms, es0, es1));
     R.ms_symbolic = ms;
@@ -2644,6 +2723,10 @@ int xfk_set_option(xfk_problem *P, int option, double value)
     case XFK_OPT_AMG_F32:
         XFK_REQUIRE(value == 0 || value == 1, XFK_ERR_ARG, "AMG f32 level-0 operators is 0 or 1");
         P->amg_f32 = (int)value;
+        return XFK_OK;
+    case XFK_OPT_NEWTON_INEXACT:
+        XFK_REQUIRE(value == 0 || value == 1, XFK_ERR_ARG, "inexact Newton is 0 or 1");
+        P->newton_inexact = (int)value;
         return XFK_OK;
     case XFK_OPT_AMG_WLEVEL:
         XFK_REQUIRE(value >= -2 && value < kAmgMaxLevels && value == (int)value, XFK_ERR_ARG,

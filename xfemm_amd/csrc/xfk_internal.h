@@ -128,6 +128,8 @@ struct CgState {
     double alp[2];    // alpha_i
     double er;        // sqrt(gamma_i / res_o)
     double tol;
+    double tol_rel;   // inexact Newton passes: stop also at er <= tol_rel er0 (0: off)
+    double er0;       // er of iteration 0
     int done;
     int singular;
     long long iters;
@@ -280,7 +282,12 @@ void host_par_for(long long n, long long min_per_thread, F f)
 // streams here when it is destroyed and the next problem takes them back.
 hipError_t stream_acquire(hipStream_t *s);
 void stream_release(hipStream_t s);   // idle streams only (the caller synchronised it)
-void stream_pool_drain();             // destroy the idle pooled streams (xfk_release_cache)
+void stream_pool_drain();
+// xfk_sort.hip: the reference's comb sort of the element scores on the device
+// (perm_dev may alias score_dev: the scores are read first)
+int sort_elements_device(hipStream_t s, int n, const unsigned *score_dev, int *perm_dev, unsigned long long *key,
+                         unsigned long long *tmp, unsigned long long *red, unsigned long long *cin, int *flag,
+                         int *passes);             // destroy the idle pooled streams (xfk_release_cache)
 long long stream_pool_idle();
 struct SideStream {
     hipStream_t cs = nullptr;
@@ -460,6 +467,9 @@ struct xfk_problem {
     int amg_col16 = -1;               // XFK_OPT_AMG_COL16 (-1: on unless XFK_NO_COL16)
     int amg_wlevel = -2;              // XFK_OPT_AMG_WLEVEL (-2: the default level)
     int amg_f32 = -1;                 // XFK_OPT_AMG_F32 (-1: on unless XFK_AMG_F32=0)
+    int newton_inexact = -1;          // XFK_OPT_NEWTON_INEXACT (-1: on unless XFK_NEWTON_INEXACT=0)
+    double pcg_tol = 0;               // PCG stopping tolerance of the running pass (0: precision)
+    double pcg_tol_rel = 0;           // ... and its relative stop (er <= tol_rel er0; 0: none)
     bool f64_fallback = false;        // a stagnating PCG switched the f32 parts of the AMG to f64 (sticky)
     long long pcg_discarded = 0;     // PCG iterations of this solve spent before a restart (stale hierarchy / f64)
     int amg_reuse = 1;

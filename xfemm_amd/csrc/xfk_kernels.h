@@ -65,7 +65,7 @@ void launch_cg_spmv(hipStream_t s, int N, const int *rowptr, const int *col, con
                     double *part_gam = nullptr, const int *tiles = nullptr, int ntiles = 0,
                     const unsigned short *c16 = nullptr, const int *cbase = nullptr);
 void launch_cg_dot(hipStream_t s, int N, const double *a, const double *b, double *part);
-void launch_cg_state_init(hipStream_t s, CgState *S, double tol);
+void launch_cg_state_init(hipStream_t s, CgState *S, double tol, double tol_rel = 0.0);
 
 void launch_count_incidence(hipStream_t s, int NE, const int *p, int *deg);
 void launch_fill_n2e(hipStream_t s, int NE, const int *p, const int *ptr, int *cursor, int *n2e);

@@ -176,9 +176,14 @@ __global__ void __launch_bounds__(kAxBlock) k_cg_axpy(CgAxpyArgs A)
         alpha = gam / (del - beta * gam / ap);
     }
     const double er = (res_o == 0.0) ? 0.0 : sqrt(gam / res_o);
-    const bool stop = (res_o == 0.0) || (A.it >= 1 && er <= S->tol);   // spars.cpp:259, 313
+    // spars.cpp:259, 313; an inexact Newton pass also stops once the residual
+    // ratio fell by tol_rel from its iteration-0 value
+    const bool stop = (res_o == 0.0) || (A.it >= 1 && (er <= S->tol || er <= S->tol_rel * S->er0));
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (A.it == 0) S->res_o = res_o;
+        if (A.it == 0) {
+            S->res_o = res_o;
+            S->er0 = er;
+        }
         S->er = er;
         S->iters = A.it;
         if (stop) S->done = 1;
@@ -252,16 +257,20 @@ __global__ void __launch_bounds__(kAxBlock) k_cg_axpy(CgAxpyArgs A)
 }
 
 // the PCG state of a new solve (one launch instead of a host -> device copy)
-__global__ void k_cg_state_init(CgState *S, double tol)
+__global__ void k_cg_state_init(CgState *S, double tol, double tol_rel)
 {
     if (threadIdx.x == 0) {
         CgState z{};
         z.tol = tol;
+        z.tol_rel = tol_rel;
         *S = z;
     }
 }
 
-void launch_cg_state_init(hipStream_t s, CgState *S, double tol) { k_cg_state_init<<<1, 64, 0, s>>>(S, tol); }
+void launch_cg_state_init(hipStream_t s, CgState *S, double tol, double tol_rel)
+{
+    k_cg_state_init<<<1, 64, 0, s>>>(S, tol, tol_rel);
+}
 
 int cg_grid(int N) { return (N + kCgBlock - 1) / kCgBlock; }
 int cg_axpy_grid(int N)

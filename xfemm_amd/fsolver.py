@@ -29,6 +29,7 @@ EXPORTED = (
     "xfemm_fsolver_set_previous_solution_file", "xfemm_fsolver_previous_solution_file", "xfemm_fsolver_ac_solver",
     "xfemm_fsolver_frequency", "xfemm_fsolver_num_line_props", "xfemm_fsolver_num_node_props",
     "xfemm_fsolver_num_block_props", "xfemm_fsolver_num_circ_props", "xfemm_fsolver_num_block_labels",
+    "xfemm_fsolver_set_comm",
 )
 
 _lib = None
@@ -51,6 +52,7 @@ def load_library(path: str = FSOLVER_SO):
     L.xfemm_fsolver_set_pathname.argtypes = [vp, C.c_char_p]
     L.xfemm_fsolver_set_device.argtypes = [vp, C.c_int]
     L.xfemm_fsolver_set_delete_mesh_files.argtypes = [vp, C.c_int]
+    L.xfemm_fsolver_set_comm.argtypes = [vp, vp]
     for nm in ("xfemm_fsolver_load_problem_file", "xfemm_fsolver_load_mesh", "xfemm_fsolver_cuthill",
                "xfemm_fsolver_num_nodes", "xfemm_fsolver_num_elements", "xfemm_fsolver_num_pbcs",
                "xfemm_fsolver_bandwidth"):
@@ -115,12 +117,22 @@ def bh_get_slopes_ac(B, H, omega, lam_type=0, lam_fill=1.0, theta_hn=0.0, lam_d=
 class FSolver:
     """The reference FSolver workflow over the MI355X hot path."""
 
-    def __init__(self, device: int = 0, delete_mesh_files: bool = True):
+    def __init__(self, device: int = 0, delete_mesh_files: bool = True, comm=None):
         L = load_library()
         self._h = C.c_void_p(L.xfemm_fsolver_create())
         L.xfemm_fsolver_set_device(self._h, device)
         L.xfemm_fsolver_set_delete_mesh_files(self._h, int(delete_mesh_files))
         self._path = ""
+        self._comm = None
+        if comm is not None:
+            self.set_comm(comm)
+
+    def set_comm(self, comm):
+        """Shard the solve over comm's ranks (xfemm_fsolver_set_comm; a
+        kernels.Comm kept alive by this object): every rank runs its own
+        FSolver on the same files, rank 0 writes the .ans."""
+        self._comm = comm
+        _lib.xfemm_fsolver_set_comm(self._h, comm._h if comm is not None else None)
 
     def __del__(self):
         try:

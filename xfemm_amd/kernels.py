@@ -37,6 +37,7 @@ XFK_OPT_AMG_FOLD = 8
 XFK_OPT_AMG_COL16 = 9
 XFK_OPT_AMG_WLEVEL = 10
 XFK_OPT_AMG_F32 = 11
+XFK_OPT_NEWTON_INEXACT = 12
 
 # every symbol include/xfemm_kernels.h declares
 EXPORTED = (
@@ -51,7 +52,7 @@ EXPORTED = (
     "xfk_comm_unique_id", "xfk_comm_create_rccl", "xfk_comm_create_local", "xfk_comm_destroy",
     "xfk_comm_rank", "xfk_comm_size", "xfk_comm_record", "xfk_comm_log", "xfk_comm_create_replay",
     "xfk_partition_plan", "xfk_partition_plan_coupled", "xfk_problem_create_dist", "xfk_dist_get_info",
-    "xfk_magdir_eval",
+    "xfk_magdir_eval", "xfk_sort_elements",
 )
 
 
@@ -191,6 +192,7 @@ def load_library(path: str = KERNELS_SO):
                                              C.POINTER(DistInfo), iptr, iptr, iptr, iptr]
     L.xfk_problem_create_dist.argtypes = [C.POINTER(ProblemDesc), C.c_int, vp, C.POINTER(vp)]
     L.xfk_dist_get_info.argtypes = [vp, C.POINTER(DistInfo)]
+    L.xfk_sort_elements.argtypes = [C.c_int, C.POINTER(C.c_uint), C.c_int, iptr]
     L.xfk_magdir_eval.argtypes = [C.c_char_p, C.c_int, iptr, dptr, dptr, C.c_int, C.c_double, dptr]
     _lib = L
     return L
@@ -220,6 +222,16 @@ def cache_stats() -> dict:
 def release_cache():
     """Give the process-wide caches back to HIP (xfk_release_cache)."""
     _check(load_library().xfk_release_cache())
+
+
+def sort_elements(score, device: int = 0) -> np.ndarray:
+    """FEASolver::SortElements' comb sort of element scores on the device
+    (xfk_sort_elements): the permutation (position -> element)."""
+    sc = np.ascontiguousarray(score, dtype=np.uint32)
+    perm = np.empty(len(sc), dtype=np.int32)
+    _check(load_library().xfk_sort_elements(len(sc), sc.ctypes.data_as(C.POINTER(C.c_uint)), device,
+                                            perm.ctypes.data_as(iptr)))
+    return perm
 
 
 def device_count() -> int:
@@ -357,8 +369,11 @@ class Static2DProblem:
                  ext_zo: float = 0.0, ext_ro: float = 0.0, ext_ri: float = 0.0, amg_dense: Optional[int] = None,
                  ages: Sequence[dict] = (), ac_solver: int = 0, amg_fold: Optional[bool] = None,
                  amg_col16: Optional[bool] = None, amg_wlevel: Optional[int] = None,
-                 amg_f32: Optional[bool] = None):
+                 amg_f32: Optional[bool] = None, newton_inexact: Optional[bool] = None):
         """ac_solver: [ACSolver], read by the harmonic solvers only (ignored here).
+        newton_inexact: nonlinear passes before the last solved to a forcing
+        tolerance (default on; False: every pass to Precision, as the
+        reference; XFK_OPT_NEWTON_INEXACT).
         amg_fold: folded V(1,1) levels (default on; False: the plain cycle).
         amg_col16: 16-bit tile column offsets on level 0 (default on; False:
         int columns; the same bits either way).
@@ -408,6 +423,8 @@ class Static2DProblem:
             self.set_option(XFK_OPT_AMG_F32, int(bool(amg_f32)))
         if amg_wlevel is not None:
             self.set_option(XFK_OPT_AMG_WLEVEL, int(amg_wlevel))
+        if newton_inexact is not None:
+            self.set_option(XFK_OPT_NEWTON_INEXACT, int(bool(newton_inexact)))
         self.n_rows = self.dist_info()["n_own"] if comm is not None else self.n_nodes
         self.result: Optional[Result] = None
 
