@@ -1548,7 +1548,7 @@ inline char *put_i(char *p, int v) { return std::to_chars(p, p + 16, v).ptr; }
 template <class F>
 FSolver::Formatted format_lines(int n, int max_line, F line)
 {
-    const int T = (int)std::max(1, std::min<int>(HostPool::get().size(), n / 65536));
+    const int T = (int)std::max(1, std::min<int>(HostPool::get().size(), n / 8192));
     FSolver::Formatted f;
     f.buf.resize(T);
     f.len.assign(T, 0);

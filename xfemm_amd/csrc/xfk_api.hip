@@ -20,6 +20,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <iterator>
 #include <set>
 #include <type_traits>
 #include <unordered_map>
@@ -373,11 +374,21 @@ static Terms lin2(double a, const Terms &x, double b, const Terms &y)
 // post-Dirichlet values; sets of rows k are structural supersets of the
 // reference's value-based scan, which is exact because averaging zeros gives
 // zero.
+// small sorted neighbour sets (a node has ~6-20 neighbours): sorted vectors
+using NbSet = std::vector<int>;
+static inline void nb_insert(NbSet &v, int x)
+{
+    auto it = std::lower_bound(v.begin(), v.end(), x);
+    if (it == v.end() || *it != x) v.insert(it, x);
+}
+static inline bool nb_has(const NbSet &v, int x) { return std::binary_search(v.begin(), v.end(), x); }
+
 static int build_pbc_map(xfk_problem *P, bool aux)
 {
     const int npbc = (int)P->hpbc.size() / 3;
     if (npbc == 0) return XFK_OK;
-    std::unordered_map<int, std::set<int>> N0;  // original neighbours of pbc nodes
+    std::unordered_map<int, NbSet> N0;  // original neighbours of pbc nodes
+    N0.reserve(2 * (size_t)npbc);
     std::vector<char> ispbc(std::max(1, P->NL), 0);
     for (int k = 0; k < npbc; ++k)
         for (int m = 0; m < 2; ++m) {
@@ -391,34 +402,39 @@ static int build_pbc_map(xfk_problem *P, bool aux)
             if (v < 0 || v >= P->NL || !ispbc[v]) continue;
             auto it = N0.find(v);
             for (int m = 0; m < 3; ++m)
-                if (m != j) it->second.insert(P->hp[3 * e + m]);
+                if (m != j) nb_insert(it->second, P->hp[3 * e + m]);
         }
     for (long long k : P->age_key) {   // air-gap couplings are entries of the matrix too
         const int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
         if (r == c) continue;
         auto it = N0.find(r);
-        if (it != N0.end()) it->second.insert(c);
+        if (it != N0.end()) nb_insert(it->second, c);
         it = N0.find(c);
-        if (it != N0.end()) it->second.insert(r);
+        if (it != N0.end()) nb_insert(it->second, r);
     }
-    std::unordered_map<int, std::set<int>> Ncur = N0;
+    std::unordered_map<int, NbSet> Ncur = N0;
     std::unordered_map<long long, Terms> E;
+    E.reserve(16 * (size_t)npbc);
     std::unordered_map<int, Terms> Eb;
+    Eb.reserve(2 * (size_t)npbc);
     std::set<long long> fill;
     auto is_orig = [&](int r, int c) -> bool {
         if (r == c) return true;
         auto it = N0.find(r);
-        if (it != N0.end()) return it->second.count(c) > 0;
+        if (it != N0.end()) return nb_has(it->second, c);
         it = N0.find(c);
-        if (it != N0.end()) return it->second.count(r) > 0;
+        if (it != N0.end()) return nb_has(it->second, r);
         return false;
     };
-    auto get = [&](int r, int c) -> Terms {
-        long long k = ukey(r, c);
+    // the current combination of entry (r, c): the map's, else the entry itself
+    // (an original one) or nothing -- as a reference (tmp holds the implicit one)
+    auto get = [&](int r, int c, Terms &tmp) -> const Terms & {
+        const long long k = ukey(r, c);
         auto it = E.find(k);
         if (it != E.end()) return it->second;
-        if (is_orig(r, c)) return Terms{{k, 1.0}};
-        return Terms{};
+        tmp.clear();
+        if (is_orig(r, c)) tmp.push_back({k, 1.0});
+        return tmp;
     };
     // auxiliary matrices of the Newton AC solver: ordered entries
     std::unordered_map<long long, Terms> Ea;
@@ -435,6 +451,7 @@ static int build_pbc_map(xfk_problem *P, bool aux)
         if (it != Eb.end()) return it->second;
         return Terms{{(long long)i, 1.0}};
     };
+    Terms t1, t2;
     for (int q = 0; q < npbc; ++q) {
         int i = P->hpbc[3 * q], j = P->hpbc[3 * q + 1], t = P->hpbc[3 * q + 2];
         if (t != 0 && t != 1) continue;  // static2d.cpp:932-939 only handles 0 and 1
@@ -444,16 +461,21 @@ static int build_pbc_map(xfk_problem *P, bool aux)
         }
         if (j < i) std::swap(i, j);
         const double sg = (t == 0) ? 1.0 : -1.0;
-        std::set<int> K;
-        for (int k : Ncur[i]) K.insert(k);
-        for (int k : Ncur[j]) K.insert(k);
-        K.erase(i);
-        K.erase(j);
+        NbSet K;
+        {
+            const NbSet &a = Ncur[i], &b = Ncur[j];
+            std::set_union(a.begin(), a.end(), b.begin(), b.end(), std::back_inserter(K));
+            K.erase(std::remove_if(K.begin(), K.end(), [&](int x) { return x == i || x == j; }), K.end());
+        }
         for (int k : K) {
-            Terms v1 = get(k, i), v2 = get(k, j);
-            Terms c = lin2(0.5, v1, 0.5 * sg, v2);
-            E[ukey(k, i)] = c;
-            E[ukey(k, j)] = (sg > 0) ? c : lin2(-1.0, c, 0.0, Terms{});
+            Terms c = lin2(0.5, get(k, i, t1), 0.5 * sg, get(k, j, t2));
+            if (sg > 0) {
+                E[ukey(k, j)] = c;
+            } else {
+                Terms cn = lin2(-1.0, c, 0.0, Terms{});
+                E[ukey(k, j)] = std::move(cn);
+            }
+            E[ukey(k, i)] = std::move(c);
             if (aux) {   // row k and, by the Hermitian / anti-Hermitian flip of Put, column k
                 Terms ca = lin2(0.5, geta(k, i), 0.5 * sg, geta(k, j));
                 Terms ct = lin2(0.5, geta(i, k), 0.5 * sg, geta(j, k));
@@ -464,17 +486,17 @@ static int build_pbc_map(xfk_problem *P, bool aux)
             }
             for (int m : {i, j})
                 if (!is_orig(k, m)) fill.insert(ukey(k, m));
-            Ncur[i].insert(k);
-            Ncur[j].insert(k);
+            nb_insert(Ncur[i], k);
+            nb_insert(Ncur[j], k);
             auto itk = Ncur.find(k);
             if (itk != Ncur.end()) {
-                itk->second.insert(i);
-                itk->second.insert(j);
+                nb_insert(itk->second, i);
+                nb_insert(itk->second, j);
             }
         }
-        Terms d = lin2(0.5, get(i, i), 0.5, get(j, j));
+        Terms d = lin2(0.5, get(i, i, t1), 0.5, get(j, j, t2));
         E[ukey(i, i)] = d;
-        E[ukey(j, j)] = d;
+        E[ukey(j, j)] = std::move(d);
         if (aux) {   // auxiliary (i, j) block: c = (ii +- ij +- ji + jj) / 4 at ii, jj and +-c at ij, ji
             Terms da = lin2(0.25, lin2(1.0, geta(i, i), sg, geta(i, j)), 0.25, lin2(sg, geta(j, i), 1.0, geta(j, j)));
             Ea[okey(i, i)] = da;
@@ -2202,8 +2224,12 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     tr.mark("  local mesh + BC arrays");
     int rc = build_pbc_map(P, G.pbc_aux);
     if (rc != XFK_OK) return fail(rc);
+    tr.mark("  periodic map");
+    if (tr.on)
+        std::fprintf(stderr, "[create]     %zu pairs, %zu entries, %zu fill, %zu age couplings\n", P->hpbc.size() / 3,
+                     P->pbc_entry_key.size(), P->pbc_fill.size(), P->age_key.size());
     add_age_fill(P);
-    tr.mark("  periodic map + air-gap fill");
+    tr.mark("  air-gap fill");
 
     hipStream_t s = P->stream;
     hipError_t e = hipSuccess;
