@@ -36,7 +36,8 @@ Output: one JSON line (rank 0) with
   secondary      configs[3] (nonlinear M-19, Newton loop) and configs[4] on
                  one GPU (20M triangles, 10.0M DoF);
   cold_first_solve  the first solve of a fresh problem object (no capacity or
-                 round-count hints from an earlier setup);
+                 round-count hints from an earlier setup), and the next fresh
+                 problem of the process (hints of the previous one, checked);
   fsolver_end_to_end  the product path: FSolver .fem -> .ans wall time on
                  configs[1] and configs[2], split into LoadMesh / Cuthill /
                  create / solve / write.
@@ -363,13 +364,17 @@ def cold_first_solve(device, args, kw):
                 "hip_malloc_create": a_create["n_malloc"], "hip_malloc_first_solve": a_solve["n_malloc"],
                 "ms_hip_malloc_first_solve": a_solve["ms_malloc"]}
 
+    kernels.forget_amg_hints()
     first = one()
-    first["note"] = ("fresh problem object, first solve (no re-solve hints, no device blocks of a destroyed "
-                     "problem to reuse: the bench's own problem is still alive); ms_create_upload = host -> HBM "
-                     "upload of the mesh and tables (outside the step)")
+    first["note"] = ("fresh problem object, first solve (no re-solve hints, the process's AMG hints dropped "
+                     "(xfk_amg_forget_hints), no device blocks of a destroyed problem to reuse: the bench's own "
+                     "problem is still alive); ms_create_upload = host -> HBM upload of the mesh and tables "
+                     "(outside the step)")
     second = one()
     second["note"] = ("the next fresh problem of the same process (a session's next analysis, the next rotor "
-                      "angle): the previous one was destroyed, its device blocks come from the process cache")
+                      "angle): the previous one was destroyed, its device blocks come from the process cache, "
+                      "its AMG setup left capacities / MIS rounds / the coarsest plan for a problem of its size, "
+                      "taken as speculation checked on the device")
     first["next_problem_in_process"] = second
     return first
 

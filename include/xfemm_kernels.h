@@ -479,6 +479,17 @@ int xfk_problem_memory(const xfk_problem *prob, long long *out4);
 int xfk_cache_stats(long long *out3);
 int xfk_release_cache(void);
 
+/* AMG hints across problems (no reference counterpart: the reference rebuilds
+ * nothing on the device).  The last single-device AMG setup of the process
+ * leaves its SpGEMM slot capacities, MIS-2 round counts and coarsest
+ * nested-dissection plan behind, keyed by the fine level's rows and nonzeros;
+ * the next fresh problem of that size takes them as speculation checked on
+ * the device (a capacity must be the class a measurement would pick, the plan
+ * must match the coarsest pattern -- else that part is measured and redone),
+ * so answers are bit-identical with or without them.  xfk_amg_forget_hints
+ * drops them (XFK_AMG_NO_FOREIGN=1 never keeps any). */
+int xfk_amg_forget_hints(void);
+
 /* FEASolver::SortElements (cfemm/libfemm/cuthill.cpp:39-86; called from
  * FSolver::Cuthill) on the device: the reference's comb sort -- gap * 10 / 13
  * (9, 10 -> 11), swap on a strictly greater score, stop after the first pass

@@ -44,6 +44,7 @@ namespace xfk {
 constexpr int kAmgDenseMax = 2048;    // coarsest level solved by its dense inverse (blocked Gauss-Jordan)
 constexpr int kAmgMaxLevels = 16;
 constexpr int kAmgDeferSlots = 64;    // deferred SpGEMM (overflow flag, length) pairs per setup
+constexpr int kAmgDeferTotal = kAmgDeferSlots + kAmgDeferSlots / 2;   // + a class-check flag per pair
 
 struct AmgLevel {
     int n = 0;                        // rows
@@ -161,6 +162,12 @@ struct Amg {
     int *def_host = nullptr;          // pinned mirror
     int def_n = 0;
     long long *def_target[kAmgDeferSlots / 2] = {};
+    int def_verify[kAmgDeferSlots / 2] = {};   // capacity whose class the device checks (0: none)
+    bool foreign = false;
+    std::vector<char> nd_plan;        // host copy of the plan's device arrays (for the hint store)
+    size_t nd_tl_n = 0, nd_mask_n = 0;             // the capacity hints came from another problem (load_hints)
+    int load_hints(hipStream_t s, int n0, long long nnz0);
+    void save_hints(int n0, long long nnz0);
     int *host_int = nullptr;          // pinned mirror (16 ints; 8..10: the aggregation's packed check)
     hipEvent_t ev_host = nullptr;     // host waits for a check while later setup work runs
     DBuf<int> mis_out;                // packed aggregation check

@@ -1052,7 +1052,8 @@ __device__ __forceinline__ void wave_lds_sync()
 // moves it to its CSR place after the length scan.
 template <bool PMODE, int G, int CAP>
 __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int *__restrict__ cnt_out,
-                                                    int *__restrict__ pcol, double *__restrict__ pval, int *ovf)
+                                                    int *__restrict__ pcol, double *__restrict__ pval, int *ovf,
+                                                    int *need = nullptr)
 {
     constexpr int W = 64 / G;
     constexpr int S = CAP / G;
@@ -1133,6 +1134,10 @@ __global__ void __launch_bounds__(64) k_spgemm_sort(int nrows, SgX X, SgY Y, int
             }
             np += total;
         }
+        // a capacity taken from another problem (need != null): some row must
+        // need more than half of it, else a measurement would have taken a
+        // smaller class (whose sort order -- and so whose bits -- differ)
+        if (need && np > CAP / 2 && l == 0 && *(volatile int *)need == 0) *need = 1;
         // more products than slots (a capacity taken from an earlier setup):
         // the row is garbage, the host redoes the product with a measured capacity
         if (np > CAP) {
@@ -2711,22 +2716,22 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     // compaction; returns the overflow flag (rows with more products than
     // slots), read back with the scan's own synchronisation
     int *sovf = M.dev_int.p + 6;
-    auto launch_sort = [&](int cap, int *ovf) {
+    auto launch_sort = [&](int cap, int *ovf, int *need = nullptr) {
         int *pc = M.pad_col.p;
         double *pv = M.pad_val.p;
         if (nrows > 0) {
             // few lanes per row, 4-8 sorted slots per lane: many rows per
             // wavefront to overlap their dependent gathers
             if (cap == 16)
-                k_spgemm_sort<PMODE, 4, 16><<<(nrows + 15) / 16, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
+                k_spgemm_sort<PMODE, 4, 16><<<(nrows + 15) / 16, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, need);
             else if (cap == 32)
-                k_spgemm_sort<PMODE, 8, 32><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
+                k_spgemm_sort<PMODE, 8, 32><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, need);
             else if (cap == 64)
-                k_spgemm_sort<PMODE, 8, 64><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
+                k_spgemm_sort<PMODE, 8, 64><<<(nrows + 7) / 8, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, need);
             else if (cap == 128)
-                k_spgemm_sort<PMODE, 16, 128><<<(nrows + 3) / 4, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
+                k_spgemm_sort<PMODE, 16, 128><<<(nrows + 3) / 4, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, need);
             else
-                k_spgemm_sort<PMODE, 32, 256><<<(nrows + 1) / 2, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf);
+                k_spgemm_sort<PMODE, 32, 256><<<(nrows + 1) / 2, 64, 0, s>>>(nrows, X, Y, M.cnt.p, pc, pv, ovf, need);
         }
     };
     // single pass into padded rows of `cap` slots (sort-based), then scan +
@@ -2754,13 +2759,16 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     // nrows x cap, its length and the kernel's overflow flag land in a
     // deferred slot that the setup reads once at its end (an overflow there
     // rebuilds the hierarchy with measured capacities)
-    auto deferred_pass = [&](int cap) -> int {
+    auto deferred_pass = [&](int cap, bool verify = false) -> int {
         int *slot = M.def_dev.p + M.def_n;
+        // (a capacity from another problem: its class is checked on the device)
+        int *need = (verify && cap > 16) ? M.def_dev.p + kAmgDeferSlots + M.def_n / 2 : nullptr;
+        M.def_verify[M.def_n / 2] = need ? cap : 0;
         AMG_CHECK(M.pad_col.alloc((size_t)nrows * cap));
         AMG_CHECK(M.pad_val.alloc((size_t)nrows * cap));
         AMG_CHECK(ccol.alloc((size_t)std::max(1LL, (long long)nrows * cap)));
         AMG_CHECK(cval.alloc((size_t)std::max(1LL, (long long)nrows * cap)));
-        launch_sort(cap, slot);
+        launch_sort(cap, slot, need);
         int rc = scan_only(M, s, M.cnt.p, crow.p, nrows);
         if (rc != XFK_OK) return rc;
         if (nrows > 0)
@@ -2775,7 +2783,13 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     if (key >= 0) {
         auto hint = M.cap_hint.find(key);
         if (hint != M.cap_hint.end()) {
-            if (M.def_n + 2 <= kAmgDeferSlots) return deferred_pass(hint->second);
+            if (M.def_n + 2 <= kAmgDeferSlots) return deferred_pass(hint->second, M.foreign);
+            if (M.foreign) {   // (no slot to check another problem's capacity in: measure)
+                M.cap_hint.erase(hint);
+                hint = M.cap_hint.end();
+            }
+        }
+        if (hint != M.cap_hint.end()) {
             bool overflow = false;
             int rc = sort_pass(hint->second, overflow);
             if (rc != XFK_OK || !overflow) return rc;
@@ -3222,7 +3236,7 @@ int Amg::resolve_deferred(hipStream_t s, bool &overflow)
 int Amg::fetch_deferred(hipStream_t s)
 {
     if (def_n == 0) return XFK_OK;
-    AMG_CHECK(hipMemcpyAsync(def_host, def_dev.p, sizeof(int) * def_n, hipMemcpyDeviceToHost, s));
+    AMG_CHECK(hipMemcpyAsync(def_host, def_dev.p, sizeof(int) * kAmgDeferTotal, hipMemcpyDeviceToHost, s));
     AMG_CHECK(hipEventRecord(ev_host, s));
     return XFK_OK;
 }
@@ -3234,10 +3248,12 @@ int Amg::wait_deferred(hipStream_t s, bool &overflow)
     AMG_CHECK(hipEventSynchronize(ev_host));
     for (int q = 0; q < def_n / 2; ++q) {
         if (def_host[2 * q]) overflow = true;
+        else if (def_verify[q] && !def_host[kAmgDeferSlots + q]) overflow = true;   // another class measured
         else *def_target[q] = def_host[2 * q + 1];
+        def_verify[q] = 0;
     }
     def_n = 0;
-    AMG_CHECK(hipMemsetAsync(def_dev.p, 0, sizeof(int) * kAmgDeferSlots, s));
+    AMG_CHECK(hipMemsetAsync(def_dev.p, 0, sizeof(int) * kAmgDeferTotal, s));
     return XFK_OK;
 }
 
@@ -3255,7 +3271,7 @@ int Amg::host_ints(int count)
 int Amg::reserve_host()
 {
     if (!host_int) AMG_CHECK(pinned_malloc((void **)&host_int, 16 * sizeof(int)));
-    if (!def_host) AMG_CHECK(pinned_malloc((void **)&def_host, kAmgDeferSlots * sizeof(int)));
+    if (!def_host) AMG_CHECK(pinned_malloc((void **)&def_host, kAmgDeferTotal * sizeof(int)));
     if (!ev_host) AMG_CHECK(hipEventCreateWithFlags(&ev_host, hipEventDisableTiming));
     constexpr int kHostBig = 64 << 10;   // ints: a coarsest pattern of ~1600 rows x 40
     if (host_big_n < kHostBig) {
@@ -3277,12 +3293,13 @@ int Amg::init(hipStream_t s)
 {
     if (!host_int) AMG_CHECK(pinned_malloc((void **)&host_int, 16 * sizeof(int)));
     if (!ev_host) AMG_CHECK(hipEventCreateWithFlags(&ev_host, hipEventDisableTiming));
-    if (!def_host) AMG_CHECK(pinned_malloc((void **)&def_host, kAmgDeferSlots * sizeof(int)));
+    if (!def_host) AMG_CHECK(pinned_malloc((void **)&def_host, kAmgDeferTotal * sizeof(int)));
     AMG_CHECK(dev_int.alloc(8));
-    AMG_CHECK(def_dev.alloc(kAmgDeferSlots));
+    AMG_CHECK(def_dev.alloc(kAmgDeferTotal));
     def_n = 0;
+    for (int &v : def_verify) v = 0;
     AMG_CHECK(rho.alloc(2 * kAmgMaxLevels));
-    k_setup_zero<<<1, 64, 0, s>>>(def_dev.p, kAmgDeferSlots, rho.p, 2 * kAmgMaxLevels);   // (one launch, not two fills)
+    k_setup_zero<<<1, 64, 0, s>>>(def_dev.p, kAmgDeferTotal, rho.p, 2 * kAmgMaxLevels);   // (one launch, not two fills)
     if (L.empty()) L.emplace_back(new AmgLevel());
     for (auto &lv : L) {   // levels are rebuilt: none sharded until setup_dist says so
         lv->dist = false;
@@ -3309,6 +3326,125 @@ int Amg::init(hipStream_t s)
 // setups changes the Galerkin products' summation order, so repeated solves
 // would no longer be bit-identical.  XFK_AMG_NO_SEED=1: measure everything.
 
+// Hints across problems.  A fresh problem has no hints of its own; the last
+// single-device setup of the process leaves its SpGEMM capacities, MIS-2
+// round counts and the coarsest nested-dissection plan here, keyed by the
+// fine level's size (the next rotor angle, the next analysis of a session:
+// the same mesh family).  A fresh hierarchy of the same size takes them as
+// speculation, checked on the device, never trusted: a capacity must show no
+// overflow AND some row needing more than half of it (else a measurement
+// would have chosen a smaller class, with another sort order: the setup is
+// redone with measured capacities, so the bits are always those of the
+// measured class); the round counts only size the MIS-2 batches; the plan is
+// used only if the coarsest pattern equals its key (k_pattern_diff).
+// XFK_AMG_NO_FOREIGN=1: fresh problems measure everything.
+namespace {
+struct HintStore {
+    std::mutex mu;
+    bool valid = false;
+    int n0 = 0;
+    long long nnz0 = 0;
+    std::map<int, int> cap, mis;
+    std::vector<int> nd_key;
+    std::vector<Amg::NdPhase> nd_phases;
+    int nd_ld = 0, nd_key_n = -1;
+    long long nd_key_nnz = 0;
+    std::vector<char> nd_plan;   // perm, iperm, tiles, masks as nd_order uploads them
+    size_t nd_tl_n = 0, nd_mask_n = 0;
+};
+HintStore &hint_store()
+{
+    static HintStore *h = new HintStore();   // (never destroyed, like the device caches)
+    return *h;
+}
+bool foreign_on()
+{
+    static const bool v = std::getenv("XFK_AMG_NO_FOREIGN") == nullptr;
+    return v;
+}
+}  // namespace
+
+}  // namespace xfk
+
+extern "C" int xfk_amg_forget_hints(void)
+{
+    xfk::HintStore &h = xfk::hint_store();
+    std::lock_guard<std::mutex> g(h.mu);
+    h.valid = false;
+    h.cap.clear();
+    h.mis.clear();
+    h.nd_key.clear();
+    h.nd_phases.clear();
+    h.nd_plan.clear();
+    h.nd_key_n = -1;
+    return XFK_OK;
+}
+
+namespace xfk {
+
+void Amg::save_hints(int n0, long long nnz0)
+{
+    if (!foreign_on() || cap_hint.empty()) return;
+    HintStore &h = hint_store();
+    std::lock_guard<std::mutex> g(h.mu);
+    h.valid = true;
+    h.n0 = n0;
+    h.nnz0 = nnz0;
+    h.cap = cap_hint;
+    // XFK_AMG_TEST_FOREIGN_BIG=1 (tests only): store one class too large, so
+    // the next problem's device check must refuse it and rebuild
+    if (std::getenv("XFK_AMG_TEST_FOREIGN_BIG"))
+        for (auto &c : h.cap) c.second = std::min(2 * c.second, (int)kSortCap);
+    h.mis = mis_hint;
+    h.nd_key = nd_key;
+    h.nd_phases = nd_phases_key;
+    h.nd_ld = nd_ld;
+    h.nd_key_n = nd_key_n;
+    h.nd_key_nnz = nd_key_nnz;
+    h.nd_plan = nd_plan;
+    h.nd_tl_n = nd_tl_n;
+    h.nd_mask_n = nd_mask_n;
+}
+
+int Amg::load_hints(hipStream_t s, int n0, long long nnz0)
+{
+    foreign = false;
+    if (!foreign_on() || !cap_hint.empty() || !mis_hint.empty()) return XFK_OK;
+    HintStore &h = hint_store();
+    std::lock_guard<std::mutex> g(h.mu);
+    if (!h.valid || h.n0 != n0 || h.nnz0 != nnz0) return XFK_OK;
+    cap_hint = h.cap;
+    mis_hint = h.mis;
+    foreign = true;
+    const size_t plan_bytes = sizeof(int) * ((size_t)h.nd_key_n + h.nd_ld + h.nd_tl_n) + h.nd_mask_n;
+    if (h.nd_key_n > 0 && !h.nd_key.empty() && !h.nd_phases.empty() && h.nd_plan.size() == plan_bytes) {
+        const int n = h.nd_key_n, ld = h.nd_ld;
+        AMG_CHECK(cinv_perm.alloc(n));
+        AMG_CHECK(cinv_iperm.alloc(ld));
+        AMG_CHECK(nd_mask.alloc(h.nd_mask_n));
+        AMG_CHECK(nd_tiles.alloc(h.nd_tl_n));
+        const char *q = h.nd_plan.data();
+        AMG_CHECK(hipMemcpyAsync(cinv_perm.p, q, sizeof(int) * n, hipMemcpyHostToDevice, s));
+        AMG_CHECK(hipMemcpyAsync(cinv_iperm.p, q + sizeof(int) * n, sizeof(int) * ld, hipMemcpyHostToDevice, s));
+        AMG_CHECK(hipMemcpyAsync(nd_tiles.p, q + sizeof(int) * ((size_t)n + ld), sizeof(int) * h.nd_tl_n,
+                                 hipMemcpyHostToDevice, s));
+        AMG_CHECK(hipMemcpyAsync(nd_mask.p, q + sizeof(int) * ((size_t)n + ld + h.nd_tl_n), h.nd_mask_n,
+                                 hipMemcpyHostToDevice, s));
+        nd_plan = h.nd_plan;
+        nd_tl_n = h.nd_tl_n;
+        nd_mask_n = h.nd_mask_n;
+        nd_key = h.nd_key;
+        nd_phases_key = h.nd_phases;
+        nd_ld = h.nd_ld;
+        nd_key_n = h.nd_key_n;
+        nd_key_nnz = h.nd_key_nnz;
+        AMG_CHECK(nd_key_dev.alloc(nd_key.size()));
+        AMG_CHECK(hipMemcpyAsync(nd_key_dev.p, nd_key.data(), sizeof(int) * nd_key.size(), hipMemcpyHostToDevice, s));
+        AMG_CHECK(hipStreamSynchronize(s));   // (the host vector is the staging buffer; a first setup only)
+    }
+    return XFK_OK;
+}
+
 void Amg::seed_hints()
 {
     static const bool off = std::getenv("XFK_AMG_NO_SEED") != nullptr;
@@ -3324,8 +3460,10 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
     dist = false;
     comm = nullptr;
     lrep = 0;
+    int rc = load_hints(s, n0, nnz0);
+    if (rc != XFK_OK) return rc;
     seed_hints();
-    int rc = init(s);
+    rc = init(s);
     if (rc != XFK_OK) return rc;
     AmgLevel &F = *L[0];
     F.n = n0;
@@ -3335,7 +3473,12 @@ int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *c
     F.rowptr = rowptr0;
     F.col = col0;
     F.val = val0;
-    return build(s, 0);
+    rc = build(s, 0);
+    if (rc == XFK_OK) {
+        foreign = false;   // (verified, or rebuilt with measured capacities)
+        save_hints(n0, nnz0);
+    }
+    return rc;
 }
 
 // MIS-2 aggregation of level l, P = (I - omega D_F^-1 A_F) P_tent and R = P^T
@@ -3772,6 +3915,11 @@ int Amg::nd_order(hipStream_t s, const AmgLevel &C, int &ld)
     std::memcpy(h + sizeof(int) * n, iperm.data(), sizeof(int) * ld);
     std::memcpy(h + sizeof(int) * ((size_t)n + ld), tl.data(), sizeof(int) * tl.size());
     std::memcpy(h + sizeof(int) * ((size_t)n + ld + tl.size()), mask.data(), mask.size());
+    if (foreign_on()) {   // (the plan's device arrays for the next fresh problem of this size)
+        nd_plan.assign(h, h + bytes);
+        nd_tl_n = tl.size();
+        nd_mask_n = mask.size();
+    }
     AMG_CHECK(hipMemcpyAsync(cinv_perm.p, h, sizeof(int) * n, hipMemcpyHostToDevice, s));
     AMG_CHECK(hipMemcpyAsync(cinv_iperm.p, h + sizeof(int) * n, sizeof(int) * ld, hipMemcpyHostToDevice, s));
     AMG_CHECK(hipMemcpyAsync(nd_tiles.p, h + sizeof(int) * ((size_t)n + ld), sizeof(int) * tl.size(),

@@ -45,6 +45,7 @@ EXPORTED = (
     "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz", "xfk_spmv_col_bytes",
     "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_solve_csr_pc", "xfk_pcg_time", "xfk_phase_profile",
     "xfk_alloc_stats", "xfk_problem_memory", "xfk_cache_stats", "xfk_release_cache",
+    "xfk_amg_forget_hints",
     "xfk_set_option",
     "xfk_problem_create_harmonic", "xfk_problem_create_harmonic_dist", "xfk_harmonic2d",
     "xfk_get_solution_complex", "xfk_get_circuits_complex",
@@ -222,6 +223,12 @@ def cache_stats() -> dict:
 def release_cache():
     """Give the process-wide caches back to HIP (xfk_release_cache)."""
     _check(load_library().xfk_release_cache())
+
+
+def forget_amg_hints():
+    """Drop the AMG hints the last setup left for the next fresh problem of
+    its size (xfk_amg_forget_hints): the next setup measures everything."""
+    _check(load_library().xfk_amg_forget_hints())
 
 
 def sort_elements(score, device: int = 0) -> np.ndarray:
