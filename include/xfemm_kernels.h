@@ -232,8 +232,9 @@ int xfk_get_circuits(xfk_problem *prob, int *ccase, double *J, double *dV);
  * exchanges the halo of the PCG vector before every SpMV, and all-reduces the
  * PCG's per-block dot-product partials once per iteration.  Boundary
  * conditions and circuits are evaluated on the GLOBAL mesh, so every rank
- * passes the same global description.  Periodic boundaries are not supported
- * in the sharded solve (XFK_ERR_UNSUPPORTED).
+ * passes the same global description.  Periodic / antiperiodic pairs and
+ * air-gap nodes ("coupled nodes") are assembled on every rank that needs them
+ * (the averaging map of its owned rows then finds every entry locally).
  *
  * xfk_static2d and xfk_get_solution are collective over the communicator
  * (every rank calls them); xfk_get_solution returns the global solution on
@@ -392,8 +393,11 @@ int xfk_problem_create_harmonic(const xfk_problem_desc *desc, const xfk_harmonic
  * the halo of its vectors before every SpMV and all-reduces its per-block
  * partials once per iteration; the AMG preconditioner is the sharded hierarchy
  * of the real surrogate (Amg::setup_dist).  Linear problems and the
- * successive-approximation nonlinear loop (ACSolver 0); Case-2 circuits and
- * the Newton AC solver return XFK_ERR_UNSUPPORTED (one device). */
+ * successive-approximation nonlinear loop (ACSolver 0), the Newton AC solver
+ * (ACSolver 1: the auxiliary matrices assembled per rank, the KludgeSolve
+ * products exchange V / the step at the halo, its dot products all-reduced)
+ * and Case-2 circuits (each rank holds the border columns of its rows; C . y
+ * all-reduced, the small circuit system solved on every rank alike). */
 int xfk_problem_create_harmonic_dist(const xfk_problem_desc *desc, const xfk_harmonic_desc *ac, int device,
                                      xfk_comm *comm, xfk_problem **out);
 /* FSolver::Harmonic2D, or HarmonicAxisymmetric (harmonicaxi.cpp:1-800) when

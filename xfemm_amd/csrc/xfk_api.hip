@@ -959,6 +959,10 @@ int build_symbolic(xfk_problem *P)
         std::vector<double> w;
         for (size_t m = 0; m < P->pbca_entry_key.size(); ++m) {
             const long long k = P->pbca_entry_key[m];
+            // (sharded: an entry of a row assembled elsewhere -- a neighbour of a
+            // coupled node in the halo -- is that rank's; its terms lie in its own
+            // row, the rows of the kept entries' terms are all assembled here)
+            if ((int)(k >> 32) >= N) continue;
             rc_dst.push_back((int)(k >> 32));
             rc_dst.push_back((int)(k & 0xffffffff));
             for (auto &t : P->pbca_entry_terms[m]) {
@@ -1129,6 +1133,17 @@ int allreduce_host(xfk_problem *P, double &v)
     int rc = P->comm->allreduce_sum(P->nws_glob.p, P->nws_glob.p + 2, 1, s);
     if (rc != XFK_OK) return rc;
     return d2h(&v, P->nws_glob.p + 2, sizeof(double), s) == hipSuccess ? XFK_OK : XFK_ERR_HIP;
+}
+
+int allreduce_host_n(xfk_problem *P, double *v, int n)
+{
+    if (!P->comm || n <= 0) return XFK_OK;
+    hipStream_t s = P->stream;
+    XFK_CHECK(P->nws_glob.alloc(2 * (size_t)std::max(n, 2)));
+    XFK_CHECK(hipMemcpyAsync(P->nws_glob.p, v, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    int rc = P->comm->allreduce_sum(P->nws_glob.p, P->nws_glob.p + n, (size_t)n, s);
+    if (rc != XFK_OK) return rc;
+    return d2h(v, P->nws_glob.p + n, sizeof(double) * n, s) == hipSuccess ? XFK_OK : XFK_ERR_HIP;
 }
 
 static int exchange(xfk_problem *P, double *vec)

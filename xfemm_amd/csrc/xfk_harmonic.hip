@@ -834,14 +834,14 @@ __global__ void __launch_bounds__(256) k_hc_cdot(int N, const double *__restrict
         part[gridDim.x + blockIdx.x] = s2[1];
     }
 }
-// x = y0 - sum_q Y_q u_q
+// x = y0 - sum_q Y_q u_q (Y_q at stride ld: node vectors with the halo's room)
 __global__ void k_hc_border_combine(int N, int nc2, const double2 *__restrict__ y0, const double2 *__restrict__ Y,
-                                    const double2 *__restrict__ u, double2 *__restrict__ x)
+                                    int ld, const double2 *__restrict__ u, double2 *__restrict__ x)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     double2 v = y0[i];
-    for (int q = 0; q < nc2; ++q) v = csub(v, cmul(Y[(size_t)q * N + i], u[q]));
+    for (int q = 0; q < nc2; ++q) v = csub(v, cmul(Y[(size_t)q * ld + i], u[q]));
     x[i] = v;
 }
 
@@ -1478,13 +1478,19 @@ int create_harmonic(const xfk_problem_desc *d, const xfk_harmonic_desc *ac, int 
     // sharded: the row-block plan, then the per-node tables in local numbering
     PartPlan plan;
     if (comm) {
-        XFK_REQUIRE(nc2 == 0, XFK_ERR_UNSUPPORTED,
-                    "sharded harmonic problems: Case-2 circuits (a specified current in a conducting region) "
-                    "are solved on one device");
-        XFK_REQUIRE(!(nonlin && ac->ac_solver == 1), XFK_ERR_UNSUPPORTED,
-                    "sharded harmonic problems: the Newton AC solver ([ACSolver] = 1) runs on one device");
         if ((rc = plan_rank(d, G, comm, plan)) != XFK_OK) return rc;
         const int NL = plan.n_own + plan.n_halo, NR = plan.n_own + plan.n_extra;
+        if (nc2 > 0) {   // Case-2 border columns (made on the global numbering above): the owned rows
+            const int no = plan.n_own;
+            std::vector<double> Cl(2 * (size_t)nc2 * no);
+            for (int q = 0; q < nc2; ++q)
+                for (int l = 0; l < no; ++l) {
+                    const size_t g = (size_t)plan.l2g[l];
+                    Cl[2 * (size_t)q * no + l] = Cb[2 * (size_t)q * N + g];
+                    Cl[2 * (size_t)q * no + no + l] = Cb[2 * (size_t)q * N + N + g];
+                }
+            Cb.swap(Cl);
+        }
         std::vector<double> f2(2 * (size_t)NL), l2(2 * (size_t)NL);
         for (int l = 0; l < NL; ++l)
             for (int q = 0; q < 2; ++q) {
@@ -1655,7 +1661,7 @@ static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
     }
     if (ac1) {
         XFK_CHECK(P->haux.alloc(6 * (size_t)nnz));
-        XFK_CHECK(P->hk_vec.alloc(5 * (size_t)N));
+        XFK_CHECK(P->hk_vec.alloc(5 * (size_t)NL));   // (node vectors with the halo's room: Pd is exchanged)
         XFK_CHECK(P->hk_b.alloc(2 * (size_t)N));
     }
     HarmArgs A;
@@ -1923,15 +1929,16 @@ static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
                 out[q] = 0;
                 for (int k = 0; k < kResGrid; ++k) out[q] += hp[q * kResGrid + k];
             }
-            return XFK_OK;
+            return allreduce_host_n(P, out, 3);   // (sharded: over every rank's owned rows)
         };
         auto kludge = [&]() -> int {
-            double2 *bo = P->hk_vec.p, *vs = bo + N, *rr = bo + 2 * (size_t)N, *Pd = bo + 3 * (size_t)N,
-                    *U = bo + 4 * (size_t)N;
+            double2 *bo = P->hk_vec.p, *vs = bo + NL, *rr = bo + 2 * (size_t)NL, *Pd = bo + 3 * (size_t)NL,
+                    *U = bo + 4 * (size_t)NL;
             double *bre = P->hk_b.p, *bim = P->hk_b.p + N;
             const int nbn = nb256(N);
             k_hk_join<<<nbn, kBlock, 0, s>>>(N, P->b.p, P->b_im.p, bo);
             XFK_CHECK(hipMemcpyAsync(vs, v, sizeof(double2) * N, hipMemcpyDeviceToDevice, s));
+            if (int xrc = exch_c(v)) return xrc;   // (the products read V at the halo columns)
             k_hk_apply<<<nbn, 256, 0, s>>>(N, P->rowptr.p, P->col.p, P->val.p, P->val_im.p, aux, nnz, v, bo, 2, rr,
                                            nullptr, nullptr);
             double d3[3];
@@ -1942,10 +1949,12 @@ static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
             double er = std::sqrt(d3[2]) / normb;
             if (!(er < lprec)) {
                 for (int k = 0; k < 10; ++k) {
+                    if ((rc = exch_c(v)) != XFK_OK) return rc;
                     k_hk_apply<<<nbn, 256, 0, s>>>(N, P->rowptr.p, P->col.p, P->val.p, P->val_im.p, aux, nnz, v, bo,
                                                    1, nullptr, bre, bim);
                     if ((rc = solve_one(v, bre, bim, true)) != XFK_OK) return rc;
                     k_hk_diff<<<nbn, kBlock, 0, s>>>(N, v, vs, Pd);
+                    if ((rc = exch_c(Pd)) != XFK_OK) return rc;
                     k_hk_apply<<<nbn, 256, 0, s>>>(N, P->rowptr.p, P->col.p, P->val.p, P->val_im.p, aux, nnz, Pd,
                                                    nullptr, 0, U, nullptr, nullptr);
                     if ((rc = dots(rr, U, d3)) != XFK_OK) return rc;
@@ -1975,8 +1984,10 @@ static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
                 re += hp[k];
                 im += hp[kResGrid + k];
             }
-            out = hcx(re, im);
-            return XFK_OK;
+            double ri[2] = {re, im};
+            const int arc = allreduce_host_n(P, ri, 2);   // (sharded: over every rank's owned rows)
+            out = hcx(ri[0], ri[1]);
+            return arc;
         };
         // Schur complement D - C^T Y of this pass's matrix (Y = M^-1 C)
         auto schur = [&](std::vector<hcx> &Sm) -> int {
@@ -1984,7 +1995,7 @@ static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
             for (int q = 0; q < nc2; ++q)
                 for (int r = 0; r < nc2; ++r) {
                     hcx t;
-                    int rc = cdot(q, P->hc2_Y.p + (size_t)r * N, t);
+                    int rc = cdot(q, P->hc2_Y.p + (size_t)r * NL, t);
                     if (rc != XFK_OK) return rc;
                     Sm[(size_t)q * nc2 + r] = (q == r ? hc(P->hc2_D[q]) : hcx(0, 0)) - t;
                 }
@@ -2025,13 +2036,13 @@ static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
         // inner solve is the bordered [M C; C^T D] solve through the Schur
         // complement with this pass's Y = M^-1 C
         auto kludge2 = [&]() -> int {
-            double2 *bo = P->hk_vec.p, *vs = bo + N, *rr = bo + 2 * (size_t)N, *Pd = bo + 3 * (size_t)N,
-                    *U = bo + 4 * (size_t)N;
+            double2 *bo = P->hk_vec.p, *vs = bo + NL, *rr = bo + 2 * (size_t)NL, *Pd = bo + 3 * (size_t)NL,
+                    *U = bo + 4 * (size_t)NL;
             double *bre = P->hk_b.p, *bim = P->hk_b.p + N;
             const int nbn = nb256(N);
             int rc;
             for (int q = 0; q < nc2; ++q)
-                if ((rc = solve_one(P->hc2_Y.p + (size_t)q * N, Cb + 2 * (size_t)q * N, Cb + 2 * (size_t)q * N + N,
+                if ((rc = solve_one(P->hc2_Y.p + (size_t)q * NL, Cb + 2 * (size_t)q * N, Cb + 2 * (size_t)q * N + N,
                                     true)) != XFK_OK)
                     return rc;
             std::vector<hcx> Sm;
@@ -2047,6 +2058,7 @@ static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
             std::vector<hcx> rb(nc2), Ub(nc2), g(nc2);
             k_hk_join<<<nbn, kBlock, 0, s>>>(N, P->b.p, P->b_im.p, bo);
             XFK_CHECK(hipMemcpyAsync(vs, v, sizeof(double2) * N, hipMemcpyDeviceToDevice, s));
+            if (int xrc = exch_c(v)) return xrc;   // (the products read V at the halo columns)
             k_hk_apply<<<nbn, 256, 0, s>>>(N, P->rowptr.p, P->col.p, P->val.p, P->val_im.p, aux, nnz, v, bo, 2, rr,
                                            nullptr, nullptr);
             if ((rc = put(u)) != XFK_OK) return rc;
@@ -2066,6 +2078,7 @@ static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
             double er = std::sqrt(d3[2] + rb2) / normb;
             if (!(er < lprec)) {
                 for (int k = 0; k < 10; ++k) {
+                    if ((rc = exch_c(v)) != XFK_OK) return rc;
                     k_hk_apply<<<nbn, 256, 0, s>>>(N, P->rowptr.p, P->col.p, P->val.p, P->val_im.p, aux, nnz, v, bo,
                                                    1, nullptr, bre, bim);
                     if ((rc = solve_one(P->hc2_y0.p, bre, bim, true)) != XFK_OK) return rc;
@@ -2076,9 +2089,10 @@ static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
                     }
                     if ((rc = dense_solve(Sm, g, un)) != XFK_OK) return rc;
                     if ((rc = put(un)) != XFK_OK) return rc;
-                    k_hc_border_combine<<<nbn, kBlock, 0, s>>>(N, nc2, P->hc2_y0.p, P->hc2_Y.p, ud.p, v);
+                    k_hc_border_combine<<<nbn, kBlock, 0, s>>>(N, nc2, P->hc2_y0.p, P->hc2_Y.p, NL, ud.p, v);
                     k_hk_diff<<<nbn, kBlock, 0, s>>>(N, v, vs, Pd);
                     for (int q = 0; q < nc2; ++q) Pb[q] = cx(un[q].x - u[q].x, un[q].y - u[q].y);
+                    if ((rc = exch_c(Pd)) != XFK_OK) return rc;
                     k_hk_apply<<<nbn, 256, 0, s>>>(N, P->rowptr.p, P->col.p, P->val.p, P->val_im.p, aux, nnz, Pd,
                                                    nullptr, 0, U, nullptr, nullptr);
                     if ((rc = put(Pb)) != XFK_OK) return rc;
@@ -2127,12 +2141,12 @@ static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
             // complement: Y = A^-1 C, y0 = A^-1 b, (D - C^T Y) u = f - C^T y0,
             // V = y0 - Y u (one COCG solve per Case-2 circuit and one for b)
             if (iter == 0) {
-                XFK_CHECK(P->hc2_Y.alloc((size_t)nc2 * N));
-                XFK_CHECK(P->hc2_y0.alloc((size_t)N));
+                XFK_CHECK(P->hc2_Y.alloc((size_t)nc2 * NL));   // (solve_one's x: room for the halo)
+                XFK_CHECK(P->hc2_y0.alloc((size_t)NL));
                 XFK_CHECK(P->hres_part.alloc(2 * kResGrid));
             }
             for (int q = 0; q < nc2; ++q)
-                if ((src = solve_one(P->hc2_Y.p + (size_t)q * N, Cb + 2 * (size_t)q * N,
+                if ((src = solve_one(P->hc2_Y.p + (size_t)q * NL, Cb + 2 * (size_t)q * N,
                                      Cb + 2 * (size_t)q * N + N, iter > 0)) != XFK_OK)
                     return src;
             if ((src = solve_one(P->hc2_y0.p, P->b.p, P->b_im.p, iter > 0)) != XFK_OK) return src;
@@ -2150,7 +2164,7 @@ static int harmonic2d_run(xfk_problem *P, int flags, xfk_result *res)
             DBuf<double2> ud;
             XFK_CHECK(ud.alloc((size_t)nc2));
             XFK_CHECK(hipMemcpyAsync(ud.p, u.data(), sizeof(double2) * nc2, hipMemcpyHostToDevice, s));
-            k_hc_border_combine<<<nb256(N), kBlock, 0, s>>>(N, nc2, P->hc2_y0.p, P->hc2_Y.p, ud.p, v);
+            k_hc_border_combine<<<nb256(N), kBlock, 0, s>>>(N, nc2, P->hc2_y0.p, P->hc2_Y.p, NL, ud.p, v);
             XFK_CHECK(hipStreamSynchronize(s));
         }
         last_iters = P->hc_host->iters;

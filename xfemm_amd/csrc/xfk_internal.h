@@ -611,6 +611,7 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
 int build_symbolic(xfk_problem *P);
 // sum of a host scalar over the ranks of P's communicator (no-op on one device)
 int allreduce_host(xfk_problem *P, double &v);
+int allreduce_host_n(xfk_problem *P, double *v, int n);   // n doubles summed over the ranks (host in, host out)
 // the row-block plan of comm's rank (coupled nodes assembled on every rank)
 int plan_rank(const xfk_problem_desc *d, const GlobalPrep &G, xfk_comm *comm, PartPlan &plan);
 hipError_t d2h(void *dst, const void *src, size_t bytes, hipStream_t s);
