@@ -2093,7 +2093,10 @@ __device__ __forceinline__ double smooth_finish_v(int i, double ax, double w, do
 // part_gam (the PCG's last level-0 sweep only): per-tile partials of
 // b . out, i.e. gamma = r . u of the CG, in the layout and summation order of
 // k_cg_spmv's (same tiles, same workgroup sum), so the SpMV need not read r
-template <int MODE, int B, int SLOTS = 2, class V = double>
+// HB (sharded levels, implicit modes): b of the halo rows in bh (bh[j - n]),
+// D^-1 of the halo rows in dinv[n ..], one weight on every rank -- the first
+// sweep's halo values formed here instead of exchanged after a launch of their own
+template <int MODE, int B, int SLOTS = 2, class V = double, bool HB = false>
 __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__restrict__ rowptr,
                                                          const int *__restrict__ col, const V *__restrict__ val,
                                                          const double *__restrict__ dinv,
@@ -2102,7 +2105,8 @@ __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__r
                                                          double *__restrict__ rout, const int *done,
                                                          double *__restrict__ part_gam, const int *__restrict__ tl,
                                                          const unsigned short *__restrict__ c16 = nullptr,
-                                                         const int *__restrict__ cbase = nullptr)
+                                                         const int *__restrict__ cbase = nullptr,
+                                                         const double *__restrict__ bh = nullptr)
 {
     // the convergence flag, rho, the tile's row range and this row's b,
     // D^-1, x are loaded together before the first branch
@@ -2120,7 +2124,11 @@ __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__r
     if (dn) return;
     const double w = ra > 0.0 ? 1.0 / ra : 0.0;
     double ax;
-    if constexpr (implicit)
+    if constexpr (implicit && HB)
+        ax = cg_tile_spmv16<B, SLOTS>(
+            tr, c16, cb, col, val,
+            [&](int j) { return j < n ? w * dinv[j] * b[j] : (j < ncl ? w * dinv[j] * bh[j - n] : 0.0); }, lds);
+    else if constexpr (implicit)
         ax = cg_tile_spmv16<B, SLOTS>(tr, c16, cb, col, val,
                                       [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; }, lds);
     else
@@ -2152,14 +2160,14 @@ __device__ __forceinline__ double group_row_dot(int i, int n, const int *__restr
     return s;
 }
 
-// coarse levels: G lanes per row
-template <int MODE, int G>
+// coarse levels: G lanes per row (HB as k_amg_smooth's)
+template <int MODE, int G, bool HB = false>
 __global__ void __launch_bounds__(256) k_amg_smooth_g(int n, int ncl, const int *__restrict__ rowptr,
                                                       const int *__restrict__ col, const double *__restrict__ val,
                                                       const double *__restrict__ dinv, const unsigned long long *rho,
                                                       const double *__restrict__ b, const double *__restrict__ x,
                                                       double *__restrict__ out, double *__restrict__ rout,
-                                                      const int *done)
+                                                      const int *done, const double *__restrict__ bh = nullptr)
 {
     if (done && *done) return;
     const double ra = rho_of(rho);
@@ -2167,7 +2175,11 @@ __global__ void __launch_bounds__(256) k_amg_smooth_g(int n, int ncl, const int 
     const int i = (xcd_tile(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) / G;
     constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
     double ax;
-    if constexpr (implicit)
+    if constexpr (implicit && HB)
+        ax = group_row_dot<G>(i, n, rowptr, col, val, [&](int j) {
+            return j < n ? w * dinv[j] * b[j] : (j < ncl ? w * dinv[j] * bh[j - n] : 0.0);
+        });
+    else if constexpr (implicit)
         ax = group_row_dot<G>(i, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; });
     else
         ax = group_row_dot<G>(i, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; });
@@ -2708,7 +2720,7 @@ void launch_compact(hipStream_t s, int nrows, int cap, const int *crow, const in
 
 template <bool PMODE>
 int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<int> &crow, DBuf<int> &ccol,
-           DBuf<double> &cval, long long &cnnz, int key = -1)
+           DBuf<double> &cval, long long &cnnz, int key = -1, bool defer = true)
 {
     AMG_CHECK(M.cnt.alloc((size_t)nrows + 1));
     AMG_CHECK(crow.alloc((size_t)nrows + 1));
@@ -2783,7 +2795,7 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     if (key >= 0) {
         auto hint = M.cap_hint.find(key);
         if (hint != M.cap_hint.end()) {
-            if (M.def_n + 2 <= kAmgDeferSlots) return deferred_pass(hint->second, M.foreign);
+            if (defer && M.def_n + 2 <= kAmgDeferSlots) return deferred_pass(hint->second, M.foreign);
             if (M.foreign) {   // (no slot to check another problem's capacity in: measure)
                 M.cap_hint.erase(hint);
                 hint = M.cap_hint.end();
@@ -2810,7 +2822,7 @@ int spgemm(Amg &M, hipStream_t s, int nrows, const SgX &X, const SgY &Y, DBuf<in
     if (maxprod <= kSortCap) {
         const int cap = maxprod <= 16 ? 16 : maxprod <= 32 ? 32 : maxprod <= 64 ? 64 : maxprod <= 128 ? 128 : 256;
         int rc = XFK_OK;
-        if (key >= 0 && M.def_n + 2 <= kAmgDeferSlots) {
+        if (defer && key >= 0 && M.def_n + 2 <= kAmgDeferSlots) {
             // the measured capacity (no overflow possible) through the
             // deferred slot as a hinted one: the same kernels, so the same
             // bits, without the host check for the length (~20 us per call
@@ -3303,6 +3315,7 @@ int Amg::init(hipStream_t s)
     if (L.empty()) L.emplace_back(new AmgLevel());
     for (auto &lv : L) {   // levels are rebuilt: none sharded until setup_dist says so
         lv->dist = false;
+        lv->hb = false;
         lv->has16 = false;
         lv->has32 = false;
         lv->plan = HaloPlan();
@@ -3562,7 +3575,10 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     // speculatively after each batch and read back in the same host check.
     auto hint = mis_hint.find(l);
     // speculative joins and P need a round hint and a hinted (non-synchronising) P
-    const bool spec = spec_on() && !g_prof && !dist && hint != mis_hint.end() && cap_hint.count(4 * l) &&
+    // (levels of a sharded hierarchy replicated on every rank speculate like a
+    // single device's: every rank holds the same level and hints, so every
+    // rank takes the same decisions; sharded levels keep their host checks)
+    const bool spec = spec_on() && !g_prof && !A.dist && hint != mis_hint.end() && cap_hint.count(4 * l) &&
                       def_n + 4 <= kAmgDeferSlots && !std::getenv("XFK_AMG_DEBUG");
     bool joined = false;
     auto joins_and_p = [&]() { return joins_and_p_impl(s, l); };
@@ -3691,7 +3707,9 @@ int Amg::joins_and_p_impl(hipStream_t s, int l)
     SgX XS{A.rowptr, A.col, A.val, A.ncol_lim, sflag.p, dfinv.p, wF.p, cv.c16, cv.cbase};
     SgY YT{nullptr, nullptr, nullptr, agg.p};
     if (g_prof) g_prof->begin(lv + "P = (I - w D^-1 A) P_tent, R = P^T", 0.0);
-    return spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz, dist ? -1 : 4 * l);
+    // (a sharded level needs P's length on the host at once -- the halo rows'
+    // plan -- so it takes its capacity hint without deferring the length)
+    return spgemm<true>(*this, s, n, XS, YT, A.prow, A.pcol, A.pval, A.pnnz, 4 * l, !A.dist);
 }
 
 // Nested-dissection order of the coarsest level for the dense inverse: a
@@ -4286,6 +4304,46 @@ int gather_host(Amg &M, xfk_comm *comm, hipStream_t s, const double *vals, int k
 
 }  // namespace
 
+// XFK_AMG_HB=0: sharded levels form x_pre = w D^-1 b on their own rows and
+// exchange its halo (a launch and an exchange per level) instead of exchanging
+// b's halo and forming the halo rows' x_pre in the residual launch; read per setup
+static bool hb_on()
+{
+    const char *e = std::getenv("XFK_AMG_HB");
+    return !(e && std::atoi(e) == 0);
+}
+
+// rho[0..1] = the largest of every rank's (ordered bit patterns of positive doubles)
+__global__ void k_rho_max(int nranks, const unsigned long long *__restrict__ all, unsigned long long *rho)
+{
+    if (threadIdx.x >= 2) return;
+    unsigned long long m = 0;
+    for (int q = 0; q < nranks; ++q) m = all[2 * q + threadIdx.x] > m ? all[2 * q + threadIdx.x] : m;
+    rho[threadIdx.x] = m;
+}
+
+// XFK_AMG_FOLD_DIST=0: sharded levels keep the unfolded post-step
+// (prolongation, halo exchange, sweep); read per setup
+static bool dist_fold_on()
+{
+    const char *e = std::getenv("XFK_AMG_FOLD_DIST");
+    return !(e && std::atoi(e) == 0);
+}
+
+// a folded sharded level 0: P~ in f32 with 16-bit columns in the V-cycle's
+// 512-row tiles (a tile reaching the halo columns may keep the int columns,
+// decided per tile), as the single-device level 0's
+int Amg::fold_dist_tiles(hipStream_t s, int l)
+{
+    AmgLevel &A = *L[l];
+    if (!A.fold || l != 0) return XFK_OK;
+    int rc = XFK_OK;
+    if (A.has16 && (rc = build_col16<kCgBlock>(s, A.n, A.ftrow.p, A.ftcol.p, A.fnnz, A.f16, A.f16b)) != XFK_OK)
+        return rc;
+    if (A.has32 && (rc = to_f32(s, A.n, A.ftrow.p, A.fnnz, A.ftval.p, A.f32v)) != XFK_OK) return rc;
+    return XFK_OK;
+}
+
 int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n, int nh, const int *rowptr,
                     const int *col, const double *val, long long nnz)
 {
@@ -4314,12 +4372,14 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
         // f32 restriction / prolongation (converted after the aggregation)
         A.has32 = A.has16 && (prec32 < 0 ? f32_on() : prec32 != 0);
     }
+    const bool hb = sweeps == 1 && hb_on();
+    AMG_CHECK(rho_all.alloc(2 * (size_t)nranks));
     for (int l = 0;; ++l) {
         AmgLevel &A = *L[l];
         const int nl = A.n;
         stats.n[l] = nl;
         stats.nnz[l] = A.nnz;
-        AMG_CHECK(A.dinv.alloc(std::max(1, nl)));
+        AMG_CHECK(A.dinv.alloc(std::max(1, std::max(nl, A.ncol_smooth))));
         AMG_CHECK(absd.alloc(std::max(1, nl)));
         AMG_CHECK(dfinv.alloc(std::max(1, nl)));
         AMG_CHECK(wF.alloc(std::max(1, nl)));
@@ -4331,6 +4391,19 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
                                                  absd.p, A.dinv.p, sflag.p, cnt.p, dfinv.p, wF.p, rho_part.p,
                                                  signed_strength());
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(nl), rho_part.p, omega, rho.p + 2 * l);
+        A.hb = hb;
+        if (hb) {
+            // one smoother weight on every rank (the largest bound: the
+            // single device's) and D^-1 of the halo rows, so that each rank
+            // forms its halo rows' x_pre = w D^-1 b itself from b's halo
+            if ((rc = comm->allgather_bytes(rho.p + 2 * l, rho_all.p, 2 * sizeof(unsigned long long), s)) != XFK_OK)
+                return rc;
+            k_rho_max<<<1, 64, 0, s>>>(nranks, rho_all.p, rho.p + 2 * l);
+            if ((rc = comm->exchange(A.plan, A.dinv.p, s)) != XFK_OK) return rc;
+            A.plan_h = A.plan;
+            for (HaloRange &r : A.plan_h.recv) r.off -= nl;
+            AMG_CHECK(A.bh.alloc((size_t)std::max(1, A.ncol_smooth - nl)));
+        }
         long long nc = 0;
         rc = aggregate(s, l, nc, false);
         if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
@@ -4486,17 +4559,19 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
     if ((rc = comm->exchange(ep, ebuf.p, s)) != XFK_OK) return rc;
     if (nhe > 0) k_dbl2int<<<nb(nhe), kB, 0, s>>>(nhe, ebuf.p + pnnz, pe_col.p + pnnz);
     // 3. AP over the full rows, then this rank's coarse rows R (AP)
-    long long lnnz = 0;
+    long long lnnz = 0, apnnz = 0;
     AMG_CHECK(l_row.alloc((size_t)cmax + 1));
     {
         SgX XA{A.rowptr, A.col, A.val, ncl, nullptr, nullptr, nullptr};
         SgY YP{pe_row.p, pe_col.p, pe_val.p, nullptr};
-        long long apnnz = 0;
-        rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, apnnz);
+        // (the lengths are needed on the host at once: capacity hints of the
+        // last setup, rank-local, taken without deferring -- one host check
+        // per product instead of two)
+        rc = spgemm<false>(*this, s, n, XA, YP, ap_row, ap_col, ap_val, apnnz, 4 * l + 1, false);
         if (rc == XFK_OK) {
             SgX XR{A.rrow.p, A.rcol.p, A.rval.p, INT_MAX, nullptr, nullptr, nullptr};
             SgY YAP{ap_row.p, ap_col.p, ap_val.p, nullptr};
-            rc = spgemm<false>(*this, s, nc, XR, YAP, l_row, l_col, l_val, lnnz);
+            rc = spgemm<false>(*this, s, nc, XR, YAP, l_row, l_col, l_val, lnnz, 4 * l + 2, false);
         }
         if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
     }
@@ -4517,10 +4592,30 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
         set_error("AMG: a SpGEMM row exceeds the LDS hash capacity");
         return XFK_ERR_UNSUPPORTED;
     }
+    // 4b. folded post-step of this sharded level (V(1,1)): P~ = (I - w D^-1 A) P_ext
+    //     over the pattern of A P_ext -- own rows, global coarse columns (the
+    //     peers' aggregates next to the halo included); formed before the next
+    //     level reuses A P's buffers.  The V-cycle's prolongation and post-sweep
+    //     become one pass over P~ reading x_c with its coarse halo (a sharded
+    //     next level: the columns are localised with its plan below; a
+    //     replicated one: the global coarse vector every rank holds).
+    A.fold = A.fold_formed = sweeps == 1 && dist_fold_on() && (fold_on < 0 ? fold_levels() : fold_on != 0);
+    if (A.fold) {
+        A.fnnz = apnnz;
+        AMG_CHECK(A.ftrow.alloc((size_t)n + 1));
+        AMG_CHECK(A.ftcol.alloc((size_t)std::max(1LL, apnnz)));
+        AMG_CHECK(A.ftval.alloc((size_t)std::max(1LL, apnnz)));
+        AMG_CHECK(hipMemcpyAsync(A.ftrow.p, ap_row.p, sizeof(int) * ((size_t)n + 1), hipMemcpyDeviceToDevice, s));
+        if (n > 0)
+            k_fold_p<<<(int)(((long long)n * kFoldLanes + 255) / 256), 256, 0, s>>>(
+                n, rho.p + 2 * l, A.dinv.p, ap_row.p, ap_col.p, ap_val.p, pe_row.p, pe_col.p, pe_val.p, A.ftcol.p,
+                A.ftval.p);
+    }
     if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
     AmgLevel &C = *L[l + 1];
     if (!rep) {
         // 5a. stay sharded: own rows with local columns, halo spans per peer
+        //     (the spans cover A_{l+1}'s columns and P~'s)
         const int own0 = cn[rank], own1 = cn[rank + 1];
         AMG_CHECK(span_dev.alloc(2 * (size_t)nranks));
         k_fill_int<<<1, 64, 0, s>>>(nranks, span_dev.p, INT_MAX);
@@ -4528,6 +4623,9 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
         if (lnnz > 0)
             k_peer_span<<<nb(lnnz), kB, 0, s>>>(lnnz, l_col.p, own0, own1, c0_dev.p, nranks, span_dev.p,
                                                  span_dev.p + nranks);
+        if (A.fold && apnnz > 0)
+            k_peer_span<<<nb(apnnz), kB, 0, s>>>(apnnz, A.ftcol.p, own0, own1, c0_dev.p, nranks, span_dev.p,
+                                                  span_dev.p + nranks);
         std::vector<int> span(2 * nranks);
         AMG_CHECK(hipMemcpyAsync(span.data(), span_dev.p, sizeof(int) * 2 * nranks, hipMemcpyDeviceToHost, s));
         AMG_CHECK(hipStreamSynchronize(s));
@@ -4568,6 +4666,10 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
             k_localize<<<nb(lnnz), kB, 0, s>>>(lnnz, C.col_o.p, own0, own1, nc, c0_dev.p, nranks, span_dev.p,
                                                 map_dev.p);
         }
+        if (A.fold && apnnz > 0)
+            k_localize<<<nb(apnnz), kB, 0, s>>>(apnnz, A.ftcol.p, own0, own1, nc, c0_dev.p, nranks, span_dev.p,
+                                                 map_dev.p);
+        if ((rc = fold_dist_tiles(s, l)) != XFK_OK) return rc;
         C.n = nc;
         C.nnz = lnnz;
         C.ncol_lim = nc;
@@ -4581,6 +4683,7 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
         return XFK_OK;
     }
     // 5b. all-gather the coarse rows (padded per rank) into the replicated level
+    if ((rc = fold_dist_tiles(s, l)) != XFK_OK) return rc;
     c0 = cn;
     ncmax = cmax;
     AMG_CHECK(s_col.alloc((size_t)nnzmax));
@@ -4657,9 +4760,11 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
 namespace {
 
 // which: 0 every row; 1 / 2 the interior / boundary tiles of A.ts (tile levels)
-template <int MODE>
-void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
-                     const double *x, double *out, double *rout, const int *done, double *part_gam, int which)
+// bh (kResidFromZero on a sharded level): the halo rows' b (k_amg_smooth's HB)
+template <int MODE, bool HB>
+void launch_smooth_h(hipStream_t s, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
+                     const double *x, double *out, double *rout, const int *done, double *part_gam, int which,
+                     const double *bh)
 {
     const int *tl = nullptr;
     int nt = 0;
@@ -4671,39 +4776,46 @@ void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned lon
     if (l == 0) {
         const int g = tl ? nt : (A.n + kCgBlock - 1) / kCgBlock;
         if (A.has32 && f32_sweep_on())
-            k_amg_smooth<MODE, kCgBlock><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.a32.p,
-                                                                A.dinv.p, rho, b, x, out, rout, done, part_gam, tl,
-                                                                A.has16 ? A.a16.p : nullptr,
-                                                                A.has16 ? A.a16b.p : nullptr);
+            k_amg_smooth<MODE, kCgBlock, 2, float, HB><<<g, kCgBlock, 0, s>>>(
+                A.n, A.ncol_smooth, A.rowptr, A.col, A.a32.p, A.dinv.p, rho, b, x, out, rout, done, part_gam, tl,
+                A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr, bh);
         else
-            k_amg_smooth<MODE, kCgBlock><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p,
-                                                                rho, b, x, out, rout, done, part_gam, tl,
-                                                                A.has16 ? A.a16.p : nullptr,
-                                                                A.has16 ? A.a16b.p : nullptr);
+            k_amg_smooth<MODE, kCgBlock, 2, double, HB><<<g, kCgBlock, 0, s>>>(
+                A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out, rout, done, part_gam, tl,
+                A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr, bh);
         return;
     }
     if (A.n >= kTileMinRows) {
         // coarse levels carry 10-16 entries per row: 4 slots per lane, one pass per tile
         const int g = tl ? nt : (A.n + 255) / 256;
         if ((double)A.nnz <= 8.0 * A.n)
-            k_amg_smooth<MODE, 256, 2><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b,
-                                                         x, out, rout, done, nullptr, tl);
+            k_amg_smooth<MODE, 256, 2, double, HB><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val,
+                                                                     A.dinv.p, rho, b, x, out, rout, done, nullptr,
+                                                                     tl, nullptr, nullptr, bh);
         else
-            k_amg_smooth<MODE, 256, 4><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b,
-                                                         x, out, rout, done, nullptr, tl);
+            k_amg_smooth<MODE, 256, 4, double, HB><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val,
+                                                                     A.dinv.p, rho, b, x, out, rout, done, nullptr,
+                                                                     tl, nullptr, nullptr, bh);
         return;
     }
     const int G = lanes_for(A.n > 0 ? (double)A.nnz / A.n : 1.0);
     const int g = (int)(((long long)A.n * G + 255) / 256);
     if (G == 4)
-        k_amg_smooth_g<MODE, 4><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
-                                                 rout, done);
+        k_amg_smooth_g<MODE, 4, HB><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
+                                                     out, rout, done, bh);
     else if (G == 8)
-        k_amg_smooth_g<MODE, 8><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
-                                                 rout, done);
+        k_amg_smooth_g<MODE, 8, HB><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
+                                                     out, rout, done, bh);
     else
-        k_amg_smooth_g<MODE, 16><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
-                                                  out, rout, done);
+        k_amg_smooth_g<MODE, 16, HB><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b,
+                                                      x, out, rout, done, bh);
+}
+
+template <int MODE>
+void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
+                     const double *x, double *out, double *rout, const int *done, double *part_gam, int which)
+{
+    launch_smooth_h<MODE, false>(s, l, A, rho, b, x, out, rout, done, part_gam, which, nullptr);
 }
 
 void launch_smooth(hipStream_t s, int mode, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
@@ -4934,12 +5046,21 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
             [&] { launch_smooth(s, mode, l, A, rh, b, x, o, ro, done, pg, 1); },
             [&] { launch_smooth(s, mode, l, A, rh, b, x, o, ro, done, pg, 2); });
     };
-    if (A.n > 0) k_jacobi_first<<<nb(A.n), kB, 0, s>>>(A.n, rh, A.dinv.p, b, cur, done);
-    for (int k = 1; k < sweeps; ++k) {
-        if ((rc = smooth_after_exchange(kSweep, cur, oth, nullptr, nullptr)) != XFK_OK) return nullptr;
-        std::swap(cur, oth);
+    if (A.hb && sweeps == 1 && !ov) {
+        // b's halo, then r' = b - A x_pre with x_pre = w D^-1 b formed on the
+        // fly for own and halo rows (x_pre itself kept only when unfolded)
+        if ((rc = comm->exchange_to(A.plan_h, b, A.bh.p, s)) != XFK_OK) return nullptr;
+        if (A.n > 0)
+            launch_smooth_h<kResidFromZero, true>(s, l, A, rh, b, nullptr, A.fold ? nullptr : cur, A.r.p, done,
+                                                  nullptr, 0, A.bh.p);
+    } else {
+        if (A.n > 0) k_jacobi_first<<<nb(A.n), kB, 0, s>>>(A.n, rh, A.dinv.p, b, cur, done);
+        for (int k = 1; k < sweeps; ++k) {
+            if ((rc = smooth_after_exchange(kSweep, cur, oth, nullptr, nullptr)) != XFK_OK) return nullptr;
+            std::swap(cur, oth);
+        }
+        if ((rc = smooth_after_exchange(kResid, cur, nullptr, A.r.p, nullptr)) != XFK_OK) return nullptr;
     }
-    if ((rc = smooth_after_exchange(kResid, cur, nullptr, A.r.p, nullptr)) != XFK_OK) return nullptr;
     AmgLevel &C = *L[l + 1];
     const int GR = lanes_for(A.nc > 0 ? (double)A.pnnz / A.nc : 1.0);
     const double *xc;
@@ -4950,10 +5071,17 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
         else
             launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, dst, false, GR, done);
     };
+    const bool fold = A.fold && sweeps == 1;
+    const double *xfull = nullptr;   // folded: x_c with the columns P~ reads (coarse halo / global)
     if (C.dist) {
         restrict_to(C.b.p);
         xc = vc_dist(s, l + 1, C.b.p, nullptr, done, rc);
         if (rc != XFK_OK) return nullptr;
+        if (fold) {   // the coarse halo P~ reads (the next level's plan covers P~'s columns)
+            double *xh = const_cast<double *>(xc);
+            if ((rc = comm->exchange(C.plan, xh, s)) != XFK_OK) return nullptr;
+            xfull = xh;
+        }
     } else {
         // the replicated levels: gather the global right-hand side, solve the
         // same coarse problem on every rank, read the own aggregates back
@@ -4961,8 +5089,42 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
         const int te = tail_begin(s, 0);
         if ((rc = comm->allgather(cb_loc.p, cb_all.p, (size_t)ncmax, s)) != XFK_OK) return nullptr;
         k_unpad<<<nb(C.n), kB, 0, s>>>(C.n, nranks, c0_dev.p, cb_all.p, ncmax, C.b.p, done);
-        xc = vcycle_level(*this, s, l + 1, C.b.p, nullptr, done) + c0[rank];
+        xfull = vcycle_level(*this, s, l + 1, C.b.p, nullptr, done);
+        xc = xfull + c0[rank];
         tail_end(s, te);
+    }
+    if (fold) {
+        // u = w D^-1 b + w D^-1 r' + P~ x_c over the own rows: the prolongation
+        // and the post-sweep (whose halo exchange it replaces) in one pass
+        double *o = out ? out : oth;
+        if (A.n > 0) {
+            double *pg = (l == 0 && out) ? part_gam_ : nullptr;
+            if (l == 0) {
+                const int g = (A.n + kCgBlock - 1) / kCgBlock;
+                if (A.has32)
+                    k_fold_post0<kCgBlock, 2><<<g, kCgBlock, 0, s>>>(A.n, A.ftrow.p, A.ftcol.p, A.f32v.p, xfull,
+                                                                     A.dinv.p, rh, A.r.p, b, o, done, pg,
+                                                                     A.has16 ? A.f16.p : nullptr,
+                                                                     A.has16 ? A.f16b.p : nullptr);
+                else
+                    k_fold_post0<kCgBlock, 2><<<g, kCgBlock, 0, s>>>(A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xfull,
+                                                                     A.dinv.p, rh, A.r.p, b, o, done, pg,
+                                                                     A.has16 ? A.f16.p : nullptr,
+                                                                     A.has16 ? A.f16b.p : nullptr);
+            } else {
+                const int g = (A.n + 255) / 256;
+                const unsigned short *no16 = nullptr;
+                const int *nob = nullptr;
+                if ((double)A.fnnz <= 8.0 * A.n)
+                    k_fold_post0<256, 2><<<g, 256, 0, s>>>(A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xfull, A.dinv.p, rh,
+                                                           A.r.p, b, o, done, pg, no16, nob);
+                else
+                    k_fold_post0<256, 4><<<g, 256, 0, s>>>(A.n, A.ftrow.p, A.ftcol.p, A.ftval.p, xfull, A.dinv.p, rh,
+                                                           A.r.p, b, o, done, pg, no16, nob);
+            }
+        }
+        if (l == 0 && out && part_gam_) gamma_done = true;
+        return o;
     }
     if (A.n > 0) {
         const int GP = lanes_for((double)A.pnnz / A.n);
@@ -5044,6 +5206,9 @@ int Amg::refresh(hipStream_t s, bool fold)
     // that unfolds keeps P~'s arrays, so a later one may fold again
     const bool refold = fold && A.fold_formed && !dist && refold_on() && A.fnnz > 0;
     A.fold = refold;
+    // (a sharded level 0 goes back to its own weight and the exchange of
+    // x_pre: the refresh's D^-1 and rho are the rank's own rows')
+    A.hb = false;
     AMG_CHECK(absd.alloc(std::max(1, n)));
     AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(n))));
     if (n > 0) {
