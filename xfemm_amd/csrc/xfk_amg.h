@@ -74,12 +74,6 @@ struct AmgLevel {
     // coarser: spans of the peers' aggregate ids)
     bool dist = false;
     HaloPlan plan;
-    // sharded level whose first sweep reads the halo of b instead of x_pre's
-    // (one weight on every rank, D^-1 of the halo rows in dinv[n ..]): b's halo
-    // is exchanged into bh over plan_h (plan's receive offsets minus n)
-    bool hb = false;
-    HaloPlan plan_h;
-    DBuf<double> bh;
     TileSplit ts;                     // sharded level run by the tile kernels: exchange overlap
     // 16-bit column offsets per tile (single-device level 0, xfk_spmv.h
     // k_tile_col16): A and P~ in the 512-row tiles of the SpMV / sweeps /
@@ -197,7 +191,6 @@ struct Amg {
     DBuf<int> c0_dev;
     DBuf<int> span_dev, map_dev;      // peer spans of a sharded coarse level (setup scratch)
     DBuf<double> cb_loc, cb_all;      // restricted residual: own aggregates, all-gathered (padded)
-    DBuf<unsigned long long> rho_all; // every rank's rho of a sharded level (all-gathered)
     DBuf<int> pe_row, pe_col;         // P extended by the halo nodes' rows (global coarse columns)
     DBuf<double> pe_val, ebuf;
     DBuf<int> l_row, l_col, s_col;    // this rank's coarse rows (s_: padded send copy)

@@ -2093,10 +2093,7 @@ __device__ __forceinline__ double smooth_finish_v(int i, double ax, double w, do
 // part_gam (the PCG's last level-0 sweep only): per-tile partials of
 // b . out, i.e. gamma = r . u of the CG, in the layout and summation order of
 // k_cg_spmv's (same tiles, same workgroup sum), so the SpMV need not read r
-// HB (sharded levels, implicit modes): b of the halo rows in bh (bh[j - n]),
-// D^-1 of the halo rows in dinv[n ..], one weight on every rank -- the first
-// sweep's halo values formed here instead of exchanged after a launch of their own
-template <int MODE, int B, int SLOTS = 2, class V = double, bool HB = false>
+template <int MODE, int B, int SLOTS = 2, class V = double>
 __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__restrict__ rowptr,
                                                          const int *__restrict__ col, const V *__restrict__ val,
                                                          const double *__restrict__ dinv,
@@ -2105,8 +2102,7 @@ __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__r
                                                          double *__restrict__ rout, const int *done,
                                                          double *__restrict__ part_gam, const int *__restrict__ tl,
                                                          const unsigned short *__restrict__ c16 = nullptr,
-                                                         const int *__restrict__ cbase = nullptr,
-                                                         const double *__restrict__ bh = nullptr)
+                                                         const int *__restrict__ cbase = nullptr)
 {
     // the convergence flag, rho, the tile's row range and this row's b,
     // D^-1, x are loaded together before the first branch
@@ -2124,11 +2120,7 @@ __global__ void __launch_bounds__(B) k_amg_smooth(int n, int ncl, const int *__r
     if (dn) return;
     const double w = ra > 0.0 ? 1.0 / ra : 0.0;
     double ax;
-    if constexpr (implicit && HB)
-        ax = cg_tile_spmv16<B, SLOTS>(
-            tr, c16, cb, col, val,
-            [&](int j) { return j < n ? w * dinv[j] * b[j] : (j < ncl ? w * dinv[j] * bh[j - n] : 0.0); }, lds);
-    else if constexpr (implicit)
+    if constexpr (implicit)
         ax = cg_tile_spmv16<B, SLOTS>(tr, c16, cb, col, val,
                                       [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; }, lds);
     else
@@ -2160,14 +2152,14 @@ __device__ __forceinline__ double group_row_dot(int i, int n, const int *__restr
     return s;
 }
 
-// coarse levels: G lanes per row (HB as k_amg_smooth's)
-template <int MODE, int G, bool HB = false>
+// coarse levels: G lanes per row
+template <int MODE, int G>
 __global__ void __launch_bounds__(256) k_amg_smooth_g(int n, int ncl, const int *__restrict__ rowptr,
                                                       const int *__restrict__ col, const double *__restrict__ val,
                                                       const double *__restrict__ dinv, const unsigned long long *rho,
                                                       const double *__restrict__ b, const double *__restrict__ x,
                                                       double *__restrict__ out, double *__restrict__ rout,
-                                                      const int *done, const double *__restrict__ bh = nullptr)
+                                                      const int *done)
 {
     if (done && *done) return;
     const double ra = rho_of(rho);
@@ -2175,11 +2167,7 @@ __global__ void __launch_bounds__(256) k_amg_smooth_g(int n, int ncl, const int 
     const int i = (xcd_tile(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) / G;
     constexpr bool implicit = (MODE == kSweepFromZero || MODE == kResidFromZero);
     double ax;
-    if constexpr (implicit && HB)
-        ax = group_row_dot<G>(i, n, rowptr, col, val, [&](int j) {
-            return j < n ? w * dinv[j] * b[j] : (j < ncl ? w * dinv[j] * bh[j - n] : 0.0);
-        });
-    else if constexpr (implicit)
+    if constexpr (implicit)
         ax = group_row_dot<G>(i, n, rowptr, col, val, [&](int j) { return j < ncl ? w * dinv[j] * b[j] : 0.0; });
     else
         ax = group_row_dot<G>(i, n, rowptr, col, val, [&](int j) { return j < ncl ? x[j] : 0.0; });
@@ -3315,7 +3303,6 @@ int Amg::init(hipStream_t s)
     if (L.empty()) L.emplace_back(new AmgLevel());
     for (auto &lv : L) {   // levels are rebuilt: none sharded until setup_dist says so
         lv->dist = false;
-        lv->hb = false;
         lv->has16 = false;
         lv->has32 = false;
         lv->plan = HaloPlan();
@@ -4304,24 +4291,6 @@ int gather_host(Amg &M, xfk_comm *comm, hipStream_t s, const double *vals, int k
 
 }  // namespace
 
-// XFK_AMG_HB=0: sharded levels form x_pre = w D^-1 b on their own rows and
-// exchange its halo (a launch and an exchange per level) instead of exchanging
-// b's halo and forming the halo rows' x_pre in the residual launch; read per setup
-static bool hb_on()
-{
-    const char *e = std::getenv("XFK_AMG_HB");
-    return !(e && std::atoi(e) == 0);
-}
-
-// rho[0..1] = the largest of every rank's (ordered bit patterns of positive doubles)
-__global__ void k_rho_max(int nranks, const unsigned long long *__restrict__ all, unsigned long long *rho)
-{
-    if (threadIdx.x >= 2) return;
-    unsigned long long m = 0;
-    for (int q = 0; q < nranks; ++q) m = all[2 * q + threadIdx.x] > m ? all[2 * q + threadIdx.x] : m;
-    rho[threadIdx.x] = m;
-}
-
 // XFK_AMG_FOLD_DIST=0: sharded levels keep the unfolded post-step
 // (prolongation, halo exchange, sweep); read per setup
 static bool dist_fold_on()
@@ -4372,14 +4341,12 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
         // f32 restriction / prolongation (converted after the aggregation)
         A.has32 = A.has16 && (prec32 < 0 ? f32_on() : prec32 != 0);
     }
-    const bool hb = sweeps == 1 && hb_on();
-    AMG_CHECK(rho_all.alloc(2 * (size_t)nranks));
     for (int l = 0;; ++l) {
         AmgLevel &A = *L[l];
         const int nl = A.n;
         stats.n[l] = nl;
         stats.nnz[l] = A.nnz;
-        AMG_CHECK(A.dinv.alloc(std::max(1, std::max(nl, A.ncol_smooth))));
+        AMG_CHECK(A.dinv.alloc(std::max(1, nl)));
         AMG_CHECK(absd.alloc(std::max(1, nl)));
         AMG_CHECK(dfinv.alloc(std::max(1, nl)));
         AMG_CHECK(wF.alloc(std::max(1, nl)));
@@ -4391,19 +4358,6 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
                                                  absd.p, A.dinv.p, sflag.p, cnt.p, dfinv.p, wF.p, rho_part.p,
                                                  signed_strength());
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(nl), rho_part.p, omega, rho.p + 2 * l);
-        A.hb = hb;
-        if (hb) {
-            // one smoother weight on every rank (the largest bound: the
-            // single device's) and D^-1 of the halo rows, so that each rank
-            // forms its halo rows' x_pre = w D^-1 b itself from b's halo
-            if ((rc = comm->allgather_bytes(rho.p + 2 * l, rho_all.p, 2 * sizeof(unsigned long long), s)) != XFK_OK)
-                return rc;
-            k_rho_max<<<1, 64, 0, s>>>(nranks, rho_all.p, rho.p + 2 * l);
-            if ((rc = comm->exchange(A.plan, A.dinv.p, s)) != XFK_OK) return rc;
-            A.plan_h = A.plan;
-            for (HaloRange &r : A.plan_h.recv) r.off -= nl;
-            AMG_CHECK(A.bh.alloc((size_t)std::max(1, A.ncol_smooth - nl)));
-        }
         long long nc = 0;
         rc = aggregate(s, l, nc, false);
         if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
@@ -4510,13 +4464,15 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
     AMG_CHECK(cnt.alloc((size_t)std::max(n, nh) + 1));
     AMG_CHECK(flag.alloc((size_t)nh + 1));
     if (nh > 0) k_dbl2int<<<nb(nh), kB, 0, s>>>(nh, ebuf.p + n, cnt.p);
-    long long nhe = 0;
-    if ((rc = scan_total(*this, s, cnt.p, flag.p, nh, nhe)) != XFK_OK) return rc;   // flag = halo row pointer
+    // flag = halo row pointer (its total, the halo rows' P entries, read with
+    // the ranges' pointers below: one host check)
+    if ((rc = scan_only(*this, s, cnt.p, flag.p, nh)) != XFK_OK) return rc;
     AMG_CHECK(pe_row.alloc((size_t)ncl + 1));
     k_pe_row<<<nb(ncl + 1), kB, 0, s>>>(n, nh, pnnz, A.prow.p, flag.p, pe_row.p);
     const HaloPlan &hp = A.plan;
     const int nsr = (int)(hp.send.size() + hp.recv.size());
-    if ((rc = host_ints(2 * nsr)) != XFK_OK) return rc;
+    if ((rc = host_ints(2 * nsr + 1)) != XFK_OK) return rc;
+    long long nhe = 0;
     {
         int k = 0;
         for (const HaloRange &t : hp.send) {
@@ -4528,7 +4484,9 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
             AMG_CHECK(hipMemcpyAsync(host_big + k++, flag.p + (r.off - n) + r.len, sizeof(int),
                                      hipMemcpyDeviceToHost, s));
         }
+        AMG_CHECK(hipMemcpyAsync(host_big + k, flag.p + nh, sizeof(int), hipMemcpyDeviceToHost, s));
         AMG_CHECK(hipStreamSynchronize(s));
+        nhe = host_big[k];
     }
     HaloPlan ep;
     {
@@ -4575,31 +4533,16 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
         }
         if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
     }
-    // 4. entry counts and status of every rank
-    {
-        const double mine[2] = {(double)lnnz, rc == XFK_OK ? 0.0 : 1.0};
-        int rc2 = gather_host(*this, comm, s, mine, 2, all);
-        if (rc2 != XFK_OK) return rc2;
-    }
-    std::vector<int> e0(nranks + 1, 0);
-    long long nnzmax = 1;
-    for (int q = 0; q < nranks; ++q) {
-        e0[q + 1] = e0[q] + (int)all[2 * q];
-        nnzmax = std::max(nnzmax, (long long)all[2 * q]);
-        fail |= all[2 * q + 1] != 0.0;
-    }
-    if (fail) {
-        set_error("AMG: a SpGEMM row exceeds the LDS hash capacity");
-        return XFK_ERR_UNSUPPORTED;
-    }
-    // 4b. folded post-step of this sharded level (V(1,1)): P~ = (I - w D^-1 A) P_ext
-    //     over the pattern of A P_ext -- own rows, global coarse columns (the
-    //     peers' aggregates next to the halo included); formed before the next
-    //     level reuses A P's buffers.  The V-cycle's prolongation and post-sweep
-    //     become one pass over P~ reading x_c with its coarse halo (a sharded
-    //     next level: the columns are localised with its plan below; a
-    //     replicated one: the global coarse vector every rank holds).
-    A.fold = A.fold_formed = sweeps == 1 && dist_fold_on() && (fold_on < 0 ? fold_levels() : fold_on != 0);
+    // 4. folded post-step of this sharded level (V(1,1)): P~ = (I - w D^-1 A) P_ext
+    //    over the pattern of A P_ext -- own rows, global coarse columns (the
+    //    peers' aggregates next to the halo included); formed before the next
+    //    level reuses A P's buffers.  The V-cycle's prolongation and post-sweep
+    //    become one pass over P~ reading x_c with its coarse halo (a sharded
+    //    next level: the columns are localised with its plan below; a
+    //    replicated one: the global coarse vector every rank holds).
+    const bool ok3 = rc == XFK_OK;
+    A.fold = A.fold_formed =
+        ok3 && sweeps == 1 && dist_fold_on() && (fold_on < 0 ? fold_levels() : fold_on != 0);
     if (A.fold) {
         A.fnnz = apnnz;
         AMG_CHECK(A.ftrow.alloc((size_t)n + 1));
@@ -4611,33 +4554,54 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
                 n, rho.p + 2 * l, A.dinv.p, ap_row.p, ap_col.p, ap_val.p, pe_row.p, pe_col.p, pe_val.p, A.ftcol.p,
                 A.ftval.p);
     }
-    if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
-    AmgLevel &C = *L[l + 1];
-    if (!rep) {
-        // 5a. stay sharded: own rows with local columns, halo spans per peer
-        //     (the spans cover A_{l+1}'s columns and P~'s)
-        const int own0 = cn[rank], own1 = cn[rank + 1];
-        AMG_CHECK(span_dev.alloc(2 * (size_t)nranks));
-        k_fill_int<<<1, 64, 0, s>>>(nranks, span_dev.p, INT_MAX);
-        k_fill_int<<<1, 64, 0, s>>>(nranks, span_dev.p + nranks, -1);
+    // 5. entry counts, status and -- the next level staying sharded -- the
+    //    spans of the peers' aggregate ids this rank's A_{l+1} and P~ columns
+    //    reference (what each peer must send): one all-gather, one host check
+    const int own0 = cn[rank], own1 = cn[rank + 1];
+    const int RW = 2 + 2 * nranks;   // per rank: lnnz, status, lo[nranks], hi[nranks]
+    DBuf<double> recs;
+    AMG_CHECK(recs.alloc((size_t)RW * (nranks + 1)));
+    const double mine[2] = {(double)lnnz, ok3 ? 0.0 : 1.0};   // (read before the host check below)
+    AMG_CHECK(hipMemcpyAsync(recs.p, mine, sizeof(mine), hipMemcpyHostToDevice, s));
+    AMG_CHECK(span_dev.alloc(2 * (size_t)nranks));
+    k_fill_int<<<1, 64, 0, s>>>(nranks, span_dev.p, INT_MAX);
+    k_fill_int<<<1, 64, 0, s>>>(nranks, span_dev.p + nranks, -1);
+    if (!rep && ok3) {
         if (lnnz > 0)
             k_peer_span<<<nb(lnnz), kB, 0, s>>>(lnnz, l_col.p, own0, own1, c0_dev.p, nranks, span_dev.p,
                                                  span_dev.p + nranks);
         if (A.fold && apnnz > 0)
             k_peer_span<<<nb(apnnz), kB, 0, s>>>(apnnz, A.ftcol.p, own0, own1, c0_dev.p, nranks, span_dev.p,
                                                   span_dev.p + nranks);
+    }
+    k_int2dbl<<<1, 256, 0, s>>>(2LL * nranks, span_dev.p, recs.p + 2);
+    if ((rc = comm->allgather(recs.p, recs.p + RW, (size_t)RW, s)) != XFK_OK) return rc;
+    all.assign((size_t)RW * nranks, 0.0);
+    AMG_CHECK(hipMemcpyAsync(all.data(), recs.p + RW, sizeof(double) * RW * nranks, hipMemcpyDeviceToHost, s));
+    AMG_CHECK(hipStreamSynchronize(s));
+    std::vector<int> e0(nranks + 1, 0);
+    long long nnzmax = 1;
+    for (int q = 0; q < nranks; ++q) {
+        e0[q + 1] = e0[q] + (int)all[(size_t)RW * q];
+        nnzmax = std::max(nnzmax, (long long)all[(size_t)RW * q]);
+        fail |= all[(size_t)RW * q + 1] != 0.0;
+    }
+    if (fail) {
+        set_error("AMG: a SpGEMM row exceeds the LDS hash capacity");
+        return XFK_ERR_UNSUPPORTED;
+    }
+    if ((int)L.size() <= l + 1) L.emplace_back(new AmgLevel());
+    AmgLevel &C = *L[l + 1];
+    if (!rep) {
+        // 5a. stay sharded: own rows with local columns, halo spans per peer
+        //     (what I need: my spans; what each peer needs from me: its spans
+        //     of my ids)
+        auto span_of = [&](int r, int q, bool hi) { return (int)all[(size_t)RW * r + 2 + (hi ? nranks : 0) + q]; };
         std::vector<int> span(2 * nranks);
-        AMG_CHECK(hipMemcpyAsync(span.data(), span_dev.p, sizeof(int) * 2 * nranks, hipMemcpyDeviceToHost, s));
-        AMG_CHECK(hipStreamSynchronize(s));
-        // every rank's spans: what each peer needs from me
-        DBuf<int> sp_all;
-        AMG_CHECK(sp_all.alloc(2 * (size_t)nranks * (nranks + 1)));
-        AMG_CHECK(hipMemcpyAsync(sp_all.p, span.data(), sizeof(int) * 2 * nranks, hipMemcpyHostToDevice, s));
-        if ((rc = comm->allgather_bytes(sp_all.p, sp_all.p + 2 * nranks, sizeof(int) * 2 * nranks, s)) != XFK_OK)
-            return rc;
-        std::vector<int> spa(2 * (size_t)nranks * nranks);
-        AMG_CHECK(hipMemcpyAsync(spa.data(), sp_all.p + 2 * nranks, sizeof(int) * spa.size(), hipMemcpyDeviceToHost, s));
-        AMG_CHECK(hipStreamSynchronize(s));
+        for (int q = 0; q < nranks; ++q) {
+            span[q] = span_of(rank, q, false);
+            span[nranks + q] = span_of(rank, q, true);
+        }
         HaloPlan cp;
         std::vector<int> off(nranks, 0);
         int nhc = 0;
@@ -4650,7 +4614,7 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
         }
         for (int r = 0; r < nranks; ++r) {
             if (r == rank) continue;
-            const int lo = spa[2 * (size_t)nranks * r + rank], hi = spa[2 * (size_t)nranks * r + nranks + rank];
+            const int lo = span_of(r, rank, false), hi = span_of(r, rank, true);
             if (lo > hi) continue;
             cp.send.push_back(HaloRange{r, lo - own0, hi - lo + 1, lo});
         }
@@ -4760,11 +4724,9 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
 namespace {
 
 // which: 0 every row; 1 / 2 the interior / boundary tiles of A.ts (tile levels)
-// bh (kResidFromZero on a sharded level): the halo rows' b (k_amg_smooth's HB)
-template <int MODE, bool HB>
-void launch_smooth_h(hipStream_t s, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
-                     const double *x, double *out, double *rout, const int *done, double *part_gam, int which,
-                     const double *bh)
+template <int MODE>
+void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
+                     const double *x, double *out, double *rout, const int *done, double *part_gam, int which)
 {
     const int *tl = nullptr;
     int nt = 0;
@@ -4776,46 +4738,39 @@ void launch_smooth_h(hipStream_t s, int l, const AmgLevel &A, const unsigned lon
     if (l == 0) {
         const int g = tl ? nt : (A.n + kCgBlock - 1) / kCgBlock;
         if (A.has32 && f32_sweep_on())
-            k_amg_smooth<MODE, kCgBlock, 2, float, HB><<<g, kCgBlock, 0, s>>>(
-                A.n, A.ncol_smooth, A.rowptr, A.col, A.a32.p, A.dinv.p, rho, b, x, out, rout, done, part_gam, tl,
-                A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr, bh);
+            k_amg_smooth<MODE, kCgBlock><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.a32.p,
+                                                                A.dinv.p, rho, b, x, out, rout, done, part_gam, tl,
+                                                                A.has16 ? A.a16.p : nullptr,
+                                                                A.has16 ? A.a16b.p : nullptr);
         else
-            k_amg_smooth<MODE, kCgBlock, 2, double, HB><<<g, kCgBlock, 0, s>>>(
-                A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out, rout, done, part_gam, tl,
-                A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr, bh);
+            k_amg_smooth<MODE, kCgBlock><<<g, kCgBlock, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p,
+                                                                rho, b, x, out, rout, done, part_gam, tl,
+                                                                A.has16 ? A.a16.p : nullptr,
+                                                                A.has16 ? A.a16b.p : nullptr);
         return;
     }
     if (A.n >= kTileMinRows) {
         // coarse levels carry 10-16 entries per row: 4 slots per lane, one pass per tile
         const int g = tl ? nt : (A.n + 255) / 256;
         if ((double)A.nnz <= 8.0 * A.n)
-            k_amg_smooth<MODE, 256, 2, double, HB><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val,
-                                                                     A.dinv.p, rho, b, x, out, rout, done, nullptr,
-                                                                     tl, nullptr, nullptr, bh);
+            k_amg_smooth<MODE, 256, 2><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b,
+                                                         x, out, rout, done, nullptr, tl);
         else
-            k_amg_smooth<MODE, 256, 4, double, HB><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val,
-                                                                     A.dinv.p, rho, b, x, out, rout, done, nullptr,
-                                                                     tl, nullptr, nullptr, bh);
+            k_amg_smooth<MODE, 256, 4><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b,
+                                                         x, out, rout, done, nullptr, tl);
         return;
     }
     const int G = lanes_for(A.n > 0 ? (double)A.nnz / A.n : 1.0);
     const int g = (int)(((long long)A.n * G + 255) / 256);
     if (G == 4)
-        k_amg_smooth_g<MODE, 4, HB><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
-                                                     out, rout, done, bh);
+        k_amg_smooth_g<MODE, 4><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
+                                                 rout, done);
     else if (G == 8)
-        k_amg_smooth_g<MODE, 8, HB><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
-                                                     out, rout, done, bh);
+        k_amg_smooth_g<MODE, 8><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x, out,
+                                                 rout, done);
     else
-        k_amg_smooth_g<MODE, 16, HB><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b,
-                                                      x, out, rout, done, bh);
-}
-
-template <int MODE>
-void launch_smooth_t(hipStream_t s, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
-                     const double *x, double *out, double *rout, const int *done, double *part_gam, int which)
-{
-    launch_smooth_h<MODE, false>(s, l, A, rho, b, x, out, rout, done, part_gam, which, nullptr);
+        k_amg_smooth_g<MODE, 16><<<g, 256, 0, s>>>(A.n, A.ncol_smooth, A.rowptr, A.col, A.val, A.dinv.p, rho, b, x,
+                                                  out, rout, done);
 }
 
 void launch_smooth(hipStream_t s, int mode, int l, const AmgLevel &A, const unsigned long long *rho, const double *b,
@@ -5046,21 +5001,12 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
             [&] { launch_smooth(s, mode, l, A, rh, b, x, o, ro, done, pg, 1); },
             [&] { launch_smooth(s, mode, l, A, rh, b, x, o, ro, done, pg, 2); });
     };
-    if (A.hb && sweeps == 1 && !ov) {
-        // b's halo, then r' = b - A x_pre with x_pre = w D^-1 b formed on the
-        // fly for own and halo rows (x_pre itself kept only when unfolded)
-        if ((rc = comm->exchange_to(A.plan_h, b, A.bh.p, s)) != XFK_OK) return nullptr;
-        if (A.n > 0)
-            launch_smooth_h<kResidFromZero, true>(s, l, A, rh, b, nullptr, A.fold ? nullptr : cur, A.r.p, done,
-                                                  nullptr, 0, A.bh.p);
-    } else {
-        if (A.n > 0) k_jacobi_first<<<nb(A.n), kB, 0, s>>>(A.n, rh, A.dinv.p, b, cur, done);
-        for (int k = 1; k < sweeps; ++k) {
-            if ((rc = smooth_after_exchange(kSweep, cur, oth, nullptr, nullptr)) != XFK_OK) return nullptr;
-            std::swap(cur, oth);
-        }
-        if ((rc = smooth_after_exchange(kResid, cur, nullptr, A.r.p, nullptr)) != XFK_OK) return nullptr;
+    if (A.n > 0) k_jacobi_first<<<nb(A.n), kB, 0, s>>>(A.n, rh, A.dinv.p, b, cur, done);
+    for (int k = 1; k < sweeps; ++k) {
+        if ((rc = smooth_after_exchange(kSweep, cur, oth, nullptr, nullptr)) != XFK_OK) return nullptr;
+        std::swap(cur, oth);
     }
+    if ((rc = smooth_after_exchange(kResid, cur, nullptr, A.r.p, nullptr)) != XFK_OK) return nullptr;
     AmgLevel &C = *L[l + 1];
     const int GR = lanes_for(A.nc > 0 ? (double)A.pnnz / A.nc : 1.0);
     const double *xc;
@@ -5206,9 +5152,6 @@ int Amg::refresh(hipStream_t s, bool fold)
     // that unfolds keeps P~'s arrays, so a later one may fold again
     const bool refold = fold && A.fold_formed && !dist && refold_on() && A.fnnz > 0;
     A.fold = refold;
-    // (a sharded level 0 goes back to its own weight and the exchange of
-    // x_pre: the refresh's D^-1 and rho are the rank's own rows')
-    A.hb = false;
     AMG_CHECK(absd.alloc(std::max(1, n)));
     AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(n))));
     if (n > 0) {

@@ -45,9 +45,6 @@ struct xfk_comm {
     int allreduce_sum(const double *send, double *recv, size_t n, hipStream_t s);
     // fill the halo part of vec: every recv range from its peer's matching send range
     int exchange(const xfk::HaloPlan &h, double *vec, hipStream_t s);
-    // the same with the send ranges read from src and the recv ranges written
-    // to dst (offsets as in the plan, each relative to its own buffer)
-    int exchange_to(const xfk::HaloPlan &h, const double *src, double *dst, hipStream_t s);
     // recv[q * n + i] = send_q[i]
     int allgather(const double *send, double *recv, size_t n, hipStream_t s);
     // the same for raw bytes (integer arrays): recv[q * bytes + i] = send_q[i]
@@ -67,7 +64,7 @@ struct xfk_comm {
 
    protected:
     virtual int do_allreduce_sum(const double *send, double *recv, size_t n, hipStream_t s) = 0;
-    virtual int do_exchange(const xfk::HaloPlan &h, const double *src, double *dst, hipStream_t s) = 0;
+    virtual int do_exchange(const xfk::HaloPlan &h, double *vec, hipStream_t s) = 0;
     virtual int do_allgather_bytes(const void *send, void *recv, size_t bytes, hipStream_t s) = 0;
     virtual int do_allgather(const double *send, double *recv, size_t n, hipStream_t s)
     {

@@ -154,13 +154,11 @@ int xfk_comm::allreduce_sum(const double *send, double *recv, size_t n, hipStrea
     return end(s);
 }
 
-int xfk_comm::exchange(const HaloPlan &h, double *vec, hipStream_t s) { return exchange_to(h, vec, vec, s); }
-
-int xfk_comm::exchange_to(const HaloPlan &h, const double *src, double *vec, hipStream_t s)
+int xfk_comm::exchange(const HaloPlan &h, double *vec, hipStream_t s)
 {
     int idx, waited, rc;
     if ((rc = begin(XFK_COMM_EXCHANGE, s, idx, waited)) != XFK_OK) return rc;
-    if ((rc = do_exchange(h, src, vec, s)) != XFK_OK) return rc;
+    if ((rc = do_exchange(h, vec, s)) != XFK_OK) return rc;
     if (rec && rec->mode > 0) {
         const long long seq = (long long)rec->calls.size();
         rec->ops.push_back(
@@ -264,7 +262,7 @@ struct ReplayComm final : xfk_comm {
         int rc = next(XFK_COMM_ALLREDUCE, b, c);
         return rc != XFK_OK ? rc : copy(*c, 0, recv, b, s);
     }
-    int do_exchange(const HaloPlan &h, const double *, double *vec, hipStream_t s) override
+    int do_exchange(const HaloPlan &h, double *vec, hipStream_t s) override
     {
         const CommRecording::Call *c;
         int rc = next(XFK_COMM_EXCHANGE, (long long)h.recv.size(), c);
@@ -300,12 +298,12 @@ struct RcclComm final : xfk_comm {
         XFK_NCCL(ncclAllReduce(send, recv, n, ncclDouble, ncclSum, comm, s));
         return XFK_OK;
     }
-    int do_exchange(const HaloPlan &h, const double *src, double *vec, hipStream_t s) override
+    int do_exchange(const HaloPlan &h, double *vec, hipStream_t s) override
     {
         if (h.send.empty() && h.recv.empty()) return XFK_OK;
         XFK_NCCL(ncclGroupStart());
         for (const HaloRange &r : h.recv) XFK_NCCL(ncclRecv(vec + r.off, r.len, ncclDouble, r.peer, comm, s));
-        for (const HaloRange &t : h.send) XFK_NCCL(ncclSend(src + t.off, t.len, ncclDouble, t.peer, comm, s));
+        for (const HaloRange &t : h.send) XFK_NCCL(ncclSend(vec + t.off, t.len, ncclDouble, t.peer, comm, s));
         XFK_NCCL(ncclGroupEnd());
         return XFK_OK;
     }
@@ -432,9 +430,9 @@ struct LocalComm final : xfk_comm {
             return XFK_OK;
         });
     }
-    int do_exchange(const HaloPlan &h, const double *src, double *vec, hipStream_t s) override
+    int do_exchange(const HaloPlan &h, double *vec, hipStream_t s) override
     {
-        return collective(src, &h, s, "halo exchange", [&]() -> int {
+        return collective(vec, &h, s, "halo exchange", [&]() -> int {
             for (const HaloRange &r : h.recv) {
                 const HaloPlan *peer = hub->plan[r.peer];
                 const HaloRange *t = nullptr;
