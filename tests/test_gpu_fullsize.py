@@ -70,3 +70,28 @@ def test_configs3_full_size_newton_fixed_point():
     res = np.linalg.norm(b - K @ V) / np.linalg.norm(b)
     assert res <= 1e-6, "secant residual %.3e after %d Newton / %d PCG iterations" % (
         res, r["newton_iters"], r["cg_iters"])
+
+
+_CONVERGED = {}
+
+
+@pytest.mark.parametrize("inexact", [True, False])
+def test_nonlinear_180k_matches_converged_oracle(inexact):
+    """configs[3]'s problem at 180k triangles (the largest the CPU oracle runs
+    to convergence in seconds): the device's Newton loop -- inexact passes
+    with a last pass at Precision (the default), or every pass at Precision as
+    the reference's loop -- against the oracle run to Precision 1e-13, at the
+    nonlinear tolerance 1e-5 of max |A| (tests/test_gpu_static2d.py)."""
+    from util import converged
+    pr, mesh, kw = synth_to_oracle(synth.magnetostatic(300, nonlinear=True))
+    P = kernels.Static2DProblem(newton_inexact=inexact, **kw)
+    r = P.solve()
+    A = P.solution()
+    P.close()
+    if "nl180k" not in _CONVERGED:   # (one oracle run for both cases, ~20 s)
+        _CONVERGED["nl180k"] = converged(pr, mesh)
+    Ac = _CONVERGED["nl180k"]
+    err = rel_err(A, Ac)
+    assert r["newton_iters"] >= 3
+    assert err <= 1e-5, "max|A - A_converged| / max|A| = %.3e (%d Newton / %d PCG iterations)" % (
+        err, r["newton_iters"], r["cg_iters"])

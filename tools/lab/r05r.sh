@@ -11,6 +11,6 @@ for v in fold nofold; do
   rc=$?; echo "$v rc=$rc"
   [ $rc -ne 0 ] && exit $rc
   python3 tools/lab/trace_window.py $(ls $O/trace/*/run_kernel_trace.csv $O/trace/run_kernel_trace.csv 2>/dev/null | head -1) $O/err.log > $O/window.txt 2>&1
-  rm -rf $O/trace
+  gzip -f $(ls $O/trace/*/run_kernel_trace.csv $O/trace/run_kernel_trace.csv 2>/dev/null | head -1)
 done
 exit 0

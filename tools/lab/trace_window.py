@@ -14,7 +14,7 @@ def main():
     tag = sys.argv[3] if len(sys.argv) > 3 else None
     win = None
     for line in open(log, errors="replace"):
-        m = re.search(r"\[window\] (\S+) (\d+) (\d+) solves (\d+)", line)
+        m = re.search(r"\[window\] (.+?) (\d+) (\d+) solves (\d+)", line)
         if m and (tag is None or m.group(1) == tag):
             win = (int(m.group(2)), int(m.group(3)), int(m.group(4)))
     if win is None:

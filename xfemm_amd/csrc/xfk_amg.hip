@@ -4380,17 +4380,35 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
 namespace {
 
 // per peer: the smallest and largest of its ids this rank's columns reference
-__global__ void k_peer_span(long long nnz, const int *__restrict__ col, int own0, int own1,
-                            const int *__restrict__ c0, int nranks, int *lo, int *hi)
+// (reduced per workgroup in LDS first: the entries of one peer all hit the
+// same two words, and one global atomic per entry serialised ~150 us per call
+// at configs[4] / 8 ranks)
+constexpr int kSpanRanks = 64;
+__global__ void __launch_bounds__(kB) k_peer_span(long long nnz, const int *__restrict__ col, int own0, int own1,
+                                                  const int *__restrict__ c0, int nranks, int *lo, int *hi)
 {
+    __shared__ int slo[kSpanRanks], shi[kSpanRanks];
+    for (int q = threadIdx.x; q < kSpanRanks; q += blockDim.x) {
+        slo[q] = INT_MAX;
+        shi[q] = -1;
+    }
+    __syncthreads();
     const long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (e >= nnz) return;
-    const int J = col[e];
-    if (J >= own0 && J < own1) return;
-    int q = 0;
-    while (c0[q + 1] <= J) ++q;
-    atomicMin(&lo[q], J);
-    atomicMax(&hi[q], J);
+    if (e < nnz) {
+        const int J = col[e];
+        if (J < own0 || J >= own1) {
+            int q = 0;
+            while (c0[q + 1] <= J) ++q;
+            atomicMin(&slo[q], J);
+            atomicMax(&shi[q], J);
+        }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < nranks; q += blockDim.x)
+        if (shi[q] >= 0) {
+            atomicMin(&lo[q], slo[q]);
+            atomicMax(&hi[q], shi[q]);
+        }
 }
 // global ids -> local: own rows first, then the peers' spans in peer order
 __global__ void k_localize(long long nnz, int *__restrict__ col, int own0, int own1, int n,
@@ -4428,6 +4446,10 @@ int Amg::galerkin_dist(hipStream_t s, int l, int st, bool &rep)
     const int n = A.n, nh = A.ncol_smooth - A.n;
     const int nc = st ? 0 : A.nc;
     std::vector<double> all;
+    if (nranks > kSpanRanks) {   // (same on every rank)
+        set_error("AMG: a sharded hierarchy of more than 64 ranks");
+        return XFK_ERR_UNSUPPORTED;
+    }
     // 1. aggregate counts and status of every rank
     {
         const double mine[2] = {(double)nc, (double)st};
