@@ -159,6 +159,23 @@ hipError_t dev_malloc(void **p, size_t bytes)
     return hipSuccess;
 }
 
+hipError_t DevArena::reserve(size_t bytes)
+{
+    const size_t at = (off + kArenaAlign - 1) & ~(kArenaAlign - 1);
+    if (bytes == 0 || (!chunks.empty() && at + bytes <= chunks.back().second)) return hipSuccess;
+    DevArena *cur = tl_arena;
+    tl_arena = nullptr;   // (the chunk itself comes from the process cache or hipMalloc)
+    void *c = nullptr;
+    const size_t csz = ((bytes + kArenaAlign - 1) & ~(kArenaAlign - 1)) + kArenaAlign;
+    const hipError_t e = pool_malloc(&c, csz);
+    tl_arena = cur;
+    if (e != hipSuccess) return e;
+    chunks.push_back({static_cast<char *>(c), csz});
+    off = kArenaAlign;   // (carving starts one alignment step in, as in dev_malloc)
+    next_chunk = kArenaChunk;
+    return hipSuccess;
+}
+
 bool DevArena::retire(void *p)
 {
     auto it = carved.find(p);
@@ -2291,6 +2308,31 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     return XFK_OK;
 }
 
+// The first solve's device footprint, reserved in the problem's arena at
+// creation (outside any solve), so that the solve carves its buffers without a
+// hipMalloc (16 calls, 0.34 ms of a configs[2] first solve): 4.32 GB of chunks
+// at 1.0M rows (configs[2]), 0.50 GB at 103k rows (tools/lab/mem_probe.py,
+// profiles/r05t_mem_probe.txt) -- ~4.4 kB per owned row.  A larger solve takes
+// further chunks as before.  XFK_ARENA_RESERVE=0: no reservation.
+static int reserve_first_solve(xfk_problem **out)
+{
+    xfk_problem *P = *out;
+    static const long long per_row = [] {
+        const char *e = std::getenv("XFK_ARENA_RESERVE");
+        return e ? std::atoll(e) : 4400LL;
+    }();
+    if (!P || per_row <= 0) return XFK_OK;
+    XFK_CHECK(hipSetDevice(P->device));
+    const hipError_t e = P->arena.reserve((size_t)per_row * (size_t)std::max(0, P->N) + (64ull << 20));
+    if (e != hipSuccess) {
+        xfk_problem_destroy(P);
+        *out = nullptr;
+        set_error(std::string("arena reservation failed: ") + hipGetErrorString(e));
+        return XFK_ERR_HIP;
+    }
+    return XFK_OK;
+}
+
 }  // namespace xfk
 
 extern "C" {
@@ -2314,6 +2356,8 @@ int xfk_problem_create(const xfk_problem_desc *d, int device, xfk_problem **out)
     tr.mark("magdir + air gaps");
     rc = build_local(d, G, nullptr, device, nullptr, out);
     tr.mark("build_local");
+    if (rc == XFK_OK) rc = reserve_first_solve(out);
+    tr.mark("arena reserve");
     return rc;
 }
 
@@ -2402,7 +2446,8 @@ int xfk_problem_create_dist(const xfk_problem_desc *d, int device, xfk_comm *com
     if (rc != XFK_OK) return rc;
     PartPlan plan;
     if ((rc = plan_rank(d, G, comm, plan)) != XFK_OK) return rc;
-    return build_local(d, G, &plan, device, comm, out);
+    rc = build_local(d, G, &plan, device, comm, out);
+    return rc == XFK_OK ? reserve_first_solve(out) : rc;
 }
 
 int xfk_dist_get_info(const xfk_problem *P, xfk_dist_info *info)

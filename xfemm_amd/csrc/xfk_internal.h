@@ -202,6 +202,10 @@ struct DevArena {
     std::multimap<size_t, char *> reuse;              // freed blocks no device work can read any more
     std::vector<std::pair<char *, size_t>> pending;   // freed during the current solve
     size_t chunk_bytes() const;
+    // room for `bytes` more in the last chunk (a new chunk of that size
+    // otherwise): a problem's creation reserves its first solve's footprint,
+    // so the solve carves without a hipMalloc
+    hipError_t reserve(size_t bytes);
     void release();   // (the problem's device work finished)
     void recycle();   // (every stream of the problem idle) pending -> reuse
     bool retire(void *p);   // p carved here: pending until the next recycle()
