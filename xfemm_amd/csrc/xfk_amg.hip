@@ -3024,28 +3024,35 @@ int build_tile_split(hipStream_t s, int n, int B, const int *rowptr, const int *
 
 namespace {
 std::mutex g_pool_mu;
-std::map<hipStream_t, int> g_pool_dev;                 // every pooled stream -> its device
-std::map<int, std::vector<hipStream_t>> g_pool_free;   // idle streams per device
+std::map<hipStream_t, int> g_pool_dev;                 // every pooled stream -> its pool (2 device + high)
+std::map<int, std::vector<hipStream_t>> g_pool_free;   // idle streams per pool
 }  // namespace
 
-hipError_t stream_acquire(hipStream_t *s)
+hipError_t stream_acquire(hipStream_t *s, bool high)
 {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
+    const int key = 2 * dev + (high ? 1 : 0);
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
-        auto &f = g_pool_free[dev];
+        auto &f = g_pool_free[key];
         if (!f.empty()) {
             *s = f.back();
             f.pop_back();
             return hipSuccess;
         }
     }
-    e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    if (high) {
+        int lo = 0, hi = 0;
+        e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+    } else {
+        e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    }
     if (e == hipSuccess) {
         std::lock_guard<std::mutex> lk(g_pool_mu);
-        g_pool_dev[*s] = dev;
+        g_pool_dev[*s] = key;
     }
     return e;
 }
@@ -3085,10 +3092,23 @@ long long stream_pool_idle()
     return n;
 }
 
+// the setup's side stream at the device's greatest priority, so that its
+// short chains (R = P^T, the folded transfers) are dispatched between the
+// workgroups of the main stream's SpGEMMs instead of after them
+// (XFK_SIDE_PRIO=0: default priority)
+static bool side_prio_on()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("XFK_SIDE_PRIO");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+
 int SideStream::init()
 {
     if (cs) return XFK_OK;
-    AMG_CHECK(stream_acquire(&cs));
+    AMG_CHECK(stream_acquire(&cs, side_prio_on()));
     AMG_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
     AMG_CHECK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
     AMG_CHECK(hipEventCreateWithFlags(&c, hipEventDisableTiming));

@@ -349,7 +349,125 @@ void pinned_free(void *p)
 thread_local PhaseProf *g_prof = nullptr;
 void set_error(const std::string &msg) { g_err = msg; }
 
-using Terms = std::vector<std::pair<long long, double>>;
+// Symbolic composition of CBigLinProb::Periodicity / AntiPeriodicity
+// (spars.cpp:366-474) applied in pbclist order (static2d.cpp:929-940).  Each
+// touched matrix entry / RHS entry becomes a linear combination of the
+// post-Dirichlet values; sets of rows k are structural supersets of the
+// reference's value-based scan, which is exact because averaging zeros gives
+// zero.
+//
+// Storage: every combination is an immutable run of (key, weight) terms in
+// one pool (a handle = offset + length; entries that share a combination
+// share the run), the current combination of each entry / RHS row sits in an
+// open-addressing table, and the neighbour sets of the coupled nodes are
+// indexed by a dense node -> slot array -- no allocation per entry (the
+// per-entry vectors and node maps cost ~12 ms on the 2250 pairs of the
+// refined TorqueBenchmark).
+namespace {
+using Term = std::pair<long long, double>;
+struct TRun {
+    unsigned off = 0, len = 0;
+};
+struct TermPool {
+    std::vector<Term> t;
+    // a x + b y of two runs sorted by key (every run is: a single term or
+    // lin2's own output), merged -- a key in both gets a x + b y, in one a x
+    // or b y, as the accumulation into a zeroed map gives; zeros dropped
+    TRun lin2(double a, TRun x, double b, TRun y)
+    {
+        if (t.capacity() < t.size() + x.len + y.len) t.reserve(2 * (t.size() + x.len + y.len));
+        const Term *xp = t.data() + x.off, *yp = t.data() + y.off;
+        TRun out{(unsigned)t.size(), 0};
+        unsigned i = 0, j = 0;
+        while (i < x.len || j < y.len) {
+            double v;
+            long long k;
+            if (j == y.len || (i < x.len && xp[i].first < yp[j].first)) {
+                k = xp[i].first;
+                v = a * xp[i++].second;
+            } else if (i == x.len || yp[j].first < xp[i].first) {
+                k = yp[j].first;
+                v = b * yp[j++].second;
+            } else {
+                k = xp[i].first;
+                v = a * xp[i++].second + b * yp[j++].second;
+            }
+            if (v != 0.0) t.push_back({k, v});   // (capacity reserved: xp, yp stay valid)
+        }
+        out.len = (unsigned)t.size() - out.off;
+        return out;
+    }
+    TRun single(long long k)
+    {
+        t.push_back({k, 1.0});
+        return TRun{(unsigned)t.size() - 1, 1};
+    }
+};
+// key (>= 0) -> run, linear probing
+struct RunMap {
+    std::vector<long long> key;
+    std::vector<TRun> val;
+    size_t n = 0;
+    int shift = 60;
+    explicit RunMap(size_t expect)
+    {
+        size_t c = 16;
+        while (c < 2 * expect) c <<= 1;
+        alloc(c);
+    }
+    void alloc(size_t c)
+    {
+        key.assign(c, -1);
+        val.assign(c, TRun{});
+        shift = 64 - __builtin_ctzll(c);
+    }
+    size_t home(long long k) const { return (size_t)(((unsigned long long)k * 0x9E3779B97F4A7C15ULL) >> shift); }
+    const TRun *find(long long k) const
+    {
+        const size_t m = key.size() - 1;
+        for (size_t h = home(k);; h = (h + 1) & m) {
+            if (key[h] == k) return &val[h];
+            if (key[h] < 0) return nullptr;
+        }
+    }
+    void put(long long k, TRun v)
+    {
+        if (2 * (n + 1) > key.size()) {
+            std::vector<long long> ok;
+            std::vector<TRun> ov;
+            ok.swap(key);
+            ov.swap(val);
+            alloc(2 * ok.size());
+            n = 0;
+            for (size_t h = 0; h < ok.size(); ++h)
+                if (ok[h] >= 0) put(ok[h], ov[h]);
+        }
+        const size_t m = key.size() - 1;
+        for (size_t h = home(k);; h = (h + 1) & m) {
+            if (key[h] == k) {
+                val[h] = v;
+                return;
+            }
+            if (key[h] < 0) {
+                key[h] = k;
+                val[h] = v;
+                ++n;
+                return;
+            }
+        }
+    }
+    // (key, run) pairs in ascending key order
+    std::vector<std::pair<long long, TRun>> sorted() const
+    {
+        std::vector<std::pair<long long, TRun>> o;
+        o.reserve(n);
+        for (size_t h = 0; h < key.size(); ++h)
+            if (key[h] >= 0) o.push_back({key[h], val[h]});
+        std::sort(o.begin(), o.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+        return o;
+    }
+};
+}  // namespace
 
 static inline long long ukey(int r, int c)
 {
@@ -359,38 +477,6 @@ static inline long long ukey(int r, int c)
 
 static inline long long okey(int r, int c) { return ((long long)r << 32) | (unsigned)c; }
 
-// a x + b y of two combinations sorted by key (every Terms is: the single
-// terms and lin2's own output), merged -- a key in both gets a x + b y, in
-// one a x or b y, as the accumulation into a zeroed map gives; zeros dropped
-static Terms lin2(double a, const Terms &x, double b, const Terms &y)
-{
-    Terms out;
-    out.reserve(x.size() + y.size());
-    size_t i = 0, j = 0;
-    while (i < x.size() || j < y.size()) {
-        double v;
-        long long k;
-        if (j == y.size() || (i < x.size() && x[i].first < y[j].first)) {
-            k = x[i].first;
-            v = a * x[i++].second;
-        } else if (i == x.size() || y[j].first < x[i].first) {
-            k = y[j].first;
-            v = b * y[j++].second;
-        } else {
-            k = x[i].first;
-            v = a * x[i++].second + b * y[j++].second;
-        }
-        if (v != 0.0) out.push_back({k, v});
-    }
-    return out;
-}
-
-// Symbolic composition of CBigLinProb::Periodicity / AntiPeriodicity
-// (spars.cpp:366-474) applied in pbclist order (static2d.cpp:929-940).  Each
-// touched matrix entry / RHS entry becomes a linear combination of the
-// post-Dirichlet values; sets of rows k are structural supersets of the
-// reference's value-based scan, which is exact because averaging zeros gives
-// zero.
 // small sorted neighbour sets (a node has ~6-20 neighbours): sorted vectors
 using NbSet = std::vector<int>;
 static inline void nb_insert(NbSet &v, int x)
@@ -404,162 +490,172 @@ static int build_pbc_map(xfk_problem *P, bool aux)
 {
     const int npbc = (int)P->hpbc.size() / 3;
     if (npbc == 0) return XFK_OK;
-    std::unordered_map<int, NbSet> N0;  // original neighbours of pbc nodes
+    CreateTrace tr;
+    for (int q = 0; q < npbc; ++q) {
+        const int i = P->hpbc[3 * q], j = P->hpbc[3 * q + 1], t = P->hpbc[3 * q + 2];
+        if ((t == 0 || t == 1) && (i < 0 || j < 0 || i >= P->NL || j >= P->NL)) {
+            set_error("pbc node index out of range");
+            return XFK_ERR_ARG;
+        }
+    }
+    // original neighbours of the coupled nodes (slot[v] >= 0), then the current ones
+    std::vector<int> slot(std::max(1, P->NL), -1);
+    std::vector<NbSet> N0;
     N0.reserve(2 * (size_t)npbc);
-    std::vector<char> ispbc(std::max(1, P->NL), 0);
     for (int k = 0; k < npbc; ++k)
         for (int m = 0; m < 2; ++m) {
             const int v = P->hpbc[3 * k + m];
-            N0[v];
-            if (v >= 0 && v < P->NL) ispbc[v] = 1;
+            if (v >= 0 && v < P->NL && slot[v] < 0) {
+                slot[v] = (int)N0.size();
+                N0.emplace_back();
+            }
         }
     for (int e = 0; e < P->NE; ++e)
         for (int j = 0; j < 3; ++j) {
             const int v = P->hp[3 * e + j];
-            if (v < 0 || v >= P->NL || !ispbc[v]) continue;
-            auto it = N0.find(v);
+            if (v < 0 || v >= P->NL || slot[v] < 0) continue;
+            NbSet &s = N0[slot[v]];
             for (int m = 0; m < 3; ++m)
-                if (m != j) nb_insert(it->second, P->hp[3 * e + m]);
+                if (m != j) nb_insert(s, P->hp[3 * e + m]);
         }
+    auto slot_of = [&](int v) { return (v >= 0 && v < P->NL) ? slot[v] : -1; };
     for (long long k : P->age_key) {   // air-gap couplings are entries of the matrix too
         const int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
         if (r == c) continue;
-        auto it = N0.find(r);
-        if (it != N0.end()) nb_insert(it->second, c);
-        it = N0.find(c);
-        if (it != N0.end()) nb_insert(it->second, r);
+        if (slot_of(r) >= 0) nb_insert(N0[slot_of(r)], c);
+        if (slot_of(c) >= 0) nb_insert(N0[slot_of(c)], r);
     }
-    std::unordered_map<int, NbSet> Ncur = N0;
-    std::unordered_map<long long, Terms> E;
-    E.reserve(16 * (size_t)npbc);
-    std::unordered_map<int, Terms> Eb;
-    Eb.reserve(2 * (size_t)npbc);
-    std::set<long long> fill;
+    tr.mark("    pbc neighbour sets");
+    std::vector<NbSet> Ncur = N0;
+    TermPool pool;
+    pool.t.reserve(64 * (size_t)npbc);
+    RunMap E(16 * (size_t)npbc), Eb(2 * (size_t)npbc);
+    std::vector<long long> fill;
     auto is_orig = [&](int r, int c) -> bool {
         if (r == c) return true;
-        auto it = N0.find(r);
-        if (it != N0.end()) return nb_has(it->second, c);
-        it = N0.find(c);
-        if (it != N0.end()) return nb_has(it->second, r);
+        int s = slot_of(r);
+        if (s >= 0) return nb_has(N0[s], c);
+        s = slot_of(c);
+        if (s >= 0) return nb_has(N0[s], r);
         return false;
     };
     // the current combination of entry (r, c): the map's, else the entry itself
-    // (an original one) or nothing -- as a reference (tmp holds the implicit one)
-    auto get = [&](int r, int c, Terms &tmp) -> const Terms & {
+    // (an original one) or nothing
+    auto get = [&](int r, int c) -> TRun {
         const long long k = ukey(r, c);
-        auto it = E.find(k);
-        if (it != E.end()) return it->second;
-        tmp.clear();
-        if (is_orig(r, c)) tmp.push_back({k, 1.0});
-        return tmp;
+        if (const TRun *h = E.find(k)) return *h;
+        if (is_orig(r, c)) return pool.single(k);
+        return TRun{};
     };
     // auxiliary matrices of the Newton AC solver: ordered entries
-    std::unordered_map<long long, Terms> Ea;
-    std::set<long long> afill;
-    auto geta = [&](int r, int c) -> Terms {
-        long long k = okey(r, c);
-        auto it = Ea.find(k);
-        if (it != Ea.end()) return it->second;
-        if (is_orig(r, c)) return Terms{{k, 1.0}};
-        return Terms{};
+    RunMap Ea(aux ? 32 * (size_t)npbc : 1);
+    std::vector<long long> afill;
+    auto geta = [&](int r, int c) -> TRun {
+        const long long k = okey(r, c);
+        if (const TRun *h = Ea.find(k)) return *h;
+        if (is_orig(r, c)) return pool.single(k);
+        return TRun{};
     };
-    auto getb = [&](int i) -> Terms {
-        auto it = Eb.find(i);
-        if (it != Eb.end()) return it->second;
-        return Terms{{(long long)i, 1.0}};
+    auto getb = [&](int i) -> TRun {
+        if (const TRun *h = Eb.find(i)) return *h;
+        return pool.single(i);
     };
-    Terms t1, t2;
+    const TRun none{};
+    NbSet K;
     for (int q = 0; q < npbc; ++q) {
         int i = P->hpbc[3 * q], j = P->hpbc[3 * q + 1], t = P->hpbc[3 * q + 2];
         if (t != 0 && t != 1) continue;  // static2d.cpp:932-939 only handles 0 and 1
-        if (i < 0 || j < 0 || i >= P->NL || j >= P->NL) {
-            set_error("pbc node index out of range");
-            return XFK_ERR_ARG;
-        }
         if (j < i) std::swap(i, j);
         const double sg = (t == 0) ? 1.0 : -1.0;
-        NbSet K;
-        {
-            const NbSet &a = Ncur[i], &b = Ncur[j];
-            std::set_union(a.begin(), a.end(), b.begin(), b.end(), std::back_inserter(K));
-            K.erase(std::remove_if(K.begin(), K.end(), [&](int x) { return x == i || x == j; }), K.end());
-        }
+        NbSet &Ni = Ncur[slot[i]], &Nj = Ncur[slot[j]];
+        K.clear();
+        std::set_union(Ni.begin(), Ni.end(), Nj.begin(), Nj.end(), std::back_inserter(K));
+        K.erase(std::remove_if(K.begin(), K.end(), [&](int x) { return x == i || x == j; }), K.end());
         for (int k : K) {
-            Terms c = lin2(0.5, get(k, i, t1), 0.5 * sg, get(k, j, t2));
-            if (sg > 0) {
-                E[ukey(k, j)] = c;
-            } else {
-                Terms cn = lin2(-1.0, c, 0.0, Terms{});
-                E[ukey(k, j)] = std::move(cn);
-            }
-            E[ukey(k, i)] = std::move(c);
+            const TRun c = pool.lin2(0.5, get(k, i), 0.5 * sg, get(k, j));
+            E.put(ukey(k, j), sg > 0 ? c : pool.lin2(-1.0, c, 0.0, none));
+            E.put(ukey(k, i), c);
             if (aux) {   // row k and, by the Hermitian / anti-Hermitian flip of Put, column k
-                Terms ca = lin2(0.5, geta(k, i), 0.5 * sg, geta(k, j));
-                Terms ct = lin2(0.5, geta(i, k), 0.5 * sg, geta(j, k));
-                Ea[okey(k, i)] = ca;
-                Ea[okey(k, j)] = lin2(sg, ca, 0.0, Terms{});
-                Ea[okey(i, k)] = ct;
-                Ea[okey(j, k)] = lin2(sg, ct, 0.0, Terms{});
+                const TRun ca = pool.lin2(0.5, geta(k, i), 0.5 * sg, geta(k, j));
+                const TRun ct = pool.lin2(0.5, geta(i, k), 0.5 * sg, geta(j, k));
+                Ea.put(okey(k, i), ca);
+                Ea.put(okey(k, j), pool.lin2(sg, ca, 0.0, none));
+                Ea.put(okey(i, k), ct);
+                Ea.put(okey(j, k), pool.lin2(sg, ct, 0.0, none));
             }
             for (int m : {i, j})
-                if (!is_orig(k, m)) fill.insert(ukey(k, m));
-            nb_insert(Ncur[i], k);
-            nb_insert(Ncur[j], k);
-            auto itk = Ncur.find(k);
-            if (itk != Ncur.end()) {
-                nb_insert(itk->second, i);
-                nb_insert(itk->second, j);
+                if (!is_orig(k, m)) fill.push_back(ukey(k, m));
+            nb_insert(Ni, k);
+            nb_insert(Nj, k);
+            const int sk = slot_of(k);
+            if (sk >= 0) {
+                nb_insert(Ncur[sk], i);
+                nb_insert(Ncur[sk], j);
             }
         }
-        Terms d = lin2(0.5, get(i, i, t1), 0.5, get(j, j, t2));
-        E[ukey(i, i)] = d;
-        E[ukey(j, j)] = std::move(d);
+        const TRun d = pool.lin2(0.5, get(i, i), 0.5, get(j, j));
+        E.put(ukey(i, i), d);
+        E.put(ukey(j, j), d);
         if (aux) {   // auxiliary (i, j) block: c = (ii +- ij +- ji + jj) / 4 at ii, jj and +-c at ij, ji
-            Terms da = lin2(0.25, lin2(1.0, geta(i, i), sg, geta(i, j)), 0.25, lin2(sg, geta(j, i), 1.0, geta(j, j)));
-            Ea[okey(i, i)] = da;
-            Ea[okey(j, j)] = da;
-            Ea[okey(i, j)] = lin2(sg, da, 0.0, Terms{});
-            Ea[okey(j, i)] = lin2(sg, da, 0.0, Terms{});
-            if (!is_orig(i, j) && !fill.count(ukey(i, j))) afill.insert(ukey(i, j));
+            const TRun l1 = pool.lin2(1.0, geta(i, i), sg, geta(i, j));
+            const TRun l2 = pool.lin2(sg, geta(j, i), 1.0, geta(j, j));
+            const TRun da = pool.lin2(0.25, l1, 0.25, l2);
+            Ea.put(okey(i, i), da);
+            Ea.put(okey(j, j), da);
+            Ea.put(okey(i, j), pool.lin2(sg, da, 0.0, none));
+            Ea.put(okey(j, i), pool.lin2(sg, da, 0.0, none));
+            if (!is_orig(i, j)) afill.push_back(ukey(i, j));   // (those in the fill-in are dropped below)
         }
-        Terms bi = getb(i), bj = getb(j);
-        Terms c = lin2(0.5, bi, 0.5 * sg, bj);
-        Eb[i] = c;
-        Eb[j] = (sg > 0) ? c : lin2(-1.0, c, 0.0, Terms{});
+        const TRun bi = getb(i), bj = getb(j);
+        const TRun c = pool.lin2(0.5, bi, 0.5 * sg, bj);
+        Eb.put(i, c);
+        Eb.put(j, (sg > 0) ? c : pool.lin2(-1.0, c, 0.0, none));
     }
-    P->pbc_fill.assign(fill.begin(), fill.end());
-    P->pbc_entry_key.clear();
-    P->pbc_entry_terms.clear();
-    std::vector<long long> keys;
-    for (auto &kv : E) keys.push_back(kv.first);
-    std::sort(keys.begin(), keys.end());
-    for (long long k : keys) {
-        P->pbc_entry_key.push_back(k);
-        P->pbc_entry_terms.push_back(E[k]);
+    tr.mark("    pbc composition");
+    std::sort(fill.begin(), fill.end());
+    fill.erase(std::unique(fill.begin(), fill.end()), fill.end());
+    P->pbc_fill = fill;
+    auto flatten = [&](const RunMap &M, std::vector<long long> &keys, std::vector<int> &ptr, std::vector<Term> &terms) {
+        const auto o = M.sorted();
+        keys.resize(o.size());
+        ptr.assign(1, 0);
+        ptr.reserve(o.size() + 1);
+        terms.clear();
+        for (size_t m = 0; m < o.size(); ++m) {
+            keys[m] = o[m].first;
+            terms.insert(terms.end(), pool.t.begin() + o[m].second.off,
+                         pool.t.begin() + o[m].second.off + o[m].second.len);
+            ptr.push_back((int)terms.size());
+        }
+    };
+    flatten(E, P->pbc_entry_key, P->pbc_entry_ptr, P->pbc_entry_terms);
+    if (aux) {
+        flatten(Ea, P->pbca_entry_key, P->pbca_entry_ptr, P->pbca_entry_terms);
+    } else {
+        P->pbca_entry_key.clear();
+        P->pbca_entry_ptr.assign(1, 0);
+        P->pbca_entry_terms.clear();
     }
-    P->pbca_entry_key.clear();
-    P->pbca_entry_terms.clear();
-    keys.clear();
-    for (auto &kv : Ea) keys.push_back(kv.first);
-    std::sort(keys.begin(), keys.end());
-    for (long long k : keys) {
-        P->pbca_entry_key.push_back(k);
-        P->pbca_entry_terms.push_back(Ea[k]);
-    }
+    std::sort(afill.begin(), afill.end());
+    afill.erase(std::unique(afill.begin(), afill.end()), afill.end());
     P->pbca_fill.clear();
     for (long long k : afill)
-        if (!fill.count(k)) P->pbca_fill.push_back(k);
-    P->pbc_b_key.clear();
-    P->pbc_b_terms.clear();
-    std::vector<int> bk;
-    for (auto &kv : Eb) bk.push_back(kv.first);
-    std::sort(bk.begin(), bk.end());
-    for (int k : bk) {
-        P->pbc_b_key.push_back(k);
-        std::vector<std::pair<int, double>> tt;
-        for (auto &t : Eb[k]) tt.push_back({(int)t.first, t.second});
-        P->pbc_b_terms.push_back(tt);
+        if (!std::binary_search(fill.begin(), fill.end(), k)) P->pbca_fill.push_back(k);
+    {
+        const auto o = Eb.sorted();
+        P->pbc_b_key.resize(o.size());
+        P->pbc_b_ptr.assign(1, 0);
+        P->pbc_b_terms.clear();
+        for (size_t m = 0; m < o.size(); ++m) {
+            P->pbc_b_key[m] = (int)o[m].first;
+            for (unsigned u = 0; u < o[m].second.len; ++u) {
+                const Term &t = pool.t[o[m].second.off + u];
+                P->pbc_b_terms.push_back({(int)t.first, t.second});
+            }
+            P->pbc_b_ptr.push_back((int)P->pbc_b_terms.size());
+        }
     }
+    tr.mark("    pbc sorted output");
     return XFK_OK;
 }
 
@@ -910,7 +1006,7 @@ int build_symbolic(xfk_problem *P)
         for (size_t m = 0; m < P->pbc_entry_key.size(); ++m) {
             long long k = P->pbc_entry_key[m];
             int r = (int)(k >> 32), c = (int)(k & 0xffffffff);
-            const Terms &tt = P->pbc_entry_terms[m];
+            const int t0 = P->pbc_entry_ptr[m], t1 = P->pbc_entry_ptr[m + 1];
             // one gather entry per destination slot (both triangles) in an
             // assembled row; a source (symmetric before the map) is read in
             // whichever orientation lies in an assembled row -- one of its
@@ -921,7 +1017,8 @@ int build_symbolic(xfk_problem *P)
                 if (dr >= N) continue;
                 rc_dst.push_back(dr);
                 rc_dst.push_back(dc);
-                for (auto &t : tt) {
+                for (int u = t0; u < t1; ++u) {
+                    const auto &t = P->pbc_entry_terms[u];
                     const int a = (int)(t.first >> 32), b2 = (int)(t.first & 0xffffffff);
                     src_rc.push_back(a < N ? a : b2);
                     src_rc.push_back(a < N ? b2 : a);
@@ -954,7 +1051,8 @@ int build_symbolic(xfk_problem *P)
         std::vector<double> bw;
         for (size_t m = 0; m < P->pbc_b_key.size(); ++m) {
             bd.push_back(P->pbc_b_key[m]);
-            for (auto &t : P->pbc_b_terms[m]) {
+            for (int u = P->pbc_b_ptr[m]; u < P->pbc_b_ptr[m + 1]; ++u) {
+                const auto &t = P->pbc_b_terms[u];
                 bsrc.push_back(t.first);
                 bw.push_back(t.second);
             }
@@ -982,7 +1080,8 @@ int build_symbolic(xfk_problem *P)
             if ((int)(k >> 32) >= N) continue;
             rc_dst.push_back((int)(k >> 32));
             rc_dst.push_back((int)(k & 0xffffffff));
-            for (auto &t : P->pbca_entry_terms[m]) {
+            for (int u = P->pbca_entry_ptr[m]; u < P->pbca_entry_ptr[m + 1]; ++u) {
+                const auto &t = P->pbca_entry_terms[u];
                 src_rc.push_back((int)(t.first >> 32));
                 src_rc.push_back((int)(t.first & 0xffffffff));
                 w.push_back(t.second);
@@ -2258,8 +2357,9 @@ int build_local(const xfk_problem_desc *d, const GlobalPrep &G, const PartPlan *
     if (rc != XFK_OK) return fail(rc);
     tr.mark("  periodic map");
     if (tr.on)
-        std::fprintf(stderr, "[create]     %zu pairs, %zu entries, %zu fill, %zu age couplings\n", P->hpbc.size() / 3,
-                     P->pbc_entry_key.size(), P->pbc_fill.size(), P->age_key.size());
+        std::fprintf(stderr, "[create]     %zu pairs, %zu entries (%zu terms), %zu fill, %zu age couplings\n",
+                     P->hpbc.size() / 3, P->pbc_entry_key.size(), P->pbc_entry_terms.size(), P->pbc_fill.size(),
+                     P->age_key.size());
     add_age_fill(P);
     tr.mark("  air-gap fill");
 

@@ -284,7 +284,8 @@ void host_par_for(long long n, long long min_per_thread, F f)
 // Process-wide pool of non-blocking streams on the current device: creating a
 // HIP stream costs ~4 ms on MI355X (a hardware queue), so a problem returns its
 // streams here when it is destroyed and the next problem takes them back.
-hipError_t stream_acquire(hipStream_t *s);
+// high: a stream of the device's greatest priority (its own pool)
+hipError_t stream_acquire(hipStream_t *s, bool high = false);
 void stream_release(hipStream_t s);   // idle streams only (the caller synchronised it)
 void stream_pool_drain();
 // xfk_sort.hip: the reference's comb sort of the element scores on the device
@@ -426,15 +427,19 @@ struct xfk_problem {
     xfk::DBuf<int> age_slot;           // CSR slot of every full-storage air-gap entry
     xfk::DBuf<double> age_v;
     int age_n = 0;
-    std::vector<std::vector<std::pair<long long, double>>> pbc_entry_terms;  // host form
+    // host form, entry m's terms at [pbc_entry_ptr[m], pbc_entry_ptr[m + 1]) of pbc_entry_terms
+    std::vector<std::pair<long long, double>> pbc_entry_terms;
+    std::vector<int> pbc_entry_ptr;
     std::vector<long long> pbc_entry_key;
-    std::vector<std::vector<std::pair<int, double>>> pbc_b_terms;
+    std::vector<std::pair<int, double>> pbc_b_terms;   // (the same layout, pbc_b_ptr)
+    std::vector<int> pbc_b_ptr;
     std::vector<int> pbc_b_key;
     // the same composition for the Newton AC solver's auxiliary matrices
     // (cspars.cpp:648-670, 732-754): ordered (row, col) entries -- they are
     // Hermitian / anti-Hermitian, not symmetric -- whose (i, j) block of each
     // pair is the mean of its four entries; the entries (i, j) it creates
-    std::vector<std::vector<std::pair<long long, double>>> pbca_entry_terms;
+    std::vector<std::pair<long long, double>> pbca_entry_terms;   // (pbca_entry_ptr)
+    std::vector<int> pbca_entry_ptr;
     std::vector<long long> pbca_entry_key;
     std::vector<long long> pbca_fill;
     xfk::DBuf<int> pa_dst, pa_ptr, pa_src;
