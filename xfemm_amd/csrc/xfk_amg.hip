@@ -3092,23 +3092,10 @@ long long stream_pool_idle()
     return n;
 }
 
-// the setup's side stream at the device's greatest priority, so that its
-// short chains (R = P^T, the folded transfers) are dispatched between the
-// workgroups of the main stream's SpGEMMs instead of after them
-// (XFK_SIDE_PRIO=0: default priority)
-static bool side_prio_on()
-{
-    static const bool v = [] {
-        const char *e = std::getenv("XFK_SIDE_PRIO");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return v;
-}
-
 int SideStream::init()
 {
     if (cs) return XFK_OK;
-    AMG_CHECK(stream_acquire(&cs, side_prio_on()));
+    AMG_CHECK(stream_acquire(&cs));
     AMG_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
     AMG_CHECK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
     AMG_CHECK(hipEventCreateWithFlags(&c, hipEventDisableTiming));
