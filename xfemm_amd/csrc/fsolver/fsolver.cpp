@@ -376,6 +376,18 @@ void par_for(long long n, long long min_per_thread, F f)
     pool.run(T, [&](int t) { f(n * t / T, n * (t + 1) / T); });
 }
 
+// v = n copies of val, the storage first-touched by the pool's threads
+template <class T>
+void par_assign(BigVec<T> &v, size_t n, const T &val)
+{
+    huge_reserve(v, n);
+    v.clear();
+    v.resize(n);   // (NoInitAlloc: nothing written)
+    par_for((long long)n, 1 << 16, [&](long long a, long long b) {
+        for (long long k = a; k < b; k++) ::new (&v[k]) T(val);
+    });
+}
+
 // A whole mesh file in memory, read as the token stream fscanf sees.
 struct TextBuf {
     // the file's bytes + a terminating NUL; not value-initialised (the
@@ -390,7 +402,8 @@ struct TextBuf {
         char &operator[](size_t i) { return b[i]; }
     } d;
     size_t pos = 0;
-    size_t hint = 0;   // bytes to allocate at least (the largest file to come)
+    size_t hint = 0;      // bytes to allocate at least (the largest file to come)
+    double ms_count = 0;  // (trace: the record-count pass of the last records())
     bool load(const std::string &path)
     {
         const int fd = ::open(path.c_str(), O_RDONLY);
@@ -457,6 +470,8 @@ struct TextBuf {
         const long long len = end - base;
         const int T = (int)std::max<long long>(1, std::min<long long>(HostPool::get().size(), len / (1 << 20)));
         bool ok = T > 1;
+        const auto tc = std::chrono::steady_clock::now();
+        ms_count = 0;
         if (ok) {
             // chunk starts at line starts; records (non-blank lines) per chunk
             std::vector<const char *> cs(T + 1);
@@ -470,20 +485,22 @@ struct TextBuf {
             std::vector<long long> cnt(T + 1, 0);
             par_for(T, 1, [&](long long a, long long b) {
                 for (long long t = a; t < b; ++t) {
+                    // lines found by memchr; a line counts when a non-blank
+                    // character precedes its end (leading blanks are few)
                     long long c = 0;
-                    bool blank = true;
-                    for (const char *q = cs[t]; q < cs[t + 1]; ++q) {
-                        if (*q == '\n') {
-                            c += !blank;
-                            blank = true;
-                        } else if (!ws(*q)) {
-                            blank = false;
-                        }
+                    const char *q = cs[t], *const e = cs[t + 1];
+                    while (q < e) {
+                        const char *nl = static_cast<const char *>(std::memchr(q, '\n', (size_t)(e - q)));
+                        const char *le = nl ? nl : e;
+                        while (q < le && ws(*q)) ++q;
+                        c += q < le;
+                        q = nl ? nl + 1 : e;
                     }
-                    cnt[t + 1] = c + !blank;
+                    cnt[t + 1] = c;
                 }
             });
             for (int t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+            ms_count = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
             ok = cnt[T] >= count;
             std::vector<char> good(T, 1);
             if (ok)
@@ -535,8 +552,7 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
     int k = 0, j = 0;
     if (!tb.header_int(k)) return BADNODEFILE;
     NumNodes = k;
-    huge_reserve(meshnode, (size_t)std::max(0, k));
-    meshnode.assign(k, CNode());
+    par_assign(meshnode, (size_t)std::max(0, k), CNode());
     const double conv = 100 * kLengthConvMeters[LengthUnits];
     if (!tb.records(k, [&](const char *&p, int i, bool nl) {
             int a, m;
@@ -550,6 +566,7 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
             return true;
         }))
         return BADNODEFILE;
+    if (tr.on) std::fprintf(stderr, "[load]   (record count pass %.1f ms)\n", tb.ms_count);
     tr.mark("nodes");
 
     infile = PathName + ".pbc";
@@ -602,8 +619,7 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
     tr.mark("  .ele read");
     if (!tb.header_int(k)) return BADELEMENTFILE;
     NumEls = k;
-    huge_reserve(meshele, (size_t)std::max(0, k));
-    meshele.assign(k, CMElement());
+    par_assign(meshele, (size_t)std::max(0, k), CMElement());
     tr.mark("  element array");
     int defaultLabel = -1;
     for (int i = 0; i < (int)labellist.size(); i++)
@@ -618,6 +634,8 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
                    read_int(p, elm.p[2], nl) && read_int(p, elm.lbl, nl);
         }))
         return BADELEMENTFILE;
+    if (tr.on) std::fprintf(stderr, "[load]   (record count pass %.1f ms)\n", tb.ms_count);
+    tr.mark("  element records");
     {
         // labels and node ids checked per element, in parallel; the first
         // failing element (in file order) decides the error, as the
@@ -671,14 +689,14 @@ LoadMeshErr FSolver::LoadMesh(bool deleteFiles)
     tr.mark("  .edge read");
     int nedge = 0, flag = 0;
     if (!tb.next_int(nedge) || !tb.next_int(flag)) return BADEDGEFILE;
-    huge_reserve(edges_, (size_t)std::max(0, nedge));
-    edges_.assign(std::max(0, nedge), {0, 0, 0});
+    par_assign(edges_, (size_t)std::max(0, nedge), std::array<int, 3>{0, 0, 0});
     if (nedge > 0 && !tb.records(nedge, [&](const char *&p, int i, bool nl) {
             int a;
             auto &e = edges_[i];
             return read_int(p, a, nl) && read_int(p, e[0], nl) && read_int(p, e[1], nl) && read_int(p, e[2], nl);
         }))
         return BADEDGEFILE;
+    if (tr.on) std::fprintf(stderr, "[load]   (record count pass %.1f ms)\n", tb.ms_count);
     tr.mark("edge records");
     // boundary-marked edges (marker < 0) set the boundary property of the
     // element sides they match (fsolver.cpp:660-704: per edge, every element
@@ -896,22 +914,19 @@ unsigned long long scan_rows(unsigned long long *car, const unsigned long long *
 }
 }  // namespace
 
-// meshele[k] = the old meshele[src(k)]: through raw storage (copy-constructed
-// in parallel, then assigned back), no serial value-initialisation of a second
-// element array
+// meshele[k] = the old meshele[src(k)]: a second element array copy-constructed
+// in parallel (no serial value-initialisation), then swapped in
 template <class Src>
 bool FSolver::permute_elements(Src src)
 {
-    HugeBuf<char> store;
-    if (!store.allocate(sizeof(CMElement) * (size_t)std::max(1, NumEls))) return false;
-    CMElement *raw = reinterpret_cast<CMElement *>(store.data());
+    BigVec<CMElement> out;
+    huge_reserve(out, (size_t)std::max(0, NumEls));
+    out.resize((size_t)std::max(0, NumEls));   // (NoInitAlloc: written below, in parallel)
     par_for(NumEls, 1 << 16, [&](long long a, long long b) {
-        for (long long k = a; k < b; k++) new (raw + k) CMElement(meshele[src(k)]);
+        for (long long k = a; k < b; k++) ::new (&out[k]) CMElement(meshele[src(k)]);
     });
-    par_for(NumEls, 1 << 16, [&](long long a, long long b) {
-        for (long long k = a; k < b; k++) meshele[k] = raw[k];
-    });
-    static_assert(std::is_trivially_destructible<CMElement>::value, "raw storage freed without destructors");
+    meshele.swap(out);
+    static_assert(std::is_trivially_destructible<CMElement>::value, "uninitialised storage");
     return true;
 }
 
@@ -1066,9 +1081,7 @@ int FSolver::SortElements()
         std::fprintf(stderr, "[load]   comb passes: %d wide %.1f ms, %d narrow %.1f ms\n", n_wide, ms_wide, n_narrow,
                      ms_narrow);
     tr.mark("  comb sort");
-    // the permutation applied through raw storage (copy-constructed in
-    // parallel, then assigned back): no serial value-initialisation of a
-    // second element array
+    // the permutation applied through a second element array (permute_elements)
     if (!permute_elements([&](long long k) { return (int)(key[k] & 0xffffffffu); })) return false;
     tr.mark("  permute");
     return true;
@@ -1079,51 +1092,72 @@ int FSolver::Cuthill(bool deleteFiles)
     // reverse-less Cuthill-McKee of cuthill.cpp:88-390, on the .edge connectivity
     LoadTrace tr;
     const int n_lines = (int)edges_.size();
-    std::vector<int> numcon(NumNodes, 0), newnum(NumNodes, -1), nxtnum(NumNodes, -1);
+    BigVec<int> numcon, newnum, nxtnum;
+    par_assign(numcon, (size_t)NumNodes, 0);
+    par_assign(newnum, (size_t)NumNodes, -1);
+    par_assign(nxtnum, (size_t)NumNodes, -1);
     // neighbour lists as CSR, each in the order the reference's lists get
-    // their entries (edge order).  Each thread owns a range of nodes and
-    // scans every edge for the ends it owns -- counts, then the fill -- so
-    // each list is appended in edge order, as the sequential loop does.
-    std::vector<int> aptr, adj;
-    huge_reserve(aptr, (size_t)NumNodes + 1);
+    // their entries (edge order).  Thread t takes the edges of its range and
+    // bins both ends by the node range that owns them (bucket (t, u)); owner u
+    // then reads its buckets in t order -- every list in edge order, as the
+    // sequential loop appends it -- counts, scans and fills its own nodes.
+    // The edge array is read twice in all (not once per thread).
+    BigVec<int> aptr, adj;
+    par_assign(aptr, (size_t)NumNodes + 1, 0);
     huge_reserve(adj, 2 * edges_.size());
-    aptr.assign((size_t)NumNodes + 1, 0);
-    adj.resize(2 * edges_.size());
+    adj.resize(2 * edges_.size());   // (every slot written by the fill below)
     {
         const int T = (int)std::max<long long>(1, std::min<long long>(HostPool::get().size(), (long long)n_lines / 65536));
-        auto lo = [&](int t) { return (int)((long long)NumNodes * t / T); };
-        std::vector<long long> part(T + 1, 0);
+        const int chunk = (int)std::max<long long>(1, ((long long)NumNodes + T - 1) / T);
+        auto lo = [&](int u) { return (int)std::min<long long>(NumNodes, (long long)chunk * u); };
+        auto elo = [&](int t) { return (long long)n_lines * t / T; };
+        std::vector<long long> bc((size_t)T * T + 1, 0);   // bucket (t, u) at t * T + u: ends counted, then offsets
         par_for(T, 1, [&](long long t0, long long t1) {
             for (long long t = t0; t < t1; ++t) {
-                const int a = lo((int)t);
-                const unsigned span = (unsigned)(lo((int)t + 1) - a);
-                for (const auto &e : edges_) {
-                    if ((unsigned)(e[0] - a) < span) numcon[e[0]]++;
-                    if ((unsigned)(e[1] - a) < span) numcon[e[1]]++;
-                }
-                long long sum = 0;
-                for (int v = a; v < a + (int)span; ++v) sum += numcon[v];
-                part[t + 1] = sum;
-            }
-        });
-        for (int t = 0; t < T; ++t) part[t + 1] += part[t];
-        par_for(T, 1, [&](long long t0, long long t1) {
-            for (long long t = t0; t < t1; ++t) {
-                const int a = lo((int)t);
-                const unsigned span = (unsigned)(lo((int)t + 1) - a);
-                long long o = part[t];
-                for (int v = a; v < a + (int)span; ++v) {
-                    aptr[v] = (int)o;
-                    o += numcon[v];
-                }
-                std::vector<int> cur(aptr.begin() + a, aptr.begin() + a + span);
-                for (const auto &e : edges_) {
-                    if ((unsigned)(e[0] - a) < span) adj[cur[e[0] - a]++] = e[1];
-                    if ((unsigned)(e[1] - a) < span) adj[cur[e[1] - a]++] = e[0];
+                long long *c = bc.data() + t * T;
+                for (long long i = elo((int)t); i < elo((int)t + 1); ++i) {
+                    c[edges_[i][0] / chunk]++;
+                    c[edges_[i][1] / chunk]++;
                 }
             }
         });
-        aptr[NumNodes] = (int)part[T];
+        // layout: owner u's region holds its buckets t = 0 .. T-1 in order
+        std::vector<long long> off((size_t)T * T), ubase(T + 1, 0);
+        long long o = 0;
+        for (int u = 0; u < T; ++u) {
+            ubase[u] = o;
+            for (int t = 0; t < T; ++t) {
+                off[(size_t)t * T + u] = o;
+                o += bc[(size_t)t * T + u];
+            }
+        }
+        ubase[T] = o;
+        BigVec<std::array<int, 2>> ends;   // (owned end, other end)
+        huge_reserve(ends, (size_t)o);
+        ends.resize((size_t)o);
+        par_for(T, 1, [&](long long t0, long long t1) {
+            for (long long t = t0; t < t1; ++t) {
+                long long *w = off.data() + t * T;
+                for (long long i = elo((int)t); i < elo((int)t + 1); ++i) {
+                    const int e0 = edges_[i][0], e1 = edges_[i][1];
+                    ends[w[e0 / chunk]++] = {e0, e1};
+                    ends[w[e1 / chunk]++] = {e1, e0};
+                }
+            }
+        });
+        par_for(T, 1, [&](long long u0, long long u1) {
+            for (long long u = u0; u < u1; ++u) {
+                for (long long k = ubase[u]; k < ubase[u + 1]; ++k) numcon[ends[k][0]]++;
+                long long q = ubase[u];   // (= the ends owned by the ranges before u)
+                for (int v = lo((int)u); v < lo((int)u + 1); ++v) {
+                    aptr[v] = (int)q;
+                    q += numcon[v];
+                }
+                std::vector<int> cur(aptr.begin() + lo((int)u), aptr.begin() + lo((int)u + 1));
+                for (long long k = ubase[u]; k < ubase[u + 1]; ++k) adj[cur[ends[k][0] - lo((int)u)]++] = ends[k][1];
+            }
+        });
+        aptr[NumNodes] = (int)ubase[T];
     }
     if (deleteFiles) remove_async({PathName + ".edge"});
     tr.mark("adjacency");
@@ -1211,9 +1245,11 @@ int FSolver::Cuthill(bool deleteFiles)
             for (int q = 0; q < 3; q++) meshele[k].p[q] = newnum[meshele[k].p[q]];
     });
     // SortNodes (fsolver.cpp:1341-1353): node i moves to slot newnum[i]
-    std::vector<CNode> sorted(NumNodes);
+    BigVec<CNode> sorted;
+    huge_reserve(sorted, (size_t)NumNodes);
+    sorted.resize(NumNodes);   // (every slot written below: newnum is a permutation)
     par_for(NumNodes, 1 << 16, [&](long long a, long long b) {
-        for (long long k = a; k < b; k++) sorted[newnum[k]] = meshnode[k];
+        for (long long k = a; k < b; k++) ::new (&sorted[newnum[k]]) CNode(meshnode[k]);
     });
     meshnode.swap(sorted);
     tr.mark("bandwidth + renumber");
@@ -1436,7 +1472,11 @@ int FSolver::Static2D()
     // the .ans element section depends on the mesh only: formatted while the
     // device solves (joined by WriteStatic2D, or below on failure)
     if (ele_fmt_.joinable()) ele_fmt_.join();
-    if (writes_output()) ele_fmt_ = std::thread([this] { ele_text_ = format_static_elements(); });
+    if (writes_output())
+        ele_fmt_ = std::thread([this] {
+            ele_text_ = format_static_elements();
+            node_parts_ = format_static_node_parts();
+        });
     xfk_problem *prob = nullptr;
     int rc = comm ? xfk_problem_create_dist(&ds.d, device, comm, &prob) : xfk_problem_create(&ds.d, device, &prob);
     ms_phase[2] = ms_since(t);
@@ -1459,6 +1499,7 @@ int FSolver::Static2D()
         warn(std::string("GPU solver error: ") + xfk_last_error() + "\n");
         if (ele_fmt_.joinable()) ele_fmt_.join();
         ele_text_ = Formatted();
+        node_parts_ = NodeParts();
     }
     if (prob) xfk_problem_destroy(prob);
     ms_phase[3] = ms_since(t);
@@ -1545,10 +1586,11 @@ inline char *put_i(char *p, int v) { return std::to_chars(p, p + 16, v).ptr; }
 // its end; formatted in parallel chunks into huge-page buffers, then written
 // in order by fwrite (one write of ~10 GB/s on the box; a shared mapping of
 // the file was measured 5x slower, tools/lab/io_probe.cpp)
+int format_chunks(int n) { return (int)std::max(1, std::min<int>(HostPool::get().size(), n / 8192)); }
 template <class F>
 FSolver::Formatted format_lines(int n, int max_line, F line)
 {
-    const int T = (int)std::max(1, std::min<int>(HostPool::get().size(), n / 8192));
+    const int T = format_chunks(n);
     FSolver::Formatted f;
     f.buf.resize(T);
     f.len.assign(T, 0);
@@ -1588,6 +1630,35 @@ FSolver::Formatted FSolver::format_static_elements() const
     });
 }
 
+FSolver::NodeParts FSolver::format_static_node_parts() const
+{
+    const double unitconv[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};
+    const double cf = unitconv[LengthUnits];
+    NodeParts np;
+    const int n = NumNodes, T = format_chunks(n);
+    np.lo.resize(T + 1);
+    for (int t = 0; t <= T; ++t) np.lo[t] = (int)((long long)n * t / T);
+    np.pre.resize(n);
+    np.suf.resize(n);
+    np.f = format_lines(n, 104, [&](int i, char *q) {
+        char *q0 = q;
+        q = put_g17(q, meshnode[i].x / cf);
+        *q++ = '\t';
+        q = put_g17(q, meshnode[i].y / cf);
+        *q++ = '\t';
+        np.pre[i] = (unsigned char)(q - q0);
+        q0 = q;
+        *q++ = '\t';
+        q = put_i(q, meshnode[i].BoundaryMarker);
+        // static2d.cpp:1093-1101: Aprev follows the marker with no separator
+        if (!Aprev.empty()) q = put_g17(q, Aprev[i]);
+        *q++ = '\n';
+        np.suf[i] = (unsigned char)(q - q0);
+        return q;
+    });
+    return np;
+}
+
 // an existing .ans is moved aside and unlinked beside the write (truncating
 // ~130 MB of page cache in fopen costs ~7 ms); the new file is written whole
 void FSolver::clear_old_output(const std::string &path)
@@ -1623,24 +1694,55 @@ int FSolver::WriteStatic2D()
     const double cf = unitconv[LengthUnits];
     fprintf(fp, "%i\n", NumNodes);
     fflush(fp);
-    write_lines(fp, NumNodes, 128, [&](int i, char *q) {
-        q = put_g17(q, meshnode[i].x / cf);
-        *q++ = '\t';
-        q = put_g17(q, meshnode[i].y / cf);
-        *q++ = '\t';
-        q = put_g17(q, A[i]);
-        *q++ = '\t';
-        q = put_i(q, meshnode[i].BoundaryMarker);
-        // static2d.cpp:1093-1101: Aprev follows the marker with no separator
-        if (!Aprev.empty()) q = put_g17(q, Aprev[i]);
-        *q++ = '\n';
-        return q;
-    });
-    tr.mark("  .ans nodes");
+    if (ele_fmt_.joinable()) ele_fmt_.join();   // (element text and node parts formatted beside the device solve)
+    Formatted nodes_text;
+    NodeParts &np = node_parts_;
+    if (np.lo.size() >= 2 && np.lo.back() == NumNodes && (int)np.f.buf.size() == (int)np.lo.size() - 1) {
+        // the parts around A, with A put in between
+        const int T = (int)np.lo.size() - 1;
+        nodes_text.buf.resize(T);
+        nodes_text.len.assign(T, 0);
+        par_for(T, 1, [&](long long t0, long long t1) {
+            for (long long t = t0; t < t1; ++t) {
+                const int a = np.lo[t], b = np.lo[t + 1];
+                nodes_text.buf[t].allocate(np.f.len[t] + (size_t)(b - a) * 25 + 1);
+                const char *p = np.f.buf[t].data();
+                char *q = nodes_text.buf[t].data();
+                for (int i = a; i < b; ++i) {
+                    std::memcpy(q, p, np.pre[i]);
+                    q += np.pre[i];
+                    p += np.pre[i];
+                    q = put_g17(q, A[i]);
+                    std::memcpy(q, p, np.suf[i]);
+                    q += np.suf[i];
+                    p += np.suf[i];
+                }
+                nodes_text.len[t] = (size_t)(q - nodes_text.buf[t].data());
+            }
+        });
+    } else {
+        nodes_text = format_lines(NumNodes, 128, [&](int i, char *q) {
+            q = put_g17(q, meshnode[i].x / cf);
+            *q++ = '\t';
+            q = put_g17(q, meshnode[i].y / cf);
+            *q++ = '\t';
+            q = put_g17(q, A[i]);
+            *q++ = '\t';
+            q = put_i(q, meshnode[i].BoundaryMarker);
+            // static2d.cpp:1093-1101: Aprev follows the marker with no separator
+            if (!Aprev.empty()) q = put_g17(q, Aprev[i]);
+            *q++ = '\n';
+            return q;
+        });
+    }
+    node_parts_ = NodeParts();
+    tr.mark("  .ans nodes formatted");
+    write_formatted(fp, nodes_text);
+    tr.mark("  .ans nodes written");
     fprintf(fp, "%i\n", NumEls);
     fflush(fp);
-    if (ele_fmt_.joinable()) ele_fmt_.join();   // (formatted beside the device solve)
-    else ele_text_ = format_static_elements();
+    if (ele_text_.buf.empty()) ele_text_ = format_static_elements();
+    tr.mark("  .ans element text joined");
     write_formatted(fp, ele_text_);
     ele_text_ = Formatted();
     tr.mark("  .ans elements");

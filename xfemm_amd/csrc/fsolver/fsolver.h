@@ -36,8 +36,8 @@ public:
     std::string PathName;
     double Relax = 0.0;
     int NumNodes = 0, NumEls = 0, BandWidth = 0, NumPBCs = 0, NumAirGapElems = 0, NumCircPropsOrig = 0;
-    std::vector<CNode> meshnode;
-    std::vector<CMElement> meshele;
+    BigVec<CNode> meshnode;      // (parallel first touch: hostmem.h)
+    BigVec<CMElement> meshele;
     std::vector<CCommonPoint> pbclist;
     // CAirGapElement as read from the .pbc file (fsolver.cpp:425-515)
     struct AirGap {
@@ -97,7 +97,7 @@ public:
     std::string lastError;
 
 private:
-    std::vector<std::array<int, 3>> edges_;   // .edge content: n0, n1, marker
+    BigVec<std::array<int, 3>> edges_;        // .edge content: n0, n1, marker
     std::vector<std::thread> removers_;       // mesh-file deletions in flight (joined by runSolver)
     void remove_async(std::vector<std::string> paths);
     template <class Src>
@@ -105,6 +105,16 @@ private:
     std::thread ele_fmt_;                     // the .ans element section, formatted beside the solve
     Formatted ele_text_;
     Formatted format_static_elements() const;
+    // the .ans node lines without A (x, y before it; the marker and the
+    // previous-solution A after it), formatted beside the solve: the lines of
+    // chunk t are [lo[t], lo[t + 1]) with pre[i] / suf[i] bytes around A
+    struct NodeParts {
+        Formatted f;
+        std::vector<int> lo;
+        std::vector<unsigned char> pre, suf;
+    };
+    NodeParts node_parts_;
+    NodeParts format_static_node_parts() const;
     void clear_old_output(const std::string &path);
     void remove_mesh_files_after_collective_solve();
     void warn(const std::string &msg);
