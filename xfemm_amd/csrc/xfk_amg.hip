@@ -3024,35 +3024,28 @@ int build_tile_split(hipStream_t s, int n, int B, const int *rowptr, const int *
 
 namespace {
 std::mutex g_pool_mu;
-std::map<hipStream_t, int> g_pool_dev;                 // every pooled stream -> its pool (2 device + high)
-std::map<int, std::vector<hipStream_t>> g_pool_free;   // idle streams per pool
+std::map<hipStream_t, int> g_pool_dev;                 // every pooled stream -> its device
+std::map<int, std::vector<hipStream_t>> g_pool_free;   // idle streams per device
 }  // namespace
 
-hipError_t stream_acquire(hipStream_t *s, bool high)
+hipError_t stream_acquire(hipStream_t *s)
 {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    const int key = 2 * dev + (high ? 1 : 0);
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
-        auto &f = g_pool_free[key];
+        auto &f = g_pool_free[dev];
         if (!f.empty()) {
             *s = f.back();
             f.pop_back();
             return hipSuccess;
         }
     }
-    if (high) {
-        int lo = 0, hi = 0;
-        e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
-    } else {
-        e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-    }
+    e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
     if (e == hipSuccess) {
         std::lock_guard<std::mutex> lk(g_pool_mu);
-        g_pool_dev[*s] = key;
+        g_pool_dev[*s] = dev;
     }
     return e;
 }

@@ -284,8 +284,7 @@ void host_par_for(long long n, long long min_per_thread, F f)
 // Process-wide pool of non-blocking streams on the current device: creating a
 // HIP stream costs ~4 ms on MI355X (a hardware queue), so a problem returns its
 // streams here when it is destroyed and the next problem takes them back.
-// high: a stream of the device's greatest priority (its own pool)
-hipError_t stream_acquire(hipStream_t *s, bool high = false);
+hipError_t stream_acquire(hipStream_t *s);
 void stream_release(hipStream_t s);   // idle streams only (the caller synchronised it)
 void stream_pool_drain();
 // xfk_sort.hip: the reference's comb sort of the element scores on the device
