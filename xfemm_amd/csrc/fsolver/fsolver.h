@@ -70,10 +70,10 @@ public:
     bool runSolver(bool verbose = false);                // fsolver.cpp:1213-1338
     int Static2D();                                      // static2d.cpp:53-1033 (on the GPU)
     int WriteStatic2D();                                 // static2d.cpp:1038-1195
-    int Harmonic2D();                                    // harmonic2d.cpp:36-790 (on the GPU, linear)
+    int Harmonic2D();                                    // harmonic2d.cpp:36-790 (on the GPU: linear, successive approximation, Newton AC)
     int WriteHarmonic2D();                               // harmonic2d.cpp:793-960
     void WriteAirGapElements(FILE *fp) const;            // static2d.cpp:1161-1190, harmonic2d.cpp:1002-1030
-    void GetFillFactor(int lbl);                         // fsolver.cpp:1083-1105 (static)
+    void GetFillFactor(int lbl);                         // fsolver.cpp:1083-1193 (incl. ProximityMu)
     static std::string getErrorString(LoadMeshErr err);
     void join_removals();   // wait for the mesh-file deletions LoadMesh / Cuthill started
     // .ans text formatted in parallel chunks (fsolver.cpp: format_lines)
