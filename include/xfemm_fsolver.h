@@ -59,6 +59,13 @@ int xfemm_fsolver_get_element_edges(xfemm_fsolver *s, int *e);
 int xfemm_fsolver_get_pbcs(xfemm_fsolver *s, int *pbc3);
 int xfemm_fsolver_num_pbcs(xfemm_fsolver *s);
 int xfemm_fsolver_bandwidth(xfemm_fsolver *s);
+/* Air gaps (FEASolver::agelist, feasolver.h:141): the number of quadNodes of
+ * each (totalArcElements + 1) into counts[num_air_gaps], and their node ids
+ * n0..n3 (CQuadPoint, libfemm/CQuadPoint.h) air gap by air gap into quad4 --
+ * after Cuthill in the renumbered ids (cuthill.cpp:320-330).  Returns the
+ * total number of quadNodes; either array may be NULL to query sizes. */
+int xfemm_fsolver_num_air_gaps(xfemm_fsolver *s);
+int xfemm_fsolver_get_air_gap_nodes(xfemm_fsolver *s, int *counts, int *quad4);
 /* processed B-H curve of block k after LoadProblemFile (GetSlopes); returns BHpoints */
 int xfemm_fsolver_get_block_bh(xfemm_fsolver *s, int k, double *B, double *H, double *slope, double *mu_x);
 

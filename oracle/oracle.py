@@ -22,6 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 REF_PATH = os.path.join(HERE, "_ref", "libxfemm_ref.so")
 LUA_PATH = os.path.join(HERE, "_ref", "libreflua.so")
+CUTHILL_PATH = os.path.join(HERE, "_ref", "libref_cuthill.so")
 
 dptr = C.POINTER(C.c_double)
 iptr = C.POINTER(C.c_int)
@@ -173,6 +174,47 @@ def ref():
             getattr(_ref, nm).restype = dptr
             getattr(_ref, nm).argtypes = [C.c_void_p]
     return _ref
+
+
+_cut = None
+
+
+def ref_cuthill_available() -> bool:
+    return os.path.exists(CUTHILL_PATH)
+
+
+def ref_cuthill(base: str, num_nodes: int, p, pbc=None, age_counts=None, age_quad=None):
+    """The reference's own FEASolver::Cuthill(false) + SortNodes + SortElements
+    (cfemm/libfemm/cuthill.cpp:33-391, compiled into oracle/_ref/libref_cuthill.so
+    by ref_cuthill.cpp) on a mesh in LoadMesh order.  It reads ``base``.edge
+    itself, as the reference does.  p: (NE, 3) corners; pbc: (NP, 2) node pairs;
+    age_counts / age_quad: quadNodes per air gap and their (NQ, 4) node ids.
+    Returns dict(p, elem_order, newnum, pbc, age_quad, bandwidth): the
+    renumbered corners in the sorted element order, the LoadMesh index of the
+    element at each position, the node map old -> new, the remapped pairs and
+    quadNodes, and BandWidth."""
+    global _cut
+    if _cut is None:
+        if not os.path.exists(CUTHILL_PATH):
+            raise FileNotFoundError(CUTHILL_PATH)
+        _cut = C.CDLL(CUTHILL_PATH)
+        _cut.ref_cuthill_run.argtypes = [C.c_char_p, C.c_int, C.c_int, iptr, iptr, iptr, C.c_int, iptr,
+                                         C.c_int, iptr, iptr]
+        _cut.ref_cuthill_run.restype = C.c_int
+    p = np.ascontiguousarray(np.asarray(p, dtype=np.int32).reshape(-1, 3)).copy()
+    ne = len(p)
+    pbc = np.ascontiguousarray(np.zeros((0, 2), np.int32) if pbc is None else np.asarray(pbc, np.int32)[:, :2]).copy()
+    counts = np.ascontiguousarray(np.zeros(0, np.int32) if age_counts is None else np.asarray(age_counts, np.int32))
+    quad = np.ascontiguousarray(np.zeros((0, 4), np.int32) if age_quad is None else np.asarray(age_quad, np.int32)).copy()
+    assert quad.shape[0] == int(counts.sum())
+    order = np.zeros(ne, np.int32)
+    newnum = np.zeros(num_nodes, np.int32)
+    bw = _cut.ref_cuthill_run(base.encode(), num_nodes, ne, p.ctypes.data_as(iptr), order.ctypes.data_as(iptr),
+                              newnum.ctypes.data_as(iptr), len(pbc), pbc.ctypes.data_as(iptr), len(counts),
+                              counts.ctypes.data_as(iptr), quad.ctypes.data_as(iptr))
+    if bw < 0:
+        raise RuntimeError("reference Cuthill failed on %s.edge" % base)
+    return dict(p=p, elem_order=order, newnum=newnum, pbc=pbc, age_quad=quad, bandwidth=bw)
 
 
 _lua = None

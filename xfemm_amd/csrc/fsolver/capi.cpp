@@ -1,6 +1,7 @@
 // extern "C" surface of FSolver (include/xfemm_fsolver.h).
 #include "../../../include/xfemm_fsolver.h"
 
+#include <algorithm>
 #include <cstring>
 
 #include "fsolver.h"
@@ -109,6 +110,22 @@ int xfemm_fsolver_get_pbcs(xfemm_fsolver *h, int *pbc3)
 }
 
 int xfemm_fsolver_bandwidth(xfemm_fsolver *h) { return h ? h->s.BandWidth : 0; }
+
+int xfemm_fsolver_num_air_gaps(xfemm_fsolver *h) { return h ? (int)h->s.agelist.size() : 0; }
+
+int xfemm_fsolver_get_air_gap_nodes(xfemm_fsolver *h, int *counts, int *quad4)
+{
+    if (!h) return 0;
+    int total = 0;
+    for (size_t i = 0; i < h->s.agelist.size(); i++) {
+        const std::vector<int> &qn = h->s.agelist[i].qn;
+        const int nq = (int)(qn.size() / 4);
+        if (counts) counts[i] = nq;
+        if (quad4) std::copy(qn.begin(), qn.end(), quad4 + 4 * (size_t)total);
+        total += nq;
+    }
+    return total;
+}
 
 int xfemm_fsolver_get_block_bh(xfemm_fsolver *h, int k, double *B, double *H, double *slope, double *mu_x)
 {

@@ -29,7 +29,7 @@ EXPORTED = (
     "xfemm_fsolver_set_previous_solution_file", "xfemm_fsolver_previous_solution_file", "xfemm_fsolver_ac_solver",
     "xfemm_fsolver_frequency", "xfemm_fsolver_num_line_props", "xfemm_fsolver_num_node_props",
     "xfemm_fsolver_num_block_props", "xfemm_fsolver_num_circ_props", "xfemm_fsolver_num_block_labels",
-    "xfemm_fsolver_set_comm",
+    "xfemm_fsolver_set_comm", "xfemm_fsolver_num_air_gaps", "xfemm_fsolver_get_air_gap_nodes",
 )
 
 _lib = None
@@ -55,13 +55,15 @@ def load_library(path: str = FSOLVER_SO):
     L.xfemm_fsolver_set_comm.argtypes = [vp, vp]
     for nm in ("xfemm_fsolver_load_problem_file", "xfemm_fsolver_load_mesh", "xfemm_fsolver_cuthill",
                "xfemm_fsolver_num_nodes", "xfemm_fsolver_num_elements", "xfemm_fsolver_num_pbcs",
-               "xfemm_fsolver_bandwidth"):
+               "xfemm_fsolver_bandwidth", "xfemm_fsolver_num_air_gaps"):
         getattr(L, nm).argtypes = [vp]
         getattr(L, nm).restype = C.c_int
     L.xfemm_fsolver_run_solver.argtypes = [vp, C.c_int]
     L.xfemm_fsolver_get_nodes.argtypes = [vp, dptr, dptr, iptr]
     L.xfemm_fsolver_get_element_edges.argtypes = [vp, iptr]
     L.xfemm_fsolver_get_pbcs.argtypes = [vp, iptr]
+    L.xfemm_fsolver_get_air_gap_nodes.argtypes = [vp, iptr, iptr]
+    L.xfemm_fsolver_get_air_gap_nodes.restype = C.c_int
     L.xfemm_fsolver_get_block_bh.argtypes = [vp, C.c_int, dptr, dptr, dptr, dptr]
     L.xfemm_fsolver_get_solution.argtypes = [vp, dptr, dptr, dptr]
     L.xfemm_fsolver_get_elements.argtypes = [vp, iptr, iptr]
@@ -225,6 +227,16 @@ class FSolver:
         a = np.zeros((max(n, 1), 3), np.int32)
         _lib.xfemm_fsolver_get_pbcs(self._h, a.ctypes.data_as(iptr))
         return a[:n]
+
+    def air_gap_nodes(self):
+        """(counts, quad) of FEASolver::agelist: quadNodes per air gap and their
+        node ids n0..n3, one row per quadNode (renumbered after Cuthill)."""
+        na = _lib.xfemm_fsolver_num_air_gaps(self._h)
+        counts = np.zeros(max(na, 1), np.int32)
+        nq = _lib.xfemm_fsolver_get_air_gap_nodes(self._h, counts.ctypes.data_as(iptr), None)
+        quad = np.zeros((max(nq, 1), 4), np.int32)
+        _lib.xfemm_fsolver_get_air_gap_nodes(self._h, None, quad.ctypes.data_as(iptr))
+        return counts[:na], quad[:nq]
 
     def block_bh(self, k: int, nmax: int = 4096):
         B, H, S = np.zeros(nmax), np.zeros(nmax), np.zeros(nmax)
