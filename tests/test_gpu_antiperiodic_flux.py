@@ -15,7 +15,7 @@ import pytest
 
 from antiperiodic import check, flux_post, write_case
 from oracle import femfile, oracle
-from util import converged, parity_message, rel_err
+from util import assert_parity, converged, rel_err
 from xfemm_amd import fsolver
 
 pytestmark = pytest.mark.gpu
@@ -39,7 +39,7 @@ def test_antiperiodic_flux_machine_fem_to_ans(tmp_path):
     failed, mx, mx_rel, rows = check(flux_post(pr, ans.x, ans.y, ans.A, ans.p, ans.lbl))
     print("antiperiodic flux: %d Newton / %d PCG iterations, A vs converged oracle %.3e; |B| check: %d failed, "
           "max diff %.4f T, %.1f %%" % (st["newton_iters"], st["cg_iters"], err, failed, mx, mx_rel))
-    assert err <= TOL_A, parity_message(ans.A, Ao, Ac, TOL_A)
+    assert_parity(ans.A, Ao, Ac, TOL_A)
     assert failed == 0, [r for r in rows if r[-1]]
     # the AMG on the antiperiodic seam (signed strength: the seam's couplings of
     # the diagonal's sign are weak, so no aggregate spans it): at most 30 PCG

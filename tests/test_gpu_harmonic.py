@@ -19,7 +19,7 @@ import pytest
 import scipy.sparse as sp
 
 from oracle import harmonic as oh
-from util import C_ANS, converged, parity_message, rel_err, synth_to_oracle
+from util import C_ANS, assert_parity, converged, rel_err, synth_to_oracle
 from xfemm_amd import kernels, synth
 
 pytestmark = pytest.mark.gpu
@@ -59,7 +59,7 @@ def test_harmonic_solution_matches_oracle(cells, periodic):
     n = len(rp) - 1
     G = sp.csr_matrix((val, col, rp), shape=(n, n))
     Ac = converged(pr, mesh, oh.solve)
-    assert rel_err(A, Ac) <= TOL_A, parity_message(A, Ao, Ac, TOL_A)
+    assert_parity(A, Ao, Ac, TOL_A)
     V = A / C_ANS
     assert np.linalg.norm(b - G @ V) / np.linalg.norm(b) <= 2 * kk["precision"]
     cc, J, dV = P.circuits()
@@ -78,7 +78,7 @@ def test_harmonic_without_circuits_and_high_frequency():
     A = P.solution()
     Ao, _, _ = oh.solve(pr, mesh)
     Ac = converged(pr, mesh, oh.solve)
-    assert rel_err(A, Ac) <= TOL_A, parity_message(A, Ao, Ac, TOL_A)
+    assert_parity(A, Ao, Ac, TOL_A)
     P.close()
 
 
@@ -109,7 +109,7 @@ def test_harmonic_proximity_winding_matches_oracle(wiretype):
     P.close()
     Ao, _, _ = oh.solve(pr, mesh)
     Ac = converged(pr, mesh, oh.solve)
-    assert rel_err(A, Ac) <= TOL_A, parity_message(A, Ao, Ac, TOL_A)
+    assert_parity(A, Ao, Ac, TOL_A)
     pr0, mesh0, _ = _problem(synth.harmonic(20, frequency=20000.0))
     A0 = converged(pr0, mesh0, oh.solve)
     assert rel_err(A0, Ac) > 10 * TOL_A
@@ -129,7 +129,7 @@ def test_harmonic_axisymmetric_proximity_winding_matches_oracle(wiretype):
     P.close()
     Ao, _, _ = oh.solve(pr, mesh)
     Ac = converged(pr, mesh, oh.solve)
-    assert rel_err(A, Ac) <= TOL_A, parity_message(A, Ao, Ac, TOL_A)
+    assert_parity(A, Ao, Ac, TOL_A)
     pr0, mesh0, _ = _problem(synth.harmonic_axisymmetric(16, frequency=20000.0))
     assert rel_err(converged(pr0, mesh0, oh.solve), Ac) > 10 * TOL_A
 
@@ -155,7 +155,7 @@ def test_harmonic_proximity_winding_file_interface(tmp_path):
     assert fs.runSolver(False), fs.last_error()
     nodes, _ = _read_harmonic_ans(base + ".ans")
     A = nodes[:, 2] + 1j * nodes[:, 3]
-    assert rel_err(A, Ac) <= TOL_A, parity_message(A, Ao, Ac, TOL_A)
+    assert_parity(A, Ao, Ac, TOL_A)
 
 
 @pytest.mark.parametrize("frequency", [60.0, 2000.0])
@@ -223,7 +223,7 @@ def test_harmonic_file_interface_end_to_end(tmp_path):
     nodes, els = _read_harmonic_ans(base + ".ans")
     A = nodes[:, 2] + 1j * nodes[:, 3]
     Ac = converged(pr, mesh, oh.solve)
-    assert rel_err(A, Ac) <= TOL_A, parity_message(A, Ao, Ac, TOL_A)
+    assert_parity(A, Ao, Ac, TOL_A)
     assert np.array_equal(els[:, :3], mesh.p) and np.array_equal(els[:, 3], mesh.lbl)
     assert open(base + ".ans").read().startswith(open(base + ".fem").read())
 

@@ -13,7 +13,7 @@ import pytest
 import scipy.sparse as sp
 
 from oracle import harmonic as oh
-from util import converged, parity_message, rel_err, synth_to_oracle
+from util import assert_parity, converged, rel_err, synth_to_oracle
 from xfemm_amd import kernels, synth
 
 pytestmark = pytest.mark.gpu
@@ -42,7 +42,7 @@ def test_harmonic_axi_solution_matches_oracle(opts):
     A = P.solution()
     Ao, _, circ_o = oh.solve(pr, mesh)
     Ac = converged(pr, mesh, oh.solve)
-    assert rel_err(A, Ac) <= 1e-6, parity_message(A, Ao, Ac, 1e-6)
+    assert_parity(A, Ao, Ac, 1e-6)
     cc, J, dV = P.circuits()
     for k, (case, Jo, dVo) in enumerate(circ_o):
         assert cc[k] == case and abs(J[k] - Jo) <= 1e-12 * max(1.0, abs(Jo))

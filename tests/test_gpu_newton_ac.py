@@ -30,7 +30,7 @@ import numpy as np
 import pytest
 
 from oracle import harmonic as oh
-from util import converged, parity_message, rel_err, synth_to_oracle
+from util import assert_parity, converged, rel_err, synth_to_oracle
 from xfemm_amd import kernels, synth
 
 pytestmark = pytest.mark.gpu
@@ -71,8 +71,7 @@ def test_newton_ac_matches_oracle(kind, n):
     P.close()
     assert r["newton_iters"] >= 2
     print("newton AC %s %d: |A - Ac| %.3e, oracle at Precision %.3e" % (kind, n, rel_err(A, Ac), rel_err(Ao, Ac)))
-    assert rel_err(A, Ac) <= _tol(Ao, Ac), parity_message(A, Ao, Ac, _tol(Ao, Ac)) + " (%d / %d passes)" % (
-        r["newton_iters"], st["newton_iters"])
+    assert_parity(A, Ao, Ac, _tol(Ao, Ac), " (%d / %d passes)" % (r["newton_iters"], st["newton_iters"]))
     for k, (case, Jo, dVo) in enumerate(circ_o):
         assert cc[k] == case and abs(J[k] - Jo) <= 1e-12 * max(1.0, abs(Jo))
     kw0 = dict(kw, ac_solver=0)
@@ -112,7 +111,7 @@ def test_newton_ac_file_interface_end_to_end(tmp_path):
     nodes = np.array([[float(v) for v in ln.split()] for ln in lines[k + 1:k + 1 + n]])
     A = nodes[:, 2] + 1j * nodes[:, 3]
     print("newton AC file interface: |A - Ac| %.3e, oracle at Precision %.3e" % (rel_err(A, Ac), rel_err(Ao, Ac)))
-    assert rel_err(A, Ac) <= _tol(Ao, Ac), parity_message(A, Ao, Ac, _tol(Ao, Ac))
+    assert_parity(A, Ao, Ac, _tol(Ao, Ac))
 
 
 @pytest.mark.parametrize("n,kind", [(14, "planar"), (20, "planar"), (14, "periodic"), (16, "anti")])
@@ -138,8 +137,7 @@ def test_newton_ac_case2_matches_oracle(n, kind):
     P.close()
     assert r["newton_iters"] >= 2
     print("newton AC %s %d: |A - Ac| %.3e, oracle at Precision %.3e" % (kind, n, rel_err(A, Ac), rel_err(Ao, Ac)))
-    assert rel_err(A, Ac) <= _tol(Ao, Ac), parity_message(A, Ao, Ac, _tol(Ao, Ac)) + " (%d / %d passes)" % (
-        r["newton_iters"], st["newton_iters"])
+    assert_parity(A, Ao, Ac, _tol(Ao, Ac), " (%d / %d passes)" % (r["newton_iters"], st["newton_iters"]))
     for k, (case, Jo, dVo) in enumerate(circ_c):
         assert cc[k] == case and abs(J[k] - Jo) <= 1e-12 * max(1.0, abs(Jo))
         if case == 2:

@@ -24,7 +24,7 @@ import ansfile
 from oracle import femfile, gaptorque, oracle
 from oracle import harmonic as oh
 from torque import torque_ok, write_case
-from util import converged, parity_message, rel_err
+from util import assert_parity, converged, rel_err
 from xfemm_amd import fsolver, synth
 
 pytestmark = pytest.mark.gpu
@@ -66,7 +66,7 @@ def test_prev_torque_benchmark_resolve(tmp_path):
     assert rel_err(again.A, first.A) <= 1e-12
     Ao, _, _ = oracle.solve(pr2, mesh2)
     Ac = converged(pr2, mesh2)
-    assert rel_err(again.A, Ac) <= TOL_A, parity_message(again.A, Ao, Ac, TOL_A)
+    assert rel_err(again.A, Ac) <= TOL_A(again.A, Ao, Ac, TOL_A)
     tq = gaptorque.gap_dc_torque(again.ages[0], again.A, pr2.Depth, pr2.LengthUnits)
     assert torque_ok(tq, deg)[0], tq
 
@@ -109,7 +109,7 @@ def test_prev_harmonic_incremental_linear(tmp_path):
     assert np.array_equal(Aprev, dc_ans.A) and not Jprev.any()
     Ao, _, _ = oh.solve(pr, mesh)
     Ac = converged(pr, mesh, oh.solve)
-    assert rel_err(A, Ac) <= TOL_A, parity_message(A, Ao, Ac, TOL_A)
+    assert_parity(A, Ao, Ac, TOL_A)
 
 
 def test_prev_refusals_through_fsolver(tmp_path):

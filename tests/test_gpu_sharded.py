@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle
-from util import converged, parity_message, rel_err, synth_to_oracle
+from util import assert_parity, converged, rel_err, synth_to_oracle
 from xfemm_amd import kernels, synth
 
 pytestmark = pytest.mark.gpu
@@ -143,11 +143,11 @@ def test_sharded_nonlinear_matches_oracle():
     A1 = P.solution()
     P.close()
     Ac = converged(pr, mesh)
-    assert rel_err(A1, Ac) <= TOL_NONLINEAR, parity_message(A1, Ao, Ac, TOL_NONLINEAR)
+    assert_parity(A1, Ao, Ac, TOL_NONLINEAR)
     outs = run_sharded(kw, 3)
     for res, A, _, _ in outs:
         assert res["newton_iters"] >= 3
-        assert rel_err(A, Ac) <= TOL_NONLINEAR, parity_message(A, Ao, Ac, TOL_NONLINEAR)
+        assert_parity(A, Ao, Ac, TOL_NONLINEAR)
         assert rel_err(A, A1) <= TOL_NONLINEAR
     assert len({o[0]["newton_iters"] for o in outs}) == 1
 
@@ -202,7 +202,7 @@ def test_sharded_periodic_matches_oracle(anti, nranks):
     outs = run_sharded(kw, nranks)
     assert any(o[3]["n_extra"] > 0 for o in outs)
     for res, A, _, info in outs:
-        assert rel_err(A, Ac) <= TOL_LINEAR, parity_message(A, Ao, Ac, TOL_LINEAR)
+        assert_parity(A, Ao, Ac, TOL_LINEAR)
         assert rel_err(A, A1) <= TOL_LINEAR
     assert np.array_equal(outs[0][1], outs[-1][1])
 
@@ -212,7 +212,7 @@ def test_sharded_periodic_nonlinear():
     Ao, _, _ = oracle.solve(pr, mesh)
     Ac = converged(pr, mesh)
     for res, A, _, _ in run_sharded(kw, 3):
-        assert rel_err(A, Ac) <= TOL_NONLINEAR, parity_message(A, Ao, Ac, TOL_NONLINEAR)
+        assert_parity(A, Ao, Ac, TOL_NONLINEAR)
 
 
 @pytest.mark.parametrize("nranks", [2, 4])
@@ -230,7 +230,7 @@ def test_sharded_torque_benchmark(tmp_path, nranks):
     outs = run_sharded(kw, nranks)
     assert any(o[3]["n_extra"] > 0 for o in outs)
     for res, A, _, info in outs:
-        assert rel_err(A, Ac) <= TOL_LINEAR, parity_message(A, Ao, Ac, TOL_LINEAR)
+        assert_parity(A, Ao, Ac, TOL_LINEAR)
         tq = gaptorque.gap_dc_torque(mesh.ages[0], A, pr.Depth, pr.LengthUnits)
         assert torque_ok(tq, deg)[0], tq
 

@@ -3,12 +3,35 @@
 
 #include <algorithm>
 #include <cstring>
+#include <new>
+#include <stdexcept>
+#include <string>
 
 #include "fsolver.h"
 
 struct xfemm_fsolver {
     xfemm::FSolver s;
 };
+
+// No C++ exception crosses the C-ABI: a host allocation failure (or any
+// other exception) of a step becomes its false return, with the reason in
+// last_error.
+template <class F>
+int guarded(xfemm_fsolver *h, F &&f)
+{
+    if (!h) return 0;
+    try {
+        return f() ? 1 : 0;
+    } catch (const std::bad_alloc &) {
+        h->s.join_removals();
+        h->s.lastError = "out of host memory\n";
+    } catch (const std::exception &e) {
+        h->s.join_removals();
+        h->s.lastError = std::string(e.what()) + "\n";
+    }
+    h->s.WarnMessage("%s", h->s.lastError.c_str());
+    return 0;
+}
 
 extern "C" {
 
@@ -53,28 +76,36 @@ int xfemm_fsolver_set_delete_mesh_files(xfemm_fsolver *h, int del)
     return 1;
 }
 
-int xfemm_fsolver_load_problem_file(xfemm_fsolver *h) { return (h && h->s.LoadProblemFile()) ? 1 : 0; }
+int xfemm_fsolver_load_problem_file(xfemm_fsolver *h)
+{
+    return guarded(h, [&] { return h->s.LoadProblemFile(); });
+}
 
-int xfemm_fsolver_run_solver(xfemm_fsolver *h, int verbose) { return (h && h->s.runSolver(verbose != 0)) ? 1 : 0; }
+int xfemm_fsolver_run_solver(xfemm_fsolver *h, int verbose)
+{
+    return guarded(h, [&] { return h->s.runSolver(verbose != 0); });
+}
 
 int xfemm_fsolver_load_mesh(xfemm_fsolver *h)
 {
-    if (!h) return 0;
-    xfemm::LoadMeshErr err = h->s.LoadMesh(h->s.deleteMeshFiles);
-    h->s.join_removals();
-    if (err != xfemm::NOERROR) {
-        h->s.lastError = xfemm::FSolver::getErrorString(err);
-        return 0;
-    }
-    return 1;
+    return guarded(h, [&] {
+        xfemm::LoadMeshErr err = h->s.LoadMesh(h->s.deleteMeshFiles);
+        h->s.join_removals();
+        if (err != xfemm::NOERROR) {
+            h->s.lastError = xfemm::FSolver::getErrorString(err);
+            return false;
+        }
+        return true;
+    });
 }
 
 int xfemm_fsolver_cuthill(xfemm_fsolver *h)
 {
-    if (!h) return 0;
-    const int ok = h->s.Cuthill(h->s.deleteMeshFiles);
-    h->s.join_removals();
-    return ok ? 1 : 0;
+    return guarded(h, [&] {
+        const int ok = h->s.Cuthill(h->s.deleteMeshFiles);
+        h->s.join_removals();
+        return ok != 0;
+    });
 }
 
 int xfemm_fsolver_get_nodes(xfemm_fsolver *h, double *x, double *y, int *marker)

@@ -62,9 +62,13 @@ bool FSolver::writes_output() const { return !comm || xfk_comm_rank(comm) == 0; 
 
 void FSolver::remove_mesh_files_after_collective_solve()
 {
-    if (!comm || !deleteMeshFiles || xfk_comm_rank(comm) != 0 || !previousSolutionFile.empty()) return;
+    // what a one-device run deletes: LoadMesh's four files whenever it read
+    // them (not for a mesh taken from the previous solution, fsolver.cpp:357-360),
+    // the .edge only after Cuthill (which runs without a previous solution)
+    if (!comm || !deleteMeshFiles || xfk_comm_rank(comm) != 0 || meshLoadedFromPrevSolution) return;
     std::vector<std::string> v;
-    for (const char *ext : {".ele", ".node", ".pbc", ".poly", ".edge"}) v.push_back(PathName + ext);
+    for (const char *ext : {".ele", ".node", ".pbc", ".poly"}) v.push_back(PathName + ext);
+    if (previousSolutionFile.empty()) v.push_back(PathName + ".edge");
     remove_async(std::move(v));
 }
 
@@ -1597,7 +1601,7 @@ FSolver::Formatted format_lines(int n, int max_line, F line)
     par_for(T, 1, [&](long long t0, long long t1) {
         for (long long t = t0; t < t1; ++t) {
             const int a = (int)((long long)n * t / T), b = (int)((long long)n * (t + 1) / T);
-            f.buf[t].allocate((size_t)(b - a) * max_line + 1);
+            if (!f.buf[t].allocate((size_t)(b - a) * max_line + 1)) continue;   // (Formatted::ok() fails)
             char *q = f.buf[t].data();
             for (int i = a; i < b; ++i) q = line(i, q);
             f.len[t] = (size_t)(q - f.buf[t].data());
@@ -1605,15 +1609,17 @@ FSolver::Formatted format_lines(int n, int max_line, F line)
     });
     return f;
 }
-void write_formatted(FILE *fp, const FSolver::Formatted &f)
+bool write_formatted(FILE *fp, const FSolver::Formatted &f)
 {
+    if (!f.ok()) return false;   // (a chunk's buffer could not be allocated)
     for (size_t t = 0; t < f.buf.size(); ++t)
         if (f.len[t]) fwrite(f.buf[t].data(), 1, f.len[t], fp);
+    return true;
 }
 template <class F>
-void write_lines(FILE *fp, int n, int max_line, F line)
+bool write_lines(FILE *fp, int n, int max_line, F line)
 {
-    write_formatted(fp, format_lines(n, max_line, line));
+    return write_formatted(fp, format_lines(n, max_line, line));
 }
 }  // namespace
 
@@ -1660,13 +1666,21 @@ FSolver::NodeParts FSolver::format_static_node_parts() const
 }
 
 // an existing .ans is moved aside and unlinked beside the write (truncating
-// ~130 MB of page cache in fopen costs ~7 ms); the new file is written whole
+// ~130 MB of page cache in fopen costs ~7 ms); the new file is written whole.
+// A symlinked or hard-linked .ans keeps the reference's fopen("wt") behaviour
+// (truncated in place: the link target, inode and permissions stay); the
+// aside name is unique (mkstemp in the same directory, replaced by rename).
 void FSolver::clear_old_output(const std::string &path)
 {
     struct stat st;
-    if (::stat(path.c_str(), &st) != 0 || st.st_size < (1 << 20)) return;
-    const std::string aside = path + ".xfemm-old";
+    if (::lstat(path.c_str(), &st) != 0 || !S_ISREG(st.st_mode) || st.st_nlink > 1 || st.st_size < (1 << 20))
+        return;
+    std::string aside = path + ".xfemm-old-XXXXXX";
+    const int fd = ::mkstemp(&aside[0]);
+    if (fd < 0) return;
+    ::close(fd);
     if (::rename(path.c_str(), aside.c_str()) == 0) remove_async({aside});
+    else ::unlink(aside.c_str());
 }
 
 int FSolver::WriteStatic2D()
@@ -1705,7 +1719,7 @@ int FSolver::WriteStatic2D()
         par_for(T, 1, [&](long long t0, long long t1) {
             for (long long t = t0; t < t1; ++t) {
                 const int a = np.lo[t], b = np.lo[t + 1];
-                nodes_text.buf[t].allocate(np.f.len[t] + (size_t)(b - a) * 25 + 1);
+                if (!nodes_text.buf[t].allocate(np.f.len[t] + (size_t)(b - a) * 25 + 1)) continue;
                 const char *p = np.f.buf[t].data();
                 char *q = nodes_text.buf[t].data();
                 for (int i = a; i < b; ++i) {
@@ -1737,14 +1751,23 @@ int FSolver::WriteStatic2D()
     }
     node_parts_ = NodeParts();
     tr.mark("  .ans nodes formatted");
-    write_formatted(fp, nodes_text);
+    if (!write_formatted(fp, nodes_text)) {
+        fclose(fp);
+        warn("couldn't allocate the .ans node text\n");
+        return false;
+    }
     tr.mark("  .ans nodes written");
     fprintf(fp, "%i\n", NumEls);
     fflush(fp);
     if (ele_text_.buf.empty()) ele_text_ = format_static_elements();
     tr.mark("  .ans element text joined");
-    write_formatted(fp, ele_text_);
+    const bool ele_ok = write_formatted(fp, ele_text_);
     ele_text_ = Formatted();
+    if (!ele_ok) {
+        fclose(fp);
+        warn("couldn't allocate the .ans element text\n");
+        return false;
+    }
     tr.mark("  .ans elements");
     fprintf(fp, "%i\n", (int)labellist.size());
     for (size_t k = 0; k < labellist.size(); k++) {
@@ -1807,7 +1830,7 @@ int FSolver::WriteHarmonic2D()
     // incremental problems add A of the previous solution per node and J per
     // element (harmonic2d.cpp:929-949)
     fflush(fp);
-    write_lines(fp, NumNodes, 160, [&](int i, char *q) {
+    bool text_ok = write_lines(fp, NumNodes, 160, [&](int i, char *q) {
         for (double v : {meshnode[i].x / cf, meshnode[i].y / cf, A[i], A_im[i]}) {
             q = put_g17(q, v);
             *q++ = '\t';
@@ -1820,9 +1843,9 @@ int FSolver::WriteHarmonic2D()
         *q++ = '\n';
         return q;
     });
-    fprintf(fp, "%i\n", NumEls);
+    if (text_ok) fprintf(fp, "%i\n", NumEls);
     fflush(fp);
-    write_lines(fp, NumEls, 128, [&](int i, char *q) {
+    text_ok = text_ok && write_lines(fp, NumEls, 128, [&](int i, char *q) {
         const CMElement &e = meshele[i];
         for (int v : {e.p[0], e.p[1], e.p[2], e.lbl, e.e[0], e.e[1]}) {
             q = put_i(q, v);
@@ -1836,6 +1859,11 @@ int FSolver::WriteHarmonic2D()
         *q++ = '\n';
         return q;
     });
+    if (!text_ok) {
+        fclose(fp);
+        warn("couldn't allocate the .ans text\n");
+        return false;
+    }
     fprintf(fp, "%i\n", (int)labellist.size());
     for (size_t k = 0; k < labellist.size(); k++) {
         int i = labellist[k].InCircuit;

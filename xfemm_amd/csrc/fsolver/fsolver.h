@@ -80,6 +80,13 @@ public:
     struct Formatted {
         std::vector<HugeBuf<char>> buf;
         std::vector<size_t> len;
+        // every chunk's buffer was allocated (a failed chunk is left empty)
+        bool ok() const
+        {
+            for (const auto &b : buf)
+                if (!b.data()) return false;
+            return true;
+        }
     };
 
     // result of the last Static2D: A (= V*c) per node, in meshnode order;

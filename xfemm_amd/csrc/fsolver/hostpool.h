@@ -6,13 +6,16 @@
 // the GPU box's host, i.e. tens of ms per analysis.  The pool's workers live
 // for the process and take loop chunks through an atomic counter; a dispatch
 // costs a wake-up.  A loop started from inside a pool job, or while another
-// thread's loop holds the pool, runs on the calling thread alone.
+// thread's loop holds the pool, runs on the calling thread alone.  A job that
+// throws on any thread has its first exception rethrown by run() on the
+// calling thread, after every claimed chunk has finished.
 #pragma once
 
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -60,8 +63,13 @@ class HostPool {
             std::unique_lock<std::mutex> lk(mu_);
             done_cv_.wait(lk, [&] { return left_.load(std::memory_order_acquire) == 0; });
         }
-        std::lock_guard<std::mutex> g(mu_);
-        job_ = nullptr;
+        std::exception_ptr err;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = nullptr;
+            std::swap(err, err_);
+        }
+        if (err) std::rethrow_exception(err);
     }
 
   private:
@@ -107,7 +115,12 @@ class HostPool {
                 }
             }
             if (t < 0) break;
-            (*j)(t);
+            try {
+                (*j)(t);
+            } catch (...) {   // (kept for run(); the chunk still counts as done)
+                std::lock_guard<std::mutex> lk(mu_);
+                if (!err_) err_ = std::current_exception();
+            }
             if (left_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
                 std::lock_guard<std::mutex> lk(mu_);
                 done_cv_.notify_all();
@@ -133,6 +146,7 @@ class HostPool {
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
     std::function<void(int)> *job_ = nullptr;
+    std::exception_ptr err_;   // first exception of the running job (under mu_)
     int n_ = 0;
     unsigned long long gen_ = 0;
     std::atomic<unsigned long long> ticket_{0};
