@@ -40,7 +40,11 @@ Output: one JSON line (rank 0) with
                  problem of the process (hints of the previous one, checked);
   fsolver_end_to_end  the product path: FSolver .fem -> .ans wall time on
                  configs[1] and configs[2], split into LoadMesh / Cuthill /
-                 create / solve / write.
+                 create / solve / write;
+  fsolver_cold_process  bin/fsolver as a fresh child process per analysis
+                 (the reference's command-line use), start to exit;
+  sharded_diagnosis  (sharded runs) time inside each kind of collective on
+                 every rank, the per-rank phases and their maximum over ranks.
 """
 import argparse
 import ctypes
@@ -286,6 +290,120 @@ def configs4_rank0_of_8(device, args):
                                                "(first + repeated), halved: per solve")}
 
 
+def diagnosis_row(P, comm, rank):
+    """One rank's share of a sharded step (after the timed region): one more
+    solve with every collective bracketed by HIP events on its stream
+    (xfk_comm_time: the interval includes the wait for the peers' matching
+    call), then one with the replicated coarse levels timed apart
+    (XFK_TIME_TAIL).  Rows / halo, the step's phases, PCG iterations, calls and
+    microseconds inside each kind of collective."""
+    comm.time(True)
+    r = P.solve(rebuild_symbolic=True)
+    tm = comm.timing()
+    comm.time(False)
+    rt = P.solve(rebuild_symbolic=True, time_tail=True)
+    info = P.dist_info()
+    it = max(1, r["cg_iters"])
+    return {"rank": rank, "rows": info["n_own"], "halo": info["n_halo"], "pcg_iters": r["cg_iters"],
+            "ms_symbolic": r["ms_symbolic"], "ms_assemble": r["ms_assemble"], "ms_amg_setup": r["ms_amg_setup"],
+            "ms_pcg": r["ms_solve"] - r["ms_amg_setup"], "ms_solve": r["ms_solve"],
+            "us_per_pcg_iteration": 1e3 * (r["ms_solve"] - r["ms_amg_setup"]) / it,
+            "ms_in_collectives": 1e-3 * sum(v["us"] for v in tm.values()), "collectives": tm,
+            "replicated_tail": {"ms_setup": rt["ms_rep_setup"],
+                                "us_per_vcycle": 1e3 * rt["ms_rep_cycle"] / max(1, rt["rep_cycles"]),
+                                "vcycles": rt["rep_cycles"]}}
+
+
+def diagnosis_summary(rows, transport):
+    """Every rank's diagnosis_row with the maxima over ranks: the N > 1 line
+    says where a sharded step's time went."""
+    def mx(key):
+        return max(q[key] for q in rows)
+    ops = {nm: {"calls_per_solve": rows[0]["collectives"][nm]["calls"],
+                "us_rank0": rows[0]["collectives"][nm]["us"],
+                "us_max_over_ranks": max(q["collectives"][nm]["us"] for q in rows),
+                "us_longest_call": max(q["collectives"][nm]["us_max_call"] for q in rows)}
+           for nm in ("allreduce", "exchange", "allgather")}
+    return {"transport": transport,
+            "comm": {"ops": ops, "calls_per_solve": sum(v["calls_per_solve"] for v in ops.values()),
+                     "ms_in_collectives_rank0": rows[0]["ms_in_collectives"],
+                     "ms_in_collectives_max_over_ranks": mx("ms_in_collectives"),
+                     "note": "one diagnostic solve after the timed region, HIP events around every collective on "
+                             "its stream (xfk_comm_time): transfer + wait for the peers' matching call"},
+            "max_over_ranks": {k: mx(k) for k in ("ms_symbolic", "ms_assemble", "ms_amg_setup", "ms_pcg",
+                                                  "ms_solve", "us_per_pcg_iteration")},
+            "ranks": rows}
+
+
+def sharded_diagnosis(P, comm, dist, rank, world):
+    """diagnosis_row on every rank, gathered on rank 0 (gloo all_gather_object)."""
+    row = diagnosis_row(P, comm, rank)
+    rows = [row]
+    if dist is not None:
+        rows = [None] * world
+        dist.all_gather_object(rows, row)
+    return diagnosis_summary(rows, "rccl") if rank == 0 else None
+
+
+def local_ranks_run(args):
+    """--force-sharded --local-ranks R: the sharded step of R ranks through the
+    in-process transport (one host thread per rank, all on device 0) -- the
+    plumbing of the N > 1 line where only one GPU exists.  The ranks
+    time-share one GPU, so the step time is NOT a scaling number; the line
+    carries the sharded_diagnosis block of the same code path the RCCL run
+    reports."""
+    import threading
+    from xfemm_amd import kernels, synth
+    R = args.local_ranks
+    kw = synth.magnetostatic(args.shard_cells, nonlinear=args.nonlinear)
+    comms = kernels.Comm.local_group(R)
+    probs = [kernels.Static2DProblem(device=0, comm=comms[q], precond=args.precond, amg_sweeps=args.amg_sweeps,
+                                     amg_omega=args.amg_omega, amg_dense=args.amg_dense, amg_theta=args.amg_theta,
+                                     amg_replicate=args.amg_replicate, **kw) for q in range(R)]
+    bar = threading.Barrier(R)
+    t = [0.0, 0.0]
+    rows, err = [None] * R, [None] * R
+
+    def work(q):
+        try:
+            for _ in range(args.warmup):
+                probs[q].solve(rebuild_symbolic=True)
+            _hip_sync()
+            bar.wait()
+            if q == 0:
+                t[0] = time.perf_counter()
+            for _ in range(args.steps):
+                probs[q].solve(rebuild_symbolic=True)
+            _hip_sync()
+            bar.wait()
+            if q == 0:
+                t[1] = time.perf_counter()
+            rows[q] = diagnosis_row(probs[q], comms[q], q)
+        except Exception as ex:   # surfaced below
+            err[q] = ex
+            bar.abort()
+
+    th = [threading.Thread(target=work, args=(q,)) for q in range(R)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    n = probs[0].n_nodes
+    for p in probs:
+        p.close()
+    for c in comms:
+        c.close()
+    for e in err:
+        if e is not None:
+            raise e
+    dt = (t[1] - t[0]) / args.steps
+    return {"metric": "sharded step plumbing (in-process ranks time-sharing one GPU; not a scaling number)",
+            "ms_per_step": 1e3 * dt, "steps": args.steps, "warmup": args.warmup, "local_ranks": R,
+            "config": {"workload": "synthetic %d-tri square-domain magnetostatic, row-block sharded over %d "
+                                   "in-process ranks on one GPU" % (2 * args.shard_cells ** 2, R), "dof": n},
+            "sharded_diagnosis": diagnosis_summary(rows, "in-process (LocalComm)")}
+
+
 def fsolver_end_to_end(device, args):
     """The drop-in product path timed whole: FSolver .fem + fmesher files ->
     .ans (fsolver.cpp:1213-1340's sequence: LoadMesh, Cuthill-McKee, problem
@@ -334,6 +452,59 @@ def fsolver_end_to_end(device, args):
                 del fs
             out.append(rec)
     return out
+
+
+def fsolver_cold_process(args):
+    """The one-shot command line as the reference runs it (cfemm/fsolver/main.cpp:
+    a fresh process per analysis): xfemm_amd/bin/fsolver <problem> started as a
+    child process and timed from start to exit, on configs[1] and configs[2].
+    Run before this process touches the GPU (the children bring it up
+    themselves).  Each case twice: with the HIP bring-up on its own thread
+    beside LoadMesh / Cuthill (the default, xfk_device_init) and with it left
+    to the first device call (XFEMM_NO_HIP_WARMUP=1, the serial order); the two
+    .ans files must be byte-identical."""
+    import filecmp
+    import shutil
+    import tarfile
+    import tempfile
+    from xfemm_amd import synth
+    exe = os.path.join(ROOT, "xfemm_amd", "bin", "fsolver")
+    out = []
+    with tempfile.TemporaryDirectory() as td:
+        with tarfile.open(os.path.join(ROOT, "tests", "golden", "torque", "TorqueBenchmark_fine_30.tgz")) as tf:
+            tf.extractall(td)
+        cases = [("configs[1]: TorqueBenchmark refined (~200k tri, periodic + air gap), 30 deg",
+                  os.path.join(td, "TorqueBenchmark_fine_30"))]
+        b2 = os.path.join(td, "square")
+        synth.write_problem(b2, synth.magnetostatic(args.cells))
+        cases.append(("configs[2]: synthetic %d-tri square" % (2 * args.cells ** 2), b2))
+        for name, base in cases:
+            rec = {"workload": name}
+            ans = {}
+            for mode in ("overlapped", "serial"):
+                run = os.path.join(td, "run_" + mode)
+                os.makedirs(run, exist_ok=True)
+                dst = os.path.join(run, os.path.basename(base))
+                for ext in (".fem", ".node", ".ele", ".edge", ".pbc"):
+                    shutil.copy(base + ext, dst + ext)
+                env = dict(os.environ)
+                env.pop("XFEMM_NO_HIP_WARMUP", None)
+                if mode == "serial":
+                    env["XFEMM_NO_HIP_WARMUP"] = "1"
+                t0 = time.perf_counter()
+                r = subprocess.run([exe, dst], capture_output=True, text=True, env=env, timeout=300)
+                dt = time.perf_counter() - t0
+                if r.returncode != 0:
+                    raise RuntimeError("bin/fsolver failed on %s (%s): rc %d\n%s%s"
+                                       % (name, mode, r.returncode, r.stdout[-2000:], r.stderr[-2000:]))
+                rec["ms_wall_" + mode] = 1e3 * dt
+                ans[mode] = dst + ".ans"
+            rec["ans_byte_identical"] = filecmp.cmp(ans["overlapped"], ans["serial"], shallow=False)
+            out.append(rec)
+    return {"cases": out, "note": "xfemm_amd/bin/fsolver <problem> as a child process, start to exit (process start, "
+                                  "HIP runtime + device bring-up, LoadMesh, Cuthill, solve, .ans write); "
+                                  "'overlapped': bring-up on its own thread from LoadProblemFile (default); "
+                                  "'serial': XFEMM_NO_HIP_WARMUP=1"}
 
 
 def cold_first_solve(device, args, kw):
@@ -565,10 +736,15 @@ def main():
                     help="cells per side of the sharded mesh (3162 -> 20M triangles, configs[4])")
     ap.add_argument("--force-sharded", action="store_true",
                     help="run the RCCL sharded path even at N = 1 (plumbing check)")
+    ap.add_argument("--local-ranks", type=int, default=0,
+                    help="with --force-sharded: R in-process ranks on one GPU (plumbing of the N > 1 line)")
     ap.add_argument("--no-same-mesh-1gpu", action="store_true",
                     help="skip rank 0's single-GPU solve of the sharded mesh")
     args = ap.parse_args()
 
+    if args.force_sharded and args.local_ranks > 1:
+        print(json.dumps(local_ranks_run(args)), flush=True)
+        return
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus is not None and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
@@ -583,6 +759,9 @@ def main():
                                                                os.environ.get("LOCAL_RANK", "0")),
               file=sys.stderr, flush=True)
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cold_process = None
+    if world == 1 and not args.no_fsolver and not args.force_sharded:
+        cold_process = fsolver_cold_process(args)   # (before this process touches the GPU)
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
@@ -664,6 +843,8 @@ def main():
                             "frac": gbs / HBM_PEAK_GBS, "bound": "unmeasured"})
             phases.append(row)
         phases_src = annotate_phases(phases)
+
+    diagnosis = sharded_diagnosis(P, comm, dist, rank, world) if sharded else None
 
     same_mesh = None
     if sharded and world > 1 and not args.no_same_mesh_1gpu:
@@ -750,10 +931,13 @@ def main():
                 sum(p["us_per_launch"] * p["launches_per_iteration"] for p in it_phases), phases_src))
     if same_mesh is not None:
         out["config"]["same_mesh_1gpu"] = same_mesh
+    if diagnosis is not None:
+        out["sharded_diagnosis"] = diagnosis
     if rank == 0 and world == 1 and not sharded:
         out["cold_first_solve"] = cold_first_solve(local, args, kw)
         if not args.no_fsolver:
             out["fsolver_end_to_end"] = fsolver_end_to_end(local, args)
+            out["fsolver_cold_process"] = cold_process
     if rank == 0 and world == 1 and not sharded and not args.nonlinear and not args.no_secondary:
         P.close()
         out["secondary"] = [nonlinear_secondary(local, args)]

@@ -154,6 +154,13 @@ typedef struct xfk_problem xfk_problem;
 
 const char *xfk_last_error(void);
 int xfk_device_count(void);
+/* Bring up the HIP runtime on `device` ahead of the first solve: the runtime
+ * and the device context (~0.4 s in a fresh process), every code object of
+ * this library, and a few streams for the process's stream pool.  Idempotent
+ * and thread-safe; the FSolver runs it on a thread of its own beside
+ * LoadMesh / Cuthill, so a fresh `fsolver` process does not wait for it in
+ * series.  XFK_OK, or XFK_ERR_HIP when there is no such device. */
+int xfk_device_init(int device);
 
 /* Upload a problem; nothing is computed yet.  Host arrays may be freed after. */
 int xfk_problem_create(const xfk_problem_desc *desc, int device, xfk_problem **out);
@@ -294,6 +301,16 @@ int xfk_comm_log(const xfk_comm *comm, xfk_comm_op *out, int cap, int *count);
  * exact inputs of the recorded run: the per-rank compute time without the
  * transport. */
 int xfk_comm_create_replay(const xfk_comm *recorded, xfk_comm **out);
+/* Time inside collectives (the N > 1 bench line's diagnosis).  With timing on
+ * (xfk_comm_time(comm, 1)) every collective is bracketed by two HIP events on
+ * the stream it is issued on: the interval covers the transfer and any wait
+ * for the peers' matching call (an RCCL kernel starts only when its peers'
+ * have).  xfk_comm_timing waits for those events and returns, per op
+ * (index 0 all-reduce, 1 halo exchange, 2 all-gather), the number of calls
+ * and the summed and longest microseconds since the last read, then clears
+ * them.  Timing off (the default): no events. */
+int xfk_comm_time(xfk_comm *comm, int on);
+int xfk_comm_timing(xfk_comm *comm, long long calls[3], double us_total[3], double us_max[3]);
 
 typedef struct {
     int rank, nranks;

@@ -45,7 +45,22 @@ FSolver::FSolver() : WarnMessage(&PrintWarningMsg), PrintMessage(&PrintWarningMs
 FSolver::~FSolver()
 {
     if (ele_fmt_.joinable()) ele_fmt_.join();
+    join_hip_warmup();
     join_removals();
+}
+
+void FSolver::start_hip_warmup()
+{
+    // a sharded FSolver's communicator has brought the device up already;
+    // XFEMM_NO_HIP_WARMUP=1 leaves the bring-up to the first device call
+    if (comm || hip_warm_.joinable() || std::getenv("XFEMM_NO_HIP_WARMUP")) return;
+    const int dev = device;
+    hip_warm_ = std::thread([dev] { (void)xfk_device_init(dev); });
+}
+
+void FSolver::join_hip_warmup()
+{
+    if (hip_warm_.joinable()) hip_warm_.join();
 }
 
 // The mesh files the reference deletes once read (fsolver.cpp:711-716,
@@ -103,6 +118,7 @@ std::string FSolver::getErrorString(LoadMeshErr err)
 
 bool FSolver::LoadProblemFile()
 {
+    start_hip_warmup();
     Relax = 1.;
     std::string err;
     FemmProblemData &base = *this;
@@ -943,6 +959,7 @@ int FSolver::SortElements()
     // (xfk_sort_elements: ~2 ms instead of ~45 on 16 host cores); without
     // one, or with XFEMM_HOST_SORT set, on the host below.
     LoadTrace tr;
+    join_hip_warmup();
     if (NumEls > 1 && !std::getenv("XFEMM_HOST_SORT") && xfk_device_count() > 0) {
         HugeBuf<unsigned> score;
         HugeBuf<int> perm;
@@ -1470,6 +1487,7 @@ double ms_since(std::chrono::steady_clock::time_point &t)
 
 int FSolver::Static2D()
 {
+    join_hip_warmup();
     auto t = std::chrono::steady_clock::now();
     DescStore ds;
     if (!make_desc(ds)) return false;
@@ -1512,6 +1530,7 @@ int FSolver::Static2D()
 
 int FSolver::Harmonic2D()
 {
+    join_hip_warmup();
     auto t = std::chrono::steady_clock::now();
     DescStore ds;
     if (!make_desc(ds)) return false;

@@ -110,6 +110,13 @@ private:
     template <class Src>
     bool permute_elements(Src src);
     std::thread ele_fmt_;                     // the .ans element section, formatted beside the solve
+    // HIP runtime / device / code-object bring-up (xfk_device_init) started by
+    // LoadProblemFile on a thread of its own, so a fresh process pays it beside
+    // LoadMesh and Cuthill instead of inside the first device call; joined
+    // before the first device use (SortElements, Static2D, Harmonic2D)
+    std::thread hip_warm_;
+    void start_hip_warmup();
+    void join_hip_warmup();
     Formatted ele_text_;
     Formatted format_static_elements() const;
     // the .ans node lines without A (x, y before it; the marker and the

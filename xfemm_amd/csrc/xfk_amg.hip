@@ -5214,3 +5214,11 @@ int Amg::vcycle(hipStream_t s, const double *r, double *u, const int *done, doub
 }
 
 }  // namespace xfk
+
+// xfk_device_init: loads this translation unit's code object onto the device
+// (the first use of any of its kernels would otherwise do it inside a solve)
+hipError_t xfk::warm_module_amg()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&k_max_reduce));
+}

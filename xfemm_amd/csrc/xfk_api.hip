@@ -1802,6 +1802,30 @@ int xfk_device_count(void)
     return n;
 }
 
+int xfk_device_init(int device)
+{
+    static std::mutex mu;
+    static std::set<int> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.count(device)) return XFK_OK;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+        (void)hipGetLastError();
+        set_error("xfk_device_init: no HIP device " + std::to_string(device));
+        return XFK_ERR_HIP;
+    }
+    XFK_CHECK(hipSetDevice(device));
+    XFK_CHECK(hipFree(nullptr));
+    for (hipError_t (*w)() : {warm_module_device, warm_module_pcg, warm_module_amg, warm_module_harmonic,
+                              warm_module_sort, warm_module_comm})
+        XFK_CHECK(w());
+    hipStream_t s[3] = {};   // a problem's solve stream, the AMG's side stream and the sort's
+    for (hipStream_t &q : s) XFK_CHECK(stream_acquire(&q));
+    for (hipStream_t q : s) stream_release(q);
+    done.insert(device);
+    return XFK_OK;
+}
+
 void xfk_problem_destroy(xfk_problem *P)
 {
     if (!P) return;

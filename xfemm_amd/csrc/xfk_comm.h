@@ -61,6 +61,16 @@ struct xfk_comm {
     std::vector<hipStream_t> streams;            // first-use order: the stream index of a record
     std::shared_ptr<xfk::CommRecording> rec;     // non-null while recording
     long long n_collectives = 0;
+    // xfk_comm_time: (op slot, start, stop) per timed collective, and a pool
+    // of events to reuse once read
+    bool timing = false;
+    struct Timed {
+        int slot;
+        hipEvent_t a, b;
+    };
+    std::vector<Timed> timed;
+    std::vector<hipEvent_t> ev_pool;
+    int take_timing(long long calls[3], double us_total[3], double us_max[3]);
 
    protected:
     virtual int do_allreduce_sum(const double *send, double *recv, size_t n, hipStream_t s) = 0;
@@ -74,4 +84,7 @@ struct xfk_comm {
    private:
     int begin(int op, hipStream_t s, int &stream_idx, int &waited);
     int end(hipStream_t s);
+    int op_slot = -1;   // (the timed collective in flight between begin and end)
+    hipEvent_t op_start = nullptr;
+    int pooled_event(hipEvent_t *e);
 };

@@ -87,6 +87,45 @@ using namespace xfk;
 xfk_comm::~xfk_comm()
 {
     if (order_ev) (void)hipEventDestroy(order_ev);
+    for (const Timed &t : timed) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+}
+
+int xfk_comm::pooled_event(hipEvent_t *e)
+{
+    if (!ev_pool.empty()) {
+        *e = ev_pool.back();
+        ev_pool.pop_back();
+        return XFK_OK;
+    }
+    XFK_CHECK(hipEventCreate(e));
+    return XFK_OK;
+}
+
+int xfk_comm::take_timing(long long calls[3], double us_total[3], double us_max[3])
+{
+    for (int k = 0; k < 3; ++k) {
+        calls[k] = 0;
+        us_total[k] = 0.0;
+        us_max[k] = 0.0;
+    }
+    int rc = XFK_OK;
+    for (const Timed &t : timed) {
+        float ms = 0.f;
+        if (rc == XFK_OK && (hipEventSynchronize(t.b) != hipSuccess || hipEventElapsedTime(&ms, t.a, t.b) != hipSuccess))
+            rc = XFK_ERR_HIP;
+        calls[t.slot] += 1;
+        us_total[t.slot] += 1e3 * ms;
+        us_max[t.slot] = std::max(us_max[t.slot], 1e3 * (double)ms);
+        ev_pool.push_back(t.a);
+        ev_pool.push_back(t.b);
+    }
+    timed.clear();
+    if (rc != XFK_OK) set_error("xfk_comm_timing: a collective's events could not be read");
+    return rc;
 }
 
 // every collective runs after the previous one of this communicator: a new
@@ -106,7 +145,12 @@ int xfk_comm::begin(int op, hipStream_t s, int &idx, int &waited)
         idx = (int)streams.size();
         streams.push_back(s);
     }
-    (void)op;
+    op_slot = -1;
+    if (timing) {   // the start event follows the order wait: the interval is the collective itself
+        op_slot = op == XFK_COMM_ALLREDUCE ? 0 : op == XFK_COMM_EXCHANGE ? 1 : 2;
+        if (pooled_event(&op_start) != XFK_OK) return XFK_ERR_HIP;
+        XFK_CHECK(hipEventRecord(op_start, s));
+    }
     return XFK_OK;
 }
 
@@ -118,6 +162,13 @@ int xfk_comm::solve_boundary()
 
 int xfk_comm::end(hipStream_t s)
 {
+    if (op_slot >= 0) {
+        hipEvent_t stop;
+        if (pooled_event(&stop) != XFK_OK) return XFK_ERR_HIP;
+        XFK_CHECK(hipEventRecord(stop, s));
+        timed.push_back({op_slot, op_start, stop});
+        op_slot = -1;
+    }
     XFK_CHECK(hipEventRecord(order_ev, s));
     order_s = s;
     ++n_collectives;
@@ -539,6 +590,19 @@ int xfk_comm_record(xfk_comm *c, int mode)
     return XFK_OK;
 }
 
+int xfk_comm_time(xfk_comm *c, int on)
+{
+    XFK_REQUIRE(c, XFK_ERR_ARG, "xfk_comm_time: null communicator");
+    c->timing = on != 0;
+    return XFK_OK;
+}
+
+int xfk_comm_timing(xfk_comm *c, long long calls[3], double us_total[3], double us_max[3])
+{
+    XFK_REQUIRE(c && calls && us_total && us_max, XFK_ERR_ARG, "xfk_comm_timing: null argument");
+    return c->take_timing(calls, us_total, us_max);
+}
+
 int xfk_comm_log(const xfk_comm *c, xfk_comm_op *out, int cap, int *count)
 {
     XFK_REQUIRE(c && count, XFK_ERR_ARG, "null argument");
@@ -563,3 +627,11 @@ int xfk_comm_create_replay(const xfk_comm *recorded, xfk_comm **out)
 }
 
 }  // extern "C"
+
+// xfk_device_init: loads this translation unit's code object onto the device
+// (the first use of any of its kernels would otherwise do it inside a solve)
+hipError_t xfk::warm_module_comm()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&k_sum_ptrs));
+}

@@ -1540,3 +1540,11 @@ void launch_scale(hipStream_t s, int N, double sc, const double *V, double *out)
 }
 
 }  // namespace xfk
+
+// xfk_device_init: loads this translation unit's code object onto the device
+// (the first use of any of its kernels would otherwise do it inside a solve)
+hipError_t xfk::warm_module_device()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&k_count_incidence));
+}

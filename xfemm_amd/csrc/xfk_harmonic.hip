@@ -2318,3 +2318,11 @@ int xfk_get_csr_complex(xfk_problem *P, int *rowptr, int *col, double *val, doub
 }
 
 }  // extern "C"
+
+// xfk_device_init: loads this translation unit's code object onto the device
+// (the first use of any of its kernels would otherwise do it inside a solve)
+hipError_t xfk::warm_module_harmonic()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&k_hassemble_color));
+}

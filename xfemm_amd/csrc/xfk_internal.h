@@ -285,6 +285,14 @@ void host_par_for(long long n, long long min_per_thread, F f)
 // HIP stream costs ~4 ms on MI355X (a hardware queue), so a problem returns its
 // streams here when it is destroyed and the next problem takes them back.
 hipError_t stream_acquire(hipStream_t *s);
+// one kernel of each translation unit queried, so its code object is loaded
+// (xfk_device_init)
+hipError_t warm_module_amg();
+hipError_t warm_module_comm();
+hipError_t warm_module_device();
+hipError_t warm_module_harmonic();
+hipError_t warm_module_pcg();
+hipError_t warm_module_sort();
 void stream_release(hipStream_t s);   // idle streams only (the caller synchronised it)
 void stream_pool_drain();
 // xfk_sort.hip: the reference's comb sort of the element scores on the device

@@ -322,3 +322,11 @@ void launch_cg_dot(hipStream_t s, int N, const double *a, const double *b, doubl
 }
 
 }  // namespace xfk
+
+// xfk_device_init: loads this translation unit's code object onto the device
+// (the first use of any of its kernels would otherwise do it inside a solve)
+hipError_t xfk::warm_module_pcg()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&k_cg_init_r));
+}

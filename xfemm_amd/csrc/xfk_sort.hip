@@ -188,3 +188,11 @@ int sort_elements_device(hipStream_t s, int n, const unsigned *score_dev, int *p
 }
 
 }  // namespace xfk
+
+// xfk_device_init: loads this translation unit's code object onto the device
+// (the first use of any of its kernels would otherwise do it inside a solve)
+hipError_t xfk::warm_module_sort()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&k_sort_keys));
+}

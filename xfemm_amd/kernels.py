@@ -41,7 +41,7 @@ XFK_OPT_NEWTON_INEXACT = 12
 
 # every symbol include/xfemm_kernels.h declares
 EXPORTED = (
-    "xfk_last_error", "xfk_age_element_matrix", "xfk_device_count", "xfk_problem_create", "xfk_problem_destroy",
+    "xfk_last_error", "xfk_age_element_matrix", "xfk_device_count", "xfk_device_init", "xfk_problem_create", "xfk_problem_destroy",
     "xfk_static2d", "xfk_get_solution", "xfk_get_circuits", "xfk_get_csr", "xfk_get_nnz", "xfk_spmv_col_bytes",
     "xfk_get_stream", "xfk_pcg_solve_csr", "xfk_pcg_solve_csr_pc", "xfk_pcg_time", "xfk_phase_profile",
     "xfk_alloc_stats", "xfk_problem_memory", "xfk_cache_stats", "xfk_release_cache",
@@ -52,6 +52,7 @@ EXPORTED = (
     "xfk_get_csr_complex",
     "xfk_comm_unique_id", "xfk_comm_create_rccl", "xfk_comm_create_local", "xfk_comm_destroy",
     "xfk_comm_rank", "xfk_comm_size", "xfk_comm_record", "xfk_comm_log", "xfk_comm_create_replay",
+    "xfk_comm_time", "xfk_comm_timing",
     "xfk_partition_plan", "xfk_partition_plan_coupled", "xfk_problem_create_dist", "xfk_dist_get_info",
     "xfk_magdir_eval", "xfk_sort_elements",
 )
@@ -186,6 +187,8 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_comm_size.argtypes = [vp]
     L.xfk_comm_record.argtypes = [vp, C.c_int]
     L.xfk_comm_log.argtypes = [vp, vp, C.c_int, C.POINTER(C.c_int)]
+    L.xfk_comm_time.argtypes = [vp, C.c_int]
+    L.xfk_comm_timing.argtypes = [vp, C.POINTER(C.c_longlong), dptr, dptr]
     L.xfk_comm_create_replay.argtypes = [vp, C.POINTER(vp)]
     L.xfk_partition_plan.argtypes = [C.c_int, C.c_int, iptr, C.c_int, C.c_int, C.POINTER(DistInfo),
                                      iptr, iptr, iptr, iptr]
@@ -726,6 +729,21 @@ class Comm:
         _check(L.xfk_comm_log(self._h, C.cast(buf, C.c_void_p), n.value, C.byref(n)))
         return [dict(seq=o.seq, op=COMM_OPS.get(o.op, str(o.op)), stream=o.stream, waited=o.waited, peer=o.peer,
                      bytes=o.bytes, g0=o.g0) for o in buf[:n.value]]
+
+    def time(self, on: bool = True):
+        """Bracket every collective with HIP events (xfk_comm_time)."""
+        _check(load_library().xfk_comm_time(self._h, int(bool(on))))
+
+    def timing(self) -> dict:
+        """Per op (allreduce / exchange / allgather): calls, summed and longest
+        microseconds inside the collectives since the last read
+        (xfk_comm_timing; waits for the events, then clears them)."""
+        calls = (C.c_longlong * 3)()
+        tot = (C.c_double * 3)()
+        mx = (C.c_double * 3)()
+        _check(load_library().xfk_comm_timing(self._h, calls, tot, mx))
+        return {nm: {"calls": int(calls[k]), "us": float(tot[k]), "us_max_call": float(mx[k])}
+                for k, nm in enumerate(("allreduce", "exchange", "allgather"))}
 
     def replay(self) -> "Comm":
         """A communicator serving this rank's mode-2 recording cyclically
