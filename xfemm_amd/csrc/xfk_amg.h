@@ -81,7 +81,6 @@ struct AmgLevel {
     bool has16 = false;
     DBuf<unsigned short> a16, f16, r16, p16;
     DBuf<int> a16b, f16b, r16b, p16b;
-    DBuf<int> r16s;                   // R's tile column spans: the restriction's LDS window of r' (k_csr_mv_win)
     // level 0 (with has16): the V-cycle's transfers R and P~ with f32 values
     // (products and sums in f64; A keeps f64 -- a32 only with XFK_AMG_F32_SWEEP=1);
     // a sharded level 0 (unfolded) keeps R and P in f32, P with 16-bit

@@ -2195,62 +2195,6 @@ __global__ void __launch_bounds__(B) k_csr_mv_tile(int n, const int *__restrict_
     if (i < n) y[i] = ACC ? y0 + s : s;
 }
 
-// y = M x for the level-0 restriction R r' (f32 values, 16-bit tile columns):
-// the tile shape of k_csr_mv_tile, but the tile's window of x -- its columns
-// [cb, cb + span), read as 16-B pieces from an even start -- is first staged
-// in LDS, so the ~27 products of each row take x from LDS instead of as
-// scattered 8-B gathers from L2 (a 256-row tile of R reaches ~8k fine rows:
-// ~6.9k products over a 64 KiB window).  The same products summed in the
-// same order: bit-identical to k_csr_mv_tile.  A tile whose window does not
-// fit (span > WIN, or no 16-bit base) takes k_csr_mv_tile's path.
-template <int B, int SLOTS, int WIN>
-__global__ void __launch_bounds__(B) k_csr_mv_win(int n, int nx, const int *__restrict__ rowptr,
-                                                  const int *__restrict__ col, const float *__restrict__ val,
-                                                  const double *__restrict__ x, double *__restrict__ y,
-                                                  const int *done, const unsigned short *__restrict__ c16,
-                                                  const int *__restrict__ cbase, const int *__restrict__ span)
-{
-    const int dn = load_flag_v(done);
-    __shared__ __attribute__((aligned(16))) double lds[4 * SLOTS * B];
-    __shared__ __attribute__((aligned(16))) double xw[WIN];
-    const int t = xcd_tile(blockIdx.x, gridDim.x);
-    const int r0 = t * B;
-    const int i = r0 + threadIdx.x;
-    const TileRows tr = tile_rows<B>(r0, n, rowptr);
-    int cb = load_col_base(cbase, t);
-    int sp = load_col_base(span, t);
-    if (dn) return;
-    cb = __builtin_amdgcn_readfirstlane(cb);
-    sp = __builtin_amdgcn_readfirstlane(sp);
-    const int wb = cb & ~1;            // (16-B aligned start: x is hipMalloc'd)
-    const int wl = sp + (cb - wb);     // window length from wb
-    double s;
-    if (cb == kNoColBase || wl > WIN) {
-        s = cg_tile_spmv16<B, SLOTS>(tr, c16, cb, col, val, [&](int j) { return x[j]; }, lds);
-    } else {
-        for (int k = 2 * (int)threadIdx.x; k < wl; k += 2 * B) {
-            if (wb + k + 1 < nx) {
-                const double2 v = *reinterpret_cast<const double2 *>(x + wb + k);
-                xw[k] = v.x;
-                xw[k + 1] = v.y;
-            } else {
-                xw[k] = x[wb + k];
-            }
-        }
-        __syncthreads();
-        const int off = cb - wb;
-        s = tile_spmv_impl<B, SLOTS>(
-            tr,
-            [&](int k) {
-                const uint2 u = *reinterpret_cast<const uint2 *>(c16 + k);
-                return make_int4(off + (int)(u.x & 0xffffu), off + (int)(u.x >> 16), off + (int)(u.y & 0xffffu),
-                                 off + (int)(u.y >> 16));
-            },
-            [&](int k) { return off + (int)c16[k]; }, val, [&](int j) { return xw[j]; }, lds);
-    }
-    if (i < n) y[i] = s;
-}
-
 // y = M x (ACC: y += M x), G lanes per row (restriction R r, prolongation x += P xc)
 template <int G, bool ACC>
 __global__ void __launch_bounds__(256) k_csr_mv_g(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
@@ -2976,33 +2920,11 @@ static int r0_slots()
     return v;
 }
 
-// the level-0 restriction's LDS window of r' (XFK_R0_WIN, lab): 0 = off
-// (k_csr_mv_tile), 1 = 8192-entry window with 2 staging slots per lane,
-// 2 = 6144 with 4 slots, 3 = 4096 with 6 slots (80 KiB of LDS each)
-static int r0_win_mode()
-{
-    static const int v = [] {
-        const char *e = std::getenv("XFK_R0_WIN");
-        return e ? std::atoi(e) : 1;
-    }();
-    return v;
-}
-
-// span / nx: with R's tile spans (the level-0 restriction), the windowed
-// kernel over x of nx entries
 void launch_mv32(hipStream_t s, int n, const int *rowptr, const int *col, const float *val, const double *x,
-                 double *y, bool acc, int G, const int *done, const unsigned short *c16, const int *cbase,
-                 const int *span = nullptr, int nx = 0)
+                 double *y, bool acc, int G, const int *done, const unsigned short *c16, const int *cbase)
 {
     if (n <= 0) return;
     const int g = (n + 255) / 256;
-    if (span && c16 && !acc && r0_win_mode() > 0) {
-        const int m = r0_win_mode();
-        if (m == 2) k_csr_mv_win<256, 4, 6144><<<g, 256, 0, s>>>(n, nx, rowptr, col, val, x, y, done, c16, cbase, span);
-        else if (m == 3) k_csr_mv_win<256, 6, 4096><<<g, 256, 0, s>>>(n, nx, rowptr, col, val, x, y, done, c16, cbase, span);
-        else k_csr_mv_win<256, 2, 8192><<<g, 256, 0, s>>>(n, nx, rowptr, col, val, x, y, done, c16, cbase, span);
-        return;
-    }
     if (G > 4 && r0_slots() != 6 && !acc) {
         const int v = r0_slots();
         if (v == 8) k_csr_mv_tile<256, false, 8><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
@@ -3605,13 +3527,12 @@ static int transpose_csr(DBuf<int> &cnt, DBuf<char> &tmp, hipStream_t s, int n, 
 // 16-bit tile columns (xfk_spmv.h) of an n-row CSR in tiles of B rows, on st
 template <int B>
 static int build_col16(hipStream_t st, int n, const int *rowptr, const int *col, long long nnz,
-                       DBuf<unsigned short> &c16, DBuf<int> &base, DBuf<int> *span = nullptr)
+                       DBuf<unsigned short> &c16, DBuf<int> &base)
 {
     const int nt = (n + B - 1) / B;
     AMG_CHECK(c16.alloc((size_t)std::max(1LL, nnz)));
     AMG_CHECK(base.alloc((size_t)std::max(1, nt)));
-    if (span) AMG_CHECK(span->alloc((size_t)std::max(1, nt)));
-    if (nt > 0) k_tile_col16<B><<<nt, 256, 0, st>>>(n, rowptr, col, c16.p, base.p, span ? span->p : nullptr);
+    if (nt > 0) k_tile_col16<B><<<nt, 256, 0, st>>>(n, rowptr, col, c16.p, base.p);
     AMG_CHECK(hipGetLastError());
     return XFK_OK;
 }
@@ -3723,8 +3644,7 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         AMG_CHECK(hipEventRecord(sw.b, sw.cs));
         rt_pending = true;
     }
-    if (l == 0 && A.has16 &&
-        (rc = build_col16<256>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b, &A.r16s)) != XFK_OK)
+    if (l == 0 && A.has16 && (rc = build_col16<256>(ts, (int)nc, A.rrow.p, A.rcol.p, A.pnnz, A.r16, A.r16b)) != XFK_OK)
         return rc;
     if (l == 0 && A.has32 &&
         ((rc = to_f32(ts, (int)nc, A.rrow.p, A.pnnz, A.rval.p, A.r32)) != XFK_OK ||
@@ -5044,7 +4964,7 @@ static double *vcycle_level(Amg &M, hipStream_t s, int l, const double *b, doubl
     const long long rnnz = A.pnnz;
     XFK_PHASE(lv + "restriction R r", A.nz_bytes() * rnnz + 4.0 * (A.nc + 1) + 8.0 * A.n + 8.0 * A.nc,
               (A.has32 ? launch_mv32(s, A.nc, A.rrow.p, A.rcol.p, A.r32.p, A.r.p, C.b.p, false,
-                                     lanes_for((double)rnnz / A.nc), done, A.r16.p, A.r16b.p, A.r16s.p, A.n)
+                                     lanes_for((double)rnnz / A.nc), done, A.r16.p, A.r16b.p)
                        : launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, C.b.p, false,
                                    lanes_for((double)rnnz / A.nc), done, A.has16 ? A.r16.p : nullptr,
                                    A.has16 ? A.r16b.p : nullptr)));
@@ -5115,8 +5035,7 @@ double *Amg::vc_dist(hipStream_t s, int l, const double *b, double *out, const i
     // level 0 with f32 transfers: R and P in f32 with 16-bit tile columns
     auto restrict_to = [&](double *dst) {
         if (A.has32)
-            launch_mv32(s, A.nc, A.rrow.p, A.rcol.p, A.r32.p, A.r.p, dst, false, GR, done, A.r16.p, A.r16b.p,
-                        A.r16s.p, A.n);
+            launch_mv32(s, A.nc, A.rrow.p, A.rcol.p, A.r32.p, A.r.p, dst, false, GR, done, A.r16.p, A.r16b.p);
         else
             launch_mv(s, A.nc, A.rrow.p, A.rcol.p, A.rval.p, A.r.p, dst, false, GR, done);
     };

@@ -214,12 +214,10 @@ __device__ __forceinline__ double cg_tile_spmv(int r0, int N, const int *__restr
 // Per-tile 16-bit column offsets of a CSR (tiles of B rows): base[t] = the
 // tile's smallest column, c16[k] = col[k] - base[t]; kNoColBase when the
 // tile's columns span more than 65535.  One workgroup per tile.
-// span (optional): the tile's column extent hi - lo + 1 (0 for an empty
-// tile), for kernels that stage the tile's window of x in LDS
 template <int B>
 __global__ void __launch_bounds__(256) k_tile_col16(int n, const int *__restrict__ rowptr,
                                                     const int *__restrict__ col, unsigned short *__restrict__ c16,
-                                                    int *__restrict__ base, int *__restrict__ span = nullptr)
+                                                    int *__restrict__ base)
 {
     __shared__ int red[2 * 4];
     const int t = blockIdx.x, r0 = t * B, r1 = min(n, r0 + B);
@@ -243,10 +241,7 @@ __global__ void __launch_bounds__(256) k_tile_col16(int n, const int *__restrict
     lo = min(min(red[0], red[1]), min(red[2], red[3]));
     hi = max(max(red[4], red[5]), max(red[6], red[7]));
     const bool fits = e == s || (long long)hi - lo <= 65535;
-    if (threadIdx.x == 0) {
-        base[t] = fits ? (e == s ? 0 : lo) : kNoColBase;
-        if (span) span[t] = e == s ? 0 : (int)min(2147483647LL, (long long)hi - lo + 1);
-    }
+    if (threadIdx.x == 0) base[t] = fits ? (e == s ? 0 : lo) : kNoColBase;
     if (!fits) return;
     for (int k = s + threadIdx.x; k < e; k += 256) c16[k] = (unsigned short)(col[k] - lo);
 }
