@@ -18,6 +18,10 @@ for st in $STEPS; do
     bench) timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; rc=$? ;;
     benchq) timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; rc=$? ;;
     prof) bash tools/profile.sh $TAG; rc=$? ;;
+    sharded) timeout -k 10 300 python bench.py --force-sharded --steps 3 --warmup 1 --no-cpu-baseline \
+               > gpurun_out/bench_force_sharded_$TAG.json 2> gpurun_out/bench_force_sharded_$TAG.err && \
+             timeout -k 10 400 python bench.py --force-sharded --local-ranks 8 --shard-cells 3162 --steps 2 --warmup 1 \
+               > gpurun_out/bench_local8_$TAG.json 2> gpurun_out/bench_local8_$TAG.err; rc=$? ;;
     smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
