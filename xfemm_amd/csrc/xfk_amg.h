@@ -102,6 +102,8 @@ struct AmgStats {
 struct Amg {
     // parameters
     double theta = 0.08;              // strength threshold
+    double theta_coarse = -1.0;       // levels >= 1 (< 0: theta; XFK_AMG_THETA_COARSE overrides)
+    double theta_at(int l) const;
     int sweeps = 1;                   // Jacobi sweeps before and after the coarse correction
     int wlevel = -2;                  // W-cycle (two coarse corrections) at this folded level (-1: none; -2: XFK_AMG_W)
     int wcycle_level() const;

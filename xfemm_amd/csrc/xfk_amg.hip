@@ -3454,6 +3454,17 @@ void Amg::seed_hints()
     for (int l = 0; l < kAmgMaxLevels; ++l) mis_hint[l] = 12;
 }
 
+double Amg::theta_at(int l) const
+{
+    static const double env = [] {
+        const char *e = std::getenv("XFK_AMG_THETA_COARSE");
+        return e ? std::atof(e) : -1.0;
+    }();
+    if (l == 0) return theta;
+    if (env >= 0.0) return env;
+    return theta_coarse >= 0.0 ? theta_coarse : theta;
+}
+
 int Amg::setup(hipStream_t s, int n0, int ncl0, const int *rowptr0, const int *col0, const double *val0,
                long long nnz0)
 {
@@ -4087,7 +4098,7 @@ int Amg::build(hipStream_t s, int l0)
         }
         AMG_CHECK(sflag.alloc((size_t)A.nnz));
         AMG_CHECK(rho_part.alloc(2 * (size_t)nb_str(n)));
-        k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta, A.rowptr,
+        k_amg_strength<<<nb_str(n), kB, 0, s>>>(n, A.ncol_lim, theta_at(l), A.rowptr,
                                                 ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
                                                 A.val, absd.p, A.dinv.p, sflag.p, cnt.p,
                                                 dfinv.p, wF.p, rho_part.p, signed_strength());
@@ -4354,7 +4365,7 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
         AMG_CHECK(sflag.alloc((size_t)std::max(1LL, A.nnz)));
         AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(nl))));
         k_amg_diag<<<nb(nl), kB, 0, s>>>(nl, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
-        k_amg_strength<<<nb_str(nl), kB, 0, s>>>(nl, nl, theta, A.rowptr, ColView{A.col, nullptr, nullptr}, A.val,
+        k_amg_strength<<<nb_str(nl), kB, 0, s>>>(nl, nl, theta_at(l), A.rowptr, ColView{A.col, nullptr, nullptr}, A.val,
                                                  absd.p, A.dinv.p, sflag.p, cnt.p, dfinv.p, wF.p, rho_part.p,
                                                  signed_strength());
         k_max_reduce<<<1, 1024, 0, s>>>(nb_str(nl), rho_part.p, omega, rho.p + 2 * l);
