@@ -260,7 +260,6 @@ struct Amg {
     int build(hipStream_t s, int l0);
     int aggregate(hipStream_t s, int l, long long &nc, bool allow_stop);
     int joins_and_p_impl(hipStream_t s, int l);
-    const int *mis_und_last = nullptr;   // the undecided flag of the level's last MIS-2 round (device)
     int galerkin_dist(hipStream_t s, int l, int st, bool &rep);
     int fold_dist_tiles(hipStream_t s, int l);
     double *vc_dist(hipStream_t s, int l, const double *b, double *out, const int *done, int &rc);

@@ -523,37 +523,6 @@ __global__ void k_agg_join2(int n, const int *__restrict__ rowptr, ColView cv,
     agg[i] = (bj >= 0) ? agg1[bj] : -1;   // -1: isolated (or unreachable) -> no coarse dof
 }
 
-// a capped MIS-2 (XFK_MIS_CAP) leaves undecided rows without a root within
-// distance 2: one more join ring -- rows still out join the aggregate of their
-// largest-key strong neighbour that has one (ping-pong: in -> out).  und = 0
-// (the MIS finished within the cap): a copy
-__global__ void k_agg_joinx(int n, const int *__restrict__ rowptr, ColView cv, const unsigned char *__restrict__ sflag,
-                            const MisKey *__restrict__ key, const int *__restrict__ in, int *__restrict__ out,
-                            const int *und)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int a = in[i];
-    if (a >= 0 || *und == 0) {
-        out[i] = a;
-        return;
-    }
-    int bj = -1;
-    MisKey best = 0;
-    const int cb = cv.base(i);
-    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
-        if (sflag[k] != 1) continue;
-        const int j = cv.at(cb, k);
-        if (in[j] < 0) continue;
-        const MisKey kl = key_low(key[j]);
-        if (bj < 0 || kl > best) {
-            best = kl;
-            bj = j;
-        }
-    }
-    out[i] = (bj >= 0) ? in[bj] : -1;
-}
-
 // --------------------------------------------------------------------------
 // setup: R = P^T
 // --------------------------------------------------------------------------
@@ -3233,19 +3202,6 @@ static bool mis_xcd_on()
 }
 
 // XFK_NO_SPEC=1: no setup work enqueued ahead of a host check
-// MIS-2 rounds per level at most (XFK_MIS_CAP, lab; 0 = until the set is
-// maximal): rows still undecided then join neighbouring aggregates through
-// two more join rings (k_agg_joinx) instead of waiting for the last rounds,
-// whose launches handle < 0.5 % of the rows
-static int mis_cap()
-{
-    static const int v = [] {
-        const char *e = std::getenv("XFK_MIS_CAP");
-        return e ? std::max(0, std::atoi(e)) : 0;
-    }();
-    return v;
-}
-
 static bool spec_on()
 {
     static const bool v = [] {
@@ -3625,9 +3581,7 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
     bool joined = false;
     auto joins_and_p = [&]() { return joins_and_p_impl(s, l); };
     AMG_CHECK(mis_out.alloc(4));
-    const int cap = A.dist ? 0 : mis_cap();
     for (int batch = hint != mis_hint.end() ? std::max(1, hint->second) : 12;; batch = 2) {
-        if (cap > 0) batch = std::max(1, std::min(batch, cap - rounds));
         for (int b = 0; b < batch; ++b, ++rounds) {
             int *cur = und2 + (rounds & 1), *prev = und2 + ((rounds + 1) & 1);
             const bool last = b + 1 == batch;   // its update also writes the root flags
@@ -3653,8 +3607,7 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         }
         int rc = scan_only(*this, s, flag.p, cursor.p, n);   // cursor = root ids
         if (rc != XFK_OK) return rc;
-        mis_und_last = und2 + ((rounds - 1) & 1);
-        k_mis_pack<<<1, 64, 0, s>>>(cursor.p + n, mis_und_last, run, mis_out.p);
+        k_mis_pack<<<1, 64, 0, s>>>(cursor.p + n, und2 + ((rounds - 1) & 1), run, mis_out.p);
         AMG_CHECK(hipMemcpyAsync(host_int + 8, mis_out.p, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
         AMG_CHECK(hipEventRecord(ev_host, s));
         // while the host waits for the check, the device goes on with the
@@ -3663,7 +3616,7 @@ int Amg::aggregate(hipStream_t s, int l, long long &nc, bool allow_stop)
         joined = spec;
         if (spec && (rc = joins_and_p()) != XFK_OK) return rc;
         AMG_CHECK(hipEventSynchronize(ev_host));
-        if (!host_int[9] || (cap > 0 && rounds >= cap)) break;   // (capped: the joins take the rest)
+        if (!host_int[9]) break;
         joined = false;
         if (rounds > 4096) {
             set_error("AMG: MIS-2 aggregation did not terminate");
@@ -3727,10 +3680,6 @@ int Amg::joins_and_p_impl(hipStream_t s, int l)
     AMG_CHECK(agg.alloc(n));
     k_agg_join1<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, cursor.p, agg1.p);
     k_agg_join2<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, agg1.p, agg.p);
-    if (!A.dist && mis_cap() > 0) {   // capped MIS: two more rings for the rows left undecided
-        k_agg_joinx<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, agg.p, agg1.p, mis_und_last);
-        k_agg_joinx<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, agg1.p, agg.p, mis_und_last);
-    }
     k_agg_join3<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, A.rowptr, cv, A.val, agg.p, agg1.p);
     std::swap(agg.p, agg1.p);   // agg = the joined map
     std::swap(agg.n, agg1.n);
