@@ -66,8 +66,49 @@ def _configs2(tmp_path):
     return base
 
 
+def islands(cells=(30, 20), seed=3):
+    """Two disconnected square problems side by side, the second's node and
+    element numbering scrambled and interleaved with the first's: Cuthill's
+    restart for a multiply connected mesh (cuthill.cpp:267-301)."""
+    a, b = synth.magnetostatic(cells[0]), synth.magnetostatic(cells[1])
+    na = len(a["x"])
+    rng = np.random.default_rng(seed)
+    nb = len(b["x"])
+    perm = rng.permutation(nb)
+    inv = np.argsort(perm)
+    x = np.concatenate([a["x"], b["x"][inv] + 12.0])
+    y = np.concatenate([a["y"], b["y"][inv]])
+    p = np.concatenate([a["p"], perm[b["p"]] + na]).astype(np.int32)
+    lbl = np.concatenate([a["lbl"], b["lbl"]]).astype(np.int32)
+    e = np.concatenate([a["e"], b["e"]]).astype(np.int32)
+    order = rng.permutation(len(p))
+    return dict(a, x=x, y=y, p=p[order], lbl=lbl[order], e=e[order])
+
+
+def _islands(tmp_path):
+    base = str(tmp_path / "isl")
+    synth.write_problem(base, islands())
+    return base
+
+
+def _tiny(tmp_path):
+    """The smallest mesh: one square cell, two triangles, four nodes."""
+    base = str(tmp_path / "tiny")
+    synth.write_problem(base, synth.magnetostatic(1))
+    return base
+
+
+def _isolated_node(tmp_path):
+    """A node no element or edge uses (numcon 0: the reference's start node)."""
+    kw = synth.magnetostatic(12)
+    kw = dict(kw, x=np.append(kw["x"], 20.0), y=np.append(kw["y"], 20.0))
+    base = str(tmp_path / "iso")
+    synth.write_problem(base, kw)
+    return base
+
+
 CASES = {"temp": _temp, "torque": _torque, "torque_fine": _torque_fine, "scrambled80k": _scrambled,
-         "configs2": _configs2}
+         "configs2": _configs2, "islands": _islands, "tiny": _tiny, "isolated_node": _isolated_node}
 
 
 def renumber_matches_reference(base):
@@ -100,7 +141,8 @@ def renumber_matches_reference(base):
     return dict(nodes=len(x), elements=len(p), pbcs=len(pbc), quad=len(quad), bandwidth=fs.BandWidth)
 
 
-@pytest.mark.parametrize("case", ["temp", "torque", "torque_fine", "scrambled80k", "configs2"])
+@pytest.mark.parametrize("case", ["temp", "torque", "torque_fine", "scrambled80k", "configs2", "islands", "tiny",
+                                  "isolated_node"])
 def test_host_renumbering_equals_reference_cuthill(tmp_path, case, monkeypatch):
     monkeypatch.setenv("XFEMM_HOST_SORT", "1")
     info = renumber_matches_reference(CASES[case](tmp_path))
@@ -109,7 +151,8 @@ def test_host_renumbering_equals_reference_cuthill(tmp_path, case, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["temp", "torque", "torque_fine", "scrambled80k", "configs2"])
+@pytest.mark.parametrize("case", ["temp", "torque", "torque_fine", "scrambled80k", "configs2", "islands", "tiny",
+                                  "isolated_node"])
 def test_device_sort_renumbering_equals_reference_cuthill(tmp_path, case, monkeypatch):
     monkeypatch.delenv("XFEMM_HOST_SORT", raising=False)
     assert kernels.device_count() > 0
