@@ -863,7 +863,7 @@ int build_symbolic(xfk_problem *P)
         XFK_CHECK(hipcub::DeviceReduce::Max(tmp, bytes, T.rowcnt, T.cnt + 3, N, s));
         XFK_CHECK(hipMemcpyAsync(P->hpin + 5, T.cnt + 3, sizeof(int), hipMemcpyDeviceToHost, s));
     }
-    // single-device static problems without air gaps or periodic maps read
+    // static problems without air gaps or periodic maps read
     // the lengths back later (xfk_resolve_nnz, at the preconditioner setup):
     // the pattern is filled and the matrix assembled into arrays sized for
     // the bound 6 NE + N + fill-in (a triangle adds at most six off-diagonal
@@ -872,7 +872,9 @@ int build_symbolic(xfk_problem *P)
     // meshes the one host check is negligible next to the memory the bound
     // would hold, ~0.7 GB on the configs[4] mesh)
     const long long bound_nnz = 6LL * NE + N + nfill;
-    const bool defer = !P->harmonic && !P->comm && P->age_key.empty() && P->pbc_entry_key.empty() &&
+    // (a sharded rank defers too: its halo plan was made at creation, and the
+    // lengths are first needed by the AMG setup, after the assembly)
+    const bool defer = !P->harmonic && P->age_key.empty() && P->pbc_entry_key.empty() &&
                        bound_nnz * 12 <= (512LL << 20);
     long long cap_nnz;
     if (defer) {
