@@ -15,7 +15,7 @@ for st in $STEPS; do
   case $st in
     tests) timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread \
              > gpurun_out/gpu_tests_$TAG.log 2>&1; rc=$? ;;
-    bench) timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; rc=$? ;;
+    bench) timeout -k 10 500 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; rc=$? ;;
     benchq) timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; rc=$? ;;
     prof) bash tools/profile.sh $TAG; rc=$? ;;
     sharded) timeout -k 10 300 python bench.py --force-sharded --steps 3 --warmup 1 --no-cpu-baseline \
