@@ -469,6 +469,8 @@ def fsolver_cold_process(args):
     import tempfile
     from xfemm_amd import synth
     exe = os.path.join(ROOT, "xfemm_amd", "bin", "fsolver")
+    if not os.path.exists(exe):
+        return {"skipped": "xfemm_amd/bin/fsolver is not built"}
     out = []
     with tempfile.TemporaryDirectory() as td:
         with tarfile.open(os.path.join(ROOT, "tests", "golden", "torque", "TorqueBenchmark_fine_30.tgz")) as tf:

@@ -145,6 +145,7 @@ int xfk_comm::begin(int op, hipStream_t s, int &idx, int &waited)
         idx = (int)streams.size();
         streams.push_back(s);
     }
+    if (op_slot >= 0) ev_pool.push_back(op_start);   // (a collective that failed before end(): its start event back)
     op_slot = -1;
     if (timing) {   // the start event follows the order wait: the interval is the collective itself
         op_slot = op == XFK_COMM_ALLREDUCE ? 0 : op == XFK_COMM_EXCHANGE ? 1 : 2;
