@@ -2195,41 +2195,6 @@ __global__ void __launch_bounds__(B) k_csr_mv_tile(int n, const int *__restrict_
     if (i < n) y[i] = ACC ? y0 + s : s;
 }
 
-// y = M x with one lane per row, f32 values, 16-bit columns in 256-row tiles
-// (lab, XFK_R0_ROW1=1: the level-0 restriction without the LDS staging --
-// each lane walks its own ~27-entry row, its loads in flight four at a time;
-// the products summed in the row's order, as k_csr_mv_tile sums them)
-__global__ void __launch_bounds__(256) k_csr_mv_row1(int n, const int *__restrict__ rowptr,
-                                                     const int *__restrict__ col, const float *__restrict__ val,
-                                                     const double *__restrict__ x, double *__restrict__ y,
-                                                     const int *done, const unsigned short *__restrict__ c16,
-                                                     const int *__restrict__ cbase)
-{
-    const int dn = load_flag_v(done);
-    const int t = xcd_tile(blockIdx.x, gridDim.x);
-    const int i = t * 256 + threadIdx.x;
-    const int cb = load_col_base(cbase, t);
-    const int s = i < n ? rowptr[i] : 0, e = i < n ? rowptr[i + 1] : 0;
-    if (dn || i >= n) return;
-    double acc = 0.0;
-    int k = s;
-    if (cb != kNoColBase) {
-        for (; k + 4 <= e; k += 4) {
-            const int j0 = cb + c16[k], j1 = cb + c16[k + 1], j2 = cb + c16[k + 2], j3 = cb + c16[k + 3];
-            const float v0 = val[k], v1 = val[k + 1], v2 = val[k + 2], v3 = val[k + 3];
-            const double x0 = x[j0], x1 = x[j1], x2 = x[j2], x3 = x[j3];
-            acc += (double)v0 * x0;
-            acc += (double)v1 * x1;
-            acc += (double)v2 * x2;
-            acc += (double)v3 * x3;
-        }
-        for (; k < e; ++k) acc += (double)val[k] * x[cb + c16[k]];
-    } else {
-        for (; k < e; ++k) acc += (double)val[k] * x[col[k]];
-    }
-    y[i] = acc;
-}
-
 // y = M x (ACC: y += M x), G lanes per row (restriction R r, prolongation x += P xc)
 template <int G, bool ACC>
 __global__ void __launch_bounds__(256) k_csr_mv_g(int n, const int *__restrict__ rowptr, const int *__restrict__ col,
@@ -2955,24 +2920,11 @@ static int r0_slots()
     return v;
 }
 
-static bool r0_row1_on()
-{
-    static const bool v = [] {
-        const char *e = std::getenv("XFK_R0_ROW1");
-        return e && std::atoi(e) != 0;
-    }();
-    return v;
-}
-
 void launch_mv32(hipStream_t s, int n, const int *rowptr, const int *col, const float *val, const double *x,
                  double *y, bool acc, int G, const int *done, const unsigned short *c16, const int *cbase)
 {
     if (n <= 0) return;
     const int g = (n + 255) / 256;
-    if (G > 4 && !acc && c16 && r0_row1_on()) {
-        k_csr_mv_row1<<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
-        return;
-    }
     if (G > 4 && r0_slots() != 6 && !acc) {
         const int v = r0_slots();
         if (v == 8) k_csr_mv_tile<256, false, 8><<<g, 256, 0, s>>>(n, rowptr, col, val, x, y, done, c16, cbase);
