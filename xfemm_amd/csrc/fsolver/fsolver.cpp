@@ -943,7 +943,13 @@ bool FSolver::permute_elements(Src src)
     huge_reserve(out, (size_t)std::max(0, NumEls));
     out.resize((size_t)std::max(0, NumEls));   // (NoInitAlloc: written below, in parallel)
     par_for(NumEls, 1 << 16, [&](long long a, long long b) {
-        for (long long k = a; k < b; k++) ::new (&out[k]) CMElement(meshele[src(k)]);
+        // (the sources are scattered: each 40-B record is a cache miss, so the
+        // one kPf ahead is requested while this one is copied)
+        constexpr long long kPf = 16;
+        for (long long k = a; k < b; k++) {
+            if (k + kPf < b) __builtin_prefetch(&meshele[src(k + kPf)], 0, 0);
+            ::new (&out[k]) CMElement(meshele[src(k)]);
+        }
     });
     meshele.swap(out);
     static_assert(std::is_trivially_destructible<CMElement>::value, "uninitialised storage");
