@@ -1833,6 +1833,7 @@ void xfk_problem_destroy(xfk_problem *P)
     if (!P) return;
     (void)hipSetDevice(P->device);
     if (P->stream) (void)hipStreamSynchronize(P->stream);
+    for (auto &ev : P->pass_ev) (void)hipEventDestroy(ev);
     for (auto &ev : P->spmv_ev) (void)hipEventDestroy(ev);
     for (auto &ev : P->setup_ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -2697,6 +2698,15 @@ static int static2d_run(xfk_problem *P, int flags, xfk_result *res)
         }
         P->pcg_tol = pass_tol;
         P->pcg_tol_rel = pass_rel;
+        // per-pass events, read once after the loop (no host wait per pass)
+        while ((int)P->pass_ev.size() < 3 * (Iter + 1)) {
+            hipEvent_t ev_new = nullptr;
+            XFK_CHECK(hipEventCreate(&ev_new));
+            P->pass_ev.push_back(ev_new);
+        }
+        e0 = P->pass_ev[3 * Iter];
+        e1 = P->pass_ev[3 * Iter + 1];
+        e2 = P->pass_ev[3 * Iter + 2];
         XFK_CHECK(hipEventRecord(e0, s));
         if (Iter > 0 && (rc = exchange(P, P->V.p)) != XFK_OK) return rc;   // halo of V for the element B
         rc = assemble(P, Iter);
@@ -2708,11 +2718,6 @@ static int static2d_run(xfk_problem *P, int flags, xfk_result *res)
         rc = pcg_solve(P, Iter, cap);
         if (rc != XFK_OK) return rc;
         XFK_CHECK(hipEventRecord(e2, s));
-        XFK_CHECK(hipEventSynchronize(e2));
-        XFK_CHECK(hipEventElapsedTime(&ms, e0, e1));
-        R.ms_assemble += ms;
-        XFK_CHECK(hipEventElapsedTime(&ms, e1, e2));
-        R.ms_solve += ms;
         R.cg_iters += P->pcg_host->iters;
         R.final_er = P->pcg_host->er;
         P->amg_last_iters = P->pcg_host->iters - P->pcg_discarded;
@@ -2760,6 +2765,12 @@ static int static2d_run(xfk_problem *P, int flags, xfk_result *res)
     XFK_CHECK(hipStreamSynchronize(s));
     XFK_CHECK(hipEventElapsedTime(&ms, es0, es1));
     R.ms_symbolic = ms;
+    for (int k = 0; k < Iter; ++k) {
+        XFK_CHECK(hipEventElapsedTime(&ms, P->pass_ev[3 * k], P->pass_ev[3 * k + 1]));
+        R.ms_assemble += ms;
+        XFK_CHECK(hipEventElapsedTime(&ms, P->pass_ev[3 * k + 1], P->pass_ev[3 * k + 2]));
+        R.ms_solve += ms;
+    }
     for (int k = 0; k < P->setup_used; ++k) {
         float m = 0;
         XFK_CHECK(hipEventElapsedTime(&m, P->setup_ev[2 * k], P->setup_ev[2 * k + 1]));

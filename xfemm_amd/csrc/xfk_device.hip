@@ -1312,8 +1312,19 @@ __global__ void __launch_bounds__(kBlock) k_newton_res(int N, const double *__re
     __shared__ double red[8];
     __shared__ int last;
     double dx = 0.0, vv = 0.0;
-    for (int r = blockIdx.x * kBlock + threadIdx.x; r < N; r += gridDim.x * kBlock) {
-        double v = V[r], d = v - Vold[r];
+    // two rows per lane and step (16-B loads; V, Vold hipMalloc'd), the odd
+    // last row by the lane that would hold its pair
+    const int np = N >> 1;
+    for (int q = blockIdx.x * kBlock + threadIdx.x; q < np; q += gridDim.x * kBlock) {
+        const double2 v = reinterpret_cast<const double2 *>(V)[q], o = reinterpret_cast<const double2 *>(Vold)[q];
+        const double d0 = v.x - o.x, d1 = v.y - o.y;
+        dx += d0 * d0;
+        dx += d1 * d1;
+        vv += v.x * v.x;
+        vv += v.y * v.y;
+    }
+    if ((N & 1) && blockIdx.x * kBlock + threadIdx.x == np % (gridDim.x * kBlock)) {
+        const double v = V[N - 1], d = v - Vold[N - 1];
         dx += d * d;
         vv += v * v;
     }
@@ -1528,7 +1539,9 @@ void launch_diag_inv(hipStream_t s, int N, const int *diag, const double *val, d
 void launch_newton_res(hipStream_t s, int N, const double *V, const double *Vold, double *partials,
                        unsigned *counter, NewtonScalars *S)
 {
-    k_newton_res<<<grid_reduce(N), kBlock, 0, s>>>(N, V, Vold, partials, counter, S);
+    // (256 workgroups: the last-workgroup ticket is one atomic per workgroup
+    // on one counter -- 1024 of them cost ~15 us of a 21 us launch at 1M rows)
+    k_newton_res<<<std::min(grid_reduce(N), 256), kBlock, 0, s>>>(N, V, Vold, partials, counter, S);
 }
 void launch_relax(hipStream_t s, int N, double relax, double *V, const double *Vold)
 {

@@ -534,6 +534,7 @@ struct xfk_problem {
     // live SpMV launch timing (XFK_TIME_SPMV)
     bool time_spmv = false;
     std::vector<hipEvent_t> spmv_ev;   // pairs
+    std::vector<hipEvent_t> pass_ev;   // static Newton loop: (start, assembled, solved) per pass, read at the end
     int spmv_used = 0;
 
     // last-solve statistics
