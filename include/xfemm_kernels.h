@@ -525,14 +525,29 @@ int xfk_sort_elements(int n_elems, const unsigned *score, int device, int *perm)
  * as the reference's element loop does (FSolver::Static2D,
  * cfemm/fsolver/static2d.cpp:509-583; StaticAxisymmetric staticaxi.cpp:350-406):
  * the centroid of element i (nodes p[3i..3i+2], coordinates x, y in cm)
- * in drawing units gives x y r z theta R, and t[i] is the real part of
- * `fctn` in degrees (mag_dir when the expression returns nothing).  The
- * expression language is the reference Lua's (complex numbers, the math
- * library, PI, I), evaluated natively; errors carry the reference's messages
- * ("Lua error occurred when evaluating: ...", "... does not evaluate to a
- * numerical value").  Host only: no device is needed. */
+ * in drawing units gives x y r z theta R, and t[i] is the real part of the
+ * last value `fctn` returns, in degrees (mag_dir when it returns nothing).
+ * The chunk runs on a native restatement of the reference's Lua 4
+ * interpreter (complex numbers; the base, string and math libraries; tables,
+ * closures, LuaInstance's Complex and pi; xfk_lua.h lists what is refused),
+ * one interpreter for all n_elems elements in order, globals persisting from
+ * one to the next; errors carry the reference's messages ("Lua error occurred
+ * when evaluating: ...", "... does not evaluate to a numerical value").
+ * Host only: no device is needed. */
 int xfk_magdir_eval(const char *fctn, int n_elems, const int *p, const double *x, const double *y,
                     int length_units, double mag_dir, double *t);
+
+/* A whole problem's element loop (what xfk_problem_create runs): element i
+ * runs its label lbl[i]'s function fctns[lbl[i]] (NULL or "": the label's
+ * mag_dirs[lbl[i]], nothing run) on ONE interpreter, in element order, as the
+ * reference's one Lua state per FSolver does; `axisymmetric` selects
+ * staticaxi.cpp's chunk (r and z set first).  `repeats` != 0: the problem is
+ * nonlinear, whose Newton loop re-runs the element loop every pass
+ * (static2d.cpp:997-1008) -- refused (XFK_ERR_ARG, "not supported") when a
+ * chunk changed state a later pass would see or left values on the stack. */
+int xfk_magdir_eval_labels(int n_labels, const char *const *fctns, const double *mag_dirs, int n_elems,
+                           const int *p, const int *lbl, const double *x, const double *y, int length_units,
+                           int axisymmetric, int repeats, double *t);
 
 #ifdef __cplusplus
 }

@@ -283,16 +283,36 @@ class _Keep:
 def element_magdir(pr: femfile.FemProblem, mesh: femfile.Mesh) -> np.ndarray:
     """Per-element magnetisation direction (degrees): the label's MagDir, or
     what the reference's Lua makes of its MagDirFctn at the element centroid
-    (ref_magdir).  Static problems only, as the reference."""
-    lbl = np.asarray(mesh.lbl)
-    t = np.array([lb.MagDir for lb in pr.labels], float)[lbl]
-    for k, lb in enumerate(pr.labels):
-        if not lb.MagDirFctn:
-            continue
-        sel = np.where(lbl == k)[0]
-        if len(sel):
-            t[sel] = ref_magdir(lb.MagDirFctn, np.asarray(mesh.p)[sel], mesh.x, mesh.y, pr.LengthUnits, lb.MagDir)
-    return t
+    -- the whole element loop on one interpreter, in element order, as the
+    reference's one Lua state per FSolver (ref_magdir_labels).  Static
+    problems only, as the reference."""
+    return ref_magdir_labels([lb.MagDirFctn for lb in pr.labels], [lb.MagDir for lb in pr.labels], mesh.p,
+                             mesh.lbl, mesh.x, mesh.y, pr.LengthUnits, pr.ProblemType == 1)
+
+
+def ref_magdir_labels(fctns, mag_dirs, p, lbl, x, y, length_units: int, axisymmetric: bool = False) -> np.ndarray:
+    """A whole problem's element loop through the reference's own Lua
+    (oracle/_ref/libreflua.so ref_lua_magdir_labels: element i runs label
+    lbl[i]'s function on one interpreter, static2d.cpp:509-583 /
+    staticaxi.cpp:350-406).  Raises ValueError with the reference's message."""
+    ref_magdir("", np.zeros((0, 3), np.int32), np.zeros(1), np.zeros(1), 0, 0.0)   # (loads the library)
+    _lua.ref_lua_magdir_labels.argtypes = [C.POINTER(C.c_char_p), dptr, C.c_int, iptr, iptr, dptr, dptr, C.c_int,
+                                           C.c_int, dptr, C.c_char_p, C.c_int]
+    _lua.ref_lua_magdir_labels.restype = C.c_int
+    p = _arr(np.asarray(p).reshape(-1), np.int32)
+    lbl = _arr(lbl, np.int32)
+    x, y = _arr(x, np.float64), _arr(y, np.float64)
+    md = _arr(mag_dirs, np.float64)
+    fa = (C.c_char_p * max(1, len(fctns)))(*[(f or "").encode() for f in fctns])
+    n = len(lbl)
+    t = np.zeros(max(1, n))
+    msg = C.create_string_buffer(8192)
+    rc = _lua.ref_lua_magdir_labels(fa, md.ctypes.data_as(dptr), n, p.ctypes.data_as(iptr), lbl.ctypes.data_as(iptr),
+                                    x.ctypes.data_as(dptr), y.ctypes.data_as(dptr), int(length_units),
+                                    int(bool(axisymmetric)), t.ctypes.data_as(dptr), msg, len(msg))
+    if rc != 0:
+        raise ValueError(msg.value.decode())
+    return t[:n]
 
 
 def make_problem(pr: femfile.FemProblem, mesh: femfile.Mesh):

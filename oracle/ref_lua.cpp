@@ -6,12 +6,18 @@
 // does (cfemm/fsolver/static2d.cpp:509-583): centroid in CComplex, the chunk
 // "x=%.17g\ny=%.17g\nr=x\nz=y\ntheta=%.17g\nR=%.17g\nreturn %s", lua_dostring
 // on one interpreter kept across elements (LuaInstance opens the base, string,
-// math and io libraries, LuaInstance.cpp:185-197), Re of the value left on
-// the stack.  The product's native evaluator (xfemm_amd/csrc/xfk_magdir.cpp)
+// math and io libraries, then LuaInstance's own globals, LuaInstance.cpp:
+// 185-208), Re of the value left on the stack.  LuaInstance.cpp itself needs
+// the build-generated femmversion.h, so its five C functions are restated
+// here as harness code (Complex as LuaInstance.cpp:228-241; the compatibility
+// flag; femmVersion raises a Lua error; trace does nothing) and registered in
+// its order, with its `pi` global -- the global table then holds the same
+// names in the same order as the reference's.  The product's native evaluator (xfemm_amd/csrc/xfk_magdir.cpp)
 // and the oracle's per-element directions are checked against this.
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "femmcomplex.h"
 #include "lua.h"
@@ -19,10 +25,43 @@
 
 #define PI 3.141592653589793238462643383   // femmconstants.h:28
 
-// Returns 0, or -7 (Static2D's return code) with `msg` set to the reference's
-// warning text.
-extern "C" int ref_lua_magdir(const char *fctn, int n, const int *p, const double *x, const double *y,
-                              int length_units, double mag_dir, double *t, char *msg, int msglen)
+static bool compat_mode = false;
+
+static int h_complex(lua_State *L)   // LuaInstance::luaComplex (LuaInstance.cpp:228-241)
+{
+    CComplex y;
+    int numArgs = lua_gettop(L);
+    if (numArgs == 2) y = lua_tonumber(L, 1) + I * lua_tonumber(L, 2);
+    else if (numArgs == 1) y = lua_tonumber(L, 1);
+    else y = 0;
+    lua_pushnumber(L, y);
+    return 1;
+}
+static int h_setcompat(lua_State *L)
+{
+    if (lua_gettop(L) != 0) compat_mode = (1 == lua_tonumber(L, 1).Re());
+    return 0;
+}
+static int h_getcompat(lua_State *L)
+{
+    lua_pushnumber(L, CComplex(compat_mode ? 1.0 : 0.0));
+    return 1;
+}
+static int h_femmversion(lua_State *L)
+{
+    lua_error(L, "femmVersion: not available in this harness");
+    return 0;
+}
+static int h_trace(lua_State *) { return 0; }
+
+// One interpreter for the whole element loop, as the reference keeps one per
+// FSolver: element i runs its label's function (`fctn_of(i)`, NULL: the
+// label's MagDir, nothing run).  Axisymmetric problems use staticaxi.cpp's
+// chunk (r and z first, staticaxi.cpp:366-367).  Returns 0, or -7 (Static2D's
+// return code) with `msg` set to the reference's warning text.
+template <class F>
+static int run_elements(F fctn_of, const double *mag_dirs_of_elem, int n, const int *p, const double *x,
+                        const double *y, int length_units, int axisymmetric, double *t, char *msg, int msglen)
 {
     double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};   // static2d.cpp:67
     lua_State *lua = lua_open(4096);
@@ -30,19 +69,31 @@ extern "C" int ref_lua_magdir(const char *fctn, int n, const int *p, const doubl
     lua_strlibopen(lua);
     lua_mathlibopen(lua);
     lua_iolibopen(lua);
+    compat_mode = false;
+    lua_register(lua, "Complex", h_complex);   // LuaInstance.cpp:200-207
+    lua_register(lua, "setcompatibilitymode", h_setcompat);
+    lua_register(lua, "getcompatibilitymode", h_getcompat);
+    lua_register(lua, "femmVersion", h_femmversion);
+    lua_register(lua, "trace", h_trace);
+    lua_pushnumber(lua, CComplex(PI));
+    lua_setglobal(lua, "pi");
     int rc = 0;
     for (int i = 0; i < n && rc == 0; ++i) {
+        const char *fctn = fctn_of(i);
+        t[i] = mag_dirs_of_elem[i];
+        if (!fctn) continue;
         const int *nd = p + 3L * i;
         char magbuff[4096];
         CComplex X;
         int j;
         for (j = 0, X = 0; j < 3; j++) X += (CComplex)(x[nd[j]] + I * y[nd[j]]);
         X = X / units[length_units] / 3.;
-        snprintf(magbuff, sizeof magbuff, "x=%.17g\ny=%.17g\nr=x\nz=y\ntheta=%.17g\nR=%.17g\nreturn %s", (X.re),
-                 (X.im), (arg(X) * 180 / PI), (abs(X)), fctn);
+        snprintf(magbuff, sizeof magbuff,
+                 axisymmetric ? "r=%.17g\nz=%.17g\nx=r\ny=z\ntheta=%.17g\nR=%.17g\nreturn %s"
+                              : "x=%.17g\ny=%.17g\nr=x\nz=y\ntheta=%.17g\nR=%.17g\nreturn %s",
+                 (X.re), (X.im), (arg(X) * 180 / PI), (abs(X)), fctn);
         const int top1 = lua_gettop(lua);
         const int code = lua_dostring(lua, magbuff);
-        t[i] = mag_dir;
         if (code != 0) {
             snprintf(msg, msglen, "Lua error occurred when evaluating:\n\"%s\"", fctn);
             rc = -7;
@@ -62,4 +113,26 @@ extern "C" int ref_lua_magdir(const char *fctn, int n, const int *p, const doubl
     }
     lua_close(lua);
     return rc;
+}
+
+// One function over n elements (a planar label's elements).
+extern "C" int ref_lua_magdir(const char *fctn, int n, const int *p, const double *x, const double *y,
+                              int length_units, double mag_dir, double *t, char *msg, int msglen)
+{
+    std::vector<double> md((size_t)n, mag_dir);
+    return run_elements([&](int) { return fctn; }, md.data(), n, p, x, y, length_units, 0, t, msg, msglen);
+}
+
+// A whole problem's element loop: label lbl[i]'s function (NULL or "" for
+// none) and MagDir.
+extern "C" int ref_lua_magdir_labels(const char *const *fctns, const double *mag_dirs, int n, const int *p,
+                                     const int *lbl, const double *x, const double *y, int length_units,
+                                     int axisymmetric, double *t, char *msg, int msglen)
+{
+    std::vector<double> md((size_t)n);
+    for (int i = 0; i < n; ++i) md[i] = mag_dirs[lbl[i]];
+    return run_elements([&](int i) -> const char * {
+        const char *f = fctns[lbl[i]];
+        return (f && *f) ? f : nullptr;
+    }, md.data(), n, p, x, y, length_units, axisymmetric, t, msg, msglen);
 }

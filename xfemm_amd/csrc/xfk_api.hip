@@ -1964,50 +1964,44 @@ int prepare_magdir(const xfk_problem_desc *d, GlobalPrep &G)
 {
     // Functional magnetisation directions (static2d.cpp:509-583,
     // staticaxi.cpp:350-406): the reference runs the label's Lua chunk for
-    // every element in every Newton pass; the result depends on the centroid
-    // only, so it is evaluated once here (xfk_magdir.cpp, the same angle to
-    // the bit) and each element of such a label gets a label entry of its own
+    // every element in every Newton pass, on one interpreter whose globals
+    // persist from element to element.  The chunks run here once, in element
+    // order on one native interpreter (xfk_magdir.cpp over xfk_lua.cpp, the
+    // same angle to the bit); a nonlinear problem's later passes would give
+    // the same angles unless a chunk changed state, which MagDir::repeatable
+    // refuses.  Each element of such a label gets a label entry of its own
     // carrying cos / sin of its angle -- the device kernels are unchanged.
-    std::vector<std::shared_ptr<const MagDirExpr>> ex(d->n_labels);
-    bool any = false;
-    std::string err;
-    // only labels that own elements: the reference runs the chunk while
-    // assembling an element, so a label without elements is never evaluated
-    std::vector<char> used(d->n_labels, 0), fctn(d->n_labels, 0);
     bool any_fctn = false;
     for (int k = 0; k < d->n_labels; ++k) {
         const char *f = d->labels[k].mag_dir_fctn;
-        fctn[k] = (f && *f) ? 1 : 0;
-        any_fctn |= fctn[k] != 0;
+        any_fctn |= (f && *f);
     }
     if (!any_fctn) return XFK_OK;
-    for (int i = 0; i < d->n_elems; ++i) used[d->lbl[i]] = 1;
-    for (int k = 0; k < d->n_labels; ++k) {
-        const char *f = d->labels[k].mag_dir_fctn;
-        if (!fctn[k] || !used[k]) continue;
-        ex[k] = magdir_parse(f, err);
-        XFK_REQUIRE(ex[k] != nullptr, XFK_ERR_ARG, err.c_str());
-        any = true;
-    }
-    if (!any) return XFK_OK;
     const int NE = d->n_elems;
-    G.elab.assign(d->lbl, d->lbl + NE);
+    MagDir md(d->problem_type == XFK_AXISYMMETRIC);
+    std::string err;
+    bool any = false;
+    std::vector<int> elab(d->lbl, d->lbl + NE);
     for (int i = 0; i < NE; ++i) {
         const int l = d->lbl[i];
-        if (!ex[l]) continue;
+        const char *f = d->labels[l].mag_dir_fctn;
+        if (!f || !*f) continue;
         double X[3], Y[3], t = 0;
         for (int j = 0; j < 3; ++j) {
             X[j] = d->x[d->p[3LL * i + j]];
             Y[j] = d->y[d->p[3LL * i + j]];
         }
-        XFK_REQUIRE(magdir_eval(*ex[l], X, Y, d->length_units, d->labels[l].mag_dir, &t, err), XFK_ERR_ARG,
-                    err.c_str());
+        XFK_REQUIRE(md.eval(f, X, Y, d->length_units, d->labels[l].mag_dir, &t, err), XFK_ERR_ARG, err.c_str());
         DevLabel v = G.lab[l];
         v.cos_m = cos(t * kPI / 180.);   // static2d.cpp:593-595
         v.sin_m = sin(t * kPI / 180.);
-        G.elab[i] = (int)G.lab.size();
+        elab[i] = (int)G.lab.size();
         G.lab.push_back(v);
+        any = true;
     }
+    if (!any) return XFK_OK;
+    if (G.any_nonlinear) XFK_REQUIRE(md.repeatable(err), XFK_ERR_ARG, err.c_str());
+    G.elab.swap(elab);
     return XFK_OK;
 }
 

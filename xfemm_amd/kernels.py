@@ -54,7 +54,7 @@ EXPORTED = (
     "xfk_comm_rank", "xfk_comm_size", "xfk_comm_record", "xfk_comm_log", "xfk_comm_create_replay",
     "xfk_comm_time", "xfk_comm_timing",
     "xfk_partition_plan", "xfk_partition_plan_coupled", "xfk_problem_create_dist", "xfk_dist_get_info",
-    "xfk_magdir_eval", "xfk_sort_elements",
+    "xfk_magdir_eval", "xfk_magdir_eval_labels", "xfk_sort_elements",
 )
 
 
@@ -198,6 +198,8 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_dist_get_info.argtypes = [vp, C.POINTER(DistInfo)]
     L.xfk_sort_elements.argtypes = [C.c_int, C.POINTER(C.c_uint), C.c_int, iptr]
     L.xfk_magdir_eval.argtypes = [C.c_char_p, C.c_int, iptr, dptr, dptr, C.c_int, C.c_double, dptr]
+    L.xfk_magdir_eval_labels.argtypes = [C.c_int, C.POINTER(C.c_char_p), dptr, C.c_int, iptr, iptr, dptr, dptr,
+                                         C.c_int, C.c_int, C.c_int, dptr]
     _lib = L
     return L
 
@@ -350,6 +352,27 @@ def magdir_eval(fctn: str, p, x, y, length_units: int = 0, mag_dir: float = 0.0)
     t = np.zeros(max(1, n))
     _check(L.xfk_magdir_eval(fctn.encode(), n, p.ctypes.data_as(iptr), x.ctypes.data_as(dptr),
                              y.ctypes.data_as(dptr), int(length_units), float(mag_dir), t.ctypes.data_as(dptr)))
+    return t[:n]
+
+
+def magdir_eval_labels(fctns, mag_dirs, p, lbl, x, y, length_units: int = 0, axisymmetric: bool = False,
+                       repeats: bool = False) -> np.ndarray:
+    """A whole problem's element loop of MagDirFctn (xfk_magdir_eval_labels):
+    element i runs label lbl[i]'s function (None / "" for the label's MagDir)
+    on one interpreter, in element order.  Host only."""
+    L = load_library()
+    p = np.ascontiguousarray(np.asarray(p, dtype=np.int32).reshape(-1))
+    lbl = np.ascontiguousarray(lbl, dtype=np.int32)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    md = np.ascontiguousarray(mag_dirs, dtype=np.float64)
+    fa = (C.c_char_p * max(1, len(fctns)))(*[(f or "").encode() for f in fctns])
+    n = len(lbl)
+    t = np.zeros(max(1, n))
+    _check(L.xfk_magdir_eval_labels(len(fctns), fa, md.ctypes.data_as(dptr), n, p.ctypes.data_as(iptr),
+                                    lbl.ctypes.data_as(iptr), x.ctypes.data_as(dptr), y.ctypes.data_as(dptr),
+                                    int(length_units), int(bool(axisymmetric)), int(bool(repeats)),
+                                    t.ctypes.data_as(dptr)))
     return t[:n]
 
 
