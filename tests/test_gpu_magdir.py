@@ -60,8 +60,8 @@ def test_lua_mag_direction_fixture_fem_to_ans(tmp_path):
     assert err <= TOL, err
 
 
-def magnet_problem(fctn, axisymmetric=False):
-    kw = synth.axisymmetric(40) if axisymmetric else synth.magnetostatic(40)
+def magnet_problem(fctn, axisymmetric=False, nonlinear=False):
+    kw = synth.axisymmetric(40, nonlinear) if axisymmetric else synth.magnetostatic(40, nonlinear)
     kw = dict(kw)
     kw["labels"] = [dict(l) for l in kw["labels"]]
     mag = next(k for k, l in enumerate(kw["labels"]) if kw["blocks"][l["block"]].get("H_c", 0) > 0)
@@ -134,4 +134,43 @@ def test_label_without_elements_is_not_evaluated():
     kw["labels"] = kw["labels"] + [dict(kw["labels"][0], mag_dir_fctn="theta +")]
     P = kernels.Static2DProblem(**synth_to_oracle(kw)[2])
     P.solve()
+    P.close()
+
+
+LUA_PROGRAMS = [
+    # statements, a table traversed in the reference's order, a closure
+    "call(function() local t = {x, y, 5} local s = 0 for k, v in t do s = s * 2 + v end return s end, {})",
+    "call(function() local f = function(a) return a * %theta end return f(0.5) + 45 end, {})",
+    # state carried from element to element (one interpreter per problem): a
+    # linear problem runs the element loop once, so this is exact
+    "call(function() cnt = (cnt or 0) + 1 return mod(cnt, 4) * 90 end, {})",
+]
+
+
+@pytest.mark.parametrize("fctn", LUA_PROGRAMS)
+def test_lua_program_magnet_matches_oracle(fctn):
+    """MagDirFctn as Lua programs (xfk_lua.cpp, pinned to the reference's
+    liblua by tests/test_lua_interp.py) through problem creation: the
+    oracle's directions come from the reference's liblua running the same
+    element loop on one interpreter (oracle.element_magdir)."""
+    pr, mesh, kw = synth_to_oracle(magnet_problem(fctn))
+    P = kernels.Static2DProblem(**kw)
+    P.solve()
+    A = P.solution()
+    P.close()
+    Ao, _, _ = oracle.solve(pr, mesh)
+    Ac = converged(pr, mesh)
+    assert_parity(A, Ao, Ac, TOL)
+
+
+def test_nonlinear_problem_refuses_a_stateful_chunk():
+    """A nonlinear problem re-runs the element loop in every Newton pass: a
+    chunk whose value depends on earlier runs is refused at creation (named,
+    not a Lua error); a pure program is accepted."""
+    kw = synth_to_oracle(magnet_problem("call(function() cnt = (cnt or 0) + 1 return cnt end, {})",
+                                        nonlinear=True))[2]
+    with pytest.raises(kernels.XfkError, match="not supported by the native Lua interpreter"):
+        kernels.Static2DProblem(**kw)
+    kw = synth_to_oracle(magnet_problem(LUA_PROGRAMS[0], nonlinear=True))[2]
+    P = kernels.Static2DProblem(**kw)
     P.close()

@@ -132,6 +132,17 @@ UNSUPPORTED = ["random()*0", 'dofile("x")', 'openfile("x", "r")', 'settagmethod(
                'write("x")', "globals({})", "randomseed(3)", 'date()']
 
 
+def same_bits(ref, got):
+    """Bit-identical, except that a NaN matches any NaN: which operand's NaN
+    an SSE instruction propagates follows the compiler's operand order, so
+    the sign of a NaN (the text "nan" / "-nan") is not pinned."""
+    ref, got = np.asarray(ref), np.asarray(got)
+    if ref.shape != got.shape:
+        return False
+    nan = np.isnan(ref)
+    return bool((nan == np.isnan(got)).all() and np.array_equal(ref[~nan].view(np.int64), got[~nan].view(np.int64)))
+
+
 def compare(e, lu=0, n=400, seed=1):
     p, x, y = mesh_sample(n, seed)
     ref = evaluate(oracle.ref_magdir, e, p, x, y, lu, 7.0)
@@ -149,7 +160,7 @@ def test_lua_programs_bit_identical_to_reference(lu):
             if not (isinstance(got, str) and ref in got):
                 bad.append((e, ref, got))
             continue
-        if isinstance(got, str) or not np.array_equal(ref.view(np.int64), got.view(np.int64)):
+        if isinstance(got, str) or not same_bits(ref, got):
             bad.append((e, ref[:3], got if isinstance(got, str) else got[:3]))
     assert not bad, bad
 
@@ -181,7 +192,7 @@ def test_lua_state_persists_across_many_elements():
          'strrep("x", mod(cnt, 7)) local s = 0 for k, v in acc do s = s + strlen(v) * k end return s + cnt end, {})')
     ref, got = compare(e, 0, 5000, 3)
     assert not isinstance(ref, str) and not isinstance(got, str), (ref, got)
-    assert np.array_equal(ref.view(np.int64), got.view(np.int64))
+    assert same_bits(ref, got)
 
 
 @needs_lua
@@ -190,7 +201,7 @@ def test_lua_leaked_values_within_the_stack():
     element: fine up to 3000 (the reference's 4096-slot stack holds them),
     refused beyond (it overflows near 4096)."""
     ref, got = compare("theta, R", 0, 2500, 5)
-    assert np.array_equal(ref.view(np.int64), got.view(np.int64))
+    assert same_bits(ref, got)
     got = evaluate(kernels.magdir_eval, "theta, R", *mesh_sample(3500, 5), 0, 0.0)
     assert isinstance(got, str) and "not supported" in got
 
@@ -213,7 +224,7 @@ def test_lua_problem_loop_shares_one_interpreter(axi):
     md = [1.0, 2.0, 3.0, 4.0]
     ref = oracle.ref_magdir_labels(fctns, md, p, lbl, x, y, 2, axi)
     got = kernels.magdir_eval_labels(fctns, md, p, lbl, x, y, 2, axi)
-    assert np.array_equal(ref.view(np.int64), got.view(np.int64))
+    assert same_bits(ref, got)
     assert (got[lbl == 1] == 2.0).all()
 
 
@@ -233,4 +244,26 @@ def test_lua_nonlinear_problem_refuses_stateful_chunks():
     pure = 'call(function() local t = {x, y} local s = 0 for k, v in t do s = s + v end return s end, {})'
     ref = oracle.ref_magdir_labels([pure], [0.0], p, lbl, x, y, 0)
     got = kernels.magdir_eval_labels([pure], [0.0], p, lbl, x, y, 0, False, True)
-    assert np.array_equal(ref.view(np.int64), got.view(np.int64))
+    assert same_bits(ref, got)
+
+
+@needs_lua
+@pytest.mark.parametrize("seed", [11, 12])
+def test_lua_random_programs(seed):
+    """Seeded random programs (tests/lua_fuzz.py: locals, loops over ranges
+    and tables, closures with upvalues, sort with a comparator, string and
+    format functions, complex arithmetic) -- the same angles, or the same
+    error, as the reference's liblua."""
+    import lua_fuzz
+    p, x, y = mesh_sample(6, 3)
+    bad = []
+    for e in lua_fuzz.programs(300, seed):
+        ref = evaluate(oracle.ref_magdir, e, p, x, y, 0, 7.0)
+        got = evaluate(kernels.magdir_eval, e, p, x, y, 0, 7.0)
+        if isinstance(ref, str):
+            ok = isinstance(got, str) and ref in got
+        else:
+            ok = not isinstance(got, str) and same_bits(ref, got)
+        if not ok:
+            bad.append((e, ref, got))
+    assert not bad, bad[:3]
