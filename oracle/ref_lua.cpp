@@ -15,6 +15,7 @@
 // names in the same order as the reference's.  The product's native evaluator (xfemm_amd/csrc/xfk_magdir.cpp)
 // and the oracle's per-element directions are checked against this.
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -64,6 +65,7 @@ static int run_elements(F fctn_of, const double *mag_dirs_of_elem, int n, const 
                         const double *y, int length_units, int axisymmetric, double *t, char *msg, int msglen)
 {
     double units[] = {2.54, 0.1, 1., 100., 0.00254, 1.e-04};   // static2d.cpp:67
+    srand(1);   // the C library's generator as a fresh fsolver process has it (random())
     lua_State *lua = lua_open(4096);
     lua_baselibopen(lua);
     lua_strlibopen(lua);

@@ -520,6 +520,32 @@ struct Interp {
     long long epoch = 0;                   // the running element (tables record it)
     bool changed = false;                  // see Session::state_changed
     bool compat = false;                   // LuaInstance compatibility mode
+    // the C library's rand() (glibc's TYPE_3 additive feedback generator,
+    // state as after srand(1): what a fresh reference process starts from)
+    uint32_t rng[34];
+    int rng_i = 0;
+    void srand_(unsigned seed)
+    {
+        int32_t r[34];
+        r[0] = (int32_t)(seed == 0 ? 1 : seed);
+        for (int i = 1; i < 31; ++i) {   // 16807 r mod (2^31 - 1), Schrage's method
+            const int32_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+            int32_t w = 16807 * lo - 2836 * hi;
+            if (w < 0) w += 2147483647;
+            r[i] = w;
+        }
+        for (int i = 31; i < 34; ++i) r[i] = r[i - 31];
+        for (int i = 0; i < 34; ++i) rng[i] = (uint32_t)r[i];
+        rng_i = 0;   // rng holds r[k .. k+33] as a ring; k = 0
+        for (int i = 0; i < 310; ++i) rand_();   // outputs 0 .. 309 are discarded
+    }
+    int rand_()   // r[i] = r[i-31] + r[i-3] (i >= 34), output r[i] >> 1
+    {
+        const uint32_t v = rng[(rng_i + 3) % 34] + rng[(rng_i + 31) % 34];
+        rng[rng_i] = v;   // r[i] replaces r[i-34]
+        rng_i = (rng_i + 1) % 34;
+        return (int)(v >> 1);
+    }
     int depth = 0;                         // Lua calls active
     long long units = 0;                   // estimated stack slots of the active calls
     long long steps = 0;                   // statements + calls in this element
@@ -2353,8 +2379,33 @@ void u_newtag(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupporte
 void u_settag(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("settag"); }
 void u_settagmethod(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("settagmethod"); }
 void u_io(Interp &, std::vector<Value> &, std::vector<Value> &) { throw Unsupported("the io library"); }
-void u_random(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("random"); }
-void u_randomseed(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("randomseed"); }
+// math_random / math_randomseed (lmathlib.cpp:196-234) over the C library's rand()
+void m_random(Interp &I, std::vector<Value> &a, std::vector<Value> &r)
+{
+    I.changed = true;   // (the generator's state moves)
+    const double x = (double)(I.rand_() % 2147483647) / (double)2147483647;
+    switch (a.size()) {
+    case 0: r.assign(1, num(x)); return;
+    case 1: {
+        const int u = check_int(a, 1);
+        if (!(1 <= u)) argerror(1, "interval is empty");
+        r.assign(1, num((double)((int)(x * u) + 1)));
+        return;
+    }
+    case 2: {
+        const int l = check_int(a, 1), u = check_int(a, 2);
+        if (!(l <= u)) argerror(2, "interval is empty");
+        r.assign(1, num((double)((int)(x * (u - l + 1)) + l)));
+        return;
+    }
+    default: rt_error("wrong number of arguments");
+    }
+}
+void m_randomseed(Interp &I, std::vector<Value> &a, std::vector<Value> &)
+{
+    I.changed = true;
+    I.srand_((unsigned)check_int(a, 1));
+}
 void u_femmversion(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("femmVersion"); }
 
 // -- string library (lstrlib.cpp) ---------------------------------------------
@@ -2898,6 +2949,7 @@ void l_trace(Interp &, std::vector<Value> &, std::vector<Value> &) {}
 // ===========================================================================
 Interp::Interp(bool axisymmetric) : axi(axisymmetric)
 {
+    srand_(1);
     Value g = table(10);   // lstate.cpp:58
     G = tv(g);
     G->fixed = true;
@@ -2938,7 +2990,7 @@ Interp::Interp(bool axisymmetric) : axi(axisymmetric)
                 {"acos", m_acos}, {"atan", m_atan}, {"atan2", m_atan2}, {"ceil", m_ceil}, {"floor", m_floor},
                 {"mod", m_mod}, {"frexp", m_frexp}, {"ldexp", m_ldexp}, {"sqrt", m_sqrt}, {"min", m_min},
                 {"max", m_max}, {"log", m_log}, {"log10", m_log10}, {"exp", m_exp}, {"deg", m_deg},
-                {"rad", m_rad}, {"random", u_random}, {"randomseed", u_randomseed}, {"arg", m_arg},
+                {"rad", m_rad}, {"random", m_random}, {"randomseed", m_randomseed}, {"arg", m_arg},
                 {"re", m_re}, {"im", m_im}, {"conj", m_conj}, {"tanh", m_tanh}, {"cosh", m_cosh},
                 {"sinh", m_sinh}};
     for (const auto &b : math) reg(b.n, b.f);
