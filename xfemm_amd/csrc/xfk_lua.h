@@ -19,17 +19,17 @@
 //
 // What is refused (an Unsupported exception naming the construct -- never a
 // silent difference): the io library and dofile (files, the process), tag
-// methods (settagmethod
-// and friends), globals(t) (replacing the global table), gcinfo, femmVersion
-// (a build-generated constant), call's error-method argument, an error caught
-// by call / dostring while _ERRORMESSAGE or _ALERT is not the library's,
-// recursion deeper than 200 calls, more than 3000 values left on the
-// reference's 4096-slot stack (it overflows near there), and a chunk that
-// runs more than 10^9 steps for one element (the reference would not return
-// either).  random / randomseed run glibc's rand() restated, seeded as a
-// fresh reference process has it.  Addresses (tostring of a table / function, table keys that are
-// tables or functions, whose traversal order follows their address in the
-// reference) are this process's, not the reference's.
+// methods (settagmethod and friends), globals(t) (replacing the global
+// table), gcinfo, femmVersion (a build-generated constant), call's
+// error-method argument, an error caught by call / dostring while
+// _ERRORMESSAGE or _ALERT is not the library's, recursion deeper than 200
+// calls, more than 3000 values left on the reference's 4096-slot stack (it
+// overflows near there), and a chunk that runs more than 10^9 steps for one
+// element (the reference would not return either).  random / randomseed run
+// glibc's rand() restated, seeded as a fresh reference process has it.
+// Addresses (tostring of a table / function, table keys that are tables or
+// functions, whose traversal order follows their address in the reference)
+// are this process's, not the reference's.
 #pragma once
 
 #include <memory>
