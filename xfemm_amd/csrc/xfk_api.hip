@@ -1543,6 +1543,9 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
     // of this problem's last solve (an iteration launched after convergence
     // still costs its ~14 launches: 8 of them in a 1-iteration pass ~0.5 ms)
     else if (flag != 0 && P->pc_used == XFK_PRECOND_AMG && P->pcg_rate < 0) batch = 1;
+    // the speculative Newton residual goes with polls expected to be the last:
+    // not with the one-iteration probe of a warm start
+    bool expect_last = batch != 1 || flag == 0;
     long long it0 = -1;   // the first poll: iterations and er, for the observed rate
     double er0 = 0;
     // Every batch ends with an update, whose convergence test the poll reads:
@@ -1570,6 +1573,10 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
         }
         XFK_CHECK(hipGetLastError());
         XFK_CHECK(hipMemcpyAsync(P->pcg_host, P->pcg.p, sizeof(CgState), hipMemcpyDeviceToHost, s));
+        if (P->nws_at_poll && expect_last) {   // speculative: the Newton residual of the iterate as it stands
+            launch_newton_res(s, P->N, P->V.p, P->Vold.p, P->partials.p, P->counters.p + 3, P->nws.p);
+            XFK_CHECK(hipMemcpyAsync(P->nws_host, P->nws.p, sizeof(NewtonScalars), hipMemcpyDeviceToHost, s));
+        }
         const bool miss_read = !P->miss_checked && P->asm_miss.p;   // the assembly's slot check, first poll
         if (miss_read) XFK_CHECK(hipMemcpyAsync(P->hpin + 4, P->asm_miss.p, sizeof(int), hipMemcpyDeviceToHost, s));
         XFK_CHECK(hipStreamSynchronize(s));
@@ -1587,7 +1594,11 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
             set_error("singular flag tripped: zero diagonal entry in the assembled matrix");
             return XFK_ERR_SINGULAR;
         }
-        if (S.done) break;
+        if (S.done) {   // (iterations launched after the stop leave V as it is)
+            P->nws_ready = P->nws_at_poll && expect_last;
+            break;
+        }
+        expect_last = true;   // (every later batch is sized to reach the stop)
         if (it >= max_iters) {
             set_error("PCG did not converge within the iteration cap");
             return XFK_ERR_NOCONV;
@@ -1635,6 +1646,7 @@ static int pcg_solve_once(xfk_problem *P, int flag, long long max_iters)
 static int pcg_solve(xfk_problem *P, int flag, long long max_iters)
 {
     P->pcg_discarded = 0;
+    P->nws_ready = false;
     int rc = pcg_solve_once(P, flag, max_iters);
     if (rc == kRetryFresh) {   // a fresh hierarchy, the PCG restarted from the iterate
         P->pcg_discarded = P->pcg_host->iters;
@@ -2709,7 +2721,10 @@ static int static2d_run(xfk_problem *P, int flags, xfk_result *res)
         // has neither)
         if (!LinearFlag) XFK_CHECK(hipMemcpyAsync(P->Vold.p, P->V.p, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
         XFK_CHECK(hipEventRecord(e1, s));
+        static const bool nws_poll = !std::getenv("XFK_NWS_AT_POLL") || std::atoi(std::getenv("XFK_NWS_AT_POLL")) != 0;
+        P->nws_at_poll = nws_poll && !LinearFlag && !P->comm;
         rc = pcg_solve(P, Iter, cap);
+        P->nws_at_poll = false;
         if (rc != XFK_OK) return rc;
         XFK_CHECK(hipEventRecord(e2, s));
         R.cg_iters += P->pcg_host->iters;
@@ -2718,16 +2733,19 @@ static int static2d_run(xfk_problem *P, int flags, xfk_result *res)
         if (P->amg_fresh) P->amg_fresh_iters = P->pcg_host->iters - P->pcg_discarded;
 
         if (!LinearFlag) {
-            launch_newton_res(s, N, P->V.p, P->Vold.p, P->partials.p, P->counters.p + 3, P->nws.p);
-            const double *nws_src = reinterpret_cast<const double *>(P->nws.p);
-            if (P->comm) {
-                XFK_CHECK(P->nws_glob.alloc(4));
-                rc = P->comm->allreduce_sum(nws_src, P->nws_glob.p, 2, s);
-                if (rc != XFK_OK) return rc;
-                nws_src = P->nws_glob.p;
+            if (!P->nws_ready) {   // (else read with the PCG's final poll)
+                launch_newton_res(s, N, P->V.p, P->Vold.p, P->partials.p, P->counters.p + 3, P->nws.p);
+                const double *nws_src = reinterpret_cast<const double *>(P->nws.p);
+                if (P->comm) {
+                    XFK_CHECK(P->nws_glob.alloc(4));
+                    rc = P->comm->allreduce_sum(nws_src, P->nws_glob.p, 2, s);
+                    if (rc != XFK_OK) return rc;
+                    nws_src = P->nws_glob.p;
+                }
+                XFK_CHECK(hipMemcpyAsync(P->nws_host, nws_src, sizeof(NewtonScalars), hipMemcpyDeviceToHost, s));
+                XFK_CHECK(hipStreamSynchronize(s));
             }
-            XFK_CHECK(hipMemcpyAsync(P->nws_host, nws_src, sizeof(NewtonScalars), hipMemcpyDeviceToHost, s));
-            XFK_CHECK(hipStreamSynchronize(s));
+            P->nws_ready = false;
             const double x = P->nws_host->dx2, y = P->nws_host->v2;
             if (y == 0) LinearFlag = true;
             else {

@@ -471,6 +471,12 @@ struct xfk_problem {
     xfk::DBuf<xfk::NewtonScalars> nws;
     xfk::CgState *pcg_host = nullptr;  // pinned mirror
     xfk::NewtonScalars *nws_host = nullptr;
+    // single device, nonlinear static pass: the Newton residual is enqueued
+    // at every PCG poll and read with it; nws_ready once the final (done)
+    // poll's copy holds this pass's |dV|^2, |V|^2 -- the Newton loop then
+    // needs no host round trip of its own
+    bool nws_at_poll = false;
+    bool nws_ready = false;
 
     // preconditioner (xfk_set_option): XFK_PRECOND_AMG (default) or XFK_PRECOND_JACOBI
     int precond = XFK_PRECOND_AMG;
