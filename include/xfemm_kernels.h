@@ -545,6 +545,14 @@ int xfk_magdir_eval(const char *fctn, int n_elems, const int *p, const double *x
  * nonlinear, whose Newton loop re-runs the element loop every pass
  * (static2d.cpp:997-1008) -- refused (XFK_ERR_ARG, "not supported") when a
  * chunk changed state a later pass would see or left values on the stack. */
+/* A whole Lua chunk on a fresh interpreter of the kind MagDirFctn runs on (a
+ * femmcli-style script: the reference's LuaInstance, LuaInstance.cpp:185-208,
+ * through lua_dostring): what print / write send to the standard output is
+ * returned in out (NUL-terminated, at most cap - 1 bytes; *out_len the full
+ * length).  0; -2 when the chunk raised a Lua error (syntax or run-time), -1
+ * for a construct the interpreter refuses.  Host only. */
+int xfk_lua_run(const char *chunk, char *out, long long cap, long long *out_len);
+
 int xfk_magdir_eval_labels(int n_labels, const char *const *fctns, const double *mag_dirs, int n_elems,
                            const int *p, const int *lbl, const double *x, const double *y, int length_units,
                            int axisymmetric, int repeats, double *t);

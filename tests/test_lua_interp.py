@@ -132,7 +132,7 @@ BAD = ['call(function() error("x") end, {})', 'dostring("return")', 'call(functi
 UNSUPPORTED = ['dofile("x")', 'openfile("x", "r")', 'settagmethod(tag({}), "index", print)',
                "femmVersion()", 'call(function() return 1 end, {}, "", print)', "gcinfo()", "newtag()",
                'call(function() g = function(n) return g(n + 1) end return g(1) end, {})',
-               'write("x")', "globals({})", 'date()']
+               'writeto("x")', "globals({})", 'date()']
 
 
 def same_bits(ref, got):

@@ -550,6 +550,12 @@ struct Interp {
     long long units = 0;                   // estimated stack slots of the active calls
     long long steps = 0;                   // statements + calls in this element
     bool in_prelude = false;
+    std::string *capture = nullptr;        // stdout of print / write (nullptr: the process's stdout)
+    void out(int fd, const std::string &t)
+    {
+        if (fd == 1 && capture) capture->append(t);
+        else std::fwrite(t.data(), 1, t.size(), fd == 2 ? stderr : stdout);
+    }
     Value nm[7];                           // "x" "y" "r" "z" "theta" "R" "n" (fixed)
     std::string last_text;                 // the last element's function (one-entry cache)
     Chunk *last_chunk = nullptr;           // ... compiled (nullptr: no entry)
@@ -2170,10 +2176,10 @@ void b_print(Interp &I, std::vector<Value> &a, std::vector<Value> &)   // lbasel
         I.call(ts, args, res);
         std::string s;
         if (res.empty() || !I.tostring(res[0], &s)) rt_error("`tostring' must return a string to `print'");
-        if (i > 0) std::fputs("\t", stdout);
-        std::fputs(s.c_str(), stdout);
+        if (i > 0) I.out(1, "\t");
+        I.out(1, s.substr(0, std::strlen(s.c_str())));   // (fputs: up to a '\0')
     }
-    std::fputs("\n", stdout);
+    I.out(1, "\n");
 }
 void b_rawget(Interp &I, std::vector<Value> &a, std::vector<Value> &r)
 {
@@ -2379,6 +2385,37 @@ void u_newtag(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupporte
 void u_settag(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("settag"); }
 void u_settagmethod(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("settagmethod"); }
 void u_io(Interp &, std::vector<Value> &, std::vector<Value> &) { throw Unsupported("the io library"); }
+// io_write (liolib.cpp:504-532) on the predefined handles: the first argument
+// if it is one, else _OUTPUT; numbers as CComplex::ToString
+void io_write(Interp &I, std::vector<Value> &a, std::vector<Value> &r)
+{
+    auto handle = [](const Value &v, int *fd) {
+        if (v.t != TUD) return false;
+        const UdObj *u = static_cast<const UdObj *>(v.o);
+        if (!u->ptr || u->tag != 6) return false;
+        *fd = *static_cast<const int *>(u->ptr);
+        return true;
+    };
+    int fd = 1;
+    size_t k = 0;
+    if (!a.empty() && handle(a[0], &fd)) k = 1;
+    else if (!handle(I.getglobal("_OUTPUT"), &fd)) rt_error("global variable `_OUTPUT' is not a file handle");
+    if (fd == 0) throw Unsupported("write() to the standard input");
+    for (; k < a.size(); ++k) {
+        std::string t;
+        if (a[k].t == TNUM) {
+            t = number2str(a[k].n);
+            if (t.empty()) throw Unsupported("write() of a number with a NaN imaginary part");
+        } else {
+            t = check_str(I, a, (int)k + 1);
+        }
+        I.out(fd, t);
+    }
+    Value u;
+    u.t = TUD;
+    u.o = I.null_ud;
+    r.assign(1, u);
+}
 // math_random / math_randomseed (lmathlib.cpp:196-234) over the C library's rand()
 void m_random(Interp &I, std::vector<Value> &a, std::vector<Value> &r)
 {
@@ -2998,9 +3035,10 @@ Interp::Interp(bool axisymmetric) : axi(axisymmetric)
     setglobal("I", num(Cx{0., 1.}));
     reg("_ERRORMESSAGE", b_errormessage);   // liolib.cpp's errorfb replaces it
     for (const char *n : {"clock", "date", "debug", "execute", "exit", "getenv", "remove", "rename", "setlocale",
-                          "tmpname", "appendto", "closefile", "flush", "openfile", "read", "readfrom", "seek",
-                          "write", "writeto"})
+                          "tmpname", "appendto", "closefile", "flush", "openfile", "read", "readfrom", "seek"})
         reg(n, u_io);
+    reg("write", io_write);
+    reg("writeto", u_io);
     // the predefined file handles (liolib.cpp:129-137, 785-790): userdata of the io tag
     static const int kStdin = 0, kStdout = 1, kStderr = 2;
     setglobal("_INPUT", udata(&kStdin, 6));
@@ -3082,6 +3120,25 @@ void Interp::gc()
 // Session: one element of static2d.cpp:509-583 / staticaxi.cpp:350-406
 // ===========================================================================
 bool text_to_number(const char *s, Cx *out) { return str2d(s, out); }
+
+int Session::run_chunk(const std::string &text, std::string *output)
+{
+    I->capture = output;
+    I->steps = 0;
+    I->depth = 0;
+    I->units = 0;
+    ++I->epoch;
+    std::vector<Value> res;
+    int status;
+    try {
+        status = I->dostring(text, res);
+    } catch (...) {
+        I->capture = nullptr;
+        throw;
+    }
+    I->capture = nullptr;
+    return status;
+}
 
 Session::Session(bool axisymmetric) : I(new Interp(axisymmetric)) {}
 Session::~Session() = default;

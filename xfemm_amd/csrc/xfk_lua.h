@@ -18,7 +18,8 @@
 // they do in the reference.
 //
 // What is refused (an Unsupported exception naming the construct -- never a
-// silent difference): the io library and dofile (files, the process), tag
+// silent difference): the io library but write() on the standard handles,
+// and dofile (files, the process), tag
 // methods (settagmethod and friends), globals(t) (replacing the global
 // table), gcinfo, femmVersion (a build-generated constant), call's
 // error-method argument, an error caught by call / dostring while
@@ -82,6 +83,12 @@ public:
     bool state_changed() const;
     // values left on the reference's stack so far (all but the popped one)
     long long leaked() const;
+
+    // A whole chunk, as lua_dostring on this interpreter (a femmcli script):
+    // 0, or the Lua error status (1 run-time, 3 syntax).  `output` (if not
+    // null) receives what print / write send to the standard output.
+    // Throws Unsupported.
+    int run_chunk(const std::string &text, std::string *output);
 
 private:
     std::unique_ptr<Interp> I;

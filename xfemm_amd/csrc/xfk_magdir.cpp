@@ -8,7 +8,9 @@
 // lua_tostring left, and the label's MagDir when nothing is returned.
 #include "xfk_magdir.h"
 
+#include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 namespace xfk {
@@ -142,6 +144,34 @@ extern "C" int xfk_magdir_eval_labels(int n_labels, const char *const *fctns, co
     if (any && repeats && !md.repeatable(err)) {
         xfk::set_error(err);
         return -1;
+    }
+    return 0;
+}
+
+extern "C" int xfk_lua_run(const char *chunk, char *out, long long cap, long long *out_len)
+{
+    if (!chunk || cap < 0 || (cap > 0 && !out)) {
+        xfk::set_error("xfk_lua_run: bad arguments");
+        return -1;
+    }
+    xfk::lua::Session S(false);
+    std::string text;
+    int status;
+    try {
+        status = S.run_chunk(chunk, &text);
+    } catch (const xfk::lua::Unsupported &u) {
+        xfk::set_error(std::string(u.what()) + " not supported by the native Lua interpreter");
+        return -1;
+    }
+    if (out_len) *out_len = (long long)text.size();
+    if (cap > 0) {
+        const size_t n = std::min<size_t>((size_t)cap - 1, text.size());
+        std::memcpy(out, text.data(), n);
+        out[n] = '\0';
+    }
+    if (status != 0) {
+        xfk::set_error(status == 3 ? "Lua syntax error" : "Lua run-time error");
+        return -2;
     }
     return 0;
 }

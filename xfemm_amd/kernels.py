@@ -54,7 +54,7 @@ EXPORTED = (
     "xfk_comm_rank", "xfk_comm_size", "xfk_comm_record", "xfk_comm_log", "xfk_comm_create_replay",
     "xfk_comm_time", "xfk_comm_timing",
     "xfk_partition_plan", "xfk_partition_plan_coupled", "xfk_problem_create_dist", "xfk_dist_get_info",
-    "xfk_magdir_eval", "xfk_magdir_eval_labels", "xfk_sort_elements",
+    "xfk_magdir_eval", "xfk_magdir_eval_labels", "xfk_lua_run", "xfk_sort_elements",
 )
 
 
@@ -198,6 +198,7 @@ def load_library(path: str = KERNELS_SO):
     L.xfk_dist_get_info.argtypes = [vp, C.POINTER(DistInfo)]
     L.xfk_sort_elements.argtypes = [C.c_int, C.POINTER(C.c_uint), C.c_int, iptr]
     L.xfk_magdir_eval.argtypes = [C.c_char_p, C.c_int, iptr, dptr, dptr, C.c_int, C.c_double, dptr]
+    L.xfk_lua_run.argtypes = [C.c_char_p, C.c_char_p, C.c_longlong, C.POINTER(C.c_longlong)]
     L.xfk_magdir_eval_labels.argtypes = [C.c_int, C.POINTER(C.c_char_p), dptr, C.c_int, iptr, iptr, dptr, dptr,
                                          C.c_int, C.c_int, C.c_int, dptr]
     _lib = L
@@ -374,6 +375,21 @@ def magdir_eval_labels(fctns, mag_dirs, p, lbl, x, y, length_units: int = 0, axi
                                     int(length_units), int(bool(axisymmetric)), int(bool(repeats)),
                                     t.ctypes.data_as(dptr)))
     return t[:n]
+
+
+def lua_run(chunk: str) -> str:
+    """Run a whole Lua chunk on a fresh native interpreter (xfk_lua_run) and
+    return what it printed / wrote to the standard output.  Raises XfkError
+    (code -2) for a Lua error, (-1) for a refused construct."""
+    L = load_library()
+    n = C.c_longlong(0)
+    buf = C.create_string_buffer(1 << 16)
+    rc = L.xfk_lua_run(chunk.encode(), buf, len(buf), C.byref(n))
+    if n.value >= len(buf) and rc == 0:
+        buf = C.create_string_buffer(n.value + 1)
+        rc = L.xfk_lua_run(chunk.encode(), buf, len(buf), C.byref(n))
+    _check(rc)
+    return buf.raw[:n.value].decode("latin-1")
 
 
 def age_element_matrix(ci: float, co: float, K: float, Ki: float) -> np.ndarray:
