@@ -120,6 +120,52 @@ PROGRAMS = [
     'x, y, theta', 'strfind("abc", "b")', 'frexp(R)',
 ]
 
+
+TAGM = [
+    # tag methods (ltm.cpp, lvm.cpp): operator overloading on tagged tables,
+    # `a - k` reaching the "add" method with -k (the ADDI peephole), index /
+    # gettable / settable / function methods, getglobal / setglobal on nil,
+    # numbers' pow replaced, the tag-0 fallback, copytagmethods
+    'call(function() local tg = newtag() settagmethod(tg, "add", function(a, b, e) '
+    'return (type(a) == "table" and a.v or a) * 1000 + (type(b) == "table" and b.v or b) + strlen(e) end) '
+    'local t = settag({v = x}, tg) return (t + y) + (y + t) + (t - 1) + (t + 2) end, {})',
+    'call(function() local tg = newtag() settagmethod(tg, "sub", function(a, b, e) return a.v - b * 3 end) '
+    'settagmethod(tg, "mul", function(a, b) return 5 end) settagmethod(tg, "div", function(a, b) return b.v end) '
+    'local t = settag({v = theta}, tg) return (t - y) + t * 2 + x / t end, {})',
+    'call(function() local tg = newtag() settagmethod(tg, "unm", function(a, b, e) return a.v * 2 + (b and 1 or 0) end) '
+    'return -settag({v = x}, tg) end, {})',
+    'call(function() local tg = newtag() settagmethod(tg, "concat", function(a, b, e) '
+    'return (type(a) == "string" and strlen(a) or 0) + (type(b) == "table" and b.v or 0) + strlen(e) end) '
+    'local t = settag({v = y}, tg) return ("ab" .. t) + (t .. 5) end, {})',
+    'call(function() local tg = newtag() settagmethod(tg, "lt", function(a, b) return a.v < b.v end) '
+    'local p, q = settag({v = x}, tg), settag({v = y}, tg) '
+    'return (p < q and 1 or 0) + (p > q and 2 or 0) + (p <= q and 4 or 0) + (p >= q and 8 or 0) end, {})',
+    'call(function() local tg = newtag() settagmethod(tg, "index", function(t, k) return strlen(k) * 10 end) '
+    'local t = settag({a = x}, tg) return t.abc + t.q + t.a end, {})',
+    'call(function() settagmethod(tag({}), "index", function(t, k) return 7 end) local t = {} return t.zz + x end, {})',
+    'call(function() local tg = newtag() settagmethod(tg, "gettable", function(t, k) return (rawget(t, k) or 99) + 1 end) '
+    'settagmethod(tg, "settable", function(t, k, v) rawset(t, k, v * 2) end) '
+    'local t = settag({}, tg) t.a = x t[3] = y return t.a + t[3] + t.nothing end, {})',
+    'call(function() local tg = newtag() settagmethod(tg, "function", function(self, a, b) return a + b * self.v end) '
+    'local t = settag({v = 3}, tg) return t(x, y) end, {})',
+    'call(function() settagmethod(tag(nil), "getglobal", function(name, v) return strlen(name) end) '
+    'return undefined_name_xyz + 1 end, {})',
+    'call(function() settagmethod(tag(nil), "setglobal", function(name, old, new) rawset(globals(), name, new * 2) end) '
+    'newglob_q = x return newglob_q end, {})',
+    'call(function() settagmethod(tag(1), "pow", function(a, b, e) return a * 100 + b end) return x ^ 2 end, {})',
+    'call(function() settagmethod(0, "add", function(a, b) return 42 end) return {} + {} end, {})',
+    'call(function() local t1 = newtag() settagmethod(t1, "add", function(a, b) return b * 7 end) '
+    'local t2 = copytagmethods(newtag(), t1) return settag({}, t2) + x end, {})',
+    'call(function() return (gettagmethod(tag(1), "pow") == gettagmethod(tag(2), "pow") and 1 or 0) + '
+    '(gettagmethod(newtag(), "add") == nil and 2 or 0) end, {})',
+    'tag(x) + tag({}) * 10 + tag(print) * 100 + tag(nil) * 1000 + tag("s") * 10000 + tag(_STDOUT) * 100000',
+    'call(function() tnew = tnew or newtag() return tnew end, {})',
+    'call(function() local tg = newtag() local old = settagmethod(tg, "add", function() return 1 end) '
+    'local old2 = settagmethod(tg, "add", nil) return (old == nil and 1 or 0) + (type(old2) == "function" and 2 or 0) '
+    '+ (gettagmethod(tg, "add") == nil and 4 or 0) end, {})',
+]
+PROGRAMS = PROGRAMS + TAGM
+
 # Lua errors (the reference's message) and non-numeric results
 BAD = ['call(function() error("x") end, {})', 'dostring("return")', 'call(function() return {} end, {})',
        "getn(5)", 'strsub("a")', 'format("%y", 1)', 'strrep("a")', 'sort({1, "a"})', "{1, a = 2}",
@@ -127,10 +173,14 @@ BAD = ['call(function() error("x") end, {})', 'dostring("return")', 'call(functi
        "function() end", 'call(function() for i = 1, "a" do end end, {})',
        'call(function() for k, v in 5 do end end, {})', "next({}, 1)", "tinsert(nil, 1)", 'strfind("a", "(")',
        'strfind("a", "%")', 'gsub("a", "a", {})', "foreach({}, 5)", "call(5, {})", "assert(nil)",
-       'format("%d", "z")', "x = 1", "return 1", "1 1"]
+       'format("%d", "z")', "x = 1", "return 1", "1 1",
+       'settagmethod(tag(1), "add", print)', "settag({}, 3)", 'settagmethod(tag({}), "gc", print)',
+       'settagmethod(newtag(), "le", print)', 'gettagmethod(99, "add")', 'settagmethod(newtag(), "foo", print)',
+       'settagmethod(newtag(), "add")', 'settagmethod(newtag(), "add", 5)', "settag(5, newtag())",
+       "call(function() local t = {} return t + 1 end, {})"]
 
-UNSUPPORTED = ['dofile("x")', 'openfile("x", "r")', 'settagmethod(tag({}), "index", print)',
-               "femmVersion()", 'call(function() return 1 end, {}, "", print)', "gcinfo()", "newtag()",
+UNSUPPORTED = ['dofile("x")', 'openfile("x", "r")',
+               "femmVersion()", 'call(function() return 1 end, {}, "", print)', "gcinfo()",
                'call(function() g = function(n) return g(n + 1) end return g(1) end, {})',
                'writeto("x")', "globals({})", 'date()']
 

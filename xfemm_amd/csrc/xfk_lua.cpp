@@ -261,6 +261,7 @@ struct Node {
 struct TableObj : Obj {
     std::vector<Node> node;
     int firstfree = 0;
+    int htag = TTAB;        // settag()
     long long epoch = 0;   // the element whose run created it
 };
 
@@ -317,6 +318,22 @@ struct LuaError {
     std::string msg;
 };
 [[noreturn]] void rt_error(const std::string &m) { throw LuaError{1, m}; }
+
+// tag-method events (ltm.h ORDER TM; ltm.cpp:14-20)
+enum TMS { TM_GETTABLE, TM_SETTABLE, TM_INDEX, TM_GETGLOBAL, TM_SETGLOBAL, TM_ADD, TM_SUB, TM_MUL, TM_DIV, TM_POW,
+           TM_UNM, TM_LT, TM_CONCAT, TM_GC, TM_FUNCTION, TM_N };
+const char *const kEventName[] = {"gettable", "settable", "index", "getglobal", "setglobal", "add", "sub", "mul",
+                                  "div", "pow", "unm", "lt", "concat", "gc", "function", "le", "gt", "ge"};
+const int kNumTags = 6;   // NUM_TAGS
+// luaT_validevents (ltm.cpp:52-60), ORDER LUA_T x ORDER TM
+const char kValidEvents[kNumTags][TM_N] = {
+    {1, 1, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 0, 1},   // userdata
+    {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1},   // nil
+    {1, 1, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1},   // number
+    {1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1},   // string
+    {0, 0, 1, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 0, 1},   // table
+    {1, 1, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0}};  // function
+inline bool valid_event(int t, int e) { return t >= kNumTags || kValidEvents[t][e]; }
 
 // ===========================================================================
 // tables: the chained scatter table of ltable.cpp
@@ -550,6 +567,41 @@ struct Interp {
     long long units = 0;                   // estimated stack slots of the active calls
     long long steps = 0;                   // statements + calls in this element
     bool in_prelude = false;
+    // tag methods (ltm.cpp): per tag, per event; tags 0..5 the basic types,
+    // 6 and 7 the io library's (liolib.cpp:775-776), then newtag()'s
+    std::vector<std::vector<Value>> tms;
+    int last_tag = kNumTags - 1;
+    int newtag()
+    {
+        tms.emplace_back(TM_N, Value());
+        return ++last_tag;
+    }
+    static int tag_of(const Value &v)   // luaT_tag (ltm.cpp:124-136)
+    {
+        if (v.t == TUD) return static_cast<const UdObj *>(v.o)->tag;
+        if (v.t == TTAB) return static_cast<const TableObj *>(v.o)->htag;
+        return v.t;
+    }
+    const Value &gettm(int tag, int e) const { return tms[(size_t)tag][(size_t)e]; }
+    // a tag method's call (luaD_callTM): its first result (or none)
+    Value call_tm(const Value &tm, std::vector<Value> args)
+    {
+        std::vector<Value> res;
+        call(tm, args, res);
+        return res.empty() ? Value() : res[0];
+    }
+    // call_binTM (lvm.cpp:262-280): the first operand's method, the second's,
+    // then tag 0's (the "global" method); false if none
+    bool bin_tm(const Value &a, const Value &b, int e, Value *out)
+    {
+        Value tm = gettm(tag_of(a), e);
+        if (tm.t == TNIL) tm = gettm(tag_of(b), e);
+        if (tm.t == TNIL) tm = gettm(0, e);
+        if (tm.t == TNIL) return false;
+        *out = call_tm(tm, {a, b, str(kEventName[e])});
+        return true;
+    }
+    bool lessthan(const Value &l, const Value &r);
     std::string *capture = nullptr;        // stdout of print / write (nullptr: the process's stdout)
     void out(int fd, const std::string &t)
     {
@@ -638,22 +690,55 @@ struct Interp {
     Value rawgeti(TableObj *t, int i) { return rawget(t, num((double)i)); }
     void rawseti(TableObj *t, int i, const Value &v) { rawset(t, num((double)i), v); }
 
-    // luaV_gettable / settable without tag methods (lvm.cpp:125-197): a
-    // table, else "attempt to index"
+    // luaV_gettable (lvm.cpp:125-163): a table with the default tag or no
+    // "gettable" method reads primitively, then its "index" method on nil;
+    // anything else goes to its "gettable" method
     Value gettable(const Value &t, const Value &k)
     {
-        if (t.t != TTAB) rt_error(std::string("attempt to index a ") + kTypeName[t.t] + " value");
-        return rawget(tv(t), k);
+        Value tm;
+        if (t.t == TTAB && (tv(t)->htag == TTAB || gettm(tv(t)->htag, TM_GETTABLE).t == TNIL)) {
+            const Value v = rawget(tv(t), k);
+            if (v.t != TNIL || (tm = gettm(tv(t)->htag, TM_INDEX)).t == TNIL) return v;
+        } else {
+            tm = gettm(tag_of(t), TM_GETTABLE);
+        }
+        if (tm.t == TNIL) rt_error(std::string("attempt to index a ") + kTypeName[t.t] + " value");
+        return call_tm(tm, {t, k});
     }
+    // luaV_settable (lvm.cpp:169-197)
     void settable(const Value &t, const Value &k, const Value &v)
     {
-        if (t.t != TTAB) rt_error(std::string("attempt to index a ") + kTypeName[t.t] + " value");
-        rawset(tv(t), k, v);
+        if (t.t == TTAB && (tv(t)->htag == TTAB || gettm(tv(t)->htag, TM_SETTABLE).t == TNIL)) {
+            rawset(tv(t), k, v);
+            return;
+        }
+        const Value tm = gettm(tag_of(t), TM_SETTABLE);
+        if (tm.t == TNIL) rt_error(std::string("attempt to index a ") + kTypeName[t.t] + " value");
+        std::vector<Value> res;
+        call(tm, {t, k, v}, res);
     }
-    Value getglobal(const Value &name) { return rawget(G, name); }
-    Value getglobal(const char *name) { return rawget(G, str(name)); }
-    void setglobal(const Value &name, const Value &v) { rawset(G, name, v); }
-    void setglobal(const char *name, const Value &v) { rawset(G, str(name), v); }
+    // luaV_getglobal / luaV_setglobal (lvm.cpp:200-257): the method of the
+    // value's (the old value's) tag
+    Value getglobal(const Value &name)
+    {
+        const Value v = rawget(G, name);
+        const Value tm = gettm(tag_of(v), TM_GETGLOBAL);
+        if (tm.t == TNIL) return v;
+        return call_tm(tm, {name, v});
+    }
+    Value getglobal(const char *name) { return getglobal(str(name)); }
+    void setglobal(const Value &name, const Value &v)
+    {
+        const Value old = rawget(G, name);
+        const Value tm = gettm(tag_of(old), TM_SETGLOBAL);
+        if (tm.t == TNIL) {
+            rawset(G, name, v);
+            return;
+        }
+        std::vector<Value> res;
+        call(tm, {name, old, v}, res);
+    }
+    void setglobal(const char *name, const Value &v) { setglobal(str(name), v); }
 
     // -- conversions (lvm.cpp:42-68, lapi.cpp) -----------------------------
     static bool tonumber(Value &a)   // in place, as luaV_tonumber
@@ -675,6 +760,7 @@ struct Interp {
 
     // -- calls ---------------------------------------------------------------
     void call(const Value &f, std::vector<Value> &args, std::vector<Value> &res);
+    void call(const Value &f, std::vector<Value> &&args, std::vector<Value> &res) { call(f, args, res); }
     void run_proto(const FuncObj *cl, std::vector<Value> &args, std::vector<Value> &res);
     int protected_call(const Value &f, std::vector<Value> &args, std::vector<Value> &res);
     int dostring(const std::string &text, std::vector<Value> &res);
@@ -1535,7 +1621,9 @@ struct Parser {
 // ===========================================================================
 enum Flow { F_NORMAL, F_BREAK, F_RETURN };
 
-bool lua_lessthan(const Value &l, const Value &r)   // luaV_lessthan (lvm.cpp:306-323), no tag methods
+}  // namespace
+
+bool Interp::lessthan(const Value &l, const Value &r)   // luaV_lessthan (lvm.cpp:306-323)
 {
     if (l.t == TNUM && r.t == TNUM) return l.n.re < r.n.re;
     if (l.t == TSTR && r.t == TSTR) {   // luaV_strcomp: strcoll over the '\0'-separated pieces
@@ -1555,8 +1643,12 @@ bool lua_lessthan(const Value &l, const Value &r)   // luaV_lessthan (lvm.cpp:30
             lb -= len;
         }
     }
-    rt_error("attempt to compare");
+    Value v;
+    if (!bin_tm(l, r, TM_LT, &v)) rt_error("attempt to compare");
+    return v.t != TNIL;
 }
+
+namespace {
 
 const long long kMaxSteps = 1000000000LL;
 const int kMaxDepth = 200;
@@ -1583,18 +1675,23 @@ struct Exec {
     // -- arithmetic (lvm.cpp:575-660) ------------------------------------------
     Value arith(int op, Value a, Value b, const Expr *rhs)
     {
-        if (op == B_POW) {   // the math library's "pow" tag method on numbers (lmathlib.cpp:114-118, 319-320)
-            if (a.t != TNUM && b.t != TNUM) rt_error("undefined operation");
-            if (!Interp::tonumber(a) || !Interp::tonumber(b)) rt_error("bad argument to `pow'");
-            const Cx x = a.n, y = b.n;
-            if (y.im == 0 && y.re == std::floor(y.re)) {
-                if (std::fabs(y.re) > 1048576.0)
-                    throw Unsupported("an integral exponent beyond 2^20 (the reference multiplies that many times)");
-                return num(cpow_int(x, (long long)(int)y.re));
-            }
-            return num(cexp(mul(y, clog(x))));
+        Value v;
+        if (op == B_POW) {   // OP_POW: always the "pow" method (the math library's on numbers, lmathlib.cpp:319-320)
+            if (!I.bin_tm(a, b, TM_POW, &v)) rt_error("undefined operation");
+            return v;
         }
-        if (!Interp::tonumber(a) || !Interp::tonumber(b)) rt_error("attempt to perform arithmetic");
+        // `a + k` / `a - k` with an integer literal k are ADDI +-k (lcode.cpp:609-634):
+        // on a non-number the "add" method sees the literal, negated for `-`
+        const bool addi = (op == B_ADD || op == B_SUB) && rhs->k == X_INT;
+        if (!Interp::tonumber(a) || !Interp::tonumber(b)) {   // (in place, the left operand first)
+            static const int ev[] = {TM_ADD, TM_SUB, TM_MUL, TM_DIV};
+            if (addi) {
+                b = num((double)(op == B_SUB ? -rhs->op : rhs->op));
+                op = B_ADD;
+            }
+            if (!I.bin_tm(a, b, ev[op], &v)) rt_error("attempt to perform arithmetic");
+            return v;
+        }
         const Cx x = a.n, y = b.n;
         switch (op) {
         case B_ADD: return num(add(x, y));
@@ -1608,12 +1705,18 @@ struct Exec {
         }
     }
 
-    static bool lessthan(const Value &l, const Value &r) { return lua_lessthan(l, r); }
+    bool lessthan(const Value &l, const Value &r) { return I.lessthan(l, r); }
 
-    Value concat(const Value &a, const Value &b)   // luaV_strconc (lvm.cpp:326-362)
+    Value concat(Value a, const Value &b)   // luaV_strconc (lvm.cpp:326-362)
     {
         std::string sa, sb;
-        if (!I.tostring(a, &sa) || !I.tostring(b, &sb)) rt_error("attempt to concat");
+        const bool oka = I.tostring(a, &sa);
+        if (oka && a.t == TNUM) a = I.str(sa);   // (converted in place before the other is tried)
+        if (!oka || !I.tostring(b, &sb)) {
+            Value v;
+            if (!I.bin_tm(a, b, TM_CONCAT, &v)) rt_error("attempt to concat");
+            return v;
+        }
         return I.str(sa + sb);
     }
 
@@ -1643,7 +1746,11 @@ struct Exec {
         case X_TABLE: return constructor(e);
         case X_UNM: {   // OP_MINUS (lvm.cpp:651-660); constants were folded by the parser
             Value a = eval(e->a);
-            if (!Interp::tonumber(a)) rt_error("attempt to perform arithmetic");
+            if (!Interp::tonumber(a)) {
+                Value v;
+                if (!I.bin_tm(a, Value(), TM_UNM, &v)) rt_error("attempt to perform arithmetic");
+                return v;
+            }
             return num(neg(a.n));
         }
         case X_NOT: {
@@ -1929,7 +2036,13 @@ void Interp::call(const Value &f, std::vector<Value> &args, std::vector<Value> &
 {
     if (++steps > kMaxSteps)
         throw Unsupported("more than 10^9 steps for one element (the reference's Lua would not return either)");
-    if (f.t != TFUN) rt_error(std::string("attempt to call a ") + kTypeName[f.t] + " value");
+    if (f.t != TFUN) {   // luaD_call (ldo.cpp:178-187): the "function" method, with f first
+        const Value tm = gettm(tag_of(f), TM_FUNCTION);
+        if (tm.t == TNIL) rt_error(std::string("attempt to call a ") + kTypeName[f.t] + " value");
+        args.insert(args.begin(), f);
+        call(tm, args, res);
+        return;
+    }
     const FuncObj *c = fv(f);
     res.clear();
     if (c->c) {
@@ -2204,8 +2317,7 @@ void b_setglobal(Interp &I, std::vector<Value> &a, std::vector<Value> &)   // th
 void b_tag(Interp &, std::vector<Value> &a, std::vector<Value> &r)
 {
     check_any(a, 1);
-    if (a[0].t == TUD) r.assign(1, num((double)static_cast<UdObj *>(a[0].o)->tag));
-    else r.assign(1, num((double)a[0].t));
+    r.assign(1, num((double)Interp::tag_of(a[0])));
 }
 void b_tonumber(Interp &I, std::vector<Value> &a, std::vector<Value> &r)   // lbaselib.cpp:90-122
 {
@@ -2301,7 +2413,7 @@ struct Sorter {
             I.call(f, args, res);
             return !res.empty() && res[0].t != TNIL;
         }
-        return lua_lessthan(a, b);
+        return I.lessthan(a, b);
     }
     Value get(int i) { return I.rawgeti(t, i); }
     void set(int i, const Value &v) { I.rawseti(t, i, v); }
@@ -2377,13 +2489,75 @@ void b_sort(Interp &I, std::vector<Value> &a, std::vector<Value> &)
 }
 void b_deprecated(Interp &, std::vector<Value> &, std::vector<Value> &) { rt_error("function is deprecated"); }
 
-void u_copytagmethods(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("copytagmethods"); }
 void u_dofile(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("dofile"); }
 void u_gcinfo(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("gcinfo"); }
-void u_gettagmethod(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("gettagmethod"); }
-void u_newtag(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("newtag"); }
-void u_settag(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("settag"); }
-void u_settagmethod(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("settagmethod"); }
+
+// tag methods from Lua (lbaselib.cpp:140-230, lapi.cpp:484-499, ltm.cpp:22-184)
+int check_event(const std::string &name, int t)   // luaI_checkevent
+{
+    int e = -1;
+    for (int i = 0; i < 18; ++i)
+        if (name == kEventName[i]) e = i;
+    if (e >= TM_N) rt_error("event `" + name + "' is deprecated");
+    if (e == TM_GC && t == TTAB) rt_error("event `gc' for tables is deprecated");
+    if (e < 0) rt_error("`" + name + "' is not a valid event name");
+    return e;
+}
+void check_tag(Interp &I, int t)
+{
+    if (!(0 <= t && t <= I.last_tag)) rt_error("not a valid tag");
+}
+Value get_tag_method(Interp &I, int t, const std::string &event)   // lua_gettagmethod
+{
+    const int e = check_event(event, t);
+    check_tag(I, t);
+    return valid_event(t, e) ? I.gettm(t, e) : Value();
+}
+void b_newtag(Interp &I, std::vector<Value> &, std::vector<Value> &r)
+{
+    I.changed = true;
+    r.assign(1, num((double)I.newtag()));
+}
+void b_settag(Interp &I, std::vector<Value> &a, std::vector<Value> &r)
+{
+    TableObj *t = check_table(a, 1);
+    const int tg = check_int(a, 2);
+    if (!(kNumTags <= tg && tg <= I.last_tag)) rt_error("tag was not created by `newtag'");   // luaT_realtag
+    if (t->htag != tg) I.changed = true;
+    t->htag = tg;
+    r.assign(1, a[0]);
+}
+void b_settagmethod(Interp &I, std::vector<Value> &a, std::vector<Value> &r)
+{
+    const int t = check_int(a, 1);
+    const std::string event = check_str(I, a, 2);
+    if (isnull(a, 3) || !(a[2].t == TFUN || a[2].t == TNIL)) argerror(3, "function or nil expected");
+    if (event == "gc") rt_error("deprecated use: cannot set the `gc' tag method from Lua");
+    const Value old = get_tag_method(I, t, event);
+    const int e = check_event(event, t);   // lua_settagmethod
+    check_tag(I, t);
+    if (!valid_event(t, e)) rt_error("cannot change tag method for this type");
+    I.tms[(size_t)t][(size_t)e] = arg(a, 3);
+    I.changed = true;
+    r.assign(1, old);
+}
+void b_gettagmethod(Interp &I, std::vector<Value> &a, std::vector<Value> &r)
+{
+    const int t = check_int(a, 1);
+    const std::string event = check_str(I, a, 2);
+    if (event == "gc") rt_error("deprecated use: cannot get the `gc' tag method from Lua");
+    r.assign(1, get_tag_method(I, t, event));
+}
+void b_copytagmethods(Interp &I, std::vector<Value> &a, std::vector<Value> &r)
+{
+    const int to = check_int(a, 1), from = check_int(a, 2);
+    check_tag(I, to);
+    check_tag(I, from);
+    for (int e = 0; e < TM_N; ++e)
+        if (valid_event(to, e)) I.tms[(size_t)to][(size_t)e] = I.gettm(from, e);
+    I.changed = true;
+    r.assign(1, num((double)to));
+}
 void u_io(Interp &, std::vector<Value> &, std::vector<Value> &) { throw Unsupported("the io library"); }
 // io_write (liolib.cpp:504-532) on the predefined handles: the first argument
 // if it is one, else _OUTPUT; numbers as CComplex::ToString
@@ -2915,6 +3089,17 @@ MATH1(m_tanh, ctanh(x))
 MATH1(m_cosh, ccosh(x))
 MATH1(m_sinh, csinh(x))
 #undef MATH1
+void m_pow(Interp &, std::vector<Value> &a, std::vector<Value> &r)   // math_pow (lmathlib.cpp:114-118)
+{
+    const Cx x = check_number(a, 1), y = check_number(a, 2);
+    if (y.im == 0 && y.re == std::floor(y.re)) {   // pow(CComplex, CComplex) (femmcomplex.cpp:807-812)
+        if (std::fabs(y.re) > 1048576.0)
+            throw Unsupported("an integral exponent beyond 2^20 (the reference multiplies that many times)");
+        r.assign(1, num(cpow_int(x, (long long)(int)y.re)));
+        return;
+    }
+    r.assign(1, num(cexp(mul(y, clog(x)))));
+}
 void m_atan2(Interp &, std::vector<Value> &a, std::vector<Value> &r)
 {
     const Cx y = check_number(a, 1), x = check_number(a, 2);
@@ -2987,6 +3172,7 @@ void l_trace(Interp &, std::vector<Value> &, std::vector<Value> &) {}
 Interp::Interp(bool axisymmetric) : axi(axisymmetric)
 {
     srand_(1);
+    tms.assign(kNumTags, std::vector<Value>(TM_N));   // luaT_init
     Value g = table(10);   // lstate.cpp:58
     G = tv(g);
     G->fixed = true;
@@ -3002,12 +3188,12 @@ Interp::Interp(bool axisymmetric) : axi(axisymmetric)
         const char *n;
         Builtin f;
     } base[] = {{"_ALERT", b_alert}, {"_ERRORMESSAGE", b_errormessage}, {"call", b_call},
-                {"collectgarbage", b_collectgarbage}, {"copytagmethods", u_copytagmethods}, {"dofile", u_dofile},
+                {"collectgarbage", b_collectgarbage}, {"copytagmethods", b_copytagmethods}, {"dofile", u_dofile},
                 {"dostring", b_dostring}, {"error", b_error}, {"foreach", b_foreach}, {"foreachi", b_foreachi},
-                {"gcinfo", u_gcinfo}, {"getglobal", b_getglobal}, {"gettagmethod", u_gettagmethod},
-                {"globals", b_globals}, {"newtag", u_newtag}, {"next", b_next}, {"print", b_print},
+                {"gcinfo", u_gcinfo}, {"getglobal", b_getglobal}, {"gettagmethod", b_gettagmethod},
+                {"globals", b_globals}, {"newtag", b_newtag}, {"next", b_next}, {"print", b_print},
                 {"rawget", b_rawget}, {"rawset", b_rawset}, {"rawgettable", b_rawget}, {"rawsettable", b_rawset},
-                {"setglobal", b_setglobal}, {"settag", u_settag}, {"settagmethod", u_settagmethod}, {"tag", b_tag},
+                {"setglobal", b_setglobal}, {"settag", b_settag}, {"settagmethod", b_settagmethod}, {"tag", b_tag},
                 {"tonumber", b_tonumber}, {"tostring", b_tostring}, {"type", b_type}, {"assert", b_assert},
                 {"getn", b_getn}, {"sort", b_sort}, {"tinsert", b_tinsert}, {"tremove", b_tremove}};
     for (const auto &b : base) reg(b.n, b.f);
@@ -3031,6 +3217,7 @@ Interp::Interp(bool axisymmetric) : axi(axisymmetric)
                 {"re", m_re}, {"im", m_im}, {"conj", m_conj}, {"tanh", m_tanh}, {"cosh", m_cosh},
                 {"sinh", m_sinh}};
     for (const auto &b : math) reg(b.n, b.f);
+    tms[TNUM][TM_POW] = builtin(m_pow, "pow");   // lmathlib.cpp:319-320
     setglobal("PI", num(kPi));
     setglobal("I", num(Cx{0., 1.}));
     reg("_ERRORMESSAGE", b_errormessage);   // liolib.cpp's errorfb replaces it
@@ -3039,6 +3226,8 @@ Interp::Interp(bool axisymmetric) : axi(axisymmetric)
         reg(n, u_io);
     reg("write", io_write);
     reg("writeto", u_io);
+    newtag();   // the io library's iotag (6) and closedtag (7), liolib.cpp:775-776
+    newtag();
     // the predefined file handles (liolib.cpp:129-137, 785-790): userdata of the io tag
     static const int kStdin = 0, kStdout = 1, kStderr = 2;
     setglobal("_INPUT", udata(&kStdin, 6));
@@ -3087,6 +3276,8 @@ void Interp::gc()
     for (const Value &v : leaked) push(v);
     push(errormessage_fn);
     push(alert_fn);
+    for (const auto &per_tag : tms)
+        for (const Value &v : per_tag) push(v);
     while (!work.empty()) {
         Obj *o = work.back();
         work.pop_back();

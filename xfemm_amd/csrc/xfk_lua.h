@@ -9,9 +9,10 @@
 // every element in assembly order, leaving the results on the stack and
 // popping one (LuaInstance::LuaStackMode::Unsafe).  This interpreter restates
 // that: Lua 4.0's language (lparser.cpp, lvm.cpp, ldo.cpp) with the xfemm
-// complex number (femmcomplex.cpp), Lua 4.0's tables as the chained scatter
-// table of ltable.cpp (so traversal order -- next, foreach, `for k, v in t` --
-// is the reference's for number and string keys), the base library
+// complex number (femmcomplex.cpp) and tag methods (ltm.cpp), Lua 4.0's
+// tables as the chained scatter table of ltable.cpp (so traversal order --
+// next, foreach, `for k, v in t` -- is the reference's for number and string
+// keys), the base library
 // (lbaselib.cpp), the string library with its pattern matcher (lstrlib.cpp),
 // the math library (lmathlib.cpp) and LuaInstance's Complex / pi /
 // compatibility-mode functions.  Globals persist from element to element as
@@ -19,8 +20,7 @@
 //
 // What is refused (an Unsupported exception naming the construct -- never a
 // silent difference): the io library but write() on the standard handles,
-// and dofile (files, the process), tag
-// methods (settagmethod and friends), globals(t) (replacing the global
+// and dofile (files, the process), globals(t) (replacing the global
 // table), gcinfo, femmVersion (a build-generated constant), call's
 // error-method argument, an error caught by call / dostring while
 // _ERRORMESSAGE or _ALERT is not the library's, recursion deeper than 200
