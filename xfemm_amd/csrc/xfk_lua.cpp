@@ -617,6 +617,8 @@ struct Interp {
 
     template <class T> T *alloc()
     {
+        // (collected only between elements: one element's garbage is bounded)
+        if (nobjs > 50000000LL) throw Unsupported("more than 5 * 10^7 Lua objects alive within one element");
         T *o = new T();
         o->gcnext = gclist;
         gclist = o;
@@ -1325,8 +1327,21 @@ struct Parser {
     static int left(BinOp o) { static const int p[] = {5, 5, 6, 6, 9, 4, 2, 2, 2, 2, 2, 2, 1, 1}; return p[o]; }
     static int right(BinOp o) { static const int p[] = {5, 5, 6, 6, 8, 3, 2, 2, 2, 2, 2, 2, 1, 1}; return p[o]; }
 
+    // nesting of expressions and blocks (the reference's recursive-descent
+    // parser has no limit but the C stack's; this one stops loudly)
+    int nest = 0;
+    struct Nest {
+        Parser &P;
+        explicit Nest(Parser &p) : P(p)
+        {
+            if (++P.nest > 1000) throw Unsupported("expressions or blocks nested more than 1000 deep");
+        }
+        ~Nest() { --P.nest; }
+    };
+
     Expr *subexpr(int limit, BinOp *stop)   // lparser.cpp:828-853
     {
+        Nest guard(*this);
         Expr *v;
         if (L.tok == '-' || L.tok == T_NOT) {
             const bool minus = L.tok == '-';
@@ -1380,6 +1395,7 @@ struct Parser {
 
     Block *chunk()   // lparser.cpp:1302-1313
     {
+        Nest guard(*this);
         Block *b = blk();
         bool last = false;
         while (!last && !block_follow(L.tok)) {
@@ -2084,6 +2100,7 @@ Chunk *Interp::compile(const std::string &text)
 {
     auto it = chunks.find(text);
     if (it != chunks.end()) return it->second.get();
+    if (chunks.size() >= 100000) throw Unsupported("more than 10^5 distinct chunks compiled (dostring)");
     std::unique_ptr<Chunk> c(new Chunk());
     Parser P(text, *this, *c);
     P.main_chunk();   // throws LuaError{3}
@@ -2765,6 +2782,7 @@ int singlematch(int c, const char *p, const char *ep)
 struct Matcher {
     Interp &I;
     long long calls = 0;
+    int depth = 0;   // recursion of match (the reference's: the C stack's only)
     const char *match(const char *s, const char *p, Capture *cap);
 
     const char *matchbalance(const char *s, const char *p, Capture *cap)
@@ -2833,6 +2851,14 @@ struct Matcher {
 const char *Matcher::match(const char *s, const char *p, Capture *cap)
 {
     if (++calls > 100000000LL) throw Unsupported("a pattern match of more than 10^8 steps");
+    struct Depth {
+        int &d;
+        explicit Depth(int &x) : d(x)
+        {
+            if (++d > 5000) throw Unsupported("a pattern match recursing more than 5000 deep");
+        }
+        ~Depth() { --d; }
+    } guard(depth);
 init:
     switch (*p) {
     case '(': return start_capture(s, p, cap);
