@@ -25,8 +25,9 @@
 // error-method argument, an error caught by call / dostring while
 // _ERRORMESSAGE or _ALERT is not the library's, recursion deeper than 200
 // calls, more than 3000 values left on the reference's 4096-slot stack (it
-// overflows near there), and a chunk that runs more than 10^9 steps for one
-// element (the reference would not return either).  random / randomseed run
+// overflows near there), more than 10^9 steps, 5 * 10^7 live objects or 10^5
+// dostring chunks for one element, nesting beyond 1000 levels or pattern
+// recursion beyond 5000 (the reference's limits there: its C stack, memory).  random / randomseed run
 // glibc's rand() restated, seeded as a fresh reference process has it.
 // Addresses (tostring of a table / function, table keys that are tables or
 // functions, whose traversal order follows their address in the reference)
