@@ -564,6 +564,15 @@ struct Interp {
         return (int)(v >> 1);
     }
     int depth = 0;                         // Lua calls active
+    const char *stack_top = nullptr;       // the C stack at the run's entry (see check_stack)
+    // deep recursion in the evaluator (nested calls of nested expressions)
+    // stops before the thread's C stack would: at 2 MB below the entry
+    void check_stack()
+    {
+        char here;
+        if (stack_top && stack_top - &here > (2 << 20))
+            throw Unsupported("nesting of calls and expressions beyond 2 MB of the evaluator's stack");
+    }
     long long units = 0;                   // estimated stack slots of the active calls
     long long steps = 0;                   // statements + calls in this element
     bool in_prelude = false;
@@ -1739,6 +1748,7 @@ struct Exec {
     // -- expressions -------------------------------------------------------------
     Value eval(const Expr *e)
     {
+        if (e->a && e->a->a) I.check_stack();   // (nested operands only: the leaves stay cheap)
         switch (e->k) {
         case X_NIL: return Value();
         case X_INT: return num((double)e->op);
@@ -2036,6 +2046,7 @@ void Interp::run_proto(const FuncObj *cl, std::vector<Value> &args, std::vector<
         F.slots[p.nparams] = t;
     }
     const long long u = 1 + p.maxslots + 10;
+    check_stack();
     if (++depth > kMaxDepth) throw Unsupported("recursion deeper than 200 calls");
     units += u;
     if (units + (long long)leaked.size() > kMaxUnits)
@@ -3340,6 +3351,8 @@ bool text_to_number(const char *s, Cx *out) { return str2d(s, out); }
 
 int Session::run_chunk(const std::string &text, std::string *output)
 {
+    char top;
+    I->stack_top = &top;
     I->capture = output;
     I->steps = 0;
     I->depth = 0;
@@ -3385,6 +3398,8 @@ Value literal(Interp &I, double v)
 ElementResult Session::run_element(const std::string &fctn, Cx X)
 {
     Interp &S = *I;
+    char top;
+    S.stack_top = &top;
     ElementResult R;
     ++S.epoch;
     S.steps = 0;
