@@ -63,6 +63,12 @@ PROGRAMS = [
     'or 0 end, {})',
     'call(function() local n = 0 foreach({a = 1, b = 2, c = 3}, function(k, v) n = (n or 0) + v end) return 1 end, {})',
     'rawget({5}, 1) + getn(rawset({}, 1, x))',
+    # another table of globals (lua_setglobals), for the call and for the elements after it
+    'call(function() local gl = globals local old = gl({x = 5, y = 2}) local v = x + y gl(old) return v end, {})',
+    'call(function() if not done_ then local gl = globals local t = {} for k, v in gl() do t[k] = v end '
+    't.done_ = 1 gl(t) end return x + (rawget(globals(), "done_") or 0) end, {})',
+    "dofile('/nonexistent/xfemm/defs.lua') == nil and 3 or 4",
+    "call(function() local a, b = dofile('/nonexistent/xfemm/defs.lua') return strlen(b) end, {})",
     # the whole table of globals, in the reference's hash order
     'call(function() acc = "" foreach(globals(), function(k, v) if type(v) == "function" then '
     'acc = acc .. strsub(k, 1, 1) end end) local h = 0 for i = 1, strlen(acc) do h = mod(h * 31 + strbyte(acc, i), '
@@ -179,10 +185,10 @@ BAD = ['call(function() error("x") end, {})', 'dostring("return")', 'call(functi
        'settagmethod(newtag(), "add")', 'settagmethod(newtag(), "add", 5)', "settag(5, newtag())",
        "call(function() local t = {} return t + 1 end, {})"]
 
-UNSUPPORTED = ['dofile("x")', 'openfile("x", "r")',
+UNSUPPORTED = ['dofile()', 'openfile("x", "r")',
                "femmVersion()", 'call(function() return 1 end, {}, "", print)', "gcinfo()",
                'call(function() g = function(n) return g(n + 1) end return g(1) end, {})',
-               'writeto("x")', "globals({})", 'date()']
+               'writeto("x")', 'date()']
 
 
 def same_bits(ref, got):
@@ -320,3 +326,20 @@ def test_lua_random_programs(seed):
         if not ok:
             bad.append((e, ref, got))
     assert not bad, bad[:3]
+
+
+@needs_lua
+def test_lua_dofile_runs_a_file(tmp_path):
+    """dofile: the chunk in the file runs on the same interpreter (its globals
+    stay), its results are dofile's; a syntax error in it gives nil and
+    "syntax error"; a missing file nil and "file error"."""
+    defs = tmp_path / "defs.lua"
+    defs.write_text("k_ = (k_ or 0) + 1\nfunction ang(t) return t * 2 + k_ end\nreturn 7, 8\n")
+    bad = tmp_path / "bad.lua"
+    bad.write_text("x = = 1\n")
+    for e in ['call(function() dofile("%s") return ang(theta) end, {})' % defs,
+              'call(function() local a, b = dofile("%s") return a * 10 + b end, {})' % defs,
+              'call(function() local a, b = dofile("%s") return (a == nil and 1 or 0) + strlen(b) end, {})' % bad]:
+        ref, got = compare(e, 0, 50, 4)
+        assert not isinstance(ref, str) and not isinstance(got, str), (e, ref, got)
+        assert same_bits(ref, got), e

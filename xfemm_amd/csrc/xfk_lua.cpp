@@ -2086,8 +2086,10 @@ void Interp::call(const Value &f, std::vector<Value> &args, std::vector<Value> &
 // replaced
 static void check_error_handlers(Interp &I)
 {
-    const Value em = I.getglobal("_ERRORMESSAGE"), al = I.getglobal("_ALERT");
-    if (!raweq(em, I.errormessage_fn) || !raweq(al, I.alert_fn))
+    // (luaH_getglobal: raw, in the current table of globals; a non-function
+    // is not called -- ldo.cpp:368-380)
+    const Value em = I.rawget(I.G, I.str("_ERRORMESSAGE")), al = I.rawget(I.G, I.str("_ALERT"));
+    if ((em.t == TFUN && !raweq(em, I.errormessage_fn)) || (al.t == TFUN && !raweq(al, I.alert_fn)))
         throw Unsupported("an error caught while _ERRORMESSAGE or _ALERT is not the library's");
 }
 
@@ -2291,12 +2293,16 @@ void b_getglobal(Interp &I, std::vector<Value> &a, std::vector<Value> &r)
 {
     r.assign(1, I.getglobal(I.str(check_str(I, a, 1))));
 }
-void b_globals(Interp &I, std::vector<Value> &a, std::vector<Value> &r)
+void b_globals(Interp &I, std::vector<Value> &a, std::vector<Value> &r)   // lbaselib.cpp:175-185
 {
-    if (!isnull(a, 1)) throw Unsupported("globals() with a new table of globals");
     Value g;
     g.t = TTAB;
     g.o = I.G;
+    if (!isnull(a, 1)) {   // lua_setglobals: the new table of globals
+        TableObj *t = check_table(a, 1);
+        if (t != I.G) I.changed = true;
+        I.G = t;
+    }
     r.assign(1, g);
 }
 void b_next(Interp &, std::vector<Value> &a, std::vector<Value> &r)   // lbaselib.cpp:242-253
@@ -2517,7 +2523,40 @@ void b_sort(Interp &I, std::vector<Value> &a, std::vector<Value> &)
 }
 void b_deprecated(Interp &, std::vector<Value> &, std::vector<Value> &) { rt_error("function is deprecated"); }
 
-void u_dofile(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("dofile"); }
+// dofile (lbaselib.cpp:297-304 over lua_dofile, ldo.cpp:290-325): a text
+// chunk read from the file, run as dostring runs its string
+void b_dofile(Interp &I, std::vector<Value> &a, std::vector<Value> &r)
+{
+    if (isnull(a, 1)) throw Unsupported("dofile() of the standard input");
+    const std::string name = check_str(I, a, 1);
+    std::string text;
+    FILE *f = std::fopen(name.c_str(), "r");
+    int status = 0;
+    if (!f) {
+        status = 2;   // LUA_ERRFILE
+    } else {
+        char buf[65536];
+        size_t n;
+        while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) text.append(buf, n);
+        std::fclose(f);
+        if (!text.empty() && text[0] == '\27') throw Unsupported("dofile() of a precompiled chunk");
+    }
+    if (status == 0) status = I.dostring(text, r);
+    else r.clear();
+    if (status == 0) {
+        if (r.empty()) {
+            Value u;
+            u.t = TUD;
+            u.o = I.null_ud;
+            r.push_back(u);
+        }
+        return;
+    }
+    static const char *const names[] = {"ok", "run-time error", "file error", "syntax error", "memory error",
+                                        "error in error handling"};
+    r.assign(1, Value());
+    r.push_back(I.str(names[status]));
+}
 void u_gcinfo(Interp &, std::vector<Value> &, std::vector<Value> &) { unsupported_fn("gcinfo"); }
 
 // tag methods from Lua (lbaselib.cpp:140-230, lapi.cpp:484-499, ltm.cpp:22-184)
@@ -3225,7 +3264,7 @@ Interp::Interp(bool axisymmetric) : axi(axisymmetric)
         const char *n;
         Builtin f;
     } base[] = {{"_ALERT", b_alert}, {"_ERRORMESSAGE", b_errormessage}, {"call", b_call},
-                {"collectgarbage", b_collectgarbage}, {"copytagmethods", b_copytagmethods}, {"dofile", u_dofile},
+                {"collectgarbage", b_collectgarbage}, {"copytagmethods", b_copytagmethods}, {"dofile", b_dofile},
                 {"dostring", b_dostring}, {"error", b_error}, {"foreach", b_foreach}, {"foreachi", b_foreachi},
                 {"gcinfo", u_gcinfo}, {"getglobal", b_getglobal}, {"gettagmethod", b_gettagmethod},
                 {"globals", b_globals}, {"newtag", b_newtag}, {"next", b_next}, {"print", b_print},

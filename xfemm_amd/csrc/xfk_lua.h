@@ -19,9 +19,8 @@
 // they do in the reference.
 //
 // What is refused (an Unsupported exception naming the construct -- never a
-// silent difference): the io library but write() on the standard handles,
-// and dofile (files, the process), globals(t) (replacing the global
-// table), gcinfo, femmVersion (a build-generated constant), call's
+// silent difference): the io library but write() on the standard handles
+// (dofile of a text file runs), gcinfo, femmVersion (a build-generated constant), call's
 // error-method argument, an error caught by call / dostring while
 // _ERRORMESSAGE or _ALERT is not the library's, recursion deeper than 200
 // calls, more than 3000 values left on the reference's 4096-slot stack (it
