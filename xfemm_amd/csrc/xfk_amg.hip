@@ -102,17 +102,36 @@ __device__ __forceinline__ void block_max2(double &a, double &b, double *red)
         }
 }
 
+constexpr int kMaxReduceT = 256;
+
 // per-block maxima (2 arrays of nblk) -> rho[0..1] as ordered bit patterns;
 // rho[0] (read only by the smoothers, weight 1 / rho[0]) is divided by the
 // Jacobi weight factor omega
-__global__ void __launch_bounds__(1024) k_max_reduce(int nblk, const double *__restrict__ part, double omega,
+__global__ void __launch_bounds__(kMaxReduceT) k_max_reduce(int nblk, const double *__restrict__ part, double omega,
                                                      unsigned long long *rho)
 {
     __shared__ double red[2 * 16];
     double a = 0.0, b = 0.0;
-    for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
-        a = fmax(a, part[i]);
-        b = fmax(b, part[nblk + i]);
+    // kMaxU partials per array per thread loaded before the first fmax: one
+    // load latency per kMaxU * blockDim partials (level 0 has ~2e4 blocks).
+    // Launched with 256 threads (kMaxReduceT), not 1024: a 16-wave workgroup
+    // waits for 16 free wave slots on one CU, which the side stream's
+    // k_fold_p (31k 4-wave blocks) did not leave until it drained -- up to
+    // 50 us of the setup's critical path at level 1
+    constexpr int kMaxU = 16;
+    for (int i0 = threadIdx.x; i0 < nblk; i0 += kMaxU * blockDim.x) {
+        double pa[kMaxU], pb[kMaxU];
+#pragma unroll
+        for (int q = 0; q < kMaxU; ++q) {
+            const int i = i0 + q * (int)blockDim.x;
+            pa[q] = i < nblk ? part[i] : 0.0;
+            pb[q] = i < nblk ? part[nblk + i] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kMaxU; ++q) {   // (fmax of non-negative bounds: any order, the same bits)
+            a = fmax(a, pa[q]);
+            b = fmax(b, pb[q]);
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -4102,7 +4121,7 @@ int Amg::build(hipStream_t s, int l0)
                                                 ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
                                                 A.val, absd.p, A.dinv.p, sflag.p, cnt.p,
                                                 dfinv.p, wF.p, rho_part.p, signed_strength());
-        k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p + 2 * l);
+        k_max_reduce<<<1, kMaxReduceT, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p + 2 * l);
         if (g_prof) g_prof->end();
         if (l == kAmgMaxLevels - 1) break;   // smoother-only coarsest level
         long long nc = 0;
@@ -4368,7 +4387,7 @@ int Amg::setup_dist(hipStream_t s, xfk_comm *comm_, const HaloPlan &halo_, int n
         k_amg_strength<<<nb_str(nl), kB, 0, s>>>(nl, nl, theta_at(l), A.rowptr, ColView{A.col, nullptr, nullptr}, A.val,
                                                  absd.p, A.dinv.p, sflag.p, cnt.p, dfinv.p, wF.p, rho_part.p,
                                                  signed_strength());
-        k_max_reduce<<<1, 1024, 0, s>>>(nb_str(nl), rho_part.p, omega, rho.p + 2 * l);
+        k_max_reduce<<<1, kMaxReduceT, 0, s>>>(nb_str(nl), rho_part.p, omega, rho.p + 2 * l);
         long long nc = 0;
         rc = aggregate(s, l, nc, false);
         if (rc != XFK_OK && rc != XFK_ERR_UNSUPPORTED) return rc;
@@ -5192,7 +5211,7 @@ int Amg::refresh(hipStream_t s, bool fold)
         k_amg_rho<<<nb_str(n), kB, 0, s>>>(n, A.rowptr,
                                            ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
                                            A.val, rho_part.p);
-        k_max_reduce<<<1, 1024, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p);
+        k_max_reduce<<<1, kMaxReduceT, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p);
     }
     if (A.has32 && f32_sweep_on()) {   // the sweeps' f32 copy of the new values
         int rc = to_f32(s, n, A.rowptr, A.nnz, A.val, A.a32);
