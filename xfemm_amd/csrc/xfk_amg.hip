@@ -459,22 +459,46 @@ __global__ void k_pattern_diff(int n, const int *__restrict__ rowptr, const int 
     if (d) out[0] = 1;
 }
 
+// The joins take G lanes per row (consecutive entries on consecutive lanes,
+// G = 1 on the fine level): each lane keeps its best candidate in its own
+// (increasing) entry order and the lanes' candidates are combined by the
+// same total order the one-thread loop applies -- the largest key, on a tie
+// the earlier entry (joins 1, 2), the largest |a_ij| and then the larger j
+// (join 3) -- so every G selects the same neighbour.  The coarse levels'
+// rows hold 10-40 entries: one thread walking them took 30-40 us per level.
+template <int G>
+__device__ __forceinline__ void join_best_key(MisKey &best, int &bk, int &bj)
+{
+#pragma unroll
+    for (int off = 1; off < G; off <<= 1) {
+        const MisKey ob = __shfl_xor(best, off, G);
+        const int obk = __shfl_xor(bk, off, G), obj = __shfl_xor(bj, off, G);
+        if (obj >= 0 && (bj < 0 || ob > best || (ob == best && obk < bk))) {
+            best = ob;
+            bk = obk;
+            bj = obj;
+        }
+    }
+}
+
 // distance 1: roots keep their aggregate, neighbours of roots join the root
 // with the largest key
 // rows left out that have (weak) couplings to aggregated owned rows join the
 // aggregate of the largest |a_ij| (ties: larger j); their P row is the
 // tentative injection (no strong couplings -> smoothing weight 0)
-__global__ void k_agg_join3(int n, int ncl, const int *__restrict__ rowptr, ColView cv,
-                            const double *__restrict__ val, const int *__restrict__ agg2, int *__restrict__ agg)
+template <int G>
+__global__ void __launch_bounds__(kB) k_agg_join3(int n, int ncl, const int *__restrict__ rowptr, ColView cv,
+                                                  const double *__restrict__ val, const int *__restrict__ agg2,
+                                                  int *__restrict__ agg)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / G, l = threadIdx.x % G;
+    if (i >= n) return;   // (whole groups)
     int a = agg2[i];
     if (a < 0) {
         double best = 0.0;
         int bj = -1;
         const int cb = cv.base(i);
-        for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        for (int k = rowptr[i] + l; k < rowptr[i + 1]; k += G) {
             const int j = cv.at(cb, k);
             if (j == i || j >= ncl || agg2[j] < 0) continue;
             const double v = fabs(val[k]);
@@ -483,53 +507,68 @@ __global__ void k_agg_join3(int n, int ncl, const int *__restrict__ rowptr, ColV
                 bj = j;
             }
         }
+#pragma unroll
+        for (int off = 1; off < G; off <<= 1) {
+            const double ob = __shfl_xor(best, off, G);
+            const int obj = __shfl_xor(bj, off, G);
+            if (obj >= 0 && (ob > best || (ob == best && ob > 0.0 && obj > bj))) {
+                best = ob;
+                bj = obj;
+            }
+        }
         if (bj >= 0) a = agg2[bj];
     }
-    agg[i] = a;
+    if (l == 0) agg[i] = a;
 }
 
-__global__ void k_agg_join1(int n, const int *__restrict__ rowptr, ColView cv,
-                            const unsigned char *__restrict__ sflag, const MisKey *__restrict__ key,
-                            const int *__restrict__ rootid, int *__restrict__ agg1)
+template <int G>
+__global__ void __launch_bounds__(kB) k_agg_join1(int n, const int *__restrict__ rowptr, ColView cv,
+                                                  const unsigned char *__restrict__ sflag,
+                                                  const MisKey *__restrict__ key, const int *__restrict__ rootid,
+                                                  int *__restrict__ agg1)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / G, l = threadIdx.x % G;
     if (i >= n) return;
     if (key_st(key[i]) == kStIn) {
-        agg1[i] = rootid[i];
+        if (l == 0) agg1[i] = rootid[i];
         return;
     }
-    int bj = -1;
+    int bj = -1, bk = INT_MAX;
     MisKey best = 0;
     const int cb = cv.base(i);
-    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+    for (int k = rowptr[i] + l; k < rowptr[i + 1]; k += G) {
         if (sflag[k] != 1) continue;
         const int j = cv.at(cb, k);
         const MisKey kj = key[j];
         if (key_st(kj) == kStIn && (bj < 0 || key_low(kj) > best)) {
             best = key_low(kj);
             bj = j;
+            bk = k;
         }
     }
-    agg1[i] = (bj >= 0) ? rootid[bj] : -1;
+    join_best_key<G>(best, bk, bj);
+    if (l == 0) agg1[i] = (bj >= 0) ? rootid[bj] : -1;
 }
 
 // distance 2: the rest join the aggregate of their largest-key neighbour
 // that joined at distance 1
-__global__ void k_agg_join2(int n, const int *__restrict__ rowptr, ColView cv,
-                            const unsigned char *__restrict__ sflag, const MisKey *__restrict__ key,
-                            const int *__restrict__ agg1, int *__restrict__ agg)
+template <int G>
+__global__ void __launch_bounds__(kB) k_agg_join2(int n, const int *__restrict__ rowptr, ColView cv,
+                                                  const unsigned char *__restrict__ sflag,
+                                                  const MisKey *__restrict__ key, const int *__restrict__ agg1,
+                                                  int *__restrict__ agg)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) / G, l = threadIdx.x % G;
     if (i >= n) return;
     const int a = agg1[i];
     if (a >= 0) {
-        agg[i] = a;
+        if (l == 0) agg[i] = a;
         return;
     }
-    int bj = -1;
+    int bj = -1, bk = INT_MAX;
     MisKey best = 0;
     const int cb = cv.base(i);
-    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+    for (int k = rowptr[i] + l; k < rowptr[i + 1]; k += G) {
         if (sflag[k] != 1) continue;
         const int j = cv.at(cb, k);
         if (agg1[j] < 0) continue;
@@ -537,9 +576,22 @@ __global__ void k_agg_join2(int n, const int *__restrict__ rowptr, ColView cv,
         if (bj < 0 || kl > best) {
             best = kl;
             bj = j;
+            bk = k;
         }
     }
-    agg[i] = (bj >= 0) ? agg1[bj] : -1;   // -1: isolated (or unreachable) -> no coarse dof
+    join_best_key<G>(best, bk, bj);
+    if (l == 0) agg[i] = (bj >= 0) ? agg1[bj] : -1;   // -1: isolated (or unreachable) -> no coarse dof
+}
+
+// lanes per row of the aggregation joins for rows of this average length
+static int join_lanes(double per_row)
+{
+    static const int v = [] {
+        const char *e = std::getenv("XFK_JOIN_LANES");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (v == 1 || v == 4 || v == 8) return v;
+    return per_row <= 8.0 ? 1 : (per_row <= 16.0 ? 4 : 8);
 }
 
 // --------------------------------------------------------------------------
@@ -1315,33 +1367,46 @@ constexpr int kBj = 64;
 // Gauss-Jordan pivot (a Schur-complement diagonal) lies in (0, 1].
 // perm / iperm (nested-dissection order, nullptr: identity): dense index of
 // coarse row r is perm[r]; iperm[q] the coarse row of dense index q (-1: padding)
+// kDsG lanes per dense row (consecutive entries on consecutive lanes): the
+// row's column, permutation and scale loads of 16 entries in flight at once
+// instead of one dependent chain per row (one thread per row took 11 + 26 us
+// for the 1.6k-row coarsest level of configs[2]).  The coarse operator's rows
+// hold distinct columns (SpGEMM output), so every entry is written once:
+// 0 + v, the value the former accumulation into the zeroed matrix produced.
+constexpr int kDsG = 16;
 __global__ void k_dense_dscale(int n, int ld, const int *__restrict__ rowptr, const int *__restrict__ col,
                                const double *__restrict__ val, const int *__restrict__ iperm, double *__restrict__ sc)
 {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= ld) return;
+    const int q = (blockIdx.x * blockDim.x + threadIdx.x) / kDsG, l = threadIdx.x % kDsG;
+    if (q >= ld) return;   // (whole groups: ld * kDsG threads exactly cover the rows)
     const int i = iperm ? iperm[q] : (q < n ? q : -1);
-    double d = 0.0;
+    int kd = -1;
     if (i >= 0)
-        for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
-            if (col[k] == i) d += val[k];
+        for (int k = rowptr[i] + l; k < rowptr[i + 1]; k += kDsG)
+            if (col[k] == i) kd = k;
+#pragma unroll
+    for (int off = 1; off < kDsG; off <<= 1) kd = max(kd, __shfl_xor(kd, off, kDsG));
+    if (l != 0) return;
+    const double d = kd >= 0 ? 0.0 + val[kd] : 0.0;
     sc[q] = d > 0.0 ? 1.0 / sqrt(d) : 1.0;
 }
 __global__ void k_dense_scatter(int n, int ld, const int *__restrict__ rowptr, const int *__restrict__ col,
                                 const double *__restrict__ val, const int *__restrict__ perm,
                                 const int *__restrict__ iperm, const double *__restrict__ sc, double *__restrict__ M)
 {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const int q = (blockIdx.x * blockDim.x + threadIdx.x) / kDsG, l = threadIdx.x % kDsG;
     if (q >= ld) return;
     const int i = iperm ? iperm[q] : (q < n ? q : -1);
     if (i < 0) {
-        M[(size_t)q * ld + q] = 1.0;
+        if (l == 0) M[(size_t)q * ld + q] = 1.0;
         return;
     }
-    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
-        if (col[k] >= n) continue;
-        const int c = perm ? perm[col[k]] : col[k];
-        M[(size_t)q * ld + c] += val[k] * sc[q] * sc[c];
+    const double sq = sc[q];
+    for (int k = rowptr[i] + l; k < rowptr[i + 1]; k += kDsG) {
+        const int cj = col[k];
+        if (cj >= n) continue;
+        const int c = perm ? perm[cj] : cj;
+        M[(size_t)q * ld + c] = 0.0 + val[k] * sq * sc[c];
     }
 }
 
@@ -3697,9 +3762,18 @@ int Amg::joins_and_p_impl(hipStream_t s, int l)
     const std::string lv = g_prof ? "setup L" + std::to_string(l) + " " : std::string();
     AMG_CHECK(agg1.alloc(n));
     AMG_CHECK(agg.alloc(n));
-    k_agg_join1<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, cursor.p, agg1.p);
-    k_agg_join2<<<nb(n), kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, agg1.p, agg.p);
-    k_agg_join3<<<nb(n), kB, 0, s>>>(n, A.ncol_lim, A.rowptr, cv, A.val, agg.p, agg1.p);
+    // lanes per row for the joins (XFK_JOIN_LANES: 1 = one thread per row)
+    const int jg = join_lanes((double)A.nnz / std::max(1, n));
+    auto joins = [&](auto g) {
+        constexpr int G = decltype(g)::value;
+        const int blocks = nb((long long)n * G);
+        k_agg_join1<G><<<blocks, kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, cursor.p, agg1.p);
+        k_agg_join2<G><<<blocks, kB, 0, s>>>(n, A.rowptr, cv, sflag.p, key.p, agg1.p, agg.p);
+        k_agg_join3<G><<<blocks, kB, 0, s>>>(n, A.ncol_lim, A.rowptr, cv, A.val, agg.p, agg1.p);
+    };
+    if (jg == 8) joins(std::integral_constant<int, 8>{});
+    else if (jg == 4) joins(std::integral_constant<int, 4>{});
+    else joins(std::integral_constant<int, 1>{});
     std::swap(agg.p, agg1.p);   // agg = the joined map
     std::swap(agg.n, agg1.n);
     if (g_prof) g_prof->end();
@@ -3984,8 +4058,8 @@ int Amg::dense_inverse(hipStream_t s, const AmgLevel &C, int ld)
     double *maxd = bgj_tmp.p + 2 * kNdChains * per, *sc = maxd + 1;
     const int *pm = nd ? cinv_perm.p : nullptr, *ipm = nd ? cinv_iperm.p : nullptr;
     AMG_CHECK(hipMemsetAsync(cinv.p, 0, sizeof(double) * (size_t)ld * ld, s));
-    k_dense_dscale<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, ipm, sc);
-    k_dense_scatter<<<nb(ld), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, pm, ipm, sc, cinv.p);
+    k_dense_dscale<<<nb((long long)ld * kDsG), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, ipm, sc);
+    k_dense_scatter<<<nb((long long)ld * kDsG), kB, 0, s>>>(C.n, ld, C.rowptr, C.col, C.val, pm, ipm, sc, cinv.p);
     k_dense_maxdiag<<<1, 1024, 0, s>>>(ld, ld, cinv.p, maxd);
     // (a lookahead variant -- block column k+1 first, its pivot block
     // inverted on a second stream during the rest of the update -- was
