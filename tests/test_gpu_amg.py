@@ -495,3 +495,18 @@ def test_refold_threshold_unfolds_short_passes(monkeypatch):
     A2b, _ = _solve(kw, precond="amg")
     assert rel_err(A2, Ac) <= TOL_NONLINEAR
     assert np.array_equal(A2.view(np.int64), A2b.view(np.int64))
+
+
+def test_lane_parallel_joins_select_the_same_aggregates(monkeypatch):
+    """The aggregation joins take 4 / 8 lanes per row on the coarse levels
+    (rows of 128-256 entries under the smoothed prolongator), each lane's
+    candidate combined in the one-thread loop's own order: the same neighbour
+    as one thread per row (XFK_JOIN_LANES=1), so the same hierarchy and the
+    same solution bits."""
+    kw = synth.magnetostatic(300)
+    A, r = _solve(kw, precond="amg")
+    monkeypatch.setenv("XFK_JOIN_LANES", "1")
+    A1, r1 = _solve(kw, precond="amg")
+    assert r["amg_levels"] >= 3
+    assert (r1["cg_iters"], r1["amg_levels"]) == (r["cg_iters"], r["amg_levels"])
+    assert np.array_equal(A.view(np.int64), A1.view(np.int64))

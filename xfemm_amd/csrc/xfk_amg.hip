@@ -586,10 +586,8 @@ __global__ void __launch_bounds__(kB) k_agg_join2(int n, const int *__restrict__
 // lanes per row of the aggregation joins for rows of this average length
 static int join_lanes(double per_row)
 {
-    static const int v = [] {
-        const char *e = std::getenv("XFK_JOIN_LANES");
-        return e ? std::atoi(e) : 0;
-    }();
+    const char *e = std::getenv("XFK_JOIN_LANES");   // (read per level: tests toggle it)
+    const int v = e ? std::atoi(e) : 0;
     if (v == 1 || v == 4 || v == 8) return v;
     return per_row <= 8.0 ? 1 : (per_row <= 16.0 ? 4 : 8);
 }
