@@ -298,9 +298,12 @@ __global__ void __launch_bounds__(kB) k_amg_strength(int n, int ncl, double thet
 // a Newton refresh (same aggregates, P and weights; new values): only the
 // Gershgorin bound of D^-1 A, summed as k_amg_strength sums it (each lane's
 // entries in order, the same butterfly: the same bits); rho[1] is not used
-// after a setup and is left 0
+// after a setup and is left 0.  The row's diagonal found here also gives
+// |a_ii| and D^-1 (k_amg_diag's values: the other lanes add 0.0 to it), so the
+// refresh reads the matrix once
 __global__ void __launch_bounds__(kB) k_amg_rho(int n, const int *__restrict__ rowptr, ColView cv,
-                                                const double *__restrict__ val, double *__restrict__ rho_part)
+                                                const double *__restrict__ val, double *__restrict__ rho_part,
+                                                double *__restrict__ absd, double *__restrict__ dinv)
 {
     __shared__ double red[2 * (kB / 64)];
     const int i = (blockIdx.x * blockDim.x + threadIdx.x) / kStrG;
@@ -321,7 +324,11 @@ __global__ void __launch_bounds__(kB) k_amg_rho(int n, const int *__restrict__ r
         aii += __shfl_xor(aii, off, kStrG);
         sumA += __shfl_xor(sumA, off, kStrG);
     }
-    if (i < n && g == 0 && aii != 0.0) rA = (fabs(aii) + sumA) / fabs(aii);
+    if (i < n && g == 0) {
+        if (aii != 0.0) rA = (fabs(aii) + sumA) / fabs(aii);
+        absd[i] = fabs(aii);
+        dinv[i] = (aii != 0.0) ? 1.0 / aii : 0.0;
+    }
     block_max2(rA, rF, red);
     if (threadIdx.x == 0) {
         rho_part[blockIdx.x] = rA;
@@ -5279,10 +5286,9 @@ int Amg::refresh(hipStream_t s, bool fold)
     AMG_CHECK(absd.alloc(std::max(1, n)));
     AMG_CHECK(rho_part.alloc(2 * (size_t)std::max(1, nb_str(n))));
     if (n > 0) {
-        k_amg_diag<<<nb(n), kB, 0, s>>>(n, A.rowptr, A.col, A.val, absd.p, A.dinv.p);
         k_amg_rho<<<nb_str(n), kB, 0, s>>>(n, A.rowptr,
                                            ColView{A.col, A.has16 ? A.a16.p : nullptr, A.has16 ? A.a16b.p : nullptr},
-                                           A.val, rho_part.p);
+                                           A.val, rho_part.p, absd.p, A.dinv.p);
         k_max_reduce<<<1, kMaxReduceT, 0, s>>>(nb_str(n), rho_part.p, omega, rho.p);
     }
     if (A.has32 && f32_sweep_on()) {   // the sweeps' f32 copy of the new values
